@@ -1,0 +1,289 @@
+"""Benchmark: X2-GNN training step (molecules/s, fwd+bwd) on synthetic QM9-U0-shaped molecules.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+One step = the reference trainer's step (trainer.py:37-48) on one resident batch of 128
+molecules per GPU: xgnn_poly forward (GPU triplet build, basis, 4 SBF-transformer layers,
+readouts), smooth-L1 loss, backward, one RCCL all-reduce of the flat gradient bucket (N>1),
+grad-norm clip (max 100), Adam step and the EMA update.  Weak scaling: every rank owns its own
+128 molecules.  Rank 0 prints ONE JSON line (contract in the task statement); besides the
+metric it carries the dominant kernel's roofline (HIP-event timed here, on the stream it runs
+on) and the CPU baseline (the oracle restatement, torch-CPU, on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "x2-gnn_amd"))
+
+import x2gnn  # noqa: E402
+from x2gnn import ops  # noqa: E402
+from x2gnn._lib import call, ptr, stream_ptr  # noqa: E402
+from x2gnn.data import collate  # noqa: E402
+from x2gnn.dist import GradBucket  # noqa: E402
+from x2gnn.synth import synthetic_molecules  # noqa: E402
+
+CFG = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embedding_size=128)  # config.json
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+METRIC = "molecules/sec (fwd+bwd) on QM9 U0, batch=128, 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=128, help="molecules per GPU")
+    ap.add_argument("--shape", default="S160", choices=["S160", "S5A"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--kernel-reps", type=int, default=20)
+    return ap.parse_args()
+
+
+class Trainer:
+    """The reference trainer's per-batch step (trainer.py:37-48) with a flat gradient bucket."""
+
+    def __init__(self, model, lr=1e-3, max_norm=100.0, ema_decay=0.95):
+        self.model = model
+        self.bucket = GradBucket(model.parameters())
+        self.opt = torch.optim.Adam(model.parameters(), lr=lr, foreach=True)
+        self.max_norm = max_norm
+        self.ema = [p.detach().clone() for p in model.parameters()]
+        self.ema_decay = ema_decay
+        self.params = list(model.parameters())
+
+    def step(self, batch):
+        self.bucket.zero()
+        res = self.model(batch)
+        loss = torch.nn.functional.smooth_l1_loss(res, batch.y)
+        loss.backward()
+        self.bucket.allreduce_mean()
+        torch.nn.utils.clip_grad_norm_(self.params, self.max_norm, foreach=True)
+        self.opt.step()
+        with torch.no_grad():  # AveragedModel(avg_fn = d*avg + (1-d)*p), train_ema.py:45-47
+            torch._foreach_lerp_(self.ema, self.params, 1.0 - self.ema_decay)
+        return loss
+
+
+# ------------------------------------------------------------------------------------------ kernels
+def attention_probe(model, batch, reps):
+    """Time the fused attention kernels of conv layer 0 on this step's real inputs with HIP
+    events on the launch stream; returns {kernel: (avg_ms, algorithmic_bytes_per_launch)}."""
+    conv = model.fin_model.convs[0]
+    with torch.no_grad():
+        line, plan = model.line_graph_data(batch)
+        lg = plan.lg
+        x, rbf, sbf = line.x, line.node_rbf, line.edge_sbf
+        table = conv.lin_edge(model.fin_model.edgenn(line.edge_attr)).contiguous()
+        row = plan.dst_type
+        x_src = x * conv.lin_rbf(rbf)
+        q, k, v = conv.lin_query(x), conv.lin_key(x_src), conv.lin_value(x_src)
+        skip = conv.lin_skip(x)
+    E, T, H, C = lg.E, lg.T, conv.heads, conv.out_channels
+    D = H * C
+    W, bsb = conv.lin_sbf.weight.detach().contiguous(), conv.lin_sbf.bias.detach().contiguous()
+    f32 = dict(dtype=torch.float32, device=x.device)
+    out = torch.empty(E, D, **f32)
+    alpha, smax, sden = torch.empty(T, H, **f32), torch.empty(E, H, **f32), torch.empty(E, H, **f32)
+    dout = torch.randn(E, D, **f32)
+    dq, dk, dv, dedge = (torch.empty(E, D, **f32) for _ in range(4))
+    dlogit, dproj = torch.empty(T, H, **f32), torch.empty(T, D, **f32)
+    src_rowptr, src_perm = lg.src_csr()
+    S = sbf.shape[1]
+
+    def fwd():
+        call("x2g_sbf_attention_fwd", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(row), ops.EDGE_PER_DST,
+             ptr(sbf), ptr(W), ptr(bsb), ptr(lg.trip_rowptr), ptr(lg.trip_src), E, T, H, C, S, ptr(out),
+             ptr(alpha), ptr(smax), ptr(sden), stream_ptr())
+
+    def bwd_dst():
+        call("x2g_sbf_attention_bwd_dst", ptr(q), ptr(k), ptr(v), ptr(table), ptr(row), ops.EDGE_PER_DST, ptr(sbf),
+             ptr(W), ptr(bsb), ptr(lg.trip_rowptr), ptr(lg.trip_src), ptr(alpha), ptr(smax), ptr(sden), ptr(dout),
+             E, T, H, C, S, ptr(dq), ptr(dedge), ptr(dlogit), ptr(dproj), stream_ptr())
+
+    def bwd_src():
+        call("x2g_sbf_attention_bwd_src", ptr(q), ptr(sbf), ptr(W), ptr(bsb), ptr(src_rowptr), ptr(src_perm),
+             ptr(lg.trip_dst), ptr(alpha), ptr(smax), ptr(sden), ptr(dlogit), ptr(dout), E, T, H, C, S, ptr(dk),
+             ptr(dv), stream_ptr())
+
+    row_b = 4 * D
+    # algorithmic bytes per launch: every logical read/write once per use (gathered rows per triplet)
+    fwd_bytes = T * (4 + 2 * row_b + 4 * S + 4 * H) + E * (8 + 4 * row_b + 8 * H + 4)
+    dst_bytes = T * (4 + 2 * row_b + 4 * S + 4 * H * 3 + row_b) + E * (8 + 4 * row_b + 8 * H + 4)
+    src_bytes = T * (8 + 2 * row_b + 4 * S + 4 * H * 2 + 8 * H) + E * (8 + 2 * row_b)
+    res = {}
+    for name, fn, nbytes in (("attn_fwd", fwd, fwd_bytes), ("attn_bwd_dst", bwd_dst, dst_bytes),
+                             ("attn_bwd_src", bwd_src, src_bytes)):
+        res[name] = (_event_time(fn, reps), nbytes)
+    return res, dict(E=E, T=T, D=D)
+
+
+def _event_time(fn, reps):
+    st = torch.cuda.current_stream()
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    start.record(st)
+    for _ in range(reps):
+        fn()
+    end.record(st)
+    end.synchronize()
+    return start.elapsed_time(end) / reps
+
+
+def scatter_add_probe(lg, reps):
+    """The graded CSR-by-destination scatter-add (x2g_segment_sum) at the step's line-graph
+    shape: [T, 128] messages -> [E, 128], algorithmic bytes 4*T*D + 4*(E+1) + 4*E*D.
+    Timed L2/MALL-warm (back-to-back) and cache-busted (512 MiB written between launches)."""
+    E, T, D = lg.E, lg.T, 128
+    dev = lg.trip_rowptr.device
+    msgs = torch.randn(T, D, device=dev)
+    out = torch.empty(E, D, device=dev)
+    nbytes = 4 * T * D + 4 * (E + 1) + 4 * E * D
+
+    def fn():
+        call("x2g_segment_sum", ptr(msgs), None, ptr(lg.trip_rowptr), E, D, ptr(out), stream_ptr())
+
+    warm = _event_time(fn, reps)
+    flush = torch.empty(512 * 2 ** 20 // 4, device=dev)
+    st = torch.cuda.current_stream()
+    times = []
+    for _ in range(reps):
+        flush.fill_(1.0)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        fn()
+        b.record(st)
+        b.synchronize()
+        times.append(a.elapsed_time(b))
+    ref = torch.zeros(E, D, device=dev).index_add_(0, lg.trip_dst.long(), msgs)
+    ok = torch.allclose(out, ref, rtol=1e-4, atol=1e-4)
+    return dict(bytes=nbytes, warm_ms=warm, cold_ms=float(np.median(times)), parity=bool(ok))
+
+
+# ------------------------------------------------------------------------------------------ cpu
+def cpu_baseline(mols, budget_s):
+    """The oracle (torch-CPU restatement of the reference) fwd+bwd on the same 128-molecule batch,
+    timed for ~budget_s seconds on this host's cores."""
+    from oracle import ref_cpu
+
+    threads = torch.get_num_threads()
+    model = ref_cpu.XGNN(**CFG)
+    b = collate(mols)
+    times = []
+    t_end = time.perf_counter() + budget_s
+    for i in range(100):
+        t0 = time.perf_counter()
+        res = ref_cpu.run_batch(model, b)
+        loss = torch.nn.functional.smooth_l1_loss(res, b.y)
+        loss.backward()
+        dt = time.perf_counter() - t0
+        if i > 0:
+            times.append(dt)
+        if time.perf_counter() > t_end and len(times) >= 2:
+            break
+    step = float(np.median(times))
+    return {"value": round(len(mols) / step, 2), "unit": "molecules/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ref_cpu.py fwd+bwd (no optimizer) on the same {len(mols)}-molecule "
+                      f"batch, median of {len(times)} steps after 1 warm-up, torch-CPU fp32, "
+                      f"{threads} threads of {os.cpu_count()} logical CPUs"}
+
+
+# ------------------------------------------------------------------------------------------ main
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    torch.manual_seed(0)  # identical initial weights on every rank
+
+    mols = synthetic_molecules(args.batch, args.shape, seed=1000 + rank)  # this rank's own shard
+    batch = collate(mols).to(dev)
+    model = x2gnn.xgnn_poly(device="cuda", **CFG).to(dev)
+    trainer = Trainer(model)
+
+    for _ in range(args.warmup):
+        trainer.step(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = trainer.step(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t_max = float(t.item())
+    final_loss = float(loss.item())
+
+    meta = batch.host_meta()
+    probe, shape = attention_probe(model, batch, args.kernel_reps)
+    plan_lg = model.line_graph_data(batch)[1].lg
+    sa = scatter_add_probe(plan_lg, args.kernel_reps)
+    dom_name, (dom_ms, dom_bytes) = max(probe.items(), key=lambda kv: kv[1][0])
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(world * args.batch * args.steps / t_max, 2),
+            "unit": "molecules/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * t_max / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": f"synthetic QM9-shaped molecules ({args.shape}: ~18 atoms, "
+                    f"{meta['edges'].mean():.0f} directed edges, {meta['triplets'].mean():.0f} triplets per "
+                    f"molecule, random 338-wide edge features), random-init weights",
+            "config": {"workload": f"xgnn_poly U0 train step (config.json: L=4, D=128, H=16, sbf 7x6), "
+                                   f"{args.shape}, fwd+loss+bwd+allreduce+clip+Adam+EMA",
+                       "per_gpu_batch": args.batch, "global_batch": world * args.batch,
+                       "line_nodes_per_gpu": shape["E"], "triplets_per_gpu": shape["T"],
+                       "parallelism": f"dp{world}"},
+            "roofline": {"kernel": dom_name, "bound": "hbm", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None, "avg_ms": round(dom_ms, 5), "bytes_per_launch": int(dom_bytes)},
+            "kernels_ms": {k: round(v[0], 5) for k, v in probe.items()},
+            "roofline_scatter_add": {
+                "kernel": "x2g_segment_sum [T,128]->[E,128]", "bytes_per_launch": sa["bytes"],
+                "warm_GBs": round(sa["bytes"] / (sa["warm_ms"] * 1e-3) / 1e9, 1),
+                "cold_GBs": round(sa["bytes"] / (sa["cold_ms"] * 1e-3) / 1e9, 1),
+                "cold_frac": round(sa["bytes"] / (sa["cold_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "parity": sa["parity"]},
+            "final_loss": round(final_loss, 6),
+        }
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(mols, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,156 @@
+/*
+ * x2g.h — C ABI of libx2g.so, the MI355X (gfx950) kernels behind X2-GNN's message-passing
+ * hot path.  Plain pointers and sizes only; no torch / HIP types in the signatures.
+ *
+ * Conventions:
+ *  - every pointer is a DEVICE pointer that stays valid until the work enqueued on `stream`
+ *    completes; `stream` is a hipStream_t passed as void* (NULL = default stream);
+ *  - the library never allocates or frees: outputs and workspaces are caller-owned
+ *    (the Python host layer allocates them from PyTorch's caching allocator);
+ *  - index arrays are int32; float tensors are fp32, row-major, contiguous;
+ *  - functions only enqueue work: no host synchronisation, no device->host reads; every size
+ *    comes from the caller;
+ *  - return 0 on success, a hipError_t value on a launch failure, or an X2G_E* code below;
+ *    never abort, never throw across the ABI;
+ *  - results are deterministic: segmented reductions run in a fixed order, no float atomics.
+ *
+ * Each entry point names the reference interface it replaces (file:line in zfwangDP/X2-GNN,
+ * plus the un-vendored torch_scatter 2.1.0 / PyG 2.1.0 operators it reached).
+ */
+#ifndef X2G_H
+#define X2G_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define X2G_OK 0
+#define X2G_EINVAL 1001        /* bad size / null pointer */
+#define X2G_EUNSUPPORTED 1002  /* shape outside the compiled kernel set */
+#define X2G_EWORKSPACE 1003    /* workspace too small */
+
+/* edge-term modes of the attention kernels */
+#define X2G_EDGE_NONE 0        /* edge_dim=None: no lin_edge term */
+#define X2G_EDGE_PER_TRIPLET 1 /* edge[T, H*C]: one row per triplet (reference layout) */
+#define X2G_EDGE_PER_DST 2     /* edge[R, H*C] indexed by edge_row[E]: one row per destination line node */
+
+int x2g_abi_version(void);
+const char* x2g_status_string(int status);
+
+/* ---------------------------------------------------------------- line graph (triplets) */
+
+/* rowptr[s] = first i with keys[i] >= s, for s in [0, n_seg]; keys sorted ascending.
+ * Replaces the CSR row pointer scipy builds in edge_graph.py:14 (adj_matrix.tocsr()). */
+int x2g_csr_rowptr(const int32_t* keys, int64_t n, int64_t n_seg, int32_t* rowptr, void* stream);
+
+/* Workspace bytes for x2g_vertex_to_edge / x2g_line_graph_transpose. */
+size_t x2g_vertex_to_edge_workspace(int64_t num_edges, int64_t num_nodes);
+
+/* vertex_to_edge_2 (edge_graph.py:12-30): for every directed edge e=(a->b), in edge order, and
+ * every k in N_out(b) ascending with k != a, emit triplet t with
+ *   trip_src[t] = id(b->k), trip_dst[t] = e, atom_j[t] = b, atom_i[t] = a, atom_k[t] = k.
+ * edge_src/edge_dst: int32[E], sorted by (src, dst) (np.argwhere order, atom_graph.py:42-45).
+ * num_triplets must equal the true count (host metadata); trip_rowptr[E+1] receives the
+ * CSR-by-destination row pointer; atom_rowptr[N+1] the source-atom CSR of the edges.
+ * Any of atom_j/atom_i/atom_k may be NULL. */
+int x2g_vertex_to_edge(const int32_t* edge_src, const int32_t* edge_dst, int64_t num_edges,
+                       int64_t num_nodes, int64_t num_triplets, int32_t* atom_rowptr,
+                       int32_t* trip_rowptr, int32_t* trip_src, int32_t* trip_dst, int32_t* atom_j,
+                       int32_t* atom_i, int32_t* atom_k, void* workspace, size_t workspace_bytes,
+                       void* stream);
+
+/* Triplets regrouped by source line node (the transpose the backward of the k_j / v_j gathers
+ * needs): src_rowptr[E+1]; src_perm[T] lists triplet ids of each source in ascending order.
+ * Replaces the atomics of ATen index_add_ behind PyG's index_select backward. */
+int x2g_line_graph_transpose(const int32_t* trip_src, int64_t num_triplets, int64_t num_edges,
+                             int32_t* src_rowptr, int32_t* src_perm, void* workspace,
+                             size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- basis (featurisation) */
+
+/* rbf_env[e, l*R+n] = env(d_e) * N_ln j_l(z_ln d_e/cutoff)   (l < 7, n < 6, R = 6)
+ * = the E-row part of F_B_2D.forward (angular_basis_layer.py:80-86) with poly_envelop
+ * (envelop.py:16-21, exponent 5). */
+int x2g_bessel_env(const float* dist, int64_t num_edges, float cutoff, float* rbf_env, void* stream);
+
+/* sbf[t, l*R+n] = rbf_env[trip_src[t], l*R+n] * Y_l0(theta_t), theta_t = atan2(|ji x jk|, ji.jk),
+ * ji = pos[atom_i]-pos[atom_j], jk = pos[atom_k]-pos[atom_j]  (xgnn.py:61-65,
+ * angular_basis_layer.py:87-93).  If theta[T] is non-NULL it is used instead of the positions
+ * (F_B_2D.forward(d, Angles, edge_index_1) signature; pos/atom_* may then be NULL).
+ * cos_theta[T] (optional, may be NULL) receives cos(theta). */
+int x2g_spherical_basis(const float* pos, const int32_t* atom_i, const int32_t* atom_j,
+                        const int32_t* atom_k, const float* theta, const int32_t* trip_src,
+                        const float* rbf_env, int64_t num_triplets, float* sbf, float* cos_theta,
+                        void* stream);
+
+/* ---------------------------------------------------------------- SBF-transformer attention */
+
+/* Fused SBFTransformerConv.message + PyG softmax + 'add' aggregation + root skip
+ * (sbftransformer_conv.py:109-127,138-162), CSR by destination:
+ *   kk_t = k[src]+edge_t, u_t = v[src]+edge_t, alpha_t,h = <q[dst]_h, kk_t,h>/sqrt(C),
+ *   a = softmax_dst(alpha) (max shift, /(sum+1e-16)), S_t = W_sbf sbf_t + b_sbf,
+ *   out[e] = sum_{t in seg(e)} u_t*S_t*a_t,h + skip[e].
+ * Saves alpha_raw[T,H], seg_max[E,H], seg_den[E,H] for the backward.
+ * Compiled for H*C in {32,64,128,256}, C in {4,8,16,32} with C >= channels-per-lane, sbf_dim 42. */
+int x2g_sbf_attention_fwd(const float* q, const float* k, const float* v, const float* skip,
+                          const float* edge, const int32_t* edge_row, int edge_mode, const float* sbf,
+                          const float* w_sbf, const float* b_sbf, const int32_t* trip_rowptr,
+                          const int32_t* trip_src, int64_t num_edges, int64_t num_triplets,
+                          int32_t heads, int32_t channels, int32_t sbf_dim, float* out,
+                          float* alpha_raw, float* seg_max, float* seg_den, void* stream);
+
+/* Backward, destination-major: dq[E,HC]; d_edge ([E,HC] per destination for EDGE_PER_DST,
+ * [T,HC] for EDGE_PER_TRIPLET); dlogit[T,H] (grad of alpha_raw); d_sbfproj[T,HC] (grad of S_t,
+ * so dW_sbf = d_sbfproj^T sbf and db_sbf = column sums). */
+int x2g_sbf_attention_bwd_dst(const float* q, const float* k, const float* v, const float* edge,
+                              const int32_t* edge_row, int edge_mode, const float* sbf,
+                              const float* w_sbf, const float* b_sbf, const int32_t* trip_rowptr,
+                              const int32_t* trip_src, const float* alpha_raw, const float* seg_max,
+                              const float* seg_den, const float* dout, int64_t num_edges,
+                              int64_t num_triplets, int32_t heads, int32_t channels, int32_t sbf_dim,
+                              float* dq, float* d_edge, float* dlogit, float* d_sbfproj, void* stream);
+
+/* Backward, source-major over x2g_line_graph_transpose's lists: dk[E,HC], dv[E,HC]
+ * (the adjoint of PyG's index_select(key/value, edge_index[0]) lift, without atomics). */
+int x2g_sbf_attention_bwd_src(const float* q, const float* sbf, const float* w_sbf,
+                              const float* b_sbf, const int32_t* src_rowptr, const int32_t* src_perm,
+                              const int32_t* trip_dst, const float* alpha_raw, const float* seg_max,
+                              const float* seg_den, const float* dlogit, const float* dout,
+                              int64_t num_edges, int64_t num_triplets, int32_t heads, int32_t channels,
+                              int32_t sbf_dim, float* dk, float* dv, void* stream);
+
+/* ---------------------------------------------------------------- segmented reductions */
+
+/* out[g, :] = sum_{r in [rowptr[g], rowptr[g+1])} x[r, :] (* mul[r, :] if mul != NULL).
+ * torch_scatter scatter_add(src, index, dim=0, dim_size) for a sorted index
+ * (readout.py:37, model.py:190, and the 'add' aggregation of MessagePassing). */
+int x2g_segment_sum(const float* x, const float* mul, const int32_t* rowptr, int64_t num_segments,
+                    int64_t dim, float* out, void* stream);
+
+/* out[r, :] = g[seg(r), :] (* mul[r, :] if mul != NULL): adjoint of x2g_segment_sum. */
+int x2g_segment_broadcast(const float* g, const float* mul, const int32_t* rowptr, int64_t num_segments,
+                          int64_t dim, float* out, void* stream);
+
+/* PyG utils.softmax(src[R,H], index) for a sorted index (CSR rowptr): per segment and column,
+ * exp(src - max) / (sum + 1e-16). */
+int x2g_segment_softmax_fwd(const float* src, const int32_t* rowptr, int64_t num_segments, int64_t heads,
+                            float* out, void* stream);
+int x2g_segment_softmax_bwd(const float* out, const float* dout, const int32_t* rowptr,
+                            int64_t num_segments, int64_t heads, float* dsrc, void* stream);
+
+/* PyG nn.LayerNorm(mode='graph', affine=False) (model.py:161,183): per segment g of rows,
+ * mu = sum x / (n_g*D), var = sum (x-mu)^2 / (n_g*D) (n_g clamped >= 1), out = (x-mu)/sqrt(var+eps).
+ * mean/rstd[num_segments] are saved for the backward. */
+int x2g_graph_layernorm_fwd(const float* x, const int32_t* rowptr, int64_t num_segments, int64_t dim,
+                            float eps, float* out, float* mean, float* rstd, void* stream);
+int x2g_graph_layernorm_bwd(const float* out, const float* dout, const float* rstd, const int32_t* rowptr,
+                            int64_t num_segments, int64_t dim, float* dx, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* X2G_H */

@@ -1,0 +1,45 @@
+"""Test helpers: rebuild fixture inputs as batches, seeded models, comparisons."""
+import numpy as np
+import torch
+
+from conftest import golden  # noqa: F401
+from weights import load_seeded
+
+
+def batch_from_fixture(z, prefix=""):
+    """Collated x2gnn Batch (host) from a fixture's stored inputs."""
+    from x2gnn.data import Batch, Data
+
+    nodes, edges, trips = z[prefix + "nodes"], z[prefix + "edges"], z[prefix + "triplets"]
+    b = Batch()
+    b._store["x"] = torch.from_numpy(z[prefix + "x"].astype(np.int64))
+    b._store["atom_pos"] = torch.from_numpy(z[prefix + "atom_pos"])
+    b._store["edge_index"] = torch.from_numpy(z[prefix + "edge_index"].astype(np.int64))
+    b._store["edge_attr"] = torch.from_numpy(z[prefix + "edge_attr"])
+    b._store["edge_num"] = torch.from_numpy(edges.astype(np.int64))
+    b._store["y"] = torch.from_numpy(z[prefix + "y"])
+    b._store["batch"] = torch.repeat_interleave(torch.arange(len(nodes)), torch.from_numpy(nodes.astype(np.int64)))
+    b._store["ptr"] = torch.from_numpy(np.concatenate([[0], np.cumsum(nodes)]).astype(np.int64))
+    object.__setattr__(b, "_meta", {"nodes": nodes.astype(np.int64), "edges": edges.astype(np.int64),
+                                    "triplets": trips.astype(np.int64)})
+    assert isinstance(b, Data)
+    return b
+
+
+def model_cfg(z):
+    return dict(zip([str(k) for k in z["cfg_keys"]], [int(v) for v in z["cfg_vals"]]))
+
+
+def oracle_model(z):
+    from oracle.ref_cpu import XGNN
+
+    kind = str(z["kind"])
+    m = XGNN(global_pool="mean" if kind == "global" else None, **model_cfg(z))
+    load_seeded(m, int(z["weight_seed"]))
+    return m
+
+
+def rel_err(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))

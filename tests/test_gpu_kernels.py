@@ -1,0 +1,316 @@
+"""Kernel-level parity on the GPU: every libx2g.so operator against the reference fixtures and the
+CPU oracle on the same seeded inputs (integer work bit-exact, float work within stated
+tolerances)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from helpers import rel_err
+
+from oracle import ref_cpu, triplets
+
+pytestmark = pytest.mark.gpu
+
+
+def _lg(ei_np, n, T, dev):
+    from x2gnn import ops
+
+    return ops.vertex_to_edge(torch.from_numpy(ei_np.astype(np.int64)).to(dev), n, T)
+
+
+# ------------------------------------------------------------------------------ triplets
+def _check_transpose(lg):
+    rp, perm = (t.cpu().numpy() for t in lg.src_csr())
+    src = lg.trip_src.cpu().numpy()
+    assert rp[0] == 0 and rp[-1] == lg.T
+    assert np.array_equal(np.sort(perm), np.arange(lg.T))            # a permutation
+    assert np.all(np.diff(src[perm]) >= 0)                            # grouped by source
+    np.testing.assert_array_equal(np.diff(rp), np.bincount(src, minlength=lg.E))
+    for s in range(lg.E):                                             # ascending inside a group
+        seg = perm[rp[s]:rp[s + 1]]
+        assert np.all(np.diff(seg) > 0)
+
+
+def test_vertex_to_edge_matches_reference(cuda):
+    z = golden("triplets.npz")
+    for case in z["cases"]:
+        ei, n = z[f"{case}_edge_index"], int(z[f"{case}_num_nodes"])
+        ref = z[f"{case}_trip"]
+        lg = _lg(ei, n, ref.shape[1], cuda)
+        np.testing.assert_array_equal(lg.trip_src.cpu().numpy(), ref[0])
+        np.testing.assert_array_equal(lg.trip_dst.cpu().numpy(), ref[1])
+        np.testing.assert_array_equal(lg.atom_j.cpu().numpy(), z[f"{case}_j"])
+        np.testing.assert_array_equal(lg.atom_i.cpu().numpy(), z[f"{case}_i"])
+        np.testing.assert_array_equal(lg.atom_k.cpu().numpy(), z[f"{case}_k"])
+        rp = lg.trip_rowptr.cpu().numpy()
+        np.testing.assert_array_equal(np.diff(rp), np.bincount(ref[1], minlength=ei.shape[1]))
+        np.testing.assert_array_equal(lg.atom_rowptr.cpu().numpy(),
+                                      np.searchsorted(ei[0], np.arange(n + 1), side="left"))
+        if case in ("s160", "directed"):
+            _check_transpose(lg)
+
+
+def test_vertex_to_edge_full_batch_vs_oracle(cuda):
+    from x2gnn.data import collate
+    from x2gnn.synth import synthetic_molecules
+
+    b = collate(synthetic_molecules(128, "S160", seed=3))
+    ei = b.edge_index.numpy()
+    T = int(b._meta["triplets"].sum())
+    lg = _lg(ei, b.num_nodes, T, cuda)
+    trip, j, i, k = triplets.vertex_to_edge(ei, b.num_nodes)
+    np.testing.assert_array_equal(lg.trip_src.cpu().numpy(), trip[0])
+    np.testing.assert_array_equal(lg.trip_dst.cpu().numpy(), trip[1])
+    np.testing.assert_array_equal(lg.atom_k.cpu().numpy(), k)
+    rp, perm = (t.cpu().numpy() for t in lg.src_csr())
+    assert np.all(np.diff(trip[0][perm]) >= 0) and np.array_equal(np.sort(perm), np.arange(T))
+
+
+def test_vertex_to_edge_edge_cases(cuda):
+    from x2gnn import ops
+
+    # no edges at all
+    lg = ops.vertex_to_edge(torch.zeros(2, 0, dtype=torch.int64, device=cuda), 5, 0)
+    assert lg.T == 0 and lg.trip_rowptr.cpu().tolist() == [0]
+    assert lg.atom_rowptr.cpu().tolist() == [0] * 6
+    # one bond (a <-> b): no triplets; isolated trailing atoms
+    ei = np.array([[0, 1], [1, 0]])
+    lg = _lg(ei, 4, 0, cuda)
+    assert lg.trip_rowptr.cpu().tolist() == [0, 0, 0]
+    assert lg.atom_rowptr.cpu().tolist() == [0, 1, 2, 2, 2]
+    # a star with a hub of degree 70 (> one 64-lane chunk)
+    hub = np.array([[0] * 70 + list(range(1, 71)), list(range(1, 71)) + [0] * 70])
+    order = np.lexsort((hub[1], hub[0]))
+    hub = hub[:, order]
+    trip, *_ = triplets.vertex_to_edge(hub, 71)
+    lg = _lg(hub, 71, trip.shape[1], cuda)
+    np.testing.assert_array_equal(lg.trip_src.cpu().numpy(), trip[0])
+    _check_transpose(lg)
+
+
+def test_csr_rowptr(cuda):
+    from x2gnn import ops
+
+    keys = np.array([0, 0, 2, 2, 2, 5, 7, 7])
+    rp = ops.csr_rowptr(torch.from_numpy(keys).to(cuda), 9).cpu().numpy()
+    np.testing.assert_array_equal(rp, np.searchsorted(keys, np.arange(10), side="left"))
+
+
+# ------------------------------------------------------------------------------ basis
+BASIS_TOL = [1e-5, 1e-5, 1e-5, 1e-4, 1e-3, 5e-3, 3e-2]  # per l: the reference's fp32 cancellation
+
+
+def test_spherical_basis_vs_reference(cuda):
+    from x2gnn import ops
+
+    z = golden("basis.npz")
+    ei = z["edge_index"].astype(np.int64)
+    n = int(z["nodes"].sum())
+    lg = _lg(ei, n, z["trip"].shape[1], cuda)
+    d = torch.from_numpy(z["dist"]).to(cuda)
+    rbf_env = ops.bessel_env(d)
+    pos = torch.from_numpy(z["atom_pos"]).to(cuda)
+    sbf, cos_t = ops.spherical_basis(pos, lg, rbf_env, want_cos=True)
+    sbf = sbf.cpu().numpy()
+    for l in range(7):
+        blk = slice(6 * l, 6 * l + 6)
+        assert np.abs(sbf[:, blk] - z["sbf"][:, blk]).max() < BASIS_TOL[l], l
+    np.testing.assert_allclose(cos_t.cpu().numpy(), np.cos(z["theta"]), atol=2e-6)
+    # the theta-input entry point (F_B_2D.forward(d, Angles, edge_index_1) signature)
+    sbf2 = ops.spherical_basis_from_angles(torch.from_numpy(z["theta"]).to(cuda), lg.trip_src, rbf_env).cpu().numpy()
+    for l in range(7):
+        blk = slice(6 * l, 6 * l + 6)
+        assert np.abs(sbf2[:, blk] - z["sbf"][:, blk]).max() < BASIS_TOL[l], l
+    # against the fp64 oracle, l <= 3 the reference formula is accurate to ~1e-6
+    orc = ref_cpu.spherical_basis(torch.from_numpy(z["dist"]), torch.from_numpy(z["theta"]),
+                                  torch.from_numpy(z["trip"][0].astype(np.int64))).numpy()
+    assert np.abs(sbf[:, :24] - orc[:, :24]).max() < 1e-4
+
+
+def test_radial_parts_vs_reference(cuda):
+    from x2gnn.layers import RadialBasis, poly_envelop
+
+    z = golden("basis.npz")
+    d = torch.from_numpy(z["dist"]).to(cuda)
+    env = poly_envelop(5.0, 5)(d)
+    np.testing.assert_allclose(env.cpu().numpy(), z["env"], rtol=2e-6, atol=1e-6)
+    rbf = RadialBasis(6, 5.0).to(cuda)(d) * env[:, None]
+    np.testing.assert_allclose(rbf.detach().cpu().numpy(), z["rbf"], rtol=1e-5, atol=1e-6)
+
+
+# ------------------------------------------------------------------------------ segments
+def _rowptr_with_empties(rng, n_seg, max_len):
+    lens = rng.integers(0, max_len + 1, size=n_seg)
+    lens[rng.random(n_seg) < 0.2] = 0
+    return np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+
+
+@pytest.mark.parametrize("D", [1, 6, 32, 128, 256])
+@pytest.mark.parametrize("with_mul", [False, True])
+def test_segment_sum_and_adjoint(cuda, D, with_mul):
+    from x2gnn import ops
+
+    rng = np.random.default_rng(D)
+    rp = _rowptr_with_empties(rng, 333, 40)
+    R = int(rp[-1])
+    x = torch.randn(R, D, dtype=torch.float64)
+    m = torch.randn(R, D, dtype=torch.float64) if with_mul else None
+    seg = np.repeat(np.arange(333), np.diff(rp))
+    ref = torch.zeros(333, D, dtype=torch.float64).index_add_(0, torch.from_numpy(seg), x * m if with_mul else x)
+    xg = x.float().to(cuda).requires_grad_(True)
+    mg = m.float().to(cuda).requires_grad_(True) if with_mul else None
+    out = ops.segment_sum(xg, torch.from_numpy(rp).to(cuda), 333, mul=mg)
+    assert rel_err(out.detach().cpu().numpy(), ref.numpy()) < 1e-5
+    g = torch.randn(333, D)
+    out.backward(g.to(cuda))
+    gx = g.double()[torch.from_numpy(seg)]
+    np.testing.assert_allclose(xg.grad.cpu().numpy(), (gx * m if with_mul else gx).numpy(), rtol=1e-5, atol=1e-5)
+    if with_mul:
+        np.testing.assert_allclose(mg.grad.cpu().numpy(), (gx * x).numpy(), rtol=1e-5, atol=1e-5)
+
+
+def test_segment_sum_is_deterministic(cuda):
+    from x2gnn import ops
+
+    rng = np.random.default_rng(0)
+    rp = torch.from_numpy(_rowptr_with_empties(rng, 5000, 30)).to(cuda)
+    x = torch.randn(int(rp[-1]), 128, device=cuda)
+    a = ops.segment_sum(x, rp, 5000)
+    b = ops.segment_sum(x, rp, 5000)
+    assert torch.equal(a, b)
+
+
+def test_segment_softmax_vs_oracle(cuda):
+    from x2gnn import ops
+
+    rng = np.random.default_rng(1)
+    rp = _rowptr_with_empties(rng, 200, 25)
+    R = int(rp[-1])
+    seg = torch.from_numpy(np.repeat(np.arange(200), np.diff(rp)))
+    src = (3 * torch.randn(R, 16)).requires_grad_(True)
+    ref = ref_cpu.pyg_softmax(src, seg, 200)
+    g = torch.randn(R, 16)
+    ref.backward(g)
+    sg = src.detach().to(cuda).requires_grad_(True)
+    out = ops.segment_softmax(sg, torch.from_numpy(rp).to(cuda), 200)
+    out.backward(g.to(cuda))
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref.detach().numpy(), rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(sg.grad.cpu().numpy(), src.grad.numpy(), rtol=1e-4, atol=1e-6)
+
+
+def test_graph_layernorm_vs_oracle(cuda):
+    from x2gnn import ops
+
+    counts = np.array([162, 0, 1, 288, 40, 2037])  # includes an empty and a one-row molecule
+    rp = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+    batch = torch.from_numpy(np.repeat(np.arange(len(counts)), counts))
+    x = (torch.randn(int(rp[-1]), 128) * 3 + 1).requires_grad_(True)
+    ref = ref_cpu.graph_layer_norm(x, batch, 1e-8)
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    xg = x.detach().to(cuda).requires_grad_(True)
+    out = ops.graph_layer_norm(xg, torch.from_numpy(rp).to(cuda), len(counts), 1e-8)
+    out.backward(g.to(cuda))
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref.detach().numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(xg.grad.cpu().numpy(), x.grad.numpy(), rtol=1e-3, atol=1e-5)
+
+
+# ------------------------------------------------------------------------------ attention
+def _product_conv(z, cuda):
+    from weights import load_seeded
+    from x2gnn import SBFTransformerConv
+
+    conv = SBFTransformerConv(in_channels=128, out_channels=8, heads=16, sbf_dim=42, rbf_dim=6, dropout=0,
+                              edge_dim=128)
+    load_seeded(conv, int(z["weight_seed"]))
+    return conv.to(cuda)
+
+
+def test_conv_layer_vs_reference(cuda):
+    """Drop-in SBFTransformerConv.forward(sbf, rbf, x, edge_index, edge_attr), per-triplet edge_attr."""
+    z = golden("conv1.npz")
+    conv = _product_conv(z, cuda)
+    x = torch.from_numpy(z["conv_x"]).to(cuda).requires_grad_(True)
+    ea = torch.from_numpy(z["conv_edge_attr"]).to(cuda).requires_grad_(True)
+    out = conv(torch.from_numpy(z["sbf"]).to(cuda), torch.from_numpy(z["rbf"]).to(cuda), x,
+               torch.from_numpy(z["trip"].astype(np.int64)).to(cuda), ea)
+    assert rel_err(out.detach().cpu().numpy(), z["out"]) < 1e-5
+    (out * torch.from_numpy(z["upstream"]).to(cuda)).sum().backward()
+    assert rel_err(x.grad.cpu().numpy(), z["grad_x"]) < 1e-4
+    assert rel_err(ea.grad.cpu().numpy(), z["grad_edge_attr"]) < 1e-4
+    for n, p in conv.named_parameters():
+        if n == "lin_key.bias":  # analytically zero: compare on the scale of the weight gradient
+            assert np.abs(p.grad.cpu().numpy()).max() < 1e-5 * np.abs(z["grad.lin_key.weight"]).max()
+            continue
+        assert rel_err(p.grad.cpu().numpy(), z["grad." + n]) < 1e-4, n
+
+
+def test_conv_attention_weights(cuda):
+    z = golden("conv1.npz")
+    conv = _product_conv(z, cuda)
+    trip = torch.from_numpy(z["trip"].astype(np.int64)).to(cuda)
+    out, (ei, alpha) = conv(torch.from_numpy(z["sbf"]).to(cuda), torch.from_numpy(z["rbf"]).to(cuda),
+                            torch.from_numpy(z["conv_x"]).to(cuda), trip,
+                            torch.from_numpy(z["conv_edge_attr"]).to(cuda), return_attention_weights=True)
+    a = alpha.cpu().numpy()
+    sums = np.zeros((z["conv_x"].shape[0], 16))
+    np.add.at(sums, z["trip"][1], a)
+    has = np.bincount(z["trip"][1], minlength=sums.shape[0]) > 0
+    np.testing.assert_allclose(sums[has], 1.0, atol=1e-5)
+
+
+def test_per_destination_edge_table_equals_per_triplet(cuda):
+    """EDGE_PER_DST (table row per destination) == EDGE_PER_TRIPLET with the expanded rows."""
+    from x2gnn import ops
+
+    z = golden("conv1.npz")
+    conv = _product_conv(z, cuda)
+    trip = torch.from_numpy(z["trip"].astype(np.int64)).to(cuda)
+    E = z["conv_x"].shape[0]
+    g = torch.Generator().manual_seed(3)
+    table = torch.randn(10, 128, generator=g).to(cuda)
+    row = torch.randint(1, 10, (E,), generator=g).to(cuda)
+    sbf = torch.from_numpy(z["sbf"]).to(cuda)
+    rbf = torch.from_numpy(z["rbf"]).to(cuda)
+    x = torch.from_numpy(z["conv_x"]).to(cuda)
+    t1 = table.clone().requires_grad_(True)
+    a = conv(sbf, rbf, x, trip, t1.index_select(0, row.index_select(0, trip[1])))
+    t2 = table.clone().requires_grad_(True)
+    lg = ops.LineGraph.from_triplets(trip, E)
+    b = conv(sbf, rbf, x, trip, t2, line_graph=lg, edge_row=row)
+    assert rel_err(b.detach().cpu().numpy(), a.detach().cpu().numpy()) < 1e-5
+    up = torch.randn(E, 128, generator=g).to(cuda)
+    (a * up).sum().backward()
+    (b * up).sum().backward()
+    assert rel_err(t2.grad.cpu().numpy(), t1.grad.cpu().numpy()) < 1e-4
+
+
+def test_conv_small_width_vs_oracle(cuda):
+    """D=32, H=4 (the reduced-width configuration of model_small) against the oracle conv."""
+    from weights import load_seeded
+    from x2gnn import SBFTransformerConv
+
+    z = golden("conv1.npz")
+    E, T = z["conv_x"].shape[0], z["trip"].shape[1]
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(E, 32, generator=g)
+    ea = torch.randn(T, 32, generator=g)
+    sbf, rbf = torch.from_numpy(z["sbf"]), torch.from_numpy(z["rbf"])
+    trip = torch.from_numpy(z["trip"].astype(np.int64))
+    orc = ref_cpu.SBFTransformerConv(32, 4, 42, 6, 32)
+    load_seeded(orc, 5)
+    xr, er = x.clone().requires_grad_(True), ea.clone().requires_grad_(True)
+    ref = orc(sbf, rbf, xr, trip, er)
+    up = torch.randn(E, 32, generator=g)
+    (ref * up).sum().backward()
+    conv = SBFTransformerConv(32, 8, heads=4, sbf_dim=42, rbf_dim=6, edge_dim=32)
+    load_seeded(conv, 5)
+    conv = conv.to(cuda)
+    xg, eg = x.to(cuda).requires_grad_(True), ea.to(cuda).requires_grad_(True)
+    out = conv(sbf.to(cuda), rbf.to(cuda), xg, trip.to(cuda), eg)
+    (out * up.to(cuda)).sum().backward()
+    assert rel_err(out.detach().cpu().numpy(), ref.detach().numpy()) < 1e-5
+    assert rel_err(xg.grad.cpu().numpy(), xr.grad.numpy()) < 1e-4
+    assert rel_err(eg.grad.cpu().numpy(), er.grad.numpy()) < 1e-4
+    assert rel_err(conv.lin_sbf.weight.grad.cpu().numpy(), orc.lin_sbf.weight.grad.numpy()) < 1e-4

@@ -1,0 +1,112 @@
+"""Host-side logic: synthetic data, collate, module trees, generated basis constants."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from helpers import model_cfg
+
+
+def test_synthetic_shapes_match_survey():
+    from x2gnn.synth import synthetic_molecules
+
+    ms = synthetic_molecules(32, "S160", seed=0)
+    assert np.mean([len(m["x"]) for m in ms]) == 18
+    assert 140 < np.mean([m["edge_num"] for m in ms]) < 185       # ~160 directed edges
+    assert 1200 < np.mean([m["triplet_num"] for m in ms]) < 1750  # ~1460 triplets
+    m = ms[0]
+    ei = m["edge_index"]
+    key = ei[0] * 100 + ei[1]
+    assert np.all(np.diff(key) > 0)  # sorted by (src, dst), no duplicates
+    assert m["edge_attr"].shape == (ei.shape[1], 338) and m["edge_attr"].dtype == np.float32
+
+
+def test_synthetic_is_deterministic():
+    from x2gnn.synth import synthetic_molecules
+
+    a = synthetic_molecules(3, "S5A", seed=5)
+    b = synthetic_molecules(3, "S5A", seed=5)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x["atom_pos"], y["atom_pos"])
+        np.testing.assert_array_equal(x["edge_attr"], y["edge_attr"])
+
+
+def test_collate_pyg_semantics():
+    from x2gnn.data import collate
+    from x2gnn.synth import synthetic_molecules
+
+    ms = synthetic_molecules(3, "S160", seed=1)
+    b = collate(ms)
+    n = [len(m["x"]) for m in ms]
+    e = [m["edge_num"] for m in ms]
+    assert b.num_graphs == 3
+    assert "batch" in b._store
+    assert b.edge_index.shape == (2, sum(e))
+    # edge_index incremented by the running atom count (PyG __inc__ for edge_index)
+    np.testing.assert_array_equal(b.edge_index[:, e[0]:e[0] + e[1]].numpy(), ms[1]["edge_index"] + n[0])
+    np.testing.assert_array_equal(b.edge_num.numpy(), e)
+    np.testing.assert_array_equal(b.ptr.numpy(), np.concatenate([[0], np.cumsum(n)]))
+    np.testing.assert_array_equal(b.batch.numpy(), np.repeat(np.arange(3), n))
+    assert list(b._meta["triplets"]) == [m["triplet_num"] for m in ms]
+    # reference quirk (xgnn.py:42-43): setting num_graphs on a batch must not change it
+    b.num_graphs = 1
+    assert b.num_graphs == 3
+
+
+def test_meta_fallback_matches_collate():
+    from x2gnn.data import _meta_from_tensors, collate
+    from x2gnn.synth import synthetic_molecules
+
+    b = collate(synthetic_molecules(4, "S160", seed=2))
+    m = _meta_from_tensors(b)
+    for k in ("nodes", "edges", "triplets"):
+        np.testing.assert_array_equal(m[k], b._meta[k])
+
+
+@pytest.mark.parametrize("fixture", ["model_small.npz", "model_full.npz", "model_global.npz"])
+def test_state_dict_names_equal_reference(fixture):
+    import x2gnn
+
+    z = golden(fixture)
+    cls = x2gnn.xgnn_poly if str(z["kind"]) == "poly" else x2gnn.xgnn_poly_global
+    m = cls(**model_cfg(z))
+    assert [n for n, _ in m.named_parameters()] == list(z["param_names"])
+    assert [str(tuple(p.shape)) for _, p in m.named_parameters()] == list(z["param_shapes"])
+    assert list(m.state_dict().keys()) == list(z["state_keys"])
+
+
+def test_generated_basis_constants_vs_oracle():
+    """The device's expanded Rayleigh coefficients reproduce N_ln j_l(z_ln x) (fp64 check)."""
+    from x2gnn import basis_consts as bc
+
+    from oracle import ref_cpu
+
+    np.testing.assert_allclose(np.array(bc.ZEROS), ref_cpu._ZEROS, rtol=0, atol=0)
+    x = np.linspace(0.15, 1.0, 61)
+    ref = ref_cpu.bessel_radial(x)
+    coef = np.array(bc.COEF)
+    for l in range(7):
+        for n in range(6):
+            z = bc.ZEROS[l][n]
+            acc = np.zeros_like(x)
+            for m in range(l, -1, -1):
+                trig = np.sin(z * x) if m % 2 == 0 else np.cos(z * x)
+                acc += coef[l, n, m] * x ** m * trig
+            np.testing.assert_allclose(acc / x ** (l + 1), ref[:, 6 * l + n], rtol=1e-6, atol=1e-9)
+    y = np.array(bc.YCOEF)
+    c = np.cos(np.linspace(0, math.pi, 17))
+    for l in range(7):
+        val = sum(y[l, p] * c ** p for p in range(7))
+        np.testing.assert_allclose(val, ref_cpu.sph_y0(np.arccos(c))[:, l], atol=1e-12)
+
+
+def test_device_ops_refuse_cpu_tensors():
+    from x2gnn import ops
+
+    x = torch.zeros(4, 128)
+    with pytest.raises(RuntimeError, match="GPU"):
+        ops.segment_sum(x, torch.zeros(3, dtype=torch.int32), 2)
+    with pytest.raises(RuntimeError, match="GPU"):
+        ops.vertex_to_edge(torch.zeros(2, 3, dtype=torch.int64), 3, 0)

@@ -1,0 +1,474 @@
+// Fused SBF-transformer attention over the line graph (the hot loop of X2-GNN).
+//
+// Reference: SBFTransformerConv (sbftransformer_conv.py:93-162) through PyG 2.1's
+// MessagePassing.propagate: q_i = q[edge_index[1]], k_j/v_j = k/v[edge_index[0]] lifted to
+// [T,H,C] by index_select, the per-triplet message, torch_geometric.utils.softmax over each
+// destination, torch_scatter 'add' aggregation to [E,H,C], + lin_skip(x).  The reference
+// materialises ~10 [T,128] fp32 tensors per layer for this; here nothing T x 128 is written in
+// the forward.
+//
+// Layout: triplets are CSR by destination (trip_rowptr / trip_src, the order vertex_to_edge_2
+// produces).  One 64-lane wave owns one destination line node at a time and walks its
+// triplets in order (deterministic); each lane owns CPL consecutive channels, so a head of C
+// channels spans LPH = C/CPL lanes and the q.k dot product is a LPH-lane xor-shuffle reduction.
+// The neighbour rows k[src], v[src] are read as one coalesced 512 B row per wave (D=128), the
+// 42-float sbf row of the triplet is wave-uniform (scalar loads), and the lin_sbf weight lives
+// in registers (S=42 floats per channel), so the [T,42]x[42,128] projection is computed on the
+// fly instead of being materialised.  Softmax is the online (running max / rescale) form; the
+// per-(destination, head) max and denominator are saved for the backward.
+//
+// Backward is two passes with no float atomics:
+//  * destination-major (bwd_dst): dq, the edge-term gradient, the softmax-logit gradient
+//    dlogit[T,H], and d_sbfproj[T,HC] (for dW_sbf = d_sbfproj^T sbf);
+//  * source-major (bwd_src) over the transposed triplet lists: dk and dv, each a fixed-order
+//    segmented sum (the adjoint of the k_j / v_j gathers).
+#include <math.h>
+
+#include "common.hpp"
+
+namespace x2g {
+
+constexpr int kS = 42;           // sbf_dim compiled in (7 spherical x 6 radial)
+constexpr int kAttnWaves = 4;    // waves per 256-thread block
+constexpr int kMaxBlocks = 2048; // persistent-ish grid: waves grid-stride over line nodes
+constexpr float kSoftmaxEps = 1e-16f;
+
+struct AttnArgs {
+  const float* q;
+  const float* k;
+  const float* v;
+  const float* skip;
+  const float* edge;
+  const int32_t* edge_row;
+  int edge_mode;
+  const float* sbf;
+  const float* w;
+  const float* b;
+  const int32_t* rowptr;   // fwd/bwd_dst: trip_rowptr; bwd_src: src_rowptr
+  const int32_t* tidx;     // fwd/bwd_dst: trip_src;    bwd_src: src_perm
+  const int32_t* tdst;     // bwd_src: trip_dst
+  const float* alpha;
+  const float* smax;
+  const float* sden;
+  const float* dlogit_in;
+  const float* dout;
+  int64_t E;
+  int D;
+  int H;
+  float sqrt_c;
+  float* out;
+  float* alpha_out;
+  float* smax_out;
+  float* sden_out;
+  float* dq;
+  float* d_edge;
+  float* dlogit;
+  float* dproj;
+  float* dk;
+  float* dv;
+};
+
+template <int CPL>
+__device__ __forceinline__ void load_row(const float* __restrict__ p, bool act, float (&r)[CPL]) {
+  if (CPL == 2) {
+    float2 x = act ? *reinterpret_cast<const float2*>(p) : make_float2(0.f, 0.f);
+    r[0] = x.x;
+    r[1] = x.y;
+  } else if (CPL == 4) {
+    float4 x = act ? *reinterpret_cast<const float4*>(p) : make_float4(0.f, 0.f, 0.f, 0.f);
+    r[0] = x.x;
+    r[1] = x.y;
+    r[2] = x.z;
+    r[3] = x.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) r[j] = act ? p[j] : 0.f;
+  }
+}
+
+template <int CPL>
+__device__ __forceinline__ void store_row(float* __restrict__ p, bool act, const float (&r)[CPL]) {
+  if (!act) return;
+  if (CPL == 2) {
+    *reinterpret_cast<float2*>(p) = make_float2(r[0], r[1]);
+  } else if (CPL == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(r[0], r[1], r[2], r[3]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) p[j] = r[j];
+  }
+}
+
+// sp[j] = b[j] + sum_s W[c0+j][s] * sbf_t[s]; the sbf row pointer is wave-uniform.
+template <int CPL>
+__device__ __forceinline__ void sbf_project(const float (&wr)[CPL][kS], const float (&br)[CPL],
+                                            const float* __restrict__ srow, float (&sp)[CPL]) {
+  float acc[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) acc[j] = 0.f;
+#pragma unroll
+  for (int s = 0; s < kS; ++s) {
+    const float x = srow[s];
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) acc[j] = fmaf(wr[j][s], x, acc[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) sp[j] = acc[j] + br[j];
+}
+
+template <int CPL>
+__device__ __forceinline__ void load_weights(const AttnArgs& a, int c0, bool act, float (&wr)[CPL][kS],
+                                             float (&br)[CPL]) {
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const float* wrow = a.w + static_cast<int64_t>(c0 + j) * kS;
+#pragma unroll
+    for (int s = 0; s < kS; ++s) wr[j][s] = act ? wrow[s] : 0.f;
+    br[j] = act ? a.b[c0 + j] : 0.f;
+  }
+}
+
+__device__ __forceinline__ int wave_id_global() {
+  return uniform(static_cast<int>(blockIdx.x) * kAttnWaves + static_cast<int>(threadIdx.x >> 6));
+}
+
+// ------------------------------------------------------------------------------ forward
+template <int CPL, int LPH>
+__global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int D = a.D, H = a.H;
+  const bool act = lane * CPL < D;
+  const int c0 = act ? lane * CPL : 0;
+  const int head = lane / LPH;
+  const bool leader = act && (lane % LPH) == 0;
+  float wr[CPL][kS], br[CPL];
+  load_weights<CPL>(a, c0, act, wr, br);
+  const int nwaves = gridDim.x * kAttnWaves;
+  for (int64_t e = wave_id_global(); e < a.E; e += nwaves) {
+    const int t0 = a.rowptr[e], t1 = a.rowptr[e + 1];
+    float qv[CPL], ed[CPL], acc[CPL];
+    load_row<CPL>(a.q + e * D + c0, act, qv);
+    if (a.edge_mode == X2G_EDGE_PER_DST) {
+      const int64_t r = a.edge_row ? a.edge_row[e] : e;
+      load_row<CPL>(a.edge + r * D + c0, act, ed);
+    } else {
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) ed[j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) acc[j] = 0.f;
+    float m = -INFINITY, den = 0.f;
+    // software pipeline: the next triplet's neighbour rows are in flight while this one computes
+    float kc[CPL], vc[CPL];
+    if (t0 < t1) {
+      const int64_t s = a.tidx[t0];
+      load_row<CPL>(a.k + s * D + c0, act, kc);
+      load_row<CPL>(a.v + s * D + c0, act, vc);
+    }
+    for (int t = t0; t < t1; ++t) {
+      float kn[CPL], vn[CPL];
+      if (t + 1 < t1) {
+        const int64_t sn = a.tidx[t + 1];
+        load_row<CPL>(a.k + sn * D + c0, act, kn);
+        load_row<CPL>(a.v + sn * D + c0, act, vn);
+      }
+      float et[CPL];
+      if (a.edge_mode == X2G_EDGE_PER_TRIPLET) {
+        load_row<CPL>(a.edge + static_cast<int64_t>(t) * D + c0, act, et);
+      } else {
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) et[j] = ed[j];
+      }
+      float dot = 0.f;
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) dot = fmaf(qv[j], kc[j] + et[j], dot);
+      const float logit = group_sum<LPH>(dot) / a.sqrt_c;
+      float sp[CPL];
+      sbf_project<CPL>(wr, br, a.sbf + static_cast<int64_t>(t) * kS, sp);
+      const float m_new = fmaxf(m, logit);
+      const float corr = expf(m - m_new);
+      const float p = expf(logit - m_new);
+      den = den * corr + p;
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) acc[j] = acc[j] * corr + p * ((vc[j] + et[j]) * sp[j]);
+      m = m_new;
+      if (leader) a.alpha_out[static_cast<int64_t>(t) * H + head] = logit;
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) {
+        kc[j] = kn[j];
+        vc[j] = vn[j];
+      }
+    }
+    float sk[CPL], o[CPL];
+    load_row<CPL>(a.skip + e * D + c0, act, sk);
+    const float inv = 1.0f / (den + kSoftmaxEps);
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) o[j] = acc[j] * inv + sk[j];
+    store_row<CPL>(a.out + e * D + c0, act, o);
+    if (leader) {
+      a.smax_out[e * H + head] = m;
+      a.sden_out[e * H + head] = den;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ backward (dst)
+template <int CPL, int LPH>
+__global__ void __launch_bounds__(256) attn_bwd_dst_kernel(AttnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int D = a.D, H = a.H;
+  const bool act = lane * CPL < D;
+  const int c0 = act ? lane * CPL : 0;
+  const int head = lane / LPH;
+  const bool leader = act && (lane % LPH) == 0;
+  const bool per_trip = a.edge_mode == X2G_EDGE_PER_TRIPLET;
+  const bool per_dst = a.edge_mode == X2G_EDGE_PER_DST;
+  float wr[CPL][kS], br[CPL];
+  load_weights<CPL>(a, c0, act, wr, br);
+  const int nwaves = gridDim.x * kAttnWaves;
+  for (int64_t e = wave_id_global(); e < a.E; e += nwaves) {
+    const int t0 = a.rowptr[e], t1 = a.rowptr[e + 1];
+    float go[CPL], qv[CPL], ed[CPL], edacc[CPL], dqa[CPL];
+    load_row<CPL>(a.dout + e * D + c0, act, go);
+    load_row<CPL>(a.q + e * D + c0, act, qv);
+    if (per_dst) {
+      const int64_t r = a.edge_row ? a.edge_row[e] : e;
+      load_row<CPL>(a.edge + r * D + c0, act, ed);
+    } else {
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) ed[j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      edacc[j] = 0.f;
+      dqa[j] = 0.f;
+    }
+    const float mx = act ? a.smax[e * H + head] : 0.f;
+    const float inv = act ? 1.0f / (a.sden[e * H + head] + kSoftmaxEps) : 0.f;
+    // pass 1: g_t = d(loss)/d(a_t) per head, rho = sum_t a_t g_t; d_sbfproj and the value part
+    float rho = 0.f;
+    for (int t = t0; t < t1; ++t) {
+      const int64_t s = a.tidx[t];
+      float vv[CPL], et[CPL], sp[CPL];
+      load_row<CPL>(a.v + s * D + c0, act, vv);
+      if (per_trip) {
+        load_row<CPL>(a.edge + static_cast<int64_t>(t) * D + c0, act, et);
+      } else {
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) et[j] = ed[j];
+      }
+      sbf_project<CPL>(wr, br, a.sbf + static_cast<int64_t>(t) * kS, sp);
+      const float at = act ? expf(a.alpha[static_cast<int64_t>(t) * H + head] - mx) * inv : 0.f;
+      float gpart = 0.f, dp[CPL], du[CPL];
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) {
+        const float u = vv[j] + et[j];
+        gpart = fmaf(go[j] * u, sp[j], gpart);
+        dp[j] = go[j] * u * at;
+        du[j] = go[j] * sp[j] * at;
+      }
+      const float g = group_sum<LPH>(gpart);
+      rho = fmaf(at, g, rho);
+      store_row<CPL>(a.dproj + static_cast<int64_t>(t) * D + c0, act, dp);
+      if (per_trip) {
+        store_row<CPL>(a.d_edge + static_cast<int64_t>(t) * D + c0, act, du);
+      } else {
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) edacc[j] += du[j];
+      }
+      if (leader) a.dlogit[static_cast<int64_t>(t) * H + head] = g;
+    }
+    // pass 2: dlogit = a (g - rho); dq, and the key part of the edge gradient
+    for (int t = t0; t < t1; ++t) {
+      const int64_t s = a.tidx[t];
+      float kk[CPL], et[CPL];
+      load_row<CPL>(a.k + s * D + c0, act, kk);
+      if (per_trip) {
+        load_row<CPL>(a.edge + static_cast<int64_t>(t) * D + c0, act, et);
+      } else {
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) et[j] = ed[j];
+      }
+      const float at = act ? expf(a.alpha[static_cast<int64_t>(t) * H + head] - mx) * inv : 0.f;
+      // only the leader lane wrote g for this head: read it back in that lane, then broadcast
+      const float g = group_sum<LPH>(leader ? a.dlogit[static_cast<int64_t>(t) * H + head] : 0.f);
+      const float dl = at * (g - rho);
+      const float ds = dl / a.sqrt_c;
+      float dk[CPL];
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) {
+        dqa[j] = fmaf(ds, kk[j] + et[j], dqa[j]);
+        dk[j] = ds * qv[j];
+      }
+      if (per_trip) {
+        float cur[CPL];
+        load_row<CPL>(a.d_edge + static_cast<int64_t>(t) * D + c0, act, cur);
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) cur[j] += dk[j];
+        store_row<CPL>(a.d_edge + static_cast<int64_t>(t) * D + c0, act, cur);
+      } else {
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) edacc[j] += dk[j];
+      }
+      if (leader) a.dlogit[static_cast<int64_t>(t) * H + head] = dl;
+    }
+    store_row<CPL>(a.dq + e * D + c0, act, dqa);
+    if (per_dst) store_row<CPL>(a.d_edge + e * D + c0, act, edacc);
+  }
+}
+
+// ------------------------------------------------------------------------------ backward (src)
+template <int CPL, int LPH>
+__global__ void __launch_bounds__(256) attn_bwd_src_kernel(AttnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int D = a.D, H = a.H;
+  const bool act = lane * CPL < D;
+  const int c0 = act ? lane * CPL : 0;
+  const int head = lane / LPH;
+  float wr[CPL][kS], br[CPL];
+  load_weights<CPL>(a, c0, act, wr, br);
+  const int nwaves = gridDim.x * kAttnWaves;
+  for (int64_t s = wave_id_global(); s < a.E; s += nwaves) {
+    const int p0 = a.rowptr[s], p1 = a.rowptr[s + 1];
+    float dka[CPL], dva[CPL];
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      dka[j] = 0.f;
+      dva[j] = 0.f;
+    }
+    for (int p = p0; p < p1; ++p) {
+      const int64_t t = a.tidx[p];
+      const int64_t e = a.tdst[t];
+      float go[CPL], qv[CPL], sp[CPL];
+      load_row<CPL>(a.dout + e * D + c0, act, go);
+      load_row<CPL>(a.q + e * D + c0, act, qv);
+      float at = 0.f, dl = 0.f;
+      if (act) {
+        const float mx = a.smax[e * H + head];
+        const float inv = 1.0f / (a.sden[e * H + head] + kSoftmaxEps);
+        at = expf(a.alpha[t * H + head] - mx) * inv;
+        dl = a.dlogit_in[t * H + head];
+      }
+      sbf_project<CPL>(wr, br, a.sbf + t * kS, sp);
+      const float ds = dl / a.sqrt_c;
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) {
+        dva[j] = fmaf(go[j] * sp[j], at, dva[j]);
+        dka[j] = fmaf(ds, qv[j], dka[j]);
+      }
+    }
+    store_row<CPL>(a.dk + s * D + c0, act, dka);
+    store_row<CPL>(a.dv + s * D + c0, act, dva);
+  }
+}
+
+// ------------------------------------------------------------------------------ dispatch
+enum class Pass { kFwd, kBwdDst, kBwdSrc };
+
+template <int CPL, int LPH>
+void launch_one(Pass pass, const AttnArgs& a, unsigned blocks, hipStream_t st) {
+  switch (pass) {
+    case Pass::kFwd: attn_fwd_kernel<CPL, LPH><<<blocks, 256, 0, st>>>(a); break;
+    case Pass::kBwdDst: attn_bwd_dst_kernel<CPL, LPH><<<blocks, 256, 0, st>>>(a); break;
+    case Pass::kBwdSrc: attn_bwd_src_kernel<CPL, LPH><<<blocks, 256, 0, st>>>(a); break;
+  }
+}
+
+template <int CPL>
+int launch_cpl(Pass pass, const AttnArgs& a, int lph, unsigned blocks, hipStream_t st) {
+  switch (lph) {
+    case 1: if (CPL >= 4) { launch_one<CPL, 1>(pass, a, blocks, st); return X2G_OK; } break;
+    case 2: launch_one<CPL, 2>(pass, a, blocks, st); return X2G_OK;
+    case 4: launch_one<CPL, 4>(pass, a, blocks, st); return X2G_OK;
+    case 8: launch_one<CPL, 8>(pass, a, blocks, st); return X2G_OK;
+    case 16: if (CPL == 1) { launch_one<CPL, 16>(pass, a, blocks, st); return X2G_OK; } break;
+    default: break;
+  }
+  return X2G_EUNSUPPORTED;
+}
+
+int dispatch(Pass pass, AttnArgs a, int heads, int channels, int sbf_dim, hipStream_t st) {
+  if (a.E < 0 || heads <= 0 || channels <= 0) return X2G_EINVAL;
+  if (sbf_dim != kS) return X2G_EUNSUPPORTED;
+  const int D = heads * channels;
+  int cpl;
+  if (D == 32 || D == 64) cpl = 1;
+  else if (D == 128) cpl = 2;
+  else if (D == 256) cpl = 4;
+  else return X2G_EUNSUPPORTED;
+  if (channels % cpl) return X2G_EUNSUPPORTED;
+  const int lph = channels / cpl;
+  if (lph > 64 || (lph & (lph - 1))) return X2G_EUNSUPPORTED;
+  a.D = D;
+  a.H = heads;
+  a.sqrt_c = static_cast<float>(sqrt(static_cast<double>(channels)));
+  if (a.E == 0) return X2G_OK;
+  int64_t want = (a.E + kAttnWaves - 1) / kAttnWaves;
+  const unsigned blocks = static_cast<unsigned>(want < kMaxBlocks ? want : kMaxBlocks);
+  int rc;
+  switch (cpl) {
+    case 1: rc = launch_cpl<1>(pass, a, lph, blocks, st); break;
+    case 2: rc = launch_cpl<2>(pass, a, lph, blocks, st); break;
+    default: rc = launch_cpl<4>(pass, a, lph, blocks, st); break;
+  }
+  if (rc) return rc;
+  return last_launch_status();
+}
+
+}  // namespace x2g
+
+using namespace x2g;
+
+X2G_API int x2g_sbf_attention_fwd(const float* q, const float* k, const float* v, const float* skip,
+                                  const float* edge, const int32_t* edge_row, int edge_mode, const float* sbf,
+                                  const float* w_sbf, const float* b_sbf, const int32_t* trip_rowptr,
+                                  const int32_t* trip_src, int64_t E, int64_t T, int32_t heads,
+                                  int32_t channels, int32_t sbf_dim, float* out, float* alpha_raw,
+                                  float* seg_max, float* seg_den, void* stream) {
+  if (E > 0 && (!q || !k || !v || !skip || !sbf || !w_sbf || !b_sbf || !trip_rowptr || !out || !seg_max ||
+                !seg_den))
+    return X2G_EINVAL;
+  if (T > 0 && (!trip_src || !alpha_raw)) return X2G_EINVAL;
+  if (edge_mode != X2G_EDGE_NONE && !edge) return X2G_EINVAL;
+  AttnArgs a{};
+  a.q = q; a.k = k; a.v = v; a.skip = skip; a.edge = edge; a.edge_row = edge_row; a.edge_mode = edge_mode;
+  a.sbf = sbf; a.w = w_sbf; a.b = b_sbf; a.rowptr = trip_rowptr; a.tidx = trip_src; a.E = E;
+  a.out = out; a.alpha_out = alpha_raw; a.smax_out = seg_max; a.sden_out = seg_den;
+  return dispatch(Pass::kFwd, a, heads, channels, sbf_dim, as_stream(stream));
+}
+
+X2G_API int x2g_sbf_attention_bwd_dst(const float* q, const float* k, const float* v, const float* edge,
+                                      const int32_t* edge_row, int edge_mode, const float* sbf,
+                                      const float* w_sbf, const float* b_sbf, const int32_t* trip_rowptr,
+                                      const int32_t* trip_src, const float* alpha_raw, const float* seg_max,
+                                      const float* seg_den, const float* dout, int64_t E, int64_t T,
+                                      int32_t heads, int32_t channels, int32_t sbf_dim, float* dq,
+                                      float* d_edge, float* dlogit, float* d_sbfproj, void* stream) {
+  if (E > 0 && (!q || !k || !v || !sbf || !w_sbf || !b_sbf || !trip_rowptr || !seg_max || !seg_den || !dout ||
+                !dq))
+    return X2G_EINVAL;
+  if (T > 0 && (!trip_src || !alpha_raw || !dlogit || !d_sbfproj)) return X2G_EINVAL;
+  if (edge_mode != X2G_EDGE_NONE && (!edge || !d_edge)) return X2G_EINVAL;
+  AttnArgs a{};
+  a.q = q; a.k = k; a.v = v; a.edge = edge; a.edge_row = edge_row; a.edge_mode = edge_mode;
+  a.sbf = sbf; a.w = w_sbf; a.b = b_sbf; a.rowptr = trip_rowptr; a.tidx = trip_src; a.alpha = alpha_raw;
+  a.smax = seg_max; a.sden = seg_den; a.dout = dout; a.E = E;
+  a.dq = dq; a.d_edge = d_edge; a.dlogit = dlogit; a.dproj = d_sbfproj;
+  return dispatch(Pass::kBwdDst, a, heads, channels, sbf_dim, as_stream(stream));
+}
+
+X2G_API int x2g_sbf_attention_bwd_src(const float* q, const float* sbf, const float* w_sbf, const float* b_sbf,
+                                      const int32_t* src_rowptr, const int32_t* src_perm, const int32_t* trip_dst,
+                                      const float* alpha_raw, const float* seg_max, const float* seg_den,
+                                      const float* dlogit, const float* dout, int64_t E, int64_t T,
+                                      int32_t heads, int32_t channels, int32_t sbf_dim, float* dk, float* dv,
+                                      void* stream) {
+  if (E > 0 && (!q || !sbf || !w_sbf || !b_sbf || !src_rowptr || !seg_max || !seg_den || !dout || !dk || !dv))
+    return X2G_EINVAL;
+  if (T > 0 && (!src_perm || !trip_dst || !alpha_raw || !dlogit)) return X2G_EINVAL;
+  AttnArgs a{};
+  a.q = q; a.sbf = sbf; a.w = w_sbf; a.b = b_sbf; a.rowptr = src_rowptr; a.tidx = src_perm; a.tdst = trip_dst;
+  a.alpha = alpha_raw; a.smax = seg_max; a.sden = seg_den; a.dlogit_in = dlogit; a.dout = dout; a.E = E;
+  a.dk = dk; a.dv = dv;
+  return dispatch(Pass::kBwdSrc, a, heads, channels, sbf_dim, as_stream(stream));
+}

@@ -1,0 +1,291 @@
+// Line-graph (triplet) construction on the device.
+//
+// Replaces vertex_to_edge_2 (edge_graph.py:12-30), which the reference runs on the CPU with
+// scipy on every forward (xgnn.py:52-53: a D2H copy of edge_index, scipy CSR slicing, an H2D
+// copy of the triplets).  Here it is count -> exclusive scan -> emit, all integer work, with
+// sizes from host metadata so nothing is read back.
+//
+// Ordering contract (the reference's): triplets are grouped by destination line node
+// e=(a->b) in edge order, and inside a group k ascends (scipy CSR rows are column-sorted).
+// With edges sorted by (src, dst) -- np.argwhere order, atom_graph.py:42-45 -- the edges out
+// of atom b are the contiguous range atom_rowptr[b]..atom_rowptr[b+1] in ascending k, and the
+// id of edge (b->k) is its position in that range.
+#include "common.hpp"
+
+namespace x2g {
+
+// ----------------------------------------------------------------------------- CSR row ptr
+__global__ void rowptr_kernel(const int32_t* __restrict__ keys, int64_t n, int64_t n_seg,
+                              int32_t* __restrict__ rowptr) {
+  int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  int64_t prev = (i == 0) ? -1 : keys[i - 1];
+  int64_t cur = (i == n) ? n_seg : keys[i];
+  if (prev < -1) prev = -1;  // out-of-range keys never write outside rowptr
+  if (cur > n_seg) cur = n_seg;
+  for (int64_t s = prev + 1; s <= cur; ++s) rowptr[s] = static_cast<int32_t>(i);
+}
+
+// ----------------------------------------------------------------------------- exclusive scan
+// Three-phase scan of int32 counts: 1024 elements per 256-thread block, block totals scanned
+// by one block, then offsets added.  out has n+1 entries (out[n] = total).
+constexpr int kScanThreads = 256;
+constexpr int kScanPerThread = 4;
+constexpr int kScanTile = kScanThreads * kScanPerThread;
+
+__device__ __forceinline__ int block_exclusive_scan(int v, int* lds_wave, int* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int incl = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    int y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) lds_wave[wave] = incl;
+  __syncthreads();
+  int wave_off = 0, tot = 0;
+  const int nw = blockDim.x >> 6;
+  for (int w = 0; w < nw; ++w) {
+    int s = lds_wave[w];
+    if (w < wave) wave_off += s;
+    tot += s;
+  }
+  *total = tot;
+  __syncthreads();
+  return wave_off + incl - v;
+}
+
+__global__ void __launch_bounds__(kScanThreads) scan_tiles(const int32_t* __restrict__ in, int64_t n,
+                                                           int32_t* __restrict__ out,
+                                                           int32_t* __restrict__ partial) {
+  __shared__ int lds[kScanThreads / 64];
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kScanTile + threadIdx.x * kScanPerThread;
+  int v[kScanPerThread];
+  int sum = 0;
+#pragma unroll
+  for (int i = 0; i < kScanPerThread; ++i) {
+    v[i] = (base + i < n) ? in[base + i] : 0;
+    sum += v[i];
+  }
+  int total;
+  int run = block_exclusive_scan(sum, lds, &total);
+#pragma unroll
+  for (int i = 0; i < kScanPerThread; ++i) {
+    if (base + i < n) out[base + i] = run;
+    run += v[i];
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = total;
+}
+
+// One block: exclusive scan of the tile totals in place; partial[nb] = grand total.
+__global__ void __launch_bounds__(1024) scan_partials(int32_t* __restrict__ partial, int64_t nb) {
+  __shared__ int lds[1024 / 64];
+  int carry = 0;
+  for (int64_t c = 0; c < nb; c += blockDim.x) {
+    int64_t i = c + threadIdx.x;
+    int v = (i < nb) ? partial[i] : 0;
+    int total;
+    int ex = block_exclusive_scan(v, lds, &total);
+    if (i < nb) partial[i] = carry + ex;
+    carry += total;
+  }
+  if (threadIdx.x == 0) partial[nb] = carry;
+}
+
+__global__ void scan_add(int32_t* __restrict__ out, int64_t n, const int32_t* __restrict__ partial,
+                         int64_t nb) {
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kScanTile;
+  const int off = partial[blockIdx.x];
+  for (int i = threadIdx.x; i < kScanTile; i += blockDim.x)
+    if (base + i < n) out[base + i] += off;
+  if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = partial[nb];
+}
+
+inline int64_t scan_partials_ints(int64_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
+
+int exclusive_scan(const int32_t* in, int64_t n, int32_t* out, int32_t* partial, hipStream_t st) {
+  const int64_t nb = (n + kScanTile - 1) / kScanTile;
+  if (nb == 0) {
+    const hipError_t e = hipMemsetAsync(out, 0, sizeof(int32_t), st);
+    return e == hipSuccess ? X2G_OK : static_cast<int>(e);
+  }
+  scan_tiles<<<static_cast<unsigned>(nb), kScanThreads, 0, st>>>(in, n, out, partial);
+  scan_partials<<<1, 1024, 0, st>>>(partial, nb);
+  scan_add<<<static_cast<unsigned>(nb), kScanThreads, 0, st>>>(out, n, partial, nb);
+  return last_launch_status();
+}
+
+// ----------------------------------------------------------------------------- triplets
+__device__ __forceinline__ int lower_bound(const int32_t* __restrict__ a, int lo, int hi, int key) {
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (a[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// count[e] = |N_out(b) \ {a}| for e = (a->b)
+__global__ void triplet_count_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                                     const int32_t* __restrict__ atom_rowptr, int64_t E,
+                                     int32_t* __restrict__ count) {
+  int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int a = src[e], b = dst[e];
+  const int lo = atom_rowptr[b], hi = atom_rowptr[b + 1];
+  const int p = lower_bound(dst, lo, hi, a);
+  const int has_rev = (p < hi && dst[p] == a) ? 1 : 0;
+  count[e] = hi - lo - has_rev;
+}
+
+// Emit the triplets of 8 destination edges per wave: lane group of 8 walks N_out(b) in
+// chunks of 8, compacts with a ballot so writes of one group are contiguous.
+constexpr int kEmitGroup = 8;
+__global__ void triplet_emit_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                                    const int32_t* __restrict__ atom_rowptr,
+                                    const int32_t* __restrict__ trip_rowptr, int64_t E, int64_t T,
+                                    int32_t* __restrict__ trip_src, int32_t* __restrict__ trip_dst,
+                                    int32_t* __restrict__ atom_j, int32_t* __restrict__ atom_i,
+                                    int32_t* __restrict__ atom_k) {
+  const int64_t gtid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t e = gtid / kEmitGroup;
+  const int sub = threadIdx.x & (kEmitGroup - 1);
+  const int lane = threadIdx.x & 63;
+  const uint64_t group_mask = ((1ull << kEmitGroup) - 1) << (lane & ~(kEmitGroup - 1));
+  const bool valid = e < E;
+  int a = 0, b = 0, lo = 0, hi = 0, p = 0;
+  if (valid) {
+    a = src[e];
+    b = dst[e];
+    lo = atom_rowptr[b];
+    hi = atom_rowptr[b + 1];
+    p = trip_rowptr[e];
+  }
+  // loop until every group in the wave is done (wave-uniform trip count via __any)
+  for (int base = lo; __any(valid && base < hi); base += kEmitGroup) {
+    const int idx = base + sub;
+    const bool in = valid && idx < hi;
+    const int k = in ? dst[idx] : -1;
+    const bool keep = in && k != a;
+    const uint64_t ball = __ballot(keep) & group_mask;
+    const uint64_t below = ball & ((1ull << lane) - 1);
+    const int q = p + __popcll(below);
+    if (keep && q < T) {  // q >= T only if the host-provided T is too small: never write past it
+      trip_src[q] = idx;
+      trip_dst[q] = static_cast<int32_t>(e);
+      if (atom_j) atom_j[q] = b;
+      if (atom_i) atom_i[q] = a;
+      if (atom_k) atom_k[q] = k;
+    }
+    p += __popcll(ball);
+  }
+}
+
+// ----------------------------------------------------------------------------- transpose
+__global__ void count_by_key(const int32_t* __restrict__ keys, int64_t n, int32_t* __restrict__ count) {
+  int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) atomicAdd(&count[keys[i]], 1);
+}
+
+__global__ void fill_by_key(const int32_t* __restrict__ keys, int64_t n, const int32_t* __restrict__ rowptr,
+                            int32_t* __restrict__ cursor, int32_t* __restrict__ perm) {
+  int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int s = keys[i];
+  const int pos = atomicAdd(&cursor[s], 1);
+  perm[rowptr[s] + pos] = static_cast<int32_t>(i);
+}
+
+// The atomic fill leaves each segment in arrival order; sort it (segments are short:
+// the in-degree of one atom) so the result, and every float sum over it, is deterministic.
+__global__ void sort_segments(const int32_t* __restrict__ rowptr, int64_t n_seg, int32_t* __restrict__ perm) {
+  int64_t s = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (s >= n_seg) return;
+  const int lo = rowptr[s], hi = rowptr[s + 1];
+  for (int i = lo + 1; i < hi; ++i) {
+    const int v = perm[i];
+    int j = i - 1;
+    while (j >= lo && perm[j] > v) {
+      perm[j + 1] = perm[j];
+      --j;
+    }
+    perm[j + 1] = v;
+  }
+}
+
+}  // namespace x2g
+
+using namespace x2g;
+
+X2G_API int x2g_abi_version(void) { return 1; }
+
+X2G_API const char* x2g_status_string(int status) {
+  switch (status) {
+    case X2G_OK: return "ok";
+    case X2G_EINVAL: return "X2G_EINVAL: bad size or null pointer";
+    case X2G_EUNSUPPORTED: return "X2G_EUNSUPPORTED: shape outside the compiled kernel set";
+    case X2G_EWORKSPACE: return "X2G_EWORKSPACE: workspace too small";
+    default: return hipGetErrorString(static_cast<hipError_t>(status));
+  }
+}
+
+X2G_API int x2g_csr_rowptr(const int32_t* keys, int64_t n, int64_t n_seg, int32_t* rowptr, void* stream) {
+  if (n < 0 || n_seg < 0 || !rowptr || (n > 0 && !keys)) return X2G_EINVAL;
+  rowptr_kernel<<<blocks_for(n + 1, 256), 256, 0, as_stream(stream)>>>(keys, n, n_seg, rowptr);
+  return last_launch_status();
+}
+
+X2G_API size_t x2g_vertex_to_edge_workspace(int64_t num_edges, int64_t num_nodes) {
+  const int64_t n = num_edges > num_nodes ? num_edges : num_nodes;
+  // counts/cursor [n] + scan partials, 256-byte aligned
+  const int64_t ints = 2 * (n + 64) + scan_partials_ints(n + 1) + 64;
+  return static_cast<size_t>(ints) * sizeof(int32_t);
+}
+
+X2G_API int x2g_vertex_to_edge(const int32_t* edge_src, const int32_t* edge_dst, int64_t E, int64_t N,
+                               int64_t T, int32_t* atom_rowptr, int32_t* trip_rowptr, int32_t* trip_src,
+                               int32_t* trip_dst, int32_t* atom_j, int32_t* atom_i, int32_t* atom_k,
+                               void* workspace, size_t workspace_bytes, void* stream) {
+  if (E < 0 || N < 0 || T < 0 || !atom_rowptr || !trip_rowptr) return X2G_EINVAL;
+  if (E > 0 && (!edge_src || !edge_dst)) return X2G_EINVAL;
+  if (T > 0 && (!trip_src || !trip_dst)) return X2G_EINVAL;
+  if (workspace_bytes < x2g_vertex_to_edge_workspace(E, N) || !workspace) return X2G_EWORKSPACE;
+  hipStream_t st = as_stream(stream);
+  int32_t* count = static_cast<int32_t*>(workspace);
+  const int64_t n = E > N ? E : N;
+  int32_t* partial = count + 2 * (n + 64);
+  int rc = x2g_csr_rowptr(edge_src, E, N, atom_rowptr, stream);
+  if (rc) return rc;
+  if (E > 0) {
+    triplet_count_kernel<<<blocks_for(E, 256), 256, 0, st>>>(edge_src, edge_dst, atom_rowptr, E, count);
+    if ((rc = last_launch_status())) return rc;
+  }
+  if ((rc = exclusive_scan(count, E, trip_rowptr, partial, st))) return rc;
+  if (E > 0) {
+    triplet_emit_kernel<<<blocks_for(E * kEmitGroup, 256), 256, 0, st>>>(
+        edge_src, edge_dst, atom_rowptr, trip_rowptr, E, T, trip_src, trip_dst, atom_j, atom_i, atom_k);
+  }
+  return last_launch_status();
+}
+
+X2G_API int x2g_line_graph_transpose(const int32_t* trip_src, int64_t T, int64_t E, int32_t* src_rowptr,
+                                     int32_t* src_perm, void* workspace, size_t workspace_bytes, void* stream) {
+  if (T < 0 || E < 0 || !src_rowptr || (T > 0 && (!trip_src || !src_perm))) return X2G_EINVAL;
+  if (workspace_bytes < x2g_vertex_to_edge_workspace(E, 0) || !workspace) return X2G_EWORKSPACE;
+  hipStream_t st = as_stream(stream);
+  int32_t* count = static_cast<int32_t*>(workspace);
+  int32_t* cursor = count + (E + 64);
+  int32_t* partial = count + 2 * (E + 64);
+  int rc;
+  const hipError_t me = hipMemsetAsync(count, 0, sizeof(int32_t) * (2 * (E + 64)), st);
+  if (me != hipSuccess) return static_cast<int>(me);
+  if (T > 0) {
+    count_by_key<<<blocks_for(T, 256), 256, 0, st>>>(trip_src, T, count);
+    if ((rc = last_launch_status())) return rc;
+  }
+  if ((rc = exclusive_scan(count, E, src_rowptr, partial, st))) return rc;
+  if (T > 0) {
+    fill_by_key<<<blocks_for(T, 256), 256, 0, st>>>(trip_src, T, src_rowptr, cursor, src_perm);
+    sort_segments<<<blocks_for(E, 256), 256, 0, st>>>(src_rowptr, E, src_perm);
+  }
+  return last_launch_status();
+}

@@ -1,0 +1,341 @@
+// CSR segmented reductions: scatter-add, its adjoint broadcast, segment softmax, graph LayerNorm.
+//
+// These replace the torch_scatter 2.1.0 / PyG 2.1.0 operators X2-GNN reaches with sorted
+// indices: scatter_add over edges by source atom (readout.py:37, AtomWise) and over atoms by
+// molecule (model.py:190, the global add pool), scatter_mean (readout.py:69, MolWise),
+// utils.softmax and nn.LayerNorm(mode='graph') (model.py:183).  Because every index here is
+// sorted, each destination row is a contiguous segment [rowptr[g], rowptr[g+1]) and the sum
+// is a fixed-order in-register reduction: no atomics, bitwise reproducible.
+#include <math.h>
+
+#include "common.hpp"
+
+namespace x2g {
+
+constexpr int kSegWaves = 4;
+constexpr unsigned kSegMaxBlocks = 4096;
+
+__device__ __forceinline__ float4 f4_fma(float4 a, float4 b, float4 c) {
+  return make_float4(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y), fmaf(a.z, b.z, c.z), fmaf(a.w, b.w, c.w));
+}
+__device__ __forceinline__ float4 f4_add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float4 f4_mul(float4 a, float4 b) {
+  return make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w);
+}
+__device__ __forceinline__ float4 f4_shfl_xor(float4 v, int off) {
+  return make_float4(__shfl_xor(v.x, off, 64), __shfl_xor(v.y, off, 64), __shfl_xor(v.z, off, 64),
+                     __shfl_xor(v.w, off, 64));
+}
+
+// ------------------------------------------------------------------------------ segment sum
+// One wave per segment (grid-stride).  LPR = D/4 lanes cover a row with 16-byte loads, so a
+// wave-instruction reads RPI = 64/LPR whole rows (D=128: two 512 B rows = 1 KiB); each lane
+// keeps UNROLL loads in flight, then the RPI partial rows are folded with xor shuffles.
+template <int LPR, bool MUL>
+__global__ void __launch_bounds__(256) seg_sum_vec(const float4* __restrict__ x, const float4* __restrict__ mul,
+                                                   const int32_t* __restrict__ rowptr, int64_t G,
+                                                   float4* __restrict__ out) {
+  constexpr int RPI = 64 / LPR;
+  constexpr int UNROLL = 4;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane % LPR, slot = lane / LPR;
+  const int nwaves = gridDim.x * kSegWaves;
+  for (int64_t g = uniform(blockIdx.x * kSegWaves + (threadIdx.x >> 6)); g < G; g += nwaves) {
+    const int r0 = rowptr[g], r1 = rowptr[g + 1];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int r = r0 + slot;
+    for (; r + (UNROLL - 1) * RPI < r1; r += UNROLL * RPI) {
+      float4 v[UNROLL], w[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const int64_t idx = static_cast<int64_t>(r + u * RPI) * LPR + sub;
+        v[u] = x[idx];
+        if (MUL) w[u] = mul[idx];
+      }
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) acc = MUL ? f4_fma(v[u], w[u], acc) : f4_add(acc, v[u]);
+    }
+    for (; r < r1; r += RPI) {
+      const int64_t idx = static_cast<int64_t>(r) * LPR + sub;
+      acc = MUL ? f4_fma(x[idx], mul[idx], acc) : f4_add(acc, x[idx]);
+    }
+#pragma unroll
+    for (int off = LPR; off < 64; off <<= 1) acc = f4_add(acc, f4_shfl_xor(acc, off));
+    if (slot == 0) out[g * LPR + sub] = acc;
+  }
+}
+
+// Any width: one thread per (segment, column), sequential over the segment's rows.
+template <bool MUL>
+__global__ void seg_sum_scalar(const float* __restrict__ x, const float* __restrict__ mul,
+                               const int32_t* __restrict__ rowptr, int64_t G, int64_t D, float* __restrict__ out) {
+  const int64_t gid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (gid >= G * D) return;
+  const int64_t g = gid / D, c = gid - g * D;
+  float acc = 0.f;
+  for (int64_t r = rowptr[g]; r < rowptr[g + 1]; ++r)
+    acc = MUL ? fmaf(x[r * D + c], mul[r * D + c], acc) : acc + x[r * D + c];
+  out[gid] = acc;
+}
+
+// ------------------------------------------------------------------------------ broadcast (adjoint)
+template <int LPR, bool MUL>
+__global__ void __launch_bounds__(256) seg_bcast_vec(const float4* __restrict__ g_in, const float4* __restrict__ mul,
+                                                     const int32_t* __restrict__ rowptr, int64_t G,
+                                                     float4* __restrict__ out) {
+  constexpr int RPI = 64 / LPR;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane % LPR, slot = lane / LPR;
+  const int nwaves = gridDim.x * kSegWaves;
+  for (int64_t g = uniform(blockIdx.x * kSegWaves + (threadIdx.x >> 6)); g < G; g += nwaves) {
+    const int r0 = rowptr[g], r1 = rowptr[g + 1];
+    if (r0 == r1) continue;
+    const float4 gv = g_in[g * LPR + sub];
+    for (int r = r0 + slot; r < r1; r += RPI) {
+      const int64_t idx = static_cast<int64_t>(r) * LPR + sub;
+      out[idx] = MUL ? f4_mul(gv, mul[idx]) : gv;
+    }
+  }
+}
+
+template <bool MUL>
+__global__ void seg_bcast_scalar(const float* __restrict__ g_in, const float* __restrict__ mul,
+                                 const int32_t* __restrict__ rowptr, int64_t G, int64_t D, float* __restrict__ out) {
+  const int64_t gid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (gid >= G * D) return;
+  const int64_t g = gid / D, c = gid - g * D;
+  const float gv = g_in[gid];
+  for (int64_t r = rowptr[g]; r < rowptr[g + 1]; ++r) out[r * D + c] = MUL ? gv * mul[r * D + c] : gv;
+}
+
+unsigned seg_grid(int64_t G) {
+  const int64_t want = (G + kSegWaves - 1) / kSegWaves;
+  return static_cast<unsigned>(want < kSegMaxBlocks ? want : kSegMaxBlocks);
+}
+
+template <bool MUL>
+int seg_sum_launch(const float* x, const float* mul, const int32_t* rowptr, int64_t G, int64_t D, float* out,
+                   hipStream_t st) {
+  const auto* xv = reinterpret_cast<const float4*>(x);
+  const auto* mv = reinterpret_cast<const float4*>(mul);
+  auto* ov = reinterpret_cast<float4*>(out);
+  const unsigned grid = seg_grid(G);
+  const bool aligned = (reinterpret_cast<uintptr_t>(x) % 16 == 0) && (reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
+                       (!MUL || reinterpret_cast<uintptr_t>(mul) % 16 == 0);
+  switch (aligned ? D : -1) {
+    case 4: seg_sum_vec<1, MUL><<<grid, 256, 0, st>>>(xv, mv, rowptr, G, ov); break;
+    case 8: seg_sum_vec<2, MUL><<<grid, 256, 0, st>>>(xv, mv, rowptr, G, ov); break;
+    case 16: seg_sum_vec<4, MUL><<<grid, 256, 0, st>>>(xv, mv, rowptr, G, ov); break;
+    case 32: seg_sum_vec<8, MUL><<<grid, 256, 0, st>>>(xv, mv, rowptr, G, ov); break;
+    case 64: seg_sum_vec<16, MUL><<<grid, 256, 0, st>>>(xv, mv, rowptr, G, ov); break;
+    case 128: seg_sum_vec<32, MUL><<<grid, 256, 0, st>>>(xv, mv, rowptr, G, ov); break;
+    case 256: seg_sum_vec<64, MUL><<<grid, 256, 0, st>>>(xv, mv, rowptr, G, ov); break;
+    default: seg_sum_scalar<MUL><<<blocks_for(G * D, 256), 256, 0, st>>>(x, mul, rowptr, G, D, out); break;
+  }
+  return last_launch_status();
+}
+
+template <bool MUL>
+int seg_bcast_launch(const float* g, const float* mul, const int32_t* rowptr, int64_t G, int64_t D, float* out,
+                     hipStream_t st) {
+  const auto* gv = reinterpret_cast<const float4*>(g);
+  const auto* mv = reinterpret_cast<const float4*>(mul);
+  auto* ov = reinterpret_cast<float4*>(out);
+  const unsigned grid = seg_grid(G);
+  const bool aligned = (reinterpret_cast<uintptr_t>(g) % 16 == 0) && (reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
+                       (!MUL || reinterpret_cast<uintptr_t>(mul) % 16 == 0);
+  switch (aligned ? D : -1) {
+    case 4: seg_bcast_vec<1, MUL><<<grid, 256, 0, st>>>(gv, mv, rowptr, G, ov); break;
+    case 8: seg_bcast_vec<2, MUL><<<grid, 256, 0, st>>>(gv, mv, rowptr, G, ov); break;
+    case 16: seg_bcast_vec<4, MUL><<<grid, 256, 0, st>>>(gv, mv, rowptr, G, ov); break;
+    case 32: seg_bcast_vec<8, MUL><<<grid, 256, 0, st>>>(gv, mv, rowptr, G, ov); break;
+    case 64: seg_bcast_vec<16, MUL><<<grid, 256, 0, st>>>(gv, mv, rowptr, G, ov); break;
+    case 128: seg_bcast_vec<32, MUL><<<grid, 256, 0, st>>>(gv, mv, rowptr, G, ov); break;
+    case 256: seg_bcast_vec<64, MUL><<<grid, 256, 0, st>>>(gv, mv, rowptr, G, ov); break;
+    default: seg_bcast_scalar<MUL><<<blocks_for(G * D, 256), 256, 0, st>>>(g, mul, rowptr, G, D, out); break;
+  }
+  return last_launch_status();
+}
+
+// ------------------------------------------------------------------------------ segment softmax
+__global__ void seg_softmax_fwd_kernel(const float* __restrict__ src, const int32_t* __restrict__ rowptr,
+                                       int64_t G, int64_t H, float* __restrict__ out) {
+  const int64_t gid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (gid >= G * H) return;
+  const int64_t g = gid / H, h = gid - g * H;
+  const int64_t r0 = rowptr[g], r1 = rowptr[g + 1];
+  float mx = -INFINITY;
+  for (int64_t r = r0; r < r1; ++r) mx = fmaxf(mx, src[r * H + h]);
+  float sum = 0.f;
+  for (int64_t r = r0; r < r1; ++r) sum += expf(src[r * H + h] - mx);
+  const float den = sum + 1e-16f;
+  for (int64_t r = r0; r < r1; ++r) out[r * H + h] = expf(src[r * H + h] - mx) / den;
+}
+
+__global__ void seg_softmax_bwd_kernel(const float* __restrict__ out, const float* __restrict__ dout,
+                                       const int32_t* __restrict__ rowptr, int64_t G, int64_t H,
+                                       float* __restrict__ dsrc) {
+  const int64_t gid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (gid >= G * H) return;
+  const int64_t g = gid / H, h = gid - g * H;
+  const int64_t r0 = rowptr[g], r1 = rowptr[g + 1];
+  float dot = 0.f;
+  for (int64_t r = r0; r < r1; ++r) dot = fmaf(out[r * H + h], dout[r * H + h], dot);
+  for (int64_t r = r0; r < r1; ++r) dsrc[r * H + h] = out[r * H + h] * (dout[r * H + h] - dot);
+}
+
+// ------------------------------------------------------------------------------ graph LayerNorm
+constexpr int kLnThreads = 256;
+
+__device__ __forceinline__ float block_sum(float v, float* lds) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  if (lane == 0) lds[wave] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int w = 0; w < kLnThreads / 64; ++w) s += lds[w];
+  __syncthreads();
+  return s;
+}
+
+// One 256-thread block per segment (molecule); the segment is swept three times (sum,
+// centred sum of squares, write), re-reads served by L2.
+__global__ void __launch_bounds__(kLnThreads) graph_ln_fwd_kernel(const float* __restrict__ x,
+                                                                 const int32_t* __restrict__ rowptr, int64_t D,
+                                                                 float eps, float* __restrict__ out,
+                                                                 float* __restrict__ mean_out,
+                                                                 float* __restrict__ rstd_out) {
+  __shared__ float lds[kLnThreads / 64];
+  const int64_t g = blockIdx.x;
+  const int64_t r0 = rowptr[g], r1 = rowptr[g + 1];
+  const int64_t n = r1 - r0, M = n * D;
+  const float norm = static_cast<float>((n > 0 ? n : 1) * D);
+  const float* xs = x + r0 * D;
+  float* os = out + r0 * D;
+  const bool vec = (D % 4 == 0) && (reinterpret_cast<uintptr_t>(xs) % 16 == 0) &&
+                   (reinterpret_cast<uintptr_t>(os) % 16 == 0);
+  float s = 0.f;
+  if (vec) {
+    for (int64_t i = threadIdx.x; i < M / 4; i += kLnThreads) {
+      const float4 v = reinterpret_cast<const float4*>(xs)[i];
+      s += (v.x + v.y) + (v.z + v.w);
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < M; i += kLnThreads) s += xs[i];
+  }
+  const float mu = block_sum(s, lds) / norm;
+  float q = 0.f;
+  if (vec) {
+    for (int64_t i = threadIdx.x; i < M / 4; i += kLnThreads) {
+      const float4 v = reinterpret_cast<const float4*>(xs)[i];
+      const float a = v.x - mu, b = v.y - mu, c = v.z - mu, d = v.w - mu;
+      q += (a * a + b * b) + (c * c + d * d);
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < M; i += kLnThreads) {
+      const float a = xs[i] - mu;
+      q += a * a;
+    }
+  }
+  const float var = block_sum(q, lds) / norm;
+  const float denom = sqrtf(var + eps);
+  if (vec) {
+    for (int64_t i = threadIdx.x; i < M / 4; i += kLnThreads) {
+      const float4 v = reinterpret_cast<const float4*>(xs)[i];
+      reinterpret_cast<float4*>(os)[i] =
+          make_float4((v.x - mu) / denom, (v.y - mu) / denom, (v.z - mu) / denom, (v.w - mu) / denom);
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < M; i += kLnThreads) os[i] = (xs[i] - mu) / denom;
+  }
+  if (threadIdx.x == 0) {
+    mean_out[g] = mu;
+    rstd_out[g] = 1.0f / denom;
+  }
+}
+
+// dx = rstd * (dy - mean(dy) - y * mean(dy * y)), means over the segment's n*D elements.
+__global__ void __launch_bounds__(kLnThreads) graph_ln_bwd_kernel(const float* __restrict__ y,
+                                                                 const float* __restrict__ dy,
+                                                                 const float* __restrict__ rstd,
+                                                                 const int32_t* __restrict__ rowptr, int64_t D,
+                                                                 float* __restrict__ dx) {
+  __shared__ float lds[kLnThreads / 64];
+  const int64_t g = blockIdx.x;
+  const int64_t r0 = rowptr[g], r1 = rowptr[g + 1];
+  const int64_t n = r1 - r0, M = n * D;
+  if (n == 0) return;
+  const float norm = static_cast<float>(n * D);
+  const float* ys = y + r0 * D;
+  const float* gs = dy + r0 * D;
+  float* xs = dx + r0 * D;
+  float s1 = 0.f, s2 = 0.f;
+  for (int64_t i = threadIdx.x; i < M; i += kLnThreads) {
+    const float gv = gs[i];
+    s1 += gv;
+    s2 = fmaf(gv, ys[i], s2);
+  }
+  const float m1 = block_sum(s1, lds) / norm;
+  const float m2 = block_sum(s2, lds) / norm;
+  const float r = rstd[g];
+  for (int64_t i = threadIdx.x; i < M; i += kLnThreads) xs[i] = r * (gs[i] - m1 - ys[i] * m2);
+}
+
+}  // namespace x2g
+
+using namespace x2g;
+
+X2G_API int x2g_segment_sum(const float* x, const float* mul, const int32_t* rowptr, int64_t G, int64_t D,
+                            float* out, void* stream) {
+  if (G < 0 || D <= 0 || (G > 0 && (!rowptr || !out || !x))) return X2G_EINVAL;
+  if (G == 0) return X2G_OK;
+  hipStream_t st = as_stream(stream);
+  return mul ? seg_sum_launch<true>(x, mul, rowptr, G, D, out, st) : seg_sum_launch<false>(x, mul, rowptr, G, D, out, st);
+}
+
+X2G_API int x2g_segment_broadcast(const float* g, const float* mul, const int32_t* rowptr, int64_t G, int64_t D,
+                                  float* out, void* stream) {
+  if (G < 0 || D <= 0 || (G > 0 && (!rowptr || !out || !g))) return X2G_EINVAL;
+  if (G == 0) return X2G_OK;
+  hipStream_t st = as_stream(stream);
+  return mul ? seg_bcast_launch<true>(g, mul, rowptr, G, D, out, st)
+             : seg_bcast_launch<false>(g, mul, rowptr, G, D, out, st);
+}
+
+X2G_API int x2g_segment_softmax_fwd(const float* src, const int32_t* rowptr, int64_t G, int64_t H, float* out,
+                                    void* stream) {
+  if (G < 0 || H <= 0 || (G > 0 && (!src || !rowptr || !out))) return X2G_EINVAL;
+  if (G == 0) return X2G_OK;
+  seg_softmax_fwd_kernel<<<blocks_for(G * H, 256), 256, 0, as_stream(stream)>>>(src, rowptr, G, H, out);
+  return last_launch_status();
+}
+
+X2G_API int x2g_segment_softmax_bwd(const float* out, const float* dout, const int32_t* rowptr, int64_t G,
+                                    int64_t H, float* dsrc, void* stream) {
+  if (G < 0 || H <= 0 || (G > 0 && (!out || !dout || !rowptr || !dsrc))) return X2G_EINVAL;
+  if (G == 0) return X2G_OK;
+  seg_softmax_bwd_kernel<<<blocks_for(G * H, 256), 256, 0, as_stream(stream)>>>(out, dout, rowptr, G, H, dsrc);
+  return last_launch_status();
+}
+
+X2G_API int x2g_graph_layernorm_fwd(const float* x, const int32_t* rowptr, int64_t G, int64_t D, float eps,
+                                    float* out, float* mean, float* rstd, void* stream) {
+  if (G < 0 || D <= 0 || (G > 0 && (!x || !rowptr || !out || !mean || !rstd))) return X2G_EINVAL;
+  if (G == 0) return X2G_OK;
+  graph_ln_fwd_kernel<<<static_cast<unsigned>(G), kLnThreads, 0, as_stream(stream)>>>(x, rowptr, D, eps, out,
+                                                                                     mean, rstd);
+  return last_launch_status();
+}
+
+X2G_API int x2g_graph_layernorm_bwd(const float* out, const float* dout, const float* rstd, const int32_t* rowptr,
+                                    int64_t G, int64_t D, float* dx, void* stream) {
+  if (G < 0 || D <= 0 || (G > 0 && (!out || !dout || !rstd || !rowptr || !dx))) return X2G_EINVAL;
+  if (G == 0) return X2G_OK;
+  graph_ln_bwd_kernel<<<static_cast<unsigned>(G), kLnThreads, 0, as_stream(stream)>>>(out, dout, rstd, rowptr, D,
+                                                                                     dx);
+  return last_launch_status();
+}

@@ -1,0 +1,84 @@
+"""ctypes binding of libx2g.so (the C ABI declared in include/x2g.h).
+
+The library is loaded after ``torch`` so that it binds to the HIP runtime PyTorch already
+loaded (same soname), and every call is enqueued on PyTorch's current stream.  There is no
+fallback: if the library or a GPU is missing, the product path raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be imported before the HIP library is loaded)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("X2G_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libx2g.so"))
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+_F = ctypes.c_float
+_SZ = ctypes.c_size_t
+
+# name -> argtypes (restype int unless noted); mirrors include/x2g.h
+SIGNATURES = {
+    "x2g_abi_version": [],
+    "x2g_status_string": [ctypes.c_int],
+    "x2g_csr_rowptr": [_P, _I64, _I64, _P, _P],
+    "x2g_vertex_to_edge_workspace": [_I64, _I64],
+    "x2g_vertex_to_edge": [_P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P],
+    "x2g_line_graph_transpose": [_P, _I64, _I64, _P, _P, _P, _SZ, _P],
+    "x2g_bessel_env": [_P, _I64, _F, _P, _P],
+    "x2g_spherical_basis": [_P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P],
+    "x2g_sbf_attention_fwd": [_P, _P, _P, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _I64, _I64, _I32, _I32,
+                              _I32, _P, _P, _P, _P, _P],
+    "x2g_sbf_attention_bwd_dst": [_P, _P, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64,
+                                  _I32, _I32, _I32, _P, _P, _P, _P, _P],
+    "x2g_sbf_attention_bwd_src": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I32, _I32, _I32, _P,
+                                  _P, _P],
+    "x2g_segment_sum": [_P, _P, _P, _I64, _I64, _P, _P],
+    "x2g_segment_broadcast": [_P, _P, _P, _I64, _I64, _P, _P],
+    "x2g_segment_softmax_fwd": [_P, _P, _I64, _I64, _P, _P],
+    "x2g_segment_softmax_bwd": [_P, _P, _P, _I64, _I64, _P, _P],
+    "x2g_graph_layernorm_fwd": [_P, _P, _I64, _I64, _F, _P, _P, _P, _P],
+    "x2g_graph_layernorm_bwd": [_P, _P, _P, _P, _I64, _I64, _P, _P],
+}
+RESTYPES = {"x2g_status_string": ctypes.c_char_p, "x2g_vertex_to_edge_workspace": _SZ}
+
+_lib = None
+
+
+def load():
+    """Load libx2g.so and declare every entry point (raises if the library is missing)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libx2g.so not found at {LIB_PATH}: build it (make -C x2-gnn_amd) first")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, args in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = RESTYPES.get(name, ctypes.c_int)
+        _lib = lib
+    return _lib
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def check(rc: int, name: str):
+    if rc != 0:
+        msg = load().x2g_status_string(rc).decode()
+        raise RuntimeError(f"{name} failed with status {rc}: {msg}")
+
+
+def call(name: str, *args):
+    check(getattr(load(), name)(*args), name)

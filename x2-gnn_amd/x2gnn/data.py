@@ -1,0 +1,155 @@
+"""Minimal PyG-compatible ``Data`` / ``Batch`` (the operator surface the reference consumes).
+
+The reference's ``xgnn_poly.forward(data)`` (xgnn.py:38-75) reads ``data.x`` (atomic numbers),
+``data.edge_index`` (int64 [2,E], molecule-offset, sorted by source atom), ``data.edge_attr``
+([E,338]), ``data.atom_pos`` ([N,3]), ``data.edge_num`` (directed edges per molecule),
+``data.batch`` and ``data.num_graphs`` and tests ``"batch" in data._store`` (xgnn.py:41).  PyG
+2.1's ``Batch.from_data_list`` collate increments ``edge_index`` by the running atom count and
+stacks per-graph scalars; this module restates exactly that for the keys X2-GNN uses.
+
+Besides the tensors, a collated batch carries host-side size metadata (atoms, edges and
+triplets per molecule).  The device path takes every size from it, so a forward never reads a
+size back from the GPU (the reference syncs on ``int(batch.max())`` and on the CPU triplet
+round-trip, xgnn.py:52-53, model.py:190).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .synth import triplet_count
+
+
+class _Store(dict):
+    pass
+
+
+class Data:
+    """Attribute bag with a ``_store`` mapping (PyG ``Data`` semantics for the used keys)."""
+
+    def __init__(self, **kwargs):
+        object.__setattr__(self, "_store", _Store())
+        object.__setattr__(self, "_meta", None)
+        for k, v in kwargs.items():
+            if v is not None:
+                self._store[k] = v
+
+    def __getattr__(self, key):
+        store = object.__getattribute__(self, "_store")
+        if key in store:
+            return store[key]
+        raise AttributeError(key)
+
+    def __setattr__(self, key, value):
+        prop = getattr(type(self), key, None)
+        if isinstance(prop, property):
+            if prop.fset is not None:
+                prop.fset(self, value)
+            else:  # PyG stores into _store when the property has no setter
+                self._store[key] = value
+            return
+        self._store[key] = value
+
+    def __contains__(self, key):
+        return key in self._store
+
+    def keys(self):
+        return list(self._store.keys())
+
+    @property
+    def num_nodes(self):
+        return int(self._store["x"].shape[0])
+
+    def to(self, device, non_blocking=False):
+        out = type(self).__new__(type(self))
+        object.__setattr__(out, "_store", _Store())
+        object.__setattr__(out, "_meta", self._meta)
+        for k, v in self._store.items():
+            out._store[k] = v.to(device, non_blocking=non_blocking) if torch.is_tensor(v) else v
+        return out
+
+    def host_meta(self):
+        """Per-molecule (atoms, edges, triplets) counts as int64 numpy arrays (host)."""
+        if self._meta is None:
+            object.__setattr__(self, "_meta", _meta_from_tensors(self))
+        return self._meta
+
+
+def _meta_from_tensors(data):
+    """Fallback when a Data was built without host metadata: derive it (one device->host copy)."""
+    ei = data.edge_index.detach().cpu().numpy()
+    n = data.num_nodes
+    if "ptr" in data._store:
+        ptr = data.ptr.detach().cpu().numpy()
+        nodes = np.diff(ptr)
+    else:
+        nodes = np.array([n])
+    en = data.edge_num
+    edges = (en.detach().cpu().numpy().reshape(-1) if torch.is_tensor(en)
+             else np.array([en]).reshape(-1)).astype(np.int64)
+    trips = []
+    e0, a0 = 0, 0
+    for m in range(len(nodes)):
+        sub = ei[:, e0:e0 + edges[m]] - a0
+        trips.append(triplet_count(sub, int(nodes[m])))
+        e0 += edges[m]
+        a0 += nodes[m]
+    return {"nodes": nodes.astype(np.int64), "edges": edges, "triplets": np.array(trips, dtype=np.int64)}
+
+
+class Batch(Data):
+    """Collated molecules (PyG ``Batch.from_data_list`` restated for X2-GNN's keys)."""
+
+    @property
+    def num_graphs(self):
+        return int(self._meta["nodes"].shape[0])
+
+    @classmethod
+    def from_data_list(cls, data_list):
+        out = cls()
+        nodes = np.array([d.num_nodes for d in data_list], dtype=np.int64)
+        edges = np.array([int(d.edge_index.shape[1]) for d in data_list], dtype=np.int64)
+        trips = []
+        for d in data_list:
+            if d._meta is not None:
+                trips.append(int(d._meta["triplets"][0]))
+            else:
+                trips.append(triplet_count(d.edge_index.numpy(), d.num_nodes))
+        object.__setattr__(out, "_meta", {"nodes": nodes, "edges": edges,
+                                          "triplets": np.array(trips, dtype=np.int64)})
+        offs = np.concatenate([[0], np.cumsum(nodes)[:-1]])
+        keys = data_list[0].keys()
+        for k in keys:
+            vals = [d._store[k] for d in data_list]
+            if k == "edge_index":
+                out._store[k] = torch.cat([v + int(o) for v, o in zip(vals, offs)], dim=1)
+            elif torch.is_tensor(vals[0]) and vals[0].dim() > 0:
+                out._store[k] = torch.cat(vals, dim=0)
+            else:
+                out._store[k] = torch.as_tensor(np.array([np.asarray(v) for v in vals]).reshape(-1))
+        out._store["batch"] = torch.repeat_interleave(torch.arange(len(data_list)), torch.as_tensor(nodes))
+        out._store["ptr"] = torch.as_tensor(np.concatenate([[0], np.cumsum(nodes)]))
+        return out
+
+
+def molecule_to_data(mol: dict) -> Data:
+    """One synthetic/xyz molecule dict (see :mod:`x2gnn.synth`) as a ``Data``."""
+    d = Data(
+        x=torch.as_tensor(mol["x"], dtype=torch.int64),
+        atom_pos=torch.as_tensor(mol["atom_pos"], dtype=torch.float32),
+        edge_index=torch.as_tensor(mol["edge_index"], dtype=torch.int64),
+        edge_attr=torch.as_tensor(mol["edge_attr"], dtype=torch.float32) if "edge_attr" in mol else None,
+        edge_num=int(mol["edge_num"]),
+        y=float(mol.get("y", 0.0)),
+    )
+    object.__setattr__(d, "_meta", {"nodes": np.array([len(mol["x"])]),
+                                    "edges": np.array([int(mol["edge_num"])]),
+                                    "triplets": np.array([int(mol["triplet_num"])])})
+    return d
+
+
+def collate(mols) -> Batch:
+    """Molecule dicts -> collated ``Batch`` on the host."""
+    b = Batch.from_data_list([molecule_to_data(m) for m in mols])
+    b._store["y"] = b._store["y"].to(torch.float32)
+    return b

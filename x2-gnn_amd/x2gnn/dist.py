@@ -1,0 +1,50 @@
+"""Molecule-sharded data parallelism (one process per GPU, torch.distributed over RCCL/xGMI).
+
+The reference is single-device (train_ema.py:40); the build adds exactly one strategy:
+molecules are independent (triplets, LayerNorm segments, readouts and pools never cross a
+molecule), so each rank runs forward+backward on its own shard and the only exchange is one
+all-reduce of a flat fp32 gradient bucket (1,158,795 parameters = 4.6 MB at config.json
+widths) plus the scalar loss.  Shards are balanced by triplet count, the unit of work.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def shard_by_triplets(triplet_counts, world: int):
+    """Greedy longest-processing-time assignment of molecules to ``world`` ranks by triplet
+    count; returns one sorted index array per rank (molecule order kept inside a shard)."""
+    counts = np.asarray(triplet_counts, dtype=np.int64)
+    order = np.argsort(-counts, kind="stable")
+    load = np.zeros(world, dtype=np.int64)
+    owner = np.empty(len(counts), dtype=np.int64)
+    for m in order:
+        r = int(np.argmin(load))
+        owner[m] = r
+        load[r] += counts[m]
+    return [np.nonzero(owner == r)[0] for r in range(world)]
+
+
+class GradBucket:
+    """All parameters' gradients as views of ONE flat buffer, so the per-step exchange is a
+    single all-reduce (ring over xGMI) with no pack/unpack copies."""
+
+    def __init__(self, params):
+        self.params = [p for p in params if p.requires_grad]
+        n = sum(p.numel() for p in self.params)
+        dev = self.params[0].device
+        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        off = 0
+        for p in self.params:
+            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+
+    def zero(self):
+        self.flat.zero_()
+
+    def allreduce_mean(self, group=None):
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+            self.flat.div_(dist.get_world_size(group))

@@ -1,0 +1,209 @@
+"""Featurisation and readout blocks of X2-GNN with the reference's constructor arguments and
+parameter names (so reference ``state_dict``s load unchanged).
+
+================  =======================================  ==========================================
+class             reference                                 device path here
+================  =======================================  ==========================================
+poly_envelop      envelop.py:5-21                           elementwise (E-sized, torch)
+RadialBasis       radial_basis_layer.py:26-40 (trainable)   elementwise (E-sized, torch autograd)
+F_B_2D            angular_basis_layer.py:51-93 (+sympy)      x2g_bessel_env + x2g_spherical_basis;
+                                                            constants precomputed, no sympy at run time
+EmbeddingBlock    atom_embedding.py:10-25                    F.embedding, or the per-element table
+ResidualLayer     residual_layer.py:5-27                     hipBLASLt fp32 GEMMs
+AtomWise          readout.py:7-43                            lin_rbf GEMM + fused x2g_segment_sum(x*rf)
+MolWise           readout.py:45-76                           + segment sum/mean over molecules
+================  =======================================  ==========================================
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+
+
+class poly_envelop(nn.Module):
+    """u(d) = 1/x + a x^(p-1) + b x^p + c x^(p+1), x = d/cutoff, p = exponent+1 (no cutoff mask)."""
+
+    def __init__(self, cutoff, exponent):
+        super().__init__()
+        self.inv_cutoff = 1.0 / cutoff
+        self.exponent = exponent
+        self.p = exponent + 1
+        p = self.p
+        self.a, self.b, self.c = -(p + 1) * (p + 2) / 2, p * (p + 2), -p * (p + 1) / 2
+
+    def forward(self, distances):
+        x = distances * self.inv_cutoff
+        xp = x ** (self.p - 1)
+        return 1.0 / x + self.a * xp + self.b * (xp * x) + self.c * (xp * x * x)
+
+
+class RadialBasis(nn.Module):
+    """sin(f_n d / cutoff), f_n initialised to n*pi and trainable (the ``frequencies`` parameter)."""
+
+    def __init__(self, embedding_size, cutoff, Trainable=True, **kwargs):
+        super().__init__(**kwargs)
+        self.num_radial = embedding_size
+        self.inv_cutoff = 1.0 / cutoff
+        f = math.pi * torch.arange(1, embedding_size + 1, dtype=torch.float32)
+        if Trainable:
+            self.frequencies = nn.Parameter(f)
+        else:
+            self.register_buffer("frequencies", f)
+
+    def forward(self, bond_distances):
+        return torch.sin(self.frequencies * (bond_distances * self.inv_cutoff).unsqueeze(-1))
+
+
+class F_B_2D(nn.Module):
+    """Spherical-Bessel x Y_l0 basis, [T, num_spherical*num_radial], l-major columns.
+
+    Only (num_spherical, num_radial) = (7, 6) is compiled (config.json); the expanded
+    formulas' coefficients come from scripts/gen_basis_consts.py.
+    """
+
+    def __init__(self, num_spherical, num_radial, cutoff, envelope_exponent=5):
+        super().__init__()
+        if (num_spherical, num_radial) != (7, 6) or envelope_exponent != 5:
+            raise NotImplementedError("compiled basis: num_spherical=7, num_radial=6, envelope exponent 5")
+        self.num_spherical, self.num_radial, self.cutoff = num_spherical, num_radial, cutoff
+
+    def radial(self, d):
+        """[E, 42] env(d) * N_ln j_l(z_ln d / cutoff) (the E-row half of the reference forward)."""
+        return ops.bessel_env(d, self.cutoff)
+
+    def forward(self, d, Angles, edge_index_1):
+        return ops.spherical_basis_from_angles(Angles, edge_index_1, self.radial(d))
+
+    def from_positions(self, d, pos, line_graph):
+        """Fast path: angles computed in-kernel from the triplets' atom positions (xgnn.py:61-65)."""
+        return ops.spherical_basis(pos, line_graph, self.radial(d))
+
+
+class _ScaleGradByCount(torch.autograd.Function):
+    """Identity on the embedding table; backward divides row z by its count (scale_grad_by_freq)
+    and zeroes the padding row, as ATen's embedding backward does."""
+
+    @staticmethod
+    def forward(ctx, weight, counts, padding_idx):
+        ctx.save_for_backward(counts)
+        ctx.padding_idx = padding_idx
+        return weight.view_as(weight)
+
+    @staticmethod
+    def backward(ctx, g):
+        (counts,) = ctx.saved_tensors
+        g = g / counts.clamp(min=1).to(g.dtype).unsqueeze(1)
+        if ctx.padding_idx is not None:
+            g = g.clone()
+            g[ctx.padding_idx] = 0
+        return g, None, None
+
+
+class EmbeddingBlock(nn.Module):
+    """SiLU(Linear(Embedding(Z))) with Embedding(10, D, padding_idx=0, max_norm=3, scale_grad_by_freq)."""
+
+    def __init__(self, embedding_size=128, activation=True, **kwargs):
+        super().__init__(**kwargs)
+        self.AF = nn.SiLU()
+        self.embedding = nn.Embedding(10, embedding_size, padding_idx=0, max_norm=3.0, scale_grad_by_freq=True)
+        self.lin = nn.Linear(embedding_size, embedding_size, bias=True)
+        self.activate = activation
+
+    def forward(self, atomic_num):
+        h = self.lin(self.embedding(atomic_num))
+        return self.AF(h) if self.activate else h
+
+    def element_table(self, atomic_num):
+        """Per-element rows [num_embeddings, D] equal to forward(z) for every z present.
+
+        Reproduces the in-place max_norm renormalisation of the rows referenced by
+        ``atomic_num`` (torch.embedding_renorm_) and the scale_grad_by_freq gradient, without
+        materialising the [N, D] output: row z of the result stands for every atom of type z.
+        """
+        emb = self.embedding
+        counts = torch.bincount(atomic_num.reshape(-1), minlength=emb.num_embeddings)[: emb.num_embeddings]
+        w = emb.weight
+        if emb.max_norm is not None:
+            with torch.no_grad():
+                norms = w.norm(p=emb.norm_type, dim=1)
+                scale = torch.where((counts > 0) & (norms > emb.max_norm), emb.max_norm / (norms + 1e-7),
+                                    torch.ones_like(norms))
+                w.mul_(scale.unsqueeze(1))
+        if emb.scale_grad_by_freq or emb.padding_idx is not None:
+            c = counts if emb.scale_grad_by_freq else torch.ones_like(counts)
+            w = _ScaleGradByCount.apply(w, c, emb.padding_idx)
+        h = self.lin(w)
+        return self.AF(h) if self.activate else h
+
+
+class ResidualLayer(nn.Module):
+    """x + SiLU(lin1(SiLU(lin0(x))))."""
+
+    def __init__(self, in_channels, bias=True):
+        super().__init__()
+        self.lin0 = nn.Linear(in_channels, in_channels, bias=bias)
+        self.lin1 = nn.Linear(in_channels, in_channels, bias=bias)
+        self.AF = nn.SiLU()
+
+    def forward(self, x):
+        return x + self.AF(self.lin1(self.AF(self.lin0(x))))
+
+
+def _mlp(in_channels, num_target, depth):
+    layers = []
+    for _ in range(depth - 1):
+        layers += [nn.Linear(in_channels, in_channels), nn.SiLU()]
+    layers.append(nn.Linear(in_channels, num_target))
+    return nn.ModuleList(layers)
+
+
+def _edge_pool(x, rbf_filter, edge_index_0, num_atoms, atom_rowptr):
+    """sum over edges e with source atom n of rbf_filter[e] * x[e] -> [num_atoms, D]."""
+    if atom_rowptr is None:
+        atom_rowptr = ops.csr_rowptr(edge_index_0, num_atoms)
+    return ops.segment_sum(x, atom_rowptr, num_atoms, mul=rbf_filter)
+
+
+class AtomWise(nn.Module):
+    """Per-atom readout: (lin_rbf(rbf) * x) pooled edges->atoms by source atom, then an MLP."""
+
+    def __init__(self, mlp_depth=3, in_channels=256, rbf_dim=16, num_target=1):
+        super().__init__()
+        self.mlp = _mlp(in_channels, num_target, mlp_depth)
+        self.lin_rbf = nn.Linear(rbf_dim, in_channels)
+
+    def forward(self, x, rbf, num_atoms, edge_index_0, atom_rowptr=None):
+        out = _edge_pool(x, self.lin_rbf(rbf), edge_index_0, num_atoms, atom_rowptr)
+        for layer in self.mlp:
+            out = layer(out)
+        return out
+
+
+class MolWise(nn.Module):
+    """Per-molecule readout: edges->atoms pool, atoms->molecules mean/add pool, then an MLP."""
+
+    def __init__(self, mlp_depth=3, in_channels=256, rbf_dim=6, num_target=1, pool_option="mean"):
+        super().__init__()
+        if pool_option not in ("mean", "add"):
+            raise AssertionError("unsupport pooling option")
+        self.lin_rbf = nn.Linear(rbf_dim, in_channels)
+        self.mlp = _mlp(in_channels, num_target, mlp_depth)
+        self.pool_option = pool_option
+
+    def forward(self, x, rbf, num_atoms, edge_index_0, atom_batch, dim_size, atom_rowptr=None, mol_rowptr=None):
+        out = _edge_pool(x, self.lin_rbf(rbf), edge_index_0, num_atoms, atom_rowptr)
+        if mol_rowptr is None:
+            mol_rowptr = ops.csr_rowptr(atom_batch, dim_size)
+        pooled = ops.segment_sum(out, mol_rowptr, dim_size)
+        if self.pool_option == "mean":
+            cnt = (mol_rowptr[1:] - mol_rowptr[:-1]).clamp(min=1).to(pooled.dtype)
+            pooled = pooled / cnt.unsqueeze(1)
+        out = pooled
+        for layer in self.mlp:
+            out = layer(out)
+        return out

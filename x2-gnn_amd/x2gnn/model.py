@@ -1,0 +1,124 @@
+"""SBF-transformer trunk over the line graph (reference model.py:11-98), same module tree and
+``forward(data, edge_index_0, atom_batch)`` surface.
+
+Per layer: conv -> graph LayerNorm (per molecule) -> ResidualLayer -> SiLU(Linear) -> +residual
+-> 2 x ResidualLayer -> readout; energies are the per-atom readouts summed over layers and
+pooled per molecule.  Graph kernels (attention, LayerNorm, pools) run in libx2g.so; the dense
+E- and N-row layers are fp32 GEMMs.
+
+``data`` is the line-graph ``Data`` of the reference (x[E,D], edge_index[2,T], edge_attr,
+batch[E], edge_sbf[T,42], node_rbf[E,R]).  Two additions let ``xgnn_poly`` skip work the
+reference repeats per triplet: ``data._x2g_plan`` (a prebuilt :class:`GraphPlan`) and
+``data.edge_attr_row`` — when present, ``edge_attr`` is a per-element table [10, D] and line
+node e uses row ``edge_attr_row[e]``, so ``edgenn`` and every ``lin_edge`` run on 10 rows
+instead of T (the reference's edge_attr rows are copies of those rows, xgnn.py:57-58).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+from torch.nn import Linear, ModuleList, Sequential, SiLU
+
+from . import ops
+from .layers import AtomWise, MolWise, ResidualLayer
+from .plan import GraphPlan
+from .sbftransformer_conv import SBFTransformerConv
+
+
+class LayerNorm(nn.Module):
+    """torch_geometric.nn.LayerNorm(mode='graph', affine=False) on contiguous molecule segments."""
+
+    def __init__(self, in_channels, eps=1e-5, affine=False, mode="graph"):
+        super().__init__()
+        if affine or mode != "graph":
+            raise NotImplementedError("graph mode, affine=False (X2-GNN's configuration)")
+        self.in_channels, self.eps = in_channels, eps
+
+    def forward(self, x, batch=None, rowptr=None, num_graphs=None):
+        if rowptr is None and batch is None:
+            xc = x - x.mean()
+            return xc / (xc.std(unbiased=False) + self.eps)
+        if rowptr is None:
+            num_graphs = int(batch.max()) + 1
+            rowptr = ops.csr_rowptr(batch, num_graphs)
+        return ops.graph_layer_norm(x, rowptr, num_graphs, self.eps)
+
+
+def _plan_of(data, edge_index_0, atom_batch):
+    plan = data._store.get("_x2g_plan") if hasattr(data, "_store") else None
+    return plan if plan is not None else GraphPlan.from_line_data(data, edge_index_0, atom_batch)
+
+
+class _Trunk(nn.Module):
+    def _build(self, conv_layers, emb_size, sbf_dim, rbf_dim, in_channels, heads, readout):
+        self.in_channels = in_channels
+        self.rbf_dim = rbf_dim
+        self.edgenn = Sequential(Linear(emb_size, emb_size), SiLU(), Linear(emb_size, emb_size))
+        self.convs = ModuleList([
+            SBFTransformerConv(in_channels=in_channels, out_channels=int(in_channels / heads), heads=heads,
+                               sbf_dim=sbf_dim * rbf_dim, rbf_dim=rbf_dim, dropout=0, edge_dim=emb_size)
+            for _ in range(conv_layers)])
+        self.readouts = ModuleList([readout() for _ in range(conv_layers + 1)])
+        self.bf_skip = ModuleList([ResidualLayer(in_channels) for _ in range(conv_layers)])
+        self.af_skip = ModuleList([Sequential(ResidualLayer(in_channels), ResidualLayer(in_channels))
+                                   for _ in range(conv_layers)])
+        self.dense_bf_skip = ModuleList([Linear(in_channels, in_channels, bias=True) for _ in range(conv_layers)])
+        self.AF = SiLU()
+        self.LayerNorm = LayerNorm(in_channels=in_channels, eps=1e-8, affine=False)
+        self.conv_layers = conv_layers
+
+    def _layers(self, data, plan, readout_fn):
+        per_dst = "edge_attr_row" in data._store
+        edge_attr = self.edgenn(data.edge_attr)
+        edge_row = data.edge_attr_row if per_dst else None
+        out = data.x
+        results = readout_fn(0, out)
+        for i in range(self.conv_layers):
+            res0 = out
+            out = self.convs[i](sbf=data.edge_sbf, rbf=data.node_rbf, x=out, edge_index=data._store.get("edge_index"),
+                                edge_attr=edge_attr, line_graph=plan.lg, edge_row=edge_row)
+            out = self.LayerNorm(out, rowptr=plan.line_ptr, num_graphs=plan.num_graphs)
+            out = self.bf_skip[i](out)
+            out = self.AF(self.dense_bf_skip[i](out))
+            out = out + res0
+            out = self.af_skip[i](out)
+            results = results + readout_fn(i + 1, out)
+        return results
+
+
+class SBFTransformer(_Trunk):
+    """Trunk with per-atom readouts (extensive targets, reference model.py:11-54)."""
+
+    def __init__(self, conv_layers, emb_size, sbf_dim, rbf_dim=16, in_channels=128, heads=8):
+        super().__init__()
+        self._build(conv_layers, emb_size, sbf_dim, rbf_dim, in_channels, heads,
+                    lambda: AtomWise(in_channels=in_channels, rbf_dim=rbf_dim, num_target=1))
+
+    def forward(self, data, edge_index_0, atom_batch):
+        plan = _plan_of(data, edge_index_0, atom_batch)
+
+        def readout(i, x):
+            return self.readouts[i](x=x, rbf=data.node_rbf, num_atoms=plan.num_atoms, edge_index_0=edge_index_0,
+                                    atom_rowptr=plan.atom_rowptr)
+
+        per_atom = self._layers(data, plan, readout)
+        return ops.segment_sum(per_atom, plan.mol_ptr, plan.out_graphs).view(-1)
+
+
+class SBFTransformerGlobal(_Trunk):
+    """Trunk with per-molecule readouts (intensive targets, reference model.py:56-98)."""
+
+    def __init__(self, conv_layers, emb_size, sbf_dim, rbf_dim=16, in_channels=128, heads=8, pool_option="mean"):
+        super().__init__()
+        self._build(conv_layers, emb_size, sbf_dim, rbf_dim, in_channels, heads,
+                    lambda: MolWise(in_channels=in_channels, rbf_dim=rbf_dim, num_target=1, pool_option=pool_option))
+
+    def forward(self, data, edge_index_0, atom_batch):
+        plan = _plan_of(data, edge_index_0, atom_batch)
+
+        def readout(i, x):
+            return self.readouts[i](x=x, rbf=data.node_rbf, num_atoms=plan.num_atoms, edge_index_0=edge_index_0,
+                                    atom_batch=atom_batch, dim_size=plan.out_graphs, atom_rowptr=plan.atom_rowptr,
+                                    mol_rowptr=plan.mol_ptr[: plan.out_graphs + 1])
+
+        return self._layers(data, plan, readout).view(-1)

@@ -1,0 +1,326 @@
+"""Device operators of the hot path: thin wrappers over libx2g.so + their autograd rules.
+
+Every function here runs on the GPU through the C ABI (include/x2g.h) on PyTorch's current
+stream; inputs must be CUDA (HIP) tensors.  There is deliberately no CPU fallback.
+
+Operator                     replaces (reference / un-vendored dependency)
+---------------------------  ----------------------------------------------------------------
+``vertex_to_edge``           edge_graph.vertex_to_edge_2 (edge_graph.py:12-30), scipy on CPU
+``bessel_env`` /             F_B_2D.forward (angular_basis_layer.py:80-93) + poly_envelop
+``spherical_basis``          (envelop.py:16-21) + the angle code of xgnn.py:61-65
+``sbf_attention``            SBFTransformerConv.propagate/message/softmax/aggregate + skip
+                             (sbftransformer_conv.py:99-162; PyG MessagePassing, utils.softmax)
+``segment_sum``              torch_scatter.scatter_add with a sorted index (readout.py:37,
+                             model.py:190) and its backward gather
+``segment_softmax``          torch_geometric.utils.softmax
+``graph_layer_norm``         torch_geometric.nn.LayerNorm(mode='graph') (model.py:161,183)
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_ptr
+
+EDGE_NONE, EDGE_PER_TRIPLET, EDGE_PER_DST = 0, 1, 2
+
+
+def _need_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("x2gnn device ops need GPU tensors (no CPU fallback by design)")
+
+
+def _f32(t):
+    return t if t.dtype == torch.float32 and t.is_contiguous() else t.to(torch.float32).contiguous()
+
+
+def _i32(t):
+    return t if t.dtype == torch.int32 and t.is_contiguous() else t.to(torch.int32).contiguous()
+
+
+# ---------------------------------------------------------------------------------- line graph
+class LineGraph:
+    """Triplet structure of one collated batch (all int32, on the device).
+
+    trip_rowptr/trip_src/trip_dst: CSR by destination line node, in the reference's order.
+    atom_i/atom_j/atom_k: the three atoms of each triplet (xgnn.py:52 edge_i/edge_j/edge_k).
+    src_rowptr/src_perm: the same triplets grouped by source line node (built on first use).
+    """
+
+    def __init__(self, edge_src, edge_dst, num_nodes, num_triplets):
+        self.E = int(edge_src.shape[0])
+        self.N = int(num_nodes)
+        self.T = int(num_triplets)
+        self.edge_src, self.edge_dst = edge_src, edge_dst
+        dev = edge_src.device
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.atom_rowptr = torch.empty(self.N + 1, **i32)
+        self.trip_rowptr = torch.empty(self.E + 1, **i32)
+        self.trip_src = torch.empty(self.T, **i32)
+        self.trip_dst = torch.empty(self.T, **i32)
+        self.atom_j = torch.empty(self.T, **i32)
+        self.atom_i = torch.empty(self.T, **i32)
+        self.atom_k = torch.empty(self.T, **i32)
+        self._src_rowptr = None
+        self._src_perm = None
+        ws_bytes = int(_lib.load().x2g_vertex_to_edge_workspace(self.E, self.N))
+        self._ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        call("x2g_vertex_to_edge", ptr(edge_src), ptr(edge_dst), self.E, self.N, self.T, ptr(self.atom_rowptr),
+             ptr(self.trip_rowptr), ptr(self.trip_src), ptr(self.trip_dst), ptr(self.atom_j), ptr(self.atom_i),
+             ptr(self.atom_k), ptr(self._ws), ws_bytes, stream_ptr())
+
+    @classmethod
+    def from_triplets(cls, triplet_index, num_line_nodes: int):
+        """Wrap an existing triplet index [2, T] (row 1 sorted ascending, as vertex_to_edge_2 emits)."""
+        lg = cls.__new__(cls)
+        lg.E, lg.N, lg.T = int(num_line_nodes), None, int(triplet_index.shape[1])
+        lg.edge_src = lg.edge_dst = lg.atom_rowptr = None
+        lg.atom_i = lg.atom_j = lg.atom_k = None
+        lg.trip_src = _i32(triplet_index[0])
+        lg.trip_dst = _i32(triplet_index[1])
+        lg.trip_rowptr = csr_rowptr(lg.trip_dst, lg.E)
+        lg._src_rowptr = lg._src_perm = None
+        ws_bytes = int(_lib.load().x2g_vertex_to_edge_workspace(lg.E, 0))
+        lg._ws = torch.empty(ws_bytes, dtype=torch.uint8, device=lg.trip_src.device)
+        return lg
+
+    def src_csr(self):
+        if self._src_rowptr is None:
+            dev = self.trip_src.device
+            self._src_rowptr = torch.empty(self.E + 1, dtype=torch.int32, device=dev)
+            self._src_perm = torch.empty(self.T, dtype=torch.int32, device=dev)
+            call("x2g_line_graph_transpose", ptr(self.trip_src), self.T, self.E, ptr(self._src_rowptr),
+                 ptr(self._src_perm), ptr(self._ws), self._ws.numel(), stream_ptr())
+        return self._src_rowptr, self._src_perm
+
+    def triplet_index(self):
+        """int64 [2, T] (row 0 = source line node id(b->k), row 1 = destination id(a->b))."""
+        return torch.stack([self.trip_src.long(), self.trip_dst.long()])
+
+
+def vertex_to_edge(edge_index, num_nodes: int, num_triplets: int) -> LineGraph:
+    """Build the line graph of a (src, dst)-sorted directed edge list on the device."""
+    _need_cuda(edge_index)
+    ei = _i32(edge_index)
+    return LineGraph(ei[0].contiguous(), ei[1].contiguous(), num_nodes, num_triplets)
+
+
+def csr_rowptr(sorted_keys, num_segments: int):
+    _need_cuda(sorted_keys)
+    keys = _i32(sorted_keys)
+    out = torch.empty(num_segments + 1, dtype=torch.int32, device=keys.device)
+    call("x2g_csr_rowptr", ptr(keys), keys.numel(), num_segments, ptr(out), stream_ptr())
+    return out
+
+
+# ---------------------------------------------------------------------------------- basis
+def bessel_env(dist, cutoff: float = 5.0):
+    """[E] distances -> [E, 42] env(d) * N_ln j_l(z_ln d / cutoff)."""
+    _need_cuda(dist)
+    d = _f32(dist)
+    out = torch.empty(d.shape[0], 42, dtype=torch.float32, device=d.device)
+    call("x2g_bessel_env", ptr(d), d.shape[0], float(cutoff), ptr(out), stream_ptr())
+    return out
+
+
+def spherical_basis(pos, lg: LineGraph, rbf_env, want_cos=False):
+    """[T, 42] sbf = rbf_env[src] * Y_l0(theta), theta from the triplet's atom positions."""
+    _need_cuda(pos, rbf_env)
+    pos = _f32(pos)
+    out = torch.empty(lg.T, 42, dtype=torch.float32, device=pos.device)
+    cos_t = torch.empty(lg.T, dtype=torch.float32, device=pos.device) if want_cos else None
+    call("x2g_spherical_basis", ptr(pos), ptr(lg.atom_i), ptr(lg.atom_j), ptr(lg.atom_k), None, ptr(lg.trip_src),
+         ptr(_f32(rbf_env)), lg.T, ptr(out), ptr(cos_t), stream_ptr())
+    return (out, cos_t) if want_cos else out
+
+
+def spherical_basis_from_angles(theta, trip_src, rbf_env):
+    """[T, 42] sbf = rbf_env[trip_src] * Y_l0(theta) for given angles (F_B_2D signature)."""
+    _need_cuda(theta, trip_src, rbf_env)
+    th = _f32(theta)
+    src = _i32(trip_src)
+    out = torch.empty(th.shape[0], 42, dtype=torch.float32, device=th.device)
+    call("x2g_spherical_basis", None, None, None, None, ptr(th), ptr(src), ptr(_f32(rbf_env)), th.shape[0], ptr(out),
+         None, stream_ptr())
+    return out
+
+
+# ---------------------------------------------------------------------------------- attention
+class _SBFAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row, heads, channels):
+        q, k, v, skip = _f32(q), _f32(k), _f32(v), _f32(skip)
+        sbf, w_sbf, b_sbf = _f32(sbf), _f32(w_sbf), _f32(b_sbf)
+        edge = _f32(edge) if edge is not None else None
+        E, T, D = q.shape[0], lg.T, heads * channels
+        dev = q.device
+        out = torch.empty(E, D, dtype=torch.float32, device=dev)
+        alpha = torch.empty(T, heads, dtype=torch.float32, device=dev)
+        smax = torch.empty(E, heads, dtype=torch.float32, device=dev)
+        sden = torch.empty(E, heads, dtype=torch.float32, device=dev)
+        call("x2g_sbf_attention_fwd", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(edge_row), edge_mode,
+             ptr(sbf), ptr(w_sbf), ptr(b_sbf), ptr(lg.trip_rowptr), ptr(lg.trip_src), E, T, heads, channels,
+             sbf.shape[1], ptr(out), ptr(alpha), ptr(smax), ptr(sden), stream_ptr())
+        ctx.save_for_backward(q, k, v, edge, sbf, w_sbf, b_sbf, alpha, smax, sden)
+        ctx.lg, ctx.edge_mode, ctx.edge_row, ctx.heads, ctx.channels = lg, edge_mode, edge_row, heads, channels
+        ctx.edge_shape = None if edge is None else edge.shape
+        ctx.mark_non_differentiable(alpha, smax, sden)
+        return out, alpha, smax, sden
+
+    @staticmethod
+    def backward(ctx, dout, _da=None, _dm=None, _ds=None):
+        q, k, v, edge, sbf, w_sbf, b_sbf, alpha, smax, sden = ctx.saved_tensors
+        lg, mode, heads, channels = ctx.lg, ctx.edge_mode, ctx.heads, ctx.channels
+        dout = _f32(dout)
+        E, T, D = q.shape[0], lg.T, heads * channels
+        dev = q.device
+        dq = torch.empty(E, D, dtype=torch.float32, device=dev)
+        dk = torch.empty_like(dq)
+        dv = torch.empty_like(dq)
+        dlogit = torch.empty(T, heads, dtype=torch.float32, device=dev)
+        dproj = torch.empty(T, D, dtype=torch.float32, device=dev)
+        if mode == EDGE_PER_TRIPLET:
+            d_edge = torch.empty(T, D, dtype=torch.float32, device=dev)
+        elif mode == EDGE_PER_DST:
+            d_edge = torch.empty(E, D, dtype=torch.float32, device=dev)
+        else:
+            d_edge = None
+        st = stream_ptr()
+        call("x2g_sbf_attention_bwd_dst", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(ctx.edge_row), mode, ptr(sbf),
+             ptr(w_sbf), ptr(b_sbf), ptr(lg.trip_rowptr), ptr(lg.trip_src), ptr(alpha), ptr(smax), ptr(sden),
+             ptr(dout), E, T, heads, channels, sbf.shape[1], ptr(dq), ptr(d_edge), ptr(dlogit), ptr(dproj), st)
+        src_rowptr, src_perm = lg.src_csr()
+        call("x2g_sbf_attention_bwd_src", ptr(q), ptr(sbf), ptr(w_sbf), ptr(b_sbf), ptr(src_rowptr), ptr(src_perm),
+             ptr(lg.trip_dst), ptr(alpha), ptr(smax), ptr(sden), ptr(dlogit), ptr(dout), E, T, heads, channels,
+             sbf.shape[1], ptr(dk), ptr(dv), st)
+        if mode == EDGE_PER_DST and ctx.edge_row is not None:
+            # rows of the edge table are shared by many destinations: sum d_edge per table row
+            onehot = torch.nn.functional.one_hot(ctx.edge_row.long(), ctx.edge_shape[0]).to(torch.float32)
+            d_edge = onehot.t() @ d_edge
+        dw = dproj.t() @ sbf
+        db = dproj.sum(0)
+        return dq, dk, dv, dout, d_edge, None, dw, db, None, None, None, None, None
+
+
+def sbf_attention(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg: LineGraph, heads: int, channels: int,
+                  edge_mode: int = EDGE_PER_TRIPLET, edge_row=None, return_attention=False):
+    """Fused SBFTransformerConv message/softmax/aggregate/skip (see csrc/attention.hip).
+
+    With ``return_attention`` also returns the softmax probabilities [T, heads] (the
+    reference's ``return_attention_weights`` alpha)."""
+    _need_cuda(q, k, v, skip, sbf)
+    if edge is None:
+        edge_mode = EDGE_NONE
+    if edge_row is not None:
+        edge_row = _i32(edge_row)
+    out, alpha, smax, sden = _SBFAttention.apply(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row,
+                                                 heads, channels)
+    if not return_attention:
+        return out
+    dst = lg.trip_dst.long()
+    prob = torch.exp(alpha - smax.index_select(0, dst)) / (sden.index_select(0, dst) + 1e-16)
+    return out, prob
+
+
+# ---------------------------------------------------------------------------------- segments
+def _seg_sum_raw(x, mul, rowptr, n_seg):
+    D = x.shape[1]
+    out = torch.empty(n_seg, D, dtype=torch.float32, device=x.device)
+    call("x2g_segment_sum", ptr(x), ptr(mul), ptr(rowptr), n_seg, D, ptr(out), stream_ptr())
+    return out
+
+
+def _seg_bcast_raw(g, mul, rowptr, n_rows):
+    D = g.shape[1]
+    out = torch.empty(n_rows, D, dtype=torch.float32, device=g.device)
+    call("x2g_segment_broadcast", ptr(g), ptr(mul), ptr(rowptr), g.shape[0], D, ptr(out), stream_ptr())
+    return out
+
+
+class _SegmentSum(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, mul, rowptr, n_seg):
+        x = _f32(x)
+        mul = _f32(mul) if mul is not None else None
+        ctx.save_for_backward(x, mul, rowptr)
+        return _seg_sum_raw(x, mul, rowptr, n_seg)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, mul, rowptr = ctx.saved_tensors
+        g = _f32(g)
+        dx = _seg_bcast_raw(g, mul, rowptr, x.shape[0]) if ctx.needs_input_grad[0] else None
+        dmul = None
+        if mul is not None and ctx.needs_input_grad[1]:
+            dmul = _seg_bcast_raw(g, x, rowptr, x.shape[0])
+        return dx, dmul, None, None
+
+
+def segment_sum(x, rowptr, num_segments: int, mul=None):
+    """out[g] = sum_{r in segment g} x[r] (* mul[r]); rows of a segment are contiguous."""
+    _need_cuda(x, rowptr)
+    squeeze = x.dim() == 1
+    if squeeze:
+        x = x.unsqueeze(1)
+        mul = mul.unsqueeze(1) if mul is not None else None
+    out = _SegmentSum.apply(x, mul, _i32(rowptr), int(num_segments))
+    return out.squeeze(1) if squeeze else out
+
+
+class _SegmentSoftmax(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, src, rowptr, n_seg):
+        src = _f32(src)
+        out = torch.empty_like(src)
+        call("x2g_segment_softmax_fwd", ptr(src), ptr(rowptr), n_seg, src.shape[1], ptr(out), stream_ptr())
+        ctx.save_for_backward(out, rowptr)
+        ctx.n_seg = n_seg
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        out, rowptr = ctx.saved_tensors
+        g = _f32(g)
+        ds = torch.empty_like(out)
+        call("x2g_segment_softmax_bwd", ptr(out), ptr(g), ptr(rowptr), ctx.n_seg, out.shape[1], ptr(ds), stream_ptr())
+        return ds, None, None
+
+
+def segment_softmax(src, rowptr, num_segments: int):
+    """PyG utils.softmax for a sorted index, [R] or [R, H]."""
+    _need_cuda(src, rowptr)
+    squeeze = src.dim() == 1
+    s = src.unsqueeze(1) if squeeze else src
+    out = _SegmentSoftmax.apply(s, _i32(rowptr), int(num_segments))
+    return out.squeeze(1) if squeeze else out
+
+
+class _GraphLayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, rowptr, n_seg, eps):
+        x = _f32(x)
+        D = x.shape[1]
+        out = torch.empty_like(x)
+        mean = torch.empty(n_seg, dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        call("x2g_graph_layernorm_fwd", ptr(x), ptr(rowptr), n_seg, D, float(eps), ptr(out), ptr(mean), ptr(rstd),
+             stream_ptr())
+        ctx.save_for_backward(out, rstd, rowptr)
+        ctx.n_seg = n_seg
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        out, rstd, rowptr = ctx.saved_tensors
+        g = _f32(g)
+        dx = torch.empty_like(out)
+        call("x2g_graph_layernorm_bwd", ptr(out), ptr(g), ptr(rstd), ptr(rowptr), ctx.n_seg, out.shape[1], ptr(dx),
+             stream_ptr())
+        return dx, None, None, None
+
+
+def graph_layer_norm(x, rowptr, num_segments: int, eps: float = 1e-5):
+    """PyG LayerNorm(mode='graph', affine=False) over contiguous row segments."""
+    _need_cuda(x, rowptr)
+    return _GraphLayerNorm.apply(x, _i32(rowptr), int(num_segments), float(eps))

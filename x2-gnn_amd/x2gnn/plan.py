@@ -1,0 +1,95 @@
+"""Per-batch device plan: every index structure the hot path needs, built once per forward.
+
+The reference recomputes these implicitly inside each operator (scatter sizes via
+``int(batch.max()) + 1`` host syncs at model.py:190 and inside PyG's LayerNorm/softmax, the
+triplets via a CPU round trip at xgnn.py:52-53).  Here they are built once on the device from
+host-side size metadata, so a whole forward+backward enqueues without a single device->host
+read (and can be captured in a HIP graph).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import ops
+
+
+class GraphPlan:
+    """Index structures of one collated batch.
+
+    lg            LineGraph (triplets, CSR by destination; source-major transpose on demand)
+    atom_rowptr   [N+1]  line nodes (= directed edges) grouped by source atom, i.e. the CSR of
+                         ``edge_index_0`` that AtomWise pools over (readout.py:37)
+    line_ptr      [B+1]  line nodes per molecule (graph LayerNorm segments, model.py:183)
+    mol_ptr       [B+1]  atoms per molecule (global add pool, model.py:190)
+    dst_type      [E]    atomic number of the middle atom b of each line node e=(a->b): the
+                         row of the per-element edge table every triplet into e uses
+    num_atoms, num_lines, num_triplets, num_graphs, out_graphs (host ints)
+    """
+
+    def __init__(self):
+        self.lg = None
+        self.atom_rowptr = self.line_ptr = self.mol_ptr = self.dst_type = None
+        self.num_atoms = self.num_lines = self.num_triplets = self.num_graphs = self.out_graphs = 0
+
+    # ------------------------------------------------------------------ from an atom batch
+    @classmethod
+    def from_atom_batch(cls, data):
+        """Plan for ``xgnn_poly.forward(data)`` inputs (edge_index sorted by (src, dst))."""
+        meta = data.host_meta()
+        p = cls()
+        nodes, edges, trips = meta["nodes"], meta["edges"], meta["triplets"]
+        p.num_atoms, p.num_lines, p.num_triplets = int(nodes.sum()), int(edges.sum()), int(trips.sum())
+        p.num_graphs = int(len(nodes))
+        nz = np.nonzero(edges)[0]
+        # the reference sizes the pool by the last molecule that has line nodes (model.py:190)
+        p.out_graphs = int(nz[-1]) + 1 if len(nz) else 0
+        ei = data.edge_index
+        dev = ei.device
+        p.lg = ops.vertex_to_edge(ei, p.num_atoms, p.num_triplets)
+        p.atom_rowptr = p.lg.atom_rowptr
+        p.line_ptr = _ptr_from_counts(data.edge_num, p.num_graphs, dev)
+        if "ptr" in data._store:
+            p.mol_ptr = ops._i32(data.ptr)
+        else:
+            p.mol_ptr = (torch.arange(2, device=dev, dtype=torch.int32) * p.num_atoms)
+        p.dst_type = ops._i32(data.x.index_select(0, p.lg.edge_dst))
+        return p
+
+    # ------------------------------------------------------------------ from line-graph tensors
+    @classmethod
+    def from_line_data(cls, data, edge_index_0, atom_batch):
+        """Plan for the drop-in ``SBFTransformer.forward(data, edge_index_0, atom_batch)`` API.
+
+        Sizes are read back from the device here (as the reference does with
+        ``int(batch.max())``); the fast path through ``xgnn_poly`` never takes this branch.
+        """
+        p = cls()
+        p.num_lines = int(data.x.shape[0])
+        p.num_atoms = int(atom_batch.shape[0])
+        p.num_triplets = int(data.edge_index.shape[1])
+        _require_sorted(data.edge_index[1], "line-graph edge_index[1] (triplet destinations)")
+        _require_sorted(edge_index_0, "edge_index_0 (source atom of each line node)")
+        p.lg = ops.LineGraph.from_triplets(data.edge_index, p.num_lines)
+        p.atom_rowptr = ops.csr_rowptr(edge_index_0, p.num_atoms)
+        b = data.batch
+        p.num_graphs = p.out_graphs = int(b.max()) + 1 if b.numel() else 0
+        _require_sorted(b, "line-graph batch")
+        _require_sorted(atom_batch, "atom_batch")
+        p.line_ptr = ops.csr_rowptr(b, p.num_graphs)
+        p.mol_ptr = ops.csr_rowptr(atom_batch, p.num_graphs)
+        return p
+
+
+def _ptr_from_counts(counts, n, device):
+    if torch.is_tensor(counts):
+        c = counts.reshape(-1).to(device=device)
+    else:
+        c = torch.full((1,), int(counts), device=device, dtype=torch.int64)
+    return F.pad(torch.cumsum(c, 0), (1, 0)).to(torch.int32)
+
+
+def _require_sorted(idx, what):
+    if idx.numel() > 1 and bool((idx[1:] < idx[:-1]).any()):
+        raise ValueError(f"{what} must be sorted ascending (the order the reference produces)")

@@ -1,0 +1,84 @@
+"""SBFTransformerConv on the line graph, backed by the fused gfx950 attention kernels.
+
+Same constructor and ``forward(sbf, rbf, x, edge_index, edge_attr)`` contract as the
+reference (sbftransformer_conv.py:16-166, a PyG ``MessagePassing`` with aggr='add'):
+
+    x_src = x * lin_rbf(rbf);  q = lin_query(x);  k, v = lin_key(x_src), lin_value(x_src)
+    per triplet t = (src -> dst):  e_t = lin_edge(edge_attr_t)
+        alpha_t = softmax_dst( <q[dst], k[src] + e_t> / sqrt(C) )          (per head)
+        m_t     = (v[src] + e_t) * lin_sbf(sbf_t) * alpha_t
+    out[dst] = sum_t m_t  (+ lin_skip(x) with root_weight)
+
+The dense projections (q/k/v/skip/rbf/edge) stay fp32 GEMMs on hipBLASLt; everything per
+triplet (gathers, logits, softmax, the 42->H*C sbf projection, the weighted sum) runs in one
+kernel (``ops.sbf_attention``) without materialising a [T, H*C] tensor.
+
+Extra keyword-only arguments for the in-framework fast path:
+``line_graph`` (a prebuilt ``ops.LineGraph``) and ``edge_row`` (when ``edge_attr`` is a small
+table and triplets into line node e use row ``edge_row[e]``: X2-GNN's edge attribute is the
+embedding of the middle atom, identical for all triplets into e, xgnn.py:57-58).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple, Union
+
+import torch
+import torch.nn as nn
+
+from . import ops
+
+
+class SBFTransformerConv(nn.Module):
+    def __init__(self, in_channels: Union[int, Tuple[int, int]], out_channels: int, heads: int = 1,
+                 sbf_dim: int = 16, rbf_dim: int = 16, concat: bool = True, beta: bool = False,
+                 dropout: float = 0.0, edge_dim: Optional[int] = None, bias: bool = True,
+                 root_weight: bool = True, **kwargs):
+        super().__init__()
+        if not concat or (beta and root_weight):
+            raise NotImplementedError("compiled configuration: concat=True, beta=False (X2-GNN's)")
+        self.in_channels, self.out_channels, self.heads = in_channels, out_channels, heads
+        self.sbf_dim, self.rbf_dim = sbf_dim, rbf_dim
+        self.beta, self.root_weight, self.concat = False, root_weight, concat
+        self.dropout, self.edge_dim = dropout, edge_dim
+        cin = (in_channels, in_channels) if isinstance(in_channels, int) else tuple(in_channels)
+        hc = heads * out_channels
+        self.lin_key = nn.Linear(cin[0], hc)
+        self.lin_query = nn.Linear(cin[1], hc)
+        self.lin_value = nn.Linear(cin[0], hc)
+        self.lin_edge = nn.Linear(edge_dim, hc, bias=False) if edge_dim is not None else None
+        self.lin_skip = nn.Linear(cin[1], hc, bias=bias)
+        self.lin_beta = None
+        self.lin_sbf = nn.Linear(sbf_dim, hc, bias=True)
+        self.lin_rbf = nn.Linear(rbf_dim, cin[0], bias=False)
+        self._alpha = None
+
+    def forward(self, sbf, rbf, x, edge_index, edge_attr=None, return_attention_weights=None, *,
+                line_graph: Optional[ops.LineGraph] = None, edge_row=None):
+        H, C = self.heads, self.out_channels
+        if self.training and self.dropout > 0:
+            raise NotImplementedError("attention dropout is not compiled (X2-GNN uses dropout=0)")
+        x_src = x * self.lin_rbf(rbf)
+        q = self.lin_query(x)
+        k = self.lin_key(x_src)
+        v = self.lin_value(x_src)
+        skip = self.lin_skip(x) if self.root_weight else torch.zeros_like(q)
+        if line_graph is None:
+            if edge_index.numel() > 1 and bool((edge_index[1, 1:] < edge_index[1, :-1]).any()):
+                raise ValueError("triplet edge_index[1] must be sorted ascending (vertex_to_edge_2 order)")
+            line_graph = ops.LineGraph.from_triplets(edge_index, x.shape[0])
+        if edge_attr is not None and self.lin_edge is not None:
+            e = self.lin_edge(edge_attr)
+            mode = ops.EDGE_PER_DST if edge_row is not None else ops.EDGE_PER_TRIPLET
+        else:
+            e, mode = None, ops.EDGE_NONE
+        want = isinstance(return_attention_weights, bool)
+        res = ops.sbf_attention(q, k, v, skip, e, sbf, self.lin_sbf.weight, self.lin_sbf.bias, line_graph, H, C,
+                                edge_mode=mode, edge_row=edge_row, return_attention=want)
+        if want:
+            out, alpha = res
+            return out, (edge_index, alpha)
+        return res
+
+    def __repr__(self):
+        return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels}, heads={self.heads})"
+
