@@ -1,0 +1,33 @@
+#!/bin/bash
+# GPU validation/profiling run (used through gpurun): each step under its own time limit; stop
+# at the first step that ends in anything but pass/fail (fault, abort, timeout).
+#   bash scripts/gpu_check.sh [kernels] [model] [smoke] [bench] [prof] [pmc]
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+ROOT=$(pwd)
+step() {  # step <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "=== $name: $*" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a gpurun_out/steps.log
+  tail -n 4 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+TAG=${TAG:-r1}
+for s in "$@"; do
+  case $s in
+    kernels) step kernels 420 python -m pytest tests/test_gpu_kernels.py -q -m gpu -rf ;;
+    model) step model 420 python -m pytest tests/test_gpu_model.py -q -m gpu -rf ;;
+    gpu) step gputests 600 python -m pytest tests -q -m gpu -rf ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 420 python bench.py --steps 20 --warmup 5 ;;
+    prof) step prof 420 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv \
+            -- python "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline ;;
+    pmc) step pmc 420 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch_$TAG -o run \
+            --output-format csv -- python "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --kernel-reps 3 &&
+         step pmc2 420 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write_$TAG -o run \
+            --output-format csv -- python "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --kernel-reps 3 ;;
+  esac
+done

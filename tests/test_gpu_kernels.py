@@ -134,9 +134,10 @@ def test_radial_parts_vs_reference(cuda):
     z = golden("basis.npz")
     d = torch.from_numpy(z["dist"]).to(cuda)
     env = poly_envelop(5.0, 5)(d)
-    np.testing.assert_allclose(env.cpu().numpy(), z["env"], rtol=2e-6, atol=1e-6)
+    # near d = cutoff the envelope is a difference of O(50) terms: absolute slack of a few ulps of them
+    np.testing.assert_allclose(env.cpu().numpy(), z["env"], rtol=2e-6, atol=2e-5)
     rbf = RadialBasis(6, 5.0).to(cuda)(d) * env[:, None]
-    np.testing.assert_allclose(rbf.detach().cpu().numpy(), z["rbf"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(rbf.detach().cpu().numpy(), z["rbf"], rtol=1e-5, atol=2e-5)
 
 
 # ------------------------------------------------------------------------------ segments

@@ -92,7 +92,8 @@ class _ScaleGradByCount(torch.autograd.Function):
     def forward(ctx, weight, counts, padding_idx):
         ctx.save_for_backward(counts)
         ctx.padding_idx = padding_idx
-        return weight.view_as(weight)
+        # a copy, not a view: the renorm mutates the weight in place on the next forward
+        return weight.clone()
 
     @staticmethod
     def backward(ctx, g):
