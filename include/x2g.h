@@ -149,6 +149,34 @@ int x2g_graph_layernorm_fwd(const float* x, const int32_t* rowptr, int64_t num_s
 int x2g_graph_layernorm_bwd(const float* out, const float* dout, const float* rstd, const int32_t* rowptr,
                             int64_t num_segments, int64_t dim, float* dx, void* stream);
 
+/* ---------------------------------------------------------------- dense-layer gradients */
+
+/* Workspace bytes for x2g_linear_wgrad (row-split partial slabs). */
+size_t x2g_linear_wgrad_workspace(int64_t rows, int32_t out_features, int32_t in_features);
+
+/* dW[O,I] = dy[R,O]^T x[R,I] and db[O] = column sums of dy (db may be NULL): the weight/bias
+ * gradient of every nn.Linear the reference applies row-wise (residual_layer.py, model.py:39,48,
+ * readout.py, sbftransformer_conv.py:99-148, xgnn.py:54-70), split over rows with f32 MFMA and
+ * summed in a fixed order (deterministic; replaces ATen's addmm backward through hipBLASLt). */
+int x2g_linear_wgrad(const float* dy, const float* x, int64_t rows, int32_t out_features,
+                     int32_t in_features, float* dw, float* db, void* workspace, size_t workspace_bytes,
+                     void* stream);
+
+#define X2G_ACT_NONE 0
+#define X2G_ACT_SILU 1
+
+/* Row-wise dense layer with fused epilogue: y[R,N] = act(x[R,K] w[N,K]^T + b[N]) (+ res[R,N]);
+ * z[R,N] (optional) receives the pre-activation x w^T + b for the backward.  Replaces the
+ * Linear -> SiLU -> add chains of residual_layer.py:21-27, model.py:39,47-50, readout.py:38-42,
+ * xgnn.py:54-55,70 and the projections of sbftransformer_conv.py:99-107,127.  b, res, z may be NULL. */
+int x2g_dense_fwd(const float* x, const float* w, const float* b, int64_t rows, int32_t in_features,
+                  int32_t out_features, int act, const float* res, float* y, float* z, void* stream);
+
+/* Data gradient of x2g_dense_fwd: dz = dy * act'(z) (written to dz when non-NULL), dx = dz w.
+ * dy, z, dz: [R, N]; w: [N, K]; dx: [R, K]. */
+int x2g_dense_bwd_data(const float* dy, const float* z, int act, const float* w, int64_t rows,
+                       int32_t in_features, int32_t out_features, float* dx, float* dz, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -315,3 +315,71 @@ def test_conv_small_width_vs_oracle(cuda):
     assert rel_err(xg.grad.cpu().numpy(), xr.grad.numpy()) < 1e-4
     assert rel_err(eg.grad.cpu().numpy(), er.grad.numpy()) < 1e-4
     assert rel_err(conv.lin_sbf.weight.grad.cpu().numpy(), orc.lin_sbf.weight.grad.numpy()) < 1e-4
+
+
+# ------------------------------------------------------------------------------ dense layers
+@pytest.mark.parametrize("R,O,I", [(21058, 128, 128), (194060, 128, 42), (1000, 256, 338), (77, 1, 128),
+                                   (5, 128, 6), (130, 128, 10), (0, 128, 128)])
+def test_linear_wgrad_vs_fp64(cuda, R, O, I):
+    from x2gnn import ops
+
+    g = torch.Generator().manual_seed(R + O + I)
+    dy = torch.randn(R, O, generator=g, dtype=torch.float64)
+    x = torch.randn(R, I, generator=g, dtype=torch.float64)
+    dw, db = ops.linear_wgrad(dy.float().to(cuda), x.float().to(cuda))
+    ref_w, ref_b = dy.t() @ x, dy.sum(0)
+    scale = max(1.0, float(np.sqrt(max(R, 1))))  # random-sign sums grow like sqrt(R)
+    np.testing.assert_allclose(dw.cpu().numpy(), ref_w.numpy(), atol=2e-5 * scale, rtol=1e-5)
+    np.testing.assert_allclose(db.cpu().numpy(), ref_b.numpy(), atol=2e-5 * scale, rtol=1e-5)
+    dw2, _ = ops.linear_wgrad(dy.float().to(cuda), x.float().to(cuda))
+    assert torch.equal(dw, dw2)  # deterministic
+
+
+def test_linear_module_grads_match_torch(cuda):
+    from x2gnn.layers import Linear
+
+    torch.manual_seed(0)
+    lin = Linear(128, 64).to(cuda)
+    ref = torch.nn.Linear(128, 64).to(cuda)
+    ref.load_state_dict(lin.state_dict())
+    x = torch.randn(3, 700, 128, device=cuda)
+    x1, x2 = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    g = torch.randn(3, 700, 64, device=cuda)
+    (lin(x1) * g).sum().backward()
+    (ref(x2) * g).sum().backward()
+    for a, b in ((x1.grad, x2.grad), (lin.weight.grad, ref.weight.grad), (lin.bias.grad, ref.bias.grad)):
+        np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("R,K,N", [(21058, 128, 128), (3000, 338, 256), (2304, 128, 1), (777, 6, 128),
+                                   (10, 128, 128), (500, 256, 128), (130, 42, 160)])
+@pytest.mark.parametrize("act", [0, 1])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_dense_fused_vs_torch(cuda, R, K, N, act, with_res):
+    from x2gnn import ops
+
+    g = torch.Generator().manual_seed(R * 7 + K + N)
+    x = torch.randn(R, K, generator=g, dtype=torch.float64)
+    w = torch.randn(N, K, generator=g, dtype=torch.float64) / np.sqrt(K)
+    b = torch.randn(N, generator=g, dtype=torch.float64)
+    res = torch.randn(R, N, generator=g, dtype=torch.float64) if with_res else None
+    up = torch.randn(R, N, generator=g, dtype=torch.float64)
+    xs, ws, bs = (t.clone().requires_grad_(True) for t in (x, w, b))
+    ref = xs @ ws.t() + bs
+    if act:
+        ref = torch.nn.functional.silu(ref)
+    if with_res:
+        rs = res.clone().requires_grad_(True)
+        ref = ref + rs
+    (ref * up).sum().backward()
+    xg, wg, bg = (t.float().to(cuda).requires_grad_(True) for t in (x, w, b))
+    rg = res.float().to(cuda).requires_grad_(True) if with_res else None
+    y = ops.dense(xg, wg, bg, act=act, res=rg)
+    (y * up.float().to(cuda)).sum().backward()
+    tol = dict(rtol=1e-4, atol=1e-4 * max(1.0, np.sqrt(R / 100)))
+    np.testing.assert_allclose(y.detach().cpu().numpy(), ref.detach().numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(xg.grad.cpu().numpy(), xs.grad.numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(wg.grad.cpu().numpy(), ws.grad.numpy(), **tol)
+    np.testing.assert_allclose(bg.grad.cpu().numpy(), bs.grad.numpy(), **tol)
+    if with_res:
+        np.testing.assert_allclose(rg.grad.cpu().numpy(), rs.grad.numpy(), rtol=1e-6, atol=1e-6)

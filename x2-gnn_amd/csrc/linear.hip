@@ -1,0 +1,204 @@
+// Weight gradients of the row-wise dense layers: dW[o,i] = sum_r dY[r,o] X[r,i], db[o] = sum_r dY[r,o].
+//
+// Every dense layer of X2-GNN runs on E (line nodes), N (atoms) or T (triplets) rows with tiny
+// weights (128x128, 128x42, 256x338, ...).  Their weight gradient is a GEMM with a huge K
+// (the row count, 2e4..2e5) and a tiny M x N output; the vendor GEMMs pick a handful of
+// output tiles and no K split for that shape (hipBLASLt: 90 us for 128x128 over 21k rows,
+// 440 us for lin_sbf's 128x42 over 194k rows on MI355X).  Here the rows are split over many
+// workgroups (<= 160 slices of >= 64 rows), every workgroup computes its slice's full 128x128 output
+// block with f32 MFMA (v_mfma_f32_32x32x2_f32: exact fp32 FMA chains), writes it to a partial
+// slab, and a second pass sums the slabs in a fixed order: deterministic, no atomics.
+#include "common.hpp"
+
+namespace x2g {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int kWgTile = 128;       // output block (o) x (i) per workgroup
+constexpr int kWgChunk = 32;       // rows staged in LDS per iteration
+constexpr int kWgMaxSplits = 160;  // row splits (workgroups per output block)
+constexpr int kLdsStride = kWgTile + 4;  // keeps 16-byte row alignment for the float4 stores
+
+// Chunk of 32 rows x 128 columns of one operand, held in registers between global and LDS:
+// VEC = 4 float4 per thread (columns a multiple of 4), else 16 scalars per thread.
+template <bool VEC>
+struct ChunkRegs {
+  float v[16];
+};
+
+template <bool VEC>
+__device__ __forceinline__ void load_chunk(const float* __restrict__ m, int cols, int c0, int64_t r0,
+                                           int64_t r_end, ChunkRegs<VEC>& reg) {
+  const int tid = threadIdx.x;
+  if (VEC) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = tid + 256 * u, rr = q >> 5, c = c0 + 4 * (q & 31);
+      const int64_t r = r0 + rr;
+      float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < r_end && c < cols) f = *reinterpret_cast<const float4*>(m + r * cols + c);
+      reg.v[4 * u] = f.x;
+      reg.v[4 * u + 1] = f.y;
+      reg.v[4 * u + 2] = f.z;
+      reg.v[4 * u + 3] = f.w;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int q = tid + 256 * u, rr = q >> 7, c = c0 + (q & 127);
+      const int64_t r = r0 + rr;
+      reg.v[u] = (r < r_end && c < cols) ? m[r * cols + c] : 0.f;
+    }
+  }
+}
+
+template <bool VEC>
+__device__ __forceinline__ void store_chunk(float (*lds)[kLdsStride], const ChunkRegs<VEC>& reg) {
+  const int tid = threadIdx.x;
+  if (VEC) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = tid + 256 * u;
+      *reinterpret_cast<float4*>(&lds[q >> 5][4 * (q & 31)]) =
+          make_float4(reg.v[4 * u], reg.v[4 * u + 1], reg.v[4 * u + 2], reg.v[4 * u + 3]);
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int q = tid + 256 * u;
+      lds[q >> 7][q & 127] = reg.v[u];
+    }
+  }
+}
+
+// One workgroup = one 128x128 output block x one row slice.  The next 32-row chunk is loaded
+// into registers while the MFMAs consume the current one from LDS.
+template <bool VEC>
+__global__ void __launch_bounds__(256) wgrad_partial(const float* __restrict__ dy, const float* __restrict__ x,
+                                                     int64_t R, int O, int I, int tiles_i, int64_t rows_per_split,
+                                                     float* __restrict__ part, float* __restrict__ part_b) {
+  __shared__ __attribute__((aligned(16))) float As[kWgChunk][kLdsStride];
+  __shared__ __attribute__((aligned(16))) float Bs[kWgChunk][kLdsStride];
+  const int ob = blockIdx.x / tiles_i, ib = blockIdx.x % tiles_i;
+  const int split = blockIdx.y;
+  const int64_t r_begin = static_cast<int64_t>(split) * rows_per_split;
+  const int64_t r_end = r_begin + rows_per_split < R ? r_begin + rows_per_split : R;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int o0 = ob * kWgTile, i0 = ib * kWgTile;
+  const bool do_bias = part_b && ib == 0;
+  floatx16 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[t][j] = 0.f;
+  float bsum = 0.f;
+  ChunkRegs<VEC> ra, rb;
+  load_chunk<VEC>(dy, O, o0, r_begin, r_end, ra);
+  load_chunk<VEC>(x, I, i0, r_begin, r_end, rb);
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += kWgChunk) {
+    store_chunk<VEC>(As, ra);
+    store_chunk<VEC>(Bs, rb);
+    __syncthreads();
+    if (r0 + kWgChunk < r_end) {  // prefetch the next chunk; it lands while the MFMAs run
+      load_chunk<VEC>(dy, O, o0, r0 + kWgChunk, r_end, ra);
+      load_chunk<VEC>(x, I, i0, r0 + kWgChunk, r_end, rb);
+    }
+#pragma unroll 4
+    for (int ks = 0; ks < kWgChunk / 2; ++ks) {
+      const int kr = 2 * ks + (lane >> 5);
+      const float a = As[kr][wave * 32 + (lane & 31)];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float b = Bs[kr][t * 32 + (lane & 31)];
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[t], 0, 0, 0);
+      }
+    }
+    if (do_bias && tid < kWgTile) {
+#pragma unroll 8
+      for (int rr = 0; rr < kWgChunk; ++rr) bsum += As[rr][tid];
+    }
+    __syncthreads();
+  }
+  // C/D layout of the 32x32 f32 accumulator: col = lane&31, row = (j&3) + 8*(j>>2) + 4*(lane>>5)
+  float* slab = part + static_cast<int64_t>(split) * O * I;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int i = i0 + t * 32 + (lane & 31);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int o = o0 + wave * 32 + (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
+      if (o < O && i < I) slab[static_cast<int64_t>(o) * I + i] = acc[t][j];
+    }
+  }
+  if (do_bias && tid < kWgTile && o0 + tid < O) part_b[static_cast<int64_t>(split) * O + o0 + tid] = bsum;
+}
+
+// out[e] = sum_s part[s][e] in a fixed order: each of the 4 waves of a block sums a quarter of
+// the slabs for the block's 64 elements, then the quarters are added in wave order.
+__global__ void __launch_bounds__(256) sum_slabs(const float* __restrict__ part, int64_t n, int splits,
+                                                 float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * 64 + lane;
+  const int per = (splits + 3) / 4;
+  const int k0 = wave * per, k1 = k0 + per < splits ? k0 + per : splits;
+  float s = 0.f;
+  if (e < n) {
+#pragma unroll 8
+    for (int k = k0; k < k1; ++k) s += part[static_cast<int64_t>(k) * n + e];
+  }
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && e < n) out[e] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+// rows per split: a multiple of the 32-row chunk, at least 64, at most kWgMaxSplits splits
+inline int64_t wgrad_rows_per_split(int64_t R) {
+  int64_t rps = (R + kWgMaxSplits - 1) / kWgMaxSplits;
+  rps = (rps + kWgChunk - 1) / kWgChunk * kWgChunk;
+  return rps < 64 ? 64 : rps;
+}
+inline int wgrad_splits(int64_t R) {
+  const int64_t rps = wgrad_rows_per_split(R);
+  return static_cast<int>((R + rps - 1) / rps);
+}
+
+}  // namespace x2g
+
+using namespace x2g;
+
+X2G_API size_t x2g_linear_wgrad_workspace(int64_t R, int32_t O, int32_t I) {
+  if (R <= 0 || O <= 0 || I <= 0) return 0;
+  const int64_t s = wgrad_splits(R);
+  return static_cast<size_t>(s) * (static_cast<int64_t>(O) * I + O) * sizeof(float);
+}
+
+X2G_API int x2g_linear_wgrad(const float* dy, const float* x, int64_t R, int32_t O, int32_t I, float* dw, float* db,
+                             void* workspace, size_t workspace_bytes, void* stream) {
+  if (R < 0 || O <= 0 || I <= 0 || !dw) return X2G_EINVAL;
+  hipStream_t st = as_stream(stream);
+  if (R == 0) {
+    hipError_t e = hipMemsetAsync(dw, 0, sizeof(float) * O * I, st);
+    if (e == hipSuccess && db) e = hipMemsetAsync(db, 0, sizeof(float) * O, st);
+    return e == hipSuccess ? X2G_OK : static_cast<int>(e);
+  }
+  if (!dy || !x) return X2G_EINVAL;
+  if (!workspace || workspace_bytes < x2g_linear_wgrad_workspace(R, O, I)) return X2G_EWORKSPACE;
+  const int splits = wgrad_splits(R);
+  float* part = static_cast<float*>(workspace);
+  float* part_b = db ? part + static_cast<int64_t>(splits) * O * I : nullptr;
+  const int tiles_o = (O + kWgTile - 1) / kWgTile, tiles_i = (I + kWgTile - 1) / kWgTile;
+  dim3 grid(tiles_o * tiles_i, splits);
+  const bool vec = (O % 4 == 0) && (I % 4 == 0) && (reinterpret_cast<uintptr_t>(dy) % 16 == 0) &&
+                   (reinterpret_cast<uintptr_t>(x) % 16 == 0);
+  if (vec)
+    wgrad_partial<true><<<grid, 256, 0, st>>>(dy, x, R, O, I, tiles_i, wgrad_rows_per_split(R), part, part_b);
+  else
+    wgrad_partial<false><<<grid, 256, 0, st>>>(dy, x, R, O, I, tiles_i, wgrad_rows_per_split(R), part, part_b);
+  int rc = last_launch_status();
+  if (rc) return rc;
+  const int64_t n = static_cast<int64_t>(O) * I;
+  sum_slabs<<<blocks_for(n, 64), 256, 0, st>>>(part, n, splits, dw);
+  if (db) sum_slabs<<<blocks_for(O, 64), 256, 0, st>>>(part_b, O, splits, db);
+  return last_launch_status();
+}

@@ -25,6 +25,39 @@ import torch.nn.functional as F
 from . import ops
 
 
+class Linear(nn.Linear):
+    """nn.Linear (same parameters / state_dict keys) running the fused dense kernels.
+
+    ``fused(x, act, res)`` = act(x W^T + b) + res in one kernel.  On CPU tensors it is plain
+    nn.Linear math so modules can be built, loaded and inspected on the host."""
+
+    def forward(self, x):
+        return self.fused(x)
+
+    def fused(self, x, act=ops.ACT_NONE, res=None):
+        if x.is_cuda:
+            return ops.dense(x, self.weight, self.bias, act=act, res=res)
+        y = super().forward(x)
+        if act == ops.ACT_SILU:
+            y = F.silu(y)
+        return y if res is None else y + res
+
+
+def run_mlp(layers, x):
+    """Apply a [Linear, SiLU, ..., Linear] stack, fusing each Linear with the SiLU after it."""
+    mods = list(layers)
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if isinstance(m, Linear) and i + 1 < len(mods) and isinstance(mods[i + 1], nn.SiLU):
+            x = m.fused(x, act=ops.ACT_SILU)
+            i += 2
+        else:
+            x = m(x)
+            i += 1
+    return x
+
+
 class poly_envelop(nn.Module):
     """u(d) = 1/x + a x^(p-1) + b x^p + c x^(p+1), x = d/cutoff, p = exponent+1 (no cutoff mask)."""
 
@@ -112,12 +145,11 @@ class EmbeddingBlock(nn.Module):
         super().__init__(**kwargs)
         self.AF = nn.SiLU()
         self.embedding = nn.Embedding(10, embedding_size, padding_idx=0, max_norm=3.0, scale_grad_by_freq=True)
-        self.lin = nn.Linear(embedding_size, embedding_size, bias=True)
+        self.lin = Linear(embedding_size, embedding_size, bias=True)
         self.activate = activation
 
     def forward(self, atomic_num):
-        h = self.lin(self.embedding(atomic_num))
-        return self.AF(h) if self.activate else h
+        return self.lin.fused(self.embedding(atomic_num), act=ops.ACT_SILU if self.activate else ops.ACT_NONE)
 
     def element_table(self, atomic_num):
         """Per-element rows [num_embeddings, D] equal to forward(z) for every z present.
@@ -138,8 +170,7 @@ class EmbeddingBlock(nn.Module):
         if emb.scale_grad_by_freq or emb.padding_idx is not None:
             c = counts if emb.scale_grad_by_freq else torch.ones_like(counts)
             w = _ScaleGradByCount.apply(w, c, emb.padding_idx)
-        h = self.lin(w)
-        return self.AF(h) if self.activate else h
+        return self.lin.fused(w, act=ops.ACT_SILU if self.activate else ops.ACT_NONE)
 
 
 class ResidualLayer(nn.Module):
@@ -147,19 +178,20 @@ class ResidualLayer(nn.Module):
 
     def __init__(self, in_channels, bias=True):
         super().__init__()
-        self.lin0 = nn.Linear(in_channels, in_channels, bias=bias)
-        self.lin1 = nn.Linear(in_channels, in_channels, bias=bias)
+        self.lin0 = Linear(in_channels, in_channels, bias=bias)
+        self.lin1 = Linear(in_channels, in_channels, bias=bias)
         self.AF = nn.SiLU()
 
     def forward(self, x):
-        return x + self.AF(self.lin1(self.AF(self.lin0(x))))
+        h = self.lin0.fused(x, act=ops.ACT_SILU)
+        return self.lin1.fused(h, act=ops.ACT_SILU, res=x)
 
 
 def _mlp(in_channels, num_target, depth):
     layers = []
     for _ in range(depth - 1):
-        layers += [nn.Linear(in_channels, in_channels), nn.SiLU()]
-    layers.append(nn.Linear(in_channels, num_target))
+        layers += [Linear(in_channels, in_channels), nn.SiLU()]
+    layers.append(Linear(in_channels, num_target))
     return nn.ModuleList(layers)
 
 
@@ -176,13 +208,11 @@ class AtomWise(nn.Module):
     def __init__(self, mlp_depth=3, in_channels=256, rbf_dim=16, num_target=1):
         super().__init__()
         self.mlp = _mlp(in_channels, num_target, mlp_depth)
-        self.lin_rbf = nn.Linear(rbf_dim, in_channels)
+        self.lin_rbf = Linear(rbf_dim, in_channels)
 
     def forward(self, x, rbf, num_atoms, edge_index_0, atom_rowptr=None):
         out = _edge_pool(x, self.lin_rbf(rbf), edge_index_0, num_atoms, atom_rowptr)
-        for layer in self.mlp:
-            out = layer(out)
-        return out
+        return run_mlp(self.mlp, out)
 
 
 class MolWise(nn.Module):
@@ -192,7 +222,7 @@ class MolWise(nn.Module):
         super().__init__()
         if pool_option not in ("mean", "add"):
             raise AssertionError("unsupport pooling option")
-        self.lin_rbf = nn.Linear(rbf_dim, in_channels)
+        self.lin_rbf = Linear(rbf_dim, in_channels)
         self.mlp = _mlp(in_channels, num_target, mlp_depth)
         self.pool_option = pool_option
 
@@ -204,7 +234,4 @@ class MolWise(nn.Module):
         if self.pool_option == "mean":
             cnt = (mol_rowptr[1:] - mol_rowptr[:-1]).clamp(min=1).to(pooled.dtype)
             pooled = pooled / cnt.unsqueeze(1)
-        out = pooled
-        for layer in self.mlp:
-            out = layer(out)
-        return out
+        return run_mlp(self.mlp, pooled)

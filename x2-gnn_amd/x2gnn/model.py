@@ -17,10 +17,10 @@ from __future__ import annotations
 
 import torch
 import torch.nn as nn
-from torch.nn import Linear, ModuleList, Sequential, SiLU
+from torch.nn import ModuleList, Sequential, SiLU
 
 from . import ops
-from .layers import AtomWise, MolWise, ResidualLayer
+from .layers import AtomWise, Linear, MolWise, ResidualLayer, run_mlp
 from .plan import GraphPlan
 from .sbftransformer_conv import SBFTransformerConv
 
@@ -69,7 +69,7 @@ class _Trunk(nn.Module):
 
     def _layers(self, data, plan, readout_fn):
         per_dst = "edge_attr_row" in data._store
-        edge_attr = self.edgenn(data.edge_attr)
+        edge_attr = run_mlp(self.edgenn, data.edge_attr)
         edge_row = data.edge_attr_row if per_dst else None
         out = data.x
         results = readout_fn(0, out)
@@ -79,8 +79,7 @@ class _Trunk(nn.Module):
                                 edge_attr=edge_attr, line_graph=plan.lg, edge_row=edge_row)
             out = self.LayerNorm(out, rowptr=plan.line_ptr, num_graphs=plan.num_graphs)
             out = self.bf_skip[i](out)
-            out = self.AF(self.dense_bf_skip[i](out))
-            out = out + res0
+            out = self.dense_bf_skip[i].fused(out, act=ops.ACT_SILU, res=res0)  # SiLU(dense(out)) + res0
             out = self.af_skip[i](out)
             results = results + readout_fn(i + 1, out)
         return results

@@ -197,9 +197,8 @@ class _SBFAttention(torch.autograd.Function):
         if mode == EDGE_PER_DST and ctx.edge_row is not None:
             # rows of the edge table are shared by many destinations: sum d_edge per table row
             onehot = torch.nn.functional.one_hot(ctx.edge_row.long(), ctx.edge_shape[0]).to(torch.float32)
-            d_edge = onehot.t() @ d_edge
-        dw = dproj.t() @ sbf
-        db = dproj.sum(0)
+            d_edge = linear_wgrad(d_edge, onehot, bias=False)[0].t().contiguous()
+        dw, db = linear_wgrad(dproj, sbf)
         return dq, dk, dv, dout, d_edge, None, dw, db, None, None, None, None, None
 
 
@@ -221,6 +220,81 @@ def sbf_attention(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg: LineGraph, heads: 
     dst = lg.trip_dst.long()
     prob = torch.exp(alpha - smax.index_select(0, dst)) / (sden.index_select(0, dst) + 1e-16)
     return out, prob
+
+
+# ---------------------------------------------------------------------------------- dense layers
+def linear_wgrad(dy, x, bias=True):
+    """(dW [O, I], db [O] or None) with dW = dy^T x, db = column sums of dy, for row-major
+    dy [R, O], x [R, I]: row-split MFMA partials + fixed-order slab sum (csrc/linear.hip)."""
+    _need_cuda(dy, x)
+    dy, x = _f32(dy), _f32(x)
+    R, O = dy.shape
+    I = x.shape[1]
+    dw = torch.empty(O, I, dtype=torch.float32, device=dy.device)
+    db = torch.empty(O, dtype=torch.float32, device=dy.device) if bias else None
+    ws_bytes = int(_lib.load().x2g_linear_wgrad_workspace(R, O, I))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dy.device)
+    call("x2g_linear_wgrad", ptr(dy), ptr(x), R, O, I, ptr(dw), ptr(db), ptr(ws), ws_bytes, stream_ptr())
+    return dw, db
+
+
+ACT_NONE, ACT_SILU = 0, 1
+
+
+class _DenseFn(torch.autograd.Function):
+    """y = act(x W^T + b) (+ res) in one kernel; backward = one data-gradient kernel (with the
+    activation derivative fused) + the row-split weight-gradient kernel."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, res, act):
+        N, K = weight.shape
+        lead = x.shape[:-1]
+        x2 = _f32(x.reshape(-1, K))
+        R = x2.shape[0]
+        w = _f32(weight)
+        b = _f32(bias) if bias is not None else None
+        r2 = _f32(res.reshape(-1, N)) if res is not None else None
+        y = torch.empty(R, N, dtype=torch.float32, device=x.device)
+        z = torch.empty(R, N, dtype=torch.float32, device=x.device) if act != ACT_NONE else None
+        call("x2g_dense_fwd", ptr(x2), ptr(w), ptr(b), R, K, N, act, ptr(r2), ptr(y), ptr(z), stream_ptr())
+        ctx.save_for_backward(x2, w, z)
+        ctx.act, ctx.has_bias, ctx.has_res, ctx.lead = act, bias is not None, res is not None, lead
+        return y.view(*lead, N)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, w, z = ctx.saved_tensors
+        N, K = w.shape
+        gy2 = _f32(gy.reshape(-1, N))
+        R = gy2.shape[0]
+        dx = dz = None
+        need_x = ctx.needs_input_grad[0]
+        if ctx.act != ACT_NONE:
+            dz = torch.empty(R, N, dtype=torch.float32, device=gy.device)
+            dx = torch.empty(R, K, dtype=torch.float32, device=gy.device)
+            call("x2g_dense_bwd_data", ptr(gy2), ptr(z), ctx.act, ptr(w), R, K, N, ptr(dx), ptr(dz), stream_ptr())
+        else:
+            dz = gy2
+            if need_x:
+                dx = torch.empty(R, K, dtype=torch.float32, device=gy.device)
+                call("x2g_dense_bwd_data", ptr(gy2), None, ACT_NONE, ptr(w), R, K, N, ptr(dx), None, stream_ptr())
+        dw = db = None
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            dw, db = linear_wgrad(dz, x2, bias=ctx.has_bias)
+        dres = gy if ctx.has_res else None
+        dx = dx.view(*ctx.lead, K) if (need_x and dx is not None) else None
+        return dx, dw, db, dres, None
+
+
+def dense(x, weight, bias=None, act=ACT_NONE, res=None):
+    """Fused row-wise Linear (+ SiLU) (+ residual) on the GPU (csrc/dense.hip)."""
+    if not x.is_cuda:
+        raise RuntimeError("x2gnn device ops need GPU tensors (no CPU fallback by design)")
+    return _DenseFn.apply(x, weight, bias, res, act)
+
+
+def linear(x, weight, bias=None):
+    return dense(x, weight, bias)
 
 
 # ---------------------------------------------------------------------------------- segments

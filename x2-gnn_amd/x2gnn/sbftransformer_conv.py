@@ -26,6 +26,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
+from .layers import Linear
 
 
 class SBFTransformerConv(nn.Module):
@@ -42,14 +43,14 @@ class SBFTransformerConv(nn.Module):
         self.dropout, self.edge_dim = dropout, edge_dim
         cin = (in_channels, in_channels) if isinstance(in_channels, int) else tuple(in_channels)
         hc = heads * out_channels
-        self.lin_key = nn.Linear(cin[0], hc)
-        self.lin_query = nn.Linear(cin[1], hc)
-        self.lin_value = nn.Linear(cin[0], hc)
-        self.lin_edge = nn.Linear(edge_dim, hc, bias=False) if edge_dim is not None else None
-        self.lin_skip = nn.Linear(cin[1], hc, bias=bias)
+        self.lin_key = Linear(cin[0], hc)
+        self.lin_query = Linear(cin[1], hc)
+        self.lin_value = Linear(cin[0], hc)
+        self.lin_edge = Linear(edge_dim, hc, bias=False) if edge_dim is not None else None
+        self.lin_skip = Linear(cin[1], hc, bias=bias)
         self.lin_beta = None
-        self.lin_sbf = nn.Linear(sbf_dim, hc, bias=True)
-        self.lin_rbf = nn.Linear(rbf_dim, cin[0], bias=False)
+        self.lin_sbf = Linear(sbf_dim, hc, bias=True)
+        self.lin_rbf = Linear(rbf_dim, cin[0], bias=False)
         self._alpha = None
 
     def forward(self, sbf, rbf, x, edge_index, edge_attr=None, return_attention_weights=None, *,

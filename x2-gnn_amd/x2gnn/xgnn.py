@@ -19,8 +19,9 @@ import torch
 import torch.nn as nn
 from torch.nn import SiLU
 
+from . import ops
 from .data import Data
-from .layers import EmbeddingBlock, F_B_2D, RadialBasis, poly_envelop
+from .layers import EmbeddingBlock, F_B_2D, Linear, RadialBasis, poly_envelop
 from .model import SBFTransformer, SBFTransformerGlobal
 from .plan import GraphPlan
 
@@ -34,9 +35,9 @@ class _XGNNBase(nn.Module):
         self.sbf_layer = F_B_2D(sbf_dim, rbf_dim, 5.0, 5)
         self.rbf_layer = RadialBasis(cutoff=5.0, embedding_size=rbf_dim)
         self.fin_model = trunk
-        self.mat_trans = nn.Linear(338, 2 * embedding_size)
-        self.rbf_trans = nn.Linear(rbf_dim, embedding_size)  # unused by the reference forward too
-        self.emb_trans = nn.Linear(embedding_size * 2, in_channels)
+        self.mat_trans = Linear(338, 2 * embedding_size)
+        self.rbf_trans = Linear(rbf_dim, embedding_size)  # unused by the reference forward too
+        self.emb_trans = Linear(embedding_size * 2, in_channels)
 
     def line_graph_data(self, data):
         """Featurisation (reference xgnn.py:39-72) -> (line-graph Data, GraphPlan)."""
@@ -47,11 +48,11 @@ class _XGNNBase(nn.Module):
         pos = data.atom_pos
         dist = (pos.index_select(0, lg.edge_src) - pos.index_select(0, lg.edge_dst)).norm(dim=1)
         env = self.envelop_function(dist).unsqueeze(1)
-        neo_x = self.AF(self.mat_trans(data.edge_attr * env))
+        neo_x = self.mat_trans.fused(data.edge_attr * env, act=ops.ACT_SILU)
         table = self.emb_block.element_table(data.x)
         sbf = self.sbf_layer.from_positions(dist, pos, lg)
         node_rbf = self.rbf_layer(dist) * env
-        neo_x = self.AF(self.emb_trans(neo_x))
+        neo_x = self.emb_trans.fused(neo_x, act=ops.ACT_SILU)
         line = Data(x=neo_x, edge_attr=table, edge_attr_row=plan.dst_type, edge_sbf=sbf, node_rbf=node_rbf)
         line._store["_x2g_plan"] = plan
         return line, plan
