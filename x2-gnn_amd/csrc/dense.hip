@@ -139,6 +139,173 @@ __global__ void __launch_bounds__(256) dense_rows(const float* __restrict__ A, c
   }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Persistent forms for the common case K <= 128 and N <= 128 (every 128x128 layer, lin_rbf with
+// K = 6, the readout head with N = 1): the weight is staged into LDS ONCE per workgroup and the
+// workgroup walks 32-row tiles, prefetching the next tile into registers while the MFMAs run.
+// One workgroup per CU (grid <= 256), 4 waves, wave w owns output columns 32w..32w+31.
+constexpr int kPTile = 32;       // rows per tile
+constexpr int kPStride = 129;    // LDS row stride (floats): conflict-free row and column access
+constexpr int kPGrid = 256;      // workgroups (one per CU)
+
+
+// 32 rows x 128 columns of a row-major [R, cols] matrix -> 16 floats per thread (coalesced).
+__device__ __forceinline__ void tile_load(const float* __restrict__ m, int64_t r0, int64_t R, int cols, float (&v)[16]) {
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int idx = threadIdx.x + 256 * u, rr = idx >> 7, cc = idx & 127;
+    const int64_t r = r0 + rr;
+    v[u] = (r < R && cc < cols) ? m[r * cols + cc] : 0.f;
+  }
+}
+
+__device__ __forceinline__ void tile_store(float (*lds)[kPStride], const float (&v)[16]) {
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int idx = threadIdx.x + 256 * u;
+    lds[idx >> 7][idx & 127] = v[u];
+  }
+}
+
+// y = act(x w^T + b) (+ res), z = x w^T + b.  KSTEPS = 2-row k steps compiled (K <= 2*KSTEPS).
+template <int KSTEPS>
+__global__ void __launch_bounds__(256) dense_fwd_persist(const float* __restrict__ X, const float* __restrict__ W,
+                                                         const float* __restrict__ bias,
+                                                         const float* __restrict__ res, int64_t R, int K, int N,
+                                                         int act, float* __restrict__ Y, float* __restrict__ Z) {
+  __shared__ float Ws[128][kPStride];          // B operand [k][n] = w[n][k]
+  __shared__ float As[2][kPTile][kPStride];    // x tile [r][k], double buffered
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int idx = tid; idx < 128 * 128; idx += 256) {
+    const int n = idx >> 7, k = idx & 127;
+    Ws[k][n] = (n < N && k < K) ? W[static_cast<int64_t>(n) * K + k] : 0.f;
+  }
+  const int64_t ntiles = (R + kPTile - 1) / kPTile;
+  const int n = wave * 32 + (lane & 31);
+  const float bn = (bias && n < N) ? bias[n] : 0.f;
+  float va[16];
+  int64_t t = blockIdx.x;
+  if (t < ntiles) tile_load(X, t * kPTile, R, K, va);
+  for (int it = 0; t < ntiles; t += gridDim.x, ++it) {
+    const int buf = it & 1;
+    tile_store(As[buf], va);
+    __syncthreads();
+    if (t + gridDim.x < ntiles) tile_load(X, (t + gridDim.x) * kPTile, R, K, va);
+    floatx16 acc;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KSTEPS; ++ks) {
+      const int kr = 2 * ks + (lane >> 5);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[buf][lane & 31][kr], Ws[kr][wave * 32 + (lane & 31)], acc, 0, 0, 0);
+    }
+    if (n < N) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int64_t r = t * kPTile + (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
+        if (r >= R) continue;
+        float v = acc[j] + bn;
+        const int64_t o = r * N + n;
+        if (Z) Z[o] = v;
+        if (act == kActSilu) v = v / (1.0f + expf(-v));
+        if (res) v += res[o];
+        Y[o] = v;
+      }
+    }
+  }
+}
+
+// Backward of dense_fwd_persist, fused: dz = dy * act'(z); dx = dz w (if dx != NULL);
+// per-workgroup partial weight / bias gradients dz^T x and colsum(dz) over the workgroup's
+// tiles, written to slab blockIdx.x (summed afterwards in a fixed order).  NSTEPS: N <= 2*NSTEPS.
+template <int NSTEPS>
+__global__ void __launch_bounds__(256) dense_bwd_persist(const float* __restrict__ dY, const float* __restrict__ Zin,
+                                                         const float* __restrict__ X, const float* __restrict__ W,
+                                                         int64_t R, int K, int N, int act, float* __restrict__ dX,
+                                                         float* __restrict__ part_w, float* __restrict__ part_b) {
+  __shared__ float Ws[128][kPStride];          // B operand of dx = dz w: [n][k] = w[n][k]
+  __shared__ float Ds[2][kPTile][kPStride];    // dz tile [r][n]
+  __shared__ float Xs[2][kPTile][kPStride];    // x tile [r][k]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int idx = tid; idx < 128 * 128; idx += 256) {
+    const int nn = idx >> 7, k = idx & 127;
+    Ws[nn][k] = (nn < N && k < K) ? W[static_cast<int64_t>(nn) * K + k] : 0.f;
+  }
+  const int64_t ntiles = (R + kPTile - 1) / kPTile;
+  floatx16 accw[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) accw[q][j] = 0.f;
+  float bsum = 0.f;
+  float vd[16], vz[16], vx[16];
+  int64_t t = blockIdx.x;
+  auto load = [&](int64_t tt) {
+    tile_load(dY, tt * kPTile, R, N, vd);
+    if (act == kActSilu) tile_load(Zin, tt * kPTile, R, N, vz);
+    tile_load(X, tt * kPTile, R, K, vx);
+  };
+  if (t < ntiles) load(t);
+  for (int it = 0; t < ntiles; t += gridDim.x, ++it) {
+    const int buf = it & 1;
+    if (act == kActSilu) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const float s = 1.0f / (1.0f + expf(-vz[u]));
+        vd[u] = vd[u] * (s * (1.0f + vz[u] * (1.0f - s)));
+      }
+    }
+    tile_store(Ds[buf], vd);
+    tile_store(Xs[buf], vx);
+    __syncthreads();
+    if (t + gridDim.x < ntiles) load(t + gridDim.x);
+    if (dX) {  // dx tile = dz (32 x N) . w (N x K): wave w owns k columns 32w..
+      floatx16 acc;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < NSTEPS; ++ks) {
+        const int kr = 2 * ks + (lane >> 5);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ds[buf][lane & 31][kr], Ws[kr][wave * 32 + (lane & 31)], acc, 0, 0,
+                                                   0);
+      }
+      const int k = wave * 32 + (lane & 31);
+      if (k < K) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int64_t r = t * kPTile + (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
+          if (r < R) dX[r * K + k] = acc[j];
+        }
+      }
+    }
+    // dW[n][k] += sum_r dz[r][n] x[r][k]: wave w owns n rows 32w..32w+31, four 32-wide k blocks
+#pragma unroll 4
+    for (int ks = 0; ks < kPTile / 2; ++ks) {
+      const int rr = 2 * ks + (lane >> 5);
+      const float a = Ds[buf][rr][wave * 32 + (lane & 31)];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        accw[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Xs[buf][rr][q * 32 + (lane & 31)], accw[q], 0, 0, 0);
+    }
+    if (part_b && tid < 128) {
+#pragma unroll 8
+      for (int rr = 0; rr < kPTile; ++rr) bsum += Ds[buf][rr][tid];
+    }
+  }
+  float* slab = part_w + static_cast<int64_t>(blockIdx.x) * N * K;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int k = q * 32 + (lane & 31);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int nn = wave * 32 + (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
+      if (nn < N && k < K) slab[static_cast<int64_t>(nn) * K + k] = accw[q][j];
+    }
+  }
+  if (part_b && tid < N) part_b[static_cast<int64_t>(blockIdx.x) * N + tid] = bsum;
+}
+
 }  // namespace x2g
 
 using namespace x2g;
@@ -148,9 +315,18 @@ X2G_API int x2g_dense_fwd(const float* x, const float* w, const float* b, int64_
   if (R < 0 || K <= 0 || N <= 0 || (act != kActNone && act != kActSilu)) return X2G_EINVAL;
   if (R == 0) return X2G_OK;
   if (!x || !w || !y) return X2G_EINVAL;
+  hipStream_t st = as_stream(stream);
+  if (K <= 128 && N <= 128) {
+    const int64_t ntiles = (R + kPTile - 1) / kPTile;
+    const unsigned grid = static_cast<unsigned>(ntiles < kPGrid ? ntiles : kPGrid);
+    if (K <= 8)
+      dense_fwd_persist<4><<<grid, 256, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
+    else
+      dense_fwd_persist<64><<<grid, 256, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
+    return last_launch_status();
+  }
   dim3 grid(static_cast<unsigned>((R + kDenseRows - 1) / kDenseRows), (N + kDenseCols - 1) / kDenseCols);
-  dense_rows<true, kActNone><<<grid, 256, 0, as_stream(stream)>>>(x, w, b, res, nullptr, R, K, N, act, y, z,
-                                                                   nullptr);
+  dense_rows<true, kActNone><<<grid, 256, 0, st>>>(x, w, b, res, nullptr, R, K, N, act, y, z, nullptr);
   return last_launch_status();
 }
 
@@ -169,4 +345,68 @@ X2G_API int x2g_dense_bwd_data(const float* dy, const float* z, int act, const f
     dense_rows<false, kActNone><<<grid, 256, 0, as_stream(stream)>>>(dy, w, nullptr, nullptr, nullptr, R, N, K,
                                                                       kActNone, dx, nullptr, dz);
   return last_launch_status();
+}
+
+namespace x2g {  // slab sums come from linear.hip
+int sum_slabs_launch(const float* part, int64_t n, int splits, float* out, hipStream_t st);
+}  // namespace x2g
+
+X2G_API size_t x2g_linear_wgrad_workspace(int64_t R, int32_t O, int32_t I);
+X2G_API int x2g_linear_wgrad(const float* dy, const float* x, int64_t R, int32_t O, int32_t I, float* dw, float* db,
+                             void* workspace, size_t workspace_bytes, void* stream);
+
+static inline bool dense_persistent_bwd(int64_t R, int32_t K, int32_t N) { return K <= 128 && N <= 128 && R > 0; }
+
+X2G_API size_t x2g_dense_bwd_workspace(int64_t R, int32_t K, int32_t N) {
+  if (R <= 0 || K <= 0 || N <= 0) return 0;
+  if (dense_persistent_bwd(R, K, N)) {
+    const int64_t ntiles = (R + kPTile - 1) / kPTile;
+    const int64_t g = ntiles < kPGrid ? ntiles : kPGrid;
+    return static_cast<size_t>(g) * (static_cast<int64_t>(N) * K + N) * sizeof(float);
+  }
+  // general path: dz [R, N] + the row-split weight-gradient slabs
+  const size_t dz = ((static_cast<size_t>(R) * N * sizeof(float)) + 255) / 256 * 256;
+  return dz + x2g_linear_wgrad_workspace(R, N, K);
+}
+
+X2G_API int x2g_dense_bwd(const float* dy, const float* z, int act, const float* x, const float* w, int64_t R,
+                          int32_t K, int32_t N, float* dx, float* dw, float* db, void* workspace,
+                          size_t workspace_bytes, void* stream) {
+  if (R < 0 || K <= 0 || N <= 0 || (act != kActNone && act != kActSilu) || !dw) return X2G_EINVAL;
+  hipStream_t st = as_stream(stream);
+  if (R == 0) {
+    hipError_t e = hipMemsetAsync(dw, 0, sizeof(float) * N * K, st);
+    if (e == hipSuccess && db) e = hipMemsetAsync(db, 0, sizeof(float) * N, st);
+    return e == hipSuccess ? X2G_OK : static_cast<int>(e);
+  }
+  if (!dy || !x || !w || (act == kActSilu && !z)) return X2G_EINVAL;
+  if (!workspace || workspace_bytes < x2g_dense_bwd_workspace(R, K, N)) return X2G_EWORKSPACE;
+  if (dense_persistent_bwd(R, K, N)) {
+    const int64_t ntiles = (R + kPTile - 1) / kPTile;
+    const int grid = static_cast<int>(ntiles < kPGrid ? ntiles : kPGrid);
+    float* part_w = static_cast<float*>(workspace);
+    float* part_b = db ? part_w + static_cast<int64_t>(grid) * N * K : nullptr;
+    if (N <= 8)
+      dense_bwd_persist<4><<<grid, 256, 0, st>>>(dy, z, x, w, R, K, N, act, dx, part_w, part_b);
+    else
+      dense_bwd_persist<64><<<grid, 256, 0, st>>>(dy, z, x, w, R, K, N, act, dx, part_w, part_b);
+    int rc = last_launch_status();
+    if (rc) return rc;
+    if ((rc = sum_slabs_launch(part_w, static_cast<int64_t>(N) * K, grid, dw, st))) return rc;
+    if (db && (rc = sum_slabs_launch(part_b, N, grid, db, st))) return rc;
+    return X2G_OK;
+  }
+  // general shapes: dz = dy * act'(z) and dx = dz w in one kernel, then the weight gradient
+  float* dzbuf = static_cast<float*>(workspace);
+  const size_t dz_bytes = ((static_cast<size_t>(R) * N * sizeof(float)) + 255) / 256 * 256;
+  const float* dzp = dy;
+  int rc;
+  if (act != kActNone || dx) {
+    float* dx_tmp = dx;
+    if (!dx_tmp) return X2G_EUNSUPPORTED;  // general path needs a dx buffer when an activation is fused
+    if ((rc = x2g_dense_bwd_data(dy, z, act, w, R, K, N, dx_tmp, act != kActNone ? dzbuf : nullptr, stream))) return rc;
+    if (act != kActNone) dzp = dzbuf;
+  }
+  return x2g_linear_wgrad(dzp, x, R, N, K, dw, db, static_cast<char*>(workspace) + dz_bytes,
+                          workspace_bytes - dz_bytes, stream);
 }

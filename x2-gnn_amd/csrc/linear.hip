@@ -153,6 +153,11 @@ __global__ void __launch_bounds__(256) sum_slabs(const float* __restrict__ part,
 }
 
 // rows per split: a multiple of the 32-row chunk, at least 64, at most kWgMaxSplits splits
+int sum_slabs_launch(const float* part, int64_t n, int splits, float* out, hipStream_t st) {
+  sum_slabs<<<blocks_for(n, 64), 256, 0, st>>>(part, n, splits, out);
+  return last_launch_status();
+}
+
 inline int64_t wgrad_rows_per_split(int64_t R) {
   int64_t rps = (R + kWgMaxSplits - 1) / kWgMaxSplits;
   rps = (rps + kWgChunk - 1) / kWgChunk * kWgChunk;

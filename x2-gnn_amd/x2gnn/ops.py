@@ -267,22 +267,17 @@ class _DenseFn(torch.autograd.Function):
         N, K = w.shape
         gy2 = _f32(gy.reshape(-1, N))
         R = gy2.shape[0]
-        dx = dz = None
+        dev = gy.device
         need_x = ctx.needs_input_grad[0]
-        if ctx.act != ACT_NONE:
-            dz = torch.empty(R, N, dtype=torch.float32, device=gy.device)
-            dx = torch.empty(R, K, dtype=torch.float32, device=gy.device)
-            call("x2g_dense_bwd_data", ptr(gy2), ptr(z), ctx.act, ptr(w), R, K, N, ptr(dx), ptr(dz), stream_ptr())
-        else:
-            dz = gy2
-            if need_x:
-                dx = torch.empty(R, K, dtype=torch.float32, device=gy.device)
-                call("x2g_dense_bwd_data", ptr(gy2), None, ACT_NONE, ptr(w), R, K, N, ptr(dx), None, stream_ptr())
-        dw = db = None
-        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
-            dw, db = linear_wgrad(dz, x2, bias=ctx.has_bias)
+        dx = torch.empty(R, K, dtype=torch.float32, device=dev) if (need_x or ctx.act != ACT_NONE) else None
+        dw = torch.empty(N, K, dtype=torch.float32, device=dev)
+        db = torch.empty(N, dtype=torch.float32, device=dev) if ctx.has_bias else None
+        ws_bytes = int(_lib.load().x2g_dense_bwd_workspace(R, K, N))
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        call("x2g_dense_bwd", ptr(gy2), ptr(z), ctx.act, ptr(x2), ptr(w), R, K, N, ptr(dx), ptr(dw), ptr(db), ptr(ws),
+             ws_bytes, stream_ptr())
         dres = gy if ctx.has_res else None
-        dx = dx.view(*ctx.lead, K) if (need_x and dx is not None) else None
+        dx = dx.view(*ctx.lead, K) if need_x else None
         return dx, dw, db, dres, None
 
 
