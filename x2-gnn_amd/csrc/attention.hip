@@ -68,21 +68,26 @@ struct AttnArgs {
   float* dv;
 };
 
+// Inactive lanes (D < 64 * CPL) read the row's first element instead of being branched around,
+// so consecutive row loads stay independent (see ld_pin in common.hpp).
 template <int CPL>
 __device__ __forceinline__ void load_row(const float* __restrict__ p, bool act, float (&r)[CPL]) {
   if (CPL == 2) {
-    float2 x = act ? *reinterpret_cast<const float2*>(p) : make_float2(0.f, 0.f);
-    r[0] = x.x;
-    r[1] = x.y;
+    const float2 x = ld_pin2(p);
+    r[0] = keep(x.x, act);
+    r[1] = keep(x.y, act);
   } else if (CPL == 4) {
-    float4 x = act ? *reinterpret_cast<const float4*>(p) : make_float4(0.f, 0.f, 0.f, 0.f);
-    r[0] = x.x;
-    r[1] = x.y;
-    r[2] = x.z;
-    r[3] = x.w;
+    const float4 x = ld_pin4(p);
+    r[0] = keep(x.x, act);
+    r[1] = keep(x.y, act);
+    r[2] = keep(x.z, act);
+    r[3] = keep(x.w, act);
   } else {
 #pragma unroll
-    for (int j = 0; j < CPL; ++j) r[j] = act ? p[j] : 0.f;
+    for (int j = 0; j < CPL; ++j) {
+      const float x = ld_pin(p + j);
+      r[j] = keep(x, act);
+    }
   }
 }
 
@@ -123,7 +128,7 @@ __device__ __forceinline__ void load_weights(const AttnArgs& a, int c0, bool act
   for (int j = 0; j < CPL; ++j) {
     const float* wrow = a.w + static_cast<int64_t>(c0 + j) * kS;
 #pragma unroll
-    for (int s = 0; s < kS; ++s) wr[j][s] = act ? wrow[s] : 0.f;
+    for (int s = 0; s < kS; ++s) wr[j][s] = keep(wrow[s], act);
     br[j] = act ? a.b[c0 + j] : 0.f;
   }
 }

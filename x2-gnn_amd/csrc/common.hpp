@@ -23,6 +23,19 @@ inline unsigned blocks_for(int64_t n, int per_block) {
   return static_cast<unsigned>((n + per_block - 1) / per_block);
 }
 
+// Tuning knobs for A/B experiments (x2g_tuning in line_graph.hip); 0 = default everywhere.
+enum TuneKey { kTuneDenseFwd = 0, kTuneDenseBwd = 1, kTuneAttn = 2, kTuneCount = 16 };
+int tuning(int key);
+
+// Masked loads without control flow.  Written as `ok ? load : 0`, the compiler sinks each load
+// into a conditional block and then waits for it (s_waitcnt vmcnt(0)) before issuing the next:
+// a batch of independent loads becomes a serial chain.  Loading from a clamped (always valid)
+// address and multiplying by a 0/1 mask keeps every load unconditional and in flight together.
+__device__ __forceinline__ float ld_pin(const float* p) { return *p; }
+__device__ __forceinline__ float2 ld_pin2(const float* p) { return *reinterpret_cast<const float2*>(p); }
+__device__ __forceinline__ float4 ld_pin4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float keep(float v, bool ok) { return v * (ok ? 1.0f : 0.0f); }
+
 // Wave-uniform value (forces the compiler to treat it as scalar).
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 

@@ -57,16 +57,14 @@ __global__ void __launch_bounds__(256) dense_rows(const float* __restrict__ A, c
       const int q = tid + 256 * u, rr = q >> 5, kk = q & 31;
       const int64_t r = m0 + rr;
       const int k = k0 + kk;
-      float v = 0.f;
-      if (r < R && k < K) {
-        v = A[r * K + k];
-        if (ACT_IN == kActSilu) {  // dZ = dY * silu'(Z)
-          const float z = zin[r * K + k];
-          const float s = sigmoidf_(z);
-          v = v * (s * (1.0f + z * (1.0f - s)));
-        }
+      const int64_t o = (r < R ? r : R - 1) * K + (k < K ? k : K - 1);
+      float v = ld_pin(A + o);
+      if (ACT_IN == kActSilu) {  // dZ = dY * silu'(Z)
+        const float z = ld_pin(zin + o);
+        const float s = sigmoidf_(z);
+        v = v * (s * (1.0f + z * (1.0f - s)));
       }
-      ra[u] = v;
+      ra[u] = keep(v, r < R && k < K);
     }
 #pragma unroll
     for (int u = 0; u < 16; ++u) {  // B chunk: 32 k x 128 n
@@ -80,9 +78,9 @@ __global__ void __launch_bounds__(256) dense_rows(const float* __restrict__ A, c
         nn = q & 127;
       }
       const int k = k0 + kk, n = n0 + nn;
-      float v = 0.f;
-      if (k < K && n < N) v = BT ? Bm[static_cast<int64_t>(n) * K + k] : Bm[static_cast<int64_t>(k) * N + n];
-      rb[u] = v;
+      const int kc = k < K ? k : K - 1, nc = n < N ? n : N - 1;
+      const float v = ld_pin(BT ? Bm + static_cast<int64_t>(nc) * K + kc : Bm + static_cast<int64_t>(kc) * N + nc);
+      rb[u] = keep(v, k < K && n < N);
     }
   };
   auto store = [&](int k0) {
@@ -151,12 +149,40 @@ constexpr int kPGrid = 256;      // workgroups (one per CU)
 
 
 // 32 rows x 128 columns of a row-major [R, cols] matrix -> 16 floats per thread (coalesced).
+// Branch-free: addresses are clamped into the matrix and out-of-range values masked to 0, so
+// all 16 loads issue back to back.
 __device__ __forceinline__ void tile_load(const float* __restrict__ m, int64_t r0, int64_t R, int cols, float (&v)[16]) {
 #pragma unroll
   for (int u = 0; u < 16; ++u) {
     const int idx = threadIdx.x + 256 * u, rr = idx >> 7, cc = idx & 127;
     const int64_t r = r0 + rr;
-    v[u] = (r < R && cc < cols) ? m[r * cols + cc] : 0.f;
+    const int64_t rc = r < R ? r : R - 1;
+    const int ccc = cc < cols ? cc : cols - 1;
+    const float x = ld_pin(m + rc * cols + ccc);
+    v[u] = keep(x, r < R && cc < cols);
+  }
+}
+
+// Stage a [N, K] weight (N, K <= 128, zero padded) into LDS, transposed ([k][n]) or not ([n][k]).
+// Loads go out 16 at a time so their latencies overlap (the weight is L2-resident after the
+// first workgroup touches it).
+template <bool TRANSPOSE>
+__device__ __forceinline__ void stage_weight(float (*ws)[kPStride], const float* __restrict__ W, int N, int K) {
+#pragma unroll 1
+  for (int round = 0; round < 4; ++round) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int idx = threadIdx.x + 256 * (16 * round + u), n = idx >> 7, k = idx & 127;
+      const float x = ld_pin(W + static_cast<int64_t>(n < N ? n : N - 1) * K + (k < K ? k : K - 1));
+      v[u] = keep(x, n < N && k < K);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int idx = threadIdx.x + 256 * (16 * round + u), n = idx >> 7, k = idx & 127;
+      if (TRANSPOSE) ws[k][n] = v[u];
+      else ws[n][k] = v[u];
+    }
   }
 }
 
@@ -176,11 +202,8 @@ __global__ void __launch_bounds__(256) dense_fwd_persist(const float* __restrict
                                                          int act, float* __restrict__ Y, float* __restrict__ Z) {
   __shared__ float Ws[128][kPStride];          // B operand [k][n] = w[n][k]
   __shared__ float As[2][kPTile][kPStride];    // x tile [r][k], double buffered
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int idx = tid; idx < 128 * 128; idx += 256) {
-    const int n = idx >> 7, k = idx & 127;
-    Ws[k][n] = (n < N && k < K) ? W[static_cast<int64_t>(n) * K + k] : 0.f;
-  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  stage_weight<true>(Ws, W, N, K);
   const int64_t ntiles = (R + kPTile - 1) / kPTile;
   const int n = wave * 32 + (lane & 31);
   const float bn = (bias && n < N) ? bias[n] : 0.f;
@@ -192,25 +215,43 @@ __global__ void __launch_bounds__(256) dense_fwd_persist(const float* __restrict
     tile_store(As[buf], va);
     __syncthreads();
     if (t + gridDim.x < ntiles) tile_load(X, (t + gridDim.x) * kPTile, R, K, va);
-    floatx16 acc;
+    // two independent accumulator chains (k steps [0, KSTEPS/2) and [KSTEPS/2, KSTEPS)) so
+    // consecutive MFMAs never wait on each other's result
+    floatx16 acc0, acc1;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+    for (int j = 0; j < 16; ++j) {
+      acc0[j] = 0.f;
+      acc1[j] = 0.f;
+    }
+    constexpr int HALF = KSTEPS / 2;
 #pragma unroll
-    for (int ks = 0; ks < KSTEPS; ++ks) {
-      const int kr = 2 * ks + (lane >> 5);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[buf][lane & 31][kr], Ws[kr][wave * 32 + (lane & 31)], acc, 0, 0, 0);
+    for (int ks = 0; ks < HALF; ++ks) {
+      const int k0 = 2 * ks + (lane >> 5), k1 = 2 * (ks + HALF) + (lane >> 5);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(As[buf][lane & 31][k0], Ws[k0][wave * 32 + (lane & 31)], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(As[buf][lane & 31][k1], Ws[k1][wave * 32 + (lane & 31)], acc1, 0, 0, 0);
+    }
+    // epilogue: all residual loads first (clamped rows), then bias / activation / stores
+    const int64_t rbase = t * kPTile + 4 * (lane >> 5);
+    float rv[16];
+    if (res) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int64_t r = rbase + (j & 3) + 8 * (j >> 2);
+        rv[j] = res[(r < R ? r : R - 1) * N + (n < N ? n : N - 1)];
+      }
     }
     if (n < N) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        const int64_t r = t * kPTile + (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
-        if (r >= R) continue;
-        float v = acc[j] + bn;
+        const int64_t r = rbase + (j & 3) + 8 * (j >> 2);
+        float v = acc0[j] + acc1[j] + bn;
         const int64_t o = r * N + n;
-        if (Z) Z[o] = v;
-        if (act == kActSilu) v = v / (1.0f + expf(-v));
-        if (res) v += res[o];
-        Y[o] = v;
+        if (r < R) {
+          if (Z) Z[o] = v;
+          if (act == kActSilu) v = v / (1.0f + expf(-v));
+          if (res) v += rv[j];
+          Y[o] = v;
+        }
       }
     }
   }
@@ -228,10 +269,7 @@ __global__ void __launch_bounds__(256) dense_bwd_persist(const float* __restrict
   __shared__ float Ds[2][kPTile][kPStride];    // dz tile [r][n]
   __shared__ float Xs[2][kPTile][kPStride];    // x tile [r][k]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int idx = tid; idx < 128 * 128; idx += 256) {
-    const int nn = idx >> 7, k = idx & 127;
-    Ws[nn][k] = (nn < N && k < K) ? W[static_cast<int64_t>(nn) * K + k] : 0.f;
-  }
+  stage_weight<false>(Ws, W, N, K);
   const int64_t ntiles = (R + kPTile - 1) / kPTile;
   floatx16 accw[4];
 #pragma unroll
@@ -261,21 +299,27 @@ __global__ void __launch_bounds__(256) dense_bwd_persist(const float* __restrict
     __syncthreads();
     if (t + gridDim.x < ntiles) load(t + gridDim.x);
     if (dX) {  // dx tile = dz (32 x N) . w (N x K): wave w owns k columns 32w..
-      floatx16 acc;
+      floatx16 acc0, acc1;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+      for (int j = 0; j < 16; ++j) {
+        acc0[j] = 0.f;
+        acc1[j] = 0.f;
+      }
+      constexpr int HALF = NSTEPS / 2;
 #pragma unroll
-      for (int ks = 0; ks < NSTEPS; ++ks) {
-        const int kr = 2 * ks + (lane >> 5);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Ds[buf][lane & 31][kr], Ws[kr][wave * 32 + (lane & 31)], acc, 0, 0,
-                                                   0);
+      for (int ks = 0; ks < HALF; ++ks) {
+        const int k0 = 2 * ks + (lane >> 5), k1 = 2 * (ks + HALF) + (lane >> 5);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(Ds[buf][lane & 31][k0], Ws[k0][wave * 32 + (lane & 31)], acc0, 0,
+                                                    0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(Ds[buf][lane & 31][k1], Ws[k1][wave * 32 + (lane & 31)], acc1, 0,
+                                                    0, 0);
       }
       const int k = wave * 32 + (lane & 31);
       if (k < K) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           const int64_t r = t * kPTile + (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
-          if (r < R) dX[r * K + k] = acc[j];
+          if (r < R) dX[r * K + k] = acc0[j] + acc1[j];
         }
       }
     }
@@ -306,6 +350,134 @@ __global__ void __launch_bounds__(256) dense_bwd_persist(const float* __restrict
   if (part_b && tid < N) part_b[static_cast<int64_t>(blockIdx.x) * N + tid] = bsum;
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Weight-in-registers form (K, N <= 128).  A workgroup (4 waves) walks 64-row blocks; wave w owns
+// rows 32*(w>>1).. and output columns 64*(w&1).. (two 32x32 MFMA tiles), and keeps the MFMA B
+// fragments of its 64 weight columns in VGPRs for the whole kernel, so the inner loop is ONE
+// LDS read (the A fragment) feeding two independent MFMAs.  LDS holds the weight only during the
+// prologue and is then reused as the double-buffered 64-row A block (66 KB: two workgroups per CU).
+//   DGRAD = false: y = act(x w^T + b) (+ res), z = x w^T + b           (B[k][n] = w[n][k])
+//   DGRAD = true : a = dy * act'(z) -> dz (optional), dx = a w         (B[k][n] = w[k][n])
+constexpr int kWBlock = 64;
+constexpr int kWGrid = 512;
+constexpr int kWPer = kWBlock * 128 / 256;  // A elements staged per thread per block
+
+template <bool DGRAD>
+__device__ __forceinline__ void wreg_load_block(const float* __restrict__ A, const float* __restrict__ zin,
+                                                int64_t blk, int64_t R, int Kin, int act, float (&xa)[kWPer]) {
+#pragma unroll
+  for (int u = 0; u < kWPer; ++u) {
+    const int idx = threadIdx.x + 256 * u, rr = idx >> 7, cc = idx & 127;
+    const int64_t r = blk * kWBlock + rr;
+    const int64_t rc = r < R ? r : R - 1;
+    const int ccc = cc < Kin ? cc : Kin - 1;
+    float v = ld_pin(A + rc * Kin + ccc);
+    if (DGRAD && act == kActSilu) {
+      const float z = ld_pin(zin + rc * Kin + ccc);
+      const float sg = 1.0f / (1.0f + expf(-z));
+      v = v * (sg * (1.0f + z * (1.0f - sg)));
+    }
+    xa[u] = keep(v, r < R && cc < Kin);
+  }
+}
+
+template <int KSTEPS, bool DGRAD>
+__global__ void __launch_bounds__(256) dense_wreg(const float* __restrict__ A, const float* __restrict__ W,
+                                                     const float* __restrict__ bias, const float* __restrict__ res,
+                                                     const float* __restrict__ zin, int64_t R, int Kin, int Nout,
+                                                     int Nw, int Kw, int act, float* __restrict__ Y,
+                                                     float* __restrict__ zout, float* __restrict__ aout) {
+  // Kin: contraction length (columns of A); Nout: output columns; W is [Nw, Kw] row-major.
+  // prologue: the weight image [128][129]; afterwards the same bytes hold the A blocks [2][64][129]
+  __shared__ union {
+    float w[128][kPStride];
+    float a[2][kWBlock][kPStride];
+  } sh;
+  auto& Ws = sh.w;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rt = wave >> 1, ch = wave & 1;
+  stage_weight<false>(Ws, W, Nw, Kw);
+  __syncthreads();
+  float wr[2][KSTEPS];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int s2 = 0; s2 < KSTEPS; ++s2) {
+      const int kk = 2 * s2 + (lane >> 5), nn = 64 * ch + 32 * t + (lane & 31);
+      wr[t][s2] = DGRAD ? Ws[kk][nn] : Ws[nn][kk];
+    }
+  float bn[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int n = 64 * ch + 32 * t + (lane & 31);
+    bn[t] = (bias && n < Nout) ? bias[n] : 0.f;
+  }
+  __syncthreads();  // the weight image is dead from here on; the space becomes the A blocks
+  const int64_t nblocks = (R + kWBlock - 1) / kWBlock;
+  constexpr int PER = kWPer;
+  float xa[PER];
+  int64_t blk = blockIdx.x;
+  if (blk < nblocks) wreg_load_block<DGRAD>(A, zin, blk, R, Kin, act, xa);
+  for (int it = 0; blk < nblocks; blk += gridDim.x, ++it) {
+    auto& As = sh.a[it & 1];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int idx = tid + 256 * u;
+      As[idx >> 7][idx & 127] = xa[u];
+    }
+    if (DGRAD && aout) {  // dz = dy * act'(z), kept for the weight gradient
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int idx = tid + 256 * u, rr = idx >> 7, cc = idx & 127;
+        const int64_t r = blk * kWBlock + rr;
+        if (r < R && cc < Kin) aout[r * Kin + cc] = xa[u];
+      }
+    }
+    __syncthreads();
+    if (blk + gridDim.x < nblocks) wreg_load_block<DGRAD>(A, zin, blk + gridDim.x, R, Kin, act, xa);
+    floatx16 acc0, acc1;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      acc0[j] = 0.f;
+      acc1[j] = 0.f;
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < KSTEPS; ++s2) {
+      const float a = As[32 * rt + (lane & 31)][2 * s2 + (lane >> 5)];
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, wr[0][s2], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, wr[1][s2], acc1, 0, 0, 0);
+    }
+    const int64_t rbase = blk * kWBlock + 32 * rt + 4 * (lane >> 5);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = 64 * ch + 32 * t + (lane & 31);
+      float rv[16];
+      if (res) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int64_t r = rbase + (j & 3) + 8 * (j >> 2);
+          rv[j] = ld_pin(res + (r < R ? r : R - 1) * Nout + (n < Nout ? n : Nout - 1));
+        }
+      }
+      if (n < Nout) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int64_t r = rbase + (j & 3) + 8 * (j >> 2);
+          if (r < R) {
+            float v = (t == 0 ? acc0[j] : acc1[j]) + bn[t];
+            const int64_t o = r * Nout + n;
+            if (zout) zout[o] = v;
+            if (!DGRAD && act == kActSilu) v = v / (1.0f + expf(-v));
+            if (res) v += rv[j];
+            Y[o] = v;
+          }
+        }
+      }
+    }
+  }
+}
+
 }  // namespace x2g
 
 using namespace x2g;
@@ -316,13 +488,23 @@ X2G_API int x2g_dense_fwd(const float* x, const float* w, const float* b, int64_
   if (R == 0) return X2G_OK;
   if (!x || !w || !y) return X2G_EINVAL;
   hipStream_t st = as_stream(stream);
-  if (K <= 128 && N <= 128) {
+  const int variant = tuning(kTuneDenseFwd);  // 0: LDS-persistent, 1: weight-in-registers, 2: tiled
+  if (K <= 128 && N <= 128 && variant == 0) {
     const int64_t ntiles = (R + kPTile - 1) / kPTile;
     const unsigned grid = static_cast<unsigned>(ntiles < kPGrid ? ntiles : kPGrid);
     if (K <= 8)
       dense_fwd_persist<4><<<grid, 256, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
     else
       dense_fwd_persist<64><<<grid, 256, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
+    return last_launch_status();
+  }
+  if (K <= 128 && N <= 128 && variant == 1) {
+    const int64_t nblk = (R + kWBlock - 1) / kWBlock;
+    const unsigned grid = static_cast<unsigned>(nblk < kWGrid ? nblk : kWGrid);
+    if (K <= 8)
+      dense_wreg<4, false><<<grid, 256, 0, st>>>(x, w, b, res, nullptr, R, K, N, N, K, act, y, z, nullptr);
+    else
+      dense_wreg<64, false><<<grid, 256, 0, st>>>(x, w, b, res, nullptr, R, K, N, N, K, act, y, z, nullptr);
     return last_launch_status();
   }
   dim3 grid(static_cast<unsigned>((R + kDenseRows - 1) / kDenseRows), (N + kDenseCols - 1) / kDenseCols);

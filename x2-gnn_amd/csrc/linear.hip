@@ -35,19 +35,21 @@ __device__ __forceinline__ void load_chunk(const float* __restrict__ m, int cols
     for (int u = 0; u < 4; ++u) {
       const int q = tid + 256 * u, rr = q >> 5, c = c0 + 4 * (q & 31);
       const int64_t r = r0 + rr;
-      float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (r < r_end && c < cols) f = *reinterpret_cast<const float4*>(m + r * cols + c);
-      reg.v[4 * u] = f.x;
-      reg.v[4 * u + 1] = f.y;
-      reg.v[4 * u + 2] = f.z;
-      reg.v[4 * u + 3] = f.w;
+      const bool ok = r < r_end && c < cols;
+      const float4 f = ld_pin4(m + (ok ? r * cols + c : 0));
+      reg.v[4 * u] = keep(f.x, ok);
+      reg.v[4 * u + 1] = keep(f.y, ok);
+      reg.v[4 * u + 2] = keep(f.z, ok);
+      reg.v[4 * u + 3] = keep(f.w, ok);
     }
   } else {
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       const int q = tid + 256 * u, rr = q >> 7, c = c0 + (q & 127);
       const int64_t r = r0 + rr;
-      reg.v[u] = (r < r_end && c < cols) ? m[r * cols + c] : 0.f;
+      const bool ok = r < r_end && c < cols;
+      const float x = ld_pin(m + (ok ? r * cols + c : 0));
+      reg.v[u] = keep(x, ok);
     }
   }
 }

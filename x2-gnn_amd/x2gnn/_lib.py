@@ -23,6 +23,7 @@ _SZ = ctypes.c_size_t
 # name -> argtypes (restype int unless noted); mirrors include/x2g.h
 SIGNATURES = {
     "x2g_abi_version": [],
+    "x2g_tuning": [ctypes.c_int, ctypes.c_int],
     "x2g_status_string": [ctypes.c_int],
     "x2g_csr_rowptr": [_P, _I64, _I64, _P, _P],
     "x2g_vertex_to_edge_workspace": [_I64, _I64],
