@@ -104,7 +104,7 @@ __device__ __forceinline__ void store_row(float* __restrict__ p, bool act, const
   }
 }
 
-// sp[j] = b[j] + sum_s W[c0+j][s] * sbf_t[s]; the sbf row pointer is wave-uniform.
+// sp[j] = b[j] + sum_s W[c0+j][s] * sbf_t[s]; the sbf row pointer is wave-uniform (scalar loads).
 template <int CPL>
 __device__ __forceinline__ void sbf_project(const float (&wr)[CPL][kS], const float (&br)[CPL],
                                             const float* __restrict__ srow, float (&sp)[CPL]) {
@@ -122,14 +122,14 @@ __device__ __forceinline__ void sbf_project(const float (&wr)[CPL][kS], const fl
 }
 
 template <int CPL>
-__device__ __forceinline__ void load_weights(const AttnArgs& a, int c0, bool act, float (&wr)[CPL][kS],
-                                             float (&br)[CPL]) {
+__device__ __forceinline__ void load_weights(const float* __restrict__ w, const float* __restrict__ b, int c0,
+                                             bool act, float (&wr)[CPL][kS], float (&br)[CPL]) {
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
-    const float* wrow = a.w + static_cast<int64_t>(c0 + j) * kS;
+    const float* wrow = w + static_cast<int64_t>(c0 + j) * kS;
 #pragma unroll
     for (int s = 0; s < kS; ++s) wr[j][s] = keep(wrow[s], act);
-    br[j] = act ? a.b[c0 + j] : 0.f;
+    br[j] = keep(b[c0 + j], act);
   }
 }
 
@@ -137,133 +137,157 @@ __device__ __forceinline__ int wave_id_global() {
   return uniform(static_cast<int>(blockIdx.x) * kAttnWaves + static_cast<int>(threadIdx.x >> 6));
 }
 
+template <int CPL>
+__device__ __forceinline__ void zero_row(float (&r)[CPL]) {
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) r[j] = 0.f;
+}
+
+// Every kernel below takes its pointers as __restrict__ parameters: with them the compiler may
+// serve wave-uniform reads (row pointers, triplet indices, the sbf row) from the scalar cache.
+
 // ------------------------------------------------------------------------------ forward
-template <int CPL, int LPH>
-__global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
+template <int CPL, int LPH, int MODE>
+__global__ void __launch_bounds__(256) attn_fwd_kernel(
+    const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
+    const float* __restrict__ skip, const float* __restrict__ edge, const int32_t* __restrict__ edge_row,
+    const float* __restrict__ sbf, const float* __restrict__ w, const float* __restrict__ b,
+    const int32_t* __restrict__ rowptr, const int32_t* __restrict__ tsrc, int64_t E, int D, int H, float sqrt_c,
+    float* __restrict__ out, float* __restrict__ alpha_out, float* __restrict__ smax_out,
+    float* __restrict__ sden_out) {
   const int lane = threadIdx.x & 63;
-  const int D = a.D, H = a.H;
   const bool act = lane * CPL < D;
   const int c0 = act ? lane * CPL : 0;
   const int head = lane / LPH;
   const bool leader = act && (lane % LPH) == 0;
   float wr[CPL][kS], br[CPL];
-  load_weights<CPL>(a, c0, act, wr, br);
+  load_weights<CPL>(w, b, c0, act, wr, br);
   const int nwaves = gridDim.x * kAttnWaves;
-  for (int64_t e = wave_id_global(); e < a.E; e += nwaves) {
-    const int t0 = a.rowptr[e], t1 = a.rowptr[e + 1];
+  for (int64_t e = wave_id_global(); e < E; e += nwaves) {
+    const int t0 = uniform(rowptr[e]), t1 = uniform(rowptr[e + 1]);
     float qv[CPL], ed[CPL], acc[CPL];
-    load_row<CPL>(a.q + e * D + c0, act, qv);
-    if (a.edge_mode == X2G_EDGE_PER_DST) {
-      const int64_t r = a.edge_row ? a.edge_row[e] : e;
-      load_row<CPL>(a.edge + r * D + c0, act, ed);
+    load_row<CPL>(q + e * D + c0, act, qv);
+    if (MODE == X2G_EDGE_PER_DST) {
+      const int64_t r = edge_row ? uniform(edge_row[e]) : e;
+      load_row<CPL>(edge + r * D + c0, act, ed);
     } else {
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) ed[j] = 0.f;
+      zero_row<CPL>(ed);
     }
-#pragma unroll
-    for (int j = 0; j < CPL; ++j) acc[j] = 0.f;
+    zero_row<CPL>(acc);
     float m = -INFINITY, den = 0.f;
-    // software pipeline: the next triplet's neighbour rows are in flight while this one computes
-    float kc[CPL], vc[CPL];
+    // two triplets' neighbour rows in flight ahead of the one being consumed
+    float k0[CPL], v0[CPL], k1[CPL], v1[CPL];
+    zero_row<CPL>(k0); zero_row<CPL>(v0); zero_row<CPL>(k1); zero_row<CPL>(v1);
     if (t0 < t1) {
-      const int64_t s = a.tidx[t0];
-      load_row<CPL>(a.k + s * D + c0, act, kc);
-      load_row<CPL>(a.v + s * D + c0, act, vc);
+      const int64_t s = uniform(tsrc[t0]);
+      load_row<CPL>(k + s * D + c0, act, k0);
+      load_row<CPL>(v + s * D + c0, act, v0);
+    }
+    if (t0 + 1 < t1) {
+      const int64_t s = uniform(tsrc[t0 + 1]);
+      load_row<CPL>(k + s * D + c0, act, k1);
+      load_row<CPL>(v + s * D + c0, act, v1);
     }
     for (int t = t0; t < t1; ++t) {
-      float kn[CPL], vn[CPL];
-      if (t + 1 < t1) {
-        const int64_t sn = a.tidx[t + 1];
-        load_row<CPL>(a.k + sn * D + c0, act, kn);
-        load_row<CPL>(a.v + sn * D + c0, act, vn);
+      float k2[CPL], v2[CPL];
+      zero_row<CPL>(k2); zero_row<CPL>(v2);
+      if (t + 2 < t1) {
+        const int64_t s = uniform(tsrc[t + 2]);
+        load_row<CPL>(k + s * D + c0, act, k2);
+        load_row<CPL>(v + s * D + c0, act, v2);
       }
       float et[CPL];
-      if (a.edge_mode == X2G_EDGE_PER_TRIPLET) {
-        load_row<CPL>(a.edge + static_cast<int64_t>(t) * D + c0, act, et);
+      if (MODE == X2G_EDGE_PER_TRIPLET) {
+        load_row<CPL>(edge + static_cast<int64_t>(t) * D + c0, act, et);
       } else {
 #pragma unroll
         for (int j = 0; j < CPL; ++j) et[j] = ed[j];
       }
       float dot = 0.f;
 #pragma unroll
-      for (int j = 0; j < CPL; ++j) dot = fmaf(qv[j], kc[j] + et[j], dot);
-      const float logit = group_sum<LPH>(dot) / a.sqrt_c;
+      for (int j = 0; j < CPL; ++j) dot = fmaf(qv[j], k0[j] + et[j], dot);
+      const float logit = group_sum<LPH>(dot) / sqrt_c;
       float sp[CPL];
-      sbf_project<CPL>(wr, br, a.sbf + static_cast<int64_t>(t) * kS, sp);
+      sbf_project<CPL>(wr, br, sbf + static_cast<int64_t>(t) * kS, sp);
       const float m_new = fmaxf(m, logit);
       const float corr = expf(m - m_new);
       const float p = expf(logit - m_new);
       den = den * corr + p;
 #pragma unroll
-      for (int j = 0; j < CPL; ++j) acc[j] = acc[j] * corr + p * ((vc[j] + et[j]) * sp[j]);
+      for (int j = 0; j < CPL; ++j) acc[j] = acc[j] * corr + p * ((v0[j] + et[j]) * sp[j]);
       m = m_new;
-      if (leader) a.alpha_out[static_cast<int64_t>(t) * H + head] = logit;
+      if (leader) alpha_out[static_cast<int64_t>(t) * H + head] = logit;
 #pragma unroll
       for (int j = 0; j < CPL; ++j) {
-        kc[j] = kn[j];
-        vc[j] = vn[j];
+        k0[j] = k1[j]; v0[j] = v1[j];
+        k1[j] = k2[j]; v1[j] = v2[j];
       }
     }
     float sk[CPL], o[CPL];
-    load_row<CPL>(a.skip + e * D + c0, act, sk);
+    load_row<CPL>(skip + e * D + c0, act, sk);
     const float inv = 1.0f / (den + kSoftmaxEps);
 #pragma unroll
     for (int j = 0; j < CPL; ++j) o[j] = acc[j] * inv + sk[j];
-    store_row<CPL>(a.out + e * D + c0, act, o);
+    store_row<CPL>(out + e * D + c0, act, o);
     if (leader) {
-      a.smax_out[e * H + head] = m;
-      a.sden_out[e * H + head] = den;
+      smax_out[e * H + head] = m;
+      sden_out[e * H + head] = den;
     }
   }
 }
 
 // ------------------------------------------------------------------------------ backward (dst)
-template <int CPL, int LPH>
-__global__ void __launch_bounds__(256) attn_bwd_dst_kernel(AttnArgs a) {
+template <int CPL, int LPH, int MODE>
+__global__ void __launch_bounds__(256) attn_bwd_dst_kernel(
+    const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
+    const float* __restrict__ edge, const int32_t* __restrict__ edge_row, const float* __restrict__ sbf,
+    const float* __restrict__ w, const float* __restrict__ b, const int32_t* __restrict__ rowptr,
+    const int32_t* __restrict__ tsrc, const float* __restrict__ alpha, const float* __restrict__ smax,
+    const float* __restrict__ sden, const float* __restrict__ dout, int64_t E, int D, int H, float sqrt_c,
+    float* __restrict__ dq, float* __restrict__ d_edge, float* __restrict__ dlogit, float* __restrict__ dproj) {
   const int lane = threadIdx.x & 63;
-  const int D = a.D, H = a.H;
   const bool act = lane * CPL < D;
   const int c0 = act ? lane * CPL : 0;
   const int head = lane / LPH;
   const bool leader = act && (lane % LPH) == 0;
-  const bool per_trip = a.edge_mode == X2G_EDGE_PER_TRIPLET;
-  const bool per_dst = a.edge_mode == X2G_EDGE_PER_DST;
+  constexpr bool per_trip = MODE == X2G_EDGE_PER_TRIPLET;
+  constexpr bool per_dst = MODE == X2G_EDGE_PER_DST;
   float wr[CPL][kS], br[CPL];
-  load_weights<CPL>(a, c0, act, wr, br);
+  load_weights<CPL>(w, b, c0, act, wr, br);
   const int nwaves = gridDim.x * kAttnWaves;
-  for (int64_t e = wave_id_global(); e < a.E; e += nwaves) {
-    const int t0 = a.rowptr[e], t1 = a.rowptr[e + 1];
+  for (int64_t e = wave_id_global(); e < E; e += nwaves) {
+    const int t0 = uniform(rowptr[e]), t1 = uniform(rowptr[e + 1]);
     float go[CPL], qv[CPL], ed[CPL], edacc[CPL], dqa[CPL];
-    load_row<CPL>(a.dout + e * D + c0, act, go);
-    load_row<CPL>(a.q + e * D + c0, act, qv);
+    load_row<CPL>(dout + e * D + c0, act, go);
+    load_row<CPL>(q + e * D + c0, act, qv);
     if (per_dst) {
-      const int64_t r = a.edge_row ? a.edge_row[e] : e;
-      load_row<CPL>(a.edge + r * D + c0, act, ed);
+      const int64_t r = edge_row ? uniform(edge_row[e]) : e;
+      load_row<CPL>(edge + r * D + c0, act, ed);
     } else {
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) ed[j] = 0.f;
+      zero_row<CPL>(ed);
     }
-#pragma unroll
-    for (int j = 0; j < CPL; ++j) {
-      edacc[j] = 0.f;
-      dqa[j] = 0.f;
-    }
-    const float mx = act ? a.smax[e * H + head] : 0.f;
-    const float inv = act ? 1.0f / (a.sden[e * H + head] + kSoftmaxEps) : 0.f;
+    zero_row<CPL>(edacc);
+    zero_row<CPL>(dqa);
+    const float mx = keep(smax[e * H + head], act);
+    const float inv = act ? 1.0f / (sden[e * H + head] + kSoftmaxEps) : 0.f;
     // pass 1: g_t = d(loss)/d(a_t) per head, rho = sum_t a_t g_t; d_sbfproj and the value part
     float rho = 0.f;
+    float vn[CPL];
+    zero_row<CPL>(vn);
+    if (t0 < t1) load_row<CPL>(v + static_cast<int64_t>(uniform(tsrc[t0])) * D + c0, act, vn);
     for (int t = t0; t < t1; ++t) {
-      const int64_t s = a.tidx[t];
       float vv[CPL], et[CPL], sp[CPL];
-      load_row<CPL>(a.v + s * D + c0, act, vv);
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) vv[j] = vn[j];
+      if (t + 1 < t1) load_row<CPL>(v + static_cast<int64_t>(uniform(tsrc[t + 1])) * D + c0, act, vn);
       if (per_trip) {
-        load_row<CPL>(a.edge + static_cast<int64_t>(t) * D + c0, act, et);
+        load_row<CPL>(edge + static_cast<int64_t>(t) * D + c0, act, et);
       } else {
 #pragma unroll
         for (int j = 0; j < CPL; ++j) et[j] = ed[j];
       }
-      sbf_project<CPL>(wr, br, a.sbf + static_cast<int64_t>(t) * kS, sp);
-      const float at = act ? expf(a.alpha[static_cast<int64_t>(t) * H + head] - mx) * inv : 0.f;
+      sbf_project<CPL>(wr, br, sbf + static_cast<int64_t>(t) * kS, sp);
+      const float at = act ? expf(alpha[static_cast<int64_t>(t) * H + head] - mx) * inv : 0.f;
       float gpart = 0.f, dp[CPL], du[CPL];
 #pragma unroll
       for (int j = 0; j < CPL; ++j) {
@@ -274,31 +298,35 @@ __global__ void __launch_bounds__(256) attn_bwd_dst_kernel(AttnArgs a) {
       }
       const float g = group_sum<LPH>(gpart);
       rho = fmaf(at, g, rho);
-      store_row<CPL>(a.dproj + static_cast<int64_t>(t) * D + c0, act, dp);
+      store_row<CPL>(dproj + static_cast<int64_t>(t) * D + c0, act, dp);
       if (per_trip) {
-        store_row<CPL>(a.d_edge + static_cast<int64_t>(t) * D + c0, act, du);
+        store_row<CPL>(d_edge + static_cast<int64_t>(t) * D + c0, act, du);
       } else {
 #pragma unroll
         for (int j = 0; j < CPL; ++j) edacc[j] += du[j];
       }
-      if (leader) a.dlogit[static_cast<int64_t>(t) * H + head] = g;
+      if (leader) dlogit[static_cast<int64_t>(t) * H + head] = g;
     }
     // pass 2: dlogit = a (g - rho); dq, and the key part of the edge gradient
+    float kn[CPL];
+    zero_row<CPL>(kn);
+    if (t0 < t1) load_row<CPL>(k + static_cast<int64_t>(uniform(tsrc[t0])) * D + c0, act, kn);
     for (int t = t0; t < t1; ++t) {
-      const int64_t s = a.tidx[t];
       float kk[CPL], et[CPL];
-      load_row<CPL>(a.k + s * D + c0, act, kk);
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) kk[j] = kn[j];
+      if (t + 1 < t1) load_row<CPL>(k + static_cast<int64_t>(uniform(tsrc[t + 1])) * D + c0, act, kn);
       if (per_trip) {
-        load_row<CPL>(a.edge + static_cast<int64_t>(t) * D + c0, act, et);
+        load_row<CPL>(edge + static_cast<int64_t>(t) * D + c0, act, et);
       } else {
 #pragma unroll
         for (int j = 0; j < CPL; ++j) et[j] = ed[j];
       }
-      const float at = act ? expf(a.alpha[static_cast<int64_t>(t) * H + head] - mx) * inv : 0.f;
+      const float at = act ? expf(alpha[static_cast<int64_t>(t) * H + head] - mx) * inv : 0.f;
       // only the leader lane wrote g for this head: read it back in that lane, then broadcast
-      const float g = group_sum<LPH>(leader ? a.dlogit[static_cast<int64_t>(t) * H + head] : 0.f);
+      const float g = group_sum<LPH>(leader ? dlogit[static_cast<int64_t>(t) * H + head] : 0.f);
       const float dl = at * (g - rho);
-      const float ds = dl / a.sqrt_c;
+      const float ds = dl / sqrt_c;
       float dk[CPL];
 #pragma unroll
       for (int j = 0; j < CPL; ++j) {
@@ -307,75 +335,120 @@ __global__ void __launch_bounds__(256) attn_bwd_dst_kernel(AttnArgs a) {
       }
       if (per_trip) {
         float cur[CPL];
-        load_row<CPL>(a.d_edge + static_cast<int64_t>(t) * D + c0, act, cur);
+        load_row<CPL>(d_edge + static_cast<int64_t>(t) * D + c0, act, cur);
 #pragma unroll
         for (int j = 0; j < CPL; ++j) cur[j] += dk[j];
-        store_row<CPL>(a.d_edge + static_cast<int64_t>(t) * D + c0, act, cur);
+        store_row<CPL>(d_edge + static_cast<int64_t>(t) * D + c0, act, cur);
       } else {
 #pragma unroll
         for (int j = 0; j < CPL; ++j) edacc[j] += dk[j];
       }
-      if (leader) a.dlogit[static_cast<int64_t>(t) * H + head] = dl;
+      if (leader) dlogit[static_cast<int64_t>(t) * H + head] = dl;
     }
-    store_row<CPL>(a.dq + e * D + c0, act, dqa);
-    if (per_dst) store_row<CPL>(a.d_edge + e * D + c0, act, edacc);
+    store_row<CPL>(dq + e * D + c0, act, dqa);
+    if (per_dst) store_row<CPL>(d_edge + e * D + c0, act, edacc);
   }
 }
 
 // ------------------------------------------------------------------------------ backward (src)
 template <int CPL, int LPH>
-__global__ void __launch_bounds__(256) attn_bwd_src_kernel(AttnArgs a) {
+__global__ void __launch_bounds__(256) attn_bwd_src_kernel(
+    const float* __restrict__ q, const float* __restrict__ sbf, const float* __restrict__ w,
+    const float* __restrict__ b, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ perm,
+    const int32_t* __restrict__ tdst, const float* __restrict__ alpha, const float* __restrict__ smax,
+    const float* __restrict__ sden, const float* __restrict__ dlogit_in, const float* __restrict__ dout,
+    int64_t E, int D, int H, float sqrt_c, float* __restrict__ dk, float* __restrict__ dv) {
   const int lane = threadIdx.x & 63;
-  const int D = a.D, H = a.H;
   const bool act = lane * CPL < D;
   const int c0 = act ? lane * CPL : 0;
   const int head = lane / LPH;
   float wr[CPL][kS], br[CPL];
-  load_weights<CPL>(a, c0, act, wr, br);
+  load_weights<CPL>(w, b, c0, act, wr, br);
   const int nwaves = gridDim.x * kAttnWaves;
-  for (int64_t s = wave_id_global(); s < a.E; s += nwaves) {
-    const int p0 = a.rowptr[s], p1 = a.rowptr[s + 1];
+  for (int64_t s = wave_id_global(); s < E; s += nwaves) {
+    const int p0 = uniform(rowptr[s]), p1 = uniform(rowptr[s + 1]);
     float dka[CPL], dva[CPL];
-#pragma unroll
-    for (int j = 0; j < CPL; ++j) {
-      dka[j] = 0.f;
-      dva[j] = 0.f;
+    zero_row<CPL>(dka);
+    zero_row<CPL>(dva);
+    // next triplet's gathered rows (dout, q of its destination) in flight
+    float gn[CPL], qn[CPL];
+    zero_row<CPL>(gn);
+    zero_row<CPL>(qn);
+    int64_t tn = 0, en = 0;
+    if (p0 < p1) {
+      tn = uniform(perm[p0]);
+      en = uniform(tdst[tn]);
+      load_row<CPL>(dout + en * D + c0, act, gn);
+      load_row<CPL>(q + en * D + c0, act, qn);
     }
     for (int p = p0; p < p1; ++p) {
-      const int64_t t = a.tidx[p];
-      const int64_t e = a.tdst[t];
+      const int64_t t = tn, e = en;
       float go[CPL], qv[CPL], sp[CPL];
-      load_row<CPL>(a.dout + e * D + c0, act, go);
-      load_row<CPL>(a.q + e * D + c0, act, qv);
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) {
+        go[j] = gn[j];
+        qv[j] = qn[j];
+      }
+      if (p + 1 < p1) {
+        tn = uniform(perm[p + 1]);
+        en = uniform(tdst[tn]);
+        load_row<CPL>(dout + en * D + c0, act, gn);
+        load_row<CPL>(q + en * D + c0, act, qn);
+      }
       float at = 0.f, dl = 0.f;
       if (act) {
-        const float mx = a.smax[e * H + head];
-        const float inv = 1.0f / (a.sden[e * H + head] + kSoftmaxEps);
-        at = expf(a.alpha[t * H + head] - mx) * inv;
-        dl = a.dlogit_in[t * H + head];
+        const float mx = smax[e * H + head];
+        const float inv = 1.0f / (sden[e * H + head] + kSoftmaxEps);
+        at = expf(alpha[t * H + head] - mx) * inv;
+        dl = dlogit_in[t * H + head];
       }
-      sbf_project<CPL>(wr, br, a.sbf + t * kS, sp);
-      const float ds = dl / a.sqrt_c;
+      sbf_project<CPL>(wr, br, sbf + t * kS, sp);
+      const float ds = dl / sqrt_c;
 #pragma unroll
       for (int j = 0; j < CPL; ++j) {
         dva[j] = fmaf(go[j] * sp[j], at, dva[j]);
         dka[j] = fmaf(ds, qv[j], dka[j]);
       }
     }
-    store_row<CPL>(a.dk + s * D + c0, act, dka);
-    store_row<CPL>(a.dv + s * D + c0, act, dva);
+    store_row<CPL>(dk + s * D + c0, act, dka);
+    store_row<CPL>(dv + s * D + c0, act, dva);
   }
 }
 
 // ------------------------------------------------------------------------------ dispatch
 enum class Pass { kFwd, kBwdDst, kBwdSrc };
 
+template <int CPL, int LPH, int MODE>
+void launch_mode(Pass pass, const AttnArgs& a, unsigned blocks, hipStream_t st) {
+  switch (pass) {
+    case Pass::kFwd:
+      attn_fwd_kernel<CPL, LPH, MODE><<<blocks, 256, 0, st>>>(a.q, a.k, a.v, a.skip, a.edge, a.edge_row, a.sbf, a.w,
+                                                              a.b, a.rowptr, a.tidx, a.E, a.D, a.H, a.sqrt_c, a.out,
+                                                              a.alpha_out, a.smax_out, a.sden_out);
+      break;
+    case Pass::kBwdDst:
+      attn_bwd_dst_kernel<CPL, LPH, MODE><<<blocks, 256, 0, st>>>(
+          a.q, a.k, a.v, a.edge, a.edge_row, a.sbf, a.w, a.b, a.rowptr, a.tidx, a.alpha, a.smax, a.sden, a.dout,
+          a.E, a.D, a.H, a.sqrt_c, a.dq, a.d_edge, a.dlogit, a.dproj);
+      break;
+    case Pass::kBwdSrc:
+      attn_bwd_src_kernel<CPL, LPH><<<blocks, 256, 0, st>>>(a.q, a.sbf, a.w, a.b, a.rowptr, a.tidx, a.tdst, a.alpha,
+                                                            a.smax, a.sden, a.dlogit_in, a.dout, a.E, a.D, a.H,
+                                                            a.sqrt_c, a.dk, a.dv);
+      break;
+  }
+}
+
 template <int CPL, int LPH>
 void launch_one(Pass pass, const AttnArgs& a, unsigned blocks, hipStream_t st) {
-  switch (pass) {
-    case Pass::kFwd: attn_fwd_kernel<CPL, LPH><<<blocks, 256, 0, st>>>(a); break;
-    case Pass::kBwdDst: attn_bwd_dst_kernel<CPL, LPH><<<blocks, 256, 0, st>>>(a); break;
-    case Pass::kBwdSrc: attn_bwd_src_kernel<CPL, LPH><<<blocks, 256, 0, st>>>(a); break;
+  if (pass == Pass::kBwdSrc) {
+    launch_mode<CPL, LPH, X2G_EDGE_NONE>(pass, a, blocks, st);
+    return;
+  }
+  switch (a.edge_mode) {
+    case X2G_EDGE_PER_TRIPLET: launch_mode<CPL, LPH, X2G_EDGE_PER_TRIPLET>(pass, a, blocks, st); break;
+    case X2G_EDGE_PER_DST: launch_mode<CPL, LPH, X2G_EDGE_PER_DST>(pass, a, blocks, st); break;
+    default: launch_mode<CPL, LPH, X2G_EDGE_NONE>(pass, a, blocks, st); break;
   }
 }
 
@@ -395,6 +468,8 @@ int launch_cpl(Pass pass, const AttnArgs& a, int lph, unsigned blocks, hipStream
 int dispatch(Pass pass, AttnArgs a, int heads, int channels, int sbf_dim, hipStream_t st) {
   if (a.E < 0 || heads <= 0 || channels <= 0) return X2G_EINVAL;
   if (sbf_dim != kS) return X2G_EUNSUPPORTED;
+  if (a.edge_mode != X2G_EDGE_NONE && a.edge_mode != X2G_EDGE_PER_TRIPLET && a.edge_mode != X2G_EDGE_PER_DST)
+    return X2G_EINVAL;
   const int D = heads * channels;
   int cpl;
   if (D == 32 || D == 64) cpl = 1;
