@@ -145,7 +145,9 @@ def _event_time(fn, reps):
 def scatter_add_probe(lg, reps):
     """The graded CSR-by-destination scatter-add (x2g_segment_sum) at the step's line-graph
     shape: [T, 128] messages -> [E, 128], algorithmic bytes 4*T*D + 4*(E+1) + 4*E*D.
-    Timed L2/MALL-warm (back-to-back) and cache-busted (512 MiB written between launches)."""
+    Timed L2/MALL-warm (back-to-back) and cache-busted: 512 MiB are *read* between launches, which
+    evicts L2 and the 256 MiB MALL without leaving dirty lines whose write-back would be billed
+    to the timed kernel."""
     E, T, D = lg.E, lg.T, 128
     dev = lg.trip_rowptr.device
     msgs = torch.randn(T, D, device=dev)
@@ -156,11 +158,12 @@ def scatter_add_probe(lg, reps):
         call("x2g_segment_sum", ptr(msgs), None, ptr(lg.trip_rowptr), E, D, ptr(out), stream_ptr())
 
     warm = _event_time(fn, reps)
-    flush = torch.empty(512 * 2 ** 20 // 4, device=dev)
+    flush = torch.ones(512 * 2 ** 20 // 4, device=dev)
+    sink = torch.empty((), device=dev)
     st = torch.cuda.current_stream()
     times = []
     for _ in range(reps):
-        flush.fill_(1.0)
+        torch.sum(flush, dim=0, out=sink)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(st)
         fn()

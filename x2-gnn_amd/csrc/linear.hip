@@ -137,11 +137,10 @@ __global__ void __launch_bounds__(256) wgrad_partial(const float* __restrict__ d
 
 // out[e] = sum_s part[s][e] in a fixed order: each of the 4 waves of a block sums a quarter of
 // the slabs for the block's 64 elements, then the quarters are added in wave order.
-__global__ void __launch_bounds__(256) sum_slabs(const float* __restrict__ part, int64_t n, int splits,
-                                                 float* __restrict__ out) {
-  __shared__ float red[4][64];
+__device__ __forceinline__ void sum_slabs_block(const float* __restrict__ part, int64_t n, int splits, int64_t blk,
+                                                float* __restrict__ out, float (*red)[64]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t e = static_cast<int64_t>(blockIdx.x) * 64 + lane;
+  const int64_t e = blk * 64 + lane;
   const int per = (splits + 3) / 4;
   const int k0 = wave * per, k1 = k0 + per < splits ? k0 + per : splits;
   float s = 0.f;
@@ -152,6 +151,34 @@ __global__ void __launch_bounds__(256) sum_slabs(const float* __restrict__ part,
   red[wave][lane] = s;
   __syncthreads();
   if (wave == 0 && e < n) out[e] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+__global__ void __launch_bounds__(256) sum_slabs(const float* __restrict__ part, int64_t n, int splits,
+                                                 float* __restrict__ out) {
+  __shared__ float red[4][64];
+  sum_slabs_block(part, n, splits, blockIdx.x, out, red);
+}
+
+// Two slab sets (weight and bias partials) in one launch: blocks [0, nblk_a) take the first.
+__global__ void __launch_bounds__(256) sum_slabs2(const float* __restrict__ part_a, int64_t na,
+                                                  const float* __restrict__ part_b, int64_t nb, int splits,
+                                                  float* __restrict__ out_a, float* __restrict__ out_b) {
+  __shared__ float red[4][64];
+  const int64_t nblk_a = (na + 63) / 64;
+  if (static_cast<int64_t>(blockIdx.x) < nblk_a)
+    sum_slabs_block(part_a, na, splits, blockIdx.x, out_a, red);
+  else
+    sum_slabs_block(part_b, nb, splits, blockIdx.x - nblk_a, out_b, red);
+}
+
+// dw (and db when part_b != NULL) from their slabs, one launch
+int sum_slabs_launch(const float* part_w, int64_t nw, const float* part_b, int64_t nb, int splits, float* dw,
+                     float* db, hipStream_t st) {
+  if (part_b && db)
+    sum_slabs2<<<blocks_for(nw, 64) + blocks_for(nb, 64), 256, 0, st>>>(part_w, nw, part_b, nb, splits, dw, db);
+  else
+    sum_slabs<<<blocks_for(nw, 64), 256, 0, st>>>(part_w, nw, splits, dw);
+  return last_launch_status();
 }
 
 // rows per split: a multiple of the 32-row chunk, at least 64, at most kWgMaxSplits splits
@@ -204,8 +231,5 @@ X2G_API int x2g_linear_wgrad(const float* dy, const float* x, int64_t R, int32_t
     wgrad_partial<false><<<grid, 256, 0, st>>>(dy, x, R, O, I, tiles_i, wgrad_rows_per_split(R), part, part_b);
   int rc = last_launch_status();
   if (rc) return rc;
-  const int64_t n = static_cast<int64_t>(O) * I;
-  sum_slabs<<<blocks_for(n, 64), 256, 0, st>>>(part, n, splits, dw);
-  if (db) sum_slabs<<<blocks_for(O, 64), 256, 0, st>>>(part_b, O, splits, db);
-  return last_launch_status();
+  return sum_slabs_launch(part, static_cast<int64_t>(O) * I, part_b, O, splits, dw, db, st);
 }

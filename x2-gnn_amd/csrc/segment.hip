@@ -13,7 +13,7 @@
 namespace x2g {
 
 constexpr int kSegWaves = 4;
-constexpr unsigned kSegMaxBlocks = 4096;
+constexpr unsigned kSegMaxBlocks = 16384;
 
 __device__ __forceinline__ float4 f4_fma(float4 a, float4 b, float4 c) {
   return make_float4(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y), fmaf(a.z, b.z, c.z), fmaf(a.w, b.w, c.w));
@@ -31,35 +31,42 @@ __device__ __forceinline__ float4 f4_shfl_xor(float4 v, int off) {
 
 // ------------------------------------------------------------------------------ segment sum
 // One wave per segment (grid-stride).  LPR = D/4 lanes cover a row with 16-byte loads, so a
-// wave-instruction reads RPI = 64/LPR whole rows (D=128: two 512 B rows = 1 KiB); each lane
-// keeps UNROLL loads in flight, then the RPI partial rows are folded with xor shuffles.
+// wave-instruction reads RPI = 64/LPR whole rows (D=128: two 512 B rows = 1 KiB).  Each lane
+// issues UNROLL loads per batch unconditionally — rows past the segment end read a clamped row
+// of the same segment and are zeroed by keep() — so a typical segment (T/E ~ 9 rows at S160)
+// is one batch of 8 loads in flight per lane, one memory round trip.  The RPI partial rows are
+// then folded with xor shuffles.  (A non-finite row stays non-finite in the sum, but a masked
+// duplicate of an inf row contributes NaN instead of 0: both give a non-finite segment.)
 template <int LPR, bool MUL>
 __global__ void __launch_bounds__(256) seg_sum_vec(const float4* __restrict__ x, const float4* __restrict__ mul,
                                                    const int32_t* __restrict__ rowptr, int64_t G,
                                                    float4* __restrict__ out) {
   constexpr int RPI = 64 / LPR;
-  constexpr int UNROLL = 4;
+  constexpr int UNROLL = 8;
   const int lane = threadIdx.x & 63;
   const int sub = lane % LPR, slot = lane / LPR;
   const int nwaves = gridDim.x * kSegWaves;
   for (int64_t g = uniform(blockIdx.x * kSegWaves + (threadIdx.x >> 6)); g < G; g += nwaves) {
-    const int r0 = rowptr[g], r1 = rowptr[g + 1];
+    const int r0 = uniform(rowptr[g]), r1 = uniform(rowptr[g + 1]);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    int r = r0 + slot;
-    for (; r + (UNROLL - 1) * RPI < r1; r += UNROLL * RPI) {
+    for (int rb = r0; rb < r1; rb += UNROLL * RPI) {
       float4 v[UNROLL], w[UNROLL];
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
-        const int64_t idx = static_cast<int64_t>(r + u * RPI) * LPR + sub;
+        const int r = rb + u * RPI + slot;
+        const int64_t idx = static_cast<int64_t>(r < r1 ? r : r1 - 1) * LPR + sub;
         v[u] = x[idx];
         if (MUL) w[u] = mul[idx];
       }
 #pragma unroll
-      for (int u = 0; u < UNROLL; ++u) acc = MUL ? f4_fma(v[u], w[u], acc) : f4_add(acc, v[u]);
-    }
-    for (; r < r1; r += RPI) {
-      const int64_t idx = static_cast<int64_t>(r) * LPR + sub;
-      acc = MUL ? f4_fma(x[idx], mul[idx], acc) : f4_add(acc, x[idx]);
+      for (int u = 0; u < UNROLL; ++u) {
+        const bool ok = rb + u * RPI + slot < r1;
+        const float4 t = MUL ? f4_mul(v[u], w[u]) : v[u];
+        acc.x += keep(t.x, ok);
+        acc.y += keep(t.y, ok);
+        acc.z += keep(t.z, ok);
+        acc.w += keep(t.w, ok);
+      }
     }
 #pragma unroll
     for (int off = LPR; off < 64; off <<= 1) acc = f4_add(acc, f4_shfl_xor(acc, off));
