@@ -36,6 +36,8 @@ from x2gnn.synth import synthetic_molecules  # noqa: E402
 
 CFG = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embedding_size=128)  # config.json
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+MFMA_F32_PEAK_TFS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32) peak, MI355X_MICROARCH.md
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")  # scripts/pmc_traffic.py output
 METRIC = "molecules/sec (fwd+bwd) on QM9 U0, batch=128, 1/2/4/8 MI355X"
 
 
@@ -128,6 +130,53 @@ def attention_probe(model, batch, reps):
                              ("attn_bwd_src", bwd_src, src_bytes)):
         res[name] = (_event_time(fn, reps), nbytes)
     return res, dict(E=E, T=T, D=D)
+
+
+def dense_probe(R, reps):
+    """The trunk's dense layer at this step's row count: [R,128] x [128,128] + bias, SiLU and
+    residual fused (x2g_dense_fwd), and its fused backward (x2g_dense_bwd: dz, dx, dW, db =
+    dense_bwd_persist + the fixed-order slab sum), HIP-event timed on the launch stream."""
+    K = N = 128
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(R, K, device=dev, generator=g)
+    w = 0.1 * torch.randn(N, K, device=dev, generator=g)
+    b = torch.randn(N, device=dev, generator=g)
+    dy = torch.randn(R, N, device=dev, generator=g)
+    y, z, dx = (torch.empty(R, N, device=dev) for _ in range(3))
+    dw, db = torch.empty(N, K, device=dev), torch.empty(N, device=dev)
+    wsb = _lib_ws("x2g_dense_bwd_workspace", R, K, N)
+    ws = torch.empty(max(wsb, 4) // 4 + 1, device=dev)
+
+    def fwd():
+        call("x2g_dense_fwd", ptr(x), ptr(w), ptr(b), R, K, N, ops.ACT_SILU, ptr(x), ptr(y), ptr(z), stream_ptr())
+
+    def bwd():
+        call("x2g_dense_bwd", ptr(dy), ptr(z), ops.ACT_SILU, ptr(x), ptr(w), R, K, N, ptr(dx), ptr(dw), ptr(db),
+             ptr(ws), wsb, stream_ptr())
+
+    fwd()
+    return {"dense_fwd": (_event_time(fwd, reps), 2.0 * R * K * N), "dense_bwd": (_event_time(bwd, reps), 4.0 * R * K * N)}
+
+
+def _lib_ws(name, *args):
+    from x2gnn import _lib
+
+    return int(getattr(_lib.load(), name)(*args))
+
+
+def pmc_traffic(keys):
+    """HBM bytes per launch of the named kernels (sum), from the committed PMC summary."""
+    if not os.path.exists(TRAFFIC_JSON):
+        return None
+    table = json.load(open(TRAFFIC_JSON))["kernels"]
+    total = 0
+    for name, grid in keys:
+        hit = [v for k, v in table.items() if k.startswith(name) and k.endswith("|" + grid)]
+        if not hit or hit[0]["fetch_bytes"] is None or hit[0]["write_bytes"] is None:
+            return None
+        total += hit[0]["fetch_bytes"] + hit[0]["write_bytes"]
+    return total
 
 
 def _event_time(fn, reps):
@@ -244,8 +293,13 @@ def main():
     probe, shape = attention_probe(model, batch, args.kernel_reps)
     plan_lg = model.line_graph_data(batch)[1].lg
     sa = scatter_add_probe(plan_lg, args.kernel_reps)
-    dom_name, (dom_ms, dom_bytes) = max(probe.items(), key=lambda kv: kv[1][0])
-    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    dense = dense_probe(shape["E"], args.kernel_reps)
+    # the roofline kernel: the fused dense backward, the largest share of the step in the
+    # committed profile (profiles/r1_v2_bench_kernel_stats.csv: dense_bwd_persist 1.9 ms/step)
+    dbw_ms, dbw_flops = dense["dense_bwd"]
+    dbw_tfs = dbw_flops / (dbw_ms * 1e-3) / 1e12
+    grid = str(256 * 512 if (shape["E"] + 63) // 64 >= 256 else ((shape["E"] + 63) // 64) * 512)
+    traffic = pmc_traffic([("void x2g::dense_bwd_persist<64>", grid), ("x2g::sum_slabs2", str(258 * 256))])
 
     if rank == 0:
         line = {
@@ -268,10 +322,16 @@ def main():
                        "per_gpu_batch": args.batch, "global_batch": world * args.batch,
                        "line_nodes_per_gpu": shape["E"], "triplets_per_gpu": shape["T"],
                        "parallelism": f"dp{world}"},
-            "roofline": {"kernel": dom_name, "bound": "hbm", "achieved": round(achieved, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "avg_ms": round(dom_ms, 5), "bytes_per_launch": int(dom_bytes)},
-            "kernels_ms": {k: round(v[0], 5) for k, v in probe.items()},
+            "roofline": {"kernel": "x2g_dense_bwd [E,128]x[128,128] SiLU (dense_bwd_persist<64> + sum_slabs2)",
+                         "bound": "mfma", "achieved": round(dbw_tfs, 2), "peak": MFMA_F32_PEAK_TFS,
+                         "unit": "TFLOP/s", "frac": round(dbw_tfs / MFMA_F32_PEAK_TFS, 4), "traffic": traffic,
+                         "avg_ms": round(dbw_ms, 5), "flops_per_launch": int(dbw_flops),
+                         "traffic_source": os.path.relpath(TRAFFIC_JSON, ROOT) if traffic else None},
+            "kernels": dict(
+                {k: {"ms": round(v[0], 5), "bytes": int(v[1]), "GBs": round(v[1] / (v[0] * 1e-3) / 1e9, 1)}
+                 for k, v in probe.items()},
+                **{k: {"ms": round(v[0], 5), "flops": int(v[1]), "TFs": round(v[1] / (v[0] * 1e-3) / 1e12, 2)}
+                   for k, v in dense.items()}),
             "roofline_scatter_add": {
                 "kernel": "x2g_segment_sum [T,128]->[E,128]", "bytes_per_launch": sa["bytes"],
                 "warm_GBs": round(sa["bytes"] / (sa["warm_ms"] * 1e-3) / 1e9, 1),

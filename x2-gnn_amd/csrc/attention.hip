@@ -133,8 +133,22 @@ __device__ __forceinline__ void load_weights(const float* __restrict__ w, const 
   }
 }
 
-__device__ __forceinline__ int wave_id_global() {
-  return uniform(static_cast<int>(blockIdx.x) * kAttnWaves + static_cast<int>(threadIdx.x >> 6));
+// XCD-aware work split.  Workgroups are dispatched round-robin over the 8 XCDs (block b runs on
+// XCD b % 8) and each XCD has its own 4 MiB L2.  Triplets never leave a molecule and molecules
+// are contiguous ranges of line nodes, so giving XCD x the contiguous range [E x/8, E (x+1)/8)
+// keeps the k/v/q rows its triplets gather (1 KiB per line node) inside ITS L2 instead of every
+// XCD streaming every molecule through its cache.  Within an XCD the waves grid-stride.
+// The grid is a multiple of 8 (dispatch rounds it up).
+struct WaveRange {
+  int64_t first, end, stride;
+};
+
+__device__ __forceinline__ WaveRange xcd_wave_range(int64_t n) {
+  const int b = blockIdx.x, nb = gridDim.x;
+  const int xcd = b & 7, per_xcd = nb >> 3;
+  const int w = uniform((b >> 3) * kAttnWaves + static_cast<int>(threadIdx.x >> 6));
+  const int64_t lo = n * xcd / 8, hi = n * (xcd + 1) / 8;
+  return {lo + w, hi, static_cast<int64_t>(per_xcd) * kAttnWaves};
 }
 
 template <int CPL>
@@ -162,8 +176,8 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(
   const bool leader = act && (lane % LPH) == 0;
   float wr[CPL][kS], br[CPL];
   load_weights<CPL>(w, b, c0, act, wr, br);
-  const int nwaves = gridDim.x * kAttnWaves;
-  for (int64_t e = wave_id_global(); e < E; e += nwaves) {
+  const WaveRange wr_ = xcd_wave_range(E);
+  for (int64_t e = wr_.first; e < wr_.end; e += wr_.stride) {
     const int t0 = uniform(rowptr[e]), t1 = uniform(rowptr[e + 1]);
     float qv[CPL], ed[CPL], acc[CPL];
     load_row<CPL>(q + e * D + c0, act, qv);
@@ -254,8 +268,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dst_kernel(
   constexpr bool per_dst = MODE == X2G_EDGE_PER_DST;
   float wr[CPL][kS], br[CPL];
   load_weights<CPL>(w, b, c0, act, wr, br);
-  const int nwaves = gridDim.x * kAttnWaves;
-  for (int64_t e = wave_id_global(); e < E; e += nwaves) {
+  const WaveRange wr_ = xcd_wave_range(E);
+  for (int64_t e = wr_.first; e < wr_.end; e += wr_.stride) {
     const int t0 = uniform(rowptr[e]), t1 = uniform(rowptr[e + 1]);
     float go[CPL], qv[CPL], ed[CPL], edacc[CPL], dqa[CPL];
     load_row<CPL>(dout + e * D + c0, act, go);
@@ -364,8 +378,8 @@ __global__ void __launch_bounds__(256) attn_bwd_src_kernel(
   const int head = lane / LPH;
   float wr[CPL][kS], br[CPL];
   load_weights<CPL>(w, b, c0, act, wr, br);
-  const int nwaves = gridDim.x * kAttnWaves;
-  for (int64_t s = wave_id_global(); s < E; s += nwaves) {
+  const WaveRange wr_ = xcd_wave_range(E);
+  for (int64_t s = wr_.first; s < wr_.end; s += wr_.stride) {
     const int p0 = uniform(rowptr[s]), p1 = uniform(rowptr[s + 1]);
     float dka[CPL], dva[CPL];
     zero_row<CPL>(dka);
@@ -484,7 +498,8 @@ int dispatch(Pass pass, AttnArgs a, int heads, int channels, int sbf_dim, hipStr
   a.sqrt_c = static_cast<float>(sqrt(static_cast<double>(channels)));
   if (a.E == 0) return X2G_OK;
   int64_t want = (a.E + kAttnWaves - 1) / kAttnWaves;
-  const unsigned blocks = static_cast<unsigned>(want < kMaxBlocks ? want : kMaxBlocks);
+  want = want < kMaxBlocks ? want : kMaxBlocks;
+  const unsigned blocks = static_cast<unsigned>((want + 7) / 8 * 8);  // a multiple of the 8 XCDs
   int rc;
   switch (cpl) {
     case 1: rc = launch_cpl<1>(pass, a, lph, blocks, st); break;
