@@ -164,6 +164,15 @@ int x2g_linear_wgrad(const float* dy, const float* x, int64_t rows, int32_t out_
                      int32_t in_features, float* dw, float* db, void* workspace, size_t workspace_bytes,
                      void* stream);
 
+/* flags of the *_ex gradient entry points */
+#define X2G_ACCUM_WGRAD 1 /* dw += ..., db += ... (write straight into a gradient buffer that already
+                             holds a value, e.g. a zeroed flat all-reduce bucket) instead of dw = ... */
+
+/* x2g_linear_wgrad with flags (X2G_ACCUM_WGRAD). */
+int x2g_linear_wgrad_ex(const float* dy, const float* x, int64_t rows, int32_t out_features,
+                        int32_t in_features, float* dw, float* db, int flags, void* workspace,
+                        size_t workspace_bytes, void* stream);
+
 #define X2G_ACT_NONE 0
 #define X2G_ACT_SILU 1
 
@@ -189,6 +198,14 @@ size_t x2g_dense_bwd_workspace(int64_t rows, int32_t in_features, int32_t out_fe
 int x2g_dense_bwd(const float* dy, const float* z, int act, const float* x, const float* w, int64_t rows,
                   int32_t in_features, int32_t out_features, float* dx, float* dw, float* db, void* workspace,
                   size_t workspace_bytes, void* stream);
+
+/* x2g_dense_bwd plus: dx = dz w + dx_add (dx_add [R,K] optional, may alias dx: the gradient
+ * contributions autograd would otherwise sum in a separate kernel — a residual branch, a tensor
+ * feeding several layers) and flags (X2G_ACCUM_WGRAD: accumulate dw / db into their buffers).
+ * dx_add is supported for in/out features <= 128 (X2G_EUNSUPPORTED otherwise). */
+int x2g_dense_bwd_ex(const float* dy, const float* z, int act, const float* x, const float* w, int64_t rows,
+                     int32_t in_features, int32_t out_features, float* dx, const float* dx_add, float* dw,
+                     float* db, int flags, void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

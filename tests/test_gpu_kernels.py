@@ -383,3 +383,39 @@ def test_dense_fused_vs_torch(cuda, R, K, N, act, with_res):
     np.testing.assert_allclose(bg.grad.cpu().numpy(), bs.grad.numpy(), **tol)
     if with_res:
         np.testing.assert_allclose(rg.grad.cpu().numpy(), rs.grad.numpy(), rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,K,N,act", [(21058, 128, 128, 1), (300, 128, 128, 0), (2304, 128, 4, 1),
+                                       (1000, 6, 128, 1)])
+def test_dense_bwd_ex_dx_add_and_accumulate(cuda, R, K, N, act):
+    """x2g_dense_bwd_ex: dx = dz w + dx_add (dx_add aliasing dx too) and X2G_ACCUM_WGRAD
+    (dw += ..., db += ...) give exactly the plain backward's values plus the addend."""
+    from x2gnn import _lib
+    from x2gnn._lib import call, ptr, stream_ptr
+
+    g = torch.Generator(device=cuda).manual_seed(R + K + N)
+    x = torch.randn(R, K, device=cuda, generator=g)
+    w = torch.randn(N, K, device=cuda, generator=g) / np.sqrt(K)
+    z = torch.randn(R, N, device=cuda, generator=g)
+    dy = torch.randn(R, N, device=cuda, generator=g)
+    add = torch.randn(R, K, device=cuda, generator=g)
+    wsb = int(_lib.load().x2g_dense_bwd_workspace(R, K, N))
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=cuda)
+    dx0, dw0, db0 = torch.empty(R, K, device=cuda), torch.empty(N, K, device=cuda), torch.empty(N, device=cuda)
+    call("x2g_dense_bwd", ptr(dy), ptr(z), act, ptr(x), ptr(w), R, K, N, ptr(dx0), ptr(dw0), ptr(db0), ptr(ws), wsb,
+         stream_ptr())
+    # separate addend, accumulate into pre-filled weight-gradient buffers
+    dx1 = torch.empty(R, K, device=cuda)
+    dw1, db1 = torch.full((N, K), 0.5, device=cuda), torch.full((N,), -0.25, device=cuda)
+    call("x2g_dense_bwd_ex", ptr(dy), ptr(z), act, ptr(x), ptr(w), R, K, N, ptr(dx1), ptr(add), ptr(dw1), ptr(db1), 1,
+         ptr(ws), wsb, stream_ptr())
+    # in-place: dx_add aliases dx
+    dx2 = add.clone()
+    dw2, db2 = torch.empty(N, K, device=cuda), torch.empty(N, device=cuda)
+    call("x2g_dense_bwd_ex", ptr(dy), ptr(z), act, ptr(x), ptr(w), R, K, N, ptr(dx2), ptr(dx2), ptr(dw2), ptr(db2), 0,
+         ptr(ws), wsb, stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dx1, dx0 + add) and torch.equal(dx2, dx0 + add)
+    assert torch.equal(dw1, dw0 + 0.5) and torch.equal(db1, db0 - 0.25)
+    assert torch.equal(dw2, dw0) and torch.equal(db2, db0)

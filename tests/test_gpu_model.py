@@ -67,6 +67,27 @@ def test_model_is_deterministic(cuda):
         assert torch.equal(a, c)
 
 
+def test_bucket_gradients_equal_autograd(cuda):
+    """With a GradBucket the fused backwards sum weight gradients straight into the flat buffer
+    (X2G_ACCUM_WGRAD, ops.grad_sink); the result must equal plain autograd's bit for bit."""
+    from x2gnn.dist import GradBucket
+
+    z = golden("model_full.npz")
+    b = batch_from_fixture(z).to(cuda)
+    m = product_model(z, cuda)
+    for _ in range(2):  # two forwards on both sides: each applies the embedding's max_norm renorm
+        m.zero_grad(set_to_none=True)
+        torch.nn.functional.smooth_l1_loss(m(b), b.y).backward()
+    plain = [p.grad.detach().clone() if p.grad is not None else torch.zeros_like(p) for p in m.parameters()]
+    m2 = product_model(z, cuda)
+    bucket = GradBucket(m2.parameters())
+    for _ in range(2):  # the second pass checks that zero() + accumulate starts from scratch
+        bucket.zero()
+        torch.nn.functional.smooth_l1_loss(m2(b), b.y).backward()
+    for p, g in zip(m2.parameters(), plain):
+        assert torch.equal(p.grad, g)
+
+
 def test_trunk_drop_in_api_vs_fast_path(cuda):
     """SBFTransformer.forward(line_data, edge_index_0, atom_batch) with reference-layout inputs
     (per-triplet edge_attr, int64 triplet edge_index) equals the fused fast path."""

@@ -24,7 +24,7 @@ inline unsigned blocks_for(int64_t n, int per_block) {
 }
 
 // Tuning knobs for A/B experiments (x2g_tuning in line_graph.hip); 0 = default everywhere.
-enum TuneKey { kTuneDenseFwd = 0, kTuneDenseBwd = 1, kTuneAttn = 2, kTuneCount = 16 };
+enum TuneKey { kTuneDenseFwd = 0, kTuneDenseBwd = 1, kTuneAttn = 2, kTuneDenseDbg = 3, kTuneCount = 16 };
 int tuning(int key);
 
 // Masked loads without control flow.  Written as `ok ? load : 0`, the compiler sinks each load

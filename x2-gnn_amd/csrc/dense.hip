@@ -288,6 +288,274 @@ __global__ void __launch_bounds__(512) dense_fwd_persist(const float* __restrict
     fwd_tile<STEPS, VEC>(Ws, X, res, t, R, K, N, act, n, bn, Y, Z);
 }
 
+// ---------------------------------------------------------------- forward, LDS-staged x tiles
+// The same product for K % 4 == 0 (every trunk layer), with x staged through LDS in full
+// 512-byte rows instead of fragment-shaped loads (lane-per-row 16-byte loads touch 64 cache
+// lines per instruction and load the tile once per column wave: texture-address bound).
+//   * 8 waves, two 32-row tiles per iteration (slot = wave >> 2), wave w -> columns 32 (w & 3)..;
+//   * the next tile pair is loaded into registers (4 x 16 B per thread, coalesced rows) while the
+//     current pair is multiplied, then written to the other LDS buffer (double buffered);
+//   * LDS x tile: row r, 16-byte chunk q at chunk position q ^ (r & 15) — writes of 16
+//     consecutive chunks and the A-fragment reads (lane = row, chunk 16h + g) are both
+//     conflict-free; a lane's ds_read_b128 yields A values for 4 consecutive MFMA steps
+//     (c = 64h + 4g .. 64h + 4g + 3, the cmap<64> order of the slot-layout weight);
+//   * residual fragments for the current pair are loaded before the next pair's tile loads, so
+//     waiting for them never drains the prefetch.
+
+__device__ __forceinline__ void xpair_load(const float* __restrict__ X, int64_t tp, int64_t R, int K,
+                                           float4 (&v)[4]) {
+  const int kc = K >> 2;  // valid chunks per row
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int idx = threadIdx.x + 512 * u, row = idx >> 5, q = idx & 31;
+    const int r = static_cast<int>(tp) * 64 + row, rmax = static_cast<int>(R) - 1;
+    v[u] = *reinterpret_cast<const float4*>(X + (r < rmax ? r : rmax) * K + 4 * (q < kc ? q : kc - 1));
+  }
+}
+
+__device__ __forceinline__ void xpair_store(float* __restrict__ buf, const float4 (&v)[4]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int idx = threadIdx.x + 512 * u, row = idx >> 5, q = idx & 31;
+    *reinterpret_cast<float4*>(buf + row * 128 + 4 * (q ^ (row & 15))) = v[u];
+  }
+}
+
+template <int DBG>
+__global__ void __launch_bounds__(512) dense_fwd_staged(const float* __restrict__ X, const float* __restrict__ W,
+                                                        const float* __restrict__ bias,
+                                                        const float* __restrict__ res, int64_t R, int K, int N,
+                                                        int act, float* __restrict__ Y, float* __restrict__ Z) {
+  constexpr int dbg = DBG;  // phase switches for measurements (x2g_tuning key 3); 0 in production
+  __shared__ __attribute__((aligned(16))) float Ws[64 * 128 * 2];
+  __shared__ __attribute__((aligned(16))) float Xs[2][64 * 128];  // [buffer][slot*32 + row][128]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, i = lane & 31;
+  const int slot = wave >> 2;
+  const int n = 32 * (wave & 3) + i;
+  const int64_t npairs = (R + 63) / 64;
+  const int64_t G = gridDim.x;
+  const float bn = (bias && n < N) ? bias[n] : 0.f;
+  int64_t tp = blockIdx.x;
+  float4 stage[4];
+  {
+    float wv[32];
+    if (!(dbg & 1)) wslot_load<64, true, 512>(W, N, K, wv);
+    xpair_load(X, tp, R, K, stage);
+    if (!(dbg & 1)) wslot_store<512>(Ws, wv);
+    xpair_store(Xs[0], stage);
+    if (tp + G < npairs) xpair_load(X, tp + G, R, K, stage);
+    __syncthreads();
+  }
+  const float* wb = Ws + n * 2 + h;
+  for (int it = 0; tp < npairs; tp += G, ++it) {
+    const float* xs = Xs[it & 1] + (slot * 32 + i) * 128;
+    const int t = static_cast<int>(tp) * 2 + slot;  // this wave's 32-row tile
+    float rv[16];
+    if (res) cfrag_load(res, static_cast<int64_t>(t) * kPTile, R, N, n, rv);
+    // the pair after next: write the staged pair to the other buffer, then refill the registers
+    const bool more = tp + G < npairs;
+    if (more) xpair_store(Xs[(it + 1) & 1], stage);
+    if (tp + 2 * G < npairs) xpair_load(X, tp + 2 * G, R, K, stage);
+    floatx16 acc0, acc1;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      acc0[j] = 0.f;
+      acc1[j] = 0.f;
+    }
+#pragma unroll
+    for (int g = 0; g < ((dbg & 2) ? 1 : 16); ++g) {
+      const float4 a = *reinterpret_cast<const float4*>(xs + 4 * ((16 * h + g) ^ (i & 15)));
+      const int s = 4 * g;
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, wb[s * 256], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, wb[(s + 1) * 256], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, wb[(s + 2) * 256], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, wb[(s + 3) * 256], acc1, 0, 0, 0);
+    }
+    const int rbase = t * kPTile + 4 * h;
+    if (n < N && !(dbg & 4)) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int r = rbase + (j & 3) + 8 * (j >> 2);
+        const float zv = acc0[j] + acc1[j] + bn;
+        float v = act == kActSilu ? zv / (1.0f + expf(-zv)) : zv;
+        if (res) v += rv[j];
+        if (r < R) {
+          if (Z) Z[r * N + n] = zv;
+          Y[r * N + n] = v;
+        }
+      }
+    } else if (dbg & 4) {
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) sum += acc0[j] + acc1[j] + (res ? rv[j] : 0.f);
+      if (sum == 12345.678f) Y[n] = sum;
+    }
+    __syncthreads();  // the next buffer is complete; this one is free for the pair after next
+  }
+}
+
+// ---------------------------------------------------------------- forward, v5 (default)
+// dense_fwd_staged plus the two fixes its phase measurements called for (R = 21k rows: weight
+// staging 5.6 us, epilogue stores 6.3 us of 40 us):
+//   * the weight is read row-contiguous (coalesced) and written to a slot layout padded to 258
+//     floats per slot: 2-way bank conflicts on the staging writes, conflict-free B reads;
+//   * the epilogue goes through LDS: the C fragments (one column, 16 rows per lane) are written
+//     into the consumed x buffer, then every thread handles whole 16-byte row chunks: bias,
+//     activation, residual (loaded row-wise and early), and 16-byte stores of z and y
+//     (4x fewer store instructions than per-lane dword stores, which are issue-bound).
+constexpr int kSlotStride = 258;
+
+__device__ __forceinline__ void wpad_load(const float* __restrict__ W, int N, int K, float (&v)[32]) {
+#pragma unroll
+  for (int u = 0; u < 32; ++u) {
+    const int idx = threadIdx.x + 512 * u, n = idx >> 7, k = idx & 127;
+    const float x = ld_pin(W + (n < N ? n : N - 1) * K + (k < K ? k : K - 1));
+    v[u] = (n < N && k < K) ? x : 0.f;
+  }
+}
+
+__device__ __forceinline__ void wpad_store(float* __restrict__ ws, const float (&v)[32]) {
+#pragma unroll
+  for (int u = 0; u < 32; ++u) {
+    const int idx = threadIdx.x + 512 * u, n = idx >> 7, k = idx & 127;
+    ws[(k & 63) * kSlotStride + 2 * n + (k >> 6)] = v[u];  // B[c=k][j=n], cmap<64>: c = 64h + s
+  }
+}
+
+// 64 rows x 128 columns of a row-major [R, N] matrix (N % 4 == 0) in the x-pair thread mapping.
+__device__ __forceinline__ void rows_load(const float* __restrict__ m, int64_t tp, int64_t R, int N,
+                                          float4 (&v)[4]) {
+  const int nc = N >> 2;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int idx = threadIdx.x + 512 * u, row = idx >> 5, q = idx & 31;
+    const int r = static_cast<int>(tp) * 64 + row, rmax = static_cast<int>(R) - 1;
+    v[u] = *reinterpret_cast<const float4*>(m + (r < rmax ? r : rmax) * N + 4 * (q < nc ? q : nc - 1));
+  }
+}
+
+typedef float f4 __attribute__((ext_vector_type(4)));  // native vector: loads/stores stay in registers
+
+struct Stage4 {
+  f4 v0, v1, v2, v3;
+};
+
+// The tile-pair staging on named registers: a float4[4] carried across the tile loop with a
+// conditional refill stayed a private (scratch) array.  Chunk u of this thread: row
+// (tid >> 5) + 16 u of the pair, 16-byte column chunk tid & 31.
+template <int U>
+__device__ __forceinline__ f4 st_get(const Stage4& st) {
+  if constexpr (U == 0) return st.v0;
+  else if constexpr (U == 1) return st.v1;
+  else if constexpr (U == 2) return st.v2;
+  else return st.v3;
+}
+
+__device__ __forceinline__ void xpair_load4(const float* __restrict__ X, int64_t tp, int64_t R, int K, Stage4& st) {
+  const int kc = K >> 2, q = threadIdx.x & 31, qc = 4 * (q < kc ? q : kc - 1);
+  const int rmax = static_cast<int>(R) - 1, r0 = static_cast<int>(tp) * 64 + (threadIdx.x >> 5);
+  const int ra = r0 < rmax ? r0 : rmax, rb = r0 + 16 < rmax ? r0 + 16 : rmax;
+  const int rc = r0 + 32 < rmax ? r0 + 32 : rmax, rd = r0 + 48 < rmax ? r0 + 48 : rmax;
+  st.v0 = *reinterpret_cast<const f4*>(X + ra * K + qc);
+  st.v1 = *reinterpret_cast<const f4*>(X + rb * K + qc);
+  st.v2 = *reinterpret_cast<const f4*>(X + rc * K + qc);
+  st.v3 = *reinterpret_cast<const f4*>(X + rd * K + qc);
+}
+
+__device__ __forceinline__ void xpair_store4(float* __restrict__ buf, const Stage4& st) {
+  const int q = threadIdx.x & 31, row = threadIdx.x >> 5;  // rows row, +16, +32, +48 share (row & 15)
+  float* p = buf + row * 128 + 4 * (q ^ (row & 15));
+  *reinterpret_cast<f4*>(p) = st.v0;
+  *reinterpret_cast<f4*>(p + 16 * 128) = st.v1;
+  *reinterpret_cast<f4*>(p + 32 * 128) = st.v2;
+  *reinterpret_cast<f4*>(p + 48 * 128) = st.v3;
+}
+
+__device__ __forceinline__ float act_apply(float z, int act) { return act == kActSilu ? z / (1.0f + expf(-z)) : z; }
+
+// Row-wise epilogue of one 16-byte chunk (row (tid >> 5) + 16 U of the pair): bias, activation,
+// residual, 16-byte stores of z and y.
+template <int U>
+__device__ __forceinline__ void epi_chunk(const float* __restrict__ buf, const Stage4& rres, f4 b4, int64_t tp,
+                                          int64_t R, int N, int act, float* __restrict__ Y, float* __restrict__ Z) {
+  const int q = threadIdx.x & 31, row = (threadIdx.x >> 5) + 16 * U;
+  const int r = static_cast<int>(tp) * 64 + row;
+  const f4 zc = *reinterpret_cast<const f4*>(buf + row * 128 + 4 * (q ^ (row & 15))) + b4;
+  const f4 rr = st_get<U>(rres);
+  f4 yv;
+  yv.x = act_apply(zc.x, act) + rr.x;
+  yv.y = act_apply(zc.y, act) + rr.y;
+  yv.z = act_apply(zc.z, act) + rr.z;
+  yv.w = act_apply(zc.w, act) + rr.w;
+  if (r < R && 4 * q < N) {
+    if (Z) *reinterpret_cast<f4*>(Z + r * N + 4 * q) = zc;
+    *reinterpret_cast<f4*>(Y + r * N + 4 * q) = yv;
+  }
+}
+
+__global__ void __launch_bounds__(512) dense_fwd_v5(const float* __restrict__ X, const float* __restrict__ W,
+                                                    const float* __restrict__ bias, const float* __restrict__ res,
+                                                    int64_t R, int K, int N, int act, float* __restrict__ Y,
+                                                    float* __restrict__ Z) {
+  __shared__ __attribute__((aligned(16))) float Ws[64 * kSlotStride];
+  __shared__ __attribute__((aligned(16))) float Xs[2][64 * 128];  // [buffer][slot*32 + row][128]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, i = lane & 31;
+  const int slot = wave >> 2;
+  const int n = 32 * (wave & 3) + i;
+  const int q = tid & 31;  // this thread's 16-byte column chunk in the row-wise epilogue
+  const int64_t npairs = (R + 63) / 64;
+  const int64_t G = gridDim.x;
+  f4 b4 = {0.f, 0.f, 0.f, 0.f};
+  if (bias && 4 * q < N) b4 = *reinterpret_cast<const f4*>(bias + 4 * q);
+  int64_t tp = blockIdx.x;
+  Stage4 stage;
+  {
+    float wv[32];
+    wpad_load(W, N, K, wv);
+    xpair_load4(X, tp, R, K, stage);
+    wpad_store(Ws, wv);
+    xpair_store4(Xs[0], stage);
+    if (tp + G < npairs) xpair_load4(X, tp + G, R, K, stage);
+    __syncthreads();
+  }
+  const float* wb = Ws + 2 * n + h;
+  for (int it = 0; tp < npairs; tp += G, ++it) {
+    float* buf = Xs[it & 1];
+    const float* xs = buf + (slot * 32 + i) * 128;
+    Stage4 rres{};
+    if (res) xpair_load4(res, tp, R, N, rres);  // before the prefetch: waiting for it never drains that
+    if (tp + G < npairs) xpair_store4(Xs[(it + 1) & 1], stage);
+    if (tp + 2 * G < npairs) xpair_load4(X, tp + 2 * G, R, K, stage);
+    floatx16 acc0, acc1;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      acc0[j] = 0.f;
+      acc1[j] = 0.f;
+    }
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const float4 a = *reinterpret_cast<const float4*>(xs + 4 * ((16 * h + g) ^ (i & 15)));
+      const int sb = 4 * g * kSlotStride;
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, wb[sb], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, wb[sb + kSlotStride], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, wb[sb + 2 * kSlotStride], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, wb[sb + 3 * kSlotStride], acc1, 0, 0, 0);
+    }
+    __syncthreads();  // every wave is done with this buffer's x: it now stages the output
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int r = slot * 32 + (j & 3) + 8 * (j >> 2) + 4 * h;
+      buf[r * 128 + 4 * ((n >> 2) ^ (r & 15)) + (n & 3)] = acc0[j] + acc1[j];
+    }
+    __syncthreads();
+    epi_chunk<0>(buf, rres, b4, tp, R, N, act, Y, Z);
+    epi_chunk<1>(buf, rres, b4, tp, R, N, act, Y, Z);
+    epi_chunk<2>(buf, rres, b4, tp, R, N, act, Y, Z);
+    epi_chunk<3>(buf, rres, b4, tp, R, N, act, Y, Z);
+    __syncthreads();  // this buffer is rewritten with the pair after next
+  }
+}
+
 // ---------------------------------------------------------------------------------- backward
 // Backward of dense_fwd_persist, fused: dz = dy * act'(z); dx = dz w (if dx != NULL); partial
 // weight / bias gradients dz^T x and colsum(dz) over the workgroup's tiles, written to slab
@@ -343,7 +611,8 @@ __device__ __forceinline__ void bwd_tile(float* __restrict__ Ds, float* __restri
                                          BwdRegs& cur, BwdRegs& nxt, const float* __restrict__ dY,
                                          const float* __restrict__ Zin, const float* __restrict__ X, int64_t t,
                                          int64_t G, int64_t ntiles, int64_t R, int K, int N, int act,
-                                         float* __restrict__ dX, floatx16 (&accw)[2], float& bsum, bool do_bias) {
+                                         float* __restrict__ dX, const float* __restrict__ dXadd,
+                                         floatx16 (&accw)[2], float& bsum, bool do_bias) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, i = lane & 31;
   if (act == kActSilu) {
 #pragma unroll
@@ -375,7 +644,7 @@ __device__ __forceinline__ void bwd_tile(float* __restrict__ Ds, float* __restri
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const int r = static_cast<int>(t) * kBTile + rt + (j & 3) + 8 * (j >> 2) + 4 * h;
-        if (r < R) dX[r * K + k] = acc0[j] + acc1[j];
+        if (r < R) dX[r * K + k] = acc0[j] + acc1[j] + (dXadd ? dXadd[r * K + k] : 0.f);
       }
     }
   }
@@ -401,7 +670,8 @@ template <int NSTEPS>
 __global__ void __launch_bounds__(512) dense_bwd_persist(const float* __restrict__ dY, const float* __restrict__ Zin,
                                                          const float* __restrict__ X, const float* __restrict__ W,
                                                          int64_t R, int K, int N, int act, float* __restrict__ dX,
-                                                         float* __restrict__ part_w, float* __restrict__ part_b) {
+                                                         const float* __restrict__ dXadd, float* __restrict__ part_w,
+                                                         float* __restrict__ part_b) {
   __shared__ __attribute__((aligned(16))) float Ws[64 * 128 * 2];
   __shared__ float Ds[kBTile * kBwdStride];
   __shared__ float Xs[kBTile * kBwdStride];
@@ -424,9 +694,10 @@ __global__ void __launch_bounds__(512) dense_bwd_persist(const float* __restrict
   }
   const bool do_bias = part_b != nullptr;
   for (; t < ntiles; t += 2 * G) {
-    bwd_tile<NSTEPS>(Ds, Xs, Ws, A, B, dY, Zin, X, t, G, ntiles, R, K, N, act, dX, accw, bsum, do_bias);
+    bwd_tile<NSTEPS>(Ds, Xs, Ws, A, B, dY, Zin, X, t, G, ntiles, R, K, N, act, dX, dXadd, accw, bsum, do_bias);
     if (t + G >= ntiles) break;
-    bwd_tile<NSTEPS>(Ds, Xs, Ws, B, A, dY, Zin, X, t + G, G, ntiles, R, K, N, act, dX, accw, bsum, do_bias);
+    bwd_tile<NSTEPS>(Ds, Xs, Ws, B, A, dY, Zin, X, t + G, G, ntiles, R, K, N, act, dX, dXadd, accw, bsum,
+                     do_bias);
   }
   float* slab = part_w + static_cast<int64_t>(blockIdx.x) * N * K;
   const int nb = 32 * (wave & 3), kb = 64 * (wave >> 2);
@@ -442,9 +713,178 @@ __global__ void __launch_bounds__(512) dense_bwd_persist(const float* __restrict
   if (part_b && tid < N) part_b[static_cast<int64_t>(blockIdx.x) * N + tid] = bsum;
 }
 
+// ---------------------------------------------------------------- backward, v5 (default)
+// dense_bwd_persist restructured like dense_fwd_v5 (K % 4 == 0, N % 4 == 0, 16-byte aligned):
+//   * dy, z, x tiles (64 rows) are read with 16-byte loads (4 per thread per matrix instead of
+//     16 dword loads) into registers, the next tile's loads fly during the MFMAs;
+//   * LDS: weight in the padded slot layout (cmap<64>, B[c = n][j = k] = w[n][k], staged from
+//     coalesced rows), dz and x tiles in the chunk-swizzled [64][128] layout: dx's A fragments
+//     are ds_read_b128 (4 MFMA steps each) and dW's row pairs (r, r ^ 8) hit disjoint banks;
+//   * dx leaves through LDS (transposed into the consumed x tile) as 16-byte row stores.
+// 8 waves: dx wave w -> rows 32 (w >> 2).., k columns 32 (w & 3)..;
+//          dW wave w -> n rows 32 (w & 3).., k columns 64 (w >> 2)...
+__device__ __forceinline__ int swz(int r, int c) { return r * 128 + 4 * ((c >> 2) ^ (r & 15)) + (c & 3); }
+
+__device__ __forceinline__ void wpad_load_bwd(const float* __restrict__ W, int N, int K, float (&v)[32]) {
+#pragma unroll
+  for (int u = 0; u < 32; ++u) {  // row n = idx >> 7 of w, k = idx & 127: coalesced
+    const int idx = threadIdx.x + 512 * u, n = idx >> 7, k = idx & 127;
+    const float x = ld_pin(W + (n < N ? n : N - 1) * K + (k < K ? k : K - 1));
+    v[u] = (n < N && k < K) ? x : 0.f;
+  }
+}
+
+__device__ __forceinline__ void wpad_store_bwd(float* __restrict__ ws, const float (&v)[32]) {
+#pragma unroll
+  for (int u = 0; u < 32; ++u) {
+    const int idx = threadIdx.x + 512 * u, n = idx >> 7, k = idx & 127;
+    ws[(n & 63) * kSlotStride + 2 * k + (n >> 6)] = v[u];  // B[c=n][j=k], c = 64h + s
+  }
+}
+
+template <int U>
+__device__ __forceinline__ f4 silu_grad4(f4 d, f4 z) {
+  f4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float sg = 1.0f / (1.0f + expf(-z[e]));
+    o[e] = d[e] * (sg * (1.0f + z[e] * (1.0f - sg)));
+  }
+  return o;
+}
+
+// rows >= R and columns >= cols of a staged tile are zeroed on the way into LDS
+__device__ __forceinline__ f4 mask4(f4 v, int64_t tp, int U, int64_t R, int cols) {
+  const int q = threadIdx.x & 31, row = (threadIdx.x >> 5) + 16 * U;
+  const bool ok = tp * 64 + row < R && 4 * q < cols;
+  return ok ? v : f4{0.f, 0.f, 0.f, 0.f};
+}
+
+__global__ void __launch_bounds__(512) dense_bwd_v5(const float* __restrict__ dY, const float* __restrict__ Zin,
+                                                    const float* __restrict__ X, const float* __restrict__ W,
+                                                    int64_t R, int K, int N, int act, float* __restrict__ dX,
+                                                    const float* __restrict__ dXadd, float* __restrict__ part_w,
+                                                    float* __restrict__ part_b) {
+  __shared__ __attribute__((aligned(16))) float Ws[64 * kSlotStride];
+  __shared__ __attribute__((aligned(16))) float Ds[64 * 128];
+  __shared__ __attribute__((aligned(16))) float Xs[64 * 128];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, i = lane & 31;
+  const int64_t ntiles = (R + 63) / 64;
+  const int64_t G = gridDim.x;
+  const bool silu = act == kActSilu;
+  floatx16 accw0, accw1;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    accw0[j] = 0.f;
+    accw1[j] = 0.f;
+  }
+  float bsum = 0.f;
+  int64_t t = blockIdx.x;
+  Stage4 sd, sz, sx;
+  {
+    float wv[32];
+    if (dX) wpad_load_bwd(W, N, K, wv);
+    xpair_load4(dY, t, R, N, sd);
+    if (silu) xpair_load4(Zin, t, R, N, sz);
+    xpair_load4(X, t, R, K, sx);
+    if (dX) wpad_store_bwd(Ws, wv);
+  }
+  const int rt = 32 * (wave >> 2), kcol = 32 * (wave & 3) + i;  // dx block
+  const int nb = 32 * (wave & 3), kb = 64 * (wave >> 2);        // dW block
+  for (; t < ntiles; t += G) {
+    // dz = dy * act'(z) -> Ds, x -> Xs (masked rows / columns)
+    {
+      f4 d0 = sd.v0, d1 = sd.v1, d2 = sd.v2, d3 = sd.v3;
+      if (silu) {
+        d0 = silu_grad4<0>(d0, sz.v0);
+        d1 = silu_grad4<1>(d1, sz.v1);
+        d2 = silu_grad4<2>(d2, sz.v2);
+        d3 = silu_grad4<3>(d3, sz.v3);
+      }
+      Stage4 dz{mask4(d0, t, 0, R, N), mask4(d1, t, 1, R, N), mask4(d2, t, 2, R, N), mask4(d3, t, 3, R, N)};
+      Stage4 xm{mask4(sx.v0, t, 0, R, K), mask4(sx.v1, t, 1, R, K), mask4(sx.v2, t, 2, R, K),
+                mask4(sx.v3, t, 3, R, K)};
+      xpair_store4(Ds, dz);
+      xpair_store4(Xs, xm);
+    }
+    __syncthreads();
+    if (t + G < ntiles) {  // next tile's loads fly during the MFMAs below
+      xpair_load4(dY, t + G, R, N, sd);
+      if (silu) xpair_load4(Zin, t + G, R, N, sz);
+      xpair_load4(X, t + G, R, K, sx);
+    }
+    floatx16 acc0, acc1;
+    if (dX) {  // dx[rt + i][kcol] = sum_n dz[r][n] w[n][k], n = 64h + 4g + e
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        acc0[j] = 0.f;
+        acc1[j] = 0.f;
+      }
+      const float* ds = Ds + (rt + i) * 128;
+      const float* wb = Ws + 2 * kcol + h;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const f4 a = *reinterpret_cast<const f4*>(ds + 4 * ((16 * h + g) ^ (i & 15)));
+        const int sb = 4 * g * kSlotStride;
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, wb[sb], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, wb[sb + kSlotStride], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, wb[sb + 2 * kSlotStride], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, wb[sb + 3 * kSlotStride], acc1, 0, 0, 0);
+      }
+    }
+    // dW[n][k] += sum_r dz[r][n] x[r][k]; step s: rows ra = (s & 7) + 16 (s >> 3) and ra + 8
+    // (r & 15) = (s & 7) + 8h is the same for the 4 row groups: 8 address patterns, one loop of 4
+#pragma unroll 1
+    for (int sg = 0; sg < 4; ++sg) {
+      const float* dsg = Ds + sg * 16 * 128;
+      const float* xsg = Xs + sg * 16 * 128;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int r = s + 8 * h;
+        const float a = dsg[swz(r, nb + i)];
+        accw0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xsg[swz(r, kb + i)], accw0, 0, 0, 0);
+        accw1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xsg[swz(r, kb + 32 + i)], accw1, 0, 0, 0);
+      }
+    }
+    if (part_b && tid < 128) {
+#pragma unroll 8
+      for (int rr = 0; rr < 64; ++rr) bsum += Ds[swz(rr, tid)];
+    }
+    __syncthreads();  // Ds / Xs consumed
+    if (dX) {  // dx through LDS (into Xs), then 16-byte row stores
+#pragma unroll
+      for (int j = 0; j < 16; ++j) Xs[swz(rt + (j & 3) + 8 * (j >> 2) + 4 * h, kcol)] = acc0[j] + acc1[j];
+      __syncthreads();
+      const int q = tid & 31;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int row = (tid >> 5) + 16 * u;
+        const int r = static_cast<int>(t) * 64 + row;
+        f4 v = *reinterpret_cast<const f4*>(Xs + row * 128 + 4 * (q ^ (row & 15)));
+        if (r < R && 4 * q < K) {
+          if (dXadd) v += *reinterpret_cast<const f4*>(dXadd + r * K + 4 * q);
+          *reinterpret_cast<f4*>(dX + r * K + 4 * q) = v;
+        }
+      }
+      __syncthreads();  // Xs is rewritten by the next tile
+    }
+  }
+  float* slab = part_w + static_cast<int64_t>(blockIdx.x) * N * K;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int nn = nb + (j & 3) + 8 * (j >> 2) + 4 * h;
+    const int k0 = kb + i, k1 = kb + 32 + i;
+    if (nn < N && k0 < K) slab[nn * K + k0] = accw0[j];
+    if (nn < N && k1 < K) slab[nn * K + k1] = accw1[j];
+  }
+  if (part_b && tid < N) part_b[static_cast<int64_t>(blockIdx.x) * N + tid] = bsum;
+}
+
 }  // namespace x2g
 
 using namespace x2g;
+
+static inline bool aligned16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 
 X2G_API int x2g_dense_fwd(const float* x, const float* w, const float* b, int64_t R, int32_t K, int32_t N, int act,
                           const float* res, float* y, float* z, void* stream) {
@@ -452,14 +892,25 @@ X2G_API int x2g_dense_fwd(const float* x, const float* w, const float* b, int64_
   if (R == 0) return X2G_OK;
   if (!x || !w || !y) return X2G_EINVAL;
   hipStream_t st = as_stream(stream);
-  const int variant = tuning(kTuneDenseFwd);  // 0: persistent (default), other: tiled
-  if (K <= 128 && N <= 128 && variant == 0 && R * 128 < (int64_t(1) << 31)) {
+  const int variant = tuning(kTuneDenseFwd);  // 0: LDS-staged (default), 1: register fragments, 2: tiled
+  if (K <= 128 && N <= 128 && variant <= 1 && R * 128 < (int64_t(1) << 31)) {
     const int64_t ntiles = (R + kPTile - 1) / kPTile;
     const int64_t want = (ntiles + 1) / 2;
     const unsigned grid = static_cast<unsigned>(want < kPFwdGrid ? want : kPFwdGrid);
     const bool vec = K % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0;
     if (K <= 8)
       dense_fwd_persist<4, false><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
+    else if (vec && variant == 0 && N % 4 == 0 && aligned16(y) && aligned16(z) && aligned16(res) && aligned16(b))
+      dense_fwd_v5<<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
+    else if (vec && variant == 0)
+      switch (tuning(kTuneDenseDbg)) {
+        case 1: dense_fwd_staged<1><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z); break;
+        case 2: dense_fwd_staged<2><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z); break;
+        case 4: dense_fwd_staged<4><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z); break;
+        case 6: dense_fwd_staged<6><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z); break;
+        case 7: dense_fwd_staged<7><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z); break;
+        default: dense_fwd_staged<0><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z); break;
+      }
     else if (vec)
       dense_fwd_persist<64, true><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
     else
@@ -490,7 +941,7 @@ X2G_API int x2g_dense_bwd_data(const float* dy, const float* z, int act, const f
 
 namespace x2g {  // slab sums come from linear.hip
 int sum_slabs_launch(const float* part_w, int64_t nw, const float* part_b, int64_t nb, int splits, float* dw,
-                     float* db, hipStream_t st);
+                     float* db, bool accum, hipStream_t st);
 }  // namespace x2g
 
 X2G_API size_t x2g_linear_wgrad_workspace(int64_t R, int32_t O, int32_t I);
@@ -513,12 +964,19 @@ X2G_API size_t x2g_dense_bwd_workspace(int64_t R, int32_t K, int32_t N) {
   return dz + x2g_linear_wgrad_workspace(R, N, K);
 }
 
-X2G_API int x2g_dense_bwd(const float* dy, const float* z, int act, const float* x, const float* w, int64_t R,
-                          int32_t K, int32_t N, float* dx, float* dw, float* db, void* workspace,
-                          size_t workspace_bytes, void* stream) {
-  if (R < 0 || K <= 0 || N <= 0 || (act != kActNone && act != kActSilu) || !dw) return X2G_EINVAL;
+X2G_API int x2g_linear_wgrad_ex(const float* dy, const float* x, int64_t R, int32_t O, int32_t I, float* dw,
+                                float* db, int flags, void* workspace, size_t workspace_bytes, void* stream);
+
+X2G_API int x2g_dense_bwd_ex(const float* dy, const float* z, int act, const float* x, const float* w, int64_t R,
+                             int32_t K, int32_t N, float* dx, const float* dx_add, float* dw, float* db, int flags,
+                             void* workspace, size_t workspace_bytes, void* stream) {
+  if (R < 0 || K <= 0 || N <= 0 || (act != kActNone && act != kActSilu) || !dw || (flags & ~X2G_ACCUM_WGRAD))
+    return X2G_EINVAL;
+  if (dx_add && !dx) return X2G_EINVAL;
+  const bool accum = flags & X2G_ACCUM_WGRAD;
   hipStream_t st = as_stream(stream);
   if (R == 0) {
+    if (accum) return X2G_OK;
     hipError_t e = hipMemsetAsync(dw, 0, sizeof(float) * N * K, st);
     if (e == hipSuccess && db) e = hipMemsetAsync(db, 0, sizeof(float) * N, st);
     return e == hipSuccess ? X2G_OK : static_cast<int>(e);
@@ -530,15 +988,20 @@ X2G_API int x2g_dense_bwd(const float* dy, const float* z, int act, const float*
     const int grid = static_cast<int>(ntiles < kPBwdGrid ? ntiles : kPBwdGrid);
     float* part_w = static_cast<float*>(workspace);
     float* part_b = db ? part_w + static_cast<int64_t>(grid) * N * K : nullptr;
-    if (N <= 8)
-      dense_bwd_persist<4><<<grid, 512, 0, st>>>(dy, z, x, w, R, K, N, act, dx, part_w, part_b);
+    const bool v5 = tuning(kTuneDenseBwd) == 0 && K % 4 == 0 && N % 4 == 0 && N > 8 && aligned16(dy) &&
+                    aligned16(z) && aligned16(x) && aligned16(dx) && aligned16(dx_add);
+    if (v5)
+      dense_bwd_v5<<<grid, 512, 0, st>>>(dy, z, x, w, R, K, N, act, dx, dx_add, part_w, part_b);
+    else if (N <= 8)
+      dense_bwd_persist<4><<<grid, 512, 0, st>>>(dy, z, x, w, R, K, N, act, dx, dx_add, part_w, part_b);
     else
-      dense_bwd_persist<64><<<grid, 512, 0, st>>>(dy, z, x, w, R, K, N, act, dx, part_w, part_b);
+      dense_bwd_persist<64><<<grid, 512, 0, st>>>(dy, z, x, w, R, K, N, act, dx, dx_add, part_w, part_b);
     int rc = last_launch_status();
     if (rc) return rc;
-    return sum_slabs_launch(part_w, static_cast<int64_t>(N) * K, part_b, N, grid, dw, db, st);
+    return sum_slabs_launch(part_w, static_cast<int64_t>(N) * K, part_b, N, grid, dw, db, accum, st);
   }
   // general shapes: dz = dy * act'(z) and dx = dz w in one kernel, then the weight gradient
+  if (dx_add) return X2G_EUNSUPPORTED;
   float* dzbuf = static_cast<float*>(workspace);
   const size_t dz_bytes = ((static_cast<size_t>(R) * N * sizeof(float)) + 255) / 256 * 256;
   const float* dzp = dy;
@@ -549,6 +1012,12 @@ X2G_API int x2g_dense_bwd(const float* dy, const float* z, int act, const float*
     if ((rc = x2g_dense_bwd_data(dy, z, act, w, R, K, N, dx_tmp, act != kActNone ? dzbuf : nullptr, stream))) return rc;
     if (act != kActNone) dzp = dzbuf;
   }
-  return x2g_linear_wgrad(dzp, x, R, N, K, dw, db, static_cast<char*>(workspace) + dz_bytes,
-                          workspace_bytes - dz_bytes, stream);
+  return x2g_linear_wgrad_ex(dzp, x, R, N, K, dw, db, flags, static_cast<char*>(workspace) + dz_bytes,
+                             workspace_bytes - dz_bytes, stream);
+}
+
+X2G_API int x2g_dense_bwd(const float* dy, const float* z, int act, const float* x, const float* w, int64_t R,
+                          int32_t K, int32_t N, float* dx, float* dw, float* db, void* workspace,
+                          size_t workspace_bytes, void* stream) {
+  return x2g_dense_bwd_ex(dy, z, act, x, w, R, K, N, dx, nullptr, dw, db, 0, workspace, workspace_bytes, stream);
 }

@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(256) wgrad_partial(const float* __restrict__ d
 // out[e] = sum_s part[s][e] in a fixed order: each of the 4 waves of a block sums a quarter of
 // the slabs for the block's 64 elements, then the quarters are added in wave order.
 __device__ __forceinline__ void sum_slabs_block(const float* __restrict__ part, int64_t n, int splits, int64_t blk,
-                                                float* __restrict__ out, float (*red)[64]) {
+                                                bool accum, float* __restrict__ out, float (*red)[64]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t e = blk * 64 + lane;
   const int per = (splits + 3) / 4;
@@ -150,42 +150,42 @@ __device__ __forceinline__ void sum_slabs_block(const float* __restrict__ part, 
   }
   red[wave][lane] = s;
   __syncthreads();
-  if (wave == 0 && e < n) out[e] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  if (wave == 0 && e < n) {
+    const float v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    out[e] = accum ? out[e] + v : v;
+  }
 }
 
-__global__ void __launch_bounds__(256) sum_slabs(const float* __restrict__ part, int64_t n, int splits,
+__global__ void __launch_bounds__(256) sum_slabs(const float* __restrict__ part, int64_t n, int splits, int accum,
                                                  float* __restrict__ out) {
   __shared__ float red[4][64];
-  sum_slabs_block(part, n, splits, blockIdx.x, out, red);
+  sum_slabs_block(part, n, splits, blockIdx.x, accum != 0, out, red);
 }
 
 // Two slab sets (weight and bias partials) in one launch: blocks [0, nblk_a) take the first.
 __global__ void __launch_bounds__(256) sum_slabs2(const float* __restrict__ part_a, int64_t na,
-                                                  const float* __restrict__ part_b, int64_t nb, int splits,
+                                                  const float* __restrict__ part_b, int64_t nb, int splits, int accum,
                                                   float* __restrict__ out_a, float* __restrict__ out_b) {
   __shared__ float red[4][64];
   const int64_t nblk_a = (na + 63) / 64;
   if (static_cast<int64_t>(blockIdx.x) < nblk_a)
-    sum_slabs_block(part_a, na, splits, blockIdx.x, out_a, red);
+    sum_slabs_block(part_a, na, splits, blockIdx.x, accum != 0, out_a, red);
   else
-    sum_slabs_block(part_b, nb, splits, blockIdx.x - nblk_a, out_b, red);
+    sum_slabs_block(part_b, nb, splits, blockIdx.x - nblk_a, accum != 0, out_b, red);
 }
 
-// dw (and db when part_b != NULL) from their slabs, one launch
+// dw (and db when part_b != NULL) from their slabs, one launch; accum: dw += ..., db += ...
 int sum_slabs_launch(const float* part_w, int64_t nw, const float* part_b, int64_t nb, int splits, float* dw,
-                     float* db, hipStream_t st) {
+                     float* db, bool accum, hipStream_t st) {
   if (part_b && db)
-    sum_slabs2<<<blocks_for(nw, 64) + blocks_for(nb, 64), 256, 0, st>>>(part_w, nw, part_b, nb, splits, dw, db);
+    sum_slabs2<<<blocks_for(nw, 64) + blocks_for(nb, 64), 256, 0, st>>>(part_w, nw, part_b, nb, splits, accum,
+                                                                          dw, db);
   else
-    sum_slabs<<<blocks_for(nw, 64), 256, 0, st>>>(part_w, nw, splits, dw);
+    sum_slabs<<<blocks_for(nw, 64), 256, 0, st>>>(part_w, nw, splits, accum, dw);
   return last_launch_status();
 }
 
 // rows per split: a multiple of the 32-row chunk, at least 64, at most kWgMaxSplits splits
-int sum_slabs_launch(const float* part, int64_t n, int splits, float* out, hipStream_t st) {
-  sum_slabs<<<blocks_for(n, 64), 256, 0, st>>>(part, n, splits, out);
-  return last_launch_status();
-}
 
 inline int64_t wgrad_rows_per_split(int64_t R) {
   int64_t rps = (R + kWgMaxSplits - 1) / kWgMaxSplits;
@@ -207,11 +207,13 @@ X2G_API size_t x2g_linear_wgrad_workspace(int64_t R, int32_t O, int32_t I) {
   return static_cast<size_t>(s) * (static_cast<int64_t>(O) * I + O) * sizeof(float);
 }
 
-X2G_API int x2g_linear_wgrad(const float* dy, const float* x, int64_t R, int32_t O, int32_t I, float* dw, float* db,
-                             void* workspace, size_t workspace_bytes, void* stream) {
-  if (R < 0 || O <= 0 || I <= 0 || !dw) return X2G_EINVAL;
+X2G_API int x2g_linear_wgrad_ex(const float* dy, const float* x, int64_t R, int32_t O, int32_t I, float* dw,
+                                float* db, int flags, void* workspace, size_t workspace_bytes, void* stream) {
+  if (R < 0 || O <= 0 || I <= 0 || !dw || (flags & ~X2G_ACCUM_WGRAD)) return X2G_EINVAL;
+  const bool accum = flags & X2G_ACCUM_WGRAD;
   hipStream_t st = as_stream(stream);
   if (R == 0) {
+    if (accum) return X2G_OK;
     hipError_t e = hipMemsetAsync(dw, 0, sizeof(float) * O * I, st);
     if (e == hipSuccess && db) e = hipMemsetAsync(db, 0, sizeof(float) * O, st);
     return e == hipSuccess ? X2G_OK : static_cast<int>(e);
@@ -231,5 +233,10 @@ X2G_API int x2g_linear_wgrad(const float* dy, const float* x, int64_t R, int32_t
     wgrad_partial<false><<<grid, 256, 0, st>>>(dy, x, R, O, I, tiles_i, wgrad_rows_per_split(R), part, part_b);
   int rc = last_launch_status();
   if (rc) return rc;
-  return sum_slabs_launch(part, static_cast<int64_t>(O) * I, part_b, O, splits, dw, db, st);
+  return sum_slabs_launch(part, static_cast<int64_t>(O) * I, part_b, O, splits, dw, db, accum, st);
+}
+
+X2G_API int x2g_linear_wgrad(const float* dy, const float* x, int64_t R, int32_t O, int32_t I, float* dw, float* db,
+                             void* workspace, size_t workspace_bytes, void* stream) {
+  return x2g_linear_wgrad_ex(dy, x, R, O, I, dw, db, 0, workspace, workspace_bytes, stream);
 }

@@ -39,6 +39,9 @@ class GradBucket:
         off = 0
         for p in self.params:
             p.grad = self.flat[off:off + p.numel()].view_as(p)
+            # the fused dense / attention backwards may sum weight gradients straight into this
+            # buffer (ops.grad_sink) instead of returning them for autograd to add
+            p._x2g_grad_sink = True
             off += p.numel()
 
     def zero(self):

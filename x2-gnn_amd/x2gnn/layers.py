@@ -159,7 +159,11 @@ class EmbeddingBlock(nn.Module):
         materialising the [N, D] output: row z of the result stands for every atom of type z.
         """
         emb = self.embedding
-        counts = torch.bincount(atomic_num.reshape(-1), minlength=emb.num_embeddings)[: emb.num_embeddings]
+        z = atomic_num.reshape(-1)
+        # counts per element without torch.bincount (its output size is data-dependent: a host sync
+        # that would also break HIP-graph capture); float counts are exact below 2^24
+        counts = torch.zeros(emb.num_embeddings, dtype=torch.float32, device=z.device)
+        counts.index_add_(0, z, torch.ones(z.shape[0], dtype=torch.float32, device=z.device))
         w = emb.weight
         if emb.max_norm is not None:
             with torch.no_grad():

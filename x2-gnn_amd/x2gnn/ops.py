@@ -150,6 +150,7 @@ def spherical_basis_from_angles(theta, trip_src, rbf_env):
 class _SBFAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row, heads, channels):
+        w_param, b_param = w_sbf, b_sbf
         q, k, v, skip = _f32(q), _f32(k), _f32(v), _f32(skip)
         sbf, w_sbf, b_sbf = _f32(sbf), _f32(w_sbf), _f32(b_sbf)
         edge = _f32(edge) if edge is not None else None
@@ -163,6 +164,7 @@ class _SBFAttention(torch.autograd.Function):
              ptr(sbf), ptr(w_sbf), ptr(b_sbf), ptr(lg.trip_rowptr), ptr(lg.trip_src), E, T, heads, channels,
              sbf.shape[1], ptr(out), ptr(alpha), ptr(smax), ptr(sden), stream_ptr())
         ctx.save_for_backward(q, k, v, edge, sbf, w_sbf, b_sbf, alpha, smax, sden)
+        ctx.w_param, ctx.b_param = w_param, b_param
         ctx.lg, ctx.edge_mode, ctx.edge_row, ctx.heads, ctx.channels = lg, edge_mode, edge_row, heads, channels
         ctx.edge_shape = None if edge is None else edge.shape
         ctx.mark_non_differentiable(alpha, smax, sden)
@@ -198,7 +200,11 @@ class _SBFAttention(torch.autograd.Function):
             # rows of the edge table are shared by many destinations: sum d_edge per table row
             onehot = torch.nn.functional.one_hot(ctx.edge_row.long(), ctx.edge_shape[0]).to(torch.float32)
             d_edge = linear_wgrad(d_edge, onehot, bias=False)[0].t().contiguous()
-        dw, db = linear_wgrad(dproj, sbf)
+        gw, gb = grad_sink(ctx.w_param), grad_sink(ctx.b_param)
+        if gw is not None and gb is not None:
+            dw, db = linear_wgrad(dproj, sbf, dw_out=gw, db_out=gb)  # summed into the bucket: None
+        else:
+            dw, db = linear_wgrad(dproj, sbf)
         return dq, dk, dv, dout, d_edge, None, dw, db, None, None, None, None, None
 
 
@@ -223,19 +229,41 @@ def sbf_attention(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg: LineGraph, heads: 
 
 
 # ---------------------------------------------------------------------------------- dense layers
-def linear_wgrad(dy, x, bias=True):
+ACCUM_WGRAD = 1  # X2G_ACCUM_WGRAD
+
+
+def grad_sink(param):
+    """The parameter's gradient buffer when the kernels may accumulate into it directly.
+
+    ``dist.GradBucket`` marks its parameters: their ``.grad`` is a view of one flat zeroed buffer,
+    so a weight gradient can be summed straight into it by the slab-sum kernel (X2G_ACCUM_WGRAD)
+    and the Function returns None for that input — autograd then launches no add kernel for it.
+    Unmarked parameters (tests, plain ``loss.backward()``) get their gradient returned as usual."""
+    if param is None or not getattr(param, "_x2g_grad_sink", False):
+        return None
+    g = param.grad
+    if g is None or not g.is_contiguous() or g.dtype != torch.float32:
+        return None
+    return g
+
+
+def linear_wgrad(dy, x, bias=True, dw_out=None, db_out=None):
     """(dW [O, I], db [O] or None) with dW = dy^T x, db = column sums of dy, for row-major
     dy [R, O], x [R, I]: row-split MFMA partials + fixed-order slab sum (csrc/linear.hip)."""
     _need_cuda(dy, x)
     dy, x = _f32(dy), _f32(x)
     R, O = dy.shape
     I = x.shape[1]
-    dw = torch.empty(O, I, dtype=torch.float32, device=dy.device)
-    db = torch.empty(O, dtype=torch.float32, device=dy.device) if bias else None
+    accum = dw_out is not None
+    if accum and bias and db_out is None:
+        raise ValueError("accumulating dW needs the bias-gradient buffer too")
+    dw = dw_out if accum else torch.empty(O, I, dtype=torch.float32, device=dy.device)
+    db = (db_out if accum else torch.empty(O, dtype=torch.float32, device=dy.device)) if bias else None
     ws_bytes = int(_lib.load().x2g_linear_wgrad_workspace(R, O, I))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dy.device)
-    call("x2g_linear_wgrad", ptr(dy), ptr(x), R, O, I, ptr(dw), ptr(db), ptr(ws), ws_bytes, stream_ptr())
-    return dw, db
+    call("x2g_linear_wgrad_ex", ptr(dy), ptr(x), R, O, I, ptr(dw), ptr(db), ACCUM_WGRAD if accum else 0, ptr(ws),
+         ws_bytes, stream_ptr())
+    return (None, None) if accum else (dw, db)
 
 
 ACT_NONE, ACT_SILU = 0, 1
@@ -259,6 +287,7 @@ class _DenseFn(torch.autograd.Function):
         call("x2g_dense_fwd", ptr(x2), ptr(w), ptr(b), R, K, N, act, ptr(r2), ptr(y), ptr(z), stream_ptr())
         ctx.save_for_backward(x2, w, z)
         ctx.act, ctx.has_bias, ctx.has_res, ctx.lead = act, bias is not None, res is not None, lead
+        ctx.w_param, ctx.b_param = weight, bias
         return y.view(*lead, N)
 
     @staticmethod
@@ -270,14 +299,22 @@ class _DenseFn(torch.autograd.Function):
         dev = gy.device
         need_x = ctx.needs_input_grad[0]
         dx = torch.empty(R, K, dtype=torch.float32, device=dev) if (need_x or ctx.act != ACT_NONE) else None
-        dw = torch.empty(N, K, dtype=torch.float32, device=dev)
-        db = torch.empty(N, dtype=torch.float32, device=dev) if ctx.has_bias else None
+        gw = grad_sink(ctx.w_param)
+        gb = grad_sink(ctx.b_param) if ctx.has_bias else None
+        accum = gw is not None and (gb is not None or not ctx.has_bias)
+        if accum:  # summed straight into the flat gradient bucket; autograd gets None
+            dw, db = gw, gb
+        else:
+            dw = torch.empty(N, K, dtype=torch.float32, device=dev)
+            db = torch.empty(N, dtype=torch.float32, device=dev) if ctx.has_bias else None
         ws_bytes = int(_lib.load().x2g_dense_bwd_workspace(R, K, N))
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-        call("x2g_dense_bwd", ptr(gy2), ptr(z), ctx.act, ptr(x2), ptr(w), R, K, N, ptr(dx), ptr(dw), ptr(db), ptr(ws),
-             ws_bytes, stream_ptr())
+        call("x2g_dense_bwd_ex", ptr(gy2), ptr(z), ctx.act, ptr(x2), ptr(w), R, K, N, ptr(dx), None, ptr(dw),
+             ptr(db), ACCUM_WGRAD if accum else 0, ptr(ws), ws_bytes, stream_ptr())
         dres = gy if ctx.has_res else None
         dx = dx.view(*ctx.lead, K) if need_x else None
+        if accum:
+            return dx, None, None, dres, None
         return dx, dw, db, dres, None
 
 
