@@ -32,12 +32,13 @@ from x2gnn import ops  # noqa: E402
 from x2gnn._lib import call, ptr, stream_ptr  # noqa: E402
 from x2gnn.data import collate  # noqa: E402
 from x2gnn.dist import GradBucket  # noqa: E402
+from x2gnn.optim import FlatAdam  # noqa: E402
 from x2gnn.synth import synthetic_molecules  # noqa: E402
 
 CFG = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embedding_size=128)  # config.json
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32) peak, MI355X_MICROARCH.md
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")  # scripts/pmc_traffic.py output
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r1_pmc_traffic_v2.json")  # scripts/pmc_traffic.py output
 METRIC = "molecules/sec (fwd+bwd) on QM9 U0, batch=128, 1/2/4/8 MI355X"
 
 
@@ -66,11 +67,9 @@ class Trainer:
     def __init__(self, model, lr=1e-3, max_norm=100.0, ema_decay=0.95):
         self.model = model
         self.bucket = GradBucket(model.parameters())
-        self.opt = torch.optim.Adam(model.parameters(), lr=lr, foreach=True, capturable=True)
-        self.max_norm = max_norm
-        self.ema = [p.detach().clone() for p in model.parameters()]
-        self.ema_decay = ema_decay
-        self.params = list(model.parameters())
+        # clip_grad_norm_(100) + Adam(1e-3) + EMA(0.95) (config.json) in three launches over the
+        # flat parameter / gradient buffers (x2gnn.optim.FlatAdam, csrc/optim.hip)
+        self.opt = FlatAdam(model.parameters(), lr=lr, max_norm=max_norm, ema_decay=ema_decay, bucket=self.bucket)
         self.graphs = None
         self.loss = None
 
@@ -82,10 +81,7 @@ class Trainer:
         return loss
 
     def _update(self):
-        torch.nn.utils.clip_grad_norm_(self.params, self.max_norm, foreach=True)
         self.opt.step()
-        with torch.no_grad():  # AveragedModel(avg_fn = d*avg + (1-d)*p), train_ema.py:45-47
-            torch._foreach_lerp_(self.ema, self.params, 1.0 - self.ema_decay)
 
     def step(self, batch):
         if self.graphs is None:
@@ -338,8 +334,10 @@ def main():
     # committed profile (profiles/r1_v2_bench_kernel_stats.csv: dense_bwd_persist 1.9 ms/step)
     dbw_ms, dbw_flops = dense["dense_bwd"]
     dbw_tfs = dbw_flops / (dbw_ms * 1e-3) / 1e12
-    grid = str(256 * 512 if (shape["E"] + 63) // 64 >= 256 else ((shape["E"] + 63) // 64) * 512)
-    traffic = pmc_traffic([("void x2g::dense_bwd_persist<64>", grid), ("x2g::sum_slabs2", str(258 * 256))])
+    ntiles = (shape["E"] + 63) // 64  # dense.hip bwd_grid(): fewest workgroups at ceil(tiles/256) tiles each
+    per = (ntiles + 255) // 256
+    grid = str(((ntiles + per - 1) // per) * 512)
+    traffic = pmc_traffic([("x2g::dense_bwd_v5", grid), ("x2g::sum_slabs2", str(258 * 256))])
 
     if rank == 0:
         line = {
@@ -362,7 +360,7 @@ def main():
                        "per_gpu_batch": args.batch, "global_batch": world * args.batch,
                        "line_nodes_per_gpu": shape["E"], "triplets_per_gpu": shape["T"],
                        "parallelism": f"dp{world}", "hip_graph": graphed},
-            "roofline": {"kernel": "x2g_dense_bwd [E,128]x[128,128] SiLU (dense_bwd_persist<64> + sum_slabs2)",
+            "roofline": {"kernel": "x2g_dense_bwd [E,128]x[128,128] SiLU (dense_bwd_v5 + sum_slabs2)",
                          "bound": "mfma", "achieved": round(dbw_tfs, 2), "peak": MFMA_F32_PEAK_TFS,
                          "unit": "TFLOP/s", "frac": round(dbw_tfs / MFMA_F32_PEAK_TFS, 4), "traffic": traffic,
                          "avg_ms": round(dbw_ms, 5), "flops_per_launch": int(dbw_flops),

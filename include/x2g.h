@@ -207,6 +207,33 @@ int x2g_dense_bwd_ex(const float* dy, const float* z, int act, const float* x, c
                      int32_t in_features, int32_t out_features, float* dx, const float* dx_add, float* dw,
                      float* db, int flags, void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------- parameter update */
+
+/* float[16] device scalar block of x2g_clip_adam_ema: the caller sets the hyper-parameters,
+ * the library maintains the rest (so a captured HIP graph replays correct steps). */
+#define X2G_OPT_LR 0
+#define X2G_OPT_BETA1 1
+#define X2G_OPT_BETA2 2
+#define X2G_OPT_EPS 3
+#define X2G_OPT_MAX_NORM 4  /* <= 0: no clipping */
+#define X2G_OPT_EMA_DECAY 5
+#define X2G_OPT_STEP 6      /* steps taken (float); incremented by every call */
+#define X2G_OPT_NORM 7      /* out: total gradient 2-norm before clipping */
+#define X2G_OPT_CLIP 8      /* out: clip coefficient applied */
+#define X2G_OPT_STEP_SIZE 9 /* internal: lr / (1 - beta1^t) */
+#define X2G_OPT_BC2_SQRT 10 /* internal: sqrt(1 - beta2^t) */
+
+/* Workspace bytes for x2g_clip_adam_ema. */
+size_t x2g_optimizer_workspace(int64_t n);
+
+/* The reference trainer's update (trainer.py:43-48, train_ema.py:45-48) over one flat fp32
+ * parameter buffer of n elements: clip_grad_norm_(max_norm) (coef = max_norm/(norm+1e-6),
+ * clamped to 1), torch.optim.Adam (amsgrad=False, no weight decay), then the EMA
+ * ema = d*ema + (1-d)*p (ema may be NULL).  grads must be 16-byte aligned; the gradient
+ * buffer is read, not modified.  Deterministic (fixed-order norm reduction). */
+int x2g_clip_adam_ema(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* ema,
+                      int64_t n, float* scalars, void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -319,7 +319,7 @@ def test_conv_small_width_vs_oracle(cuda):
 
 # ------------------------------------------------------------------------------ dense layers
 @pytest.mark.parametrize("R,O,I", [(21058, 128, 128), (194060, 128, 42), (1000, 256, 338), (77, 1, 128),
-                                   (5, 128, 6), (130, 128, 10), (0, 128, 128)])
+                                   (5, 128, 6), (130, 128, 10), (0, 128, 128), (1001, 42, 128), (333, 6, 7)])
 def test_linear_wgrad_vs_fp64(cuda, R, O, I):
     from x2gnn import ops
 
@@ -419,3 +419,39 @@ def test_dense_bwd_ex_dx_add_and_accumulate(cuda, R, K, N, act):
     assert torch.equal(dx1, dx0 + add) and torch.equal(dx2, dx0 + add)
     assert torch.equal(dw1, dw0 + 0.5) and torch.equal(db1, db0 - 0.25)
     assert torch.equal(dw2, dw0) and torch.equal(db2, db0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_norm", [100.0, 0.05])
+def test_flat_adam_matches_torch(cuda, max_norm):
+    """x2g_clip_adam_ema (FlatAdam) vs torch clip_grad_norm_ + Adam + AveragedModel-style EMA,
+    three steps, clipping inactive (100) and active (0.05)."""
+    from x2gnn.dist import GradBucket
+    from x2gnn.optim import FlatAdam
+
+    g = torch.Generator(device=cuda).manual_seed(11)
+    shapes = [(128, 128), (128,), (6, 128), (1,), (42, 3)]
+    ref = [torch.randn(s, device=cuda, generator=g).requires_grad_(True) for s in shapes]
+    mine = [r.detach().clone().requires_grad_(True) for r in ref]
+    opt_ref = torch.optim.Adam(ref, lr=1e-3)
+    ema_ref = [r.detach().clone() for r in ref]
+    bucket = GradBucket(mine)
+    opt = FlatAdam(mine, lr=1e-3, max_norm=max_norm, ema_decay=0.95, bucket=bucket)
+    for step in range(3):
+        grads = [torch.randn(s, device=cuda, generator=g) for s in shapes]
+        for r, gr in zip(ref, grads):
+            r.grad = gr.clone()
+        torch.nn.utils.clip_grad_norm_(ref, max_norm)
+        opt_ref.step()
+        with torch.no_grad():
+            for e, r in zip(ema_ref, ref):
+                e.lerp_(r, 0.05)
+        bucket.zero()
+        for m, gr in zip(mine, grads):
+            m.grad.copy_(gr)
+        opt.step()
+        for r, m in zip(ref, mine):
+            torch.testing.assert_close(m.detach(), r.detach(), rtol=2e-6, atol=2e-7)
+        for e, m in zip(ema_ref, opt.ema_params()):
+            torch.testing.assert_close(m, e, rtol=2e-6, atol=2e-7)
+    assert float(opt.steps) == 3.0

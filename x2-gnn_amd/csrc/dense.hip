@@ -506,7 +506,7 @@ __global__ void __launch_bounds__(512) dense_fwd_v5(const float* __restrict__ X,
   const int64_t npairs = (R + 63) / 64;
   const int64_t G = gridDim.x;
   f4 b4 = {0.f, 0.f, 0.f, 0.f};
-  if (bias && 4 * q < N) b4 = *reinterpret_cast<const f4*>(bias + 4 * q);
+  if (bias && 4 * q < N) b4 = f4{bias[4 * q], bias[4 * q + 1], bias[4 * q + 2], bias[4 * q + 3]};  // any alignment
   int64_t tp = blockIdx.x;
   Stage4 stage;
   {
@@ -900,7 +900,7 @@ X2G_API int x2g_dense_fwd(const float* x, const float* w, const float* b, int64_
     const bool vec = K % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0;
     if (K <= 8)
       dense_fwd_persist<4, false><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
-    else if (vec && variant == 0 && N % 4 == 0 && aligned16(y) && aligned16(z) && aligned16(res) && aligned16(b))
+    else if (vec && variant == 0 && N % 4 == 0 && aligned16(y) && aligned16(z) && aligned16(res))
       dense_fwd_v5<<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
     else if (vec && variant == 0)
       switch (tuning(kTuneDenseDbg)) {
@@ -948,6 +948,15 @@ X2G_API size_t x2g_linear_wgrad_workspace(int64_t R, int32_t O, int32_t I);
 X2G_API int x2g_linear_wgrad(const float* dy, const float* x, int64_t R, int32_t O, int32_t I, float* dw, float* db,
                              void* workspace, size_t workspace_bytes, void* stream);
 
+// Backward grid: the fewest workgroups that keep the busiest one at ceil(tiles / 256) tiles —
+// every workgroup writes a full weight-gradient slab, so idle-making extra workgroups would only
+// add slab traffic (330 tiles at config 2: 165 workgroups x 2 tiles instead of 256).
+static inline int64_t bwd_grid(int64_t R) {
+  const int64_t ntiles = (R + kBTile - 1) / kBTile;
+  const int64_t per = (ntiles + kPBwdGrid - 1) / kPBwdGrid;
+  return (ntiles + per - 1) / per;
+}
+
 static inline bool dense_persistent_bwd(int64_t R, int32_t K, int32_t N) {
   return K <= 128 && N <= 128 && R > 0 && R * 128 < (int64_t(1) << 31);  // 32-bit offsets inside
 }
@@ -955,8 +964,7 @@ static inline bool dense_persistent_bwd(int64_t R, int32_t K, int32_t N) {
 X2G_API size_t x2g_dense_bwd_workspace(int64_t R, int32_t K, int32_t N) {
   if (R <= 0 || K <= 0 || N <= 0) return 0;
   if (dense_persistent_bwd(R, K, N)) {
-    const int64_t ntiles = (R + kBTile - 1) / kBTile;
-    const int64_t g = ntiles < kPBwdGrid ? ntiles : kPBwdGrid;
+    const int64_t g = bwd_grid(R);
     return static_cast<size_t>(g) * (static_cast<int64_t>(N) * K + N) * sizeof(float);
   }
   // general path: dz [R, N] + the row-split weight-gradient slabs
@@ -984,8 +992,7 @@ X2G_API int x2g_dense_bwd_ex(const float* dy, const float* z, int act, const flo
   if (!dy || !x || !w || (act == kActSilu && !z)) return X2G_EINVAL;
   if (!workspace || workspace_bytes < x2g_dense_bwd_workspace(R, K, N)) return X2G_EWORKSPACE;
   if (dense_persistent_bwd(R, K, N)) {
-    const int64_t ntiles = (R + kBTile - 1) / kBTile;
-    const int grid = static_cast<int>(ntiles < kPBwdGrid ? ntiles : kPBwdGrid);
+    const int grid = static_cast<int>(bwd_grid(R));
     float* part_w = static_cast<float*>(workspace);
     float* part_b = db ? part_w + static_cast<int64_t>(grid) * N * K : nullptr;
     const bool v5 = tuning(kTuneDenseBwd) == 0 && K % 4 == 0 && N % 4 == 0 && N > 8 && aligned16(dy) &&

@@ -19,18 +19,37 @@ constexpr int kWgChunk = 32;       // rows staged in LDS per iteration
 constexpr int kWgMaxSplits = 160;  // row splits (workgroups per output block)
 constexpr int kLdsStride = kWgTile + 4;  // keeps 16-byte row alignment for the float4 stores
 
-// Chunk of 32 rows x 128 columns of one operand, held in registers between global and LDS:
-// VEC = 4 float4 per thread (columns a multiple of 4), else 16 scalars per thread.
-template <bool VEC>
+// Chunk of 32 rows x 128 columns of one operand, held in registers between global and LDS.
+// Load modes: kScalar = 16 scalars per thread; kVec = 4 float4 per thread (columns a multiple of
+// 4); kFlat = the chunk's 32 full rows are one contiguous span of 32*cols floats (cols <= 128),
+// read as float4 whatever cols is (32*cols is a multiple of 4 and the span starts 16-byte
+// aligned): lin_sbf's 42-wide sbf rows take this path.
+enum { kScalar = 0, kVec = 1, kFlat = 2 };
+
+template <int MODE>
 struct ChunkRegs {
   float v[16];
 };
 
-template <bool VEC>
+template <int MODE>
 __device__ __forceinline__ void load_chunk(const float* __restrict__ m, int cols, int c0, int64_t r0,
-                                           int64_t r_end, ChunkRegs<VEC>& reg) {
+                                           int64_t r_end, ChunkRegs<MODE>& reg) {
   const int tid = threadIdx.x;
-  if (VEC) {
+  if (MODE == kFlat) {
+    const int64_t nval = (r_end - r0 < kWgChunk ? r_end - r0 : kWgChunk) * cols;  // valid floats
+    const int nq = (kWgChunk * cols) >> 2;
+    const float* base = m + r0 * cols;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int qi = tid + 256 * u;
+      const bool ok = qi < nq && 4 * qi < nval;
+      const float4 f = ld_pin4(base + (ok ? 4 * qi : 0));
+      reg.v[4 * u] = keep(f.x, ok && 4 * qi < nval);
+      reg.v[4 * u + 1] = keep(f.y, ok && 4 * qi + 1 < nval);
+      reg.v[4 * u + 2] = keep(f.z, ok && 4 * qi + 2 < nval);
+      reg.v[4 * u + 3] = keep(f.w, ok && 4 * qi + 3 < nval);
+    }
+  } else if (MODE == kVec) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int q = tid + 256 * u, rr = q >> 5, c = c0 + 4 * (q & 31);
@@ -54,10 +73,26 @@ __device__ __forceinline__ void load_chunk(const float* __restrict__ m, int cols
   }
 }
 
-template <bool VEC>
-__device__ __forceinline__ void store_chunk(float (*lds)[kLdsStride], const ChunkRegs<VEC>& reg) {
+template <int MODE>
+__device__ __forceinline__ void store_chunk(float (*lds)[kLdsStride], const ChunkRegs<MODE>& reg, int cols) {
   const int tid = threadIdx.x;
-  if (VEC) {
+  if (MODE == kFlat) {
+    const int nq = (kWgChunk * cols) >> 2;
+    const unsigned magic = 0xFFFFFFFFu / static_cast<unsigned>(cols) + 1u;  // wraps to 0 for cols == 1
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int qi = tid + 256 * u;
+      if (qi < nq) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {  // f / cols by a multiply-high (exact for f < 2^16)
+          const unsigned f = 4 * qi + e, rr = cols == 1 ? f : __umulhi(f, magic), c = f - rr * cols;
+          lds[rr][c] = reg.v[4 * u + e];
+        }
+      }
+    }
+    // columns cols..127 of the chunk stay as they are: they only meet output columns >= cols,
+    // which are never written back
+  } else if (MODE == kVec) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int q = tid + 256 * u;
@@ -75,7 +110,7 @@ __device__ __forceinline__ void store_chunk(float (*lds)[kLdsStride], const Chun
 
 // One workgroup = one 128x128 output block x one row slice.  The next 32-row chunk is loaded
 // into registers while the MFMAs consume the current one from LDS.
-template <bool VEC>
+template <int MA, int MB>
 __global__ void __launch_bounds__(256) wgrad_partial(const float* __restrict__ dy, const float* __restrict__ x,
                                                      int64_t R, int O, int I, int tiles_i, int64_t rows_per_split,
                                                      float* __restrict__ part, float* __restrict__ part_b) {
@@ -88,22 +123,24 @@ __global__ void __launch_bounds__(256) wgrad_partial(const float* __restrict__ d
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int o0 = ob * kWgTile, i0 = ib * kWgTile;
   const bool do_bias = part_b && ib == 0;
+  const int nt = uniform((I - i0 + 31) / 32 < 4 ? (I - i0 + 31) / 32 : 4);  // live 32-wide column blocks
   floatx16 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[t][j] = 0.f;
   float bsum = 0.f;
-  ChunkRegs<VEC> ra, rb;
-  load_chunk<VEC>(dy, O, o0, r_begin, r_end, ra);
-  load_chunk<VEC>(x, I, i0, r_begin, r_end, rb);
+  ChunkRegs<MA> ra;
+  ChunkRegs<MB> rb;
+  load_chunk<MA>(dy, O, o0, r_begin, r_end, ra);
+  load_chunk<MB>(x, I, i0, r_begin, r_end, rb);
   for (int64_t r0 = r_begin; r0 < r_end; r0 += kWgChunk) {
-    store_chunk<VEC>(As, ra);
-    store_chunk<VEC>(Bs, rb);
+    store_chunk<MA>(As, ra, O);
+    store_chunk<MB>(Bs, rb, I);
     __syncthreads();
     if (r0 + kWgChunk < r_end) {  // prefetch the next chunk; it lands while the MFMAs run
-      load_chunk<VEC>(dy, O, o0, r0 + kWgChunk, r_end, ra);
-      load_chunk<VEC>(x, I, i0, r0 + kWgChunk, r_end, rb);
+      load_chunk<MA>(dy, O, o0, r0 + kWgChunk, r_end, ra);
+      load_chunk<MB>(x, I, i0, r0 + kWgChunk, r_end, rb);
     }
 #pragma unroll 4
     for (int ks = 0; ks < kWgChunk / 2; ++ks) {
@@ -111,8 +148,10 @@ __global__ void __launch_bounds__(256) wgrad_partial(const float* __restrict__ d
       const float a = As[kr][wave * 32 + (lane & 31)];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const float b = Bs[kr][t * 32 + (lane & 31)];
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[t], 0, 0, 0);
+        if (t < nt) {  // column blocks past I (e.g. lin_sbf's 42 columns: 2 of 4) are skipped
+          const float b = Bs[kr][t * 32 + (lane & 31)];
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[t], 0, 0, 0);
+        }
       }
     }
     if (do_bias && tid < kWgTile) {
@@ -225,12 +264,20 @@ X2G_API int x2g_linear_wgrad_ex(const float* dy, const float* x, int64_t R, int3
   float* part_b = db ? part + static_cast<int64_t>(splits) * O * I : nullptr;
   const int tiles_o = (O + kWgTile - 1) / kWgTile, tiles_i = (I + kWgTile - 1) / kWgTile;
   dim3 grid(tiles_o * tiles_i, splits);
-  const bool vec = (O % 4 == 0) && (I % 4 == 0) && (reinterpret_cast<uintptr_t>(dy) % 16 == 0) &&
-                   (reinterpret_cast<uintptr_t>(x) % 16 == 0);
-  if (vec)
-    wgrad_partial<true><<<grid, 256, 0, st>>>(dy, x, R, O, I, tiles_i, wgrad_rows_per_split(R), part, part_b);
-  else
-    wgrad_partial<false><<<grid, 256, 0, st>>>(dy, x, R, O, I, tiles_i, wgrad_rows_per_split(R), part, part_b);
+  auto mode = [](int cols, const float* p) {
+    if (reinterpret_cast<uintptr_t>(p) % 16 != 0) return static_cast<int>(kScalar);
+    if (cols % 4 == 0) return static_cast<int>(kVec);
+    return cols <= kWgTile ? static_cast<int>(kFlat) : static_cast<int>(kScalar);
+  };
+  const int ma = mode(O, dy), mb = mode(I, x);
+  const int64_t rps = wgrad_rows_per_split(R);
+#define X2G_WGRAD(A, B) wgrad_partial<A, B><<<grid, 256, 0, st>>>(dy, x, R, O, I, tiles_i, rps, part, part_b)
+  if (ma == kVec && mb == kVec) X2G_WGRAD(kVec, kVec);
+  else if (ma == kVec && mb == kFlat) X2G_WGRAD(kVec, kFlat);
+  else if (ma == kFlat && mb == kVec) X2G_WGRAD(kFlat, kVec);
+  else if (ma == kFlat && mb == kFlat) X2G_WGRAD(kFlat, kFlat);
+  else X2G_WGRAD(kScalar, kScalar);
+#undef X2G_WGRAD
   int rc = last_launch_status();
   if (rc) return rc;
   return sum_slabs_launch(part, static_cast<int64_t>(O) * I, part_b, O, splits, dw, db, accum, st);

@@ -1,0 +1,121 @@
+// The reference trainer's parameter update (trainer.py:39-48, train_ema.py:45-48) over ONE flat
+// fp32 parameter buffer: clip_grad_norm_(max_norm) -> Adam(amsgrad=False) -> EMA
+// (AveragedModel with avg_fn = d*avg + (1-d)*p).  torch's capturable Adam issues a few kernels
+// per parameter tensor (~300 launches for X2-GNN's 155 tensors); here it is three launches:
+//   1. per-block partial sums of g^2 over contiguous chunks (fixed order),
+//   2. one block: total norm, clip coefficient, step count + bias corrections -> scalars,
+//   3. elementwise Adam + EMA.
+// Every value the update depends on that changes between steps (step count, norm, clip scale)
+// lives in device memory, so a captured HIP graph replays correctly; the hyper-parameters
+// (lr, betas, eps, max_norm, ema decay) are read from the same device scalar block so a
+// scheduler may rewrite them between replays.
+#include <math.h>
+
+#include "common.hpp"
+
+namespace x2g {
+
+constexpr int kNormBlocks = 1024;
+constexpr int kNormThreads = 256;
+
+// scalars layout (float[16]); see x2g.h X2G_OPT_*
+__global__ void __launch_bounds__(kNormThreads) grad_sq_partial(const float4* __restrict__ g4,
+                                                                const float* __restrict__ g, int64_t n,
+                                                                float* __restrict__ partial) {
+  __shared__ float red[kNormThreads];
+  const int64_t n4 = n >> 2;
+  const int64_t per = (n4 + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = per * blockIdx.x, hi = lo + per < n4 ? lo + per : n4;
+  float s = 0.f;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kNormThreads) {
+    const float4 v = g4[i];
+    s = fmaf(v.x, v.x, s);
+    s = fmaf(v.y, v.y, s);
+    s = fmaf(v.z, v.z, s);
+    s = fmaf(v.w, v.w, s);
+  }
+  if (blockIdx.x == 0)  // the n % 4 tail
+    for (int64_t i = 4 * n4 + threadIdx.x; i < n; i += kNormThreads) s = fmaf(g[i], g[i], s);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = kNormThreads / 2; off > 0; off >>= 1) {
+    if (static_cast<int>(threadIdx.x) < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(kNormThreads) opt_finalize(const float* __restrict__ partial, int nparts,
+                                                             float* __restrict__ sc) {
+  __shared__ float red[kNormThreads];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += kNormThreads) s += partial[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = kNormThreads / 2; off > 0; off >>= 1) {
+    if (static_cast<int>(threadIdx.x) < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float norm = sqrtf(red[0]);
+    const float max_norm = sc[X2G_OPT_MAX_NORM];
+    // torch.nn.utils.clip_grad_norm_: coef = max_norm / (norm + 1e-6), clamped to <= 1
+    const float coef = max_norm > 0.f ? fminf(max_norm / (norm + 1e-6f), 1.0f) : 1.0f;
+    const float step = sc[X2G_OPT_STEP] + 1.0f;
+    sc[X2G_OPT_STEP] = step;
+    sc[X2G_OPT_NORM] = norm;
+    sc[X2G_OPT_CLIP] = coef;
+    // bias corrections as torch.optim.Adam computes them (in double, rounded to float)
+    const double b1 = sc[X2G_OPT_BETA1], b2 = sc[X2G_OPT_BETA2];
+    const double bc1 = 1.0 - pow(b1, static_cast<double>(step));
+    const double bc2 = 1.0 - pow(b2, static_cast<double>(step));
+    sc[X2G_OPT_STEP_SIZE] = static_cast<float>(sc[X2G_OPT_LR] / bc1);
+    sc[X2G_OPT_BC2_SQRT] = static_cast<float>(sqrt(bc2));
+  }
+}
+
+__global__ void __launch_bounds__(256) adam_ema(float* __restrict__ p, const float* __restrict__ g,
+                                                float* __restrict__ m, float* __restrict__ v,
+                                                float* __restrict__ ema, int64_t n, const float* __restrict__ sc) {
+  const float clip = sc[X2G_OPT_CLIP], b1 = sc[X2G_OPT_BETA1], b2 = sc[X2G_OPT_BETA2];
+  const float eps = sc[X2G_OPT_EPS], step_size = sc[X2G_OPT_STEP_SIZE], bc2s = sc[X2G_OPT_BC2_SQRT];
+  const float d = sc[X2G_OPT_EMA_DECAY];
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float gi = g[i] * clip;
+    // exp_avg.lerp_(grad, 1 - beta1); exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
+    const float mi = m[i] + (1.0f - b1) * (gi - m[i]);
+    const float vi = v[i] * b2 + (1.0f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    // param.addcdiv_(exp_avg, sqrt(exp_avg_sq) / sqrt(bc2) + eps, value=-lr/bc1)
+    const float denom = sqrtf(vi) / bc2s + eps;
+    const float pi = p[i] - step_size * (mi / denom);
+    p[i] = pi;
+    // ema.lerp_(p, 1 - d)
+    if (ema) ema[i] = ema[i] + (1.0f - d) * (pi - ema[i]);
+  }
+}
+
+}  // namespace x2g
+
+using namespace x2g;
+
+X2G_API size_t x2g_optimizer_workspace(int64_t n) { return n > 0 ? kNormBlocks * sizeof(float) : 0; }
+
+X2G_API int x2g_clip_adam_ema(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* ema,
+                              int64_t n, float* scalars, void* workspace, size_t workspace_bytes, void* stream) {
+  if (n < 0 || !scalars) return X2G_EINVAL;
+  if (n == 0) return X2G_OK;
+  if (!params || !grads || !exp_avg || !exp_avg_sq) return X2G_EINVAL;
+  if (!workspace || workspace_bytes < x2g_optimizer_workspace(n)) return X2G_EWORKSPACE;
+  if (reinterpret_cast<uintptr_t>(grads) % 16) return X2G_EINVAL;
+  hipStream_t st = as_stream(stream);
+  float* partial = static_cast<float*>(workspace);
+  grad_sq_partial<<<kNormBlocks, kNormThreads, 0, st>>>(reinterpret_cast<const float4*>(grads), grads, n, partial);
+  opt_finalize<<<1, kNormThreads, 0, st>>>(partial, kNormBlocks, scalars);
+  const int64_t want = (n + 255) / 256;
+  adam_ema<<<static_cast<unsigned>(want < 4096 ? want : 4096), 256, 0, st>>>(params, grads, exp_avg, exp_avg_sq, ema,
+                                                                              n, scalars);
+  return last_launch_status();
+}

@@ -27,22 +27,31 @@ def shard_by_triplets(triplet_counts, world: int):
     return [np.nonzero(owner == r)[0] for r in range(world)]
 
 
+def flat_layout(params, align=4):
+    """Offsets of each parameter in a flat fp32 buffer, each rounded up to ``align`` floats
+    (16 bytes) so views of the buffer keep the alignment the vectorised kernels want; returns
+    (offsets, total)."""
+    offs, off = [], 0
+    for p in params:
+        offs.append(off)
+        off += (p.numel() + align - 1) // align * align
+    return offs, off
+
+
 class GradBucket:
     """All parameters' gradients as views of ONE flat buffer, so the per-step exchange is a
     single all-reduce (ring over xGMI) with no pack/unpack copies."""
 
     def __init__(self, params):
         self.params = [p for p in params if p.requires_grad]
-        n = sum(p.numel() for p in self.params)
+        self.offsets, n = flat_layout(self.params)
         dev = self.params[0].device
-        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
-        off = 0
-        for p in self.params:
+        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)  # padding stays zero
+        for p, off in zip(self.params, self.offsets):
             p.grad = self.flat[off:off + p.numel()].view_as(p)
             # the fused dense / attention backwards may sum weight gradients straight into this
             # buffer (ops.grad_sink) instead of returning them for autograd to add
             p._x2g_grad_sink = True
-            off += p.numel()
 
     def zero(self):
         self.flat.zero_()
