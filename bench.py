@@ -137,29 +137,37 @@ def attention_probe(model, batch, reps):
     src_rowptr, src_perm = lg.src_csr()
     S = sbf.shape[1]
 
+    sproj = torch.empty(T, D, **f32)
+
+    def proj():
+        call("x2g_sbf_project", ptr(sbf), T, S, ptr(W), ptr(bsb), D, ptr(sproj), stream_ptr())
+
+    proj()  # the model's path: S = lin_sbf(sbf) once per layer, kernels read S rows (weight NULL)
+
     def fwd():
         call("x2g_sbf_attention_fwd", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(row), ops.EDGE_PER_DST,
-             ptr(sbf), ptr(W), ptr(bsb), ptr(lg.trip_rowptr), ptr(lg.trip_src), E, T, H, C, S, ptr(out),
-             ptr(alpha), ptr(smax), ptr(sden), stream_ptr())
+             ptr(sproj), None, None, ptr(lg.trip_rowptr), ptr(lg.trip_src), E, T, H, C, D, ptr(out), ptr(alpha),
+             ptr(smax), ptr(sden), stream_ptr())
 
     def bwd_dst():
-        call("x2g_sbf_attention_bwd_dst", ptr(q), ptr(k), ptr(v), ptr(table), ptr(row), ops.EDGE_PER_DST, ptr(sbf),
-             ptr(W), ptr(bsb), ptr(lg.trip_rowptr), ptr(lg.trip_src), ptr(alpha), ptr(smax), ptr(sden), ptr(dout),
-             E, T, H, C, S, ptr(dq), ptr(dedge), ptr(dlogit), ptr(dproj), stream_ptr())
+        call("x2g_sbf_attention_bwd_dst", ptr(q), ptr(k), ptr(v), ptr(table), ptr(row), ops.EDGE_PER_DST, ptr(sproj),
+             None, None, ptr(lg.trip_rowptr), ptr(lg.trip_src), ptr(alpha), ptr(smax), ptr(sden), ptr(dout), E, T, H,
+             C, D, ptr(dq), ptr(dedge), ptr(dlogit), ptr(dproj), stream_ptr())
 
     def bwd_src():
-        call("x2g_sbf_attention_bwd_src", ptr(q), ptr(sbf), ptr(W), ptr(bsb), ptr(src_rowptr), ptr(src_perm),
-             ptr(lg.trip_dst), ptr(alpha), ptr(smax), ptr(sden), ptr(dlogit), ptr(dout), E, T, H, C, S, ptr(dk),
+        call("x2g_sbf_attention_bwd_src", ptr(q), ptr(sproj), None, None, ptr(src_rowptr), ptr(src_perm),
+             ptr(lg.trip_dst), ptr(alpha), ptr(smax), ptr(sden), ptr(dlogit), ptr(dout), E, T, H, C, D, ptr(dk),
              ptr(dv), stream_ptr())
 
     row_b = 4 * D
     # algorithmic bytes per launch: every logical read/write once per use (gathered rows per triplet)
-    fwd_bytes = T * (4 + 2 * row_b + 4 * S + 4 * H) + E * (8 + 4 * row_b + 8 * H + 4)
-    dst_bytes = T * (4 + 2 * row_b + 4 * S + 4 * H * 3 + row_b) + E * (8 + 4 * row_b + 8 * H + 4)
-    src_bytes = T * (8 + 2 * row_b + 4 * S + 4 * H * 2 + 8 * H) + E * (8 + 2 * row_b)
+    proj_bytes = T * (4 * S + row_b)
+    fwd_bytes = T * (4 + 3 * row_b + 4 * H) + E * (8 + 4 * row_b + 8 * H + 4)
+    dst_bytes = T * (4 + 3 * row_b + 4 * H * 3 + row_b) + E * (8 + 4 * row_b + 8 * H + 4)
+    src_bytes = T * (8 + 3 * row_b + 4 * H * 2 + 8 * H) + E * (8 + 2 * row_b)
     res = {}
-    for name, fn, nbytes in (("attn_fwd", fwd, fwd_bytes), ("attn_bwd_dst", bwd_dst, dst_bytes),
-                             ("attn_bwd_src", bwd_src, src_bytes)):
+    for name, fn, nbytes in (("sbf_project", proj, proj_bytes), ("attn_fwd", fwd, fwd_bytes),
+                             ("attn_bwd_dst", bwd_dst, dst_bytes), ("attn_bwd_src", bwd_src, src_bytes)):
         res[name] = (_event_time(fn, reps), nbytes)
     return res, dict(E=E, T=T, D=D)
 

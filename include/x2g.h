@@ -90,6 +90,16 @@ int x2g_spherical_basis(const float* pos, const int32_t* atom_i, const int32_t* 
 
 /* ---------------------------------------------------------------- SBF-transformer attention */
 
+/* S[t, :] = w_sbf[out_dim, sbf_dim] sbf[t, :] + b_sbf: lin_sbf of sbftransformer_conv.py:148,
+ * materialised once per layer so the attention kernels read one row per triplet instead of
+ * re-projecting it.  out_dim in {32, 64, 128, 256}, sbf_dim 42. */
+int x2g_sbf_project(const float* sbf, int64_t num_triplets, int32_t sbf_dim, const float* w_sbf,
+                    const float* b_sbf, int32_t out_dim, float* sbfproj, void* stream);
+
+/* In the three attention entry points below, w_sbf == NULL (and b_sbf == NULL) means `sbf` is
+ * that precomputed projection S [T, heads*channels] and sbf_dim must equal heads*channels;
+ * otherwise `sbf` is the raw basis [T, 42] and the projection is computed per triplet. */
+
 /* Fused SBFTransformerConv.message + PyG softmax + 'add' aggregation + root skip
  * (sbftransformer_conv.py:109-127,138-162), CSR by destination:
  *   kk_t = k[src]+edge_t, u_t = v[src]+edge_t, alpha_t,h = <q[dst]_h, kk_t,h>/sqrt(C),

@@ -455,3 +455,39 @@ def test_flat_adam_matches_torch(cuda, max_norm):
         for e, m in zip(ema_ref, opt.ema_params()):
             torch.testing.assert_close(m, e, rtol=2e-6, atol=2e-7)
     assert float(opt.steps) == 3.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [194060, 1000, 37, 0])
+def test_sbf_project_both_paths_vs_torch(cuda, T):
+    """x2g_sbf_project: MFMA narrow-K path (default) and the VALU path (x2g_tuning key 2 = 1)."""
+    from x2gnn import _lib
+    from x2gnn._lib import call, ptr, stream_ptr
+
+    g = torch.Generator(device=cuda).manual_seed(T + 5)
+    sbf = torch.randn(T, 42, device=cuda, generator=g)
+    w = torch.randn(128, 42, device=cuda, generator=g) / 6.5
+    b = torch.randn(128, device=cuda, generator=g)
+    ref = (sbf.double() @ w.double().t() + b.double()).float()
+    lib = _lib.load()
+    for knob in (0, 1):
+        prev = lib.x2g_tuning(2, knob)
+        out = torch.full((T, 128), float("nan"), device=cuda)
+        call("x2g_sbf_project", ptr(sbf), T, 42, ptr(w), ptr(b), 128, ptr(out), stream_ptr())
+        lib.x2g_tuning(2, prev)
+        torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,K", [(5000, 42), (333, 10), (64, 42), (65, 126)])
+def test_dense_narrow_k_vs_torch(cuda, R, K):
+    from x2gnn import ops
+
+    g = torch.Generator(device=cuda).manual_seed(R + K)
+    x = torch.randn(R, K, device=cuda, generator=g)
+    w = torch.randn(128, K, device=cuda, generator=g) / np.sqrt(K)
+    b = torch.randn(128, device=cuda, generator=g)
+    res = torch.randn(R, 128, device=cuda, generator=g)
+    y = ops.dense(x, w, b, act=ops.ACT_SILU, res=res)
+    ref = torch.nn.functional.silu(x.double() @ w.double().t() + b.double()) + res.double()
+    torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=1e-5)

@@ -160,8 +160,91 @@ __device__ __forceinline__ void zero_row(float (&r)[CPL]) {
 // Every kernel below takes its pointers as __restrict__ parameters: with them the compiler may
 // serve wave-uniform reads (row pointers, triplet indices, the sbf row) from the scalar cache.
 
+// The sbf projection S_t = W sbf_t + b either comes precomputed (PRE: S[T, D] from
+// x2g_sbf_project, read as one coalesced row per triplet) or is computed on the fly from the
+// 42-float sbf row with W held in registers (84 VGPRs at CPL = 2).
+template <int CPL, bool PRE>
+struct Proj {
+  float wr[CPL][kS];
+  float br[CPL];
+  __device__ __forceinline__ void init(const float* __restrict__ w, const float* __restrict__ b, int c0, bool act) {
+    load_weights<CPL>(w, b, c0, act, wr, br);
+  }
+};
+
+template <int CPL>
+struct Proj<CPL, true> {
+  __device__ __forceinline__ void init(const float*, const float*, int, bool) {}
+};
+
+template <int CPL, bool PRE>
+__device__ __forceinline__ void proj_row(const Proj<CPL, PRE>& P, const float* __restrict__ sbf, int64_t t,
+                                         const float (&pre)[CPL], float (&sp)[CPL]) {
+  if constexpr (PRE) {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) sp[j] = pre[j];
+  } else {
+    sbf_project<CPL>(P.wr, P.br, sbf + t * kS, sp);
+  }
+}
+
+// Triplet loops keep three register sets in flight and rotate their ROLES by unrolling the loop
+// three times, never their contents: copying a set whose loads are still in flight would wait
+// for them (a v_mov of a pending VGPR), shrinking the prefetch distance to nothing.
+
 // ------------------------------------------------------------------------------ forward
-template <int CPL, int LPH, int MODE>
+template <int CPL>
+struct FwdSet {
+  float k[CPL], v[CPL], s[CPL];
+};
+
+template <int CPL, bool PRE>
+__device__ __forceinline__ void fwd_load(FwdSet<CPL>& S, const float* __restrict__ k, const float* __restrict__ v,
+                                         const float* __restrict__ sbf, const int32_t* __restrict__ tsrc, int t,
+                                         int D, int c0, bool act) {
+  const int64_t src = uniform(tsrc[t]);
+  load_row<CPL>(k + src * D + c0, act, S.k);
+  load_row<CPL>(v + src * D + c0, act, S.v);
+  if (PRE) load_row<CPL>(sbf + static_cast<int64_t>(t) * D + c0, act, S.s);
+}
+
+template <int CPL>
+struct FwdState {
+  float qv[CPL], ed[CPL], acc[CPL];
+  float m, den;
+};
+
+template <int CPL, int LPH, int MODE, bool PRE>
+__device__ __forceinline__ void fwd_step(FwdSet<CPL>& S, int t, int t1, FwdState<CPL>& st, const Proj<CPL, PRE>& P,
+                                         const float* __restrict__ k, const float* __restrict__ v,
+                                         const float* __restrict__ edge, const float* __restrict__ sbf,
+                                         const int32_t* __restrict__ tsrc, int D, int H, int c0, int head, bool act,
+                                         bool leader, float sqrt_c, float* __restrict__ alpha_out) {
+  float et[CPL];
+  if (MODE == X2G_EDGE_PER_TRIPLET) {
+    load_row<CPL>(edge + static_cast<int64_t>(t) * D + c0, act, et);
+  } else {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) et[j] = st.ed[j];
+  }
+  float dot = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) dot = fmaf(st.qv[j], S.k[j] + et[j], dot);
+  const float logit = group_sum<LPH>(dot) / sqrt_c;
+  float sp[CPL];
+  proj_row<CPL, PRE>(P, sbf, t, S.s, sp);
+  const float m_new = fmaxf(st.m, logit);
+  const float corr = expf(st.m - m_new);
+  const float p = expf(logit - m_new);
+  st.den = st.den * corr + p;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) st.acc[j] = st.acc[j] * corr + p * ((S.v[j] + et[j]) * sp[j]);
+  st.m = m_new;
+  if (leader) alpha_out[static_cast<int64_t>(t) * H + head] = logit;
+  if (t + 3 < t1) fwd_load<CPL, PRE>(S, k, v, sbf, tsrc, t + 3, D, c0, act);  // this set's next triplet
+}
+
+template <int CPL, int LPH, int MODE, bool PRE>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
     const float* __restrict__ skip, const float* __restrict__ edge, const int32_t* __restrict__ edge_row,
@@ -174,84 +257,173 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(
   const int c0 = act ? lane * CPL : 0;
   const int head = lane / LPH;
   const bool leader = act && (lane % LPH) == 0;
-  float wr[CPL][kS], br[CPL];
-  load_weights<CPL>(w, b, c0, act, wr, br);
+  Proj<CPL, PRE> P;
+  P.init(w, b, c0, act);
   const WaveRange wr_ = xcd_wave_range(E);
   for (int64_t e = wr_.first; e < wr_.end; e += wr_.stride) {
     const int t0 = uniform(rowptr[e]), t1 = uniform(rowptr[e + 1]);
-    float qv[CPL], ed[CPL], acc[CPL];
-    load_row<CPL>(q + e * D + c0, act, qv);
+    FwdState<CPL> st;
+    load_row<CPL>(q + e * D + c0, act, st.qv);
     if (MODE == X2G_EDGE_PER_DST) {
       const int64_t r = edge_row ? uniform(edge_row[e]) : e;
-      load_row<CPL>(edge + r * D + c0, act, ed);
+      load_row<CPL>(edge + r * D + c0, act, st.ed);
     } else {
-      zero_row<CPL>(ed);
+      zero_row<CPL>(st.ed);
     }
-    zero_row<CPL>(acc);
-    float m = -INFINITY, den = 0.f;
-    // two triplets' neighbour rows in flight ahead of the one being consumed
-    float k0[CPL], v0[CPL], k1[CPL], v1[CPL];
-    zero_row<CPL>(k0); zero_row<CPL>(v0); zero_row<CPL>(k1); zero_row<CPL>(v1);
-    if (t0 < t1) {
-      const int64_t s = uniform(tsrc[t0]);
-      load_row<CPL>(k + s * D + c0, act, k0);
-      load_row<CPL>(v + s * D + c0, act, v0);
-    }
-    if (t0 + 1 < t1) {
-      const int64_t s = uniform(tsrc[t0 + 1]);
-      load_row<CPL>(k + s * D + c0, act, k1);
-      load_row<CPL>(v + s * D + c0, act, v1);
-    }
-    for (int t = t0; t < t1; ++t) {
-      float k2[CPL], v2[CPL];
-      zero_row<CPL>(k2); zero_row<CPL>(v2);
-      if (t + 2 < t1) {
-        const int64_t s = uniform(tsrc[t + 2]);
-        load_row<CPL>(k + s * D + c0, act, k2);
-        load_row<CPL>(v + s * D + c0, act, v2);
-      }
-      float et[CPL];
-      if (MODE == X2G_EDGE_PER_TRIPLET) {
-        load_row<CPL>(edge + static_cast<int64_t>(t) * D + c0, act, et);
-      } else {
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) et[j] = ed[j];
-      }
-      float dot = 0.f;
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) dot = fmaf(qv[j], k0[j] + et[j], dot);
-      const float logit = group_sum<LPH>(dot) / sqrt_c;
-      float sp[CPL];
-      sbf_project<CPL>(wr, br, sbf + static_cast<int64_t>(t) * kS, sp);
-      const float m_new = fmaxf(m, logit);
-      const float corr = expf(m - m_new);
-      const float p = expf(logit - m_new);
-      den = den * corr + p;
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) acc[j] = acc[j] * corr + p * ((v0[j] + et[j]) * sp[j]);
-      m = m_new;
-      if (leader) alpha_out[static_cast<int64_t>(t) * H + head] = logit;
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) {
-        k0[j] = k1[j]; v0[j] = v1[j];
-        k1[j] = k2[j]; v1[j] = v2[j];
-      }
+    zero_row<CPL>(st.acc);
+    st.m = -INFINITY;
+    st.den = 0.f;
+    FwdSet<CPL> A{}, B{}, C{};
+    if (t0 < t1) fwd_load<CPL, PRE>(A, k, v, sbf, tsrc, t0, D, c0, act);
+    if (t0 + 1 < t1) fwd_load<CPL, PRE>(B, k, v, sbf, tsrc, t0 + 1, D, c0, act);
+    if (t0 + 2 < t1) fwd_load<CPL, PRE>(C, k, v, sbf, tsrc, t0 + 2, D, c0, act);
+    for (int t = t0; t < t1; t += 3) {
+      fwd_step<CPL, LPH, MODE, PRE>(A, t, t1, st, P, k, v, edge, sbf, tsrc, D, H, c0, head, act, leader, sqrt_c,
+                                    alpha_out);
+      if (t + 1 >= t1) break;
+      fwd_step<CPL, LPH, MODE, PRE>(B, t + 1, t1, st, P, k, v, edge, sbf, tsrc, D, H, c0, head, act, leader, sqrt_c,
+                                    alpha_out);
+      if (t + 2 >= t1) break;
+      fwd_step<CPL, LPH, MODE, PRE>(C, t + 2, t1, st, P, k, v, edge, sbf, tsrc, D, H, c0, head, act, leader, sqrt_c,
+                                    alpha_out);
     }
     float sk[CPL], o[CPL];
     load_row<CPL>(skip + e * D + c0, act, sk);
-    const float inv = 1.0f / (den + kSoftmaxEps);
+    const float inv = 1.0f / (st.den + kSoftmaxEps);
 #pragma unroll
-    for (int j = 0; j < CPL; ++j) o[j] = acc[j] * inv + sk[j];
+    for (int j = 0; j < CPL; ++j) o[j] = st.acc[j] * inv + sk[j];
     store_row<CPL>(out + e * D + c0, act, o);
     if (leader) {
-      smax_out[e * H + head] = m;
-      sden_out[e * H + head] = den;
+      smax_out[e * H + head] = st.m;
+      sden_out[e * H + head] = st.den;
     }
   }
 }
 
 // ------------------------------------------------------------------------------ backward (dst)
+// pass 1 (per triplet): g = d loss / d a_t per head (sum over the head's channels of
+// go (v + e) S), rho = sum_t a_t g_t, d_sbfproj = go (v + e) a, the value part of d_edge.
+// pass 2: dlogit = a (g - rho), dq, the key part of d_edge.
+template <int CPL>
+struct DstSet1 {
+  float v[CPL], s[CPL];
+  float al;  // raw logit of the triplet (this lane's head)
+};
+
+template <int CPL>
+struct DstSet2 {
+  float k[CPL];
+  float al, g;
+};
+
+template <int CPL>
+struct DstState {
+  float go[CPL], qv[CPL], ed[CPL], edacc[CPL], dqa[CPL];
+  float mx, inv, rho;
+};
+
+template <int CPL, bool PRE>
+__device__ __forceinline__ void dst_load1(DstSet1<CPL>& S, const float* __restrict__ v,
+                                          const float* __restrict__ sbf, const float* __restrict__ alpha,
+                                          const int32_t* __restrict__ tsrc, int t, int D, int H, int c0, int head,
+                                          bool act) {
+  const int64_t src = uniform(tsrc[t]);
+  load_row<CPL>(v + src * D + c0, act, S.v);
+  if (PRE) load_row<CPL>(sbf + static_cast<int64_t>(t) * D + c0, act, S.s);
+  S.al = alpha[static_cast<int64_t>(t) * H + (act ? head : 0)];
+}
+
+template <int CPL, int LPH, int MODE, bool PRE>
+__device__ __forceinline__ void dst_step1(DstSet1<CPL>& S, int t, int t1, DstState<CPL>& st,
+                                          const Proj<CPL, PRE>& P, const float* __restrict__ v,
+                                          const float* __restrict__ edge, const float* __restrict__ sbf,
+                                          const float* __restrict__ alpha, const int32_t* __restrict__ tsrc, int D,
+                                          int H, int c0, int head, bool act, bool leader,
+                                          float* __restrict__ d_edge, float* __restrict__ dlogit,
+                                          float* __restrict__ dproj) {
+  constexpr bool per_trip = MODE == X2G_EDGE_PER_TRIPLET;
+  float et[CPL], sp[CPL];
+  if (per_trip) {
+    load_row<CPL>(edge + static_cast<int64_t>(t) * D + c0, act, et);
+  } else {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) et[j] = st.ed[j];
+  }
+  proj_row<CPL, PRE>(P, sbf, t, S.s, sp);
+  const float at = act ? expf(S.al - st.mx) * st.inv : 0.f;
+  float gpart = 0.f, dp[CPL], du[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const float u = S.v[j] + et[j];
+    gpart = fmaf(st.go[j] * u, sp[j], gpart);
+    dp[j] = st.go[j] * u * at;
+    du[j] = st.go[j] * sp[j] * at;
+  }
+  const float g = group_sum<LPH>(gpart);
+  st.rho = fmaf(at, g, st.rho);
+  store_row<CPL>(dproj + static_cast<int64_t>(t) * D + c0, act, dp);
+  if (per_trip) {
+    store_row<CPL>(d_edge + static_cast<int64_t>(t) * D + c0, act, du);
+  } else {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) st.edacc[j] += du[j];
+  }
+  if (leader) dlogit[static_cast<int64_t>(t) * H + head] = g;
+  if (t + 3 < t1) dst_load1<CPL, PRE>(S, v, sbf, alpha, tsrc, t + 3, D, H, c0, head, act);
+}
+
+template <int CPL>
+__device__ __forceinline__ void dst_load2(DstSet2<CPL>& S, const float* __restrict__ k,
+                                          const float* __restrict__ alpha, const float* __restrict__ dlogit,
+                                          const int32_t* __restrict__ tsrc, int t, int D, int H, int c0, int head,
+                                          bool act, bool leader) {
+  const int64_t src = uniform(tsrc[t]);
+  load_row<CPL>(k + src * D + c0, act, S.k);
+  const int64_t ah = static_cast<int64_t>(t) * H + (act ? head : 0);
+  S.al = alpha[ah];
+  // pass 1's g of this (triplet, head) was written by the head's leader lane: only that lane
+  // reads it back (its own earlier store), the others get it by a shuffle at use
+  S.g = leader ? dlogit[ah] : 0.f;
+}
+
 template <int CPL, int LPH, int MODE>
+__device__ __forceinline__ void dst_step2(DstSet2<CPL>& S, int t, int t1, DstState<CPL>& st,
+                                          const float* __restrict__ k, const float* __restrict__ edge,
+                                          const float* __restrict__ alpha, const int32_t* __restrict__ tsrc, int D,
+                                          int H, int c0, int head, bool act, bool leader, float sqrt_c,
+                                          float* __restrict__ d_edge, float* __restrict__ dlogit) {
+  constexpr bool per_trip = MODE == X2G_EDGE_PER_TRIPLET;
+  float et[CPL];
+  if (per_trip) {
+    load_row<CPL>(edge + static_cast<int64_t>(t) * D + c0, act, et);
+  } else {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) et[j] = st.ed[j];
+  }
+  const float at = act ? expf(S.al - st.mx) * st.inv : 0.f;
+  const float dl = at * (group_sum<LPH>(S.g) - st.rho);
+  const float ds = dl / sqrt_c;
+  float dk[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    st.dqa[j] = fmaf(ds, S.k[j] + et[j], st.dqa[j]);
+    dk[j] = ds * st.qv[j];
+  }
+  if (per_trip) {
+    float cur[CPL];
+    load_row<CPL>(d_edge + static_cast<int64_t>(t) * D + c0, act, cur);
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) cur[j] += dk[j];
+    store_row<CPL>(d_edge + static_cast<int64_t>(t) * D + c0, act, cur);
+  } else {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) st.edacc[j] += dk[j];
+  }
+  if (t + 3 < t1) dst_load2<CPL>(S, k, alpha, dlogit, tsrc, t + 3, D, H, c0, head, act, leader);
+  if (leader) dlogit[static_cast<int64_t>(t) * H + head] = dl;  // after the prefetch read t + 3, not t
+}
+
+template <int CPL, int LPH, int MODE, bool PRE>
 __global__ void __launch_bounds__(256) attn_bwd_dst_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
     const float* __restrict__ edge, const int32_t* __restrict__ edge_row, const float* __restrict__ sbf,
@@ -264,108 +436,112 @@ __global__ void __launch_bounds__(256) attn_bwd_dst_kernel(
   const int c0 = act ? lane * CPL : 0;
   const int head = lane / LPH;
   const bool leader = act && (lane % LPH) == 0;
-  constexpr bool per_trip = MODE == X2G_EDGE_PER_TRIPLET;
   constexpr bool per_dst = MODE == X2G_EDGE_PER_DST;
-  float wr[CPL][kS], br[CPL];
-  load_weights<CPL>(w, b, c0, act, wr, br);
+  Proj<CPL, PRE> P;
+  P.init(w, b, c0, act);
   const WaveRange wr_ = xcd_wave_range(E);
   for (int64_t e = wr_.first; e < wr_.end; e += wr_.stride) {
     const int t0 = uniform(rowptr[e]), t1 = uniform(rowptr[e + 1]);
-    float go[CPL], qv[CPL], ed[CPL], edacc[CPL], dqa[CPL];
-    load_row<CPL>(dout + e * D + c0, act, go);
-    load_row<CPL>(q + e * D + c0, act, qv);
+    DstState<CPL> st;
+    load_row<CPL>(dout + e * D + c0, act, st.go);
+    load_row<CPL>(q + e * D + c0, act, st.qv);
     if (per_dst) {
       const int64_t r = edge_row ? uniform(edge_row[e]) : e;
-      load_row<CPL>(edge + r * D + c0, act, ed);
+      load_row<CPL>(edge + r * D + c0, act, st.ed);
     } else {
-      zero_row<CPL>(ed);
+      zero_row<CPL>(st.ed);
     }
-    zero_row<CPL>(edacc);
-    zero_row<CPL>(dqa);
-    const float mx = keep(smax[e * H + head], act);
-    const float inv = act ? 1.0f / (sden[e * H + head] + kSoftmaxEps) : 0.f;
-    // pass 1: g_t = d(loss)/d(a_t) per head, rho = sum_t a_t g_t; d_sbfproj and the value part
-    float rho = 0.f;
-    float vn[CPL];
-    zero_row<CPL>(vn);
-    if (t0 < t1) load_row<CPL>(v + static_cast<int64_t>(uniform(tsrc[t0])) * D + c0, act, vn);
-    for (int t = t0; t < t1; ++t) {
-      float vv[CPL], et[CPL], sp[CPL];
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) vv[j] = vn[j];
-      if (t + 1 < t1) load_row<CPL>(v + static_cast<int64_t>(uniform(tsrc[t + 1])) * D + c0, act, vn);
-      if (per_trip) {
-        load_row<CPL>(edge + static_cast<int64_t>(t) * D + c0, act, et);
-      } else {
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) et[j] = ed[j];
+    zero_row<CPL>(st.edacc);
+    zero_row<CPL>(st.dqa);
+    st.mx = keep(smax[e * H + head], act);
+    st.inv = act ? 1.0f / (sden[e * H + head] + kSoftmaxEps) : 0.f;
+    st.rho = 0.f;
+    {
+      DstSet1<CPL> A{}, B{}, C{};
+      if (t0 < t1) dst_load1<CPL, PRE>(A, v, sbf, alpha, tsrc, t0, D, H, c0, head, act);
+      if (t0 + 1 < t1) dst_load1<CPL, PRE>(B, v, sbf, alpha, tsrc, t0 + 1, D, H, c0, head, act);
+      if (t0 + 2 < t1) dst_load1<CPL, PRE>(C, v, sbf, alpha, tsrc, t0 + 2, D, H, c0, head, act);
+      for (int t = t0; t < t1; t += 3) {
+        dst_step1<CPL, LPH, MODE, PRE>(A, t, t1, st, P, v, edge, sbf, alpha, tsrc, D, H, c0, head, act, leader,
+                                       d_edge, dlogit, dproj);
+        if (t + 1 >= t1) break;
+        dst_step1<CPL, LPH, MODE, PRE>(B, t + 1, t1, st, P, v, edge, sbf, alpha, tsrc, D, H, c0, head, act, leader,
+                                       d_edge, dlogit, dproj);
+        if (t + 2 >= t1) break;
+        dst_step1<CPL, LPH, MODE, PRE>(C, t + 2, t1, st, P, v, edge, sbf, alpha, tsrc, D, H, c0, head, act, leader,
+                                       d_edge, dlogit, dproj);
       }
-      sbf_project<CPL>(wr, br, sbf + static_cast<int64_t>(t) * kS, sp);
-      const float at = act ? expf(alpha[static_cast<int64_t>(t) * H + head] - mx) * inv : 0.f;
-      float gpart = 0.f, dp[CPL], du[CPL];
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) {
-        const float u = vv[j] + et[j];
-        gpart = fmaf(go[j] * u, sp[j], gpart);
-        dp[j] = go[j] * u * at;
-        du[j] = go[j] * sp[j] * at;
-      }
-      const float g = group_sum<LPH>(gpart);
-      rho = fmaf(at, g, rho);
-      store_row<CPL>(dproj + static_cast<int64_t>(t) * D + c0, act, dp);
-      if (per_trip) {
-        store_row<CPL>(d_edge + static_cast<int64_t>(t) * D + c0, act, du);
-      } else {
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) edacc[j] += du[j];
-      }
-      if (leader) dlogit[static_cast<int64_t>(t) * H + head] = g;
     }
-    // pass 2: dlogit = a (g - rho); dq, and the key part of the edge gradient
-    float kn[CPL];
-    zero_row<CPL>(kn);
-    if (t0 < t1) load_row<CPL>(k + static_cast<int64_t>(uniform(tsrc[t0])) * D + c0, act, kn);
-    for (int t = t0; t < t1; ++t) {
-      float kk[CPL], et[CPL];
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) kk[j] = kn[j];
-      if (t + 1 < t1) load_row<CPL>(k + static_cast<int64_t>(uniform(tsrc[t + 1])) * D + c0, act, kn);
-      if (per_trip) {
-        load_row<CPL>(edge + static_cast<int64_t>(t) * D + c0, act, et);
-      } else {
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) et[j] = ed[j];
+    {
+      DstSet2<CPL> A{}, B{}, C{};
+      if (t0 < t1) dst_load2<CPL>(A, k, alpha, dlogit, tsrc, t0, D, H, c0, head, act, leader);
+      if (t0 + 1 < t1) dst_load2<CPL>(B, k, alpha, dlogit, tsrc, t0 + 1, D, H, c0, head, act, leader);
+      if (t0 + 2 < t1) dst_load2<CPL>(C, k, alpha, dlogit, tsrc, t0 + 2, D, H, c0, head, act, leader);
+      for (int t = t0; t < t1; t += 3) {
+        dst_step2<CPL, LPH, MODE>(A, t, t1, st, k, edge, alpha, tsrc, D, H, c0, head, act, leader, sqrt_c, d_edge, dlogit);
+        if (t + 1 >= t1) break;
+        dst_step2<CPL, LPH, MODE>(B, t + 1, t1, st, k, edge, alpha, tsrc, D, H, c0, head, act, leader, sqrt_c, d_edge,
+                             dlogit);
+        if (t + 2 >= t1) break;
+        dst_step2<CPL, LPH, MODE>(C, t + 2, t1, st, k, edge, alpha, tsrc, D, H, c0, head, act, leader, sqrt_c, d_edge,
+                             dlogit);
       }
-      const float at = act ? expf(alpha[static_cast<int64_t>(t) * H + head] - mx) * inv : 0.f;
-      // only the leader lane wrote g for this head: read it back in that lane, then broadcast
-      const float g = group_sum<LPH>(leader ? dlogit[static_cast<int64_t>(t) * H + head] : 0.f);
-      const float dl = at * (g - rho);
-      const float ds = dl / sqrt_c;
-      float dk[CPL];
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) {
-        dqa[j] = fmaf(ds, kk[j] + et[j], dqa[j]);
-        dk[j] = ds * qv[j];
-      }
-      if (per_trip) {
-        float cur[CPL];
-        load_row<CPL>(d_edge + static_cast<int64_t>(t) * D + c0, act, cur);
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) cur[j] += dk[j];
-        store_row<CPL>(d_edge + static_cast<int64_t>(t) * D + c0, act, cur);
-      } else {
-#pragma unroll
-        for (int j = 0; j < CPL; ++j) edacc[j] += dk[j];
-      }
-      if (leader) dlogit[static_cast<int64_t>(t) * H + head] = dl;
     }
-    store_row<CPL>(dq + e * D + c0, act, dqa);
-    if (per_dst) store_row<CPL>(d_edge + e * D + c0, act, edacc);
+    store_row<CPL>(dq + e * D + c0, act, st.dqa);
+    if (per_dst) store_row<CPL>(d_edge + e * D + c0, act, st.edacc);
   }
 }
 
 // ------------------------------------------------------------------------------ backward (src)
-template <int CPL, int LPH>
+template <int CPL>
+struct SrcSet {
+  float go[CPL], qv[CPL], s[CPL];
+  float al, mx, den, dl;
+  int64_t t;
+};
+
+template <int CPL, bool PRE>
+__device__ __forceinline__ void src_load(SrcSet<CPL>& S, const float* __restrict__ q, const float* __restrict__ sbf,
+                                         const int32_t* __restrict__ perm, const int32_t* __restrict__ tdst,
+                                         const float* __restrict__ alpha, const float* __restrict__ smax,
+                                         const float* __restrict__ sden, const float* __restrict__ dlogit_in,
+                                         const float* __restrict__ dout, int p, int D, int H, int c0, int head,
+                                         bool act) {
+  const int64_t t = uniform(perm[p]);
+  const int64_t e = uniform(tdst[t]);
+  S.t = t;
+  load_row<CPL>(dout + e * D + c0, act, S.go);
+  load_row<CPL>(q + e * D + c0, act, S.qv);
+  if (PRE) load_row<CPL>(sbf + t * D + c0, act, S.s);
+  const int hh = act ? head : 0;
+  S.al = alpha[t * H + hh];
+  S.dl = dlogit_in[t * H + hh];
+  S.mx = smax[e * H + hh];
+  S.den = sden[e * H + hh];
+}
+
+template <int CPL, bool PRE>
+__device__ __forceinline__ void src_step(SrcSet<CPL>& S, int p, int p1, const Proj<CPL, PRE>& P,
+                                         float (&dka)[CPL], float (&dva)[CPL], const float* __restrict__ q,
+                                         const float* __restrict__ sbf, const int32_t* __restrict__ perm,
+                                         const int32_t* __restrict__ tdst, const float* __restrict__ alpha,
+                                         const float* __restrict__ smax, const float* __restrict__ sden,
+                                         const float* __restrict__ dlogit_in, const float* __restrict__ dout, int D,
+                                         int H, int c0, int head, bool act, float sqrt_c) {
+  float sp[CPL];
+  proj_row<CPL, PRE>(P, sbf, S.t, S.s, sp);
+  const float at = act ? expf(S.al - S.mx) / (S.den + kSoftmaxEps) : 0.f;
+  const float ds = act ? S.dl / sqrt_c : 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    dva[j] = fmaf(S.go[j] * sp[j], at, dva[j]);
+    dka[j] = fmaf(ds, S.qv[j], dka[j]);
+  }
+  if (p + 3 < p1) src_load<CPL, PRE>(S, q, sbf, perm, tdst, alpha, smax, sden, dlogit_in, dout, p + 3, D, H, c0, head,
+                                     act);
+}
+
+template <int CPL, int LPH, bool PRE>
 __global__ void __launch_bounds__(256) attn_bwd_src_kernel(
     const float* __restrict__ q, const float* __restrict__ sbf, const float* __restrict__ w,
     const float* __restrict__ b, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ perm,
@@ -376,81 +552,88 @@ __global__ void __launch_bounds__(256) attn_bwd_src_kernel(
   const bool act = lane * CPL < D;
   const int c0 = act ? lane * CPL : 0;
   const int head = lane / LPH;
-  float wr[CPL][kS], br[CPL];
-  load_weights<CPL>(w, b, c0, act, wr, br);
+  Proj<CPL, PRE> P;
+  P.init(w, b, c0, act);
   const WaveRange wr_ = xcd_wave_range(E);
   for (int64_t s = wr_.first; s < wr_.end; s += wr_.stride) {
     const int p0 = uniform(rowptr[s]), p1 = uniform(rowptr[s + 1]);
     float dka[CPL], dva[CPL];
     zero_row<CPL>(dka);
     zero_row<CPL>(dva);
-    // next triplet's gathered rows (dout, q of its destination) in flight
-    float gn[CPL], qn[CPL];
-    zero_row<CPL>(gn);
-    zero_row<CPL>(qn);
-    int64_t tn = 0, en = 0;
-    if (p0 < p1) {
-      tn = uniform(perm[p0]);
-      en = uniform(tdst[tn]);
-      load_row<CPL>(dout + en * D + c0, act, gn);
-      load_row<CPL>(q + en * D + c0, act, qn);
-    }
-    for (int p = p0; p < p1; ++p) {
-      const int64_t t = tn, e = en;
-      float go[CPL], qv[CPL], sp[CPL];
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) {
-        go[j] = gn[j];
-        qv[j] = qn[j];
-      }
-      if (p + 1 < p1) {
-        tn = uniform(perm[p + 1]);
-        en = uniform(tdst[tn]);
-        load_row<CPL>(dout + en * D + c0, act, gn);
-        load_row<CPL>(q + en * D + c0, act, qn);
-      }
-      float at = 0.f, dl = 0.f;
-      if (act) {
-        const float mx = smax[e * H + head];
-        const float inv = 1.0f / (sden[e * H + head] + kSoftmaxEps);
-        at = expf(alpha[t * H + head] - mx) * inv;
-        dl = dlogit_in[t * H + head];
-      }
-      sbf_project<CPL>(wr, br, sbf + t * kS, sp);
-      const float ds = dl / sqrt_c;
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) {
-        dva[j] = fmaf(go[j] * sp[j], at, dva[j]);
-        dka[j] = fmaf(ds, qv[j], dka[j]);
-      }
+    SrcSet<CPL> A{}, B{}, C{};
+    if (p0 < p1) src_load<CPL, PRE>(A, q, sbf, perm, tdst, alpha, smax, sden, dlogit_in, dout, p0, D, H, c0, head, act);
+    if (p0 + 1 < p1)
+      src_load<CPL, PRE>(B, q, sbf, perm, tdst, alpha, smax, sden, dlogit_in, dout, p0 + 1, D, H, c0, head, act);
+    if (p0 + 2 < p1)
+      src_load<CPL, PRE>(C, q, sbf, perm, tdst, alpha, smax, sden, dlogit_in, dout, p0 + 2, D, H, c0, head, act);
+    for (int p = p0; p < p1; p += 3) {
+      src_step<CPL, PRE>(A, p, p1, P, dka, dva, q, sbf, perm, tdst, alpha, smax, sden, dlogit_in, dout, D, H, c0, head,
+                         act, sqrt_c);
+      if (p + 1 >= p1) break;
+      src_step<CPL, PRE>(B, p + 1, p1, P, dka, dva, q, sbf, perm, tdst, alpha, smax, sden, dlogit_in, dout, D, H, c0,
+                         head, act, sqrt_c);
+      if (p + 2 >= p1) break;
+      src_step<CPL, PRE>(C, p + 2, p1, P, dka, dva, q, sbf, perm, tdst, alpha, smax, sden, dlogit_in, dout, D, H, c0,
+                         head, act, sqrt_c);
     }
     store_row<CPL>(dk + s * D + c0, act, dka);
     store_row<CPL>(dv + s * D + c0, act, dva);
   }
 }
 
+// ------------------------------------------------------------------------------ sbf projection
+// S[t, :] = W sbf_t + b for all triplets (x2g_sbf_project): one wave per triplet row (grid-
+// stride), CPL channels per lane with W in registers, the 42-float sbf row wave-uniform (scalar
+// loads), one coalesced row store.  Every attention kernel then reads S rows instead of
+// re-projecting (3 x 84 FMAs per triplet and lane, and 84 weight VGPRs, saved per layer).
+template <int CPL>
+__global__ void __launch_bounds__(256) sbf_project_kernel(const float* __restrict__ sbf, const float* __restrict__ w,
+                                                          const float* __restrict__ b, int64_t T, int D,
+                                                          float* __restrict__ S) {
+  const int lane = threadIdx.x & 63;
+  const bool act = lane * CPL < D;
+  const int c0 = act ? lane * CPL : 0;
+  float wr[CPL][kS], br[CPL];
+  load_weights<CPL>(w, b, c0, act, wr, br);
+  const int64_t nw = static_cast<int64_t>(gridDim.x) * kAttnWaves;
+  for (int64_t t = uniform(blockIdx.x * kAttnWaves + (threadIdx.x >> 6)); t < T; t += nw) {
+    float sp[CPL];
+    sbf_project<CPL>(wr, br, sbf + t * kS, sp);
+    store_row<CPL>(S + t * D + c0, act, sp);
+  }
+}
+
 // ------------------------------------------------------------------------------ dispatch
 enum class Pass { kFwd, kBwdDst, kBwdSrc };
 
-template <int CPL, int LPH, int MODE>
-void launch_mode(Pass pass, const AttnArgs& a, unsigned blocks, hipStream_t st) {
+template <int CPL, int LPH, int MODE, bool PRE>
+void launch_pre(Pass pass, const AttnArgs& a, unsigned blocks, hipStream_t st) {
   switch (pass) {
     case Pass::kFwd:
-      attn_fwd_kernel<CPL, LPH, MODE><<<blocks, 256, 0, st>>>(a.q, a.k, a.v, a.skip, a.edge, a.edge_row, a.sbf, a.w,
-                                                              a.b, a.rowptr, a.tidx, a.E, a.D, a.H, a.sqrt_c, a.out,
-                                                              a.alpha_out, a.smax_out, a.sden_out);
+      attn_fwd_kernel<CPL, LPH, MODE, PRE><<<blocks, 256, 0, st>>>(
+          a.q, a.k, a.v, a.skip, a.edge, a.edge_row, a.sbf, a.w, a.b, a.rowptr, a.tidx, a.E, a.D, a.H, a.sqrt_c, a.out,
+          a.alpha_out, a.smax_out, a.sden_out);
       break;
     case Pass::kBwdDst:
-      attn_bwd_dst_kernel<CPL, LPH, MODE><<<blocks, 256, 0, st>>>(
+      attn_bwd_dst_kernel<CPL, LPH, MODE, PRE><<<blocks, 256, 0, st>>>(
           a.q, a.k, a.v, a.edge, a.edge_row, a.sbf, a.w, a.b, a.rowptr, a.tidx, a.alpha, a.smax, a.sden, a.dout,
           a.E, a.D, a.H, a.sqrt_c, a.dq, a.d_edge, a.dlogit, a.dproj);
       break;
     case Pass::kBwdSrc:
-      attn_bwd_src_kernel<CPL, LPH><<<blocks, 256, 0, st>>>(a.q, a.sbf, a.w, a.b, a.rowptr, a.tidx, a.tdst, a.alpha,
-                                                            a.smax, a.sden, a.dlogit_in, a.dout, a.E, a.D, a.H,
-                                                            a.sqrt_c, a.dk, a.dv);
+      attn_bwd_src_kernel<CPL, LPH, PRE><<<blocks, 256, 0, st>>>(a.q, a.sbf, a.w, a.b, a.rowptr, a.tidx, a.tdst,
+                                                                 a.alpha, a.smax, a.sden, a.dlogit_in, a.dout, a.E,
+                                                                 a.D, a.H, a.sqrt_c, a.dk, a.dv);
       break;
   }
+}
+
+// w == NULL: `sbf` is the precomputed projection S[T, D] (x2g_sbf_project)
+template <int CPL, int LPH, int MODE>
+void launch_mode(Pass pass, const AttnArgs& a, unsigned blocks, hipStream_t st) {
+  if (a.w == nullptr)
+    launch_pre<CPL, LPH, MODE, true>(pass, a, blocks, st);
+  else
+    launch_pre<CPL, LPH, MODE, false>(pass, a, blocks, st);
 }
 
 template <int CPL, int LPH>
@@ -481,7 +664,7 @@ int launch_cpl(Pass pass, const AttnArgs& a, int lph, unsigned blocks, hipStream
 
 int dispatch(Pass pass, AttnArgs a, int heads, int channels, int sbf_dim, hipStream_t st) {
   if (a.E < 0 || heads <= 0 || channels <= 0) return X2G_EINVAL;
-  if (sbf_dim != kS) return X2G_EUNSUPPORTED;
+  if (a.w ? sbf_dim != kS : sbf_dim != heads * channels) return X2G_EUNSUPPORTED;
   if (a.edge_mode != X2G_EDGE_NONE && a.edge_mode != X2G_EDGE_PER_TRIPLET && a.edge_mode != X2G_EDGE_PER_DST)
     return X2G_EINVAL;
   const int D = heads * channels;
@@ -520,7 +703,7 @@ X2G_API int x2g_sbf_attention_fwd(const float* q, const float* k, const float* v
                                   const int32_t* trip_src, int64_t E, int64_t T, int32_t heads,
                                   int32_t channels, int32_t sbf_dim, float* out, float* alpha_raw,
                                   float* seg_max, float* seg_den, void* stream) {
-  if (E > 0 && (!q || !k || !v || !skip || !sbf || !w_sbf || !b_sbf || !trip_rowptr || !out || !seg_max ||
+  if (E > 0 && (!q || !k || !v || !skip || !sbf || (w_sbf && !b_sbf) || !trip_rowptr || !out || !seg_max ||
                 !seg_den))
     return X2G_EINVAL;
   if (T > 0 && (!trip_src || !alpha_raw)) return X2G_EINVAL;
@@ -539,7 +722,7 @@ X2G_API int x2g_sbf_attention_bwd_dst(const float* q, const float* k, const floa
                                       const float* seg_den, const float* dout, int64_t E, int64_t T,
                                       int32_t heads, int32_t channels, int32_t sbf_dim, float* dq,
                                       float* d_edge, float* dlogit, float* d_sbfproj, void* stream) {
-  if (E > 0 && (!q || !k || !v || !sbf || !w_sbf || !b_sbf || !trip_rowptr || !seg_max || !seg_den || !dout ||
+  if (E > 0 && (!q || !k || !v || !sbf || (w_sbf && !b_sbf) || !trip_rowptr || !seg_max || !seg_den || !dout ||
                 !dq))
     return X2G_EINVAL;
   if (T > 0 && (!trip_src || !alpha_raw || !dlogit || !d_sbfproj)) return X2G_EINVAL;
@@ -558,7 +741,7 @@ X2G_API int x2g_sbf_attention_bwd_src(const float* q, const float* sbf, const fl
                                       const float* dlogit, const float* dout, int64_t E, int64_t T,
                                       int32_t heads, int32_t channels, int32_t sbf_dim, float* dk, float* dv,
                                       void* stream) {
-  if (E > 0 && (!q || !sbf || !w_sbf || !b_sbf || !src_rowptr || !seg_max || !seg_den || !dout || !dk || !dv))
+  if (E > 0 && (!q || !sbf || (w_sbf && !b_sbf) || !src_rowptr || !seg_max || !seg_den || !dout || !dk || !dv))
     return X2G_EINVAL;
   if (T > 0 && (!src_perm || !trip_dst || !alpha_raw || !dlogit)) return X2G_EINVAL;
   AttnArgs a{};
@@ -566,4 +749,30 @@ X2G_API int x2g_sbf_attention_bwd_src(const float* q, const float* sbf, const fl
   a.alpha = alpha_raw; a.smax = seg_max; a.sden = seg_den; a.dlogit_in = dlogit; a.dout = dout; a.E = E;
   a.dk = dk; a.dv = dv;
   return dispatch(Pass::kBwdSrc, a, heads, channels, sbf_dim, as_stream(stream));
+}
+
+namespace x2g {  // csrc/dense.hip: the narrow-K MFMA dense forward
+int dense_fwd_narrow_launch(const float* x, const float* w, const float* b, const float* res, int64_t R, int K, int N,
+                            int act, float* y, float* z, hipStream_t st);
+}  // namespace x2g
+
+X2G_API int x2g_sbf_project(const float* sbf, int64_t T, int32_t sbf_dim, const float* w_sbf, const float* b_sbf,
+                            int32_t out_dim, float* sbfproj, void* stream) {
+  if (T < 0 || out_dim <= 0) return X2G_EINVAL;
+  if (sbf_dim != kS) return X2G_EUNSUPPORTED;
+  if (T == 0) return X2G_OK;
+  if (!sbf || !w_sbf || !b_sbf || !sbfproj) return X2G_EINVAL;
+  hipStream_t st = as_stream(stream);
+  if (out_dim % 4 == 0 && reinterpret_cast<uintptr_t>(sbf) % 16 == 0 && reinterpret_cast<uintptr_t>(sbfproj) % 16 == 0 &&
+      tuning(kTuneAttn) == 0)  // f32 MFMA, tiles staged through LDS (dense.hip)
+    return dense_fwd_narrow_launch(sbf, w_sbf, b_sbf, nullptr, T, kS, out_dim, 0, sbfproj, nullptr, st);
+  int64_t want = (T + kAttnWaves - 1) / kAttnWaves;
+  const unsigned blocks = static_cast<unsigned>(want < 4096 ? want : 4096);
+  switch (out_dim) {
+    case 32: case 64: sbf_project_kernel<1><<<blocks, 256, 0, st>>>(sbf, w_sbf, b_sbf, T, out_dim, sbfproj); break;
+    case 128: sbf_project_kernel<2><<<blocks, 256, 0, st>>>(sbf, w_sbf, b_sbf, T, out_dim, sbfproj); break;
+    case 256: sbf_project_kernel<4><<<blocks, 256, 0, st>>>(sbf, w_sbf, b_sbf, T, out_dim, sbfproj); break;
+    default: return X2G_EUNSUPPORTED;
+  }
+  return last_launch_status();
 }

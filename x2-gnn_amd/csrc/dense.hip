@@ -713,6 +713,99 @@ __global__ void __launch_bounds__(512) dense_bwd_persist(const float* __restrict
   if (part_b && tid < N) part_b[static_cast<int64_t>(blockIdx.x) * N + tid] = bsum;
 }
 
+// ---------------------------------------------------------------- forward, narrow K (K % 4 != 0)
+// For rows too narrow / odd for 16-byte row chunks (lin_sbf: K = 42): a 64-row tile pair is one
+// contiguous span of 64*K floats, read with 16-byte loads regardless of K and scattered into
+// an LDS tile [64][KP] (KP = K rounded up to 4, zero padded).  Contraction order
+// c(s, h) = 4 (s >> 1) + 2h + (s & 1): a lane's two consecutive steps read one 8-byte pair.
+// Weight in the padded slot layout with the same order; epilogue as dense_fwd_v5.
+__device__ __forceinline__ int cmap_n(int s, int h) { return 4 * (s >> 1) + 2 * h + (s & 1); }
+
+template <int STEPS>
+__global__ void __launch_bounds__(512) dense_fwd_narrow(const float* __restrict__ X, const float* __restrict__ W,
+                                                        const float* __restrict__ bias,
+                                                        const float* __restrict__ res, int64_t R, int K, int N,
+                                                        int act, float* __restrict__ Y, float* __restrict__ Z) {
+  constexpr int KP = 2 * STEPS;  // padded row length (>= K, multiple of 4)
+  __shared__ __attribute__((aligned(16))) float Ws[STEPS * kSlotStride];
+  __shared__ __attribute__((aligned(16))) float Xs[64 * 128];  // x tile [64][KP], then the output tile
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, i = lane & 31;
+  const int slot = wave >> 2;
+  const int n = 32 * (wave & 3) + i;
+  const int q = tid & 31;
+  const int64_t npairs = (R + 63) / 64;
+  const int64_t G = gridDim.x;
+  f4 b4 = {0.f, 0.f, 0.f, 0.f};
+  if (bias && 4 * q < N) b4 = f4{bias[4 * q], bias[4 * q + 1], bias[4 * q + 2], bias[4 * q + 3]};
+  // weight: B[c][j] = w[j][c] for c < K, zero beyond
+  for (int idx = tid; idx < STEPS * 2 * 128; idx += 512) {
+    const int j = idx / (2 * STEPS), r = idx - j * 2 * STEPS;  // r = contraction index c
+    const int sl = 2 * (r >> 2) + (r & 1), hh = (r >> 1) & 1;
+    const float wv = (j < N && r < K) ? W[j * K + r] : 0.f;
+    Ws[sl * kSlotStride + 2 * j + hh] = wv;
+  }
+  const unsigned magic = 0xFFFFFFFFu / static_cast<unsigned>(K) + 1u;  // K >= 2 here
+  const float* wb = Ws + 2 * n + h;
+  for (int64_t tp = blockIdx.x; tp < npairs; tp += G) {
+    // stage the pair: rows [64 tp, 64 tp + 64) are floats [64 tp K, 64 tp K + 64 K)
+    const int64_t base = tp * 64 * K;
+    const int64_t nvalid = ((R - tp * 64) < 64 ? (R - tp * 64) : 64) * K;
+    const int nq = (64 * K) >> 2;
+    __syncthreads();  // previous pair's output tile fully stored
+    for (int qi = tid; qi < nq; qi += 512) {
+      const bool ok = 4 * qi < nvalid;
+      const f4 v = *reinterpret_cast<const f4*>(X + base + (ok ? 4 * qi : 0));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const unsigned f = 4 * qi + e, row = __umulhi(f, magic), c = f - row * K;
+        Xs[row * KP + c] = (4 * qi + e < nvalid) ? v[e] : 0.f;
+      }
+    }
+    for (int idx = tid; idx < 64 * (KP - K); idx += 512) {  // zero the pad columns
+      const int row = idx / (KP - K), c = K + idx - row * (KP - K);
+      Xs[row * KP + c] = 0.f;
+    }
+    __syncthreads();
+    floatx16 acc0, acc1;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      acc0[j] = 0.f;
+      acc1[j] = 0.f;
+    }
+    const float* xs = Xs + (slot * 32 + i) * KP + 2 * h;
+#pragma unroll
+    for (int g = 0; g < STEPS / 2; ++g) {
+      const float2 a = *reinterpret_cast<const float2*>(xs + 4 * g);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, wb[(2 * g) * kSlotStride], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, wb[(2 * g + 1) * kSlotStride], acc1, 0, 0, 0);
+    }
+    __syncthreads();  // x tile consumed: the buffer stages the output
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int r = slot * 32 + (j & 3) + 8 * (j >> 2) + 4 * h;
+      Xs[r * 128 + 4 * ((n >> 2) ^ (r & 15)) + (n & 3)] = acc0[j] + acc1[j];
+    }
+    __syncthreads();
+    Stage4 rres{};
+    if (res) xpair_load4(res, tp, R, N, rres);
+    epi_chunk<0>(Xs, rres, b4, tp, R, N, act, Y, Z);
+    epi_chunk<1>(Xs, rres, b4, tp, R, N, act, Y, Z);
+    epi_chunk<2>(Xs, rres, b4, tp, R, N, act, Y, Z);
+    epi_chunk<3>(Xs, rres, b4, tp, R, N, act, Y, Z);
+  }
+}
+
+int dense_fwd_narrow_launch(const float* x, const float* w, const float* b, const float* res, int64_t R, int K, int N,
+                            int act, float* y, float* z, hipStream_t st) {
+  const int64_t npairs = (R + 63) / 64;
+  const unsigned grid = static_cast<unsigned>(npairs < 512 ? npairs : 512);
+  if (K <= 44)
+    dense_fwd_narrow<22><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
+  else
+    dense_fwd_narrow<64><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
+  return last_launch_status();
+}
+
 // ---------------------------------------------------------------- backward, v5 (default)
 // dense_bwd_persist restructured like dense_fwd_v5 (K % 4 == 0, N % 4 == 0, 16-byte aligned):
 //   * dy, z, x tiles (64 rows) are read with 16-byte loads (4 per thread per matrix instead of
@@ -900,6 +993,9 @@ X2G_API int x2g_dense_fwd(const float* x, const float* w, const float* b, int64_
     const bool vec = K % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0;
     if (K <= 8)
       dense_fwd_persist<4, false><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
+    else if (!vec && variant == 0 && K % 4 != 0 && N % 4 == 0 && aligned16(x) && aligned16(y) && aligned16(z) &&
+             aligned16(res))
+      return dense_fwd_narrow_launch(x, w, b, res, R, K, N, act, y, z, st);
     else if (vec && variant == 0 && N % 4 == 0 && aligned16(y) && aligned16(z) && aligned16(res))
       dense_fwd_v5<<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
     else if (vec && variant == 0)

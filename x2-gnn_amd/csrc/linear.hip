@@ -16,7 +16,9 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kWgTile = 128;       // output block (o) x (i) per workgroup
 constexpr int kWgChunk = 32;       // rows staged in LDS per iteration
-constexpr int kWgMaxSplits = 160;  // row splits (workgroups per output block)
+constexpr int kWgMinSplits = 160;        // row splits for a full 128x128 output block
+constexpr int kWgMaxSplits = 1024;       // ... and for narrow outputs (cheap slabs)
+constexpr int64_t kWgSlabBudget = 16 << 20;  // bytes of partial slabs one call may write
 constexpr int kLdsStride = kWgTile + 4;  // keeps 16-byte row alignment for the float4 stores
 
 // Chunk of 32 rows x 128 columns of one operand, held in registers between global and LDS.
@@ -224,15 +226,23 @@ int sum_slabs_launch(const float* part_w, int64_t nw, const float* part_b, int64
   return last_launch_status();
 }
 
-// rows per split: a multiple of the 32-row chunk, at least 64, at most kWgMaxSplits splits
-
-inline int64_t wgrad_rows_per_split(int64_t R) {
-  int64_t rps = (R + kWgMaxSplits - 1) / kWgMaxSplits;
+// Row splits: as many workgroups as the slab budget allows (a 128x128 output: 160 x 64 KB; lin_sbf's
+// 128x42: 512+, so the 194k-row reduction fills the chip), rows per split a multiple of the
+// 32-row chunk and at least 64.
+inline int max_splits(int O, int I) {
+  const int64_t per = (static_cast<int64_t>(O) * I + O) * static_cast<int64_t>(sizeof(float));
+  int64_t m = kWgSlabBudget / per;
+  m = m < kWgMinSplits ? kWgMinSplits : m;
+  return static_cast<int>(m > kWgMaxSplits ? kWgMaxSplits : m);
+}
+inline int64_t wgrad_rows_per_split(int64_t R, int O, int I) {
+  const int ms = max_splits(O, I);
+  int64_t rps = (R + ms - 1) / ms;
   rps = (rps + kWgChunk - 1) / kWgChunk * kWgChunk;
   return rps < 64 ? 64 : rps;
 }
-inline int wgrad_splits(int64_t R) {
-  const int64_t rps = wgrad_rows_per_split(R);
+inline int wgrad_splits(int64_t R, int O, int I) {
+  const int64_t rps = wgrad_rows_per_split(R, O, I);
   return static_cast<int>((R + rps - 1) / rps);
 }
 
@@ -242,7 +252,7 @@ using namespace x2g;
 
 X2G_API size_t x2g_linear_wgrad_workspace(int64_t R, int32_t O, int32_t I) {
   if (R <= 0 || O <= 0 || I <= 0) return 0;
-  const int64_t s = wgrad_splits(R);
+  const int64_t s = wgrad_splits(R, O, I);
   return static_cast<size_t>(s) * (static_cast<int64_t>(O) * I + O) * sizeof(float);
 }
 
@@ -259,7 +269,7 @@ X2G_API int x2g_linear_wgrad_ex(const float* dy, const float* x, int64_t R, int3
   }
   if (!dy || !x) return X2G_EINVAL;
   if (!workspace || workspace_bytes < x2g_linear_wgrad_workspace(R, O, I)) return X2G_EWORKSPACE;
-  const int splits = wgrad_splits(R);
+  const int splits = wgrad_splits(R, O, I);
   float* part = static_cast<float*>(workspace);
   float* part_b = db ? part + static_cast<int64_t>(splits) * O * I : nullptr;
   const int tiles_o = (O + kWgTile - 1) / kWgTile, tiles_i = (I + kWgTile - 1) / kWgTile;
@@ -270,7 +280,7 @@ X2G_API int x2g_linear_wgrad_ex(const float* dy, const float* x, int64_t R, int3
     return cols <= kWgTile ? static_cast<int>(kFlat) : static_cast<int>(kScalar);
   };
   const int ma = mode(O, dy), mb = mode(I, x);
-  const int64_t rps = wgrad_rows_per_split(R);
+  const int64_t rps = wgrad_rows_per_split(R, O, I);
 #define X2G_WGRAD(A, B) wgrad_partial<A, B><<<grid, 256, 0, st>>>(dy, x, R, O, I, tiles_i, rps, part, part_b)
   if (ma == kVec && mb == kVec) X2G_WGRAD(kVec, kVec);
   else if (ma == kVec && mb == kFlat) X2G_WGRAD(kVec, kFlat);

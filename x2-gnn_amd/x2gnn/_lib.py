@@ -51,6 +51,7 @@ SIGNATURES = {
     "x2g_dense_bwd": [_P, _P, ctypes.c_int, _P, _P, _I64, _I32, _I32, _P, _P, _P, _P, _SZ, _P],
     "x2g_linear_wgrad_ex": [_P, _P, _I64, _I32, _I32, _P, _P, ctypes.c_int, _P, _SZ, _P],
     "x2g_optimizer_workspace": [_I64],
+    "x2g_sbf_project": [_P, _I64, _I32, _P, _P, _I32, _P, _P],
     "x2g_clip_adam_ema": [_P, _P, _P, _P, _P, _I64, _P, _P, _SZ, _P],
     "x2g_dense_bwd_ex": [_P, _P, ctypes.c_int, _P, _P, _I64, _I32, _I32, _P, _P, _P, _P, ctypes.c_int, _P, _SZ,
                          _P],

@@ -160,10 +160,14 @@ class _SBFAttention(torch.autograd.Function):
         alpha = torch.empty(T, heads, dtype=torch.float32, device=dev)
         smax = torch.empty(E, heads, dtype=torch.float32, device=dev)
         sden = torch.empty(E, heads, dtype=torch.float32, device=dev)
+        # S = lin_sbf(sbf) once per layer [T, D]; the three attention kernels read its rows
+        # (sbf pointer = S, weight pointer NULL) instead of re-projecting per triplet
+        sproj = torch.empty(T, D, dtype=torch.float32, device=dev)
+        call("x2g_sbf_project", ptr(sbf), T, sbf.shape[1], ptr(w_sbf), ptr(b_sbf), D, ptr(sproj), stream_ptr())
         call("x2g_sbf_attention_fwd", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(edge_row), edge_mode,
-             ptr(sbf), ptr(w_sbf), ptr(b_sbf), ptr(lg.trip_rowptr), ptr(lg.trip_src), E, T, heads, channels,
-             sbf.shape[1], ptr(out), ptr(alpha), ptr(smax), ptr(sden), stream_ptr())
-        ctx.save_for_backward(q, k, v, edge, sbf, w_sbf, b_sbf, alpha, smax, sden)
+             ptr(sproj), None, None, ptr(lg.trip_rowptr), ptr(lg.trip_src), E, T, heads, channels, D, ptr(out),
+             ptr(alpha), ptr(smax), ptr(sden), stream_ptr())
+        ctx.save_for_backward(q, k, v, edge, sbf, sproj, alpha, smax, sden)
         ctx.w_param, ctx.b_param = w_param, b_param
         ctx.lg, ctx.edge_mode, ctx.edge_row, ctx.heads, ctx.channels = lg, edge_mode, edge_row, heads, channels
         ctx.edge_shape = None if edge is None else edge.shape
@@ -172,7 +176,7 @@ class _SBFAttention(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout, _da=None, _dm=None, _ds=None):
-        q, k, v, edge, sbf, w_sbf, b_sbf, alpha, smax, sden = ctx.saved_tensors
+        q, k, v, edge, sbf, sproj, alpha, smax, sden = ctx.saved_tensors
         lg, mode, heads, channels = ctx.lg, ctx.edge_mode, ctx.heads, ctx.channels
         dout = _f32(dout)
         E, T, D = q.shape[0], lg.T, heads * channels
@@ -189,13 +193,13 @@ class _SBFAttention(torch.autograd.Function):
         else:
             d_edge = None
         st = stream_ptr()
-        call("x2g_sbf_attention_bwd_dst", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(ctx.edge_row), mode, ptr(sbf),
-             ptr(w_sbf), ptr(b_sbf), ptr(lg.trip_rowptr), ptr(lg.trip_src), ptr(alpha), ptr(smax), ptr(sden),
-             ptr(dout), E, T, heads, channels, sbf.shape[1], ptr(dq), ptr(d_edge), ptr(dlogit), ptr(dproj), st)
+        call("x2g_sbf_attention_bwd_dst", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(ctx.edge_row), mode, ptr(sproj),
+             None, None, ptr(lg.trip_rowptr), ptr(lg.trip_src), ptr(alpha), ptr(smax), ptr(sden), ptr(dout), E, T,
+             heads, channels, D, ptr(dq), ptr(d_edge), ptr(dlogit), ptr(dproj), st)
         src_rowptr, src_perm = lg.src_csr()
-        call("x2g_sbf_attention_bwd_src", ptr(q), ptr(sbf), ptr(w_sbf), ptr(b_sbf), ptr(src_rowptr), ptr(src_perm),
-             ptr(lg.trip_dst), ptr(alpha), ptr(smax), ptr(sden), ptr(dlogit), ptr(dout), E, T, heads, channels,
-             sbf.shape[1], ptr(dk), ptr(dv), st)
+        call("x2g_sbf_attention_bwd_src", ptr(q), ptr(sproj), None, None, ptr(src_rowptr), ptr(src_perm),
+             ptr(lg.trip_dst), ptr(alpha), ptr(smax), ptr(sden), ptr(dlogit), ptr(dout), E, T, heads, channels, D,
+             ptr(dk), ptr(dv), st)
         if mode == EDGE_PER_DST and ctx.edge_row is not None:
             # rows of the edge table are shared by many destinations: sum d_edge per table row
             onehot = torch.nn.functional.one_hot(ctx.edge_row.long(), ctx.edge_shape[0]).to(torch.float32)
