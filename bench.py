@@ -77,7 +77,8 @@ class Trainer:
         self.bucket.zero()
         res = self.model(batch)
         loss = torch.nn.functional.smooth_l1_loss(res, batch.y)
-        loss.backward()
+        with ops.deferred_wgrad():  # all layers' weight-gradient slab sums in one launch
+            loss.backward()
         return loss
 
     def _update(self):

@@ -177,6 +177,32 @@ int x2g_linear_wgrad(const float* dy, const float* x, int64_t rows, int32_t out_
 /* flags of the *_ex gradient entry points */
 #define X2G_ACCUM_WGRAD 1 /* dw += ..., db += ... (write straight into a gradient buffer that already
                              holds a value, e.g. a zeroed flat all-reduce bucket) instead of dw = ... */
+#define X2G_DEFER_SLAB_SUM 2 /* leave the per-workgroup weight-gradient partials in the workspace and
+                                skip their fixed-order sum: the caller keeps the workspace alive and
+                                sums many layers' partials in one x2g_slab_sum_batch launch */
+
+/* One deferred weight-gradient reduction: dw[n_w] (+)= sum over `splits` slabs of part_w
+ * (slab s at part_w + s*n_w), likewise db[n_b] from part_b (part_b/db may be NULL). */
+typedef struct {
+  const float* part_w;
+  const float* part_b;
+  float* dw;
+  float* db;
+  int64_t n_w;
+  int32_t n_b;
+  int32_t splits;
+} x2g_slab_job;
+
+/* Sum the slabs of njobs deferred reductions (host array of jobs) in as few launches as
+ * possible; accum != 0: add into dw/db.  Same fixed order as the immediate sums. */
+int x2g_slab_sum_batch(const x2g_slab_job* jobs, int32_t njobs, int32_t accum, void* stream);
+
+/* Slab counts (and so the part_b offset, part_w + splits*n_w) of a deferred call. */
+int32_t x2g_linear_wgrad_splits(int64_t rows, int32_t out_features, int32_t in_features);
+int32_t x2g_dense_bwd_splits(int64_t rows, int32_t in_features, int32_t out_features);
+/* Byte offset of those slabs inside x2g_dense_bwd_ex's workspace (part_w = workspace + offset;
+ * x2g_linear_wgrad_ex's slabs start at its workspace). */
+int64_t x2g_dense_bwd_slab_offset(int64_t rows, int32_t in_features, int32_t out_features);
 
 /* x2g_linear_wgrad with flags (X2G_ACCUM_WGRAD). */
 int x2g_linear_wgrad_ex(const float* dy, const float* x, int64_t rows, int32_t out_features,

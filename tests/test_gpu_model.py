@@ -81,9 +81,16 @@ def test_bucket_gradients_equal_autograd(cuda):
     plain = [p.grad.detach().clone() if p.grad is not None else torch.zeros_like(p) for p in m.parameters()]
     m2 = product_model(z, cuda)
     bucket = GradBucket(m2.parameters())
-    for _ in range(2):  # the second pass checks that zero() + accumulate starts from scratch
+    from x2gnn import ops
+
+    for i in range(2):  # the second pass: zero() + accumulate starts from scratch, slab sums deferred
         bucket.zero()
-        torch.nn.functional.smooth_l1_loss(m2(b), b.y).backward()
+        loss = torch.nn.functional.smooth_l1_loss(m2(b), b.y)
+        if i == 0:
+            loss.backward()
+        else:
+            with ops.deferred_wgrad():
+                loss.backward()
     for p, g in zip(m2.parameters(), plain):
         assert torch.equal(p.grad, g)
 

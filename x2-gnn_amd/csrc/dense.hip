@@ -1074,8 +1074,10 @@ X2G_API int x2g_linear_wgrad_ex(const float* dy, const float* x, int64_t R, int3
 X2G_API int x2g_dense_bwd_ex(const float* dy, const float* z, int act, const float* x, const float* w, int64_t R,
                              int32_t K, int32_t N, float* dx, const float* dx_add, float* dw, float* db, int flags,
                              void* workspace, size_t workspace_bytes, void* stream) {
-  if (R < 0 || K <= 0 || N <= 0 || (act != kActNone && act != kActSilu) || !dw || (flags & ~X2G_ACCUM_WGRAD))
+  if (R < 0 || K <= 0 || N <= 0 || (act != kActNone && act != kActSilu) || !dw ||
+      (flags & ~(X2G_ACCUM_WGRAD | X2G_DEFER_SLAB_SUM)))
     return X2G_EINVAL;
+  if ((flags & X2G_DEFER_SLAB_SUM) && R == 0) return X2G_EINVAL;
   if (dx_add && !dx) return X2G_EINVAL;
   const bool accum = flags & X2G_ACCUM_WGRAD;
   hipStream_t st = as_stream(stream);
@@ -1101,6 +1103,7 @@ X2G_API int x2g_dense_bwd_ex(const float* dy, const float* z, int act, const flo
       dense_bwd_persist<64><<<grid, 512, 0, st>>>(dy, z, x, w, R, K, N, act, dx, dx_add, part_w, part_b);
     int rc = last_launch_status();
     if (rc) return rc;
+    if (flags & X2G_DEFER_SLAB_SUM) return X2G_OK;
     return sum_slabs_launch(part_w, static_cast<int64_t>(N) * K, part_b, N, grid, dw, db, accum, st);
   }
   // general shapes: dz = dy * act'(z) and dx = dz w in one kernel, then the weight gradient
@@ -1117,6 +1120,21 @@ X2G_API int x2g_dense_bwd_ex(const float* dy, const float* z, int act, const flo
   }
   return x2g_linear_wgrad_ex(dzp, x, R, N, K, dw, db, flags, static_cast<char*>(workspace) + dz_bytes,
                              workspace_bytes - dz_bytes, stream);
+}
+
+X2G_API int32_t x2g_linear_wgrad_splits(int64_t R, int32_t O, int32_t I);
+
+// slab count of a deferred x2g_dense_bwd_ex; the general path's slabs follow its dz buffer
+X2G_API int32_t x2g_dense_bwd_splits(int64_t R, int32_t K, int32_t N) {
+  if (R <= 0 || K <= 0 || N <= 0) return 0;
+  if (dense_persistent_bwd(R, K, N)) return static_cast<int32_t>(bwd_grid(R));
+  return x2g_linear_wgrad_splits(R, N, K);
+}
+
+// byte offset of the weight-gradient slabs inside x2g_dense_bwd_ex's workspace
+X2G_API int64_t x2g_dense_bwd_slab_offset(int64_t R, int32_t K, int32_t N) {
+  if (R <= 0 || K <= 0 || N <= 0 || dense_persistent_bwd(R, K, N)) return 0;
+  return static_cast<int64_t>(((static_cast<size_t>(R) * N * sizeof(float)) + 255) / 256 * 256);
 }
 
 X2G_API int x2g_dense_bwd(const float* dy, const float* z, int act, const float* x, const float* w, int64_t R,

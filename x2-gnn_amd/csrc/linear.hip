@@ -258,8 +258,9 @@ X2G_API size_t x2g_linear_wgrad_workspace(int64_t R, int32_t O, int32_t I) {
 
 X2G_API int x2g_linear_wgrad_ex(const float* dy, const float* x, int64_t R, int32_t O, int32_t I, float* dw,
                                 float* db, int flags, void* workspace, size_t workspace_bytes, void* stream) {
-  if (R < 0 || O <= 0 || I <= 0 || !dw || (flags & ~X2G_ACCUM_WGRAD)) return X2G_EINVAL;
+  if (R < 0 || O <= 0 || I <= 0 || !dw || (flags & ~(X2G_ACCUM_WGRAD | X2G_DEFER_SLAB_SUM))) return X2G_EINVAL;
   const bool accum = flags & X2G_ACCUM_WGRAD;
+  if ((flags & X2G_DEFER_SLAB_SUM) && R == 0) return X2G_EINVAL;  // nothing to defer: caller's bug
   hipStream_t st = as_stream(stream);
   if (R == 0) {
     if (accum) return X2G_OK;
@@ -290,7 +291,66 @@ X2G_API int x2g_linear_wgrad_ex(const float* dy, const float* x, int64_t R, int3
 #undef X2G_WGRAD
   int rc = last_launch_status();
   if (rc) return rc;
+  if (flags & X2G_DEFER_SLAB_SUM) return X2G_OK;
   return sum_slabs_launch(part, static_cast<int64_t>(O) * I, part_b, O, splits, dw, db, accum, st);
+}
+
+X2G_API int32_t x2g_linear_wgrad_splits(int64_t R, int32_t O, int32_t I) {
+  return (R > 0 && O > 0 && I > 0) ? wgrad_splits(R, O, I) : 0;
+}
+
+// ------------------------------------------------------------------------------ batched slab sums
+constexpr int kBatchJobs = 40;  // jobs per launch (kernel arguments, < 4 KB)
+
+struct SlabBatch {
+  const float* part[2 * kBatchJobs];  // job j: entry 2j = weight slabs, 2j+1 = bias slabs
+  float* out[2 * kBatchJobs];
+  int64_t n[2 * kBatchJobs];
+  int splits[kBatchJobs];
+  int block_end[2 * kBatchJobs];  // exclusive prefix of 64-element blocks
+  int nent;
+  int accum;
+};
+
+__global__ void __launch_bounds__(256) sum_slabs_batch(const SlabBatch b) {
+  __shared__ float red[4][64];
+  int ent = 0;
+  while (ent + 1 < b.nent && static_cast<int>(blockIdx.x) >= b.block_end[ent]) ++ent;  // block-uniform
+  const int first = ent ? b.block_end[ent - 1] : 0;
+  sum_slabs_block(b.part[ent], b.n[ent], b.splits[ent >> 1], blockIdx.x - first, b.accum != 0, b.out[ent], red);
+}
+
+X2G_API int x2g_slab_sum_batch(const x2g_slab_job* jobs, int32_t njobs, int32_t accum, void* stream) {
+  if (njobs < 0 || (njobs > 0 && !jobs)) return X2G_EINVAL;
+  hipStream_t st = as_stream(stream);
+  for (int j0 = 0; j0 < njobs; j0 += kBatchJobs) {
+    SlabBatch b{};
+    b.accum = accum;
+    int blocks = 0;
+    for (int j = j0; j < njobs && j < j0 + kBatchJobs; ++j) {
+      const x2g_slab_job& jb = jobs[j];
+      if (!jb.part_w || !jb.dw || jb.n_w <= 0 || jb.splits <= 0 || (jb.part_b && !jb.db)) return X2G_EINVAL;
+      const int k = j - j0;
+      b.splits[k] = jb.splits;
+      const int e0 = 2 * k, e1 = 2 * k + 1;
+      b.part[e0] = jb.part_w;
+      b.out[e0] = jb.dw;
+      b.n[e0] = jb.n_w;
+      blocks += static_cast<int>(blocks_for(jb.n_w, 64));
+      b.block_end[e0] = blocks;
+      b.part[e1] = jb.part_b;
+      b.out[e1] = jb.db;
+      b.n[e1] = (jb.part_b && jb.db) ? jb.n_b : 0;
+      blocks += static_cast<int>(blocks_for(b.n[e1], 64));
+      b.block_end[e1] = blocks;
+      b.nent = e1 + 1;
+    }
+    if (blocks == 0) continue;
+    sum_slabs_batch<<<blocks, 256, 0, st>>>(b);
+    const int rc = last_launch_status();
+    if (rc) return rc;
+  }
+  return X2G_OK;
 }
 
 X2G_API int x2g_linear_wgrad(const float* dy, const float* x, int64_t R, int32_t O, int32_t I, float* dw, float* db,

@@ -51,13 +51,19 @@ SIGNATURES = {
     "x2g_dense_bwd": [_P, _P, ctypes.c_int, _P, _P, _I64, _I32, _I32, _P, _P, _P, _P, _SZ, _P],
     "x2g_linear_wgrad_ex": [_P, _P, _I64, _I32, _I32, _P, _P, ctypes.c_int, _P, _SZ, _P],
     "x2g_optimizer_workspace": [_I64],
+    "x2g_slab_sum_batch": [_P, _I32, _I32, _P],
+    "x2g_linear_wgrad_splits": [_I64, _I32, _I32],
+    "x2g_dense_bwd_splits": [_I64, _I32, _I32],
+    "x2g_dense_bwd_slab_offset": [_I64, _I32, _I32],
     "x2g_sbf_project": [_P, _I64, _I32, _P, _P, _I32, _P, _P],
     "x2g_clip_adam_ema": [_P, _P, _P, _P, _P, _I64, _P, _P, _SZ, _P],
     "x2g_dense_bwd_ex": [_P, _P, ctypes.c_int, _P, _P, _I64, _I32, _I32, _P, _P, _P, _P, ctypes.c_int, _P, _SZ,
                          _P],
 }
 RESTYPES = {"x2g_status_string": ctypes.c_char_p, "x2g_vertex_to_edge_workspace": _SZ,
-            "x2g_linear_wgrad_workspace": _SZ, "x2g_dense_bwd_workspace": _SZ, "x2g_optimizer_workspace": _SZ}
+            "x2g_linear_wgrad_workspace": _SZ, "x2g_dense_bwd_workspace": _SZ, "x2g_optimizer_workspace": _SZ,
+            "x2g_linear_wgrad_splits": ctypes.c_int32, "x2g_dense_bwd_splits": ctypes.c_int32,
+            "x2g_dense_bwd_slab_offset": ctypes.c_int64}
 
 _lib = None
 

@@ -17,6 +17,9 @@ Operator                     replaces (reference / un-vendored dependency)
 """
 from __future__ import annotations
 
+import contextlib
+import ctypes
+
 import torch
 
 from . import _lib
@@ -234,6 +237,47 @@ def sbf_attention(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg: LineGraph, heads: 
 
 # ---------------------------------------------------------------------------------- dense layers
 ACCUM_WGRAD = 1  # X2G_ACCUM_WGRAD
+DEFER_SLAB_SUM = 2  # X2G_DEFER_SLAB_SUM
+
+
+class SlabJob(ctypes.Structure):
+    """x2g_slab_job (include/x2g.h)."""
+    _fields_ = [("part_w", ctypes.c_void_p), ("part_b", ctypes.c_void_p), ("dw", ctypes.c_void_p),
+                ("db", ctypes.c_void_p), ("n_w", ctypes.c_int64), ("n_b", ctypes.c_int32), ("splits", ctypes.c_int32)]
+
+
+class _SlabDeferral:
+    def __init__(self):
+        self.jobs = []
+        self.keep = []  # workspaces holding the partial slabs until the batched sum is enqueued
+
+
+_DEFER = None
+
+
+@contextlib.contextmanager
+def deferred_wgrad():
+    """Within this context, weight gradients that go straight into a gradient bucket
+    (``grad_sink``) leave their per-workgroup partial slabs in place; on exit ONE
+    x2g_slab_sum_batch launch sums every layer's slabs (instead of one small launch per layer)."""
+    global _DEFER
+    prev, _DEFER = _DEFER, _SlabDeferral()
+    try:
+        yield
+        d = _DEFER
+        if d.jobs:
+            arr = (SlabJob * len(d.jobs))(*d.jobs)
+            call("x2g_slab_sum_batch", ctypes.cast(arr, ctypes.c_void_p), len(d.jobs), 1, stream_ptr())
+    finally:
+        _DEFER = prev
+
+
+def _defer_job(ws, offset, splits, n_w, n_b, dw, db):
+    base = ws.data_ptr() + int(offset)
+    part_b = base + 4 * splits * n_w if db is not None else None
+    _DEFER.jobs.append(SlabJob(base, part_b, dw.data_ptr(), db.data_ptr() if db is not None else None, n_w,
+                               n_b if db is not None else 0, splits))
+    _DEFER.keep.append(ws)
 
 
 def grad_sink(param):
@@ -265,8 +309,11 @@ def linear_wgrad(dy, x, bias=True, dw_out=None, db_out=None):
     db = (db_out if accum else torch.empty(O, dtype=torch.float32, device=dy.device)) if bias else None
     ws_bytes = int(_lib.load().x2g_linear_wgrad_workspace(R, O, I))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dy.device)
-    call("x2g_linear_wgrad_ex", ptr(dy), ptr(x), R, O, I, ptr(dw), ptr(db), ACCUM_WGRAD if accum else 0, ptr(ws),
-         ws_bytes, stream_ptr())
+    defer = accum and _DEFER is not None and R > 0
+    flags = (ACCUM_WGRAD if accum else 0) | (DEFER_SLAB_SUM if defer else 0)
+    call("x2g_linear_wgrad_ex", ptr(dy), ptr(x), R, O, I, ptr(dw), ptr(db), flags, ptr(ws), ws_bytes, stream_ptr())
+    if defer:
+        _defer_job(ws, 0, int(_lib.load().x2g_linear_wgrad_splits(R, O, I)), O * I, O, dw, db)
     return (None, None) if accum else (dw, db)
 
 
@@ -311,10 +358,16 @@ class _DenseFn(torch.autograd.Function):
         else:
             dw = torch.empty(N, K, dtype=torch.float32, device=dev)
             db = torch.empty(N, dtype=torch.float32, device=dev) if ctx.has_bias else None
-        ws_bytes = int(_lib.load().x2g_dense_bwd_workspace(R, K, N))
+        lib = _lib.load()
+        ws_bytes = int(lib.x2g_dense_bwd_workspace(R, K, N))
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        defer = accum and _DEFER is not None and R > 0
+        flags = (ACCUM_WGRAD if accum else 0) | (DEFER_SLAB_SUM if defer else 0)
         call("x2g_dense_bwd_ex", ptr(gy2), ptr(z), ctx.act, ptr(x2), ptr(w), R, K, N, ptr(dx), None, ptr(dw),
-             ptr(db), ACCUM_WGRAD if accum else 0, ptr(ws), ws_bytes, stream_ptr())
+             ptr(db), flags, ptr(ws), ws_bytes, stream_ptr())
+        if defer:
+            _defer_job(ws, lib.x2g_dense_bwd_slab_offset(R, K, N), int(lib.x2g_dense_bwd_splits(R, K, N)), N * K, N,
+                       dw, db)
         dres = gy if ctx.has_res else None
         dx = dx.view(*ctx.lead, K) if need_x else None
         if accum:
