@@ -351,7 +351,7 @@ def test_linear_module_grads_match_torch(cuda):
         np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("R,K,N", [(21058, 128, 128), (3000, 338, 256), (2304, 128, 1), (777, 6, 128),
+@pytest.mark.parametrize("R,K,N", [(21058, 128, 128), (3000, 338, 256), (2304, 128, 1), (777, 6, 128), (21058, 6, 128), (5, 6, 128),
                                    (10, 128, 128), (500, 256, 128), (130, 42, 160)])
 @pytest.mark.parametrize("act", [0, 1])
 @pytest.mark.parametrize("with_res", [False, True])

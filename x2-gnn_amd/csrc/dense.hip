@@ -806,6 +806,114 @@ int dense_fwd_narrow_launch(const float* x, const float* w, const float* b, cons
   return last_launch_status();
 }
 
+// ---------------------------------------------------------------- backward, narrow input (K <= 8)
+// The radial-basis layers (lin_rbf: 6 -> 128, sbftransformer_conv.py:99, readout.py:38) have
+// almost no data gradient to compute: dx[r, 0:K] = dz[r, :] w[:, 0:K] is K dot products of
+// length N per row.  One wave per row (grid-stride): lane holds CPL = N/64 channels of dz,
+// forms its K partial products, and a 64-lane xor reduction leaves dx[r, k] in every lane;
+// dW[n, k] += dz[r, n] x[r, k] accumulates in registers (x row wave-uniform: scalar loads),
+// db[n] += dz[r, n].  Waves fold their partials through LDS into one slab per workgroup.
+template <int CPL, int KMAX>
+__global__ void __launch_bounds__(256) dense_bwd_narrow(const float* __restrict__ dY, const float* __restrict__ Zin,
+                                                        const float* __restrict__ X, const float* __restrict__ W,
+                                                        int64_t R, int K, int N, int act, float* __restrict__ dX,
+                                                        const float* __restrict__ dXadd, float* __restrict__ part_w,
+                                                        float* __restrict__ part_b) {
+  __shared__ float red[4][64 * CPL * (KMAX + 1)];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c0 = lane * CPL;
+  float wr[CPL][KMAX];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j)
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) wr[j][k] = (c0 + j < N && k < K) ? W[(c0 + j) * K + k] : 0.f;
+  float gw[CPL][KMAX], gb[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    gb[j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) gw[j][k] = 0.f;
+  }
+  // four rows per iteration (rows r, r + nw, r + 2nw, r + 3nw) so their loads are in flight together
+  constexpr int ROWS = 4;
+  const int64_t nw = static_cast<int64_t>(gridDim.x) * 4;
+  for (int64_t r0 = uniform(blockIdx.x * 4 + wave); r0 < R; r0 += ROWS * nw) {
+    float d[ROWS][CPL], xr[ROWS][KMAX];
+#pragma unroll
+    for (int u = 0; u < ROWS; ++u) {
+      const int64_t r = r0 + u * nw;
+      const bool rok = r < R;
+      const int64_t rc = rok ? r : R - 1;
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) {
+        const bool ok = rok && c0 + j < N;
+        float v = dY[rc * N + (c0 + j < N ? c0 + j : N - 1)];
+        if (act == kActSilu) {
+          const float z = Zin[rc * N + (c0 + j < N ? c0 + j : N - 1)];
+          const float sg = 1.0f / (1.0f + expf(-z));
+          v *= sg * (1.0f + z * (1.0f - sg));
+        }
+        d[u][j] = ok ? v : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) xr[u][k] = (k < K) ? keep(X[rc * K + (k < K ? k : 0)], rok) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < ROWS; ++u) {
+      const int64_t r = r0 + u * nw;
+      float px[KMAX];
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        float acc = 0.f;
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+          acc = fmaf(d[u][j], wr[j][k], acc);
+          gw[j][k] = fmaf(d[u][j], xr[u][k], gw[j][k]);
+        }
+        px[k] = group_sum<64>(acc);
+      }
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) gb[j] += d[u][j];
+      if (dX && lane < K && r < R) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) v = lane == k ? px[k] : v;
+        if (dXadd) v += dXadd[r * K + lane];
+        dX[r * K + lane] = v;
+      }
+    }
+  }
+  // fold the 4 waves (fixed order) and write this workgroup's slab
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) red[wave][(c0 + j) * (KMAX + 1) + k] = gw[j][k];
+    red[wave][(c0 + j) * (KMAX + 1) + KMAX] = gb[j];
+  }
+  __syncthreads();
+  if (wave == 0) {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int n = c0 + j;
+      if (n >= N) continue;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        const int o = n * (KMAX + 1) + k;
+        if (k < K) part_w[static_cast<int64_t>(blockIdx.x) * N * K + n * K + k] =
+            ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
+      }
+      const int o = n * (KMAX + 1) + KMAX;
+      if (part_b) part_b[static_cast<int64_t>(blockIdx.x) * N + n] = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
+    }
+  }
+}
+
+constexpr int kNarrowBwdGrid = 512;
+
+static inline bool dense_narrow_bwd(int64_t R, int32_t K, int32_t N) {
+  return R > 0 && K <= 8 && N <= 128 && N > 64 && N % 64 == 0;
+}
+
 // ---------------------------------------------------------------- backward, v5 (default)
 // dense_bwd_persist restructured like dense_fwd_v5 (K % 4 == 0, N % 4 == 0, 16-byte aligned):
 //   * dy, z, x tiles (64 rows) are read with 16-byte loads (4 per thread per matrix instead of
@@ -1057,8 +1165,15 @@ static inline bool dense_persistent_bwd(int64_t R, int32_t K, int32_t N) {
   return K <= 128 && N <= 128 && R > 0 && R * 128 < (int64_t(1) << 31);  // 32-bit offsets inside
 }
 
+static inline int64_t narrow_bwd_grid(int64_t R) {
+  const int64_t want = (R + 15) / 16;  // >= 4 rows per wave
+  return want < kNarrowBwdGrid ? (want > 0 ? want : 1) : kNarrowBwdGrid;
+}
+
 X2G_API size_t x2g_dense_bwd_workspace(int64_t R, int32_t K, int32_t N) {
   if (R <= 0 || K <= 0 || N <= 0) return 0;
+  if (dense_narrow_bwd(R, K, N))
+    return static_cast<size_t>(narrow_bwd_grid(R)) * (static_cast<int64_t>(N) * K + N) * sizeof(float);
   if (dense_persistent_bwd(R, K, N)) {
     const int64_t g = bwd_grid(R);
     return static_cast<size_t>(g) * (static_cast<int64_t>(N) * K + N) * sizeof(float);
@@ -1089,6 +1204,19 @@ X2G_API int x2g_dense_bwd_ex(const float* dy, const float* z, int act, const flo
   }
   if (!dy || !x || !w || (act == kActSilu && !z)) return X2G_EINVAL;
   if (!workspace || workspace_bytes < x2g_dense_bwd_workspace(R, K, N)) return X2G_EWORKSPACE;
+  if (dense_narrow_bwd(R, K, N)) {
+    const int grid = static_cast<int>(narrow_bwd_grid(R));
+    float* part_w = static_cast<float*>(workspace);
+    float* part_b = db ? part_w + static_cast<int64_t>(grid) * N * K : nullptr;
+    if (N == 128)
+      dense_bwd_narrow<2, 8><<<grid, 256, 0, st>>>(dy, z, x, w, R, K, N, act, dx, dx_add, part_w, part_b);
+    else
+      dense_bwd_narrow<1, 8><<<grid, 256, 0, st>>>(dy, z, x, w, R, K, N, act, dx, dx_add, part_w, part_b);
+    int rc = last_launch_status();
+    if (rc) return rc;
+    if (flags & X2G_DEFER_SLAB_SUM) return X2G_OK;
+    return sum_slabs_launch(part_w, static_cast<int64_t>(N) * K, part_b, N, grid, dw, db, accum, st);
+  }
   if (dense_persistent_bwd(R, K, N)) {
     const int grid = static_cast<int>(bwd_grid(R));
     float* part_w = static_cast<float*>(workspace);
@@ -1127,6 +1255,7 @@ X2G_API int32_t x2g_linear_wgrad_splits(int64_t R, int32_t O, int32_t I);
 // slab count of a deferred x2g_dense_bwd_ex; the general path's slabs follow its dz buffer
 X2G_API int32_t x2g_dense_bwd_splits(int64_t R, int32_t K, int32_t N) {
   if (R <= 0 || K <= 0 || N <= 0) return 0;
+  if (dense_narrow_bwd(R, K, N)) return static_cast<int32_t>(narrow_bwd_grid(R));
   if (dense_persistent_bwd(R, K, N)) return static_cast<int32_t>(bwd_grid(R));
   return x2g_linear_wgrad_splits(R, N, K);
 }

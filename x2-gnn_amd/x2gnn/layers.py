@@ -187,6 +187,8 @@ class ResidualLayer(nn.Module):
         self.AF = nn.SiLU()
 
     def forward(self, x):
+        if x.is_cuda:  # both dense kernels + a backward that folds the residual into dx
+            return ops.residual_layer(x, self.lin0.weight, self.lin0.bias, self.lin1.weight, self.lin1.bias)
         h = self.lin0.fused(x, act=ops.ACT_SILU)
         return self.lin1.fused(h, act=ops.ACT_SILU, res=x)
 

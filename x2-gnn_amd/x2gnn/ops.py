@@ -320,22 +320,64 @@ def linear_wgrad(dy, x, bias=True, dw_out=None, db_out=None):
 ACT_NONE, ACT_SILU = 0, 1
 
 
+def _dense_fwd_raw(x2, w, b, act, r2=None, want_z=True):
+    """y (and z = pre-activation, when act != none and want_z) for row-major x2 [R, K]."""
+    N, K = w.shape
+    R = x2.shape[0]
+    y = torch.empty(R, N, dtype=torch.float32, device=x2.device)
+    z = torch.empty(R, N, dtype=torch.float32, device=x2.device) if (act != ACT_NONE and want_z) else None
+    call("x2g_dense_fwd", ptr(x2), ptr(w), ptr(b), R, K, N, act, ptr(r2), ptr(y), ptr(z), stream_ptr())
+    return y, z
+
+
+def _dense_bwd_raw(gy2, z, act, x2, w, w_param, b_param, has_bias, need_dx, dx_add=None, dx_out=None):
+    """Fused backward of one dense layer: returns (dx or None, dw or None, db or None).
+
+    dx = dz W (+ dx_add; dx_out may alias dx_add for an in-place accumulation).  Weight grads go
+    straight into the flat gradient bucket when the parameters are bucket-backed (grad_sink; then
+    (None, None) is returned for them), with their slab sums deferred inside deferred_wgrad()."""
+    N, K = w.shape
+    R = gy2.shape[0]
+    dev = gy2.device
+    dx = None
+    if need_dx or act != ACT_NONE or dx_add is not None:
+        dx = dx_out if dx_out is not None else torch.empty(R, K, dtype=torch.float32, device=dev)
+    gw = grad_sink(w_param)
+    gb = grad_sink(b_param) if has_bias else None
+    accum = gw is not None and (gb is not None or not has_bias)
+    if accum:
+        dw, db = gw, gb
+    else:
+        dw = torch.empty(N, K, dtype=torch.float32, device=dev)
+        db = torch.empty(N, dtype=torch.float32, device=dev) if has_bias else None
+    lib = _lib.load()
+    ws_bytes = int(lib.x2g_dense_bwd_workspace(R, K, N))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    defer = accum and _DEFER is not None and R > 0
+    flags = (ACCUM_WGRAD if accum else 0) | (DEFER_SLAB_SUM if defer else 0)
+    call("x2g_dense_bwd_ex", ptr(gy2), ptr(z), act, ptr(x2), ptr(w), R, K, N, ptr(dx), ptr(dx_add), ptr(dw), ptr(db),
+         flags, ptr(ws), ws_bytes, stream_ptr())
+    if defer:
+        _defer_job(ws, lib.x2g_dense_bwd_slab_offset(R, K, N), int(lib.x2g_dense_bwd_splits(R, K, N)), N * K, N, dw,
+                   db)
+    if accum:
+        return dx, None, None
+    return dx, dw, db
+
+
 class _DenseFn(torch.autograd.Function):
-    """y = act(x W^T + b) (+ res) in one kernel; backward = one data-gradient kernel (with the
-    activation derivative fused) + the row-split weight-gradient kernel."""
+    """y = act(x W^T + b) (+ res) in one kernel; backward = one fused kernel (activation
+    derivative, data gradient, per-workgroup weight-gradient partials) + a fixed-order slab sum."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, res, act):
         N, K = weight.shape
         lead = x.shape[:-1]
         x2 = _f32(x.reshape(-1, K))
-        R = x2.shape[0]
         w = _f32(weight)
         b = _f32(bias) if bias is not None else None
         r2 = _f32(res.reshape(-1, N)) if res is not None else None
-        y = torch.empty(R, N, dtype=torch.float32, device=x.device)
-        z = torch.empty(R, N, dtype=torch.float32, device=x.device) if act != ACT_NONE else None
-        call("x2g_dense_fwd", ptr(x2), ptr(w), ptr(b), R, K, N, act, ptr(r2), ptr(y), ptr(z), stream_ptr())
+        y, z = _dense_fwd_raw(x2, w, b, act, r2)
         ctx.save_for_backward(x2, w, z)
         ctx.act, ctx.has_bias, ctx.has_res, ctx.lead = act, bias is not None, res is not None, lead
         ctx.w_param, ctx.b_param = weight, bias
@@ -345,34 +387,95 @@ class _DenseFn(torch.autograd.Function):
     def backward(ctx, gy):
         x2, w, z = ctx.saved_tensors
         N, K = w.shape
-        gy2 = _f32(gy.reshape(-1, N))
-        R = gy2.shape[0]
-        dev = gy.device
         need_x = ctx.needs_input_grad[0]
-        dx = torch.empty(R, K, dtype=torch.float32, device=dev) if (need_x or ctx.act != ACT_NONE) else None
-        gw = grad_sink(ctx.w_param)
-        gb = grad_sink(ctx.b_param) if ctx.has_bias else None
-        accum = gw is not None and (gb is not None or not ctx.has_bias)
-        if accum:  # summed straight into the flat gradient bucket; autograd gets None
-            dw, db = gw, gb
-        else:
-            dw = torch.empty(N, K, dtype=torch.float32, device=dev)
-            db = torch.empty(N, dtype=torch.float32, device=dev) if ctx.has_bias else None
-        lib = _lib.load()
-        ws_bytes = int(lib.x2g_dense_bwd_workspace(R, K, N))
-        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-        defer = accum and _DEFER is not None and R > 0
-        flags = (ACCUM_WGRAD if accum else 0) | (DEFER_SLAB_SUM if defer else 0)
-        call("x2g_dense_bwd_ex", ptr(gy2), ptr(z), ctx.act, ptr(x2), ptr(w), R, K, N, ptr(dx), None, ptr(dw),
-             ptr(db), flags, ptr(ws), ws_bytes, stream_ptr())
-        if defer:
-            _defer_job(ws, lib.x2g_dense_bwd_slab_offset(R, K, N), int(lib.x2g_dense_bwd_splits(R, K, N)), N * K, N,
-                       dw, db)
+        dx, dw, db = _dense_bwd_raw(_f32(gy.reshape(-1, N)), z, ctx.act, x2, w, ctx.w_param, ctx.b_param,
+                                    ctx.has_bias, need_x)
         dres = gy if ctx.has_res else None
         dx = dx.view(*ctx.lead, K) if need_x else None
-        if accum:
-            return dx, None, None, dres, None
         return dx, dw, db, dres, None
+
+
+class _ResidualFn(torch.autograd.Function):
+    """ResidualLayer (residual_layer.py:21-27): y = x + SiLU(W1 SiLU(W0 x + b0) + b1), forward as
+    two fused dense kernels; the backward's residual term is folded into the second data
+    gradient (dx = dz0 W0 + gy via x2g_dense_bwd_ex's dx_add) instead of an autograd add."""
+
+    @staticmethod
+    def forward(ctx, x, w0, b0, w1, b1):
+        D = x.shape[-1]
+        lead = x.shape[:-1]
+        x2 = _f32(x.reshape(-1, D))
+        W0, W1 = _f32(w0), _f32(w1)
+        B0 = _f32(b0) if b0 is not None else None
+        B1 = _f32(b1) if b1 is not None else None
+        h, z0 = _dense_fwd_raw(x2, W0, B0, ACT_SILU)
+        y, z1 = _dense_fwd_raw(h, W1, B1, ACT_SILU, r2=x2)
+        ctx.save_for_backward(x2, h, z0, z1, W0, W1)
+        ctx.params = (w0, b0, w1, b1)
+        ctx.lead = lead
+        return y.view(*lead, W1.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, h, z0, z1, W0, W1 = ctx.saved_tensors
+        w0, b0, w1, b1 = ctx.params
+        gy2 = _f32(gy.reshape(-1, W1.shape[0]))
+        dh, dw1, db1 = _dense_bwd_raw(gy2, z1, ACT_SILU, h, W1, w1, b1, b1 is not None, True)
+        dx, dw0, db0 = _dense_bwd_raw(dh, z0, ACT_SILU, x2, W0, w0, b0, b0 is not None, True, dx_add=gy2)
+        return dx.view(*ctx.lead, W0.shape[1]), dw0, db0, dw1, db1
+
+
+def residual_layer(x, w0, b0, w1, b1):
+    if not x.is_cuda:
+        raise RuntimeError("x2gnn device ops need GPU tensors (no CPU fallback by design)")
+    return _ResidualFn.apply(x, w0, b0, w1, b1)
+
+
+class _ConvProjFn(torch.autograd.Function):
+    """The dense projections of SBFTransformerConv.forward (sbftransformer_conv.py:99-107,127):
+    rf = lin_rbf(rbf), x_src = x * rf, q = lin_query(x), k = lin_key(x_src), v = lin_value(x_src),
+    skip = lin_skip(x).  The backward chains the four data gradients into one buffer per input
+    (x2g_dense_bwd_ex dx_add, in place) instead of summing them with autograd adds."""
+
+    @staticmethod
+    def forward(ctx, x, rbf, wr, wq, bq, wk, bk, wv, bv, ws, bs):
+        E, D = x.shape
+        x2, rbf2 = _f32(x), _f32(rbf)
+        Wr, Wq, Wk, Wv, Ws = (_f32(t) for t in (wr, wq, wk, wv, ws))
+        Bq, Bk, Bv, Bs = (_f32(t) if t is not None else None for t in (bq, bk, bv, bs))
+        rf, _ = _dense_fwd_raw(rbf2, Wr, None, ACT_NONE)
+        xs = x2 * rf
+        q, _ = _dense_fwd_raw(x2, Wq, Bq, ACT_NONE)
+        k, _ = _dense_fwd_raw(xs, Wk, Bk, ACT_NONE)
+        v, _ = _dense_fwd_raw(xs, Wv, Bv, ACT_NONE)
+        skip, _ = _dense_fwd_raw(x2, Ws, Bs, ACT_NONE)
+        ctx.save_for_backward(x2, rbf2, rf, xs, Wr, Wq, Wk, Wv, Ws)
+        ctx.params = (wr, wq, bq, wk, bk, wv, bv, ws, bs)
+        return q, k, v, skip
+
+    @staticmethod
+    def backward(ctx, gq, gk, gv, gskip):
+        x2, rbf2, rf, xs, Wr, Wq, Wk, Wv, Ws = ctx.saved_tensors
+        wr, wq, bq, wk, bk, wv, bv, ws, bs = ctx.params
+        g = [_f32(t) if t is not None else torch.zeros_like(x2) for t in (gq, gk, gv, gskip)]
+        gxs, dwk, dbk = _dense_bwd_raw(g[1], None, ACT_NONE, xs, Wk, wk, bk, bk is not None, True)
+        gxs, dwv, dbv = _dense_bwd_raw(g[2], None, ACT_NONE, xs, Wv, wv, bv, bv is not None, True, dx_add=gxs,
+                                       dx_out=gxs)
+        grf = gxs * x2  # d rf
+        gx = gxs * rf   # x_src = x * rf
+        gx, dwq, dbq = _dense_bwd_raw(g[0], None, ACT_NONE, x2, Wq, wq, bq, bq is not None, True, dx_add=gx,
+                                      dx_out=gx)
+        gx, dws, dbs = _dense_bwd_raw(g[3], None, ACT_NONE, x2, Ws, ws, bs, bs is not None, True, dx_add=gx,
+                                      dx_out=gx)
+        need_rbf = ctx.needs_input_grad[1]
+        grbf, dwr, _ = _dense_bwd_raw(grf, None, ACT_NONE, rbf2, Wr, wr, None, False, need_rbf)
+        return gx, (grbf if need_rbf else None), dwr, dwq, dbq, dwk, dbk, dwv, dbv, dws, dbs
+
+
+def conv_projections(x, rbf, wr, wq, bq, wk, bk, wv, bv, ws, bs):
+    if not x.is_cuda:
+        raise RuntimeError("x2gnn device ops need GPU tensors (no CPU fallback by design)")
+    return _ConvProjFn.apply(x, rbf, wr, wq, bq, wk, bk, wv, bv, ws, bs)
 
 
 def dense(x, weight, bias=None, act=ACT_NONE, res=None):

@@ -58,11 +58,18 @@ class SBFTransformerConv(nn.Module):
         H, C = self.heads, self.out_channels
         if self.training and self.dropout > 0:
             raise NotImplementedError("attention dropout is not compiled (X2-GNN uses dropout=0)")
-        x_src = x * self.lin_rbf(rbf)
-        q = self.lin_query(x)
-        k = self.lin_key(x_src)
-        v = self.lin_value(x_src)
-        skip = self.lin_skip(x) if self.root_weight else torch.zeros_like(q)
+        if x.is_cuda and self.root_weight and x.dim() == 2:
+            # one autograd node for the five projections: the backward chains the data
+            # gradients into one buffer per input instead of autograd adds
+            q, k, v, skip = ops.conv_projections(
+                x, rbf, self.lin_rbf.weight, self.lin_query.weight, self.lin_query.bias, self.lin_key.weight,
+                self.lin_key.bias, self.lin_value.weight, self.lin_value.bias, self.lin_skip.weight, self.lin_skip.bias)
+        else:
+            x_src = x * self.lin_rbf(rbf)
+            q = self.lin_query(x)
+            k = self.lin_key(x_src)
+            v = self.lin_value(x_src)
+            skip = self.lin_skip(x) if self.root_weight else torch.zeros_like(q)
         if line_graph is None:
             if edge_index.numel() > 1 and bool((edge_index[1, 1:] < edge_index[1, :-1]).any()):
                 raise ValueError("triplet edge_index[1] must be sorted ascending (vertex_to_edge_2 order)")
