@@ -40,10 +40,11 @@ for R in (32, 8192, 21058, 65536, 262144):
     wsb = lib.x2g_dense_bwd_workspace(R, K, N)
     ws = torch.empty(max(wsb, 4) // 4 + 1, device=dev)
     fwd_v = []
-    for v in (1, 0):
-        lib.x2g_tuning(0, v)
+    for v in (1, 0):  # key 3: 1 = v5, 0 = v6 (default)
+        lib.x2g_tuning(3, v)
         fwd_v.append(t(lambda: call("x2g_dense_fwd", ptr(x), ptr(w), ptr(b), R, K, N, 1, ptr(res), ptr(y), ptr(z),
                                     stream_ptr())))
+    lib.x2g_tuning(3, 0)
     fwd = fwd_v[-1]
     bwd = t(lambda: call("x2g_dense_bwd", ptr(dy), ptr(z), 1, ptr(x), ptr(w), R, K, N, ptr(dx), ptr(dw), ptr(db),
                          ptr(ws), wsb, stream_ptr()))
@@ -51,6 +52,6 @@ for R in (32, 8192, 21058, 65536, 262144):
     err = float((y - ref).abs().max())
     gemm = t(lambda: torch.nn.functional.linear(x, w, b))
     fl = 2 * R * K * N
-    print(f"R={R:7d} fwd(v1) {fwd_v[0]:8.1f}us fwd {fwd:8.1f}us ({fl / fwd / 1e6:6.1f} TF/s, {4 * R * (K + 3 * N) / fwd / 1e3:6.0f} GB/s) "
+    print(f"R={R:7d} fwd(v5) {fwd_v[0]:8.1f}us fwd(v6) {fwd:8.1f}us ({fl / fwd / 1e6:6.1f} TF/s, {4 * R * (K + 3 * N) / fwd / 1e3:6.0f} GB/s) "
           f"bwd {bwd:8.1f}us ({2 * fl / bwd / 1e6:6.1f} TF/s) | torch linear {gemm:7.1f}us | err {err:.1e}",
           flush=True)

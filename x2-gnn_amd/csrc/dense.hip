@@ -713,6 +713,124 @@ __global__ void __launch_bounds__(512) dense_bwd_persist(const float* __restrict
   if (part_b && tid < N) part_b[static_cast<int64_t>(blockIdx.x) * N + tid] = bsum;
 }
 
+// ---------------------------------------------------------------- forward, v6: two workgroups per CU
+// 4 waves and 80 KB of LDS per workgroup (weight 64 KB + one 32-row x tile 16 KB), so two
+// workgroups share a CU and one multiplies while the other loads / stores: at 21k rows the
+// busiest CU then holds 3 tiles of 32 rows instead of 2 pairs of 64 (v5).  The weight slot
+// layout is unpadded with an XOR swizzle instead: B[c(s,h)][j] at s*256 + 2 (j ^ (s & 31)) + h
+// (staging writes 2-way, B reads conflict-free).
+__device__ __forceinline__ int wswz(int s, int j, int h) { return s * 256 + 2 * (j ^ (s & 31)) + h; }
+
+__device__ __forceinline__ void xtile_load(const float* __restrict__ X, int64_t t, int64_t R, int K, Stage4& st) {
+  const int kc = K >> 2, q = threadIdx.x & 31, qc = 4 * (q < kc ? q : kc - 1);
+  const int rmax = static_cast<int>(R) - 1, r0 = static_cast<int>(t) * 32 + (threadIdx.x >> 5);
+  const int ra = r0 < rmax ? r0 : rmax, rb = r0 + 8 < rmax ? r0 + 8 : rmax;
+  const int rc = r0 + 16 < rmax ? r0 + 16 : rmax, rd = r0 + 24 < rmax ? r0 + 24 : rmax;
+  st.v0 = *reinterpret_cast<const f4*>(X + ra * K + qc);
+  st.v1 = *reinterpret_cast<const f4*>(X + rb * K + qc);
+  st.v2 = *reinterpret_cast<const f4*>(X + rc * K + qc);
+  st.v3 = *reinterpret_cast<const f4*>(X + rd * K + qc);
+}
+
+__device__ __forceinline__ void xtile_store(float* __restrict__ buf, const Stage4& st) {
+  const int q = threadIdx.x & 31, row = threadIdx.x >> 5;  // rows row, +8, +16, +24 (row & 15 differs by 8)
+  *reinterpret_cast<f4*>(buf + row * 128 + 4 * (q ^ (row & 15))) = st.v0;
+  *reinterpret_cast<f4*>(buf + (row + 8) * 128 + 4 * (q ^ ((row + 8) & 15))) = st.v1;
+  *reinterpret_cast<f4*>(buf + (row + 16) * 128 + 4 * (q ^ ((row + 16) & 15))) = st.v2;
+  *reinterpret_cast<f4*>(buf + (row + 24) * 128 + 4 * (q ^ ((row + 24) & 15))) = st.v3;
+}
+
+template <int U>
+__device__ __forceinline__ void epi_tile(const float* __restrict__ buf, const Stage4& rres, f4 b4, int64_t t,
+                                         int64_t R, int N, int act, float* __restrict__ Y, float* __restrict__ Z) {
+  const int q = threadIdx.x & 31, row = (threadIdx.x >> 5) + 8 * U;
+  const int r = static_cast<int>(t) * 32 + row;
+  const f4 zc = *reinterpret_cast<const f4*>(buf + row * 128 + 4 * (q ^ (row & 15))) + b4;
+  const f4 rr = st_get<U>(rres);
+  f4 yv;
+  yv.x = act_apply(zc.x, act) + rr.x;
+  yv.y = act_apply(zc.y, act) + rr.y;
+  yv.z = act_apply(zc.z, act) + rr.z;
+  yv.w = act_apply(zc.w, act) + rr.w;
+  if (r < R && 4 * q < N) {
+    if (Z) *reinterpret_cast<f4*>(Z + r * N + 4 * q) = zc;
+    *reinterpret_cast<f4*>(Y + r * N + 4 * q) = yv;
+  }
+}
+
+__global__ void __launch_bounds__(256, 2) dense_fwd_v6(const float* __restrict__ X, const float* __restrict__ W,
+                                                       const float* __restrict__ bias, const float* __restrict__ res,
+                                                       int64_t R, int K, int N, int act, float* __restrict__ Y,
+                                                       float* __restrict__ Z) {
+  __shared__ __attribute__((aligned(16))) float Ws[64 * 256];
+  __shared__ __attribute__((aligned(16))) float Xs[32 * 128];  // x tile, then the output tile
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, i = lane & 31;
+  const int n = 32 * wave + i;
+  const int q = tid & 31;
+  const int64_t ntiles = (R + 31) / 32;
+  const int64_t G = gridDim.x;
+  f4 b4 = {0.f, 0.f, 0.f, 0.f};
+  if (bias && 4 * q < N) b4 = f4{bias[4 * q], bias[4 * q + 1], bias[4 * q + 2], bias[4 * q + 3]};
+  int64_t t = blockIdx.x;
+  {
+    Stage4 first;
+    xtile_load(X, t, R, K, first);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {  // weight in two halves of 32 loads per thread
+      float v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {
+        const int idx = tid + 256 * (32 * half + u), nn = idx >> 7, k = idx & 127;
+        const float x = ld_pin(W + (nn < N ? nn : N - 1) * K + (k < K ? k : K - 1));
+        v[u] = (nn < N && k < K) ? x : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {
+        const int idx = tid + 256 * (32 * half + u), nn = idx >> 7, k = idx & 127;
+        Ws[wswz(k & 63, nn, k >> 6)] = v[u];
+      }
+    }
+    xtile_store(Xs, first);
+    __syncthreads();
+  }
+  for (; t < ntiles; t += G) {
+    const bool more = t + G < ntiles;
+    Stage4 rres{}, nxt;
+    if (res) xtile_load(res, t, R, N, rres);  // first: waiting for it never drains the prefetch
+    if (more) xtile_load(X, t + G, R, K, nxt);
+    floatx16 acc0, acc1;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      acc0[j] = 0.f;
+      acc1[j] = 0.f;
+    }
+    const float* xs = Xs + i * 128;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const f4 a = *reinterpret_cast<const f4*>(xs + 4 * ((16 * h + g) ^ (i & 15)));
+      const int s = 4 * g;
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, Ws[wswz(s, n, h)], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, Ws[wswz(s + 1, n, h)], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, Ws[wswz(s + 2, n, h)], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, Ws[wswz(s + 3, n, h)], acc1, 0, 0, 0);
+    }
+    __syncthreads();  // the x tile is consumed: the buffer stages the output
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int r = (j & 3) + 8 * (j >> 2) + 4 * h;
+      Xs[r * 128 + 4 * ((n >> 2) ^ (r & 15)) + (n & 3)] = acc0[j] + acc1[j];
+    }
+    __syncthreads();
+    epi_tile<0>(Xs, rres, b4, t, R, N, act, Y, Z);
+    epi_tile<1>(Xs, rres, b4, t, R, N, act, Y, Z);
+    epi_tile<2>(Xs, rres, b4, t, R, N, act, Y, Z);
+    epi_tile<3>(Xs, rres, b4, t, R, N, act, Y, Z);
+    __syncthreads();
+    if (more) xtile_store(Xs, nxt);
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------- forward, narrow K (K % 4 != 0)
 // For rows too narrow / odd for 16-byte row chunks (lin_sbf: K = 42): a 64-row tile pair is one
 // contiguous span of 64*K floats, read with 16-byte loads regardless of K and scattered into
@@ -1104,8 +1222,14 @@ X2G_API int x2g_dense_fwd(const float* x, const float* w, const float* b, int64_
     else if (!vec && variant == 0 && K % 4 != 0 && N % 4 == 0 && aligned16(x) && aligned16(y) && aligned16(z) &&
              aligned16(res))
       return dense_fwd_narrow_launch(x, w, b, res, R, K, N, act, y, z, st);
-    else if (vec && variant == 0 && N % 4 == 0 && aligned16(y) && aligned16(z) && aligned16(res))
-      dense_fwd_v5<<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
+    else if (vec && variant == 0 && N % 4 == 0 && aligned16(y) && aligned16(z) && aligned16(res)) {
+      if (tuning(kTuneDenseDbg) == 0) {  // v6 (default); knob 3 = 1 selects v5
+        const unsigned g6 = static_cast<unsigned>(ntiles < 512 ? ntiles : 512);
+        dense_fwd_v6<<<g6, 256, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
+      } else {
+        dense_fwd_v5<<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
+      }
+    }
     else if (vec && variant == 0)
       switch (tuning(kTuneDenseDbg)) {
         case 1: dense_fwd_staged<1><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z); break;

@@ -79,6 +79,10 @@ def load():
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = RESTYPES.get(name, ctypes.c_int)
+        # kernel-variant knobs for A/B measurements: X2G_TUNE="key=value,key=value"
+        for kv in filter(None, os.environ.get("X2G_TUNE", "").split(",")):
+            key, value = kv.split("=")
+            lib.x2g_tuning(int(key), int(value))
         _lib = lib
     return _lib
 
