@@ -292,6 +292,158 @@ __global__ void __launch_bounds__(kLnThreads) graph_ln_bwd_kernel(const float* _
   for (int64_t i = threadIdx.x; i < M; i += kLnThreads) xs[i] = r * (gs[i] - m1 - ys[i] * m2);
 }
 
+// Register-resident graph LayerNorm for segments of up to 1024 * CAP float4 (a QM9 molecule:
+// ~165 line nodes x 128 = 5.3k float4, CAP = 8): one 1024-thread block per molecule reads its
+// rows ONCE into registers (16-byte loads, all in flight together), then the mean, the centred
+// variance and the output come from registers — same two-pass arithmetic as graph_ln_fwd_kernel.
+// Larger segments take the looping kernels above.
+constexpr int kLnBig = 1024;
+
+__device__ __forceinline__ float block_sum_big(float v, float* lds) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  if (lane == 0) lds[wave] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int w = 0; w < kLnBig / 64; ++w) s += lds[w];
+  __syncthreads();
+  return s;
+}
+
+template <int CAP>
+__global__ void __launch_bounds__(kLnBig) graph_ln_fwd_reg(const float4* __restrict__ x, const int32_t* __restrict__ rowptr,
+                                                           int64_t D4, float eps, float4* __restrict__ out,
+                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  __shared__ float lds[kLnBig / 64];
+  const int64_t g = blockIdx.x;
+  const int64_t r0 = rowptr[g], r1 = rowptr[g + 1];
+  const int64_t M4 = (r1 - r0) * D4;
+  const float norm = static_cast<float>((r1 > r0 ? r1 - r0 : 1) * D4 * 4);
+  const float4* xs = x + r0 * D4;
+  float4* os = out + r0 * D4;
+  if (M4 > static_cast<int64_t>(kLnBig) * CAP) {  // too big for registers: three sweeps
+    float s = 0.f;
+    for (int64_t i = threadIdx.x; i < M4; i += kLnBig) s += (xs[i].x + xs[i].y) + (xs[i].z + xs[i].w);
+    const float mu = block_sum_big(s, lds) / norm;
+    float q = 0.f;
+    for (int64_t i = threadIdx.x; i < M4; i += kLnBig) {
+      const float4 t = xs[i];
+      const float a = t.x - mu, b = t.y - mu, c = t.z - mu, d = t.w - mu;
+      q += (a * a + b * b) + (c * c + d * d);
+    }
+    const float denom = sqrtf(block_sum_big(q, lds) / norm + eps);
+    for (int64_t i = threadIdx.x; i < M4; i += kLnBig) {
+      const float4 t = xs[i];
+      os[i] = make_float4((t.x - mu) / denom, (t.y - mu) / denom, (t.z - mu) / denom, (t.w - mu) / denom);
+    }
+    if (threadIdx.x == 0) {
+      if (mean_out) mean_out[g] = mu;
+      rstd_out[g] = 1.0f / denom;
+    }
+    return;
+  }
+  float4 v[CAP];
+  float sum = 0.f;
+#pragma unroll
+  for (int u = 0; u < CAP; ++u) {
+    const int64_t i = threadIdx.x + static_cast<int64_t>(kLnBig) * u;
+    const bool ok = i < M4;
+    const float4 t = xs[ok ? i : 0];
+    v[u] = ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int u = 0; u < CAP; ++u) sum += (v[u].x + v[u].y) + (v[u].z + v[u].w);
+  const float mu = block_sum_big(sum, lds) / norm;
+  float q = 0.f;
+#pragma unroll
+  for (int u = 0; u < CAP; ++u) {
+    const int64_t i = threadIdx.x + static_cast<int64_t>(kLnBig) * u;
+    if (i < M4) {
+      const float a = v[u].x - mu, b = v[u].y - mu, c = v[u].z - mu, d = v[u].w - mu;
+      q += (a * a + b * b) + (c * c + d * d);
+    }
+  }
+  const float var = block_sum_big(q, lds) / norm;
+  const float denom = sqrtf(var + eps);
+#pragma unroll
+  for (int u = 0; u < CAP; ++u) {
+    const int64_t i = threadIdx.x + static_cast<int64_t>(kLnBig) * u;
+    if (i < M4)
+      os[i] = make_float4((v[u].x - mu) / denom, (v[u].y - mu) / denom, (v[u].z - mu) / denom, (v[u].w - mu) / denom);
+  }
+  if (threadIdx.x == 0) {
+    if (mean_out) mean_out[g] = mu;
+    rstd_out[g] = 1.0f / denom;
+  }
+}
+
+template <int CAP>
+__global__ void __launch_bounds__(kLnBig) graph_ln_bwd_reg(const float4* __restrict__ y, const float4* __restrict__ dy,
+                                                           const float* __restrict__ rstd,
+                                                           const int32_t* __restrict__ rowptr, int64_t D4,
+                                                           float4* __restrict__ dx) {
+  __shared__ float lds[kLnBig / 64];
+  const int64_t g = blockIdx.x;
+  const int64_t r0 = rowptr[g], r1 = rowptr[g + 1];
+  if (r1 == r0) return;
+  const int64_t M4 = (r1 - r0) * D4;
+  const float norm = static_cast<float>((r1 - r0) * D4 * 4);
+  const float4* ys = y + r0 * D4;
+  const float4* gs = dy + r0 * D4;
+  float4* xs = dx + r0 * D4;
+  if (M4 > static_cast<int64_t>(kLnBig) * CAP) {  // too big for registers: two sweeps
+    float a1 = 0.f, a2 = 0.f;
+    for (int64_t i = threadIdx.x; i < M4; i += kLnBig) {
+      const float4 gg = gs[i], yy = ys[i];
+      a1 += (gg.x + gg.y) + (gg.z + gg.w);
+      a2 = fmaf(gg.x, yy.x, a2);
+      a2 = fmaf(gg.y, yy.y, a2);
+      a2 = fmaf(gg.z, yy.z, a2);
+      a2 = fmaf(gg.w, yy.w, a2);
+    }
+    const float m1 = block_sum_big(a1, lds) / norm;
+    const float m2 = block_sum_big(a2, lds) / norm;
+    const float r = rstd[g];
+    for (int64_t i = threadIdx.x; i < M4; i += kLnBig) {
+      const float4 gg = gs[i], yy = ys[i];
+      xs[i] = make_float4(r * (gg.x - m1 - yy.x * m2), r * (gg.y - m1 - yy.y * m2), r * (gg.z - m1 - yy.z * m2),
+                          r * (gg.w - m1 - yy.w * m2));
+    }
+    return;
+  }
+  float4 yv[CAP], gv[CAP];
+#pragma unroll
+  for (int u = 0; u < CAP; ++u) {
+    const int64_t i = threadIdx.x + static_cast<int64_t>(kLnBig) * u;
+    const bool ok = i < M4;
+    const float4 a = ys[ok ? i : 0], b = gs[ok ? i : 0];
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    yv[u] = ok ? a : z;
+    gv[u] = ok ? b : z;
+  }
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int u = 0; u < CAP; ++u) {
+    s1 += (gv[u].x + gv[u].y) + (gv[u].z + gv[u].w);
+    s2 = fmaf(gv[u].x, yv[u].x, s2);
+    s2 = fmaf(gv[u].y, yv[u].y, s2);
+    s2 = fmaf(gv[u].z, yv[u].z, s2);
+    s2 = fmaf(gv[u].w, yv[u].w, s2);
+  }
+  const float m1 = block_sum_big(s1, lds) / norm;
+  const float m2 = block_sum_big(s2, lds) / norm;
+  const float r = rstd[g];
+#pragma unroll
+  for (int u = 0; u < CAP; ++u) {
+    const int64_t i = threadIdx.x + static_cast<int64_t>(kLnBig) * u;
+    if (i < M4)
+      xs[i] = make_float4(r * (gv[u].x - m1 - yv[u].x * m2), r * (gv[u].y - m1 - yv[u].y * m2),
+                          r * (gv[u].z - m1 - yv[u].z * m2), r * (gv[u].w - m1 - yv[u].w * m2));
+  }
+}
+
 }  // namespace x2g
 
 using namespace x2g;
@@ -333,8 +485,12 @@ X2G_API int x2g_graph_layernorm_fwd(const float* x, const int32_t* rowptr, int64
                                     float* out, float* mean, float* rstd, void* stream) {
   if (G < 0 || D <= 0 || (G > 0 && (!x || !rowptr || !out || !mean || !rstd))) return X2G_EINVAL;
   if (G == 0) return X2G_OK;
-  graph_ln_fwd_kernel<<<static_cast<unsigned>(G), kLnThreads, 0, as_stream(stream)>>>(x, rowptr, D, eps, out,
-                                                                                     mean, rstd);
+  if (D % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0)
+    graph_ln_fwd_reg<8><<<static_cast<unsigned>(G), kLnBig, 0, as_stream(stream)>>>(
+        reinterpret_cast<const float4*>(x), rowptr, D / 4, eps, reinterpret_cast<float4*>(out), mean, rstd);
+  else
+    graph_ln_fwd_kernel<<<static_cast<unsigned>(G), kLnThreads, 0, as_stream(stream)>>>(x, rowptr, D, eps, out, mean,
+                                                                                       rstd);
   return last_launch_status();
 }
 
@@ -342,7 +498,13 @@ X2G_API int x2g_graph_layernorm_bwd(const float* out, const float* dout, const f
                                     int64_t G, int64_t D, float* dx, void* stream) {
   if (G < 0 || D <= 0 || (G > 0 && (!out || !dout || !rstd || !rowptr || !dx))) return X2G_EINVAL;
   if (G == 0) return X2G_OK;
-  graph_ln_bwd_kernel<<<static_cast<unsigned>(G), kLnThreads, 0, as_stream(stream)>>>(out, dout, rstd, rowptr, D,
-                                                                                     dx);
+  if (D % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0 && reinterpret_cast<uintptr_t>(dout) % 16 == 0 &&
+      reinterpret_cast<uintptr_t>(dx) % 16 == 0)
+    graph_ln_bwd_reg<8><<<static_cast<unsigned>(G), kLnBig, 0, as_stream(stream)>>>(
+        reinterpret_cast<const float4*>(out), reinterpret_cast<const float4*>(dout), rstd, rowptr, D / 4,
+        reinterpret_cast<float4*>(dx));
+  else
+    graph_ln_bwd_kernel<<<static_cast<unsigned>(G), kLnThreads, 0, as_stream(stream)>>>(out, dout, rstd, rowptr, D,
+                                                                                       dx);
   return last_launch_status();
 }
