@@ -33,13 +33,23 @@ from x2gnn._lib import call, ptr, stream_ptr  # noqa: E402
 from x2gnn.data import collate  # noqa: E402
 from x2gnn.dist import GradBucket  # noqa: E402
 from x2gnn.optim import FlatAdam  # noqa: E402
-from x2gnn.synth import synthetic_molecules  # noqa: E402
+from x2gnn.datasets import ATOMWISE_TARGETS, LABELS, model_for_target  # noqa: E402
+from x2gnn.synth import molecules_from_geometry_file, synthetic_molecules  # noqa: E402
 
 CFG = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embedding_size=128)  # config.json
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32) peak, MI355X_MICROARCH.md
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r1_pmc_traffic_v2.json")  # scripts/pmc_traffic.py output
 METRIC = "molecules/sec (fwd+bwd) on QM9 U0, batch=128, 1/2/4/8 MI355X"
+AID_GEOM = os.path.join(ROOT, "tests", "golden", "aid_geom.npz")  # raw/AID_kcal.xyz as arrays
+# BASELINE.json configs: [1] is the metric's; [2] and [4] are the other single-GPU shapes
+WORKLOADS = {
+    "qm9_u0": dict(batch=128, train=True, metric=METRIC),
+    "qm9_allprop": dict(batch=256, train=True,
+                        metric="molecules/sec (fwd+bwd) on QM9 all-property target model, batch=256, MI355X"),
+    "aid_infer": dict(batch=64, train=False,
+                      metric="molecules/sec (inference) on AID_kcal (~83 atoms), batch=64, MI355X"),
+}
 
 
 def parse():
@@ -47,13 +57,21 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=128, help="molecules per GPU")
+    ap.add_argument("--batch", type=int, default=None, help="molecules per GPU (default: the workload's)")
     ap.add_argument("--shape", default="S160", choices=["S160", "S5A"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--kernel-reps", type=int, default=20)
     ap.add_argument("--eager", action="store_true", help="no HIP-graph capture of the step")
-    return ap.parse_args()
+    ap.add_argument("--workload", default="qm9_u0", choices=sorted(WORKLOADS),
+                    help="qm9_u0: BASELINE config 2 (the metric); qm9_allprop: config 3 (one target's model, "
+                         "B=256); aid_infer: config 5 (AID_kcal geometries, B=64, inference)")
+    ap.add_argument("--target", type=int, default=0, help="qm9_allprop: QM9 target 0-11 (train_ema.py:41-44)")
+    args = ap.parse_args()
+    w = WORKLOADS[args.workload]
+    if args.batch is None:
+        args.batch = w["batch"]
+    return args
 
 
 class Trainer:
@@ -110,6 +128,37 @@ class Trainer:
         with torch.cuda.graph(g_up):
             self._update()
         self.graphs = (g_fb, g_up)
+
+
+class Inference:
+    """Config 5's step: the model forward on a resident batch (trainer.test's path without the
+    MAE, trainer.py:63-77), captured in one HIP graph; ``step`` returns the energies' sum."""
+
+    def __init__(self, model):
+        self.model = model.eval()
+        self.graph = None
+        self.out = None
+
+    def _fwd(self, batch):
+        with torch.no_grad():
+            return self.model(batch).sum()
+
+    def step(self, batch):
+        if self.graph is None:
+            return self._fwd(batch)
+        self.graph.replay()
+        return self.out
+
+    def capture(self, batch, warm=2):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warm):
+                self._fwd(batch)
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = self._fwd(batch)
 
 
 # ------------------------------------------------------------------------------------------ kernels
@@ -266,21 +315,29 @@ def scatter_add_probe(lg, reps):
 
 
 # ------------------------------------------------------------------------------------------ cpu
-def cpu_baseline(mols, budget_s):
-    """The oracle (torch-CPU restatement of the reference) fwd+bwd on the same 128-molecule batch,
-    timed for ~budget_s seconds on this host's cores."""
+def cpu_baseline(mols, budget_s, global_pool=None, train=True, sample=None):
+    """The oracle (torch-CPU restatement of the reference) fwd+bwd (or forward only) on the same
+    batch — or its first ``sample`` molecules, rate scaled per molecule — timed for ~budget_s
+    seconds on this host's cores."""
     from oracle import ref_cpu
 
     threads = torch.get_num_threads()
-    model = ref_cpu.XGNN(**CFG)
+    model = ref_cpu.XGNN(global_pool=global_pool, **CFG)
+    full = len(mols)
+    if sample is not None and sample < full:
+        mols = mols[:sample]
     b = collate(mols)
     times = []
     t_end = time.perf_counter() + budget_s
     for i in range(100):
         t0 = time.perf_counter()
-        res = ref_cpu.run_batch(model, b)
-        loss = torch.nn.functional.smooth_l1_loss(res, b.y)
-        loss.backward()
+        if train:
+            res = ref_cpu.run_batch(model, b)
+            loss = torch.nn.functional.smooth_l1_loss(res, b.y)
+            loss.backward()
+        else:
+            with torch.no_grad():
+                ref_cpu.run_batch(model, b)
         dt = time.perf_counter() - t0
         if i > 0:
             times.append(dt)
@@ -288,8 +345,9 @@ def cpu_baseline(mols, budget_s):
             break
     step = float(np.median(times))
     return {"value": round(len(mols) / step, 2), "unit": "molecules/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/ref_cpu.py fwd+bwd (no optimizer) on the same {len(mols)}-molecule "
-                      f"batch, median of {len(times)} steps after 1 warm-up, torch-CPU fp32, "
+            "sample": f"oracle/ref_cpu.py {'fwd+bwd (no optimizer)' if train else 'forward'} on "
+                      f"{'the same' if len(mols) == full else f'the first {len(mols)} molecules of the'} "
+                      f"{full}-molecule batch, median of {len(times)} steps after 1 warm-up, torch-CPU fp32, "
                       f"{threads} threads of {os.cpu_count()} logical CPUs"}
 
 
@@ -305,24 +363,36 @@ def main():
     dev = torch.device("cuda", local)
     torch.manual_seed(0)  # identical initial weights on every rank
 
-    mols = synthetic_molecules(args.batch, args.shape, seed=1000 + rank)  # this rank's own shard
+    wl = WORKLOADS[args.workload]
+    if args.workload == "aid_infer":  # each rank its own consecutive slice of the AID molecules
+        n_aid = int(np.load(AID_GEOM)["counts"].shape[0])
+        idx = [(rank * args.batch + i) % n_aid for i in range(args.batch)]
+        mols = molecules_from_geometry_file(AID_GEOM, indices=idx, seed=rank)
+    else:
+        mols = synthetic_molecules(args.batch, args.shape, seed=1000 + rank)  # this rank's own shard
     batch = collate(mols).to(dev)
-    model = x2gnn.xgnn_poly(device="cuda", **CFG).to(dev)
-    trainer = Trainer(model)
+    global_pool = None
+    if args.workload == "qm9_allprop":
+        model = model_for_target(args.target, CFG, device="cuda").to(dev)  # train_ema.py:41-44
+        if args.target not in ATOMWISE_TARGETS:
+            global_pool = "mean"
+    else:
+        model = x2gnn.xgnn_poly(device="cuda", **CFG).to(dev)
+    runner = Trainer(model) if wl["train"] else Inference(model)
 
     graphed = False
     if not args.eager:
-        trainer.capture(batch)  # its warm-up steps are extra, untimed
+        runner.capture(batch)  # its warm-up steps are extra, untimed
         graphed = True
     for _ in range(args.warmup):
-        trainer.step(batch)
+        runner.step(batch)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = trainer.step(batch)
+        loss = runner.step(batch)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -347,10 +417,37 @@ def main():
     per = (ntiles + 255) // 256
     grid = str(((ntiles + per - 1) // per) * 512)
     traffic = pmc_traffic([("x2g::dense_bwd_v5", grid), ("x2g::sum_slabs2", str(258 * 256))])
+    roof = {"kernel": "x2g_dense_bwd [E,128]x[128,128] SiLU (dense_bwd_v5 + sum_slabs2)",
+            "bound": "mfma", "achieved": round(dbw_tfs, 2), "peak": MFMA_F32_PEAK_TFS,
+            "unit": "TFLOP/s", "frac": round(dbw_tfs / MFMA_F32_PEAK_TFS, 4), "traffic": traffic,
+            "avg_ms": round(dbw_ms, 5), "flops_per_launch": int(dbw_flops),
+            "traffic_source": os.path.relpath(TRAFFIC_JSON, ROOT) if traffic else None}
+    if not wl["train"]:  # inference: no backward; the T-row attention forward dominates
+        a_ms, a_bytes = probe["attn_fwd"]
+        a_gbs = a_bytes / (a_ms * 1e-3) / 1e9
+        roof = {"kernel": "x2g_sbf_attention_fwd (attn_fwd_kernel, PRE: S = lin_sbf(sbf) precomputed)",
+                "bound": "hbm", "achieved": round(a_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(a_gbs / HBM_PEAK_GBS, 4), "traffic": None, "avg_ms": round(a_ms, 5),
+                "bytes_per_launch": int(a_bytes), "traffic_source": None}
+    if args.workload == "aid_infer":
+        data_desc = (f"AID_kcal geometries (tests/golden/aid_geom.npz = the reference's raw/AID_kcal.xyz; "
+                     f"{meta['nodes'].mean():.1f} atoms, {meta['edges'].mean():.0f} directed edges, "
+                     f"{meta['triplets'].mean():.0f} triplets per molecule), random 338-wide edge features, "
+                     f"random-init weights")
+        work = "xgnn_poly U0 inference (config.json widths), forward only, energies"
+    else:
+        data_desc = (f"synthetic QM9-shaped molecules ({args.shape}: ~18 atoms, {meta['edges'].mean():.0f} "
+                     f"directed edges, {meta['triplets'].mean():.0f} triplets per molecule, random 338-wide "
+                     f"edge features), random-init weights")
+        kind = "xgnn_poly U0" if args.workload == "qm9_u0" else (
+            f"target {args.target} ({LABELS[args.target]}) "
+            f"{'xgnn_poly AtomWise' if global_pool is None else 'xgnn_poly_global MolWise mean-pool'}")
+        work = (f"{kind} train step (config.json: L=4, D=128, H=16, sbf 7x6), {args.shape}, "
+                f"fwd+loss+bwd+allreduce+clip+Adam+EMA")
 
     if rank == 0:
         line = {
-            "metric": METRIC,
+            "metric": wl["metric"],
             "value": round(world * args.batch * args.steps / t_max, 2),
             "unit": "molecules/s",
             "n_gpus": world,
@@ -361,19 +458,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": f"synthetic QM9-shaped molecules ({args.shape}: ~18 atoms, "
-                    f"{meta['edges'].mean():.0f} directed edges, {meta['triplets'].mean():.0f} triplets per "
-                    f"molecule, random 338-wide edge features), random-init weights",
-            "config": {"workload": f"xgnn_poly U0 train step (config.json: L=4, D=128, H=16, sbf 7x6), "
-                                   f"{args.shape}, fwd+loss+bwd+allreduce+clip+Adam+EMA",
+            "data": data_desc,
+            "config": {"workload": work,
                        "per_gpu_batch": args.batch, "global_batch": world * args.batch,
                        "line_nodes_per_gpu": shape["E"], "triplets_per_gpu": shape["T"],
                        "parallelism": f"dp{world}", "hip_graph": graphed},
-            "roofline": {"kernel": "x2g_dense_bwd [E,128]x[128,128] SiLU (dense_bwd_v5 + sum_slabs2)",
-                         "bound": "mfma", "achieved": round(dbw_tfs, 2), "peak": MFMA_F32_PEAK_TFS,
-                         "unit": "TFLOP/s", "frac": round(dbw_tfs / MFMA_F32_PEAK_TFS, 4), "traffic": traffic,
-                         "avg_ms": round(dbw_ms, 5), "flops_per_launch": int(dbw_flops),
-                         "traffic_source": os.path.relpath(TRAFFIC_JSON, ROOT) if traffic else None},
+            "roofline": roof,
             "kernels": dict(
                 {k: {"ms": round(v[0], 5), "bytes": int(v[1]), "GBs": round(v[1] / (v[0] * 1e-3) / 1e9, 1)}
                  for k, v in probe.items()},
@@ -385,10 +475,11 @@ def main():
                 "cold_GBs": round(sa["bytes"] / (sa["cold_ms"] * 1e-3) / 1e9, 1),
                 "cold_frac": round(sa["bytes"] / (sa["cold_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "parity": sa["parity"]},
-            "final_loss": round(final_loss, 6),
+            ("final_loss" if wl["train"] else "energy_sum"): round(final_loss, 6),
         }
         if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(mols, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(mols, args.cpu_seconds, global_pool=global_pool, train=wl["train"],
+                                                sample=8 if args.workload == "aid_infer" else None)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

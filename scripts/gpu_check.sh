@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU validation/profiling run (used through gpurun): each step under its own time limit; stop
 # at the first step that ends in anything but pass/fail (fault, abort, timeout).
-#   bash scripts/gpu_check.sh [kernels] [model] [smoke] [bench] [prof] [pmc]
+#   bash scripts/gpu_check.sh [kernels] [model] [gpu] [smoke] [bench] [bench_c3] [bench_c3a] [bench_c5] [prof] [prof_c5] [pmc]
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 ROOT=$(pwd)
@@ -23,6 +23,11 @@ for s in "$@"; do
     gpu) step gputests 600 python -m pytest tests -q -m gpu -rf ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 420 python bench.py --steps 20 --warmup 5 ;;
+    bench_c3) step bench_c3 420 python bench.py --workload qm9_allprop --target 0 --steps 20 --warmup 5 ;;
+    bench_c3a) step bench_c3a 420 python bench.py --workload qm9_allprop --target 7 --steps 20 --warmup 5 --no-cpu-baseline ;;
+    bench_c5) step bench_c5 420 python bench.py --workload aid_infer --steps 10 --warmup 3 ;;
+    prof_c5) step prof_c5 420 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5_$TAG -o run --output-format csv \
+            -- python "$ROOT/bench.py" --workload aid_infer --steps 5 --warmup 2 --no-cpu-baseline ;;
     prof) step prof 420 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv \
             -- python "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline ;;
     pmc) step pmc 420 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch_$TAG -o run \

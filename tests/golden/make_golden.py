@@ -155,9 +155,11 @@ def gen_conv1(ref):
     np.savez_compressed(os.path.join(HERE, "conv1.npz"), **out)
 
 
-def gen_model(ref, fname, kind, cfg, n_mol, seed_mol, seed_w, grads="all", pool_option="mean", shape="S160"):
+def gen_model(ref, fname, kind, cfg, n_mol, seed_mol, seed_w, grads="all", pool_option="mean", shape="S160",
+              mols=None):
     out = {}
-    mols = synthetic_molecules(n_mol, shape, seed=seed_mol)
+    if mols is None:
+        mols = synthetic_molecules(n_mol, shape, seed=seed_mol)
     b = pack_batch("", mols, out)
     if kind == "poly":
         model = ref.xgnn.xgnn_poly(device="cpu", **cfg)
@@ -175,6 +177,7 @@ def gen_model(ref, fname, kind, cfg, n_mol, seed_mol, seed_w, grads="all", pool_
     out["cfg_keys"] = np.array(list(cfg.keys()))
     out["cfg_vals"] = np.array(list(cfg.values()))
     out["kind"] = np.array(kind)
+    out["pool_option"] = np.array(pool_option)
     out["param_names"] = np.array([n for n, _ in model.named_parameters()])
     out["param_shapes"] = np.array([str(tuple(p.shape)) for _, p in model.named_parameters()])
     out["state_keys"] = np.array(list(model.state_dict().keys()))
@@ -187,20 +190,62 @@ def gen_model(ref, fname, kind, cfg, n_mol, seed_mol, seed_w, grads="all", pool_
     np.savez_compressed(os.path.join(HERE, fname), **out)
 
 
+def gen_aid_geometry():
+    """aid_geom.npz: every molecule of raw/AID_kcal.xyz (config 5's data) as Z / positions /
+    label arrays, parsed with the reference's read_xyz grammar (x2gnn.datasets.read_xyz), so the
+    GPU box (where /root/reference does not exist) can rebuild the molecules."""
+    from x2gnn.datasets import read_xyz
+    recs = read_xyz(os.path.join(REF, "raw/AID_kcal.xyz"))
+    np.savez_compressed(os.path.join(HERE, "aid_geom.npz"),
+                        counts=np.array([r.Z.shape[0] for r in recs], dtype=np.int32),
+                        z=np.concatenate([r.Z.numpy() for r in recs]).astype(np.int8),
+                        pos=np.concatenate([r.R.numpy() for r in recs]).astype(np.float32),
+                        label=np.array([float(r.Label.reshape(-1)[0]) for r in recs]))
+    print(f"aid_geom.npz: {len(recs)} molecules")
+
+
+SMALL = dict(conv_layers=2, sbf_dim=7, rbf_dim=6, in_channels=32, heads=4, embedding_size=32)
+FULL = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embedding_size=128)
+SEL = ["fin_model.convs.0.lin_sbf.weight", "fin_model.convs.3.lin_query.weight",
+       "fin_model.convs.1.lin_edge.weight", "emb_block.embedding.weight", "rbf_layer.frequencies",
+       "fin_model.readouts.2.lin_rbf.weight", "fin_model.edgenn.0.weight", "mat_trans.weight"]
+
+
+def aid_molecules(k, seed=0):
+    """The k smallest AID_kcal molecules (config 5 geometry, seeded synthetic edge features)."""
+    from x2gnn.datasets import read_xyz
+    recs = sorted(read_xyz(os.path.join(REF, "raw/AID_kcal.xyz")), key=lambda r: r.Z.shape[0])[:k]
+    return [molecule_from_geometry(r.Z.numpy(), r.R.numpy().astype(np.float64), 5.0,
+                                   np.random.default_rng(1000 * seed + i + 17), y=float(r.Label.reshape(-1)[0]))
+            for i, r in enumerate(recs)]
+
+
+GENERATORS = {
+    "triplets": lambda ref: gen_triplets(ref),
+    "basis": lambda ref: gen_basis(ref),
+    "conv1": lambda ref: gen_conv1(ref),
+    "model_small": lambda ref: gen_model(ref, "model_small.npz", "poly", SMALL, n_mol=4, seed_mol=41, seed_w=201),
+    "model_full": lambda ref: gen_model(ref, "model_full.npz", "poly", FULL, n_mol=2, seed_mol=42, seed_w=202,
+                                        grads=SEL),
+    "model_global": lambda ref: gen_model(ref, "model_global.npz", "global", SMALL, n_mol=4, seed_mol=43,
+                                          seed_w=203, pool_option="mean"),
+    "model_s5a": lambda ref: gen_model(ref, "model_s5a.npz", "poly", SMALL, n_mol=2, seed_mol=44, seed_w=204,
+                                       shape="S5A"),
+    # config 3: the MolWise model with the other pool option, at full width
+    "model_global_add": lambda ref: gen_model(ref, "model_global_add.npz", "global", FULL, n_mol=3, seed_mol=45,
+                                              seed_w=205, pool_option="add", grads=SEL[:5]),
+    # config 5: real AID geometry (the two smallest molecules), full width
+    "model_aid": lambda ref: gen_model(ref, "model_aid.npz", "poly", FULL, n_mol=1, seed_mol=0, seed_w=206,
+                                       grads=SEL, mols=aid_molecules(2)),
+    "aid_geom": lambda ref: gen_aid_geometry(),
+}
+
+
 def main():
+    names = sys.argv[1:] or list(GENERATORS)
     ref = import_reference()
-    gen_triplets(ref)
-    gen_basis(ref)
-    gen_conv1(ref)
-    small = dict(conv_layers=2, sbf_dim=7, rbf_dim=6, in_channels=32, heads=4, embedding_size=32)
-    full = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embedding_size=128)
-    gen_model(ref, "model_small.npz", "poly", small, n_mol=4, seed_mol=41, seed_w=201)
-    sel = ["fin_model.convs.0.lin_sbf.weight", "fin_model.convs.3.lin_query.weight",
-           "fin_model.convs.1.lin_edge.weight", "emb_block.embedding.weight", "rbf_layer.frequencies",
-           "fin_model.readouts.2.lin_rbf.weight", "fin_model.edgenn.0.weight", "mat_trans.weight"]
-    gen_model(ref, "model_full.npz", "poly", full, n_mol=2, seed_mol=42, seed_w=202, grads=sel)
-    gen_model(ref, "model_global.npz", "global", small, n_mol=4, seed_mol=43, seed_w=203, pool_option="mean")
-    gen_model(ref, "model_s5a.npz", "poly", small, n_mol=2, seed_mol=44, seed_w=204, shape="S5A")
+    for n in names:
+        GENERATORS[n](ref)
 
 
 if __name__ == "__main__":

@@ -30,11 +30,15 @@ def model_cfg(z):
     return dict(zip([str(k) for k in z["cfg_keys"]], [int(v) for v in z["cfg_vals"]]))
 
 
+def pool_option(z):
+    return str(z["pool_option"]) if "pool_option" in z.files else "mean"
+
+
 def oracle_model(z):
     from oracle.ref_cpu import XGNN
 
     kind = str(z["kind"])
-    m = XGNN(global_pool="mean" if kind == "global" else None, **model_cfg(z))
+    m = XGNN(global_pool=pool_option(z) if kind == "global" else None, **model_cfg(z))
     load_seeded(m, int(z["weight_seed"]))
     return m
 

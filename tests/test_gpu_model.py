@@ -6,7 +6,7 @@ import pytest
 import torch
 
 from conftest import golden
-from helpers import batch_from_fixture, model_cfg, oracle_model, rel_err
+from helpers import batch_from_fixture, model_cfg, oracle_model, pool_option, rel_err
 from weights import load_seeded
 
 from oracle import ref_cpu
@@ -19,8 +19,10 @@ ENERGY_RTOL = 1e-4
 def product_model(z, cuda):
     import x2gnn
 
-    cls = x2gnn.xgnn_poly if str(z["kind"]) == "poly" else x2gnn.xgnn_poly_global
-    m = cls(device="cuda", **model_cfg(z))
+    if str(z["kind"]) == "poly":
+        m = x2gnn.xgnn_poly(device="cuda", **model_cfg(z))
+    else:
+        m = x2gnn.xgnn_poly_global(device="cuda", pool_option=pool_option(z), **model_cfg(z))
     load_seeded(m, int(z["weight_seed"]))
     return m.to(cuda)
 
@@ -29,7 +31,8 @@ def grad_scale(z, names):
     return max(float(z["gnorm." + n]) for n in names)
 
 
-@pytest.mark.parametrize("fixture", ["model_small.npz", "model_full.npz", "model_global.npz", "model_s5a.npz"])
+@pytest.mark.parametrize("fixture", ["model_small.npz", "model_full.npz", "model_global.npz", "model_s5a.npz",
+                                     "model_global_add.npz", "model_aid.npz"])
 def test_model_energies_and_gradients_vs_reference(cuda, fixture):
     z = golden(fixture)
     m = product_model(z, cuda)
@@ -161,3 +164,82 @@ def test_full_size_properties(cuda):
                 p -= (1e-3 / gnorm) * p.grad
         loss2 = torch.nn.functional.smooth_l1_loss(m(b), b.y)
     assert loss2 < loss
+
+
+def test_config3_molwise_add_batch256_vs_oracle(cuda):
+    """Config 3 shape: the MolWise model (targets 0-5, train_ema.py:43-44) with add pooling at
+    B=256 S160, full width: energies and the loss gradient of every parameter vs the oracle."""
+    import x2gnn
+    from x2gnn.data import collate
+    from x2gnn.synth import synthetic_molecules
+
+    cfg = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embedding_size=128)
+    b = collate(synthetic_molecules(256, "S160", seed=31))
+    orc = ref_cpu.XGNN(global_pool="add", **cfg)
+    load_seeded(orc, 78)
+    ref = ref_cpu.run_batch(orc, b)
+    torch.nn.functional.smooth_l1_loss(ref, b.y).backward()
+    m = x2gnn.xgnn_poly_global(device="cuda", pool_option="add", **cfg)
+    load_seeded(m, 78)
+    m = m.to(cuda)
+    res = m(b.to(cuda))
+    assert res.shape == (256,)
+    assert rel_err(res.detach().cpu().numpy(), ref.detach().numpy()) < ENERGY_RTOL
+    torch.nn.functional.smooth_l1_loss(res, b.y.to(cuda)).backward()
+    grads = dict(orc.named_parameters())
+    scale = max(float(p.grad.norm()) for p in grads.values() if p.grad is not None)
+    for n, p in m.named_parameters():
+        g_ref = grads[n].grad
+        if g_ref is None:
+            continue
+        err = float((p.grad.cpu() - g_ref).abs().max())
+        assert err <= 2e-3 * float(g_ref.abs().max()) + 1e-6 * scale, (n, err)
+
+
+def test_config5_aid_batch64_inference(cuda):
+    """Config 5 shape: 64 AID_kcal molecules (~83 atoms, T ~3.4M triplets) at full width,
+    inference: finite energies, per-molecule energies invariant to batch composition, and the
+    two smallest-triplet molecules of the batch against the oracle."""
+    import os
+
+    import x2gnn
+    from conftest import GOLDEN
+    from x2gnn.data import collate
+    from x2gnn.synth import molecules_from_geometry_file
+
+    cfg = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embedding_size=128)
+    mols = molecules_from_geometry_file(os.path.join(GOLDEN, "aid_geom.npz"), indices=range(64))
+    b = collate(mols)
+    T = int(b._meta["triplets"].sum())
+    assert T > 3_000_000
+    m = x2gnn.xgnn_poly(device="cuda", **cfg)
+    load_seeded(m, 79)
+    m = m.to(cuda).eval()
+    with torch.no_grad():
+        res = m(b.to(cuda)).cpu().numpy()
+        assert np.isfinite(res).all() and res.shape == (64,)
+        small = np.argsort(b._meta["triplets"])[:2]
+        sub = [mols[i] for i in small]
+        part = m(collate(sub).to(cuda)).cpu().numpy()
+    assert rel_err(part, res[small]) < 1e-5
+    orc = ref_cpu.XGNN(**cfg)
+    load_seeded(orc, 79)
+    with torch.no_grad():
+        ref = ref_cpu.run_batch(orc, collate(sub)).numpy()
+    assert rel_err(part, ref) < ENERGY_RTOL
+
+
+def test_inference_fused_projection_matches_training_path(cuda, monkeypatch):
+    """With X2G_INFER_SBF=fused and grad mode off the attention forward projects sbf per triplet
+    in-kernel (no [T,D] S tensor); its energies equal the training path's (S materialised) to
+    fp32 rounding."""
+    from x2gnn import ops
+
+    monkeypatch.setattr(ops, "_INFER_FUSED", True)
+    z = golden("model_full.npz")
+    m = product_model(z, cuda)
+    b = batch_from_fixture(z).to(cuda)
+    train = m(b).detach()
+    with torch.no_grad():
+        infer = m(b)
+    assert rel_err(infer.cpu().numpy(), train.cpu().numpy()) < 1e-5

@@ -86,7 +86,8 @@ def test_conv_layer_vs_reference():
         assert rel_err(p.grad.numpy(), z["grad." + n]) < 1e-4, n
 
 
-@pytest.mark.parametrize("fixture", ["model_small.npz", "model_full.npz", "model_global.npz", "model_s5a.npz"])
+@pytest.mark.parametrize("fixture", ["model_small.npz", "model_full.npz", "model_global.npz", "model_s5a.npz",
+                                     "model_global_add.npz", "model_aid.npz"])
 def test_model_vs_reference(fixture):
     z = golden(fixture)
     m = oracle_model(z)

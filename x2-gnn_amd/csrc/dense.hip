@@ -1223,7 +1223,10 @@ X2G_API int x2g_dense_fwd(const float* x, const float* w, const float* b, int64_
              aligned16(res))
       return dense_fwd_narrow_launch(x, w, b, res, R, K, N, act, y, z, st);
     else if (vec && variant == 0 && N % 4 == 0 && aligned16(y) && aligned16(z) && aligned16(res)) {
-      if (tuning(kTuneDenseDbg) == 0) {  // v6 (default); knob 3 = 1 selects v5
+      // v6 (default); knob 3 = 1 selects v5.  (A register-resident-weight variant with one tile
+      // per workgroup measured no faster: at 21k rows the layer is bound by its 43 MB of
+      // x / res / y / z traffic plus the launch ramp, not by the weight staging.)
+      if (tuning(kTuneDenseDbg) != 1) {
         const unsigned g6 = static_cast<unsigned>(ntiles < 512 ? ntiles : 512);
         dense_fwd_v6<<<g6, 256, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
       } else {

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import os
 
 import torch
 
@@ -215,6 +216,26 @@ class _SBFAttention(torch.autograd.Function):
         return dq, dk, dv, dout, d_edge, None, dw, db, None, None, None, None, None
 
 
+# Inference (grad mode off): nothing is saved for a backward, so the [T, D] projection S is not
+# worth materialising; the forward kernel projects each triplet's sbf row itself (W_sbf in
+# registers), reading 4*sbf_dim bytes per triplet instead of writing and re-reading 4*D.
+_INFER_FUSED = os.environ.get("X2G_INFER_SBF", "pre") == "fused"  # measured slower at config 5
+
+
+def _attention_fwd_fused(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row, heads, channels):
+    q, k, v, skip = _f32(q), _f32(k), _f32(v), _f32(skip)
+    sbf, w_sbf, b_sbf = _f32(sbf), _f32(w_sbf), _f32(b_sbf)
+    edge = _f32(edge) if edge is not None else None
+    E, T, D = q.shape[0], lg.T, heads * channels
+    f32 = dict(dtype=torch.float32, device=q.device)
+    out, alpha = torch.empty(E, D, **f32), torch.empty(T, heads, **f32)
+    smax, sden = torch.empty(E, heads, **f32), torch.empty(E, heads, **f32)
+    call("x2g_sbf_attention_fwd", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(edge_row), edge_mode,
+         ptr(sbf), ptr(w_sbf), ptr(b_sbf), ptr(lg.trip_rowptr), ptr(lg.trip_src), E, T, heads, channels,
+         sbf.shape[1], ptr(out), ptr(alpha), ptr(smax), ptr(sden), stream_ptr())
+    return out, alpha, smax, sden
+
+
 def sbf_attention(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg: LineGraph, heads: int, channels: int,
                   edge_mode: int = EDGE_PER_TRIPLET, edge_row=None, return_attention=False):
     """Fused SBFTransformerConv message/softmax/aggregate/skip (see csrc/attention.hip).
@@ -226,7 +247,11 @@ def sbf_attention(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg: LineGraph, heads: 
         edge_mode = EDGE_NONE
     if edge_row is not None:
         edge_row = _i32(edge_row)
-    out, alpha, smax, sden = _SBFAttention.apply(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row,
+    if _INFER_FUSED and not torch.is_grad_enabled():
+        out, alpha, smax, sden = _attention_fwd_fused(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode,
+                                                      edge_row, heads, channels)
+    else:
+        out, alpha, smax, sden = _SBFAttention.apply(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row,
                                                  heads, channels)
     if not return_attention:
         return out

@@ -138,3 +138,21 @@ def read_xyz_molecules(path: str, limit: int | None = None, cutoff: float = 5.0,
         if limit is not None and len(mols) >= limit:
             break
     return mols
+
+
+def molecules_from_geometry_file(path: str, indices=None, cutoff: float = 5.0, seed: int = 0):
+    """Molecules from a geometry archive (``counts`` int [M], ``z`` [sum], ``pos`` [sum, 3],
+    optional ``label`` [M]; e.g. tests/golden/aid_geom.npz, the reference's raw/AID_kcal.xyz as
+    arrays) with seeded synthetic edge features; ``indices`` selects molecules (default all)."""
+    arc = np.load(path, allow_pickle=False)
+    counts = arc["counts"].astype(np.int64)
+    off = np.concatenate([[0], np.cumsum(counts)])
+    labels = arc["label"] if "label" in arc.files else np.zeros(len(counts))
+    idx = range(len(counts)) if indices is None else indices
+    mols = []
+    for j, m in enumerate(idx):
+        z = arc["z"][off[m]:off[m + 1]].astype(np.int64)
+        pos = arc["pos"][off[m]:off[m + 1]].astype(np.float64)
+        feat = np.random.default_rng(1000 * seed + j + 17)
+        mols.append(molecule_from_geometry(z, pos, cutoff, feat, y=float(labels[m])))
+    return mols
