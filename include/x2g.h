@@ -78,6 +78,52 @@ int x2g_line_graph_transpose(const int32_t* trip_src, int64_t num_triplets, int6
  * (envelop.py:16-21, exponent 5). */
 int x2g_bessel_env(const float* dist, int64_t num_edges, float cutoff, float* rbf_env, void* stream);
 
+/* The whole E-row featurisation in one launch (xgnn.py:49-53 + radial_basis_layer.py:36-40 +
+ * envelop.py:16-21 + the E-row half of angular_basis_layer.py:80-86), per directed edge e = (a, b):
+ *   dist[e] = |pos[a] - pos[b]|,  env[e] = poly_envelop(dist / cutoff) (exponent 5),
+ *   rbf_env[e, n] = sin(freq[n] * dist / cutoff) * env[e]   (n < num_radial <= 16; the trainable
+ *                   RadialBasis times the envelope: xgnn_poly's node_rbf),
+ *   bessel_env[e, :] = x2g_bessel_env's 42 values (optional, NULL skips).
+ * edge_src/edge_dst int32 atom ids. */
+int x2g_edge_basis(const float* pos, const int32_t* edge_src, const int32_t* edge_dst, int64_t num_edges,
+                   float cutoff, const float* freq, int32_t num_radial, float* dist, float* env, float* rbf_env,
+                   float* bessel_env, void* stream);
+
+/* d loss / d freq[n] = sum_e g[e, n] * env[e] * cos(freq[n] x_e) * x_e, x_e = dist[e] / cutoff
+ * (the backward of rbf_env w.r.t. RadialBasis.frequencies).  Deterministic: per-workgroup
+ * partials + a fixed-order sum; flags X2G_ACCUM_WGRAD (dfreq +=) and X2G_DEFER_SLAB_SUM (leave
+ * the partials for x2g_slab_sum_batch: x2g_edge_basis_freq_grad_splits slabs of num_radial floats
+ * at the start of the workspace). */
+size_t x2g_edge_basis_freq_grad_workspace(int64_t num_edges, int32_t num_radial);
+int32_t x2g_edge_basis_freq_grad_splits(int64_t num_edges);
+int x2g_edge_basis_freq_grad(const float* g, const float* dist, const float* env, const float* freq,
+                             int64_t num_edges, int32_t num_radial, float cutoff, float* dfreq, int flags,
+                             void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- rbf gates (x * lin_rbf(rbf))
+ * f[e, c] = sum_j w[c, j] rbf[e, j] + b[c]   (w [D, R] row-major, R <= 8, b optional; D % 4 == 0)
+ * gate:  out[e, :] = x[e, :] * f[e, :]                 (SBFTransformerConv x_src,
+ *                                                       sbftransformer_conv.py:99-101)
+ * pool:  out[n, :] = sum_{e in [rowptr[n], rowptr[n+1])} x[e, :] * f[e, :]
+ *        (AtomWise / MolWise edge->atom pooling, readout.py:39-41,66-67; rows sorted by owner)
+ * The [E, D] filter f is never materialised. */
+int x2g_rbf_gate_fwd(const float* x, const float* rbf, const float* w, const float* b, int64_t rows, int32_t D,
+                     int32_t R, float* out, void* stream);
+int x2g_rbf_pool_fwd(const float* x, const float* rbf, const float* w, const float* b, const int32_t* rowptr,
+                     int64_t num_segments, int32_t D, int32_t R, float* out, void* stream);
+
+/* Backward of both: g_row(e) = g[e] (gate, owner == NULL) or g[owner[e]] (pool):
+ *   dx[e] = g_row * f[e] (+ dx_add[e]; dx may alias dx_add),  drbf[e, j] = sum_c (g_row x[e])_c w[c, j],
+ *   dw[c, j] (+)= sum_e (g_row x[e])_c rbf[e, j],  db[c] (+)= sum_e (g_row x[e])_c   (db optional).
+ * dx / drbf may be NULL (not needed).  Weight gradients: per-workgroup partials + fixed-order
+ * sum, flags as x2g_linear_wgrad_ex (slabs of D*R then D floats at the start of the workspace). */
+size_t x2g_rbf_gate_bwd_workspace(int64_t rows, int32_t D, int32_t R);
+int32_t x2g_rbf_gate_bwd_splits(int64_t rows);
+int x2g_rbf_gate_bwd(const float* g, const int32_t* owner, const float* x, const float* rbf, const float* w,
+                     const float* b, int64_t rows, int32_t D, int32_t R, float* dx, const float* dx_add,
+                     float* drbf, float* dw, float* db, int flags, void* workspace, size_t workspace_bytes,
+                     void* stream);
+
 /* sbf[t, l*R+n] = rbf_env[trip_src[t], l*R+n] * Y_l0(theta_t), theta_t = atan2(|ji x jk|, ji.jk),
  * ji = pos[atom_i]-pos[atom_j], jk = pos[atom_k]-pos[atom_j]  (xgnn.py:61-65,
  * angular_basis_layer.py:87-93).  If theta[T] is non-NULL it is used instead of the positions

@@ -491,3 +491,108 @@ def test_dense_narrow_k_vs_torch(cuda, R, K):
     y = ops.dense(x, w, b, act=ops.ACT_SILU, res=res)
     ref = torch.nn.functional.silu(x.double() @ w.double().t() + b.double()) + res.double()
     torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("E", [0, 1, 3000])
+def test_edge_basis_vs_torch(cuda, E):
+    """x2g_edge_basis (dist, envelope, trainable radial basis, Bessel terms) and its frequency
+    gradient against the torch formulas (xgnn.py:49-53, radial_basis_layer.py:36-40)."""
+    from x2gnn import ops
+    from x2gnn.layers import RadialBasis, poly_envelop
+
+    g = torch.Generator().manual_seed(5)
+    n_atoms = 40
+    pos = (torch.rand(n_atoms, 3, generator=g) * 4.0).to(cuda)
+    src = torch.randint(0, n_atoms, (E,), generator=g)
+    dst = (src + torch.randint(1, n_atoms, (E,), generator=g)) % n_atoms
+    lg = ops.LineGraph.__new__(ops.LineGraph)
+    lg.E, lg.edge_src, lg.edge_dst = E, src.to(torch.int32).to(cuda), dst.to(torch.int32).to(cuda)
+    rb = RadialBasis(embedding_size=6, cutoff=5.0).to(cuda)
+    with torch.no_grad():
+        rb.frequencies.mul_(1.0 + 0.1 * torch.rand(6, generator=g).to(cuda))
+    dist, env, rbf, bes = ops.edge_basis(pos, lg, rb.frequencies, 5.0)
+    d_ref = (pos[src.to(cuda)] - pos[dst.to(cuda)]).norm(dim=1)
+    env_ref = poly_envelop(5.0, 5)(d_ref)
+    torch.testing.assert_close(dist, d_ref, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(env, env_ref, rtol=2e-5, atol=1e-5)
+    f2 = rb.frequencies.detach().clone().requires_grad_(True)
+    rbf_ref = torch.sin(f2 * (d_ref * 0.2).unsqueeze(-1)) * env_ref.unsqueeze(1)
+    torch.testing.assert_close(rbf, rbf_ref, rtol=5e-5, atol=5e-5)
+    torch.testing.assert_close(bes, ops.bessel_env(dist, 5.0), rtol=1e-6, atol=1e-6)
+    up = torch.randn(E, 6, generator=g).to(cuda)
+    (rbf * up).sum().backward()
+    (rbf_ref * up).sum().backward()
+    if E == 0:
+        assert rb.frequencies.grad is None or float(rb.frequencies.grad.abs().max()) == 0.0
+    else:
+        torch.testing.assert_close(rb.frequencies.grad, f2.grad, rtol=2e-4, atol=2e-4)
+
+
+def _gate_inputs(cuda, rows, D, R, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(rows, D, generator=g).to(cuda)
+    rbf = torch.randn(rows, R, generator=g).to(cuda)
+    w = (0.3 * torch.randn(D, R, generator=g)).to(cuda)
+    b = (0.1 * torch.randn(D, generator=g)).to(cuda)
+    return x, rbf, w, b
+
+
+@pytest.mark.parametrize("rows,D,R,bias", [(1, 128, 6, True), (2049, 128, 6, False), (777, 64, 3, True),
+                                           (300, 256, 8, True), (21058, 128, 6, False)])
+def test_rbf_gate_vs_torch(cuda, rows, D, R, bias):
+    """x2g_rbf_gate_fwd/bwd: x * (W rbf + b) and all four gradients vs torch autograd."""
+    from x2gnn import _lib, ops
+    from x2gnn._lib import call, ptr, stream_ptr
+
+    x, rbf, w, b = _gate_inputs(cuda, rows, D, R, rows + D)
+    b = b if bias else None
+    out = torch.empty_like(x)
+    call("x2g_rbf_gate_fwd", ptr(x), ptr(rbf), ptr(w), ptr(b), rows, D, R, ptr(out), stream_ptr())
+    xr, rr, wr = (t.clone().requires_grad_(True) for t in (x, rbf, w))
+    br = b.clone().requires_grad_(True) if bias else None
+    f = torch.nn.functional.linear(rr, wr, br)
+    ref = xr * f
+    torch.testing.assert_close(out, ref.detach(), rtol=1e-5, atol=1e-5)
+    gy = torch.randn(rows, D, device=cuda)
+    ref.backward(gy)
+    add = torch.randn(rows, D, device=cuda)
+    dx, drbf, dw, db = ops._gate_bwd(gy, None, x, rbf, w, b, None, None, True, True, dx_add=add)
+    torch.testing.assert_close(dx, xr.grad + add, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(drbf, rr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dw, wr.grad, rtol=1e-4, atol=1e-3)
+    if bias:
+        torch.testing.assert_close(db, br.grad, rtol=1e-4, atol=1e-3)
+    # accumulate into existing buffers (X2G_ACCUM_WGRAD)
+    dw2, db2 = torch.ones_like(w), (torch.ones_like(b) if bias else None)
+    ws_bytes = int(_lib.load().x2g_rbf_gate_bwd_workspace(rows, D, R))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=cuda)
+    call("x2g_rbf_gate_bwd", ptr(gy), None, ptr(x), ptr(rbf), ptr(w), ptr(b), rows, D, R, None, None, None, ptr(dw2),
+         ptr(db2), 1, ptr(ws), ws_bytes, stream_ptr())
+    torch.testing.assert_close(dw2, wr.grad + 1, rtol=1e-4, atol=1e-3)
+
+
+def test_rbf_pool_vs_torch(cuda):
+    """x2g_rbf_pool_fwd + the owner-indexed backward: segment sums of x * (W rbf + b) over
+    ragged (and empty) segments vs torch index_add + autograd."""
+    from x2gnn import ops
+
+    rng = np.random.default_rng(3)
+    rowptr = _rowptr_with_empties(rng, 300, 17)
+    rows = int(rowptr[-1])
+    owner = torch.from_numpy(np.repeat(np.arange(300), np.diff(rowptr))).to(cuda)
+    x, rbf, w, b = _gate_inputs(cuda, rows, 128, 6, 9)
+    w.requires_grad_(True)
+    b.requires_grad_(True)
+    xr, rr = x.clone().requires_grad_(True), rbf.clone().requires_grad_(True)
+    out = ops.rbf_pool(xr, rr, w, b, owner, torch.from_numpy(rowptr).to(cuda), 300)
+    xq, rq = x.clone().requires_grad_(True), rbf.clone().requires_grad_(True)
+    wq, bq = w.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    ref = torch.zeros(300, 128, device=cuda).index_add(0, owner, xq * torch.nn.functional.linear(rq, wq, bq))
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-4)
+    gy = torch.randn(300, 128, device=cuda)
+    out.backward(gy)
+    ref.backward(gy)
+    torch.testing.assert_close(xr.grad, xq.grad, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(rr.grad, rq.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(w.grad, wq.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(b.grad, bq.grad, rtol=1e-4, atol=1e-3)

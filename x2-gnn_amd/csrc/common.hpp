@@ -24,8 +24,20 @@ inline unsigned blocks_for(int64_t n, int per_block) {
 }
 
 // Tuning knobs for A/B experiments (x2g_tuning in line_graph.hip); 0 = default everywhere.
-enum TuneKey { kTuneDenseFwd = 0, kTuneDenseBwd = 1, kTuneAttn = 2, kTuneDenseDbg = 3, kTuneCount = 16 };
+enum TuneKey {
+  kTuneDenseFwd = 0,
+  kTuneDenseBwd = 1,
+  kTuneAttn = 2,
+  kTuneDenseDbg = 3,
+  kTuneGateSplits = 4,  // rbf gate backward: workgroup cap (0 = default)
+  kTuneCount = 16
+};
 int tuning(int key);
+
+// Fixed-order sum of `splits` per-workgroup partial slabs (linear.hip): dw[i] (+)= sum_s part_w[s][i]
+// and, when part_b and db are given, db likewise.
+int sum_slabs_launch(const float* part_w, int64_t nw, const float* part_b, int64_t nb, int splits, float* dw,
+                     float* db, bool accum, hipStream_t st);
 
 // Masked loads without control flow.  Written as `ok ? load : 0`, the compiler sinks each load
 // into a conditional block and then waits for it (s_waitcnt vmcnt(0)) before issuing the next:

@@ -30,6 +30,15 @@ SIGNATURES = {
     "x2g_vertex_to_edge": [_P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P],
     "x2g_line_graph_transpose": [_P, _I64, _I64, _P, _P, _P, _SZ, _P],
     "x2g_bessel_env": [_P, _I64, _F, _P, _P],
+    "x2g_edge_basis": [_P, _P, _P, _I64, _F, _P, _I32, _P, _P, _P, _P, _P],
+    "x2g_edge_basis_freq_grad_workspace": [_I64, _I32],
+    "x2g_edge_basis_freq_grad_splits": [_I64],
+    "x2g_edge_basis_freq_grad": [_P, _P, _P, _P, _I64, _I32, _F, _P, ctypes.c_int, _P, _SZ, _P],
+    "x2g_rbf_gate_fwd": [_P, _P, _P, _P, _I64, _I32, _I32, _P, _P],
+    "x2g_rbf_pool_fwd": [_P, _P, _P, _P, _P, _I64, _I32, _I32, _P, _P],
+    "x2g_rbf_gate_bwd_workspace": [_I64, _I32, _I32],
+    "x2g_rbf_gate_bwd_splits": [_I64],
+    "x2g_rbf_gate_bwd": [_P, _P, _P, _P, _P, _P, _I64, _I32, _I32, _P, _P, _P, _P, _P, ctypes.c_int, _P, _SZ, _P],
     "x2g_spherical_basis": [_P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P],
     "x2g_sbf_attention_fwd": [_P, _P, _P, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _I64, _I64, _I32, _I32,
                               _I32, _P, _P, _P, _P, _P],
@@ -63,7 +72,9 @@ SIGNATURES = {
 RESTYPES = {"x2g_status_string": ctypes.c_char_p, "x2g_vertex_to_edge_workspace": _SZ,
             "x2g_linear_wgrad_workspace": _SZ, "x2g_dense_bwd_workspace": _SZ, "x2g_optimizer_workspace": _SZ,
             "x2g_linear_wgrad_splits": ctypes.c_int32, "x2g_dense_bwd_splits": ctypes.c_int32,
-            "x2g_dense_bwd_slab_offset": ctypes.c_int64}
+            "x2g_dense_bwd_slab_offset": ctypes.c_int64, "x2g_edge_basis_freq_grad_workspace": _SZ,
+            "x2g_edge_basis_freq_grad_splits": ctypes.c_int32, "x2g_rbf_gate_bwd_workspace": _SZ,
+            "x2g_rbf_gate_bwd_splits": ctypes.c_int32}
 
 _lib = None
 

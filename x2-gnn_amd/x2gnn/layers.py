@@ -112,9 +112,10 @@ class F_B_2D(nn.Module):
     def forward(self, d, Angles, edge_index_1):
         return ops.spherical_basis_from_angles(Angles, edge_index_1, self.radial(d))
 
-    def from_positions(self, d, pos, line_graph):
-        """Fast path: angles computed in-kernel from the triplets' atom positions (xgnn.py:61-65)."""
-        return ops.spherical_basis(pos, line_graph, self.radial(d))
+    def from_positions(self, d, pos, line_graph, radial=None):
+        """Fast path: angles computed in-kernel from the triplets' atom positions (xgnn.py:61-65);
+        ``radial`` = precomputed ``self.radial(d)`` (x2g_edge_basis writes it)."""
+        return ops.spherical_basis(pos, line_graph, self.radial(d) if radial is None else radial)
 
 
 class _ScaleGradByCount(torch.autograd.Function):
@@ -201,11 +202,13 @@ def _mlp(in_channels, num_target, depth):
     return nn.ModuleList(layers)
 
 
-def _edge_pool(x, rbf_filter, edge_index_0, num_atoms, atom_rowptr):
-    """sum over edges e with source atom n of rbf_filter[e] * x[e] -> [num_atoms, D]."""
+def _edge_pool(x, rbf, lin_rbf, edge_index_0, num_atoms, atom_rowptr):
+    """sum over edges e with source atom n of lin_rbf(rbf)[e] * x[e] -> [num_atoms, D]."""
     if atom_rowptr is None:
         atom_rowptr = ops.csr_rowptr(edge_index_0, num_atoms)
-    return ops.segment_sum(x, atom_rowptr, num_atoms, mul=rbf_filter)
+    if ops.gate_supported(x.shape[1], rbf.shape[1]):  # the [E, D] filter is never materialised
+        return ops.rbf_pool(x, rbf, lin_rbf.weight, lin_rbf.bias, edge_index_0, atom_rowptr, num_atoms)
+    return ops.segment_sum(x, atom_rowptr, num_atoms, mul=lin_rbf(rbf))
 
 
 class AtomWise(nn.Module):
@@ -217,7 +220,7 @@ class AtomWise(nn.Module):
         self.lin_rbf = Linear(rbf_dim, in_channels)
 
     def forward(self, x, rbf, num_atoms, edge_index_0, atom_rowptr=None):
-        out = _edge_pool(x, self.lin_rbf(rbf), edge_index_0, num_atoms, atom_rowptr)
+        out = _edge_pool(x, rbf, self.lin_rbf, edge_index_0, num_atoms, atom_rowptr)
         return run_mlp(self.mlp, out)
 
 
@@ -233,7 +236,7 @@ class MolWise(nn.Module):
         self.pool_option = pool_option
 
     def forward(self, x, rbf, num_atoms, edge_index_0, atom_batch, dim_size, atom_rowptr=None, mol_rowptr=None):
-        out = _edge_pool(x, self.lin_rbf(rbf), edge_index_0, num_atoms, atom_rowptr)
+        out = _edge_pool(x, rbf, self.lin_rbf, edge_index_0, num_atoms, atom_rowptr)
         if mol_rowptr is None:
             mol_rowptr = ops.csr_rowptr(atom_batch, dim_size)
         pooled = ops.segment_sum(out, mol_rowptr, dim_size)

@@ -128,6 +128,52 @@ def bessel_env(dist, cutoff: float = 5.0):
     return out
 
 
+class _EdgeBasis(torch.autograd.Function):
+    """dist, env, rbf_env = sin(freq * d / cutoff) * env, bessel_env in one kernel
+    (x2g_edge_basis); the backward gives the RadialBasis.frequencies gradient."""
+
+    @staticmethod
+    def forward(ctx, freq, pos, lg, cutoff):
+        E, R = lg.E, freq.shape[0]
+        f32 = dict(dtype=torch.float32, device=pos.device)
+        dist, env = torch.empty(E, **f32), torch.empty(E, **f32)
+        rbf, bes = torch.empty(E, R, **f32), torch.empty(E, 42, **f32)
+        call("x2g_edge_basis", ptr(_f32(pos)), ptr(lg.edge_src), ptr(lg.edge_dst), E, float(cutoff), ptr(_f32(freq)), R,
+             ptr(dist), ptr(env), ptr(rbf), ptr(bes), stream_ptr())
+        ctx.save_for_backward(dist, env, freq)
+        ctx.freq_param = freq  # the Parameter object itself (grad_sink looks at its attributes)
+        ctx.cutoff = float(cutoff)
+        ctx.mark_non_differentiable(dist, env, bes)
+        ctx.set_materialize_grads(False)
+        return dist, env, rbf, bes
+
+    @staticmethod
+    def backward(ctx, _gd, _ge, grbf, _gb):
+        if grbf is None or not ctx.needs_input_grad[0]:
+            return None, None, None, None
+        dist, env, freq = ctx.saved_tensors
+        E, R = dist.shape[0], freq.shape[0]
+        lib = _lib.load()
+        sink = grad_sink(ctx.freq_param)
+        dfreq = sink if sink is not None else torch.empty(R, dtype=torch.float32, device=dist.device)
+        ws_bytes = int(lib.x2g_edge_basis_freq_grad_workspace(E, R))
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dist.device)
+        defer = sink is not None and _DEFER is not None and E > 0
+        flags = (ACCUM_WGRAD if sink is not None else 0) | (DEFER_SLAB_SUM if defer else 0)
+        call("x2g_edge_basis_freq_grad", ptr(_f32(grbf)), ptr(dist), ptr(env), ptr(freq), E, R, ctx.cutoff, ptr(dfreq),
+             flags, ptr(ws), ws_bytes, stream_ptr())
+        if defer:
+            _defer_job(ws, 0, int(lib.x2g_edge_basis_freq_grad_splits(E)), R, 0, dfreq, None)
+        return (None if sink is not None else dfreq), None, None, None
+
+
+def edge_basis(pos, lg: LineGraph, freq, cutoff: float = 5.0):
+    """(dist [E], env [E], rbf_env [E, R] = sin(freq d / cutoff) env, bessel_env [E, 42]) for the
+    line graph's directed edges; rbf_env carries the gradient to ``freq`` (xgnn.py:49-53,66-70)."""
+    _need_cuda(pos, freq)
+    return _EdgeBasis.apply(freq, pos, lg, cutoff)
+
+
 def spherical_basis(pos, lg: LineGraph, rbf_env, want_cos=False):
     """[T, 42] sbf = rbf_env[src] * Y_l0(theta), theta from the triplet's atom positions."""
     _need_cuda(pos, rbf_env)
@@ -176,6 +222,9 @@ class _SBFAttention(torch.autograd.Function):
         ctx.lg, ctx.edge_mode, ctx.edge_row, ctx.heads, ctx.channels = lg, edge_mode, edge_row, heads, channels
         ctx.edge_shape = None if edge is None else edge.shape
         ctx.mark_non_differentiable(alpha, smax, sden)
+        # the logits / max / denominator outputs never receive gradients: do not let autograd
+        # materialise zero-filled [T, H] / [E, H] tensors for them (three fill launches per layer)
+        ctx.set_materialize_grads(False)
         return out, alpha, smax, sden
 
     @staticmethod
@@ -468,13 +517,18 @@ class _ConvProjFn(torch.autograd.Function):
         x2, rbf2 = _f32(x), _f32(rbf)
         Wr, Wq, Wk, Wv, Ws = (_f32(t) for t in (wr, wq, wk, wv, ws))
         Bq, Bk, Bv, Bs = (_f32(t) if t is not None else None for t in (bq, bk, bv, bs))
-        rf, _ = _dense_fwd_raw(rbf2, Wr, None, ACT_NONE)
-        xs = x2 * rf
+        if gate_supported(D, rbf2.shape[1]):  # x_src = x * lin_rbf(rbf), filter not materialised
+            rf = None
+            xs = torch.empty_like(x2)
+            call("x2g_rbf_gate_fwd", ptr(x2), ptr(rbf2), ptr(Wr), None, E, D, rbf2.shape[1], ptr(xs), stream_ptr())
+        else:
+            rf, _ = _dense_fwd_raw(rbf2, Wr, None, ACT_NONE)
+            xs = x2 * rf
         q, _ = _dense_fwd_raw(x2, Wq, Bq, ACT_NONE)
         k, _ = _dense_fwd_raw(xs, Wk, Bk, ACT_NONE)
         v, _ = _dense_fwd_raw(xs, Wv, Bv, ACT_NONE)
         skip, _ = _dense_fwd_raw(x2, Ws, Bs, ACT_NONE)
-        ctx.save_for_backward(x2, rbf2, rf, xs, Wr, Wq, Wk, Wv, Ws)
+        ctx.save_for_backward(x2, rbf2, rf, xs, Wr, Wq, Wk, Wv, Ws)  # rf None on the gate path
         ctx.params = (wr, wq, bq, wk, bk, wv, bv, ws, bs)
         return q, k, v, skip
 
@@ -486,15 +540,81 @@ class _ConvProjFn(torch.autograd.Function):
         gxs, dwk, dbk = _dense_bwd_raw(g[1], None, ACT_NONE, xs, Wk, wk, bk, bk is not None, True)
         gxs, dwv, dbv = _dense_bwd_raw(g[2], None, ACT_NONE, xs, Wv, wv, bv, bv is not None, True, dx_add=gxs,
                                        dx_out=gxs)
-        grf = gxs * x2  # d rf
-        gx = gxs * rf   # x_src = x * rf
+        need_rbf = ctx.needs_input_grad[1]
+        if rf is None:  # one pass: gx = gxs * f, grbf, dWr
+            gx, grbf, dwr, _ = _gate_bwd(gxs, None, x2, rbf2, Wr, None, wr, None, True, need_rbf)
+        else:
+            grf = gxs * x2  # d rf
+            gx = gxs * rf   # x_src = x * rf
         gx, dwq, dbq = _dense_bwd_raw(g[0], None, ACT_NONE, x2, Wq, wq, bq, bq is not None, True, dx_add=gx,
                                       dx_out=gx)
         gx, dws, dbs = _dense_bwd_raw(g[3], None, ACT_NONE, x2, Ws, ws, bs, bs is not None, True, dx_add=gx,
                                       dx_out=gx)
-        need_rbf = ctx.needs_input_grad[1]
-        grbf, dwr, _ = _dense_bwd_raw(grf, None, ACT_NONE, rbf2, Wr, wr, None, False, need_rbf)
+        if rf is not None:
+            grbf, dwr, _ = _dense_bwd_raw(grf, None, ACT_NONE, rbf2, Wr, wr, None, False, need_rbf)
         return gx, (grbf if need_rbf else None), dwr, dwq, dbq, dwk, dbk, dwv, dbv, dws, dbs
+
+
+def gate_supported(D, R):
+    """Shapes the rbf-gate kernels are compiled for (csrc/rbf_gate.hip)."""
+    return D in (64, 128, 256) and 1 <= R <= 8
+
+
+def _gate_bwd(g, owner, x, rbf, w, b, w_param, b_param, need_dx, need_rbf, dx_add=None):
+    """x2g_rbf_gate_bwd: (dx, drbf, dw, db); dw / db are None when summed into the gradient bucket."""
+    rows, D = x.shape
+    R = rbf.shape[1]
+    dev = x.device
+    dx = torch.empty(rows, D, dtype=torch.float32, device=dev) if need_dx else None
+    drbf = torch.empty(rows, R, dtype=torch.float32, device=dev) if need_rbf else None
+    has_bias = b is not None
+    gw, gb = grad_sink(w_param), (grad_sink(b_param) if has_bias else None)
+    accum = gw is not None and (gb is not None or not has_bias)
+    if accum:
+        dw, db = gw, gb
+    else:
+        dw = torch.empty(D, R, dtype=torch.float32, device=dev)
+        db = torch.empty(D, dtype=torch.float32, device=dev) if has_bias else None
+    lib = _lib.load()
+    ws_bytes = int(lib.x2g_rbf_gate_bwd_workspace(rows, D, R))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    defer = accum and _DEFER is not None and rows > 0
+    flags = (ACCUM_WGRAD if accum else 0) | (DEFER_SLAB_SUM if defer else 0)
+    call("x2g_rbf_gate_bwd", ptr(g), ptr(owner), ptr(x), ptr(rbf), ptr(w), ptr(b), rows, D, R, ptr(dx), ptr(dx_add),
+         ptr(drbf), ptr(dw), ptr(db), flags, ptr(ws), ws_bytes, stream_ptr())
+    if defer:
+        _defer_job(ws, 0, int(lib.x2g_rbf_gate_bwd_splits(rows)), D * R, D, dw, db)
+    return dx, drbf, (None if accum else dw), (None if accum else db)
+
+
+class _RbfPoolFn(torch.autograd.Function):
+    """out[n] = sum over rows e of segment n of x[e] * (W rbf[e] + b) (readout.py:39-41,66-67:
+    lin_rbf(rbf) * x pooled edges -> atoms) without the [E, D] filter tensor."""
+
+    @staticmethod
+    def forward(ctx, x, rbf, w, b, owner, rowptr, n_seg):
+        x2, rbf2, W = _f32(x), _f32(rbf), _f32(w)
+        B = _f32(b) if b is not None else None
+        D, R = x2.shape[1], rbf2.shape[1]
+        out = torch.empty(n_seg, D, dtype=torch.float32, device=x2.device)
+        call("x2g_rbf_pool_fwd", ptr(x2), ptr(rbf2), ptr(W), ptr(B), ptr(rowptr), n_seg, D, R, ptr(out), stream_ptr())
+        ctx.save_for_backward(x2, rbf2, W, B)
+        ctx.owner, ctx.params = owner, (w, b)
+        return out
+
+    @staticmethod
+    def backward(ctx, gp):
+        x2, rbf2, W, B = ctx.saved_tensors
+        w, b = ctx.params
+        dx, drbf, dw, db = _gate_bwd(_f32(gp), ctx.owner, x2, rbf2, W, B, w, b, ctx.needs_input_grad[0],
+                                     ctx.needs_input_grad[1])
+        return dx, drbf, dw, db, None, None, None
+
+
+def rbf_pool(x, rbf, weight, bias, owner, rowptr, n_seg: int):
+    """Segment sums of x * lin_rbf(rbf) over rows sorted by ``owner`` (CSR ``rowptr``)."""
+    _need_cuda(x, rbf)
+    return _RbfPoolFn.apply(x, rbf, weight, bias, _i32(owner), _i32(rowptr), int(n_seg))
 
 
 def conv_projections(x, rbf, wr, wq, bq, wk, bk, wv, bv, ws, bs):

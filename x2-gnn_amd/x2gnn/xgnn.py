@@ -29,6 +29,7 @@ from .plan import GraphPlan
 class _XGNNBase(nn.Module):
     def _build(self, trunk, sbf_dim, rbf_dim, in_channels, embedding_size, device):
         self.device = device
+        self.cutoff = 5.0  # xgnn.py:30-33 (envelope, sbf and rbf layers all use 5.0)
         self.AF = SiLU()
         self.emb_block = EmbeddingBlock(embedding_size=embedding_size)
         self.envelop_function = poly_envelop(cutoff=5.0, exponent=5)
@@ -39,6 +40,12 @@ class _XGNNBase(nn.Module):
         self.rbf_trans = Linear(rbf_dim, embedding_size)  # unused by the reference forward too
         self.emb_trans = Linear(embedding_size * 2, in_channels)
 
+    def _fused_basis(self):
+        env, rbf = self.envelop_function, self.rbf_layer
+        return (env.exponent == 5 and abs(env.inv_cutoff * self.cutoff - 1.0) < 1e-12
+                and isinstance(getattr(rbf, "frequencies", None), torch.Tensor) and rbf.frequencies.numel() <= 16
+                and abs(rbf.inv_cutoff * self.cutoff - 1.0) < 1e-12)
+
     def line_graph_data(self, data):
         """Featurisation (reference xgnn.py:39-72) -> (line-graph Data, GraphPlan)."""
         if "batch" not in data._store:  # single molecule: the reference adds a zero batch vector
@@ -46,12 +53,17 @@ class _XGNNBase(nn.Module):
         plan = GraphPlan.from_atom_batch(data)
         lg = plan.lg
         pos = data.atom_pos
-        dist = (pos.index_select(0, lg.edge_src) - pos.index_select(0, lg.edge_dst)).norm(dim=1)
-        env = self.envelop_function(dist).unsqueeze(1)
+        if self._fused_basis():  # distances, envelope, radial basis and the 42 Bessel terms: one kernel
+            dist, env, node_rbf, bessel = ops.edge_basis(pos, lg, self.rbf_layer.frequencies, self.cutoff)
+            env = env.unsqueeze(1)
+        else:
+            dist = (pos.index_select(0, lg.edge_src) - pos.index_select(0, lg.edge_dst)).norm(dim=1)
+            env = self.envelop_function(dist).unsqueeze(1)
+            node_rbf = self.rbf_layer(dist) * env
+            bessel = None
         neo_x = self.mat_trans.fused(data.edge_attr * env, act=ops.ACT_SILU)
         table = self.emb_block.element_table(data.x)
-        sbf = self.sbf_layer.from_positions(dist, pos, lg)
-        node_rbf = self.rbf_layer(dist) * env
+        sbf = self.sbf_layer.from_positions(dist, pos, lg, bessel)
         neo_x = self.emb_trans.fused(neo_x, act=ops.ACT_SILU)
         line = Data(x=neo_x, edge_attr=table, edge_attr_row=plan.dst_type, edge_sbf=sbf, node_rbf=node_rbf)
         line._store["_x2g_plan"] = plan
