@@ -100,6 +100,22 @@ int x2g_edge_basis_freq_grad(const float* g, const float* dist, const float* env
                              int64_t num_edges, int32_t num_radial, float cutoff, float* dfreq, int flags,
                              void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------- element embedding table
+ * EmbeddingBlock's Embedding(num_embeddings, D, padding_idx, max_norm, scale_grad_by_freq)
+ * (atom_embedding.py:13-25) evaluated once per ELEMENT instead of per atom:
+ *   counts[v] = #{n : z[n] == v}  (exact, integer atomics),
+ *   rows v with counts[v] > 0 and ||weight[v]||_2 > max_norm are rescaled IN PLACE by
+ *   max_norm / (norm + 1e-7)  (torch.embedding_renorm_; max_norm <= 0 disables),
+ *   table[v, :] = weight[v, :] after the renorm.
+ * z: int64 atomic numbers in [0, V), V <= 64.  One workgroup. */
+int x2g_embedding_table(float* weight, const int64_t* z, int64_t num_atoms, int32_t num_embeddings, int32_t dim,
+                        float max_norm, float* counts, float* table, void* stream);
+
+/* d weight[v, :] (+)= g[v, :] / max(counts[v], 1)  (scale_grad_by_freq; counts NULL: no scaling),
+ * zero for v == padding_idx (< 0: none); flags X2G_ACCUM_WGRAD (+=). */
+int x2g_embedding_table_bwd(const float* g, const float* counts, int32_t num_embeddings, int32_t dim,
+                            int32_t padding_idx, float* dweight, int flags, void* stream);
+
 /* ---------------------------------------------------------------- rbf gates (x * lin_rbf(rbf))
  * f[e, c] = sum_j w[c, j] rbf[e, j] + b[c]   (w [D, R] row-major, R <= 8, b optional; D % 4 == 0)
  * gate:  out[e, :] = x[e, :] * f[e, :]                 (SBFTransformerConv x_src,
@@ -191,6 +207,15 @@ int x2g_segment_sum(const float* x, const float* mul, const int32_t* rowptr, int
 /* out[r, :] = g[seg(r), :] (* mul[r, :] if mul != NULL): adjoint of x2g_segment_sum. */
 int x2g_segment_broadcast(const float* g, const float* mul, const int32_t* rowptr, int64_t num_segments,
                           int64_t dim, float* out, void* stream);
+
+/* out[k, :] (+)= sum_{r : key[r] == k} src[r, :]  for an UNSORTED key in [0, num_keys), num_keys <= 16,
+ * dim % 4 == 0, dim <= 256: the gradient of a row gather table[key] (the per-element edge table
+ * that every triplet of destination e reads, xgnn.py:57-58 -> lin_edge, sbftransformer_conv.py:144).
+ * Deterministic: per-workgroup partials in LDS (one accumulator set per row slot) + a fixed-order
+ * sum; flags X2G_ACCUM_WGRAD (out +=). */
+size_t x2g_keyed_row_sum_workspace(int64_t rows, int32_t dim, int32_t num_keys);
+int x2g_keyed_row_sum(const float* src, const int32_t* key, int64_t rows, int32_t dim, int32_t num_keys,
+                      float* out, int flags, void* workspace, size_t workspace_bytes, void* stream);
 
 /* PyG utils.softmax(src[R,H], index) for a sorted index (CSR rowptr): per segment and column,
  * exp(src - max) / (sum + 1e-16). */
@@ -288,6 +313,64 @@ int x2g_dense_bwd(const float* dy, const float* z, int act, const float* x, cons
 int x2g_dense_bwd_ex(const float* dy, const float* z, int act, const float* x, const float* w, int64_t rows,
                      int32_t in_features, int32_t out_features, float* dx, const float* dx_add, float* dw,
                      float* db, int flags, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- batched layers (readout MLPs)
+ * The trunk's conv_layers+1 readouts (model.py:41,50) run the same MLP shape on different inputs
+ * with different weights: Linear(D,D)+SiLU, Linear(D,D)+SiLU, Linear(D,1) (readout.py:25-31,
+ * 55-62), summed over readouts.  Each batched call runs G <= X2G_MAX_GROUPS of those layers in
+ * one launch (blockIdx.y = group).  Supported: in/out features <= 128, multiples of 4, 16-byte
+ * aligned rows (X2G_EUNSUPPORTED otherwise).  Group arrays are host memory, read at the call. */
+#define X2G_MAX_GROUPS 8
+
+typedef struct {
+  const float* x;   /* [R, K] */
+  const float* w;   /* [N, K] */
+  const float* b;   /* [N] or NULL */
+  const float* res; /* [R, N] or NULL */
+  float* y;         /* [R, N] */
+  float* z;         /* [R, N] pre-activation or NULL */
+} x2g_dense_fwd_group;
+
+typedef struct {
+  const float* dy;     /* [R, N] */
+  const float* z;      /* [R, N] (act == X2G_ACT_SILU) */
+  const float* x;      /* [R, K] */
+  const float* w;      /* [N, K] */
+  float* dx;           /* [R, K] or NULL */
+  const float* dx_add; /* [R, K] or NULL */
+  float* dw;           /* [N, K] */
+  float* db;           /* [N] or NULL */
+} x2g_dense_bwd_group;
+
+int x2g_dense_fwd_batched(const x2g_dense_fwd_group* groups, int32_t num_groups, int64_t rows,
+                          int32_t in_features, int32_t out_features, int act, void* stream);
+
+/* Workspace: num_groups * x2g_dense_bwd_workspace(rows, K, N); group g's weight-gradient slabs
+ * (x2g_dense_bwd_splits of them) start at byte g * x2g_dense_bwd_workspace(rows, K, N).  Flags as
+ * x2g_dense_bwd_ex; without X2G_DEFER_SLAB_SUM one x2g_slab_sum_batch launch sums all groups. */
+int x2g_dense_bwd_batched(const x2g_dense_bwd_group* groups, int32_t num_groups, int64_t rows,
+                          int32_t in_features, int32_t out_features, int act, int flags, void* workspace,
+                          size_t workspace_bytes, void* stream);
+
+/* The readouts' last Linear(D, 1) summed over groups: out[r] = sum_g (h_g[r, :] . w_g + b_g). */
+typedef struct {
+  const float* h; /* [R, D] */
+  const float* w; /* [D] */
+  const float* b; /* [1] or NULL */
+  float* dh;      /* backward: [R, D] = dout[r] * w_g (NULL: not needed) */
+  float* dw;      /* backward: [D] */
+  float* db;      /* backward: [1] or NULL */
+} x2g_head_group;
+
+int x2g_readout_head_fwd(const x2g_head_group* groups, int32_t num_groups, int64_t rows, int32_t dim, float* out,
+                         void* stream);
+size_t x2g_readout_head_bwd_workspace(int64_t rows, int32_t dim, int32_t num_groups);
+int32_t x2g_readout_head_bwd_splits(int64_t rows);
+/* dh_g = dout w_g^T, dw_g (+)= sum_r dout[r] h_g[r], db_g (+)= sum_r dout[r]; flags as
+ * x2g_linear_wgrad_ex (group g's slabs: splits*dim floats at g*splits*(dim+1) floats into the
+ * workspace, then its bias slabs: splits floats). */
+int x2g_readout_head_bwd(const float* dout, const x2g_head_group* groups, int32_t num_groups, int64_t rows,
+                         int32_t dim, int flags, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- parameter update */
 

@@ -596,3 +596,72 @@ def test_rbf_pool_vs_torch(cuda):
     torch.testing.assert_close(rr.grad, rq.grad, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(w.grad, wq.grad, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(b.grad, bq.grad, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("R,D,K", [(0, 128, 10), (1, 128, 10), (21058, 128, 10), (999, 64, 16), (5000, 12, 3)])
+def test_keyed_row_sum_vs_torch(cuda, R, D, K):
+    """x2g_keyed_row_sum (gradient of a per-element table gather) vs index_add, and bitwise repeatable."""
+    from x2gnn import ops
+
+    g = torch.Generator().manual_seed(R + D)
+    src = torch.randn(R, D, generator=g).to(cuda)
+    key = torch.randint(0, K, (R,), generator=g).to(torch.int32).to(cuda)
+    out = ops.keyed_row_sum(src, key, K)
+    ref = torch.zeros(K, D, device=cuda).index_add_(0, key.long(), src)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-4)
+    assert torch.equal(out, ops.keyed_row_sum(src, key, K))
+
+
+@pytest.mark.parametrize("max_norm", [None, 3.0, 0.5])
+def test_embedding_table_vs_torch(cuda, max_norm):
+    """x2g_embedding_table (in-place renorm of the used rows, per-element rows) and its backward
+    (scale_grad_by_freq, padding row) vs nn.Embedding on the same atoms."""
+    from x2gnn import ops
+
+    g = torch.Generator().manual_seed(11)
+    z = torch.tensor([1, 6, 6, 8, 1, 1, 7, 0, 6, 1], dtype=torch.int64)
+    ref = torch.nn.Embedding(10, 32, padding_idx=0, max_norm=max_norm, scale_grad_by_freq=True).to(cuda)
+    with torch.no_grad():
+        ref.weight.copy_(torch.randn(10, 32, generator=g).to(cuda))
+    w = torch.nn.Parameter(ref.weight.detach().clone())
+    table = ops.embedding_table(w, z.to(cuda), max_norm, 0, True)
+    out = ref(z.to(cuda))
+    torch.testing.assert_close(w.detach(), ref.weight.detach(), rtol=1e-6, atol=1e-7)  # same in-place renorm
+    torch.testing.assert_close(table[z.to(cuda)], out.detach(), rtol=1e-6, atol=1e-7)
+    up = torch.randn(10, 32, generator=g).to(cuda)
+    out.backward(up)
+    # the per-atom upstream gradient summed per element is what the table receives
+    gt = torch.zeros(10, 32, device=cuda).index_add_(0, z.to(cuda), up)
+    table.backward(gt)
+    torch.testing.assert_close(w.grad, ref.weight.grad, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("R,G", [(2304, 5), (1, 1), (37, 8), (128, 5)])
+def test_readout_mlps_batched_vs_separate(cuda, R, G):
+    """ops.readout_mlps (batched dense fwd/bwd + the fused Linear(D,1) head summed over readouts)
+    equals sum_g run_mlp(mlp_g, feat_g) in value and in every gradient."""
+    from x2gnn import ops
+    from x2gnn.layers import _mlp, run_mlp
+
+    torch.manual_seed(R + G)
+    mlps = [_mlp(128, 1, 3).to(cuda) for _ in range(G)]
+    mlps_ref = [_mlp(128, 1, 3).to(cuda) for _ in range(G)]
+    for a, b in zip(mlps, mlps_ref):
+        b.load_state_dict(a.state_dict())
+    feats = [torch.randn(R, 128, device=cuda, requires_grad=True) for _ in range(G)]
+    feats_ref = [f.detach().clone().requires_grad_(True) for f in feats]
+    assert ops.readout_mlps_supported(feats, mlps)
+    out = ops.readout_mlps(feats, mlps)
+    ref = None
+    for m, f in zip(mlps_ref, feats_ref):
+        r = run_mlp(m, f)
+        ref = r if ref is None else ref + r
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+    up = torch.randn(R, 1, device=cuda)
+    out.backward(up)
+    ref.backward(up)
+    for f, fr in zip(feats, feats_ref):
+        torch.testing.assert_close(f.grad, fr.grad, rtol=1e-5, atol=1e-5)
+    for a, b in zip(mlps, mlps_ref):
+        for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
+            torch.testing.assert_close(p.grad, q.grad, rtol=1e-4, atol=1e-4, msg=n)

@@ -758,12 +758,11 @@ __device__ __forceinline__ void epi_tile(const float* __restrict__ buf, const St
   }
 }
 
-__global__ void __launch_bounds__(256, 2) dense_fwd_v6(const float* __restrict__ X, const float* __restrict__ W,
-                                                       const float* __restrict__ bias, const float* __restrict__ res,
-                                                       int64_t R, int K, int N, int act, float* __restrict__ Y,
-                                                       float* __restrict__ Z) {
-  __shared__ __attribute__((aligned(16))) float Ws[64 * 256];
-  __shared__ __attribute__((aligned(16))) float Xs[32 * 128];  // x tile, then the output tile
+__device__ __forceinline__ void dense_fwd_v6_body(const float* __restrict__ X, const float* __restrict__ W,
+                                                  const float* __restrict__ bias, const float* __restrict__ res,
+                                                  int64_t R, int K, int N, int act, float* __restrict__ Y,
+                                                  float* __restrict__ Z, float* __restrict__ Ws,
+                                                  float* __restrict__ Xs /* x tile, then the output tile */) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, i = lane & 31;
   const int n = 32 * wave + i;
   const int q = tid & 31;
@@ -829,6 +828,28 @@ __global__ void __launch_bounds__(256, 2) dense_fwd_v6(const float* __restrict__
     if (more) xtile_store(Xs, nxt);
     __syncthreads();
   }
+}
+
+__global__ void __launch_bounds__(256, 2) dense_fwd_v6(const float* __restrict__ X, const float* __restrict__ W,
+                                                       const float* __restrict__ bias, const float* __restrict__ res,
+                                                       int64_t R, int K, int N, int act, float* __restrict__ Y,
+                                                       float* __restrict__ Z) {
+  __shared__ __attribute__((aligned(16))) float Ws[64 * 256];
+  __shared__ __attribute__((aligned(16))) float Xs[32 * 128];
+  dense_fwd_v6_body(X, W, bias, res, R, K, N, act, Y, Z, Ws, Xs);
+}
+
+// G independent layers of one shape in one launch (blockIdx.y = layer): the readout MLPs
+struct DenseFwdBatch {
+  x2g_dense_fwd_group g[X2G_MAX_GROUPS];
+};
+
+__global__ void __launch_bounds__(256, 2) dense_fwd_v6_batched(const DenseFwdBatch b, int64_t R, int K, int N,
+                                                               int act) {
+  __shared__ __attribute__((aligned(16))) float Ws[64 * 256];
+  __shared__ __attribute__((aligned(16))) float Xs[32 * 128];
+  const x2g_dense_fwd_group& p = b.g[blockIdx.y];
+  dense_fwd_v6_body(p.x, p.w, p.b, p.res, R, K, N, act, p.y, p.z, Ws, Xs);
 }
 
 // ---------------------------------------------------------------- forward, narrow K (K % 4 != 0)
@@ -1079,14 +1100,12 @@ __device__ __forceinline__ f4 mask4(f4 v, int64_t tp, int U, int64_t R, int cols
   return ok ? v : f4{0.f, 0.f, 0.f, 0.f};
 }
 
-__global__ void __launch_bounds__(512) dense_bwd_v5(const float* __restrict__ dY, const float* __restrict__ Zin,
-                                                    const float* __restrict__ X, const float* __restrict__ W,
-                                                    int64_t R, int K, int N, int act, float* __restrict__ dX,
-                                                    const float* __restrict__ dXadd, float* __restrict__ part_w,
-                                                    float* __restrict__ part_b) {
-  __shared__ __attribute__((aligned(16))) float Ws[64 * kSlotStride];
-  __shared__ __attribute__((aligned(16))) float Ds[64 * 128];
-  __shared__ __attribute__((aligned(16))) float Xs[64 * 128];
+__device__ __forceinline__ void dense_bwd_v5_body(const float* __restrict__ dY, const float* __restrict__ Zin,
+                                                  const float* __restrict__ X, const float* __restrict__ W, int64_t R,
+                                                  int K, int N, int act, float* __restrict__ dX,
+                                                  const float* __restrict__ dXadd, float* __restrict__ part_w,
+                                                  float* __restrict__ part_b, float* __restrict__ Ws,
+                                                  float* __restrict__ Ds, float* __restrict__ Xs) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, i = lane & 31;
   const int64_t ntiles = (R + 63) / 64;
   const int64_t G = gridDim.x;
@@ -1197,6 +1216,32 @@ __global__ void __launch_bounds__(512) dense_bwd_v5(const float* __restrict__ dY
     if (nn < N && k1 < K) slab[nn * K + k1] = accw1[j];
   }
   if (part_b && tid < N) part_b[static_cast<int64_t>(blockIdx.x) * N + tid] = bsum;
+}
+
+__global__ void __launch_bounds__(512) dense_bwd_v5(const float* __restrict__ dY, const float* __restrict__ Zin,
+                                                    const float* __restrict__ X, const float* __restrict__ W,
+                                                    int64_t R, int K, int N, int act, float* __restrict__ dX,
+                                                    const float* __restrict__ dXadd, float* __restrict__ part_w,
+                                                    float* __restrict__ part_b) {
+  __shared__ __attribute__((aligned(16))) float Ws[64 * kSlotStride];
+  __shared__ __attribute__((aligned(16))) float Ds[64 * 128];
+  __shared__ __attribute__((aligned(16))) float Xs[64 * 128];
+  dense_bwd_v5_body(dY, Zin, X, W, R, K, N, act, dX, dXadd, part_w, part_b, Ws, Ds, Xs);
+}
+
+struct DenseBwdBatch {
+  x2g_dense_bwd_group g[X2G_MAX_GROUPS];
+  float* part_w[X2G_MAX_GROUPS];
+  float* part_b[X2G_MAX_GROUPS];
+};
+
+__global__ void __launch_bounds__(512) dense_bwd_v5_batched(const DenseBwdBatch b, int64_t R, int K, int N, int act) {
+  __shared__ __attribute__((aligned(16))) float Ws[64 * kSlotStride];
+  __shared__ __attribute__((aligned(16))) float Ds[64 * 128];
+  __shared__ __attribute__((aligned(16))) float Xs[64 * 128];
+  const int gi = blockIdx.y;
+  const x2g_dense_bwd_group& p = b.g[gi];
+  dense_bwd_v5_body(p.dy, p.z, p.x, p.w, R, K, N, act, p.dx, p.dx_add, b.part_w[gi], b.part_b[gi], Ws, Ds, Xs);
 }
 
 }  // namespace x2g
@@ -1397,4 +1442,52 @@ X2G_API int x2g_dense_bwd(const float* dy, const float* z, int act, const float*
                           int32_t K, int32_t N, float* dx, float* dw, float* db, void* workspace,
                           size_t workspace_bytes, void* stream) {
   return x2g_dense_bwd_ex(dy, z, act, x, w, R, K, N, dx, nullptr, dw, db, 0, workspace, workspace_bytes, stream);
+}
+
+// ------------------------------------------------------------------------------- batched layers
+X2G_API int x2g_dense_fwd_batched(const x2g_dense_fwd_group* groups, int32_t G, int64_t R, int32_t K, int32_t N,
+                                  int act, void* stream) {
+  if (!groups || G < 1 || G > X2G_MAX_GROUPS || R < 0 || K <= 0 || N <= 0 || (act != kActNone && act != kActSilu))
+    return X2G_EINVAL;
+  if (R == 0) return X2G_OK;
+  if (K > 128 || N > 128 || K % 4 || N % 4 || K <= 8 || R * 128 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  DenseFwdBatch b{};
+  for (int g = 0; g < G; ++g) {
+    const x2g_dense_fwd_group& p = groups[g];
+    if (!p.x || !p.w || !p.y) return X2G_EINVAL;
+    if (!aligned16(p.x) || !aligned16(p.y) || !aligned16(p.z) || !aligned16(p.res)) return X2G_EUNSUPPORTED;
+    b.g[g] = p;
+  }
+  const int64_t ntiles = (R + 31) / 32;
+  const dim3 grid(static_cast<unsigned>(ntiles < 512 ? ntiles : 512), G);
+  dense_fwd_v6_batched<<<grid, 256, 0, as_stream(stream)>>>(b, R, K, N, act);
+  return last_launch_status();
+}
+
+X2G_API int x2g_dense_bwd_batched(const x2g_dense_bwd_group* groups, int32_t G, int64_t R, int32_t K, int32_t N,
+                                  int act, int flags, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!groups || G < 1 || G > X2G_MAX_GROUPS || R <= 0 || K <= 0 || N <= 0 ||
+      (act != kActNone && act != kActSilu) || (flags & ~(X2G_ACCUM_WGRAD | X2G_DEFER_SLAB_SUM)))
+    return X2G_EINVAL;
+  if (!dense_persistent_bwd(R, K, N) || K % 4 || N % 4 || N <= 8) return X2G_EUNSUPPORTED;
+  const size_t wsz = x2g_dense_bwd_workspace(R, K, N);
+  if (!workspace || workspace_bytes < wsz * G) return X2G_EWORKSPACE;
+  const int grid = static_cast<int>(bwd_grid(R));
+  DenseBwdBatch b{};
+  x2g_slab_job jobs[X2G_MAX_GROUPS];
+  for (int g = 0; g < G; ++g) {
+    const x2g_dense_bwd_group& p = groups[g];
+    if (!p.dy || !p.x || !p.w || !p.dw || (act == kActSilu && !p.z) || (p.dx_add && !p.dx)) return X2G_EINVAL;
+    if (!aligned16(p.dy) || !aligned16(p.z) || !aligned16(p.x) || !aligned16(p.dx) || !aligned16(p.dx_add))
+      return X2G_EUNSUPPORTED;
+    b.g[g] = p;
+    b.part_w[g] = reinterpret_cast<float*>(static_cast<char*>(workspace) + wsz * g);
+    b.part_b[g] = p.db ? b.part_w[g] + static_cast<int64_t>(grid) * N * K : nullptr;
+    jobs[g] = x2g_slab_job{b.part_w[g], b.part_b[g], p.dw, p.db, static_cast<int64_t>(N) * K, p.db ? N : 0, grid};
+  }
+  hipStream_t st = as_stream(stream);
+  dense_bwd_v5_batched<<<dim3(grid, G), 512, 0, st>>>(b, R, K, N, act);
+  if (int rc = last_launch_status()) return rc;
+  if (flags & X2G_DEFER_SLAB_SUM) return X2G_OK;
+  return x2g_slab_sum_batch(jobs, G, (flags & X2G_ACCUM_WGRAD) ? 1 : 0, stream);
 }

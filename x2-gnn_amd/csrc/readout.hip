@@ -1,0 +1,164 @@
+// The readouts' final Linear(D, 1), all readouts at once (readout.py:25-31,42 and 55-62,76; the
+// per-layer results summed in model.py:41,50-53).  Forward: out[r] = sum_g (h_g[r] . w_g + b_g),
+// 64 / LPR rows per wave, one 16-byte chunk of each row per lane, group dot products reduced
+// over the row's lanes.  Backward: dh_g[r] = dout[r] w_g (row-parallel) and dw_g / db_g as
+// per-workgroup partials (one accumulator set per row slot in LDS, folded in a fixed order) +
+// the batched fixed-order slab sum.
+#include "common.hpp"
+
+namespace x2g {
+
+constexpr int kHeadSplits = 256;
+
+struct HeadBatch {
+  x2g_head_group g[X2G_MAX_GROUPS];
+};
+
+typedef float f4h __attribute__((ext_vector_type(4)));
+
+template <int LPR>
+__global__ void __launch_bounds__(256) readout_head_fwd_kernel(const HeadBatch b, int G, int64_t R,
+                                                               float* __restrict__ out) {
+  constexpr int RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, sub = lane % LPR;
+  const int64_t nw = static_cast<int64_t>(gridDim.x) * 4;
+  for (int64_t r = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR; r < R;
+       r += nw * RPW) {
+    float acc = 0.f;
+    for (int g = 0; g < G; ++g) {
+      const f4h hv = reinterpret_cast<const f4h*>(b.g[g].h)[r * LPR + sub];
+      const f4h wv = reinterpret_cast<const f4h*>(b.g[g].w)[sub];
+      float d = hv.x * wv.x + hv.y * wv.y + hv.z * wv.z + hv.w * wv.w;
+      d = group_sum<LPR>(d);
+      acc += d + (b.g[g].b ? b.g[g].b[0] : 0.f);
+    }
+    if (sub == 0) out[r] = acc;
+  }
+}
+
+// block k owns rows [k * per, (k + 1) * per); partial slabs: part[g][k][D] and part[g][splits*D + k]
+template <int LPR>
+__global__ void __launch_bounds__(256) readout_head_bwd_kernel(const float* __restrict__ dout, const HeadBatch b, int G,
+                                                               int64_t R, float* __restrict__ part) {
+  constexpr int RPB = 256 / LPR;
+  constexpr int D = 4 * LPR;
+  __shared__ f4h red[RPB * LPR];
+  __shared__ float redb[RPB];
+  const int sub = threadIdx.x % LPR, slot = threadIdx.x / LPR;
+  const int64_t per = (R + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = per * blockIdx.x, hi = lo + per < R ? lo + per : R;
+  const int splits = gridDim.x;
+  for (int g = 0; g < G; ++g) {
+    const f4h wv = reinterpret_cast<const f4h*>(b.g[g].w)[sub];
+    f4h aw = {0.f, 0.f, 0.f, 0.f};
+    float ab = 0.f;
+    for (int64_t r = lo + slot; r < hi; r += RPB) {
+      const float d = dout[r];
+      const f4h hv = reinterpret_cast<const f4h*>(b.g[g].h)[r * LPR + sub];
+      aw += hv * d;
+      ab += d;
+      if (b.g[g].dh) reinterpret_cast<f4h*>(b.g[g].dh)[r * LPR + sub] = wv * d;
+    }
+    red[slot * LPR + sub] = aw;
+    if (sub == 0) redb[slot] = ab;
+    __syncthreads();
+    float* pg = part + static_cast<int64_t>(g) * splits * (D + 1);
+    if (threadIdx.x < LPR) {
+      f4h s = {0.f, 0.f, 0.f, 0.f};
+      for (int sl = 0; sl < RPB; ++sl) s += red[sl * LPR + threadIdx.x];
+      reinterpret_cast<f4h*>(pg + static_cast<int64_t>(blockIdx.x) * D)[threadIdx.x] = s;
+    }
+    if (threadIdx.x == 0) {
+      float s = 0.f;
+      for (int sl = 0; sl < RPB; ++sl) s += redb[sl];
+      pg[static_cast<int64_t>(splits) * D + blockIdx.x] = s;
+    }
+    __syncthreads();
+  }
+}
+
+inline int head_splits(int64_t R) {
+  const int64_t want = (R + 31) / 32;
+  return static_cast<int>(want < kHeadSplits ? (want < 1 ? 1 : want) : kHeadSplits);
+}
+
+inline bool head_ok(const x2g_head_group* groups, int G, int D) {
+  if (G < 1 || G > X2G_MAX_GROUPS || D % 4 || D < 4 || D > 256 || ((D / 4) & (D / 4 - 1))) return false;
+  for (int g = 0; g < G; ++g)
+    if (!groups[g].h || !groups[g].w || reinterpret_cast<uintptr_t>(groups[g].h) % 16 ||
+        reinterpret_cast<uintptr_t>(groups[g].w) % 16 || reinterpret_cast<uintptr_t>(groups[g].dh) % 16)
+      return false;
+  return true;
+}
+
+}  // namespace x2g
+
+using namespace x2g;
+
+#define X2G_HEAD_DISPATCH(KERNEL, GRID, ...)                                     \
+  switch (D / 4) {                                                               \
+    case 1: KERNEL<1><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                 \
+    case 2: KERNEL<2><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                 \
+    case 4: KERNEL<4><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                 \
+    case 8: KERNEL<8><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;                 \
+    case 16: KERNEL<16><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;               \
+    case 32: KERNEL<32><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;               \
+    default: KERNEL<64><<<GRID, 256, 0, st>>>(__VA_ARGS__); break;               \
+  }
+
+X2G_API int x2g_readout_head_fwd(const x2g_head_group* groups, int32_t G, int64_t R, int32_t D, float* out,
+                                 void* stream) {
+  if (R < 0 || !groups || !out) return X2G_EINVAL;
+  if (!head_ok(groups, G, D)) return X2G_EUNSUPPORTED;
+  if (R == 0) return X2G_OK;
+  HeadBatch b{};
+  for (int g = 0; g < G; ++g) b.g[g] = groups[g];
+  hipStream_t st = as_stream(stream);
+  const int64_t waves = (R * (D / 4) + 63) / 64;
+  const unsigned grid = static_cast<unsigned>((waves + 3) / 4 < 2048 ? (waves + 3) / 4 : 2048);
+  X2G_HEAD_DISPATCH(readout_head_fwd_kernel, grid, b, G, R, out)
+  return last_launch_status();
+}
+
+X2G_API int32_t x2g_readout_head_bwd_splits(int64_t R) { return R > 0 ? head_splits(R) : 0; }
+
+X2G_API size_t x2g_readout_head_bwd_workspace(int64_t R, int32_t D, int32_t G) {
+  if (R <= 0 || D <= 0 || G <= 0) return 0;
+  return static_cast<size_t>(G) * head_splits(R) * (D + 1) * sizeof(float);
+}
+
+X2G_API int x2g_readout_head_bwd(const float* dout, const x2g_head_group* groups, int32_t G, int64_t R, int32_t D,
+                                 int flags, void* ws, size_t wsb, void* stream) {
+  if (R < 0 || !groups) return X2G_EINVAL;
+  if (!head_ok(groups, G, D)) return X2G_EUNSUPPORTED;
+  for (int g = 0; g < G; ++g)
+    if (!groups[g].dw) return X2G_EINVAL;
+  const bool accum = flags & X2G_ACCUM_WGRAD;
+  hipStream_t st = as_stream(stream);
+  if (R == 0) {
+    if (flags & X2G_DEFER_SLAB_SUM) return X2G_EINVAL;
+    if (accum) return X2G_OK;
+    for (int g = 0; g < G; ++g) {
+      hipError_t e = hipMemsetAsync(groups[g].dw, 0, sizeof(float) * D, st);
+      if (e == hipSuccess && groups[g].db) e = hipMemsetAsync(groups[g].db, 0, sizeof(float), st);
+      if (e != hipSuccess) return static_cast<int>(e);
+    }
+    return X2G_OK;
+  }
+  if (!dout) return X2G_EINVAL;
+  if (!ws || wsb < x2g_readout_head_bwd_workspace(R, D, G)) return X2G_EWORKSPACE;
+  HeadBatch b{};
+  for (int g = 0; g < G; ++g) b.g[g] = groups[g];
+  const int splits = head_splits(R);
+  float* part = static_cast<float*>(ws);
+  X2G_HEAD_DISPATCH(readout_head_bwd_kernel, splits, dout, b, G, R, part)
+  if (int rc = last_launch_status()) return rc;
+  if (flags & X2G_DEFER_SLAB_SUM) return X2G_OK;
+  x2g_slab_job jobs[X2G_MAX_GROUPS];
+  for (int g = 0; g < G; ++g) {
+    float* pg = part + static_cast<int64_t>(g) * splits * (D + 1);
+    jobs[g] = x2g_slab_job{pg, groups[g].db ? pg + static_cast<int64_t>(splits) * D : nullptr, groups[g].dw,
+                           groups[g].db, D, groups[g].db ? 1 : 0, splits};
+  }
+  return x2g_slab_sum_batch(jobs, G, accum ? 1 : 0, stream);
+}

@@ -481,6 +481,105 @@ X2G_API int x2g_segment_softmax_bwd(const float* out, const float* dout, const i
   return last_launch_status();
 }
 
+namespace x2g {
+
+constexpr int kKeyedMaxKeys = 16;
+constexpr int kKeyedSplits = 256;
+
+// block b sums rows [b * per, (b + 1) * per): row slot s (of 256 / LPR) adds its rows into its own
+// LDS accumulator set acc[s][key][:] (lanes own disjoint 16-byte column chunks: no races), then the
+// slots are folded in a fixed order into part[b][key][:]
+template <int LPR>
+__global__ void __launch_bounds__(256) keyed_row_sum_partial(const float4* __restrict__ src,
+                                                             const int32_t* __restrict__ key, int64_t rows, int nkeys,
+                                                             float4* __restrict__ part) {
+  constexpr int RPB = 256 / LPR;
+  __shared__ float4 acc[RPB * kKeyedMaxKeys * LPR];
+  const int sub = threadIdx.x % LPR, slot = threadIdx.x / LPR;
+  for (int i = threadIdx.x; i < RPB * kKeyedMaxKeys * LPR; i += 256) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  const int64_t per = (rows + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = per * blockIdx.x, hi = lo + per < rows ? lo + per : rows;
+  float4* mine = acc + slot * kKeyedMaxKeys * LPR + sub;
+  constexpr int U = 4;
+  for (int64_t r0 = lo + slot; r0 < hi; r0 += RPB * U) {
+    float4 v[U];
+    int k[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = r0 + u * RPB, rc = r < hi ? r : hi - 1;
+      v[u] = src[rc * LPR + sub];
+      k[u] = key[rc];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (r0 + u * RPB < hi) {
+        float4& a = mine[k[u] * LPR];
+        a.x += v[u].x;
+        a.y += v[u].y;
+        a.z += v[u].z;
+        a.w += v[u].w;
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nkeys * LPR; i += 256) {
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int sl = 0; sl < RPB; ++sl) {
+      const float4 a = acc[sl * kKeyedMaxKeys * LPR + i];
+      s.x += a.x;
+      s.y += a.y;
+      s.z += a.z;
+      s.w += a.w;
+    }
+    part[static_cast<int64_t>(blockIdx.x) * nkeys * LPR + i] = s;
+  }
+}
+
+inline int keyed_splits(int64_t rows) {
+  const int64_t want = (rows + 63) / 64;
+  return static_cast<int>(want < kKeyedSplits ? (want < 1 ? 1 : want) : kKeyedSplits);
+}
+
+}  // namespace x2g
+
+X2G_API size_t x2g_keyed_row_sum_workspace(int64_t rows, int32_t dim, int32_t nkeys) {
+  if (rows <= 0 || dim <= 0 || nkeys <= 0) return 0;
+  return static_cast<size_t>(keyed_splits(rows)) * dim * nkeys * sizeof(float);
+}
+
+X2G_API int x2g_keyed_row_sum(const float* src, const int32_t* key, int64_t rows, int32_t dim, int32_t nkeys,
+                              float* out, int flags, void* ws, size_t wsb, void* stream) {
+  if (rows < 0 || dim <= 0 || nkeys <= 0 || !out) return X2G_EINVAL;
+  if (nkeys > kKeyedMaxKeys || dim % 4 != 0 || dim > 256) return X2G_EUNSUPPORTED;
+  const bool accum = flags & X2G_ACCUM_WGRAD;
+  hipStream_t st = as_stream(stream);
+  if (rows == 0) {
+    if (accum) return X2G_OK;
+    const hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * dim * nkeys, st);
+    return e == hipSuccess ? X2G_OK : static_cast<int>(e);
+  }
+  if (!src || !key) return X2G_EINVAL;
+  if (reinterpret_cast<uintptr_t>(src) % 16) return X2G_EINVAL;
+  if (!ws || wsb < x2g_keyed_row_sum_workspace(rows, dim, nkeys)) return X2G_EWORKSPACE;
+  const int splits = keyed_splits(rows);
+  auto* part = static_cast<float4*>(ws);
+  const auto* sv = reinterpret_cast<const float4*>(src);
+  switch (dim / 4) {
+    case 1: keyed_row_sum_partial<1><<<splits, 256, 0, st>>>(sv, key, rows, nkeys, part); break;
+    case 2: keyed_row_sum_partial<2><<<splits, 256, 0, st>>>(sv, key, rows, nkeys, part); break;
+    case 4: keyed_row_sum_partial<4><<<splits, 256, 0, st>>>(sv, key, rows, nkeys, part); break;
+    case 8: keyed_row_sum_partial<8><<<splits, 256, 0, st>>>(sv, key, rows, nkeys, part); break;
+    case 16: keyed_row_sum_partial<16><<<splits, 256, 0, st>>>(sv, key, rows, nkeys, part); break;
+    case 32: keyed_row_sum_partial<32><<<splits, 256, 0, st>>>(sv, key, rows, nkeys, part); break;
+    case 64: keyed_row_sum_partial<64><<<splits, 256, 0, st>>>(sv, key, rows, nkeys, part); break;
+    default: return X2G_EUNSUPPORTED;
+  }
+  if (int rc = last_launch_status()) return rc;
+  return sum_slabs_launch(static_cast<const float*>(ws), static_cast<int64_t>(dim) * nkeys, nullptr, 0, splits, out,
+                          nullptr, accum, st);
+}
+
 X2G_API int x2g_graph_layernorm_fwd(const float* x, const int32_t* rowptr, int64_t G, int64_t D, float eps,
                                     float* out, float* mean, float* rstd, void* stream) {
   if (G < 0 || D <= 0 || (G > 0 && (!x || !rowptr || !out || !mean || !rstd))) return X2G_EINVAL;

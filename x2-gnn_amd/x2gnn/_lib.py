@@ -34,6 +34,16 @@ SIGNATURES = {
     "x2g_edge_basis_freq_grad_workspace": [_I64, _I32],
     "x2g_edge_basis_freq_grad_splits": [_I64],
     "x2g_edge_basis_freq_grad": [_P, _P, _P, _P, _I64, _I32, _F, _P, ctypes.c_int, _P, _SZ, _P],
+    "x2g_keyed_row_sum_workspace": [_I64, _I32, _I32],
+    "x2g_dense_fwd_batched": [_P, _I32, _I64, _I32, _I32, ctypes.c_int, _P],
+    "x2g_dense_bwd_batched": [_P, _I32, _I64, _I32, _I32, ctypes.c_int, ctypes.c_int, _P, _SZ, _P],
+    "x2g_readout_head_fwd": [_P, _I32, _I64, _I32, _P, _P],
+    "x2g_readout_head_bwd_workspace": [_I64, _I32, _I32],
+    "x2g_readout_head_bwd_splits": [_I64],
+    "x2g_readout_head_bwd": [_P, _P, _I32, _I64, _I32, ctypes.c_int, _P, _SZ, _P],
+    "x2g_embedding_table": [_P, _P, _I64, _I32, _I32, _F, _P, _P, _P],
+    "x2g_embedding_table_bwd": [_P, _P, _I32, _I32, _I32, _P, ctypes.c_int, _P],
+    "x2g_keyed_row_sum": [_P, _P, _I64, _I32, _I32, _P, ctypes.c_int, _P, _SZ, _P],
     "x2g_rbf_gate_fwd": [_P, _P, _P, _P, _I64, _I32, _I32, _P, _P],
     "x2g_rbf_pool_fwd": [_P, _P, _P, _P, _P, _I64, _I32, _I32, _P, _P],
     "x2g_rbf_gate_bwd_workspace": [_I64, _I32, _I32],
@@ -74,7 +84,8 @@ RESTYPES = {"x2g_status_string": ctypes.c_char_p, "x2g_vertex_to_edge_workspace"
             "x2g_linear_wgrad_splits": ctypes.c_int32, "x2g_dense_bwd_splits": ctypes.c_int32,
             "x2g_dense_bwd_slab_offset": ctypes.c_int64, "x2g_edge_basis_freq_grad_workspace": _SZ,
             "x2g_edge_basis_freq_grad_splits": ctypes.c_int32, "x2g_rbf_gate_bwd_workspace": _SZ,
-            "x2g_rbf_gate_bwd_splits": ctypes.c_int32}
+            "x2g_rbf_gate_bwd_splits": ctypes.c_int32, "x2g_keyed_row_sum_workspace": _SZ,
+            "x2g_readout_head_bwd_workspace": _SZ, "x2g_readout_head_bwd_splits": ctypes.c_int32}
 
 _lib = None
 

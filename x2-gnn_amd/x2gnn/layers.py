@@ -161,6 +161,9 @@ class EmbeddingBlock(nn.Module):
         """
         emb = self.embedding
         z = atomic_num.reshape(-1)
+        if z.is_cuda and emb.norm_type == 2.0 and emb.num_embeddings <= 64:  # one launch (csrc/embedding.hip)
+            w = ops.embedding_table(emb.weight, z, emb.max_norm, emb.padding_idx, emb.scale_grad_by_freq)
+            return self.lin.fused(w, act=ops.ACT_SILU if self.activate else ops.ACT_NONE)
         # counts per element without torch.bincount (its output size is data-dependent: a host sync
         # that would also break HIP-graph capture); float counts are exact below 2^24
         counts = torch.zeros(emb.num_embeddings, dtype=torch.float32, device=z.device)
@@ -219,9 +222,12 @@ class AtomWise(nn.Module):
         self.mlp = _mlp(in_channels, num_target, mlp_depth)
         self.lin_rbf = Linear(rbf_dim, in_channels)
 
+    def features(self, x, rbf, num_atoms, edge_index_0, atom_rowptr=None):
+        """The MLP input (everything before readout.py:42's MLP)."""
+        return _edge_pool(x, rbf, self.lin_rbf, edge_index_0, num_atoms, atom_rowptr)
+
     def forward(self, x, rbf, num_atoms, edge_index_0, atom_rowptr=None):
-        out = _edge_pool(x, rbf, self.lin_rbf, edge_index_0, num_atoms, atom_rowptr)
-        return run_mlp(self.mlp, out)
+        return run_mlp(self.mlp, self.features(x, rbf, num_atoms, edge_index_0, atom_rowptr))
 
 
 class MolWise(nn.Module):
@@ -235,7 +241,8 @@ class MolWise(nn.Module):
         self.mlp = _mlp(in_channels, num_target, mlp_depth)
         self.pool_option = pool_option
 
-    def forward(self, x, rbf, num_atoms, edge_index_0, atom_batch, dim_size, atom_rowptr=None, mol_rowptr=None):
+    def features(self, x, rbf, num_atoms, edge_index_0, atom_batch, dim_size, atom_rowptr=None, mol_rowptr=None):
+        """The MLP input: edges -> atoms -> molecules (readout.py:66-71)."""
         out = _edge_pool(x, rbf, self.lin_rbf, edge_index_0, num_atoms, atom_rowptr)
         if mol_rowptr is None:
             mol_rowptr = ops.csr_rowptr(atom_batch, dim_size)
@@ -243,4 +250,8 @@ class MolWise(nn.Module):
         if self.pool_option == "mean":
             cnt = (mol_rowptr[1:] - mol_rowptr[:-1]).clamp(min=1).to(pooled.dtype)
             pooled = pooled / cnt.unsqueeze(1)
-        return run_mlp(self.mlp, pooled)
+        return pooled
+
+    def forward(self, x, rbf, num_atoms, edge_index_0, atom_batch, dim_size, atom_rowptr=None, mol_rowptr=None):
+        return run_mlp(self.mlp, self.features(x, rbf, num_atoms, edge_index_0, atom_batch, dim_size, atom_rowptr,
+                                               mol_rowptr))

@@ -80,7 +80,7 @@ class _Trunk(nn.Module):
         self.LayerNorm = LayerNorm(in_channels=in_channels, eps=1e-8, affine=False)
         self.conv_layers = conv_layers
 
-    def _layers(self, data, plan, readout_fn):
+    def _layers(self, data, plan, readout_fn, feature_fn=None):
         per_dst = "edge_attr_row" in data._store
         edge_attr = run_mlp(self.edgenn, data.edge_attr)
         edge_row = data.edge_attr_row if per_dst else None
@@ -94,9 +94,17 @@ class _Trunk(nn.Module):
         side = _side_stream(out.device) if use_side else None
         main = torch.cuda.current_stream(out.device) if side is not None else None
         results = None
+        # Batched readout MLPs: collect every readout's MLP input, then one batched launch per MLP
+        # layer for all readouts (ops.readout_mlps) instead of three launches per readout.
+        grouped = (out.is_cuda and side is None and feature_fn is not None
+                   and os.environ.get("X2G_GROUPED_READOUT", "1") == "1")
+        feats = []
 
         def readout(i, x):
             nonlocal results
+            if grouped:
+                feats.append(feature_fn(i, x))
+                return
             if side is None:
                 r = readout_fn(i, x)
                 results = r if results is None else results + r
@@ -120,6 +128,13 @@ class _Trunk(nn.Module):
         if side is not None:
             main.wait_stream(side)
             results.record_stream(main)
+        if grouped:
+            mlps = [r.mlp for r in self.readouts]
+            if ops.readout_mlps_supported(feats, mlps):
+                return ops.readout_mlps(feats, mlps)
+            for m, f in zip(mlps, feats):
+                r = run_mlp(m, f)
+                results = r if results is None else results + r
         return results
 
 
@@ -138,7 +153,11 @@ class SBFTransformer(_Trunk):
             return self.readouts[i](x=x, rbf=data.node_rbf, num_atoms=plan.num_atoms, edge_index_0=edge_index_0,
                                     atom_rowptr=plan.atom_rowptr)
 
-        per_atom = self._layers(data, plan, readout)
+        def features(i, x):
+            return self.readouts[i].features(x=x, rbf=data.node_rbf, num_atoms=plan.num_atoms,
+                                             edge_index_0=edge_index_0, atom_rowptr=plan.atom_rowptr)
+
+        per_atom = self._layers(data, plan, readout, features)
         return ops.segment_sum(per_atom, plan.mol_ptr, plan.out_graphs).view(-1)
 
 
@@ -153,9 +172,13 @@ class SBFTransformerGlobal(_Trunk):
     def forward(self, data, edge_index_0, atom_batch):
         plan = _plan_of(data, edge_index_0, atom_batch)
 
-        def readout(i, x):
-            return self.readouts[i](x=x, rbf=data.node_rbf, num_atoms=plan.num_atoms, edge_index_0=edge_index_0,
-                                    atom_batch=atom_batch, dim_size=plan.out_graphs, atom_rowptr=plan.atom_rowptr,
-                                    mol_rowptr=plan.mol_ptr[: plan.out_graphs + 1])
+        kw = dict(rbf=data.node_rbf, num_atoms=plan.num_atoms, edge_index_0=edge_index_0, atom_batch=atom_batch,
+                  dim_size=plan.out_graphs, atom_rowptr=plan.atom_rowptr, mol_rowptr=plan.mol_ptr[: plan.out_graphs + 1])
 
-        return self._layers(data, plan, readout).view(-1)
+        def readout(i, x):
+            return self.readouts[i](x=x, **kw)
+
+        def features(i, x):
+            return self.readouts[i].features(x=x, **kw)
+
+        return self._layers(data, plan, readout, features).view(-1)

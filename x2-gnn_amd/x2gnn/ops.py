@@ -255,8 +255,7 @@ class _SBFAttention(torch.autograd.Function):
              ptr(dk), ptr(dv), st)
         if mode == EDGE_PER_DST and ctx.edge_row is not None:
             # rows of the edge table are shared by many destinations: sum d_edge per table row
-            onehot = torch.nn.functional.one_hot(ctx.edge_row.long(), ctx.edge_shape[0]).to(torch.float32)
-            d_edge = linear_wgrad(d_edge, onehot, bias=False)[0].t().contiguous()
+            d_edge = keyed_row_sum(d_edge, ctx.edge_row, ctx.edge_shape[0])
         gw, gb = grad_sink(ctx.w_param), grad_sink(ctx.b_param)
         if gw is not None and gb is not None:
             dw, db = linear_wgrad(dproj, sbf, dw_out=gw, db_out=gb)  # summed into the bucket: None
@@ -283,6 +282,212 @@ def _attention_fwd_fused(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, 
          ptr(sbf), ptr(w_sbf), ptr(b_sbf), ptr(lg.trip_rowptr), ptr(lg.trip_src), E, T, heads, channels,
          sbf.shape[1], ptr(out), ptr(alpha), ptr(smax), ptr(sden), stream_ptr())
     return out, alpha, smax, sden
+
+
+class _EmbeddingTable(torch.autograd.Function):
+    """Embedding rows per element with torch.embedding_renorm_ (in place) and the
+    scale_grad_by_freq / padding_idx gradient rules, one launch each way (csrc/embedding.hip)."""
+
+    @staticmethod
+    def forward(ctx, weight, z, max_norm, padding_idx, scale_grad):
+        V, D = weight.shape
+        if weight.dtype != torch.float32 or not weight.is_contiguous():
+            raise ValueError("embedding weight must be contiguous fp32")
+        zz = z if z.dtype == torch.int64 and z.is_contiguous() else z.to(torch.int64).contiguous()
+        table = torch.empty_like(weight)
+        counts = torch.empty(V, dtype=torch.float32, device=weight.device)
+        call("x2g_embedding_table", ptr(weight), ptr(zz), zz.numel(), V, D, float(max_norm or 0.0), ptr(counts),
+             ptr(table), stream_ptr())
+        ctx.save_for_backward(counts)
+        ctx.w_param, ctx.pad, ctx.scale = weight, (-1 if padding_idx is None else int(padding_idx)), bool(scale_grad)
+        return table
+
+    @staticmethod
+    def backward(ctx, g):
+        (counts,) = ctx.saved_tensors
+        V, D = counts.shape[0], g.shape[1]
+        sink = grad_sink(ctx.w_param)
+        dw = sink if sink is not None else torch.empty(V, D, dtype=torch.float32, device=g.device)
+        call("x2g_embedding_table_bwd", ptr(_f32(g)), ptr(counts) if ctx.scale else None, V, D, ctx.pad, ptr(dw),
+             ACCUM_WGRAD if sink is not None else 0, stream_ptr())
+        return (None if sink is not None else dw), None, None, None, None
+
+
+def embedding_table(weight, z, max_norm, padding_idx, scale_grad_by_freq):
+    """Rows of ``weight`` per element (see _EmbeddingTable); renormalises the used rows in place."""
+    _need_cuda(weight, z)
+    return _EmbeddingTable.apply(weight, z, max_norm, padding_idx, scale_grad_by_freq)
+
+
+class DenseFwdGroup(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_void_p), ("w", ctypes.c_void_p), ("b", ctypes.c_void_p), ("res", ctypes.c_void_p),
+                ("y", ctypes.c_void_p), ("z", ctypes.c_void_p)]
+
+
+class DenseBwdGroup(ctypes.Structure):
+    _fields_ = [("dy", ctypes.c_void_p), ("z", ctypes.c_void_p), ("x", ctypes.c_void_p), ("w", ctypes.c_void_p),
+                ("dx", ctypes.c_void_p), ("dx_add", ctypes.c_void_p), ("dw", ctypes.c_void_p),
+                ("db", ctypes.c_void_p)]
+
+
+class HeadGroup(ctypes.Structure):
+    _fields_ = [("h", ctypes.c_void_p), ("w", ctypes.c_void_p), ("b", ctypes.c_void_p), ("dh", ctypes.c_void_p),
+                ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p)]
+
+
+def _dp(t):
+    return t.data_ptr() if t is not None else None
+
+
+def _wgrad_targets(params, shapes, dev):
+    """Per parameter: (buffer, accum) — the bucket view when every one of them is bucket-backed
+    (summed straight into it), fresh buffers otherwise; returns (buffers, accum)."""
+    sinks = [grad_sink(p) for p in params]
+    if all(s is not None for s in sinks):
+        return sinks, True
+    return [torch.empty(sh, dtype=torch.float32, device=dev) for sh in shapes], False
+
+
+class _ReadoutMLPs(torch.autograd.Function):
+    """sum_g mlp_g(feat_g) for the trunk's readouts (readout.py:25-31,42 / 55-62,76, summed in
+    model.py:41,50): every readout's Linear+SiLU, Linear+SiLU, Linear(D,1) run as three batched
+    launches (blockIdx.y = readout) instead of three per readout, and the sum over readouts is
+    fused into the last one; backward likewise (the weight-gradient slab sums deferred)."""
+
+    @staticmethod
+    def forward(ctx, G, *args):
+        feats, params = args[:G], args[G:]
+        W1, B1, W2, B2, W3, B3 = (params[i::6] for i in range(6))
+        R, D = feats[0].shape
+        dev = feats[0].device
+        f32 = dict(dtype=torch.float32, device=dev)
+        xs = [_f32(f) for f in feats]
+        h1 = [torch.empty(R, D, **f32) for _ in range(G)]
+        z1 = [torch.empty(R, D, **f32) for _ in range(G)]
+        h2 = [torch.empty(R, D, **f32) for _ in range(G)]
+        z2 = [torch.empty(R, D, **f32) for _ in range(G)]
+        st = stream_ptr()
+        for (src, w, b, y, z) in ((xs, W1, B1, h1, z1), (h1, W2, B2, h2, z2)):
+            grp = (DenseFwdGroup * G)(*[DenseFwdGroup(_dp(src[g]), _dp(w[g]), _dp(b[g]), None, _dp(y[g]), _dp(z[g]))
+                                        for g in range(G)])
+            call("x2g_dense_fwd_batched", grp, G, R, D, D, ACT_SILU, st)
+        out = torch.empty(R, 1, **f32)
+        heads = (HeadGroup * G)(*[HeadGroup(_dp(h2[g]), _dp(W3[g]), _dp(B3[g]), None, None, None) for g in range(G)])
+        call("x2g_readout_head_fwd", heads, G, R, D, ptr(out), st)
+        ctx.save_for_backward(*xs, *h1, *z1, *h2, *z2)
+        ctx.G, ctx.params = G, params
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        G = ctx.G
+        saved = ctx.saved_tensors
+        xs, h1, z1, h2, z2 = (saved[i * G:(i + 1) * G] for i in range(5))
+        W1, B1, W2, B2, W3, B3 = (ctx.params[i::6] for i in range(6))
+        R, D = xs[0].shape
+        dev = xs[0].device
+        f32 = dict(dtype=torch.float32, device=dev)
+        lib = _lib.load()
+        st = stream_ptr()
+        dout = _f32(dout.reshape(-1))
+        # head: dh2_g = dout w3_g; dW3_g, db3_g
+        dh2 = [torch.empty(R, D, **f32) for _ in range(G)]
+        (dw3, db3), acc3 = _wgrad_pairs(W3, B3, dev)
+        heads = (HeadGroup * G)(*[HeadGroup(_dp(h2[g]), _dp(W3[g]), None, _dp(dh2[g]), _dp(dw3[g]), _dp(db3[g]))
+                                  for g in range(G)])
+        ws_bytes = int(lib.x2g_readout_head_bwd_workspace(R, D, G))
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        defer = acc3 and _DEFER is not None
+        call("x2g_readout_head_bwd", ptr(dout), heads, G, R, D, (ACCUM_WGRAD if acc3 else 0) |
+             (DEFER_SLAB_SUM if defer else 0), ptr(ws), ws_bytes, st)
+        if defer:
+            splits = int(lib.x2g_readout_head_bwd_splits(R))
+            for g in range(G):
+                _defer_job(ws, g * splits * (D + 1) * 4, splits, D, 1, dw3[g], db3[g])
+        grads = {}
+        # layer 2 then layer 1: dz = dy * SiLU'(z), dx = dz W, dW / db
+        dy = dh2
+        for (layer, x_in, z, W, B) in ((2, h1, z2, W2, B2), (1, xs, z1, W1, B1)):
+            dx = [torch.empty(R, D, **f32) for _ in range(G)]
+            (dw, db), acc = _wgrad_pairs(W, B, dev)
+            grp = (DenseBwdGroup * G)(*[DenseBwdGroup(_dp(dy[g]), _dp(z[g]), _dp(x_in[g]), _dp(W[g]), _dp(dx[g]), None,
+                                                      _dp(dw[g]), _dp(db[g])) for g in range(G)])
+            wsz = int(lib.x2g_dense_bwd_workspace(R, D, D))
+            ws = torch.empty(max(wsz * G, 1), dtype=torch.uint8, device=dev)
+            defer = acc and _DEFER is not None
+            call("x2g_dense_bwd_batched", grp, G, R, D, D, ACT_SILU, (ACCUM_WGRAD if acc else 0) |
+                 (DEFER_SLAB_SUM if defer else 0), ptr(ws), wsz * G, st)
+            if defer:
+                splits = int(lib.x2g_dense_bwd_splits(R, D, D))
+                for g in range(G):
+                    _defer_job(ws, g * wsz, splits, D * D, D, dw[g], db[g])
+            grads[layer] = (None, None) if acc else (dw, db)
+            dy = dx
+        dfeat = dy
+        pg = []
+        for g in range(G):
+            for (dw, db) in (grads[1], grads[2]):
+                pg += [None if dw is None else dw[g], None if db is None else db[g]]
+            pg += [None if acc3 else dw3[g].view_as(W3[g]), None if acc3 else db3[g]]
+        return (None, *dfeat, *pg)
+
+
+def _wgrad_pairs(Ws, Bs, dev):
+    """Weight / bias gradient buffers of a group of layers: the bucket views (accumulate) when all
+    are bucket-backed, fresh buffers otherwise."""
+    params = list(Ws) + list(Bs)
+    bufs, acc = _wgrad_targets(params, [tuple(p.shape) for p in params], dev)
+    n = len(Ws)
+    return (bufs[:n], bufs[n:]), acc
+
+
+def readout_mlps_supported(feats, mlps):
+    """True when _ReadoutMLPs covers these readouts (same row count and width, the 3-layer
+    Linear/SiLU/Linear/SiLU/Linear(D,1) MLP with biases, G <= 8, compiled widths)."""
+    from .layers import Linear as _Lin
+    G = len(feats)
+    if G < 1 or G > 8 or not all(f.is_cuda and f.dim() == 2 and f.shape == feats[0].shape for f in feats):
+        return False
+    R, D = feats[0].shape
+    if D % 4 or D <= 8 or D > 128 or (D // 4) & (D // 4 - 1) or R * 128 >= 2 ** 31:
+        return False
+    for m in mlps:
+        mods = list(m)
+        if len(mods) != 5 or not all(isinstance(mods[i], _Lin) for i in (0, 2, 4)):
+            return False
+        if not all(isinstance(mods[i], torch.nn.SiLU) for i in (1, 3)):
+            return False
+        if any(mods[i].bias is None for i in (0, 2, 4)):
+            return False
+        if tuple(mods[0].weight.shape) != (D, D) or tuple(mods[2].weight.shape) != (D, D):
+            return False
+        if tuple(mods[4].weight.shape) != (1, D):
+            return False
+    return True
+
+
+def readout_mlps(feats, mlps):
+    """sum_g mlp_g(feats[g]) -> [R, 1] (see _ReadoutMLPs)."""
+    params = []
+    for m in mlps:
+        mods = list(m)
+        params += [mods[0].weight, mods[0].bias, mods[2].weight, mods[2].bias, mods[4].weight, mods[4].bias]
+    return _ReadoutMLPs.apply(len(feats), *feats, *params)
+
+
+def keyed_row_sum(src, key, num_keys: int):
+    """out[k] = sum of src rows r with key[r] == k (unsorted key): the gradient of table[key]."""
+    _need_cuda(src, key)
+    src = _f32(src)
+    R, D = src.shape
+    if num_keys > 16 or D % 4 or D > 256 or (D // 4) & (D // 4 - 1):  # outside the compiled kernel
+        onehot = torch.nn.functional.one_hot(key.long(), num_keys).to(torch.float32)
+        return linear_wgrad(src, onehot, bias=False)[0].t().contiguous()
+    out = torch.empty(num_keys, D, dtype=torch.float32, device=src.device)
+    ws_bytes = int(_lib.load().x2g_keyed_row_sum_workspace(R, D, num_keys))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=src.device)
+    call("x2g_keyed_row_sum", ptr(src), ptr(_i32(key)), R, D, num_keys, ptr(out), 0, ptr(ws), ws_bytes, stream_ptr())
+    return out
 
 
 def sbf_attention(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg: LineGraph, heads: int, channels: int,
