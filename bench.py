@@ -413,11 +413,11 @@ def main():
     # committed profile (profiles/r1_v2_bench_kernel_stats.csv: dense_bwd_persist 1.9 ms/step)
     dbw_ms, dbw_flops = dense["dense_bwd"]
     dbw_tfs = dbw_flops / (dbw_ms * 1e-3) / 1e12
-    ntiles = (shape["E"] + 63) // 64  # dense.hip bwd_grid(): fewest workgroups at ceil(tiles/256) tiles each
+    ntiles = (shape["E"] + 31) // 32  # dense.hip bwd_grid(): fewest workgroups at ceil(tiles/256) 32-row tiles each
     per = (ntiles + 255) // 256
     grid = str(((ntiles + per - 1) // per) * 512)
-    traffic = pmc_traffic([("x2g::dense_bwd_v5", grid), ("x2g::sum_slabs2", str(258 * 256))])
-    roof = {"kernel": "x2g_dense_bwd [E,128]x[128,128] SiLU (dense_bwd_v5 + sum_slabs2)",
+    traffic = pmc_traffic([("x2g::dense_bwd_v8", grid), ("x2g::sum_slabs2", str(258 * 256))])
+    roof = {"kernel": "x2g_dense_bwd [E,128]x[128,128] SiLU (dense_bwd_v8 + sum_slabs2)",
             "bound": "mfma", "achieved": round(dbw_tfs, 2), "peak": MFMA_F32_PEAK_TFS,
             "unit": "TFLOP/s", "frac": round(dbw_tfs / MFMA_F32_PEAK_TFS, 4), "traffic": traffic,
             "avg_ms": round(dbw_ms, 5), "flops_per_launch": int(dbw_flops),

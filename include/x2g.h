@@ -314,6 +314,13 @@ int x2g_dense_bwd_ex(const float* dy, const float* z, int act, const float* x, c
                      int32_t in_features, int32_t out_features, float* dx, const float* dx_add, float* dw,
                      float* db, int flags, void* workspace, size_t workspace_bytes, void* stream);
 
+/* ResidualLayer forward (residual_layer.py:21-27) in one persistent kernel:
+ *   z0 = x w0^T + b0, h = SiLU(z0), z1 = h w1^T + b1, y = x + SiLU(z1)   (w0, w1: [D, D]; b optional)
+ * h, z0, z1 are kept for the backward.  D <= 128, D % 4 == 0, 16-byte aligned rows
+ * (X2G_EUNSUPPORTED otherwise). */
+int x2g_residual_fwd(const float* x, const float* w0, const float* b0, const float* w1, const float* b1,
+                     int64_t rows, int32_t dim, float* h, float* z0, float* z1, float* y, void* stream);
+
 /* ---------------------------------------------------------------- batched layers (readout MLPs)
  * The trunk's conv_layers+1 readouts (model.py:41,50) run the same MLP shape on different inputs
  * with different weights: Linear(D,D)+SiLU, Linear(D,D)+SiLU, Linear(D,1) (readout.py:25-31,

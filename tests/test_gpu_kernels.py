@@ -665,3 +665,29 @@ def test_readout_mlps_batched_vs_separate(cuda, R, G):
     for a, b in zip(mlps, mlps_ref):
         for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
             torch.testing.assert_close(p.grad, q.grad, rtol=1e-4, atol=1e-4, msg=n)
+
+
+@pytest.mark.parametrize("R,D", [(1, 128), (33, 128), (21058, 128), (500, 64), (77, 12)])
+def test_fused_residual_layer_vs_torch(cuda, R, D):
+    """x2g_residual_fwd (both GEMMs of a ResidualLayer in one kernel) + the layer's backward vs
+    torch: y = x + SiLU(W1 SiLU(W0 x + b0) + b1)."""
+    from x2gnn.layers import ResidualLayer
+
+    torch.manual_seed(R + D)
+    layer = ResidualLayer(D).to(cuda)
+    x = torch.randn(R, D, device=cuda, requires_grad=True)
+    y = layer(x)
+    xr = x.detach().clone().requires_grad_(True)
+    F = torch.nn.functional
+    ref = xr + F.silu(F.linear(F.silu(F.linear(xr, layer.lin0.weight, layer.lin0.bias)), layer.lin1.weight,
+                               layer.lin1.bias))
+    torch.testing.assert_close(y, ref, rtol=2e-5, atol=2e-5)
+    up = torch.randn(R, D, device=cuda)
+    y.backward(up)
+    gw = [p.grad.clone() for p in layer.parameters()]
+    for p in layer.parameters():
+        p.grad = None
+    ref.backward(up)
+    torch.testing.assert_close(x.grad, xr.grad, rtol=1e-4, atol=1e-4)
+    for a, p in zip(gw, layer.parameters()):
+        torch.testing.assert_close(a, p.grad, rtol=1e-4, atol=1e-3)

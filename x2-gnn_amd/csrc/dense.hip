@@ -852,6 +852,141 @@ __global__ void __launch_bounds__(256, 2) dense_fwd_v6_batched(const DenseFwdBat
   dense_fwd_v6_body(p.x, p.w, p.b, p.res, R, K, N, act, p.y, p.z, Ws, Xs);
 }
 
+// ---------------------------------------------------------------- ResidualLayer forward, fused
+// y = x + SiLU(W1 SiLU(W0 x + b0) + b1) (residual_layer.py:21-27) for D <= 128 in ONE persistent
+// kernel: both weights staged once per CU (2 x 64 KB, the v6 swizzled slot layout), and per
+// 32-row tile: GEMM 1 from the x tile, its C fragments transposed into the h tile (16 KB), bias +
+// SiLU applied in place (z0 and h stored for the backward), GEMM 2 from the h tile, and the
+// epilogue adds the residual straight from the x tile still in LDS.  160 KB of LDS: one
+// workgroup per CU.  Versus two v6 launches: no second weight staging / launch ramp and no
+// re-read of h and x from HBM.
+__device__ __forceinline__ void stage_w_swz(const float* __restrict__ W, int N, int K, float* __restrict__ Ws) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    float v[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const int idx = tid + 256 * (32 * half + u), nn = idx >> 7, k = idx & 127;
+      const float x = ld_pin(W + (nn < N ? nn : N - 1) * K + (k < K ? k : K - 1));
+      v[u] = (nn < N && k < K) ? x : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const int idx = tid + 256 * (32 * half + u), nn = idx >> 7, k = idx & 127;
+      Ws[wswz(k & 63, nn, k >> 6)] = v[u];
+    }
+  }
+}
+
+// acc = A tile (rows swizzled, [32][128]) x B (slot layout): this wave's 32 output columns
+__device__ __forceinline__ void tile_mfma(const float* __restrict__ As, const float* __restrict__ Ws, int n, int h,
+                                          int i, floatx16& acc0, floatx16& acc1) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    acc0[j] = 0.f;
+    acc1[j] = 0.f;
+  }
+  const float* xs = As + i * 128;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    const f4 a = *reinterpret_cast<const f4*>(xs + 4 * ((16 * h + g) ^ (i & 15)));
+    const int s = 4 * g;
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, Ws[wswz(s, n, h)], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, Ws[wswz(s + 1, n, h)], acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, Ws[wswz(s + 2, n, h)], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, Ws[wswz(s + 3, n, h)], acc1, 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void acc_to_rows(float* __restrict__ buf, const floatx16& acc0, const floatx16& acc1, int n,
+                                            int h) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int r = (j & 3) + 8 * (j >> 2) + 4 * h;
+    buf[r * 128 + 4 * ((n >> 2) ^ (r & 15)) + (n & 3)] = acc0[j] + acc1[j];
+  }
+}
+
+__global__ void __launch_bounds__(256, 1) residual_fwd_kernel(const float* __restrict__ X, const float* __restrict__ W0,
+                                                              const float* __restrict__ B0,
+                                                              const float* __restrict__ W1,
+                                                              const float* __restrict__ B1, int64_t R, int D,
+                                                              float* __restrict__ H, float* __restrict__ Z0,
+                                                              float* __restrict__ Z1, float* __restrict__ Y) {
+  __shared__ __attribute__((aligned(16))) float Ws0[64 * 256];
+  __shared__ __attribute__((aligned(16))) float Ws1[64 * 256];
+  __shared__ __attribute__((aligned(16))) float Xs[32 * 128];
+  __shared__ __attribute__((aligned(16))) float Hs[32 * 128];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, i = lane & 31;
+  const int n = 32 * wave + i;
+  const int q = tid & 31;
+  const int64_t ntiles = (R + 31) / 32;
+  const int64_t G = gridDim.x;
+  const bool colok = 4 * q < D;
+  f4 b0 = {0.f, 0.f, 0.f, 0.f}, b1 = {0.f, 0.f, 0.f, 0.f};
+  if (B0 && colok) b0 = f4{B0[4 * q], B0[4 * q + 1], B0[4 * q + 2], B0[4 * q + 3]};
+  if (B1 && colok) b1 = f4{B1[4 * q], B1[4 * q + 1], B1[4 * q + 2], B1[4 * q + 3]};
+  int64_t t = blockIdx.x;
+  {
+    Stage4 first;
+    xtile_load(X, t, R, D, first);
+    stage_w_swz(W0, D, D, Ws0);
+    stage_w_swz(W1, D, D, Ws1);
+    xtile_store(Xs, first);
+    __syncthreads();
+  }
+  for (; t < ntiles; t += G) {
+    const bool more = t + G < ntiles;
+    Stage4 nxt;
+    if (more) xtile_load(X, t + G, R, D, nxt);
+    floatx16 acc0, acc1;
+    tile_mfma(Xs, Ws0, n, h, i, acc0, acc1);
+    acc_to_rows(Hs, acc0, acc1, n, h);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // z0 = . + b0 -> Z0; h = SiLU(z0) -> H and in place
+      const int row = (tid >> 5) + 8 * u, r = static_cast<int>(t) * 32 + row;
+      f4* hp = reinterpret_cast<f4*>(Hs + row * 128 + 4 * (q ^ (row & 15)));
+      const f4 z = *hp + b0;
+      f4 hv;
+      hv.x = act_apply(z.x, kActSilu);
+      hv.y = act_apply(z.y, kActSilu);
+      hv.z = act_apply(z.z, kActSilu);
+      hv.w = act_apply(z.w, kActSilu);
+      *hp = hv;
+      if (r < R && colok) {
+        *reinterpret_cast<f4*>(Z0 + r * D + 4 * q) = z;
+        *reinterpret_cast<f4*>(H + r * D + 4 * q) = hv;
+      }
+    }
+    __syncthreads();
+    tile_mfma(Hs, Ws1, n, h, i, acc0, acc1);
+    __syncthreads();  // h consumed: Hs stages the second output
+    acc_to_rows(Hs, acc0, acc1, n, h);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // z1 = . + b1 -> Z1; y = SiLU(z1) + x -> Y
+      const int row = (tid >> 5) + 8 * u, r = static_cast<int>(t) * 32 + row;
+      const int off = row * 128 + 4 * (q ^ (row & 15));
+      const f4 z = *reinterpret_cast<const f4*>(Hs + off) + b1;
+      const f4 xv = *reinterpret_cast<const f4*>(Xs + off);
+      f4 yv;
+      yv.x = act_apply(z.x, kActSilu) + xv.x;
+      yv.y = act_apply(z.y, kActSilu) + xv.y;
+      yv.z = act_apply(z.z, kActSilu) + xv.z;
+      yv.w = act_apply(z.w, kActSilu) + xv.w;
+      if (r < R && colok) {
+        *reinterpret_cast<f4*>(Z1 + r * D + 4 * q) = z;
+        *reinterpret_cast<f4*>(Y + r * D + 4 * q) = yv;
+      }
+    }
+    __syncthreads();
+    if (more) xtile_store(Xs, nxt);
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------- forward, narrow K (K % 4 != 0)
 // For rows too narrow / odd for 16-byte row chunks (lin_sbf: K = 42): a 64-row tile pair is one
 // contiguous span of 64*K floats, read with 16-byte loads regardless of K and scattered into
@@ -1244,6 +1379,177 @@ __global__ void __launch_bounds__(512) dense_bwd_v5_batched(const DenseBwdBatch 
   dense_bwd_v5_body(p.dy, p.z, p.x, p.w, R, K, N, act, p.dx, p.dx_add, b.part_w[gi], b.part_b[gi], Ws, Ds, Xs);
 }
 
+// ---------------------------------------------------------------- backward, v8: 32-row tiles
+// As v5 (weight in the padded slot layout, dz and x tiles chunk-swizzled in LDS, next tile
+// prefetched into registers during the MFMAs, dx through LDS as 16-byte row stores), but on
+// 32-row tiles with the work split by wave role: waves 0-3 compute the tile's dx (32 rows x 32
+// columns each, K = N), waves 4-7 its dW contribution (32 n-rows x all K columns each, over the
+// tile's 32 rows).  Each SIMD then holds one dx wave and one dW wave (64 MFMAs each per tile), and
+// the 32-row granularity balances the chip: at 21k rows 658 tiles over 220 workgroups (<= 3
+// tiles each, 10.2 us of MFMA per CU) instead of 330 64-row tiles over 165 (2 x 6.8 us).
+struct Stage2 {
+  f4 v0, v1;
+};
+
+__device__ __forceinline__ void xt32_load(const float* __restrict__ X, int64_t t, int64_t R, int K, Stage2& st) {
+  const int kc = K >> 2, q = threadIdx.x & 31, qc = 4 * (q < kc ? q : kc - 1);
+  const int rmax = static_cast<int>(R) - 1, r0 = static_cast<int>(t) * 32 + (threadIdx.x >> 5);
+  const int ra = r0 < rmax ? r0 : rmax, rb = r0 + 16 < rmax ? r0 + 16 : rmax;
+  st.v0 = *reinterpret_cast<const f4*>(X + ra * K + qc);
+  st.v1 = *reinterpret_cast<const f4*>(X + rb * K + qc);
+}
+
+__device__ __forceinline__ f4 mask32(f4 v, int64_t t, int U, int64_t R, int cols) {
+  const int q = threadIdx.x & 31, row = (threadIdx.x >> 5) + 16 * U;
+  const bool ok = t * 32 + row < R && 4 * q < cols;
+  return ok ? v : f4{0.f, 0.f, 0.f, 0.f};
+}
+
+__device__ __forceinline__ void xt32_store(float* __restrict__ buf, f4 v0, f4 v1) {
+  const int q = threadIdx.x & 31, row = threadIdx.x >> 5;  // rows row and row + 16 share (row & 15)
+  float* p = buf + row * 128 + 4 * (q ^ (row & 15));
+  *reinterpret_cast<f4*>(p) = v0;
+  *reinterpret_cast<f4*>(p + 16 * 128) = v1;
+}
+
+__device__ __forceinline__ void dense_bwd_v8_body(const float* __restrict__ dY, const float* __restrict__ Zin,
+                                                  const float* __restrict__ X, const float* __restrict__ W, int64_t R,
+                                                  int K, int N, int act, float* __restrict__ dX,
+                                                  const float* __restrict__ dXadd, float* __restrict__ part_w,
+                                                  float* __restrict__ part_b, float* __restrict__ Ws,
+                                                  float* __restrict__ Ds, float* __restrict__ Xs,
+                                                  float* __restrict__ Os) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, i = lane & 31;
+  const int64_t ntiles = (R + 31) / 32;
+  const int64_t G = gridDim.x;
+  const bool silu = act == kActSilu;
+  const bool dw_wave = wave >= 4;
+  floatx16 accw[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) accw[m][j] = 0.f;
+  float bsum = 0.f;
+  int64_t t = blockIdx.x;
+  Stage2 sd, sz, sx;
+  {
+    float wv[32];
+    if (dX) wpad_load_bwd(W, N, K, wv);
+    xt32_load(dY, t, R, N, sd);
+    if (silu) xt32_load(Zin, t, R, N, sz);
+    xt32_load(X, t, R, K, sx);
+    if (dX) wpad_store_bwd(Ws, wv);
+  }
+  const int kcol = 32 * (wave & 3) + i;  // dx waves: output columns
+  const int nb = 32 * (wave & 3);        // dW waves: n rows
+  for (; t < ntiles; t += G) {
+    {
+      f4 d0 = sd.v0, d1 = sd.v1;
+      if (silu) {
+        d0 = silu_grad4<0>(d0, sz.v0);
+        d1 = silu_grad4<1>(d1, sz.v1);
+      }
+      xt32_store(Ds, mask32(d0, t, 0, R, N), mask32(d1, t, 1, R, N));
+      xt32_store(Xs, mask32(sx.v0, t, 0, R, K), mask32(sx.v1, t, 1, R, K));
+    }
+    __syncthreads();
+    if (t + G < ntiles) {  // the next tile's loads fly during the MFMAs below
+      xt32_load(dY, t + G, R, N, sd);
+      if (silu) xt32_load(Zin, t + G, R, N, sz);
+      xt32_load(X, t + G, R, K, sx);
+    }
+    if (!dw_wave) {
+      if (dX) {  // dx[i][kcol] = sum_n dz[i][n] w[n][kcol], n = 64h + 4g + e
+        floatx16 acc0, acc1;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          acc0[j] = 0.f;
+          acc1[j] = 0.f;
+        }
+        const float* ds = Ds + i * 128;
+        const float* wb = Ws + 2 * kcol + h;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          const f4 a = *reinterpret_cast<const f4*>(ds + 4 * ((16 * h + g) ^ (i & 15)));
+          const int sb = 4 * g * kSlotStride;
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, wb[sb], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, wb[sb + kSlotStride], acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, wb[sb + 2 * kSlotStride], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, wb[sb + 3 * kSlotStride], acc1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) Os[swz((j & 3) + 8 * (j >> 2) + 4 * h, kcol)] = acc0[j] + acc1[j];
+      }
+    } else {
+      // dW[n][k] += sum_r dz[r][n] x[r][k]; step (sg, s): rows r = 16 sg + s + 8h
+#pragma unroll
+      for (int sg = 0; sg < 2; ++sg) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const int r = 16 * sg + s + 8 * h;
+          const float a = Ds[swz(r, nb + i)];
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+            accw[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Xs[swz(r, 32 * m + i)], accw[m], 0, 0, 0);
+        }
+      }
+      if (part_b && tid - 256 < 128) {
+#pragma unroll 8
+        for (int rr = 0; rr < 32; ++rr) bsum += Ds[swz(rr, tid - 256)];
+      }
+    }
+    __syncthreads();  // Ds / Xs consumed, the dx tile is in Os
+    if (dX) {
+      const int q = tid & 31;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int row = (tid >> 5) + 16 * u;
+        const int r = static_cast<int>(t) * 32 + row;
+        f4 v = *reinterpret_cast<const f4*>(Os + row * 128 + 4 * (q ^ (row & 15)));
+        if (r < R && 4 * q < K) {
+          if (dXadd) v += *reinterpret_cast<const f4*>(dXadd + r * K + 4 * q);
+          *reinterpret_cast<f4*>(dX + r * K + 4 * q) = v;
+        }
+      }
+    }
+  }
+  if (dw_wave) {
+    float* slab = part_w + static_cast<int64_t>(blockIdx.x) * N * K;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int nn = nb + (j & 3) + 8 * (j >> 2) + 4 * h;
+        const int k = 32 * m + i;
+        if (nn < N && k < K) slab[nn * K + k] = accw[m][j];
+      }
+    }
+    if (part_b && tid - 256 < N && tid - 256 < 128) part_b[static_cast<int64_t>(blockIdx.x) * N + tid - 256] = bsum;
+  }
+}
+
+__global__ void __launch_bounds__(512) dense_bwd_v8(const float* __restrict__ dY, const float* __restrict__ Zin,
+                                                    const float* __restrict__ X, const float* __restrict__ W,
+                                                    int64_t R, int K, int N, int act, float* __restrict__ dX,
+                                                    const float* __restrict__ dXadd, float* __restrict__ part_w,
+                                                    float* __restrict__ part_b) {
+  __shared__ __attribute__((aligned(16))) float Ws[64 * kSlotStride];
+  __shared__ __attribute__((aligned(16))) float Ds[32 * 128];
+  __shared__ __attribute__((aligned(16))) float Xs[32 * 128];
+  __shared__ __attribute__((aligned(16))) float Os[32 * 128];
+  dense_bwd_v8_body(dY, Zin, X, W, R, K, N, act, dX, dXadd, part_w, part_b, Ws, Ds, Xs, Os);
+}
+
+__global__ void __launch_bounds__(512) dense_bwd_v8_batched(const DenseBwdBatch b, int64_t R, int K, int N, int act) {
+  __shared__ __attribute__((aligned(16))) float Ws[64 * kSlotStride];
+  __shared__ __attribute__((aligned(16))) float Ds[32 * 128];
+  __shared__ __attribute__((aligned(16))) float Xs[32 * 128];
+  __shared__ __attribute__((aligned(16))) float Os[32 * 128];
+  const int gi = blockIdx.y;
+  const x2g_dense_bwd_group& p = b.g[gi];
+  dense_bwd_v8_body(p.dy, p.z, p.x, p.w, R, K, N, act, p.dx, p.dx_add, b.part_w[gi], b.part_b[gi], Ws, Ds, Xs, Os);
+}
+
 }  // namespace x2g
 
 using namespace x2g;
@@ -1327,8 +1633,12 @@ X2G_API int x2g_linear_wgrad(const float* dy, const float* x, int64_t R, int32_t
 // Backward grid: the fewest workgroups that keep the busiest one at ceil(tiles / 256) tiles —
 // every workgroup writes a full weight-gradient slab, so idle-making extra workgroups would only
 // add slab traffic (330 tiles at config 2: 165 workgroups x 2 tiles instead of 256).
+// tuning key 1 (kTuneDenseBwd): 0 = v8 (default, 32-row tiles), 2 = v5 (64-row tiles), else the
+// register-fragment persistent kernel
+static inline bool bwd_v8() { return tuning(kTuneDenseBwd) == 0; }
+
 static inline int64_t bwd_grid(int64_t R) {
-  const int64_t ntiles = (R + kBTile - 1) / kBTile;
+  const int64_t ntiles = (R + (bwd_v8() ? 31 : kBTile - 1)) / (bwd_v8() ? 32 : kBTile);
   const int64_t per = (ntiles + kPBwdGrid - 1) / kPBwdGrid;
   return (ntiles + per - 1) / per;
 }
@@ -1393,9 +1703,11 @@ X2G_API int x2g_dense_bwd_ex(const float* dy, const float* z, int act, const flo
     const int grid = static_cast<int>(bwd_grid(R));
     float* part_w = static_cast<float*>(workspace);
     float* part_b = db ? part_w + static_cast<int64_t>(grid) * N * K : nullptr;
-    const bool v5 = tuning(kTuneDenseBwd) == 0 && K % 4 == 0 && N % 4 == 0 && N > 8 && aligned16(dy) &&
-                    aligned16(z) && aligned16(x) && aligned16(dx) && aligned16(dx_add);
-    if (v5)
+    const bool vec = K % 4 == 0 && N % 4 == 0 && N > 8 && aligned16(dy) && aligned16(z) && aligned16(x) &&
+                     aligned16(dx) && aligned16(dx_add);
+    if (vec && bwd_v8())
+      dense_bwd_v8<<<grid, 512, 0, st>>>(dy, z, x, w, R, K, N, act, dx, dx_add, part_w, part_b);
+    else if (vec && tuning(kTuneDenseBwd) == 2)
       dense_bwd_v5<<<grid, 512, 0, st>>>(dy, z, x, w, R, K, N, act, dx, dx_add, part_w, part_b);
     else if (N <= 8)
       dense_bwd_persist<4><<<grid, 512, 0, st>>>(dy, z, x, w, R, K, N, act, dx, dx_add, part_w, part_b);
@@ -1444,6 +1756,20 @@ X2G_API int x2g_dense_bwd(const float* dy, const float* z, int act, const float*
   return x2g_dense_bwd_ex(dy, z, act, x, w, R, K, N, dx, nullptr, dw, db, 0, workspace, workspace_bytes, stream);
 }
 
+// ------------------------------------------------------------------------------- fused ResidualLayer
+X2G_API int x2g_residual_fwd(const float* x, const float* w0, const float* b0, const float* w1, const float* b1,
+                             int64_t R, int32_t D, float* h, float* z0, float* z1, float* y, void* stream) {
+  if (R < 0 || D <= 0) return X2G_EINVAL;
+  if (R == 0) return X2G_OK;
+  if (!x || !w0 || !w1 || !h || !z0 || !z1 || !y) return X2G_EINVAL;
+  if (D > 128 || D % 4 || D <= 8 || R * 128 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  if (!aligned16(x) || !aligned16(h) || !aligned16(z0) || !aligned16(z1) || !aligned16(y)) return X2G_EUNSUPPORTED;
+  const int64_t ntiles = (R + 31) / 32;
+  const unsigned grid = static_cast<unsigned>(ntiles < 256 ? ntiles : 256);
+  residual_fwd_kernel<<<grid, 256, 0, as_stream(stream)>>>(x, w0, b0, w1, b1, R, D, h, z0, z1, y);
+  return last_launch_status();
+}
+
 // ------------------------------------------------------------------------------- batched layers
 X2G_API int x2g_dense_fwd_batched(const x2g_dense_fwd_group* groups, int32_t G, int64_t R, int32_t K, int32_t N,
                                   int act, void* stream) {
@@ -1486,7 +1812,10 @@ X2G_API int x2g_dense_bwd_batched(const x2g_dense_bwd_group* groups, int32_t G, 
     jobs[g] = x2g_slab_job{b.part_w[g], b.part_b[g], p.dw, p.db, static_cast<int64_t>(N) * K, p.db ? N : 0, grid};
   }
   hipStream_t st = as_stream(stream);
-  dense_bwd_v5_batched<<<dim3(grid, G), 512, 0, st>>>(b, R, K, N, act);
+  if (bwd_v8())
+    dense_bwd_v8_batched<<<dim3(grid, G), 512, 0, st>>>(b, R, K, N, act);
+  else
+    dense_bwd_v5_batched<<<dim3(grid, G), 512, 0, st>>>(b, R, K, N, act);
   if (int rc = last_launch_status()) return rc;
   if (flags & X2G_DEFER_SLAB_SUM) return X2G_OK;
   return x2g_slab_sum_batch(jobs, G, (flags & X2G_ACCUM_WGRAD) ? 1 : 0, stream);

@@ -674,6 +674,9 @@ class _DenseFn(torch.autograd.Function):
         return dx, dw, db, dres, None
 
 
+_FUSED_RESIDUAL = os.environ.get("X2G_FUSED_RESIDUAL", "1") == "1"
+
+
 class _ResidualFn(torch.autograd.Function):
     """ResidualLayer (residual_layer.py:21-27): y = x + SiLU(W1 SiLU(W0 x + b0) + b1), forward as
     two fused dense kernels; the backward's residual term is folded into the second data
@@ -687,8 +690,15 @@ class _ResidualFn(torch.autograd.Function):
         W0, W1 = _f32(w0), _f32(w1)
         B0 = _f32(b0) if b0 is not None else None
         B1 = _f32(b1) if b1 is not None else None
-        h, z0 = _dense_fwd_raw(x2, W0, B0, ACT_SILU)
-        y, z1 = _dense_fwd_raw(h, W1, B1, ACT_SILU, r2=x2)
+        R = x2.shape[0]
+        if _FUSED_RESIDUAL and W0.shape == (D, D) and W1.shape == (D, D) and D % 4 == 0 and 8 < D <= 128:
+            f32 = dict(dtype=torch.float32, device=x2.device)
+            h, z0, z1, y = (torch.empty(R, D, **f32) for _ in range(4))
+            call("x2g_residual_fwd", ptr(x2), ptr(W0), ptr(B0), ptr(W1), ptr(B1), R, D, ptr(h), ptr(z0), ptr(z1),
+                 ptr(y), stream_ptr())
+        else:
+            h, z0 = _dense_fwd_raw(x2, W0, B0, ACT_SILU)
+            y, z1 = _dense_fwd_raw(h, W1, B1, ACT_SILU, r2=x2)
         ctx.save_for_backward(x2, h, z0, z1, W0, W1)
         ctx.params = (w0, b0, w1, b1)
         ctx.lead = lead
@@ -729,10 +739,7 @@ class _ConvProjFn(torch.autograd.Function):
         else:
             rf, _ = _dense_fwd_raw(rbf2, Wr, None, ACT_NONE)
             xs = x2 * rf
-        q, _ = _dense_fwd_raw(x2, Wq, Bq, ACT_NONE)
-        k, _ = _dense_fwd_raw(xs, Wk, Bk, ACT_NONE)
-        v, _ = _dense_fwd_raw(xs, Wv, Bv, ACT_NONE)
-        skip, _ = _dense_fwd_raw(x2, Ws, Bs, ACT_NONE)
+        q, k, v, skip = _projections4(x2, xs, (Wq, Bq), (Wk, Bk), (Wv, Bv), (Ws, Bs))
         ctx.save_for_backward(x2, rbf2, rf, xs, Wr, Wq, Wk, Wv, Ws)  # rf None on the gate path
         ctx.params = (wr, wq, bq, wk, bk, wv, bv, ws, bs)
         return q, k, v, skip
@@ -758,6 +765,23 @@ class _ConvProjFn(torch.autograd.Function):
         if rf is not None:
             grbf, dwr, _ = _dense_bwd_raw(grf, None, ACT_NONE, rbf2, Wr, wr, None, False, need_rbf)
         return gx, (grbf if need_rbf else None), dwr, dwq, dbq, dwk, dbk, dwv, dbv, dws, dbs
+
+
+def _projections4(x2, xs, pq, pk, pv, ps):
+    """q = lin_query(x), k = lin_key(x_src), v = lin_value(x_src), skip = lin_skip(x) as ONE
+    batched launch (x2g_dense_fwd_batched, 4 groups) when the shapes allow, else four."""
+    R, K = x2.shape
+    N = pq[0].shape[0]
+    outs = [torch.empty(R, N, dtype=torch.float32, device=x2.device) for _ in range(4)]
+    ok = (K % 4 == 0 and N % 4 == 0 and 8 < K <= 128 and N <= 128 and R * 128 < 2 ** 31
+          and all(p[0].shape == pq[0].shape for p in (pk, pv, ps)))
+    if ok and R > 0:
+        srcs = (x2, xs, xs, x2)
+        grp = (DenseFwdGroup * 4)(*[DenseFwdGroup(_dp(srcs[g]), _dp(p[0]), _dp(p[1]), None, _dp(outs[g]), None)
+                                    for g, p in enumerate((pq, pk, pv, ps))])
+        call("x2g_dense_fwd_batched", grp, 4, R, K, N, ACT_NONE, stream_ptr())
+        return outs
+    return [_dense_fwd_raw(src, p[0], p[1], ACT_NONE)[0] for src, p in zip((x2, xs, xs, x2), (pq, pk, pv, ps))]
 
 
 def gate_supported(D, R):
