@@ -28,7 +28,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "x2-gnn_amd"))
 
 import x2gnn  # noqa: E402
-from x2gnn import ops  # noqa: E402
+from x2gnn import _lib, ops  # noqa: E402
 from x2gnn._lib import call, ptr, stream_ptr  # noqa: E402
 from x2gnn.data import collate  # noqa: E402
 from x2gnn.dist import GradBucket  # noqa: E402
@@ -166,9 +166,10 @@ def attention_probe(model, batch, reps):
     """Time the fused attention kernels of conv layer 0 on this step's real inputs with HIP
     events on the launch stream; returns {kernel: (avg_ms, algorithmic_bytes_per_launch)}."""
     conv = model.fin_model.convs[0]
+    line, plan = model.line_graph_data(batch)  # grad mode on: keeps the sbf factors (rbf_env, Y)
+    lg = plan.lg
+    _, radial, ylm = lg.sbf_factors
     with torch.no_grad():
-        line, plan = model.line_graph_data(batch)
-        lg = plan.lg
         x, rbf, sbf = line.x, line.node_rbf, line.edge_sbf
         table = conv.lin_edge(model.fin_model.edgenn(line.edge_attr)).contiguous()
         row = plan.dst_type
@@ -199,25 +200,39 @@ def attention_probe(model, batch, reps):
              ptr(sproj), None, None, ptr(lg.trip_rowptr), ptr(lg.trip_src), E, T, H, C, D, ptr(out), ptr(alpha),
              ptr(smax), ptr(sden), stream_ptr())
 
-    def bwd_dst():
-        call("x2g_sbf_attention_bwd_dst", ptr(q), ptr(k), ptr(v), ptr(table), ptr(row), ops.EDGE_PER_DST, ptr(sproj),
-             None, None, ptr(lg.trip_rowptr), ptr(lg.trip_src), ptr(alpha), ptr(smax), ptr(sden), ptr(dout), E, T, H,
-             C, D, ptr(dq), ptr(dedge), ptr(dlogit), ptr(dproj), stream_ptr())
+    prob, rho = torch.empty(T, H, **f32), torch.empty(E, H, **f32)
+    gfold = torch.empty(E, 8, D, **f32)
+    dwr, dbr = torch.empty(D, S, **f32), torch.empty(D, **f32)
+    ws_bytes = int(_lib.load().x2g_sbf_radial_wgrad_workspace(E, D))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
+
+    def bwd_dst():  # the factorised backward the model runs (csrc/attention_fold.inc)
+        call("x2g_sbf_attention_bwd_dst_g", ptr(q), ptr(k), ptr(v), ptr(table), ptr(row), ops.EDGE_PER_DST,
+             ptr(sproj), ptr(lg.trip_rowptr), ptr(lg.trip_src), ptr(alpha), ptr(smax), ptr(sden), ptr(dout), E, T, H,
+             C, ptr(dq), ptr(dedge), ptr(dlogit), ptr(prob), ptr(rho), stream_ptr())
 
     def bwd_src():
-        call("x2g_sbf_attention_bwd_src", ptr(q), ptr(sproj), None, None, ptr(src_rowptr), ptr(src_perm),
-             ptr(lg.trip_dst), ptr(alpha), ptr(smax), ptr(sden), ptr(dlogit), ptr(dout), E, T, H, C, D, ptr(dk),
-             ptr(dv), stream_ptr())
+        call("x2g_sbf_attention_bwd_src_fold", ptr(q), ptr(v), ptr(table), ptr(row), table.shape[0],
+             ops.EDGE_PER_DST, ptr(sproj), ptr(ylm), ptr(src_rowptr), ptr(src_perm), ptr(lg.trip_dst), ptr(prob),
+             ptr(dlogit), ptr(rho), ptr(dout), E, T, H, C, ptr(dk), ptr(dv), ptr(gfold), stream_ptr())
+
+    def radial_wgrad():
+        call("x2g_sbf_radial_wgrad", ptr(gfold), ptr(radial), E, D, ptr(dwr), ptr(dbr), 0, ptr(ws), ws_bytes,
+             stream_ptr())
 
     row_b = 4 * D
-    # algorithmic bytes per launch: every logical read/write once per use (gathered rows per triplet)
+    # algorithmic bytes per launch: every logical read/write once per use (gathered rows per triplet;
+    # the per-destination edge-table row counts as a row read per destination, the LDS-staged table
+    # of the source pass not at all)
     proj_bytes = T * (4 * S + row_b)
     fwd_bytes = T * (4 + 3 * row_b + 4 * H) + E * (8 + 4 * row_b + 8 * H + 4)
-    dst_bytes = T * (4 + 3 * row_b + 4 * H * 3 + row_b) + E * (8 + 4 * row_b + 8 * H + 4)
-    src_bytes = T * (8 + 3 * row_b + 4 * H * 2 + 8 * H) + E * (8 + 2 * row_b)
+    dst_bytes = T * (4 + 3 * row_b + 12 * H) + E * (8 + 5 * row_b + 12 * H)
+    src_bytes = T * (12 + 3 * row_b + 12 * H + 32) + E * (8 + 11 * row_b)
+    radial_bytes = E * (8 * row_b + 4 * S) + 4 * D * (S + 1)
     res = {}
     for name, fn, nbytes in (("sbf_project", proj, proj_bytes), ("attn_fwd", fwd, fwd_bytes),
-                             ("attn_bwd_dst", bwd_dst, dst_bytes), ("attn_bwd_src", bwd_src, src_bytes)):
+                             ("attn_bwd_dst", bwd_dst, dst_bytes), ("attn_bwd_src", bwd_src, src_bytes),
+                             ("sbf_radial_wgrad", radial_wgrad, radial_bytes)):
         res[name] = (_event_time(fn, reps), nbytes)
     return res, dict(E=E, T=T, D=D)
 

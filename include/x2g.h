@@ -144,11 +144,13 @@ int x2g_rbf_gate_bwd(const float* g, const int32_t* owner, const float* x, const
  * ji = pos[atom_i]-pos[atom_j], jk = pos[atom_k]-pos[atom_j]  (xgnn.py:61-65,
  * angular_basis_layer.py:87-93).  If theta[T] is non-NULL it is used instead of the positions
  * (F_B_2D.forward(d, Angles, edge_index_1) signature; pos/atom_* may then be NULL).
- * cos_theta[T] (optional, may be NULL) receives cos(theta). */
+ * cos_theta[T] (optional, may be NULL) receives cos(theta).  sph_y[T, 8] (optional, 16-byte
+ * aligned) receives Y_0..Y_6 (theta_t) and a 1: the angular factor of sbf, which the factorised
+ * lin_sbf backward (x2g_sbf_attention_bwd_src_fold) folds per triplet. */
 int x2g_spherical_basis(const float* pos, const int32_t* atom_i, const int32_t* atom_j,
                         const int32_t* atom_k, const float* theta, const int32_t* trip_src,
                         const float* rbf_env, int64_t num_triplets, float* sbf, float* cos_theta,
-                        void* stream);
+                        float* sph_y, void* stream);
 
 /* ---------------------------------------------------------------- SBF-transformer attention */
 
@@ -195,6 +197,36 @@ int x2g_sbf_attention_bwd_src(const float* q, const float* sbf, const float* w_s
                               const float* seg_den, const float* dlogit, const float* dout,
                               int64_t num_edges, int64_t num_triplets, int32_t heads, int32_t channels,
                               int32_t sbf_dim, float* dk, float* dv, void* stream);
+
+/* Factorised backward for X2-GNN's sbf = rbf_env[trip_src] * Y_l0(theta) (angular_basis_layer.py:87-91),
+ * three launches instead of the two attention passes + the [T, HC] d_sbfproj + its T-row weight GEMM:
+ *  (1) x2g_sbf_attention_bwd_dst_g: ONE pass per destination -> dq, d_edge (EDGE_NONE / EDGE_PER_DST
+ *      only), g[T,H] = sum over the head's channels of dout (v[src]+edge) S_t (the softmax-output
+ *      gradient), prob[T,H] = a_t (the softmax probabilities) and seg_rho[E,H] = sum_t a_t g_t;
+ *  (2) x2g_sbf_attention_bwd_src_fold: source-major -> dk, dv (dlogit = a (g - rho) formed here) and
+ *      radial_grad[E, 8, HC]: G[s, l, :] = sum_{t: src(t)=s} d_sbfproj[t, :] Y_l(t) (sph_y from
+ *      x2g_spherical_basis; slot 7 = sum of d_sbfproj).  EDGE_PER_DST requires edge_row and a table
+ *      of edge_rows <= 16 rows (staged in LDS), else X2G_EUNSUPPORTED;
+ *  (3) x2g_sbf_radial_wgrad: dW_sbf[c, 6l+n] (+)= sum_s radial[s, 6l+n] G[s, l, c], db_sbf[c] (+)= sum_s
+ *      G[s, 7, c]; radial = rbf_env [E, 42]; per-workgroup slabs + fixed-order sum, flags as
+ *      x2g_linear_wgrad_ex (weight slabs then bias slabs at the start of the workspace).
+ * sbfproj is the precomputed S = lin_sbf(sbf) [T, HC] (x2g_sbf_project). */
+int x2g_sbf_attention_bwd_dst_g(const float* q, const float* k, const float* v, const float* edge,
+                                const int32_t* edge_row, int edge_mode, const float* sbfproj,
+                                const int32_t* trip_rowptr, const int32_t* trip_src, const float* alpha_raw,
+                                const float* seg_max, const float* seg_den, const float* dout, int64_t num_edges,
+                                int64_t num_triplets, int32_t heads, int32_t channels, float* dq, float* d_edge,
+                                float* g_out, float* prob_out, float* seg_rho, void* stream);
+int x2g_sbf_attention_bwd_src_fold(const float* q, const float* v, const float* edge, const int32_t* edge_row,
+                                   int32_t edge_rows, int edge_mode, const float* sbfproj, const float* sph_y,
+                                   const int32_t* src_rowptr, const int32_t* src_perm, const int32_t* trip_dst,
+                                   const float* prob, const float* g_in, const float* seg_rho, const float* dout,
+                                   int64_t num_edges, int64_t num_triplets, int32_t heads, int32_t channels,
+                                   float* dk, float* dv, float* radial_grad, void* stream);
+int32_t x2g_sbf_radial_wgrad_splits(int64_t num_edges);
+size_t x2g_sbf_radial_wgrad_workspace(int64_t num_edges, int32_t out_dim);
+int x2g_sbf_radial_wgrad(const float* radial_grad, const float* radial, int64_t num_edges, int32_t out_dim,
+                         float* dw, float* db, int flags, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- segmented reductions */
 

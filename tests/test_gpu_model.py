@@ -243,3 +243,61 @@ def test_inference_fused_projection_matches_training_path(cuda, monkeypatch):
     with torch.no_grad():
         infer = m(b)
     assert rel_err(infer.cpu().numpy(), train.cpu().numpy()) < 1e-5
+
+
+def _dense_cluster(n_atoms=72, seed=5):
+    """One molecule whose atoms all sit within 5 A of each other (a 2.4 A-radius ball, >= 0.8 A
+    apart): every line node has n_atoms - 2 > 64 triplets, past the kernels' 64-id index chunks."""
+    from x2gnn.synth import molecule_from_geometry
+
+    rng = np.random.default_rng(seed)
+    pts = []
+    while len(pts) < n_atoms:
+        p = rng.uniform(-2.4, 2.4, 3)
+        if np.linalg.norm(p) <= 2.4 and all(np.linalg.norm(p - q) >= 0.8 for q in pts):
+            pts.append(p)
+    return molecule_from_geometry(rng.choice([1, 6, 7, 8], n_atoms), np.array(pts), feat_rng=rng, y=1.0)
+
+
+@pytest.mark.parametrize("shape", ["S160", "dense"])
+def test_factorised_sbf_backward_equals_two_pass(cuda, monkeypatch, shape):
+    """The folded lin_sbf backward (one destination pass, dS folded per source line node into
+    G[E, 8, D], dW_sbf = sum_s R_s G_s; csrc/attention_fold.inc), in its batched (default) and
+    3-set pipelined (tuning knob 5 = 1) forms, against the two-pass backward with the
+    materialised d_sbfproj [T, D] and its T-row weight GEMM: same energies, every parameter
+    gradient within fp32 reassociation error.  "dense": segments longer than 64 triplets."""
+    import x2gnn
+    from x2gnn import _lib, ops
+    from x2gnn.data import collate
+    from x2gnn.synth import synthetic_molecules
+
+    cfg = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embedding_size=128)
+    mols = synthetic_molecules(48, "S160", seed=7) if shape == "S160" else [_dense_cluster()]
+    batch = collate(mols).to(cuda)
+    calls = []
+    real = ops.sbf_radial_wgrad
+    monkeypatch.setattr(ops, "sbf_radial_wgrad", lambda *a, **k: calls.append(1) or real(*a, **k))
+    lib = _lib.load()
+    runs = []
+    try:
+        for fold, knob in ((True, 0), (True, 1), (False, 0)):
+            monkeypatch.setattr(ops, "_FOLD_SBF", fold)
+            lib.x2g_tuning(5, knob)
+            torch.manual_seed(0)
+            m = x2gnn.xgnn_poly(device="cuda", **cfg).to(cuda)
+            res = m(batch)
+            torch.nn.functional.smooth_l1_loss(res, batch.y).backward()
+            runs.append((res.detach().clone(), {n: p.grad.detach().clone() for n, p in m.named_parameters()
+                                                if p.grad is not None}))
+    finally:
+        lib.x2g_tuning(5, 0)
+    assert len(calls) == 8  # one folded weight gradient per conv layer in each folded run
+    ref_res, ref_grads = runs[-1]
+    for res, grads in runs[:-1]:
+        assert torch.equal(res, ref_res)
+        assert grads.keys() == ref_grads.keys()
+        for n, g in grads.items():
+            ref = ref_grads[n]
+            # lin_key.bias: analytically zero (softmax shift invariance) -> weight-gradient scale
+            scale = float(ref_grads[n.replace("lin_key.bias", "lin_key.weight")].abs().max())
+            assert float((g - ref).abs().max()) <= 1e-5 * scale + 1e-9, n

@@ -29,6 +29,7 @@
 namespace x2g {
 
 constexpr int kS = 42;           // sbf_dim compiled in (7 spherical x 6 radial)
+constexpr int kSph = 7;
 constexpr int kAttnWaves = 4;    // waves per 256-thread block
 constexpr int kMaxBlocks = 2048; // persistent-ish grid: waves grid-stride over line nodes
 constexpr float kSoftmaxEps = 1e-16f;
@@ -292,6 +293,91 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(
     const float inv = 1.0f / (st.den + kSoftmaxEps);
 #pragma unroll
     for (int j = 0; j < CPL; ++j) o[j] = st.acc[j] * inv + sk[j];
+    store_row<CPL>(out + e * D + c0, act, o);
+    if (leader) {
+      smax_out[e * H + head] = st.m;
+      sden_out[e * H + head] = st.den;
+    }
+  }
+}
+
+// Batched forward (the default for precomputed S): the destination's triplets are contiguous, so
+// their source ids arrive as one coalesced load (lane i <-> triplet t0 + i, broadcast with
+// v_readlane) and the k/v/S rows of up to B triplets are issued back to back (clamped to the
+// segment, masked in the arithmetic) — one memory round trip per batch instead of a dependent
+// scalar index chain per triplet.  Same online softmax, same order: bitwise equal results.
+template <int CPL, int LPH, int MODE, int B>
+__device__ __forceinline__ void fwd_batch(int k0, int n, int tb, int sl, FwdState<CPL>& st,
+                                          const float* __restrict__ k, const float* __restrict__ v,
+                                          const float* __restrict__ sp, int D, int H, int c0, int head, bool act,
+                                          bool leader, float sqrt_c, float* __restrict__ alpha_out) {
+  float kv[B][CPL], vv[B][CPL], sv[B][CPL];
+#pragma unroll
+  for (int j = 0; j < B; ++j) {
+    const int idx = k0 + j < n ? k0 + j : n - 1;
+    const int64_t src = lane_bcast(sl, idx);
+    load_row<CPL>(k + src * D + c0, act, kv[j]);
+    load_row<CPL>(v + src * D + c0, act, vv[j]);
+    load_row<CPL>(sp + static_cast<int64_t>(tb + idx) * D + c0, act, sv[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < B; ++j) {
+    if (k0 + j >= n) break;  // wave-uniform
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) dot = fmaf(st.qv[c], kv[j][c] + st.ed[c], dot);
+    const float logit = group_sum<LPH>(dot) / sqrt_c;
+    const float m_new = fmaxf(st.m, logit);
+    const float corr = expf(st.m - m_new);
+    const float p = expf(logit - m_new);
+    st.den = st.den * corr + p;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) st.acc[c] = st.acc[c] * corr + p * ((vv[j][c] + st.ed[c]) * sv[j][c]);
+    st.m = m_new;
+    if (leader) alpha_out[static_cast<int64_t>(tb + k0 + j) * H + head] = logit;
+  }
+}
+
+template <int CPL, int LPH, int MODE>
+__global__ void __launch_bounds__(256) attn_fwd_batched(
+    const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
+    const float* __restrict__ skip, const float* __restrict__ edge, const int32_t* __restrict__ edge_row,
+    const float* __restrict__ sp, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ tsrc, int64_t E,
+    int D, int H, float sqrt_c, float* __restrict__ out, float* __restrict__ alpha_out, float* __restrict__ smax_out,
+    float* __restrict__ sden_out) {
+  const int lane = threadIdx.x & 63;
+  const bool act = lane * CPL < D;
+  const int c0 = act ? lane * CPL : 0;
+  const int head = lane / LPH;
+  const bool leader = act && (lane % LPH) == 0;
+  const WaveRange wr_ = xcd_wave_range(E);
+  for (int64_t e = wr_.first; e < wr_.end; e += wr_.stride) {
+    const int t0 = uniform(rowptr[e]), t1 = uniform(rowptr[e + 1]);
+    FwdState<CPL> st;
+    load_row<CPL>(q + e * D + c0, act, st.qv);
+    if (MODE == X2G_EDGE_PER_DST) {
+      const int64_t r = edge_row ? uniform(edge_row[e]) : e;
+      load_row<CPL>(edge + r * D + c0, act, st.ed);
+    } else {
+      zero_row<CPL>(st.ed);
+    }
+    zero_row<CPL>(st.acc);
+    st.m = -INFINITY;
+    st.den = 0.f;
+    for (int tb = t0; tb < t1; tb += 64) {
+      const int n = t1 - tb < 64 ? t1 - tb : 64;
+      const int sl = tsrc[tb + (lane < n ? lane : n - 1)];
+      int k0 = 0;
+      for (; n - k0 > 4; k0 += 8)
+        fwd_batch<CPL, LPH, MODE, 8>(k0, n, tb, sl, st, k, v, sp, D, H, c0, head, act, leader, sqrt_c, alpha_out);
+      if (k0 < n)
+        fwd_batch<CPL, LPH, MODE, 4>(k0, n, tb, sl, st, k, v, sp, D, H, c0, head, act, leader, sqrt_c, alpha_out);
+    }
+    float sk[CPL], o[CPL];
+    load_row<CPL>(skip + e * D + c0, act, sk);
+    const float inv = 1.0f / (st.den + kSoftmaxEps);
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) o[c] = st.acc[c] * inv + sk[c];
     store_row<CPL>(out + e * D + c0, act, o);
     if (leader) {
       smax_out[e * H + head] = st.m;
@@ -581,6 +667,8 @@ __global__ void __launch_bounds__(256) attn_bwd_src_kernel(
   }
 }
 
+#include "attention_fold.inc"
+
 // ------------------------------------------------------------------------------ sbf projection
 // S[t, :] = W sbf_t + b for all triplets (x2g_sbf_project): one wave per triplet row (grid-
 // stride), CPL channels per lane with W in registers, the 42-float sbf row wave-uniform (scalar
@@ -610,6 +698,12 @@ template <int CPL, int LPH, int MODE, bool PRE>
 void launch_pre(Pass pass, const AttnArgs& a, unsigned blocks, hipStream_t st) {
   switch (pass) {
     case Pass::kFwd:
+      if (PRE && MODE != X2G_EDGE_PER_TRIPLET && tuning(kTuneFold) == 0) {  // batched (default)
+        attn_fwd_batched<CPL, LPH, MODE><<<blocks, 256, 0, st>>>(a.q, a.k, a.v, a.skip, a.edge, a.edge_row, a.sbf,
+                                                                 a.rowptr, a.tidx, a.E, a.D, a.H, a.sqrt_c, a.out,
+                                                                 a.alpha_out, a.smax_out, a.sden_out);
+        break;
+      }
       attn_fwd_kernel<CPL, LPH, MODE, PRE><<<blocks, 256, 0, st>>>(
           a.q, a.k, a.v, a.skip, a.edge, a.edge_row, a.sbf, a.w, a.b, a.rowptr, a.tidx, a.E, a.D, a.H, a.sqrt_c, a.out,
           a.alpha_out, a.smax_out, a.sden_out);
@@ -775,4 +869,170 @@ X2G_API int x2g_sbf_project(const float* sbf, int64_t T, int32_t sbf_dim, const 
     default: return X2G_EUNSUPPORTED;
   }
   return last_launch_status();
+}
+
+// ------------------------------------------------------------------------------ factorised backward
+namespace x2g {
+
+struct FoldArgs {
+  const float *q, *k, *v, *edge;
+  const int32_t* edge_row;
+  int edge_rows;
+  int mode;
+  const float *sp, *y;
+  const int32_t *rowptr, *tidx, *tdst;
+  const float *alpha, *smax, *sden, *prob, *rho_in, *g_in, *dout;
+  int64_t E;
+  int D, H;
+  float sqrt_c;
+  float *dq, *d_edge, *g_out, *prob_out, *rho_out, *dk, *dv, *gfold;
+};
+
+template <int CPL, int LPH>
+void fold_launch_mode(bool dst, const FoldArgs& a, unsigned blocks, hipStream_t st) {
+  if (dst && tuning(kTuneFold) == 0) {  // batched destination pass (default)
+    if (a.mode == X2G_EDGE_PER_DST)
+      attn_bwd_dst_g_batched<CPL, LPH, X2G_EDGE_PER_DST><<<blocks, 256, 0, st>>>(
+          a.q, a.k, a.v, a.edge, a.edge_row, a.sp, a.rowptr, a.tidx, a.alpha, a.smax, a.sden, a.dout, a.E, a.D, a.H,
+          a.sqrt_c, a.dq, a.d_edge, a.g_out, a.prob_out, a.rho_out);
+    else
+      attn_bwd_dst_g_batched<CPL, LPH, X2G_EDGE_NONE><<<blocks, 256, 0, st>>>(
+          a.q, a.k, a.v, a.edge, a.edge_row, a.sp, a.rowptr, a.tidx, a.alpha, a.smax, a.sden, a.dout, a.E, a.D, a.H,
+          a.sqrt_c, a.dq, a.d_edge, a.g_out, a.prob_out, a.rho_out);
+  } else if (dst) {
+    if (a.mode == X2G_EDGE_PER_DST)
+      attn_bwd_dst_g_kernel<CPL, LPH, X2G_EDGE_PER_DST><<<blocks, 256, 0, st>>>(
+          a.q, a.k, a.v, a.edge, a.edge_row, a.sp, a.rowptr, a.tidx, a.alpha, a.smax, a.sden, a.dout, a.E, a.D, a.H,
+          a.sqrt_c, a.dq, a.d_edge, a.g_out, a.prob_out, a.rho_out);
+    else
+      attn_bwd_dst_g_kernel<CPL, LPH, X2G_EDGE_NONE><<<blocks, 256, 0, st>>>(
+          a.q, a.k, a.v, a.edge, a.edge_row, a.sp, a.rowptr, a.tidx, a.alpha, a.smax, a.sden, a.dout, a.E, a.D, a.H,
+          a.sqrt_c, a.dq, a.d_edge, a.g_out, a.prob_out, a.rho_out);
+  } else if (tuning(kTuneFold) == 0) {  // batched source pass (default); knob 5 = 1: the 3-set pipeline
+    const int C = a.D / a.H;
+    if (a.mode == X2G_EDGE_PER_DST)
+      attn_bwd_src_fold_batched<CPL, true><<<blocks, 256, 0, st>>>(
+          a.q, a.v, a.edge, a.edge_row, a.edge_rows, a.sp, a.y, a.rowptr, a.tidx, a.tdst, a.prob, a.rho_in, a.g_in,
+          a.dout, a.E, a.D, a.H, C, a.dk, a.dv, a.gfold);
+    else
+      attn_bwd_src_fold_batched<CPL, false><<<blocks, 256, 0, st>>>(
+          a.q, a.v, a.edge, a.edge_row, a.edge_rows, a.sp, a.y, a.rowptr, a.tidx, a.tdst, a.prob, a.rho_in, a.g_in,
+          a.dout, a.E, a.D, a.H, C, a.dk, a.dv, a.gfold);
+  } else {
+    if (a.mode == X2G_EDGE_PER_DST)
+      attn_bwd_src_fold_kernel<CPL, LPH, true><<<blocks, 256, 0, st>>>(
+          a.q, a.v, a.edge, a.edge_row, a.edge_rows, a.sp, a.y, a.rowptr, a.tidx, a.tdst, a.prob, a.rho_in, a.g_in,
+          a.dout, a.E, a.D, a.H, a.sqrt_c, a.dk, a.dv, a.gfold);
+    else
+      attn_bwd_src_fold_kernel<CPL, LPH, false><<<blocks, 256, 0, st>>>(
+          a.q, a.v, a.edge, a.edge_row, a.edge_rows, a.sp, a.y, a.rowptr, a.tidx, a.tdst, a.prob, a.rho_in, a.g_in,
+          a.dout, a.E, a.D, a.H, a.sqrt_c, a.dk, a.dv, a.gfold);
+  }
+}
+
+int fold_dispatch(bool dst, FoldArgs a, int heads, int channels, hipStream_t st) {
+  if (a.E < 0 || heads <= 0 || channels <= 0) return X2G_EINVAL;
+  if (a.mode != X2G_EDGE_NONE && a.mode != X2G_EDGE_PER_DST) return X2G_EUNSUPPORTED;
+  const int D = heads * channels;
+  int cpl;
+  if (D == 32 || D == 64) cpl = 1;
+  else if (D == 128) cpl = 2;
+  else if (D == 256) cpl = 4;
+  else return X2G_EUNSUPPORTED;
+  if (channels % cpl) return X2G_EUNSUPPORTED;
+  const int lph = channels / cpl;
+  a.D = D;
+  a.H = heads;
+  a.sqrt_c = static_cast<float>(sqrt(static_cast<double>(channels)));
+  if (a.E == 0) return X2G_OK;
+  int64_t want = (a.E + kAttnWaves - 1) / kAttnWaves;
+  want = want < kMaxBlocks ? want : kMaxBlocks;
+  const unsigned blocks = static_cast<unsigned>((want + 7) / 8 * 8);
+  const int key = cpl * 100 + lph;
+  switch (key) {
+    case 102: fold_launch_mode<1, 2>(dst, a, blocks, st); break;
+    case 104: fold_launch_mode<1, 4>(dst, a, blocks, st); break;
+    case 108: fold_launch_mode<1, 8>(dst, a, blocks, st); break;
+    case 116: fold_launch_mode<1, 16>(dst, a, blocks, st); break;
+    case 202: fold_launch_mode<2, 2>(dst, a, blocks, st); break;
+    case 204: fold_launch_mode<2, 4>(dst, a, blocks, st); break;
+    case 208: fold_launch_mode<2, 8>(dst, a, blocks, st); break;
+    case 401: fold_launch_mode<4, 1>(dst, a, blocks, st); break;
+    case 402: fold_launch_mode<4, 2>(dst, a, blocks, st); break;
+    case 404: fold_launch_mode<4, 4>(dst, a, blocks, st); break;
+    case 408: fold_launch_mode<4, 8>(dst, a, blocks, st); break;
+    default: return X2G_EUNSUPPORTED;
+  }
+  return last_launch_status();
+}
+
+}  // namespace x2g
+
+X2G_API int x2g_sbf_attention_bwd_dst_g(const float* q, const float* k, const float* v, const float* edge,
+                                        const int32_t* edge_row, int edge_mode, const float* sbfproj,
+                                        const int32_t* trip_rowptr, const int32_t* trip_src, const float* alpha_raw,
+                                        const float* seg_max, const float* seg_den, const float* dout, int64_t E,
+                                        int64_t T, int32_t heads, int32_t channels, float* dq, float* d_edge,
+                                        float* g_out, float* prob_out, float* seg_rho, void* stream) {
+  if (E > 0 && (!q || !k || !v || !sbfproj || !trip_rowptr || !seg_max || !seg_den || !dout || !dq || !seg_rho))
+    return X2G_EINVAL;
+  if (T > 0 && (!trip_src || !alpha_raw || !g_out || !prob_out)) return X2G_EINVAL;
+  if (edge_mode != X2G_EDGE_NONE && (!edge || !d_edge)) return X2G_EINVAL;
+  FoldArgs a{};
+  a.q = q; a.k = k; a.v = v; a.edge = edge; a.edge_row = edge_row; a.mode = edge_mode; a.sp = sbfproj;
+  a.rowptr = trip_rowptr; a.tidx = trip_src; a.alpha = alpha_raw; a.smax = seg_max; a.sden = seg_den; a.dout = dout;
+  a.E = E; a.dq = dq; a.d_edge = d_edge; a.g_out = g_out; a.prob_out = prob_out; a.rho_out = seg_rho;
+  return fold_dispatch(true, a, heads, channels, as_stream(stream));
+}
+
+X2G_API int x2g_sbf_attention_bwd_src_fold(const float* q, const float* v, const float* edge, const int32_t* edge_row,
+                                           int32_t edge_rows, int edge_mode, const float* sbfproj, const float* sph_y,
+                                           const int32_t* src_rowptr, const int32_t* src_perm, const int32_t* trip_dst,
+                                           const float* prob, const float* g_in, const float* seg_rho,
+                                           const float* dout, int64_t E, int64_t T, int32_t heads, int32_t channels,
+                                           float* dk, float* dv, float* radial_grad, void* stream) {
+  if (E > 0 && (!q || !v || !sbfproj || !src_rowptr || !seg_rho || !dout || !dk || !dv || !radial_grad))
+    return X2G_EINVAL;
+  if (T > 0 && (!src_perm || !trip_dst || !prob || !g_in || !sph_y)) return X2G_EINVAL;
+  // the source pass reads the edge term from a small table staged in LDS (X2-GNN's element table)
+  if (edge_mode == X2G_EDGE_PER_DST && (!edge || !edge_row || edge_rows < 1 || edge_rows > kFoldTableRows))
+    return X2G_EUNSUPPORTED;
+  if (T > 0x7fffffff || E > 0x7fffffff) return X2G_EUNSUPPORTED;  // int32 triplet ids in the prefetch sets
+  FoldArgs a{};
+  a.q = q; a.v = v; a.edge = edge; a.edge_row = edge_row; a.edge_rows = edge_rows; a.mode = edge_mode;
+  a.sp = sbfproj; a.y = sph_y; a.rowptr = src_rowptr; a.tidx = src_perm; a.tdst = trip_dst; a.prob = prob;
+  a.rho_in = seg_rho; a.g_in = g_in; a.dout = dout; a.E = E; a.dk = dk; a.dv = dv; a.gfold = radial_grad;
+  return fold_dispatch(false, a, heads, channels, as_stream(stream));
+}
+
+X2G_API int32_t x2g_sbf_radial_wgrad_splits(int64_t E) { return radial_splits(E); }
+
+X2G_API size_t x2g_sbf_radial_wgrad_workspace(int64_t E, int32_t D) {
+  if (E <= 0 || D <= 0) return 0;
+  return static_cast<size_t>(radial_splits(E)) * (static_cast<int64_t>(D) * kS + D) * sizeof(float);
+}
+
+X2G_API int x2g_sbf_radial_wgrad(const float* radial_grad, const float* radial, int64_t E, int32_t D, float* dw,
+                                 float* db, int flags, void* workspace, size_t workspace_bytes, void* stream) {
+  if (E < 0 || !dw || !db || (flags & ~(X2G_ACCUM_WGRAD | X2G_DEFER_SLAB_SUM))) return X2G_EINVAL;
+  if (D != 32 && D != 64 && D != 128) return X2G_EUNSUPPORTED;  // blockDim = 2 D threads
+  const bool accum = flags & X2G_ACCUM_WGRAD;
+  if ((flags & X2G_DEFER_SLAB_SUM) && E == 0) return X2G_EINVAL;
+  hipStream_t st = as_stream(stream);
+  if (E == 0) {
+    if (accum) return X2G_OK;
+    hipError_t e = hipMemsetAsync(dw, 0, sizeof(float) * D * kS, st);
+    if (e == hipSuccess) e = hipMemsetAsync(db, 0, sizeof(float) * D, st);
+    return e == hipSuccess ? X2G_OK : static_cast<int>(e);
+  }
+  if (!radial_grad || !radial) return X2G_EINVAL;
+  if (!workspace || workspace_bytes < x2g_sbf_radial_wgrad_workspace(E, D)) return X2G_EWORKSPACE;
+  const int splits = radial_splits(E);
+  const int64_t rps = radial_rows_per_split(E);
+  float* part_w = static_cast<float*>(workspace);
+  float* part_b = part_w + static_cast<int64_t>(splits) * D * kS;
+  sbf_radial_wgrad_kernel<<<splits, 2 * D * kRadialGroups, 0, st>>>(radial_grad, radial, E, D, rps, part_w, part_b);
+  if (int rc = last_launch_status()) return rc;
+  if (flags & X2G_DEFER_SLAB_SUM) return X2G_OK;
+  return sum_slabs_launch(part_w, static_cast<int64_t>(D) * kS, part_b, D, splits, dw, db, accum, st);
 }

@@ -30,6 +30,7 @@ enum TuneKey {
   kTuneAttn = 2,
   kTuneDenseDbg = 3,
   kTuneGateSplits = 4,  // rbf gate backward: workgroup cap (0 = default)
+  kTuneFold = 5,        // factorised attention backward: 0 = batched passes, 1 = 3-set pipelined passes
   kTuneCount = 16
 };
 int tuning(int key);
@@ -53,6 +54,12 @@ __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirs
 
 // Sum over aligned groups of `G` consecutive lanes (G power of two, <= 64); every lane of a
 // group ends with the group total.
+// Value of lane `lane` (wave-uniform index) in every lane: v_readlane into a scalar register.
+__device__ __forceinline__ int lane_bcast(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ float lane_bcast(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
 template <int G>
 __device__ __forceinline__ float group_sum(float v) {
 #pragma unroll

@@ -175,13 +175,21 @@ def edge_basis(pos, lg: LineGraph, freq, cutoff: float = 5.0):
 
 
 def spherical_basis(pos, lg: LineGraph, rbf_env, want_cos=False):
-    """[T, 42] sbf = rbf_env[src] * Y_l0(theta), theta from the triplet's atom positions."""
+    """[T, 42] sbf = rbf_env[src] * Y_l0(theta), theta from the triplet's atom positions.
+
+    When gradients are being recorded the two factors are kept on the line graph
+    (``lg.sbf_factors = (sbf, rbf_env, Y[T, 8])``): the attention backward then folds lin_sbf's
+    weight gradient per source line node instead of materialising d(lin_sbf(sbf)) [T, D]
+    (csrc/attention_fold.inc)."""
     _need_cuda(pos, rbf_env)
     pos = _f32(pos)
+    rbf_env = _f32(rbf_env)
     out = torch.empty(lg.T, 42, dtype=torch.float32, device=pos.device)
     cos_t = torch.empty(lg.T, dtype=torch.float32, device=pos.device) if want_cos else None
+    ylm = torch.empty(lg.T, 8, dtype=torch.float32, device=pos.device) if _FOLD_SBF and torch.is_grad_enabled() else None
     call("x2g_spherical_basis", ptr(pos), ptr(lg.atom_i), ptr(lg.atom_j), ptr(lg.atom_k), None, ptr(lg.trip_src),
-         ptr(_f32(rbf_env)), lg.T, ptr(out), ptr(cos_t), stream_ptr())
+         ptr(rbf_env), lg.T, ptr(out), ptr(cos_t), ptr(ylm), stream_ptr())
+    lg.sbf_factors = (out, rbf_env, ylm) if ylm is not None else None
     return (out, cos_t) if want_cos else out
 
 
@@ -192,15 +200,31 @@ def spherical_basis_from_angles(theta, trip_src, rbf_env):
     src = _i32(trip_src)
     out = torch.empty(th.shape[0], 42, dtype=torch.float32, device=th.device)
     call("x2g_spherical_basis", None, None, None, None, ptr(th), ptr(src), ptr(_f32(rbf_env)), th.shape[0], ptr(out),
-         None, stream_ptr())
+         None, None, stream_ptr())
     return out
 
 
 # ---------------------------------------------------------------------------------- attention
+# Factorised lin_sbf backward (csrc/attention_fold.inc): X2G_FOLD_SBF=0 restores the two-pass
+# backward + [T, D] d_sbfproj + T-row weight GEMM (kept for the drop-in conv API, whose sbf is
+# an arbitrary [T, 42] tensor).
+_FOLD_SBF = os.environ.get("X2G_FOLD_SBF", "1") == "1"
+
+
+def _sbf_factors(lg, sbf, edge_mode, D, edge, edge_row):
+    fac = getattr(lg, "sbf_factors", None)
+    if fac is None or fac[0] is not sbf or edge_mode == EDGE_PER_TRIPLET or D not in (32, 64, 128):
+        return None
+    if edge_mode == EDGE_PER_DST and (edge_row is None or edge is None or edge.shape[0] > 16):
+        return None  # the source pass stages the per-destination edge table in LDS
+    return fac[1], fac[2]
+
+
 class _SBFAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row, heads, channels):
         w_param, b_param = w_sbf, b_sbf
+        factors = _sbf_factors(lg, sbf, edge_mode, heads * channels, edge, edge_row)
         q, k, v, skip = _f32(q), _f32(k), _f32(v), _f32(skip)
         sbf, w_sbf, b_sbf = _f32(sbf), _f32(w_sbf), _f32(b_sbf)
         edge = _f32(edge) if edge is not None else None
@@ -217,7 +241,11 @@ class _SBFAttention(torch.autograd.Function):
         call("x2g_sbf_attention_fwd", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(edge_row), edge_mode,
              ptr(sproj), None, None, ptr(lg.trip_rowptr), ptr(lg.trip_src), E, T, heads, channels, D, ptr(out),
              ptr(alpha), ptr(smax), ptr(sden), stream_ptr())
-        ctx.save_for_backward(q, k, v, edge, sbf, sproj, alpha, smax, sden)
+        if factors is not None:  # the factorised backward never reads sbf itself
+            ctx.save_for_backward(q, k, v, edge, factors[0], factors[1], sproj, alpha, smax, sden)
+        else:
+            ctx.save_for_backward(q, k, v, edge, sbf, None, sproj, alpha, smax, sden)
+        ctx.fold = factors is not None
         ctx.w_param, ctx.b_param = w_param, b_param
         ctx.lg, ctx.edge_mode, ctx.edge_row, ctx.heads, ctx.channels = lg, edge_mode, edge_row, heads, channels
         ctx.edge_shape = None if edge is None else edge.shape
@@ -229,7 +257,7 @@ class _SBFAttention(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout, _da=None, _dm=None, _ds=None):
-        q, k, v, edge, sbf, sproj, alpha, smax, sden = ctx.saved_tensors
+        q, k, v, edge, sbf, ylm, sproj, alpha, smax, sden = ctx.saved_tensors
         lg, mode, heads, channels = ctx.lg, ctx.edge_mode, ctx.heads, ctx.channels
         dout = _f32(dout)
         E, T, D = q.shape[0], lg.T, heads * channels
@@ -237,6 +265,8 @@ class _SBFAttention(torch.autograd.Function):
         dq = torch.empty(E, D, dtype=torch.float32, device=dev)
         dk = torch.empty_like(dq)
         dv = torch.empty_like(dq)
+        if ctx.fold:  # sbf here is the radial factor rbf_env [E, 42]
+            return _SBFAttention._backward_fold(ctx, dout, q, k, v, edge, sbf, ylm, sproj, alpha, smax, sden, dq, dk, dv)
         dlogit = torch.empty(T, heads, dtype=torch.float32, device=dev)
         dproj = torch.empty(T, D, dtype=torch.float32, device=dev)
         if mode == EDGE_PER_TRIPLET:
@@ -262,6 +292,55 @@ class _SBFAttention(torch.autograd.Function):
         else:
             dw, db = linear_wgrad(dproj, sbf)
         return dq, dk, dv, dout, d_edge, None, dw, db, None, None, None, None, None
+
+    @staticmethod
+    def _backward_fold(ctx, dout, q, k, v, edge, radial, ylm, sproj, alpha, smax, sden, dq, dk, dv):
+        lg, mode, heads, channels = ctx.lg, ctx.edge_mode, ctx.heads, ctx.channels
+        E, T, D = q.shape[0], lg.T, heads * channels
+        dev = q.device
+        g = torch.empty(T, heads, dtype=torch.float32, device=dev)
+        prob = torch.empty(T, heads, dtype=torch.float32, device=dev)
+        rho = torch.empty(E, heads, dtype=torch.float32, device=dev)
+        d_edge = torch.empty(E, D, dtype=torch.float32, device=dev) if mode == EDGE_PER_DST else None
+        gfold = torch.empty(E, 8, D, dtype=torch.float32, device=dev)
+        st = stream_ptr()
+        call("x2g_sbf_attention_bwd_dst_g", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(ctx.edge_row), mode, ptr(sproj),
+             ptr(lg.trip_rowptr), ptr(lg.trip_src), ptr(alpha), ptr(smax), ptr(sden), ptr(dout), E, T, heads, channels,
+             ptr(dq), ptr(d_edge), ptr(g), ptr(prob), ptr(rho), st)
+        src_rowptr, src_perm = lg.src_csr()
+        rows = 0 if edge is None else edge.shape[0]
+        call("x2g_sbf_attention_bwd_src_fold", ptr(q), ptr(v), ptr(edge), ptr(ctx.edge_row), rows, mode, ptr(sproj),
+             ptr(ylm), ptr(src_rowptr), ptr(src_perm), ptr(lg.trip_dst), ptr(prob), ptr(g), ptr(rho), ptr(dout), E, T,
+             heads, channels, ptr(dk), ptr(dv), ptr(gfold), st)
+        if mode == EDGE_PER_DST and ctx.edge_row is not None:
+            d_edge = keyed_row_sum(d_edge, ctx.edge_row, ctx.edge_shape[0])
+        gw, gb = grad_sink(ctx.w_param), grad_sink(ctx.b_param)
+        if gw is not None and gb is not None:
+            dw, db = sbf_radial_wgrad(gfold, radial, dw_out=gw, db_out=gb)
+        else:
+            dw, db = sbf_radial_wgrad(gfold, radial)
+        return dq, dk, dv, dout, d_edge, None, dw, db, None, None, None, None, None
+
+
+def sbf_radial_wgrad(gfold, radial, dw_out=None, db_out=None):
+    """(dW_sbf [D, 42], db_sbf [D]) from the source-folded gradient G [E, 8, D] and the radial
+    factor rbf_env [E, 42] (x2g_sbf_radial_wgrad); accumulates into dw_out/db_out when given."""
+    E, _, D = gfold.shape
+    accum = dw_out is not None
+    if accum and db_out is None:
+        raise ValueError("accumulating dW_sbf needs the bias-gradient buffer too")
+    dw = dw_out if accum else torch.empty(D, 42, dtype=torch.float32, device=gfold.device)
+    db = db_out if accum else torch.empty(D, dtype=torch.float32, device=gfold.device)
+    lib = _lib.load()
+    ws_bytes = int(lib.x2g_sbf_radial_wgrad_workspace(E, D))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=gfold.device)
+    defer = accum and _DEFER is not None and E > 0
+    flags = (ACCUM_WGRAD if accum else 0) | (DEFER_SLAB_SUM if defer else 0)
+    call("x2g_sbf_radial_wgrad", ptr(gfold), ptr(_f32(radial)), E, D, ptr(dw), ptr(db), flags, ptr(ws), ws_bytes,
+         stream_ptr())
+    if defer:
+        _defer_job(ws, 0, int(lib.x2g_sbf_radial_wgrad_splits(E)), D * 42, D, dw, db)
+    return (None, None) if accum else (dw, db)
 
 
 # Inference (grad mode off): nothing is saved for a backward, so the [T, D] projection S is not
