@@ -1020,19 +1020,35 @@ __global__ void __launch_bounds__(512) dense_fwd_narrow(const float* __restrict_
   }
   const unsigned magic = 0xFFFFFFFFu / static_cast<unsigned>(K) + 1u;  // K >= 2 here
   const float* wb = Ws + 2 * n + h;
+  const int nq = (64 * K) >> 2;
+  // register double buffer: the next pair's x span is in flight while this pair's MFMAs and
+  // epilogue run (NQI 16-byte chunks per thread cover 64 rows x KP floats)
+  constexpr int NQI = (16 * KP + 511) / 512;
+  f4 pre[NQI];
+  auto prefetch = [&](int64_t tpn) {
+    const int64_t bn = tpn * 64 * K;
+    const int64_t nv = ((R - tpn * 64) < 64 ? (R - tpn * 64) : 64) * K;
+#pragma unroll
+    for (int u = 0; u < NQI; ++u) {
+      const int qi = tid + 512 * u;
+      const bool ok = qi < nq && 4 * qi < nv;
+      pre[u] = ok ? *reinterpret_cast<const f4*>(X + bn + 4 * qi) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  if (blockIdx.x < npairs) prefetch(blockIdx.x);
   for (int64_t tp = blockIdx.x; tp < npairs; tp += G) {
     // stage the pair: rows [64 tp, 64 tp + 64) are floats [64 tp K, 64 tp K + 64 K)
-    const int64_t base = tp * 64 * K;
     const int64_t nvalid = ((R - tp * 64) < 64 ? (R - tp * 64) : 64) * K;
-    const int nq = (64 * K) >> 2;
     __syncthreads();  // previous pair's output tile fully stored
-    for (int qi = tid; qi < nq; qi += 512) {
-      const bool ok = 4 * qi < nvalid;
-      const f4 v = *reinterpret_cast<const f4*>(X + base + (ok ? 4 * qi : 0));
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const unsigned f = 4 * qi + e, row = __umulhi(f, magic), c = f - row * K;
-        Xs[row * KP + c] = (4 * qi + e < nvalid) ? v[e] : 0.f;
+    for (int u = 0; u < NQI; ++u) {
+      const int qi = tid + 512 * u;
+      if (qi < nq) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const unsigned f = 4 * qi + e, row = __umulhi(f, magic), c = f - row * K;
+          Xs[row * KP + c] = (4 * qi + e < nvalid) ? pre[u][e] : 0.f;
+        }
       }
     }
     for (int idx = tid; idx < 64 * (KP - K); idx += 512) {  // zero the pad columns
@@ -1040,6 +1056,7 @@ __global__ void __launch_bounds__(512) dense_fwd_narrow(const float* __restrict_
       Xs[row * KP + c] = 0.f;
     }
     __syncthreads();
+    if (tp + G < npairs) prefetch(tp + G);
     floatx16 acc0, acc1;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
