@@ -990,7 +990,7 @@ __global__ void __launch_bounds__(256, 1) residual_fwd_kernel(const float* __res
 // ---------------------------------------------------------------- forward, narrow K (K % 4 != 0)
 // For rows too narrow / odd for 16-byte row chunks (lin_sbf: K = 42): a 64-row tile pair is one
 // contiguous span of 64*K floats, read with 16-byte loads regardless of K and scattered into
-// an LDS tile [64][KP] (KP = K rounded up to 4, zero padded).  Contraction order
+// LDS unchanged (row stride K, 16-byte writes); the MFMA operand read strides by K.  Contraction order
 // c(s, h) = 4 (s >> 1) + 2h + (s & 1): a lane's two consecutive steps read one 8-byte pair.
 // Weight in the padded slot layout with the same order; epilogue as dense_fwd_v5.
 __device__ __forceinline__ int cmap_n(int s, int h) { return 4 * (s >> 1) + 2 * h + (s & 1); }
@@ -1018,7 +1018,6 @@ __global__ void __launch_bounds__(512) dense_fwd_narrow(const float* __restrict_
     const float wv = (j < N && r < K) ? W[j * K + r] : 0.f;
     Ws[sl * kSlotStride + 2 * j + hh] = wv;
   }
-  const unsigned magic = 0xFFFFFFFFu / static_cast<unsigned>(K) + 1u;  // K >= 2 here
   const float* wb = Ws + 2 * n + h;
   const int nq = (64 * K) >> 2;
   // register double buffer: the next pair's x span is in flight while this pair's MFMAs and
@@ -1041,20 +1040,19 @@ __global__ void __launch_bounds__(512) dense_fwd_narrow(const float* __restrict_
     const int64_t nvalid = ((R - tp * 64) < 64 ? (R - tp * 64) : 64) * K;
     __syncthreads();  // previous pair's output tile fully stored
 #pragma unroll
-    for (int u = 0; u < NQI; ++u) {
+    for (int u = 0; u < NQI; ++u) {  // the span lands as-is (row stride K): one 16-byte LDS write
       const int qi = tid + 512 * u;
       if (qi < nq) {
+        f4 v = pre[u];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const unsigned f = 4 * qi + e, row = __umulhi(f, magic), c = f - row * K;
-          Xs[row * KP + c] = (4 * qi + e < nvalid) ? pre[u][e] : 0.f;
-        }
+        for (int e = 0; e < 4; ++e)
+          if (4 * qi + e >= nvalid) v[e] = 0.f;
+        *reinterpret_cast<f4*>(Xs + 4 * qi) = v;
       }
     }
-    for (int idx = tid; idx < 64 * (KP - K); idx += 512) {  // zero the pad columns
-      const int row = idx / (KP - K), c = K + idx - row * (KP - K);
-      Xs[row * KP + c] = 0.f;
-    }
+    // contraction columns K..KP-1 of a row read the next row's first floats against zero weight;
+    // the last row reads this zeroed tail
+    if (tid < KP - K) Xs[64 * K + tid] = 0.f;
     __syncthreads();
     if (tp + G < npairs) prefetch(tp + G);
     floatx16 acc0, acc1;
@@ -1063,12 +1061,12 @@ __global__ void __launch_bounds__(512) dense_fwd_narrow(const float* __restrict_
       acc0[j] = 0.f;
       acc1[j] = 0.f;
     }
-    const float* xs = Xs + (slot * 32 + i) * KP + 2 * h;
+    const float* xs = Xs + (slot * 32 + i) * K + 2 * h;
 #pragma unroll
     for (int g = 0; g < STEPS / 2; ++g) {
-      const float2 a = *reinterpret_cast<const float2*>(xs + 4 * g);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, wb[(2 * g) * kSlotStride], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, wb[(2 * g + 1) * kSlotStride], acc1, 0, 0, 0);
+      const float a0 = xs[4 * g], a1 = xs[4 * g + 1];
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, wb[(2 * g) * kSlotStride], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, wb[(2 * g + 1) * kSlotStride], acc1, 0, 0, 0);
     }
     __syncthreads();  // x tile consumed: the buffer stages the output
 #pragma unroll
