@@ -20,7 +20,7 @@ for s in "$@"; do
   case $s in
     kernels) step kernels 420 python -m pytest tests/test_gpu_kernels.py -q -m gpu -rf ;;
     model) step model 420 python -m pytest tests/test_gpu_model.py -q -m gpu -rf ;;
-    gpu) step gputests 600 python -m pytest tests -q -m gpu -rf ;;
+    gpu) step gputests 600 python -u -m pytest tests -q -m gpu -rf --timeout 300 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 420 python bench.py --steps 20 --warmup 5 ;;
     bench_c3) step bench_c3 420 python bench.py --workload qm9_allprop --target 0 --steps 20 --warmup 5 ;;

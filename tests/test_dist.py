@@ -2,8 +2,8 @@
 
 Each rank runs the oracle model (same seeded weights) forward+backward on its own shard of
 molecules, the flat gradient bucket is all-reduced (``GradBucket.allreduce_mean``), and the
-result must equal the single-process gradient of the whole batch (shards of equal size, loss =
-mean over molecules, so mean-of-shard-means == full-batch mean).
+result must equal the single-process gradient of the whole batch (loss = mean over molecules:
+for equal shards the mean of the shard means, for unequal shards the count-weighted sum).
 """
 import os
 import socket
@@ -44,7 +44,7 @@ def _grads(model, mols):
     return loss.detach()
 
 
-def _worker(rank, world, port, shards, out_q):
+def _worker(rank, world, port, shards, out_q, weighted=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(2)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -54,10 +54,18 @@ def _worker(rank, world, port, shards, out_q):
         bucket = GradBucket(model.parameters())
         bucket.zero()
         loss = _grads(model, [mols[i] for i in shards[rank]])
-        bucket.allreduce_mean()
-        t = loss.clone()
-        dist.all_reduce(t)
-        out_q.put((rank, bucket.flat.clone().numpy(), float(t) / world))
+        n_local = len(shards[rank])
+        n_global = sum(len(s) for s in shards)
+        if weighted:
+            bucket.allreduce_mean(local_count=n_local, global_count=n_global)
+            t = loss.clone() * n_local / n_global
+            dist.all_reduce(t)
+            out_q.put((rank, bucket.flat.clone().numpy(), float(t)))
+        else:
+            bucket.allreduce_mean()
+            t = loss.clone()
+            dist.all_reduce(t)
+            out_q.put((rank, bucket.flat.clone().numpy(), float(t) / world))
     finally:
         dist.destroy_process_group()
 
@@ -84,14 +92,20 @@ def test_gradbucket_views_and_zero():
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_allreduce_equals_full_batch_gradient():
+@pytest.mark.parametrize("weighted", [False, True])
+def test_two_rank_allreduce_equals_full_batch_gradient(weighted):
+    """Equal shards with the plain mean; unequal shards (5 + 3 molecules, as shard_by_triplets
+    produces) with the count-weighted all-reduce."""
     world = 2
     mols = synthetic_molecules(8, "S160", seed=5)
-    shards = [np.arange(0, 8, 2), np.arange(1, 8, 2)]  # equal sizes -> mean of means == mean
+    if weighted:
+        shards = [np.array([0, 2, 3, 5, 6]), np.array([1, 4, 7])]
+    else:
+        shards = [np.arange(0, 8, 2), np.arange(1, 8, 2)]  # equal sizes -> mean of means == mean
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, shards, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, shards, q, weighted)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict()

@@ -424,8 +424,11 @@ def test_dense_bwd_ex_dx_add_and_accumulate(cuda, R, K, N, act):
 @pytest.mark.gpu
 @pytest.mark.parametrize("max_norm", [100.0, 0.05])
 def test_flat_adam_matches_torch(cuda, max_norm):
-    """x2g_clip_adam_ema (FlatAdam) vs torch clip_grad_norm_ + Adam + AveragedModel-style EMA,
-    three steps, clipping inactive (100) and active (0.05)."""
+    """x2g_clip_adam_ema (FlatAdam) vs torch clip_grad_norm_ + Adam + the reference's EMA
+    (torch.optim.swa_utils.AveragedModel with avg_fn = d*avg + (1-d)*p, train_ema.py:45-47: the
+    first update copies the parameters), three steps, clipping inactive (100) and active (0.05)."""
+    from torch.optim.swa_utils import AveragedModel
+
     from x2gnn.dist import GradBucket
     from x2gnn.optim import FlatAdam
 
@@ -434,18 +437,20 @@ def test_flat_adam_matches_torch(cuda, max_norm):
     ref = [torch.randn(s, device=cuda, generator=g).requires_grad_(True) for s in shapes]
     mine = [r.detach().clone().requires_grad_(True) for r in ref]
     opt_ref = torch.optim.Adam(ref, lr=1e-3)
-    ema_ref = [r.detach().clone() for r in ref]
+    holder = torch.nn.Module()
+    holder.ps = torch.nn.ParameterList([torch.nn.Parameter(r) for r in ref])
+    decay = 0.95
+    ema_model = AveragedModel(holder, avg_fn=lambda avg, p, n: decay * avg + (1 - decay) * p)
+    ema_ref = list(ema_model.module.ps)
     bucket = GradBucket(mine)
-    opt = FlatAdam(mine, lr=1e-3, max_norm=max_norm, ema_decay=0.95, bucket=bucket)
+    opt = FlatAdam(mine, lr=1e-3, max_norm=max_norm, ema_decay=decay, bucket=bucket)
     for step in range(3):
         grads = [torch.randn(s, device=cuda, generator=g) for s in shapes]
         for r, gr in zip(ref, grads):
             r.grad = gr.clone()
         torch.nn.utils.clip_grad_norm_(ref, max_norm)
         opt_ref.step()
-        with torch.no_grad():
-            for e, r in zip(ema_ref, ref):
-                e.lerp_(r, 0.05)
+        ema_model.update_parameters(holder)
         bucket.zero()
         for m, gr in zip(mine, grads):
             m.grad.copy_(gr)
@@ -453,33 +458,66 @@ def test_flat_adam_matches_torch(cuda, max_norm):
         for r, m in zip(ref, mine):
             torch.testing.assert_close(m.detach(), r.detach(), rtol=2e-6, atol=2e-7)
         for e, m in zip(ema_ref, opt.ema_params()):
-            torch.testing.assert_close(m, e, rtol=2e-6, atol=2e-7)
+            torch.testing.assert_close(m, e.detach(), rtol=2e-6, atol=2e-7)
+        if step == 0:  # AveragedModel's first update is a copy of the stepped parameters
+            for r, m in zip(ref, opt.ema_params()):
+                assert torch.equal(m, r.detach())
     assert float(opt.steps) == 3.0
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("T", [194060, 1000, 37, 0])
-def test_sbf_project_both_paths_vs_torch(cuda, T):
-    """x2g_sbf_project: MFMA narrow-K path (default) and the VALU path (x2g_tuning key 2 = 1)."""
+@pytest.mark.parametrize("T,out_dim", [(194060, 128), (1000, 128), (37, 128), (0, 128), (1000, 256), (37, 256),
+                                       (1000, 64), (37, 32)])
+def test_sbf_project_both_paths_vs_torch(cuda, T, out_dim):
+    """x2g_sbf_project: MFMA narrow-K path (default, out_dim <= 128) and the VALU path
+    (x2g_tuning key 2 = 1; the only path for out_dim 256, e.g. xgnn_poly's default in_channels=256,
+    xgnn.py:16).  T = 37 makes 37*42 floats, not a multiple of 4: the last 16-byte chunk is partial."""
     from x2gnn import _lib
     from x2gnn._lib import call, ptr, stream_ptr
 
-    g = torch.Generator(device=cuda).manual_seed(T + 5)
+    g = torch.Generator(device=cuda).manual_seed(T + 5 + out_dim)
     sbf = torch.randn(T, 42, device=cuda, generator=g)
-    w = torch.randn(128, 42, device=cuda, generator=g) / 6.5
-    b = torch.randn(128, device=cuda, generator=g)
+    w = torch.randn(out_dim, 42, device=cuda, generator=g) / 6.5
+    b = torch.randn(out_dim, device=cuda, generator=g)
     ref = (sbf.double() @ w.double().t() + b.double()).float()
     lib = _lib.load()
     for knob in (0, 1):
         prev = lib.x2g_tuning(2, knob)
-        out = torch.full((T, 128), float("nan"), device=cuda)
-        call("x2g_sbf_project", ptr(sbf), T, 42, ptr(w), ptr(b), 128, ptr(out), stream_ptr())
+        out = torch.full((T, out_dim), float("nan"), device=cuda)
+        call("x2g_sbf_project", ptr(sbf), T, 42, ptr(w), ptr(b), out_dim, ptr(out), stream_ptr())
         lib.x2g_tuning(2, prev)
         torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("R,K", [(5000, 42), (333, 10), (64, 42), (65, 126)])
+def test_sbf_project_rows_independent_of_nonfinite_neighbours(cuda):
+    """A non-finite sbf row poisons only its own projection (the reference's lin_sbf is row-wise):
+    the narrow-K kernel's LDS span has row stride K, so a row's pad columns alias the next row."""
+    from x2gnn._lib import call, ptr, stream_ptr
+
+    T = 200
+    g = torch.Generator(device=cuda).manual_seed(3)
+    sbf = torch.randn(T, 42, device=cuda, generator=g)
+    bad = [5, 64, 65, 127, 199]  # inside a tile, first rows of a pair, the last row
+    sbf[bad[0], 0] = float("inf")
+    sbf[bad[1], :4] = float("nan")
+    sbf[bad[2], 1] = float("-inf")
+    sbf[bad[3], 0] = float("nan")
+    sbf[bad[4], 3] = float("inf")
+    w = torch.randn(128, 42, device=cuda, generator=g) / 6.5
+    b = torch.randn(128, device=cuda, generator=g)
+    out = torch.empty(T, 128, device=cuda)
+    call("x2g_sbf_project", ptr(sbf), T, 42, ptr(w), ptr(b), 128, ptr(out), stream_ptr())
+    torch.cuda.synchronize()
+    good = torch.ones(T, dtype=torch.bool)
+    good[bad] = False
+    assert torch.isfinite(out[good.to(cuda)]).all()
+    ref = (sbf.double() @ w.double().t() + b.double()).float()
+    torch.testing.assert_close(out[good.to(cuda)], ref[good.to(cuda)], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,K", [(5000, 42), (333, 10), (64, 42), (65, 126), (37, 42), (1, 42), (63, 6 * 7 + 1)])
 def test_dense_narrow_k_vs_torch(cuda, R, K):
     from x2gnn import ops
 

@@ -137,6 +137,44 @@ def test_full_size_batch_vs_oracle(cuda):
     assert rel_err(res, ref) < ENERGY_RTOL
 
 
+@pytest.mark.parametrize("model_kind", ["poly", "global"])
+def test_reference_default_width_256_vs_oracle(cuda, model_kind):
+    """xgnn_poly's constructor default width (in_channels=256, heads=16 -> 16 channels per head,
+    xgnn.py:16 / :78) through every wide-row path: the per-row S projection (out_dim 256), the
+    CPL=4 attention kernels, the general dense kernels (K or N > 128).  Energies and all
+    parameter gradients vs the oracle."""
+    import x2gnn
+    from x2gnn.data import collate
+    from x2gnn.synth import synthetic_molecules
+
+    cfg = dict(conv_layers=2, sbf_dim=7, rbf_dim=6, in_channels=256, heads=16, embedding_size=128)
+    b = collate(synthetic_molecules(6, "S160", seed=21))
+    if model_kind == "poly":
+        orc = ref_cpu.XGNN(**cfg)
+        m = x2gnn.xgnn_poly(device="cuda", **cfg)
+    else:
+        orc = ref_cpu.XGNN(global_pool="add", **cfg)
+        m = x2gnn.xgnn_poly_global(device="cuda", pool_option="add", **cfg)
+    load_seeded(orc, 5)
+    load_seeded(m, 5)
+    m = m.to(cuda)
+    ref = ref_cpu.run_batch(orc, b)
+    torch.nn.functional.smooth_l1_loss(ref, b.y).backward()
+    bd = b.to(cuda)
+    res = m(bd)
+    torch.nn.functional.smooth_l1_loss(res, bd.y).backward()
+    assert rel_err(res.detach().cpu().numpy(), ref.detach().numpy()) < ENERGY_RTOL
+    ref_grads = {n: p.grad for n, p in orc.named_parameters()}
+    scale = max(float(g.abs().max()) for g in ref_grads.values() if g is not None)
+    for n, p in m.named_parameters():
+        rg = ref_grads.get(n)
+        if rg is None:
+            assert p.grad is None or float(p.grad.abs().max()) == 0.0, n
+            continue
+        got = p.grad.detach().cpu()
+        assert float((got - rg).abs().max()) <= 2e-3 * float(rg.abs().max()) + 1e-6 * scale, n
+
+
 def test_full_size_properties(cuda):
     """B=128 S160 (BASELINE config 2): finite outputs, loss decreases under one SGD step,
     per-molecule energies invariant to batch composition (molecules are independent)."""

@@ -1030,8 +1030,16 @@ __global__ void __launch_bounds__(512) dense_fwd_narrow(const float* __restrict_
 #pragma unroll
     for (int u = 0; u < NQI; ++u) {
       const int qi = tid + 512 * u;
-      const bool ok = qi < nq && 4 * qi < nv;
-      pre[u] = ok ? *reinterpret_cast<const f4*>(X + bn + 4 * qi) : f4{0.f, 0.f, 0.f, 0.f};
+      // whole 16-byte chunks load as one vector; the span's last partial chunk (64*K or the
+      // ragged tail's length need not be a multiple of 4) element-wise, never past the end of X
+      if (qi < nq && 4 * qi + 4 <= nv) {
+        pre[u] = *reinterpret_cast<const f4*>(X + bn + 4 * qi);
+      } else {
+        pre[u] = f4{0.f, 0.f, 0.f, 0.f};
+        if (qi < nq && 4 * qi < nv)
+          for (int e = 0; e < 4; ++e)
+            if (4 * qi + e < nv) pre[u][e] = X[bn + 4 * qi + e];
+      }
     }
   };
   if (blockIdx.x < npairs) prefetch(blockIdx.x);
@@ -1050,8 +1058,8 @@ __global__ void __launch_bounds__(512) dense_fwd_narrow(const float* __restrict_
         *reinterpret_cast<f4*>(Xs + 4 * qi) = v;
       }
     }
-    // contraction columns K..KP-1 of a row read the next row's first floats against zero weight;
-    // the last row reads this zeroed tail
+    // contraction columns K..KP-1 of a row fall on the next row's first floats: the operand read
+    // below masks them (a zero weight alone would turn a neighbour's Inf/NaN into NaN here)
     if (tid < KP - K) Xs[64 * K + tid] = 0.f;
     __syncthreads();
     if (tp + G < npairs) prefetch(tp + G);
@@ -1062,9 +1070,10 @@ __global__ void __launch_bounds__(512) dense_fwd_narrow(const float* __restrict_
       acc1[j] = 0.f;
     }
     const float* xs = Xs + (slot * 32 + i) * K + 2 * h;
+    const int klim = K - 2 * h;  // contraction index 4g + 2h (+1) must stay below K
 #pragma unroll
     for (int g = 0; g < STEPS / 2; ++g) {
-      const float a0 = xs[4 * g], a1 = xs[4 * g + 1];
+      const float a0 = 4 * g < klim ? xs[4 * g] : 0.f, a1 = 4 * g + 1 < klim ? xs[4 * g + 1] : 0.f;
       acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, wb[(2 * g) * kSlotStride], acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, wb[(2 * g + 1) * kSlotStride], acc1, 0, 0, 0);
     }
@@ -1086,6 +1095,8 @@ __global__ void __launch_bounds__(512) dense_fwd_narrow(const float* __restrict_
 
 int dense_fwd_narrow_launch(const float* x, const float* w, const float* b, const float* res, int64_t R, int K, int N,
                             int act, float* y, float* z, hipStream_t st) {
+  // the kernel covers N <= 128 columns and K <= 2*64; row offsets are 32-bit
+  if (N > 128 || K > 128 || R * 128 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
   const int64_t npairs = (R + 63) / 64;
   const unsigned grid = static_cast<unsigned>(npairs < 512 ? npairs : 512);
   if (K <= 44)

@@ -4,7 +4,7 @@
 // per parameter tensor (~300 launches for X2-GNN's 155 tensors); here it is three launches:
 //   1. per-block partial sums of g^2 over contiguous chunks (fixed order),
 //   2. one block: total norm, clip coefficient, step count + bias corrections -> scalars,
-//   3. elementwise Adam + EMA.
+//   3. elementwise Adam + EMA (a copy of the parameters at step 1, as AveragedModel does).
 // Every value the update depends on that changes between steps (step count, norm, clip scale)
 // lives in device memory, so a captured HIP graph replays correctly; the hyper-parameters
 // (lr, betas, eps, max_norm, ema decay) are read from the same device scalar block so a
@@ -80,6 +80,9 @@ __global__ void __launch_bounds__(256) adam_ema(float* __restrict__ p, const flo
   const float clip = sc[X2G_OPT_CLIP], b1 = sc[X2G_OPT_BETA1], b2 = sc[X2G_OPT_BETA2];
   const float eps = sc[X2G_OPT_EPS], step_size = sc[X2G_OPT_STEP_SIZE], bc2s = sc[X2G_OPT_BC2_SQRT];
   const float d = sc[X2G_OPT_EMA_DECAY];
+  // AveragedModel.update_parameters copies the parameters on its first call (n_averaged == 0) and
+  // applies avg_fn from the second on; the step count is already on the device (graph-safe)
+  const bool first = sc[X2G_OPT_STEP] == 1.0f;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
     const float gi = g[i] * clip;
@@ -93,7 +96,7 @@ __global__ void __launch_bounds__(256) adam_ema(float* __restrict__ p, const flo
     const float pi = p[i] - step_size * (mi / denom);
     p[i] = pi;
     // ema.lerp_(p, 1 - d)
-    if (ema) ema[i] = ema[i] + (1.0f - d) * (pi - ema[i]);
+    if (ema) ema[i] = first ? pi : ema[i] + (1.0f - d) * (pi - ema[i]);
   }
 }
 

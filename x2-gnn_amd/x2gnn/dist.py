@@ -56,7 +56,23 @@ class GradBucket:
     def zero(self):
         self.flat.zero_()
 
-    def allreduce_mean(self, group=None):
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    def allreduce_mean(self, group=None, local_count=None, global_count=None):
+        """Turn each rank's gradient of its own mean loss into the gradient of the global-batch
+        mean loss (trainer.py:41, smooth_l1 with reduction='mean').
+
+        Without counts every rank's shard is taken to hold the same number of molecules, and the
+        per-rank gradients are averaged.  With ``local_count`` (molecules on this rank) and
+        ``global_count`` (molecules over all ranks, known on the host from the sharding), each
+        rank's gradient is weighted by local/global before the sum, which is what unequal shards
+        (e.g. ``shard_by_triplets``) need."""
+        multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        if local_count is not None:
+            if global_count is None or global_count <= 0:
+                raise ValueError("weighted all-reduce needs the global molecule count")
+            self.flat.mul_(float(local_count) / float(global_count))
+            if multi:
+                dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+            return
+        if multi:
             dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
             self.flat.div_(dist.get_world_size(group))
