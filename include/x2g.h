@@ -341,7 +341,7 @@ int x2g_dense_bwd(const float* dy, const float* z, int act, const float* x, cons
 /* x2g_dense_bwd plus: dx = dz w + dx_add (dx_add [R,K] optional, may alias dx: the gradient
  * contributions autograd would otherwise sum in a separate kernel — a residual branch, a tensor
  * feeding several layers) and flags (X2G_ACCUM_WGRAD: accumulate dw / db into their buffers).
- * dx_add is supported for in/out features <= 128 (X2G_EUNSUPPORTED otherwise). */
+ * Every shape supports dx_add (wider layers add it in the general kernel's epilogue). */
 int x2g_dense_bwd_ex(const float* dy, const float* z, int act, const float* x, const float* w, int64_t rows,
                      int32_t in_features, int32_t out_features, float* dx, const float* dx_add, float* dw,
                      float* db, int flags, void* workspace, size_t workspace_bytes, void* stream);
@@ -433,10 +433,73 @@ size_t x2g_optimizer_workspace(int64_t n);
 /* The reference trainer's update (trainer.py:43-48, train_ema.py:45-48) over one flat fp32
  * parameter buffer of n elements: clip_grad_norm_(max_norm) (coef = max_norm/(norm+1e-6),
  * clamped to 1), torch.optim.Adam (amsgrad=False, no weight decay), then the EMA
- * ema = d*ema + (1-d)*p (ema may be NULL).  grads must be 16-byte aligned; the gradient
+ * ema = d*ema + (1-d)*p (ema may be NULL; at step 1 ema = p, as AveragedModel's first
+ * update_parameters copies).  grads must be 16-byte aligned; the gradient
  * buffer is read, not modified.  Deterministic (fixed-order norm reduction). */
 int x2g_clip_adam_ema(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* ema,
                       int64_t n, float* scalars, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- row chains (trunk tail)
+ *
+ * One conv layer of the trunk ends in seven row-wise Linear layers on the same E rows
+ * (model.py:47-50): bf_skip = ResidualLayer (2 Linear), SiLU(dense_bf_skip(.)) + the conv
+ * input, af_skip = 2 x ResidualLayer (4 Linear).  A "chain" runs such a sequence of D x D
+ * stages in ONE kernel with every 16-row tile held in registers from the first stage to the
+ * last (the stage weights stream through LDS), so the chain pays one launch and one pipeline
+ * ramp instead of seven.  Stage s:  z_s = in_s W_s^T + b_s,  out_s = act_s(z_s) (+ residual),
+ * in_{s+1} = out_s.  Compiled for D = 128 (X2G_EUNSUPPORTED otherwise), rows * 128 < 2^31,
+ * 16-byte aligned row-major [rows, 128] tensors. */
+#define X2G_CHAIN_MAX_STAGES 8
+#define X2G_CHAIN_SILU 1     /* act_s = SiLU (else identity) */
+#define X2G_CHAIN_HOLD 2     /* in_s becomes the held residual (the input of a ResidualLayer) */
+#define X2G_CHAIN_RES_HELD 4 /* out_s += the held residual */
+#define X2G_CHAIN_RES_EXT 8  /* out_s += res_ext (at most one stage; a HOLD .. RES_HELD pair must
+                                not span it, and a stage adds one residual at most) */
+
+typedef struct {
+  const float* w; /* [D, D] nn.Linear weight, row n = output feature n */
+  const float* b; /* [D] or NULL */
+  float* z;       /* [rows, D] pre-activation out (kept for the backward), or NULL */
+  float* y;       /* [rows, D] stage output out (the next stage's input); required for the last stage */
+  float* wt;      /* [D, D] out: w transposed, for x2g_chain_bwd (NULL: not written) */
+  int32_t flags;
+} x2g_chain_stage;
+
+/* Forward of a chain of n_stages (1..X2G_CHAIN_MAX_STAGES) stages on x [rows, dim]. */
+int x2g_chain_fwd(const float* x, const float* res_ext, const x2g_chain_stage* stages, int32_t n_stages,
+                  int64_t rows, int32_t dim, void* stream);
+
+typedef struct {
+  const float* w; /* [D, D] the stage's weight */
+  const float* wt; /* [D, D] w transposed (x2g_chain_fwd's wt output), or NULL: w is read transposed */
+  const float* z; /* [rows, D] its saved pre-activation (required for SiLU stages) */
+  float* dz;      /* [rows, D] out: dL/dz_s (the input of the stage's weight gradient) */
+  int32_t flags;  /* the forward's flags */
+} x2g_chain_bwd_stage;
+
+/* Data gradients of x2g_chain_fwd: dy (+ dy_add, may be NULL) = dL/d out_{n-1}; writes every
+ * stage's dz, dx = dL/dx and d_res_ext = dL/d res_ext (NULL when no stage has RES_EXT).
+ * Weight gradients: x2g_wgrad_batched over (dz_s, in_s) pairs. */
+int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_bwd_stage* stages, int32_t n_stages,
+                  int64_t rows, int32_t dim, float* dx, float* d_res_ext, void* stream);
+
+/* Weight / bias gradients of up to X2G_CHAIN_MAX_STAGES independent D x D Linear layers over the
+ * same rows: dw_g = dy_g^T x_g, db_g = column sums of dy_g (db_g may be NULL).  Rows are split
+ * into fixed chunks per layer (one workgroup each, f32 MFMA), chunk partials summed in a fixed
+ * order (deterministic); flags X2G_ACCUM_WGRAD / X2G_DEFER_SLAB_SUM as x2g_linear_wgrad_ex.  Layer
+ * g's slabs: x2g_wgrad_batched_splits() slabs of D*D floats starting at byte g * (workspace(rows,
+ * dim, num_jobs) / num_jobs), then its bias slabs (D floats each). */
+typedef struct {
+  const float* dy; /* [rows, D] */
+  const float* x;  /* [rows, D] */
+  float* dw;       /* [D, D] */
+  float* db;       /* [D] or NULL */
+} x2g_wgrad_job;
+
+size_t x2g_wgrad_batched_workspace(int64_t rows, int32_t dim, int32_t num_jobs);
+int32_t x2g_wgrad_batched_splits(int64_t rows, int32_t dim, int32_t num_jobs);
+int x2g_wgrad_batched(const x2g_wgrad_job* jobs, int32_t num_jobs, int64_t rows, int32_t dim, int flags,
+                      void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -460,8 +460,8 @@ def test_flat_adam_matches_torch(cuda, max_norm):
         for e, m in zip(ema_ref, opt.ema_params()):
             torch.testing.assert_close(m, e.detach(), rtol=2e-6, atol=2e-7)
         if step == 0:  # AveragedModel's first update is a copy of the stepped parameters
-            for r, m in zip(ref, opt.ema_params()):
-                assert torch.equal(m, r.detach())
+            for p, m in zip(mine, opt.ema_params()):
+                assert torch.equal(m, p.detach())
     assert float(opt.steps) == 3.0
 
 
@@ -750,3 +750,160 @@ def test_sbf_radial_wgrad_vs_fp64(cuda, E, D):
     assert bool(((db.cpu().double() - ref_b).abs() <= 1e-6 * G[:, 7].double().abs().sum(0) + 1e-6).all())
     dw2, _ = ops.sbf_radial_wgrad(G.to(cuda), R.to(cuda))
     assert torch.equal(dw, dw2)
+
+
+def _chain_ref(x, res, ws, bs, flags):
+    """fp64 torch restatement of x2g_chain_fwd (include/x2g.h: row chains)."""
+    from x2gnn import ops
+
+    held = None
+    cur = x
+    for w, b, f in zip(ws, bs, flags):
+        if f & ops.CHAIN_RES_EXT:
+            held = res
+        if f & ops.CHAIN_HOLD:
+            held = cur
+        z = cur @ w.t() + (b if b is not None else 0.0)
+        y = torch.nn.functional.silu(z) if f & ops.CHAIN_SILU else z
+        if f & (ops.CHAIN_RES_HELD | ops.CHAIN_RES_EXT):
+            y = y + held
+        cur = y
+    return cur
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [21058, 1000, 37, 16, 1])
+@pytest.mark.parametrize("kind", ["trunk", "plain", "residual"])
+def test_row_chain_fwd_bwd_vs_torch(cuda, R, kind):
+    """x2g_chain_fwd / x2g_chain_bwd / x2g_wgrad_batched (ops.row_chain) against fp64 torch
+    autograd: the trunk tail of model.py:47-50 (7 stages), a plain Linear without activation,
+    and one ResidualLayer; ragged tiles (R % 16 != 0) and fewer rows than one tile."""
+    from x2gnn import ops
+
+    S, H, RH, RE = ops.CHAIN_SILU, ops.CHAIN_HOLD, ops.CHAIN_RES_HELD, ops.CHAIN_RES_EXT
+    flags = {"trunk": [S | H, S | RH, S | RE, S | H, S | RH, S | H, S | RH], "plain": [0],
+             "residual": [S | H, S | RH]}[kind]
+    n = len(flags)
+    g = torch.Generator(device=cuda).manual_seed(R + n)
+    lins = [torch.nn.Linear(128, 128, bias=(i != 1 or kind != "trunk")).to(cuda) for i in range(n)]
+    with torch.no_grad():
+        for m in lins:
+            m.weight.copy_(torch.randn(128, 128, device=cuda, generator=g) / 11.3)
+            if m.bias is not None:
+                m.bias.copy_(torch.randn(128, device=cuda, generator=g) * 0.1)
+    x = torch.randn(R, 128, device=cuda, generator=g).requires_grad_(True)
+    res = torch.randn(R, 128, device=cuda, generator=g).requires_grad_(True) if kind == "trunk" else None
+    y = ops.row_chain(x, res, lins, flags)
+    dy = torch.randn(R, 128, device=cuda, generator=g)
+    y.backward(dy)
+    xd = x.detach().double().requires_grad_(True)
+    rd = res.detach().double().requires_grad_(True) if res is not None else None
+    wd = [m.weight.detach().double().requires_grad_(True) for m in lins]
+    bd = [m.bias.detach().double().requires_grad_(True) if m.bias is not None else None for m in lins]
+    yr = _chain_ref(xd, rd, wd, bd, flags)
+    yr.backward(dy.double())
+    torch.testing.assert_close(y.double(), yr, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(x.grad.double(), xd.grad, rtol=1e-5, atol=1e-5)
+    if res is not None:
+        torch.testing.assert_close(res.grad.double(), rd.grad, rtol=1e-5, atol=1e-5)
+    for m, w, b in zip(lins, wd, bd):
+        scale = float(w.grad.abs().max())
+        assert float((m.weight.grad.double() - w.grad).abs().max()) <= 2e-5 * scale + 1e-6
+        if b is not None:
+            assert float((m.bias.grad.double() - b.grad).abs().max()) <= 2e-5 * float(b.grad.abs().max()) + 1e-6
+
+
+@pytest.mark.gpu
+def test_row_chain_rejects_bad_programs(cuda):
+    """RES_HELD without a HOLD, two RES_EXT stages, a HOLD..RES_HELD pair spanning the RES_EXT
+    stage, and a width other than 128 are refused at the ABI (no kernel runs)."""
+    from x2gnn import _lib, ops
+    from x2gnn._lib import ptr, stream_ptr
+
+    lib = _lib.load()
+    R = 64
+    x = torch.randn(R, 128, device=cuda)
+    w = torch.randn(128, 128, device=cuda)
+    ys = [torch.empty(R, 128, device=cuda) for _ in range(3)]
+    S, H, RH, RE = ops.CHAIN_SILU, ops.CHAIN_HOLD, ops.CHAIN_RES_HELD, ops.CHAIN_RES_EXT
+
+    def run(flags, dim=128):
+        st = (ops.ChainStage * len(flags))(*[ops.ChainStage(w.data_ptr(), None, None, ys[i].data_ptr(), None, f)
+                                              for i, f in enumerate(flags)])
+        return lib.x2g_chain_fwd(ptr(x), ptr(x), st, len(flags), R, dim, stream_ptr())
+
+    assert run([S | RH]) != 0
+    assert run([S | RE, S | RE]) != 0
+    assert run([S | H, S | RE, S | RH]) != 0
+    assert run([S | H, S | RH], dim=64) != 0
+    assert run([S | H, S | RH]) == 0
+    torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+def test_model_chain_matches_layerwise_path(cuda, monkeypatch):
+    """xgnn_poly at config width with the row-chain trunk tail (default) vs the layer-by-layer
+    kernels (ops._CHAIN off): energies and every parameter gradient agree to fp32 rounding."""
+    import x2gnn
+    from x2gnn import ops
+    from x2gnn.data import collate
+    from x2gnn.synth import synthetic_molecules
+
+    from weights import load_seeded
+
+    cfg = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embedding_size=128)
+    b = collate(synthetic_molecules(16, "S160", seed=31)).to(cuda)
+    out = []
+    for on in (True, False):
+        monkeypatch.setattr(ops, "_CHAIN", on)
+        m = x2gnn.xgnn_poly(device="cuda", **cfg)
+        load_seeded(m, 3)
+        m = m.to(cuda)
+        res = m(b)
+        torch.nn.functional.smooth_l1_loss(res, b.y).backward()
+        out.append((res.detach(), {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}))
+    (r1, g1), (r0, g0) = out
+    torch.testing.assert_close(r1, r0, rtol=1e-5, atol=1e-5)
+    assert g1.keys() == g0.keys()
+    for k in g1:
+        scale = float(g0[k].abs().max())
+        assert float((g1[k] - g0[k]).abs().max()) <= 1e-4 * scale + 1e-7, k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [3000, 21])
+def test_row_chain_bwd_with_and_without_transposed_weights(cuda, R):
+    """x2g_chain_bwd reads each stage's weight slice from x2g_chain_fwd's W^T output when given
+    (contiguous loads) or transposes W itself: both give the same bits; W^T equals w.t()."""
+    from x2gnn._lib import call, ptr, stream_ptr
+    from x2gnn import ops
+
+    S, H, RH, RE = ops.CHAIN_SILU, ops.CHAIN_HOLD, ops.CHAIN_RES_HELD, ops.CHAIN_RES_EXT
+    flags = [S | H, S | RH, S | RE, S | H, S | RH]
+    n = len(flags)
+    g = torch.Generator(device=cuda).manual_seed(R)
+    W = [torch.randn(128, 128, device=cuda, generator=g) / 11.3 for _ in range(n)]
+    B = [torch.randn(128, device=cuda, generator=g) * 0.1 for _ in range(n)]
+    x = torch.randn(R, 128, device=cuda, generator=g)
+    res = torch.randn(R, 128, device=cuda, generator=g)
+    Z = [torch.empty(R, 128, device=cuda) for _ in range(n)]
+    Y = [torch.empty(R, 128, device=cuda) for _ in range(n)]
+    WT = torch.empty(n, 128, 128, device=cuda)
+    st = (ops.ChainStage * n)(*[ops.ChainStage(W[i].data_ptr(), B[i].data_ptr(), Z[i].data_ptr(), Y[i].data_ptr(),
+                                               WT[i].data_ptr(), flags[i]) for i in range(n)])
+    call("x2g_chain_fwd", ptr(x), ptr(res), st, n, R, 128, stream_ptr())
+    dy = torch.randn(R, 128, device=cuda, generator=g)
+    outs = []
+    for use_wt in (True, False):
+        DZ = [torch.empty(R, 128, device=cuda) for _ in range(n)]
+        dx, dres = torch.empty(R, 128, device=cuda), torch.empty(R, 128, device=cuda)
+        bst = (ops.ChainBwdStage * n)(*[ops.ChainBwdStage(W[i].data_ptr(), WT[i].data_ptr() if use_wt else None,
+                                                          Z[i].data_ptr(), DZ[i].data_ptr(), flags[i]) for i in range(n)])
+        call("x2g_chain_bwd", ptr(dy), None, bst, n, R, 128, ptr(dx), ptr(dres), stream_ptr())
+        outs.append((dx, dres, DZ))
+    torch.cuda.synchronize()
+    for i in range(n):
+        assert torch.equal(WT[i], W[i].t())
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    for a, b in zip(outs[0][2], outs[1][2]):
+        assert torch.equal(a, b)

@@ -1,0 +1,811 @@
+// Row chains: a sequence of D x D Linear stages (bias, SiLU, residual) applied to the same rows in
+// ONE kernel, every 16-row tile held in registers from the first stage to the last.
+//
+// X2-GNN's trunk ends each conv layer with seven such layers on the E line-node rows
+// (model.py:47-50: bf_skip = ResidualLayer, SiLU(dense_bf_skip(.)) + the conv input, af_skip =
+// 2 x ResidualLayer; residual_layer.py:21-27).  At QM9 batch sizes (E ~ 21k rows) one Linear is
+// ~5 us of f32 MFMA work spread over the chip, so as separate launches each pays its own
+// ramp (weight staging, first tile's load latency) and drain; here the chain pays them once.
+//
+// Row layout of a tile: lane l = (r = l & 15, g = l >> 4) of the owning wave holds row r's
+// features 16b + 4g + e (b = 0..7, e = 0..3) as eight float4 x[b].  A stage computes the
+// transposed product D = M X^T with v_mfma_f32_16x16x4_f32 (exact f32 FMA chains): A operand =
+// rows of M from LDS, B operand = the tile itself — lane (r, g) supplies X[r][k] for the k of
+// MFMA step (b, e) in its lane group g, k = 16b + 4g + e, which is its own register x[b][e] —
+// and output block bp comes back as lane (r, g) holding out[r][16bp + 4g + e]: the same row
+// layout, so the next stage takes it as its B operand with no data movement.
+// M = W for the forward (y = x W^T), W^T for the backward (dx = dz W).
+//
+// M sits in LDS as 128 rows of 32 16-byte chunks, chunk c of row n at position c ^ (n & 15).
+// The A-operand read of lane (n, g) is chunk 4b + g of row 16bp + n; within every ds_read_b128
+// lane group the 16 chunks then fall on distinct bank quads (lanes 0-3/12-15 of group g and
+// lanes 4-11 of group g+1 differ in the chunk's low bit after the XOR).  Two weight images are
+// double-buffered (128 KB): the next stage's weight is loaded into registers while this stage's
+// MFMAs run and written to LDS after them.
+#include <math.h>
+
+#include "common.hpp"
+
+namespace x2g {
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kCD = 128;                // compiled width
+constexpr int kCWaves = 8;              // 512 threads: two waves per SIMD, one 16-row tile each
+constexpr int kCThreads = kCWaves * 64;
+constexpr int kMChunks = kCD * kCD / 4;  // 16-byte chunks per weight image (64 KB)
+
+struct ChainFwdArgs {
+  const float* x;
+  const float* res;
+  int64_t R;
+  int n;
+  int dbg;  // diagnostic ablations (x2g_tuning key 7 bits, timing only: results are wrong when set)
+  x2g_chain_stage st[X2G_CHAIN_MAX_STAGES];
+};
+
+struct ChainBwdArgs {
+  const float* dy;
+  const float* dy_add;
+  float* dx;
+  float* dres;
+  int64_t R;
+  int n;
+  x2g_chain_bwd_stage st[X2G_CHAIN_MAX_STAGES];
+};
+
+__device__ __forceinline__ f4 zero4() { return f4{0.f, 0.f, 0.f, 0.f}; }
+
+// weight image staging: global -> registers (8 chunks per thread) ...
+template <bool TRANS>
+__device__ __forceinline__ void load_w(const float* __restrict__ W, f4 (&pre)[8]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    if (!TRANS) {  // chunk q = row n, 16-byte column chunk c of W
+      pre[u] = reinterpret_cast<const f4*>(W)[tid + kCThreads * u];
+    } else {  // M[k][4c..4c+3] = W[4c..4c+3][k]: one wave reads 64 consecutive k of a W row
+      const int k = tid & 127, c = (tid >> 7) + 4 * u;
+      const float* p = W + 4 * c * kCD + k;
+      pre[u] = f4{p[0], p[kCD], p[2 * kCD], p[3 * kCD]};
+    }
+  }
+}
+
+// ... -> the swizzled LDS image
+template <bool TRANS>
+__device__ __forceinline__ void store_w(f4* __restrict__ Ms, const f4 (&pre)[8]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    int n, c;
+    if (!TRANS) {
+      const int q = tid + kCThreads * u;
+      n = q >> 5;
+      c = q & 31;
+    } else {
+      n = tid & 127;
+      c = (tid >> 7) + 4 * u;
+    }
+    Ms[n * 32 + (c ^ (n & 15))] = pre[u];
+  }
+}
+
+// acc[bp] = rows 16bp..16bp+15 of M times the tile (see the header comment).  The A operands of
+// k-group b + 1 (eight ds_read_b128) are issued before the 32 MFMAs of group b.
+__device__ __forceinline__ void chain_gemm(const f4* __restrict__ Ms, const f4 (&x)[8], f4 (&acc)[8], int nl,
+                                           int g) {
+#pragma unroll
+  for (int bp = 0; bp < 8; ++bp) acc[bp] = zero4();
+  f4 a[2][8];
+#pragma unroll
+  for (int bp = 0; bp < 8; ++bp) a[0][bp] = Ms[(16 * bp + nl) * 32 + (g ^ nl)];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const int cur = b & 1;
+    if (b + 1 < 8) {
+#pragma unroll
+      for (int bp = 0; bp < 8; ++bp) a[cur ^ 1][bp] = Ms[(16 * bp + nl) * 32 + ((4 * (b + 1) + g) ^ nl)];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int bp = 0; bp < 8; ++bp)
+        acc[bp] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][bp][e], x[b][e], acc[bp], 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ float silu_f(float z) { return z / (1.0f + expf(-z)); }
+
+__device__ __forceinline__ float silu_grad_f(float z) {
+  const float s = 1.0f / (1.0f + expf(-z));
+  return s * (1.0f + z * (1.0f - s));
+}
+
+// The v2 epilogues use the hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32: ~1 ulp each) instead
+// of libm expf and IEEE division (~25 VALU instructions per element): the epilogue runs between
+// barriers with no MFMA to hide behind, and the exact forms cost ~1.7 us per stage at config 2.
+// sigmoid(z) = rcp(1 + 2^(-z log2 e)); z -> -inf gives 0, z -> +inf gives 1, NaN stays NaN.
+__device__ __forceinline__ float sigmoid_fast(float z) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * z));
+}
+__device__ __forceinline__ float silu_fast(float z) { return z * sigmoid_fast(z); }
+__device__ __forceinline__ float silu_grad_fast(float z) {
+  const float s = sigmoid_fast(z);
+  return s * (1.0f + z * (1.0f - s));
+}
+
+// row r of the tile, float4 b of the lane's row layout: clamped address + 0/1 mask (the loads
+// stay unconditional so all eight are in flight together)
+__device__ __forceinline__ void load_rows(const float* __restrict__ P, int rc, bool rok, int g, f4 (&v)[8]) {
+  const float m = rok ? 1.0f : 0.0f;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) v[b] = *reinterpret_cast<const f4*>(P + rc * kCD + 16 * b + 4 * g) * m;
+}
+
+__device__ __forceinline__ void store_rows(float* __restrict__ P, int row, bool rok, int g, const f4 (&v)[8]) {
+  if (!rok) return;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) *reinterpret_cast<f4*>(P + row * kCD + 16 * b + 4 * g) = v[b];
+}
+
+__global__ void __launch_bounds__(kCThreads, 1) chain_fwd_kernel(const ChainFwdArgs a) {
+  __shared__ f4 Ms[2][kMChunks];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rl = lane & 15, g = lane >> 4;
+  const int64_t ntiles = (a.R + 15) / 16;
+  const int64_t groups = (ntiles + kCWaves - 1) / kCWaves;
+  const int n = a.n;
+  f4 pre[8];
+  int buf = 0;
+  if (static_cast<int64_t>(blockIdx.x) < groups) {
+    load_w<false>(a.st[0].w, pre);
+    store_w<false>(Ms[0], pre);
+  }
+  __syncthreads();
+  for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+    const int64_t tile = grp * kCWaves + wave;
+    const bool active = tile < ntiles;  // wave-uniform
+    const int row = static_cast<int>(tile) * 16 + rl;
+    const bool rok = active && row < a.R;
+    const int rc = rok ? row : 0;
+    f4 x[8], held[8];
+    load_rows(a.x, rc, rok, g, x);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) held[b] = zero4();
+    for (int s = 0; s < n; ++s) {
+      const x2g_chain_stage& S = a.st[s];
+      const int fl = S.flags;
+      const bool more = (s + 1 < n || grp + gridDim.x < groups) && !(a.dbg & 1);
+      if (more) load_w<false>(s + 1 < n ? a.st[s + 1].w : a.st[0].w, pre);
+      // the held registers carry either a ResidualLayer input (HOLD) or the external residual
+      // (RES_EXT loads it here, during the MFMAs; the host rejects chains that would need both)
+      if (fl & X2G_CHAIN_RES_EXT) load_rows(a.res, rc, rok, g, held);
+      if (fl & X2G_CHAIN_HOLD) {
+#pragma unroll
+        for (int b = 0; b < 8; ++b) held[b] = x[b];
+      }
+      f4 acc[8];
+      if (active) {
+        chain_gemm(Ms[buf], x, acc, rl, g);
+#pragma unroll
+        for (int bp = 0; bp < 8; ++bp) {
+          f4 z = acc[bp];
+          if (S.b) z += *reinterpret_cast<const f4*>(S.b + 16 * bp + 4 * g);
+          if (rok && S.z && !(a.dbg & 2)) *reinterpret_cast<f4*>(S.z + row * kCD + 16 * bp + 4 * g) = z;
+          f4 y = z;
+          if ((fl & X2G_CHAIN_SILU) && !(a.dbg & 4)) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) y[e] = silu_f(z[e]);
+          }
+          if (fl & (X2G_CHAIN_RES_HELD | X2G_CHAIN_RES_EXT)) y += held[bp];
+          x[bp] = y;
+        }
+        if (S.y && !(a.dbg & 2)) store_rows(S.y, row, rok, g, x);
+      }
+      if (more) store_w<false>(Ms[buf ^ 1], pre);
+      if (!(a.dbg & 8)) {
+        __syncthreads();  // every wave is past stage s: its image may be overwritten next stage
+        buf ^= 1;
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kCThreads, 1) chain_bwd_kernel(const ChainBwdArgs a) {
+  __shared__ f4 Ms[2][kMChunks];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rl = lane & 15, g = lane >> 4;
+  const int64_t ntiles = (a.R + 15) / 16;
+  const int64_t groups = (ntiles + kCWaves - 1) / kCWaves;
+  const int n = a.n;
+  f4 pre[8];
+  int buf = 0;
+  if (static_cast<int64_t>(blockIdx.x) < groups) {
+    load_w<true>(a.st[n - 1].w, pre);
+    store_w<true>(Ms[0], pre);
+  }
+  __syncthreads();
+  for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+    const int64_t tile = grp * kCWaves + wave;
+    const bool active = tile < ntiles;
+    const int row = static_cast<int>(tile) * 16 + rl;
+    const bool rok = active && row < a.R;
+    const int rc = rok ? row : 0;
+    f4 gcur[8], dh[8], zc[8];
+    load_rows(a.dy, rc, rok, g, gcur);
+    if (a.dy_add) {
+      f4 t[8];
+      load_rows(a.dy_add, rc, rok, g, t);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) gcur[b] += t[b];
+    }
+    if (a.st[n - 1].flags & X2G_CHAIN_SILU) load_rows(a.st[n - 1].z, rc, rok, g, zc);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) dh[b] = zero4();
+    for (int s = n - 1; s >= 0; --s) {
+      const x2g_chain_bwd_stage& S = a.st[s];
+      const int fl = S.flags;
+      const bool more = s > 0 || grp + gridDim.x < groups;
+      if (more) load_w<true>(s > 0 ? a.st[s - 1].w : a.st[n - 1].w, pre);
+      if (active) {
+        if (fl & X2G_CHAIN_RES_HELD) {
+#pragma unroll
+          for (int b = 0; b < 8; ++b) dh[b] += gcur[b];
+        }
+        if ((fl & X2G_CHAIN_RES_EXT) && a.dres) store_rows(a.dres, row, rok, g, gcur);
+        if (fl & X2G_CHAIN_SILU) {  // dz = g * SiLU'(z)
+#pragma unroll
+          for (int b = 0; b < 8; ++b)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) gcur[b][e] *= silu_grad_f(zc[b][e]);
+        }
+        if (S.dz) store_rows(S.dz, row, rok, g, gcur);
+        // the previous stage's z flies during this stage's MFMAs (zc is dead from here)
+        if (s > 0 && (a.st[s - 1].flags & X2G_CHAIN_SILU)) load_rows(a.st[s - 1].z, rc, rok, g, zc);
+        f4 acc[8];
+        chain_gemm(Ms[buf], gcur, acc, rl, g);
+        if (fl & X2G_CHAIN_HOLD) {  // in_s was also the held residual
+#pragma unroll
+          for (int b = 0; b < 8; ++b) {
+            acc[b] += dh[b];
+            dh[b] = zero4();
+          }
+        }
+#pragma unroll
+        for (int b = 0; b < 8; ++b) gcur[b] = acc[b];
+      }
+      if (more) store_w<true>(Ms[buf ^ 1], pre);
+      __syncthreads();
+      buf ^= 1;
+    }
+    if (active) store_rows(a.dx, row, rok, g, gcur);
+  }
+}
+
+// ------------------------------------------------------------------------- v2: rows in LDS
+// The register-tile kernels above give every wave a whole 16-row tile: at E ~ 21k rows that is
+// 1317 tiles on 165 CUs, two per SIMD (a third of the chip idle), and the stage's stores and SiLU
+// run in lock-step on every wave between barriers.  v2 instead gives each workgroup (one per CU,
+// 8 waves) a contiguous range of <= 96 rows (E / 256 ~ 82 rows at config 2: every CU busy, at most
+// 6 16-row blocks each) held in LDS as a swizzled [96][128] image, and each wave a 16-feature
+// slice of every stage's output: wave w computes out[:, 16w .. 16w+15] for all of the range's row
+// blocks, with its slice of the weight in registers (buffer loads from L2, the next stage's while
+// this one runs; no LDS weight image).  MFMA v_mfma_f32_16x16x4_f32 with A = the weight slice,
+// B = image rows (ds_read_b128, conflict-free with the chunk swizzle c ^ (row & 15)), so lane
+// (r, g) of wave w ends with out[row 16rb + r][16w + 4g + e] — written to the other image (the
+// next stage's input) and, for z, straight to global memory; y leaves coalesced, 512-byte rows
+// at a time, from the LDS image after the stage's barrier.  A third image holds the external
+// residual rows.  Backward likewise with the weight slice read transposed (dx = dz W) and dz
+// formed in LDS before the product.
+constexpr int kV2RB = 6;                 // row blocks (16 rows) per workgroup chunk
+constexpr int kV2Img = kV2RB * 16 * 32;  // 16-byte chunks per image (48 KB)
+
+__device__ __forceinline__ int ipos(int r, int c) { return r * 32 + (c ^ (r & 15)); }
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+// buffer descriptor of a wave-uniform base pointer (32-bit per-lane offsets, immediate offsets
+// folded: fewer address registers than 64-bit flat addresses)
+__device__ __forceinline__ rsrc_t rsrc(const float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), static_cast<short>(0), 0x7fffffff, 0x00020000);
+}
+
+__device__ __forceinline__ f4 bload4(rsrc_t r, int voff_bytes, int soff_bytes) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, voff_bytes, soff_bytes, 0));
+}
+
+__device__ __forceinline__ float bload1(rsrc_t r, int voff_bytes, int soff_bytes) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff_bytes, soff_bytes, 0));
+}
+
+// rows [r0, r0 + nrows) of a row-major [R, 128] tensor (+ a second one) -> image (rows >= nrows zero)
+__device__ __forceinline__ void stage_rows(f4* __restrict__ img, const float* __restrict__ P,
+                                           const float* __restrict__ P2, int r0, int nrows) {
+  const int tid = threadIdx.x;
+  f4 v[kV2RB];
+#pragma unroll
+  for (int u = 0; u < kV2RB; ++u) {
+    const int q = tid + kCThreads * u, r = q >> 5, c = q & 31;
+    const bool ok = r < nrows;
+    const int rr = r0 + (ok ? r : 0);
+    v[u] = *reinterpret_cast<const f4*>(P + rr * kCD + 4 * c) * (ok ? 1.0f : 0.0f);
+    if (P2) v[u] += *reinterpret_cast<const f4*>(P2 + rr * kCD + 4 * c) * (ok ? 1.0f : 0.0f);
+  }
+#pragma unroll
+  for (int u = 0; u < kV2RB; ++u) {
+    const int q = tid + kCThreads * u;
+    img[ipos(q >> 5, q & 31)] = v[u];
+  }
+}
+
+// image rows < nrows -> global rows [r0, r0 + nrows), full 512-byte rows per half-wave
+__device__ __forceinline__ void store_img(float* __restrict__ P, const f4* __restrict__ img, int r0, int nrows) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < kV2RB; ++u) {
+    const int q = tid + kCThreads * u, r = q >> 5, c = q & 31;
+    if (r < nrows) *reinterpret_cast<f4*>(P + (r0 + r) * kCD + 4 * c) = img[ipos(r, c)];
+  }
+}
+
+// the wave's weight slice as MFMA A operands: fwd A[b][e] = W[16w + rl][16b + 4g + e];
+// transposed (dx = dz W) A[b][e] = W[16b + 4g + e][16w + rl]
+template <bool TRANS>
+__device__ __forceinline__ void load_slice(const float* W, int w, int rl, int g, f4 (&A)[8]) {
+  const rsrc_t r = rsrc(W);
+  if (!TRANS) {
+    const int vo = 4 * ((16 * w + rl) * kCD + 4 * g);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) A[b] = bload4(r, vo, 64 * b);
+  } else {
+    const int vo = 4 * (4 * g * kCD + 16 * w + rl);
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) A[b][e] = bload1(r, vo, 4 * (16 * b + e) * kCD);
+  }
+}
+
+// acc[rb] = the wave's 16 output features of row block rb: sum over k of A (weight slice) and
+// the image rows; the image chunks of step group b + 1 are read before group b's MFMAs
+__device__ __forceinline__ void slice_gemm(const f4* __restrict__ img, const f4 (&A)[8], f4 (&acc)[kV2RB], int rl,
+                                           int g) {
+#pragma unroll
+  for (int rb = 0; rb < kV2RB; ++rb) acc[rb] = zero4();
+  f4 bo[2][kV2RB];
+#pragma unroll
+  for (int rb = 0; rb < kV2RB; ++rb) bo[0][rb] = img[(16 * rb + rl) * 32 + (g ^ rl)];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const int cur = b & 1;
+    if (b + 1 < 8) {
+#pragma unroll
+      for (int rb = 0; rb < kV2RB; ++rb) bo[cur ^ 1][rb] = img[(16 * rb + rl) * 32 + ((4 * (b + 1) + g) ^ rl)];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int rb = 0; rb < kV2RB; ++rb)
+        acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[b][e], bo[cur][rb][e], acc[rb], 0, 0, 0);
+  }
+}
+
+// Pin prefetched registers: the compiler otherwise sinks the next stage's weight-slice (and z)
+// loads across the stage loop's back edge to their first use, i.e. to the start of the next
+// stage, where their L2 latency is exposed before the first MFMA.  An empty asm that "modifies"
+// the registers at the END of this stage keeps the loads issued here, ahead of this stage's
+// product, and retires them by then.
+template <int N>
+__device__ __forceinline__ void pin(f4 (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
+}
+
+// chunk ch of nch: row blocks [ch * nblk / nch, (ch + 1) * nblk / nch)
+__device__ __forceinline__ void chunk_rows(int64_t ch, int64_t nch, int64_t nblk, int64_t R, int& r0, int& nrows) {
+  const int64_t b0 = ch * nblk / nch, b1 = (ch + 1) * nblk / nch;
+  const int64_t e = b1 * 16 < R ? b1 * 16 : R;
+  r0 = static_cast<int>(b0 * 16);
+  nrows = static_cast<int>(e - b0 * 16);
+}
+
+__global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v2(const ChainFwdArgs a) {
+  __shared__ f4 img[3][kV2Img];  // two ping-pong stage images + the external residual rows
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rl = lane & 15, g = lane >> 4;
+  const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
+  const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
+  const int n = a.n;
+  const int64_t wt_groups = G < 8 ? G : 8;
+  for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
+    int r0, nrows;
+    chunk_rows(ch, nch, nblk, a.R, r0, nrows);
+    __syncthreads();  // the previous chunk's images are no longer read
+    stage_rows(img[0], a.x, nullptr, r0, nrows);
+    if (a.res) stage_rows(img[2], a.res, nullptr, r0, nrows);
+    f4 A[8], held[kV2RB];
+    load_slice<false>(a.st[0].w, w, rl, g, A);
+#pragma unroll
+    for (int rb = 0; rb < kV2RB; ++rb) held[rb] = zero4();
+    int cur = 0;
+    __syncthreads();
+    for (int s = 0; s < n; ++s) {
+      const x2g_chain_stage& S = a.st[s];
+      const int fl = S.flags;
+      f4 An[8];
+      load_slice<false>(a.st[s + 1 < n ? s + 1 : 0].w, w, rl, g, An);
+      const f4 bias = bload4(rsrc(S.b ? S.b : S.w), 4 * (16 * w + 4 * g), 0) * (S.b ? 1.0f : 0.0f);
+      if (S.wt && ch < wt_groups) {  // W^T for the backward from the waves' slices (rows 16b + 4g + e,
+        // cols 16w + rl), the 8 row groups b spread over the first workgroups
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+          if (b % wt_groups == ch)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) S.wt[(16 * b + 4 * g + e) * kCD + 16 * w + rl] = A[b][e];
+      }
+      const f4* in = img[cur];
+      if (fl & (X2G_CHAIN_HOLD | X2G_CHAIN_RES_EXT)) {  // the residual this stage or a later one adds
+        const f4* src = (fl & X2G_CHAIN_HOLD) ? in : img[2];
+#pragma unroll
+        for (int rb = 0; rb < kV2RB; ++rb) held[rb] = src[ipos(16 * rb + rl, 4 * w + g)];
+      }
+      f4 acc[kV2RB];
+      if (!(a.dbg & 16)) {
+        slice_gemm(in, A, acc, rl, g);
+      } else {
+#pragma unroll
+        for (int rb = 0; rb < kV2RB; ++rb) acc[rb] = in[ipos(16 * rb + rl, 4 * w + g)] + A[rb];
+      }
+      f4* out = img[cur ^ 1];
+#pragma unroll
+      for (int rb = 0; rb < kV2RB; ++rb) {
+        const int r = 16 * rb + rl;
+        const f4 z = acc[rb] + bias;
+        if (S.z && r < nrows && !(a.dbg & 2)) *reinterpret_cast<f4*>(S.z + (r0 + r) * kCD + 16 * w + 4 * g) = z;
+        f4 y = z;
+        if ((fl & X2G_CHAIN_SILU) && !(a.dbg & 4)) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) y[e] = silu_fast(z[e]);
+        }
+        if (fl & (X2G_CHAIN_RES_HELD | X2G_CHAIN_RES_EXT)) y += held[rb];
+        out[ipos(r, 4 * w + g)] = y;
+      }
+      pin(An);
+      if (!(a.dbg & 8)) __syncthreads();  // the stage output image is complete and the input image fully read
+      if (S.y && !(a.dbg & 2)) store_img(S.y, out, r0, nrows);
+      cur ^= 1;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) A[b] = An[b];
+    }
+  }
+}
+
+// Backward: img[p] holds dz_s (the product's B operand); the product's output slice is the
+// gradient of out_{s-1} at the wave's 16 features, so stage s-1's elementwise part (held /
+// external residual gradients, dz_{s-1} = g * SiLU'(z_{s-1})) runs on it in registers and writes
+// dz_{s-1} into the other image: one barrier per stage.
+__global__ void __launch_bounds__(kCThreads, 1) chain_bwd_v2(const ChainBwdArgs a) {
+  __shared__ f4 img[2][kV2Img];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rl = lane & 15, g = lane >> 4;
+  const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
+  const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
+  const int n = a.n;
+  const int col = 16 * w + 4 * g;
+  for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
+    int r0, nrows;
+    chunk_rows(ch, nch, nblk, a.R, r0, nrows);
+    f4 A[8], dh[kV2RB], zc[kV2RB], gs[kV2RB];
+    // the stage's saved z at the wave's slice (rows clamped; dy when the stage has no SiLU: unused)
+    auto load_z = [&](int s) {
+      const rsrc_t zr = rsrc((a.st[s].flags & X2G_CHAIN_SILU) ? a.st[s].z : a.dy);
+#pragma unroll
+      for (int rb = 0; rb < kV2RB; ++rb) {
+        const int r = 16 * rb + rl;
+        zc[rb] = bload4(zr, 4 * ((r0 + (r < nrows ? r : 0)) * kCD + col), 0);
+      }
+    };
+    auto load_wslice = [&](int s, f4 (&dst)[8]) {  // W^T rows 16w + rl: contiguous when wt is given
+      if (a.st[s].wt)
+        load_slice<false>(a.st[s].wt, w, rl, g, dst);
+      else
+        load_slice<true>(a.st[s].w, w, rl, g, dst);
+    };
+    load_wslice(n - 1, A);
+    load_z(n - 1);
+    {
+      const rsrc_t yr = rsrc(a.dy), ar = rsrc(a.dy_add ? a.dy_add : a.dy);
+      const float am = a.dy_add ? 1.0f : 0.0f;
+#pragma unroll
+      for (int rb = 0; rb < kV2RB; ++rb) {
+        const int r = 16 * rb + rl;
+        const int vo = 4 * ((r0 + (r < nrows ? r : 0)) * kCD + col);
+        gs[rb] = bload4(yr, vo, 0) + bload4(ar, vo, 0) * am;
+        dh[rb] = zero4();
+      }
+    }
+    int p = 0;
+    __syncthreads();  // the previous chunk's images are no longer read
+    // elementwise part of stage s on the wave's slice g = dL/d out_s: residual gradients, dz
+    auto elementwise = [&](int s) {
+      const x2g_chain_bwd_stage& S = a.st[s];
+      const int fl = S.flags;
+#pragma unroll
+      for (int rb = 0; rb < kV2RB; ++rb) {
+        const int r = 16 * rb + rl;
+        const bool ok = r < nrows;
+        if (fl & X2G_CHAIN_RES_HELD) dh[rb] += gs[rb];
+        if ((fl & X2G_CHAIN_RES_EXT) && a.dres && ok) *reinterpret_cast<f4*>(a.dres + (r0 + r) * kCD + col) = gs[rb];
+        f4 dz = gs[rb];
+        if (fl & X2G_CHAIN_SILU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dz[e] *= silu_grad_fast(zc[rb][e]);
+        }
+        if (S.dz && ok) *reinterpret_cast<f4*>(S.dz + (r0 + r) * kCD + col) = dz;
+        img[p][ipos(r, 4 * w + g)] = dz;
+      }
+    };
+    elementwise(n - 1);
+    __syncthreads();
+    for (int s = n - 1; s >= 0; --s) {
+      f4 An[8];
+      load_wslice(s > 0 ? s - 1 : n - 1, An);
+      load_z(s > 0 ? s - 1 : 0);  // consumed by stage s-1's elementwise part after this product
+      f4 acc[kV2RB];
+      slice_gemm(img[p], A, acc, rl, g);  // dL/d out_{s-1} = dz_s W_s at the wave's slice
+      const bool hold = a.st[s].flags & X2G_CHAIN_HOLD;
+#pragma unroll
+      for (int rb = 0; rb < kV2RB; ++rb) {
+        gs[rb] = acc[rb];
+        if (hold) {  // in_s was also the held residual
+          gs[rb] += dh[rb];
+          dh[rb] = zero4();
+        }
+      }
+      p ^= 1;
+      if (s > 0) {
+        elementwise(s - 1);
+      } else {
+#pragma unroll
+        for (int rb = 0; rb < kV2RB; ++rb) img[p][ipos(16 * rb + rl, 4 * w + g)] = gs[rb];
+      }
+      pin(An);
+      __syncthreads();
+#pragma unroll
+      for (int b = 0; b < 8; ++b) A[b] = An[b];
+    }
+    store_img(a.dx, img[p], r0, nrows);
+  }
+}
+
+// ------------------------------------------------------------------------- batched weight gradients
+// dW_j[n][k] = sum_r dy_j[r][n] x_j[r][k] for up to 8 layers: workgroup (chunk, j) owns a fixed
+// range of rows of layer j; 32-row tiles of dy and x are staged through LDS (double-buffered,
+// next tile in registers during the MFMAs) and wave w accumulates dW rows 32w..32w+31 x all 128
+// columns (4 x v_mfma_f32_32x32x2_f32 accumulators) over the chunk; the chunk's partial goes to
+// its slab, summed later in a fixed order (x2g_slab_sum_batch).
+constexpr int kWThreads = 256;
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct WgradArgs {
+  x2g_wgrad_job job[X2G_CHAIN_MAX_STAGES];
+  float* part_w[X2G_CHAIN_MAX_STAGES];
+  float* part_b[X2G_CHAIN_MAX_STAGES];
+  int64_t R;
+  int chunk_rows;
+};
+
+__device__ __forceinline__ int wswz(int r, int c) { return r * 128 + 4 * ((c >> 2) ^ (r & 15)) + (c & 3); }
+
+__device__ __forceinline__ void wtile_load(const float* __restrict__ P, int64_t r0, int64_t r1, f4 (&v)[4]) {
+  const int tid = threadIdx.x, q = tid & 31;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t r = r0 + (tid >> 5) + 8 * u;
+    const bool ok = r < r1;
+    const int64_t rc = ok ? r : r0;
+    v[u] = *reinterpret_cast<const f4*>(P + rc * kCD + 4 * q) * (ok ? 1.0f : 0.0f);
+  }
+}
+
+__device__ __forceinline__ void wtile_store(float* __restrict__ T, const f4 (&v)[4]) {
+  const int tid = threadIdx.x, q = tid & 31;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int r = (tid >> 5) + 8 * u;
+    *reinterpret_cast<f4*>(T + r * 128 + 4 * (q ^ (r & 15))) = v[u];
+  }
+}
+
+__global__ void __launch_bounds__(kWThreads, 2) wgrad_batched_kernel(const WgradArgs a) {
+  __shared__ __attribute__((aligned(16))) float Ds[2][32 * 128];
+  __shared__ __attribute__((aligned(16))) float Xs[2][32 * 128];
+  const int j = blockIdx.y;
+  const x2g_wgrad_job& J = a.job[j];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, i = lane & 31;
+  const int nb = 32 * wave;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * a.chunk_rows;
+  const int64_t r1 = r0 + a.chunk_rows < a.R ? r0 + a.chunk_rows : a.R;
+  floatx16 acc[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[m][e] = 0.f;
+  float bsum = 0.f;
+  f4 vd[4], vx[4];
+  int buf = 0;
+  if (r0 < r1) {
+    wtile_load(J.dy, r0, r1, vd);
+    wtile_load(J.x, r0, r1, vx);
+  }
+  for (int64_t t = r0; t < r1; t += 32) {
+    wtile_store(Ds[buf], vd);
+    wtile_store(Xs[buf], vx);
+    __syncthreads();
+    if (t + 32 < r1) {  // the next tile's loads fly during the MFMAs
+      wtile_load(J.dy, t + 32, r1, vd);
+      wtile_load(J.x, t + 32, r1, vx);
+    }
+    const float* D = Ds[buf];
+    const float* X = Xs[buf];
+#pragma unroll
+    for (int sg = 0; sg < 2; ++sg) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const int r = 16 * sg + s + 8 * h;
+        const float av = D[wswz(r, nb + i)];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, X[wswz(r, 32 * m + i)], acc[m], 0, 0, 0);
+      }
+    }
+    if (J.db && tid < 128) {
+#pragma unroll 8
+      for (int rr = 0; rr < 32; ++rr) bsum += D[wswz(rr, tid)];
+    }
+    buf ^= 1;  // the other buffer was last read before this tile's barrier
+  }
+  float* slab = a.part_w[j] + static_cast<int64_t>(blockIdx.x) * kCD * kCD;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) slab[(nb + (e & 3) + 8 * (e >> 2) + 4 * h) * kCD + 32 * m + i] = acc[m][e];
+  if (J.db && tid < 128) a.part_b[j][static_cast<int64_t>(blockIdx.x) * kCD + tid] = bsum;
+}
+
+inline bool al16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
+
+// rows per weight-gradient chunk: about two workgroups per CU over all jobs, >= 64 rows
+inline int wgrad_chunk_rows(int64_t R, int jobs) {
+  const int64_t target = 512;
+  const int64_t per_job = (target + jobs - 1) / jobs;
+  int64_t cr = (R + per_job - 1) / per_job;
+  cr = (cr + 31) / 32 * 32;
+  return static_cast<int>(cr < 64 ? 64 : cr);
+}
+
+}  // namespace
+}  // namespace x2g
+
+using namespace x2g;
+
+X2G_API int x2g_chain_fwd(const float* x, const float* res_ext, const x2g_chain_stage* stages, int32_t n_stages,
+                          int64_t rows, int32_t dim, void* stream) {
+  if (!stages || n_stages < 1 || n_stages > X2G_CHAIN_MAX_STAGES || rows < 0 || dim <= 0) return X2G_EINVAL;
+  if (dim != kCD || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  ChainFwdArgs a{};
+  a.x = x;
+  a.res = res_ext;
+  a.R = rows;
+  a.n = n_stages;
+  a.dbg = tuning(kTuneChainDbg);
+  int n_ext = 0, held = 0;
+  for (int s = 0; s < n_stages; ++s) {
+    const x2g_chain_stage& S = stages[s];
+    if (!S.w || (s == n_stages - 1 && !S.y)) return X2G_EINVAL;
+    if (S.flags & ~(X2G_CHAIN_SILU | X2G_CHAIN_HOLD | X2G_CHAIN_RES_HELD | X2G_CHAIN_RES_EXT)) return X2G_EINVAL;
+    // one register set holds the residual: a ResidualLayer input (HOLD .. RES_HELD) must not span
+    // the RES_EXT stage, and a stage adds at most one residual
+    if ((S.flags & X2G_CHAIN_RES_EXT) && (S.flags & (X2G_CHAIN_HOLD | X2G_CHAIN_RES_HELD))) return X2G_EINVAL;
+    if (S.flags & X2G_CHAIN_RES_EXT) held = 0;
+    if (S.flags & X2G_CHAIN_HOLD) held = 1;
+    if ((S.flags & X2G_CHAIN_RES_HELD) && !held) return X2G_EINVAL;
+    if (S.flags & X2G_CHAIN_RES_EXT) ++n_ext;
+    if (!al16(S.w) || !al16(S.b) || !al16(S.z) || !al16(S.y) || !al16(S.wt)) return X2G_EUNSUPPORTED;
+    a.st[s] = S;
+  }
+  if (n_ext > 1 || (n_ext && !res_ext)) return X2G_EINVAL;
+  if (rows == 0) return X2G_OK;
+  if (!x) return X2G_EINVAL;
+  if (!al16(x) || !al16(res_ext)) return X2G_EUNSUPPORTED;
+  hipStream_t st = as_stream(stream);
+  if (tuning(kTuneChain) == 1) {  // register-tile kernel
+    const int64_t groups = ((rows + 15) / 16 + kCWaves - 1) / kCWaves;
+    chain_fwd_kernel<<<static_cast<unsigned>(groups < 256 ? groups : 256), kCThreads, 0, st>>>(a);
+  } else {  // v2: one workgroup per CU, <= 96 rows in LDS
+    const int64_t nblk = (rows + 15) / 16;
+    chain_fwd_v2<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, st>>>(a);
+  }
+  return last_launch_status();
+}
+
+X2G_API int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_bwd_stage* stages, int32_t n_stages,
+                          int64_t rows, int32_t dim, float* dx, float* d_res_ext, void* stream) {
+  if (!stages || n_stages < 1 || n_stages > X2G_CHAIN_MAX_STAGES || rows < 0 || dim <= 0) return X2G_EINVAL;
+  if (dim != kCD || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  ChainBwdArgs a{};
+  a.dy = dy;
+  a.dy_add = dy_add;
+  a.dx = dx;
+  a.dres = d_res_ext;
+  a.R = rows;
+  a.n = n_stages;
+  int n_ext = 0, held = 0;
+  for (int s = 0; s < n_stages; ++s) {
+    const x2g_chain_bwd_stage& S = stages[s];
+    if (!S.w || ((S.flags & X2G_CHAIN_SILU) && !S.z)) return X2G_EINVAL;
+    if (S.flags & ~(X2G_CHAIN_SILU | X2G_CHAIN_HOLD | X2G_CHAIN_RES_HELD | X2G_CHAIN_RES_EXT)) return X2G_EINVAL;
+    if ((S.flags & X2G_CHAIN_RES_EXT) && (S.flags & (X2G_CHAIN_HOLD | X2G_CHAIN_RES_HELD))) return X2G_EINVAL;
+    if (S.flags & X2G_CHAIN_RES_EXT) held = 0;
+    if (S.flags & X2G_CHAIN_HOLD) held = 1;
+    if ((S.flags & X2G_CHAIN_RES_HELD) && !held) return X2G_EINVAL;
+    if (S.flags & X2G_CHAIN_RES_EXT) ++n_ext;
+    if (!al16(S.w) || !al16(S.wt) || !al16(S.z) || !al16(S.dz)) return X2G_EUNSUPPORTED;
+    a.st[s] = S;
+  }
+  if (n_ext > 1) return X2G_EINVAL;
+  if (rows == 0) return X2G_OK;
+  if (!dy || !dx) return X2G_EINVAL;
+  if (!al16(dy) || !al16(dy_add) || !al16(dx) || !al16(d_res_ext)) return X2G_EUNSUPPORTED;
+  hipStream_t st = as_stream(stream);
+  if (tuning(kTuneChain) == 1) {
+    const int64_t groups = ((rows + 15) / 16 + kCWaves - 1) / kCWaves;
+    chain_bwd_kernel<<<static_cast<unsigned>(groups < 256 ? groups : 256), kCThreads, 0, st>>>(a);
+  } else {
+    const int64_t nblk = (rows + 15) / 16;
+    chain_bwd_v2<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, st>>>(a);
+  }
+  return last_launch_status();
+}
+
+X2G_API int32_t x2g_wgrad_batched_splits(int64_t rows, int32_t dim, int32_t num_jobs) {
+  if (rows <= 0 || dim != kCD || num_jobs < 1 || num_jobs > X2G_CHAIN_MAX_STAGES) return 0;
+  const int cr = wgrad_chunk_rows(rows, num_jobs);
+  return static_cast<int32_t>((rows + cr - 1) / cr);
+}
+
+X2G_API size_t x2g_wgrad_batched_workspace(int64_t rows, int32_t dim, int32_t num_jobs) {
+  const int32_t splits = x2g_wgrad_batched_splits(rows, dim, num_jobs);
+  return static_cast<size_t>(num_jobs > 0 ? num_jobs : 0) * splits * (kCD * kCD + kCD) * sizeof(float);
+}
+
+X2G_API int x2g_wgrad_batched(const x2g_wgrad_job* jobs, int32_t num_jobs, int64_t rows, int32_t dim, int flags,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+  if (!jobs || num_jobs < 1 || num_jobs > X2G_CHAIN_MAX_STAGES || rows <= 0 || dim <= 0 ||
+      (flags & ~(X2G_ACCUM_WGRAD | X2G_DEFER_SLAB_SUM)))
+    return X2G_EINVAL;
+  if (dim != kCD || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  const size_t need = x2g_wgrad_batched_workspace(rows, dim, num_jobs);
+  if (!workspace || workspace_bytes < need) return X2G_EWORKSPACE;
+  WgradArgs a{};
+  a.R = rows;
+  a.chunk_rows = wgrad_chunk_rows(rows, num_jobs);
+  const int splits = x2g_wgrad_batched_splits(rows, dim, num_jobs);
+  const size_t per_job = need / num_jobs;
+  x2g_slab_job sj[X2G_CHAIN_MAX_STAGES];
+  for (int j = 0; j < num_jobs; ++j) {
+    const x2g_wgrad_job& J = jobs[j];
+    if (!J.dy || !J.x || !J.dw) return X2G_EINVAL;
+    if (!al16(J.dy) || !al16(J.x)) return X2G_EUNSUPPORTED;
+    a.job[j] = J;
+    a.part_w[j] = reinterpret_cast<float*>(static_cast<char*>(workspace) + per_job * j);
+    a.part_b[j] = a.part_w[j] + static_cast<int64_t>(splits) * kCD * kCD;
+    sj[j] = x2g_slab_job{a.part_w[j], J.db ? a.part_b[j] : nullptr, J.dw, J.db, kCD * kCD, J.db ? kCD : 0, splits};
+  }
+  hipStream_t st = as_stream(stream);
+  wgrad_batched_kernel<<<dim3(static_cast<unsigned>(splits), static_cast<unsigned>(num_jobs)), kWThreads, 0, st>>>(a);
+  const int rc = last_launch_status();
+  if (rc || (flags & X2G_DEFER_SLAB_SUM)) return rc;
+  return x2g_slab_sum_batch(sj, num_jobs, (flags & X2G_ACCUM_WGRAD) ? 1 : 0, stream);
+}

@@ -31,6 +31,8 @@ enum TuneKey {
   kTuneDenseDbg = 3,
   kTuneGateSplits = 4,  // rbf gate backward: workgroup cap (0 = default)
   kTuneFold = 5,        // factorised attention backward: 0 = batched passes, 1 = 3-set pipelined passes
+  kTuneChainDbg = 7,    // row-chain forward ablations for timing (1 no restaging, 2 no stores, 4 no SiLU, 8 no barrier)
+  kTuneChain = 6,       // row chains: 0 = v2 (rows in LDS, one workgroup per CU), 1 = register-tile kernels
   kTuneCount = 16
 };
 int tuning(int key);

@@ -1630,21 +1630,27 @@ X2G_API int x2g_dense_fwd(const float* x, const float* w, const float* b, int64_
   return last_launch_status();
 }
 
+// dx (+)= (dy * act'(z)) w for any shape; dx_add (optional, may alias dx) is added in the epilogue,
+// where every element is read and then written by the same thread
+static int dense_bwd_data_impl(const float* dy, const float* z, int act, const float* w, int64_t R, int32_t K,
+                               int32_t N, float* dx, const float* dx_add, float* dz, hipStream_t st) {
+  // as a row GEMM: A = dY' [R, N] (contraction over N), B[k'=n][n'=k] = w[n][k] (row-major, no transpose)
+  dim3 grid(static_cast<unsigned>((R + kDenseRows - 1) / kDenseRows), (K + kDenseCols - 1) / kDenseCols);
+  if (act == kActSilu)
+    dense_rows<false, kActSilu><<<grid, 256, 0, st>>>(dy, w, nullptr, dx_add, z, R, N, K, kActNone, dx, nullptr, dz);
+  else
+    dense_rows<false, kActNone><<<grid, 256, 0, st>>>(dy, w, nullptr, dx_add, nullptr, R, N, K, kActNone, dx, nullptr,
+                                                       dz);
+  return last_launch_status();
+}
+
 X2G_API int x2g_dense_bwd_data(const float* dy, const float* z, int act, const float* w, int64_t R, int32_t K,
                                int32_t N, float* dx, float* dz, void* stream) {
   // dy, z: [R, N]; w: [N, K]; dx: [R, K]; dz (optional, [R, N]) receives dy * act'(z)
   if (R < 0 || K <= 0 || N <= 0 || (act != kActNone && act != kActSilu)) return X2G_EINVAL;
   if (R == 0) return X2G_OK;
   if (!dy || !w || !dx || (act == kActSilu && !z)) return X2G_EINVAL;
-  // as a row GEMM: A = dY' [R, N] (contraction over N), B[k'=n][n'=k] = w[n][k] (row-major, no transpose)
-  dim3 grid(static_cast<unsigned>((R + kDenseRows - 1) / kDenseRows), (K + kDenseCols - 1) / kDenseCols);
-  if (act == kActSilu)
-    dense_rows<false, kActSilu><<<grid, 256, 0, as_stream(stream)>>>(dy, w, nullptr, nullptr, z, R, N, K, kActNone,
-                                                                      dx, nullptr, dz);
-  else
-    dense_rows<false, kActNone><<<grid, 256, 0, as_stream(stream)>>>(dy, w, nullptr, nullptr, nullptr, R, N, K,
-                                                                      kActNone, dx, nullptr, dz);
-  return last_launch_status();
+  return dense_bwd_data_impl(dy, z, act, w, R, K, N, dx, nullptr, dz, as_stream(stream));
 }
 
 namespace x2g {  // slab sums come from linear.hip
@@ -1744,8 +1750,7 @@ X2G_API int x2g_dense_bwd_ex(const float* dy, const float* z, int act, const flo
     if (flags & X2G_DEFER_SLAB_SUM) return X2G_OK;
     return sum_slabs_launch(part_w, static_cast<int64_t>(N) * K, part_b, N, grid, dw, db, accum, st);
   }
-  // general shapes: dz = dy * act'(z) and dx = dz w in one kernel, then the weight gradient
-  if (dx_add) return X2G_EUNSUPPORTED;
+  // general shapes: dz = dy * act'(z) and dx = dz w (+ dx_add) in one kernel, then the weight gradient
   float* dzbuf = static_cast<float*>(workspace);
   const size_t dz_bytes = ((static_cast<size_t>(R) * N * sizeof(float)) + 255) / 256 * 256;
   const float* dzp = dy;
@@ -1753,7 +1758,8 @@ X2G_API int x2g_dense_bwd_ex(const float* dy, const float* z, int act, const flo
   if (act != kActNone || dx) {
     float* dx_tmp = dx;
     if (!dx_tmp) return X2G_EUNSUPPORTED;  // general path needs a dx buffer when an activation is fused
-    if ((rc = x2g_dense_bwd_data(dy, z, act, w, R, K, N, dx_tmp, act != kActNone ? dzbuf : nullptr, stream))) return rc;
+    if ((rc = dense_bwd_data_impl(dy, z, act, w, R, K, N, dx_tmp, dx_add, act != kActNone ? dzbuf : nullptr, st)))
+      return rc;
     if (act != kActNone) dzp = dzbuf;
   }
   return x2g_linear_wgrad_ex(dzp, x, R, N, K, dw, db, flags, static_cast<char*>(workspace) + dz_bytes,

@@ -121,9 +121,7 @@ class _Trunk(nn.Module):
             out = self.convs[i](sbf=data.edge_sbf, rbf=data.node_rbf, x=out, edge_index=data._store.get("edge_index"),
                                 edge_attr=edge_attr, line_graph=plan.lg, edge_row=edge_row)
             out = self.LayerNorm(out, rowptr=plan.line_ptr, num_graphs=plan.num_graphs)
-            out = self.bf_skip[i](out)
-            out = self.dense_bf_skip[i].fused(out, act=ops.ACT_SILU, res=res0)  # SiLU(dense(out)) + res0
-            out = self.af_skip[i](out)
+            out = self._tail(i, out, res0)
             readout(i + 1, out)
         if side is not None:
             main.wait_stream(side)
@@ -136,6 +134,21 @@ class _Trunk(nn.Module):
                 r = run_mlp(m, f)
                 results = r if results is None else results + r
         return results
+
+
+    def _tail(self, i, out, res0):
+        """bf_skip -> SiLU(dense_bf_skip(.)) + res0 -> af_skip (model.py:47-50): one row-chain
+        kernel each way (ops.row_chain, 7 Linear stages) where compiled, else layer by layer."""
+        lins = [self.bf_skip[i].lin0, self.bf_skip[i].lin1, self.dense_bf_skip[i]]
+        for r in self.af_skip[i]:
+            lins += [r.lin0, r.lin1]
+        if ops._CHAIN and ops.chain_supported(out, lins):
+            S, H, RH, RE = ops.CHAIN_SILU, ops.CHAIN_HOLD, ops.CHAIN_RES_HELD, ops.CHAIN_RES_EXT
+            flags = [S | H, S | RH, S | RE, S | H, S | RH, S | H, S | RH]
+            return ops.row_chain(out, res0, lins, flags)
+        out = self.bf_skip[i](out)
+        out = self.dense_bf_skip[i].fused(out, act=ops.ACT_SILU, res=res0)  # SiLU(dense(out)) + res0
+        return self.af_skip[i](out)
 
 
 class SBFTransformer(_Trunk):

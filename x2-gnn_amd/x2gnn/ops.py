@@ -799,6 +799,133 @@ def residual_layer(x, w0, b0, w1, b1):
     return _ResidualFn.apply(x, w0, b0, w1, b1)
 
 
+CHAIN_SILU, CHAIN_HOLD, CHAIN_RES_HELD, CHAIN_RES_EXT = 1, 2, 4, 8  # X2G_CHAIN_* (include/x2g.h)
+CHAIN_MAX_STAGES = 8
+
+
+class ChainStage(ctypes.Structure):
+    """x2g_chain_stage."""
+    _fields_ = [("w", ctypes.c_void_p), ("b", ctypes.c_void_p), ("z", ctypes.c_void_p), ("y", ctypes.c_void_p),
+                ("wt", ctypes.c_void_p), ("flags", ctypes.c_int32)]
+
+
+class ChainBwdStage(ctypes.Structure):
+    """x2g_chain_bwd_stage."""
+    _fields_ = [("w", ctypes.c_void_p), ("wt", ctypes.c_void_p), ("z", ctypes.c_void_p), ("dz", ctypes.c_void_p),
+                ("flags", ctypes.c_int32)]
+
+
+class WgradJob(ctypes.Structure):
+    """x2g_wgrad_job."""
+    _fields_ = [("dy", ctypes.c_void_p), ("x", ctypes.c_void_p), ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p)]
+
+
+def wgrad_batched(dys, xs, weights, biases):
+    """Weight / bias gradients of several D x D Linear layers over the same rows in one launch
+    (x2g_wgrad_batched): dW_g = dy_g^T x_g, db_g = colsum(dy_g).  Summed straight into the
+    gradient bucket when every parameter is bucket-backed (returns Nones for them then), slab sums
+    deferred inside ``deferred_wgrad()``; otherwise returns fresh (dW, db) per layer."""
+    G = len(dys)
+    R, D = dys[0].shape
+    dev = dys[0].device
+    params = list(weights) + [b for b in biases if b is not None]
+    bufs, acc = _wgrad_targets(params, [tuple(p.shape) for p in params], dev)
+    dws, rest = bufs[:G], iter(bufs[G:])
+    dbs = [next(rest) if b is not None else None for b in biases]
+    lib = _lib.load()
+    ws_bytes = int(lib.x2g_wgrad_batched_workspace(R, D, G))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    jobs = (WgradJob * G)(*[WgradJob(_dp(dys[g]), _dp(xs[g]), _dp(dws[g]), _dp(dbs[g])) for g in range(G)])
+    defer = acc and _DEFER is not None
+    call("x2g_wgrad_batched", jobs, G, R, D, (ACCUM_WGRAD if acc else 0) | (DEFER_SLAB_SUM if defer else 0), ptr(ws),
+         ws_bytes, stream_ptr())
+    if defer:
+        splits = int(lib.x2g_wgrad_batched_splits(R, D, G))
+        per = ws_bytes // G
+        for g in range(G):
+            _defer_job(ws, g * per, splits, D * D, D, dws[g], dbs[g])
+    if acc:
+        return [None] * G, [None] * G
+    return dws, dbs
+
+
+class _ChainFn(torch.autograd.Function):
+    """A chain of D x D Linear stages on the same rows in ONE kernel (x2g_chain_fwd, csrc/chain.hip):
+    stage s computes z_s = in_s W_s^T + b_s, out_s = act(z_s) (+ the held ResidualLayer input or
+    the external residual), in_{s+1} = out_s.  Backward: one kernel for every stage's data gradient
+    (x2g_chain_bwd, residual gradients folded in registers) + one batched weight-gradient launch."""
+
+    @staticmethod
+    def forward(ctx, x, res, flags, *params):
+        n = len(flags)
+        ws, bs = params[0::2], params[1::2]
+        x2 = _f32(x)
+        R, D = x2.shape
+        r2 = _f32(res) if res is not None else None
+        f32 = dict(dtype=torch.float32, device=x2.device)
+        zs = [torch.empty(R, D, **f32) if flags[i] & CHAIN_SILU else None for i in range(n)]
+        ys = [torch.empty(R, D, **f32) for _ in range(n)]
+        W = [_f32(w) for w in ws]
+        B = [_f32(b) if b is not None else None for b in bs]
+        # W^T of every stage (written by the forward kernel) for the backward's data gradient
+        WT = torch.empty(n, D, D, **f32) if torch.is_grad_enabled() else None
+        st = (ChainStage * n)(*[ChainStage(_dp(W[i]), _dp(B[i]), _dp(zs[i]), _dp(ys[i]),
+                                           None if WT is None else WT[i].data_ptr(), flags[i]) for i in range(n)])
+        call("x2g_chain_fwd", ptr(x2), ptr(r2), st, n, R, D, stream_ptr())
+        ins = [x2] + ys[:-1]
+        ctx.save_for_backward(*W, *[z if z is not None else x2 for z in zs], *ins, WT)
+        ctx.flags, ctx.params, ctx.has_res = tuple(flags), params, res is not None
+        return ys[-1]
+
+    @staticmethod
+    def backward(ctx, gy):
+        flags = ctx.flags
+        n = len(flags)
+        saved = ctx.saved_tensors
+        W, zs, ins, WT = saved[:n], saved[n:2 * n], saved[2 * n:3 * n], saved[3 * n]
+        gy2 = _f32(gy)
+        R, D = gy2.shape
+        f32 = dict(dtype=torch.float32, device=gy2.device)
+        dzs = [torch.empty(R, D, **f32) for _ in range(n)]
+        dx = torch.empty(R, D, **f32)
+        dres = torch.empty(R, D, **f32) if ctx.has_res else None
+        st = (ChainBwdStage * n)(*[ChainBwdStage(_dp(W[i]), None if WT is None else WT[i].data_ptr(),
+                                                 _dp(zs[i]) if flags[i] & CHAIN_SILU else None, _dp(dzs[i]), flags[i])
+                                   for i in range(n)])
+        call("x2g_chain_bwd", ptr(gy2), None, st, n, R, D, ptr(dx), ptr(dres), stream_ptr())
+        ws, bs = ctx.params[0::2], ctx.params[1::2]
+        dws, dbs = wgrad_batched(dzs, list(ins), ws, bs)
+        grads = []
+        for i in range(n):
+            grads += [None if dws[i] is None else dws[i], None if dbs[i] is None else dbs[i]]
+        return (dx, dres, None, *grads)
+
+
+def chain_supported(x, linears):
+    """True when _ChainFn's kernels cover these layers (D = 128 rows of 16-byte aligned fp32)."""
+    if not x.is_cuda or x.dim() != 2 or x.shape[1] != 128 or x.shape[0] * 128 >= 2 ** 31:
+        return False
+    if len(linears) < 1 or len(linears) > CHAIN_MAX_STAGES:
+        return False
+    for m in linears:
+        if tuple(m.weight.shape) != (128, 128) or m.weight.dtype != torch.float32 or m.weight.data_ptr() % 16:
+            return False
+        if m.bias is not None and m.bias.data_ptr() % 16:
+            return False
+    return True
+
+
+_CHAIN = os.environ.get("X2G_CHAIN", "1") == "1"
+
+
+def row_chain(x, res, linears, flags):
+    """Apply the chain of ``linears`` (nn.Linear modules, D x D) with per-stage X2G_CHAIN_* flags."""
+    params = []
+    for m in linears:
+        params += [m.weight, m.bias]
+    return _ChainFn.apply(x, res, tuple(flags), *params)
+
+
 class _ConvProjFn(torch.autograd.Function):
     """The dense projections of SBFTransformerConv.forward (sbftransformer_conv.py:99-107,127):
     rf = lin_rbf(rbf), x_src = x * rf, q = lin_query(x), k = lin_key(x_src), v = lin_value(x_src),
