@@ -465,9 +465,15 @@ typedef struct {
   int32_t flags;
 } x2g_chain_stage;
 
-/* Forward of a chain of n_stages (1..X2G_CHAIN_MAX_STAGES) stages on x [rows, dim]. */
+/* Forward of a chain of n_stages (1..X2G_CHAIN_MAX_STAGES) stages on x [rows, dim].
+ * in_t (optional): every stage's input (x, then each stage's output) in the tiled-transposed layout
+ * below, stage s at in_t + s * x2g_chain_t_floats(rows, dim) — the operand x2g_chain_wgrad reads. */
 int x2g_chain_fwd(const float* x, const float* res_ext, const x2g_chain_stage* stages, int32_t n_stages,
-                  int64_t rows, int32_t dim, void* stream);
+                  int64_t rows, int32_t dim, float* in_t, void* stream);
+
+/* Tiled-transposed ("T") layout of a [rows, D] tensor: 16-row tiles; tile t holds element (r, f)
+ * at t*16*D + f*16 + (r - 16t), rows past `rows` in the last tile zero.  Floats per tensor: */
+int64_t x2g_chain_t_floats(int64_t rows, int32_t dim);
 
 typedef struct {
   const float* w; /* [D, D] the stage's weight */
@@ -478,10 +484,22 @@ typedef struct {
 } x2g_chain_bwd_stage;
 
 /* Data gradients of x2g_chain_fwd: dy (+ dy_add, may be NULL) = dL/d out_{n-1}; writes every
- * stage's dz, dx = dL/dx and d_res_ext = dL/d res_ext (NULL when no stage has RES_EXT).
- * Weight gradients: x2g_wgrad_batched over (dz_s, in_s) pairs. */
+ * stage's dz (row-major where the stage's dz is set; T layout at dz_t + s * x2g_chain_t_floats when
+ * dz_t is set), dx = dL/dx and d_res_ext = dL/d res_ext (NULL when no stage has RES_EXT).
+ * Weight gradients: x2g_chain_wgrad over (in_t, dz_t), or x2g_wgrad_batched over row-major pairs. */
 int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_bwd_stage* stages, int32_t n_stages,
-                  int64_t rows, int32_t dim, float* dx, float* d_res_ext, void* stream);
+                  int64_t rows, int32_t dim, float* dx, float* d_res_ext, float* dz_t, void* stream);
+
+/* Weight / bias gradients of every chain stage: dw[s] = dz_s^T in_s, db[s] = colsum(dz_s) (db[s] may
+ * be NULL) from the T-layout operands of x2g_chain_fwd / x2g_chain_bwd; dw / db are host arrays of
+ * n_stages device pointers.  Rows are split into fixed tile ranges per stage, the partials summed
+ * in a fixed order; flags and slab layout as x2g_wgrad_batched (stage s's slabs at byte
+ * s * (workspace / n_stages)). */
+size_t x2g_chain_wgrad_workspace(int64_t rows, int32_t dim, int32_t n_stages);
+int32_t x2g_chain_wgrad_splits(int64_t rows, int32_t dim, int32_t n_stages);
+int x2g_chain_wgrad(const float* in_t, const float* dz_t, int32_t n_stages, int64_t rows, int32_t dim,
+                    float* const* dw, float* const* db, int flags, void* workspace, size_t workspace_bytes,
+                    void* stream);
 
 /* Weight / bias gradients of up to X2G_CHAIN_MAX_STAGES independent D x D Linear layers over the
  * same rows: dw_g = dy_g^T x_g, db_g = column sums of dy_g (db_g may be NULL).  Rows are split

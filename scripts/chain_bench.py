@@ -1,5 +1,6 @@
 """Row-chain kernels at config-2 size (E = 21,058 rows): time per launch of x2g_chain_fwd /
 x2g_chain_bwd / x2g_wgrad_batched for 1..7 stages and both kernel variants (x2g_tuning key 6)."""
+import ctypes
 import os
 import sys
 
@@ -49,12 +50,27 @@ for knob in (0, 1):
         flags = TRUNK[:n] if n != 1 else [S]
         if n == 2:
             flags = [S | H, S | RH]
-        st = (ops.ChainStage * n)(*[ops.ChainStage(W[i].data_ptr(), B[i].data_ptr(), Z[i].data_ptr(), Y[i].data_ptr(),
+        # as the model runs it (ops._ChainFn): v2 keeps the stage inputs / dz in the T layout only
+        t_only = knob == 0
+        st = (ops.ChainStage * n)(*[ops.ChainStage(W[i].data_ptr(), B[i].data_ptr(), Z[i].data_ptr(),
+                                                   Y[i].data_ptr() if (i == n - 1 or not t_only) else None,
                                                    WT[i].data_ptr(), flags[i]) for i in range(n)])
-        bst = (ops.ChainBwdStage * n)(*[ops.ChainBwdStage(W[i].data_ptr(), WT[i].data_ptr() if knob == 0 else None,
-                                                          Z[i].data_ptr(), DZ[i].data_ptr(), flags[i]) for i in range(n)])
-        f = t(lambda: lib.x2g_chain_fwd(ptr(x), ptr(res), st, n, R, D, stream_ptr()))
-        b = t(lambda: lib.x2g_chain_bwd(ptr(dy), None, bst, n, R, D, ptr(dx), ptr(dres), stream_ptr()))
+        bst = (ops.ChainBwdStage * n)(*[ops.ChainBwdStage(W[i].data_ptr(), WT[i].data_ptr() if t_only else None,
+                                                          Z[i].data_ptr(), None if t_only else DZ[i].data_ptr(),
+                                                          flags[i]) for i in range(n)])
+        tf = int(lib.x2g_chain_t_floats(R, D))
+        in_t = torch.empty(n, tf, device=dev) if knob == 0 else None
+        dz_t = torch.empty(n, tf, device=dev) if knob == 0 else None
+        f = t(lambda: lib.x2g_chain_fwd(ptr(x), ptr(res), st, n, R, D, ptr(in_t), stream_ptr()))
+        b = t(lambda: lib.x2g_chain_bwd(ptr(dy), None, bst, n, R, D, ptr(dx), ptr(dres), ptr(dz_t), stream_ptr()))
+        if knob == 0:
+            wsz = int(lib.x2g_chain_wgrad_workspace(R, D, n))
+            wsb = torch.empty(wsz, dtype=torch.uint8, device=dev)
+            dwa = (ctypes.c_void_p * n)(*[DW[i].data_ptr() for i in range(n)])
+            dba = (ctypes.c_void_p * n)(*[DB[i].data_ptr() for i in range(n)])
+            cw = t(lambda: lib.x2g_chain_wgrad(ptr(in_t), ptr(dz_t), n, R, D, dwa, dba, 2, ptr(wsb), wsz, stream_ptr()))
+            print(f"  chain_wgrad stages {n}: {cw:7.1f} us deferred ({2 * R * D * D * n / cw / 1e6:5.1f} TF/s), "
+                  f"splits {lib.x2g_chain_wgrad_splits(R, D, n)}", flush=True)
         print(f"knob {knob} stages {n}: fwd {f:7.1f} us ({f / n:5.1f}/stage, {2 * R * D * D * n / f / 1e6:5.1f} TF/s)  "
               f"bwd-data {b:7.1f} us ({b / n:5.1f}/stage)", flush=True)
 lib.x2g_tuning(6, 0)
@@ -74,6 +90,6 @@ st = (ops.ChainStage * n)(*[ops.ChainStage(W[i].data_ptr(), B[i].data_ptr(), Z[i
                                            TRUNK[i]) for i in range(n)])
 for dbg in (0, 2, 4, 8, 2 | 4 | 8, 16, 2 | 16, 2 | 4 | 8 | 16):
     lib.x2g_tuning(7, dbg)
-    f = t(lambda: lib.x2g_chain_fwd(ptr(x), ptr(res), st, n, R, D, stream_ptr()))
+    f = t(lambda: lib.x2g_chain_fwd(ptr(x), ptr(res), st, n, R, D, None, stream_ptr()))
     print(f"ablation {dbg:2d}: fwd {f:7.1f} us ({f / n:5.1f}/stage)", flush=True)
 lib.x2g_tuning(7, 0)

@@ -830,7 +830,7 @@ def test_row_chain_rejects_bad_programs(cuda):
     def run(flags, dim=128):
         st = (ops.ChainStage * len(flags))(*[ops.ChainStage(w.data_ptr(), None, None, ys[i].data_ptr(), None, f)
                                               for i, f in enumerate(flags)])
-        return lib.x2g_chain_fwd(ptr(x), ptr(x), st, len(flags), R, dim, stream_ptr())
+        return lib.x2g_chain_fwd(ptr(x), ptr(x), st, len(flags), R, dim, None, stream_ptr())
 
     assert run([S | RH]) != 0
     assert run([S | RE, S | RE]) != 0
@@ -891,7 +891,7 @@ def test_row_chain_bwd_with_and_without_transposed_weights(cuda, R):
     WT = torch.empty(n, 128, 128, device=cuda)
     st = (ops.ChainStage * n)(*[ops.ChainStage(W[i].data_ptr(), B[i].data_ptr(), Z[i].data_ptr(), Y[i].data_ptr(),
                                                WT[i].data_ptr(), flags[i]) for i in range(n)])
-    call("x2g_chain_fwd", ptr(x), ptr(res), st, n, R, 128, stream_ptr())
+    call("x2g_chain_fwd", ptr(x), ptr(res), st, n, R, 128, None, stream_ptr())
     dy = torch.randn(R, 128, device=cuda, generator=g)
     outs = []
     for use_wt in (True, False):
@@ -899,7 +899,7 @@ def test_row_chain_bwd_with_and_without_transposed_weights(cuda, R):
         dx, dres = torch.empty(R, 128, device=cuda), torch.empty(R, 128, device=cuda)
         bst = (ops.ChainBwdStage * n)(*[ops.ChainBwdStage(W[i].data_ptr(), WT[i].data_ptr() if use_wt else None,
                                                           Z[i].data_ptr(), DZ[i].data_ptr(), flags[i]) for i in range(n)])
-        call("x2g_chain_bwd", ptr(dy), None, bst, n, R, 128, ptr(dx), ptr(dres), stream_ptr())
+        call("x2g_chain_bwd", ptr(dy), None, bst, n, R, 128, ptr(dx), ptr(dres), None, stream_ptr())
         outs.append((dx, dres, DZ))
     torch.cuda.synchronize()
     for i in range(n):

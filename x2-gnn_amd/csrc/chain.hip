@@ -39,6 +39,8 @@ constexpr int kMChunks = kCD * kCD / 4;  // 16-byte chunks per weight image (64 
 struct ChainFwdArgs {
   const float* x;
   const float* res;
+  float* in_t;    // T-layout stage inputs for the weight gradient (or NULL)
+  int64_t tf;     // floats per T-layout tensor
   int64_t R;
   int n;
   int dbg;  // diagnostic ablations (x2g_tuning key 7 bits, timing only: results are wrong when set)
@@ -50,6 +52,8 @@ struct ChainBwdArgs {
   const float* dy_add;
   float* dx;
   float* dres;
+  float* dz_t;    // T-layout dz per stage (or NULL)
+  int64_t tf;
   int64_t R;
   int n;
   x2g_chain_bwd_stage st[X2G_CHAIN_MAX_STAGES];
@@ -350,6 +354,48 @@ __device__ __forceinline__ void store_img(float* __restrict__ P, const f4* __res
   }
 }
 
+// 4 x 4 transpose inside each lane quad (lanes 4m..4m+3 of a 16-lane row group, DPP quad
+// permutes, no LDS): lane 4m + j holding (row 4m + j, features 0..3) ends with (feature j, rows
+// 4m..4m+3) — a 16-byte run of the tiled-transposed layout.
+__device__ __forceinline__ float dpp_xor1(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_xor2(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+}
+__device__ __forceinline__ f4 quad_transpose(f4 v, int j) {
+  f4 b, c;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float t = dpp_xor1(v[k ^ 1]);
+    b[k] = ((k ^ j) & 1) ? t : v[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float t = dpp_xor2(b[k ^ 2]);
+    c[k] = ((k ^ j) & 2) ? t : b[k];
+  }
+  return c;
+}
+
+// The wave's row-layout slice v[rb] (lane (rl, g): rows 16rb + rl, features 16w + 4g + e) -> the
+// T layout (tile t of the chunk at dst + (r0/16 + t) * 2048, element (r, f) at f * 16 + r % 16),
+// rows >= nrows written as zero; a wave's store is 1 KB contiguous (16 features x 16 rows).
+__device__ __forceinline__ void store_t_slice(float* __restrict__ dst, const f4 (&v)[kV2RB], int r0, int nrows, int w,
+                                              int rl, int g) {
+  const int j = rl & 3, m = rl >> 2, f = 16 * w + 4 * g + j;
+  const int ntile = (nrows + 15) >> 4;
+#pragma unroll
+  for (int rb = 0; rb < kV2RB; ++rb) {
+    f4 t = quad_transpose(v[rb], j);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (16 * rb + 4 * m + e >= nrows) t[e] = 0.0f;
+    if (rb < ntile)
+      *reinterpret_cast<f4*>(dst + (static_cast<int64_t>(r0 >> 4) + rb) * (16 * kCD) + f * 16 + 4 * m) = t;
+  }
+}
+
 // the wave's weight slice as MFMA A operands: fwd A[b][e] = W[16w + rl][16b + 4g + e];
 // transposed (dx = dz W) A[b][e] = W[16b + 4g + e][16w + rl]
 template <bool TRANS>
@@ -431,6 +477,12 @@ __global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v2(const ChainFwdArgs 
     for (int rb = 0; rb < kV2RB; ++rb) held[rb] = zero4();
     int cur = 0;
     __syncthreads();
+    if (a.in_t) {  // the chain input's T copy (later stage inputs: from the stage epilogues)
+      f4 xs[kV2RB];
+#pragma unroll
+      for (int rb = 0; rb < kV2RB; ++rb) xs[rb] = img[0][ipos(16 * rb + rl, 4 * w + g)];
+      store_t_slice(a.in_t, xs, r0, nrows, w, rl, g);
+    }
     for (int s = 0; s < n; ++s) {
       const x2g_chain_stage& S = a.st[s];
       const int fl = S.flags;
@@ -471,7 +523,9 @@ __global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v2(const ChainFwdArgs 
         }
         if (fl & (X2G_CHAIN_RES_HELD | X2G_CHAIN_RES_EXT)) y += held[rb];
         out[ipos(r, 4 * w + g)] = y;
+        acc[rb] = y;
       }
+      if (a.in_t && s + 1 < n) store_t_slice(a.in_t + (s + 1) * a.tf, acc, r0, nrows, w, rl, g);
       pin(An);
       if (!(a.dbg & 8)) __syncthreads();  // the stage output image is complete and the input image fully read
       if (S.y && !(a.dbg & 2)) store_img(S.y, out, r0, nrows);
@@ -545,7 +599,9 @@ __global__ void __launch_bounds__(kCThreads, 1) chain_bwd_v2(const ChainBwdArgs 
         }
         if (S.dz && ok) *reinterpret_cast<f4*>(S.dz + (r0 + r) * kCD + col) = dz;
         img[p][ipos(r, 4 * w + g)] = dz;
+        gs[rb] = dz;
       }
+      if (a.dz_t) store_t_slice(a.dz_t + s * a.tf, gs, r0, nrows, w, rl, g);
     };
     elementwise(n - 1);
     __syncthreads();
@@ -674,6 +730,108 @@ __global__ void __launch_bounds__(kWThreads, 2) wgrad_batched_kernel(const Wgrad
   if (J.db && tid < 128) a.part_b[j][static_cast<int64_t>(blockIdx.x) * kCD + tid] = bsum;
 }
 
+// ---------------------------------------------------------------- chain weight gradients (T layout)
+// dW_s = dz_s^T in_s over all rows: workgroup (c, s) owns a fixed range of 16-row tiles of stage s.
+// Two T tiles (32 rows) per step are copied into LDS as-is (8 KB each, double-buffered, the next
+// pair in registers during the MFMAs), so both MFMA operands come as ds_read_b128 of 4 consecutive
+// rows of one feature: wave w accumulates dW rows 16w..16w+15 x all 128 columns (8 blocks of
+// v_mfma_f32_16x16x4_f32).  Image position of (feature f, row quad q): f * 4 + (q ^ sigma(f)),
+// sigma(f) = 3 * ((f >> 3) & 1): conflict-free in every ds_read_b128 lane group.
+constexpr int kWTiles = 2;  // T tiles per step
+
+__device__ __forceinline__ int tpos(int f, int q) { return f * 4 + (q ^ (((f >> 3) & 1) * 3)); }
+
+struct ChainWgradArgs {
+  const float* in_t;
+  const float* dz_t;
+  int64_t tf;
+  int64_t ntiles;
+  float* part_w[X2G_CHAIN_MAX_STAGES];
+  float* part_b[X2G_CHAIN_MAX_STAGES];
+  int has_b[X2G_CHAIN_MAX_STAGES];
+  int splits;
+};
+
+// Three LDS buffers, filled by global_load_lds (no registers: each wave's instruction lands 1 KB
+// lane-linearly, the swizzle applied to the source addresses), two steps in flight ahead of the
+// product; raw s_barrier with counted vmcnt waits so the in-flight copies survive the barriers.
+__global__ void __launch_bounds__(kCThreads, 1) chain_wgrad_kernel(const ChainWgradArgs a) {
+  __shared__ f4 Ds[3][kWTiles][512];
+  __shared__ f4 Xs[3][kWTiles][512];
+  const int s = blockIdx.y, c = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rl = lane & 15, g = lane >> 4;
+  const int64_t t0 = c * a.ntiles / a.splits, t1 = (c + 1) * a.ntiles / a.splits;
+  const int nsteps = static_cast<int>((t1 - t0 + kWTiles - 1) / kWTiles);
+  const float* dz = a.dz_t + s * a.tf;
+  const float* xin = a.in_t + s * a.tf;
+  // LDS position P = 64w + lane of a tile image holds source chunk (P >> 2) * 4 + ((P & 3) ^ sigma)
+  const int P = 64 * w + lane;
+  const int src_chunk = (P >> 2) * 4 + ((P & 3) ^ (((P >> 5) & 1) * 3));
+  auto issue = [&](int step) {  // the step's tiles into buffer step % 3 (tiles past t1: tile t0)
+    const int b = step % 3;
+#pragma unroll
+    for (int k = 0; k < kWTiles; ++k) {
+      int64_t t = t0 + static_cast<int64_t>(step) * kWTiles + k;
+      t = t < t1 ? t : t0;
+      __builtin_amdgcn_global_load_lds(dz + t * 2048 + 4 * src_chunk, &Ds[b][k][64 * w], 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(xin + t * 2048 + 4 * src_chunk, &Xs[b][k][64 * w], 16, 0, 0);
+    }
+  };
+  f4 acc[8];
+#pragma unroll
+  for (int bk = 0; bk < 8; ++bk) acc[bk] = zero4();
+  float bsum = 0.f;
+  if (nsteps > 0) issue(0);
+  if (nsteps > 1) issue(1);
+  for (int i = 0; i < nsteps; ++i) {
+    // this step's copies are done when at most the next step's 2 * kWTiles remain in flight
+    if (i + 1 < nsteps)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's copies of this step have landed; step i-1 is read
+    if (i + 2 < nsteps) issue(i + 2);
+    const int b = i % 3;
+#pragma unroll
+    for (int k = 0; k < kWTiles; ++k) {
+      if (t0 + static_cast<int64_t>(i) * kWTiles + k >= t1) break;  // wave-uniform
+      const f4 av = Ds[b][k][tpos(16 * w + rl, g)];
+      f4 bv[8];
+#pragma unroll
+      for (int bk = 0; bk < 8; ++bk) bv[bk] = Xs[b][k][tpos(16 * bk + rl, g)];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int bk = 0; bk < 8; ++bk) acc[bk] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[bk][e], acc[bk], 0, 0, 0);
+      if (tid < 128) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f4 v = Ds[b][k][tpos(tid, q)];
+          bsum += (v[0] + v[1]) + (v[2] + v[3]);
+        }
+      }
+    }
+  }
+  // slab: dW[16w + 4g + e][16bk + rl]
+  float* slab = a.part_w[s] + static_cast<int64_t>(c) * kCD * kCD;
+#pragma unroll
+  for (int bk = 0; bk < 8; ++bk)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) slab[(16 * w + 4 * g + e) * kCD + 16 * bk + rl] = acc[bk][e];
+  if (a.has_b[s] && tid < 128) a.part_b[s][static_cast<int64_t>(c) * kCD + tid] = bsum;
+}
+
+inline int chain_wgrad_splits_of(int64_t ntiles, int stages) {
+  // at most one workgroup per CU over all stages (96 KB of LDS each: a 257th would run alone in a
+  // second round), >= 4 tiles each
+  int64_t per = 256 / stages;
+  const int64_t cap = (ntiles + 3) / 4;
+  if (per > cap) per = cap;
+  return static_cast<int>(per < 1 ? 1 : per);
+}
+
 inline bool al16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 
 // rows per weight-gradient chunk: about two workgroups per CU over all jobs, >= 64 rows
@@ -690,13 +848,19 @@ inline int wgrad_chunk_rows(int64_t R, int jobs) {
 
 using namespace x2g;
 
+X2G_API int64_t x2g_chain_t_floats(int64_t rows, int32_t dim) {
+  return rows > 0 && dim > 0 ? (rows + 15) / 16 * 16 * dim : 0;
+}
+
 X2G_API int x2g_chain_fwd(const float* x, const float* res_ext, const x2g_chain_stage* stages, int32_t n_stages,
-                          int64_t rows, int32_t dim, void* stream) {
+                          int64_t rows, int32_t dim, float* in_t, void* stream) {
   if (!stages || n_stages < 1 || n_stages > X2G_CHAIN_MAX_STAGES || rows < 0 || dim <= 0) return X2G_EINVAL;
   if (dim != kCD || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
   ChainFwdArgs a{};
   a.x = x;
   a.res = res_ext;
+  a.in_t = in_t;
+  a.tf = x2g_chain_t_floats(rows, dim);
   a.R = rows;
   a.n = n_stages;
   a.dbg = tuning(kTuneChainDbg);
@@ -718,9 +882,9 @@ X2G_API int x2g_chain_fwd(const float* x, const float* res_ext, const x2g_chain_
   if (n_ext > 1 || (n_ext && !res_ext)) return X2G_EINVAL;
   if (rows == 0) return X2G_OK;
   if (!x) return X2G_EINVAL;
-  if (!al16(x) || !al16(res_ext)) return X2G_EUNSUPPORTED;
+  if (!al16(x) || !al16(res_ext) || !al16(in_t)) return X2G_EUNSUPPORTED;
   hipStream_t st = as_stream(stream);
-  if (tuning(kTuneChain) == 1) {  // register-tile kernel
+  if (tuning(kTuneChain) == 1 && !in_t) {  // register-tile kernel (no T-layout output)
     const int64_t groups = ((rows + 15) / 16 + kCWaves - 1) / kCWaves;
     chain_fwd_kernel<<<static_cast<unsigned>(groups < 256 ? groups : 256), kCThreads, 0, st>>>(a);
   } else {  // v2: one workgroup per CU, <= 96 rows in LDS
@@ -731,7 +895,7 @@ X2G_API int x2g_chain_fwd(const float* x, const float* res_ext, const x2g_chain_
 }
 
 X2G_API int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_bwd_stage* stages, int32_t n_stages,
-                          int64_t rows, int32_t dim, float* dx, float* d_res_ext, void* stream) {
+                          int64_t rows, int32_t dim, float* dx, float* d_res_ext, float* dz_t, void* stream) {
   if (!stages || n_stages < 1 || n_stages > X2G_CHAIN_MAX_STAGES || rows < 0 || dim <= 0) return X2G_EINVAL;
   if (dim != kCD || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
   ChainBwdArgs a{};
@@ -739,6 +903,8 @@ X2G_API int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_
   a.dy_add = dy_add;
   a.dx = dx;
   a.dres = d_res_ext;
+  a.dz_t = dz_t;
+  a.tf = x2g_chain_t_floats(rows, dim);
   a.R = rows;
   a.n = n_stages;
   int n_ext = 0, held = 0;
@@ -757,9 +923,9 @@ X2G_API int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_
   if (n_ext > 1) return X2G_EINVAL;
   if (rows == 0) return X2G_OK;
   if (!dy || !dx) return X2G_EINVAL;
-  if (!al16(dy) || !al16(dy_add) || !al16(dx) || !al16(d_res_ext)) return X2G_EUNSUPPORTED;
+  if (!al16(dy) || !al16(dy_add) || !al16(dx) || !al16(d_res_ext) || !al16(dz_t)) return X2G_EUNSUPPORTED;
   hipStream_t st = as_stream(stream);
-  if (tuning(kTuneChain) == 1) {
+  if (tuning(kTuneChain) == 1 && !dz_t) {
     const int64_t groups = ((rows + 15) / 16 + kCWaves - 1) / kCWaves;
     chain_bwd_kernel<<<static_cast<unsigned>(groups < 256 ? groups : 256), kCThreads, 0, st>>>(a);
   } else {
@@ -808,4 +974,48 @@ X2G_API int x2g_wgrad_batched(const x2g_wgrad_job* jobs, int32_t num_jobs, int64
   const int rc = last_launch_status();
   if (rc || (flags & X2G_DEFER_SLAB_SUM)) return rc;
   return x2g_slab_sum_batch(sj, num_jobs, (flags & X2G_ACCUM_WGRAD) ? 1 : 0, stream);
+}
+
+X2G_API int32_t x2g_chain_wgrad_splits(int64_t rows, int32_t dim, int32_t n_stages) {
+  if (rows <= 0 || dim != kCD || n_stages < 1 || n_stages > X2G_CHAIN_MAX_STAGES) return 0;
+  return chain_wgrad_splits_of((rows + 15) / 16, n_stages);
+}
+
+X2G_API size_t x2g_chain_wgrad_workspace(int64_t rows, int32_t dim, int32_t n_stages) {
+  const int32_t splits = x2g_chain_wgrad_splits(rows, dim, n_stages);
+  return static_cast<size_t>(splits > 0 ? n_stages : 0) * splits * (kCD * kCD + kCD) * sizeof(float);
+}
+
+X2G_API int x2g_chain_wgrad(const float* in_t, const float* dz_t, int32_t n_stages, int64_t rows, int32_t dim,
+                            float* const* dw, float* const* db, int flags, void* workspace, size_t workspace_bytes,
+                            void* stream) {
+  if (!in_t || !dz_t || !dw || n_stages < 1 || n_stages > X2G_CHAIN_MAX_STAGES || rows <= 0 || dim <= 0 ||
+      (flags & ~(X2G_ACCUM_WGRAD | X2G_DEFER_SLAB_SUM)))
+    return X2G_EINVAL;
+  if (dim != kCD || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  if (!al16(in_t) || !al16(dz_t)) return X2G_EUNSUPPORTED;
+  const size_t need = x2g_chain_wgrad_workspace(rows, dim, n_stages);
+  if (!workspace || workspace_bytes < need) return X2G_EWORKSPACE;
+  ChainWgradArgs a{};
+  a.in_t = in_t;
+  a.dz_t = dz_t;
+  a.tf = x2g_chain_t_floats(rows, dim);
+  a.ntiles = (rows + 15) / 16;
+  a.splits = x2g_chain_wgrad_splits(rows, dim, n_stages);
+  const size_t per = need / n_stages;
+  x2g_slab_job sj[X2G_CHAIN_MAX_STAGES];
+  for (int j = 0; j < n_stages; ++j) {
+    if (!dw[j]) return X2G_EINVAL;
+    const bool hb = db && db[j];
+    a.part_w[j] = reinterpret_cast<float*>(static_cast<char*>(workspace) + per * j);
+    a.part_b[j] = a.part_w[j] + static_cast<int64_t>(a.splits) * kCD * kCD;
+    a.has_b[j] = hb;
+    sj[j] = x2g_slab_job{a.part_w[j], hb ? a.part_b[j] : nullptr, dw[j], hb ? db[j] : nullptr, kCD * kCD,
+                         hb ? kCD : 0, a.splits};
+  }
+  chain_wgrad_kernel<<<dim3(static_cast<unsigned>(a.splits), static_cast<unsigned>(n_stages)), kCThreads, 0,
+                       as_stream(stream)>>>(a);
+  const int rc = last_launch_status();
+  if (rc || (flags & X2G_DEFER_SLAB_SUM)) return rc;
+  return x2g_slab_sum_batch(sj, n_stages, (flags & X2G_ACCUM_WGRAD) ? 1 : 0, stream);
 }

@@ -86,8 +86,12 @@ SIGNATURES = {
     "x2g_clip_adam_ema": [_P, _P, _P, _P, _P, _I64, _P, _P, _SZ, _P],
     "x2g_dense_bwd_ex": [_P, _P, ctypes.c_int, _P, _P, _I64, _I32, _I32, _P, _P, _P, _P, ctypes.c_int, _P, _SZ,
                          _P],
-    "x2g_chain_fwd": [_P, _P, _P, _I32, _I64, _I32, _P],
-    "x2g_chain_bwd": [_P, _P, _P, _I32, _I64, _I32, _P, _P, _P],
+    "x2g_chain_fwd": [_P, _P, _P, _I32, _I64, _I32, _P, _P],
+    "x2g_chain_bwd": [_P, _P, _P, _I32, _I64, _I32, _P, _P, _P, _P],
+    "x2g_chain_t_floats": [_I64, _I32],
+    "x2g_chain_wgrad_workspace": [_I64, _I32, _I32],
+    "x2g_chain_wgrad_splits": [_I64, _I32, _I32],
+    "x2g_chain_wgrad": [_P, _P, _I32, _I64, _I32, _P, _P, ctypes.c_int, _P, _SZ, _P],
     "x2g_wgrad_batched_workspace": [_I64, _I32, _I32],
     "x2g_wgrad_batched_splits": [_I64, _I32, _I32],
     "x2g_wgrad_batched": [_P, _I32, _I64, _I32, ctypes.c_int, _P, _SZ, _P],
@@ -100,7 +104,9 @@ RESTYPES = {"x2g_status_string": ctypes.c_char_p, "x2g_vertex_to_edge_workspace"
             "x2g_rbf_gate_bwd_splits": ctypes.c_int32, "x2g_keyed_row_sum_workspace": _SZ,
             "x2g_readout_head_bwd_workspace": _SZ, "x2g_readout_head_bwd_splits": ctypes.c_int32,
             "x2g_sbf_radial_wgrad_splits": ctypes.c_int32, "x2g_sbf_radial_wgrad_workspace": _SZ,
-            "x2g_wgrad_batched_workspace": _SZ, "x2g_wgrad_batched_splits": ctypes.c_int32}
+            "x2g_wgrad_batched_workspace": _SZ, "x2g_wgrad_batched_splits": ctypes.c_int32,
+            "x2g_chain_t_floats": ctypes.c_int64, "x2g_chain_wgrad_workspace": _SZ,
+            "x2g_chain_wgrad_splits": ctypes.c_int32}
 
 _lib = None
 

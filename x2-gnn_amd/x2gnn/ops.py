@@ -849,11 +849,41 @@ def wgrad_batched(dys, xs, weights, biases):
     return dws, dbs
 
 
+def chain_wgrad(in_t, dz_t, R, weights, biases):
+    """Weight / bias gradients of every chain stage from the T-layout operands (x2g_chain_wgrad);
+    bucket-backed parameters are summed into the bucket (Nones returned for them), slab sums
+    deferred inside ``deferred_wgrad()``."""
+    n = len(weights)
+    D = weights[0].shape[1]
+    dev = in_t.device
+    params = list(weights) + [b for b in biases if b is not None]
+    bufs, acc = _wgrad_targets(params, [tuple(p.shape) for p in params], dev)
+    dws, rest = bufs[:n], iter(bufs[n:])
+    dbs = [next(rest) if b is not None else None for b in biases]
+    lib = _lib.load()
+    ws_bytes = int(lib.x2g_chain_wgrad_workspace(R, D, n))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    dw_arr = (ctypes.c_void_p * n)(*[_dp(t) for t in dws])
+    db_arr = (ctypes.c_void_p * n)(*[_dp(t) for t in dbs])
+    defer = acc and _DEFER is not None
+    call("x2g_chain_wgrad", ptr(in_t), ptr(dz_t), n, R, D, dw_arr, db_arr,
+         (ACCUM_WGRAD if acc else 0) | (DEFER_SLAB_SUM if defer else 0), ptr(ws), ws_bytes, stream_ptr())
+    if defer:
+        splits = int(lib.x2g_chain_wgrad_splits(R, D, n))
+        per = ws_bytes // n
+        for g in range(n):
+            _defer_job(ws, g * per, splits, D * D, D, dws[g], dbs[g])
+    if acc:
+        return [None] * n, [None] * n
+    return dws, dbs
+
+
 class _ChainFn(torch.autograd.Function):
     """A chain of D x D Linear stages on the same rows in ONE kernel (x2g_chain_fwd, csrc/chain.hip):
     stage s computes z_s = in_s W_s^T + b_s, out_s = act(z_s) (+ the held ResidualLayer input or
     the external residual), in_{s+1} = out_s.  Backward: one kernel for every stage's data gradient
-    (x2g_chain_bwd, residual gradients folded in registers) + one batched weight-gradient launch."""
+    (x2g_chain_bwd, residual gradients folded in registers) + one weight-gradient launch over the
+    stage inputs and dz that both kernels leave in the tiled-transposed layout (x2g_chain_wgrad)."""
 
     @staticmethod
     def forward(ctx, x, res, flags, *params):
@@ -863,41 +893,44 @@ class _ChainFn(torch.autograd.Function):
         R, D = x2.shape
         r2 = _f32(res) if res is not None else None
         f32 = dict(dtype=torch.float32, device=x2.device)
-        zs = [torch.empty(R, D, **f32) if flags[i] & CHAIN_SILU else None for i in range(n)]
-        ys = [torch.empty(R, D, **f32) for _ in range(n)]
+        grad = any(ctx.needs_input_grad)  # (autograd runs forward() itself with grad mode off)
+        zs = [torch.empty(R, D, **f32) if (flags[i] & CHAIN_SILU) and grad else None for i in range(n)]
+        y = torch.empty(R, D, **f32)
         W = [_f32(w) for w in ws]
         B = [_f32(b) if b is not None else None for b in bs]
-        # W^T of every stage (written by the forward kernel) for the backward's data gradient
-        WT = torch.empty(n, D, D, **f32) if torch.is_grad_enabled() else None
-        st = (ChainStage * n)(*[ChainStage(_dp(W[i]), _dp(B[i]), _dp(zs[i]), _dp(ys[i]),
+        tf = int(_lib.load().x2g_chain_t_floats(R, D))
+        # for the backward: W^T of every stage, and every stage input in the T layout
+        WT = torch.empty(n, D, D, **f32) if grad else None
+        in_t = torch.empty(n, tf, **f32) if grad else None
+        st = (ChainStage * n)(*[ChainStage(_dp(W[i]), _dp(B[i]), _dp(zs[i]), _dp(y) if i == n - 1 else None,
                                            None if WT is None else WT[i].data_ptr(), flags[i]) for i in range(n)])
-        call("x2g_chain_fwd", ptr(x2), ptr(r2), st, n, R, D, stream_ptr())
-        ins = [x2] + ys[:-1]
-        ctx.save_for_backward(*W, *[z if z is not None else x2 for z in zs], *ins, WT)
+        call("x2g_chain_fwd", ptr(x2), ptr(r2), st, n, R, D, ptr(in_t), stream_ptr())
+        if grad:
+            ctx.save_for_backward(*W, *[z if z is not None else x2 for z in zs], WT, in_t)
         ctx.flags, ctx.params, ctx.has_res = tuple(flags), params, res is not None
-        return ys[-1]
+        return y
 
     @staticmethod
     def backward(ctx, gy):
         flags = ctx.flags
         n = len(flags)
         saved = ctx.saved_tensors
-        W, zs, ins, WT = saved[:n], saved[n:2 * n], saved[2 * n:3 * n], saved[3 * n]
+        W, zs, WT, in_t = saved[:n], saved[n:2 * n], saved[2 * n], saved[2 * n + 1]
         gy2 = _f32(gy)
         R, D = gy2.shape
         f32 = dict(dtype=torch.float32, device=gy2.device)
-        dzs = [torch.empty(R, D, **f32) for _ in range(n)]
+        dz_t = torch.empty_like(in_t)
         dx = torch.empty(R, D, **f32)
         dres = torch.empty(R, D, **f32) if ctx.has_res else None
-        st = (ChainBwdStage * n)(*[ChainBwdStage(_dp(W[i]), None if WT is None else WT[i].data_ptr(),
-                                                 _dp(zs[i]) if flags[i] & CHAIN_SILU else None, _dp(dzs[i]), flags[i])
+        st = (ChainBwdStage * n)(*[ChainBwdStage(_dp(W[i]), WT[i].data_ptr(),
+                                                 _dp(zs[i]) if flags[i] & CHAIN_SILU else None, None, flags[i])
                                    for i in range(n)])
-        call("x2g_chain_bwd", ptr(gy2), None, st, n, R, D, ptr(dx), ptr(dres), stream_ptr())
+        call("x2g_chain_bwd", ptr(gy2), None, st, n, R, D, ptr(dx), ptr(dres), ptr(dz_t), stream_ptr())
         ws, bs = ctx.params[0::2], ctx.params[1::2]
-        dws, dbs = wgrad_batched(dzs, list(ins), ws, bs)
+        dws, dbs = chain_wgrad(in_t, dz_t, R, ws, bs)
         grads = []
         for i in range(n):
-            grads += [None if dws[i] is None else dws[i], None if dbs[i] is None else dbs[i]]
+            grads += [dws[i], dbs[i]]
         return (dx, dres, None, *grads)
 
 
