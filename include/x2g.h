@@ -330,8 +330,8 @@ int x2g_dense_bwd_data(const float* dy, const float* z, int act, const float* w,
 /* Workspace bytes for x2g_dense_bwd. */
 size_t x2g_dense_bwd_workspace(int64_t rows, int32_t in_features, int32_t out_features);
 
-/* Full backward of x2g_dense_fwd in one call: dz = dy * act'(z); dx = dz w (dx may be NULL when
- * act == X2G_ACT_NONE); dw = dz^T x; db = colsum(dz) (db may be NULL).  For in/out features
+/* Full backward of x2g_dense_fwd in one call: dz = dy * act'(z); dx = dz w (dx may be NULL: no
+ * data gradient is formed); dw = dz^T x; db = colsum(dz) (db may be NULL).  For in/out features
  * <= 128 this is one persistent kernel (weight staged in LDS once per CU, dx and the per-CU
  * weight-gradient partials from the same LDS tiles) plus a fixed-order slab sum. */
 int x2g_dense_bwd(const float* dy, const float* z, int act, const float* x, const float* w, int64_t rows,

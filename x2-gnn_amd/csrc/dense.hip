@@ -1630,6 +1630,17 @@ X2G_API int x2g_dense_fwd(const float* x, const float* w, const float* b, int64_
   return last_launch_status();
 }
 
+// dz = dy * SiLU'(z) alone (grid-stride, float4 where aligned)
+__global__ void __launch_bounds__(256) silu_grad_elementwise(const float* __restrict__ dy, const float* __restrict__ z,
+                                                              int64_t n, float* __restrict__ dz) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float zz = z[i];
+    const float s = 1.0f / (1.0f + expf(-zz));
+    dz[i] = dy[i] * (s * (1.0f + zz * (1.0f - s)));
+  }
+}
+
 // dx (+)= (dy * act'(z)) w for any shape; dx_add (optional, may alias dx) is added in the epilogue,
 // where every element is read and then written by the same thread
 static int dense_bwd_data_impl(const float* dy, const float* z, int act, const float* w, int64_t R, int32_t K,
@@ -1755,12 +1766,16 @@ X2G_API int x2g_dense_bwd_ex(const float* dy, const float* z, int act, const flo
   const size_t dz_bytes = ((static_cast<size_t>(R) * N * sizeof(float)) + 255) / 256 * 256;
   const float* dzp = dy;
   int rc;
-  if (act != kActNone || dx) {
-    float* dx_tmp = dx;
-    if (!dx_tmp) return X2G_EUNSUPPORTED;  // general path needs a dx buffer when an activation is fused
-    if ((rc = dense_bwd_data_impl(dy, z, act, w, R, K, N, dx_tmp, dx_add, act != kActNone ? dzbuf : nullptr, st)))
+  if (dx) {
+    if ((rc = dense_bwd_data_impl(dy, z, act, w, R, K, N, dx, dx_add, act != kActNone ? dzbuf : nullptr, st)))
       return rc;
     if (act != kActNone) dzp = dzbuf;
+  } else if (act != kActNone) {  // no data gradient wanted (e.g. a layer on non-differentiable input): dz only
+    const int64_t n = R * static_cast<int64_t>(N);
+    const int64_t blocks = (n + 1023) / 1024;
+    silu_grad_elementwise<<<static_cast<unsigned>(blocks < 65535 ? blocks : 65535), 256, 0, st>>>(dy, z, n, dzbuf);
+    if ((rc = last_launch_status())) return rc;
+    dzp = dzbuf;
   }
   return x2g_linear_wgrad_ex(dzp, x, R, N, K, dw, db, flags, static_cast<char*>(workspace) + dz_bytes,
                              workspace_bytes - dz_bytes, stream);

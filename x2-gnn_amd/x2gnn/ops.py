@@ -698,7 +698,7 @@ def _dense_bwd_raw(gy2, z, act, x2, w, w_param, b_param, has_bias, need_dx, dx_a
     R = gy2.shape[0]
     dev = gy2.device
     dx = None
-    if need_dx or act != ACT_NONE or dx_add is not None:
+    if need_dx or dx_add is not None:  # (the kernels form dz = dy * act'(z) themselves when dx is not wanted)
         dx = dx_out if dx_out is not None else torch.empty(R, K, dtype=torch.float32, device=dev)
     gw = grad_sink(w_param)
     gb = grad_sink(b_param) if has_bias else None
