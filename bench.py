@@ -14,6 +14,7 @@ on) and the CPU baseline (the oracle restatement, torch-CPU, on a bounded sample
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -264,6 +265,52 @@ def dense_probe(R, reps):
     return {"dense_fwd": (_event_time(fwd, reps), 2.0 * R * K * N), "dense_bwd": (_event_time(bwd, reps), 4.0 * R * K * N)}
 
 
+def chain_probe(R, reps):
+    """The trunk tail as the step runs it (ops.row_chain, model.py:47-50: 7 Linear stages per conv
+    layer) at this step's row count: x2g_chain_fwd (with the T-layout stage inputs), x2g_chain_bwd
+    (with the T-layout dz) and x2g_chain_wgrad (slab sums deferred, as in the step), HIP-event
+    timed on the launch stream.  FLOPs per launch: 7 * 2 * R * 128 * 128 each."""
+    D, n = 128, 7
+    S, H, RH, RE = ops.CHAIN_SILU, ops.CHAIN_HOLD, ops.CHAIN_RES_HELD, ops.CHAIN_RES_EXT
+    flags = [S | H, S | RH, S | RE, S | H, S | RH, S | H, S | RH]
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(4)
+    x, res, dy = (torch.randn(R, D, device=dev, generator=g) for _ in range(3))
+    W = [torch.randn(D, D, device=dev, generator=g) / 11.3 for _ in range(n)]
+    B = [0.1 * torch.randn(D, device=dev, generator=g) for _ in range(n)]
+    Z = [torch.empty(R, D, device=dev) for _ in range(n)]
+    y, dx, dres = (torch.empty(R, D, device=dev) for _ in range(3))
+    WT = torch.empty(n, D, D, device=dev)
+    tf = _lib_ws("x2g_chain_t_floats", R, D)
+    in_t, dz_t = torch.empty(n, tf, device=dev), torch.empty(n, tf, device=dev)
+    DW = [torch.empty(D, D, device=dev) for _ in range(n)]
+    DB = [torch.empty(D, device=dev) for _ in range(n)]
+    st = (ops.ChainStage * n)(*[ops.ChainStage(W[i].data_ptr(), B[i].data_ptr(), Z[i].data_ptr(),
+                                               y.data_ptr() if i == n - 1 else None, WT[i].data_ptr(), flags[i])
+                                for i in range(n)])
+    bst = (ops.ChainBwdStage * n)(*[ops.ChainBwdStage(W[i].data_ptr(), WT[i].data_ptr(), Z[i].data_ptr(), None,
+                                                      flags[i]) for i in range(n)])
+    wsb = _lib_ws("x2g_chain_wgrad_workspace", R, D, n)
+    ws = torch.empty(max(wsb, 4), dtype=torch.uint8, device=dev)
+    dwa = (ctypes.c_void_p * n)(*[t.data_ptr() for t in DW])
+    dba = (ctypes.c_void_p * n)(*[t.data_ptr() for t in DB])
+
+    def fwd():
+        call("x2g_chain_fwd", ptr(x), ptr(res), st, n, R, D, ptr(in_t), stream_ptr())
+
+    def bwd():
+        call("x2g_chain_bwd", ptr(dy), None, bst, n, R, D, ptr(dx), ptr(dres), ptr(dz_t), stream_ptr())
+
+    def wgrad():
+        call("x2g_chain_wgrad", ptr(in_t), ptr(dz_t), n, R, D, dwa, dba, ops.DEFER_SLAB_SUM, ptr(ws), wsb, stream_ptr())
+
+    fwd()
+    bwd()
+    flops = 2.0 * n * R * D * D
+    return {"chain_fwd": (_event_time(fwd, reps), flops), "chain_bwd": (_event_time(bwd, reps), flops),
+            "chain_wgrad": (_event_time(wgrad, reps), flops)}
+
+
 def _lib_ws(name, *args):
     from x2gnn import _lib
 
@@ -424,18 +471,18 @@ def main():
     plan_lg = model.line_graph_data(batch)[1].lg
     sa = scatter_add_probe(plan_lg, args.kernel_reps)
     dense = dense_probe(shape["E"], args.kernel_reps)
-    # the roofline kernel: the fused dense backward, the largest share of the step in the
-    # committed profile (profiles/r1_v2_bench_kernel_stats.csv: dense_bwd_persist 1.9 ms/step)
-    dbw_ms, dbw_flops = dense["dense_bwd"]
-    dbw_tfs = dbw_flops / (dbw_ms * 1e-3) / 1e12
-    ntiles = (shape["E"] + 31) // 32  # dense.hip bwd_grid(): fewest workgroups at ceil(tiles/256) 32-row tiles each
-    per = (ntiles + 255) // 256
-    grid = str(((ntiles + per - 1) // per) * 512)
-    traffic = pmc_traffic([("x2g::dense_bwd_v8", grid), ("x2g::sum_slabs2", str(258 * 256))])
-    roof = {"kernel": "x2g_dense_bwd [E,128]x[128,128] SiLU (dense_bwd_v8 + sum_slabs2)",
-            "bound": "mfma", "achieved": round(dbw_tfs, 2), "peak": MFMA_F32_PEAK_TFS,
-            "unit": "TFLOP/s", "frac": round(dbw_tfs / MFMA_F32_PEAK_TFS, 4), "traffic": traffic,
-            "avg_ms": round(dbw_ms, 5), "flops_per_launch": int(dbw_flops),
+    dense.update(chain_probe(shape["E"], args.kernel_reps))
+    # the roofline kernel: the trunk-tail chain backward (x2g_chain_bwd), the largest single
+    # kernel of the step in the committed profile (profiles/r2_*_step_kernels.txt); f32 MFMA-bound
+    # (7 x 2 R D^2 FLOP vs ~184 MB of z / dz / dy / dx traffic at config 2)
+    cb_ms, cb_flops = dense["chain_bwd"]
+    cb_tfs = cb_flops / (cb_ms * 1e-3) / 1e12
+    grid = str(min(256, (shape["E"] + 15) // 16) * 512)
+    traffic = pmc_traffic([("x2g::(anonymous namespace)::chain_bwd_v2", grid)])
+    roof = {"kernel": "x2g_chain_bwd: 7-stage trunk tail data gradient [E,128] (chain_bwd_v2)",
+            "bound": "mfma", "achieved": round(cb_tfs, 2), "peak": MFMA_F32_PEAK_TFS,
+            "unit": "TFLOP/s", "frac": round(cb_tfs / MFMA_F32_PEAK_TFS, 4), "traffic": traffic,
+            "avg_ms": round(cb_ms, 5), "flops_per_launch": int(cb_flops),
             "traffic_source": os.path.relpath(TRAFFIC_JSON, ROOT) if traffic else None}
     if not wl["train"]:  # inference: no backward; the T-row attention forward dominates
         a_ms, a_bytes = probe["attn_fwd"]

@@ -519,6 +519,53 @@ int32_t x2g_wgrad_batched_splits(int64_t rows, int32_t dim, int32_t num_jobs);
 int x2g_wgrad_batched(const x2g_wgrad_job* jobs, int32_t num_jobs, int64_t rows, int32_t dim, int flags,
                       void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------- conv projections
+ * The five projections SBFTransformerConv.forward applies to its node features
+ * (sbftransformer_conv.py:99-107,127): f = lin_rbf(rbf) (no bias), x_src = x * f,
+ * q = lin_query(x), k = lin_key(x_src), v = lin_value(x_src), skip = lin_skip(x) — one kernel with
+ * each CU's rows of x and x_src held in LDS (the row-chain v2 structure), D = 128, rbf_dim <= 8.
+ * proj[0..3] = query, key, value, skip: w [D, D], b [D] or NULL, out [rows, D], wt (optional out:
+ * w transposed, for x2g_conv_proj_bwd).  x_t / xs_t (optional): x and x_src in the T layout (the
+ * weight gradient's operands).  */
+typedef struct {
+  const float* w;
+  const float* b;
+  float* out;
+  float* wt;
+} x2g_proj;
+
+int x2g_conv_proj_fwd(const float* x, const float* rbf, int32_t rbf_dim, const float* w_rbf, const x2g_proj* proj,
+                      int64_t rows, int32_t dim, float* x_t, float* xs_t, void* stream);
+
+/* Data-gradient products of x2g_conv_proj_fwd's backward: grads[0..3] = dL/d(q, k, v, skip) with
+ * their weights (w, or wt when given) and optional T-layout copies g_t for the weight gradient
+ * (x2g_tiled_wgrad):  dx = dq Wq + dskip Ws (+ dx_add; dx may alias dx_add),  dxs = dk Wk + dv Wv
+ * = dL/d x_src.  The gate's share (dx += dxs * f, drbf, dW_rbf) is x2g_rbf_gate_bwd(dxs, ...). */
+typedef struct {
+  const float* g;
+  const float* w;
+  const float* wt;
+  float* g_t;
+} x2g_proj_grad;
+
+int x2g_conv_proj_bwd(const x2g_proj_grad* grads, int64_t rows, int32_t dim, float* dx, const float* dx_add,
+                      float* dxs, void* stream);
+
+/* Weight / bias gradients of independent D x D Linear layers over the same rows from T-layout
+ * operands: dw_j = dy_j^T x_j, db_j = colsum(dy_j) (db_j may be NULL); as x2g_chain_wgrad, with
+ * each job's operands given separately (a T-layout tensor may serve several jobs). */
+typedef struct {
+  const float* dy_t;
+  const float* x_t;
+  float* dw;
+  float* db;
+} x2g_tiled_job;
+
+size_t x2g_tiled_wgrad_workspace(int64_t rows, int32_t dim, int32_t num_jobs);
+int32_t x2g_tiled_wgrad_splits(int64_t rows, int32_t dim, int32_t num_jobs);
+int x2g_tiled_wgrad(const x2g_tiled_job* jobs, int32_t num_jobs, int64_t rows, int32_t dim, int flags,
+                    void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -907,3 +907,43 @@ def test_row_chain_bwd_with_and_without_transposed_weights(cuda, R):
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     for a, b in zip(outs[0][2], outs[1][2]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,RR", [(21058, 6), (1000, 6), (37, 8), (5, 3)])
+def test_conv_projections_fused_vs_layerwise(cuda, R, RR):
+    """x2g_conv_proj_fwd / _bwd + gate backward + T-layout weight gradients (ops._ConvProjFusedFn)
+    against the layer-by-layer kernels (ops._ConvProjFn) and fp64 torch: q, k, v, skip and every
+    input / parameter gradient of SBFTransformerConv's projections (sbftransformer_conv.py:99-107,127)."""
+    from x2gnn import ops
+
+    g = torch.Generator(device=cuda).manual_seed(R + RR)
+    x = torch.randn(R, 128, device=cuda, generator=g)
+    rbf = torch.rand(R, RR, device=cuda, generator=g)
+    wr = torch.randn(128, RR, device=cuda, generator=g) / 2
+    W = [torch.randn(128, 128, device=cuda, generator=g) / 11.3 for _ in range(4)]
+    B = [0.1 * torch.randn(128, device=cuda, generator=g) for _ in range(4)]
+    gs = [torch.randn(R, 128, device=cuda, generator=g) for _ in range(4)]
+
+    def run(fn, dtype):
+        ins = [t.detach().to(dtype).requires_grad_(True) for t in [x, rbf, wr] + [v for p in zip(W, B) for v in p]]
+        if fn is None:  # torch reference
+            xx, rb, w_r = ins[:3]
+            xs = xx * (rb @ w_r.t())
+            outs = [xx @ ins[3].t() + ins[4], xs @ ins[5].t() + ins[6], xs @ ins[7].t() + ins[8],
+                    xx @ ins[9].t() + ins[10]]
+        else:
+            outs = fn.apply(*ins)
+        torch.autograd.backward(outs, [t.to(dtype) for t in gs])
+        return [o.detach() for o in outs], [t.grad for t in ins]
+
+    o_f, g_f = run(ops._ConvProjFusedFn, torch.float32)
+    o_l, g_l = run(ops._ConvProjFn, torch.float32)
+    o_r, g_r = run(None, torch.float64)
+    for a, b, r in zip(o_f, o_l, o_r):
+        torch.testing.assert_close(a.double(), r, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+    for i, (a, b, r) in enumerate(zip(g_f, g_l, g_r)):
+        scale = float(r.abs().max()) + 1e-30
+        assert float((a.double() - r).abs().max()) <= 2e-5 * scale + 1e-6, i
+        assert float((a - b).abs().max()) <= 2e-5 * scale + 1e-6, i

@@ -742,9 +742,8 @@ constexpr int kWTiles = 2;  // T tiles per step
 __device__ __forceinline__ int tpos(int f, int q) { return f * 4 + (q ^ (((f >> 3) & 1) * 3)); }
 
 struct ChainWgradArgs {
-  const float* in_t;
-  const float* dz_t;
-  int64_t tf;
+  const float* in_t[X2G_CHAIN_MAX_STAGES];  // per job: the layer input and dz, T layout
+  const float* dz_t[X2G_CHAIN_MAX_STAGES];
   int64_t ntiles;
   float* part_w[X2G_CHAIN_MAX_STAGES];
   float* part_b[X2G_CHAIN_MAX_STAGES];
@@ -763,8 +762,8 @@ __global__ void __launch_bounds__(kCThreads, 1) chain_wgrad_kernel(const ChainWg
   const int rl = lane & 15, g = lane >> 4;
   const int64_t t0 = c * a.ntiles / a.splits, t1 = (c + 1) * a.ntiles / a.splits;
   const int nsteps = static_cast<int>((t1 - t0 + kWTiles - 1) / kWTiles);
-  const float* dz = a.dz_t + s * a.tf;
-  const float* xin = a.in_t + s * a.tf;
+  const float* dz = a.dz_t[s];
+  const float* xin = a.in_t[s];
   // LDS position P = 64w + lane of a tile image holds source chunk (P >> 2) * 4 + ((P & 3) ^ sigma)
   const int P = 64 * w + lane;
   const int src_chunk = (P >> 2) * 4 + ((P & 3) ^ (((P >> 5) & 1) * 3));
@@ -830,6 +829,184 @@ inline int chain_wgrad_splits_of(int64_t ntiles, int stages) {
   const int64_t cap = (ntiles + 3) / 4;
   if (per > cap) per = cap;
   return static_cast<int>(per < 1 ? 1 : per);
+}
+
+// ---------------------------------------------------------------- conv projections
+// SBFTransformerConv's five projections (sbftransformer_conv.py:99-107,127) with the row-chain
+// v2 structure: a workgroup's <= 96 rows of x, and of x_src = x * (rbf W_rbf^T) formed in
+// registers, sit in LDS; each wave computes its 16-feature slice of q, k, v and skip.
+constexpr int kRbfMax = 8;
+
+struct ProjFwdArgs {
+  const float* x;
+  const float* rbf;
+  const float* wr;
+  int RR;
+  x2g_proj p[4];
+  float* x_t;
+  float* xs_t;
+  int64_t R;
+};
+
+__device__ __forceinline__ void load_rows_slice(const float* P, int r0, int nrows, int w, int rl, int g,
+                                                f4 (&v)[kV2RB]) {
+  const rsrc_t pr = rsrc(P);
+#pragma unroll
+  for (int rb = 0; rb < kV2RB; ++rb) {
+    const int r = 16 * rb + rl;
+    const bool ok = r < nrows;
+    v[rb] = bload4(pr, 4 * ((r0 + (ok ? r : 0)) * kCD + 16 * w + 4 * g), 0) * (ok ? 1.0f : 0.0f);
+  }
+}
+
+// rows of rbf [R, RR] -> srbf[row * NJ + j] (zero beyond RR / nrows); W_rbf [D, RR] -> swr[c * NJ + j]
+template <int NJ>
+__device__ __forceinline__ void stage_rbf(float* __restrict__ srbf, const float* __restrict__ rbf, int RR, int r0,
+                                          int nrows) {
+  for (int i = threadIdx.x; i < kV2RB * 16 * NJ; i += kCThreads) {
+    const int r = i / NJ, j = i % NJ;
+    srbf[i] = (r < nrows && j < RR) ? rbf[static_cast<int64_t>(r0 + r) * RR + j] : 0.0f;
+  }
+}
+
+// the gate filter f = rbf W_rbf^T at (row r, features c0..c0+3), the rbf_gate kernels' order
+template <int NJ>
+__device__ __forceinline__ f4 gate_filter(const float* __restrict__ srbf, const float* __restrict__ swr, int r, int c0) {
+  f4 f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc = fmaf(swr[(c0 + e) * NJ + j], srbf[r * NJ + j], acc);
+    f[e] = acc;
+  }
+  return f;
+}
+
+template <int NJ>
+__global__ void __launch_bounds__(kCThreads, 1) conv_proj_fwd_kernel(const ProjFwdArgs a) {
+  __shared__ f4 img[2][kV2Img];  // x, x_src
+  __shared__ float srbf[kV2RB * 16 * NJ];
+  __shared__ float swr[kCD * NJ];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rl = lane & 15, g = lane >> 4;
+  const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
+  const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
+  const int64_t wt_groups = G < 8 ? G : 8;
+  for (int i = tid; i < kCD * NJ; i += kCThreads) {
+    const int c = i / NJ, j = i % NJ;
+    swr[i] = j < a.RR ? a.wr[c * a.RR + j] : 0.0f;
+  }
+  for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
+    int r0, nrows;
+    chunk_rows(ch, nch, nblk, a.R, r0, nrows);
+    __syncthreads();
+    stage_rows(img[0], a.x, nullptr, r0, nrows);
+    stage_rbf<NJ>(srbf, a.rbf, a.RR, r0, nrows);
+    f4 A[8];
+    load_slice<false>(a.p[0].w, w, rl, g, A);
+    __syncthreads();
+    {
+      f4 xv[kV2RB], xs[kV2RB];
+#pragma unroll
+      for (int rb = 0; rb < kV2RB; ++rb) {
+        const int r = 16 * rb + rl;
+        xv[rb] = img[0][ipos(r, 4 * w + g)];
+        xs[rb] = xv[rb] * gate_filter<NJ>(srbf, swr, r, 16 * w + 4 * g);
+        img[1][ipos(r, 4 * w + g)] = xs[rb];
+      }
+      if (a.x_t) store_t_slice(a.x_t, xv, r0, nrows, w, rl, g);
+      if (a.xs_t) store_t_slice(a.xs_t, xs, r0, nrows, w, rl, g);
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int p = 0; p < 4; ++p) {  // q (x), k (x_src), v (x_src), skip (x)
+      const x2g_proj& P = a.p[p];
+      f4 An[8];
+      load_slice<false>(a.p[p + 1 < 4 ? p + 1 : 0].w, w, rl, g, An);
+      const f4 bias = bload4(rsrc(P.b ? P.b : P.w), 4 * (16 * w + 4 * g), 0) * (P.b ? 1.0f : 0.0f);
+      if (P.wt && ch < wt_groups) {
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+          if (b % wt_groups == ch)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) P.wt[(16 * b + 4 * g + e) * kCD + 16 * w + rl] = A[b][e];
+      }
+      f4 acc[kV2RB];
+      slice_gemm(img[(p == 1 || p == 2) ? 1 : 0], A, acc, rl, g);
+#pragma unroll
+      for (int rb = 0; rb < kV2RB; ++rb) {
+        const int r = 16 * rb + rl;
+        if (r < nrows) *reinterpret_cast<f4*>(P.out + (r0 + r) * kCD + 16 * w + 4 * g) = acc[rb] + bias;
+      }
+      pin(An);
+#pragma unroll
+      for (int b = 0; b < 8; ++b) A[b] = An[b];
+    }
+  }
+}
+
+struct ProjBwdArgs {
+  x2g_proj_grad gr[4];
+  const float* dx_add;
+  float* dx;
+  float* dxs;
+  int64_t R;
+};
+
+// dxs = dk Wk + dv Wv, dx = dq Wq + dskip Ws (+ dx_add): the four gradients staged two at a time
+__global__ void __launch_bounds__(kCThreads, 1) conv_proj_bwd_kernel(const ProjBwdArgs a) {
+  __shared__ f4 img[2][kV2Img];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rl = lane & 15, g = lane >> 4;
+  const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
+  const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
+  const int c0 = 16 * w + 4 * g;
+  auto load_ws = [&](int p, f4 (&dst)[8]) {
+    if (a.gr[p].wt)
+      load_slice<false>(a.gr[p].wt, w, rl, g, dst);
+    else
+      load_slice<true>(a.gr[p].w, w, rl, g, dst);
+  };
+  auto t_copy = [&](int p, const f4* im, int r0, int nrows) {  // the weight gradient's dy operand
+    if (!a.gr[p].g_t) return;
+    f4 v[kV2RB];
+#pragma unroll
+    for (int rb = 0; rb < kV2RB; ++rb) v[rb] = im[ipos(16 * rb + rl, 4 * w + g)];
+    store_t_slice(a.gr[p].g_t, v, r0, nrows, w, rl, g);
+  };
+  for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
+    int r0, nrows;
+    chunk_rows(ch, nch, nblk, a.R, r0, nrows);
+#pragma unroll 1
+    for (int half = 0; half < 2; ++half) {  // (dk, dv) -> dxs, then (dq, dskip) -> dx
+      const int p0 = half ? 0 : 1, p1 = half ? 3 : 2;
+      __syncthreads();  // the images are no longer read
+      stage_rows(img[0], a.gr[p0].g, nullptr, r0, nrows);
+      stage_rows(img[1], a.gr[p1].g, nullptr, r0, nrows);
+      f4 A[8], An[8];
+      load_ws(p0, A);
+      load_ws(p1, An);
+      __syncthreads();
+      t_copy(p0, img[0], r0, nrows);
+      t_copy(p1, img[1], r0, nrows);
+      f4 acc[kV2RB], t[kV2RB];
+      slice_gemm(img[0], A, acc, rl, g);
+      slice_gemm(img[1], An, t, rl, g);
+      float* out = half ? a.dx : a.dxs;
+      const float* add = half ? a.dx_add : nullptr;
+      const rsrc_t ar = rsrc(add ? add : a.gr[0].g);
+      const float am = add ? 1.0f : 0.0f;
+#pragma unroll
+      for (int rb = 0; rb < kV2RB; ++rb) {
+        const int r = 16 * rb + rl;
+        if (r < nrows) {
+          const int off = (r0 + r) * kCD + c0;
+          *reinterpret_cast<f4*>(out + off) = acc[rb] + t[rb] + bload4(ar, 4 * off, 0) * am;
+        }
+      }
+    }
+  }
 }
 
 inline bool al16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
@@ -997,9 +1174,11 @@ X2G_API int x2g_chain_wgrad(const float* in_t, const float* dz_t, int32_t n_stag
   const size_t need = x2g_chain_wgrad_workspace(rows, dim, n_stages);
   if (!workspace || workspace_bytes < need) return X2G_EWORKSPACE;
   ChainWgradArgs a{};
-  a.in_t = in_t;
-  a.dz_t = dz_t;
-  a.tf = x2g_chain_t_floats(rows, dim);
+  const int64_t tf = x2g_chain_t_floats(rows, dim);
+  for (int j = 0; j < n_stages; ++j) {
+    a.in_t[j] = in_t + j * tf;
+    a.dz_t[j] = dz_t + j * tf;
+  }
   a.ntiles = (rows + 15) / 16;
   a.splits = x2g_chain_wgrad_splits(rows, dim, n_stages);
   const size_t per = need / n_stages;
@@ -1018,4 +1197,96 @@ X2G_API int x2g_chain_wgrad(const float* in_t, const float* dz_t, int32_t n_stag
   const int rc = last_launch_status();
   if (rc || (flags & X2G_DEFER_SLAB_SUM)) return rc;
   return x2g_slab_sum_batch(sj, n_stages, (flags & X2G_ACCUM_WGRAD) ? 1 : 0, stream);
+}
+
+static inline unsigned v2_grid(int64_t rows) {
+  const int64_t nblk = (rows + 15) / 16;
+  return static_cast<unsigned>(nblk < 256 ? nblk : 256);
+}
+
+X2G_API int x2g_conv_proj_fwd(const float* x, const float* rbf, int32_t rbf_dim, const float* w_rbf,
+                              const x2g_proj* proj, int64_t rows, int32_t dim, float* x_t, float* xs_t, void* stream) {
+  if (!proj || rows < 0 || dim <= 0 || rbf_dim <= 0) return X2G_EINVAL;
+  if (dim != kCD || rbf_dim > kRbfMax || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  if (rows == 0) return X2G_OK;
+  if (!x || !rbf || !w_rbf) return X2G_EINVAL;
+  ProjFwdArgs a{};
+  a.x = x;
+  a.rbf = rbf;
+  a.wr = w_rbf;
+  a.RR = rbf_dim;
+  a.x_t = x_t;
+  a.xs_t = xs_t;
+  a.R = rows;
+  for (int p = 0; p < 4; ++p) {
+    if (!proj[p].w || !proj[p].out) return X2G_EINVAL;
+    if (!al16(proj[p].w) || !al16(proj[p].b) || !al16(proj[p].out) || !al16(proj[p].wt)) return X2G_EUNSUPPORTED;
+    a.p[p] = proj[p];
+  }
+  if (!al16(x) || !al16(x_t) || !al16(xs_t)) return X2G_EUNSUPPORTED;
+  if (rbf_dim <= 6)
+    conv_proj_fwd_kernel<6><<<v2_grid(rows), kCThreads, 0, as_stream(stream)>>>(a);
+  else
+    conv_proj_fwd_kernel<8><<<v2_grid(rows), kCThreads, 0, as_stream(stream)>>>(a);
+  return last_launch_status();
+}
+
+X2G_API int x2g_conv_proj_bwd(const x2g_proj_grad* grads, int64_t rows, int32_t dim, float* dx, const float* dx_add,
+                              float* dxs, void* stream) {
+  if (!grads || rows < 0 || dim <= 0) return X2G_EINVAL;
+  if (dim != kCD || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  if (rows == 0) return X2G_OK;
+  if (!dx || !dxs) return X2G_EINVAL;
+  ProjBwdArgs a{};
+  for (int p = 0; p < 4; ++p) {
+    if (!grads[p].g || !grads[p].w) return X2G_EINVAL;
+    if (!al16(grads[p].g) || !al16(grads[p].w) || !al16(grads[p].wt) || !al16(grads[p].g_t)) return X2G_EUNSUPPORTED;
+    a.gr[p] = grads[p];
+  }
+  if (!al16(dx) || !al16(dx_add) || !al16(dxs)) return X2G_EUNSUPPORTED;
+  a.dx_add = dx_add;
+  a.dx = dx;
+  a.dxs = dxs;
+  a.R = rows;
+  conv_proj_bwd_kernel<<<v2_grid(rows), kCThreads, 0, as_stream(stream)>>>(a);
+  return last_launch_status();
+}
+
+X2G_API int32_t x2g_tiled_wgrad_splits(int64_t rows, int32_t dim, int32_t num_jobs) {
+  return x2g_chain_wgrad_splits(rows, dim, num_jobs);
+}
+
+X2G_API size_t x2g_tiled_wgrad_workspace(int64_t rows, int32_t dim, int32_t num_jobs) {
+  return x2g_chain_wgrad_workspace(rows, dim, num_jobs);
+}
+
+X2G_API int x2g_tiled_wgrad(const x2g_tiled_job* jobs, int32_t num_jobs, int64_t rows, int32_t dim, int flags,
+                            void* workspace, size_t workspace_bytes, void* stream) {
+  if (!jobs || num_jobs < 1 || num_jobs > X2G_CHAIN_MAX_STAGES || rows <= 0 || dim <= 0 ||
+      (flags & ~(X2G_ACCUM_WGRAD | X2G_DEFER_SLAB_SUM)))
+    return X2G_EINVAL;
+  if (dim != kCD || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  const size_t need = x2g_tiled_wgrad_workspace(rows, dim, num_jobs);
+  if (!workspace || workspace_bytes < need) return X2G_EWORKSPACE;
+  ChainWgradArgs a{};
+  a.ntiles = (rows + 15) / 16;
+  a.splits = x2g_tiled_wgrad_splits(rows, dim, num_jobs);
+  const size_t per = need / num_jobs;
+  x2g_slab_job sj[X2G_CHAIN_MAX_STAGES];
+  for (int j = 0; j < num_jobs; ++j) {
+    const x2g_tiled_job& J = jobs[j];
+    if (!J.dy_t || !J.x_t || !J.dw) return X2G_EINVAL;
+    if (!al16(J.dy_t) || !al16(J.x_t)) return X2G_EUNSUPPORTED;
+    a.in_t[j] = J.x_t;
+    a.dz_t[j] = J.dy_t;
+    a.part_w[j] = reinterpret_cast<float*>(static_cast<char*>(workspace) + per * j);
+    a.part_b[j] = a.part_w[j] + static_cast<int64_t>(a.splits) * kCD * kCD;
+    a.has_b[j] = J.db != nullptr;
+    sj[j] = x2g_slab_job{a.part_w[j], J.db ? a.part_b[j] : nullptr, J.dw, J.db, kCD * kCD, J.db ? kCD : 0, a.splits};
+  }
+  chain_wgrad_kernel<<<dim3(static_cast<unsigned>(a.splits), static_cast<unsigned>(num_jobs)), kCThreads, 0,
+                       as_stream(stream)>>>(a);
+  const int rc = last_launch_status();
+  if (rc || (flags & X2G_DEFER_SLAB_SUM)) return rc;
+  return x2g_slab_sum_batch(sj, num_jobs, (flags & X2G_ACCUM_WGRAD) ? 1 : 0, stream);
 }

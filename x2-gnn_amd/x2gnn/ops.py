@@ -959,6 +959,113 @@ def row_chain(x, res, linears, flags):
     return _ChainFn.apply(x, res, tuple(flags), *params)
 
 
+class TiledJob(ctypes.Structure):
+    """x2g_tiled_job."""
+    _fields_ = [("dy_t", ctypes.c_void_p), ("x_t", ctypes.c_void_p), ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p)]
+
+
+class Proj(ctypes.Structure):
+    """x2g_proj."""
+    _fields_ = [("w", ctypes.c_void_p), ("b", ctypes.c_void_p), ("out", ctypes.c_void_p), ("wt", ctypes.c_void_p)]
+
+
+class ProjGrad(ctypes.Structure):
+    """x2g_proj_grad."""
+    _fields_ = [("g", ctypes.c_void_p), ("w", ctypes.c_void_p), ("wt", ctypes.c_void_p), ("g_t", ctypes.c_void_p)]
+
+
+def tiled_wgrad(dy_ts, x_ts, R, weights, biases):
+    """Weight / bias gradients of D x D Linear layers from T-layout operands (x2g_tiled_wgrad), one
+    job per layer; bucket-backed parameters are summed into the bucket (Nones returned), slab sums
+    deferred inside ``deferred_wgrad()``."""
+    n = len(weights)
+    D = weights[0].shape[1]
+    dev = dy_ts[0].device
+    params = list(weights) + [b for b in biases if b is not None]
+    bufs, acc = _wgrad_targets(params, [tuple(p.shape) for p in params], dev)
+    dws, rest = bufs[:n], iter(bufs[n:])
+    dbs = [next(rest) if b is not None else None for b in biases]
+    lib = _lib.load()
+    ws_bytes = int(lib.x2g_tiled_wgrad_workspace(R, D, n))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    jobs = (TiledJob * n)(*[TiledJob(_dp(dy_ts[g]), _dp(x_ts[g]), _dp(dws[g]), _dp(dbs[g])) for g in range(n)])
+    defer = acc and _DEFER is not None
+    call("x2g_tiled_wgrad", jobs, n, R, D, (ACCUM_WGRAD if acc else 0) | (DEFER_SLAB_SUM if defer else 0), ptr(ws),
+         ws_bytes, stream_ptr())
+    if defer:
+        splits = int(lib.x2g_tiled_wgrad_splits(R, D, n))
+        per = ws_bytes // n
+        for g in range(n):
+            _defer_job(ws, g * per, splits, D * D, D, dws[g], dbs[g])
+    if acc:
+        return [None] * n, [None] * n
+    return dws, dbs
+
+
+def conv_proj_fused_supported(x, rbf, weights, biases):
+    """True when the row-chain style projection kernels (x2g_conv_proj_fwd / _bwd) cover the layer."""
+    if not _CHAIN or not x.is_cuda or x.dim() != 2 or x.shape[1] != 128 or x.shape[0] * 128 >= 2 ** 31:
+        return False
+    if rbf.dim() != 2 or not 1 <= rbf.shape[1] <= 8 or rbf.shape[0] != x.shape[0]:
+        return False
+    for w in weights:
+        if tuple(w.shape) != (128, 128) or w.dtype != torch.float32 or w.data_ptr() % 16:
+            return False
+    return all(b is None or b.data_ptr() % 16 == 0 for b in biases)
+
+
+class _ConvProjFusedFn(torch.autograd.Function):
+    """SBFTransformerConv's projections (sbftransformer_conv.py:99-107,127) in one kernel each way:
+    x2g_conv_proj_fwd (x and x_src = x * lin_rbf(rbf) in LDS, q/k/v/skip per wave slice) and
+    x2g_conv_proj_bwd (dx = dq Wq + dskip Ws, dx_src = dk Wk + dv Wv) + the gate backward
+    (x2g_rbf_gate_bwd: dx += dx_src * f, drbf, dW_rbf) + one T-layout weight-gradient launch."""
+
+    @staticmethod
+    def forward(ctx, x, rbf, wr, wq, bq, wk, bk, wv, bv, ws, bs):
+        E, D = x.shape
+        x2, rbf2, Wr = _f32(x), _f32(rbf), _f32(wr)
+        W = [_f32(t) for t in (wq, wk, wv, ws)]
+        B = [_f32(t) if t is not None else None for t in (bq, bk, bv, bs)]
+        f32 = dict(dtype=torch.float32, device=x2.device)
+        outs = [torch.empty(E, D, **f32) for _ in range(4)]
+        grad = any(ctx.needs_input_grad)
+        lib = _lib.load()
+        tf = int(lib.x2g_chain_t_floats(E, D))
+        WT = torch.empty(4, D, D, **f32) if grad else None
+        x_t = torch.empty(tf, **f32) if grad else None
+        xs_t = torch.empty(tf, **f32) if grad else None
+        proj = (Proj * 4)(*[Proj(_dp(W[i]), _dp(B[i]), _dp(outs[i]), None if WT is None else WT[i].data_ptr())
+                            for i in range(4)])
+        call("x2g_conv_proj_fwd", ptr(x2), ptr(rbf2), rbf2.shape[1], ptr(Wr), proj, E, D, ptr(x_t), ptr(xs_t),
+             stream_ptr())
+        if grad:
+            ctx.save_for_backward(x2, rbf2, Wr, *W, WT, x_t, xs_t)
+        ctx.params = (wr, wq, bq, wk, bk, wv, bv, ws, bs)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, gq, gk, gv, gskip):
+        x2, rbf2, Wr, Wq, Wk, Wv, Ws, WT, x_t, xs_t = ctx.saved_tensors
+        wr, wq, bq, wk, bk, wv, bv, ws, bs = ctx.params
+        E, D = x2.shape
+        f32 = dict(dtype=torch.float32, device=x2.device)
+        g = [_f32(t) if t is not None else torch.zeros(E, D, **f32) for t in (gq, gk, gv, gskip)]
+        tf = x_t.shape[0]
+        g_t = torch.empty(4, tf, **f32)
+        W = (Wq, Wk, Wv, Ws)
+        grads = (ProjGrad * 4)(*[ProjGrad(_dp(g[i]), _dp(W[i]), WT[i].data_ptr(), g_t[i].data_ptr())
+                                 for i in range(4)])
+        dx = torch.empty(E, D, **f32)
+        dxs = torch.empty(E, D, **f32)
+        call("x2g_conv_proj_bwd", grads, E, D, ptr(dx), None, ptr(dxs), stream_ptr())
+        need_rbf = ctx.needs_input_grad[1]
+        gx, grbf, dwr, _ = _gate_bwd(dxs, None, x2, rbf2, Wr, None, wr, None, True, need_rbf, dx_add=dx)
+        dws, dbs = tiled_wgrad([g_t[0], g_t[1], g_t[2], g_t[3]], [x_t, xs_t, xs_t, x_t], E, [wq, wk, wv, ws],
+                               [bq, bk, bv, bs])
+        return (gx, (grbf if need_rbf else None), dwr, dws[0], dbs[0], dws[1], dbs[1], dws[2], dbs[2], dws[3],
+                dbs[3])
+
+
 class _ConvProjFn(torch.autograd.Function):
     """The dense projections of SBFTransformerConv.forward (sbftransformer_conv.py:99-107,127):
     rf = lin_rbf(rbf), x_src = x * rf, q = lin_query(x), k = lin_key(x_src), v = lin_value(x_src),
@@ -1088,6 +1195,8 @@ def rbf_pool(x, rbf, weight, bias, owner, rowptr, n_seg: int):
 def conv_projections(x, rbf, wr, wq, bq, wk, bk, wv, bv, ws, bs):
     if not x.is_cuda:
         raise RuntimeError("x2gnn device ops need GPU tensors (no CPU fallback by design)")
+    if conv_proj_fused_supported(x, rbf, (wq, wk, wv, ws), (bq, bk, bv, bs)):
+        return _ConvProjFusedFn.apply(x, rbf, wr, wq, bq, wk, bk, wv, bv, ws, bs)
     return _ConvProjFn.apply(x, rbf, wr, wq, bq, wk, bk, wv, bv, ws, bs)
 
 
