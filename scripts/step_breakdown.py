@@ -18,7 +18,7 @@ for st in steps:
     d = defaultdict(float)
     c = defaultdict(int)
     for s, e, n in st:
-        k = n.split("(")[0].replace("void ", "")[:72]
+        k = n.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")[:72]
         d[k] += (e - s) / 1e3
         c[k] += 1
     for k in d:
