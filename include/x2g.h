@@ -566,6 +566,45 @@ int32_t x2g_tiled_wgrad_splits(int64_t rows, int32_t dim, int32_t num_jobs);
 int x2g_tiled_wgrad(const x2g_tiled_job* jobs, int32_t num_jobs, int64_t rows, int32_t dim, int flags,
                     void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------- small-table chains
+ * X2-GNN's edge attribute is the embedding of the middle atom (xgnn.py:57-58), so the embedding
+ * Linear (atom_embedding.py:22-25), edgenn (model.py:39) and every conv layer's lin_edge
+ * (sbftransformer_conv.py:144) act on the per-element table.  Those layers form a tree of D x D
+ * Linear stages on <= 16 rows: stage s reads x (parent -1) or the output of an earlier stage,
+ *     z_s = in_s W_s^T + b_s,   y_s = act_s(z_s).
+ * One workgroup runs the whole tree per direction (one launch instead of one GEMM per layer).
+ * D = 128, rows <= 16 (X2G_EUNSUPPORTED otherwise), 16-byte aligned weights / rows. */
+#define X2G_TABLE_MAX_STAGES 8
+
+typedef struct {
+  const float* w; /* [D, D] nn.Linear weight */
+  const float* b; /* [D] or NULL */
+  int32_t parent; /* -1: x, else an earlier stage (< s) */
+  int32_t act;    /* 0 identity, 1 SiLU */
+  float* z;       /* [rows, D] out: pre-activation (required when act = SiLU), or NULL */
+  float* y;       /* [rows, D] out: the stage output */
+} x2g_table_stage;
+
+int x2g_table_chain_fwd(const float* x, int64_t rows, int32_t dim, const x2g_table_stage* stages, int32_t n_stages,
+                        void* stream);
+
+typedef struct {
+  const float* w;  /* [D, D] the stage's weight */
+  const float* in; /* [rows, D] the stage's forward input (x or the parent's y) */
+  const float* z;  /* [rows, D] saved pre-activation (SiLU stages) */
+  const float* dy; /* [rows, D] dL/dy_s from outside the tree, or NULL (children's shares are added in) */
+  float* dw;       /* [D, D] out: dL/dW_s */
+  float* db;       /* [D] out: dL/db_s, or NULL */
+  int32_t parent;
+  int32_t act;
+  int32_t accum;   /* 1: dw / db += the gradient (a gradient bucket), 0: overwrite */
+} x2g_table_bwd_stage;
+
+/* Backward of x2g_table_chain_fwd (stages in the forward's order): every stage's weight / bias
+ * gradient and dx = dL/dx ([rows, D], may be NULL). */
+int x2g_table_chain_bwd(const x2g_table_bwd_stage* stages, int32_t n_stages, int64_t rows, int32_t dim, float* dx,
+                        void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -947,3 +947,50 @@ def test_conv_projections_fused_vs_layerwise(cuda, R, RR):
         scale = float(r.abs().max()) + 1e-30
         assert float((a.double() - r).abs().max()) <= 2e-5 * scale + 1e-6, i
         assert float((a - b).abs().max()) <= 2e-5 * scale + 1e-6, i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [1, 10, 16])
+def test_table_chain_vs_torch(cuda, R):
+    """x2g_table_chain_fwd / _bwd (ops.table_chain): X2-GNN's element-table tree — embedding Linear
+    (SiLU) -> edgenn (Linear, SiLU, Linear) -> four lin_edge (no bias) — outputs and every input /
+    parameter gradient vs fp64 torch, only some outputs receiving a gradient (as in the trunk); plus
+    the bucket-accumulating path (grad_sink) against the returned gradients."""
+    from x2gnn import ops
+    from x2gnn.layers import Linear
+
+    torch.manual_seed(R)
+    spec = [(-1, 1, True), (0, 1, True), (1, 0, True), (2, 0, False), (2, 0, False), (2, 0, False), (2, 0, False)]
+    lins = [Linear(128, 128, bias=hb).to(cuda) for _, _, hb in spec]
+    x = (0.5 * torch.randn(R, 128, device=cuda)).requires_grad_(True)
+    gys = {s: torch.randn(R, 128, device=cuda) for s in (3, 4, 5, 6)}
+    outs = ops.table_chain(x, [(m, a, p) for m, (p, a, _) in zip(lins, spec)])
+    torch.autograd.backward([outs[s] for s in gys], [gys[s] for s in gys])
+
+    xr = x.detach().double().requires_grad_(True)
+    ws = [m.weight.detach().double().requires_grad_(True) for m in lins]
+    bs = [m.bias.detach().double().requires_grad_(True) if m.bias is not None else None for m in lins]
+    ys = []
+    for s, (p, a, _) in enumerate(spec):
+        z = (xr if p < 0 else ys[p]) @ ws[s].t() + (bs[s] if bs[s] is not None else 0)
+        ys.append(torch.nn.functional.silu(z) if a else z)
+    torch.autograd.backward([ys[s] for s in gys], [gys[s].double() for s in gys])
+    for a, r in zip(outs, ys):
+        torch.testing.assert_close(a.detach().double(), r.detach(), rtol=1e-5, atol=1e-5)
+    pairs = [(x.grad, xr.grad)] + [(m.weight.grad, w.grad) for m, w in zip(lins, ws)]
+    pairs += [(m.bias.grad, b.grad) for m, b in zip(lins, bs) if b is not None]
+    for i, (a, r) in enumerate(pairs):
+        scale = float(r.abs().max()) + 1e-30
+        assert float((a.double() - r).abs().max()) <= 2e-5 * scale + 1e-6, i
+
+    # bucket-backed parameters: the kernel adds into the existing .grad buffers
+    ref = [(m.weight.grad.clone(), m.bias.grad.clone() if m.bias is not None else None) for m in lins]
+    for m in lins:
+        for p in m.parameters():
+            p._x2g_grad_sink = True
+    outs = ops.table_chain(x.detach(), [(m, a, p) for m, (p, a, _) in zip(lins, spec)])
+    torch.autograd.backward([outs[s] for s in gys], [gys[s] for s in gys])
+    for m, (gw, gb) in zip(lins, ref):
+        torch.testing.assert_close(m.weight.grad, 2 * gw, rtol=1e-6, atol=1e-7)
+        if gb is not None:
+            torch.testing.assert_close(m.bias.grad, 2 * gb, rtol=1e-6, atol=1e-7)

@@ -176,30 +176,58 @@ __global__ void __launch_bounds__(256) wgrad_partial(const float* __restrict__ d
   if (do_bias && tid < kWgTile && o0 + tid < O) part_b[static_cast<int64_t>(split) * O + o0 + tid] = bsum;
 }
 
-// out[e] = sum_s part[s][e] in a fixed order: each of the 4 waves of a block sums a quarter of
-// the slabs for the block's 64 elements, then the quarters are added in wave order.
+// out[e] = sum_s part[s][e] in a fixed order: a block owns 256 consecutive elements (4 per lane,
+// one 16-byte load per slab when the slabs allow it), each of its 4 waves sums a quarter of the
+// slabs, then the quarters are added in wave order.  The slabs are read once at 16 B per lane
+// (a wave keeps 8 KB in flight), so the pass runs at stream bandwidth instead of 256-byte requests.
+constexpr int kSlabElems = 256;  // elements per block
+
 __device__ __forceinline__ void sum_slabs_block(const float* __restrict__ part, int64_t n, int splits, int64_t blk,
-                                                bool accum, float* __restrict__ out, float (*red)[64]) {
+                                                bool accum, float* __restrict__ out, float4 (*red)[64]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t e = blk * 64 + lane;
+  const int64_t e = blk * kSlabElems + 4 * lane;
   const int per = (splits + 3) / 4;
   const int k0 = wave * per, k1 = k0 + per < splits ? k0 + per : splits;
-  float s = 0.f;
-  if (e < n) {
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  const bool vec = (n & 3) == 0 && (reinterpret_cast<uintptr_t>(part) & 15) == 0;  // block-uniform
+  if (vec) {
+    if (e < n) {
+      const float4* p = reinterpret_cast<const float4*>(part + e);
+      const int64_t stride = n / 4;
 #pragma unroll 8
-    for (int k = k0; k < k1; ++k) s += part[static_cast<int64_t>(k) * n + e];
+      for (int k = k0; k < k1; ++k) {
+        const float4 v = p[static_cast<int64_t>(k) * stride];
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
+      }
+    }
+  } else {
+    float t[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (e + c < n) {
+#pragma unroll 4
+        for (int k = k0; k < k1; ++k) t[c] += part[static_cast<int64_t>(k) * n + e + c];
+      }
+    s = make_float4(t[0], t[1], t[2], t[3]);
   }
   red[wave][lane] = s;
   __syncthreads();
   if (wave == 0 && e < n) {
-    const float v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
-    out[e] = accum ? out[e] + v : v;
+    const float4 a = red[0][lane], b = red[1][lane], c = red[2][lane], d = red[3][lane];
+    const float v[4] = {((a.x + b.x) + c.x) + d.x, ((a.y + b.y) + c.y) + d.y, ((a.z + b.z) + c.z) + d.z,
+                        ((a.w + b.w) + c.w) + d.w};
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4)
+      if (e + c4 < n) out[e + c4] = accum ? out[e + c4] + v[c4] : v[c4];
   }
 }
 
 __global__ void __launch_bounds__(256) sum_slabs(const float* __restrict__ part, int64_t n, int splits, int accum,
                                                  float* __restrict__ out) {
-  __shared__ float red[4][64];
+  __shared__ float4 red[4][64];
   sum_slabs_block(part, n, splits, blockIdx.x, accum != 0, out, red);
 }
 
@@ -207,8 +235,8 @@ __global__ void __launch_bounds__(256) sum_slabs(const float* __restrict__ part,
 __global__ void __launch_bounds__(256) sum_slabs2(const float* __restrict__ part_a, int64_t na,
                                                   const float* __restrict__ part_b, int64_t nb, int splits, int accum,
                                                   float* __restrict__ out_a, float* __restrict__ out_b) {
-  __shared__ float red[4][64];
-  const int64_t nblk_a = (na + 63) / 64;
+  __shared__ float4 red[4][64];
+  const int64_t nblk_a = (na + kSlabElems - 1) / kSlabElems;
   if (static_cast<int64_t>(blockIdx.x) < nblk_a)
     sum_slabs_block(part_a, na, splits, blockIdx.x, accum != 0, out_a, red);
   else
@@ -219,10 +247,10 @@ __global__ void __launch_bounds__(256) sum_slabs2(const float* __restrict__ part
 int sum_slabs_launch(const float* part_w, int64_t nw, const float* part_b, int64_t nb, int splits, float* dw,
                      float* db, bool accum, hipStream_t st) {
   if (part_b && db)
-    sum_slabs2<<<blocks_for(nw, 64) + blocks_for(nb, 64), 256, 0, st>>>(part_w, nw, part_b, nb, splits, accum,
-                                                                          dw, db);
+    sum_slabs2<<<blocks_for(nw, kSlabElems) + blocks_for(nb, kSlabElems), 256, 0, st>>>(part_w, nw, part_b, nb,
+                                                                                          splits, accum, dw, db);
   else
-    sum_slabs<<<blocks_for(nw, 64), 256, 0, st>>>(part_w, nw, splits, accum, dw);
+    sum_slabs<<<blocks_for(nw, kSlabElems), 256, 0, st>>>(part_w, nw, splits, accum, dw);
   return last_launch_status();
 }
 
@@ -307,13 +335,13 @@ struct SlabBatch {
   float* out[2 * kBatchJobs];
   int64_t n[2 * kBatchJobs];
   int splits[kBatchJobs];
-  int block_end[2 * kBatchJobs];  // exclusive prefix of 64-element blocks
+  int block_end[2 * kBatchJobs];  // exclusive prefix of kSlabElems-element blocks
   int nent;
   int accum;
 };
 
 __global__ void __launch_bounds__(256) sum_slabs_batch(const SlabBatch b) {
-  __shared__ float red[4][64];
+  __shared__ float4 red[4][64];
   int ent = 0;
   while (ent + 1 < b.nent && static_cast<int>(blockIdx.x) >= b.block_end[ent]) ++ent;  // block-uniform
   const int first = ent ? b.block_end[ent - 1] : 0;
@@ -336,12 +364,12 @@ X2G_API int x2g_slab_sum_batch(const x2g_slab_job* jobs, int32_t njobs, int32_t 
       b.part[e0] = jb.part_w;
       b.out[e0] = jb.dw;
       b.n[e0] = jb.n_w;
-      blocks += static_cast<int>(blocks_for(jb.n_w, 64));
+      blocks += static_cast<int>(blocks_for(jb.n_w, kSlabElems));
       b.block_end[e0] = blocks;
       b.part[e1] = jb.part_b;
       b.out[e1] = jb.db;
       b.n[e1] = (jb.part_b && jb.db) ? jb.n_b : 0;
-      blocks += static_cast<int>(blocks_for(b.n[e1], 64));
+      blocks += static_cast<int>(blocks_for(b.n[e1], kSlabElems));
       b.block_end[e1] = blocks;
       b.nent = e1 + 1;
     }

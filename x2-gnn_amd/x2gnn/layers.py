@@ -152,6 +152,16 @@ class EmbeddingBlock(nn.Module):
     def forward(self, atomic_num):
         return self.lin.fused(self.embedding(atomic_num), act=ops.ACT_SILU if self.activate else ops.ACT_NONE)
 
+    def element_rows(self, atomic_num):
+        """The embedding rows [num_embeddings, D] the Linear of ``element_table`` reads (renormalised
+        as the embedding lookup does), from one launch (csrc/embedding.hip); None where that kernel
+        does not apply (CPU, other norms, large vocabularies)."""
+        emb = self.embedding
+        z = atomic_num.reshape(-1)
+        if z.is_cuda and emb.norm_type == 2.0 and emb.num_embeddings <= 64:
+            return ops.embedding_table(emb.weight, z, emb.max_norm, emb.padding_idx, emb.scale_grad_by_freq)
+        return None
+
     def element_table(self, atomic_num):
         """Per-element rows [num_embeddings, D] equal to forward(z) for every z present.
 
@@ -161,8 +171,8 @@ class EmbeddingBlock(nn.Module):
         """
         emb = self.embedding
         z = atomic_num.reshape(-1)
-        if z.is_cuda and emb.norm_type == 2.0 and emb.num_embeddings <= 64:  # one launch (csrc/embedding.hip)
-            w = ops.embedding_table(emb.weight, z, emb.max_norm, emb.padding_idx, emb.scale_grad_by_freq)
+        w = self.element_rows(atomic_num)
+        if w is not None:
             return self.lin.fused(w, act=ops.ACT_SILU if self.activate else ops.ACT_NONE)
         # counts per element without torch.bincount (its output size is data-dependent: a host sync
         # that would also break HIP-graph capture); float counts are exact below 2^24

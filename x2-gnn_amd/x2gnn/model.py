@@ -80,9 +80,23 @@ class _Trunk(nn.Module):
         self.LayerNorm = LayerNorm(in_channels=in_channels, eps=1e-8, affine=False)
         self.conv_layers = conv_layers
 
+    def edge_table_stages(self):
+        """edgenn -> every conv's lin_edge as (Linear, act, parent) stages for ops.table_chain (parent
+        -1 = the element table, 0 = edgenn's output), or None for another layout."""
+        mods = list(self.edgenn)
+        if len(mods) != 3 or not (isinstance(mods[0], Linear) and isinstance(mods[1], SiLU)
+                                  and isinstance(mods[2], Linear)):
+            return None
+        if any(c.lin_edge is None for c in self.convs):
+            return None
+        return ([(mods[0], ops.ACT_SILU, -1), (mods[2], ops.ACT_NONE, 0)]
+                + [(c.lin_edge, ops.ACT_NONE, 1) for c in self.convs])
+
     def _layers(self, data, plan, readout_fn, feature_fn=None):
         per_dst = "edge_attr_row" in data._store
-        edge_attr = run_mlp(self.edgenn, data.edge_attr)
+        edge_proj = data._store.get("_x2g_edge_proj") if per_dst else None
+        # lin_edge tables precomputed by the featurisation's table chain, or edgenn here
+        edge_attr = run_mlp(self.edgenn, data.edge_attr) if edge_proj is None else None
         edge_row = data.edge_attr_row if per_dst else None
         out = data.x
         # The readouts (reference model.py:41,50) hang off the layer chain.  With
@@ -119,7 +133,8 @@ class _Trunk(nn.Module):
         for i in range(self.conv_layers):
             res0 = out
             out = self.convs[i](sbf=data.edge_sbf, rbf=data.node_rbf, x=out, edge_index=data._store.get("edge_index"),
-                                edge_attr=edge_attr, line_graph=plan.lg, edge_row=edge_row)
+                                edge_attr=edge_attr, line_graph=plan.lg, edge_row=edge_row,
+                                edge_proj=edge_proj[i] if edge_proj is not None else None)
             out = self.LayerNorm(out, rowptr=plan.line_ptr, num_graphs=plan.num_graphs)
             out = self._tail(i, out, res0)
             readout(i + 1, out)

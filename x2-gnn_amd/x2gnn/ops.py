@@ -959,6 +959,101 @@ def row_chain(x, res, linears, flags):
     return _ChainFn.apply(x, res, tuple(flags), *params)
 
 
+# ------------------------------------------------------------------------------ small-table chains
+TABLE_MAX_STAGES = 8  # X2G_TABLE_MAX_STAGES
+_TABLE_CHAIN = os.environ.get("X2G_TABLE_CHAIN", "1") == "1"
+
+
+class TableStage(ctypes.Structure):
+    """x2g_table_stage."""
+    _fields_ = [("w", ctypes.c_void_p), ("b", ctypes.c_void_p), ("parent", ctypes.c_int32), ("act", ctypes.c_int32),
+                ("z", ctypes.c_void_p), ("y", ctypes.c_void_p)]
+
+
+class TableBwdStage(ctypes.Structure):
+    """x2g_table_bwd_stage."""
+    _fields_ = [("w", ctypes.c_void_p), ("in_", ctypes.c_void_p), ("z", ctypes.c_void_p), ("dy", ctypes.c_void_p),
+                ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p), ("parent", ctypes.c_int32), ("act", ctypes.c_int32),
+                ("accum", ctypes.c_int32)]
+
+
+def table_chain_supported(x, linears):
+    """True when x2g_table_chain_* cover these layers: D = 128, <= 16 rows, aligned fp32 weights."""
+    if not x.is_cuda or x.dim() != 2 or x.shape[1] != 128 or x.shape[0] > 16:
+        return False
+    if not 1 <= len(linears) <= TABLE_MAX_STAGES:
+        return False
+    for m in linears:
+        if tuple(m.weight.shape) != (128, 128) or m.weight.dtype != torch.float32 or m.weight.data_ptr() % 16:
+            return False
+        if m.bias is not None and (m.bias.dtype != torch.float32 or m.bias.data_ptr() % 16):
+            return False
+    return True
+
+
+class _TableChainFn(torch.autograd.Function):
+    """A tree of D x D Linear stages on a <= 16-row table (x2g_table_chain_fwd/bwd): stage s reads
+    x (parent -1) or an earlier stage's output; one launch per direction for the whole tree."""
+
+    @staticmethod
+    def forward(ctx, x, spec, *params):
+        n = len(spec)
+        x2 = _f32(x).contiguous()
+        R, D = x2.shape
+        dev = x2.device
+        ws = [_f32(p).contiguous() for p in params[0::2]]
+        bs = [_f32(p).contiguous() if p is not None else None for p in params[1::2]]
+        f32 = dict(dtype=torch.float32, device=dev)
+        ys = [torch.empty(R, D, **f32) for _ in range(n)]
+        zs = [torch.empty(R, D, **f32) if spec[s][1] == ACT_SILU else None for s in range(n)]
+        st = (TableStage * n)(*[TableStage(_dp(ws[s]), _dp(bs[s]), spec[s][0], spec[s][1], _dp(zs[s]), _dp(ys[s]))
+                                for s in range(n)])
+        call("x2g_table_chain_fwd", ptr(x2), R, D, st, n, stream_ptr())
+        ctx.save_for_backward(x2, *ws, *ys, *zs)
+        ctx.spec = spec
+        ctx.params = params
+        ctx.set_materialize_grads(False)
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *gys):
+        spec, n = ctx.spec, len(ctx.spec)
+        saved = ctx.saved_tensors
+        x2, ws, ys, zs = saved[0], saved[1:1 + n], saved[1 + n:1 + 2 * n], saved[1 + 2 * n:1 + 3 * n]
+        R, D = x2.shape
+        dev = x2.device
+        dys = [_f32(g).contiguous() if g is not None else None for g in gys]
+        grads, stages = [], []
+        for s in range(n):
+            wp, bp = ctx.params[2 * s], ctx.params[2 * s + 1]
+            gw = grad_sink(wp)
+            gb = grad_sink(bp) if bp is not None else None
+            accum = gw is not None and (bp is None or gb is not None)
+            if accum:
+                dw, db = gw, gb
+                grads += [None, None]
+            else:
+                dw = torch.empty(D, D, dtype=torch.float32, device=dev)
+                db = torch.empty(D, dtype=torch.float32, device=dev) if bp is not None else None
+                grads += [dw, db]
+            par, act = spec[s]
+            src = x2 if par < 0 else ys[par]
+            stages.append(TableBwdStage(_dp(ws[s]), _dp(src), _dp(zs[s]), _dp(dys[s]), _dp(dw), _dp(db), par, act,
+                                        1 if accum else 0))
+        dx = torch.empty(R, D, dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None
+        call("x2g_table_chain_bwd", (TableBwdStage * n)(*stages), n, R, D, ptr(dx), stream_ptr())
+        return (dx, None, *grads)
+
+
+def table_chain(x, stages):
+    """Outputs of every stage of ``stages`` = [(Linear, act, parent), ...] applied to the table x."""
+    params, spec = [], []
+    for m, act, parent in stages:
+        params += [m.weight, m.bias]
+        spec.append((int(parent), int(act)))
+    return _TableChainFn.apply(x, tuple(spec), *params)
+
+
 class TiledJob(ctypes.Structure):
     """x2g_tiled_job."""
     _fields_ = [("dy_t", ctypes.c_void_p), ("x_t", ctypes.c_void_p), ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p)]

@@ -14,9 +14,10 @@ triplet (gathers, logits, softmax, the 42->H*C sbf projection, the weighted sum)
 kernel (``ops.sbf_attention``) without materialising a [T, H*C] tensor.
 
 Extra keyword-only arguments for the in-framework fast path:
-``line_graph`` (a prebuilt ``ops.LineGraph``) and ``edge_row`` (when ``edge_attr`` is a small
+``line_graph`` (a prebuilt ``ops.LineGraph``), ``edge_row`` (when ``edge_attr`` is a small
 table and triplets into line node e use row ``edge_row[e]``: X2-GNN's edge attribute is the
-embedding of the middle atom, identical for all triplets into e, xgnn.py:57-58).
+embedding of the middle atom, identical for all triplets into e, xgnn.py:57-58) and
+``edge_proj`` (``lin_edge(edge_attr)`` already computed, e.g. by the trunk's table chain).
 """
 from __future__ import annotations
 
@@ -54,7 +55,7 @@ class SBFTransformerConv(nn.Module):
         self._alpha = None
 
     def forward(self, sbf, rbf, x, edge_index, edge_attr=None, return_attention_weights=None, *,
-                line_graph: Optional[ops.LineGraph] = None, edge_row=None):
+                line_graph: Optional[ops.LineGraph] = None, edge_row=None, edge_proj=None):
         H, C = self.heads, self.out_channels
         if self.training and self.dropout > 0:
             raise NotImplementedError("attention dropout is not compiled (X2-GNN uses dropout=0)")
@@ -74,7 +75,10 @@ class SBFTransformerConv(nn.Module):
             if edge_index.numel() > 1 and bool((edge_index[1, 1:] < edge_index[1, :-1]).any()):
                 raise ValueError("triplet edge_index[1] must be sorted ascending (vertex_to_edge_2 order)")
             line_graph = ops.LineGraph.from_triplets(edge_index, x.shape[0])
-        if edge_attr is not None and self.lin_edge is not None:
+        if edge_proj is not None:  # lin_edge(edge_attr) computed by the caller (the trunk's table chain)
+            e = edge_proj
+            mode = ops.EDGE_PER_DST if edge_row is not None else ops.EDGE_PER_TRIPLET
+        elif edge_attr is not None and self.lin_edge is not None:
             e = self.lin_edge(edge_attr)
             mode = ops.EDGE_PER_DST if edge_row is not None else ops.EDGE_PER_TRIPLET
         else:

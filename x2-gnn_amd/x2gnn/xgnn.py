@@ -62,12 +62,30 @@ class _XGNNBase(nn.Module):
             node_rbf = self.rbf_layer(dist) * env
             bessel = None
         neo_x = self.mat_trans.fused(data.edge_attr * env, act=ops.ACT_SILU)
-        table = self.emb_block.element_table(data.x)
+        table, edge_proj = self._edge_tables(data.x)
         sbf = self.sbf_layer.from_positions(dist, pos, lg, bessel)
         neo_x = self.emb_trans.fused(neo_x, act=ops.ACT_SILU)
         line = Data(x=neo_x, edge_attr=table, edge_attr_row=plan.dst_type, edge_sbf=sbf, node_rbf=node_rbf)
         line._store["_x2g_plan"] = plan
+        if edge_proj is not None:
+            line._store["_x2g_edge_proj"] = edge_proj
         return line, plan
+
+    def _edge_tables(self, atomic_num):
+        """(element table, per-layer lin_edge tables or None).  The embedding Linear, edgenn and every
+        conv's lin_edge all act on the <= 10-row element table (xgnn.py:57-58): where compiled they
+        run as ONE small-table chain (ops.table_chain, one launch each way); the trunk then reads
+        its lin_edge tables from ``_x2g_edge_proj`` instead of applying edgenn / lin_edge itself."""
+        emb = self.emb_block
+        rows = emb.element_rows(atomic_num) if ops._TABLE_CHAIN else None
+        trunk_stages = self.fin_model.edge_table_stages() if rows is not None else None
+        if trunk_stages is not None:
+            act = ops.ACT_SILU if emb.activate else ops.ACT_NONE
+            stages = [(emb.lin, act, -1)] + [(m, a, p + 1) for (m, a, p) in trunk_stages]
+            if len(stages) <= ops.TABLE_MAX_STAGES and ops.table_chain_supported(rows, [m for m, _, _ in stages]):
+                outs = ops.table_chain(rows, stages)
+                return outs[0], tuple(outs[3:])
+        return emb.element_table(atomic_num), None
 
     def forward(self, data):
         line, plan = self.line_graph_data(data)
