@@ -285,7 +285,9 @@ int x2g_linear_wgrad(const float* dy, const float* x, int64_t rows, int32_t out_
                                 sums many layers' partials in one x2g_slab_sum_batch launch */
 
 /* One deferred weight-gradient reduction: dw[n_w] (+)= sum over `splits` slabs of part_w
- * (slab s at part_w + s*n_w), likewise db[n_b] from part_b (part_b/db may be NULL). */
+ * (slab s at part_w + s*n_w), likewise db[n_b] from part_b (part_b/db may be NULL).
+ * ld > 0: the slab is a [n_w / 128, 128] block of a larger weight: its row r lands at
+ * dw + r * ld, first `cols` (<= 128) columns only (ld = 0: dw is the contiguous n_w block). */
 typedef struct {
   const float* part_w;
   const float* part_b;
@@ -294,6 +296,8 @@ typedef struct {
   int64_t n_w;
   int32_t n_b;
   int32_t splits;
+  int32_t ld;
+  int32_t cols;
 } x2g_slab_job;
 
 /* Sum the slabs of njobs deferred reductions (host array of jobs) in as few launches as
@@ -559,6 +563,8 @@ typedef struct {
   const float* x_t;
   float* dw;
   float* db;
+  int32_t ld;   /* 0: dw is a [D, D] weight; > 0: dw is the top-left of a D x D block of a larger */
+  int32_t cols; /* weight with row stride ld, of which the first `cols` (<= D) columns are written */
 } x2g_tiled_job;
 
 size_t x2g_tiled_wgrad_workspace(int64_t rows, int32_t dim, int32_t num_jobs);
@@ -604,6 +610,24 @@ typedef struct {
  * gradient and dx = dL/dx ([rows, D], may be NULL). */
 int x2g_table_chain_bwd(const x2g_table_bwd_stage* stages, int32_t n_stages, int64_t rows, int32_t dim, float* dx,
                         void* stream);
+
+/* ---------------------------------------------------------------- line-node featurisation
+ * neo_x = SiLU(emb_trans(SiLU(mat_trans(x * env))))  (xgnn.py:49-56 of the reference: mat_trans
+ * 338 -> 256, emb_trans 256 -> 128, x the per-line-node input features, env the envelope).
+ * Forward in one kernel: y [rows, 128] plus the backward's operands in the T layout above with
+ * 128-feature planes (plane p at +p * x2g_chain_t_floats(rows, 128)): xs_t = x * env (3 planes,
+ * features past in_dim zero), z1_t / y1_t = mat_trans pre-activation / output (2 planes),
+ * z2_t = emb_trans pre-activation (1 plane).  Compiled for 256 < in_dim <= 384, in_dim even; w1
+ * [256, in_dim] 8-byte aligned, w2 [128, 256]; env may be NULL (1). */
+int x2g_feat_fwd(const float* x, const float* env, int64_t rows, int32_t in_dim, const float* w1, const float* b1,
+                 const float* w2, const float* b2, float* y, float* xs_t, float* z1_t, float* y1_t, float* z2_t,
+                 void* stream);
+
+/* Data part of the backward: dz2_t = dy SiLU'(z2), dz1_t = (dz2 W2) SiLU'(z1), T layout (1 and 2
+ * planes).  The weight gradients are x2g_tiled_wgrad jobs: dW1 block (o, i) = dz1_t plane o x
+ * xs_t plane i (ld = in_dim, cols = min(128, in_dim - 128 i)), dW2 block i = dz2_t x y1_t plane i. */
+int x2g_feat_bwd(const float* dy, const float* z2_t, const float* z1_t, const float* w2, int64_t rows, float* dz2_t,
+                 float* dz1_t, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1282,7 +1282,9 @@ X2G_API int x2g_tiled_wgrad(const x2g_tiled_job* jobs, int32_t num_jobs, int64_t
     a.part_w[j] = reinterpret_cast<float*>(static_cast<char*>(workspace) + per * j);
     a.part_b[j] = a.part_w[j] + static_cast<int64_t>(a.splits) * kCD * kCD;
     a.has_b[j] = J.db != nullptr;
-    sj[j] = x2g_slab_job{a.part_w[j], J.db ? a.part_b[j] : nullptr, J.dw, J.db, kCD * kCD, J.db ? kCD : 0, a.splits};
+    if (J.ld < 0 || (J.ld > 0 && (J.cols < 1 || J.cols > kCD || J.cols > J.ld))) return X2G_EINVAL;
+    sj[j] = x2g_slab_job{a.part_w[j], J.db ? a.part_b[j] : nullptr, J.dw, J.db, kCD * kCD, J.db ? kCD : 0,
+                         a.splits, J.ld, J.cols};
   }
   chain_wgrad_kernel<<<dim3(static_cast<unsigned>(a.splits), static_cast<unsigned>(num_jobs)), kCThreads, 0,
                        as_stream(stream)>>>(a);

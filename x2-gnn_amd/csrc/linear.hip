@@ -182,8 +182,11 @@ __global__ void __launch_bounds__(256) wgrad_partial(const float* __restrict__ d
 // (a wave keeps 8 KB in flight), so the pass runs at stream bandwidth instead of 256-byte requests.
 constexpr int kSlabElems = 256;  // elements per block
 
+// ld > 0: element e is (row e / 128, column e % 128) of a block written at out + row * ld + column,
+// columns < cols only (a 128-wide slab of a larger weight).
 __device__ __forceinline__ void sum_slabs_block(const float* __restrict__ part, int64_t n, int splits, int64_t blk,
-                                                bool accum, float* __restrict__ out, float4 (*red)[64]) {
+                                                bool accum, float* __restrict__ out, float4 (*red)[64], int ld = 0,
+                                                int cols = 0) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t e = blk * kSlabElems + 4 * lane;
   const int per = (splits + 3) / 4;
@@ -219,9 +222,18 @@ __device__ __forceinline__ void sum_slabs_block(const float* __restrict__ part, 
     const float4 a = red[0][lane], b = red[1][lane], c = red[2][lane], d = red[3][lane];
     const float v[4] = {((a.x + b.x) + c.x) + d.x, ((a.y + b.y) + c.y) + d.y, ((a.z + b.z) + c.z) + d.z,
                         ((a.w + b.w) + c.w) + d.w};
+    if (ld > 0) {  // the 4 elements share a row (128 % 4 == 0)
+      const int64_t row = e >> 7;
+      const int c0 = static_cast<int>(e & 127);
+      float* o = out + row * ld + c0;
 #pragma unroll
-    for (int c4 = 0; c4 < 4; ++c4)
-      if (e + c4 < n) out[e + c4] = accum ? out[e + c4] + v[c4] : v[c4];
+      for (int c4 = 0; c4 < 4; ++c4)
+        if (c0 + c4 < cols) o[c4] = accum ? o[c4] + v[c4] : v[c4];
+    } else {
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4)
+        if (e + c4 < n) out[e + c4] = accum ? out[e + c4] + v[c4] : v[c4];
+    }
   }
 }
 
@@ -336,6 +348,8 @@ struct SlabBatch {
   int64_t n[2 * kBatchJobs];
   int splits[kBatchJobs];
   int block_end[2 * kBatchJobs];  // exclusive prefix of kSlabElems-element blocks
+  int ld[kBatchJobs];             // weight entries: strided destination (x2g_slab_job.ld / cols)
+  int cols[kBatchJobs];
   int nent;
   int accum;
 };
@@ -345,7 +359,9 @@ __global__ void __launch_bounds__(256) sum_slabs_batch(const SlabBatch b) {
   int ent = 0;
   while (ent + 1 < b.nent && static_cast<int>(blockIdx.x) >= b.block_end[ent]) ++ent;  // block-uniform
   const int first = ent ? b.block_end[ent - 1] : 0;
-  sum_slabs_block(b.part[ent], b.n[ent], b.splits[ent >> 1], blockIdx.x - first, b.accum != 0, b.out[ent], red);
+  const bool wgt = (ent & 1) == 0;
+  sum_slabs_block(b.part[ent], b.n[ent], b.splits[ent >> 1], blockIdx.x - first, b.accum != 0, b.out[ent], red,
+                  wgt ? b.ld[ent >> 1] : 0, wgt ? b.cols[ent >> 1] : 0);
 }
 
 X2G_API int x2g_slab_sum_batch(const x2g_slab_job* jobs, int32_t njobs, int32_t accum, void* stream) {
@@ -358,8 +374,12 @@ X2G_API int x2g_slab_sum_batch(const x2g_slab_job* jobs, int32_t njobs, int32_t 
     for (int j = j0; j < njobs && j < j0 + kBatchJobs; ++j) {
       const x2g_slab_job& jb = jobs[j];
       if (!jb.part_w || !jb.dw || jb.n_w <= 0 || jb.splits <= 0 || (jb.part_b && !jb.db)) return X2G_EINVAL;
+      if (jb.ld < 0 || (jb.ld > 0 && (jb.n_w % 128 || jb.cols < 0 || jb.cols > 128 || jb.cols > jb.ld)))
+        return X2G_EINVAL;
       const int k = j - j0;
       b.splits[k] = jb.splits;
+      b.ld[k] = jb.ld;
+      b.cols[k] = jb.cols;
       const int e0 = 2 * k, e1 = 2 * k + 1;
       b.part[e0] = jb.part_w;
       b.out[e0] = jb.dw;

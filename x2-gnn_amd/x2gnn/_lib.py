@@ -99,6 +99,8 @@ SIGNATURES = {
     "x2g_tiled_wgrad": [_P, _I32, _I64, _I32, ctypes.c_int, _P, _SZ, _P],
     "x2g_table_chain_fwd": [_P, _I64, _I32, _P, _I32, _P],
     "x2g_table_chain_bwd": [_P, _I32, _I64, _I32, _P, _P],
+    "x2g_feat_fwd": [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "x2g_feat_bwd": [_P, _P, _P, _P, _I64, _P, _P, _P],
     "x2g_wgrad_batched_workspace": [_I64, _I32, _I32],
     "x2g_wgrad_batched_splits": [_I64, _I32, _I32],
     "x2g_wgrad_batched": [_P, _I32, _I64, _I32, ctypes.c_int, _P, _SZ, _P],

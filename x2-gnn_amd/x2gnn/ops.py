@@ -601,7 +601,8 @@ DEFER_SLAB_SUM = 2  # X2G_DEFER_SLAB_SUM
 class SlabJob(ctypes.Structure):
     """x2g_slab_job (include/x2g.h)."""
     _fields_ = [("part_w", ctypes.c_void_p), ("part_b", ctypes.c_void_p), ("dw", ctypes.c_void_p),
-                ("db", ctypes.c_void_p), ("n_w", ctypes.c_int64), ("n_b", ctypes.c_int32), ("splits", ctypes.c_int32)]
+                ("db", ctypes.c_void_p), ("n_w", ctypes.c_int64), ("n_b", ctypes.c_int32), ("splits", ctypes.c_int32),
+                ("ld", ctypes.c_int32), ("cols", ctypes.c_int32)]
 
 
 class _SlabDeferral:
@@ -630,11 +631,15 @@ def deferred_wgrad():
         _DEFER = prev
 
 
-def _defer_job(ws, offset, splits, n_w, n_b, dw, db):
+def _defer_job(ws, offset, splits, n_w, n_b, dw, db, ld=0, cols=0, dw_ptr=None, db_ptr=None):
+    """Queue one slab reduction (x2g_slab_job); dw_ptr / db_ptr: raw destinations (a block of a
+    larger weight) instead of the tensors' own pointers."""
     base = ws.data_ptr() + int(offset)
-    part_b = base + 4 * splits * n_w if db is not None else None
-    _DEFER.jobs.append(SlabJob(base, part_b, dw.data_ptr(), db.data_ptr() if db is not None else None, n_w,
-                               n_b if db is not None else 0, splits))
+    has_b = db is not None or db_ptr is not None
+    part_b = base + 4 * splits * n_w if has_b else None
+    _DEFER.jobs.append(SlabJob(base, part_b, dw_ptr if dw_ptr is not None else dw.data_ptr(),
+                               (db_ptr if db_ptr is not None else db.data_ptr()) if has_b else None, n_w,
+                               n_b if has_b else 0, splits, ld, cols))
     _DEFER.keep.append(ws)
 
 
@@ -962,6 +967,7 @@ def row_chain(x, res, linears, flags):
 # ------------------------------------------------------------------------------ small-table chains
 TABLE_MAX_STAGES = 8  # X2G_TABLE_MAX_STAGES
 _TABLE_CHAIN = os.environ.get("X2G_TABLE_CHAIN", "1") == "1"
+_FEATURIZE = os.environ.get("X2G_FEATURIZE", "1") == "1"
 
 
 class TableStage(ctypes.Structure):
@@ -1054,9 +1060,103 @@ def table_chain(x, stages):
     return _TableChainFn.apply(x, tuple(spec), *params)
 
 
+# --------------------------------------------------------------------------- line-node featurisation
+def featurize_supported(x, env, lin1, lin2):
+    """True when x2g_feat_fwd/bwd cover SiLU(lin2(SiLU(lin1(x * env)))): x [R, K] fp32 with
+    256 < K <= 384 even and no gradient wanted for x / env, lin1 K -> 256, lin2 256 -> 128."""
+    if not x.is_cuda or x.dim() != 2 or x.dtype != torch.float32 or x.requires_grad:
+        return False
+    R, K = x.shape
+    if not (256 < K <= 384 and K % 2 == 0) or R * 384 >= 2 ** 31:
+        return False
+    if env is not None and (env.numel() != R or env.requires_grad):
+        return False
+    if tuple(lin1.weight.shape) != (256, K) or tuple(lin2.weight.shape) != (128, 256):
+        return False
+    for p in (lin1.weight, lin1.bias, lin2.weight, lin2.bias):
+        if p is not None and (p.dtype != torch.float32 or p.data_ptr() % 16):
+            return False
+    return True
+
+
+class _FeaturizeFn(torch.autograd.Function):
+    """neo_x = SiLU(W2 SiLU(W1 (x * env) + b1) + b2) (xgnn.py:64-67): one forward kernel, one
+    backward data kernel and one 8-job T-layout weight-gradient launch (csrc/feature.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, env, w1, b1, w2, b2):
+        x2 = _f32(x)
+        R, K = x2.shape
+        dev = x2.device
+        tf = int(_lib.load().x2g_chain_t_floats(R, 128))
+        f32 = dict(dtype=torch.float32, device=dev)
+        y = torch.empty(R, 128, **f32)
+        xs_t, z1_t, y1_t, z2_t = (torch.empty(max(n * tf, 1), **f32) for n in (3, 2, 2, 1))
+        e = _f32(env.reshape(-1)) if env is not None else None
+        W1, W2 = _f32(w1), _f32(w2)
+        B1 = _f32(b1) if b1 is not None else None
+        B2 = _f32(b2) if b2 is not None else None
+        call("x2g_feat_fwd", ptr(x2), ptr(e), R, K, ptr(W1), ptr(B1), ptr(W2), ptr(B2), ptr(y), ptr(xs_t), ptr(z1_t),
+             ptr(y1_t), ptr(z2_t), stream_ptr())
+        ctx.save_for_backward(xs_t, z1_t, y1_t, z2_t, W2)
+        ctx.R, ctx.K, ctx.tf = R, K, tf
+        ctx.params = (w1, b1, w2, b2)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xs_t, z1_t, y1_t, z2_t, W2 = ctx.saved_tensors
+        R, K, tf = ctx.R, ctx.K, ctx.tf
+        dev = gy.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        dz2_t, dz1_t = torch.empty(max(tf, 1), **f32), torch.empty(max(2 * tf, 1), **f32)
+        call("x2g_feat_bwd", ptr(_f32(gy)), ptr(z2_t), ptr(z1_t), ptr(W2), R, ptr(dz2_t), ptr(dz1_t), stream_ptr())
+        w1, b1, w2, b2 = ctx.params
+        params = [p for p in (w1, b1, w2, b2) if p is not None]
+        bufs, acc = _wgrad_targets(params, [tuple(p.shape) for p in params], dev)
+        it = iter(bufs)
+        dw1 = next(it)
+        db1 = next(it) if b1 is not None else None
+        dw2 = next(it)
+        db2 = next(it) if b2 is not None else None
+        fb = 4  # bytes per float
+        specs = []  # (dy_t, x_t, dw pointer, db pointer, ld, cols)
+        for o in range(2):
+            for i in range(3):
+                specs.append((dz1_t.data_ptr() + fb * o * tf, xs_t.data_ptr() + fb * i * tf,
+                              dw1.data_ptr() + fb * (o * 128 * K + i * 128),
+                              db1.data_ptr() + fb * o * 128 if (db1 is not None and i == 0) else None, K,
+                              min(128, K - 128 * i)))
+        for i in range(2):
+            specs.append((dz2_t.data_ptr(), y1_t.data_ptr() + fb * i * tf, dw2.data_ptr() + fb * i * 128,
+                          db2.data_ptr() if (db2 is not None and i == 0) else None, 256, 128))
+        n = len(specs)
+        lib = _lib.load()
+        ws_bytes = int(lib.x2g_tiled_wgrad_workspace(R, 128, n))
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        jobs = (TiledJob * n)(*[TiledJob(*sp) for sp in specs])
+        defer = acc and _DEFER is not None
+        call("x2g_tiled_wgrad", jobs, n, R, 128, (ACCUM_WGRAD if acc else 0) | (DEFER_SLAB_SUM if defer else 0),
+             ptr(ws), ws_bytes, stream_ptr())
+        if defer:
+            splits = int(lib.x2g_tiled_wgrad_splits(R, 128, n))
+            per = ws_bytes // n
+            for g, (_, _, dwp, dbp, ld, cols) in enumerate(specs):
+                _defer_job(ws, g * per, splits, 128 * 128, 128, None, None, ld=ld, cols=cols, dw_ptr=dwp, db_ptr=dbp)
+        if acc:
+            return None, None, None, None, None, None
+        return None, None, dw1, db1, dw2, db2
+
+
+def featurize(x, env, lin1, lin2):
+    """SiLU(lin2(SiLU(lin1(x * env[:, None])))) through the fused featurisation kernels."""
+    return _FeaturizeFn.apply(x, env, lin1.weight, lin1.bias, lin2.weight, lin2.bias)
+
+
 class TiledJob(ctypes.Structure):
     """x2g_tiled_job."""
-    _fields_ = [("dy_t", ctypes.c_void_p), ("x_t", ctypes.c_void_p), ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p)]
+    _fields_ = [("dy_t", ctypes.c_void_p), ("x_t", ctypes.c_void_p), ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p),
+                ("ld", ctypes.c_int32), ("cols", ctypes.c_int32)]
 
 
 class Proj(ctypes.Structure):

@@ -61,10 +61,15 @@ class _XGNNBase(nn.Module):
             env = self.envelop_function(dist).unsqueeze(1)
             node_rbf = self.rbf_layer(dist) * env
             bessel = None
-        neo_x = self.mat_trans.fused(data.edge_attr * env, act=ops.ACT_SILU)
+        fused_feat = ops._FEATURIZE and ops.featurize_supported(data.edge_attr, env, self.mat_trans, self.emb_trans)
+        if fused_feat:  # both Linear layers, the envelope scale and SiLUs in one kernel (csrc/feature.hip)
+            neo_x = ops.featurize(data.edge_attr, env, self.mat_trans, self.emb_trans)
+        else:
+            neo_x = self.mat_trans.fused(data.edge_attr * env, act=ops.ACT_SILU)
         table, edge_proj = self._edge_tables(data.x)
         sbf = self.sbf_layer.from_positions(dist, pos, lg, bessel)
-        neo_x = self.emb_trans.fused(neo_x, act=ops.ACT_SILU)
+        if not fused_feat:
+            neo_x = self.emb_trans.fused(neo_x, act=ops.ACT_SILU)
         line = Data(x=neo_x, edge_attr=table, edge_attr_row=plan.dst_type, edge_sbf=sbf, node_rbf=node_rbf)
         line._store["_x2g_plan"] = plan
         if edge_proj is not None:
