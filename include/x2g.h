@@ -129,10 +129,12 @@ int x2g_rbf_pool_fwd(const float* x, const float* rbf, const float* w, const flo
                      int64_t num_segments, int32_t D, int32_t R, float* out, void* stream);
 
 /* Backward of both: g_row(e) = g[e] (gate, owner == NULL) or g[owner[e]] (pool):
- *   dx[e] = g_row * f[e] (+ dx_add[e]; dx may alias dx_add),  drbf[e, j] = sum_c (g_row x[e])_c w[c, j],
+ *   dx[e] = g_row * f[e] (+ dx_add[e]; dx may alias dx_add),  drbf[e, j] (+)= sum_c (g_row x[e])_c w[c, j]
+ *   (added to drbf's contents with flags X2G_GATE_DRBF_ACCUM: the rbf feeds every layer's gate),
  *   dw[c, j] (+)= sum_e (g_row x[e])_c rbf[e, j],  db[c] (+)= sum_e (g_row x[e])_c   (db optional).
  * dx / drbf may be NULL (not needed).  Weight gradients: per-workgroup partials + fixed-order
  * sum, flags as x2g_linear_wgrad_ex (slabs of D*R then D floats at the start of the workspace). */
+#define X2G_GATE_DRBF_ACCUM 4
 size_t x2g_rbf_gate_bwd_workspace(int64_t rows, int32_t D, int32_t R);
 int32_t x2g_rbf_gate_bwd_splits(int64_t rows);
 int x2g_rbf_gate_bwd(const float* g, const int32_t* owner, const float* x, const float* rbf, const float* w,
@@ -459,6 +461,8 @@ int x2g_clip_adam_ema(float* params, const float* grads, float* exp_avg, float* 
 #define X2G_CHAIN_RES_HELD 4 /* out_s += the held residual */
 #define X2G_CHAIN_RES_EXT 8  /* out_s += res_ext (at most one stage; a HOLD .. RES_HELD pair must
                                 not span it, and a stage adds one residual at most) */
+#define X2G_CHAIN_RES_ACCUM 16 /* backward only, with RES_EXT: d_res_ext += (instead of =) the
+                                  residual's gradient (res_ext feeds other layers too) */
 
 typedef struct {
   const float* w; /* [D, D] nn.Linear weight, row n = output feature n */

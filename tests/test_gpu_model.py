@@ -339,3 +339,39 @@ def test_factorised_sbf_backward_equals_two_pass(cuda, monkeypatch, shape):
             # lin_key.bias: analytically zero (softmax shift invariance) -> weight-gradient scale
             scale = float(ref_grads[n.replace("lin_key.bias", "lin_key.weight")].abs().max())
             assert float((g - ref).abs().max()) <= 1e-5 * scale + 1e-9, n
+
+
+def test_fan_in_gradients_match_autograd_adds(cuda):
+    """ops.FanIn (layer inputs and the radial basis summed in place by the fused ops' backward,
+    csrc: dx_add / X2G_GATE_DRBF_ACCUM / X2G_CHAIN_RES_ACCUM) gives the same parameter gradients as
+    autograd's own fan-in adds, at the BASELINE width (every fused path active)."""
+    import x2gnn
+    from x2gnn import ops
+    from x2gnn.data import collate
+    from x2gnn.synth import synthetic_molecules
+
+    cfg = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embedding_size=128)
+    b = collate(synthetic_molecules(6, "S160", seed=3)).to(cuda)
+    m = x2gnn.xgnn_poly(device="cuda", **cfg)
+    load_seeded(m, 11)
+    m = m.to(cuda)
+    grads = []
+    for fan in (True, False):
+        ops._FAN_IN = fan
+        try:
+            m.zero_grad(set_to_none=True)
+            line, plan = m.line_graph_data(b)
+            assert m.fin_model._fan_in_ok(line, line.x) == fan
+            e = m(b)
+            (e * torch.linspace(0.5, 1.5, e.numel(), device=cuda)).sum().backward()
+            grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None})
+        finally:
+            ops._FAN_IN = True
+    assert grads[0].keys() == grads[1].keys() and len(grads[0]) > 20
+    top = max(float(g.abs().max()) for g in grads[1].values())
+    for n in grads[0]:
+        a, r = grads[0][n], grads[1][n]
+        scale = float(r.abs().max())
+        # (summation order differs; gradients that vanish analytically, e.g. the key bias under the
+        # softmax's shift invariance, are compared at the model's gradient scale)
+        assert float((a - r).abs().max()) <= 1e-5 * scale + 1e-6 * top, n

@@ -591,7 +591,10 @@ __global__ void __launch_bounds__(kCThreads, 1) chain_bwd_v2(const ChainBwdArgs 
         const int r = 16 * rb + rl;
         const bool ok = r < nrows;
         if (fl & X2G_CHAIN_RES_HELD) dh[rb] += gs[rb];
-        if ((fl & X2G_CHAIN_RES_EXT) && a.dres && ok) *reinterpret_cast<f4*>(a.dres + (r0 + r) * kCD + col) = gs[rb];
+        if ((fl & X2G_CHAIN_RES_EXT) && a.dres && ok) {
+          f4* dr = reinterpret_cast<f4*>(a.dres + (r0 + r) * kCD + col);
+          *dr = (fl & X2G_CHAIN_RES_ACCUM) ? *dr + gs[rb] : gs[rb];
+        }
         f4 dz = gs[rb];
         if (fl & X2G_CHAIN_SILU) {
 #pragma unroll
@@ -1085,15 +1088,19 @@ X2G_API int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_
   a.R = rows;
   a.n = n_stages;
   int n_ext = 0, held = 0;
+  bool res_accum = false;
   for (int s = 0; s < n_stages; ++s) {
     const x2g_chain_bwd_stage& S = stages[s];
     if (!S.w || ((S.flags & X2G_CHAIN_SILU) && !S.z)) return X2G_EINVAL;
-    if (S.flags & ~(X2G_CHAIN_SILU | X2G_CHAIN_HOLD | X2G_CHAIN_RES_HELD | X2G_CHAIN_RES_EXT)) return X2G_EINVAL;
+    if (S.flags & ~(X2G_CHAIN_SILU | X2G_CHAIN_HOLD | X2G_CHAIN_RES_HELD | X2G_CHAIN_RES_EXT | X2G_CHAIN_RES_ACCUM))
+      return X2G_EINVAL;
+    if ((S.flags & X2G_CHAIN_RES_ACCUM) && !(S.flags & X2G_CHAIN_RES_EXT)) return X2G_EINVAL;
     if ((S.flags & X2G_CHAIN_RES_EXT) && (S.flags & (X2G_CHAIN_HOLD | X2G_CHAIN_RES_HELD))) return X2G_EINVAL;
     if (S.flags & X2G_CHAIN_RES_EXT) held = 0;
     if (S.flags & X2G_CHAIN_HOLD) held = 1;
     if ((S.flags & X2G_CHAIN_RES_HELD) && !held) return X2G_EINVAL;
     if (S.flags & X2G_CHAIN_RES_EXT) ++n_ext;
+    if (S.flags & X2G_CHAIN_RES_ACCUM) res_accum = true;
     if (!al16(S.w) || !al16(S.wt) || !al16(S.z) || !al16(S.dz)) return X2G_EUNSUPPORTED;
     a.st[s] = S;
   }
@@ -1103,6 +1110,7 @@ X2G_API int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_
   if (!al16(dy) || !al16(dy_add) || !al16(dx) || !al16(d_res_ext) || !al16(dz_t)) return X2G_EUNSUPPORTED;
   hipStream_t st = as_stream(stream);
   if (tuning(kTuneChain) == 1 && !dz_t) {
+    if (res_accum) return X2G_EUNSUPPORTED;  // the register-tile kernel overwrites d_res_ext
     const int64_t groups = ((rows + 15) / 16 + kCWaves - 1) / kCWaves;
     chain_bwd_kernel<<<static_cast<unsigned>(groups < 256 ? groups : 256), kCThreads, 0, st>>>(a);
   } else {

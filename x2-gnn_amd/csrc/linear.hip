@@ -356,8 +356,15 @@ struct SlabBatch {
 
 __global__ void __launch_bounds__(256) sum_slabs_batch(const SlabBatch b) {
   __shared__ float4 red[4][64];
-  int ent = 0;
-  while (ent + 1 < b.nent && static_cast<int>(blockIdx.x) >= b.block_end[ent]) ++ent;  // block-uniform
+  // the entry owning this block: first ent with block_end[ent] > blockIdx.x (binary search over the
+  // kernel-argument table, block-uniform)
+  int lo = 0, hi = b.nent - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (static_cast<int>(blockIdx.x) >= b.block_end[mid]) lo = mid + 1;
+    else hi = mid;
+  }
+  const int ent = lo;
   const int first = ent ? b.block_end[ent - 1] : 0;
   const bool wgt = (ent & 1) == 0;
   sum_slabs_block(b.part[ent], b.n[ent], b.splits[ent >> 1], blockIdx.x - first, b.accum != 0, b.out[ent], red,

@@ -177,7 +177,8 @@ __global__ void __launch_bounds__(256) rbf_gate_bwd_kernel(const f4v* __restrict
                                                            const float* __restrict__ W, const float* __restrict__ B,
                                                            int64_t rows, int R, f4v* __restrict__ dx,
                                                            const f4v* __restrict__ dx_add, float* __restrict__ drbf,
-                                                           float* __restrict__ part_w, float* __restrict__ part_b) {
+                                                           int drbf_acc, float* __restrict__ part_w,
+                                                           float* __restrict__ part_b) {
   constexpr int RPB = 256 / LPR;
   constexpr int D = 4 * LPR;
   __shared__ float red[RPB * D * (kGateRMax + 1)];
@@ -194,15 +195,20 @@ __global__ void __launch_bounds__(256) rbf_gate_bwd_kernel(const f4v* __restrict
     for (int j = 0; j < kGateRMax; ++j) aw[i][j] = 0.f;
   }
   constexpr int UNROLL = 2;
+  // the drbf element this lane writes (transpose_sum's j); its old value is loaded with the rows
+  const int jd = 4 * ((sub & (LPR / 2)) != 0) + 2 * ((sub & (LPR / 4)) != 0) + ((sub & (LPR / 8)) != 0);
+  const bool acc_drbf = drbf && drbf_acc && jd < R;
   const int64_t per = (rows + gridDim.x - 1) / gridDim.x;
   const int64_t lo = per * blockIdx.x, hi = lo + per < rows ? lo + per : rows;
   for (int64_t r0 = lo + slot; r0 < hi; r0 += RPB * UNROLL) {
     float rb[UNROLL][kGateRMax];
     f4v gv[UNROLL], xv[UNROLL], av[UNROLL];
+    float od[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {  // every load of the UNROLL rows first
       const int64_t r = r0 + u * RPB, rc = r < hi ? r : hi - 1;
       load_rbf(rbf, rc, R, rb[u]);
+      od[u] = acc_drbf ? drbf[rc * R + jd] : 0.0f;
       const int64_t o = owner ? owner[rc] : rc;
       gv[u] = g[o * LPR + sub];
       xv[u] = x[rc * LPR + sub];
@@ -236,7 +242,7 @@ __global__ void __launch_bounds__(256) rbf_gate_bwd_kernel(const f4v* __restrict
         }
         int j;
         const float tot = transpose_sum<LPR>(p, sub, j);
-        if ((sub & (LPR / 8 - 1)) == 0 && ok && j < R) drbf[r * R + j] = tot;
+        if ((sub & (LPR / 8 - 1)) == 0 && ok && j < R) drbf[r * R + j] = tot + od[u];  // od = 0 unless accumulating
       }
     }
   }
@@ -325,7 +331,9 @@ X2G_API int x2g_rbf_gate_bwd(const float* g, const int32_t* owner, const float* 
   if (rows < 0 || !dw) return X2G_EINVAL;
   if (!gate_shape_ok(D, R)) return X2G_EUNSUPPORTED;
   if (dx_add && !dx) return X2G_EINVAL;
+  if (flags & ~(X2G_ACCUM_WGRAD | X2G_DEFER_SLAB_SUM | X2G_GATE_DRBF_ACCUM)) return X2G_EINVAL;
   const bool accum = flags & X2G_ACCUM_WGRAD;
+  const int drbf_acc = (flags & X2G_GATE_DRBF_ACCUM) ? 1 : 0;
   hipStream_t st = as_stream(stream);
   if (rows == 0) {
     if (flags & X2G_DEFER_SLAB_SUM) return X2G_EINVAL;
@@ -346,16 +354,16 @@ X2G_API int x2g_rbf_gate_bwd(const float* g, const int32_t* owner, const float* 
   const auto* dav = reinterpret_cast<const f4v*>(dx_add);
   switch (D) {
     case 64:
-      rbf_gate_bwd_kernel<16><<<splits, 256, 0, st>>>(gv, owner, xv, rbf, w, b, rows, R, dxv, dav, drbf, part_w,
-                                                       part_b);
+      rbf_gate_bwd_kernel<16><<<splits, 256, 0, st>>>(gv, owner, xv, rbf, w, b, rows, R, dxv, dav, drbf, drbf_acc,
+                                                       part_w, part_b);
       break;
     case 128:
-      rbf_gate_bwd_kernel<32><<<splits, 256, 0, st>>>(gv, owner, xv, rbf, w, b, rows, R, dxv, dav, drbf, part_w,
-                                                       part_b);
+      rbf_gate_bwd_kernel<32><<<splits, 256, 0, st>>>(gv, owner, xv, rbf, w, b, rows, R, dxv, dav, drbf, drbf_acc,
+                                                       part_w, part_b);
       break;
     default:
-      rbf_gate_bwd_kernel<64><<<splits, 256, 0, st>>>(gv, owner, xv, rbf, w, b, rows, R, dxv, dav, drbf, part_w,
-                                                       part_b);
+      rbf_gate_bwd_kernel<64><<<splits, 256, 0, st>>>(gv, owner, xv, rbf, w, b, rows, R, dxv, dav, drbf, drbf_acc,
+                                                       part_w, part_b);
       break;
   }
   if (int rc = last_launch_status()) return rc;

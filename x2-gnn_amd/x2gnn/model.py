@@ -129,6 +129,11 @@ class _Trunk(nn.Module):
                 results = r if results is None else results + r
             x.record_stream(side)
 
+        # gradient fan-in in place: the layer inputs and the radial basis feed several fused ops each
+        fan = self._fan_in_ok(data, out)
+        if fan:
+            data.node_rbf._x2g_fanin = ops.FanIn()
+            out._x2g_fanin = ops.FanIn()
         readout(0, out)
         for i in range(self.conv_layers):
             res0 = out
@@ -137,6 +142,8 @@ class _Trunk(nn.Module):
                                 edge_proj=edge_proj[i] if edge_proj is not None else None)
             out = self.LayerNorm(out, rowptr=plan.line_ptr, num_graphs=plan.num_graphs)
             out = self._tail(i, out, res0)
+            if fan:
+                out._x2g_fanin = ops.FanIn()
             readout(i + 1, out)
         if side is not None:
             main.wait_stream(side)
@@ -151,12 +158,34 @@ class _Trunk(nn.Module):
         return results
 
 
-    def _tail(self, i, out, res0):
-        """bf_skip -> SiLU(dense_bf_skip(.)) + res0 -> af_skip (model.py:47-50): one row-chain
-        kernel each way (ops.row_chain, 7 Linear stages) where compiled, else layer by layer."""
+    def _tail_linears(self, i):
         lins = [self.bf_skip[i].lin0, self.bf_skip[i].lin1, self.dense_bf_skip[i]]
         for r in self.af_skip[i]:
             lins += [r.lin0, r.lin1]
+        return lins
+
+    def _fan_in_ok(self, data, x):
+        """True when every consumer of the layer inputs (readout rbf pool, conv projections, the
+        tail's residual) and of the radial basis (readout pools, conv gates) is a fan-aware fused op,
+        so their input gradients can be summed in place (ops.FanIn) instead of by autograd adds."""
+        if not (ops._FAN_IN and x.is_cuda and x.dim() == 2 and torch.is_grad_enabled()):
+            return False
+        rbf = data.node_rbf
+        if rbf is None or not ops.gate_supported(x.shape[1], rbf.shape[1]):
+            return False
+        for i, c in enumerate(self.convs):
+            if not c.root_weight or not ops.conv_proj_fused_supported(
+                    x, rbf, (c.lin_query.weight, c.lin_key.weight, c.lin_value.weight, c.lin_skip.weight),
+                    (c.lin_query.bias, c.lin_key.bias, c.lin_value.bias, c.lin_skip.bias)):
+                return False
+            if not (ops._CHAIN and ops.chain_supported(x, self._tail_linears(i))):
+                return False
+        return True
+
+    def _tail(self, i, out, res0):
+        """bf_skip -> SiLU(dense_bf_skip(.)) + res0 -> af_skip (model.py:47-50): one row-chain
+        kernel each way (ops.row_chain, 7 Linear stages) where compiled, else layer by layer."""
+        lins = self._tail_linears(i)
         if ops._CHAIN and ops.chain_supported(out, lins):
             S, H, RH, RE = ops.CHAIN_SILU, ops.CHAIN_HOLD, ops.CHAIN_RES_HELD, ops.CHAIN_RES_EXT
             flags = [S | H, S | RH, S | RE, S | H, S | RH, S | H, S | RH]

@@ -596,6 +596,7 @@ def sbf_attention(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg: LineGraph, heads: 
 # ---------------------------------------------------------------------------------- dense layers
 ACCUM_WGRAD = 1  # X2G_ACCUM_WGRAD
 DEFER_SLAB_SUM = 2  # X2G_DEFER_SLAB_SUM
+GATE_DRBF_ACCUM = 4  # X2G_GATE_DRBF_ACCUM
 
 
 class SlabJob(ctypes.Structure):
@@ -656,6 +657,44 @@ def grad_sink(param):
     if g is None or not g.is_contiguous() or g.dtype != torch.float32:
         return None
     return g
+
+
+class FanIn:
+    """In-place gradient fan-in for a tensor every consumer of which is an x2g op that can add its
+    share into a buffer (dx_add, X2G_GATE_DRBF_ACCUM, X2G_CHAIN_RES_ACCUM): the first consumer whose
+    backward runs writes the buffer and returns it as its gradient, every later one adds into it
+    in place and returns None.  Autograd runs the tensor's producer only after ALL consumers, so the
+    producer sees the full sum — without the add kernel autograd would launch per extra consumer.
+
+    Attach with ``t._x2g_fanin = FanIn()`` only when every consumer of ``t`` is fan-aware (a plain
+    consumer's gradient could be summed with the buffer out of place, and later in-place adds would
+    then be lost).  The trunk attaches one per layer input and one to the radial basis."""
+
+    def __init__(self):
+        self.buf = None
+        self.registered = 0
+        self.used = 0
+
+    def register(self):
+        self.registered += 1
+        return self
+
+    def take(self, shape, device):
+        """(buffer, first) for one consumer's backward."""
+        first = self.buf is None
+        if first:
+            self.buf = torch.empty(shape, dtype=torch.float32, device=device)
+        buf = self.buf
+        self.used += 1
+        if self.used >= self.registered:  # the last consumer: the next backward starts afresh
+            self.buf, self.used = None, 0
+        return buf, first
+
+
+def _fan_of(t):
+    """The FanIn attached to ``t`` (registered as one more consumer), or None."""
+    f = getattr(t, "_x2g_fanin", None) if t is not None else None
+    return f.register() if f is not None else None
 
 
 def linear_wgrad(dy, x, bias=True, dw_out=None, db_out=None):
@@ -805,6 +844,7 @@ def residual_layer(x, w0, b0, w1, b1):
 
 
 CHAIN_SILU, CHAIN_HOLD, CHAIN_RES_HELD, CHAIN_RES_EXT = 1, 2, 4, 8  # X2G_CHAIN_* (include/x2g.h)
+CHAIN_RES_ACCUM = 16  # backward only
 CHAIN_MAX_STAGES = 8
 
 
@@ -870,7 +910,7 @@ def chain_wgrad(in_t, dz_t, R, weights, biases):
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     dw_arr = (ctypes.c_void_p * n)(*[_dp(t) for t in dws])
     db_arr = (ctypes.c_void_p * n)(*[_dp(t) for t in dbs])
-    defer = acc and _DEFER is not None
+    defer = acc and _DEFER is not None and _DEFER_TILED
     call("x2g_chain_wgrad", ptr(in_t), ptr(dz_t), n, R, D, dw_arr, db_arr,
          (ACCUM_WGRAD if acc else 0) | (DEFER_SLAB_SUM if defer else 0), ptr(ws), ws_bytes, stream_ptr())
     if defer:
@@ -913,6 +953,7 @@ class _ChainFn(torch.autograd.Function):
         if grad:
             ctx.save_for_backward(*W, *[z if z is not None else x2 for z in zs], WT, in_t)
         ctx.flags, ctx.params, ctx.has_res = tuple(flags), params, res is not None
+        ctx.fan_res = _fan_of(res)
         return y
 
     @staticmethod
@@ -926,9 +967,15 @@ class _ChainFn(torch.autograd.Function):
         f32 = dict(dtype=torch.float32, device=gy2.device)
         dz_t = torch.empty_like(in_t)
         dx = torch.empty(R, D, **f32)
-        dres = torch.empty(R, D, **f32) if ctx.has_res else None
+        dres, first = None, True
+        if ctx.has_res and ctx.needs_input_grad[1]:
+            if ctx.fan_res is not None:  # add into the layer input's fan-in buffer
+                dres, first = ctx.fan_res.take((R, D), gy2.device)
+            else:
+                dres = torch.empty(R, D, **f32)
+        bflags = [f | (CHAIN_RES_ACCUM if (f & CHAIN_RES_EXT) and not first else 0) for f in flags]
         st = (ChainBwdStage * n)(*[ChainBwdStage(_dp(W[i]), WT[i].data_ptr(),
-                                                 _dp(zs[i]) if flags[i] & CHAIN_SILU else None, None, flags[i])
+                                                 _dp(zs[i]) if flags[i] & CHAIN_SILU else None, None, bflags[i])
                                    for i in range(n)])
         call("x2g_chain_bwd", ptr(gy2), None, st, n, R, D, ptr(dx), ptr(dres), ptr(dz_t), stream_ptr())
         ws, bs = ctx.params[0::2], ctx.params[1::2]
@@ -936,7 +983,7 @@ class _ChainFn(torch.autograd.Function):
         grads = []
         for i in range(n):
             grads += [dws[i], dbs[i]]
-        return (dx, dres, None, *grads)
+        return (dx, dres if first else None, None, *grads)
 
 
 def chain_supported(x, linears):
@@ -968,6 +1015,10 @@ def row_chain(x, res, linears, flags):
 TABLE_MAX_STAGES = 8  # X2G_TABLE_MAX_STAGES
 _TABLE_CHAIN = os.environ.get("X2G_TABLE_CHAIN", "1") == "1"
 _FEATURIZE = os.environ.get("X2G_FEATURIZE", "1") == "1"
+_FAN_IN = os.environ.get("X2G_FAN_IN", "1") == "1"
+# T-layout weight gradients (chain / projections / featurisation): 1 = their slab sums join the one
+# deferred batch at the end of the backward, 0 = summed right after each launch (slabs still in MALL)
+_DEFER_TILED = os.environ.get("X2G_DEFER_TILED", "1") == "1"
 
 
 class TableStage(ctypes.Structure):
@@ -1135,7 +1186,7 @@ class _FeaturizeFn(torch.autograd.Function):
         ws_bytes = int(lib.x2g_tiled_wgrad_workspace(R, 128, n))
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
         jobs = (TiledJob * n)(*[TiledJob(*sp) for sp in specs])
-        defer = acc and _DEFER is not None
+        defer = acc and _DEFER is not None and _DEFER_TILED
         call("x2g_tiled_wgrad", jobs, n, R, 128, (ACCUM_WGRAD if acc else 0) | (DEFER_SLAB_SUM if defer else 0),
              ptr(ws), ws_bytes, stream_ptr())
         if defer:
@@ -1184,7 +1235,7 @@ def tiled_wgrad(dy_ts, x_ts, R, weights, biases):
     ws_bytes = int(lib.x2g_tiled_wgrad_workspace(R, D, n))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     jobs = (TiledJob * n)(*[TiledJob(_dp(dy_ts[g]), _dp(x_ts[g]), _dp(dws[g]), _dp(dbs[g])) for g in range(n)])
-    defer = acc and _DEFER is not None
+    defer = acc and _DEFER is not None and _DEFER_TILED
     call("x2g_tiled_wgrad", jobs, n, R, D, (ACCUM_WGRAD if acc else 0) | (DEFER_SLAB_SUM if defer else 0), ptr(ws),
          ws_bytes, stream_ptr())
     if defer:
@@ -1236,6 +1287,7 @@ class _ConvProjFusedFn(torch.autograd.Function):
         if grad:
             ctx.save_for_backward(x2, rbf2, Wr, *W, WT, x_t, xs_t)
         ctx.params = (wr, wq, bq, wk, bk, wv, bv, ws, bs)
+        ctx.fan_x, ctx.fan_r = _fan_of(x), _fan_of(rbf)
         return tuple(outs)
 
     @staticmethod
@@ -1250,11 +1302,21 @@ class _ConvProjFusedFn(torch.autograd.Function):
         W = (Wq, Wk, Wv, Ws)
         grads = (ProjGrad * 4)(*[ProjGrad(_dp(g[i]), _dp(W[i]), WT[i].data_ptr(), g_t[i].data_ptr())
                                  for i in range(4)])
-        dx = torch.empty(E, D, **f32)
+        first_x = first_r = True
+        if ctx.fan_x is not None:  # dx goes into (or adds onto) the layer input's fan-in buffer
+            dx, first_x = ctx.fan_x.take((E, D), x2.device)
+        else:
+            dx = torch.empty(E, D, **f32)
         dxs = torch.empty(E, D, **f32)
-        call("x2g_conv_proj_bwd", grads, E, D, ptr(dx), None, ptr(dxs), stream_ptr())
+        call("x2g_conv_proj_bwd", grads, E, D, ptr(dx), None if first_x else ptr(dx), ptr(dxs), stream_ptr())
         need_rbf = ctx.needs_input_grad[1]
-        gx, grbf, dwr, _ = _gate_bwd(dxs, None, x2, rbf2, Wr, None, wr, None, True, need_rbf, dx_add=dx)
+        drbf_out = None
+        if need_rbf and ctx.fan_r is not None:
+            drbf_out, first_r = ctx.fan_r.take(rbf2.shape, x2.device)
+        gx, grbf, dwr, _ = _gate_bwd(dxs, None, x2, rbf2, Wr, None, wr, None, True, need_rbf, dx_add=dx, dx_out=dx,
+                                     drbf_out=drbf_out, drbf_acc=not first_r)
+        gx = gx if first_x else None
+        grbf = grbf if first_r else None
         dws, dbs = tiled_wgrad([g_t[0], g_t[1], g_t[2], g_t[3]], [x_t, xs_t, xs_t, x_t], E, [wq, wk, wv, ws],
                                [bq, bk, bv, bs])
         return (gx, (grbf if need_rbf else None), dwr, dws[0], dbs[0], dws[1], dbs[1], dws[2], dbs[2], dws[3],
@@ -1330,13 +1392,16 @@ def gate_supported(D, R):
     return D in (64, 128, 256) and 1 <= R <= 8
 
 
-def _gate_bwd(g, owner, x, rbf, w, b, w_param, b_param, need_dx, need_rbf, dx_add=None):
-    """x2g_rbf_gate_bwd: (dx, drbf, dw, db); dw / db are None when summed into the gradient bucket."""
+def _gate_bwd(g, owner, x, rbf, w, b, w_param, b_param, need_dx, need_rbf, dx_add=None, dx_out=None, drbf_out=None,
+              drbf_acc=False):
+    """x2g_rbf_gate_bwd: (dx, drbf, dw, db); dw / db are None when summed into the gradient bucket.
+    dx_out / drbf_out: caller buffers (dx_out may alias dx_add); drbf_acc: drbf_out += the gradient."""
     rows, D = x.shape
     R = rbf.shape[1]
     dev = x.device
-    dx = torch.empty(rows, D, dtype=torch.float32, device=dev) if need_dx else None
-    drbf = torch.empty(rows, R, dtype=torch.float32, device=dev) if need_rbf else None
+    dx = dx_out if dx_out is not None else (torch.empty(rows, D, dtype=torch.float32, device=dev) if need_dx else None)
+    drbf = drbf_out if drbf_out is not None else (
+        torch.empty(rows, R, dtype=torch.float32, device=dev) if need_rbf else None)
     has_bias = b is not None
     gw, gb = grad_sink(w_param), (grad_sink(b_param) if has_bias else None)
     accum = gw is not None and (gb is not None or not has_bias)
@@ -1349,7 +1414,7 @@ def _gate_bwd(g, owner, x, rbf, w, b, w_param, b_param, need_dx, need_rbf, dx_ad
     ws_bytes = int(lib.x2g_rbf_gate_bwd_workspace(rows, D, R))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     defer = accum and _DEFER is not None and rows > 0
-    flags = (ACCUM_WGRAD if accum else 0) | (DEFER_SLAB_SUM if defer else 0)
+    flags = (ACCUM_WGRAD if accum else 0) | (DEFER_SLAB_SUM if defer else 0) | (GATE_DRBF_ACCUM if drbf_acc else 0)
     call("x2g_rbf_gate_bwd", ptr(g), ptr(owner), ptr(x), ptr(rbf), ptr(w), ptr(b), rows, D, R, ptr(dx), ptr(dx_add),
          ptr(drbf), ptr(dw), ptr(db), flags, ptr(ws), ws_bytes, stream_ptr())
     if defer:
@@ -1370,15 +1435,25 @@ class _RbfPoolFn(torch.autograd.Function):
         call("x2g_rbf_pool_fwd", ptr(x2), ptr(rbf2), ptr(W), ptr(B), ptr(rowptr), n_seg, D, R, ptr(out), stream_ptr())
         ctx.save_for_backward(x2, rbf2, W, B)
         ctx.owner, ctx.params = owner, (w, b)
+        ctx.fan_x, ctx.fan_r = _fan_of(x), _fan_of(rbf)
         return out
 
     @staticmethod
     def backward(ctx, gp):
         x2, rbf2, W, B = ctx.saved_tensors
         w, b = ctx.params
-        dx, drbf, dw, db = _gate_bwd(_f32(gp), ctx.owner, x2, rbf2, W, B, w, b, ctx.needs_input_grad[0],
-                                     ctx.needs_input_grad[1])
-        return dx, drbf, dw, db, None, None, None
+        need_x, need_r = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dev = x2.device
+        dx_out = drbf_out = None
+        first_x = first_r = True
+        if need_x and ctx.fan_x is not None:
+            dx_out, first_x = ctx.fan_x.take(x2.shape, dev)
+        if need_r and ctx.fan_r is not None:
+            drbf_out, first_r = ctx.fan_r.take(rbf2.shape, dev)
+        dx, drbf, dw, db = _gate_bwd(_f32(gp), ctx.owner, x2, rbf2, W, B, w, b, need_x, need_r,
+                                     dx_add=None if first_x else dx_out, dx_out=dx_out, drbf_out=drbf_out,
+                                     drbf_acc=not first_r)
+        return (dx if first_x else None), (drbf if first_r else None), dw, db, None, None, None
 
 
 def rbf_pool(x, rbf, weight, bias, owner, rowptr, n_seg: int):
