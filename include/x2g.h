@@ -571,6 +571,16 @@ typedef struct {
   int32_t cols; /* weight with row stride ld, of which the first `cols` (<= D) columns are written */
 } x2g_tiled_job;
 
+/* The same for up to X2G_TILED_MAX_JOBS jobs (e.g. every T-layout weight gradient of a backward)
+ * in ONE launch: the jobs' 16-row tiles are concatenated and split evenly over one workgroup per
+ * CU, so a job's partials are the few workgroups overlapping it (~256 + num_jobs slabs in all).
+ * With X2G_DEFER_SLAB_SUM the num_jobs slab reductions are returned in slab_jobs (host array) for
+ * the caller's x2g_slab_sum_batch; otherwise they are summed here. */
+#define X2G_TILED_MAX_JOBS 64
+size_t x2g_tiled_wgrad_flat_workspace(int64_t rows, int32_t dim, int32_t num_jobs);
+int x2g_tiled_wgrad_flat(const x2g_tiled_job* jobs, int32_t num_jobs, int64_t rows, int32_t dim, int flags,
+                         x2g_slab_job* slab_jobs, void* workspace, size_t workspace_bytes, void* stream);
+
 size_t x2g_tiled_wgrad_workspace(int64_t rows, int32_t dim, int32_t num_jobs);
 int32_t x2g_tiled_wgrad_splits(int64_t rows, int32_t dim, int32_t num_jobs);
 int x2g_tiled_wgrad(const x2g_tiled_job* jobs, int32_t num_jobs, int64_t rows, int32_t dim, int flags,

@@ -92,10 +92,14 @@ def test_bucket_gradients_equal_autograd(cuda):
         if i == 0:
             loss.backward()
         else:
+            # deferred: the T-layout weight gradients of the whole backward run as one flat launch
+            # (x2g_tiled_wgrad_flat) whose row split differs from the per-layer launches: equal to
+            # rounding, still bitwise reproducible run to run
             with ops.deferred_wgrad():
                 loss.backward()
+    top = max(float(g.abs().max()) for g in plain)  # (vanishing gradients compared at the model's scale)
     for p, g in zip(m2.parameters(), plain):
-        assert torch.equal(p.grad, g)
+        torch.testing.assert_close(p.grad, g, rtol=1e-5, atol=1e-6 * top)
 
 
 def test_trunk_drop_in_api_vs_fast_path(cuda):

@@ -757,16 +757,14 @@ struct ChainWgradArgs {
 // Three LDS buffers, filled by global_load_lds (no registers: each wave's instruction lands 1 KB
 // lane-linearly, the swizzle applied to the source addresses), two steps in flight ahead of the
 // product; raw s_barrier with counted vmcnt waits so the in-flight copies survive the barriers.
-__global__ void __launch_bounds__(kCThreads, 1) chain_wgrad_kernel(const ChainWgradArgs a) {
-  __shared__ f4 Ds[3][kWTiles][512];
-  __shared__ f4 Xs[3][kWTiles][512];
-  const int s = blockIdx.y, c = blockIdx.x;
+// One call reduces tiles [t0, t1) of one job into a slab (dW rows 16w + 4g + e, columns 16bk + rl).
+__device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, const float* __restrict__ xin, int64_t t0,
+                                              int64_t t1, bool has_b, float* __restrict__ slab,
+                                              float* __restrict__ slab_b, f4 (*Ds)[kWTiles][512],
+                                              f4 (*Xs)[kWTiles][512]) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int rl = lane & 15, g = lane >> 4;
-  const int64_t t0 = c * a.ntiles / a.splits, t1 = (c + 1) * a.ntiles / a.splits;
   const int nsteps = static_cast<int>((t1 - t0 + kWTiles - 1) / kWTiles);
-  const float* dz = a.dz_t[s];
-  const float* xin = a.in_t[s];
   // LDS position P = 64w + lane of a tile image holds source chunk (P >> 2) * 4 + ((P & 3) ^ sigma)
   const int P = 64 * w + lane;
   const int src_chunk = (P >> 2) * 4 + ((P & 3) ^ (((P >> 5) & 1) * 3));
@@ -816,13 +814,54 @@ __global__ void __launch_bounds__(kCThreads, 1) chain_wgrad_kernel(const ChainWg
       }
     }
   }
-  // slab: dW[16w + 4g + e][16bk + rl]
-  float* slab = a.part_w[s] + static_cast<int64_t>(c) * kCD * kCD;
 #pragma unroll
   for (int bk = 0; bk < 8; ++bk)
 #pragma unroll
     for (int e = 0; e < 4; ++e) slab[(16 * w + 4 * g + e) * kCD + 16 * bk + rl] = acc[bk][e];
-  if (a.has_b[s] && tid < 128) a.part_b[s][static_cast<int64_t>(c) * kCD + tid] = bsum;
+  if (has_b && tid < 128) slab_b[tid] = bsum;
+}
+
+__global__ void __launch_bounds__(kCThreads, 1) chain_wgrad_kernel(const ChainWgradArgs a) {
+  __shared__ f4 Ds[3][kWTiles][512];
+  __shared__ f4 Xs[3][kWTiles][512];
+  const int s = blockIdx.y, c = blockIdx.x;
+  const int64_t t0 = c * a.ntiles / a.splits, t1 = (c + 1) * a.ntiles / a.splits;
+  tiled_segment(a.dz_t[s], a.in_t[s], t0, t1, a.has_b[s] != 0, a.part_w[s] + static_cast<int64_t>(c) * kCD * kCD,
+                a.part_b[s] + static_cast<int64_t>(c) * kCD, Ds, Xs);
+}
+
+// Every T-layout weight gradient of a backward in ONE launch: the jobs' tiles are concatenated
+// (job j owns [j * ntiles, (j + 1) * ntiles)) and workgroup i takes the equal share
+// [i * total / G, (i + 1) * total / G), i.e. at most a few job segments; each segment leaves one
+// slab, job j's slabs contiguous from workgroup wg_lo[j] on.  Versus one launch per layer with
+// 256 / jobs splits per job: the same MFMA work, ~256 + jobs slabs in all instead of 256 per
+// launch, and one launch tail.
+struct TiledFlatArgs {
+  const float* in_t[X2G_TILED_MAX_JOBS];
+  const float* dz_t[X2G_TILED_MAX_JOBS];
+  float* slab_w[X2G_TILED_MAX_JOBS];  // job j's slab k (k = workgroup - wg_lo[j]) at + k * D * D
+  float* slab_b[X2G_TILED_MAX_JOBS];  // ... and its bias slab at + k * D
+  int wg_lo[X2G_TILED_MAX_JOBS];
+  int has_b[X2G_TILED_MAX_JOBS];
+  int64_t ntiles;
+  int64_t total;
+  int njobs;
+};
+
+__global__ void __launch_bounds__(kCThreads, 1) tiled_flat_kernel(const TiledFlatArgs a) {
+  __shared__ f4 Ds[3][kWTiles][512];
+  __shared__ f4 Xs[3][kWTiles][512];
+  const int64_t G = gridDim.x, i = blockIdx.x;
+  const int64_t lo = i * a.total / G, hi = (i + 1) * a.total / G;
+  for (int64_t j = lo / a.ntiles; j < a.njobs && j * a.ntiles < hi; ++j) {
+    const int64_t s0 = lo > j * a.ntiles ? lo : j * a.ntiles;
+    const int64_t s1 = hi < (j + 1) * a.ntiles ? hi : (j + 1) * a.ntiles;
+    if (s0 >= s1) continue;
+    __syncthreads();  // a previous segment's last buffers are no longer read
+    const int64_t k = i - a.wg_lo[j];
+    tiled_segment(a.dz_t[j], a.in_t[j], s0 - j * a.ntiles, s1 - j * a.ntiles, a.has_b[j] != 0,
+                  a.slab_w[j] + k * kCD * kCD, a.slab_b[j] + k * kCD, Ds, Xs);
+  }
 }
 
 inline int chain_wgrad_splits_of(int64_t ntiles, int stages) {
@@ -1258,6 +1297,80 @@ X2G_API int x2g_conv_proj_bwd(const x2g_proj_grad* grads, int64_t rows, int32_t 
   a.R = rows;
   conv_proj_bwd_kernel<<<v2_grid(rows), kCThreads, 0, as_stream(stream)>>>(a);
   return last_launch_status();
+}
+
+// ---- one launch for many jobs (x2g_tiled_wgrad_flat)
+static inline unsigned flat_grid(int64_t total) {
+  return static_cast<unsigned>(total < 256 ? (total < 1 ? 1 : total) : 256);  // one workgroup per CU (96 KB LDS)
+}
+
+// slabs of job j: the workgroups overlapping its tiles
+static inline void flat_span(int64_t ntiles, int64_t total, int64_t G, int j, int& lo, int& n) {
+  // workgroup i covers [i * total / G, (i + 1) * total / G): the one holding tile t is the largest i
+  // with i * total / G <= t
+  auto owner = [&](int64_t t) {
+    int64_t i = (t * G) / total;  // close; adjust for the integer floors
+    while (i + 1 < G && (i + 1) * total / G <= t) ++i;
+    while (i > 0 && i * total / G > t) --i;
+    return static_cast<int>(i);
+  };
+  lo = owner(j * ntiles);
+  n = owner((j + 1) * ntiles - 1) - lo + 1;
+}
+
+X2G_API size_t x2g_tiled_wgrad_flat_workspace(int64_t rows, int32_t dim, int32_t num_jobs) {
+  if (rows <= 0 || dim != kCD || num_jobs < 1 || num_jobs > X2G_TILED_MAX_JOBS) return 0;
+  const int64_t ntiles = (rows + 15) / 16, total = ntiles * num_jobs, G = flat_grid(total);
+  int64_t slabs = 0;
+  for (int j = 0; j < num_jobs; ++j) {
+    int lo, n;
+    flat_span(ntiles, total, G, j, lo, n);
+    slabs += n;
+  }
+  return static_cast<size_t>(slabs) * (kCD * kCD + kCD) * sizeof(float);
+}
+
+X2G_API int x2g_tiled_wgrad_flat(const x2g_tiled_job* jobs, int32_t num_jobs, int64_t rows, int32_t dim, int flags,
+                                 x2g_slab_job* slab_jobs, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!jobs || num_jobs < 1 || num_jobs > X2G_TILED_MAX_JOBS || rows <= 0 || dim <= 0 ||
+      (flags & ~(X2G_ACCUM_WGRAD | X2G_DEFER_SLAB_SUM)))
+    return X2G_EINVAL;
+  if (dim != kCD || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  if ((flags & X2G_DEFER_SLAB_SUM) && !slab_jobs) return X2G_EINVAL;
+  const size_t need = x2g_tiled_wgrad_flat_workspace(rows, dim, num_jobs);
+  if (!workspace || workspace_bytes < need) return X2G_EWORKSPACE;
+  TiledFlatArgs a{};
+  a.ntiles = (rows + 15) / 16;
+  a.total = a.ntiles * num_jobs;
+  a.njobs = num_jobs;
+  const int64_t G = flat_grid(a.total);
+  x2g_slab_job sj[X2G_TILED_MAX_JOBS];
+  float* base = static_cast<float*>(workspace);
+  for (int j = 0; j < num_jobs; ++j) {
+    const x2g_tiled_job& J = jobs[j];
+    if (!J.dy_t || !J.x_t || !J.dw) return X2G_EINVAL;
+    if (!al16(J.dy_t) || !al16(J.x_t)) return X2G_EUNSUPPORTED;
+    if (J.ld < 0 || (J.ld > 0 && (J.cols < 1 || J.cols > kCD || J.cols > J.ld))) return X2G_EINVAL;
+    int lo, n;
+    flat_span(a.ntiles, a.total, G, j, lo, n);
+    a.in_t[j] = J.x_t;
+    a.dz_t[j] = J.dy_t;
+    a.wg_lo[j] = lo;
+    a.has_b[j] = J.db != nullptr;
+    a.slab_w[j] = base;
+    a.slab_b[j] = base + static_cast<int64_t>(n) * kCD * kCD;
+    base += static_cast<int64_t>(n) * (kCD * kCD + kCD);
+    sj[j] = x2g_slab_job{a.slab_w[j], J.db ? a.slab_b[j] : nullptr, J.dw, J.db, kCD * kCD, J.db ? kCD : 0, n,
+                         J.ld, J.cols};
+  }
+  tiled_flat_kernel<<<static_cast<unsigned>(G), kCThreads, 0, as_stream(stream)>>>(a);
+  const int rc = last_launch_status();
+  if (rc) return rc;
+  if (flags & X2G_DEFER_SLAB_SUM) {
+    for (int j = 0; j < num_jobs; ++j) slab_jobs[j] = sj[j];
+    return X2G_OK;
+  }
+  return x2g_slab_sum_batch(sj, num_jobs, (flags & X2G_ACCUM_WGRAD) ? 1 : 0, stream);
 }
 
 X2G_API int32_t x2g_tiled_wgrad_splits(int64_t rows, int32_t dim, int32_t num_jobs) {

@@ -610,6 +610,36 @@ class _SlabDeferral:
     def __init__(self):
         self.jobs = []
         self.keep = []  # workspaces holding the partial slabs until the batched sum is enqueued
+        self.tiled = {}  # rows -> [TiledJob]: T-layout weight gradients run as one launch at exit
+
+
+TILED_MAX_JOBS = 64  # X2G_TILED_MAX_JOBS
+# T-layout weight gradients inside deferred_wgrad(): 1 = queued and run as ONE x2g_tiled_wgrad_flat
+# launch at the end of the backward (operands kept alive until then), 0 = one launch per layer
+_FLAT_TILED = os.environ.get("X2G_FLAT_TILED", "1") == "1"
+
+
+def _queue_tiled(R, jobs, keep):
+    """Queue T-layout weight-gradient jobs (x2g_tiled_job, bucket-backed destinations) for the
+    deferred flat launch; ``keep``: tensors the jobs point into."""
+    _DEFER.tiled.setdefault(int(R), []).extend(jobs)
+    _DEFER.keep.extend(keep)
+
+
+def _flush_tiled(d):
+    lib = _lib.load()
+    for R, jobs in d.tiled.items():
+        for j0 in range(0, len(jobs), TILED_MAX_JOBS):
+            part = jobs[j0:j0 + TILED_MAX_JOBS]
+            n = len(part)
+            ws_bytes = int(lib.x2g_tiled_wgrad_flat_workspace(R, 128, n))
+            ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=torch.device("cuda", torch.cuda.current_device()))
+            out = (SlabJob * n)()
+            call("x2g_tiled_wgrad_flat", (TiledJob * n)(*part), n, R, 128, ACCUM_WGRAD | DEFER_SLAB_SUM, out, ptr(ws),
+                 ws_bytes, stream_ptr())
+            d.jobs.extend(out)
+            d.keep.append(ws)
+    d.tiled = {}
 
 
 _DEFER = None
@@ -625,6 +655,8 @@ def deferred_wgrad():
     try:
         yield
         d = _DEFER
+        if d.tiled:
+            _flush_tiled(d)
         if d.jobs:
             arr = (SlabJob * len(d.jobs))(*d.jobs)
             call("x2g_slab_sum_batch", ctypes.cast(arr, ctypes.c_void_p), len(d.jobs), 1, stream_ptr())
@@ -905,6 +937,11 @@ def chain_wgrad(in_t, dz_t, R, weights, biases):
     bufs, acc = _wgrad_targets(params, [tuple(p.shape) for p in params], dev)
     dws, rest = bufs[:n], iter(bufs[n:])
     dbs = [next(rest) if b is not None else None for b in biases]
+    if acc and _DEFER is not None and _FLAT_TILED:
+        tf = in_t.shape[1]
+        _queue_tiled(R, [TiledJob(dz_t.data_ptr() + 4 * g * tf, in_t.data_ptr() + 4 * g * tf, _dp(dws[g]), _dp(dbs[g]),
+                                  0, 0) for g in range(n)], [in_t, dz_t])
+        return [None] * n, [None] * n
     lib = _lib.load()
     ws_bytes = int(lib.x2g_chain_wgrad_workspace(R, D, n))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
@@ -1182,6 +1219,9 @@ class _FeaturizeFn(torch.autograd.Function):
             specs.append((dz2_t.data_ptr(), y1_t.data_ptr() + fb * i * tf, dw2.data_ptr() + fb * i * 128,
                           db2.data_ptr() if (db2 is not None and i == 0) else None, 256, 128))
         n = len(specs)
+        if acc and _DEFER is not None and _FLAT_TILED:
+            _queue_tiled(R, [TiledJob(*sp) for sp in specs], [dz1_t, dz2_t, xs_t, y1_t])
+            return None, None, None, None, None, None
         lib = _lib.load()
         ws_bytes = int(lib.x2g_tiled_wgrad_workspace(R, 128, n))
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
@@ -1231,6 +1271,10 @@ def tiled_wgrad(dy_ts, x_ts, R, weights, biases):
     bufs, acc = _wgrad_targets(params, [tuple(p.shape) for p in params], dev)
     dws, rest = bufs[:n], iter(bufs[n:])
     dbs = [next(rest) if b is not None else None for b in biases]
+    if acc and _DEFER is not None and _FLAT_TILED:
+        _queue_tiled(R, [TiledJob(_dp(dy_ts[g]), _dp(x_ts[g]), _dp(dws[g]), _dp(dbs[g]), 0, 0) for g in range(n)],
+                     list(dy_ts) + list(x_ts))
+        return [None] * n, [None] * n
     lib = _lib.load()
     ws_bytes = int(lib.x2g_tiled_wgrad_workspace(R, D, n))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
