@@ -44,14 +44,14 @@ dy = torch.randn(R, D, device=dev)
 DW = [torch.empty(D, D, device=dev) for _ in range(7)]
 WT = [torch.empty(D, D, device=dev) for _ in range(7)]
 DB = [torch.empty(D, device=dev) for _ in range(7)]
-for knob in (0, 1):
+for knob in (0, 2, 1):
     lib.x2g_tuning(6, knob)
     for n in (1, 2, 7):
         flags = TRUNK[:n] if n != 1 else [S]
         if n == 2:
             flags = [S | H, S | RH]
         # as the model runs it (ops._ChainFn): v2 keeps the stage inputs / dz in the T layout only
-        t_only = knob == 0
+        t_only = knob in (0, 2)
         st = (ops.ChainStage * n)(*[ops.ChainStage(W[i].data_ptr(), B[i].data_ptr(), Z[i].data_ptr(),
                                                    Y[i].data_ptr() if (i == n - 1 or not t_only) else None,
                                                    WT[i].data_ptr(), flags[i]) for i in range(n)])
@@ -59,8 +59,8 @@ for knob in (0, 1):
                                                           Z[i].data_ptr(), None if t_only else DZ[i].data_ptr(),
                                                           flags[i]) for i in range(n)])
         tf = int(lib.x2g_chain_t_floats(R, D))
-        in_t = torch.empty(n, tf, device=dev) if knob == 0 else None
-        dz_t = torch.empty(n, tf, device=dev) if knob == 0 else None
+        in_t = torch.empty(n, tf, device=dev) if knob in (0, 2) else None
+        dz_t = torch.empty(n, tf, device=dev) if knob in (0, 2) else None
         f = t(lambda: lib.x2g_chain_fwd(ptr(x), ptr(res), st, n, R, D, ptr(in_t), stream_ptr()))
         b = t(lambda: lib.x2g_chain_bwd(ptr(dy), None, bst, n, R, D, ptr(dx), ptr(dres), ptr(dz_t), stream_ptr()))
         if knob == 0:

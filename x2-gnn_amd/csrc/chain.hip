@@ -536,6 +536,167 @@ __global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v2(const ChainFwdArgs 
   }
 }
 
+// ---- v3 (the default forward; x2g_tuning key 6 = 2 selects v2): v2 with a branch-free epilogue
+// interleaved with the MFMAs.  The 6 row blocks are computed in thirds; third t's product is
+// scheduled together with third t-1's epilogue (SiLU, residual, LDS write, z and T-layout stores)
+// through sched_group_barrier, so the transcendental / store work runs in the MFMA shadow instead
+// of after the whole product with both waves of the SIMD idle on the matrix pipe (7-stage forward
+// 73 -> 69 us at config 2, scripts/chain_bench.py).  Conditional stores become buffer stores at an
+// out-of-range offset (dropped by the buffer unit, as composable_kernel's OOB-offset stores).
+// a store at byte offset kOOB is out of range of every descriptor below (num_records <= 2^31 - 1)
+// and dropped by the buffer unit
+constexpr int kOOB = static_cast<int>(0x80000000u);
+
+// descriptor over `bytes` bytes at p (0 when off: every store dropped)
+__device__ __forceinline__ rsrc_t rsrc_n(const float* p, int64_t bytes, bool on) {
+  const int64_t nr = on ? (bytes < 0x7fffffff ? bytes : 0x7fffffff) : 0;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), static_cast<short>(0), static_cast<int>(nr),
+                                           0x00020000);
+}
+__device__ __forceinline__ void bstore4(rsrc_t r, f4 v, int voff_bytes) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), r,
+                                         voff_bytes, 0, 0);
+}
+
+template <int RB0, int RB1>
+__device__ __forceinline__ void half_gemm(const f4* __restrict__ img, const f4 (&A)[8], f4 (&acc)[kV2RB], int rl,
+                                          int g) {
+#pragma unroll
+  for (int rb = RB0; rb < RB1; ++rb) acc[rb] = zero4();
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    f4 bo[RB1 - RB0];
+#pragma unroll
+    for (int rb = RB0; rb < RB1; ++rb) bo[rb - RB0] = img[(16 * rb + rl) * 32 + ((4 * b + g) ^ rl)];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int rb = RB0; rb < RB1; ++rb)
+        acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[b][e], bo[rb - RB0][e], acc[rb], 0, 0, 0);
+  }
+}
+
+// epilogue of blocks [RB0, RB1): z = acc + bias (stored), y = act(z) (+ residual) -> out image and
+// the T-layout copy; acc[rb] := y
+template <int RB0, int RB1>
+__device__ __forceinline__ void half_epi(f4 (&acc)[kV2RB], const f4 (&held)[kV2RB], f4 bias, float silu_m, float res_m,
+                                         rsrc_t zr, rsrc_t tr, f4* __restrict__ out, int r0, int nrows, int w,
+                                         int rl, int g) {
+  const int j = rl & 3, m = rl >> 2, f = 16 * w + 4 * g + j;
+  const int ntile = (nrows + 15) >> 4;
+#pragma unroll
+  for (int rb = RB0; rb < RB1; ++rb) {
+    const int r = 16 * rb + rl;
+    const f4 z = acc[rb] + bias;
+    bstore4(zr, z, r < nrows ? 4 * ((r0 + r) * kCD + 16 * w + 4 * g) : kOOB);
+    f4 y;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float sv = silu_fast(z[e]);
+      y[e] = silu_m * sv + (1.0f - silu_m) * z[e] + res_m * held[rb][e];
+    }
+    out[ipos(r, 4 * w + g)] = y;
+    acc[rb] = y;
+    f4 t = quad_transpose(y, j);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) t[e] = 16 * rb + 4 * m + e < nrows ? t[e] : 0.0f;
+    bstore4(tr, t, rb < ntile ? 4 * static_cast<int>((static_cast<int64_t>(r0 >> 4) + rb) * (16 * kCD) + f * 16 + 4 * m)
+                              : kOOB);
+  }
+}
+
+// scheduling pattern for one two-block product (8 k-groups x (2 LDS reads + 8 MFMAs)) with an
+// epilogue's instructions threaded between the MFMAs
+__device__ __forceinline__ void interleave_epi_sched() {
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x006, 3, 0);  // VALU / SALU
+      __builtin_amdgcn_sched_group_barrier(0x400, 1, 0);  // transcendental
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+      __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);  // VMEM write
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v3(const ChainFwdArgs a) {
+  __shared__ f4 img[3][kV2Img];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rl = lane & 15, g = lane >> 4;
+  const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
+  const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
+  const int n = a.n;
+  const int64_t wt_groups = G < 8 ? G : 8;
+  for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
+    int r0, nrows;
+    chunk_rows(ch, nch, nblk, a.R, r0, nrows);
+    __syncthreads();
+    stage_rows(img[0], a.x, nullptr, r0, nrows);
+    if (a.res) stage_rows(img[2], a.res, nullptr, r0, nrows);
+    f4 A[8], held[kV2RB];
+    load_slice<false>(a.st[0].w, w, rl, g, A);
+#pragma unroll
+    for (int rb = 0; rb < kV2RB; ++rb) held[rb] = zero4();
+    int cur = 0;
+    __syncthreads();
+    if (a.in_t) {
+      f4 xs[kV2RB];
+#pragma unroll
+      for (int rb = 0; rb < kV2RB; ++rb) xs[rb] = img[0][ipos(16 * rb + rl, 4 * w + g)];
+      store_t_slice(a.in_t, xs, r0, nrows, w, rl, g);
+    }
+    for (int s = 0; s < n; ++s) {
+      const x2g_chain_stage& S = a.st[s];
+      const int fl = S.flags;
+      f4 An[8];
+      load_slice<false>(a.st[s + 1 < n ? s + 1 : 0].w, w, rl, g, An);
+      const f4 bias = bload4(rsrc(S.b ? S.b : S.w), 4 * (16 * w + 4 * g), 0) * (S.b ? 1.0f : 0.0f);
+      if (S.wt && ch < wt_groups) {
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+          if (b % wt_groups == ch)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) S.wt[(16 * b + 4 * g + e) * kCD + 16 * w + rl] = A[b][e];
+      }
+      const f4* in = img[cur];
+      if (fl & (X2G_CHAIN_HOLD | X2G_CHAIN_RES_EXT)) {
+        const f4* src = (fl & X2G_CHAIN_HOLD) ? in : img[2];
+#pragma unroll
+        for (int rb = 0; rb < kV2RB; ++rb) held[rb] = src[ipos(16 * rb + rl, 4 * w + g)];
+      }
+      const float silu_m = (fl & X2G_CHAIN_SILU) ? 1.0f : 0.0f;
+      const float res_m = (fl & (X2G_CHAIN_RES_HELD | X2G_CHAIN_RES_EXT)) ? 1.0f : 0.0f;
+      const rsrc_t zr = rsrc_n(S.z ? S.z : S.w, a.R * kCD * 4, S.z != nullptr);
+      const bool t_on = a.in_t && s + 1 < n;
+      const rsrc_t tr = rsrc_n(t_on ? a.in_t + (s + 1) * a.tf : S.w, a.tf * 4, t_on);
+      f4* out = img[cur ^ 1];
+      f4 acc[kV2RB];
+      // three thirds of two row blocks: third t's product runs in the MFMA shadow of third t-1's
+      // epilogue (per k-group: its 2 LDS reads, then 8 MFMAs each followed by a slice of the epilogue)
+      half_gemm<0, 2>(in, A, acc, rl, g);
+      __builtin_amdgcn_sched_barrier(0);
+      half_gemm<2, 4>(in, A, acc, rl, g);
+      half_epi<0, 2>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
+      interleave_epi_sched();
+      __builtin_amdgcn_sched_barrier(0);
+      half_gemm<4, 6>(in, A, acc, rl, g);
+      half_epi<2, 4>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
+      interleave_epi_sched();
+      __builtin_amdgcn_sched_barrier(0);
+      half_epi<4, 6>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
+      pin(An);
+      __syncthreads();
+      if (S.y) store_img(S.y, out, r0, nrows);
+      cur ^= 1;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) A[b] = An[b];
+    }
+  }
+}
+
 // Backward: img[p] holds dz_s (the product's B operand); the product's output slice is the
 // gradient of out_{s-1} at the wave's 16 features, so stage s-1's elementwise part (held /
 // external residual gradients, dz_{s-1} = g * SiLU'(z_{s-1})) runs on it in registers and writes
@@ -1106,9 +1267,12 @@ X2G_API int x2g_chain_fwd(const float* x, const float* res_ext, const x2g_chain_
   if (tuning(kTuneChain) == 1 && !in_t) {  // register-tile kernel (no T-layout output)
     const int64_t groups = ((rows + 15) / 16 + kCWaves - 1) / kCWaves;
     chain_fwd_kernel<<<static_cast<unsigned>(groups < 256 ? groups : 256), kCThreads, 0, st>>>(a);
-  } else {  // v2: one workgroup per CU, <= 96 rows in LDS
+  } else if (tuning(kTuneChain) == 2) {  // v2: one workgroup per CU, <= 96 rows in LDS
     const int64_t nblk = (rows + 15) / 16;
     chain_fwd_v2<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, st>>>(a);
+  } else {  // v3 (default): v2 with the epilogue interleaved with the product
+    const int64_t nblk = (rows + 15) / 16;
+    chain_fwd_v3<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, st>>>(a);
   }
   return last_launch_status();
 }
