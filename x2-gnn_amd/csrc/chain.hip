@@ -800,6 +800,144 @@ __global__ void __launch_bounds__(kCThreads, 1) chain_bwd_v2(const ChainBwdArgs 
   }
 }
 
+// ---- backward v3 (the default; x2g_tuning key 6 = 2 selects v2): v2 with stage s-1's elementwise
+// part (residual gradients, dz = g SiLU'(z), the dz stores, the T-layout copy) computed per third of
+// the row blocks and scheduled into the next third's MFMAs, branch-free as the forward v3.
+template <int RB0, int RB1>
+__device__ __forceinline__ void bwd_elem(f4 (&gs)[kV2RB], f4 (&dh)[kV2RB], const f4 (&zc)[kV2RB], const f4 (&acc)[kV2RB],
+                                         float hold_m, float held_m, float silu_m, float dres_acc_m, rsrc_t dres_r,
+                                         rsrc_t dz_r, rsrc_t t_r, f4* __restrict__ out, int r0, int nrows, int w,
+                                         int rl, int g) {
+  const int col = 16 * w + 4 * g;
+  const int j = rl & 3, m = rl >> 2, f = 16 * w + 4 * g + j;
+  const int ntile = (nrows + 15) >> 4;
+#pragma unroll
+  for (int rb = RB0; rb < RB1; ++rb) {
+    const int r = 16 * rb + rl;
+    const int off = r < nrows ? 4 * ((r0 + r) * kCD + col) : kOOB;
+    const f4 gv = acc[rb] + dh[rb] * hold_m;  // in_s was also the held residual (stage s HOLD)
+    dh[rb] = dh[rb] * (1.0f - hold_m) + gv * held_m;  // stage s-1 adds the held residual
+    const f4 ld = bload4(dres_r, off, 0);  // (out of range / off: 0)
+    const f4 old = dres_acc_m != 0.0f ? ld : zero4();  // select, not a product: a fresh buffer may hold NaN
+    bstore4(dres_r, gv + old, off);
+    f4 dz;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dz[e] = gv[e] * (silu_m * silu_grad_fast(zc[rb][e]) + (1.0f - silu_m));
+    bstore4(dz_r, dz, off);
+    out[ipos(r, 4 * w + g)] = dz;
+    gs[rb] = dz;
+    f4 t = quad_transpose(dz, j);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) t[e] = 16 * rb + 4 * m + e < nrows ? t[e] : 0.0f;
+    bstore4(t_r, t, rb < ntile ? 4 * static_cast<int>((static_cast<int64_t>(r0 >> 4) + rb) * (16 * kCD) + f * 16 + 4 * m)
+                               : kOOB);
+  }
+}
+
+__global__ void __launch_bounds__(kCThreads, 1) chain_bwd_v3(const ChainBwdArgs a) {
+  __shared__ f4 img[2][kV2Img];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rl = lane & 15, g = lane >> 4;
+  const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
+  const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
+  const int n = a.n;
+  const int col = 16 * w + 4 * g;
+  for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
+    int r0, nrows;
+    chunk_rows(ch, nch, nblk, a.R, r0, nrows);
+    f4 A[8], dh[kV2RB], zc[kV2RB], gs[kV2RB];
+    auto load_z = [&](int s) {
+      const rsrc_t zr = rsrc((a.st[s].flags & X2G_CHAIN_SILU) ? a.st[s].z : a.dy);
+#pragma unroll
+      for (int rb = 0; rb < kV2RB; ++rb) {
+        const int r = 16 * rb + rl;
+        zc[rb] = bload4(zr, 4 * ((r0 + (r < nrows ? r : 0)) * kCD + col), 0);
+      }
+    };
+    auto load_wslice = [&](int s, f4 (&dst)[8]) {
+      if (a.st[s].wt)
+        load_slice<false>(a.st[s].wt, w, rl, g, dst);
+      else
+        load_slice<true>(a.st[s].w, w, rl, g, dst);
+    };
+    // the elementwise part's per-stage descriptors and masks
+    auto elem_args = [&](int s, float& held_m, float& silu_m, float& dres_acc_m, rsrc_t& dres_r, rsrc_t& dz_r,
+                         rsrc_t& t_r) {
+      const x2g_chain_bwd_stage& S = a.st[s];
+      const int fl = S.flags;
+      held_m = (fl & X2G_CHAIN_RES_HELD) ? 1.0f : 0.0f;
+      silu_m = (fl & X2G_CHAIN_SILU) ? 1.0f : 0.0f;
+      const bool dres_on = (fl & X2G_CHAIN_RES_EXT) && a.dres;
+      dres_acc_m = (fl & X2G_CHAIN_RES_ACCUM) ? 1.0f : 0.0f;
+      dres_r = rsrc_n(dres_on ? a.dres : a.dy, a.R * kCD * 4, dres_on);
+      dz_r = rsrc_n(S.dz ? S.dz : a.dy, a.R * kCD * 4, S.dz != nullptr);
+      t_r = rsrc_n(a.dz_t ? a.dz_t + s * a.tf : a.dy, a.tf * 4, a.dz_t != nullptr);
+    };
+    load_wslice(n - 1, A);
+    load_z(n - 1);
+    f4 acc0[kV2RB];
+    {
+      const rsrc_t yr = rsrc(a.dy), ar = rsrc(a.dy_add ? a.dy_add : a.dy);
+      const float am = a.dy_add ? 1.0f : 0.0f;
+#pragma unroll
+      for (int rb = 0; rb < kV2RB; ++rb) {
+        const int r = 16 * rb + rl;
+        const int vo = 4 * ((r0 + (r < nrows ? r : 0)) * kCD + col);
+        acc0[rb] = bload4(yr, vo, 0) + bload4(ar, vo, 0) * am;
+        dh[rb] = zero4();
+      }
+    }
+    int p = 0;
+    __syncthreads();  // the previous chunk's images are no longer read
+    {
+      float held_m, silu_m, dres_acc_m;
+      rsrc_t dres_r, dz_r, t_r;
+      elem_args(n - 1, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r);
+      bwd_elem<0, kV2RB>(gs, dh, zc, acc0, 0.0f, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, img[p], r0, nrows, w,
+                         rl, g);
+    }
+    __syncthreads();
+    for (int s = n - 1; s >= 0; --s) {
+      f4 An[8];
+      load_wslice(s > 0 ? s - 1 : n - 1, An);
+      load_z(s > 0 ? s - 1 : 0);
+      const float hold_m = (a.st[s].flags & X2G_CHAIN_HOLD) ? 1.0f : 0.0f;
+      const f4* in = img[p];
+      f4* out = img[p ^ 1];
+      f4 acc[kV2RB];
+      if (s > 0) {
+        float held_m, silu_m, dres_acc_m;
+        rsrc_t dres_r, dz_r, t_r;
+        elem_args(s - 1, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r);
+        half_gemm<0, 2>(in, A, acc, rl, g);
+        __builtin_amdgcn_sched_barrier(0);
+        half_gemm<2, 4>(in, A, acc, rl, g);
+        bwd_elem<0, 2>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows, w, rl,
+                       g);
+        interleave_epi_sched();
+        __builtin_amdgcn_sched_barrier(0);
+        half_gemm<4, 6>(in, A, acc, rl, g);
+        bwd_elem<2, 4>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows, w, rl,
+                       g);
+        interleave_epi_sched();
+        __builtin_amdgcn_sched_barrier(0);
+        bwd_elem<4, 6>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows, w, rl,
+                       g);
+      } else {
+        slice_gemm(in, A, acc, rl, g);
+#pragma unroll
+        for (int rb = 0; rb < kV2RB; ++rb) out[ipos(16 * rb + rl, 4 * w + g)] = acc[rb] + dh[rb] * hold_m;
+      }
+      p ^= 1;
+      pin(An);
+      __syncthreads();
+#pragma unroll
+      for (int b = 0; b < 8; ++b) A[b] = An[b];
+    }
+    store_img(a.dx, img[p], r0, nrows);
+  }
+}
+
 // ------------------------------------------------------------------------- batched weight gradients
 // dW_j[n][k] = sum_r dy_j[r][n] x_j[r][k] for up to 8 layers: workgroup (chunk, j) owns a fixed
 // range of rows of layer j; 32-row tiles of dy and x are staged through LDS (double-buffered,
@@ -1316,9 +1454,12 @@ X2G_API int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_
     if (res_accum) return X2G_EUNSUPPORTED;  // the register-tile kernel overwrites d_res_ext
     const int64_t groups = ((rows + 15) / 16 + kCWaves - 1) / kCWaves;
     chain_bwd_kernel<<<static_cast<unsigned>(groups < 256 ? groups : 256), kCThreads, 0, st>>>(a);
-  } else {
+  } else if (tuning(kTuneChain) == 2) {
     const int64_t nblk = (rows + 15) / 16;
     chain_bwd_v2<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, st>>>(a);
+  } else {
+    const int64_t nblk = (rows + 15) / 16;
+    chain_bwd_v3<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, st>>>(a);
   }
   return last_launch_status();
 }
