@@ -850,6 +850,95 @@ int dense_fwd_narrow_launch(const float* x, const float* w, const float* b, cons
                             int act, float* y, float* z, hipStream_t st);
 }  // namespace x2g
 
+namespace x2g {
+// S = sbf W^T + b for the 42-wide sbf rows, wave-independent: a wave takes 16-row blocks of sbf
+// (held as the MFMA B operand, lane (i, g) = row i, k = 16q + 4g + e as two 8-byte loads: the
+// 168-byte rows are 8-byte aligned) and produces all 16 NOB output columns with
+// v_mfma_f32_16x16x4_f32 against W^T fragments staged once per workgroup in LDS (the A operand,
+// read as one conflict-free 16-byte chunk per lane and group); D lane (i, g) holds the block's
+// row i, columns 16 ob + 4g .. +3: one 16-byte store each.  No barriers after the staging, the next
+// block's rows in flight during the MFMAs: the loads, MFMAs and stores of the 4-5 resident waves
+// per SIMD overlap (the tile-staged dense_fwd_narrow serialised them per workgroup: 3.1 TB/s).
+constexpr int kSPQ = 3;  // 16-wide contraction groups (K = 42 -> 48, zero-padded)
+
+template <int NOB>
+__global__ void __launch_bounds__(256) sbf_project_waves(const float* __restrict__ sbf, const float* __restrict__ w,
+                                                         const float* __restrict__ b, int64_t T,
+                                                         float* __restrict__ out, int dbg) {
+  typedef float f4t __attribute__((ext_vector_type(4)));
+  __shared__ f4t Wl[NOB * kSPQ * 64];  // [ob][q][lane]: W[16ob + i][16q + 4g .. +3]
+  __shared__ f4t Bl[NOB * 4];          // [ob][g]: b[16ob + 4g .. +3]
+  constexpr int N = 16 * NOB;
+  for (int idx = threadIdx.x; idx < NOB * kSPQ * 64; idx += blockDim.x) {
+    const int l = idx & 63, q = (idx >> 6) % kSPQ, ob = (idx >> 6) / kSPQ;
+    const int c = 16 * ob + (l & 15), k = 16 * q + 4 * (l >> 4);
+    f4t v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = k + e < kS ? w[c * kS + k + e] : 0.0f;
+    Wl[idx] = v;
+  }
+  for (int idx = threadIdx.x; idx < NOB * 4; idx += blockDim.x) {
+    f4t v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = b ? b[4 * idx + e] : 0.0f;
+    Bl[idx] = v;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int64_t nblk = (T + 15) / 16;
+  const int64_t nw = static_cast<int64_t>(gridDim.x) * 4;
+  auto load_b = [&](int64_t blk, f4t (&B)[kSPQ]) {
+    const int64_t r = blk * 16 + i;
+    const bool rok = r < T;
+    const float* row = sbf + (rok ? r : T - 1) * kS;
+#pragma unroll
+    for (int q = 0; q < kSPQ; ++q) {
+      const int k = 16 * q + 4 * g;  // k even: 8-byte aligned pairs
+      const int k0 = k < kS ? k : kS - 2, k1 = k + 2 < kS ? k + 2 : kS - 2;
+      const float2 lo = *reinterpret_cast<const float2*>(row + k0);
+      const float2 hi = *reinterpret_cast<const float2*>(row + k1);
+      const float m0 = (rok && k < kS) ? 1.0f : 0.0f, m1 = (rok && k + 2 < kS) ? 1.0f : 0.0f;
+      B[q] = f4t{lo.x * m0, lo.y * m0, hi.x * m1, hi.y * m1};
+    }
+  };
+  int64_t blk = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  f4t B[kSPQ];
+  if (blk < nblk) load_b(blk, B);
+  for (; blk < nblk; blk += nw) {
+    f4t Bn[kSPQ];
+    load_b(blk + nw < nblk ? blk + nw : blk, Bn);  // (the last block reloads itself: unused)
+    const int64_t r = blk * 16 + i;
+    float* o = out + (r < T ? r : 0) * N + 4 * g;
+    // output columns in halves of (at most) 4 blocks: 4 accumulators in flight (dependency distance
+    // 4 MFMAs >= the 40-cycle accumulator latency), fewer registers than all 8 at once
+    constexpr int HB = NOB < 4 ? NOB : 4;
+#pragma unroll
+    for (int h0 = 0; h0 < NOB; h0 += HB) {
+      f4t acc[HB];
+#pragma unroll
+      for (int j = 0; j < HB; ++j) acc[j] = Bl[(h0 + j) * 4 + g];
+#pragma unroll
+      for (int q = 0; q < ((dbg & 1) ? 0 : kSPQ); ++q) {
+        f4t a[HB];
+#pragma unroll
+        for (int j = 0; j < HB; ++j) a[j] = Wl[((h0 + j) * kSPQ + q) * 64 + lane];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int j = 0; j < HB; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][e], B[q][e], acc[j], 0, 0, 0);
+      }
+      if (dbg & 1) acc[0] += B[0] + B[1] + B[2];  // (ablation: keep the loads live)
+      if (r < T && !(dbg & 2)) {
+#pragma unroll
+        for (int j = 0; j < HB; ++j) *reinterpret_cast<f4t*>(o + 16 * (h0 + j)) = acc[j];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kSPQ; ++q) B[q] = Bn[q];
+  }
+}
+}  // namespace x2g
+
 X2G_API int x2g_sbf_project(const float* sbf, int64_t T, int32_t sbf_dim, const float* w_sbf, const float* b_sbf,
                             int32_t out_dim, float* sbfproj, void* stream) {
   if (T < 0 || out_dim <= 0) return X2G_EINVAL;
@@ -857,11 +946,25 @@ X2G_API int x2g_sbf_project(const float* sbf, int64_t T, int32_t sbf_dim, const 
   if (T == 0) return X2G_OK;
   if (!sbf || !w_sbf || !b_sbf || !sbfproj) return X2G_EINVAL;
   hipStream_t st = as_stream(stream);
+  // wave-independent f32 MFMA kernel (out_dim 128 or 64, 8-byte aligned sbf rows, 16-byte aligned
+  // output rows); x2g_tuning key 2 = 2 selects the tile-staged dense kernel
+  if ((out_dim == 128 || out_dim == 64) && reinterpret_cast<uintptr_t>(sbf) % 8 == 0 &&
+      reinterpret_cast<uintptr_t>(sbfproj) % 16 == 0 && tuning(kTuneAttn) == 0) {
+    const int64_t nblk = (T + 15) / 16;
+    int64_t want = (nblk + 3) / 4;
+    want = want < 1280 ? want : 1280;  // ~5 workgroups per CU, each wave looping over its blocks
+    const int dbg = tuning(kTuneSprojDbg);  // timing ablations only (1 no MFMA, 2 no stores)
+    if (out_dim == 128)
+      sbf_project_waves<8><<<static_cast<unsigned>(want), 256, 0, st>>>(sbf, w_sbf, b_sbf, T, sbfproj, dbg);
+    else
+      sbf_project_waves<4><<<static_cast<unsigned>(want), 256, 0, st>>>(sbf, w_sbf, b_sbf, T, sbfproj, dbg);
+    return last_launch_status();
+  }
   // f32 MFMA, tiles staged through LDS (dense.hip): that kernel covers N <= 128 output columns
   // and addresses rows with 32-bit offsets; wider projections take the per-row kernel below
   if (out_dim % 4 == 0 && out_dim <= 128 && T * 128 < (int64_t(1) << 31) &&
       reinterpret_cast<uintptr_t>(sbf) % 16 == 0 && reinterpret_cast<uintptr_t>(sbfproj) % 16 == 0 &&
-      tuning(kTuneAttn) == 0)
+      (tuning(kTuneAttn) == 0 || tuning(kTuneAttn) == 2))
     return dense_fwd_narrow_launch(sbf, w_sbf, b_sbf, nullptr, T, kS, out_dim, 0, sbfproj, nullptr, st);
   int64_t want = (T + kAttnWaves - 1) / kAttnWaves;
   const unsigned blocks = static_cast<unsigned>(want < 4096 ? want : 4096);

@@ -33,7 +33,8 @@ enum TuneKey {
   kTuneFold = 5,        // factorised attention backward: 0 = batched passes, 1 = 3-set pipelined passes
   kTuneChainDbg = 7,    // row-chain forward ablations for timing (1 no restaging, 2 no stores, 4 no SiLU, 8 no barrier)
   kTuneChain = 6,       // row chains: 0 = v3 forward / v2 backward, 1 = register-tile kernels, 2 = v2 forward
-  kTuneFeatDbg = 8,     // featurisation forward ablations for timing (1 no GEMM1, 2 no GEMM2, 4 no stores, 8 no staging)
+  kTuneFeatDbg = 8,
+  kTuneSprojDbg = 9,    // S projection (sbf_project_waves) ablations for timing (1 no MFMA, 2 no stores)     // featurisation forward ablations for timing (1 no GEMM1, 2 no GEMM2, 4 no stores, 8 no staging)
   kTuneCount = 16
 };
 int tuning(int key);

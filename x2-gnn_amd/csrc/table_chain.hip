@@ -145,8 +145,20 @@ __device__ __forceinline__ void bwd_prefetch(const TableBwdArgs& a, int s, BwdPr
   }
 }
 
+// old values of stage s's dW / db when it accumulates into a gradient bucket (zero otherwise), in
+// the MFMA D layout of the dW product: old[t][e] = dw[16w + 4g + e][16t + i]
+__device__ __forceinline__ void load_old(const TableBwdArgs& a, int s, f4 (&old)[8]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
+  const bool on = s >= 0 && a.st[s >= 0 ? s : 0].accum;
+  const float* dw = a.st[s >= 0 ? s : 0].dw;
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) old[t][e] = on ? dw[(16 * w + 4 * g + e) * kTD + 16 * t + i] : 0.0f;
+}
+
 __device__ __forceinline__ void bwd_stage(const TableBwdArgs& a, int s, BwdPre& cur, BwdPre& nxt,
-                                          float (*G)[kTRows * kTS], float* dZ, float* In) {
+                                          float (*G)[kTRows * kTS], float* dZ, float* In, f4 (&old)[8]) {
   const x2g_table_bwd_stage& S = a.st[s];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 15, g = lane >> 4, c = 16 * w + i;
@@ -160,12 +172,8 @@ __device__ __forceinline__ void bwd_stage(const TableBwdArgs& a, int s, BwdPre& 
   }
   __syncthreads();
   bwd_prefetch(a, s - 1, nxt);
-  // dW[n][k] = sum_r dz[r][n] in[r][k]: wave w owns rows n = 16w + ..., all 8 column blocks
-  f4 old[8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) old[t][e] = S.accum ? S.dw[(16 * w + 4 * g + e) * kTD + 16 * t + i] : 0.0f;
+  // dW[n][k] = sum_r dz[r][n] in[r][k]: wave w owns rows n = 16w + ..., all 8 column blocks; the
+  // old bucket values (old, loaded at the end of the previous stage) are added at the store
   float ad[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) ad[e] = dZ[(4 * g + e) * kTS + c];  // A: (n = c, r = 4g + e)
@@ -180,6 +188,7 @@ __device__ __forceinline__ void bwd_stage(const TableBwdArgs& a, int s, BwdPre& 
   for (int t = 0; t < 8; ++t)
 #pragma unroll
     for (int e = 0; e < 4; ++e) S.dw[(16 * w + 4 * g + e) * kTD + 16 * t + i] = old[t][e] + dwv[t][e];
+  load_old(a, s - 1, old);  // the next stage's, in flight through its barriers and dz
   if (S.db && tid < kTD) {
     float acc = 0.0f;
     for (int r = 0; r < a.R; ++r) acc += dZ[r * kTS + tid];
@@ -207,6 +216,8 @@ __global__ void __launch_bounds__(kTThreads) table_chain_bwd_kernel(const TableB
   const int R = a.R;
   BwdPre p0, p1;
   bwd_prefetch(a, a.n - 1, p0);
+  f4 old[8];
+  load_old(a, a.n - 1, old);
   for (int s = -1; s < a.n; ++s) {
     const float* dy = s >= 0 ? a.st[s].dy : nullptr;
     if (dy)
@@ -215,8 +226,8 @@ __global__ void __launch_bounds__(kTThreads) table_chain_bwd_kernel(const TableB
       *reinterpret_cast<f4*>(G[s + 1] + (tid >> 5) * kTS + 4 * (tid & 31)) = f4{0.f, 0.f, 0.f, 0.f};
   }
   for (int s = a.n - 1; s >= 0; s -= 2) {
-    bwd_stage(a, s, p0, p1, G, dZ, In);
-    if (s - 1 >= 0) bwd_stage(a, s - 1, p1, p0, G, dZ, In);
+    bwd_stage(a, s, p0, p1, G, dZ, In, old);
+    if (s - 1 >= 0) bwd_stage(a, s - 1, p1, p0, G, dZ, In, old);
   }
   if (a.dx) {
     __syncthreads();
