@@ -40,7 +40,7 @@ from x2gnn.synth import molecules_from_geometry_file, synthetic_molecules  # noq
 CFG = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embedding_size=128)  # config.json
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32) peak, MI355X_MICROARCH.md
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r2_pmc_traffic.json")  # scripts/pmc_traffic.py output
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r2_s_pmc_traffic.json")  # scripts/pmc_traffic.py output
 METRIC = "molecules/sec (fwd+bwd) on QM9 U0, batch=128, 1/2/4/8 MI355X"
 AID_GEOM = os.path.join(ROOT, "tests", "golden", "aid_geom.npz")  # raw/AID_kcal.xyz as arrays
 # BASELINE.json configs: [1] is the metric's; [2] and [4] are the other single-GPU shapes
@@ -311,6 +311,39 @@ def chain_probe(R, reps):
             "chain_wgrad": (_event_time(wgrad, reps), flops)}
 
 
+def flat_wgrad_probe(reps):
+    """The step's largest kernel: every T-layout weight gradient of the backward in one launch
+    (x2g_tiled_wgrad_flat, ops._flush_tiled) with the job list the captured step recorded
+    (ops.FLAT_LAUNCHES: rows R, one [128,cols] dW = dz^T x per job, K = R), on synthetic T-layout
+    operands, HIP-event timed on the launch stream.  FLOPs per launch: sum_j 2 * R * 128 * cols_j."""
+    if not ops.FLAT_LAUNCHES:
+        return None
+    R, cols = max(ops.FLAT_LAUNCHES, key=lambda rc: rc[0] * sum(rc[1]))
+    n, D = len(cols), 128
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(5)
+    tf = _lib_ws("x2g_chain_t_floats", R, D)
+    x_t = [torch.randn(tf, device=dev, generator=g) for _ in range(n)]
+    dz_t = [torch.randn(tf, device=dev, generator=g) for _ in range(n)]
+    dw = [torch.zeros(D, D, device=dev) for _ in range(n)]
+    db = [torch.zeros(D, device=dev) for _ in range(n)]
+    jobs = (ops.TiledJob * n)(*[ops.TiledJob(dz_t[j].data_ptr(), x_t[j].data_ptr(), dw[j].data_ptr(),
+                                             db[j].data_ptr(), D if cols[j] < D else 0, cols[j] if cols[j] < D else 0)
+                                for j in range(n)])
+    wsb = _lib_ws("x2g_tiled_wgrad_flat_workspace", R, D, n)
+    ws = torch.empty(max(wsb, 4), dtype=torch.uint8, device=dev)
+    out = (ops.SlabJob * n)()
+
+    def run():
+        call("x2g_tiled_wgrad_flat", jobs, n, R, D, ops.ACCUM_WGRAD | ops.DEFER_SLAB_SUM, out, ptr(ws), wsb,
+             stream_ptr())
+
+    run()
+    ms = _event_time(run, reps)
+    wgs = min(256, max(1, (R + 15) // 16 * n))  # chain.hip flat_grid: one 512-thread workgroup per CU
+    return {"ms": ms, "flops": float(sum(2.0 * R * D * c for c in cols)), "rows": R, "jobs": n, "grid": wgs * 512}
+
+
 def _lib_ws(name, *args):
     from x2gnn import _lib
 
@@ -472,18 +505,21 @@ def main():
     sa = scatter_add_probe(plan_lg, args.kernel_reps)
     dense = dense_probe(shape["E"], args.kernel_reps)
     dense.update(chain_probe(shape["E"], args.kernel_reps))
-    # the roofline kernel: the trunk-tail chain backward (x2g_chain_bwd), the largest single
-    # kernel of the step in the committed profile (profiles/r2_*_step_kernels.txt); f32 MFMA-bound
-    # (7 x 2 R D^2 FLOP vs ~184 MB of z / dz / dy / dx traffic at config 2)
-    cb_ms, cb_flops = dense["chain_bwd"]
-    cb_tfs = cb_flops / (cb_ms * 1e-3) / 1e12
-    grid = str(min(256, (shape["E"] + 15) // 16) * 512)
-    traffic = pmc_traffic([("x2g::(anonymous namespace)::chain_bwd_v2", grid)])
-    roof = {"kernel": "x2g_chain_bwd: 7-stage trunk tail data gradient [E,128] (chain_bwd_v2)",
-            "bound": "mfma", "achieved": round(cb_tfs, 2), "peak": MFMA_F32_PEAK_TFS,
-            "unit": "TFLOP/s", "frac": round(cb_tfs / MFMA_F32_PEAK_TFS, 4), "traffic": traffic,
-            "avg_ms": round(cb_ms, 5), "flops_per_launch": int(cb_flops),
-            "traffic_source": os.path.relpath(TRAFFIC_JSON, ROOT) if traffic else None}
+    # the roofline kernel: the step's largest single kernel in the committed profile
+    # (profiles/r2_*_step_kernels.txt) -- the one-launch T-layout weight gradient of the whole
+    # backward (x2g_tiled_wgrad_flat), f32 MFMA-bound (sum_j 2 R 128 cols_j FLOP, ~K = R deep)
+    roof = None
+    flat = flat_wgrad_probe(args.kernel_reps) if wl["train"] else None
+    if flat is not None:
+        f_tfs = flat["flops"] / (flat["ms"] * 1e-3) / 1e12
+        traffic = pmc_traffic([("x2g::(anonymous namespace)::tiled_flat_kernel", str(flat["grid"]))])
+        roof = {"kernel": f"x2g_tiled_wgrad_flat: {flat['jobs']} weight gradients dW = dz^T x over "
+                          f"R={flat['rows']} rows in one launch (tiled_flat_kernel)",
+                "bound": "mfma", "achieved": round(f_tfs, 2), "peak": MFMA_F32_PEAK_TFS,
+                "unit": "TFLOP/s", "frac": round(f_tfs / MFMA_F32_PEAK_TFS, 4), "traffic": traffic,
+                "avg_ms": round(flat["ms"], 5), "flops_per_launch": int(flat["flops"]),
+                "traffic_source": os.path.relpath(TRAFFIC_JSON, ROOT) if traffic else None}
+        dense["tiled_wgrad_flat"] = (flat["ms"], flat["flops"])
     if not wl["train"]:  # inference: no backward; the T-row attention forward dominates
         a_ms, a_bytes = probe["attn_fwd"]
         a_gbs = a_bytes / (a_ms * 1e-3) / 1e9

@@ -626,12 +626,17 @@ def _queue_tiled(R, jobs, keep):
     _DEFER.keep.extend(keep)
 
 
+FLAT_LAUNCHES = []  # (rows, [cols per job]) of the most recent deferred flush's flat launches (bench.py's probe)
+
+
 def _flush_tiled(d):
     lib = _lib.load()
+    FLAT_LAUNCHES.clear()
     for R, jobs in d.tiled.items():
         for j0 in range(0, len(jobs), TILED_MAX_JOBS):
             part = jobs[j0:j0 + TILED_MAX_JOBS]
             n = len(part)
+            FLAT_LAUNCHES.append((int(R), [int(j.cols) if j.ld > 0 else 128 for j in part]))
             ws_bytes = int(lib.x2g_tiled_wgrad_flat_workspace(R, 128, n))
             ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=torch.device("cuda", torch.cuda.current_device()))
             out = (SlabJob * n)()
