@@ -45,10 +45,22 @@ def t(fn, reps=40):
 
 fwd = lambda: lib.x2g_chain_fwd(ptr(x), ptr(res), st, n, R, D, ptr(in_t), stream_ptr())  # noqa: E731
 bwd = lambda: lib.x2g_chain_bwd(ptr(dy), None, bst, n, R, D, ptr(dx), ptr(dres), ptr(dz_t), stream_ptr())  # noqa: E731
-names = {0: "default (v3)", 2: "v2"}
-best = {k: [1e9, 1e9] for k in names}
+names = {0: "default (fwd v4)", 2: "v2", 3: "fwd v3"}
+knobs = [int(k) for k in os.environ.get("KNOBS", "2,0").split(",")]
+outs = {}
+for k in knobs:  # outputs of each variant (y, z, T-layout inputs; dx, d res, T-layout dz) for a bitwise comparison
+    lib.x2g_tuning(6, k)
+    fwd()
+    bwd()
+    torch.cuda.synchronize()
+    outs[k] = [y.clone(), in_t.clone()] + [z.clone() for z in Z] + [dx.clone(), dres.clone(), dz_t.clone()]
+for k in knobs[1:]:
+    same = all(torch.equal(a, b) for a, b in zip(outs[knobs[0]], outs[k]))
+    err = max(float((a - b).abs().max()) for a, b in zip(outs[knobs[0]], outs[k]))
+    print(f"{names[k]} vs {names[knobs[0]]}: forward + backward outputs bitwise equal: {same} (max abs diff {err:.3g})", flush=True)
+best = {k: [1e9, 1e9] for k in knobs}
 for rnd in range(4):
-    for k in (2, 0) if rnd % 2 == 0 else (0, 2):
+    for k in (knobs if rnd % 2 == 0 else knobs[::-1]):
         lib.x2g_tuning(6, k)
         best[k][0] = min(best[k][0], t(fwd))
         best[k][1] = min(best[k][1], t(bwd))

@@ -536,7 +536,7 @@ __global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v2(const ChainFwdArgs 
   }
 }
 
-// ---- v3 (the default forward; x2g_tuning key 6 = 2 selects v2): v2 with a branch-free epilogue
+// ---- v3 (x2g_tuning key 6 = 3; 2 selects v2): v2 with a branch-free epilogue
 // interleaved with the MFMAs.  The 6 row blocks are computed in thirds; third t's product is
 // scheduled together with third t-1's epilogue (SiLU, residual, LDS write, z and T-layout stores)
 // through sched_group_barrier, so the transcendental / store work runs in the MFMA shadow instead
@@ -693,6 +693,140 @@ __global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v3(const ChainFwdArgs 
       cur ^= 1;
 #pragma unroll
       for (int b = 0; b < 8; ++b) A[b] = An[b];
+    }
+  }
+}
+
+// ---- v4 (the default; x2g_tuning key 6 = 3 selects v3): v3 with the product's LDS reads
+// software-pipelined.  PMC on v3 (SQ_VALU_MFMA_BUSY_CYCLES: the matrix pipe busy 46 % of the kernel
+// at 2.3 GHz) and its ISA showed
+// each k-group's two B fragments read right before that group's 8 MFMAs, so every group waited out
+// the LDS latency, and the two waves of a SIMD, in lockstep, waited together.  Here group g + 1's
+// fragments (across third boundaries too) are read before group g's MFMAs; the two stage images
+// are separate __shared__ arrays (stages unrolled by two) so the compiler knows the epilogue's
+// image writes never alias the product's reads and may interleave them freely.  A/B (bitwise
+// equal outputs, scripts/chain_ab.py): 66.5 -> 64.3 us alone, +0.3 % molecules/s in the step.
+// (The same change to the backward measured 73.7 -> 72.6 us alone but -0.2 % in the step, and a
+// forward with two 256-thread workgroups per CU, so that one workgroup's stage tail overlaps the
+// other's product, measured the same as v4 alone: neither is kept.)
+template <int T>
+__device__ __forceinline__ void frag_load(const f4* __restrict__ img, int b, int rl, int g, f4 (&bo)[2]) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bo[j] = img[(16 * (2 * T + j) + rl) * 32 + ((4 * b + g) ^ rl)];
+}
+
+// third T's product (blocks 2T, 2T + 1); on entry bo[0] holds its group 0, on exit (T < 2) bo[0]
+// holds third T + 1's group 0
+template <int T>
+__device__ __forceinline__ void third_gemm(const f4* __restrict__ img, const f4 (&A)[8], f4 (&acc)[kV2RB],
+                                           f4 (&bo)[2][2], int rl, int g) {
+  acc[2 * T] = zero4();
+  acc[2 * T + 1] = zero4();
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const int cur = b & 1;
+    if (b + 1 < 8)
+      frag_load<T>(img, b + 1, rl, g, bo[cur ^ 1]);
+    else if (T < 2)
+      frag_load<(T < 2 ? T + 1 : T)>(img, 0, rl, g, bo[cur ^ 1]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[2 * T + j] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[b][e], bo[cur][j][e], acc[2 * T + j], 0, 0, 0);
+  }
+}
+
+// a third's product alone: per group its 2 (next-group) LDS reads, then 8 MFMAs
+__device__ __forceinline__ void pipe_sched() {
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+  }
+}
+
+// one stage of the v4 forward: in -> out (distinct arrays after inlining)
+__device__ __forceinline__ void fwd4_stage(const ChainFwdArgs& a, int s, const f4* __restrict__ in,
+                                           f4* __restrict__ out, const f4* __restrict__ rimg, f4 (&A)[8],
+                                           f4 (&held)[kV2RB], int64_t ch, int64_t wt_groups, int r0, int nrows,
+                                           int w, int rl, int g) {
+  const int n = a.n;
+  const x2g_chain_stage& S = a.st[s];
+  const int fl = S.flags;
+  f4 An[8];
+  load_slice<false>(a.st[s + 1 < n ? s + 1 : 0].w, w, rl, g, An);
+  const f4 bias = bload4(rsrc(S.b ? S.b : S.w), 4 * (16 * w + 4 * g), 0) * (S.b ? 1.0f : 0.0f);
+  if (S.wt && ch < wt_groups) {
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+      if (b % wt_groups == ch)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) S.wt[(16 * b + 4 * g + e) * kCD + 16 * w + rl] = A[b][e];
+  }
+  if (fl & (X2G_CHAIN_HOLD | X2G_CHAIN_RES_EXT)) {
+    const f4* src = (fl & X2G_CHAIN_HOLD) ? in : rimg;
+#pragma unroll
+    for (int rb = 0; rb < kV2RB; ++rb) held[rb] = src[ipos(16 * rb + rl, 4 * w + g)];
+  }
+  const float silu_m = (fl & X2G_CHAIN_SILU) ? 1.0f : 0.0f;
+  const float res_m = (fl & (X2G_CHAIN_RES_HELD | X2G_CHAIN_RES_EXT)) ? 1.0f : 0.0f;
+  const rsrc_t zr = rsrc_n(S.z ? S.z : S.w, a.R * kCD * 4, S.z != nullptr);
+  const bool t_on = a.in_t && s + 1 < n;
+  const rsrc_t tr = rsrc_n(t_on ? a.in_t + (s + 1) * a.tf : S.w, a.tf * 4, t_on);
+  f4 acc[kV2RB];
+  f4 bo[2][2];
+  frag_load<0>(in, 0, rl, g, bo[0]);
+  __builtin_amdgcn_sched_barrier(0);  // the region below: third 0's MFMAs and its next-group reads only
+  third_gemm<0>(in, A, acc, bo, rl, g);
+  pipe_sched();
+  __builtin_amdgcn_sched_barrier(0);
+  third_gemm<1>(in, A, acc, bo, rl, g);
+  half_epi<0, 2>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
+  interleave_epi_sched();
+  __builtin_amdgcn_sched_barrier(0);
+  third_gemm<2>(in, A, acc, bo, rl, g);
+  half_epi<2, 4>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
+  interleave_epi_sched();
+  __builtin_amdgcn_sched_barrier(0);
+  half_epi<4, 6>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
+  pin(An);
+  __syncthreads();
+  if (S.y) store_img(S.y, out, r0, nrows);
+#pragma unroll
+  for (int b = 0; b < 8; ++b) A[b] = An[b];
+}
+
+__global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4(const ChainFwdArgs a) {
+  __shared__ f4 img0[kV2Img];
+  __shared__ f4 img1[kV2Img];
+  __shared__ f4 imgr[kV2Img];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rl = lane & 15, g = lane >> 4;
+  const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
+  const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
+  const int n = a.n;
+  const int64_t wt_groups = G < 8 ? G : 8;
+  for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
+    int r0, nrows;
+    chunk_rows(ch, nch, nblk, a.R, r0, nrows);
+    __syncthreads();
+    stage_rows(img0, a.x, nullptr, r0, nrows);
+    if (a.res) stage_rows(imgr, a.res, nullptr, r0, nrows);
+    f4 A[8], held[kV2RB];
+    load_slice<false>(a.st[0].w, w, rl, g, A);
+#pragma unroll
+    for (int rb = 0; rb < kV2RB; ++rb) held[rb] = zero4();
+    __syncthreads();
+    if (a.in_t) {
+      f4 xs[kV2RB];
+#pragma unroll
+      for (int rb = 0; rb < kV2RB; ++rb) xs[rb] = img0[ipos(16 * rb + rl, 4 * w + g)];
+      store_t_slice(a.in_t, xs, r0, nrows, w, rl, g);
+    }
+    for (int s = 0; s < n; s += 2) {
+      fwd4_stage(a, s, img0, img1, imgr, A, held, ch, wt_groups, r0, nrows, w, rl, g);
+      if (s + 1 < n) fwd4_stage(a, s + 1, img1, img0, imgr, A, held, ch, wt_groups, r0, nrows, w, rl, g);
     }
   }
 }
@@ -1408,9 +1542,12 @@ X2G_API int x2g_chain_fwd(const float* x, const float* res_ext, const x2g_chain_
   } else if (tuning(kTuneChain) == 2) {  // v2: one workgroup per CU, <= 96 rows in LDS
     const int64_t nblk = (rows + 15) / 16;
     chain_fwd_v2<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, st>>>(a);
-  } else {  // v3 (default): v2 with the epilogue interleaved with the product
+  } else if (tuning(kTuneChain) == 3) {  // v3: v2 with the epilogue interleaved with the product
     const int64_t nblk = (rows + 15) / 16;
     chain_fwd_v3<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, st>>>(a);
+  } else {  // v4 (default): v3 with the product's LDS reads pipelined
+    const int64_t nblk = (rows + 15) / 16;
+    chain_fwd_v4<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, st>>>(a);
   }
   return last_launch_status();
 }
@@ -1457,7 +1594,7 @@ X2G_API int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_
   } else if (tuning(kTuneChain) == 2) {
     const int64_t nblk = (rows + 15) / 16;
     chain_bwd_v2<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, st>>>(a);
-  } else {
+  } else {  // v3 (default)
     const int64_t nblk = (rows + 15) / 16;
     chain_bwd_v3<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, st>>>(a);
   }

@@ -32,9 +32,9 @@ enum TuneKey {
   kTuneGateSplits = 4,  // rbf gate backward: workgroup cap (0 = default)
   kTuneFold = 5,        // factorised attention backward: 0 = batched passes, 1 = 3-set pipelined passes
   kTuneChainDbg = 7,    // row-chain forward ablations for timing (1 no restaging, 2 no stores, 4 no SiLU, 8 no barrier)
-  kTuneChain = 6,       // row chains: 0 = v3 forward / v2 backward, 1 = register-tile kernels, 2 = v2 forward
-  kTuneFeatDbg = 8,
-  kTuneSprojDbg = 9,    // S projection (sbf_project_waves) ablations for timing (1 no MFMA, 2 no stores)     // featurisation forward ablations for timing (1 no GEMM1, 2 no GEMM2, 4 no stores, 8 no staging)
+  kTuneChain = 6,       // row chains: 0 = v4 forward / v3 backward, 1 = register-tile kernels, 2 = v2, 3 = v3 forward
+  kTuneFeatDbg = 8,     // featurisation forward ablations for timing (1 no GEMM1, 2 no GEMM2, 4 no stores, 8 no staging)
+  kTuneSprojDbg = 9,    // S projection (sbf_project_waves) ablations for timing (1 no MFMA, 2 no stores)
   kTuneCount = 16
 };
 int tuning(int key);
