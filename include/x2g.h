@@ -306,6 +306,32 @@ typedef struct {
  * possible; accum != 0: add into dw/db.  Same fixed order as the immediate sums. */
 int x2g_slab_sum_batch(const x2g_slab_job* jobs, int32_t njobs, int32_t accum, void* stream);
 
+/* Several readout pools over the same rows, segments and basis (X2-GNN's conv_layers + 1 AtomWise /
+ * MolWise readouts all pool lin_rbf(rbf) * x_i edges -> atoms, readout.py:39-41,66-67) as ONE launch
+ * each way instead of one per readout.  Forward uses x, w, b, out; backward g, x, w, b, dx, dx_add,
+ * dw, db (meanings as x2g_rbf_gate_bwd / x2g_rbf_pool_fwd; owner maps rows to segments). */
+#define X2G_GATE_MAX_JOBS 8
+typedef struct {
+  const float* x;      /* [rows, D] */
+  const float* w;      /* lin_rbf weight [D, R] */
+  const float* b;      /* [D] or NULL */
+  float* out;          /* forward: pooled [n_seg, D] */
+  const float* g;      /* backward: gradient of out (row r reads g[owner[r]]) */
+  float* dx;           /* backward: [rows, D] or NULL */
+  const float* dx_add; /* backward: added into dx (may alias it) or NULL */
+  float* dw;           /* backward: [D, R] */
+  float* db;           /* backward: [D] or NULL */
+} x2g_gate_job;
+int x2g_rbf_pool_fwd_batch(const x2g_gate_job* jobs, int32_t n_jobs, const float* rbf, const int32_t* rowptr,
+                           int64_t n_seg, int32_t D, int32_t R, void* stream);
+/* drbf (optional) receives the SUM of the jobs' basis gradients, in job order (X2G_GATE_DRBF_ACCUM:
+ * added to it); dw / db as x2g_rbf_gate_bwd's flags, X2G_DEFER_SLAB_SUM returning one x2g_slab_job
+ * per job in slab_jobs. */
+size_t x2g_rbf_gate_bwd_batch_workspace(int64_t rows, int32_t D, int32_t R, int32_t n_jobs);
+int x2g_rbf_gate_bwd_batch(const x2g_gate_job* jobs, int32_t n_jobs, const int32_t* owner, const float* rbf,
+                           int64_t rows, int32_t D, int32_t R, float* drbf, int flags, x2g_slab_job* slab_jobs,
+                           void* workspace, size_t workspace_bytes, void* stream);
+
 /* Slab counts (and so the part_b offset, part_w + splits*n_w) of a deferred call. */
 int32_t x2g_linear_wgrad_splits(int64_t rows, int32_t out_features, int32_t in_features);
 int32_t x2g_dense_bwd_splits(int64_t rows, int32_t in_features, int32_t out_features);

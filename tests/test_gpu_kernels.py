@@ -636,6 +636,55 @@ def test_rbf_pool_vs_torch(cuda):
     torch.testing.assert_close(b.grad, bq.grad, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("n_jobs,D,bias", [(5, 128, True), (2, 64, False), (8, 256, True)])
+def test_rbf_pool_batch_vs_torch(cuda, n_jobs, D, bias):
+    """ops.rbf_pool_batch (x2g_rbf_pool_fwd_batch / x2g_rbf_gate_bwd_batch: several readouts'
+    pools in one launch each way, the basis gradient summed over jobs) vs torch index_add +
+    autograd over ragged and empty segments, with and without a gradient bucket + deferred slab
+    sums; the forward is bitwise the single-job kernel's."""
+    from x2gnn import ops
+    from x2gnn.dist import GradBucket
+
+    rng = np.random.default_rng(n_jobs + D)
+    rowptr = _rowptr_with_empties(rng, 300, 17)
+    rows = int(rowptr[-1])
+    owner = torch.from_numpy(np.repeat(np.arange(300), np.diff(rowptr))).to(cuda)
+    rp = torch.from_numpy(rowptr).to(cuda)
+    rbf = torch.randn(rows, 6, device=cuda)
+    xs = [torch.randn(rows, D, device=cuda) for _ in range(n_jobs)]
+    lins = [torch.nn.Linear(6, D, bias=bias).to(cuda) for _ in range(n_jobs)]
+    gys = [torch.randn(300, D, device=cuda) for _ in range(n_jobs)]
+    for bucket in (False, True):
+        xr = [x.clone().requires_grad_(True) for x in xs]
+        rr = rbf.clone().requires_grad_(True)
+        for m in lins:
+            m.zero_grad(set_to_none=True)
+        bk = GradBucket([p for m in lins for p in m.parameters()]) if bucket else None
+        if bk is not None:
+            bk.zero()
+        outs = ops.rbf_pool_batch(xr, rr, [m.weight for m in lins], [m.bias for m in lins], owner, rp, 300)
+        for j in range(n_jobs):
+            single = ops.rbf_pool(xs[j], rbf, lins[j].weight.detach(), None if not bias else lins[j].bias.detach(),
+                                  owner, rp, 300)
+            assert torch.equal(outs[j].detach(), single)
+        with ops.deferred_wgrad():
+            torch.autograd.backward(outs, gys)
+        xq = [x.clone().requires_grad_(True) for x in xs]
+        rq = rbf.clone().requires_grad_(True)
+        ps = [(m.weight.detach().clone().requires_grad_(True),
+               m.bias.detach().clone().requires_grad_(True) if bias else None) for m in lins]
+        refs = [torch.zeros(300, D, device=cuda).index_add(0, owner, xq[j] * torch.nn.functional.linear(rq, *ps[j]))
+                for j in range(n_jobs)]
+        torch.autograd.backward(refs, gys)
+        for j in range(n_jobs):
+            torch.testing.assert_close(outs[j], refs[j], rtol=1e-5, atol=1e-4)
+            torch.testing.assert_close(xr[j].grad, xq[j].grad, rtol=1e-5, atol=1e-5)
+            torch.testing.assert_close(lins[j].weight.grad, ps[j][0].grad, rtol=1e-4, atol=1e-3)
+            if bias:
+                torch.testing.assert_close(lins[j].bias.grad, ps[j][1].grad, rtol=1e-4, atol=1e-3)
+        torch.testing.assert_close(rr.grad, rq.grad, rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("R,D,K", [(0, 128, 10), (1, 128, 10), (21058, 128, 10), (999, 64, 16), (5000, 12, 3)])
 def test_keyed_row_sum_vs_torch(cuda, R, D, K):
     """x2g_keyed_row_sum (gradient of a per-element table gather) vs index_add, and bitwise repeatable."""

@@ -345,6 +345,43 @@ def test_factorised_sbf_backward_equals_two_pass(cuda, monkeypatch, shape):
             assert float((g - ref).abs().max()) <= 1e-5 * scale + 1e-9, n
 
 
+def test_batched_readout_pools_match_per_readout(cuda, monkeypatch):
+    """The readouts' edge -> atom pools as one batched launch each way (ops.rbf_pool_batch, the
+    default) against one pool per readout: energies bitwise, every parameter gradient within fp32
+    reassociation error (the basis and layer-input gradients are summed in another order), for
+    the AtomWise and the MolWise (mean pool) model."""
+    import x2gnn
+    from x2gnn import ops
+    from x2gnn.data import collate
+    from x2gnn.synth import synthetic_molecules
+
+    cfg = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embedding_size=128)
+    batch = collate(synthetic_molecules(48, "S160", seed=11)).to(cuda)
+    calls = []
+    real = ops.rbf_pool_batch
+    monkeypatch.setattr(ops, "rbf_pool_batch", lambda *a, **k: calls.append(1) or real(*a, **k))
+    for build in (lambda: x2gnn.xgnn_poly(device="cuda", **cfg),
+                  lambda: x2gnn.xgnn_poly_global(device="cuda", pool_option="mean", **cfg)):
+        runs = []
+        calls.clear()
+        for batched in (True, False):
+            monkeypatch.setattr(ops, "_POOL_BATCH", batched)
+            torch.manual_seed(0)
+            m = build().to(cuda)
+            res = m(batch)
+            torch.nn.functional.smooth_l1_loss(res, batch.y).backward()
+            runs.append((res.detach().clone(), {n: p.grad.detach().clone() for n, p in m.named_parameters()
+                                                if p.grad is not None}))
+        assert len(calls) == 1
+        (r1, g1), (r0, g0) = runs
+        assert torch.equal(r1, r0)
+        assert g1.keys() == g0.keys()
+        top = max(float(g.abs().max()) for g in g0.values())
+        for n, g in g1.items():
+            ref = g0[n]
+            assert float((g - ref).abs().max()) <= 1e-5 * float(ref.abs().max()) + 1e-6 * top, n
+
+
 def test_fan_in_gradients_match_autograd_adds(cuda):
     """ops.FanIn (layer inputs and the radial basis summed in place by the fused ops' backward,
     csrc: dx_add / X2G_GATE_DRBF_ACCUM / X2G_CHAIN_RES_ACCUM) gives the same parameter gradients as

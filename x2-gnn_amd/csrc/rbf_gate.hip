@@ -94,15 +94,25 @@ __global__ void __launch_bounds__(256) rbf_gate_fwd_kernel(const f4v* __restrict
 
 // pool: one wave per segment, 64 / LPR rows per load, 8 loads in flight per lane (a QM9 atom's
 // ~9 edges are one round trip)
+// up to kGateMaxJobs pools over the same rows / segments / basis in one launch: job blockIdx.y
+constexpr int kGateMaxJobs = X2G_GATE_MAX_JOBS;
+struct PoolJobs {
+  const f4v* x[kGateMaxJobs];
+  const float* w[kGateMaxJobs];
+  const float* b[kGateMaxJobs];
+  f4v* out[kGateMaxJobs];
+};
+
 template <int LPR>
-__global__ void __launch_bounds__(256) rbf_pool_fwd_kernel(const f4v* __restrict__ x, const float* __restrict__ rbf,
-                                                           const float* __restrict__ W, const float* __restrict__ B,
-                                                           const int32_t* __restrict__ rowptr, int64_t G, int R,
-                                                           f4v* __restrict__ out) {
+__global__ void __launch_bounds__(256) rbf_pool_fwd_kernel(const PoolJobs J, const float* __restrict__ rbf,
+                                                           const int32_t* __restrict__ rowptr, int64_t G, int R) {
   constexpr int RPI = 64 / LPR;
   constexpr int UNROLL = 8;
   __shared__ float sw[4 * LPR * (kGateRMax + 1)];
-  stage_gate_weights<4 * LPR>(W, B, R, sw);
+  const int job = blockIdx.y;
+  const f4v* __restrict__ x = J.x[job];
+  f4v* __restrict__ out = J.out[job];
+  stage_gate_weights<4 * LPR>(J.w[job], J.b[job], R, sw);
   const int lane = threadIdx.x & 63;
   const int sub = lane % LPR, slot = lane / LPR;
   GateW<LPR> gw;
@@ -171,19 +181,36 @@ __device__ __forceinline__ float transpose_sum(const float (&p)[kGateRMax], int 
 
 // backward: block b owns rows [b * per, (b + 1) * per); slot s of the block takes every RPB-th
 // row; partial dW / db per block through LDS (fixed order over slots)
+// backward jobs: job blockIdx.y (drbf: the job's own buffer; a batch gives each job a partial)
+struct GateBwdJobs {
+  const f4v* g[kGateMaxJobs];
+  const f4v* x[kGateMaxJobs];
+  const float* w[kGateMaxJobs];
+  const float* b[kGateMaxJobs];
+  f4v* dx[kGateMaxJobs];
+  const f4v* dx_add[kGateMaxJobs];
+  float* drbf[kGateMaxJobs];
+  float* part_w[kGateMaxJobs];
+  float* part_b[kGateMaxJobs];
+};
+
 template <int LPR>
-__global__ void __launch_bounds__(256) rbf_gate_bwd_kernel(const f4v* __restrict__ g, const int32_t* __restrict__ owner,
-                                                           const f4v* __restrict__ x, const float* __restrict__ rbf,
-                                                           const float* __restrict__ W, const float* __restrict__ B,
-                                                           int64_t rows, int R, f4v* __restrict__ dx,
-                                                           const f4v* __restrict__ dx_add, float* __restrict__ drbf,
-                                                           int drbf_acc, float* __restrict__ part_w,
-                                                           float* __restrict__ part_b) {
+__global__ void __launch_bounds__(256) rbf_gate_bwd_kernel(const GateBwdJobs J, const int32_t* __restrict__ owner,
+                                                           const float* __restrict__ rbf, int64_t rows, int R,
+                                                           int drbf_acc) {
   constexpr int RPB = 256 / LPR;
   constexpr int D = 4 * LPR;
   __shared__ float red[RPB * D * (kGateRMax + 1)];
   __shared__ float sw[D * (kGateRMax + 1)];
-  stage_gate_weights<D>(W, B, R, sw);
+  const int job = blockIdx.y;
+  const f4v* __restrict__ g = J.g[job];
+  const f4v* __restrict__ x = J.x[job];
+  f4v* __restrict__ dx = J.dx[job];
+  const f4v* __restrict__ dx_add = J.dx_add[job];
+  float* __restrict__ drbf = J.drbf[job];
+  float* __restrict__ part_w = J.part_w[job];
+  float* __restrict__ part_b = J.part_b[job];
+  stage_gate_weights<D>(J.w[job], J.b[job], R, sw);
   const int sub = threadIdx.x % LPR, slot = threadIdx.x / LPR;
   GateW<LPR> gw;
   gw.load(sw, R, sub);
@@ -299,21 +326,58 @@ X2G_API int x2g_rbf_gate_fwd(const float* x, const float* rbf, const float* w, c
   return last_launch_status();
 }
 
+static int pool_launch(const PoolJobs& J, int n_jobs, const float* rbf, const int32_t* rowptr, int64_t G, int D, int R,
+                       hipStream_t st) {
+  const int64_t want = (G + 3) / 4;
+  const dim3 grid(static_cast<unsigned>(want < 2048 ? want : 2048), static_cast<unsigned>(n_jobs));
+  switch (D) {
+    case 64: rbf_pool_fwd_kernel<16><<<grid, 256, 0, st>>>(J, rbf, rowptr, G, R); break;
+    case 128: rbf_pool_fwd_kernel<32><<<grid, 256, 0, st>>>(J, rbf, rowptr, G, R); break;
+    default: rbf_pool_fwd_kernel<64><<<grid, 256, 0, st>>>(J, rbf, rowptr, G, R); break;
+  }
+  return last_launch_status();
+}
+
 X2G_API int x2g_rbf_pool_fwd(const float* x, const float* rbf, const float* w, const float* b, const int32_t* rowptr,
                              int64_t G, int32_t D, int32_t R, float* out, void* stream) {
   if (G < 0 || !gate_shape_ok(D, R)) return G < 0 ? X2G_EINVAL : X2G_EUNSUPPORTED;
   if (G == 0) return X2G_OK;
   if (!x || !rbf || !w || !rowptr || !out) return X2G_EINVAL;
   if (!al16(x) || !al16(out)) return X2G_EINVAL;
-  const auto* xv = reinterpret_cast<const f4v*>(x);
-  auto* ov = reinterpret_cast<f4v*>(out);
-  const int64_t want = (G + 3) / 4;
-  const unsigned grid = static_cast<unsigned>(want < 2048 ? want : 2048);
-  hipStream_t st = as_stream(stream);
+  PoolJobs J{};
+  J.x[0] = reinterpret_cast<const f4v*>(x);
+  J.w[0] = w;
+  J.b[0] = b;
+  J.out[0] = reinterpret_cast<f4v*>(out);
+  return pool_launch(J, 1, rbf, rowptr, G, D, R, as_stream(stream));
+}
+
+X2G_API int x2g_rbf_pool_fwd_batch(const x2g_gate_job* jobs, int32_t n_jobs, const float* rbf, const int32_t* rowptr,
+                                   int64_t G, int32_t D, int32_t R, void* stream) {
+  if (!jobs || n_jobs < 1 || n_jobs > kGateMaxJobs || G < 0) return X2G_EINVAL;
+  if (!gate_shape_ok(D, R)) return X2G_EUNSUPPORTED;
+  if (G == 0) return X2G_OK;
+  if (!rbf || !rowptr) return X2G_EINVAL;
+  PoolJobs J{};
+  for (int j = 0; j < n_jobs; ++j) {
+    const x2g_gate_job& q = jobs[j];
+    if (!q.x || !q.w || !q.out) return X2G_EINVAL;
+    if (!al16(q.x) || !al16(q.out)) return X2G_EINVAL;
+    J.x[j] = reinterpret_cast<const f4v*>(q.x);
+    J.w[j] = q.w;
+    J.b[j] = q.b;
+    J.out[j] = reinterpret_cast<f4v*>(q.out);
+  }
+  return pool_launch(J, n_jobs, rbf, rowptr, G, D, R, as_stream(stream));
+}
+
+static int gate_bwd_launch(const GateBwdJobs& J, int n_jobs, const int32_t* owner, const float* rbf, int64_t rows,
+                           int D, int R, int drbf_acc, int splits, hipStream_t st) {
+  const dim3 grid(static_cast<unsigned>(splits), static_cast<unsigned>(n_jobs));
   switch (D) {
-    case 64: rbf_pool_fwd_kernel<16><<<grid, 256, 0, st>>>(xv, rbf, w, b, rowptr, G, R, ov); break;
-    case 128: rbf_pool_fwd_kernel<32><<<grid, 256, 0, st>>>(xv, rbf, w, b, rowptr, G, R, ov); break;
-    default: rbf_pool_fwd_kernel<64><<<grid, 256, 0, st>>>(xv, rbf, w, b, rowptr, G, R, ov); break;
+    case 64: rbf_gate_bwd_kernel<16><<<grid, 256, 0, st>>>(J, owner, rbf, rows, R, drbf_acc); break;
+    case 128: rbf_gate_bwd_kernel<32><<<grid, 256, 0, st>>>(J, owner, rbf, rows, R, drbf_acc); break;
+    default: rbf_gate_bwd_kernel<64><<<grid, 256, 0, st>>>(J, owner, rbf, rows, R, drbf_acc); break;
   }
   return last_launch_status();
 }
@@ -346,27 +410,67 @@ X2G_API int x2g_rbf_gate_bwd(const float* g, const int32_t* owner, const float* 
   if (!al16(g) || !al16(x) || (dx && !al16(dx)) || (dx_add && !al16(dx_add))) return X2G_EINVAL;
   if (!ws || wsb < x2g_rbf_gate_bwd_workspace(rows, D, R)) return X2G_EWORKSPACE;
   const int splits = gate_bwd_splits(rows);
-  float* part_w = static_cast<float*>(ws);
-  float* part_b = db ? part_w + static_cast<int64_t>(splits) * D * R : nullptr;
-  const auto* gv = reinterpret_cast<const f4v*>(g);
-  const auto* xv = reinterpret_cast<const f4v*>(x);
-  auto* dxv = reinterpret_cast<f4v*>(dx);
-  const auto* dav = reinterpret_cast<const f4v*>(dx_add);
-  switch (D) {
-    case 64:
-      rbf_gate_bwd_kernel<16><<<splits, 256, 0, st>>>(gv, owner, xv, rbf, w, b, rows, R, dxv, dav, drbf, drbf_acc,
-                                                       part_w, part_b);
-      break;
-    case 128:
-      rbf_gate_bwd_kernel<32><<<splits, 256, 0, st>>>(gv, owner, xv, rbf, w, b, rows, R, dxv, dav, drbf, drbf_acc,
-                                                       part_w, part_b);
-      break;
-    default:
-      rbf_gate_bwd_kernel<64><<<splits, 256, 0, st>>>(gv, owner, xv, rbf, w, b, rows, R, dxv, dav, drbf, drbf_acc,
-                                                       part_w, part_b);
-      break;
-  }
-  if (int rc = last_launch_status()) return rc;
+  GateBwdJobs J{};
+  J.g[0] = reinterpret_cast<const f4v*>(g);
+  J.x[0] = reinterpret_cast<const f4v*>(x);
+  J.w[0] = w;
+  J.b[0] = b;
+  J.dx[0] = reinterpret_cast<f4v*>(dx);
+  J.dx_add[0] = reinterpret_cast<const f4v*>(dx_add);
+  J.drbf[0] = drbf;
+  J.part_w[0] = static_cast<float*>(ws);
+  J.part_b[0] = db ? J.part_w[0] + static_cast<int64_t>(splits) * D * R : nullptr;
+  if (int rc = gate_bwd_launch(J, 1, owner, rbf, rows, D, R, drbf_acc, splits, st)) return rc;
   if (flags & X2G_DEFER_SLAB_SUM) return X2G_OK;
-  return sum_slabs_launch(part_w, static_cast<int64_t>(D) * R, part_b, D, splits, dw, db, accum, st);
+  return sum_slabs_launch(J.part_w[0], static_cast<int64_t>(D) * R, J.part_b[0], D, splits, dw, db, accum, st);
+}
+
+X2G_API size_t x2g_rbf_gate_bwd_batch_workspace(int64_t rows, int32_t D, int32_t R, int32_t n_jobs) {
+  if (rows <= 0 || D <= 0 || R <= 0 || n_jobs < 1) return 0;
+  return static_cast<size_t>(n_jobs) * (static_cast<size_t>(gate_bwd_splits(rows)) * D * (R + 1) + rows * R) *
+         sizeof(float);
+}
+
+X2G_API int x2g_rbf_gate_bwd_batch(const x2g_gate_job* jobs, int32_t n_jobs, const int32_t* owner, const float* rbf,
+                                   int64_t rows, int32_t D, int32_t R, float* drbf, int flags,
+                                   x2g_slab_job* slab_jobs, void* ws, size_t wsb, void* stream) {
+  if (!jobs || n_jobs < 1 || n_jobs > kGateMaxJobs || rows <= 0) return X2G_EINVAL;
+  if (!gate_shape_ok(D, R)) return X2G_EUNSUPPORTED;
+  if (flags & ~(X2G_ACCUM_WGRAD | X2G_DEFER_SLAB_SUM | X2G_GATE_DRBF_ACCUM)) return X2G_EINVAL;
+  if ((flags & X2G_DEFER_SLAB_SUM) && !slab_jobs) return X2G_EINVAL;
+  if (!rbf) return X2G_EINVAL;
+  if (!ws || wsb < x2g_rbf_gate_bwd_batch_workspace(rows, D, R, n_jobs)) return X2G_EWORKSPACE;
+  hipStream_t st = as_stream(stream);
+  const int splits = gate_bwd_splits(rows);
+  const int64_t per_w = static_cast<int64_t>(splits) * D * R, per_b = static_cast<int64_t>(splits) * D;
+  float* base = static_cast<float*>(ws);
+  float* scratch = base + n_jobs * (per_w + per_b);  // per-job drbf partials [n_jobs][rows][R]
+  GateBwdJobs J{};
+  x2g_slab_job sj[kGateMaxJobs];
+  for (int j = 0; j < n_jobs; ++j) {
+    const x2g_gate_job& q = jobs[j];
+    if (!q.g || !q.x || !q.w || !q.dw || (q.dx_add && !q.dx)) return X2G_EINVAL;
+    if (!al16(q.g) || !al16(q.x) || (q.dx && !al16(q.dx)) || (q.dx_add && !al16(q.dx_add))) return X2G_EINVAL;
+    J.g[j] = reinterpret_cast<const f4v*>(q.g);
+    J.x[j] = reinterpret_cast<const f4v*>(q.x);
+    J.w[j] = q.w;
+    J.b[j] = q.b;
+    J.dx[j] = reinterpret_cast<f4v*>(q.dx);
+    J.dx_add[j] = reinterpret_cast<const f4v*>(q.dx_add);
+    J.drbf[j] = drbf ? scratch + static_cast<int64_t>(j) * rows * R : nullptr;
+    J.part_w[j] = base + j * per_w;
+    J.part_b[j] = q.db ? base + n_jobs * per_w + j * per_b : nullptr;
+    sj[j] = x2g_slab_job{J.part_w[j], J.part_b[j], q.dw, q.db, static_cast<int64_t>(D) * R, q.db ? D : 0, splits, 0,
+                         0};
+  }
+  if (int rc = gate_bwd_launch(J, n_jobs, owner, rbf, rows, D, R, 0, splits, st)) return rc;
+  if (drbf) {  // the jobs' basis gradients summed in job order (+ the old value)
+    const bool acc = flags & X2G_GATE_DRBF_ACCUM;
+    if (int rc = sum_slabs_launch(scratch, rows * R, nullptr, 0, n_jobs, drbf, nullptr, acc, st)) return rc;
+  }
+  if (flags & X2G_DEFER_SLAB_SUM) {
+    for (int j = 0; j < n_jobs; ++j) slab_jobs[j] = sj[j];
+    return X2G_OK;
+  }
+  return x2g_slab_sum_batch(sj, n_jobs, (flags & X2G_ACCUM_WGRAD) ? 1 : 0, stream);
 }

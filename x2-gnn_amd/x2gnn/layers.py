@@ -254,6 +254,10 @@ class MolWise(nn.Module):
     def features(self, x, rbf, num_atoms, edge_index_0, atom_batch, dim_size, atom_rowptr=None, mol_rowptr=None):
         """The MLP input: edges -> atoms -> molecules (readout.py:66-71)."""
         out = _edge_pool(x, rbf, self.lin_rbf, edge_index_0, num_atoms, atom_rowptr)
+        return self.finish(out, atom_batch, dim_size, mol_rowptr)
+
+    def finish(self, out, atom_batch, dim_size, mol_rowptr=None):
+        """atoms -> molecules (readout.py:68-71) of the pooled [num_atoms, D] features."""
         if mol_rowptr is None:
             mol_rowptr = ops.csr_rowptr(atom_batch, dim_size)
         pooled = ops.segment_sum(out, mol_rowptr, dim_size)

@@ -92,7 +92,7 @@ class _Trunk(nn.Module):
         return ([(mods[0], ops.ACT_SILU, -1), (mods[2], ops.ACT_NONE, 0)]
                 + [(c.lin_edge, ops.ACT_NONE, 1) for c in self.convs])
 
-    def _layers(self, data, plan, readout_fn, feature_fn=None):
+    def _layers(self, data, plan, readout_fn, feature_fn=None, pool_fn=None):
         per_dst = "edge_attr_row" in data._store
         edge_proj = data._store.get("_x2g_edge_proj") if per_dst else None
         # lin_edge tables precomputed by the featurisation's table chain, or edgenn here
@@ -113,9 +113,15 @@ class _Trunk(nn.Module):
         grouped = (out.is_cuda and side is None and feature_fn is not None
                    and os.environ.get("X2G_GROUPED_READOUT", "1") == "1")
         feats = []
+        # the readouts' edge -> atom pools of every layer output as one launch each way (pool_fn,
+        # ops.rbf_pool_batch) after the last layer; per readout where that is unsupported
+        pooled_xs = [] if grouped and pool_fn is not None else None
 
         def readout(i, x):
             nonlocal results
+            if pooled_xs is not None:
+                pooled_xs.append(x)
+                return
             if grouped:
                 feats.append(feature_fn(i, x))
                 return
@@ -148,6 +154,10 @@ class _Trunk(nn.Module):
         if side is not None:
             main.wait_stream(side)
             results.record_stream(main)
+        if pooled_xs is not None:
+            feats = pool_fn(pooled_xs)
+            if feats is None:
+                feats = [feature_fn(i, x) for i, x in enumerate(pooled_xs)]
         if grouped:
             mlps = [r.mlp for r in self.readouts]
             if ops.readout_mlps_supported(feats, mlps):
@@ -157,6 +167,15 @@ class _Trunk(nn.Module):
                 results = r if results is None else results + r
         return results
 
+
+    def _pool_batch(self, xs, rbf, edge_index_0, plan):
+        """Every readout's edge -> atom pool (readout.py:39-41 / 66-67) in one launch each way, or
+        None where the batched kernels do not cover the shapes."""
+        lins = [r.lin_rbf for r in self.readouts]
+        if rbf is None or len(xs) != len(lins) or not ops.rbf_pool_batch_supported(xs, rbf, [l.weight for l in lins]):
+            return None
+        return ops.rbf_pool_batch(xs, rbf, [l.weight for l in lins], [l.bias for l in lins], edge_index_0,
+                                  plan.atom_rowptr, plan.num_atoms)
 
     def _tail_linears(self, i):
         lins = [self.bf_skip[i].lin0, self.bf_skip[i].lin1, self.dense_bf_skip[i]]
@@ -214,7 +233,10 @@ class SBFTransformer(_Trunk):
             return self.readouts[i].features(x=x, rbf=data.node_rbf, num_atoms=plan.num_atoms,
                                              edge_index_0=edge_index_0, atom_rowptr=plan.atom_rowptr)
 
-        per_atom = self._layers(data, plan, readout, features)
+        def pools(xs):
+            return self._pool_batch(xs, data.node_rbf, edge_index_0, plan)
+
+        per_atom = self._layers(data, plan, readout, features, pools)
         return ops.segment_sum(per_atom, plan.mol_ptr, plan.out_graphs).view(-1)
 
 
@@ -238,4 +260,10 @@ class SBFTransformerGlobal(_Trunk):
         def features(i, x):
             return self.readouts[i].features(x=x, **kw)
 
-        return self._layers(data, plan, readout, features).view(-1)
+        def pools(xs):
+            atoms = self._pool_batch(xs, data.node_rbf, edge_index_0, plan)
+            if atoms is None:
+                return None
+            return [r.finish(a, atom_batch, plan.out_graphs, kw["mol_rowptr"]) for r, a in zip(self.readouts, atoms)]
+
+        return self._layers(data, plan, readout, features, pools).view(-1)

@@ -1505,6 +1505,115 @@ class _RbfPoolFn(torch.autograd.Function):
         return (dx if first_x else None), (drbf if first_r else None), dw, db, None, None, None
 
 
+def _addr(t):
+    """Raw device address of a tensor for a ctypes struct field (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+class GateJob(ctypes.Structure):
+    """x2g_gate_job."""
+    _fields_ = [("x", ctypes.c_void_p), ("w", ctypes.c_void_p), ("b", ctypes.c_void_p), ("out", ctypes.c_void_p),
+                ("g", ctypes.c_void_p), ("dx", ctypes.c_void_p), ("dx_add", ctypes.c_void_p), ("dw", ctypes.c_void_p),
+                ("db", ctypes.c_void_p)]
+
+
+GATE_MAX_JOBS = 8  # X2G_GATE_MAX_JOBS
+# the readouts' edge -> atom pools as one launch each way (x2g_rbf_pool_fwd_batch / _gate_bwd_batch)
+_POOL_BATCH = os.environ.get("X2G_POOL_BATCH", "1") == "1"
+
+
+class _RbfPoolBatchFn(torch.autograd.Function):
+    """Several rbf pools over the same rows / atoms / basis (_RbfPoolFn's math per job), one launch
+    each way; the basis gradient is the jobs' sum (one fan-in consumer for the whole batch)."""
+
+    @staticmethod
+    def forward(ctx, n, rbf, owner, rowptr, n_seg, *tensors):
+        xs, ws, bs = tensors[:n], tensors[n:2 * n], tensors[2 * n:]
+        rbf2 = _f32(rbf)
+        x2 = [_f32(x) for x in xs]
+        W = [_f32(w) for w in ws]
+        B = [_f32(b) if b is not None else None for b in bs]
+        D, R = x2[0].shape[1], rbf2.shape[1]
+        outs = [torch.empty(n_seg, D, dtype=torch.float32, device=rbf2.device) for _ in range(n)]
+        jobs = (GateJob * n)(*[GateJob(x2[j].data_ptr(), W[j].data_ptr(), _addr(B[j]), outs[j].data_ptr(), None, None,
+                                       None, None, None) for j in range(n)])
+        call("x2g_rbf_pool_fwd_batch", jobs, n, ptr(rbf2), ptr(rowptr), n_seg, D, R, stream_ptr())
+        ctx.save_for_backward(rbf2, *x2, *W)
+        ctx.n, ctx.n_seg, ctx.B, ctx.owner, ctx.params = n, n_seg, B, owner, (ws, bs)
+        ctx.fan_x = [_fan_of(x) for x in xs]
+        ctx.fan_r = _fan_of(rbf)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gps):
+        n = ctx.n
+        saved = ctx.saved_tensors
+        rbf2, x2, W = saved[0], saved[1:1 + n], saved[1 + n:1 + 2 * n]
+        ws, bs = ctx.params
+        rows, D = x2[0].shape
+        R = rbf2.shape[1]
+        dev = rbf2.device
+        need_r = ctx.needs_input_grad[1]
+        drbf, first_r = None, True
+        if need_r:
+            if ctx.fan_r is not None:
+                drbf, first_r = ctx.fan_r.take(rbf2.shape, dev)
+            else:
+                drbf = torch.empty(rows, R, dtype=torch.float32, device=dev)
+        dx_ret, jobs, keep, sinks = [], [], [], []
+        for j in range(n):
+            need_x = ctx.needs_input_grad[5 + j]
+            dx, first = None, True
+            if need_x:
+                if ctx.fan_x[j] is not None:
+                    dx, first = ctx.fan_x[j].take(x2[j].shape, dev)
+                else:
+                    dx = torch.empty(rows, D, dtype=torch.float32, device=dev)
+            dx_ret.append(dx if (need_x and first) else None)
+            has_b = ctx.B[j] is not None
+            gw, gb = grad_sink(ws[j]), (grad_sink(bs[j]) if has_b else None)
+            accum = gw is not None and (gb is not None or not has_b)
+            if not accum:
+                gw = torch.empty(D, R, dtype=torch.float32, device=dev)
+                gb = torch.empty(D, dtype=torch.float32, device=dev) if has_b else None
+            sinks.append((accum, gw, gb))
+            g = _f32(gps[j]) if gps[j] is not None else torch.zeros(ctx.n_seg, D, dtype=torch.float32, device=dev)
+            keep.append(g)
+            jobs.append(GateJob(x2[j].data_ptr(), W[j].data_ptr(), _addr(ctx.B[j]), None, g.data_ptr(), _addr(dx),
+                                None if first else _addr(dx), gw.data_ptr(), _addr(gb)))
+        accums = {a for a, _, _ in sinks}
+        if len(accums) != 1:
+            raise RuntimeError("rbf_pool_batch: mixed bucket / plain weight gradients in one batch")
+        accum = accums.pop()
+        lib = _lib.load()
+        ws_bytes = int(lib.x2g_rbf_gate_bwd_batch_workspace(rows, D, R, n))
+        wsb = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        defer = accum and _DEFER is not None
+        flags = (ACCUM_WGRAD if accum else 0) | (DEFER_SLAB_SUM if defer else 0) | (0 if first_r else GATE_DRBF_ACCUM)
+        out = (SlabJob * n)()
+        call("x2g_rbf_gate_bwd_batch", (GateJob * n)(*jobs), n, ptr(ctx.owner), ptr(rbf2), rows, D, R, ptr(drbf), flags,
+             out, ptr(wsb), ws_bytes, stream_ptr())
+        if defer:
+            _DEFER.jobs.extend(out)
+            _DEFER.keep.append(wsb)
+        dws = [None if accum else gw for _, gw, _ in sinks]
+        dbs = [None if accum else gb for _, _, gb in sinks]
+        return (None, drbf if (need_r and first_r) else None, None, None, None, *dx_ret, *dws, *dbs)
+
+
+def rbf_pool_batch(xs, rbf, weights, biases, owner, rowptr, n_seg: int):
+    """[rbf_pool(x_j, rbf, W_j, b_j, owner, rowptr, n_seg) for j] in one launch each way."""
+    _need_cuda(rbf, *xs)
+    n = len(xs)
+    return list(_RbfPoolBatchFn.apply(n, rbf, _i32(owner), _i32(rowptr), int(n_seg), *xs, *weights, *biases))
+
+
+def rbf_pool_batch_supported(xs, rbf, weights):
+    return (_POOL_BATCH and 1 < len(xs) <= GATE_MAX_JOBS and all(x.is_cuda and x.dim() == 2 for x in xs)
+            and len({tuple(x.shape) for x in xs}) == 1 and gate_supported(xs[0].shape[1], rbf.shape[1])
+            and all(tuple(w.shape) == (xs[0].shape[1], rbf.shape[1]) for w in weights))
+
+
 def rbf_pool(x, rbf, weight, bias, owner, rowptr, n_seg: int):
     """Segment sums of x * lin_rbf(rbf) over rows sorted by ``owner`` (CSR ``rowptr``)."""
     _need_cuda(x, rbf)
