@@ -129,7 +129,25 @@ class Batch(Data):
                 out._store[k] = torch.as_tensor(np.array([np.asarray(v) for v in vals]).reshape(-1))
         out._store["batch"] = torch.repeat_interleave(torch.arange(len(data_list)), torch.as_tensor(nodes))
         out._store["ptr"] = torch.as_tensor(np.concatenate([[0], np.cumsum(nodes)]))
+        _add_device_indices(out, nodes, edges)
         return out
+
+
+def _add_device_indices(b, nodes, edges):
+    """The int32 index forms the device path consumes (GraphPlan.from_atom_batch), made here on
+    the host with the rest of the collate instead of by cast / cumsum / gather kernels in every
+    step: edge source / destination atoms, the molecule atom and line-node offsets and each line
+    node's destination element.  Under private ``_x2g_`` keys; a batch without them (built
+    elsewhere) takes the device fallback."""
+    ei = b._store.get("edge_index")
+    if ei is None or "x" not in b._store:
+        return
+    ei_np = ei.numpy()
+    b._store["_x2g_edge_src"] = torch.from_numpy(np.ascontiguousarray(ei_np[0], dtype=np.int32))
+    b._store["_x2g_edge_dst"] = torch.from_numpy(np.ascontiguousarray(ei_np[1], dtype=np.int32))
+    b._store["_x2g_mol_ptr"] = torch.from_numpy(np.concatenate([[0], np.cumsum(nodes)]).astype(np.int32))
+    b._store["_x2g_line_ptr"] = torch.from_numpy(np.concatenate([[0], np.cumsum(edges)]).astype(np.int32))
+    b._store["_x2g_dst_type"] = torch.from_numpy(b._store["x"].numpy()[ei_np[1]].astype(np.int32))
 
 
 def molecule_to_data(mol: dict) -> Data:

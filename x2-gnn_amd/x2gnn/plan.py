@@ -47,14 +47,19 @@ class GraphPlan:
         p.out_graphs = int(nz[-1]) + 1 if len(nz) else 0
         ei = data.edge_index
         dev = ei.device
-        p.lg = ops.vertex_to_edge(ei, p.num_atoms, p.num_triplets)
-        p.atom_rowptr = p.lg.atom_rowptr
-        p.line_ptr = _ptr_from_counts(data.edge_num, p.num_graphs, dev)
-        if "ptr" in data._store:
-            p.mol_ptr = ops._i32(data.ptr)
+        st = data._store
+        if "_x2g_edge_src" in st and st["_x2g_edge_src"].device == dev:  # int32 forms from the collate
+            p.lg = ops.LineGraph(st["_x2g_edge_src"], st["_x2g_edge_dst"], p.num_atoms, p.num_triplets)
+            p.line_ptr, p.mol_ptr, p.dst_type = st["_x2g_line_ptr"], st["_x2g_mol_ptr"], st["_x2g_dst_type"]
         else:
-            p.mol_ptr = (torch.arange(2, device=dev, dtype=torch.int32) * p.num_atoms)
-        p.dst_type = ops._i32(data.x.index_select(0, p.lg.edge_dst))
+            p.lg = ops.vertex_to_edge(ei, p.num_atoms, p.num_triplets)
+            p.line_ptr = _ptr_from_counts(data.edge_num, p.num_graphs, dev)
+            if "ptr" in st:
+                p.mol_ptr = ops._i32(data.ptr)
+            else:
+                p.mol_ptr = (torch.arange(2, device=dev, dtype=torch.int32) * p.num_atoms)
+            p.dst_type = ops._i32(data.x.index_select(0, p.lg.edge_dst))
+        p.atom_rowptr = p.lg.atom_rowptr
         return p
 
     # ------------------------------------------------------------------ from line-graph tensors
