@@ -9,6 +9,8 @@ read (and can be captured in a HIP graph).
 from __future__ import annotations
 
 import numpy as np
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -48,7 +50,7 @@ class GraphPlan:
         ei = data.edge_index
         dev = ei.device
         st = data._store
-        if "_x2g_edge_src" in st and st["_x2g_edge_src"].device == dev:  # int32 forms from the collate
+        if _HOST_INDICES and "_x2g_edge_src" in st and st["_x2g_edge_src"].device == dev:  # int32 forms (collate)
             p.lg = ops.LineGraph(st["_x2g_edge_src"], st["_x2g_edge_dst"], p.num_atoms, p.num_triplets)
             p.line_ptr, p.mol_ptr, p.dst_type = st["_x2g_line_ptr"], st["_x2g_mol_ptr"], st["_x2g_dst_type"]
         else:
@@ -85,6 +87,9 @@ class GraphPlan:
         p.line_ptr = ops.csr_rowptr(b, p.num_graphs)
         p.mol_ptr = ops.csr_rowptr(atom_batch, p.num_graphs)
         return p
+
+
+_HOST_INDICES = os.environ.get("X2G_HOST_INDICES", "1") == "1"
 
 
 def _ptr_from_counts(counts, n, device):
