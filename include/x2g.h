@@ -71,6 +71,20 @@ int x2g_line_graph_transpose(const int32_t* trip_src, int64_t num_triplets, int6
                              int32_t* src_rowptr, int32_t* src_perm, void* workspace,
                              size_t workspace_bytes, void* stream);
 
+/* The same two operations for a SYMMETRIC edge set (b->a present for every a->b, as every
+ * molecular graph: atom_graph.py:42-45 builds it from a symmetric distance test); the caller
+ * asserts it (x2gnn's collate checks it on the host).  Per-edge counts are then degrees (deg(b) - 1
+ * triplets per destination a->b and per source b->k), so count and scan are one launch, and the
+ * transposed lists are written in order directly (no atomics, no segment sort).  Outputs equal
+ * x2g_vertex_to_edge's / x2g_line_graph_transpose's bit for bit on such graphs. */
+int x2g_vertex_to_edge_sym(const int32_t* edge_src, const int32_t* edge_dst, int64_t num_edges, int64_t num_nodes,
+                           int64_t num_triplets, int32_t* atom_rowptr, int32_t* trip_rowptr, int32_t* trip_src,
+                           int32_t* trip_dst, int32_t* atom_j, int32_t* atom_i, int32_t* atom_k, void* workspace,
+                           size_t workspace_bytes, void* stream);
+int x2g_line_graph_transpose_sym(const int32_t* edge_src, const int32_t* edge_dst, const int32_t* atom_rowptr,
+                                 const int32_t* trip_rowptr, int64_t num_edges, int32_t* src_rowptr,
+                                 int32_t* src_perm, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------- basis (featurisation) */
 
 /* rbf_env[e, l*R+n] = env(d_e) * N_ln j_l(z_ln d_e/cutoff)   (l < 7, n < 6, R = 6)

@@ -89,6 +89,47 @@ def test_vertex_to_edge_edge_cases(cuda):
     _check_transpose(lg)
 
 
+def _sym_vs_generic(ei, n, T, cuda):
+    """x2g_vertex_to_edge_sym / x2g_line_graph_transpose_sym against the generic builder and
+    transpose on the same symmetric graph: every output bit-for-bit."""
+    from x2gnn import ops
+
+    e = torch.from_numpy(ei.astype(np.int64)).to(cuda)
+    gen = ops.vertex_to_edge(e, n, T)
+    sym = ops.vertex_to_edge(e, n, T, symmetric=True)
+    for name in ("atom_rowptr", "trip_rowptr", "trip_src", "trip_dst", "atom_j", "atom_i", "atom_k"):
+        assert torch.equal(getattr(gen, name), getattr(sym, name)), name
+    for a, b in zip(gen.src_csr(), sym.src_csr()):
+        assert torch.equal(a, b)
+    return sym
+
+
+def test_symmetric_builder_and_transpose_equal_generic(cuda):
+    """The degree-count builder and the direct (no atomics, no sort) transpose for symmetric edge
+    sets: the symmetric fixtures, a full config-2 batch (collate marks it symmetric), a hub of
+    degree 70, isolated atoms, no edges, and a graph larger than the one-workgroup scan
+    (E > 262144: the multi-workgroup scan path)."""
+    from x2gnn.data import collate
+    from x2gnn.synth import synthetic_molecules
+
+    z = golden("triplets.npz")
+    for case in z["cases"]:
+        ei, n = z[f"{case}_edge_index"], int(z[f"{case}_num_nodes"])
+        fwd = set(zip(ei[0].tolist(), ei[1].tolist()))
+        if all((b, a) in fwd for a, b in fwd):
+            _sym_vs_generic(ei, n, z[f"{case}_trip"].shape[1], cuda)
+    b = collate(synthetic_molecules(128, "S160", seed=3))
+    assert b._store["_x2g_symmetric"]
+    _sym_vs_generic(b.edge_index.numpy(), b.num_nodes, int(b._meta["triplets"].sum()), cuda)
+    hub = np.array([[0] * 70 + list(range(1, 71)), list(range(1, 71)) + [0] * 70])
+    hub = hub[:, np.lexsort((hub[1], hub[0]))]
+    _sym_vs_generic(hub, 75, triplets.vertex_to_edge(hub, 75)[0].shape[1], cuda)
+    _sym_vs_generic(np.zeros((2, 0), dtype=np.int64), 3, 0, cuda)
+    big = collate(synthetic_molecules(1800, "S160", seed=5))
+    assert big.edge_index.shape[1] > 262144
+    _sym_vs_generic(big.edge_index.numpy(), big.num_nodes, int(big._meta["triplets"].sum()), cuda)
+
+
 def test_csr_rowptr(cuda):
     from x2gnn import ops
 

@@ -212,6 +212,88 @@ __global__ void sort_segments(const int32_t* __restrict__ rowptr, int64_t n_seg,
   }
 }
 
+
+// ----------------------------------------------------------------------------- symmetric graphs
+// A molecule's edge set is symmetric (a->b present iff b->a is, atom_graph.py:42-45 builds it from
+// a symmetric distance test), which makes both per-edge counts a degree: destination e = (a->b)
+// has deg(b) - 1 triplets (b->a is the one excluded) and source s = (b->k) feeds deg(b) - 1
+// destinations (a->b), a != k.  Counting needs no search, so count and scan are one single-
+// workgroup launch (per thread a contiguous run of edges: sum, block scan, write), and the
+// transposed lists are written directly in order instead of by atomics plus a segment sort.
+constexpr int kScan1Threads = 1024;
+constexpr int64_t kScan1Max = 262144;  // one workgroup up to this many edges (256 per thread)
+
+// out[i] = sum_{j < i} (deg(atom[j]) - 1), out[n] = total, deg from atom_rowptr
+__global__ void __launch_bounds__(kScan1Threads) degree_scan_1wg(const int32_t* __restrict__ atom,
+                                                                const int32_t* __restrict__ atom_rowptr, int64_t n,
+                                                                int32_t* __restrict__ out) {
+  __shared__ int lds[kScan1Threads / 64];
+  const int64_t per = (n + kScan1Threads - 1) / kScan1Threads;
+  const int64_t lo = per * threadIdx.x, hi = lo + per < n ? lo + per : n;
+  int sum = 0;
+  for (int64_t i = lo; i < hi; ++i) {
+    const int a = atom[i];
+    const int c = atom_rowptr[a + 1] - atom_rowptr[a] - 1;
+    sum += c > 0 ? c : 0;
+  }
+  int total;
+  int run = block_exclusive_scan(sum, lds, &total);
+  for (int64_t i = lo; i < hi; ++i) {
+    out[i] = run;
+    const int a = atom[i];
+    const int c = atom_rowptr[a + 1] - atom_rowptr[a] - 1;
+    run += c > 0 ? c : 0;
+  }
+  if (threadIdx.x == 0) out[n] = total;
+}
+
+// count[i] = deg(atom[i]) - 1 for the multi-workgroup scan of larger graphs
+__global__ void degree_count(const int32_t* __restrict__ atom, const int32_t* __restrict__ atom_rowptr, int64_t n,
+                             int32_t* __restrict__ count) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int a = atom[i];
+  const int c = atom_rowptr[a + 1] - atom_rowptr[a] - 1;
+  count[i] = c > 0 ? c : 0;
+}
+
+int degree_scan(const int32_t* atom, const int32_t* atom_rowptr, int64_t n, int32_t* out, int32_t* count,
+                int32_t* partial, hipStream_t st) {
+  if (n <= kScan1Max) {
+    degree_scan_1wg<<<1, kScan1Threads, 0, st>>>(atom, atom_rowptr, n, out);
+    return last_launch_status();
+  }
+  degree_count<<<blocks_for(n, 256), 256, 0, st>>>(atom, atom_rowptr, n, count);
+  if (int rc = last_launch_status()) return rc;
+  return exclusive_scan(count, n, out, partial, st);
+}
+
+// Source s = (b->k) lists its triplets (s -> e), e = (a->b) over b's neighbours a != k in
+// ascending a (= ascending edge id of e = ascending triplet id).  In e's destination list (b's
+// out-edges minus b->a, ascending) s sits at rank_b(k) - [rank_b(a) < rank_b(k)], so the triplet
+// id is trip_rowptr[e] plus that; e itself is found in a's sorted out-list.  One thread per source.
+__global__ void transpose_sym_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                                     const int32_t* __restrict__ atom_rowptr, const int32_t* __restrict__ trip_rowptr,
+                                     const int32_t* __restrict__ src_rowptr, int64_t E,
+                                     int32_t* __restrict__ src_perm) {
+  const int64_t s = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (s >= E) return;
+  const int b = src[s], k = dst[s];
+  const int lo = atom_rowptr[b], hi = atom_rowptr[b + 1];
+  const int rank_k = static_cast<int>(s) - lo;
+  int out = src_rowptr[s];
+  for (int idx = lo; idx < hi; ++idx) {
+    const int a = dst[idx];
+    if (a == k) continue;
+    const int alo = atom_rowptr[a], ahi = atom_rowptr[a + 1];
+    const int e = lower_bound(dst, alo, ahi, b);  // edge a->b (present: the graph is symmetric)
+    src_perm[out++] = trip_rowptr[e] + rank_k - (idx - lo < rank_k ? 1 : 0);
+  }
+}
+
+}  // namespace x2g
+
+namespace x2g {
 }  // namespace x2g
 
 using namespace x2g;
@@ -299,5 +381,44 @@ X2G_API int x2g_line_graph_transpose(const int32_t* trip_src, int64_t T, int64_t
     fill_by_key<<<blocks_for(T, 256), 256, 0, st>>>(trip_src, T, src_rowptr, cursor, src_perm);
     sort_segments<<<blocks_for(E, 256), 256, 0, st>>>(src_rowptr, E, src_perm);
   }
+  return last_launch_status();
+}
+
+X2G_API int x2g_vertex_to_edge_sym(const int32_t* edge_src, const int32_t* edge_dst, int64_t E, int64_t N, int64_t T,
+                                   int32_t* atom_rowptr, int32_t* trip_rowptr, int32_t* trip_src, int32_t* trip_dst,
+                                   int32_t* atom_j, int32_t* atom_i, int32_t* atom_k, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+  if (E < 0 || N < 0 || T < 0 || !atom_rowptr || !trip_rowptr) return X2G_EINVAL;
+  if (E > 0 && (!edge_src || !edge_dst)) return X2G_EINVAL;
+  if (T > 0 && (!trip_src || !trip_dst)) return X2G_EINVAL;
+  if (workspace_bytes < x2g_vertex_to_edge_workspace(E, N) || !workspace) return X2G_EWORKSPACE;
+  hipStream_t st = as_stream(stream);
+  int32_t* count = static_cast<int32_t*>(workspace);
+  const int64_t n = E > N ? E : N;
+  int32_t* partial = count + 2 * (n + 64);
+  int rc = x2g_csr_rowptr(edge_src, E, N, atom_rowptr, stream);
+  if (rc) return rc;
+  if ((rc = degree_scan(edge_dst, atom_rowptr, E, trip_rowptr, count, partial, st))) return rc;
+  if (E > 0) {
+    triplet_emit_kernel<<<blocks_for(E * kEmitGroup, 256), 256, 0, st>>>(
+        edge_src, edge_dst, atom_rowptr, trip_rowptr, E, T, trip_src, trip_dst, atom_j, atom_i, atom_k);
+  }
+  return last_launch_status();
+}
+
+X2G_API int x2g_line_graph_transpose_sym(const int32_t* edge_src, const int32_t* edge_dst, const int32_t* atom_rowptr,
+                                         const int32_t* trip_rowptr, int64_t E, int32_t* src_rowptr,
+                                         int32_t* src_perm, void* workspace, size_t workspace_bytes, void* stream) {
+  if (E < 0 || !src_rowptr || (E > 0 && (!edge_src || !edge_dst || !atom_rowptr || !trip_rowptr || !src_perm)))
+    return X2G_EINVAL;
+  if (workspace_bytes < x2g_vertex_to_edge_workspace(E, 0) || !workspace) return X2G_EWORKSPACE;
+  hipStream_t st = as_stream(stream);
+  int32_t* count = static_cast<int32_t*>(workspace);
+  int32_t* partial = count + 2 * (E + 64);
+  int rc;
+  if ((rc = degree_scan(edge_src, atom_rowptr, E, src_rowptr, count, partial, st))) return rc;
+  if (E > 0)
+    transpose_sym_kernel<<<blocks_for(E, 256), 256, 0, st>>>(edge_src, edge_dst, atom_rowptr, trip_rowptr, src_rowptr,
+                                                             E, src_perm);
   return last_launch_status();
 }

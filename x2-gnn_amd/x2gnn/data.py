@@ -148,6 +148,16 @@ def _add_device_indices(b, nodes, edges):
     b._store["_x2g_mol_ptr"] = torch.from_numpy(np.concatenate([[0], np.cumsum(nodes)]).astype(np.int32))
     b._store["_x2g_line_ptr"] = torch.from_numpy(np.concatenate([[0], np.cumsum(edges)]).astype(np.int32))
     b._store["_x2g_dst_type"] = torch.from_numpy(b._store["x"].numpy()[ei_np[1]].astype(np.int32))
+    b._store["_x2g_symmetric"] = _is_symmetric(ei_np, int(nodes.sum()))
+
+
+def _is_symmetric(ei, n):
+    """True when the directed edge set contains b->a for every a->b (checked exactly, host side)."""
+    if ei.shape[1] == 0:
+        return True
+    fwd = ei[0].astype(np.int64) * n + ei[1]
+    rev = ei[1].astype(np.int64) * n + ei[0]
+    return bool(np.array_equal(np.sort(fwd), np.sort(rev)))
 
 
 def molecule_to_data(mol: dict) -> Data:

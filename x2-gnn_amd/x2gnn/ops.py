@@ -52,7 +52,8 @@ class LineGraph:
     src_rowptr/src_perm: the same triplets grouped by source line node (built on first use).
     """
 
-    def __init__(self, edge_src, edge_dst, num_nodes, num_triplets):
+    def __init__(self, edge_src, edge_dst, num_nodes, num_triplets, symmetric=False):
+        self.symmetric = bool(symmetric)  # caller-asserted: b->a present for every a->b (x2g_*_sym)
         self.E = int(edge_src.shape[0])
         self.N = int(num_nodes)
         self.T = int(num_triplets)
@@ -70,9 +71,10 @@ class LineGraph:
         self._src_perm = None
         ws_bytes = int(_lib.load().x2g_vertex_to_edge_workspace(self.E, self.N))
         self._ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-        call("x2g_vertex_to_edge", ptr(edge_src), ptr(edge_dst), self.E, self.N, self.T, ptr(self.atom_rowptr),
-             ptr(self.trip_rowptr), ptr(self.trip_src), ptr(self.trip_dst), ptr(self.atom_j), ptr(self.atom_i),
-             ptr(self.atom_k), ptr(self._ws), ws_bytes, stream_ptr())
+        call("x2g_vertex_to_edge_sym" if self.symmetric else "x2g_vertex_to_edge", ptr(edge_src), ptr(edge_dst),
+             self.E, self.N, self.T, ptr(self.atom_rowptr), ptr(self.trip_rowptr), ptr(self.trip_src),
+             ptr(self.trip_dst), ptr(self.atom_j), ptr(self.atom_i), ptr(self.atom_k), ptr(self._ws), ws_bytes,
+             stream_ptr())
 
     @classmethod
     def from_triplets(cls, triplet_index, num_line_nodes: int):
@@ -85,6 +87,7 @@ class LineGraph:
         lg.trip_dst = _i32(triplet_index[1])
         lg.trip_rowptr = csr_rowptr(lg.trip_dst, lg.E)
         lg._src_rowptr = lg._src_perm = None
+        lg.symmetric = False
         ws_bytes = int(_lib.load().x2g_vertex_to_edge_workspace(lg.E, 0))
         lg._ws = torch.empty(ws_bytes, dtype=torch.uint8, device=lg.trip_src.device)
         return lg
@@ -94,8 +97,13 @@ class LineGraph:
             dev = self.trip_src.device
             self._src_rowptr = torch.empty(self.E + 1, dtype=torch.int32, device=dev)
             self._src_perm = torch.empty(self.T, dtype=torch.int32, device=dev)
-            call("x2g_line_graph_transpose", ptr(self.trip_src), self.T, self.E, ptr(self._src_rowptr),
-                 ptr(self._src_perm), ptr(self._ws), self._ws.numel(), stream_ptr())
+            if self.symmetric:  # lists written in order from the degrees (no atomics, no segment sort)
+                call("x2g_line_graph_transpose_sym", ptr(self.edge_src), ptr(self.edge_dst), ptr(self.atom_rowptr),
+                     ptr(self.trip_rowptr), self.E, ptr(self._src_rowptr), ptr(self._src_perm), ptr(self._ws),
+                     self._ws.numel(), stream_ptr())
+            else:
+                call("x2g_line_graph_transpose", ptr(self.trip_src), self.T, self.E, ptr(self._src_rowptr),
+                     ptr(self._src_perm), ptr(self._ws), self._ws.numel(), stream_ptr())
         return self._src_rowptr, self._src_perm
 
     def triplet_index(self):
@@ -103,11 +111,12 @@ class LineGraph:
         return torch.stack([self.trip_src.long(), self.trip_dst.long()])
 
 
-def vertex_to_edge(edge_index, num_nodes: int, num_triplets: int) -> LineGraph:
-    """Build the line graph of a (src, dst)-sorted directed edge list on the device."""
+def vertex_to_edge(edge_index, num_nodes: int, num_triplets: int, symmetric: bool = False) -> LineGraph:
+    """Build the line graph of a (src, dst)-sorted directed edge list on the device
+    (``symmetric``: the caller asserts b->a exists for every a->b)."""
     _need_cuda(edge_index)
     ei = _i32(edge_index)
-    return LineGraph(ei[0].contiguous(), ei[1].contiguous(), num_nodes, num_triplets)
+    return LineGraph(ei[0].contiguous(), ei[1].contiguous(), num_nodes, num_triplets, symmetric)
 
 
 def csr_rowptr(sorted_keys, num_segments: int):

@@ -51,7 +51,8 @@ class GraphPlan:
         dev = ei.device
         st = data._store
         if _HOST_INDICES and "_x2g_edge_src" in st and st["_x2g_edge_src"].device == dev:  # int32 forms (collate)
-            p.lg = ops.LineGraph(st["_x2g_edge_src"], st["_x2g_edge_dst"], p.num_atoms, p.num_triplets)
+            p.lg = ops.LineGraph(st["_x2g_edge_src"], st["_x2g_edge_dst"], p.num_atoms, p.num_triplets,
+                                 st.get("_x2g_symmetric", False))
             p.line_ptr, p.mol_ptr, p.dst_type = st["_x2g_line_ptr"], st["_x2g_mol_ptr"], st["_x2g_dst_type"]
         else:
             p.lg = ops.vertex_to_edge(ei, p.num_atoms, p.num_triplets)
