@@ -221,30 +221,32 @@ __global__ void sort_segments(const int32_t* __restrict__ rowptr, int64_t n_seg,
 // workgroup launch (per thread a contiguous run of edges: sum, block scan, write), and the
 // transposed lists are written directly in order instead of by atomics plus a segment sort.
 constexpr int kScan1Threads = 1024;
-constexpr int64_t kScan1Max = 262144;  // one workgroup up to this many edges (256 per thread)
+constexpr int64_t kScan1Max = 32768;  // one-workgroup scan up to this many counts (staged in LDS)
 
-// out[i] = sum_{j < i} (deg(atom[j]) - 1), out[n] = total, deg from atom_rowptr
-__global__ void __launch_bounds__(kScan1Threads) degree_scan_1wg(const int32_t* __restrict__ atom,
-                                                                const int32_t* __restrict__ atom_rowptr, int64_t n,
-                                                                int32_t* __restrict__ out) {
+// Exclusive scan of n <= kScan1Max int32 counts in ONE workgroup (coalesced loads into LDS, then
+// each thread scans a contiguous run): out[n] = total.  One launch instead of the three-phase
+// scan's three for the line graphs of a training batch.
+__global__ void __launch_bounds__(kScan1Threads) scan_1wg(const int32_t* __restrict__ in, int64_t n,
+                                                         int32_t* __restrict__ out) {
+  __shared__ int cnt[kScan1Max];
   __shared__ int lds[kScan1Threads / 64];
+  const int tid = threadIdx.x;
+  for (int64_t i = tid; i < n; i += kScan1Threads) cnt[i] = in[i];
+  __syncthreads();
   const int64_t per = (n + kScan1Threads - 1) / kScan1Threads;
-  const int64_t lo = per * threadIdx.x, hi = lo + per < n ? lo + per : n;
+  const int64_t lo = per * tid, hi = lo + per < n ? lo + per : n;
   int sum = 0;
-  for (int64_t i = lo; i < hi; ++i) {
-    const int a = atom[i];
-    const int c = atom_rowptr[a + 1] - atom_rowptr[a] - 1;
-    sum += c > 0 ? c : 0;
-  }
+  for (int64_t i = lo; i < hi; ++i) sum += cnt[i];
   int total;
   int run = block_exclusive_scan(sum, lds, &total);
   for (int64_t i = lo; i < hi; ++i) {
-    out[i] = run;
-    const int a = atom[i];
-    const int c = atom_rowptr[a + 1] - atom_rowptr[a] - 1;
-    run += c > 0 ? c : 0;
+    const int c = cnt[i];
+    cnt[i] = run;
+    run += c;
   }
-  if (threadIdx.x == 0) out[n] = total;
+  __syncthreads();
+  for (int64_t i = tid; i < n; i += kScan1Threads) out[i] = cnt[i];  // coalesced stores
+  if (tid == 0) out[n] = total;
 }
 
 // count[i] = deg(atom[i]) - 1 for the multi-workgroup scan of larger graphs
@@ -257,37 +259,60 @@ __global__ void degree_count(const int32_t* __restrict__ atom, const int32_t* __
   count[i] = c > 0 ? c : 0;
 }
 
+// out = exclusive scan of deg(atom[i]) - 1: the counts by a grid of threads (random gathers need
+// many CUs), the scan by one workgroup when it fits
 int degree_scan(const int32_t* atom, const int32_t* atom_rowptr, int64_t n, int32_t* out, int32_t* count,
                 int32_t* partial, hipStream_t st) {
-  if (n <= kScan1Max) {
-    degree_scan_1wg<<<1, kScan1Threads, 0, st>>>(atom, atom_rowptr, n, out);
+  if (n > 0) {
+    degree_count<<<blocks_for(n, 256), 256, 0, st>>>(atom, atom_rowptr, n, count);
+    if (int rc = last_launch_status()) return rc;
+  }
+  if (n > 0 && n <= kScan1Max) {
+    scan_1wg<<<1, kScan1Threads, 0, st>>>(count, n, out);
     return last_launch_status();
   }
-  degree_count<<<blocks_for(n, 256), 256, 0, st>>>(atom, atom_rowptr, n, count);
-  if (int rc = last_launch_status()) return rc;
   return exclusive_scan(count, n, out, partial, st);
 }
 
 // Source s = (b->k) lists its triplets (s -> e), e = (a->b) over b's neighbours a != k in
 // ascending a (= ascending edge id of e = ascending triplet id).  In e's destination list (b's
 // out-edges minus b->a, ascending) s sits at rank_b(k) - [rank_b(a) < rank_b(k)], so the triplet
-// id is trip_rowptr[e] plus that; e itself is found in a's sorted out-list.  One thread per source.
+// id is trip_rowptr[e] plus that; e itself is found in a's sorted out-list.  A group of 8 lanes per
+// source walks b's neighbours 8 at a time (one search each, in parallel) and compacts with a
+// ballot, as the triplet emitter does.
 __global__ void transpose_sym_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
                                      const int32_t* __restrict__ atom_rowptr, const int32_t* __restrict__ trip_rowptr,
                                      const int32_t* __restrict__ src_rowptr, int64_t E,
                                      int32_t* __restrict__ src_perm) {
-  const int64_t s = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (s >= E) return;
-  const int b = src[s], k = dst[s];
-  const int lo = atom_rowptr[b], hi = atom_rowptr[b + 1];
+  const int64_t gtid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t s = gtid / kEmitGroup;
+  const int sub = threadIdx.x & (kEmitGroup - 1);
+  const int lane = threadIdx.x & 63;
+  const uint64_t group_mask = ((1ull << kEmitGroup) - 1) << (lane & ~(kEmitGroup - 1));
+  const bool valid = s < E;
+  int b = 0, k = 0, lo = 0, hi = 0, p = 0;
+  if (valid) {
+    b = src[s];
+    k = dst[s];
+    lo = atom_rowptr[b];
+    hi = atom_rowptr[b + 1];
+    p = src_rowptr[s];
+  }
   const int rank_k = static_cast<int>(s) - lo;
-  int out = src_rowptr[s];
-  for (int idx = lo; idx < hi; ++idx) {
-    const int a = dst[idx];
-    if (a == k) continue;
-    const int alo = atom_rowptr[a], ahi = atom_rowptr[a + 1];
-    const int e = lower_bound(dst, alo, ahi, b);  // edge a->b (present: the graph is symmetric)
-    src_perm[out++] = trip_rowptr[e] + rank_k - (idx - lo < rank_k ? 1 : 0);
+  for (int base = lo; __any(valid && base < hi); base += kEmitGroup) {
+    const int idx = base + sub;
+    const bool in = valid && idx < hi;
+    const int a = in ? dst[idx] : 0;
+    const bool keep = in && a != k;
+    int tid_out = 0;
+    if (keep) {
+      const int e = lower_bound(dst, atom_rowptr[a], atom_rowptr[a + 1], b);  // edge a->b (symmetric graph)
+      tid_out = trip_rowptr[e] + rank_k - (idx - lo < rank_k ? 1 : 0);
+    }
+    const uint64_t ball = __ballot(keep) & group_mask;
+    const int q = p + __popcll(ball & ((1ull << lane) - 1));
+    if (keep) src_perm[q] = tid_out;
+    p += __popcll(ball);
   }
 }
 
@@ -418,7 +443,7 @@ X2G_API int x2g_line_graph_transpose_sym(const int32_t* edge_src, const int32_t*
   int rc;
   if ((rc = degree_scan(edge_src, atom_rowptr, E, src_rowptr, count, partial, st))) return rc;
   if (E > 0)
-    transpose_sym_kernel<<<blocks_for(E, 256), 256, 0, st>>>(edge_src, edge_dst, atom_rowptr, trip_rowptr, src_rowptr,
-                                                             E, src_perm);
+    transpose_sym_kernel<<<blocks_for(E * kEmitGroup, 256), 256, 0, st>>>(edge_src, edge_dst, atom_rowptr, trip_rowptr,
+                                                                          src_rowptr, E, src_perm);
   return last_launch_status();
 }
