@@ -265,6 +265,15 @@ size_t x2g_keyed_row_sum_workspace(int64_t rows, int32_t dim, int32_t num_keys);
 int x2g_keyed_row_sum(const float* src, const int32_t* key, int64_t rows, int32_t dim, int32_t num_keys,
                       float* out, int flags, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Several keyed row sums over the same keys (X2-GNN: every conv layer's per-destination edge
+ * gradient summed into the element table's rows) as one partial launch + one slab-sum launch:
+ * outs[j] (+)= keyed sum of srcs[j] (flags: X2G_ACCUM_WGRAD adds). */
+#define X2G_KEYED_MAX_JOBS 8
+size_t x2g_keyed_row_sum_batch_workspace(int64_t rows, int32_t dim, int32_t num_keys, int32_t num_jobs);
+int x2g_keyed_row_sum_batch(const float* const* srcs, float* const* outs, int32_t num_jobs, const int32_t* key,
+                            int64_t rows, int32_t dim, int32_t num_keys, int flags, void* workspace,
+                            size_t workspace_bytes, void* stream);
+
 /* PyG utils.softmax(src[R,H], index) for a sorted index (CSR rowptr): per segment and column,
  * exp(src - max) / (sum + 1e-16). */
 int x2g_segment_softmax_fwd(const float* src, const int32_t* rowptr, int64_t num_segments, int64_t heads,

@@ -382,6 +382,37 @@ def test_batched_readout_pools_match_per_readout(cuda, monkeypatch):
             assert float((g - ref).abs().max()) <= 1e-5 * float(ref.abs().max()) + 1e-6 * top, n
 
 
+def test_deferred_keyed_sums_match_immediate(cuda, monkeypatch):
+    """The conv layers' edge-table gradients (keyed row sums of d_edge by destination element)
+    deferred to the table chain's backward and run as one batched launch (the default) against
+    one keyed sum per layer: every parameter gradient within fp32 reassociation error, and the
+    deferred path actually taken (one batched call for the 4 layers)."""
+    import x2gnn
+    from x2gnn import ops
+    from x2gnn.data import collate
+    from x2gnn.synth import synthetic_molecules
+
+    cfg = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embedding_size=128)
+    batch = collate(synthetic_molecules(48, "S160", seed=13)).to(cuda)
+    calls = []
+    real = ops.flush_keyed
+    monkeypatch.setattr(ops, "flush_keyed", lambda: calls.append(len(ops._KEYED_PENDING)) or real())
+    runs = []
+    for deferred in (True, False):
+        monkeypatch.setattr(ops, "_DEFER_KEYED", deferred)
+        torch.manual_seed(0)
+        m = x2gnn.xgnn_poly(device="cuda", **cfg).to(cuda)
+        res = m(batch)
+        torch.nn.functional.smooth_l1_loss(res, batch.y).backward()
+        runs.append({n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None})
+    assert calls[0] == 4 and not ops._KEYED_PENDING
+    g1, g0 = runs
+    assert g1.keys() == g0.keys()
+    top = max(float(g.abs().max()) for g in g0.values())
+    for n, g in g1.items():
+        assert float((g - g0[n]).abs().max()) <= 1e-5 * float(g0[n].abs().max()) + 1e-6 * top, n
+
+
 def test_fan_in_gradients_match_autograd_adds(cuda):
     """ops.FanIn (layer inputs and the radial basis summed in place by the fused ops' backward,
     csrc: dx_add / X2G_GATE_DRBF_ACCUM / X2G_CHAIN_RES_ACCUM) gives the same parameter gradients as

@@ -489,10 +489,17 @@ constexpr int kKeyedSplits = 256;
 // block b sums rows [b * per, (b + 1) * per): row slot s (of 256 / LPR) adds its rows into its own
 // LDS accumulator set acc[s][key][:] (lanes own disjoint 16-byte column chunks: no races), then the
 // slots are folded in a fixed order into part[b][key][:]
+constexpr int kKeyedMaxJobs = X2G_KEYED_MAX_JOBS;
+struct KeyedJobs {  // job blockIdx.y: rows of src[j] summed by key into its slabs part[j]
+  const float4* src[kKeyedMaxJobs];
+  float4* part[kKeyedMaxJobs];
+};
+
 template <int LPR>
-__global__ void __launch_bounds__(256) keyed_row_sum_partial(const float4* __restrict__ src,
-                                                             const int32_t* __restrict__ key, int64_t rows, int nkeys,
-                                                             float4* __restrict__ part) {
+__global__ void __launch_bounds__(256) keyed_row_sum_partial(const KeyedJobs J, const int32_t* __restrict__ key,
+                                                             int64_t rows, int nkeys) {
+  const float4* __restrict__ src = J.src[blockIdx.y];
+  float4* __restrict__ part = J.part[blockIdx.y];
   constexpr int RPB = 256 / LPR;
   __shared__ float4 acc[RPB * kKeyedMaxKeys * LPR];
   const int sub = threadIdx.x % LPR, slot = threadIdx.x / LPR;
@@ -543,6 +550,22 @@ inline int keyed_splits(int64_t rows) {
 
 }  // namespace x2g
 
+static int keyed_partial_launch(const KeyedJobs& J, int n_jobs, const int32_t* key, int64_t rows, int dim, int nkeys,
+                                int splits, hipStream_t st) {
+  const dim3 grid(static_cast<unsigned>(splits), static_cast<unsigned>(n_jobs));
+  switch (dim / 4) {
+    case 1: keyed_row_sum_partial<1><<<grid, 256, 0, st>>>(J, key, rows, nkeys); break;
+    case 2: keyed_row_sum_partial<2><<<grid, 256, 0, st>>>(J, key, rows, nkeys); break;
+    case 4: keyed_row_sum_partial<4><<<grid, 256, 0, st>>>(J, key, rows, nkeys); break;
+    case 8: keyed_row_sum_partial<8><<<grid, 256, 0, st>>>(J, key, rows, nkeys); break;
+    case 16: keyed_row_sum_partial<16><<<grid, 256, 0, st>>>(J, key, rows, nkeys); break;
+    case 32: keyed_row_sum_partial<32><<<grid, 256, 0, st>>>(J, key, rows, nkeys); break;
+    case 64: keyed_row_sum_partial<64><<<grid, 256, 0, st>>>(J, key, rows, nkeys); break;
+    default: return X2G_EUNSUPPORTED;
+  }
+  return last_launch_status();
+}
+
 X2G_API size_t x2g_keyed_row_sum_workspace(int64_t rows, int32_t dim, int32_t nkeys) {
   if (rows <= 0 || dim <= 0 || nkeys <= 0) return 0;
   return static_cast<size_t>(keyed_splits(rows)) * dim * nkeys * sizeof(float);
@@ -563,21 +586,39 @@ X2G_API int x2g_keyed_row_sum(const float* src, const int32_t* key, int64_t rows
   if (reinterpret_cast<uintptr_t>(src) % 16) return X2G_EINVAL;
   if (!ws || wsb < x2g_keyed_row_sum_workspace(rows, dim, nkeys)) return X2G_EWORKSPACE;
   const int splits = keyed_splits(rows);
-  auto* part = static_cast<float4*>(ws);
-  const auto* sv = reinterpret_cast<const float4*>(src);
-  switch (dim / 4) {
-    case 1: keyed_row_sum_partial<1><<<splits, 256, 0, st>>>(sv, key, rows, nkeys, part); break;
-    case 2: keyed_row_sum_partial<2><<<splits, 256, 0, st>>>(sv, key, rows, nkeys, part); break;
-    case 4: keyed_row_sum_partial<4><<<splits, 256, 0, st>>>(sv, key, rows, nkeys, part); break;
-    case 8: keyed_row_sum_partial<8><<<splits, 256, 0, st>>>(sv, key, rows, nkeys, part); break;
-    case 16: keyed_row_sum_partial<16><<<splits, 256, 0, st>>>(sv, key, rows, nkeys, part); break;
-    case 32: keyed_row_sum_partial<32><<<splits, 256, 0, st>>>(sv, key, rows, nkeys, part); break;
-    case 64: keyed_row_sum_partial<64><<<splits, 256, 0, st>>>(sv, key, rows, nkeys, part); break;
-    default: return X2G_EUNSUPPORTED;
-  }
-  if (int rc = last_launch_status()) return rc;
+  KeyedJobs J{};
+  J.src[0] = reinterpret_cast<const float4*>(src);
+  J.part[0] = static_cast<float4*>(ws);
+  if (int rc = keyed_partial_launch(J, 1, key, rows, dim, nkeys, splits, st)) return rc;
   return sum_slabs_launch(static_cast<const float*>(ws), static_cast<int64_t>(dim) * nkeys, nullptr, 0, splits, out,
                           nullptr, accum, st);
+}
+
+X2G_API size_t x2g_keyed_row_sum_batch_workspace(int64_t rows, int32_t dim, int32_t nkeys, int32_t n_jobs) {
+  return n_jobs > 0 ? static_cast<size_t>(n_jobs) * x2g_keyed_row_sum_workspace(rows, dim, nkeys) : 0;
+}
+
+X2G_API int x2g_keyed_row_sum_batch(const float* const* srcs, float* const* outs, int32_t n_jobs, const int32_t* key,
+                                    int64_t rows, int32_t dim, int32_t nkeys, int flags, void* ws, size_t wsb,
+                                    void* stream) {
+  if (!srcs || !outs || n_jobs < 1 || n_jobs > kKeyedMaxJobs || rows <= 0 || dim <= 0 || nkeys <= 0 || !key)
+    return X2G_EINVAL;
+  if (nkeys > kKeyedMaxKeys || dim % 4 != 0 || dim > 256) return X2G_EUNSUPPORTED;
+  if (!ws || wsb < x2g_keyed_row_sum_batch_workspace(rows, dim, nkeys, n_jobs)) return X2G_EWORKSPACE;
+  hipStream_t st = as_stream(stream);
+  const int splits = keyed_splits(rows);
+  const int64_t per = static_cast<int64_t>(splits) * dim * nkeys;
+  KeyedJobs J{};
+  x2g_slab_job sj[kKeyedMaxJobs];
+  for (int j = 0; j < n_jobs; ++j) {
+    if (!srcs[j] || !outs[j] || reinterpret_cast<uintptr_t>(srcs[j]) % 16) return X2G_EINVAL;
+    J.src[j] = reinterpret_cast<const float4*>(srcs[j]);
+    float* part = static_cast<float*>(ws) + j * per;
+    J.part[j] = reinterpret_cast<float4*>(part);
+    sj[j] = x2g_slab_job{part, nullptr, outs[j], nullptr, static_cast<int64_t>(dim) * nkeys, 0, splits, 0, 0};
+  }
+  if (int rc = keyed_partial_launch(J, n_jobs, key, rows, dim, nkeys, splits, st)) return rc;
+  return x2g_slab_sum_batch(sj, n_jobs, (flags & X2G_ACCUM_WGRAD) ? 1 : 0, stream);
 }
 
 X2G_API int x2g_graph_layernorm_fwd(const float* x, const int32_t* rowptr, int64_t G, int64_t D, float eps,

@@ -50,6 +50,8 @@ SIGNATURES = {
     "x2g_rbf_gate_bwd_workspace": [_I64, _I32, _I32],
     "x2g_vertex_to_edge_sym": [_P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P],
     "x2g_line_graph_transpose_sym": [_P, _P, _P, _P, _I64, _P, _P, _P, _SZ, _P],
+    "x2g_keyed_row_sum_batch_workspace": [_I64, _I32, _I32, _I32],
+    "x2g_keyed_row_sum_batch": [_P, _P, _I32, _P, _I64, _I32, _I32, ctypes.c_int, _P, _SZ, _P],
     "x2g_rbf_pool_fwd_batch": [_P, _I32, _P, _P, _I64, _I32, _I32, _P],
     "x2g_rbf_gate_bwd_batch_workspace": [_I64, _I32, _I32, _I32],
     "x2g_rbf_gate_bwd_batch": [_P, _I32, _P, _P, _I64, _I32, _I32, _P, ctypes.c_int, _P, _P, _SZ, _P],
@@ -116,7 +118,7 @@ RESTYPES = {"x2g_status_string": ctypes.c_char_p, "x2g_vertex_to_edge_workspace"
             "x2g_linear_wgrad_workspace": _SZ, "x2g_dense_bwd_workspace": _SZ, "x2g_optimizer_workspace": _SZ,
             "x2g_linear_wgrad_splits": ctypes.c_int32, "x2g_dense_bwd_splits": ctypes.c_int32,
             "x2g_dense_bwd_slab_offset": ctypes.c_int64, "x2g_edge_basis_freq_grad_workspace": _SZ,
-            "x2g_edge_basis_freq_grad_splits": ctypes.c_int32, "x2g_rbf_gate_bwd_workspace": _SZ, "x2g_rbf_gate_bwd_batch_workspace": _SZ,
+            "x2g_edge_basis_freq_grad_splits": ctypes.c_int32, "x2g_rbf_gate_bwd_workspace": _SZ, "x2g_rbf_gate_bwd_batch_workspace": _SZ, "x2g_keyed_row_sum_batch_workspace": _SZ,
             "x2g_rbf_gate_bwd_splits": ctypes.c_int32, "x2g_keyed_row_sum_workspace": _SZ,
             "x2g_readout_head_bwd_workspace": _SZ, "x2g_readout_head_bwd_splits": ctypes.c_int32,
             "x2g_sbf_radial_wgrad_splits": ctypes.c_int32, "x2g_sbf_radial_wgrad_workspace": _SZ,

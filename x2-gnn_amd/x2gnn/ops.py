@@ -233,6 +233,8 @@ class _SBFAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row, heads, channels):
         w_param, b_param = w_sbf, b_sbf
+        # its gradient is read only by the table chain's backward, which flushes deferred sums first
+        ctx.defer_edge = _DEFER_KEYED and getattr(edge, "_x2g_table_out", False)
         factors = _sbf_factors(lg, sbf, edge_mode, heads * channels, edge, edge_row)
         q, k, v, skip = _f32(q), _f32(k), _f32(v), _f32(skip)
         sbf, w_sbf, b_sbf = _f32(sbf), _f32(w_sbf), _f32(b_sbf)
@@ -322,7 +324,10 @@ class _SBFAttention(torch.autograd.Function):
              ptr(ylm), ptr(src_rowptr), ptr(src_perm), ptr(lg.trip_dst), ptr(prob), ptr(g), ptr(rho), ptr(dout), E, T,
              heads, channels, ptr(dk), ptr(dv), ptr(gfold), st)
         if mode == EDGE_PER_DST and ctx.edge_row is not None:
-            d_edge = keyed_row_sum(d_edge, ctx.edge_row, ctx.edge_shape[0])
+            if ctx.defer_edge:
+                d_edge = keyed_row_sum_deferred(d_edge, ctx.edge_row, ctx.edge_shape[0])
+            else:
+                d_edge = keyed_row_sum(d_edge, ctx.edge_row, ctx.edge_shape[0])
         gw, gb = grad_sink(ctx.w_param), grad_sink(ctx.b_param)
         if gw is not None and gb is not None:
             dw, db = sbf_radial_wgrad(gfold, radial, dw_out=gw, db_out=gb)
@@ -576,6 +581,48 @@ def keyed_row_sum(src, key, num_keys: int):
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=src.device)
     call("x2g_keyed_row_sum", ptr(src), ptr(_i32(key)), R, D, num_keys, ptr(out), 0, ptr(ws), ws_bytes, stream_ptr())
     return out
+
+
+# Keyed row sums whose results are only read by the element-table chain's backward (every conv's
+# per-destination edge gradient -> its lin_edge table rows): queued here and run as ONE batched
+# launch (x2g_keyed_row_sum_batch) when _TableChainFn.backward starts, instead of a partial + a
+# slab-sum launch per layer.  X2G_DEFER_KEYED=0 sums each immediately.
+_DEFER_KEYED = os.environ.get("X2G_DEFER_KEYED", "1") == "1"
+_KEYED_PENDING = []
+KEYED_MAX_JOBS = 8  # X2G_KEYED_MAX_JOBS
+
+
+def keyed_row_sum_deferred(src, key, num_keys: int):
+    """keyed_row_sum(src, key, num_keys) into a buffer filled by the next flush_keyed()."""
+    src = _f32(src)
+    R, D = src.shape
+    if R == 0 or num_keys > 16 or D % 4 or D > 256 or (D // 4) & (D // 4 - 1):
+        return keyed_row_sum(src, key, num_keys)
+    out = torch.empty(num_keys, D, dtype=torch.float32, device=src.device)
+    _KEYED_PENDING.append((src, _i32(key), int(num_keys), out))
+    return out
+
+
+def flush_keyed():
+    """Run every queued keyed row sum (one partial + one slab-sum launch per group of jobs that
+    share keys and shape)."""
+    if not _KEYED_PENDING:
+        return
+    pending = list(_KEYED_PENDING)
+    _KEYED_PENDING.clear()
+    groups = {}
+    for src, key, nk, out in pending:
+        groups.setdefault((key.data_ptr(), tuple(src.shape), nk), []).append((src, key, nk, out))
+    lib = _lib.load()
+    for (_, (R, D), nk), items in groups.items():
+        for j0 in range(0, len(items), KEYED_MAX_JOBS):
+            part = items[j0:j0 + KEYED_MAX_JOBS]
+            n = len(part)
+            srcs = (ctypes.c_void_p * n)(*[it[0].data_ptr() for it in part])
+            outs = (ctypes.c_void_p * n)(*[it[3].data_ptr() for it in part])
+            wsb = int(lib.x2g_keyed_row_sum_batch_workspace(R, D, nk, n))
+            ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=part[0][0].device)
+            call("x2g_keyed_row_sum_batch", srcs, outs, n, ptr(part[0][1]), R, D, nk, 0, ptr(ws), wsb, stream_ptr())
 
 
 def sbf_attention(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg: LineGraph, heads: int, channels: int,
@@ -1125,6 +1172,7 @@ class _TableChainFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *gys):
+        flush_keyed()  # the conv layers' deferred edge-table gradients (keyed_row_sum_deferred)
         spec, n = ctx.spec, len(ctx.spec)
         saved = ctx.saved_tensors
         x2, ws, ys, zs = saved[0], saved[1:1 + n], saved[1 + n:1 + 2 * n], saved[1 + 2 * n:1 + 3 * n]
@@ -1159,7 +1207,10 @@ def table_chain(x, stages):
     for m, act, parent in stages:
         params += [m.weight, m.bias]
         spec.append((int(parent), int(act)))
-    return _TableChainFn.apply(x, tuple(spec), *params)
+    outs = _TableChainFn.apply(x, tuple(spec), *params)
+    for o in outs:
+        o._x2g_table_out = True  # consumers may defer work on its gradient to this chain's backward
+    return outs
 
 
 # --------------------------------------------------------------------------- line-node featurisation
