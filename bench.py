@@ -91,9 +91,11 @@ class Trainer:
         self.opt = FlatAdam(model.parameters(), lr=lr, max_norm=max_norm, ema_decay=ema_decay, bucket=self.bucket)
         self.graphs = None
         self.loss = None
+        self.grads_zeroed = False  # the bucket starts zeroed too; the first step zeroes it anyway
 
     def _fwd_bwd(self, batch):
-        self.bucket.zero()
+        if not self.grads_zeroed:  # otherwise the previous update zeroed them (FlatAdam.step(zero_grads=True))
+            self.bucket.zero()
         res = self.model(batch)
         loss = torch.nn.functional.smooth_l1_loss(res, batch.y)
         with ops.deferred_wgrad():  # all layers' weight-gradient slab sums in one launch
@@ -101,7 +103,8 @@ class Trainer:
         return loss
 
     def _update(self):
-        self.opt.step()
+        self.opt.step(zero_grads=True)
+        self.grads_zeroed = True
 
     def step(self, batch):
         if self.graphs is None:

@@ -493,6 +493,12 @@ size_t x2g_optimizer_workspace(int64_t n);
  * buffer is read, not modified.  Deterministic (fixed-order norm reduction). */
 int x2g_clip_adam_ema(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* ema,
                       int64_t n, float* scalars, void* workspace, size_t workspace_bytes, void* stream);
+/* x2g_clip_adam_ema with flags: X2G_OPT_ZERO_GRADS zeroes each gradient element once the update
+ * has read it (optimizer.zero_grad() folded into the step: the next backward may accumulate into
+ * the buffer without a separate fill). */
+#define X2G_OPT_ZERO_GRADS 1
+int x2g_clip_adam_ema_ex(float* params, float* grads, float* exp_avg, float* exp_avg_sq, float* ema, int64_t n,
+                         float* scalars, int flags, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- row chains (trunk tail)
  *

@@ -467,7 +467,8 @@ def test_dense_bwd_ex_dx_add_and_accumulate(cuda, R, K, N, act):
 def test_flat_adam_matches_torch(cuda, max_norm):
     """x2g_clip_adam_ema (FlatAdam) vs torch clip_grad_norm_ + Adam + the reference's EMA
     (torch.optim.swa_utils.AveragedModel with avg_fn = d*avg + (1-d)*p, train_ema.py:45-47: the
-    first update copies the parameters), three steps, clipping inactive (100) and active (0.05)."""
+    first update copies the parameters), three steps, clipping inactive (100) and active (0.05);
+    each update also zeroes the gradient bucket (the trainer's folded zero_grad())."""
     from torch.optim.swa_utils import AveragedModel
 
     from x2gnn.dist import GradBucket
@@ -492,10 +493,12 @@ def test_flat_adam_matches_torch(cuda, max_norm):
         torch.nn.utils.clip_grad_norm_(ref, max_norm)
         opt_ref.step()
         ema_model.update_parameters(holder)
-        bucket.zero()
+        if step == 0:
+            bucket.zero()
+        assert float(bucket.flat.abs().max()) == 0.0  # steps 1, 2: zeroed by the previous update
         for m, gr in zip(mine, grads):
             m.grad.copy_(gr)
-        opt.step()
+        opt.step(zero_grads=True)  # zero_grad() folded into the update (X2G_OPT_ZERO_GRADS)
         for r, m in zip(ref, mine):
             torch.testing.assert_close(m.detach(), r.detach(), rtol=2e-6, atol=2e-7)
         for e, m in zip(ema_ref, opt.ema_params()):

@@ -74,9 +74,10 @@ __global__ void __launch_bounds__(kNormThreads) opt_finalize(const float* __rest
   }
 }
 
-__global__ void __launch_bounds__(256) adam_ema(float* __restrict__ p, const float* __restrict__ g,
+__global__ void __launch_bounds__(256) adam_ema(float* __restrict__ p, float* __restrict__ g,
                                                 float* __restrict__ m, float* __restrict__ v,
-                                                float* __restrict__ ema, int64_t n, const float* __restrict__ sc) {
+                                                float* __restrict__ ema, int64_t n, const float* __restrict__ sc,
+                                                int zero_grads) {
   const float clip = sc[X2G_OPT_CLIP], b1 = sc[X2G_OPT_BETA1], b2 = sc[X2G_OPT_BETA2];
   const float eps = sc[X2G_OPT_EPS], step_size = sc[X2G_OPT_STEP_SIZE], bc2s = sc[X2G_OPT_BC2_SQRT];
   const float d = sc[X2G_OPT_EMA_DECAY];
@@ -86,6 +87,7 @@ __global__ void __launch_bounds__(256) adam_ema(float* __restrict__ p, const flo
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
     const float gi = g[i] * clip;
+    if (zero_grads) g[i] = 0.0f;  // zero_grad() folded into the step
     // exp_avg.lerp_(grad, 1 - beta1); exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1 - beta2)
     const float mi = m[i] + (1.0f - b1) * (gi - m[i]);
     const float vi = v[i] * b2 + (1.0f - b2) * gi * gi;
@@ -106,8 +108,8 @@ using namespace x2g;
 
 X2G_API size_t x2g_optimizer_workspace(int64_t n) { return n > 0 ? kNormBlocks * sizeof(float) : 0; }
 
-X2G_API int x2g_clip_adam_ema(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* ema,
-                              int64_t n, float* scalars, void* workspace, size_t workspace_bytes, void* stream) {
+static int clip_adam_ema(float* params, float* grads, float* exp_avg, float* exp_avg_sq, float* ema, int64_t n,
+                         float* scalars, int zero_grads, void* workspace, size_t workspace_bytes, void* stream) {
   if (n < 0 || !scalars) return X2G_EINVAL;
   if (n == 0) return X2G_OK;
   if (!params || !grads || !exp_avg || !exp_avg_sq) return X2G_EINVAL;
@@ -119,6 +121,19 @@ X2G_API int x2g_clip_adam_ema(float* params, const float* grads, float* exp_avg,
   opt_finalize<<<1, kNormThreads, 0, st>>>(partial, kNormBlocks, scalars);
   const int64_t want = (n + 255) / 256;
   adam_ema<<<static_cast<unsigned>(want < 4096 ? want : 4096), 256, 0, st>>>(params, grads, exp_avg, exp_avg_sq, ema,
-                                                                              n, scalars);
+                                                                              n, scalars, zero_grads);
   return last_launch_status();
+}
+
+X2G_API int x2g_clip_adam_ema(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* ema,
+                              int64_t n, float* scalars, void* workspace, size_t workspace_bytes, void* stream) {
+  return clip_adam_ema(params, const_cast<float*>(grads), exp_avg, exp_avg_sq, ema, n, scalars, 0, workspace,
+                       workspace_bytes, stream);
+}
+
+X2G_API int x2g_clip_adam_ema_ex(float* params, float* grads, float* exp_avg, float* exp_avg_sq, float* ema, int64_t n,
+                                 float* scalars, int flags, void* workspace, size_t workspace_bytes, void* stream) {
+  if (flags & ~X2G_OPT_ZERO_GRADS) return X2G_EINVAL;
+  return clip_adam_ema(params, grads, exp_avg, exp_avg_sq, ema, n, scalars, (flags & X2G_OPT_ZERO_GRADS) ? 1 : 0,
+                       workspace, workspace_bytes, stream);
 }

@@ -47,9 +47,12 @@ class FlatAdam:
         self.ws_bytes = int(_lib.load().x2g_optimizer_workspace(n))
         self.ws = torch.empty(max(self.ws_bytes, 4), dtype=torch.uint8, device=dev)
 
-    def step(self):
-        call("x2g_clip_adam_ema", ptr(self.flat), ptr(self.bucket.flat), ptr(self.exp_avg), ptr(self.exp_avg_sq),
-             ptr(self.ema), self.flat.numel(), ptr(self.scalars), ptr(self.ws), self.ws_bytes, stream_ptr())
+    def step(self, zero_grads=False):
+        """One update; ``zero_grads``: also zero the gradient bucket as it is read (zero_grad()
+        folded into the step's last kernel, so the next backward needs no fill)."""
+        call("x2g_clip_adam_ema_ex", ptr(self.flat), ptr(self.bucket.flat), ptr(self.exp_avg), ptr(self.exp_avg_sq),
+             ptr(self.ema), self.flat.numel(), ptr(self.scalars), 1 if zero_grads else 0, ptr(self.ws),
+             self.ws_bytes, stream_ptr())
 
     def set_lr(self, lr):
         self.scalars[_LR] = lr
