@@ -1191,6 +1191,7 @@ struct ChainWgradArgs {
 // lane-linearly, the swizzle applied to the source addresses), two steps in flight ahead of the
 // product; raw s_barrier with counted vmcnt waits so the in-flight copies survive the barriers.
 // One call reduces tiles [t0, t1) of one job into a slab (dW rows 16w + 4g + e, columns 16bk + rl).
+template <int NB>  // LDS buffers: NB - 1 steps in flight ahead of the product
 __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, const float* __restrict__ xin, int64_t t0,
                                               int64_t t1, bool has_b, float* __restrict__ slab,
                                               float* __restrict__ slab_b, f4 (*Ds)[kWTiles][512],
@@ -1201,8 +1202,8 @@ __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, cons
   // LDS position P = 64w + lane of a tile image holds source chunk (P >> 2) * 4 + ((P & 3) ^ sigma)
   const int P = 64 * w + lane;
   const int src_chunk = (P >> 2) * 4 + ((P & 3) ^ (((P >> 5) & 1) * 3));
-  auto issue = [&](int step) {  // the step's tiles into buffer step % 3 (tiles past t1: tile t0)
-    const int b = step % 3;
+  auto issue = [&](int step) {  // the step's tiles into buffer step % NB (tiles past t1: tile t0)
+    const int b = step % NB;
 #pragma unroll
     for (int k = 0; k < kWTiles; ++k) {
       int64_t t = t0 + static_cast<int64_t>(step) * kWTiles + k;
@@ -1215,18 +1216,22 @@ __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, cons
 #pragma unroll
   for (int bk = 0; bk < 8; ++bk) acc[bk] = zero4();
   float bsum = 0.f;
-  if (nsteps > 0) issue(0);
-  if (nsteps > 1) issue(1);
+#pragma unroll
+  for (int p = 0; p < NB - 1; ++p)
+    if (p < nsteps) issue(p);
   for (int i = 0; i < nsteps; ++i) {
-    // this step's copies are done when at most the next step's 2 * kWTiles remain in flight
-    if (i + 1 < nsteps)
+    // this step's copies are done when at most the later issued steps' 2 * kWTiles each remain
+    const int ahead = nsteps - 1 - i < NB - 2 ? nsteps - 1 - i : NB - 2;
+    if (ahead >= 2)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1)
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave's copies of this step have landed; step i-1 is read
-    if (i + 2 < nsteps) issue(i + 2);
-    const int b = i % 3;
+    if (i + NB - 1 < nsteps) issue(i + NB - 1);
+    const int b = i % NB;
 #pragma unroll
     for (int k = 0; k < kWTiles; ++k) {
       if (t0 + static_cast<int64_t>(i) * kWTiles + k >= t1) break;  // wave-uniform
@@ -1259,7 +1264,7 @@ __global__ void __launch_bounds__(kCThreads, 1) chain_wgrad_kernel(const ChainWg
   __shared__ f4 Xs[3][kWTiles][512];
   const int s = blockIdx.y, c = blockIdx.x;
   const int64_t t0 = c * a.ntiles / a.splits, t1 = (c + 1) * a.ntiles / a.splits;
-  tiled_segment(a.dz_t[s], a.in_t[s], t0, t1, a.has_b[s] != 0, a.part_w[s] + static_cast<int64_t>(c) * kCD * kCD,
+  tiled_segment<3>(a.dz_t[s], a.in_t[s], t0, t1, a.has_b[s] != 0, a.part_w[s] + static_cast<int64_t>(c) * kCD * kCD,
                 a.part_b[s] + static_cast<int64_t>(c) * kCD, Ds, Xs);
 }
 
@@ -1281,9 +1286,11 @@ struct TiledFlatArgs {
   int njobs;
 };
 
+// NB LDS buffers of 2 x 2 tiles (NB x 32 KB): 4 (the default, 128 KB) keeps three steps in flight
+template <int NB>
 __global__ void __launch_bounds__(kCThreads, 1) tiled_flat_kernel(const TiledFlatArgs a) {
-  __shared__ f4 Ds[3][kWTiles][512];
-  __shared__ f4 Xs[3][kWTiles][512];
+  __shared__ f4 Ds[NB][kWTiles][512];
+  __shared__ f4 Xs[NB][kWTiles][512];
   const int64_t G = gridDim.x, i = blockIdx.x;
   const int64_t lo = i * a.total / G, hi = (i + 1) * a.total / G;
   for (int64_t j = lo / a.ntiles; j < a.njobs && j * a.ntiles < hi; ++j) {
@@ -1292,7 +1299,7 @@ __global__ void __launch_bounds__(kCThreads, 1) tiled_flat_kernel(const TiledFla
     if (s0 >= s1) continue;
     __syncthreads();  // a previous segment's last buffers are no longer read
     const int64_t k = i - a.wg_lo[j];
-    tiled_segment(a.dz_t[j], a.in_t[j], s0 - j * a.ntiles, s1 - j * a.ntiles, a.has_b[j] != 0,
+    tiled_segment<NB>(a.dz_t[j], a.in_t[j], s0 - j * a.ntiles, s1 - j * a.ntiles, a.has_b[j] != 0,
                   a.slab_w[j] + k * kCD * kCD, a.slab_b[j] + k * kCD, Ds, Xs);
   }
 }
@@ -1805,7 +1812,10 @@ X2G_API int x2g_tiled_wgrad_flat(const x2g_tiled_job* jobs, int32_t num_jobs, in
     sj[j] = x2g_slab_job{a.slab_w[j], J.db ? a.slab_b[j] : nullptr, J.dw, J.db, kCD * kCD, J.db ? kCD : 0, n,
                          J.ld, J.cols};
   }
-  tiled_flat_kernel<<<static_cast<unsigned>(G), kCThreads, 0, as_stream(stream)>>>(a);
+  if (tuning(kTuneFlatBufs) == 1)
+    tiled_flat_kernel<3><<<static_cast<unsigned>(G), kCThreads, 0, as_stream(stream)>>>(a);
+  else
+    tiled_flat_kernel<4><<<static_cast<unsigned>(G), kCThreads, 0, as_stream(stream)>>>(a);
   const int rc = last_launch_status();
   if (rc) return rc;
   if (flags & X2G_DEFER_SLAB_SUM) {

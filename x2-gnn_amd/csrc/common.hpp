@@ -35,6 +35,7 @@ enum TuneKey {
   kTuneChain = 6,       // row chains: 0 = v4 forward / v3 backward, 1 = register-tile kernels, 2 = v2, 3 = v3 forward
   kTuneFeatDbg = 8,     // featurisation forward ablations for timing (1 no GEMM1, 2 no GEMM2, 4 no stores, 8 no staging)
   kTuneSprojDbg = 9,    // S projection (sbf_project_waves) ablations for timing (1 no MFMA, 2 no stores)
+  kTuneFlatBufs = 10,   // flat T-layout weight gradient: 1 = three LDS buffers (two steps in flight)
   kTuneCount = 16
 };
 int tuning(int key);
