@@ -1243,12 +1243,9 @@ __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, cons
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int bk = 0; bk < 8; ++bk) acc[bk] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[bk][e], acc[bk], 0, 0, 0);
-      if (tid < 128) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const f4 v = Ds[b][k][tpos(tid, q)];
-          bsum += (v[0] + v[1]) + (v[2] + v[3]);
-        }
+      if (has_b) {  // bias: thread (q, f) sums feature f's row quad q (every wave takes a share)
+        const f4 v = Ds[b][k][tpos(tid & (kCD - 1), tid >> 7)];
+        bsum += (v[0] + v[1]) + (v[2] + v[3]);
       }
     }
   }
@@ -1256,7 +1253,12 @@ __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, cons
   for (int bk = 0; bk < 8; ++bk)
 #pragma unroll
     for (int e = 0; e < 4; ++e) slab[(16 * w + 4 * g + e) * kCD + 16 * bk + rl] = acc[bk][e];
-  if (has_b && tid < 128) slab_b[tid] = bsum;
+  if (has_b) {  // the four row-quad partials of each feature, in quad order
+    __shared__ float bred[4 * kCD];
+    bred[tid] = bsum;
+    __syncthreads();
+    if (tid < kCD) slab_b[tid] = ((bred[tid] + bred[kCD + tid]) + bred[2 * kCD + tid]) + bred[3 * kCD + tid];
+  }
 }
 
 __global__ void __launch_bounds__(kCThreads, 1) chain_wgrad_kernel(const ChainWgradArgs a) {
