@@ -68,6 +68,11 @@ def parse():
                     help="qm9_u0: BASELINE config 2 (the metric); qm9_allprop: config 3 (one target's model, "
                          "B=256); aid_infer: config 5 (AID_kcal geometries, B=64, inference)")
     ap.add_argument("--target", type=int, default=0, help="qm9_allprop: QM9 target 0-11 (train_ema.py:41-44)")
+    ap.add_argument("--step-only", action="store_true",
+                    help="A/B runs: print only the timed-step line fields (no kernel probes, no CPU baseline)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N>1: nccl (= RCCL over xGMI, the measured path); gloo only rehearses the "
+                         "multi-rank step on a box with fewer GPUs than ranks")
     args = ap.parse_args()
     w = WORKLOADS[args.workload]
     if args.batch is None:
@@ -455,8 +460,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; ranks beyond the visible GPUs (a gloo rehearsal on a 1-GPU box) share them
+    local = local % max(1, torch.cuda.device_count())
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     torch.manual_seed(0)  # identical initial weights on every rank
@@ -501,6 +511,17 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     t_max = float(t.item())
     final_loss = float(loss.item())
+
+    if args.step_only:
+        if rank == 0:
+            print(json.dumps({"value": round(world * args.batch * args.steps / t_max, 2),
+                              "ms_per_step": round(1e3 * t_max / args.steps, 4), "steps": args.steps,
+                              "final_loss": round(final_loss, 6), "x2g_tune": os.environ.get("X2G_TUNE", "")}),
+                  flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     meta = batch.host_meta()
     probe, shape = attention_probe(model, batch, args.kernel_reps)
@@ -563,7 +584,9 @@ def main():
             "config": {"workload": work,
                        "per_gpu_batch": args.batch, "global_batch": world * args.batch,
                        "line_nodes_per_gpu": shape["E"], "triplets_per_gpu": shape["T"],
-                       "parallelism": f"dp{world}", "hip_graph": graphed},
+                       "parallelism": f"dp{world}", "hip_graph": graphed,
+                       "grad_allreduce": None if world == 1 else (
+                           "RCCL" if args.dist_backend == "nccl" else "gloo (rehearsal)")},
             "roofline": roof,
             "kernels": dict(
                 {k: {"ms": round(v[0], 5), "bytes": int(v[1]), "GBs": round(v[1] / (v[0] * 1e-3) / 1e9, 1)}

@@ -614,6 +614,18 @@ typedef struct {
 int x2g_conv_proj_bwd(const x2g_proj_grad* grads, int64_t rows, int32_t dim, float* dx, const float* dx_add,
                       float* dxs, void* stream);
 
+/* x2g_conv_proj_bwd with the gate's backward (x2g_rbf_gate_bwd on dxs) folded in, dxs kept in
+ * registers: dx = dq Wq + dskip Ws (+ dx_add) + dxs * f with f = rbf W_rbf^T; drbf (optional,
+ * [rows, rbf_dim]) = (dxs * x) W_rbf, added to its contents with X2G_GATE_DRBF_ACCUM; dw_rbf
+ * [dim, rbf_dim] (+)= (dxs * x)^T rbf from one slab per workgroup (flags X2G_ACCUM_WGRAD,
+ * X2G_DEFER_SLAB_SUM: x2g_conv_proj_bwd_gate_splits slabs of dim*rbf_dim floats at the workspace,
+ * no part_b).  Replaces sbftransformer_conv.py:99-100's backward (x_src = x * lin_rbf(rbf)). */
+int32_t x2g_conv_proj_bwd_gate_splits(int64_t rows);
+size_t x2g_conv_proj_bwd_gate_workspace(int64_t rows, int32_t rbf_dim);
+int x2g_conv_proj_bwd_gate(const x2g_proj_grad* grads, int64_t rows, int32_t dim, const float* x, const float* rbf,
+                           int32_t rbf_dim, const float* w_rbf, float* dx, const float* dx_add, float* drbf,
+                           float* dw_rbf, int flags, void* workspace, size_t workspace_bytes, void* stream);
+
 /* Weight / bias gradients of independent D x D Linear layers over the same rows from T-layout
  * operands: dw_j = dy_j^T x_j, db_j = colsum(dy_j) (db_j may be NULL); as x2g_chain_wgrad, with
  * each job's operands given separately (a T-layout tensor may serve several jobs). */

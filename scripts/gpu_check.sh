@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU validation/profiling run (used through gpurun): each step under its own time limit; stop
 # at the first step that ends in anything but pass/fail (fault, abort, timeout).
-#   bash scripts/gpu_check.sh [kernels] [model] [gpu] [smoke] [bench] [bench_c3] [bench_c3a] [bench_c5] [prof] [prof_c5] [pmc]
+#   bash scripts/gpu_check.sh [kernels] [model] [proj] [gpu] [ab: AB_VARIANTS='name=ENV ...'] [smoke] [bench] [dist2] [bench_c3] [bench_c3a] [bench_c5] [prof] [prof_c5] [pmc]
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 ROOT=$(pwd)
@@ -20,9 +20,13 @@ for s in "$@"; do
   case $s in
     kernels) step kernels 420 python -m pytest tests/test_gpu_kernels.py -q -m gpu -rf ;;
     model) step model 420 python -m pytest tests/test_gpu_model.py -q -m gpu -rf ;;
+    proj) step proj 300 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -rf -k "conv_proj or pool" --timeout 120 --timeout-method thread ;;
+    ab) step ab 900 python -u scripts/step_ab.py ${AB_ROUNDS:-3} $AB_VARIANTS ;;
     gpu) step gputests 600 python -u -m pytest tests -q -m gpu -rf --timeout 300 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 420 python bench.py --steps 20 --warmup 5 ;;
+    dist2) step dist2 420 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+            --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 3 --dist-backend gloo --no-cpu-baseline ;;
     bench_c3) step bench_c3 420 python bench.py --workload qm9_allprop --target 0 --steps 20 --warmup 5 ;;
     bench_c3a) step bench_c3a 420 python bench.py --workload qm9_allprop --target 7 --steps 20 --warmup 5 --no-cpu-baseline ;;
     bench_c5) step bench_c5 420 python bench.py --workload aid_infer --steps 10 --warmup 3 ;;

@@ -1,0 +1,35 @@
+"""Interleaved A/B of whole training steps: bench.py --step-only under each variant's environment,
+round-robin for several rounds on one box (box-to-box spread is ~1 %, so steps are compared only
+within one call).  Usage: python scripts/step_ab.py ROUNDS NAME=ENV[;ENV...] ...
+e.g.  python scripts/step_ab.py 3 base= nogate=X2G_PROJ_GATE=0 bufs3=X2G_TUNE=10=1"""
+import json
+import os
+import subprocess
+import sys
+
+rounds = int(sys.argv[1])
+variants = []
+for spec in sys.argv[2:]:
+    name, _, envs = spec.partition("=")
+    env = {}
+    for kv in filter(None, envs.split(";")):
+        k, _, v = kv.partition("=")
+        env[k] = v
+    variants.append((name, env))
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+res = {name: [] for name, _ in variants}
+for r in range(rounds):
+    for name, env in variants:
+        e = dict(os.environ, **env)
+        out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--step-only", "--steps", "60",
+                              "--warmup", "10"], env=e, capture_output=True, text=True, timeout=300)
+        line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+        if out.returncode != 0 or not line:
+            print(name, "FAILED", out.returncode, out.stderr[-2000:], flush=True)
+            sys.exit(1)
+        d = json.loads(line[-1])
+        res[name].append(d["value"])
+        print(f"round {r} {name:>10s} {d['value']:10.1f} mol/s  {d['ms_per_step']:.4f} ms  loss {d['final_loss']}",
+              flush=True)
+for name, v in res.items():
+    print(f"{name:>10s} median {sorted(v)[len(v) // 2]:10.1f}  all {v}")

@@ -1191,7 +1191,8 @@ struct ChainWgradArgs {
 // lane-linearly, the swizzle applied to the source addresses), two steps in flight ahead of the
 // product; raw s_barrier with counted vmcnt waits so the in-flight copies survive the barriers.
 // One call reduces tiles [t0, t1) of one job into a slab (dW rows 16w + 4g + e, columns 16bk + rl).
-template <int NB>  // LDS buffers: NB - 1 steps in flight ahead of the product
+template <int NB, bool SPREAD = true>  // NB LDS buffers: NB - 1 steps in flight ahead of the product;
+// SPREAD: the bias column sums over all eight waves (else waves 0-1 only, X2G_TUNE 12=1)
 __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, const float* __restrict__ xin, int64_t t0,
                                               int64_t t1, bool has_b, float* __restrict__ slab,
                                               float* __restrict__ slab_b, f4 (*Ds)[kWTiles][512],
@@ -1243,9 +1244,16 @@ __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, cons
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int bk = 0; bk < 8; ++bk) acc[bk] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[bk][e], acc[bk], 0, 0, 0);
-      if (has_b) {  // bias: thread (q, f) sums feature f's row quad q (every wave takes a share)
+      if (SPREAD && has_b) {  // bias: thread (q, f) sums feature f's row quad q (every wave takes a share)
         const f4 v = Ds[b][k][tpos(tid & (kCD - 1), tid >> 7)];
         bsum += (v[0] + v[1]) + (v[2] + v[3]);
+      }
+      if (!SPREAD && tid < 128) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f4 v = Ds[b][k][tpos(tid, q)];
+          bsum += (v[0] + v[1]) + (v[2] + v[3]);
+        }
       }
     }
   }
@@ -1253,7 +1261,8 @@ __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, cons
   for (int bk = 0; bk < 8; ++bk)
 #pragma unroll
     for (int e = 0; e < 4; ++e) slab[(16 * w + 4 * g + e) * kCD + 16 * bk + rl] = acc[bk][e];
-  if (has_b) {  // the four row-quad partials of each feature, in quad order
+  if (!SPREAD && has_b && tid < 128) slab_b[tid] = bsum;
+  if (SPREAD && has_b) {  // the four row-quad partials of each feature, in quad order
     __shared__ float bred[4 * kCD];
     bred[tid] = bsum;
     __syncthreads();
@@ -1289,7 +1298,7 @@ struct TiledFlatArgs {
 };
 
 // NB LDS buffers of 2 x 2 tiles (NB x 32 KB): 4 (the default, 128 KB) keeps three steps in flight
-template <int NB>
+template <int NB, bool SPREAD = true>
 __global__ void __launch_bounds__(kCThreads, 1) tiled_flat_kernel(const TiledFlatArgs a) {
   __shared__ f4 Ds[NB][kWTiles][512];
   __shared__ f4 Xs[NB][kWTiles][512];
@@ -1301,7 +1310,7 @@ __global__ void __launch_bounds__(kCThreads, 1) tiled_flat_kernel(const TiledFla
     if (s0 >= s1) continue;
     __syncthreads();  // a previous segment's last buffers are no longer read
     const int64_t k = i - a.wg_lo[j];
-    tiled_segment<NB>(a.dz_t[j], a.in_t[j], s0 - j * a.ntiles, s1 - j * a.ntiles, a.has_b[j] != 0,
+    tiled_segment<NB, SPREAD>(a.dz_t[j], a.in_t[j], s0 - j * a.ntiles, s1 - j * a.ntiles, a.has_b[j] != 0,
                   a.slab_w[j] + k * kCD * kCD, a.slab_b[j] + k * kCD, Ds, Xs);
   }
 }
@@ -1490,6 +1499,170 @@ __global__ void __launch_bounds__(kCThreads, 1) conv_proj_bwd_kernel(const ProjB
         }
       }
     }
+  }
+}
+
+// conv_proj_bwd_kernel with the rbf gate's backward folded into the dxs epilogue (what
+// x2g_rbf_gate_bwd did as a separate pass over dxs, x, rbf and dx): dxs never leaves registers.
+//   dx   = (dx_add + dxs * f) + (dq Wq + dskip Ws)       f = rbf W_rbf^T (the forward's filter)
+//   (dx_add is read only when given: an uninitialised dx never meets a 0 * NaN)
+//   drbf = (dxs * x) W_rbf   (+= with drbf_acc)          per row: lanes of a wave, then waves in order
+//   dW_rbf slab of this workgroup = sum over its rows of (dxs * x)^T rbf   (fixed-order slab sum after)
+// Register budget: the base kernel already holds 256 VGPRs, so nothing new lives across the second
+// half's products — dx_add + dxs * f goes to dx (re-read, L2-hot, by the second half's epilogue),
+// the dW_rbf partials are reduced over the row lanes per chunk into an LDS slab (one owner lane per
+// element), and drbf's per-wave partials meet in LDS.
+struct ProjBwdGateArgs {
+  x2g_proj_grad gr[4];
+  const float* dx_add;
+  float* dx;
+  const float* x;
+  const float* rbf;
+  const float* wr;
+  float* drbf;
+  float* part_w;
+  int RR;
+  int drbf_acc;
+  int64_t R;
+};
+
+template <int NJ>
+__global__ void __launch_bounds__(kCThreads, 1) conv_proj_bwd_gate_kernel(const ProjBwdGateArgs a) {
+  __shared__ f4 img[2][kV2Img];
+  __shared__ float srbf[kV2RB * 16 * NJ];
+  __shared__ float swr[kCD * NJ];
+  __shared__ float sdw[kCD * NJ];                   // this workgroup's dW_rbf (owner lanes only)
+  __shared__ float red[kCWaves * kV2RB * 16 * NJ];  // drbf partials: [wave][row][j]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rl = lane & 15, g = lane >> 4;
+  const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
+  const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
+  const int c0 = 16 * w + 4 * g;
+  for (int i = tid; i < kCD * NJ; i += kCThreads) {
+    const int c = i / NJ, j = i % NJ;
+    swr[i] = j < a.RR ? a.wr[c * a.RR + j] : 0.0f;
+  }
+  if (rl == 0) {
+#pragma unroll
+    for (int i = 0; i < 4 * NJ; ++i) sdw[c0 * NJ + i] = 0.0f;
+  }
+  auto load_ws = [&](int p, f4 (&dst)[8]) {
+    if (a.gr[p].wt)
+      load_slice<false>(a.gr[p].wt, w, rl, g, dst);
+    else
+      load_slice<true>(a.gr[p].w, w, rl, g, dst);
+  };
+  auto t_copy = [&](int p, const f4* im, int r0, int nrows) {
+    if (!a.gr[p].g_t) return;
+    f4 v[kV2RB];
+#pragma unroll
+    for (int rb = 0; rb < kV2RB; ++rb) v[rb] = im[ipos(16 * rb + rl, 4 * w + g)];
+    store_t_slice(a.gr[p].g_t, v, r0, nrows, w, rl, g);
+  };
+  const rsrc_t ar = rsrc(a.dx_add ? a.dx_add : a.dx);  // read only when dx_add is given (no 0 * NaN)
+  const rsrc_t dr = rsrc(a.dx);
+  for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
+    int r0, nrows;
+    chunk_rows(ch, nch, nblk, a.R, r0, nrows);
+    {  // (dk, dv) -> dxs -> the gate's three gradients
+      __syncthreads();  // images, srbf and red of the previous chunk are no longer read
+      stage_rows(img[0], a.gr[1].g, nullptr, r0, nrows);
+      stage_rows(img[1], a.gr[2].g, nullptr, r0, nrows);
+      stage_rbf<NJ>(srbf, a.rbf, a.RR, r0, nrows);
+      f4 A[8], An[8];
+      load_ws(1, A);
+      load_ws(2, An);
+      __syncthreads();
+      t_copy(1, img[0], r0, nrows);
+      t_copy(2, img[1], r0, nrows);
+      f4 acc[kV2RB], t[kV2RB];
+      slice_gemm(img[0], A, acc, rl, g);
+      slice_gemm(img[1], An, t, rl, g);
+      f4 xv[kV2RB];
+      load_rows_slice(a.x, r0, nrows, w, rl, g, xv);  // zero beyond nrows
+      float aw[4][NJ];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) aw[i][j] = 0.0f;
+#pragma unroll
+      for (int rb = 0; rb < kV2RB; ++rb) {
+        const int r = 16 * rb + rl;
+        const f4 dxs = acc[rb] + t[rb];
+        if (r < nrows) {
+          const int off = (r0 + r) * kCD + c0;
+          const f4 gx = dxs * gate_filter<NJ>(srbf, swr, r, c0);
+          *reinterpret_cast<f4*>(a.dx + off) = a.dx_add ? bload4(ar, 4 * off, 0) + gx : gx;
+        }
+        const f4 df = dxs * xv[rb];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) aw[i][j] = fmaf(df[i], srbf[r * NJ + j], aw[i][j]);
+        if (a.drbf) {
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            float p = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) p = fmaf(df[i], swr[(c0 + i) * NJ + j], p);
+            p += __shfl_xor(p, 16);
+            p += __shfl_xor(p, 32);
+            if (g == 0) red[(w * kV2RB * 16 + r) * NJ + j] = p;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          float v = aw[i][j];
+          v += __shfl_xor(v, 1);
+          v += __shfl_xor(v, 2);
+          v += __shfl_xor(v, 4);
+          v += __shfl_xor(v, 8);
+          if (rl == 0) sdw[(c0 + i) * NJ + j] += v;
+        }
+    }
+    {  // (dq, dskip) -> dx
+      __syncthreads();  // images no longer read; red complete
+      if (a.drbf) {
+        for (int i = tid; i < nrows * a.RR; i += kCThreads) {
+          const int r = i / a.RR, j = i % a.RR;
+          float s = 0.0f;
+#pragma unroll
+          for (int ww = 0; ww < kCWaves; ++ww) s += red[(ww * kV2RB * 16 + r) * NJ + j];
+          float* d = a.drbf + static_cast<int64_t>(r0 + r) * a.RR + j;
+          *d = a.drbf_acc ? *d + s : s;
+        }
+      }
+      stage_rows(img[0], a.gr[0].g, nullptr, r0, nrows);
+      stage_rows(img[1], a.gr[3].g, nullptr, r0, nrows);
+      f4 A[8], An[8];
+      load_ws(0, A);
+      load_ws(3, An);
+      __syncthreads();
+      t_copy(0, img[0], r0, nrows);
+      t_copy(3, img[1], r0, nrows);
+      f4 acc[kV2RB], t[kV2RB];
+      slice_gemm(img[0], A, acc, rl, g);
+      slice_gemm(img[1], An, t, rl, g);
+#pragma unroll
+      for (int rb = 0; rb < kV2RB; ++rb) {
+        const int r = 16 * rb + rl;
+        if (r < nrows) {
+          const int off = (r0 + r) * kCD + c0;
+          *reinterpret_cast<f4*>(a.dx + off) = bload4(dr, 4 * off, 0) + (acc[rb] + t[rb]);
+        }
+      }
+    }
+  }
+  if (rl == 0) {  // the owner lanes' sdw entries -> this workgroup's slab
+    float* slab = a.part_w + static_cast<int64_t>(blockIdx.x) * kCD * a.RR;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        if (j < a.RR) slab[(c0 + i) * a.RR + j] = sdw[(c0 + i) * NJ + j];
   }
 }
 
@@ -1750,6 +1923,58 @@ X2G_API int x2g_conv_proj_bwd(const x2g_proj_grad* grads, int64_t rows, int32_t 
   return last_launch_status();
 }
 
+X2G_API int32_t x2g_conv_proj_bwd_gate_splits(int64_t rows) { return rows > 0 ? static_cast<int32_t>(v2_grid(rows)) : 0; }
+
+X2G_API size_t x2g_conv_proj_bwd_gate_workspace(int64_t rows, int32_t rbf_dim) {
+  if (rows <= 0 || rbf_dim <= 0) return 0;
+  return static_cast<size_t>(v2_grid(rows)) * kCD * rbf_dim * sizeof(float);
+}
+
+X2G_API int x2g_conv_proj_bwd_gate(const x2g_proj_grad* grads, int64_t rows, int32_t dim, const float* x,
+                                   const float* rbf, int32_t rbf_dim, const float* w_rbf, float* dx,
+                                   const float* dx_add, float* drbf, float* dw_rbf, int flags, void* ws, size_t wsb,
+                                   void* stream) {
+  if (!grads || rows < 0 || dim <= 0 || rbf_dim <= 0 || !dw_rbf) return X2G_EINVAL;
+  if (flags & ~(X2G_ACCUM_WGRAD | X2G_DEFER_SLAB_SUM | X2G_GATE_DRBF_ACCUM)) return X2G_EINVAL;
+  if (dim != kCD || rbf_dim > kRbfMax || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  hipStream_t st = as_stream(stream);
+  if (rows == 0) {
+    if (flags & X2G_DEFER_SLAB_SUM) return X2G_EINVAL;
+    if (flags & X2G_ACCUM_WGRAD) return X2G_OK;
+    const hipError_t e = hipMemsetAsync(dw_rbf, 0, sizeof(float) * kCD * rbf_dim, st);
+    return e == hipSuccess ? X2G_OK : static_cast<int>(e);
+  }
+  if (!dx || !x || !rbf || !w_rbf) return X2G_EINVAL;
+  if (!ws || wsb < x2g_conv_proj_bwd_gate_workspace(rows, rbf_dim)) return X2G_EWORKSPACE;
+  ProjBwdGateArgs a{};
+  for (int p = 0; p < 4; ++p) {
+    if (!grads[p].g || !grads[p].w) return X2G_EINVAL;
+    if (!al16(grads[p].g) || !al16(grads[p].w) || !al16(grads[p].wt) || !al16(grads[p].g_t)) return X2G_EUNSUPPORTED;
+    a.gr[p] = grads[p];
+  }
+  if (!al16(dx) || !al16(dx_add) || !al16(x)) return X2G_EUNSUPPORTED;
+  a.dx_add = dx_add;
+  a.dx = dx;
+  a.x = x;
+  a.rbf = rbf;
+  a.wr = w_rbf;
+  a.drbf = drbf;
+  a.part_w = static_cast<float*>(ws);
+  a.RR = rbf_dim;
+  a.drbf_acc = (flags & X2G_GATE_DRBF_ACCUM) ? 1 : 0;
+  a.R = rows;
+  const unsigned grid = v2_grid(rows);
+  if (rbf_dim <= 6)
+    conv_proj_bwd_gate_kernel<6><<<grid, kCThreads, 0, st>>>(a);
+  else
+    conv_proj_bwd_gate_kernel<8><<<grid, kCThreads, 0, st>>>(a);
+  const int rc = last_launch_status();
+  if (rc || (flags & X2G_DEFER_SLAB_SUM)) return rc;
+  x2g_slab_job sj{a.part_w, nullptr, dw_rbf, nullptr, static_cast<int64_t>(kCD) * rbf_dim, 0,
+                  static_cast<int32_t>(grid), 0, 0};
+  return x2g_slab_sum_batch(&sj, 1, (flags & X2G_ACCUM_WGRAD) ? 1 : 0, stream);
+}
+
 // ---- one launch for many jobs (x2g_tiled_wgrad_flat)
 static inline unsigned flat_grid(int64_t total) {
   return static_cast<unsigned>(total < 256 ? (total < 1 ? 1 : total) : 256);  // one workgroup per CU (96 KB LDS)
@@ -1814,10 +2039,16 @@ X2G_API int x2g_tiled_wgrad_flat(const x2g_tiled_job* jobs, int32_t num_jobs, in
     sj[j] = x2g_slab_job{a.slab_w[j], J.db ? a.slab_b[j] : nullptr, J.dw, J.db, kCD * kCD, J.db ? kCD : 0, n,
                          J.ld, J.cols};
   }
-  if (tuning(kTuneFlatBufs) == 1)
-    tiled_flat_kernel<3><<<static_cast<unsigned>(G), kCThreads, 0, as_stream(stream)>>>(a);
+  const bool nb3 = tuning(kTuneFlatBufs) == 1, spread = tuning(kTuneFlatBias) == 0;
+  const unsigned grid = static_cast<unsigned>(G);
+  if (nb3 && spread)
+    tiled_flat_kernel<3, true><<<grid, kCThreads, 0, as_stream(stream)>>>(a);
+  else if (nb3)
+    tiled_flat_kernel<3, false><<<grid, kCThreads, 0, as_stream(stream)>>>(a);
+  else if (spread)
+    tiled_flat_kernel<4, true><<<grid, kCThreads, 0, as_stream(stream)>>>(a);
   else
-    tiled_flat_kernel<4><<<static_cast<unsigned>(G), kCThreads, 0, as_stream(stream)>>>(a);
+    tiled_flat_kernel<4, false><<<grid, kCThreads, 0, as_stream(stream)>>>(a);
   const int rc = last_launch_status();
   if (rc) return rc;
   if (flags & X2G_DEFER_SLAB_SUM) {

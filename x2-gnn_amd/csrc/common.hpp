@@ -36,6 +36,7 @@ enum TuneKey {
   kTuneFeatDbg = 8,     // featurisation forward ablations for timing (1 no GEMM1, 2 no GEMM2, 4 no stores, 8 no staging)
   kTuneSprojDbg = 9,    // S projection (sbf_project_waves) ablations for timing (1 no MFMA, 2 no stores)
   kTuneFlatBufs = 10,   // flat T-layout weight gradient: 1 = three LDS buffers (two steps in flight)
+  kTuneFlatBias = 12,   // flat T-layout weight gradient: 1 = bias column sums on waves 0-1 only
   kTuneCount = 16
 };
 int tuning(int key);

@@ -102,6 +102,9 @@ SIGNATURES = {
     "x2g_chain_wgrad": [_P, _P, _I32, _I64, _I32, _P, _P, ctypes.c_int, _P, _SZ, _P],
     "x2g_conv_proj_fwd": [_P, _P, _I32, _P, _P, _I64, _I32, _P, _P, _P],
     "x2g_conv_proj_bwd": [_P, _I64, _I32, _P, _P, _P, _P],
+    "x2g_conv_proj_bwd_gate_splits": [_I64],
+    "x2g_conv_proj_bwd_gate_workspace": [_I64, _I32],
+    "x2g_conv_proj_bwd_gate": [_P, _I64, _I32, _P, _P, _I32, _P, _P, _P, _P, _P, ctypes.c_int, _P, _SZ, _P],
     "x2g_tiled_wgrad_workspace": [_I64, _I32, _I32],
     "x2g_tiled_wgrad_splits": [_I64, _I32, _I32],
     "x2g_tiled_wgrad": [_P, _I32, _I64, _I32, ctypes.c_int, _P, _SZ, _P],
@@ -126,7 +129,8 @@ RESTYPES = {"x2g_status_string": ctypes.c_char_p, "x2g_vertex_to_edge_workspace"
             "x2g_wgrad_batched_workspace": _SZ, "x2g_wgrad_batched_splits": ctypes.c_int32,
             "x2g_chain_t_floats": ctypes.c_int64, "x2g_chain_wgrad_workspace": _SZ,
             "x2g_chain_wgrad_splits": ctypes.c_int32, "x2g_tiled_wgrad_workspace": _SZ, "x2g_tiled_wgrad_flat_workspace": _SZ,
-            "x2g_tiled_wgrad_splits": ctypes.c_int32}
+            "x2g_tiled_wgrad_splits": ctypes.c_int32, "x2g_conv_proj_bwd_gate_splits": ctypes.c_int32,
+            "x2g_conv_proj_bwd_gate_workspace": _SZ}
 
 _lib = None
 

@@ -74,5 +74,8 @@ class GradBucket:
                 dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
             return
         if multi:
-            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
-            self.flat.div_(dist.get_world_size(group))
+            if dist.get_backend(group) == "nccl":  # RCCL averages in the collective: no extra div kernel
+                dist.all_reduce(self.flat, op=dist.ReduceOp.AVG, group=group)
+            else:
+                dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+                self.flat.div_(dist.get_world_size(group))

@@ -1369,6 +1369,34 @@ def conv_proj_fused_supported(x, rbf, weights, biases):
     return all(b is None or b.data_ptr() % 16 == 0 for b in biases)
 
 
+_PROJ_GATE = os.environ.get("X2G_PROJ_GATE", "1") == "1"
+
+
+def _conv_proj_bwd_gate(grads, x2, rbf2, Wr, wr, dx, first_x, need_rbf, drbf_out, first_r):
+    """x2g_conv_proj_bwd_gate: dx (in place, += when not first_x), drbf, dW_rbf of the projections'
+    backward in one launch; returns (dx, drbf, dW_rbf) with None where the gradient went into a
+    caller's buffer (fan-in, gradient bucket)."""
+    E, D = x2.shape
+    RR = rbf2.shape[1]
+    dev = x2.device
+    drbf = drbf_out if drbf_out is not None else (
+        torch.empty(E, RR, dtype=torch.float32, device=dev) if need_rbf else None)
+    gw = grad_sink(wr)
+    accum = gw is not None
+    dw = gw if accum else torch.empty(D, RR, dtype=torch.float32, device=dev)
+    lib = _lib.load()
+    ws_bytes = int(lib.x2g_conv_proj_bwd_gate_workspace(E, RR))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    defer = accum and _DEFER is not None and E > 0
+    flags = ((ACCUM_WGRAD if accum else 0) | (DEFER_SLAB_SUM if defer else 0)
+             | (GATE_DRBF_ACCUM if (need_rbf and not first_r) else 0))
+    call("x2g_conv_proj_bwd_gate", grads, E, D, ptr(x2), ptr(rbf2), RR, ptr(Wr), ptr(dx),
+         None if first_x else ptr(dx), ptr(drbf), ptr(dw), flags, ptr(ws), ws_bytes, stream_ptr())
+    if defer:
+        _defer_job(ws, 0, int(lib.x2g_conv_proj_bwd_gate_splits(E)), D * RR, 0, dw, None)
+    return dx, drbf, (None if accum else dw)
+
+
 class _ConvProjFusedFn(torch.autograd.Function):
     """SBFTransformerConv's projections (sbftransformer_conv.py:99-107,127) in one kernel each way:
     x2g_conv_proj_fwd (x and x_src = x * lin_rbf(rbf) in LDS, q/k/v/skip per wave slice) and
@@ -1416,14 +1444,17 @@ class _ConvProjFusedFn(torch.autograd.Function):
             dx, first_x = ctx.fan_x.take((E, D), x2.device)
         else:
             dx = torch.empty(E, D, **f32)
-        dxs = torch.empty(E, D, **f32)
-        call("x2g_conv_proj_bwd", grads, E, D, ptr(dx), None if first_x else ptr(dx), ptr(dxs), stream_ptr())
         need_rbf = ctx.needs_input_grad[1]
         drbf_out = None
         if need_rbf and ctx.fan_r is not None:
             drbf_out, first_r = ctx.fan_r.take(rbf2.shape, x2.device)
-        gx, grbf, dwr, _ = _gate_bwd(dxs, None, x2, rbf2, Wr, None, wr, None, True, need_rbf, dx_add=dx, dx_out=dx,
-                                     drbf_out=drbf_out, drbf_acc=not first_r)
+        if _PROJ_GATE:  # the gate's backward inside the projection kernel: dxs stays in registers
+            gx, grbf, dwr = _conv_proj_bwd_gate(grads, x2, rbf2, Wr, wr, dx, first_x, need_rbf, drbf_out, first_r)
+        else:
+            dxs = torch.empty(E, D, **f32)
+            call("x2g_conv_proj_bwd", grads, E, D, ptr(dx), None if first_x else ptr(dx), ptr(dxs), stream_ptr())
+            gx, grbf, dwr, _ = _gate_bwd(dxs, None, x2, rbf2, Wr, None, wr, None, True, need_rbf, dx_add=dx,
+                                         dx_out=dx, drbf_out=drbf_out, drbf_acc=not first_r)
         gx = gx if first_x else None
         grbf = grbf if first_r else None
         dws, dbs = tiled_wgrad([g_t[0], g_t[1], g_t[2], g_t[3]], [x_t, xs_t, xs_t, x_t], E, [wq, wk, wv, ws],
