@@ -288,6 +288,12 @@ int x2g_graph_layernorm_fwd(const float* x, const int32_t* rowptr, int64_t num_s
                             float eps, float* out, float* mean, float* rstd, void* stream);
 int x2g_graph_layernorm_bwd(const float* out, const float* dout, const float* rstd, const int32_t* rowptr,
                             int64_t num_segments, int64_t dim, float* dx, void* stream);
+/* The same backward with a workspace (x2g_graph_layernorm_bwd_workspace bytes): several workgroups
+ * per segment, a stats pass and an apply pass (the segment's partial sums added in a fixed order). */
+size_t x2g_graph_layernorm_bwd_workspace(int64_t num_segments);
+int x2g_graph_layernorm_bwd_ex(const float* out, const float* dout, const float* rstd, const int32_t* rowptr,
+                               int64_t num_segments, int64_t dim, float* dx, void* workspace, size_t workspace_bytes,
+                               void* stream);
 
 /* ---------------------------------------------------------------- dense-layer gradients */
 
@@ -534,6 +540,19 @@ typedef struct {
 int x2g_chain_fwd(const float* x, const float* res_ext, const x2g_chain_stage* stages, int32_t n_stages,
                   int64_t rows, int32_t dim, float* in_t, void* stream);
 
+/* Several independent chains over the same row count and stage count in ONE launch (job =
+ * blockIdx.y; X2-GNN's readout MLPs, readout.py:25-31 / 55-62: Linear+SiLU, Linear+SiLU on the
+ * pooled atom rows of every readout).  Each job's fields mean what x2g_chain_fwd's / _bwd's do. */
+#define X2G_CHAIN_MAX_JOBS 8
+typedef struct {
+  const float* x;
+  const float* res_ext;
+  const x2g_chain_stage* stages; /* n_stages */
+  float* in_t;
+} x2g_chain_fwd_job;
+int x2g_chain_fwd_batch(const x2g_chain_fwd_job* jobs, int32_t num_jobs, int32_t n_stages, int64_t rows, int32_t dim,
+                        void* stream);
+
 /* Tiled-transposed ("T") layout of a [rows, D] tensor: 16-row tiles; tile t holds element (r, f)
  * at t*16*D + f*16 + (r - 16t), rows past `rows` in the last tile zero.  Floats per tensor: */
 int64_t x2g_chain_t_floats(int64_t rows, int32_t dim);
@@ -552,6 +571,18 @@ typedef struct {
  * Weight gradients: x2g_chain_wgrad over (in_t, dz_t), or x2g_wgrad_batched over row-major pairs. */
 int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_bwd_stage* stages, int32_t n_stages,
                   int64_t rows, int32_t dim, float* dx, float* d_res_ext, float* dz_t, void* stream);
+
+/* x2g_chain_bwd for several chains (x2g_chain_fwd_batch's jobs) in one launch. */
+typedef struct {
+  const float* dy;
+  const float* dy_add;
+  const x2g_chain_bwd_stage* stages; /* n_stages */
+  float* dx;
+  float* d_res_ext;
+  float* dz_t;
+} x2g_chain_bwd_job;
+int x2g_chain_bwd_batch(const x2g_chain_bwd_job* jobs, int32_t num_jobs, int32_t n_stages, int64_t rows, int32_t dim,
+                        void* stream);
 
 /* Weight / bias gradients of every chain stage: dw[s] = dz_s^T in_s, db[s] = colsum(dz_s) (db[s] may
  * be NULL) from the T-layout operands of x2g_chain_fwd / x2g_chain_bwd; dw / db are host arrays of

@@ -258,6 +258,33 @@ def test_graph_layernorm_vs_oracle(cuda):
     np.testing.assert_allclose(xg.grad.cpu().numpy(), x.grad.numpy(), rtol=1e-3, atol=1e-5)
 
 
+def test_graph_layernorm_bwd_split_equals_one_block(cuda):
+    """x2g_graph_layernorm_bwd_ex (4 workgroups per segment: stats pass + apply pass) against the
+    one-workgroup-per-segment x2g_graph_layernorm_bwd on ragged segments (empty, one row, QM9- and
+    AID-sized, one past the register-resident capacity); bitwise run to run."""
+    from x2gnn._lib import call, load, ptr, stream_ptr
+
+    counts = np.array([165, 0, 1, 3, 288, 2037, 257, 7])
+    rp = torch.from_numpy(np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)).to(cuda)
+    R, G = int(counts.sum()), len(counts)
+    g = torch.Generator(device=cuda).manual_seed(5)
+    y = torch.randn(R, 128, device=cuda, generator=g)
+    dy = torch.randn(R, 128, device=cuda, generator=g)
+    rstd = torch.rand(G, device=cuda, generator=g) + 0.5
+    ref = torch.empty_like(y)
+    call("x2g_graph_layernorm_bwd", ptr(y), ptr(dy), ptr(rstd), ptr(rp), G, 128, ptr(ref), stream_ptr())
+    wsb = int(load().x2g_graph_layernorm_bwd_workspace(G))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
+    outs = []
+    for _ in range(2):
+        dx = torch.full_like(y, float("nan"))
+        call("x2g_graph_layernorm_bwd_ex", ptr(y), ptr(dy), ptr(rstd), ptr(rp), G, 128, ptr(dx), ptr(ws), wsb,
+             stream_ptr())
+        outs.append(dx)
+    torch.testing.assert_close(outs[0], ref, rtol=1e-5, atol=1e-5)
+    assert torch.equal(outs[0], outs[1])
+
+
 # ------------------------------------------------------------------------------ attention
 def _product_conv(z, cuda):
     from weights import load_seeded

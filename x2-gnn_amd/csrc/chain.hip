@@ -797,7 +797,7 @@ __device__ __forceinline__ void fwd4_stage(const ChainFwdArgs& a, int s, const f
   for (int b = 0; b < 8; ++b) A[b] = An[b];
 }
 
-__global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4(const ChainFwdArgs a) {
+__device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a) {
   __shared__ f4 img0[kV2Img];
   __shared__ f4 img1[kV2Img];
   __shared__ f4 imgr[kV2Img];
@@ -829,6 +829,18 @@ __global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4(const ChainFwdArgs 
       if (s + 1 < n) fwd4_stage(a, s + 1, img1, img0, imgr, A, held, ch, wt_groups, r0, nrows, w, rl, g);
     }
   }
+}
+
+__global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4(const ChainFwdArgs a) { chain_fwd_v4_run(a); }
+
+// several independent chains over the same row count in one launch (job = blockIdx.y): the
+// readouts' MLPs, whose 2304 atom rows alone would fill a tenth of the chip
+constexpr int kChainMaxJobs = X2G_CHAIN_MAX_JOBS;
+struct ChainFwdBatch {
+  ChainFwdArgs a[kChainMaxJobs];
+};
+__global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4_batch(const ChainFwdBatch b) {
+  chain_fwd_v4_run(b.a[blockIdx.y]);
 }
 
 // Backward: img[p] holds dz_s (the product's B operand); the product's output slice is the
@@ -968,7 +980,7 @@ __device__ __forceinline__ void bwd_elem(f4 (&gs)[kV2RB], f4 (&dh)[kV2RB], const
   }
 }
 
-__global__ void __launch_bounds__(kCThreads, 1) chain_bwd_v3(const ChainBwdArgs a) {
+__device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
   __shared__ f4 img[2][kV2Img];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int rl = lane & 15, g = lane >> 4;
@@ -1071,6 +1083,14 @@ __global__ void __launch_bounds__(kCThreads, 1) chain_bwd_v3(const ChainBwdArgs 
     store_img(a.dx, img[p], r0, nrows);
   }
 }
+
+struct ChainBwdBatch {
+  ChainBwdArgs a[kChainMaxJobs];
+};
+__global__ void __launch_bounds__(kCThreads, 1) chain_bwd_v3_batch(const ChainBwdBatch b) {
+  chain_bwd_v3_run(b.a[blockIdx.y]);
+}
+
 
 // ------------------------------------------------------------------------- batched weight gradients
 // dW_j[n][k] = sum_r dy_j[r][n] x_j[r][k] for up to 8 layers: workgroup (chunk, j) owns a fixed
@@ -1686,11 +1706,13 @@ X2G_API int64_t x2g_chain_t_floats(int64_t rows, int32_t dim) {
   return rows > 0 && dim > 0 ? (rows + 15) / 16 * 16 * dim : 0;
 }
 
-X2G_API int x2g_chain_fwd(const float* x, const float* res_ext, const x2g_chain_stage* stages, int32_t n_stages,
-                          int64_t rows, int32_t dim, float* in_t, void* stream) {
+// validate one chain's forward and fill its kernel arguments; empty = no rows (nothing to launch)
+static int chain_fwd_prepare(const float* x, const float* res_ext, const x2g_chain_stage* stages, int32_t n_stages,
+                             int64_t rows, int32_t dim, float* in_t, ChainFwdArgs& a, bool& empty) {
+  empty = false;
   if (!stages || n_stages < 1 || n_stages > X2G_CHAIN_MAX_STAGES || rows < 0 || dim <= 0) return X2G_EINVAL;
   if (dim != kCD || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
-  ChainFwdArgs a{};
+  a = ChainFwdArgs{};
   a.x = x;
   a.res = res_ext;
   a.in_t = in_t;
@@ -1714,9 +1736,21 @@ X2G_API int x2g_chain_fwd(const float* x, const float* res_ext, const x2g_chain_
     a.st[s] = S;
   }
   if (n_ext > 1 || (n_ext && !res_ext)) return X2G_EINVAL;
-  if (rows == 0) return X2G_OK;
+  if (rows == 0) {
+    empty = true;
+    return X2G_OK;
+  }
   if (!x) return X2G_EINVAL;
   if (!al16(x) || !al16(res_ext) || !al16(in_t)) return X2G_EUNSUPPORTED;
+  return X2G_OK;
+}
+
+X2G_API int x2g_chain_fwd(const float* x, const float* res_ext, const x2g_chain_stage* stages, int32_t n_stages,
+                          int64_t rows, int32_t dim, float* in_t, void* stream) {
+  ChainFwdArgs a{};
+  bool empty;
+  if (int rc = chain_fwd_prepare(x, res_ext, stages, n_stages, rows, dim, in_t, a, empty)) return rc;
+  if (empty) return X2G_OK;
   hipStream_t st = as_stream(stream);
   if (tuning(kTuneChain) == 1 && !in_t) {  // register-tile kernel (no T-layout output)
     const int64_t groups = ((rows + 15) / 16 + kCWaves - 1) / kCWaves;
@@ -1734,11 +1768,14 @@ X2G_API int x2g_chain_fwd(const float* x, const float* res_ext, const x2g_chain_
   return last_launch_status();
 }
 
-X2G_API int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_bwd_stage* stages, int32_t n_stages,
-                          int64_t rows, int32_t dim, float* dx, float* d_res_ext, float* dz_t, void* stream) {
+static int chain_bwd_prepare(const float* dy, const float* dy_add, const x2g_chain_bwd_stage* stages, int32_t n_stages,
+                             int64_t rows, int32_t dim, float* dx, float* d_res_ext, float* dz_t, ChainBwdArgs& a,
+                             bool& empty, bool& res_accum) {
+  empty = false;
+  res_accum = false;
   if (!stages || n_stages < 1 || n_stages > X2G_CHAIN_MAX_STAGES || rows < 0 || dim <= 0) return X2G_EINVAL;
   if (dim != kCD || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
-  ChainBwdArgs a{};
+  a = ChainBwdArgs{};
   a.dy = dy;
   a.dy_add = dy_add;
   a.dx = dx;
@@ -1748,7 +1785,6 @@ X2G_API int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_
   a.R = rows;
   a.n = n_stages;
   int n_ext = 0, held = 0;
-  bool res_accum = false;
   for (int s = 0; s < n_stages; ++s) {
     const x2g_chain_bwd_stage& S = stages[s];
     if (!S.w || ((S.flags & X2G_CHAIN_SILU) && !S.z)) return X2G_EINVAL;
@@ -1765,9 +1801,22 @@ X2G_API int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_
     a.st[s] = S;
   }
   if (n_ext > 1) return X2G_EINVAL;
-  if (rows == 0) return X2G_OK;
+  if (rows == 0) {
+    empty = true;
+    return X2G_OK;
+  }
   if (!dy || !dx) return X2G_EINVAL;
   if (!al16(dy) || !al16(dy_add) || !al16(dx) || !al16(d_res_ext) || !al16(dz_t)) return X2G_EUNSUPPORTED;
+  return X2G_OK;
+}
+
+X2G_API int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_bwd_stage* stages, int32_t n_stages,
+                          int64_t rows, int32_t dim, float* dx, float* d_res_ext, float* dz_t, void* stream) {
+  ChainBwdArgs a{};
+  bool empty, res_accum;
+  if (int rc = chain_bwd_prepare(dy, dy_add, stages, n_stages, rows, dim, dx, d_res_ext, dz_t, a, empty, res_accum))
+    return rc;
+  if (empty) return X2G_OK;
   hipStream_t st = as_stream(stream);
   if (tuning(kTuneChain) == 1 && !dz_t) {
     if (res_accum) return X2G_EUNSUPPORTED;  // the register-tile kernel overwrites d_res_ext
@@ -1776,10 +1825,52 @@ X2G_API int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_
   } else if (tuning(kTuneChain) == 2) {
     const int64_t nblk = (rows + 15) / 16;
     chain_bwd_v2<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, st>>>(a);
-  } else {  // v3 (default)
+  } else {  // v3 (default), through the batched kernel: a by-value ChainBwdArgs handed to the shared
+            // body by reference is copied to scratch (392 B, 79 -> 121 us); a batch entry is not
     const int64_t nblk = (rows + 15) / 16;
-    chain_bwd_v3<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, st>>>(a);
+    ChainBwdBatch b{};
+    b.a[0] = a;
+    chain_bwd_v3_batch<<<dim3(static_cast<unsigned>(nblk < 256 ? nblk : 256), 1), kCThreads, 0, st>>>(b);
   }
+  return last_launch_status();
+}
+
+// grid of a batched chain launch: about one workgroup per CU over all jobs, each job's row blocks
+// split evenly over its share (the kernels' chunking follows gridDim.x)
+static inline unsigned chain_batch_grid(int64_t rows, int n_jobs) {
+  const int64_t nblk = (rows + 15) / 16, per = 256 / n_jobs;
+  return static_cast<unsigned>(nblk < per ? nblk : (per < 1 ? 1 : per));
+}
+
+X2G_API int x2g_chain_fwd_batch(const x2g_chain_fwd_job* jobs, int32_t n_jobs, int32_t n_stages, int64_t rows,
+                                int32_t dim, void* stream) {
+  if (!jobs || n_jobs < 1 || n_jobs > kChainMaxJobs) return X2G_EINVAL;
+  ChainFwdBatch b{};
+  bool empty = false;
+  for (int j = 0; j < n_jobs; ++j) {
+    const x2g_chain_fwd_job& J = jobs[j];
+    if (int rc = chain_fwd_prepare(J.x, J.res_ext, J.stages, n_stages, rows, dim, J.in_t, b.a[j], empty)) return rc;
+  }
+  if (empty) return X2G_OK;
+  const dim3 grid(chain_batch_grid(rows, n_jobs), static_cast<unsigned>(n_jobs));
+  chain_fwd_v4_batch<<<grid, kCThreads, 0, as_stream(stream)>>>(b);
+  return last_launch_status();
+}
+
+X2G_API int x2g_chain_bwd_batch(const x2g_chain_bwd_job* jobs, int32_t n_jobs, int32_t n_stages, int64_t rows,
+                                int32_t dim, void* stream) {
+  if (!jobs || n_jobs < 1 || n_jobs > kChainMaxJobs) return X2G_EINVAL;
+  ChainBwdBatch b{};
+  bool empty = false, res_accum;
+  for (int j = 0; j < n_jobs; ++j) {
+    const x2g_chain_bwd_job& J = jobs[j];
+    if (int rc = chain_bwd_prepare(J.dy, J.dy_add, J.stages, n_stages, rows, dim, J.dx, J.d_res_ext, J.dz_t, b.a[j],
+                                   empty, res_accum))
+      return rc;
+  }
+  if (empty) return X2G_OK;
+  const dim3 grid(chain_batch_grid(rows, n_jobs), static_cast<unsigned>(n_jobs));
+  chain_bwd_v3_batch<<<grid, kCThreads, 0, as_stream(stream)>>>(b);
   return last_launch_status();
 }
 

@@ -37,6 +37,7 @@ enum TuneKey {
   kTuneSprojDbg = 9,    // S projection (sbf_project_waves) ablations for timing (1 no MFMA, 2 no stores)
   kTuneFlatBufs = 10,   // flat T-layout weight gradient: 1 = three LDS buffers (two steps in flight)
   kTuneFlatBias = 12,   // flat T-layout weight gradient: 1 = bias column sums on waves 0-1 only
+  kTuneLnBwd = 13,      // graph LayerNorm backward: 1 = one block per molecule (no split)
   kTuneCount = 16
 };
 int tuning(int key);

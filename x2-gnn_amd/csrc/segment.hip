@@ -444,6 +444,108 @@ __global__ void __launch_bounds__(kLnBig) graph_ln_bwd_reg(const float4* __restr
   }
 }
 
+// Split backward (the default with a workspace): the one-block-per-molecule form runs 128 blocks
+// at config 2 — half the CUs idle and each block's loads, two block reductions and stores in
+// series (~23 us for 32 MB).  Here kLnSplit blocks share a molecule: a stats pass writes each
+// block's (sum dy, sum dy*y) over its row range, an apply pass re-reads its range (MALL-hot) and
+// sums the molecule's kLnSplit partials in block order (fixed order: deterministic).
+constexpr int kLnSplit = 4;
+constexpr int kLnSplitThreads = 256;
+constexpr int kLnSplitUnroll = 4;
+
+__device__ __forceinline__ void ln_split_range(const int32_t* __restrict__ rowptr, int64_t D4, int64_t& g, int64_t& lo,
+                                               int64_t& hi, int64_t& n) {
+  g = blockIdx.x / kLnSplit;
+  const int64_t s = blockIdx.x % kLnSplit;
+  const int64_t r0 = rowptr[g], r1 = rowptr[g + 1];
+  n = r1 - r0;
+  lo = (r0 + n * s / kLnSplit) * D4;
+  hi = (r0 + n * (s + 1) / kLnSplit) * D4;
+}
+
+__global__ void __launch_bounds__(kLnSplitThreads) graph_ln_bwd_stats(const float4* __restrict__ y,
+                                                                      const float4* __restrict__ dy,
+                                                                      const int32_t* __restrict__ rowptr, int64_t D4,
+                                                                      float2* __restrict__ part) {
+  __shared__ float2 lds[kLnSplitThreads / 64];
+  int64_t g, lo, hi, n;
+  ln_split_range(rowptr, D4, g, lo, hi, n);
+  float s1 = 0.f, s2 = 0.f;
+  for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += kLnSplitThreads * kLnSplitUnroll) {
+    float4 gv[kLnSplitUnroll], yv[kLnSplitUnroll];
+#pragma unroll
+    for (int u = 0; u < kLnSplitUnroll; ++u) {  // every load of the batch first (clamped, masked)
+      const int64_t i = i0 + u * kLnSplitThreads;
+      const int64_t ic = i < hi ? i : lo;
+      gv[u] = dy[ic];
+      yv[u] = y[ic];
+    }
+#pragma unroll
+    for (int u = 0; u < kLnSplitUnroll; ++u) {
+      if (i0 + u * kLnSplitThreads < hi) {
+        s1 += (gv[u].x + gv[u].y) + (gv[u].z + gv[u].w);
+        s2 = fmaf(gv[u].x, yv[u].x, s2);
+        s2 = fmaf(gv[u].y, yv[u].y, s2);
+        s2 = fmaf(gv[u].z, yv[u].z, s2);
+        s2 = fmaf(gv[u].w, yv[u].w, s2);
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s1 += __shfl_xor(s1, off, 64);
+    s2 += __shfl_xor(s2, off, 64);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) lds[wave] = make_float2(s1, s2);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float2 t = lds[0];
+#pragma unroll
+    for (int w = 1; w < kLnSplitThreads / 64; ++w) {
+      t.x += lds[w].x;
+      t.y += lds[w].y;
+    }
+    part[blockIdx.x] = t;
+  }
+}
+
+__global__ void __launch_bounds__(kLnSplitThreads) graph_ln_bwd_apply(const float4* __restrict__ y,
+                                                                      const float4* __restrict__ dy,
+                                                                      const float* __restrict__ rstd,
+                                                                      const int32_t* __restrict__ rowptr, int64_t D4,
+                                                                      const float2* __restrict__ part,
+                                                                      float4* __restrict__ dx) {
+  int64_t g, lo, hi, n;
+  ln_split_range(rowptr, D4, g, lo, hi, n);
+  if (n == 0) return;
+  const float norm = static_cast<float>(n * D4 * 4);
+  float2 t = part[g * kLnSplit];
+#pragma unroll
+  for (int s = 1; s < kLnSplit; ++s) {
+    t.x += part[g * kLnSplit + s].x;
+    t.y += part[g * kLnSplit + s].y;
+  }
+  const float m1 = t.x / norm, m2 = t.y / norm, r = rstd[g];
+  for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += kLnSplitThreads * kLnSplitUnroll) {
+    float4 gv[kLnSplitUnroll], yv[kLnSplitUnroll];
+#pragma unroll
+    for (int u = 0; u < kLnSplitUnroll; ++u) {
+      const int64_t i = i0 + u * kLnSplitThreads;
+      const int64_t ic = i < hi ? i : lo;
+      gv[u] = dy[ic];
+      yv[u] = y[ic];
+    }
+#pragma unroll
+    for (int u = 0; u < kLnSplitUnroll; ++u) {
+      const int64_t i = i0 + u * kLnSplitThreads;
+      if (i < hi)
+        dx[i] = make_float4(r * (gv[u].x - m1 - yv[u].x * m2), r * (gv[u].y - m1 - yv[u].y * m2),
+                            r * (gv[u].z - m1 - yv[u].z * m2), r * (gv[u].w - m1 - yv[u].w * m2));
+    }
+  }
+}
+
 }  // namespace x2g
 
 using namespace x2g;
@@ -646,5 +748,28 @@ X2G_API int x2g_graph_layernorm_bwd(const float* out, const float* dout, const f
   else
     graph_ln_bwd_kernel<<<static_cast<unsigned>(G), kLnThreads, 0, as_stream(stream)>>>(out, dout, rstd, rowptr, D,
                                                                                        dx);
+  return last_launch_status();
+}
+
+X2G_API size_t x2g_graph_layernorm_bwd_workspace(int64_t G) {
+  return G > 0 ? static_cast<size_t>(G) * kLnSplit * sizeof(float2) : 0;
+}
+
+X2G_API int x2g_graph_layernorm_bwd_ex(const float* out, const float* dout, const float* rstd, const int32_t* rowptr,
+                                       int64_t G, int64_t D, float* dx, void* ws, size_t wsb, void* stream) {
+  if (G < 0 || D <= 0 || (G > 0 && (!out || !dout || !rstd || !rowptr || !dx))) return X2G_EINVAL;
+  if (G == 0) return X2G_OK;
+  const bool vec = D % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(dout) % 16 == 0 && reinterpret_cast<uintptr_t>(dx) % 16 == 0;
+  if (!vec || !ws || wsb < x2g_graph_layernorm_bwd_workspace(G) || tuning(kTuneLnBwd) == 1)
+    return x2g_graph_layernorm_bwd(out, dout, rstd, rowptr, G, D, dx, stream);
+  hipStream_t st = as_stream(stream);
+  const unsigned grid = static_cast<unsigned>(G * kLnSplit);
+  auto* part = static_cast<float2*>(ws);
+  graph_ln_bwd_stats<<<grid, kLnSplitThreads, 0, st>>>(reinterpret_cast<const float4*>(out),
+                                                       reinterpret_cast<const float4*>(dout), rowptr, D / 4, part);
+  graph_ln_bwd_apply<<<grid, kLnSplitThreads, 0, st>>>(reinterpret_cast<const float4*>(out),
+                                                       reinterpret_cast<const float4*>(dout), rstd, rowptr, D / 4, part,
+                                                       reinterpret_cast<float4*>(dx));
   return last_launch_status();
 }

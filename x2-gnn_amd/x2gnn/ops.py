@@ -455,11 +455,35 @@ class _ReadoutMLPs(torch.autograd.Function):
         dev = feats[0].device
         f32 = dict(dtype=torch.float32, device=dev)
         xs = [_f32(f) for f in feats]
-        h1 = [torch.empty(R, D, **f32) for _ in range(G)]
         z1 = [torch.empty(R, D, **f32) for _ in range(G)]
         h2 = [torch.empty(R, D, **f32) for _ in range(G)]
         z2 = [torch.empty(R, D, **f32) for _ in range(G)]
         st = stream_ptr()
+        ctx.chain = _READOUT_CHAIN and _readout_chain_ok(R, D, G, W1, B1, W2, B2)
+        if ctx.chain:  # both hidden layers of every readout: one x2g_chain_fwd_batch launch
+            grad = any(ctx.needs_input_grad)  # inference: no transposed weights, no T-layout inputs
+            tf = int(_lib.load().x2g_chain_t_floats(R, D))
+            WT = torch.empty(G, 2, D, D, **f32) if grad else None
+            in_t = torch.empty(G, 2, tf, **f32) if grad else None
+
+            def wt(g, i):
+                return WT[g, i].data_ptr() if grad else None
+
+            stages = [(ChainStage * 2)(ChainStage(_dp(W1[g]), _dp(B1[g]), _dp(z1[g]), None, wt(g, 0), CHAIN_SILU),
+                                       ChainStage(_dp(W2[g]), _dp(B2[g]), _dp(z2[g]), _dp(h2[g]), wt(g, 1), CHAIN_SILU))
+                      for g in range(G)]
+            jobs = (ChainFwdJob * G)(*[ChainFwdJob(_dp(xs[g]), None, ctypes.addressof(stages[g]),
+                                                   in_t[g].data_ptr() if grad else None) for g in range(G)])
+            call("x2g_chain_fwd_batch", jobs, G, 2, R, D, st)
+            out = torch.empty(R, 1, **f32)
+            heads = (HeadGroup * G)(*[HeadGroup(_dp(h2[g]), _dp(W3[g]), _dp(B3[g]), None, None, None)
+                                      for g in range(G)])
+            call("x2g_readout_head_fwd", heads, G, R, D, ptr(out), st)
+            if grad:
+                ctx.save_for_backward(*h2, *z1, *z2, WT, in_t)
+            ctx.G, ctx.params = G, params
+            return out
+        h1 = [torch.empty(R, D, **f32) for _ in range(G)]
         for (src, w, b, y, z) in ((xs, W1, B1, h1, z1), (h1, W2, B2, h2, z2)):
             grp = (DenseFwdGroup * G)(*[DenseFwdGroup(_dp(src[g]), _dp(w[g]), _dp(b[g]), None, _dp(y[g]), _dp(z[g]))
                                         for g in range(G)])
@@ -475,10 +499,14 @@ class _ReadoutMLPs(torch.autograd.Function):
     def backward(ctx, dout):
         G = ctx.G
         saved = ctx.saved_tensors
-        xs, h1, z1, h2, z2 = (saved[i * G:(i + 1) * G] for i in range(5))
+        if ctx.chain:
+            h2, z1, z2 = (saved[i * G:(i + 1) * G] for i in range(3))
+            WT, in_t = saved[3 * G], saved[3 * G + 1]
+        else:
+            xs, h1, z1, h2, z2 = (saved[i * G:(i + 1) * G] for i in range(5))
         W1, B1, W2, B2, W3, B3 = (ctx.params[i::6] for i in range(6))
-        R, D = xs[0].shape
-        dev = xs[0].device
+        R, D = h2[0].shape
+        dev = h2[0].device
         f32 = dict(dtype=torch.float32, device=dev)
         lib = _lib.load()
         st = stream_ptr()
@@ -497,6 +525,21 @@ class _ReadoutMLPs(torch.autograd.Function):
             splits = int(lib.x2g_readout_head_bwd_splits(R))
             for g in range(G):
                 _defer_job(ws, g * splits * (D + 1) * 4, splits, D, 1, dw3[g], db3[g])
+        if ctx.chain:  # both hidden layers' data gradients in one launch; dW / db from the T layout
+            dfeat = [torch.empty(R, D, **f32) for _ in range(G)]
+            dz_t = torch.empty_like(in_t)
+            stages = [(ChainBwdStage * 2)(ChainBwdStage(_dp(W1[g]), WT[g, 0].data_ptr(), _dp(z1[g]), None, CHAIN_SILU),
+                                          ChainBwdStage(_dp(W2[g]), WT[g, 1].data_ptr(), _dp(z2[g]), None, CHAIN_SILU))
+                      for g in range(G)]
+            jobs = (ChainBwdJob * G)(*[ChainBwdJob(_dp(dh2[g]), None, ctypes.addressof(stages[g]), _dp(dfeat[g]), None,
+                                                   dz_t[g].data_ptr()) for g in range(G)])
+            call("x2g_chain_bwd_batch", jobs, G, 2, R, D, st)
+            pg = []
+            for g in range(G):
+                dws, dbs = chain_wgrad(in_t[g], dz_t[g], R, [W1[g], W2[g]], [B1[g], B2[g]])
+                pg += [dws[0], dbs[0], dws[1], dbs[1]]
+                pg += [None if acc3 else dw3[g].view_as(W3[g]), None if acc3 else db3[g]]
+            return (None, *dfeat, *pg)
         grads = {}
         # layer 2 then layer 1: dz = dy * SiLU'(z), dx = dz W, dW / db
         dy = dh2
@@ -523,6 +566,34 @@ class _ReadoutMLPs(torch.autograd.Function):
                 pg += [None if dw is None else dw[g], None if db is None else db[g]]
             pg += [None if acc3 else dw3[g].view_as(W3[g]), None if acc3 else db3[g]]
         return (None, *dfeat, *pg)
+
+
+# the readouts' two hidden layers as one batched row-chain launch each way (x2g_chain_*_batch);
+# X2G_READOUT_CHAIN=0: two batched dense launches each way
+_READOUT_CHAIN = os.environ.get("X2G_READOUT_CHAIN", "1") == "1"
+CHAIN_MAX_JOBS = 8  # X2G_CHAIN_MAX_JOBS
+
+
+class ChainFwdJob(ctypes.Structure):
+    """x2g_chain_fwd_job."""
+    _fields_ = [("x", ctypes.c_void_p), ("res_ext", ctypes.c_void_p), ("stages", ctypes.c_void_p),
+                ("in_t", ctypes.c_void_p)]
+
+
+class ChainBwdJob(ctypes.Structure):
+    """x2g_chain_bwd_job."""
+    _fields_ = [("dy", ctypes.c_void_p), ("dy_add", ctypes.c_void_p), ("stages", ctypes.c_void_p),
+                ("dx", ctypes.c_void_p), ("d_res_ext", ctypes.c_void_p), ("dz_t", ctypes.c_void_p)]
+
+
+def _readout_chain_ok(R, D, G, *weights):
+    if not _CHAIN or D != 128 or not 1 <= G <= CHAIN_MAX_JOBS or R * 128 >= 2 ** 31:
+        return False
+    for ws in weights:
+        for w in ws:
+            if w is not None and (w.dtype != torch.float32 or not w.is_contiguous() or w.data_ptr() % 16):
+                return False
+    return all(tuple(w.shape) == (128, 128) for ws in (weights[0], weights[2]) for w in ws)
 
 
 def _wgrad_pairs(Ws, Bs, dev):
@@ -1822,8 +1893,10 @@ class _GraphLayerNorm(torch.autograd.Function):
         out, rstd, rowptr = ctx.saved_tensors
         g = _f32(g)
         dx = torch.empty_like(out)
-        call("x2g_graph_layernorm_bwd", ptr(out), ptr(g), ptr(rstd), ptr(rowptr), ctx.n_seg, out.shape[1], ptr(dx),
-             stream_ptr())
+        wsb = int(_lib.load().x2g_graph_layernorm_bwd_workspace(ctx.n_seg))
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=out.device)
+        call("x2g_graph_layernorm_bwd_ex", ptr(out), ptr(g), ptr(rstd), ptr(rowptr), ctx.n_seg, out.shape[1], ptr(dx),
+             ptr(ws), wsb, stream_ptr())
         return dx, None, None, None
 
 
