@@ -295,6 +295,14 @@ int x2g_graph_layernorm_bwd_ex(const float* out, const float* dout, const float*
                                int64_t num_segments, int64_t dim, float* dx, void* workspace, size_t workspace_bytes,
                                void* stream);
 
+/* ---------------------------------------------------------------- loss
+ * F.smooth_l1_loss(pred, target, reduction='mean', beta) of the trainer step (trainer.py:41):
+ * out[0] = mean over n of (|d| < beta ? 0.5 d^2 / beta : |d| - 0.5 beta), d = pred - target; the
+ * backward dpred = gout[0] / n * clamp(d / beta, -1, 1).  One launch each way. */
+int x2g_smooth_l1_mean_fwd(const float* pred, const float* target, int64_t n, float beta, float* out, void* stream);
+int x2g_smooth_l1_mean_bwd(const float* pred, const float* target, int64_t n, float beta, const float* gout,
+                           float* dpred, void* stream);
+
 /* ---------------------------------------------------------------- dense-layer gradients */
 
 /* Workspace bytes for x2g_linear_wgrad (row-split partial slabs). */

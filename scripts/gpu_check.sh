@@ -20,7 +20,7 @@ for s in "$@"; do
   case $s in
     kernels) step kernels 420 python -m pytest tests/test_gpu_kernels.py -q -m gpu -rf ;;
     model) step model 420 python -m pytest tests/test_gpu_model.py -q -m gpu -rf ;;
-    proj) step proj 300 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -rf -k "conv_proj or pool or layernorm or readout or flat" --timeout 120 --timeout-method thread ;;
+    proj) step proj 300 python -u -m pytest tests/test_gpu_kernels.py -q -m gpu -rf -k "conv_proj or pool or layernorm or readout or flat or smooth_l1" --timeout 120 --timeout-method thread ;;
     ab) step ab 900 python -u scripts/step_ab.py ${AB_ROUNDS:-3} $AB_VARIANTS ;;
     gpu) step gputests 600 python -u -m pytest tests -q -m gpu -rf --timeout 300 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;

@@ -1211,3 +1211,23 @@ def test_tiled_wgrad_flat_vs_torch(cuda, R, njobs):
         if dbs[j] is not None:
             rb = dys[j].double().sum(0)
             assert float((dbs[j].double() - 5.0 - rb).abs().max()) <= 2e-5 * float(rb.abs().max()) + 1e-4, j
+
+
+@pytest.mark.parametrize("n,beta", [(1, 1.0), (128, 1.0), (1000, 0.5), (3, 2.0)])
+def test_smooth_l1_mean_vs_torch(cuda, n, beta):
+    """ops.smooth_l1_loss (x2g_smooth_l1_mean_fwd / _bwd, trainer.py:41) vs F.smooth_l1_loss:
+    both branches (|d| < beta and beyond), mean reduction, a non-unit upstream gradient."""
+    from x2gnn import ops
+
+    g = torch.Generator(device=cuda).manual_seed(n)
+    pred = (3 * torch.randn(n, device=cuda, generator=g)).requires_grad_(True)
+    target = torch.randn(n, device=cuda, generator=g)
+    ref_pred = pred.detach().clone().requires_grad_(True)
+    loss = ops.smooth_l1_loss(pred, target, beta=beta)
+    ref = torch.nn.functional.smooth_l1_loss(ref_pred, target, beta=beta)
+    assert loss.grad_fn is not None and "SmoothL1Mean" in type(loss.grad_fn).__name__
+    torch.testing.assert_close(loss, ref, rtol=1e-6, atol=1e-7)
+    up = torch.tensor(0.37, device=cuda)
+    loss.backward(up)
+    ref.backward(up)
+    torch.testing.assert_close(pred.grad, ref_pred.grad, rtol=1e-6, atol=1e-8)

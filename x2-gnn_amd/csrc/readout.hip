@@ -162,3 +162,62 @@ X2G_API int x2g_readout_head_bwd(const float* dout, const x2g_head_group* groups
   }
   return x2g_slab_sum_batch(jobs, G, accum ? 1 : 0, stream);
 }
+
+// ---------------------------------------------------------------- loss (trainer.py:41)
+// F.smooth_l1_loss(pred, target) (reduction 'mean', beta) as one launch each way instead of
+// torch's elementwise + mean (forward) and fill + fill + elementwise (backward): one 256-thread
+// workgroup, per-thread sums then a fixed-order reduction (deterministic).
+namespace x2g {
+namespace {
+constexpr int kLossThreads = 256;
+
+__global__ void __launch_bounds__(kLossThreads) smooth_l1_mean_fwd_kernel(const float* __restrict__ pred,
+                                                                          const float* __restrict__ target, int64_t n,
+                                                                          float beta, float* __restrict__ out) {
+  __shared__ float red[kLossThreads / 64];
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += kLossThreads) {
+    const float d = pred[i] - target[i], a = fabsf(d);
+    s += a < beta ? 0.5f * d * d / beta : a - 0.5f * beta;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = red[0];
+#pragma unroll
+    for (int w = 1; w < kLossThreads / 64; ++w) t += red[w];
+    out[0] = t / static_cast<float>(n);
+  }
+}
+
+__global__ void __launch_bounds__(kLossThreads) smooth_l1_mean_bwd_kernel(const float* __restrict__ pred,
+                                                                          const float* __restrict__ target, int64_t n,
+                                                                          float beta, const float* __restrict__ gout,
+                                                                          float* __restrict__ dpred) {
+  const float g = gout[0] / static_cast<float>(n);
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(kLossThreads) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * kLossThreads) {
+    const float d = pred[i] - target[i];
+    dpred[i] = g * (d < -beta ? -1.f : (d > beta ? 1.f : d / beta));
+  }
+}
+}  // namespace
+}  // namespace x2g
+
+X2G_API int x2g_smooth_l1_mean_fwd(const float* pred, const float* target, int64_t n, float beta, float* out,
+                                   void* stream) {
+  if (n <= 0 || !pred || !target || !out || !(beta > 0.f)) return X2G_EINVAL;
+  x2g::smooth_l1_mean_fwd_kernel<<<1, x2g::kLossThreads, 0, as_stream(stream)>>>(pred, target, n, beta, out);
+  return last_launch_status();
+}
+
+X2G_API int x2g_smooth_l1_mean_bwd(const float* pred, const float* target, int64_t n, float beta, const float* gout,
+                                   float* dpred, void* stream) {
+  if (n <= 0 || !pred || !target || !gout || !dpred || !(beta > 0.f)) return X2G_EINVAL;
+  const int64_t want = (n + x2g::kLossThreads - 1) / x2g::kLossThreads;
+  x2g::smooth_l1_mean_bwd_kernel<<<static_cast<unsigned>(want < 1024 ? want : 1024), x2g::kLossThreads, 0,
+                                   as_stream(stream)>>>(pred, target, n, beta, gout, dpred);
+  return last_launch_status();
+}

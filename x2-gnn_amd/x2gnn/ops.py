@@ -1904,3 +1904,34 @@ def graph_layer_norm(x, rowptr, num_segments: int, eps: float = 1e-5):
     """PyG LayerNorm(mode='graph', affine=False) over contiguous row segments."""
     _need_cuda(x, rowptr)
     return _GraphLayerNorm.apply(x, _i32(rowptr), int(num_segments), float(eps))
+
+
+# ------------------------------------------------------------------------------ loss
+class _SmoothL1MeanFn(torch.autograd.Function):
+    """F.smooth_l1_loss(pred, target) with reduction='mean' (trainer.py:41) as one launch each way
+    (x2g_smooth_l1_mean_fwd / _bwd) instead of torch's elementwise + mean and fill + fill +
+    elementwise; the target takes no gradient (the reference's labels)."""
+
+    @staticmethod
+    def forward(ctx, pred, target, beta):
+        p, t = _f32(pred).reshape(-1), _f32(target).reshape(-1)
+        out = torch.empty((), dtype=torch.float32, device=p.device)
+        call("x2g_smooth_l1_mean_fwd", ptr(p), ptr(t), p.numel(), float(beta), ptr(out), stream_ptr())
+        ctx.save_for_backward(p, t)
+        ctx.beta, ctx.shape = float(beta), pred.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        p, t = ctx.saved_tensors
+        dp = torch.empty_like(p)
+        call("x2g_smooth_l1_mean_bwd", ptr(p), ptr(t), p.numel(), ctx.beta, ptr(_f32(g).reshape(1)), ptr(dp),
+             stream_ptr())
+        return dp.view(ctx.shape), None, None
+
+
+def smooth_l1_loss(pred, target, beta: float = 1.0):
+    """torch.nn.functional.smooth_l1_loss(pred, target, beta=beta) (mean) on the device path."""
+    if not pred.is_cuda or pred.shape != target.shape or pred.numel() == 0 or target.requires_grad:
+        return torch.nn.functional.smooth_l1_loss(pred, target, beta=beta)
+    return _SmoothL1MeanFn.apply(pred, target, beta)
