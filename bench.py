@@ -40,7 +40,7 @@ from x2gnn.synth import molecules_from_geometry_file, synthetic_molecules  # noq
 CFG = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embedding_size=128)  # config.json
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32) peak, MI355X_MICROARCH.md
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r2_s_pmc_traffic.json")  # scripts/pmc_traffic.py output
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r2_z9_pmc_traffic.json")  # scripts/pmc_traffic.py output
 METRIC = "molecules/sec (fwd+bwd) on QM9 U0, batch=128, 1/2/4/8 MI355X"
 AID_GEOM = os.path.join(ROOT, "tests", "golden", "aid_geom.npz")  # raw/AID_kcal.xyz as arrays
 # BASELINE.json configs: [1] is the metric's; [2] and [4] are the other single-GPU shapes
