@@ -328,7 +328,7 @@ static int g_tune[kTuneCount] = {0};
 int tuning(int key) { return (key >= 0 && key < kTuneCount) ? g_tune[key] : 0; }
 }  // namespace x2g
 
-X2G_API int x2g_abi_version(void) { return 6; }
+X2G_API int x2g_abi_version(void) { return 7; }
 
 X2G_API int x2g_tuning(int key, int value) {
   if (key < 0 || key >= kTuneCount) return -1;
