@@ -340,12 +340,13 @@ X2G_API int32_t x2g_linear_wgrad_splits(int64_t R, int32_t O, int32_t I) {
 }
 
 // ------------------------------------------------------------------------------ batched slab sums
-constexpr int kBatchJobs = 40;  // jobs per launch (kernel arguments, < 4 KB)
+constexpr int kBatchJobs = 60;  // jobs per launch (kernel arguments: 60 B per job, < 4 KB): a training
+                                // step's ~90 deferred reductions in two launches
 
 struct SlabBatch {
   const float* part[2 * kBatchJobs];  // job j: entry 2j = weight slabs, 2j+1 = bias slabs
   float* out[2 * kBatchJobs];
-  int64_t n[2 * kBatchJobs];
+  int32_t n[2 * kBatchJobs];
   int splits[kBatchJobs];
   int block_end[2 * kBatchJobs];  // exclusive prefix of kSlabElems-element blocks
   int ld[kBatchJobs];             // weight entries: strided destination (x2g_slab_job.ld / cols)
@@ -381,6 +382,7 @@ X2G_API int x2g_slab_sum_batch(const x2g_slab_job* jobs, int32_t njobs, int32_t 
     for (int j = j0; j < njobs && j < j0 + kBatchJobs; ++j) {
       const x2g_slab_job& jb = jobs[j];
       if (!jb.part_w || !jb.dw || jb.n_w <= 0 || jb.splits <= 0 || (jb.part_b && !jb.db)) return X2G_EINVAL;
+      if (jb.n_w >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
       if (jb.ld < 0 || (jb.ld > 0 && (jb.n_w % 128 || jb.cols < 0 || jb.cols > 128 || jb.cols > jb.ld)))
         return X2G_EINVAL;
       const int k = j - j0;
@@ -390,7 +392,7 @@ X2G_API int x2g_slab_sum_batch(const x2g_slab_job* jobs, int32_t njobs, int32_t 
       const int e0 = 2 * k, e1 = 2 * k + 1;
       b.part[e0] = jb.part_w;
       b.out[e0] = jb.dw;
-      b.n[e0] = jb.n_w;
+      b.n[e0] = static_cast<int32_t>(jb.n_w);
       blocks += static_cast<int>(blocks_for(jb.n_w, kSlabElems));
       b.block_end[e0] = blocks;
       b.part[e1] = jb.part_b;
