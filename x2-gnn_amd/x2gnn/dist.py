@@ -74,8 +74,7 @@ class GradBucket:
                 dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
             return
         if multi:
-            if dist.get_backend(group) == "nccl":  # RCCL averages in the collective: no extra div kernel
-                dist.all_reduce(self.flat, op=dist.ReduceOp.AVG, group=group)
-            else:
-                dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
-                self.flat.div_(dist.get_world_size(group))
+            # SUM then one divide: ReduceOp.AVG would save the divide under RCCL, but it is the one
+            # collective option the 1-GPU rehearsal (gloo) cannot exercise before the 8-GPU run
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+            self.flat.div_(dist.get_world_size(group))
