@@ -16,12 +16,17 @@ seed by ``weights.seeded_value`` (see that module), so fixtures stay small.  Fix
 * ``model_small.npz``/``model_full.npz``/``model_global.npz`` — ``xgnn_poly`` / ``xgnn_poly_global``
                        forward energies and smooth-L1 parameter gradients (xgnn.py:38-75, model.py:38-54,
                        trainer.py:41-42).
+* ``xyz_ref.npz``    — the reference's ``utils.read_xyz`` (utils.py:17-63) on raw/AID_kcal.xyz and on
+                       small quirk files; ``aid_geom.npz`` is that same parse of AID_kcal.xyz as arrays.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import sys
+import tempfile
 import time
+import types
 
 import numpy as np
 import torch
@@ -190,12 +195,66 @@ def gen_model(ref, fname, kind, cfg, n_mol, seed_mol, seed_w, grads="all", pool_
     np.savez_compressed(os.path.join(HERE, fname), **out)
 
 
-def gen_aid_geometry():
+def _reference_read_xyz():
+    """The reference's own ``utils.read_xyz`` (utils.py:17-63).  utils.py imports ``pyscf.lib``
+    at line 2 and never uses it; pyscf is absent here, so an empty stand-in module satisfies the
+    import (nothing else is patched)."""
+    if "pyscf" not in sys.modules:
+        pyscf = types.ModuleType("pyscf")
+        pyscf.lib = types.ModuleType("pyscf.lib")
+        sys.modules["pyscf"], sys.modules["pyscf.lib"] = pyscf, pyscf.lib
+    import utils  # noqa: E402  (/root/reference/utils.py, on sys.path via import_reference)
+    return utils.read_xyz
+
+
+# small files that exercise utils.py's quirks (blank lines skipped; the last molecule is kept
+# only when the file's last line is an atom line); the reference's results on them are pinned
+XYZ_QUIRKS = {
+    "two": "3\n-1.5\nC 0.0 0.0 0.0\nH 1.0 0.0 0.0\nH 0.0 1.0 0.0\n2\n7.25\nO 0.0 0.0 0.0\nH 0.0 0.0 0.97\n",
+    "blank_between": "3\n-1.5\nC 0.0 0.0 0.0\nH 1.0 0.0 0.0\nH 0.0 1.0 0.0\n\n2\n7.25\nO 0.0 0.0 0.0\nH 0.0 0.0 0.97\n",
+    "trailing_blank": "3\n-1.5\nC 0.0 0.0 0.0\nH 1.0 0.0 0.0\nH 0.0 1.0 0.0\n2\n7.25\nO 0.0 0.0 0.0\nH 0.0 0.0 0.97\n\n",
+    "int_label": "1\n4\nH 0.5 0.25 0.125\n2\n-3.0\nN 1 2 3\nF 4 5 6.5\n",
+}
+
+
+def _pack_records(recs, prefix, out):
+    out[prefix + "counts"] = np.array([r.Z.shape[0] for r in recs], dtype=np.int32)
+    out[prefix + "z"] = (np.concatenate([r.Z.numpy() for r in recs]) if recs else np.zeros(0)).astype(np.int64)
+    out[prefix + "pos"] = (np.concatenate([r.R.numpy().reshape(-1, 3) for r in recs]) if recs
+                           else np.zeros((0, 3))).astype(np.float32)
+    for key, attr, dt in (("label", "Label", np.float64), ("n", "N", np.int64), ("idx", "idx", np.int64)):
+        vals = [getattr(r, attr).numpy().reshape(-1) for r in recs]  # ragged: a list per record
+        out[prefix + key] = (np.concatenate(vals) if vals else np.zeros(0)).astype(dt)
+        out[prefix + key + "_len"] = np.array([len(v) for v in vals], dtype=np.int64)
+    out[prefix + "atom_sha"] = np.array([hashlib.sha256(r.atom.encode()).hexdigest() for r in recs])
+    out[prefix + "label_dtype"] = np.array([str(recs[0].Label.dtype) if recs else ""])
+
+
+def gen_xyz_ref(ref):
+    """xyz_ref.npz: the reference's utils.read_xyz run here on raw/AID_kcal.xyz (config 5's
+    data) and on the XYZ_QUIRKS texts: Z / positions / labels / counts / idx and a hash of each
+    record's xyz text, so tests/test_datasets.py pins x2gnn.datasets.read_xyz to it."""
+    read_xyz = _reference_read_xyz()
+    out = {}
+    _pack_records(read_xyz(os.path.join(REF, "raw/AID_kcal.xyz")), "aid_", out)
+    with tempfile.TemporaryDirectory() as tmp:
+        for name, text in XYZ_QUIRKS.items():
+            p = os.path.join(tmp, name + ".xyz")
+            with open(p, "w") as f:
+                f.write(text)
+            _pack_records(read_xyz(p), name + "_", out)
+    out["quirk_names"] = np.array(list(XYZ_QUIRKS))
+    for name, text in XYZ_QUIRKS.items():
+        out[name + "_text"] = np.array(text)
+    np.savez_compressed(os.path.join(HERE, "xyz_ref.npz"), **out)
+    print(f"xyz_ref.npz: {len(out['aid_counts'])} AID molecules + {len(XYZ_QUIRKS)} quirk files")
+
+
+def gen_aid_geometry(ref):
     """aid_geom.npz: every molecule of raw/AID_kcal.xyz (config 5's data) as Z / positions /
-    label arrays, parsed with the reference's read_xyz grammar (x2gnn.datasets.read_xyz), so the
-    GPU box (where /root/reference does not exist) can rebuild the molecules."""
-    from x2gnn.datasets import read_xyz
-    recs = read_xyz(os.path.join(REF, "raw/AID_kcal.xyz"))
+    label arrays, parsed by the reference's own utils.read_xyz (utils.py:17-63), so the GPU box
+    (where /root/reference does not exist) can rebuild the molecules."""
+    recs = _reference_read_xyz()(os.path.join(REF, "raw/AID_kcal.xyz"))
     np.savez_compressed(os.path.join(HERE, "aid_geom.npz"),
                         counts=np.array([r.Z.shape[0] for r in recs], dtype=np.int32),
                         z=np.concatenate([r.Z.numpy() for r in recs]).astype(np.int8),
@@ -237,7 +296,8 @@ GENERATORS = {
     # config 5: real AID geometry (the two smallest molecules), full width
     "model_aid": lambda ref: gen_model(ref, "model_aid.npz", "poly", FULL, n_mol=1, seed_mol=0, seed_w=206,
                                        grads=SEL, mols=aid_molecules(2)),
-    "aid_geom": lambda ref: gen_aid_geometry(),
+    "aid_geom": lambda ref: gen_aid_geometry(ref),
+    "xyz_ref": lambda ref: gen_xyz_ref(ref),
 }
 
 

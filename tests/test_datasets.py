@@ -47,6 +47,54 @@ def test_read_xyz_keeps_reference_quirks(tmp_path):
     assert len(ds.read_xyz(_write(tmp_path, "c.xyz", XYZ_TWO + "\n"))) == 1
 
 
+REF_AID = "/root/reference/raw/AID_kcal.xyz"
+
+
+def _check_against_reference(recs, z, prefix):
+    """x2gnn.datasets.read_xyz records == the reference's utils.read_xyz outputs stored in
+    xyz_ref.npz (tests/golden/make_golden.py gen_xyz_ref ran the reference itself)."""
+    import hashlib
+
+    counts = z[prefix + "counts"]
+    assert len(recs) == len(counts)
+    assert [r.Z.shape[0] for r in recs] == counts.tolist()
+    if len(recs):
+        np.testing.assert_array_equal(np.concatenate([r.Z.numpy() for r in recs]), z[prefix + "z"])
+        np.testing.assert_array_equal(np.concatenate([r.R.numpy().reshape(-1, 3) for r in recs]), z[prefix + "pos"])
+        assert all(r.R.dtype == torch.float32 for r in recs if r.R.numel())
+    for key, attr in (("label", "Label"), ("n", "N"), ("idx", "idx")):
+        vals = [getattr(r, attr).numpy().reshape(-1) for r in recs]
+        assert [len(v) for v in vals] == z[prefix + key + "_len"].tolist(), key
+        if len(vals) and sum(len(v) for v in vals):
+            np.testing.assert_array_equal(np.concatenate(vals).astype(z[prefix + key].dtype), z[prefix + key])
+    if len(recs):
+        assert str(recs[0].Label.dtype) == str(z[prefix + "label_dtype"][0])
+    assert [hashlib.sha256(r.atom.encode()).hexdigest() for r in recs] == z[prefix + "atom_sha"].tolist()
+
+
+def test_read_xyz_quirks_equal_reference(tmp_path):
+    z = golden("xyz_ref.npz")
+    for name in z["quirk_names"].tolist():
+        recs = ds.read_xyz(_write(tmp_path, name + ".xyz", str(z[name + "_text"])))
+        _check_against_reference(recs, z, name + "_")
+
+
+@pytest.mark.skipif(not os.path.exists(REF_AID), reason="the reference's raw/AID_kcal.xyz is only in the build container")
+def test_read_xyz_aid_equals_reference():
+    """The whole AID_kcal.xyz (config 5's data) parsed here == the reference's own parse, and the
+    committed aid_geom.npz (what the GPU box rebuilds config 5 from) is that parse."""
+    z = golden("xyz_ref.npz")
+    _check_against_reference(ds.read_xyz(REF_AID), z, "aid_")
+
+
+def test_aid_geometry_fixture_is_reference_parse():
+    z, aid = golden("xyz_ref.npz"), golden("aid_geom.npz")
+    np.testing.assert_array_equal(aid["counts"], z["aid_counts"])
+    np.testing.assert_array_equal(aid["z"].astype(np.int64), z["aid_z"])
+    np.testing.assert_array_equal(aid["pos"], z["aid_pos"])
+    np.testing.assert_array_equal(aid["label"], z["aid_label"])
+
+
 def test_read_xyz_allprop(tmp_path):
     props = "\t".join(["1.5", "2.25", "-0.25", "0.1", "0.35", "19.0", "0.12", "-40.4", "-40.3", "-40.2",
                        "-40.5", "6.4*^-1"])

@@ -447,3 +447,72 @@ def test_fan_in_gradients_match_autograd_adds(cuda):
         # (summation order differs; gradients that vanish analytically, e.g. the key bias under the
         # softmax's shift invariance, are compared at the model's gradient scale)
         assert float((a - r).abs().max()) <= 1e-5 * scale + 1e-6 * top, n
+
+
+def _trainer_setup(cuda, n=8):
+    import x2gnn
+    from x2gnn.data import collate
+    from x2gnn.synth import synthetic_molecules
+    from x2gnn.train import Trainer
+
+    cfg = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embedding_size=128)
+    torch.manual_seed(0)
+    model = x2gnn.xgnn_poly(device="cuda", **cfg).to(cuda)
+    batch = collate(synthetic_molecules(n, "S160", seed=77)).to(cuda)
+    return Trainer(model), batch
+
+
+def test_double_capture_replays_equal_eager(cuda):
+    """The training step captured TWICE on the same model and batch (two live HIP graphs with
+    their own private memory pools): replaying either must give the eager step's loss and
+    gradient bucket bit for bit, and graph B must still replay correctly after graph A (and its
+    pool) is destroyed and the freed memory is reused and overwritten — a captured kernel that
+    held a raw pointer into memory owned by another capture would read garbage here."""
+    tr, batch = _trainer_setup(cuda)
+    tr.forward_backward(batch)  # first forward applies the embedding's max_norm renorm
+    tr.bucket.zero()
+    loss_e = tr.forward_backward(batch).detach().clone()
+    eager = tr.bucket.flat.detach().clone()
+    tr.capture(batch)
+    graphs_a, loss_a = tr.graphs, tr.loss
+    tr.capture(batch)
+    graphs_b, loss_b = tr.graphs, tr.loss
+    out = []
+    for g, lo in ((graphs_a, loss_a), (graphs_b, loss_b), (graphs_a, loss_a)):
+        tr.bucket.zero()
+        g[0].replay()
+        torch.cuda.synchronize()
+        out.append((lo.detach().clone(), tr.bucket.flat.detach().clone()))
+    for lo, flat in out:
+        assert torch.equal(lo, loss_e)
+        assert torch.equal(flat, eager)
+    del graphs_a, loss_a, out
+    tr.graphs = None
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    junk = [torch.full((1 << 22,), float("nan"), device=cuda) for _ in range(64)]  # reuse freed memory
+    tr.bucket.zero()
+    graphs_b[0].replay()
+    torch.cuda.synchronize()
+    assert torch.equal(loss_b, loss_e)
+    assert torch.equal(tr.bucket.flat, eager)
+    del junk
+
+
+def test_graphed_training_steps_equal_eager_steps(cuda):
+    """Three full steps (forward, loss, backward, clip + Adam + EMA) replayed from the captured
+    graphs leave parameters, optimizer state and EMA bitwise equal to three eager steps."""
+    res = []
+    for graphed in (False, True):
+        tr, batch = _trainer_setup(cuda)
+        if graphed:
+            tr.capture(batch, warm=3)
+        else:  # the same number of forwards as the capture's warm-up: each applies the max_norm renorm
+            for _ in range(3):
+                tr.forward_backward(batch)
+        losses = [float(tr.step(batch).detach()) for _ in range(3)]
+        torch.cuda.synchronize()
+        res.append((losses, tr.opt.flat.clone(), tr.opt.exp_avg_sq.clone(), tr.opt.ema.clone()))
+    assert res[0][0] == res[1][0]
+    for a, b in zip(res[0][1:], res[1][1:]):
+        assert torch.equal(a, b)

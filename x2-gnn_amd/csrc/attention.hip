@@ -962,7 +962,7 @@ X2G_API int x2g_sbf_project(const float* sbf, int64_t T, int32_t sbf_dim, const 
   }
   // f32 MFMA, tiles staged through LDS (dense.hip): that kernel covers N <= 128 output columns
   // and addresses rows with 32-bit offsets; wider projections take the per-row kernel below
-  if (out_dim % 4 == 0 && out_dim <= 128 && T * 128 < (int64_t(1) << 31) &&
+  if (out_dim % 4 == 0 && out_dim <= 128 && T * 128 * 4 < (int64_t(1) << 31) &&
       reinterpret_cast<uintptr_t>(sbf) % 16 == 0 && reinterpret_cast<uintptr_t>(sbfproj) % 16 == 0 &&
       (tuning(kTuneAttn) == 0 || tuning(kTuneAttn) == 2))
     return dense_fwd_narrow_launch(sbf, w_sbf, b_sbf, nullptr, T, kS, out_dim, 0, sbfproj, nullptr, st);

@@ -1711,7 +1711,7 @@ static int chain_fwd_prepare(const float* x, const float* res_ext, const x2g_cha
                              int64_t rows, int32_t dim, float* in_t, ChainFwdArgs& a, bool& empty) {
   empty = false;
   if (!stages || n_stages < 1 || n_stages > X2G_CHAIN_MAX_STAGES || rows < 0 || dim <= 0) return X2G_EINVAL;
-  if (dim != kCD || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  if (dim != kCD || rows * kCD * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
   a = ChainFwdArgs{};
   a.x = x;
   a.res = res_ext;
@@ -1774,7 +1774,7 @@ static int chain_bwd_prepare(const float* dy, const float* dy_add, const x2g_cha
   empty = false;
   res_accum = false;
   if (!stages || n_stages < 1 || n_stages > X2G_CHAIN_MAX_STAGES || rows < 0 || dim <= 0) return X2G_EINVAL;
-  if (dim != kCD || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  if (dim != kCD || rows * kCD * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
   a = ChainBwdArgs{};
   a.dy = dy;
   a.dy_add = dy_add;
@@ -1890,7 +1890,7 @@ X2G_API int x2g_wgrad_batched(const x2g_wgrad_job* jobs, int32_t num_jobs, int64
   if (!jobs || num_jobs < 1 || num_jobs > X2G_CHAIN_MAX_STAGES || rows <= 0 || dim <= 0 ||
       (flags & ~(X2G_ACCUM_WGRAD | X2G_DEFER_SLAB_SUM)))
     return X2G_EINVAL;
-  if (dim != kCD || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  if (dim != kCD || rows * kCD * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
   const size_t need = x2g_wgrad_batched_workspace(rows, dim, num_jobs);
   if (!workspace || workspace_bytes < need) return X2G_EWORKSPACE;
   WgradArgs a{};
@@ -1931,7 +1931,7 @@ X2G_API int x2g_chain_wgrad(const float* in_t, const float* dz_t, int32_t n_stag
   if (!in_t || !dz_t || !dw || n_stages < 1 || n_stages > X2G_CHAIN_MAX_STAGES || rows <= 0 || dim <= 0 ||
       (flags & ~(X2G_ACCUM_WGRAD | X2G_DEFER_SLAB_SUM)))
     return X2G_EINVAL;
-  if (dim != kCD || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  if (dim != kCD || rows * kCD * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
   if (!al16(in_t) || !al16(dz_t)) return X2G_EUNSUPPORTED;
   const size_t need = x2g_chain_wgrad_workspace(rows, dim, n_stages);
   if (!workspace || workspace_bytes < need) return X2G_EWORKSPACE;
@@ -1969,7 +1969,7 @@ static inline unsigned v2_grid(int64_t rows) {
 X2G_API int x2g_conv_proj_fwd(const float* x, const float* rbf, int32_t rbf_dim, const float* w_rbf,
                               const x2g_proj* proj, int64_t rows, int32_t dim, float* x_t, float* xs_t, void* stream) {
   if (!proj || rows < 0 || dim <= 0 || rbf_dim <= 0) return X2G_EINVAL;
-  if (dim != kCD || rbf_dim > kRbfMax || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  if (dim != kCD || rbf_dim > kRbfMax || rows * kCD * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
   if (rows == 0) return X2G_OK;
   if (!x || !rbf || !w_rbf) return X2G_EINVAL;
   ProjFwdArgs a{};
@@ -1996,7 +1996,7 @@ X2G_API int x2g_conv_proj_fwd(const float* x, const float* rbf, int32_t rbf_dim,
 X2G_API int x2g_conv_proj_bwd(const x2g_proj_grad* grads, int64_t rows, int32_t dim, float* dx, const float* dx_add,
                               float* dxs, void* stream) {
   if (!grads || rows < 0 || dim <= 0) return X2G_EINVAL;
-  if (dim != kCD || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  if (dim != kCD || rows * kCD * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
   if (rows == 0) return X2G_OK;
   if (!dx || !dxs) return X2G_EINVAL;
   ProjBwdArgs a{};
@@ -2027,7 +2027,7 @@ X2G_API int x2g_conv_proj_bwd_gate(const x2g_proj_grad* grads, int64_t rows, int
                                    void* stream) {
   if (!grads || rows < 0 || dim <= 0 || rbf_dim <= 0 || !dw_rbf) return X2G_EINVAL;
   if (flags & ~(X2G_ACCUM_WGRAD | X2G_DEFER_SLAB_SUM | X2G_GATE_DRBF_ACCUM)) return X2G_EINVAL;
-  if (dim != kCD || rbf_dim > kRbfMax || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  if (dim != kCD || rbf_dim > kRbfMax || rows * kCD * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
   hipStream_t st = as_stream(stream);
   if (rows == 0) {
     if (flags & X2G_DEFER_SLAB_SUM) return X2G_EINVAL;
@@ -2102,7 +2102,7 @@ X2G_API int x2g_tiled_wgrad_flat(const x2g_tiled_job* jobs, int32_t num_jobs, in
   if (!jobs || num_jobs < 1 || num_jobs > X2G_TILED_MAX_JOBS || rows <= 0 || dim <= 0 ||
       (flags & ~(X2G_ACCUM_WGRAD | X2G_DEFER_SLAB_SUM)))
     return X2G_EINVAL;
-  if (dim != kCD || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  if (dim != kCD || rows * kCD * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
   if ((flags & X2G_DEFER_SLAB_SUM) && !slab_jobs) return X2G_EINVAL;
   const size_t need = x2g_tiled_wgrad_flat_workspace(rows, dim, num_jobs);
   if (!workspace || workspace_bytes < need) return X2G_EWORKSPACE;
@@ -2162,7 +2162,7 @@ X2G_API int x2g_tiled_wgrad(const x2g_tiled_job* jobs, int32_t num_jobs, int64_t
   if (!jobs || num_jobs < 1 || num_jobs > X2G_CHAIN_MAX_STAGES || rows <= 0 || dim <= 0 ||
       (flags & ~(X2G_ACCUM_WGRAD | X2G_DEFER_SLAB_SUM)))
     return X2G_EINVAL;
-  if (dim != kCD || rows * kCD >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  if (dim != kCD || rows * kCD * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
   const size_t need = x2g_tiled_wgrad_workspace(rows, dim, num_jobs);
   if (!workspace || workspace_bytes < need) return X2G_EWORKSPACE;
   ChainWgradArgs a{};

@@ -1096,7 +1096,7 @@ __global__ void __launch_bounds__(512) dense_fwd_narrow(const float* __restrict_
 int dense_fwd_narrow_launch(const float* x, const float* w, const float* b, const float* res, int64_t R, int K, int N,
                             int act, float* y, float* z, hipStream_t st) {
   // the kernel covers N <= 128 columns and K <= 2*64; row offsets are 32-bit
-  if (N > 128 || K > 128 || R * 128 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  if (N > 128 || K > 128 || R * 128 * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
   const int64_t npairs = (R + 63) / 64;
   const unsigned grid = static_cast<unsigned>(npairs < 512 ? npairs : 512);
   if (K <= 44)
@@ -1589,7 +1589,7 @@ X2G_API int x2g_dense_fwd(const float* x, const float* w, const float* b, int64_
   if (!x || !w || !y) return X2G_EINVAL;
   hipStream_t st = as_stream(stream);
   const int variant = tuning(kTuneDenseFwd);  // 0: LDS-staged (default), 1: register fragments, 2: tiled
-  if (K <= 128 && N <= 128 && variant <= 1 && R * 128 < (int64_t(1) << 31)) {
+  if (K <= 128 && N <= 128 && variant <= 1 && R * 128 * 4 < (int64_t(1) << 31)) {
     const int64_t ntiles = (R + kPTile - 1) / kPTile;
     const int64_t want = (ntiles + 1) / 2;
     const unsigned grid = static_cast<unsigned>(want < kPFwdGrid ? want : kPFwdGrid);
@@ -1687,7 +1687,7 @@ static inline int64_t bwd_grid(int64_t R) {
 }
 
 static inline bool dense_persistent_bwd(int64_t R, int32_t K, int32_t N) {
-  return K <= 128 && N <= 128 && R > 0 && R * 128 < (int64_t(1) << 31);  // 32-bit offsets inside
+  return K <= 128 && N <= 128 && R > 0 && R * 128 * 4 < (int64_t(1) << 31);  // 32-bit offsets inside
 }
 
 static inline int64_t narrow_bwd_grid(int64_t R) {
@@ -1809,7 +1809,7 @@ X2G_API int x2g_residual_fwd(const float* x, const float* w0, const float* b0, c
   if (R < 0 || D <= 0) return X2G_EINVAL;
   if (R == 0) return X2G_OK;
   if (!x || !w0 || !w1 || !h || !z0 || !z1 || !y) return X2G_EINVAL;
-  if (D > 128 || D % 4 || D <= 8 || R * 128 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  if (D > 128 || D % 4 || D <= 8 || R * 128 * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
   if (!aligned16(x) || !aligned16(h) || !aligned16(z0) || !aligned16(z1) || !aligned16(y)) return X2G_EUNSUPPORTED;
   const int64_t ntiles = (R + 31) / 32;
   const unsigned grid = static_cast<unsigned>(ntiles < 256 ? ntiles : 256);
@@ -1823,7 +1823,7 @@ X2G_API int x2g_dense_fwd_batched(const x2g_dense_fwd_group* groups, int32_t G, 
   if (!groups || G < 1 || G > X2G_MAX_GROUPS || R < 0 || K <= 0 || N <= 0 || (act != kActNone && act != kActSilu))
     return X2G_EINVAL;
   if (R == 0) return X2G_OK;
-  if (K > 128 || N > 128 || K % 4 || N % 4 || K <= 8 || R * 128 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  if (K > 128 || N > 128 || K % 4 || N % 4 || K <= 8 || R * 128 * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
   DenseFwdBatch b{};
   for (int g = 0; g < G; ++g) {
     const x2g_dense_fwd_group& p = groups[g];

@@ -65,7 +65,7 @@ struct FeatFwdArgs {
   int64_t R;
   int64_t tf;        // floats per T plane
   int K;
-  int dbg;           // x2g_tuning(kTuneFeatDbg) ablation bits (timing only; 0 in production)
+  int want_t;        // write the backward's T-layout operands (0: inference, the four pointers NULL)
 };
 
 // W1 operand of 16-group q for column c: W1[c][16q + 4g .. +3] as two 8-byte loads (K is even,
@@ -137,7 +137,7 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
     const int64_t r0 = tile * kFRows;
     const int nr = R - r0 < kFRows ? static_cast<int>(R - r0) : kFRows;
     __syncthreads();  // the previous tile's products no longer read A / Y1 / envs
-    if (!(a.dbg & 8)) {  // scatter the staged span into 388-float rows (rows past nr: zero)
+    {  // scatter the staged span into 388-float rows (rows past nr: zero)
       const int n = nr * K;
 #pragma unroll
       for (int u = 0; u < kFX4; ++u) {
@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
     if (tile + gridDim.x < ntiles) xtile_load(a, tile + gridDim.x, xt);  // in flight during the products
     // x * env in T layout: per 16-row tile and plane, float4 u of the 2048-float block holds
     // feature u >> 2, rows 4 (u & 3) .. +3
-    for (int idx = tid; idx < ((a.dbg & 8) ? 0 : 2 * 3 * 512); idx += kFThreads) {
+    for (int idx = tid; idx < (a.want_t ? 2 * 3 * 512 : 0); idx += kFThreads) {
       const int rt = idx / (3 * 512), p = (idx / 512) % 3, u = idx % 512;
       const int64_t t16 = r0 / 16 + rt;
       if (t16 * 16 >= R || 128 * p >= K) continue;
@@ -173,7 +173,7 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
     f4 acc[2][2] = {{zero4(), zero4()}, {zero4(), zero4()}};
     // W1 operands two groups ahead (set 0: even groups, set 1: odd; a set is reloaded right after
     // its MFMAs issue), the A rows of the next group read before this group's MFMAs
-    const int KQn = (a.dbg & 1) ? 0 : KQ;
+    const int KQn = KQ;
     f4 wa0 = w1_frag(a.w1, K, c1a, 0, g), wb0 = w1_frag(a.w1, K, c1b, 0, g);
     f4 wa1 = w1_frag(a.w1, K, c1a, 1, g), wb1 = w1_frag(a.w1, K, c1b, 1, g);
     f4 a0 = *reinterpret_cast<const f4*>(A + i * kFAS + 4 * g);
@@ -217,7 +217,7 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
           y[e] = ok ? silu_(z[e]) : 0.0f;
           Y1[r * kFYS + c] = y[e];
         }
-        if (tile_ok && !(a.dbg & 4)) {
+        if (tile_ok && a.want_t) {
           *reinterpret_cast<f4*>(a.z1_t + tpos(a.tf, t16, c, g)) = z;
           *reinterpret_cast<f4*>(a.y1_t + tpos(a.tf, t16, c, g)) = y;
         }
@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
     __syncthreads();
     // z2 = SiLU(z1) W2^T + b2: wave w -> columns 16w + i
     f4 acc2[2] = {zero4(), zero4()};
-    if (!(a.dbg & 2)) {
+    {
       f4 y0 = *reinterpret_cast<const f4*>(Y1 + i * kFYS + 4 * g);
       f4 y1 = *reinterpret_cast<const f4*>(Y1 + (16 + i) * kFYS + 4 * g);
 #pragma unroll
@@ -253,9 +253,9 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
       for (int e = 0; e < 4; ++e) {
         const int r = 16 * rb + 4 * g + e;
         z[e] = r < nr ? acc2[rb][e] + b2v : 0.0f;
-        if (r < nr && !(a.dbg & 4)) a.y2[(r0 + r) * kFN2 + c2] = silu_(z[e]);
+        if (r < nr) a.y2[(r0 + r) * kFN2 + c2] = silu_(z[e]);
       }
-      if (!(a.dbg & 4)) *reinterpret_cast<f4*>(a.z2_t + tpos(a.tf, t16, c2, g)) = z;
+      if (a.want_t) *reinterpret_cast<f4*>(a.z2_t + tpos(a.tf, t16, c2, g)) = z;
     }
   }
 }
@@ -358,15 +358,18 @@ X2G_API int x2g_feat_fwd(const float* x, const float* env, int64_t rows, int32_t
                          const float* b1, const float* w2, const float* b2, float* y, float* xs_t, float* z1_t,
                          float* y1_t, float* z2_t, void* stream) {
   if (rows < 0 || in_dim <= 0) return X2G_EINVAL;
-  if (in_dim > kFKMax || in_dim % 2 || in_dim <= 2 * 128 || rows * kFKMax >= (int64_t(1) << 31))
+  if (in_dim > kFKMax || in_dim % 2 || in_dim <= 2 * 128 || rows * kFKMax * 4 >= (int64_t(1) << 31))
     return X2G_EUNSUPPORTED;
   if (rows == 0) return X2G_OK;
-  if (!x || !w1 || !w2 || !y || !xs_t || !z1_t || !y1_t || !z2_t) return X2G_EINVAL;
+  if (!x || !w1 || !w2 || !y) return X2G_EINVAL;
+  // the four T-layout outputs feed the backward: all given (training) or all NULL (inference)
+  const int nt = (xs_t != nullptr) + (z1_t != nullptr) + (y1_t != nullptr) + (z2_t != nullptr);
+  if (nt != 0 && nt != 4) return X2G_EINVAL;
   if (!al16(x) || !al16(w2) || !al16(xs_t) || !al16(z1_t) || !al16(y1_t) || !al16(z2_t) ||
       reinterpret_cast<uintptr_t>(w1) % 8)
     return X2G_EUNSUPPORTED;
   FeatFwdArgs a{x, env, w1, b1, w2, b2, y, xs_t, z1_t, y1_t, z2_t, rows, x2g_chain_t_floats(rows, 128), in_dim,
-                tuning(kTuneFeatDbg)};
+                nt == 4 ? 1 : 0};
   feat_fwd_kernel<<<feat_grid(rows), kFThreads, 0, as_stream(stream)>>>(a);
   return last_launch_status();
 }
@@ -374,7 +377,7 @@ X2G_API int x2g_feat_fwd(const float* x, const float* env, int64_t rows, int32_t
 X2G_API int x2g_feat_bwd(const float* dy, const float* z2_t, const float* z1_t, const float* w2, int64_t rows,
                          float* dz2_t, float* dz1_t, void* stream) {
   if (rows < 0) return X2G_EINVAL;
-  if (rows * kFKMax >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  if (rows * kFKMax * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
   if (rows == 0) return X2G_OK;
   if (!dy || !z2_t || !z1_t || !w2 || !dz2_t || !dz1_t) return X2G_EINVAL;
   if (!al16(z2_t) || !al16(z1_t) || !al16(dz2_t) || !al16(dz1_t)) return X2G_EUNSUPPORTED;

@@ -157,7 +157,12 @@ def _is_symmetric(ei, n):
         return True
     fwd = ei[0].astype(np.int64) * n + ei[1]
     rev = ei[1].astype(np.int64) * n + ei[0]
-    return bool(np.array_equal(np.sort(fwd), np.sort(rev)))
+    sf = np.sort(fwd)
+    # duplicate directed edges break the symmetric builders' per-edge counts (deg(b) - 1): such a
+    # multigraph takes the generic path even when its multiset is symmetric
+    if sf.size > 1 and bool((sf[1:] == sf[:-1]).any()):
+        return False
+    return bool(np.array_equal(sf, np.sort(rev)))
 
 
 def molecule_to_data(mol: dict) -> Data:

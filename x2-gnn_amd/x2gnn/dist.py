@@ -42,11 +42,15 @@ class GradBucket:
     """All parameters' gradients as views of ONE flat buffer, so the per-step exchange is a
     single all-reduce (ring over xGMI) with no pack/unpack copies."""
 
-    def __init__(self, params):
+    def __init__(self, params, extra=0):
+        """``extra``: trailing floats after the gradients (x2gnn.train keeps the step's loss there so
+        it is all-reduced by the same collective); ``extra_view`` is that slice."""
         self.params = [p for p in params if p.requires_grad]
         self.offsets, n = flat_layout(self.params)
+        self.num_grad = n
         dev = self.params[0].device
-        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)  # padding stays zero
+        self.flat = torch.zeros(n + int(extra), dtype=torch.float32, device=dev)  # padding stays zero
+        self.extra_view = self.flat[n:]
         for p, off in zip(self.params, self.offsets):
             p.grad = self.flat[off:off + p.numel()].view_as(p)
             # the fused dense / attention backwards may sum weight gradients straight into this

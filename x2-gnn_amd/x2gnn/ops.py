@@ -29,6 +29,12 @@ from ._lib import call, ptr, stream_ptr
 EDGE_NONE, EDGE_PER_TRIPLET, EDGE_PER_DST = 0, 1, 2
 
 
+def rows_fit(rows, width):
+    """True when a [rows, width] fp32 array is addressable by the kernels' 32-bit BYTE offsets
+    (buffer-resource loads / stores: num_records is a byte count below 2^31)."""
+    return int(rows) * int(width) * 4 < 2 ** 31
+
+
 def _need_cuda(*ts):
     for t in ts:
         if t is not None and not t.is_cuda:
@@ -234,7 +240,7 @@ class _SBFAttention(torch.autograd.Function):
     def forward(ctx, q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row, heads, channels):
         w_param, b_param = w_sbf, b_sbf
         # its gradient is read only by the table chain's backward, which flushes deferred sums first
-        ctx.defer_edge = _DEFER_KEYED and getattr(edge, "_x2g_table_out", False)
+        ctx.defer_edge = _DEFER_KEYED and getattr(edge, "_x2g_table_out", False) and ctx.needs_input_grad[4]
         factors = _sbf_factors(lg, sbf, edge_mode, heads * channels, edge, edge_row)
         q, k, v, skip = _f32(q), _f32(k), _f32(v), _f32(skip)
         sbf, w_sbf, b_sbf = _f32(sbf), _f32(w_sbf), _f32(b_sbf)
@@ -294,7 +300,9 @@ class _SBFAttention(torch.autograd.Function):
         call("x2g_sbf_attention_bwd_src", ptr(q), ptr(sproj), None, None, ptr(src_rowptr), ptr(src_perm),
              ptr(lg.trip_dst), ptr(alpha), ptr(smax), ptr(sden), ptr(dlogit), ptr(dout), E, T, heads, channels, D,
              ptr(dk), ptr(dv), st)
-        if mode == EDGE_PER_DST and ctx.edge_row is not None:
+        if not ctx.needs_input_grad[4]:
+            d_edge = None
+        elif mode == EDGE_PER_DST and ctx.edge_row is not None:
             # rows of the edge table are shared by many destinations: sum d_edge per table row
             d_edge = keyed_row_sum(d_edge, ctx.edge_row, ctx.edge_shape[0])
         gw, gb = grad_sink(ctx.w_param), grad_sink(ctx.b_param)
@@ -323,7 +331,9 @@ class _SBFAttention(torch.autograd.Function):
         call("x2g_sbf_attention_bwd_src_fold", ptr(q), ptr(v), ptr(edge), ptr(ctx.edge_row), rows, mode, ptr(sproj),
              ptr(ylm), ptr(src_rowptr), ptr(src_perm), ptr(lg.trip_dst), ptr(prob), ptr(g), ptr(rho), ptr(dout), E, T,
              heads, channels, ptr(dk), ptr(dv), ptr(gfold), st)
-        if mode == EDGE_PER_DST and ctx.edge_row is not None:
+        if not ctx.needs_input_grad[4]:
+            d_edge = None  # (written by the kernel; no consumer: the table's gradient is not wanted)
+        elif mode == EDGE_PER_DST and ctx.edge_row is not None:
             if ctx.defer_edge:
                 d_edge = keyed_row_sum_deferred(d_edge, ctx.edge_row, ctx.edge_shape[0])
             else:
@@ -587,7 +597,7 @@ class ChainBwdJob(ctypes.Structure):
 
 
 def _readout_chain_ok(R, D, G, *weights):
-    if not _CHAIN or D != 128 or not 1 <= G <= CHAIN_MAX_JOBS or R * 128 >= 2 ** 31:
+    if not _CHAIN or D != 128 or not 1 <= G <= CHAIN_MAX_JOBS or not rows_fit(R, 128):
         return False
     for ws in weights:
         for w in ws:
@@ -613,7 +623,7 @@ def readout_mlps_supported(feats, mlps):
     if G < 1 or G > 8 or not all(f.is_cuda and f.dim() == 2 and f.shape == feats[0].shape for f in feats):
         return False
     R, D = feats[0].shape
-    if D % 4 or D <= 8 or D > 128 or (D // 4) & (D // 4 - 1) or R * 128 >= 2 ** 31:
+    if D % 4 or D <= 8 or D > 128 or (D // 4) & (D // 4 - 1) or not rows_fit(R, 128):
         return False
     for m in mlps:
         mods = list(m)
@@ -794,6 +804,10 @@ def deferred_wgrad():
             call("x2g_slab_sum_batch", ctypes.cast(arr, ctypes.c_void_p), len(d.jobs), 1, stream_ptr())
     finally:
         _DEFER = prev
+        # keyed row sums queued for a table-chain backward that never ran (a partial backward:
+        # frozen embedding / edge tables, autograd.grad on a subset) are dropped here, not kept
+        # alive (and growing) until some later backward
+        _KEYED_PENDING.clear()
 
 
 def _defer_job(ws, offset, splits, n_w, n_b, dw, db, ld=0, cols=0, dw_ptr=None, db_ptr=None):
@@ -1157,7 +1171,7 @@ class _ChainFn(torch.autograd.Function):
 
 def chain_supported(x, linears):
     """True when _ChainFn's kernels cover these layers (D = 128 rows of 16-byte aligned fp32)."""
-    if not x.is_cuda or x.dim() != 2 or x.shape[1] != 128 or x.shape[0] * 128 >= 2 ** 31:
+    if not x.is_cuda or x.dim() != 2 or x.shape[1] != 128 or not rows_fit(x.shape[0], 128):
         return False
     if len(linears) < 1 or len(linears) > CHAIN_MAX_STAGES:
         return False
@@ -1291,7 +1305,7 @@ def featurize_supported(x, env, lin1, lin2):
     if not x.is_cuda or x.dim() != 2 or x.dtype != torch.float32 or x.requires_grad:
         return False
     R, K = x.shape
-    if not (256 < K <= 384 and K % 2 == 0) or R * 384 >= 2 ** 31:
+    if not (256 < K <= 384 and K % 2 == 0) or not rows_fit(R, 384):
         return False
     if env is not None and (env.numel() != R or env.requires_grad):
         return False
@@ -1315,14 +1329,18 @@ class _FeaturizeFn(torch.autograd.Function):
         tf = int(_lib.load().x2g_chain_t_floats(R, 128))
         f32 = dict(dtype=torch.float32, device=dev)
         y = torch.empty(R, 128, **f32)
-        xs_t, z1_t, y1_t, z2_t = (torch.empty(max(n * tf, 1), **f32) for n in (3, 2, 2, 1))
+        # the backward's T-layout operands (8 planes, ~4 KB per row) only when a gradient is wanted
+        grad = any(ctx.needs_input_grad)
+        xs_t, z1_t, y1_t, z2_t = ((torch.empty(max(n * tf, 1), **f32) for n in (3, 2, 2, 1)) if grad
+                                  else (None, None, None, None))
         e = _f32(env.reshape(-1)) if env is not None else None
         W1, W2 = _f32(w1), _f32(w2)
         B1 = _f32(b1) if b1 is not None else None
         B2 = _f32(b2) if b2 is not None else None
         call("x2g_feat_fwd", ptr(x2), ptr(e), R, K, ptr(W1), ptr(B1), ptr(W2), ptr(B2), ptr(y), ptr(xs_t), ptr(z1_t),
              ptr(y1_t), ptr(z2_t), stream_ptr())
-        ctx.save_for_backward(xs_t, z1_t, y1_t, z2_t, W2)
+        if grad:
+            ctx.save_for_backward(xs_t, z1_t, y1_t, z2_t, W2)
         ctx.R, ctx.K, ctx.tf = R, K, tf
         ctx.params = (w1, b1, w2, b2)
         return y
@@ -1430,7 +1448,7 @@ def tiled_wgrad(dy_ts, x_ts, R, weights, biases):
 
 def conv_proj_fused_supported(x, rbf, weights, biases):
     """True when the row-chain style projection kernels (x2g_conv_proj_fwd / _bwd) cover the layer."""
-    if not _CHAIN or not x.is_cuda or x.dim() != 2 or x.shape[1] != 128 or x.shape[0] * 128 >= 2 ** 31:
+    if not _CHAIN or not x.is_cuda or x.dim() != 2 or x.shape[1] != 128 or not rows_fit(x.shape[0], 128):
         return False
     if rbf.dim() != 2 or not 1 <= rbf.shape[1] <= 8 or rbf.shape[0] != x.shape[0]:
         return False
@@ -1587,7 +1605,7 @@ def _projections4(x2, xs, pq, pk, pv, ps):
     R, K = x2.shape
     N = pq[0].shape[0]
     outs = [torch.empty(R, N, dtype=torch.float32, device=x2.device) for _ in range(4)]
-    ok = (K % 4 == 0 and N % 4 == 0 and 8 < K <= 128 and N <= 128 and R * 128 < 2 ** 31
+    ok = (K % 4 == 0 and N % 4 == 0 and 8 < K <= 128 and N <= 128 and rows_fit(R, 128)
           and all(p[0].shape == pq[0].shape for p in (pk, pv, ps)))
     if ok and R > 0:
         srcs = (x2, xs, xs, x2)
@@ -1932,6 +1950,7 @@ class _SmoothL1MeanFn(torch.autograd.Function):
 
 def smooth_l1_loss(pred, target, beta: float = 1.0):
     """torch.nn.functional.smooth_l1_loss(pred, target, beta=beta) (mean) on the device path."""
-    if not pred.is_cuda or pred.shape != target.shape or pred.numel() == 0 or target.requires_grad:
+    if (not pred.is_cuda or pred.shape != target.shape or pred.numel() == 0 or target.requires_grad
+            or beta <= 0):  # beta <= 0 is torch's L1 branch, not compiled
         return torch.nn.functional.smooth_l1_loss(pred, target, beta=beta)
     return _SmoothL1MeanFn.apply(pred, target, beta)
