@@ -32,7 +32,7 @@ import x2gnn  # noqa: E402
 from x2gnn import _lib, ops  # noqa: E402
 from x2gnn._lib import call, ptr, stream_ptr  # noqa: E402
 from x2gnn.data import collate  # noqa: E402
-from x2gnn.dist import shard_by_triplets  # noqa: E402
+from x2gnn.dist import collate_shard, shard_by_triplets  # noqa: E402
 from x2gnn.train import Inference, Trainer  # noqa: E402
 from x2gnn.datasets import ATOMWISE_TARGETS, LABELS, model_for_target  # noqa: E402
 from x2gnn.synth import molecules_from_geometry_file, synthetic_molecules  # noqa: E402
@@ -475,19 +475,18 @@ def main():
         all_mols = molecules_from_geometry_file(AID_GEOM, indices=[i % n_aid for i in range(global_batch)], seed=0)
     else:
         all_mols = synthetic_molecules(global_batch, args.shape, seed=1000)
-    shards = shard_by_triplets([m["triplet_num"] for m in all_mols], world)
-    mols = [all_mols[i] for i in shards[rank]]
-    del all_mols
-    batch = collate(mols).to(dev)
+    mols = [all_mols[i] for i in shard_by_triplets([m["triplet_num"] for m in all_mols], world)[rank]]
+    host_batch, n_local, _ = collate_shard(all_mols, world, rank)
+    batch = host_batch.to(dev)
     # the per-batch host cost a data loader has to hide under the step (side fields, not `value`):
     # collate (PyG Batch.from_data_list restated + the int32 index forms) and the H2D copy, warm
     t_c0 = time.perf_counter()
-    host_batch = collate(mols)
+    host_batch, _, _ = collate_shard(all_mols, world, rank)
     t_c1 = time.perf_counter()
     host_batch.to(dev)
     torch.cuda.synchronize()
     t_c2 = time.perf_counter()
-    del host_batch
+    del host_batch, all_mols
     global_pool = None
     if args.workload == "qm9_allprop":
         model = model_for_target(args.target, CFG, device="cuda").to(dev)  # train_ema.py:41-44
@@ -526,7 +525,7 @@ def main():
         if rank == 0:
             print(json.dumps({"value": round(global_batch * args.steps / t_max, 2),
                               "ms_per_step": round(1e3 * t_max / args.steps, 4), "steps": args.steps,
-                              "final_loss": round(final_loss, 6), "x2g_tune": os.environ.get("X2G_TUNE", "")}),
+                              "final_loss": round(final_loss, 6)}),
                   flush=True)
         if world > 1:
             dist.barrier()

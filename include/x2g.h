@@ -38,8 +38,6 @@ extern "C" {
 #define X2G_EDGE_PER_DST 2     /* edge[R, H*C] indexed by edge_row[E]: one row per destination line node */
 
 int x2g_abi_version(void);
-/* Kernel-variant knobs for A/B measurements (key < 16); returns the previous value. 0 = default. */
-int x2g_tuning(int key, int value);
 const char* x2g_status_string(int status);
 
 /* ---------------------------------------------------------------- line graph (triplets) */

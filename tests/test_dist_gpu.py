@@ -4,7 +4,8 @@ RCCL gradient all-reduce), rehearsed with two ranks on the one GPU of the test b
 Each rank is a fresh spawned process (nothing is exec'd from a GPU-initialised process) running
 ``x2gnn.xgnn_poly`` through ``x2gnn.train.Trainer`` on its shard of one global batch:
 ``dist.shard_by_triplets`` balances the shards by triplet count, so they hold UNEQUAL molecule
-counts; the backward sums weight gradients straight into the flat ``GradBucket`` (grad sinks,
+counts (``dist.collate_shard``: the embedding's per-batch renorm / scale_grad_by_freq counts are
+taken over the global batch, as in the single-device step); the backward sums weight gradients straight into the flat ``GradBucket`` (grad sinks,
 deferred slab sums, the one flat T-layout weight-gradient launch); ``reduce()`` weights each
 rank's bucket by local/global molecule count and SUM-all-reduces it together with the shard's
 loss.  The ranks use gloo (one GPU cannot host two RCCL ranks); the collective's arithmetic is
@@ -49,8 +50,7 @@ def _worker(rank, world, port, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
 
-    from x2gnn.data import collate
-    from x2gnn.dist import shard_by_triplets
+    from x2gnn.dist import collate_shard, shard_by_triplets
     from x2gnn.train import Trainer
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -58,15 +58,16 @@ def _worker(rank, world, port, out_q):
         dev = torch.device("cuda:0")
         torch.cuda.set_device(dev)
         mols = _global_molecules()
-        shards = shard_by_triplets([m["triplet_num"] for m in mols], world)
-        mine = shards[rank]
-        batch = collate([mols[i] for i in mine]).to(dev)
-        tr = Trainer(_model(dev), local_count=len(mine), global_count=len(mols))
+        mine = shard_by_triplets([m["triplet_num"] for m in mols], world)[rank]
+        host, n_local, n_global = collate_shard(mols, world, rank)
+        assert n_local == len(mine) and n_global == len(mols)
+        batch = host.to(dev)
+        tr = Trainer(_model(dev), local_count=n_local, global_count=n_global)
         # the captured step (what bench.py replays): capture (its 3 warm-up passes run eagerly),
         # zero, replay forward+backward, all-reduce
         tr.capture(batch)
         tr.bucket.zero()
-        tr.graphs[0].replay()
+        tr.replay_forward_backward()
         tr.reduce()
         torch.cuda.synchronize()
         graphed = tr.bucket.flat.detach().cpu().numpy().copy()

@@ -539,11 +539,10 @@ def test_flat_adam_matches_torch(cuda, max_norm):
 @pytest.mark.gpu
 @pytest.mark.parametrize("T,out_dim", [(194060, 128), (1000, 128), (37, 128), (0, 128), (1000, 256), (37, 256),
                                        (1000, 64), (37, 32)])
-def test_sbf_project_both_paths_vs_torch(cuda, T, out_dim):
-    """x2g_sbf_project: MFMA narrow-K path (default, out_dim <= 128) and the VALU path
-    (x2g_tuning key 2 = 1; the only path for out_dim 256, e.g. xgnn_poly's default in_channels=256,
-    xgnn.py:16).  T = 37 makes 37*42 floats, not a multiple of 4: the last 16-byte chunk is partial."""
-    from x2gnn import _lib
+def test_sbf_project_vs_torch(cuda, T, out_dim):
+    """x2g_sbf_project: the wave-independent MFMA kernel (out_dim 128 / 64) and the VALU path
+    (out_dim 256, e.g. xgnn_poly's default in_channels=256, xgnn.py:16; and 32).  T = 37 makes 37*42
+    floats, not a multiple of 4: the last 16-byte chunk is partial."""
     from x2gnn._lib import call, ptr, stream_ptr
 
     g = torch.Generator(device=cuda).manual_seed(T + 5 + out_dim)
@@ -551,13 +550,9 @@ def test_sbf_project_both_paths_vs_torch(cuda, T, out_dim):
     w = torch.randn(out_dim, 42, device=cuda, generator=g) / 6.5
     b = torch.randn(out_dim, device=cuda, generator=g)
     ref = (sbf.double() @ w.double().t() + b.double()).float()
-    lib = _lib.load()
-    for knob in (0, 1):
-        prev = lib.x2g_tuning(2, knob)
-        out = torch.full((T, out_dim), float("nan"), device=cuda)
-        call("x2g_sbf_project", ptr(sbf), T, 42, ptr(w), ptr(b), out_dim, ptr(out), stream_ptr())
-        lib.x2g_tuning(2, prev)
-        torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+    out = torch.full((T, out_dim), float("nan"), device=cuda)
+    call("x2g_sbf_project", ptr(sbf), T, 42, ptr(w), ptr(b), out_dim, ptr(out), stream_ptr())
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
 
 
 @pytest.mark.gpu

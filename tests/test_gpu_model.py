@@ -304,12 +304,11 @@ def _dense_cluster(n_atoms=72, seed=5):
 @pytest.mark.parametrize("shape", ["S160", "dense"])
 def test_factorised_sbf_backward_equals_two_pass(cuda, monkeypatch, shape):
     """The folded lin_sbf backward (one destination pass, dS folded per source line node into
-    G[E, 8, D], dW_sbf = sum_s R_s G_s; csrc/attention_fold.inc), in its batched (default) and
-    3-set pipelined (tuning knob 5 = 1) forms, against the two-pass backward with the
+    G[E, 8, D], dW_sbf = sum_s R_s G_s; csrc/attention_fold.inc) against the two-pass backward with the
     materialised d_sbfproj [T, D] and its T-row weight GEMM: same energies, every parameter
     gradient within fp32 reassociation error.  "dense": segments longer than 64 triplets."""
     import x2gnn
-    from x2gnn import _lib, ops
+    from x2gnn import ops
     from x2gnn.data import collate
     from x2gnn.synth import synthetic_molecules
 
@@ -319,21 +318,16 @@ def test_factorised_sbf_backward_equals_two_pass(cuda, monkeypatch, shape):
     calls = []
     real = ops.sbf_radial_wgrad
     monkeypatch.setattr(ops, "sbf_radial_wgrad", lambda *a, **k: calls.append(1) or real(*a, **k))
-    lib = _lib.load()
     runs = []
-    try:
-        for fold, knob in ((True, 0), (True, 1), (False, 0)):
-            monkeypatch.setattr(ops, "_FOLD_SBF", fold)
-            lib.x2g_tuning(5, knob)
-            torch.manual_seed(0)
-            m = x2gnn.xgnn_poly(device="cuda", **cfg).to(cuda)
-            res = m(batch)
-            torch.nn.functional.smooth_l1_loss(res, batch.y).backward()
-            runs.append((res.detach().clone(), {n: p.grad.detach().clone() for n, p in m.named_parameters()
-                                                if p.grad is not None}))
-    finally:
-        lib.x2g_tuning(5, 0)
-    assert len(calls) == 8  # one folded weight gradient per conv layer in each folded run
+    for fold in (True, False):
+        monkeypatch.setattr(ops, "_FOLD_SBF", fold)
+        torch.manual_seed(0)
+        m = x2gnn.xgnn_poly(device="cuda", **cfg).to(cuda)
+        res = m(batch)
+        torch.nn.functional.smooth_l1_loss(res, batch.y).backward()
+        runs.append((res.detach().clone(), {n: p.grad.detach().clone() for n, p in m.named_parameters()
+                                            if p.grad is not None}))
+    assert len(calls) == 4  # one folded weight gradient per conv layer in the folded run
     ref_res, ref_grads = runs[-1]
     for res, grads in runs[:-1]:
         assert torch.equal(res, ref_res)

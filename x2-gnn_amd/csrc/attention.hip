@@ -698,7 +698,7 @@ template <int CPL, int LPH, int MODE, bool PRE>
 void launch_pre(Pass pass, const AttnArgs& a, unsigned blocks, hipStream_t st) {
   switch (pass) {
     case Pass::kFwd:
-      if (PRE && MODE != X2G_EDGE_PER_TRIPLET && tuning(kTuneFold) == 0) {  // batched (default)
+      if (PRE && MODE != X2G_EDGE_PER_TRIPLET) {  // batched: up to 8 triplets' rows in flight per wave
         attn_fwd_batched<CPL, LPH, MODE><<<blocks, 256, 0, st>>>(a.q, a.k, a.v, a.skip, a.edge, a.edge_row, a.sbf,
                                                                  a.rowptr, a.tidx, a.E, a.D, a.H, a.sqrt_c, a.out,
                                                                  a.alpha_out, a.smax_out, a.sden_out);
@@ -864,7 +864,7 @@ constexpr int kSPQ = 3;  // 16-wide contraction groups (K = 42 -> 48, zero-padde
 template <int NOB>
 __global__ void __launch_bounds__(256) sbf_project_waves(const float* __restrict__ sbf, const float* __restrict__ w,
                                                          const float* __restrict__ b, int64_t T,
-                                                         float* __restrict__ out, int dbg) {
+                                                         float* __restrict__ out) {
   typedef float f4t __attribute__((ext_vector_type(4)));
   __shared__ f4t Wl[NOB * kSPQ * 64];  // [ob][q][lane]: W[16ob + i][16q + 4g .. +3]
   __shared__ f4t Bl[NOB * 4];          // [ob][g]: b[16ob + 4g .. +3]
@@ -918,7 +918,7 @@ __global__ void __launch_bounds__(256) sbf_project_waves(const float* __restrict
 #pragma unroll
       for (int j = 0; j < HB; ++j) acc[j] = Bl[(h0 + j) * 4 + g];
 #pragma unroll
-      for (int q = 0; q < ((dbg & 1) ? 0 : kSPQ); ++q) {
+      for (int q = 0; q < kSPQ; ++q) {
         f4t a[HB];
 #pragma unroll
         for (int j = 0; j < HB; ++j) a[j] = Wl[((h0 + j) * kSPQ + q) * 64 + lane];
@@ -927,8 +927,7 @@ __global__ void __launch_bounds__(256) sbf_project_waves(const float* __restrict
 #pragma unroll
           for (int j = 0; j < HB; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][e], B[q][e], acc[j], 0, 0, 0);
       }
-      if (dbg & 1) acc[0] += B[0] + B[1] + B[2];  // (ablation: keep the loads live)
-      if (r < T && !(dbg & 2)) {
+      if (r < T) {
 #pragma unroll
         for (int j = 0; j < HB; ++j) *reinterpret_cast<f4t*>(o + 16 * (h0 + j)) = acc[j];
       }
@@ -947,24 +946,22 @@ X2G_API int x2g_sbf_project(const float* sbf, int64_t T, int32_t sbf_dim, const 
   if (!sbf || !w_sbf || !b_sbf || !sbfproj) return X2G_EINVAL;
   hipStream_t st = as_stream(stream);
   // wave-independent f32 MFMA kernel (out_dim 128 or 64, 8-byte aligned sbf rows, 16-byte aligned
-  // output rows); x2g_tuning key 2 = 2 selects the tile-staged dense kernel
+  // output rows)
   if ((out_dim == 128 || out_dim == 64) && reinterpret_cast<uintptr_t>(sbf) % 8 == 0 &&
-      reinterpret_cast<uintptr_t>(sbfproj) % 16 == 0 && tuning(kTuneAttn) == 0) {
+      reinterpret_cast<uintptr_t>(sbfproj) % 16 == 0) {
     const int64_t nblk = (T + 15) / 16;
     int64_t want = (nblk + 3) / 4;
     want = want < 1280 ? want : 1280;  // ~5 workgroups per CU, each wave looping over its blocks
-    const int dbg = tuning(kTuneSprojDbg);  // timing ablations only (1 no MFMA, 2 no stores)
     if (out_dim == 128)
-      sbf_project_waves<8><<<static_cast<unsigned>(want), 256, 0, st>>>(sbf, w_sbf, b_sbf, T, sbfproj, dbg);
+      sbf_project_waves<8><<<static_cast<unsigned>(want), 256, 0, st>>>(sbf, w_sbf, b_sbf, T, sbfproj);
     else
-      sbf_project_waves<4><<<static_cast<unsigned>(want), 256, 0, st>>>(sbf, w_sbf, b_sbf, T, sbfproj, dbg);
+      sbf_project_waves<4><<<static_cast<unsigned>(want), 256, 0, st>>>(sbf, w_sbf, b_sbf, T, sbfproj);
     return last_launch_status();
   }
   // f32 MFMA, tiles staged through LDS (dense.hip): that kernel covers N <= 128 output columns
   // and addresses rows with 32-bit offsets; wider projections take the per-row kernel below
   if (out_dim % 4 == 0 && out_dim <= 128 && T * 128 * 4 < (int64_t(1) << 31) &&
-      reinterpret_cast<uintptr_t>(sbf) % 16 == 0 && reinterpret_cast<uintptr_t>(sbfproj) % 16 == 0 &&
-      (tuning(kTuneAttn) == 0 || tuning(kTuneAttn) == 2))
+      reinterpret_cast<uintptr_t>(sbf) % 16 == 0 && reinterpret_cast<uintptr_t>(sbfproj) % 16 == 0)
     return dense_fwd_narrow_launch(sbf, w_sbf, b_sbf, nullptr, T, kS, out_dim, 0, sbfproj, nullptr, st);
   int64_t want = (T + kAttnWaves - 1) / kAttnWaves;
   const unsigned blocks = static_cast<unsigned>(want < 4096 ? want : 4096);
@@ -996,7 +993,7 @@ struct FoldArgs {
 
 template <int CPL, int LPH>
 void fold_launch_mode(bool dst, const FoldArgs& a, unsigned blocks, hipStream_t st) {
-  if (dst && tuning(kTuneFold) == 0) {  // batched destination pass (default)
+  if (dst) {  // destination-major pass
     if (a.mode == X2G_EDGE_PER_DST)
       attn_bwd_dst_g_batched<CPL, LPH, X2G_EDGE_PER_DST><<<blocks, 256, 0, st>>>(
           a.q, a.k, a.v, a.edge, a.edge_row, a.sp, a.rowptr, a.tidx, a.alpha, a.smax, a.sden, a.dout, a.E, a.D, a.H,
@@ -1005,16 +1002,7 @@ void fold_launch_mode(bool dst, const FoldArgs& a, unsigned blocks, hipStream_t 
       attn_bwd_dst_g_batched<CPL, LPH, X2G_EDGE_NONE><<<blocks, 256, 0, st>>>(
           a.q, a.k, a.v, a.edge, a.edge_row, a.sp, a.rowptr, a.tidx, a.alpha, a.smax, a.sden, a.dout, a.E, a.D, a.H,
           a.sqrt_c, a.dq, a.d_edge, a.g_out, a.prob_out, a.rho_out);
-  } else if (dst) {
-    if (a.mode == X2G_EDGE_PER_DST)
-      attn_bwd_dst_g_kernel<CPL, LPH, X2G_EDGE_PER_DST><<<blocks, 256, 0, st>>>(
-          a.q, a.k, a.v, a.edge, a.edge_row, a.sp, a.rowptr, a.tidx, a.alpha, a.smax, a.sden, a.dout, a.E, a.D, a.H,
-          a.sqrt_c, a.dq, a.d_edge, a.g_out, a.prob_out, a.rho_out);
-    else
-      attn_bwd_dst_g_kernel<CPL, LPH, X2G_EDGE_NONE><<<blocks, 256, 0, st>>>(
-          a.q, a.k, a.v, a.edge, a.edge_row, a.sp, a.rowptr, a.tidx, a.alpha, a.smax, a.sden, a.dout, a.E, a.D, a.H,
-          a.sqrt_c, a.dq, a.d_edge, a.g_out, a.prob_out, a.rho_out);
-  } else if (tuning(kTuneFold) == 0) {  // batched source pass (default); knob 5 = 1: the 3-set pipeline
+  } else {  // source-major pass
     const int C = a.D / a.H;
     if (a.mode == X2G_EDGE_PER_DST)
       attn_bwd_src_fold_batched<CPL, true><<<blocks, 256, 0, st>>>(
@@ -1024,15 +1012,6 @@ void fold_launch_mode(bool dst, const FoldArgs& a, unsigned blocks, hipStream_t 
       attn_bwd_src_fold_batched<CPL, false><<<blocks, 256, 0, st>>>(
           a.q, a.v, a.edge, a.edge_row, a.edge_rows, a.sp, a.y, a.rowptr, a.tidx, a.tdst, a.prob, a.rho_in, a.g_in,
           a.dout, a.E, a.D, a.H, C, a.dk, a.dv, a.gfold);
-  } else {
-    if (a.mode == X2G_EDGE_PER_DST)
-      attn_bwd_src_fold_kernel<CPL, LPH, true><<<blocks, 256, 0, st>>>(
-          a.q, a.v, a.edge, a.edge_row, a.edge_rows, a.sp, a.y, a.rowptr, a.tidx, a.tdst, a.prob, a.rho_in, a.g_in,
-          a.dout, a.E, a.D, a.H, a.sqrt_c, a.dk, a.dv, a.gfold);
-    else
-      attn_bwd_src_fold_kernel<CPL, LPH, false><<<blocks, 256, 0, st>>>(
-          a.q, a.v, a.edge, a.edge_row, a.edge_rows, a.sp, a.y, a.rowptr, a.tidx, a.tdst, a.prob, a.rho_in, a.g_in,
-          a.dout, a.E, a.D, a.H, a.sqrt_c, a.dk, a.dv, a.gfold);
   }
 }
 

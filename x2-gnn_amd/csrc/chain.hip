@@ -34,7 +34,6 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 constexpr int kCD = 128;                // compiled width
 constexpr int kCWaves = 8;              // 512 threads: two waves per SIMD, one 16-row tile each
 constexpr int kCThreads = kCWaves * 64;
-constexpr int kMChunks = kCD * kCD / 4;  // 16-byte chunks per weight image (64 KB)
 
 struct ChainFwdArgs {
   const float* x;
@@ -43,7 +42,6 @@ struct ChainFwdArgs {
   int64_t tf;     // floats per T-layout tensor
   int64_t R;
   int n;
-  int dbg;  // diagnostic ablations (x2g_tuning key 7 bits, timing only: results are wrong when set)
   x2g_chain_stage st[X2G_CHAIN_MAX_STAGES];
 };
 
@@ -61,73 +59,7 @@ struct ChainBwdArgs {
 
 __device__ __forceinline__ f4 zero4() { return f4{0.f, 0.f, 0.f, 0.f}; }
 
-// weight image staging: global -> registers (8 chunks per thread) ...
-template <bool TRANS>
-__device__ __forceinline__ void load_w(const float* __restrict__ W, f4 (&pre)[8]) {
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    if (!TRANS) {  // chunk q = row n, 16-byte column chunk c of W
-      pre[u] = reinterpret_cast<const f4*>(W)[tid + kCThreads * u];
-    } else {  // M[k][4c..4c+3] = W[4c..4c+3][k]: one wave reads 64 consecutive k of a W row
-      const int k = tid & 127, c = (tid >> 7) + 4 * u;
-      const float* p = W + 4 * c * kCD + k;
-      pre[u] = f4{p[0], p[kCD], p[2 * kCD], p[3 * kCD]};
-    }
-  }
-}
-
-// ... -> the swizzled LDS image
-template <bool TRANS>
-__device__ __forceinline__ void store_w(f4* __restrict__ Ms, const f4 (&pre)[8]) {
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    int n, c;
-    if (!TRANS) {
-      const int q = tid + kCThreads * u;
-      n = q >> 5;
-      c = q & 31;
-    } else {
-      n = tid & 127;
-      c = (tid >> 7) + 4 * u;
-    }
-    Ms[n * 32 + (c ^ (n & 15))] = pre[u];
-  }
-}
-
-// acc[bp] = rows 16bp..16bp+15 of M times the tile (see the header comment).  The A operands of
-// k-group b + 1 (eight ds_read_b128) are issued before the 32 MFMAs of group b.
-__device__ __forceinline__ void chain_gemm(const f4* __restrict__ Ms, const f4 (&x)[8], f4 (&acc)[8], int nl,
-                                           int g) {
-#pragma unroll
-  for (int bp = 0; bp < 8; ++bp) acc[bp] = zero4();
-  f4 a[2][8];
-#pragma unroll
-  for (int bp = 0; bp < 8; ++bp) a[0][bp] = Ms[(16 * bp + nl) * 32 + (g ^ nl)];
-#pragma unroll
-  for (int b = 0; b < 8; ++b) {
-    const int cur = b & 1;
-    if (b + 1 < 8) {
-#pragma unroll
-      for (int bp = 0; bp < 8; ++bp) a[cur ^ 1][bp] = Ms[(16 * bp + nl) * 32 + ((4 * (b + 1) + g) ^ nl)];
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int bp = 0; bp < 8; ++bp)
-        acc[bp] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][bp][e], x[b][e], acc[bp], 0, 0, 0);
-  }
-}
-
-__device__ __forceinline__ float silu_f(float z) { return z / (1.0f + expf(-z)); }
-
-__device__ __forceinline__ float silu_grad_f(float z) {
-  const float s = 1.0f / (1.0f + expf(-z));
-  return s * (1.0f + z * (1.0f - s));
-}
-
-// The v2 epilogues use the hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32: ~1 ulp each) instead
+// The epilogues use the hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32: ~1 ulp each) instead
 // of libm expf and IEEE division (~25 VALU instructions per element): the epilogue runs between
 // barriers with no MFMA to hide behind, and the exact forms cost ~1.7 us per stage at config 2.
 // sigmoid(z) = rcp(1 + 2^(-z log2 e)); z -> -inf gives 0, z -> +inf gives 1, NaN stays NaN.
@@ -140,158 +72,10 @@ __device__ __forceinline__ float silu_grad_fast(float z) {
   return s * (1.0f + z * (1.0f - s));
 }
 
-// row r of the tile, float4 b of the lane's row layout: clamped address + 0/1 mask (the loads
-// stay unconditional so all eight are in flight together)
-__device__ __forceinline__ void load_rows(const float* __restrict__ P, int rc, bool rok, int g, f4 (&v)[8]) {
-  const float m = rok ? 1.0f : 0.0f;
-#pragma unroll
-  for (int b = 0; b < 8; ++b) v[b] = *reinterpret_cast<const f4*>(P + rc * kCD + 16 * b + 4 * g) * m;
-}
-
-__device__ __forceinline__ void store_rows(float* __restrict__ P, int row, bool rok, int g, const f4 (&v)[8]) {
-  if (!rok) return;
-#pragma unroll
-  for (int b = 0; b < 8; ++b) *reinterpret_cast<f4*>(P + row * kCD + 16 * b + 4 * g) = v[b];
-}
-
-__global__ void __launch_bounds__(kCThreads, 1) chain_fwd_kernel(const ChainFwdArgs a) {
-  __shared__ f4 Ms[2][kMChunks];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int rl = lane & 15, g = lane >> 4;
-  const int64_t ntiles = (a.R + 15) / 16;
-  const int64_t groups = (ntiles + kCWaves - 1) / kCWaves;
-  const int n = a.n;
-  f4 pre[8];
-  int buf = 0;
-  if (static_cast<int64_t>(blockIdx.x) < groups) {
-    load_w<false>(a.st[0].w, pre);
-    store_w<false>(Ms[0], pre);
-  }
-  __syncthreads();
-  for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
-    const int64_t tile = grp * kCWaves + wave;
-    const bool active = tile < ntiles;  // wave-uniform
-    const int row = static_cast<int>(tile) * 16 + rl;
-    const bool rok = active && row < a.R;
-    const int rc = rok ? row : 0;
-    f4 x[8], held[8];
-    load_rows(a.x, rc, rok, g, x);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) held[b] = zero4();
-    for (int s = 0; s < n; ++s) {
-      const x2g_chain_stage& S = a.st[s];
-      const int fl = S.flags;
-      const bool more = (s + 1 < n || grp + gridDim.x < groups) && !(a.dbg & 1);
-      if (more) load_w<false>(s + 1 < n ? a.st[s + 1].w : a.st[0].w, pre);
-      // the held registers carry either a ResidualLayer input (HOLD) or the external residual
-      // (RES_EXT loads it here, during the MFMAs; the host rejects chains that would need both)
-      if (fl & X2G_CHAIN_RES_EXT) load_rows(a.res, rc, rok, g, held);
-      if (fl & X2G_CHAIN_HOLD) {
-#pragma unroll
-        for (int b = 0; b < 8; ++b) held[b] = x[b];
-      }
-      f4 acc[8];
-      if (active) {
-        chain_gemm(Ms[buf], x, acc, rl, g);
-#pragma unroll
-        for (int bp = 0; bp < 8; ++bp) {
-          f4 z = acc[bp];
-          if (S.b) z += *reinterpret_cast<const f4*>(S.b + 16 * bp + 4 * g);
-          if (rok && S.z && !(a.dbg & 2)) *reinterpret_cast<f4*>(S.z + row * kCD + 16 * bp + 4 * g) = z;
-          f4 y = z;
-          if ((fl & X2G_CHAIN_SILU) && !(a.dbg & 4)) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) y[e] = silu_f(z[e]);
-          }
-          if (fl & (X2G_CHAIN_RES_HELD | X2G_CHAIN_RES_EXT)) y += held[bp];
-          x[bp] = y;
-        }
-        if (S.y && !(a.dbg & 2)) store_rows(S.y, row, rok, g, x);
-      }
-      if (more) store_w<false>(Ms[buf ^ 1], pre);
-      if (!(a.dbg & 8)) {
-        __syncthreads();  // every wave is past stage s: its image may be overwritten next stage
-        buf ^= 1;
-      }
-    }
-  }
-}
-
-__global__ void __launch_bounds__(kCThreads, 1) chain_bwd_kernel(const ChainBwdArgs a) {
-  __shared__ f4 Ms[2][kMChunks];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int rl = lane & 15, g = lane >> 4;
-  const int64_t ntiles = (a.R + 15) / 16;
-  const int64_t groups = (ntiles + kCWaves - 1) / kCWaves;
-  const int n = a.n;
-  f4 pre[8];
-  int buf = 0;
-  if (static_cast<int64_t>(blockIdx.x) < groups) {
-    load_w<true>(a.st[n - 1].w, pre);
-    store_w<true>(Ms[0], pre);
-  }
-  __syncthreads();
-  for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
-    const int64_t tile = grp * kCWaves + wave;
-    const bool active = tile < ntiles;
-    const int row = static_cast<int>(tile) * 16 + rl;
-    const bool rok = active && row < a.R;
-    const int rc = rok ? row : 0;
-    f4 gcur[8], dh[8], zc[8];
-    load_rows(a.dy, rc, rok, g, gcur);
-    if (a.dy_add) {
-      f4 t[8];
-      load_rows(a.dy_add, rc, rok, g, t);
-#pragma unroll
-      for (int b = 0; b < 8; ++b) gcur[b] += t[b];
-    }
-    if (a.st[n - 1].flags & X2G_CHAIN_SILU) load_rows(a.st[n - 1].z, rc, rok, g, zc);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) dh[b] = zero4();
-    for (int s = n - 1; s >= 0; --s) {
-      const x2g_chain_bwd_stage& S = a.st[s];
-      const int fl = S.flags;
-      const bool more = s > 0 || grp + gridDim.x < groups;
-      if (more) load_w<true>(s > 0 ? a.st[s - 1].w : a.st[n - 1].w, pre);
-      if (active) {
-        if (fl & X2G_CHAIN_RES_HELD) {
-#pragma unroll
-          for (int b = 0; b < 8; ++b) dh[b] += gcur[b];
-        }
-        if ((fl & X2G_CHAIN_RES_EXT) && a.dres) store_rows(a.dres, row, rok, g, gcur);
-        if (fl & X2G_CHAIN_SILU) {  // dz = g * SiLU'(z)
-#pragma unroll
-          for (int b = 0; b < 8; ++b)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) gcur[b][e] *= silu_grad_f(zc[b][e]);
-        }
-        if (S.dz) store_rows(S.dz, row, rok, g, gcur);
-        // the previous stage's z flies during this stage's MFMAs (zc is dead from here)
-        if (s > 0 && (a.st[s - 1].flags & X2G_CHAIN_SILU)) load_rows(a.st[s - 1].z, rc, rok, g, zc);
-        f4 acc[8];
-        chain_gemm(Ms[buf], gcur, acc, rl, g);
-        if (fl & X2G_CHAIN_HOLD) {  // in_s was also the held residual
-#pragma unroll
-          for (int b = 0; b < 8; ++b) {
-            acc[b] += dh[b];
-            dh[b] = zero4();
-          }
-        }
-#pragma unroll
-        for (int b = 0; b < 8; ++b) gcur[b] = acc[b];
-      }
-      if (more) store_w<true>(Ms[buf ^ 1], pre);
-      __syncthreads();
-      buf ^= 1;
-    }
-    if (active) store_rows(a.dx, row, rok, g, gcur);
-  }
-}
-
-// ------------------------------------------------------------------------- v2: rows in LDS
-// The register-tile kernels above give every wave a whole 16-row tile: at E ~ 21k rows that is
-// 1317 tiles on 165 CUs, two per SIMD (a third of the chip idle), and the stage's stores and SiLU
-// run in lock-step on every wave between barriers.  v2 instead gives each workgroup (one per CU,
+// ------------------------------------------------------------------------- rows in LDS
+// A register-tile design (every wave a whole 16-row tile: at E ~ 21k rows 1317 tiles on 165 CUs,
+// two per SIMD, a third of the chip idle, stores and SiLU in lock-step between barriers; round 1)
+// was replaced by this one: each workgroup (one per CU,
 // 8 waves) a contiguous range of <= 96 rows (E / 256 ~ 82 rows at config 2: every CU busy, at most
 // 6 16-row blocks each) held in LDS as a swizzled [96][128] image, and each wave a 16-feature
 // slice of every stage's output: wave w computes out[:, 16w .. 16w+15] for all of the range's row
@@ -457,86 +241,7 @@ __device__ __forceinline__ void chunk_rows(int64_t ch, int64_t nch, int64_t nblk
   nrows = static_cast<int>(e - b0 * 16);
 }
 
-__global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v2(const ChainFwdArgs a) {
-  __shared__ f4 img[3][kV2Img];  // two ping-pong stage images + the external residual rows
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int rl = lane & 15, g = lane >> 4;
-  const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
-  const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
-  const int n = a.n;
-  const int64_t wt_groups = G < 8 ? G : 8;
-  for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
-    int r0, nrows;
-    chunk_rows(ch, nch, nblk, a.R, r0, nrows);
-    __syncthreads();  // the previous chunk's images are no longer read
-    stage_rows(img[0], a.x, nullptr, r0, nrows);
-    if (a.res) stage_rows(img[2], a.res, nullptr, r0, nrows);
-    f4 A[8], held[kV2RB];
-    load_slice<false>(a.st[0].w, w, rl, g, A);
-#pragma unroll
-    for (int rb = 0; rb < kV2RB; ++rb) held[rb] = zero4();
-    int cur = 0;
-    __syncthreads();
-    if (a.in_t) {  // the chain input's T copy (later stage inputs: from the stage epilogues)
-      f4 xs[kV2RB];
-#pragma unroll
-      for (int rb = 0; rb < kV2RB; ++rb) xs[rb] = img[0][ipos(16 * rb + rl, 4 * w + g)];
-      store_t_slice(a.in_t, xs, r0, nrows, w, rl, g);
-    }
-    for (int s = 0; s < n; ++s) {
-      const x2g_chain_stage& S = a.st[s];
-      const int fl = S.flags;
-      f4 An[8];
-      load_slice<false>(a.st[s + 1 < n ? s + 1 : 0].w, w, rl, g, An);
-      const f4 bias = bload4(rsrc(S.b ? S.b : S.w), 4 * (16 * w + 4 * g), 0) * (S.b ? 1.0f : 0.0f);
-      if (S.wt && ch < wt_groups) {  // W^T for the backward from the waves' slices (rows 16b + 4g + e,
-        // cols 16w + rl), the 8 row groups b spread over the first workgroups
-#pragma unroll
-        for (int b = 0; b < 8; ++b)
-          if (b % wt_groups == ch)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) S.wt[(16 * b + 4 * g + e) * kCD + 16 * w + rl] = A[b][e];
-      }
-      const f4* in = img[cur];
-      if (fl & (X2G_CHAIN_HOLD | X2G_CHAIN_RES_EXT)) {  // the residual this stage or a later one adds
-        const f4* src = (fl & X2G_CHAIN_HOLD) ? in : img[2];
-#pragma unroll
-        for (int rb = 0; rb < kV2RB; ++rb) held[rb] = src[ipos(16 * rb + rl, 4 * w + g)];
-      }
-      f4 acc[kV2RB];
-      if (!(a.dbg & 16)) {
-        slice_gemm(in, A, acc, rl, g);
-      } else {
-#pragma unroll
-        for (int rb = 0; rb < kV2RB; ++rb) acc[rb] = in[ipos(16 * rb + rl, 4 * w + g)] + A[rb];
-      }
-      f4* out = img[cur ^ 1];
-#pragma unroll
-      for (int rb = 0; rb < kV2RB; ++rb) {
-        const int r = 16 * rb + rl;
-        const f4 z = acc[rb] + bias;
-        if (S.z && r < nrows && !(a.dbg & 2)) *reinterpret_cast<f4*>(S.z + (r0 + r) * kCD + 16 * w + 4 * g) = z;
-        f4 y = z;
-        if ((fl & X2G_CHAIN_SILU) && !(a.dbg & 4)) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) y[e] = silu_fast(z[e]);
-        }
-        if (fl & (X2G_CHAIN_RES_HELD | X2G_CHAIN_RES_EXT)) y += held[rb];
-        out[ipos(r, 4 * w + g)] = y;
-        acc[rb] = y;
-      }
-      if (a.in_t && s + 1 < n) store_t_slice(a.in_t + (s + 1) * a.tf, acc, r0, nrows, w, rl, g);
-      pin(An);
-      if (!(a.dbg & 8)) __syncthreads();  // the stage output image is complete and the input image fully read
-      if (S.y && !(a.dbg & 2)) store_img(S.y, out, r0, nrows);
-      cur ^= 1;
-#pragma unroll
-      for (int b = 0; b < 8; ++b) A[b] = An[b];
-    }
-  }
-}
-
-// ---- v3 (x2g_tuning key 6 = 3; 2 selects v2): v2 with a branch-free epilogue
+// ---- forward building blocks (the v3 design, kept as v4's parts): a branch-free epilogue
 // interleaved with the MFMAs.  The 6 row blocks are computed in thirds; third t's product is
 // scheduled together with third t-1's epilogue (SiLU, residual, LDS write, z and T-layout stores)
 // through sched_group_barrier, so the transcendental / store work runs in the MFMA shadow instead
@@ -622,82 +327,7 @@ __device__ __forceinline__ void interleave_epi_sched() {
   }
 }
 
-__global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v3(const ChainFwdArgs a) {
-  __shared__ f4 img[3][kV2Img];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int rl = lane & 15, g = lane >> 4;
-  const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
-  const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
-  const int n = a.n;
-  const int64_t wt_groups = G < 8 ? G : 8;
-  for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
-    int r0, nrows;
-    chunk_rows(ch, nch, nblk, a.R, r0, nrows);
-    __syncthreads();
-    stage_rows(img[0], a.x, nullptr, r0, nrows);
-    if (a.res) stage_rows(img[2], a.res, nullptr, r0, nrows);
-    f4 A[8], held[kV2RB];
-    load_slice<false>(a.st[0].w, w, rl, g, A);
-#pragma unroll
-    for (int rb = 0; rb < kV2RB; ++rb) held[rb] = zero4();
-    int cur = 0;
-    __syncthreads();
-    if (a.in_t) {
-      f4 xs[kV2RB];
-#pragma unroll
-      for (int rb = 0; rb < kV2RB; ++rb) xs[rb] = img[0][ipos(16 * rb + rl, 4 * w + g)];
-      store_t_slice(a.in_t, xs, r0, nrows, w, rl, g);
-    }
-    for (int s = 0; s < n; ++s) {
-      const x2g_chain_stage& S = a.st[s];
-      const int fl = S.flags;
-      f4 An[8];
-      load_slice<false>(a.st[s + 1 < n ? s + 1 : 0].w, w, rl, g, An);
-      const f4 bias = bload4(rsrc(S.b ? S.b : S.w), 4 * (16 * w + 4 * g), 0) * (S.b ? 1.0f : 0.0f);
-      if (S.wt && ch < wt_groups) {
-#pragma unroll
-        for (int b = 0; b < 8; ++b)
-          if (b % wt_groups == ch)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) S.wt[(16 * b + 4 * g + e) * kCD + 16 * w + rl] = A[b][e];
-      }
-      const f4* in = img[cur];
-      if (fl & (X2G_CHAIN_HOLD | X2G_CHAIN_RES_EXT)) {
-        const f4* src = (fl & X2G_CHAIN_HOLD) ? in : img[2];
-#pragma unroll
-        for (int rb = 0; rb < kV2RB; ++rb) held[rb] = src[ipos(16 * rb + rl, 4 * w + g)];
-      }
-      const float silu_m = (fl & X2G_CHAIN_SILU) ? 1.0f : 0.0f;
-      const float res_m = (fl & (X2G_CHAIN_RES_HELD | X2G_CHAIN_RES_EXT)) ? 1.0f : 0.0f;
-      const rsrc_t zr = rsrc_n(S.z ? S.z : S.w, a.R * kCD * 4, S.z != nullptr);
-      const bool t_on = a.in_t && s + 1 < n;
-      const rsrc_t tr = rsrc_n(t_on ? a.in_t + (s + 1) * a.tf : S.w, a.tf * 4, t_on);
-      f4* out = img[cur ^ 1];
-      f4 acc[kV2RB];
-      // three thirds of two row blocks: third t's product runs in the MFMA shadow of third t-1's
-      // epilogue (per k-group: its 2 LDS reads, then 8 MFMAs each followed by a slice of the epilogue)
-      half_gemm<0, 2>(in, A, acc, rl, g);
-      __builtin_amdgcn_sched_barrier(0);
-      half_gemm<2, 4>(in, A, acc, rl, g);
-      half_epi<0, 2>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
-      interleave_epi_sched();
-      __builtin_amdgcn_sched_barrier(0);
-      half_gemm<4, 6>(in, A, acc, rl, g);
-      half_epi<2, 4>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
-      interleave_epi_sched();
-      __builtin_amdgcn_sched_barrier(0);
-      half_epi<4, 6>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
-      pin(An);
-      __syncthreads();
-      if (S.y) store_img(S.y, out, r0, nrows);
-      cur ^= 1;
-#pragma unroll
-      for (int b = 0; b < 8; ++b) A[b] = An[b];
-    }
-  }
-}
-
-// ---- v4 (the default; x2g_tuning key 6 = 3 selects v3): v3 with the product's LDS reads
+// ---- forward v4 (the shipped kernel): the v3 design with the product's LDS reads
 // software-pipelined.  PMC on v3 (SQ_VALU_MFMA_BUSY_CYCLES: the matrix pipe busy 46 % of the kernel
 // at 2.3 GHz) and its ISA showed
 // each k-group's two B fragments read right before that group's 8 MFMAs, so every group waited out
@@ -843,110 +473,7 @@ __global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4_batch(const ChainFw
   chain_fwd_v4_run(b.a[blockIdx.y]);
 }
 
-// Backward: img[p] holds dz_s (the product's B operand); the product's output slice is the
-// gradient of out_{s-1} at the wave's 16 features, so stage s-1's elementwise part (held /
-// external residual gradients, dz_{s-1} = g * SiLU'(z_{s-1})) runs on it in registers and writes
-// dz_{s-1} into the other image: one barrier per stage.
-__global__ void __launch_bounds__(kCThreads, 1) chain_bwd_v2(const ChainBwdArgs a) {
-  __shared__ f4 img[2][kV2Img];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int rl = lane & 15, g = lane >> 4;
-  const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
-  const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
-  const int n = a.n;
-  const int col = 16 * w + 4 * g;
-  for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
-    int r0, nrows;
-    chunk_rows(ch, nch, nblk, a.R, r0, nrows);
-    f4 A[8], dh[kV2RB], zc[kV2RB], gs[kV2RB];
-    // the stage's saved z at the wave's slice (rows clamped; dy when the stage has no SiLU: unused)
-    auto load_z = [&](int s) {
-      const rsrc_t zr = rsrc((a.st[s].flags & X2G_CHAIN_SILU) ? a.st[s].z : a.dy);
-#pragma unroll
-      for (int rb = 0; rb < kV2RB; ++rb) {
-        const int r = 16 * rb + rl;
-        zc[rb] = bload4(zr, 4 * ((r0 + (r < nrows ? r : 0)) * kCD + col), 0);
-      }
-    };
-    auto load_wslice = [&](int s, f4 (&dst)[8]) {  // W^T rows 16w + rl: contiguous when wt is given
-      if (a.st[s].wt)
-        load_slice<false>(a.st[s].wt, w, rl, g, dst);
-      else
-        load_slice<true>(a.st[s].w, w, rl, g, dst);
-    };
-    load_wslice(n - 1, A);
-    load_z(n - 1);
-    {
-      const rsrc_t yr = rsrc(a.dy), ar = rsrc(a.dy_add ? a.dy_add : a.dy);
-      const float am = a.dy_add ? 1.0f : 0.0f;
-#pragma unroll
-      for (int rb = 0; rb < kV2RB; ++rb) {
-        const int r = 16 * rb + rl;
-        const int vo = 4 * ((r0 + (r < nrows ? r : 0)) * kCD + col);
-        gs[rb] = bload4(yr, vo, 0) + bload4(ar, vo, 0) * am;
-        dh[rb] = zero4();
-      }
-    }
-    int p = 0;
-    __syncthreads();  // the previous chunk's images are no longer read
-    // elementwise part of stage s on the wave's slice g = dL/d out_s: residual gradients, dz
-    auto elementwise = [&](int s) {
-      const x2g_chain_bwd_stage& S = a.st[s];
-      const int fl = S.flags;
-#pragma unroll
-      for (int rb = 0; rb < kV2RB; ++rb) {
-        const int r = 16 * rb + rl;
-        const bool ok = r < nrows;
-        if (fl & X2G_CHAIN_RES_HELD) dh[rb] += gs[rb];
-        if ((fl & X2G_CHAIN_RES_EXT) && a.dres && ok) {
-          f4* dr = reinterpret_cast<f4*>(a.dres + (r0 + r) * kCD + col);
-          *dr = (fl & X2G_CHAIN_RES_ACCUM) ? *dr + gs[rb] : gs[rb];
-        }
-        f4 dz = gs[rb];
-        if (fl & X2G_CHAIN_SILU) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) dz[e] *= silu_grad_fast(zc[rb][e]);
-        }
-        if (S.dz && ok) *reinterpret_cast<f4*>(S.dz + (r0 + r) * kCD + col) = dz;
-        img[p][ipos(r, 4 * w + g)] = dz;
-        gs[rb] = dz;
-      }
-      if (a.dz_t) store_t_slice(a.dz_t + s * a.tf, gs, r0, nrows, w, rl, g);
-    };
-    elementwise(n - 1);
-    __syncthreads();
-    for (int s = n - 1; s >= 0; --s) {
-      f4 An[8];
-      load_wslice(s > 0 ? s - 1 : n - 1, An);
-      load_z(s > 0 ? s - 1 : 0);  // consumed by stage s-1's elementwise part after this product
-      f4 acc[kV2RB];
-      slice_gemm(img[p], A, acc, rl, g);  // dL/d out_{s-1} = dz_s W_s at the wave's slice
-      const bool hold = a.st[s].flags & X2G_CHAIN_HOLD;
-#pragma unroll
-      for (int rb = 0; rb < kV2RB; ++rb) {
-        gs[rb] = acc[rb];
-        if (hold) {  // in_s was also the held residual
-          gs[rb] += dh[rb];
-          dh[rb] = zero4();
-        }
-      }
-      p ^= 1;
-      if (s > 0) {
-        elementwise(s - 1);
-      } else {
-#pragma unroll
-        for (int rb = 0; rb < kV2RB; ++rb) img[p][ipos(16 * rb + rl, 4 * w + g)] = gs[rb];
-      }
-      pin(An);
-      __syncthreads();
-#pragma unroll
-      for (int b = 0; b < 8; ++b) A[b] = An[b];
-    }
-    store_img(a.dx, img[p], r0, nrows);
-  }
-}
-
-// ---- backward v3 (the default; x2g_tuning key 6 = 2 selects v2): v2 with stage s-1's elementwise
+// ---- backward v3 (the shipped kernel): the v2 design with stage s-1's elementwise
 // part (residual gradients, dz = g SiLU'(z), the dz stores, the T-layout copy) computed per third of
 // the row blocks and scheduled into the next third's MFMAs, branch-free as the forward v3.
 template <int RB0, int RB1>
@@ -1212,7 +739,7 @@ struct ChainWgradArgs {
 // product; raw s_barrier with counted vmcnt waits so the in-flight copies survive the barriers.
 // One call reduces tiles [t0, t1) of one job into a slab (dW rows 16w + 4g + e, columns 16bk + rl).
 template <int NB, bool SPREAD = true>  // NB LDS buffers: NB - 1 steps in flight ahead of the product;
-// SPREAD: the bias column sums over all eight waves (else waves 0-1 only, X2G_TUNE 12=1)
+// SPREAD: the bias column sums over all eight waves (else waves 0-1 only)
 __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, const float* __restrict__ xin, int64_t t0,
                                               int64_t t1, bool has_b, float* __restrict__ slab,
                                               float* __restrict__ slab_b, f4 (*Ds)[kWTiles][512],
@@ -1719,7 +1246,6 @@ static int chain_fwd_prepare(const float* x, const float* res_ext, const x2g_cha
   a.tf = x2g_chain_t_floats(rows, dim);
   a.R = rows;
   a.n = n_stages;
-  a.dbg = tuning(kTuneChainDbg);
   int n_ext = 0, held = 0;
   for (int s = 0; s < n_stages; ++s) {
     const x2g_chain_stage& S = stages[s];
@@ -1752,19 +1278,8 @@ X2G_API int x2g_chain_fwd(const float* x, const float* res_ext, const x2g_chain_
   if (int rc = chain_fwd_prepare(x, res_ext, stages, n_stages, rows, dim, in_t, a, empty)) return rc;
   if (empty) return X2G_OK;
   hipStream_t st = as_stream(stream);
-  if (tuning(kTuneChain) == 1 && !in_t) {  // register-tile kernel (no T-layout output)
-    const int64_t groups = ((rows + 15) / 16 + kCWaves - 1) / kCWaves;
-    chain_fwd_kernel<<<static_cast<unsigned>(groups < 256 ? groups : 256), kCThreads, 0, st>>>(a);
-  } else if (tuning(kTuneChain) == 2) {  // v2: one workgroup per CU, <= 96 rows in LDS
-    const int64_t nblk = (rows + 15) / 16;
-    chain_fwd_v2<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, st>>>(a);
-  } else if (tuning(kTuneChain) == 3) {  // v3: v2 with the epilogue interleaved with the product
-    const int64_t nblk = (rows + 15) / 16;
-    chain_fwd_v3<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, st>>>(a);
-  } else {  // v4 (default): v3 with the product's LDS reads pipelined
-    const int64_t nblk = (rows + 15) / 16;
-    chain_fwd_v4<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, st>>>(a);
-  }
+  const int64_t nblk = (rows + 15) / 16;  // one workgroup per CU, <= 96 rows each
+  chain_fwd_v4<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, st>>>(a);
   return last_launch_status();
 }
 
@@ -1818,15 +1333,8 @@ X2G_API int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_
     return rc;
   if (empty) return X2G_OK;
   hipStream_t st = as_stream(stream);
-  if (tuning(kTuneChain) == 1 && !dz_t) {
-    if (res_accum) return X2G_EUNSUPPORTED;  // the register-tile kernel overwrites d_res_ext
-    const int64_t groups = ((rows + 15) / 16 + kCWaves - 1) / kCWaves;
-    chain_bwd_kernel<<<static_cast<unsigned>(groups < 256 ? groups : 256), kCThreads, 0, st>>>(a);
-  } else if (tuning(kTuneChain) == 2) {
-    const int64_t nblk = (rows + 15) / 16;
-    chain_bwd_v2<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, st>>>(a);
-  } else {  // v3 (default), through the batched kernel: a by-value ChainBwdArgs handed to the shared
-            // body by reference is copied to scratch (392 B, 79 -> 121 us); a batch entry is not
+  {  // through the batched kernel: a by-value ChainBwdArgs handed to the shared body by reference is
+     // copied to scratch (392 B, 79 -> 121 us); a batch entry is not
     const int64_t nblk = (rows + 15) / 16;
     ChainBwdBatch b{};
     b.a[0] = a;
@@ -2130,16 +1638,7 @@ X2G_API int x2g_tiled_wgrad_flat(const x2g_tiled_job* jobs, int32_t num_jobs, in
     sj[j] = x2g_slab_job{a.slab_w[j], J.db ? a.slab_b[j] : nullptr, J.dw, J.db, kCD * kCD, J.db ? kCD : 0, n,
                          J.ld, J.cols};
   }
-  const bool nb3 = tuning(kTuneFlatBufs) == 1, spread = tuning(kTuneFlatBias) == 0;
-  const unsigned grid = static_cast<unsigned>(G);
-  if (nb3 && spread)
-    tiled_flat_kernel<3, true><<<grid, kCThreads, 0, as_stream(stream)>>>(a);
-  else if (nb3)
-    tiled_flat_kernel<3, false><<<grid, kCThreads, 0, as_stream(stream)>>>(a);
-  else if (spread)
-    tiled_flat_kernel<4, true><<<grid, kCThreads, 0, as_stream(stream)>>>(a);
-  else
-    tiled_flat_kernel<4, false><<<grid, kCThreads, 0, as_stream(stream)>>>(a);
+  tiled_flat_kernel<4, true><<<static_cast<unsigned>(G), kCThreads, 0, as_stream(stream)>>>(a);
   const int rc = last_launch_status();
   if (rc) return rc;
   if (flags & X2G_DEFER_SLAB_SUM) {

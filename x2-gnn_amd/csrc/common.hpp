@@ -23,24 +23,6 @@ inline unsigned blocks_for(int64_t n, int per_block) {
   return static_cast<unsigned>((n + per_block - 1) / per_block);
 }
 
-// Tuning knobs for A/B experiments (x2g_tuning in line_graph.hip); 0 = default everywhere.
-enum TuneKey {
-  kTuneDenseFwd = 0,
-  kTuneDenseBwd = 1,
-  kTuneAttn = 2,
-  kTuneDenseDbg = 3,
-  kTuneGateSplits = 4,  // rbf gate backward: workgroup cap (0 = default)
-  kTuneFold = 5,        // factorised attention backward: 0 = batched passes, 1 = 3-set pipelined passes
-  kTuneChainDbg = 7,    // row-chain forward ablations for timing (1 no restaging, 2 no stores, 4 no SiLU, 8 no barrier)
-  kTuneChain = 6,       // row chains: 0 = v4 forward / v3 backward, 1 = register-tile kernels, 2 = v2, 3 = v3 forward
-  kTuneFeatDbg = 8,     // featurisation forward ablations for timing (1 no GEMM1, 2 no GEMM2, 4 no stores, 8 no staging)
-  kTuneSprojDbg = 9,    // S projection (sbf_project_waves) ablations for timing (1 no MFMA, 2 no stores)
-  kTuneFlatBufs = 10,   // flat T-layout weight gradient: 1 = three LDS buffers (two steps in flight)
-  kTuneFlatBias = 12,   // flat T-layout weight gradient: 1 = bias column sums on waves 0-1 only
-  kTuneLnBwd = 13,      // graph LayerNorm backward: 1 = one block per molecule (no split)
-  kTuneCount = 16
-};
-int tuning(int key);
 
 // Fixed-order sum of `splits` per-workgroup partial slabs (linear.hip): dw[i] (+)= sum_s part_w[s][i]
 // and, when part_b and db are given, db likewise.

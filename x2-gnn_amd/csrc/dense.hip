@@ -321,12 +321,10 @@ __device__ __forceinline__ void xpair_store(float* __restrict__ buf, const float
   }
 }
 
-template <int DBG>
 __global__ void __launch_bounds__(512) dense_fwd_staged(const float* __restrict__ X, const float* __restrict__ W,
                                                         const float* __restrict__ bias,
                                                         const float* __restrict__ res, int64_t R, int K, int N,
                                                         int act, float* __restrict__ Y, float* __restrict__ Z) {
-  constexpr int dbg = DBG;  // phase switches for measurements (x2g_tuning key 3); 0 in production
   __shared__ __attribute__((aligned(16))) float Ws[64 * 128 * 2];
   __shared__ __attribute__((aligned(16))) float Xs[2][64 * 128];  // [buffer][slot*32 + row][128]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, i = lane & 31;
@@ -339,9 +337,9 @@ __global__ void __launch_bounds__(512) dense_fwd_staged(const float* __restrict_
   float4 stage[4];
   {
     float wv[32];
-    if (!(dbg & 1)) wslot_load<64, true, 512>(W, N, K, wv);
+    wslot_load<64, true, 512>(W, N, K, wv);
     xpair_load(X, tp, R, K, stage);
-    if (!(dbg & 1)) wslot_store<512>(Ws, wv);
+    wslot_store<512>(Ws, wv);
     xpair_store(Xs[0], stage);
     if (tp + G < npairs) xpair_load(X, tp + G, R, K, stage);
     __syncthreads();
@@ -363,7 +361,7 @@ __global__ void __launch_bounds__(512) dense_fwd_staged(const float* __restrict_
       acc1[j] = 0.f;
     }
 #pragma unroll
-    for (int g = 0; g < ((dbg & 2) ? 1 : 16); ++g) {
+    for (int g = 0; g < 16; ++g) {
       const float4 a = *reinterpret_cast<const float4*>(xs + 4 * ((16 * h + g) ^ (i & 15)));
       const int s = 4 * g;
       acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, wb[s * 256], acc0, 0, 0, 0);
@@ -372,7 +370,7 @@ __global__ void __launch_bounds__(512) dense_fwd_staged(const float* __restrict_
       acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, wb[(s + 3) * 256], acc1, 0, 0, 0);
     }
     const int rbase = t * kPTile + 4 * h;
-    if (n < N && !(dbg & 4)) {
+    if (n < N) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const int r = rbase + (j & 3) + 8 * (j >> 2);
@@ -384,17 +382,12 @@ __global__ void __launch_bounds__(512) dense_fwd_staged(const float* __restrict_
           Y[r * N + n] = v;
         }
       }
-    } else if (dbg & 4) {
-      float sum = 0.f;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) sum += acc0[j] + acc1[j] + (res ? rv[j] : 0.f);
-      if (sum == 12345.678f) Y[n] = sum;
     }
     __syncthreads();  // the next buffer is complete; this one is free for the pair after next
   }
 }
 
-// ---------------------------------------------------------------- forward, v5 (default)
+// ---------------------------------------------------------------- forward helpers (v5 design, used by v6)
 // dense_fwd_staged plus the two fixes its phase measurements called for (R = 21k rows: weight
 // staging 5.6 us, epilogue stores 6.3 us of 40 us):
 //   * the weight is read row-contiguous (coalesced) and written to a slot layout padded to 258
@@ -490,69 +483,6 @@ __device__ __forceinline__ void epi_chunk(const float* __restrict__ buf, const S
   if (r < R && 4 * q < N) {
     if (Z) *reinterpret_cast<f4*>(Z + r * N + 4 * q) = zc;
     *reinterpret_cast<f4*>(Y + r * N + 4 * q) = yv;
-  }
-}
-
-__global__ void __launch_bounds__(512) dense_fwd_v5(const float* __restrict__ X, const float* __restrict__ W,
-                                                    const float* __restrict__ bias, const float* __restrict__ res,
-                                                    int64_t R, int K, int N, int act, float* __restrict__ Y,
-                                                    float* __restrict__ Z) {
-  __shared__ __attribute__((aligned(16))) float Ws[64 * kSlotStride];
-  __shared__ __attribute__((aligned(16))) float Xs[2][64 * 128];  // [buffer][slot*32 + row][128]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, i = lane & 31;
-  const int slot = wave >> 2;
-  const int n = 32 * (wave & 3) + i;
-  const int q = tid & 31;  // this thread's 16-byte column chunk in the row-wise epilogue
-  const int64_t npairs = (R + 63) / 64;
-  const int64_t G = gridDim.x;
-  f4 b4 = {0.f, 0.f, 0.f, 0.f};
-  if (bias && 4 * q < N) b4 = f4{bias[4 * q], bias[4 * q + 1], bias[4 * q + 2], bias[4 * q + 3]};  // any alignment
-  int64_t tp = blockIdx.x;
-  Stage4 stage;
-  {
-    float wv[32];
-    wpad_load(W, N, K, wv);
-    xpair_load4(X, tp, R, K, stage);
-    wpad_store(Ws, wv);
-    xpair_store4(Xs[0], stage);
-    if (tp + G < npairs) xpair_load4(X, tp + G, R, K, stage);
-    __syncthreads();
-  }
-  const float* wb = Ws + 2 * n + h;
-  for (int it = 0; tp < npairs; tp += G, ++it) {
-    float* buf = Xs[it & 1];
-    const float* xs = buf + (slot * 32 + i) * 128;
-    Stage4 rres{};
-    if (res) xpair_load4(res, tp, R, N, rres);  // before the prefetch: waiting for it never drains that
-    if (tp + G < npairs) xpair_store4(Xs[(it + 1) & 1], stage);
-    if (tp + 2 * G < npairs) xpair_load4(X, tp + 2 * G, R, K, stage);
-    floatx16 acc0, acc1;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      acc0[j] = 0.f;
-      acc1[j] = 0.f;
-    }
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const float4 a = *reinterpret_cast<const float4*>(xs + 4 * ((16 * h + g) ^ (i & 15)));
-      const int sb = 4 * g * kSlotStride;
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, wb[sb], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, wb[sb + kSlotStride], acc1, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, wb[sb + 2 * kSlotStride], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, wb[sb + 3 * kSlotStride], acc1, 0, 0, 0);
-    }
-    __syncthreads();  // every wave is done with this buffer's x: it now stages the output
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int r = slot * 32 + (j & 3) + 8 * (j >> 2) + 4 * h;
-      buf[r * 128 + 4 * ((n >> 2) ^ (r & 15)) + (n & 3)] = acc0[j] + acc1[j];
-    }
-    __syncthreads();
-    epi_chunk<0>(buf, rres, b4, tp, R, N, act, Y, Z);
-    epi_chunk<1>(buf, rres, b4, tp, R, N, act, Y, Z);
-    epi_chunk<2>(buf, rres, b4, tp, R, N, act, Y, Z);
-    epi_chunk<3>(buf, rres, b4, tp, R, N, act, Y, Z);
-    __syncthreads();  // this buffer is rewritten with the pair after next
   }
 }
 
@@ -1214,8 +1144,8 @@ static inline bool dense_narrow_bwd(int64_t R, int32_t K, int32_t N) {
   return R > 0 && K <= 8 && N <= 128 && N > 64 && N % 64 == 0;
 }
 
-// ---------------------------------------------------------------- backward, v5 (default)
-// dense_bwd_persist restructured like dense_fwd_v5 (K % 4 == 0, N % 4 == 0, 16-byte aligned):
+// ---------------------------------------------------------------- backward helpers (v5 design, used by v8)
+// dense_bwd_persist restructured like the v5 forward (K % 4 == 0, N % 4 == 0, 16-byte aligned):
 //   * dy, z, x tiles (64 rows) are read with 16-byte loads (4 per thread per matrix instead of
 //     16 dword loads) into registers, the next tile's loads fly during the MFMAs;
 //   * LDS: weight in the padded slot layout (cmap<64>, B[c = n][j = k] = w[n][k], staged from
@@ -1261,149 +1191,11 @@ __device__ __forceinline__ f4 mask4(f4 v, int64_t tp, int U, int64_t R, int cols
   return ok ? v : f4{0.f, 0.f, 0.f, 0.f};
 }
 
-__device__ __forceinline__ void dense_bwd_v5_body(const float* __restrict__ dY, const float* __restrict__ Zin,
-                                                  const float* __restrict__ X, const float* __restrict__ W, int64_t R,
-                                                  int K, int N, int act, float* __restrict__ dX,
-                                                  const float* __restrict__ dXadd, float* __restrict__ part_w,
-                                                  float* __restrict__ part_b, float* __restrict__ Ws,
-                                                  float* __restrict__ Ds, float* __restrict__ Xs) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, i = lane & 31;
-  const int64_t ntiles = (R + 63) / 64;
-  const int64_t G = gridDim.x;
-  const bool silu = act == kActSilu;
-  floatx16 accw0, accw1;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    accw0[j] = 0.f;
-    accw1[j] = 0.f;
-  }
-  float bsum = 0.f;
-  int64_t t = blockIdx.x;
-  Stage4 sd, sz, sx;
-  {
-    float wv[32];
-    if (dX) wpad_load_bwd(W, N, K, wv);
-    xpair_load4(dY, t, R, N, sd);
-    if (silu) xpair_load4(Zin, t, R, N, sz);
-    xpair_load4(X, t, R, K, sx);
-    if (dX) wpad_store_bwd(Ws, wv);
-  }
-  const int rt = 32 * (wave >> 2), kcol = 32 * (wave & 3) + i;  // dx block
-  const int nb = 32 * (wave & 3), kb = 64 * (wave >> 2);        // dW block
-  for (; t < ntiles; t += G) {
-    // dz = dy * act'(z) -> Ds, x -> Xs (masked rows / columns)
-    {
-      f4 d0 = sd.v0, d1 = sd.v1, d2 = sd.v2, d3 = sd.v3;
-      if (silu) {
-        d0 = silu_grad4<0>(d0, sz.v0);
-        d1 = silu_grad4<1>(d1, sz.v1);
-        d2 = silu_grad4<2>(d2, sz.v2);
-        d3 = silu_grad4<3>(d3, sz.v3);
-      }
-      Stage4 dz{mask4(d0, t, 0, R, N), mask4(d1, t, 1, R, N), mask4(d2, t, 2, R, N), mask4(d3, t, 3, R, N)};
-      Stage4 xm{mask4(sx.v0, t, 0, R, K), mask4(sx.v1, t, 1, R, K), mask4(sx.v2, t, 2, R, K),
-                mask4(sx.v3, t, 3, R, K)};
-      xpair_store4(Ds, dz);
-      xpair_store4(Xs, xm);
-    }
-    __syncthreads();
-    if (t + G < ntiles) {  // next tile's loads fly during the MFMAs below
-      xpair_load4(dY, t + G, R, N, sd);
-      if (silu) xpair_load4(Zin, t + G, R, N, sz);
-      xpair_load4(X, t + G, R, K, sx);
-    }
-    floatx16 acc0, acc1;
-    if (dX) {  // dx[rt + i][kcol] = sum_n dz[r][n] w[n][k], n = 64h + 4g + e
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        acc0[j] = 0.f;
-        acc1[j] = 0.f;
-      }
-      const float* ds = Ds + (rt + i) * 128;
-      const float* wb = Ws + 2 * kcol + h;
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        const f4 a = *reinterpret_cast<const f4*>(ds + 4 * ((16 * h + g) ^ (i & 15)));
-        const int sb = 4 * g * kSlotStride;
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, wb[sb], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, wb[sb + kSlotStride], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, wb[sb + 2 * kSlotStride], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, wb[sb + 3 * kSlotStride], acc1, 0, 0, 0);
-      }
-    }
-    // dW[n][k] += sum_r dz[r][n] x[r][k]; step s: rows ra = (s & 7) + 16 (s >> 3) and ra + 8
-    // (r & 15) = (s & 7) + 8h is the same for the 4 row groups: 8 address patterns, one loop of 4
-#pragma unroll 1
-    for (int sg = 0; sg < 4; ++sg) {
-      const float* dsg = Ds + sg * 16 * 128;
-      const float* xsg = Xs + sg * 16 * 128;
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const int r = s + 8 * h;
-        const float a = dsg[swz(r, nb + i)];
-        accw0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xsg[swz(r, kb + i)], accw0, 0, 0, 0);
-        accw1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xsg[swz(r, kb + 32 + i)], accw1, 0, 0, 0);
-      }
-    }
-    if (part_b && tid < 128) {
-#pragma unroll 8
-      for (int rr = 0; rr < 64; ++rr) bsum += Ds[swz(rr, tid)];
-    }
-    __syncthreads();  // Ds / Xs consumed
-    if (dX) {  // dx through LDS (into Xs), then 16-byte row stores
-#pragma unroll
-      for (int j = 0; j < 16; ++j) Xs[swz(rt + (j & 3) + 8 * (j >> 2) + 4 * h, kcol)] = acc0[j] + acc1[j];
-      __syncthreads();
-      const int q = tid & 31;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int row = (tid >> 5) + 16 * u;
-        const int r = static_cast<int>(t) * 64 + row;
-        f4 v = *reinterpret_cast<const f4*>(Xs + row * 128 + 4 * (q ^ (row & 15)));
-        if (r < R && 4 * q < K) {
-          if (dXadd) v += *reinterpret_cast<const f4*>(dXadd + r * K + 4 * q);
-          *reinterpret_cast<f4*>(dX + r * K + 4 * q) = v;
-        }
-      }
-      __syncthreads();  // Xs is rewritten by the next tile
-    }
-  }
-  float* slab = part_w + static_cast<int64_t>(blockIdx.x) * N * K;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int nn = nb + (j & 3) + 8 * (j >> 2) + 4 * h;
-    const int k0 = kb + i, k1 = kb + 32 + i;
-    if (nn < N && k0 < K) slab[nn * K + k0] = accw0[j];
-    if (nn < N && k1 < K) slab[nn * K + k1] = accw1[j];
-  }
-  if (part_b && tid < N) part_b[static_cast<int64_t>(blockIdx.x) * N + tid] = bsum;
-}
-
-__global__ void __launch_bounds__(512) dense_bwd_v5(const float* __restrict__ dY, const float* __restrict__ Zin,
-                                                    const float* __restrict__ X, const float* __restrict__ W,
-                                                    int64_t R, int K, int N, int act, float* __restrict__ dX,
-                                                    const float* __restrict__ dXadd, float* __restrict__ part_w,
-                                                    float* __restrict__ part_b) {
-  __shared__ __attribute__((aligned(16))) float Ws[64 * kSlotStride];
-  __shared__ __attribute__((aligned(16))) float Ds[64 * 128];
-  __shared__ __attribute__((aligned(16))) float Xs[64 * 128];
-  dense_bwd_v5_body(dY, Zin, X, W, R, K, N, act, dX, dXadd, part_w, part_b, Ws, Ds, Xs);
-}
-
 struct DenseBwdBatch {
   x2g_dense_bwd_group g[X2G_MAX_GROUPS];
   float* part_w[X2G_MAX_GROUPS];
   float* part_b[X2G_MAX_GROUPS];
 };
-
-__global__ void __launch_bounds__(512) dense_bwd_v5_batched(const DenseBwdBatch b, int64_t R, int K, int N, int act) {
-  __shared__ __attribute__((aligned(16))) float Ws[64 * kSlotStride];
-  __shared__ __attribute__((aligned(16))) float Ds[64 * 128];
-  __shared__ __attribute__((aligned(16))) float Xs[64 * 128];
-  const int gi = blockIdx.y;
-  const x2g_dense_bwd_group& p = b.g[gi];
-  dense_bwd_v5_body(p.dy, p.z, p.x, p.w, R, K, N, act, p.dx, p.dx_add, b.part_w[gi], b.part_b[gi], Ws, Ds, Xs);
-}
 
 // ---------------------------------------------------------------- backward, v8: 32-row tiles
 // As v5 (weight in the padded slot layout, dz and x tiles chunk-swizzled in LDS, next tile
@@ -1588,39 +1380,23 @@ X2G_API int x2g_dense_fwd(const float* x, const float* w, const float* b, int64_
   if (R == 0) return X2G_OK;
   if (!x || !w || !y) return X2G_EINVAL;
   hipStream_t st = as_stream(stream);
-  const int variant = tuning(kTuneDenseFwd);  // 0: LDS-staged (default), 1: register fragments, 2: tiled
-  if (K <= 128 && N <= 128 && variant <= 1 && R * 128 * 4 < (int64_t(1) << 31)) {
+  if (K <= 128 && N <= 128 && R * 128 * 4 < (int64_t(1) << 31)) {
     const int64_t ntiles = (R + kPTile - 1) / kPTile;
     const int64_t want = (ntiles + 1) / 2;
     const unsigned grid = static_cast<unsigned>(want < kPFwdGrid ? want : kPFwdGrid);
     const bool vec = K % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0;
     if (K <= 8)
       dense_fwd_persist<4, false><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
-    else if (!vec && variant == 0 && K % 4 != 0 && N % 4 == 0 && aligned16(x) && aligned16(y) && aligned16(z) &&
-             aligned16(res))
+    else if (!vec && K % 4 != 0 && N % 4 == 0 && aligned16(x) && aligned16(y) && aligned16(z) && aligned16(res))
       return dense_fwd_narrow_launch(x, w, b, res, R, K, N, act, y, z, st);
-    else if (vec && variant == 0 && N % 4 == 0 && aligned16(y) && aligned16(z) && aligned16(res)) {
-      // v6 (default); knob 3 = 1 selects v5.  (A register-resident-weight variant with one tile
+    else if (vec && N % 4 == 0 && aligned16(y) && aligned16(z) && aligned16(res)) {
+      // v6: two 256-thread workgroups per CU.  (A register-resident-weight variant with one tile
       // per workgroup measured no faster: at 21k rows the layer is bound by its 43 MB of
       // x / res / y / z traffic plus the launch ramp, not by the weight staging.)
-      if (tuning(kTuneDenseDbg) != 1) {
-        const unsigned g6 = static_cast<unsigned>(ntiles < 512 ? ntiles : 512);
-        dense_fwd_v6<<<g6, 256, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
-      } else {
-        dense_fwd_v5<<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
-      }
-    }
-    else if (vec && variant == 0)
-      switch (tuning(kTuneDenseDbg)) {
-        case 1: dense_fwd_staged<1><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z); break;
-        case 2: dense_fwd_staged<2><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z); break;
-        case 4: dense_fwd_staged<4><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z); break;
-        case 6: dense_fwd_staged<6><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z); break;
-        case 7: dense_fwd_staged<7><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z); break;
-        default: dense_fwd_staged<0><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z); break;
-      }
-    else if (vec)
-      dense_fwd_persist<64, true><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
+      const unsigned g6 = static_cast<unsigned>(ntiles < 512 ? ntiles : 512);
+      dense_fwd_v6<<<g6, 256, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
+    } else if (vec)
+      dense_fwd_staged<<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
     else
       dense_fwd_persist<64, false><<<grid, 512, 0, st>>>(x, w, b, res, R, K, N, act, y, z);
     return last_launch_status();
@@ -1676,12 +1452,9 @@ X2G_API int x2g_linear_wgrad(const float* dy, const float* x, int64_t R, int32_t
 // Backward grid: the fewest workgroups that keep the busiest one at ceil(tiles / 256) tiles —
 // every workgroup writes a full weight-gradient slab, so idle-making extra workgroups would only
 // add slab traffic (330 tiles at config 2: 165 workgroups x 2 tiles instead of 256).
-// tuning key 1 (kTuneDenseBwd): 0 = v8 (default, 32-row tiles), 2 = v5 (64-row tiles), else the
-// register-fragment persistent kernel
-static inline bool bwd_v8() { return tuning(kTuneDenseBwd) == 0; }
-
+// (32-row tiles: dense_bwd_v8; the register-fragment persistent kernel strides over the same grid)
 static inline int64_t bwd_grid(int64_t R) {
-  const int64_t ntiles = (R + (bwd_v8() ? 31 : kBTile - 1)) / (bwd_v8() ? 32 : kBTile);
+  const int64_t ntiles = (R + 31) / 32;
   const int64_t per = (ntiles + kPBwdGrid - 1) / kPBwdGrid;
   return (ntiles + per - 1) / per;
 }
@@ -1748,10 +1521,8 @@ X2G_API int x2g_dense_bwd_ex(const float* dy, const float* z, int act, const flo
     float* part_b = db ? part_w + static_cast<int64_t>(grid) * N * K : nullptr;
     const bool vec = K % 4 == 0 && N % 4 == 0 && N > 8 && aligned16(dy) && aligned16(z) && aligned16(x) &&
                      aligned16(dx) && aligned16(dx_add);
-    if (vec && bwd_v8())
+    if (vec)
       dense_bwd_v8<<<grid, 512, 0, st>>>(dy, z, x, w, R, K, N, act, dx, dx_add, part_w, part_b);
-    else if (vec && tuning(kTuneDenseBwd) == 2)
-      dense_bwd_v5<<<grid, 512, 0, st>>>(dy, z, x, w, R, K, N, act, dx, dx_add, part_w, part_b);
     else if (N <= 8)
       dense_bwd_persist<4><<<grid, 512, 0, st>>>(dy, z, x, w, R, K, N, act, dx, dx_add, part_w, part_b);
     else
@@ -1859,10 +1630,7 @@ X2G_API int x2g_dense_bwd_batched(const x2g_dense_bwd_group* groups, int32_t G, 
     jobs[g] = x2g_slab_job{b.part_w[g], b.part_b[g], p.dw, p.db, static_cast<int64_t>(N) * K, p.db ? N : 0, grid};
   }
   hipStream_t st = as_stream(stream);
-  if (bwd_v8())
-    dense_bwd_v8_batched<<<dim3(grid, G), 512, 0, st>>>(b, R, K, N, act);
-  else
-    dense_bwd_v5_batched<<<dim3(grid, G), 512, 0, st>>>(b, R, K, N, act);
+  dense_bwd_v8_batched<<<dim3(grid, G), 512, 0, st>>>(b, R, K, N, act);
   if (int rc = last_launch_status()) return rc;
   if (flags & X2G_DEFER_SLAB_SUM) return X2G_OK;
   return x2g_slab_sum_batch(jobs, G, (flags & X2G_ACCUM_WGRAD) ? 1 : 0, stream);

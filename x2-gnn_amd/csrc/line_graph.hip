@@ -318,24 +318,9 @@ __global__ void transpose_sym_kernel(const int32_t* __restrict__ src, const int3
 
 }  // namespace x2g
 
-namespace x2g {
-}  // namespace x2g
-
 using namespace x2g;
 
-namespace x2g {
-static int g_tune[kTuneCount] = {0};
-int tuning(int key) { return (key >= 0 && key < kTuneCount) ? g_tune[key] : 0; }
-}  // namespace x2g
-
-X2G_API int x2g_abi_version(void) { return 7; }
-
-X2G_API int x2g_tuning(int key, int value) {
-  if (key < 0 || key >= kTuneCount) return -1;
-  const int old = g_tune[key];
-  g_tune[key] = value;
-  return old;
-}
+X2G_API int x2g_abi_version(void) { return 8; }
 
 X2G_API const char* x2g_status_string(int status) {
   switch (status) {

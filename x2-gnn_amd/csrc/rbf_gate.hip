@@ -297,8 +297,7 @@ inline bool gate_shape_ok(int D, int R) { return R >= 1 && R <= kGateRMax && (D 
 
 inline int gate_bwd_splits(int64_t rows) {
   const int64_t want = (rows + 7) / 8;  // >= 8 rows per workgroup: one or two per slot
-  const int cap = tuning(kTuneGateSplits) > 0 ? tuning(kTuneGateSplits) : kGateBwdSplits;
-  return static_cast<int>(want < cap ? (want < 1 ? 1 : want) : cap);
+  return static_cast<int>(want < kGateBwdSplits ? (want < 1 ? 1 : want) : kGateBwdSplits);
 }
 
 }  // namespace x2g

@@ -761,7 +761,7 @@ X2G_API int x2g_graph_layernorm_bwd_ex(const float* out, const float* dout, cons
   if (G == 0) return X2G_OK;
   const bool vec = D % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
                    reinterpret_cast<uintptr_t>(dout) % 16 == 0 && reinterpret_cast<uintptr_t>(dx) % 16 == 0;
-  if (!vec || !ws || wsb < x2g_graph_layernorm_bwd_workspace(G) || tuning(kTuneLnBwd) == 1)
+  if (!vec || !ws || wsb < x2g_graph_layernorm_bwd_workspace(G))
     return x2g_graph_layernorm_bwd(out, dout, rstd, rowptr, G, D, dx, stream);
   hipStream_t st = as_stream(stream);
   const unsigned grid = static_cast<unsigned>(G * kLnSplit);

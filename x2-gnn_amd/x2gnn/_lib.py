@@ -23,7 +23,6 @@ _SZ = ctypes.c_size_t
 # name -> argtypes (restype int unless noted); mirrors include/x2g.h
 SIGNATURES = {
     "x2g_abi_version": [],
-    "x2g_tuning": [ctypes.c_int, ctypes.c_int],
     "x2g_status_string": [ctypes.c_int],
     "x2g_csr_rowptr": [_P, _I64, _I64, _P, _P],
     "x2g_vertex_to_edge_workspace": [_I64, _I64],
@@ -152,10 +151,6 @@ def load():
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = RESTYPES.get(name, ctypes.c_int)
-        # kernel-variant knobs for A/B measurements: X2G_TUNE="key=value,key=value"
-        for kv in filter(None, os.environ.get("X2G_TUNE", "").split(",")):
-            key, value = kv.split("=")
-            lib.x2g_tuning(int(key), int(value))
         _lib = lib
     return _lib
 

@@ -27,6 +27,24 @@ def shard_by_triplets(triplet_counts, world: int):
     return [np.nonzero(owner == r)[0] for r in range(world)]
 
 
+def collate_shard(mols, world: int, rank: int):
+    """This rank's share of one global batch: (collated local Batch, local molecule count, global
+    molecule count).  The shard is ``shard_by_triplets(...)[rank]``.
+
+    The local batch also carries the GLOBAL batch's atomic numbers (``_x2g_count_z``): the
+    embedding's max_norm renorm (rows present in the batch) and scale_grad_by_freq (gradient /
+    per-element count) are per-batch rules (atom_embedding.py:14), so every rank evaluates them
+    over the global batch -- the same rows renormalised on every rank (parameters never diverge)
+    and the same divisor as the single-device step over the whole batch."""
+    from .data import collate
+
+    shards = shard_by_triplets([m["triplet_num"] for m in mols], world)
+    mine = shards[rank]
+    batch = collate([mols[i] for i in mine])
+    batch._store["_x2g_count_z"] = torch.cat([torch.as_tensor(m["x"], dtype=torch.int64).reshape(-1) for m in mols])
+    return batch, len(mine), len(mols)
+
+
 def flat_layout(params, align=4):
     """Offsets of each parameter in a flat fp32 buffer, each rounded up to ``align`` floats
     (16 bytes) so views of the buffer keep the alignment the vectorised kernels want; returns

@@ -152,17 +152,19 @@ class EmbeddingBlock(nn.Module):
     def forward(self, atomic_num):
         return self.lin.fused(self.embedding(atomic_num), act=ops.ACT_SILU if self.activate else ops.ACT_NONE)
 
-    def element_rows(self, atomic_num):
+    def element_rows(self, atomic_num, count_z=None):
         """The embedding rows [num_embeddings, D] the Linear of ``element_table`` reads (renormalised
         as the embedding lookup does), from one launch (csrc/embedding.hip); None where that kernel
-        does not apply (CPU, other norms, large vocabularies)."""
+        does not apply (CPU, other norms, large vocabularies).  ``count_z``: the atomic numbers the
+        per-batch rules (renormalised rows, scale_grad_by_freq counts) are evaluated over, when not
+        ``atomic_num`` itself (a molecule shard of a global batch, dist.collate_shard)."""
         emb = self.embedding
-        z = atomic_num.reshape(-1)
+        z = (atomic_num if count_z is None else count_z).reshape(-1)
         if z.is_cuda and emb.norm_type == 2.0 and emb.num_embeddings <= 64:
             return ops.embedding_table(emb.weight, z, emb.max_norm, emb.padding_idx, emb.scale_grad_by_freq)
         return None
 
-    def element_table(self, atomic_num):
+    def element_table(self, atomic_num, count_z=None):
         """Per-element rows [num_embeddings, D] equal to forward(z) for every z present.
 
         Reproduces the in-place max_norm renormalisation of the rows referenced by
@@ -170,8 +172,8 @@ class EmbeddingBlock(nn.Module):
         materialising the [N, D] output: row z of the result stands for every atom of type z.
         """
         emb = self.embedding
-        z = atomic_num.reshape(-1)
-        w = self.element_rows(atomic_num)
+        z = (atomic_num if count_z is None else count_z).reshape(-1)
+        w = self.element_rows(atomic_num, count_z)
         if w is not None:
             return self.lin.fused(w, act=ops.ACT_SILU if self.activate else ops.ACT_NONE)
         # counts per element without torch.bincount (its output size is data-dependent: a host sync

@@ -91,11 +91,18 @@ class Trainer:
             self.reduce()
             self.update()
             return self.global_loss(loss)
-        g_fb, g_up = self.graphs
-        g_fb.replay()
+        self.replay_forward_backward()
         self.reduce()
-        g_up.replay()
+        self.graphs[1].replay()
+        self.grads_zeroed = True
         return self.global_loss(self.loss)
+
+    def replay_forward_backward(self):
+        """Replay the captured forward+loss+backward (accumulates into the bucket: zeroed by the
+        previous update, or by the caller); returns the captured loss tensor."""
+        self.graphs[0].replay()
+        self.grads_zeroed = False
+        return self.loss
 
     def capture(self, batch, warm=3):
         """Record forward+backward and the update as two HIP graphs (warm-up passes on a side
@@ -118,6 +125,7 @@ class Trainer:
         with torch.cuda.graph(g_up):
             self.update()
         self.graphs = (g_fb, g_up)
+        self.grads_zeroed = True  # (nothing ran during capture: the bucket is still the zeroed one)
 
 
 class Inference:

@@ -66,7 +66,9 @@ class _XGNNBase(nn.Module):
             neo_x = ops.featurize(data.edge_attr, env, self.mat_trans, self.emb_trans)
         else:
             neo_x = self.mat_trans.fused(data.edge_attr * env, act=ops.ACT_SILU)
-        table, edge_proj = self._edge_tables(data.x)
+        # under molecule sharding the embedding's per-batch rules count the global batch's atoms
+        # (dist.collate_shard); otherwise this batch's
+        table, edge_proj = self._edge_tables(data.x, data._store.get("_x2g_count_z"))
         sbf = self.sbf_layer.from_positions(dist, pos, lg, bessel)
         if not fused_feat:
             neo_x = self.emb_trans.fused(neo_x, act=ops.ACT_SILU)
@@ -76,13 +78,13 @@ class _XGNNBase(nn.Module):
             line._store["_x2g_edge_proj"] = edge_proj
         return line, plan
 
-    def _edge_tables(self, atomic_num):
+    def _edge_tables(self, atomic_num, count_z=None):
         """(element table, per-layer lin_edge tables or None).  The embedding Linear, edgenn and every
         conv's lin_edge all act on the <= 10-row element table (xgnn.py:57-58): where compiled they
         run as ONE small-table chain (ops.table_chain, one launch each way); the trunk then reads
         its lin_edge tables from ``_x2g_edge_proj`` instead of applying edgenn / lin_edge itself."""
         emb = self.emb_block
-        rows = emb.element_rows(atomic_num) if ops._TABLE_CHAIN else None
+        rows = emb.element_rows(atomic_num, count_z) if ops._TABLE_CHAIN else None
         trunk_stages = self.fin_model.edge_table_stages() if rows is not None else None
         if trunk_stages is not None:
             act = ops.ACT_SILU if emb.activate else ops.ACT_NONE
@@ -90,7 +92,7 @@ class _XGNNBase(nn.Module):
             if len(stages) <= ops.TABLE_MAX_STAGES and ops.table_chain_supported(rows, [m for m, _, _ in stages]):
                 outs = ops.table_chain(rows, stages)
                 return outs[0], tuple(outs[3:])
-        return emb.element_table(atomic_num), None
+        return emb.element_table(atomic_num, count_z), None
 
     def forward(self, data):
         line, plan = self.line_graph_data(data)
