@@ -85,21 +85,23 @@ int x2g_line_graph_transpose_sym(const int32_t* edge_src, const int32_t* edge_ds
 
 /* ---------------------------------------------------------------- basis (featurisation) */
 
-/* rbf_env[e, l*R+n] = env(d_e) * N_ln j_l(z_ln d_e/cutoff)   (l < 7, n < 6, R = 6)
- * = the E-row part of F_B_2D.forward (angular_basis_layer.py:80-86) with poly_envelop
- * (envelop.py:16-21, exponent 5). */
-int x2g_bessel_env(const float* dist, int64_t num_edges, float cutoff, float* rbf_env, void* stream);
+/* rbf_env[e, l*R+n] = env(d_e) * N_ln j_l(z_ln d_e/cutoff)   (l < num_spherical, n < R = num_radial)
+ * = the E-row part of F_B_2D(num_spherical, num_radial).forward (angular_basis_layer.py:51-86) with
+ * poly_envelop (envelop.py:16-21, exponent 5).  Compiled for num_spherical <= 7, num_radial <= 16
+ * (config.json: 7 x 6; the reference's default xgnn_poly: 7 x 16, xgnn.py:16), else X2G_EUNSUPPORTED. */
+int x2g_bessel_env(const float* dist, int64_t num_edges, float cutoff, int32_t num_spherical, int32_t num_radial,
+                   float* rbf_env, void* stream);
 
 /* The whole E-row featurisation in one launch (xgnn.py:49-53 + radial_basis_layer.py:36-40 +
  * envelop.py:16-21 + the E-row half of angular_basis_layer.py:80-86), per directed edge e = (a, b):
  *   dist[e] = |pos[a] - pos[b]|,  env[e] = poly_envelop(dist / cutoff) (exponent 5),
- *   rbf_env[e, n] = sin(freq[n] * dist / cutoff) * env[e]   (n < num_radial <= 16; the trainable
+ *   rbf_env[e, n] = sin(freq[n] * dist / cutoff) * env[e]   (n < num_freq <= 16; the trainable
  *                   RadialBasis times the envelope: xgnn_poly's node_rbf),
- *   bessel_env[e, :] = x2g_bessel_env's 42 values (optional, NULL skips).
+ *   bessel_env[e, :] = x2g_bessel_env's num_spherical * num_radial values (optional, NULL skips).
  * edge_src/edge_dst int32 atom ids. */
 int x2g_edge_basis(const float* pos, const int32_t* edge_src, const int32_t* edge_dst, int64_t num_edges,
-                   float cutoff, const float* freq, int32_t num_radial, float* dist, float* env, float* rbf_env,
-                   float* bessel_env, void* stream);
+                   float cutoff, const float* freq, int32_t num_freq, int32_t num_spherical, int32_t num_radial,
+                   float* dist, float* env, float* rbf_env, float* bessel_env, void* stream);
 
 /* d loss / d freq[n] = sum_e g[e, n] * env[e] * cos(freq[n] x_e) * x_e, x_e = dist[e] / cutoff
  * (the backward of rbf_env w.r.t. RadialBasis.frequencies).  Deterministic: per-workgroup
@@ -154,7 +156,7 @@ int x2g_rbf_gate_bwd(const float* g, const int32_t* owner, const float* x, const
                      float* drbf, float* dw, float* db, int flags, void* workspace, size_t workspace_bytes,
                      void* stream);
 
-/* sbf[t, l*R+n] = rbf_env[trip_src[t], l*R+n] * Y_l0(theta_t), theta_t = atan2(|ji x jk|, ji.jk),
+/* sbf[t, l*R+n] = rbf_env[trip_src[t], l*R+n] * Y_l0(theta_t)  (R = num_radial; shapes as x2g_bessel_env), theta_t = atan2(|ji x jk|, ji.jk),
  * ji = pos[atom_i]-pos[atom_j], jk = pos[atom_k]-pos[atom_j]  (xgnn.py:61-65,
  * angular_basis_layer.py:87-93).  If theta[T] is non-NULL it is used instead of the positions
  * (F_B_2D.forward(d, Angles, edge_index_1) signature; pos/atom_* may then be NULL).
@@ -163,14 +165,16 @@ int x2g_rbf_gate_bwd(const float* g, const int32_t* owner, const float* x, const
  * lin_sbf backward (x2g_sbf_attention_bwd_src_fold) folds per triplet. */
 int x2g_spherical_basis(const float* pos, const int32_t* atom_i, const int32_t* atom_j,
                         const int32_t* atom_k, const float* theta, const int32_t* trip_src,
-                        const float* rbf_env, int64_t num_triplets, float* sbf, float* cos_theta,
-                        float* sph_y, void* stream);
+                        const float* rbf_env, int64_t num_triplets, int32_t num_spherical, int32_t num_radial,
+                        float* sbf, float* cos_theta, float* sph_y, void* stream);
 
 /* ---------------------------------------------------------------- SBF-transformer attention */
 
 /* S[t, :] = w_sbf[out_dim, sbf_dim] sbf[t, :] + b_sbf: lin_sbf of sbftransformer_conv.py:148,
  * materialised once per layer so the attention kernels read one row per triplet instead of
- * re-projecting it.  out_dim in {32, 64, 128, 256}, sbf_dim 42. */
+ * re-projecting it.  sbf_dim 42 (config.json's 7 x 6 basis): out_dim in {32, 64, 128, 256} on the
+ * compiled narrow-K kernels; any other sbf_dim (e.g. 112, the reference's default 7 x 16) runs as
+ * x2g_dense_fwd. */
 int x2g_sbf_project(const float* sbf, int64_t num_triplets, int32_t sbf_dim, const float* w_sbf,
                     const float* b_sbf, int32_t out_dim, float* sbfproj, void* stream);
 

@@ -17,6 +17,7 @@ cpu_baseline.
 """
 from __future__ import annotations
 
+import functools
 import math
 
 import numpy as np
@@ -28,7 +29,7 @@ from scipy.optimize import brentq
 
 from .triplets import vertex_to_edge
 
-NUM_SPH, NUM_RAD = 7, 6
+NUM_SPH, NUM_RAD = 7, 6  # config.json; the reference's own defaults are (7, 16) (xgnn.py:16)
 
 
 # ------------------------------------------------------------------ basis constants (basis_func.py)
@@ -48,25 +49,30 @@ def _bessel_zeros(n, k):
     return z
 
 
-_ZEROS = _bessel_zeros(NUM_SPH, NUM_RAD).astype(np.float64)
-_NORM = np.array([[1.0 / math.sqrt(0.5 * _sph_jn(_ZEROS[l, n], l + 1) ** 2) for n in range(NUM_RAD)]
-                  for l in range(NUM_SPH)])
+@functools.lru_cache(maxsize=None)
+def _basis_consts(nsph, nrad):
+    """(zeros [nsph, nrad] float64 of the float32 roots, normalisers N_ln) for F_B_2D(nsph, nrad)."""
+    zeros = _bessel_zeros(nsph, nrad).astype(np.float64)
+    norm = np.array([[1.0 / math.sqrt(0.5 * _sph_jn(zeros[l, n], l + 1) ** 2) for n in range(nrad)]
+                     for l in range(nsph)])
+    return zeros, norm
 
 
-def bessel_radial(d_scaled: np.ndarray) -> np.ndarray:
-    """[E, 42] N_ln j_l(z_ln x), l-major (basis_func.py:47-71)."""
+def bessel_radial(d_scaled: np.ndarray, nsph=NUM_SPH, nrad=NUM_RAD) -> np.ndarray:
+    """[E, nsph * nrad] N_ln j_l(z_ln x), l-major (basis_func.py:47-71)."""
+    zeros, norm = _basis_consts(nsph, nrad)
     x = np.asarray(d_scaled, np.float64)
     cols = []
-    for l in range(NUM_SPH):
-        for n in range(NUM_RAD):
-            cols.append(_NORM[l, n] * special.spherical_jn(l, _ZEROS[l, n] * x))
+    for l in range(nsph):
+        for n in range(nrad):
+            cols.append(norm[l, n] * special.spherical_jn(l, zeros[l, n] * x))
     return np.stack(cols, axis=1)
 
 
-def sph_y0(theta: np.ndarray) -> np.ndarray:
-    """[T, 7] sqrt((2l+1)/4pi) P_l(cos theta) (basis_func.py:110-155, m = 0)."""
+def sph_y0(theta: np.ndarray, nsph=NUM_SPH) -> np.ndarray:
+    """[T, nsph] sqrt((2l+1)/4pi) P_l(cos theta) (basis_func.py:110-155, m = 0)."""
     c = np.cos(np.asarray(theta, np.float64))
-    return np.stack([math.sqrt((2 * l + 1) / (4 * math.pi)) * special.eval_legendre(l, c) for l in range(NUM_SPH)],
+    return np.stack([math.sqrt((2 * l + 1) / (4 * math.pi)) * special.eval_legendre(l, c) for l in range(nsph)],
                     axis=1)
 
 
@@ -78,12 +84,12 @@ def envelope(d, cutoff=5.0, exponent=5):
     return 1 / x + a * x ** (p - 1) + b * x ** p + c * x ** (p + 1)
 
 
-def spherical_basis(d, theta, jk):
-    """F_B_2D.forward (angular_basis_layer.py:80-93) -> [T, 42] float32."""
-    rbf = bessel_radial(d.detach().numpy() / 5.0)
+def spherical_basis(d, theta, jk, nsph=NUM_SPH, nrad=NUM_RAD):
+    """F_B_2D(nsph, nrad).forward (angular_basis_layer.py:80-93) -> [T, nsph * nrad] float32."""
+    rbf = bessel_radial(d.detach().numpy() / 5.0, nsph, nrad)
     env = envelope(d.detach().double()).numpy()
     rbf_env = env[:, None] * rbf
-    cbf = np.repeat(sph_y0(theta.detach().numpy()), NUM_RAD, axis=1)
+    cbf = np.repeat(sph_y0(theta.detach().numpy(), nsph), nrad, axis=1)
     return torch.from_numpy((rbf_env[jk.numpy()] * cbf).astype(np.float32))
 
 
@@ -252,7 +258,7 @@ class XGNN(nn.Module):  # xgnn.py:15-137
     def __init__(self, conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embedding_size=128,
                  global_pool=None):
         super().__init__()
-        assert (sbf_dim, rbf_dim) == (NUM_SPH, NUM_RAD)
+        self.num_spherical, self.num_radial = sbf_dim, rbf_dim  # F_B_2D(sbf_dim, rbf_dim) (xgnn.py:34)
         self.AF = nn.SiLU()
         self.emb_block = EmbeddingBlock(embedding_size)
         self.rbf_layer = RadialBasis(rbf_dim)
@@ -272,7 +278,7 @@ class XGNN(nn.Module):  # xgnn.py:15-137
         ji = atom_pos[i] - atom_pos[j]
         jk = atom_pos[k] - atom_pos[j]
         theta = torch.atan2(torch.norm(torch.cross(ji, jk, dim=1), dim=1), (ji * jk).sum(1))  # :61-64
-        sbf = spherical_basis(d, theta, trip[0])                                         # :65
+        sbf = spherical_basis(d, theta, trip[0], self.num_spherical, self.num_radial)   # :65
         rbf = self.rbf_layer(d) * env                                                    # :68-69
         neo_x = self.AF(self.emb_trans(neo_x))                                           # :70
         return self.fin_model(neo_x, trip, neo_edge_attr, batch, sbf, rbf, edge_index[0], atom_batch)

@@ -9,7 +9,7 @@ seed by ``weights.seeded_value`` (see that module), so fixtures stay small.  Fix
 
 * ``triplets.npz``   — ``edge_graph.vertex_to_edge_2`` (edge_graph.py:12-30) on S160, S5A, a
                        3-molecule batch, the smallest AID_kcal molecule and a directed graph.
-* ``basis.npz``      — ``poly_envelop`` (envelop.py:16-21), ``RadialBasis`` (radial_basis_layer.py:36-40)
+* ``basis.npz``/``basis_7x16.npz`` — ``poly_envelop`` (envelop.py:16-21), ``RadialBasis`` (radial_basis_layer.py:36-40)
                        and ``F_B_2D`` (angular_basis_layer.py:80-93) on a 2-molecule S160 batch.
 * ``conv1.npz``      — one ``SBFTransformerConv`` (sbftransformer_conv.py:93-162), D=128 H=16,
                        per-triplet edge_attr, forward + backward for a seeded upstream gradient.
@@ -130,6 +130,24 @@ def gen_basis(ref):
         out["env_probe_d"] = probe.numpy()
         out["env_probe"] = env(probe).numpy()
     np.savez_compressed(os.path.join(HERE, "basis.npz"), **out)
+
+
+def gen_basis_7x16(ref):
+    """basis_7x16.npz: F_B_2D(7, 16) (the reference's default xgnn_poly basis, xgnn.py:16) and
+    RadialBasis(16) on the basis.npz batch."""
+    out = {}
+    b = pack_batch("", synthetic_molecules(2, "S160", seed=21), out)
+    d, tri, theta, _ = line_graph_inputs(ref, b)
+    env = ref.envelop.poly_envelop(cutoff=5.0, exponent=5)
+    sbf_layer = ref.angular_basis_layer.F_B_2D(7, 16, 5.0, 5)
+    rbf_layer = ref.radial_basis_layer.RadialBasis(cutoff=5.0, embedding_size=16)
+    with torch.no_grad():
+        out["dist"] = d.numpy()
+        out["theta"] = theta.numpy()
+        out["trip"] = tri.numpy().astype(np.int32)
+        out["sbf"] = sbf_layer(d, theta, tri[0]).numpy()
+        out["rbf"] = (rbf_layer(d) * env(d)[:, None]).numpy()
+    np.savez_compressed(os.path.join(HERE, "basis_7x16.npz"), **out)
 
 
 def gen_conv1(ref):
@@ -282,6 +300,7 @@ def aid_molecules(k, seed=0):
 GENERATORS = {
     "triplets": lambda ref: gen_triplets(ref),
     "basis": lambda ref: gen_basis(ref),
+    "basis_7x16": lambda ref: gen_basis_7x16(ref),
     "conv1": lambda ref: gen_conv1(ref),
     "model_small": lambda ref: gen_model(ref, "model_small.npz", "poly", SMALL, n_mol=4, seed_mol=41, seed_w=201),
     "model_full": lambda ref: gen_model(ref, "model_full.npz", "poly", FULL, n_mol=2, seed_mol=42, seed_w=202,

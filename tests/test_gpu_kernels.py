@@ -1,6 +1,8 @@
 """Kernel-level parity on the GPU: every libx2g.so operator against the reference fixtures and the
 CPU oracle on the same seeded inputs (integer work bit-exact, float work within stated
 tolerances)."""
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -167,6 +169,36 @@ def test_spherical_basis_vs_reference(cuda):
     orc = ref_cpu.spherical_basis(torch.from_numpy(z["dist"]), torch.from_numpy(z["theta"]),
                                   torch.from_numpy(z["trip"][0].astype(np.int64))).numpy()
     assert np.abs(sbf[:, :24] - orc[:, :24]).max() < 1e-4
+
+
+def test_spherical_basis_7x16_vs_reference(cuda):
+    """F_B_2D(7, 16) (the reference's default xgnn_poly basis): x2g_edge_basis / x2g_bessel_env /
+    x2g_spherical_basis at num_radial 16 against the reference's own output (basis_7x16.npz), and
+    RadialBasis(16) times the envelope."""
+    from x2gnn import ops
+
+    z = golden("basis_7x16.npz")
+    ei = z["edge_index"].astype(np.int64)
+    n = int(z["nodes"].sum())
+    lg = _lg(ei, n, z["trip"].shape[1], cuda)
+    pos = torch.from_numpy(z["atom_pos"]).to(cuda)
+    freq = (math.pi * torch.arange(1, 17, dtype=torch.float32)).to(cuda)
+    dist, env, rbf, bes = ops.edge_basis(pos, lg, freq, 5.0, 7, 16)
+    np.testing.assert_allclose(dist.cpu().numpy(), z["dist"], rtol=2e-6, atol=2e-6)
+    np.testing.assert_allclose(rbf.cpu().numpy(), z["rbf"], rtol=1e-5, atol=5e-5)
+    for radial in (bes, ops.bessel_env(dist, 5.0, 7, 16)):
+        sbf = ops.spherical_basis(pos, lg, radial, num_spherical=7, num_radial=16).cpu().numpy()
+        assert sbf.shape == z["sbf"].shape == (lg.T, 112)
+        for l in range(7):
+            blk = slice(16 * l, 16 * l + 16)
+            # the 16-wide blocks reach |sbf| ~ 15 (vs ~ 3 at 7 x 6): a relative term of 2 ulp-ish on top
+            tol = BASIS_TOL[l] + 2e-6 * np.abs(z["sbf"][:, blk]).max()
+            assert np.abs(sbf[:, blk] - z["sbf"][:, blk]).max() < tol, l
+    sbf2 = ops.spherical_basis_from_angles(torch.from_numpy(z["theta"]).to(cuda), lg.trip_src, bes, 7, 16).cpu().numpy()
+    for l in range(7):
+        blk = slice(16 * l, 16 * l + 16)
+        tol = BASIS_TOL[l] + 2e-6 * np.abs(z["sbf"][:, blk]).max()
+        assert np.abs(sbf2[:, blk] - z["sbf"][:, blk]).max() < tol, l
 
 
 def test_radial_parts_vs_reference(cuda):

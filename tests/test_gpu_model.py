@@ -179,6 +179,46 @@ def test_reference_default_width_256_vs_oracle(cuda, model_kind):
         assert float((got - rg).abs().max()) <= 2e-3 * float(rg.abs().max()) + 1e-6 * scale, n
 
 
+@pytest.mark.parametrize("model_kind", ["poly", "global"])
+def test_reference_defaults_no_arguments_vs_oracle(cuda, model_kind):
+    """``xgnn_poly()`` / ``xgnn_poly_global()`` with the reference constructor's OWN defaults
+    (conv_layers=4, sbf_dim=7, rbf_dim=16, in_channels=256, heads=16, embedding_size=128;
+    xgnn.py:16 / :78): the 7 x 16 = 112-wide spherical basis, RadialBasis(16), D=256 attention
+    (16 channels per head), the generic dense kernels for every shape outside the fused set.
+    Energies within 1e-4 relative and every parameter gradient within 2e-3 vs the oracle."""
+    import x2gnn
+    from x2gnn.data import collate
+    from x2gnn.synth import synthetic_molecules
+
+    b = collate(synthetic_molecules(4, "S160", seed=23))
+    if model_kind == "poly":
+        m = x2gnn.xgnn_poly(device="cuda")
+        orc = ref_cpu.XGNN(conv_layers=4, sbf_dim=7, rbf_dim=16, in_channels=256, heads=16, embedding_size=128)
+    else:
+        m = x2gnn.xgnn_poly_global(device="cuda")
+        orc = ref_cpu.XGNN(conv_layers=4, sbf_dim=7, rbf_dim=16, in_channels=256, heads=16, embedding_size=128,
+                           global_pool="mean")
+    assert m.sbf_layer.num_radial == 16 and m.fin_model.convs[0].lin_sbf.weight.shape == (256, 112)
+    load_seeded(orc, 6)
+    load_seeded(m, 6)
+    m = m.to(cuda)
+    ref = ref_cpu.run_batch(orc, b)
+    torch.nn.functional.smooth_l1_loss(ref, b.y).backward()
+    bd = b.to(cuda)
+    res = m(bd)
+    torch.nn.functional.smooth_l1_loss(res, bd.y).backward()
+    assert rel_err(res.detach().cpu().numpy(), ref.detach().numpy()) < ENERGY_RTOL
+    ref_grads = {n: p.grad for n, p in orc.named_parameters()}
+    scale = max(float(g.abs().max()) for g in ref_grads.values() if g is not None)
+    for n, p in m.named_parameters():
+        rg = ref_grads.get(n)
+        if rg is None:
+            assert p.grad is None or float(p.grad.abs().max()) == 0.0, n
+            continue
+        got = p.grad.detach().cpu()
+        assert float((got - rg).abs().max()) <= 2e-3 * float(rg.abs().max()) + 1e-6 * scale, n
+
+
 def test_full_size_properties(cuda):
     """B=128 S160 (BASELINE config 2): finite outputs, loss decreases under one SGD step,
     per-molecule energies invariant to batch composition (molecules are independent)."""

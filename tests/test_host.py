@@ -83,18 +83,22 @@ def test_generated_basis_constants_vs_oracle():
 
     from oracle import ref_cpu
 
-    np.testing.assert_allclose(np.array(bc.ZEROS), ref_cpu._ZEROS, rtol=0, atol=0)
+    nrad = bc.NUM_RADIAL  # 16: compiled maximum (F_B_2D(7, 16) is the reference's default)
+    np.testing.assert_allclose(np.array(bc.ZEROS), ref_cpu._basis_consts(7, nrad)[0], rtol=0, atol=0)
+    # the config.json basis (7 x 6) uses the first 6 columns: the same float32 zeros
+    np.testing.assert_allclose(np.array(bc.ZEROS)[:, :6], ref_cpu._basis_consts(7, 6)[0], rtol=0, atol=0)
     x = np.linspace(0.15, 1.0, 61)
-    ref = ref_cpu.bessel_radial(x)
+    ref = ref_cpu.bessel_radial(x, 7, nrad)
     coef = np.array(bc.COEF)
     for l in range(7):
-        for n in range(6):
+        for n in range(nrad):
             z = bc.ZEROS[l][n]
             acc = np.zeros_like(x)
             for m in range(l, -1, -1):
                 trig = np.sin(z * x) if m % 2 == 0 else np.cos(z * x)
                 acc += coef[l, n, m] * x ** m * trig
-            np.testing.assert_allclose(acc / x ** (l + 1), ref[:, 6 * l + n], rtol=1e-6, atol=1e-9)
+            # the expanded Rayleigh form cancels at small z x (worst at l = 6, n = 0): fp64 here
+            np.testing.assert_allclose(acc / x ** (l + 1), ref[:, nrad * l + n], rtol=1e-6, atol=1e-8)
     y = np.array(bc.YCOEF)
     c = np.cos(np.linspace(0, math.pi, 17))
     for l in range(7):

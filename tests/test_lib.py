@@ -53,13 +53,22 @@ def test_status_strings_and_workspace_query():
     ("x2g_segment_sum", (None, None, None, -1, 128, None, None)),
     ("x2g_segment_sum", (None, None, None, 4, 0, None, None)),
     ("x2g_graph_layernorm_fwd", (None, None, -3, 128, 1e-8, None, None, None, None)),
-    ("x2g_bessel_env", (None, 10, -1.0, None, None)),
+    ("x2g_bessel_env", (None, 10, -1.0, 7, 6, None, None)),
 ])
 def test_argument_validation_without_gpu(name, args):
     from x2gnn import _lib
 
     fn = getattr(_lib.load(), name)
     assert fn(*args) == 1001
+
+
+@pytest.mark.parametrize("nsph,nrad", [(8, 6), (7, 17), (0, 6), (7, 0)])
+def test_basis_rejects_uncompiled_shapes(nsph, nrad):
+    """F_B_2D is compiled for num_spherical <= 7, num_radial <= 16 (the reference default 7 x 16)."""
+    from x2gnn import _lib
+
+    p = ctypes.c_void_p(16)  # never dereferenced: the shape check fails first
+    assert _lib.load().x2g_bessel_env(p, 4, 5.0, nsph, nrad, p, None) == 1002
 
 
 def test_attention_rejects_uncompiled_shapes():

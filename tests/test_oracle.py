@@ -49,7 +49,7 @@ def test_envelope_known_answers():
 
 
 def test_basis_constants_known_answers():
-    assert np.allclose(ref_cpu._ZEROS[0], np.pi * np.arange(1, 7), rtol=1e-7)   # z_0n = n pi
+    assert np.allclose(ref_cpu._basis_consts(7, 6)[0][0], np.pi * np.arange(1, 7), rtol=1e-7)   # z_0n = n pi
     y = ref_cpu.sph_y0(np.array([0.3]))
     assert abs(y[0, 0] - 1 / (2 * np.sqrt(np.pi))) < 1e-12                      # Y_00 = 1/(2 sqrt(pi))
 
@@ -107,3 +107,13 @@ def test_model_vs_reference(fixture):
         if "grad." + n in z.files:
             ref = z["grad." + n]
             assert np.abs(p.grad.numpy() - ref).max() <= 2e-3 * np.abs(ref).max() + 1e-6 * scale, n
+
+
+def test_spherical_basis_7x16_vs_reference():
+    """The oracle's F_B_2D(7, 16) (the reference's default basis, xgnn.py:16) against the
+    reference's own fp32 output: within 1e-4 (the reference's fp32 expansion vs fp64 scipy)."""
+    z = golden("basis_7x16.npz")
+    sbf = ref_cpu.spherical_basis(torch.from_numpy(z["dist"]), torch.from_numpy(z["theta"]),
+                                  torch.from_numpy(z["trip"][0].astype(np.int64)), 7, 16).numpy()
+    assert sbf.shape == z["sbf"].shape
+    assert np.abs(sbf - z["sbf"]).max() < 1e-4

@@ -940,8 +940,10 @@ __global__ void __launch_bounds__(256) sbf_project_waves(const float* __restrict
 
 X2G_API int x2g_sbf_project(const float* sbf, int64_t T, int32_t sbf_dim, const float* w_sbf, const float* b_sbf,
                             int32_t out_dim, float* sbfproj, void* stream) {
-  if (T < 0 || out_dim <= 0) return X2G_EINVAL;
-  if (sbf_dim != kS) return X2G_EUNSUPPORTED;
+  if (T < 0 || out_dim <= 0 || sbf_dim <= 0) return X2G_EINVAL;
+  // other basis sizes (e.g. the reference's default F_B_2D(7, 16): sbf_dim 112) take the generic
+  // fused dense kernels (x2g_dense_fwd: any K, N; no activation, no residual)
+  if (sbf_dim != kS) return x2g_dense_fwd(sbf, w_sbf, b_sbf, T, sbf_dim, out_dim, 0, nullptr, sbfproj, nullptr, stream);
   if (T == 0) return X2G_OK;
   if (!sbf || !w_sbf || !b_sbf || !sbfproj) return X2G_EINVAL;
   hipStream_t st = as_stream(stream);

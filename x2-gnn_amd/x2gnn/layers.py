@@ -95,27 +95,30 @@ class RadialBasis(nn.Module):
 class F_B_2D(nn.Module):
     """Spherical-Bessel x Y_l0 basis, [T, num_spherical*num_radial], l-major columns.
 
-    Only (num_spherical, num_radial) = (7, 6) is compiled (config.json); the expanded
-    formulas' coefficients come from scripts/gen_basis_consts.py.
+    Compiled for num_spherical <= 7 and num_radial <= 16 (config.json: 7 x 6; the reference's
+    default xgnn_poly: 7 x 16, xgnn.py:16) with envelope exponent 5; the expanded formulas'
+    coefficients come from scripts/gen_basis_consts.py (no sympy at run time).
     """
 
     def __init__(self, num_spherical, num_radial, cutoff, envelope_exponent=5):
         super().__init__()
-        if (num_spherical, num_radial) != (7, 6) or envelope_exponent != 5:
-            raise NotImplementedError("compiled basis: num_spherical=7, num_radial=6, envelope exponent 5")
+        if not (1 <= num_spherical <= 7 and 1 <= num_radial <= 16) or envelope_exponent != 5:
+            raise NotImplementedError("compiled basis: num_spherical <= 7, num_radial <= 16, envelope exponent 5")
         self.num_spherical, self.num_radial, self.cutoff = num_spherical, num_radial, cutoff
 
     def radial(self, d):
-        """[E, 42] env(d) * N_ln j_l(z_ln d / cutoff) (the E-row half of the reference forward)."""
-        return ops.bessel_env(d, self.cutoff)
+        """[E, S] env(d) * N_ln j_l(z_ln d / cutoff) (the E-row half of the reference forward)."""
+        return ops.bessel_env(d, self.cutoff, self.num_spherical, self.num_radial)
 
     def forward(self, d, Angles, edge_index_1):
-        return ops.spherical_basis_from_angles(Angles, edge_index_1, self.radial(d))
+        return ops.spherical_basis_from_angles(Angles, edge_index_1, self.radial(d), self.num_spherical,
+                                               self.num_radial)
 
     def from_positions(self, d, pos, line_graph, radial=None):
         """Fast path: angles computed in-kernel from the triplets' atom positions (xgnn.py:61-65);
         ``radial`` = precomputed ``self.radial(d)`` (x2g_edge_basis writes it)."""
-        return ops.spherical_basis(pos, line_graph, self.radial(d) if radial is None else radial)
+        return ops.spherical_basis(pos, line_graph, self.radial(d) if radial is None else radial,
+                                   num_spherical=self.num_spherical, num_radial=self.num_radial)
 
 
 class _ScaleGradByCount(torch.autograd.Function):

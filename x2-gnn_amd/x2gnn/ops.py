@@ -134,12 +134,12 @@ def csr_rowptr(sorted_keys, num_segments: int):
 
 
 # ---------------------------------------------------------------------------------- basis
-def bessel_env(dist, cutoff: float = 5.0):
-    """[E] distances -> [E, 42] env(d) * N_ln j_l(z_ln d / cutoff)."""
+def bessel_env(dist, cutoff: float = 5.0, num_spherical: int = 7, num_radial: int = 6):
+    """[E] distances -> [E, num_spherical * num_radial] env(d) * N_ln j_l(z_ln d / cutoff)."""
     _need_cuda(dist)
     d = _f32(dist)
-    out = torch.empty(d.shape[0], 42, dtype=torch.float32, device=d.device)
-    call("x2g_bessel_env", ptr(d), d.shape[0], float(cutoff), ptr(out), stream_ptr())
+    out = torch.empty(d.shape[0], num_spherical * num_radial, dtype=torch.float32, device=d.device)
+    call("x2g_bessel_env", ptr(d), d.shape[0], float(cutoff), num_spherical, num_radial, ptr(out), stream_ptr())
     return out
 
 
@@ -148,13 +148,13 @@ class _EdgeBasis(torch.autograd.Function):
     (x2g_edge_basis); the backward gives the RadialBasis.frequencies gradient."""
 
     @staticmethod
-    def forward(ctx, freq, pos, lg, cutoff):
+    def forward(ctx, freq, pos, lg, cutoff, nsph, nrad):
         E, R = lg.E, freq.shape[0]
         f32 = dict(dtype=torch.float32, device=pos.device)
         dist, env = torch.empty(E, **f32), torch.empty(E, **f32)
-        rbf, bes = torch.empty(E, R, **f32), torch.empty(E, 42, **f32)
+        rbf, bes = torch.empty(E, R, **f32), torch.empty(E, nsph * nrad, **f32)
         call("x2g_edge_basis", ptr(_f32(pos)), ptr(lg.edge_src), ptr(lg.edge_dst), E, float(cutoff), ptr(_f32(freq)), R,
-             ptr(dist), ptr(env), ptr(rbf), ptr(bes), stream_ptr())
+             nsph, nrad, ptr(dist), ptr(env), ptr(rbf), ptr(bes), stream_ptr())
         ctx.save_for_backward(dist, env, freq)
         ctx.freq_param = freq  # the Parameter object itself (grad_sink looks at its attributes)
         ctx.cutoff = float(cutoff)
@@ -165,7 +165,7 @@ class _EdgeBasis(torch.autograd.Function):
     @staticmethod
     def backward(ctx, _gd, _ge, grbf, _gb):
         if grbf is None or not ctx.needs_input_grad[0]:
-            return None, None, None, None
+            return None, None, None, None, None, None
         dist, env, freq = ctx.saved_tensors
         E, R = dist.shape[0], freq.shape[0]
         lib = _lib.load()
@@ -179,18 +179,20 @@ class _EdgeBasis(torch.autograd.Function):
              flags, ptr(ws), ws_bytes, stream_ptr())
         if defer:
             _defer_job(ws, 0, int(lib.x2g_edge_basis_freq_grad_splits(E)), R, 0, dfreq, None)
-        return (None if sink is not None else dfreq), None, None, None
+        return (None if sink is not None else dfreq), None, None, None, None, None
 
 
-def edge_basis(pos, lg: LineGraph, freq, cutoff: float = 5.0):
-    """(dist [E], env [E], rbf_env [E, R] = sin(freq d / cutoff) env, bessel_env [E, 42]) for the
-    line graph's directed edges; rbf_env carries the gradient to ``freq`` (xgnn.py:49-53,66-70)."""
+def edge_basis(pos, lg: LineGraph, freq, cutoff: float = 5.0, num_spherical: int = 7, num_radial: int = 6):
+    """(dist [E], env [E], rbf_env [E, R] = sin(freq d / cutoff) env, bessel_env [E, num_spherical *
+    num_radial]) for the line graph's directed edges; rbf_env carries the gradient to ``freq``
+    (xgnn.py:49-53,66-70)."""
     _need_cuda(pos, freq)
-    return _EdgeBasis.apply(freq, pos, lg, cutoff)
+    return _EdgeBasis.apply(freq, pos, lg, cutoff, int(num_spherical), int(num_radial))
 
 
-def spherical_basis(pos, lg: LineGraph, rbf_env, want_cos=False):
-    """[T, 42] sbf = rbf_env[src] * Y_l0(theta), theta from the triplet's atom positions.
+def spherical_basis(pos, lg: LineGraph, rbf_env, want_cos=False, num_spherical: int = 7, num_radial: int = 6):
+    """[T, S] sbf = rbf_env[src] * Y_l0(theta) (S = num_spherical * num_radial, l-major), theta from
+    the triplet's atom positions.
 
     When gradients are being recorded the two factors are kept on the line graph
     (``lg.sbf_factors = (sbf, rbf_env, Y[T, 8])``): the attention backward then folds lin_sbf's
@@ -199,23 +201,25 @@ def spherical_basis(pos, lg: LineGraph, rbf_env, want_cos=False):
     _need_cuda(pos, rbf_env)
     pos = _f32(pos)
     rbf_env = _f32(rbf_env)
-    out = torch.empty(lg.T, 42, dtype=torch.float32, device=pos.device)
+    S = num_spherical * num_radial
+    out = torch.empty(lg.T, S, dtype=torch.float32, device=pos.device)
     cos_t = torch.empty(lg.T, dtype=torch.float32, device=pos.device) if want_cos else None
-    ylm = torch.empty(lg.T, 8, dtype=torch.float32, device=pos.device) if _FOLD_SBF and torch.is_grad_enabled() else None
+    fold = _FOLD_SBF and torch.is_grad_enabled() and (num_spherical, num_radial) == FOLD_BASIS
+    ylm = torch.empty(lg.T, 8, dtype=torch.float32, device=pos.device) if fold else None
     call("x2g_spherical_basis", ptr(pos), ptr(lg.atom_i), ptr(lg.atom_j), ptr(lg.atom_k), None, ptr(lg.trip_src),
-         ptr(rbf_env), lg.T, ptr(out), ptr(cos_t), ptr(ylm), stream_ptr())
+         ptr(rbf_env), lg.T, num_spherical, num_radial, ptr(out), ptr(cos_t), ptr(ylm), stream_ptr())
     lg.sbf_factors = (out, rbf_env, ylm) if ylm is not None else None
     return (out, cos_t) if want_cos else out
 
 
-def spherical_basis_from_angles(theta, trip_src, rbf_env):
-    """[T, 42] sbf = rbf_env[trip_src] * Y_l0(theta) for given angles (F_B_2D signature)."""
+def spherical_basis_from_angles(theta, trip_src, rbf_env, num_spherical: int = 7, num_radial: int = 6):
+    """[T, S] sbf = rbf_env[trip_src] * Y_l0(theta) for given angles (F_B_2D signature)."""
     _need_cuda(theta, trip_src, rbf_env)
     th = _f32(theta)
     src = _i32(trip_src)
-    out = torch.empty(th.shape[0], 42, dtype=torch.float32, device=th.device)
-    call("x2g_spherical_basis", None, None, None, None, ptr(th), ptr(src), ptr(_f32(rbf_env)), th.shape[0], ptr(out),
-         None, None, stream_ptr())
+    out = torch.empty(th.shape[0], num_spherical * num_radial, dtype=torch.float32, device=th.device)
+    call("x2g_spherical_basis", None, None, None, None, ptr(th), ptr(src), ptr(_f32(rbf_env)), th.shape[0],
+         num_spherical, num_radial, ptr(out), None, None, stream_ptr())
     return out
 
 
@@ -224,11 +228,13 @@ def spherical_basis_from_angles(theta, trip_src, rbf_env):
 # backward + [T, D] d_sbfproj + T-row weight GEMM (kept for the drop-in conv API, whose sbf is
 # an arbitrary [T, 42] tensor).
 _FOLD_SBF = os.environ.get("X2G_FOLD_SBF", "1") == "1"
+FOLD_BASIS = (7, 6)  # the (num_spherical, num_radial) the folded kernels are compiled for (sbf_dim 42)
 
 
 def _sbf_factors(lg, sbf, edge_mode, D, edge, edge_row):
     fac = getattr(lg, "sbf_factors", None)
-    if fac is None or fac[0] is not sbf or edge_mode == EDGE_PER_TRIPLET or D not in (32, 64, 128):
+    if (fac is None or fac[0] is not sbf or edge_mode == EDGE_PER_TRIPLET or D not in (32, 64, 128)
+            or sbf.shape[1] != FOLD_BASIS[0] * FOLD_BASIS[1]):
         return None
     if edge_mode == EDGE_PER_DST and (edge_row is None or edge is None or edge.shape[0] > 16):
         return None  # the source pass stages the per-destination edge table in LDS

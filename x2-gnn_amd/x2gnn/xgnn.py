@@ -54,7 +54,8 @@ class _XGNNBase(nn.Module):
         lg = plan.lg
         pos = data.atom_pos
         if self._fused_basis():  # distances, envelope, radial basis and the 42 Bessel terms: one kernel
-            dist, env, node_rbf, bessel = ops.edge_basis(pos, lg, self.rbf_layer.frequencies, self.cutoff)
+            dist, env, node_rbf, bessel = ops.edge_basis(pos, lg, self.rbf_layer.frequencies, self.cutoff,
+                                                         self.sbf_layer.num_spherical, self.sbf_layer.num_radial)
             env = env.unsqueeze(1)
         else:
             dist = (pos.index_select(0, lg.edge_src) - pos.index_select(0, lg.edge_dst)).norm(dim=1)
