@@ -21,7 +21,7 @@ res = {name: [] for name, _ in variants}
 for r in range(rounds):
     for name, env in variants:
         e = dict(os.environ, **env)
-        out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--step-only", "--steps", "60",
+        out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--step-only", "--steps", "200",
                               "--warmup", "10"], env=e, capture_output=True, text=True, timeout=300)
         line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
         if out.returncode != 0 or not line:

@@ -361,6 +361,51 @@ def test_conv_attention_weights(cuda):
     np.testing.assert_allclose(sums[has], 1.0, atol=1e-5)
 
 
+def test_conv_accepts_unsorted_triplets(cuda):
+    """PyG's propagate takes triplets in any order: the drop-in conv on a shuffled edge_index (sbf
+    and per-triplet edge_attr rows shuffled alike) equals the reference's sorted-order output and
+    gradients (the same per-destination sums up to summation order), and its attention weights come
+    back in the caller's order."""
+    z = golden("conv1.npz")
+    conv = _product_conv(z, cuda)
+    T = z["trip"].shape[1]
+    perm = torch.from_numpy(np.random.default_rng(4).permutation(T)).to(cuda)
+    trip = torch.from_numpy(z["trip"].astype(np.int64)).to(cuda)
+    sbf = torch.from_numpy(z["sbf"]).to(cuda)
+    rbf = torch.from_numpy(z["rbf"]).to(cuda)
+    x = torch.from_numpy(z["conv_x"]).to(cuda).requires_grad_(True)
+    ea = torch.from_numpy(z["conv_edge_attr"]).to(cuda)
+    ea_p = ea.index_select(0, perm).requires_grad_(True)
+    out, (ei, alpha) = conv(sbf.index_select(0, perm), rbf, x, trip.index_select(1, perm), ea_p,
+                            return_attention_weights=True)
+    assert rel_err(out.detach().cpu().numpy(), z["out"]) < 1e-5
+    assert torch.equal(ei, trip.index_select(1, perm))
+    _, (_, alpha_sorted) = conv(sbf, rbf, x.detach(), trip, ea, return_attention_weights=True)
+    torch.testing.assert_close(alpha, alpha_sorted.index_select(0, perm), rtol=1e-6, atol=1e-7)
+    (out * torch.from_numpy(z["upstream"]).to(cuda)).sum().backward()
+    assert rel_err(x.grad.cpu().numpy(), z["grad_x"]) < 1e-4
+    inv = torch.argsort(perm)
+    assert rel_err(ea_p.grad.index_select(0, inv).cpu().numpy(), z["grad_edge_attr"]) < 1e-4
+
+
+def test_scatter_add_any_index_order(cuda):
+    """ops.scatter_add == torch_scatter.scatter_add(src, index, dim=0, dim_size) for a shuffled
+    index with empty segments (fp64 torch reference), forward and the gradient of src."""
+    from x2gnn import ops
+
+    g = torch.Generator().manual_seed(8)
+    idx = torch.randint(0, 50, (900,), generator=g)
+    idx[idx == 7] = 8  # an empty segment
+    src = torch.randn(900, 64, generator=g)
+    ref = torch.zeros(60, 64, dtype=torch.float64).index_add_(0, idx, src.double())
+    s = src.to(cuda).requires_grad_(True)
+    out = ops.scatter_add(s, idx.to(cuda), 60)
+    torch.testing.assert_close(out.double().cpu(), ref, rtol=1e-5, atol=1e-5)
+    up = torch.randn(60, 64, generator=g)
+    (out * up.to(cuda)).sum().backward()
+    torch.testing.assert_close(s.grad.cpu(), up.index_select(0, idx), rtol=0, atol=0)
+
+
 def test_per_destination_edge_table_equals_per_triplet(cuda):
     """EDGE_PER_DST (table row per destination) == EDGE_PER_TRIPLET with the expanded rows."""
     from x2gnn import ops

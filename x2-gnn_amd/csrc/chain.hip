@@ -108,13 +108,15 @@ __device__ __forceinline__ float bload1(rsrc_t r, int voff_bytes, int soff_bytes
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff_bytes, soff_bytes, 0));
 }
 
-// rows [r0, r0 + nrows) of a row-major [R, 128] tensor (+ a second one) -> image (rows >= nrows zero)
+// rows [r0, r0 + nrows) of a row-major [R, 128] tensor (+ a second one) -> image (rows >= nrows zero);
+// RB row blocks of 16 rows (the image's height)
+template <int RB = kV2RB>
 __device__ __forceinline__ void stage_rows(f4* __restrict__ img, const float* __restrict__ P,
                                            const float* __restrict__ P2, int r0, int nrows) {
   const int tid = threadIdx.x;
-  f4 v[kV2RB];
+  f4 v[RB];
 #pragma unroll
-  for (int u = 0; u < kV2RB; ++u) {
+  for (int u = 0; u < RB; ++u) {
     const int q = tid + kCThreads * u, r = q >> 5, c = q & 31;
     const bool ok = r < nrows;
     const int rr = r0 + (ok ? r : 0);
@@ -122,19 +124,39 @@ __device__ __forceinline__ void stage_rows(f4* __restrict__ img, const float* __
     if (P2) v[u] += *reinterpret_cast<const f4*>(P2 + rr * kCD + 4 * c) * (ok ? 1.0f : 0.0f);
   }
 #pragma unroll
-  for (int u = 0; u < kV2RB; ++u) {
+  for (int u = 0; u < RB; ++u) {
     const int q = tid + kCThreads * u;
     img[ipos(q >> 5, q & 31)] = v[u];
   }
 }
 
 // image rows < nrows -> global rows [r0, r0 + nrows), full 512-byte rows per half-wave
+template <int RB = kV2RB>
 __device__ __forceinline__ void store_img(float* __restrict__ P, const f4* __restrict__ img, int r0, int nrows) {
   const int tid = threadIdx.x;
 #pragma unroll
-  for (int u = 0; u < kV2RB; ++u) {
+  for (int u = 0; u < RB; ++u) {
     const int q = tid + kCThreads * u, r = q >> 5, c = q & 31;
     if (r < nrows) *reinterpret_cast<f4*>(P + (r0 + r) * kCD + 4 * c) = img[ipos(r, c)];
+  }
+}
+
+// rows [r0, r0 + nrows) of a row-major [R, 128] tensor -> image, through global_load_lds (no
+// registers; the copies stay in flight while the caller computes): wave w's instruction u lands
+// 1 KB (64 lanes x 16 B) at image chunks 64 (8u + w) + lane, the swizzle applied to the SOURCE
+// address (chunk position p = 32 r + cs holds chunk cs ^ (r & 15) of row r).  Rows >= nrows repeat
+// row r0 (finite values; callers mask those rows' results).  The caller waits (s_waitcnt vmcnt)
+// and barriers before reading the image.
+template <int RB>
+__device__ __forceinline__ void stage_rows_async(f4* __restrict__ img, const float* __restrict__ P, int r0,
+                                                 int nrows) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int u = 0; u < RB; ++u) {
+    const int p0 = 64 * (kCWaves * u + w);
+    const int pp = p0 + lane, r = pp >> 5, c = (pp & 31) ^ (r & 15);
+    const int rr = r0 + (r < nrows ? r : 0);
+    __builtin_amdgcn_global_load_lds(P + static_cast<int64_t>(rr) * kCD + 4 * c, img + p0, 16, 0, 0);
   }
 }
 
@@ -165,12 +187,13 @@ __device__ __forceinline__ f4 quad_transpose(f4 v, int j) {
 // The wave's row-layout slice v[rb] (lane (rl, g): rows 16rb + rl, features 16w + 4g + e) -> the
 // T layout (tile t of the chunk at dst + (r0/16 + t) * 2048, element (r, f) at f * 16 + r % 16),
 // rows >= nrows written as zero; a wave's store is 1 KB contiguous (16 features x 16 rows).
-__device__ __forceinline__ void store_t_slice(float* __restrict__ dst, const f4 (&v)[kV2RB], int r0, int nrows, int w,
+template <int RB>
+__device__ __forceinline__ void store_t_slice(float* __restrict__ dst, const f4 (&v)[RB], int r0, int nrows, int w,
                                               int rl, int g) {
   const int j = rl & 3, m = rl >> 2, f = 16 * w + 4 * g + j;
   const int ntile = (nrows + 15) >> 4;
 #pragma unroll
-  for (int rb = 0; rb < kV2RB; ++rb) {
+  for (int rb = 0; rb < RB; ++rb) {
     f4 t = quad_transpose(v[rb], j);
 #pragma unroll
     for (int e = 0; e < 4; ++e)
@@ -200,24 +223,25 @@ __device__ __forceinline__ void load_slice(const float* W, int w, int rl, int g,
 
 // acc[rb] = the wave's 16 output features of row block rb: sum over k of A (weight slice) and
 // the image rows; the image chunks of step group b + 1 are read before group b's MFMAs
-__device__ __forceinline__ void slice_gemm(const f4* __restrict__ img, const f4 (&A)[8], f4 (&acc)[kV2RB], int rl,
+template <int RB>
+__device__ __forceinline__ void slice_gemm(const f4* __restrict__ img, const f4 (&A)[8], f4 (&acc)[RB], int rl,
                                            int g) {
 #pragma unroll
-  for (int rb = 0; rb < kV2RB; ++rb) acc[rb] = zero4();
-  f4 bo[2][kV2RB];
+  for (int rb = 0; rb < RB; ++rb) acc[rb] = zero4();
+  f4 bo[2][RB];
 #pragma unroll
-  for (int rb = 0; rb < kV2RB; ++rb) bo[0][rb] = img[(16 * rb + rl) * 32 + (g ^ rl)];
+  for (int rb = 0; rb < RB; ++rb) bo[0][rb] = img[(16 * rb + rl) * 32 + (g ^ rl)];
 #pragma unroll
   for (int b = 0; b < 8; ++b) {
     const int cur = b & 1;
     if (b + 1 < 8) {
 #pragma unroll
-      for (int rb = 0; rb < kV2RB; ++rb) bo[cur ^ 1][rb] = img[(16 * rb + rl) * 32 + ((4 * (b + 1) + g) ^ rl)];
+      for (int rb = 0; rb < RB; ++rb) bo[cur ^ 1][rb] = img[(16 * rb + rl) * 32 + ((4 * (b + 1) + g) ^ rl)];
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
-      for (int rb = 0; rb < kV2RB; ++rb)
+      for (int rb = 0; rb < RB; ++rb)
         acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[b][e], bo[cur][rb][e], acc[rb], 0, 0, 0);
   }
 }
@@ -888,11 +912,12 @@ struct ProjFwdArgs {
   int64_t R;
 };
 
+template <int RB>
 __device__ __forceinline__ void load_rows_slice(const float* P, int r0, int nrows, int w, int rl, int g,
-                                                f4 (&v)[kV2RB]) {
+                                                f4 (&v)[RB]) {
   const rsrc_t pr = rsrc(P);
 #pragma unroll
-  for (int rb = 0; rb < kV2RB; ++rb) {
+  for (int rb = 0; rb < RB; ++rb) {
     const int r = 16 * rb + rl;
     const bool ok = r < nrows;
     v[rb] = bload4(pr, 4 * ((r0 + (ok ? r : 0)) * kCD + 16 * w + 4 * g), 0) * (ok ? 1.0f : 0.0f);
@@ -900,10 +925,10 @@ __device__ __forceinline__ void load_rows_slice(const float* P, int r0, int nrow
 }
 
 // rows of rbf [R, RR] -> srbf[row * NJ + j] (zero beyond RR / nrows); W_rbf [D, RR] -> swr[c * NJ + j]
-template <int NJ>
+template <int NJ, int RB = kV2RB>
 __device__ __forceinline__ void stage_rbf(float* __restrict__ srbf, const float* __restrict__ rbf, int RR, int r0,
                                           int nrows) {
-  for (int i = threadIdx.x; i < kV2RB * 16 * NJ; i += kCThreads) {
+  for (int i = threadIdx.x; i < RB * 16 * NJ; i += kCThreads) {
     const int r = i / NJ, j = i % NJ;
     srbf[i] = (r < nrows && j < RR) ? rbf[static_cast<int64_t>(r0 + r) * RR + j] : 0.0f;
   }
@@ -923,15 +948,15 @@ __device__ __forceinline__ f4 gate_filter(const float* __restrict__ srbf, const 
   return f;
 }
 
-template <int NJ>
-__global__ void __launch_bounds__(kCThreads, 1) conv_proj_fwd_kernel(const ProjFwdArgs a) {
-  __shared__ f4 img[2][kV2Img];  // x, x_src
-  __shared__ float srbf[kV2RB * 16 * NJ];
+template <int NJ, int RB = kV2RB, int WPC = 1>  // RB row blocks per chunk, WPC workgroups per CU (2 WPC waves / SIMD)
+__global__ void __launch_bounds__(kCThreads, 2 * WPC) conv_proj_fwd_kernel(const ProjFwdArgs a) {
+  __shared__ f4 img[2][RB * 16 * 32];  // x, x_src
+  __shared__ float srbf[RB * 16 * NJ];
   __shared__ float swr[kCD * NJ];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int rl = lane & 15, g = lane >> 4;
   const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
-  const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
+  const int64_t nch = (nblk + RB * G - 1) / (RB * G) * G;
   const int64_t wt_groups = G < 8 ? G : 8;
   for (int i = tid; i < kCD * NJ; i += kCThreads) {
     const int c = i / NJ, j = i % NJ;
@@ -941,15 +966,15 @@ __global__ void __launch_bounds__(kCThreads, 1) conv_proj_fwd_kernel(const ProjF
     int r0, nrows;
     chunk_rows(ch, nch, nblk, a.R, r0, nrows);
     __syncthreads();
-    stage_rows(img[0], a.x, nullptr, r0, nrows);
-    stage_rbf<NJ>(srbf, a.rbf, a.RR, r0, nrows);
+    stage_rows<RB>(img[0], a.x, nullptr, r0, nrows);
+    stage_rbf<NJ, RB>(srbf, a.rbf, a.RR, r0, nrows);
     f4 A[8];
     load_slice<false>(a.p[0].w, w, rl, g, A);
     __syncthreads();
     {
-      f4 xv[kV2RB], xs[kV2RB];
+      f4 xv[RB], xs[RB];
 #pragma unroll
-      for (int rb = 0; rb < kV2RB; ++rb) {
+      for (int rb = 0; rb < RB; ++rb) {
         const int r = 16 * rb + rl;
         xv[rb] = img[0][ipos(r, 4 * w + g)];
         xs[rb] = xv[rb] * gate_filter<NJ>(srbf, swr, r, 16 * w + 4 * g);
@@ -972,10 +997,10 @@ __global__ void __launch_bounds__(kCThreads, 1) conv_proj_fwd_kernel(const ProjF
 #pragma unroll
             for (int e = 0; e < 4; ++e) P.wt[(16 * b + 4 * g + e) * kCD + 16 * w + rl] = A[b][e];
       }
-      f4 acc[kV2RB];
+      f4 acc[RB];
       slice_gemm(img[(p == 1 || p == 2) ? 1 : 0], A, acc, rl, g);
 #pragma unroll
-      for (int rb = 0; rb < kV2RB; ++rb) {
+      for (int rb = 0; rb < RB; ++rb) {
         const int r = 16 * rb + rl;
         if (r < nrows) *reinterpret_cast<f4*>(P.out + (r0 + r) * kCD + 16 * w + 4 * g) = acc[rb] + bias;
       }
@@ -1073,17 +1098,17 @@ struct ProjBwdGateArgs {
   int64_t R;
 };
 
-template <int NJ>
-__global__ void __launch_bounds__(kCThreads, 1) conv_proj_bwd_gate_kernel(const ProjBwdGateArgs a) {
-  __shared__ f4 img[2][kV2Img];
-  __shared__ float srbf[kV2RB * 16 * NJ];
+template <int NJ, int RB = kV2RB, int WPC = 1>  // RB row blocks per chunk, WPC workgroups per CU (2 WPC waves / SIMD)
+__global__ void __launch_bounds__(kCThreads, 2 * WPC) conv_proj_bwd_gate_kernel(const ProjBwdGateArgs a) {
+  __shared__ f4 img[2][RB * 16 * 32];
+  __shared__ float srbf[RB * 16 * NJ];
   __shared__ float swr[kCD * NJ];
   __shared__ float sdw[kCD * NJ];                   // this workgroup's dW_rbf (owner lanes only)
-  __shared__ float red[kCWaves * kV2RB * 16 * NJ];  // drbf partials: [wave][row][j]
+  __shared__ float red[kCWaves * RB * 16 * NJ];  // drbf partials: [wave][row][j]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int rl = lane & 15, g = lane >> 4;
   const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
-  const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
+  const int64_t nch = (nblk + RB * G - 1) / (RB * G) * G;
   const int c0 = 16 * w + 4 * g;
   for (int i = tid; i < kCD * NJ; i += kCThreads) {
     const int c = i / NJ, j = i % NJ;
@@ -1101,9 +1126,9 @@ __global__ void __launch_bounds__(kCThreads, 1) conv_proj_bwd_gate_kernel(const 
   };
   auto t_copy = [&](int p, const f4* im, int r0, int nrows) {
     if (!a.gr[p].g_t) return;
-    f4 v[kV2RB];
+    f4 v[RB];
 #pragma unroll
-    for (int rb = 0; rb < kV2RB; ++rb) v[rb] = im[ipos(16 * rb + rl, 4 * w + g)];
+    for (int rb = 0; rb < RB; ++rb) v[rb] = im[ipos(16 * rb + rl, 4 * w + g)];
     store_t_slice(a.gr[p].g_t, v, r0, nrows, w, rl, g);
   };
   const rsrc_t ar = rsrc(a.dx_add ? a.dx_add : a.dx);  // read only when dx_add is given (no 0 * NaN)
@@ -1111,35 +1136,53 @@ __global__ void __launch_bounds__(kCThreads, 1) conv_proj_bwd_gate_kernel(const 
   for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
     int r0, nrows;
     chunk_rows(ch, nch, nblk, a.R, r0, nrows);
-    {  // (dk, dv) -> dxs -> the gate's three gradients
-      __syncthreads();  // images, srbf and red of the previous chunk are no longer read
-      stage_rows(img[0], a.gr[1].g, nullptr, r0, nrows);
-      stage_rows(img[1], a.gr[2].g, nullptr, r0, nrows);
-      stage_rbf<NJ>(srbf, a.rbf, a.RR, r0, nrows);
+    if (nrows <= 0) continue;  // (workgroup-uniform)
+    __syncthreads();  // images, srbf and red of the previous chunk are no longer read
+    // (dk, dv) -> dxs -> the gate's three gradients.  The two operand images come in through
+    // global_load_lds; the weight slices meanwhile into registers.
+    stage_rows_async<RB>(img[0], a.gr[1].g, r0, nrows);
+    stage_rows_async<RB>(img[1], a.gr[2].g, r0, nrows);
+    stage_rbf<NJ, RB>(srbf, a.rbf, a.RR, r0, nrows);
+    f4 acc[RB], t[RB];
+    {
       f4 A[8], An[8];
       load_ws(1, A);
       load_ws(2, An);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       t_copy(1, img[0], r0, nrows);
       t_copy(2, img[1], r0, nrows);
-      f4 acc[kV2RB], t[kV2RB];
       slice_gemm(img[0], A, acc, rl, g);
       slice_gemm(img[1], An, t, rl, g);
-      f4 xv[kV2RB];
-      load_rows_slice(a.x, r0, nrows, w, rl, g, xv);  // zero beyond nrows
+    }
+    // The epilogue's global reads (x; dx_add) are issued BEFORE the next operands' copies, so
+    // waiting for them (vmcnt counts in issue order) never waits for those copies.
+    f4 xv[RB], xa[RB];
+    load_rows_slice(a.x, r0, nrows, w, rl, g, xv);  // zero beyond nrows
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const int r = 16 * rb + rl;
+      xa[rb] = a.dx_add ? bload4(ar, 4 * ((r0 + (r < nrows ? r : 0)) * kCD + c0), 0) : zero4();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's product has read the images: refill them
+    // (dq, dskip) copies fly during the gate epilogue below
+    stage_rows_async<RB>(img[0], a.gr[0].g, r0, nrows);
+    stage_rows_async<RB>(img[1], a.gr[3].g, r0, nrows);
+    {
       float aw[4][NJ];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) aw[i][j] = 0.0f;
 #pragma unroll
-      for (int rb = 0; rb < kV2RB; ++rb) {
+      for (int rb = 0; rb < RB; ++rb) {
         const int r = 16 * rb + rl;
         const f4 dxs = acc[rb] + t[rb];
         if (r < nrows) {
           const int off = (r0 + r) * kCD + c0;
           const f4 gx = dxs * gate_filter<NJ>(srbf, swr, r, c0);
-          *reinterpret_cast<f4*>(a.dx + off) = a.dx_add ? bload4(ar, 4 * off, 0) + gx : gx;
+          *reinterpret_cast<f4*>(a.dx + off) = a.dx_add ? xa[rb] + gx : gx;
         }
         const f4 df = dxs * xv[rb];
 #pragma unroll
@@ -1154,7 +1197,7 @@ __global__ void __launch_bounds__(kCThreads, 1) conv_proj_bwd_gate_kernel(const 
             for (int i = 0; i < 4; ++i) p = fmaf(df[i], swr[(c0 + i) * NJ + j], p);
             p += __shfl_xor(p, 16);
             p += __shfl_xor(p, 32);
-            if (g == 0) red[(w * kV2RB * 16 + r) * NJ + j] = p;
+            if (g == 0) red[(w * RB * 16 + r) * NJ + j] = p;
           }
         }
       }
@@ -1171,35 +1214,32 @@ __global__ void __launch_bounds__(kCThreads, 1) conv_proj_bwd_gate_kernel(const 
         }
     }
     {  // (dq, dskip) -> dx
-      __syncthreads();  // images no longer read; red complete
+      f4 A[8], An[8];
+      load_ws(0, A);
+      load_ws(3, An);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // the copies have landed; red is complete
       if (a.drbf) {
         for (int i = tid; i < nrows * a.RR; i += kCThreads) {
           const int r = i / a.RR, j = i % a.RR;
           float s = 0.0f;
 #pragma unroll
-          for (int ww = 0; ww < kCWaves; ++ww) s += red[(ww * kV2RB * 16 + r) * NJ + j];
+          for (int ww = 0; ww < kCWaves; ++ww) s += red[(ww * RB * 16 + r) * NJ + j];
           float* d = a.drbf + static_cast<int64_t>(r0 + r) * a.RR + j;
           *d = a.drbf_acc ? *d + s : s;
         }
       }
-      stage_rows(img[0], a.gr[0].g, nullptr, r0, nrows);
-      stage_rows(img[1], a.gr[3].g, nullptr, r0, nrows);
-      f4 A[8], An[8];
-      load_ws(0, A);
-      load_ws(3, An);
-      __syncthreads();
       t_copy(0, img[0], r0, nrows);
       t_copy(3, img[1], r0, nrows);
-      f4 acc[kV2RB], t[kV2RB];
       slice_gemm(img[0], A, acc, rl, g);
       slice_gemm(img[1], An, t, rl, g);
+    }
 #pragma unroll
-      for (int rb = 0; rb < kV2RB; ++rb) {
-        const int r = 16 * rb + rl;
-        if (r < nrows) {
-          const int off = (r0 + r) * kCD + c0;
-          *reinterpret_cast<f4*>(a.dx + off) = bload4(dr, 4 * off, 0) + (acc[rb] + t[rb]);
-        }
+    for (int rb = 0; rb < RB; ++rb) {
+      const int r = 16 * rb + rl;
+      if (r < nrows) {
+        const int off = (r0 + r) * kCD + c0;
+        *reinterpret_cast<f4*>(a.dx + off) = bload4(dr, 4 * off, 0) + (acc[rb] + t[rb]);
       }
     }
   }
@@ -1474,6 +1514,19 @@ static inline unsigned v2_grid(int64_t rows) {
   return static_cast<unsigned>(nblk < 256 ? nblk : 256);
 }
 
+// the projection kernels' chunk height (row blocks) and workgroups per CU (compile-time A/B builds)
+#ifndef X2G_PROJ_RB
+#define X2G_PROJ_RB 6
+#endif
+#ifndef X2G_PROJ_WPC
+#define X2G_PROJ_WPC 1
+#endif
+constexpr int kProjRB = X2G_PROJ_RB, kProjWPC = X2G_PROJ_WPC;
+static inline unsigned proj_grid(int64_t rows) {
+  const int64_t nblk = (rows + 15) / 16, cap = 256 * kProjWPC;
+  return static_cast<unsigned>(nblk < cap ? nblk : cap);
+}
+
 X2G_API int x2g_conv_proj_fwd(const float* x, const float* rbf, int32_t rbf_dim, const float* w_rbf,
                               const x2g_proj* proj, int64_t rows, int32_t dim, float* x_t, float* xs_t, void* stream) {
   if (!proj || rows < 0 || dim <= 0 || rbf_dim <= 0) return X2G_EINVAL;
@@ -1495,9 +1548,9 @@ X2G_API int x2g_conv_proj_fwd(const float* x, const float* rbf, int32_t rbf_dim,
   }
   if (!al16(x) || !al16(x_t) || !al16(xs_t)) return X2G_EUNSUPPORTED;
   if (rbf_dim <= 6)
-    conv_proj_fwd_kernel<6><<<v2_grid(rows), kCThreads, 0, as_stream(stream)>>>(a);
+    conv_proj_fwd_kernel<6, kProjRB, kProjWPC><<<proj_grid(rows), kCThreads, 0, as_stream(stream)>>>(a);
   else
-    conv_proj_fwd_kernel<8><<<v2_grid(rows), kCThreads, 0, as_stream(stream)>>>(a);
+    conv_proj_fwd_kernel<8, kProjRB, kProjWPC><<<proj_grid(rows), kCThreads, 0, as_stream(stream)>>>(a);
   return last_launch_status();
 }
 
@@ -1522,11 +1575,11 @@ X2G_API int x2g_conv_proj_bwd(const x2g_proj_grad* grads, int64_t rows, int32_t 
   return last_launch_status();
 }
 
-X2G_API int32_t x2g_conv_proj_bwd_gate_splits(int64_t rows) { return rows > 0 ? static_cast<int32_t>(v2_grid(rows)) : 0; }
+X2G_API int32_t x2g_conv_proj_bwd_gate_splits(int64_t rows) { return rows > 0 ? static_cast<int32_t>(proj_grid(rows)) : 0; }
 
 X2G_API size_t x2g_conv_proj_bwd_gate_workspace(int64_t rows, int32_t rbf_dim) {
   if (rows <= 0 || rbf_dim <= 0) return 0;
-  return static_cast<size_t>(v2_grid(rows)) * kCD * rbf_dim * sizeof(float);
+  return static_cast<size_t>(proj_grid(rows)) * kCD * rbf_dim * sizeof(float);
 }
 
 X2G_API int x2g_conv_proj_bwd_gate(const x2g_proj_grad* grads, int64_t rows, int32_t dim, const float* x,
@@ -1562,11 +1615,11 @@ X2G_API int x2g_conv_proj_bwd_gate(const x2g_proj_grad* grads, int64_t rows, int
   a.RR = rbf_dim;
   a.drbf_acc = (flags & X2G_GATE_DRBF_ACCUM) ? 1 : 0;
   a.R = rows;
-  const unsigned grid = v2_grid(rows);
+  const unsigned grid = proj_grid(rows);
   if (rbf_dim <= 6)
-    conv_proj_bwd_gate_kernel<6><<<grid, kCThreads, 0, st>>>(a);
+    conv_proj_bwd_gate_kernel<6, kProjRB, kProjWPC><<<grid, kCThreads, 0, st>>>(a);
   else
-    conv_proj_bwd_gate_kernel<8><<<grid, kCThreads, 0, st>>>(a);
+    conv_proj_bwd_gate_kernel<8, kProjRB, kProjWPC><<<grid, kCThreads, 0, st>>>(a);
   const int rc = last_launch_status();
   if (rc || (flags & X2G_DEFER_SLAB_SUM)) return rc;
   x2g_slab_job sj{a.part_w, nullptr, dw_rbf, nullptr, static_cast<int64_t>(kCD) * rbf_dim, 0,

@@ -4,13 +4,15 @@ parameter names (so reference ``state_dict``s load unchanged).
 ================  =======================================  ==========================================
 class             reference                                 device path here
 ================  =======================================  ==========================================
-poly_envelop      envelop.py:5-21                           elementwise (E-sized, torch)
-RadialBasis       radial_basis_layer.py:26-40 (trainable)   elementwise (E-sized, torch autograd)
+poly_envelop      envelop.py:5-21                           fused into x2g_edge_basis
+RadialBasis       radial_basis_layer.py:26-40 (trainable)   x2g_edge_basis (+ its frequency gradient)
 F_B_2D            angular_basis_layer.py:51-93 (+sympy)      x2g_bessel_env + x2g_spherical_basis;
                                                             constants precomputed, no sympy at run time
-EmbeddingBlock    atom_embedding.py:10-25                    F.embedding, or the per-element table
-ResidualLayer     residual_layer.py:5-27                     hipBLASLt fp32 GEMMs
-AtomWise          readout.py:7-43                            lin_rbf GEMM + fused x2g_segment_sum(x*rf)
+EmbeddingBlock    atom_embedding.py:10-25                    per-element table (x2g_embedding_table)
+ResidualLayer     residual_layer.py:5-27                     fused f32-MFMA dense kernels (the trunk's
+                                                            seven tail layers: one row-chain kernel)
+AtomWise          readout.py:7-43                            x2g_rbf_pool (lin_rbf gate + pool fused) or
+                                                            lin_rbf + x2g_segment_sum(x * rf); MLP fused
 MolWise           readout.py:45-76                           + segment sum/mean over molecules
 ================  =======================================  ==========================================
 """

@@ -1870,6 +1870,20 @@ def segment_sum(x, rowptr, num_segments: int, mul=None):
     return out.squeeze(1) if squeeze else out
 
 
+def scatter_add(src, index, dim_size: int):
+    """torch_scatter.scatter_add(src, index, dim=0, dim_size=dim_size) (readout.py:37, model.py:53)
+    for ANY index order: a sorted index is reduced in place through the CSR segment sum; an
+    unsorted one is stably sorted first (its rows gathered in that order), so the per-segment
+    summation order is the caller's row order either way (deterministic, no float atomics)."""
+    _need_cuda(src, index)
+    idx = index.reshape(-1)
+    if idx.numel() > 1 and bool((idx[1:] < idx[:-1]).any()):
+        perm = torch.argsort(idx, stable=True)
+        idx = idx.index_select(0, perm)
+        src = src.index_select(0, perm)
+    return segment_sum(src, csr_rowptr(idx, int(dim_size)), int(dim_size))
+
+
 class _SegmentSoftmax(torch.autograd.Function):
     @staticmethod
     def forward(ctx, src, rowptr, n_seg):

@@ -9,9 +9,16 @@ reference (sbftransformer_conv.py:16-166, a PyG ``MessagePassing`` with aggr='ad
         m_t     = (v[src] + e_t) * lin_sbf(sbf_t) * alpha_t
     out[dst] = sum_t m_t  (+ lin_skip(x) with root_weight)
 
-The dense projections (q/k/v/skip/rbf/edge) stay fp32 GEMMs on hipBLASLt; everything per
-triplet (gathers, logits, softmax, the 42->H*C sbf projection, the weighted sum) runs in one
-kernel (``ops.sbf_attention``) without materialising a [T, H*C] tensor.
+The five projections (lin_rbf gate, q/k/v/skip) run as one fused f32-MFMA kernel each way
+(``ops.conv_projections``; the generic dense kernels for widths outside the compiled set).
+``lin_sbf(sbf)`` is materialised once per layer as S [T, H*C] (``x2g_sbf_project``), and
+everything else per triplet (gathers, logits, softmax, the weighted sum, the skip add) runs in
+one destination-major kernel (``ops.sbf_attention``); the backward folds lin_sbf's gradient per
+source line node instead of writing a [T, H*C] gradient (csrc/attention_fold.inc).
+
+Triplets may come in any order (PyG's ``propagate`` accepts any): an ``edge_index[1]`` that is
+not sorted is sorted here (stable) and the per-triplet inputs permuted alike; the attention
+weights, when requested, are returned in the caller's order.
 
 Extra keyword-only arguments for the in-framework fast path:
 ``line_graph`` (a prebuilt ``ops.LineGraph``), ``edge_row`` (when ``edge_attr`` is a small
@@ -71,9 +78,19 @@ class SBFTransformerConv(nn.Module):
             k = self.lin_key(x_src)
             v = self.lin_value(x_src)
             skip = self.lin_skip(x) if self.root_weight else torch.zeros_like(q)
+        perm = None
         if line_graph is None:
-            if edge_index.numel() > 1 and bool((edge_index[1, 1:] < edge_index[1, :-1]).any()):
-                raise ValueError("triplet edge_index[1] must be sorted ascending (vertex_to_edge_2 order)")
+            dst = edge_index[1]
+            if dst.numel() > 1 and bool((dst[1:] < dst[:-1]).any()):
+                # CSR by destination needs dst-sorted triplets (vertex_to_edge_2 emits them so; any
+                # other caller order is sorted here, stable, and the per-triplet inputs follow)
+                perm = torch.argsort(dst, stable=True)
+                edge_index = edge_index.index_select(1, perm)
+                sbf = sbf.index_select(0, perm)
+                if edge_attr is not None and edge_row is None and edge_proj is None:
+                    edge_attr = edge_attr.index_select(0, perm)
+                if edge_proj is not None and edge_row is None:
+                    edge_proj = edge_proj.index_select(0, perm)
             line_graph = ops.LineGraph.from_triplets(edge_index, x.shape[0])
         if edge_proj is not None:  # lin_edge(edge_attr) computed by the caller (the trunk's table chain)
             e = edge_proj
@@ -88,6 +105,9 @@ class SBFTransformerConv(nn.Module):
                                 edge_mode=mode, edge_row=edge_row, return_attention=want)
         if want:
             out, alpha = res
+            if perm is not None:  # back to the caller's triplet order
+                alpha = torch.empty_like(alpha).index_copy_(0, perm, alpha)
+                edge_index = torch.empty_like(edge_index).index_copy_(1, perm, edge_index)
             return out, (edge_index, alpha)
         return res
 
