@@ -141,23 +141,29 @@ __device__ __forceinline__ void store_img(float* __restrict__ P, const f4* __res
   }
 }
 
-// rows [r0, r0 + nrows) of a row-major [R, 128] tensor -> image, through global_load_lds (no
+// rows [r0, r0 + RB * 16) of a row-major [R, 128] tensor -> image, through buffer_load ... lds (no
 // registers; the copies stay in flight while the caller computes): wave w's instruction u lands
-// 1 KB (64 lanes x 16 B) at image chunks 64 (8u + w) + lane, the swizzle applied to the SOURCE
-// address (chunk position p = 32 r + cs holds chunk cs ^ (r & 15) of row r).  Rows >= nrows repeat
-// row r0 (finite values; callers mask those rows' results).  The caller waits (s_waitcnt vmcnt)
-// and barriers before reading the image.
+// 1 KB (64 lanes x 16 B) at image chunks 64 (8 u + w) + lane, the swizzle applied to the
+// SOURCE offset (chunk position p = 32 r + cs holds chunk cs ^ (r & 15) of row r).  One 32-bit lane
+// offset; instruction u's row step (16 rows: the swizzle repeats) rides in the scalar offset.  Rows past the range are
+// whatever the tensor holds there (the next range's rows: callers mask those rows' results), rows
+// past R read as zero (buffer range check).  The caller waits (s_waitcnt vmcnt) and barriers
+// before reading the image.
 template <int RB>
-__device__ __forceinline__ void stage_rows_async(f4* __restrict__ img, const float* __restrict__ P, int r0,
-                                                 int nrows) {
+__device__ __forceinline__ void stage_rows_async(f4* __restrict__ img, const float* __restrict__ P, int64_t R,
+                                                 int r0, bool on = true) {
+  static_assert(kCWaves == 8, "the swizzle repeats every 16 rows = one instruction's step");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // !on: an empty descriptor (the copies are issued but fetch nothing and land zeros), which keeps
+  // the caller's instruction stream, and so its vmcnt arithmetic, branch-free
+  const rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(P), static_cast<short>(0),
+                                                      on ? static_cast<int>(R * kCD * 4) : 0, 0x00020000);
+  const int r = (64 * w + lane) >> 5, c = (lane & 31) ^ (r & 15);
+  const int vo = 4 * ((r0 + r) * kCD + 4 * c);
 #pragma unroll
-  for (int u = 0; u < RB; ++u) {
-    const int p0 = 64 * (kCWaves * u + w);
-    const int pp = p0 + lane, r = pp >> 5, c = (pp & 31) ^ (r & 15);
-    const int rr = r0 + (r < nrows ? r : 0);
-    __builtin_amdgcn_global_load_lds(P + static_cast<int64_t>(rr) * kCD + 4 * c, img + p0, 16, 0, 0);
-  }
+  for (int u = 0; u < RB; ++u)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(pr, (__attribute__((address_space(3))) void*)(img + 64 * (8 * u + w)), 16,
+                                             vo, u * 16 * kCD * 4, 0, 0);
 }
 
 // 4 x 4 transpose inside each lane quad (lanes 4m..4m+3 of a 16-lane row group, DPP quad
@@ -168,6 +174,20 @@ __device__ __forceinline__ float dpp_xor1(float v) {
 }
 __device__ __forceinline__ float dpp_xor2(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+}
+
+// sum over the 16 lanes of each row (lanes 16k .. 16k + 15), in every lane of the row: DPP quad
+// swaps, then row_half_mirror (lane i <-> 7 - i) and row_mirror (i <-> 15 - i); no LDS round trips
+template <int CTL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  v += dpp_f<0x141>(v);  // row_half_mirror
+  v += dpp_f<0x140>(v);  // row_mirror
+  return v;
 }
 __device__ __forceinline__ f4 quad_transpose(f4 v, int j) {
   f4 b, c;
@@ -192,14 +212,19 @@ __device__ __forceinline__ void store_t_slice(float* __restrict__ dst, const f4 
                                               int rl, int g) {
   const int j = rl & 3, m = rl >> 2, f = 16 * w + 4 * g + j;
   const int ntile = (nrows + 15) >> 4;
+  // buffer stores: one 32-bit lane offset, the tile step in the scalar offset (T tensors < 2^31 B);
+  // tiles past the range (and every tile when dst is NULL: an empty descriptor) are dropped by the
+  // buffer unit, so the sequence has no branches
+  const rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(dst, static_cast<short>(0), dst ? 0x7fffffff : 0, 0x00020000);
+  const int vo = 4 * ((r0 >> 4) * (16 * kCD) + f * 16 + 4 * m);
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
     f4 t = quad_transpose(v[rb], j);
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       if (16 * rb + 4 * m + e >= nrows) t[e] = 0.0f;
-    if (rb < ntile)
-      *reinterpret_cast<f4*>(dst + (static_cast<int64_t>(r0 >> 4) + rb) * (16 * kCD) + f * 16 + 4 * m) = t;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, t), dr,
+                                           rb < ntile ? vo + rb * 4 * 16 * kCD : static_cast<int>(0x80000000u), 0, 0);
   }
 }
 
@@ -221,13 +246,15 @@ __device__ __forceinline__ void load_slice(const float* W, int w, int rl, int g,
   }
 }
 
-// acc[rb] = the wave's 16 output features of row block rb: sum over k of A (weight slice) and
-// the image rows; the image chunks of step group b + 1 are read before group b's MFMAs
-template <int RB>
+// acc[rb] (+)= the wave's 16 output features of row block rb: sum over k of A (weight slice) and
+// the image rows (ZERO: acc starts at zero, else the chain continues from acc); the image chunks of step group b + 1 are read before group b's MFMAs
+template <int RB, bool ZERO = true>
 __device__ __forceinline__ void slice_gemm(const f4* __restrict__ img, const f4 (&A)[8], f4 (&acc)[RB], int rl,
                                            int g) {
+  if (ZERO) {
 #pragma unroll
-  for (int rb = 0; rb < RB; ++rb) acc[rb] = zero4();
+    for (int rb = 0; rb < RB; ++rb) acc[rb] = zero4();
+  }
   f4 bo[2][RB];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) bo[0][rb] = img[(16 * rb + rl) * 32 + (g ^ rl)];
@@ -925,10 +952,10 @@ __device__ __forceinline__ void load_rows_slice(const float* P, int r0, int nrow
 }
 
 // rows of rbf [R, RR] -> srbf[row * NJ + j] (zero beyond RR / nrows); W_rbf [D, RR] -> swr[c * NJ + j]
-template <int NJ, int RB = kV2RB>
+template <int NJ, int RB = kV2RB, int NT = kCThreads>
 __device__ __forceinline__ void stage_rbf(float* __restrict__ srbf, const float* __restrict__ rbf, int RR, int r0,
                                           int nrows) {
-  for (int i = threadIdx.x; i < RB * 16 * NJ; i += kCThreads) {
+  for (int i = threadIdx.x; i < RB * 16 * NJ; i += NT) {
     const int r = i / NJ, j = i % NJ;
     srbf[i] = (r < nrows && j < RR) ? rbf[static_cast<int64_t>(r0 + r) * RR + j] : 0.0f;
   }
@@ -1078,12 +1105,19 @@ __global__ void __launch_bounds__(kCThreads, 1) conv_proj_bwd_kernel(const ProjB
 // x2g_rbf_gate_bwd did as a separate pass over dxs, x, rbf and dx): dxs never leaves registers.
 //   dx   = (dx_add + dxs * f) + (dq Wq + dskip Ws)       f = rbf W_rbf^T (the forward's filter)
 //   (dx_add is read only when given: an uninitialised dx never meets a 0 * NaN)
-//   drbf = (dxs * x) W_rbf   (+= with drbf_acc)          per row: lanes of a wave, then waves in order
+//   drbf = (dxs * x) W_rbf   (+= with drbf_acc)          per row: MFMA over the wave's features, then waves in order
 //   dW_rbf slab of this workgroup = sum over its rows of (dxs * x)^T rbf   (fixed-order slab sum after)
-// Register budget: the base kernel already holds 256 VGPRs, so nothing new lives across the second
-// half's products — dx_add + dxs * f goes to dx (re-read, L2-hot, by the second half's epilogue),
-// the dW_rbf partials are reduced over the row lanes per chunk into an LDS slab (one owner lane per
-// element), and drbf's per-wave partials meet in LDS.
+//
+// Software pipeline.  A workgroup walks its chunks (<= 48 rows each, kGateRB row blocks) as a
+// sequence of operand PAIRS, (dk, dv) then (dq, dskip) per chunk, through two LDS pair buffers:
+// pair q + 1's copies (buffer_load ... lds, no registers) fly while pair q's products run, so the
+// HBM traffic (operands in, T-layout copies and dx out) overlaps the matrix pipe instead of
+// alternating with it (the one-pass-per-chunk form kept the HBM busy during only ~40 % of the
+// launch: phase stamps, scripts/trace_gate.py).  The next pair's weight slices are read after this
+// pair's products, the next chunk's x rows one pair ahead, dx_add's under the (dq, dskip) products;
+// dx leaves once per row (dxs * f held in registers until then).  Each pair's two products are one
+// K = 256 accumulation chain.  Nothing between a pair's copies and its products may wait on vmcnt
+// for a load issued after those copies (a spill reload would: the kernel must not spill).
 struct ProjBwdGateArgs {
   x2g_proj_grad gr[4];
   const float* dx_add;
@@ -1098,159 +1132,198 @@ struct ProjBwdGateArgs {
   int64_t R;
 };
 
-template <int NJ, int RB = kV2RB, int WPC = 1>  // RB row blocks per chunk, WPC workgroups per CU (2 WPC waves / SIMD)
-__global__ void __launch_bounds__(kCThreads, 2 * WPC) conv_proj_bwd_gate_kernel(const ProjBwdGateArgs a) {
-  __shared__ f4 img[2][RB * 16 * 32];
+#ifdef X2G_TRACE  // phase timestamps (A/B trace builds only): thread 0 of each workgroup, 100 MHz clock
+__device__ unsigned long long x2g_trace_buf[1024 * 16];
+#define X2G_TR(k)                                                                                 \
+  do {                                                                                            \
+    if (threadIdx.x == 0 && (k) < 16) x2g_trace_buf[blockIdx.x * 16 + (k)] = wall_clock64();     \
+  } while (0)
+#else
+#define X2G_TR(k) \
+  do {            \
+  } while (0)
+#endif
+
+constexpr int kGateRB = 3;
+
+template <int NJ, bool TW>  // TW: every projection's W^T given (else W read transposed)
+__global__ void __launch_bounds__(kCThreads, 2) conv_proj_bwd_gate_kernel(const ProjBwdGateArgs a) {
+  constexpr int RB = kGateRB;
+  constexpr int kImg = RB * 16 * 32;
+  // the two pair buffers as four distinct arrays (24 KB each): the compiler then sees that a pair's
+  // products never read what the other pair's in-flight copies write, and adds no vmcnt wait
+  __shared__ f4 img_k[kImg], img_v[kImg];  // (dk, dv)
+  __shared__ f4 img_q[kImg], img_s[kImg];  // (dq, dskip)
   __shared__ float srbf[RB * 16 * NJ];
   __shared__ float swr[kCD * NJ];
-  __shared__ float sdw[kCD * NJ];                   // this workgroup's dW_rbf (owner lanes only)
-  __shared__ float red[kCWaves * RB * 16 * NJ];  // drbf partials: [wave][row][j]
+  __shared__ float red[kCWaves * RB * 16 * 16];  // drbf partials: [wave][row][16 columns, j < NJ used]
+  __shared__ float sdw[kCD * NJ];                 // this workgroup's dW_rbf
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int rl = lane & 15, g = lane >> 4;
   const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
-  const int64_t nch = (nblk + RB * G - 1) / (RB * G) * G;
+  const int64_t nch = (nblk + RB * G - 1) / (RB * G) * G;  // a multiple of G: every workgroup nk chunks
+  const int nk = static_cast<int>(nch / G);
   const int c0 = 16 * w + 4 * g;
+  X2G_TR(0);
   for (int i = tid; i < kCD * NJ; i += kCThreads) {
     const int c = i / NJ, j = i % NJ;
     swr[i] = j < a.RR ? a.wr[c * a.RR + j] : 0.0f;
-  }
-  if (rl == 0) {
-#pragma unroll
-    for (int i = 0; i < 4 * NJ; ++i) sdw[c0 * NJ + i] = 0.0f;
+    sdw[i] = 0.0f;
   }
   auto load_ws = [&](int p, f4 (&dst)[8]) {
-    if (a.gr[p].wt)
+    if (TW)
       load_slice<false>(a.gr[p].wt, w, rl, g, dst);
     else
       load_slice<true>(a.gr[p].w, w, rl, g, dst);
   };
-  auto t_copy = [&](int p, const f4* im, int r0, int nrows) {
-    if (!a.gr[p].g_t) return;
+  auto t_copy = [&](int p, const f4* im, int r0, int nrows) {  // the weight gradient's dy operand
     f4 v[RB];
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) v[rb] = im[ipos(16 * rb + rl, 4 * w + g)];
     store_t_slice(a.gr[p].g_t, v, r0, nrows, w, rl, g);
   };
-  const rsrc_t ar = rsrc(a.dx_add ? a.dx_add : a.dx);  // read only when dx_add is given (no 0 * NaN)
-  const rsrc_t dr = rsrc(a.dx);
-  for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
+  auto chunk = [&](int k, int& r0, int& nrows) { chunk_rows(blockIdx.x + k * G, nch, nblk, a.R, r0, nrows); };
+  // Every global access of the chunk loop is unconditional (a disabled one goes through an empty
+  // descriptor or to an out-of-range offset): the compiler's vmcnt waits then count exactly instead
+  // of falling back to vmcnt(0), which would wait for the next pair's copies.
+  const int64_t bytes = a.R * kCD * 4;
+  const rsrc_t ar = rsrc_n(a.dx_add, bytes, a.dx_add != nullptr);  // dx_add absent: reads 0
+  const rsrc_t dr = rsrc_n(a.dx, bytes, true);
+  const rsrc_t xr = rsrc_n(a.x, bytes, true);
+  const rsrc_t rr = rsrc_n(a.rbf, a.R * a.RR * 4, true);
+  const rsrc_t br = rsrc_n(a.drbf, a.R * a.RR * 4, a.drbf != nullptr);
+  const rsrc_t bo = rsrc_n(a.drbf, a.R * a.RR * 4, a.drbf != nullptr && a.drbf_acc);
+  static_assert(RB * 16 * NJ <= kCThreads && RB * 16 * kRbfMax <= kCThreads, "one srbf / drbf element per thread");
+  // outstanding operations a pair's top wait may leave (issued after the pair's copies): 2 RB
+  // T-layout stores, the next weight slices (kWL loads each) and, at a (dk, dv) top, RB dx stores
+  constexpr int kWL = TW ? 8 : 32;
+  constexpr int kKVWait = 3 * RB + 2 * kWL < 63 ? 3 * RB + 2 * kWL : 63;
+  constexpr int kQSWait = 2 * RB + 2 * kWL < 63 ? 2 * RB + 2 * kWL : 63;
+  if (nk > 0) {
     int r0, nrows;
-    chunk_rows(ch, nch, nblk, a.R, r0, nrows);
-    if (nrows <= 0) continue;  // (workgroup-uniform)
-    __syncthreads();  // images, srbf and red of the previous chunk are no longer read
-    // (dk, dv) -> dxs -> the gate's three gradients.  The two operand images come in through
-    // global_load_lds; the weight slices meanwhile into registers.
-    stage_rows_async<RB>(img[0], a.gr[1].g, r0, nrows);
-    stage_rows_async<RB>(img[1], a.gr[2].g, r0, nrows);
-    stage_rbf<NJ, RB>(srbf, a.rbf, a.RR, r0, nrows);
-    f4 acc[RB], t[RB];
-    {
-      f4 A[8], An[8];
-      load_ws(1, A);
-      load_ws(2, An);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      t_copy(1, img[0], r0, nrows);
-      t_copy(2, img[1], r0, nrows);
-      slice_gemm(img[0], A, acc, rl, g);
-      slice_gemm(img[1], An, t, rl, g);
-    }
-    // The epilogue's global reads (x; dx_add) are issued BEFORE the next operands' copies, so
-    // waiting for them (vmcnt counts in issue order) never waits for those copies.
-    f4 xv[RB], xa[RB];
-    load_rows_slice(a.x, r0, nrows, w, rl, g, xv);  // zero beyond nrows
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb) {
-      const int r = 16 * rb + rl;
-      xa[rb] = a.dx_add ? bload4(ar, 4 * ((r0 + (r < nrows ? r : 0)) * kCD + c0), 0) : zero4();
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave's product has read the images: refill them
-    // (dq, dskip) copies fly during the gate epilogue below
-    stage_rows_async<RB>(img[0], a.gr[0].g, r0, nrows);
-    stage_rows_async<RB>(img[1], a.gr[3].g, r0, nrows);
-    {
-      float aw[4][NJ];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) aw[i][j] = 0.0f;
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb) {
-        const int r = 16 * rb + rl;
-        const f4 dxs = acc[rb] + t[rb];
-        if (r < nrows) {
-          const int off = (r0 + r) * kCD + c0;
-          const f4 gx = dxs * gate_filter<NJ>(srbf, swr, r, c0);
-          *reinterpret_cast<f4*>(a.dx + off) = a.dx_add ? xa[rb] + gx : gx;
-        }
-        const f4 df = dxs * xv[rb];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) aw[i][j] = fmaf(df[i], srbf[r * NJ + j], aw[i][j]);
-        if (a.drbf) {
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) {
-            float p = 0.0f;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) p = fmaf(df[i], swr[(c0 + i) * NJ + j], p);
-            p += __shfl_xor(p, 16);
-            p += __shfl_xor(p, 32);
-            if (g == 0) red[(w * RB * 16 + r) * NJ + j] = p;
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          float v = aw[i][j];
-          v += __shfl_xor(v, 1);
-          v += __shfl_xor(v, 2);
-          v += __shfl_xor(v, 4);
-          v += __shfl_xor(v, 8);
-          if (rl == 0) sdw[(c0 + i) * NJ + j] += v;
-        }
-    }
-    {  // (dq, dskip) -> dx
-      f4 A[8], An[8];
-      load_ws(0, A);
-      load_ws(3, An);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();  // the copies have landed; red is complete
-      if (a.drbf) {
-        for (int i = tid; i < nrows * a.RR; i += kCThreads) {
-          const int r = i / a.RR, j = i % a.RR;
-          float s = 0.0f;
-#pragma unroll
-          for (int ww = 0; ww < kCWaves; ++ww) s += red[(ww * RB * 16 + r) * NJ + j];
-          float* d = a.drbf + static_cast<int64_t>(r0 + r) * a.RR + j;
-          *d = a.drbf_acc ? *d + s : s;
-        }
-      }
-      t_copy(0, img[0], r0, nrows);
-      t_copy(3, img[1], r0, nrows);
-      slice_gemm(img[0], A, acc, rl, g);
-      slice_gemm(img[1], An, t, rl, g);
-    }
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb) {
-      const int r = 16 * rb + rl;
-      if (r < nrows) {
-        const int off = (r0 + r) * kCD + c0;
-        *reinterpret_cast<f4*>(a.dx + off) = bload4(dr, 4 * off, 0) + (acc[rb] + t[rb]);
-      }
-    }
+    chunk(0, r0, nrows);
+    stage_rows_async<RB>(img_k, a.gr[1].g, a.R, r0);
+    stage_rows_async<RB>(img_v, a.gr[2].g, a.R, r0);
   }
-  if (rl == 0) {  // the owner lanes' sdw entries -> this workgroup's slab
-    float* slab = a.part_w + static_cast<int64_t>(blockIdx.x) * kCD * a.RR;
+  f4 A[8], An[8];  // this pair's two weight slices
+  load_ws(1, A);
+  load_ws(2, An);
+  __syncthreads();  // swr
+  float dold = 0.0f;
+  int doff = kOOB;
+  auto drbf_out = [&]() {  // the last chunk's drbf (partials in red, written before the last barrier)
+    const int i = doff == kOOB ? 0 : tid, r = i / a.RR, j = i % a.RR;
+    float sum = 0.0f;
+#pragma unroll
+    for (int ww = 0; ww < kCWaves; ++ww) sum += red[(ww * RB * 16 + r) * 16 + j];
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, dold + sum), br, doff, 0, 0);
+  };
+  for (int k = 0; k < nk; ++k) {
+    int r0, nrows;
+    chunk(k, r0, nrows);
+    // ---- (dk, dv): acc1 = dxs = [dk | dv] [Wk ; Wv]
+    if (k > 0)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kKVWait) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave's copies landed; the previous chunk's (dq, dskip), srbf and red read
+    X2G_TR(1 + 6 * k);
+    drbf_out();
+    stage_rows_async<RB>(img_q, a.gr[0].g, a.R, r0);
+    stage_rows_async<RB>(img_s, a.gr[3].g, a.R, r0);
+    asm volatile("" ::: "memory");  // every later memory operation issues after the copies (the top waits count on it)
+    f4 xv[RB];  // this chunk's x slice and rbf element, for the epilogue under the second pair
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const int r = 16 * rb + rl;
+      xv[rb] = bload4(xr, 4 * ((r0 + (r < nrows ? r : 0)) * kCD + c0), 0);  // rows past the chunk: its first
+    }
+    float rbv;
+    {
+      const int r = tid / NJ, j = tid % NJ;
+      rbv = bload1(rr, (tid < RB * 16 * NJ && r < nrows && j < a.RR) ? 4 * ((r0 + r) * a.RR + j) : kOOB, 0);
+    }
+    t_copy(1, img_k, r0, nrows);
+    t_copy(2, img_v, r0, nrows);
+    f4 acc1[RB];
+    slice_gemm(img_k, A, acc1, rl, g);
+    load_ws(0, A);  // Wq under the second product
+    slice_gemm<RB, false>(img_v, An, acc1, rl, g);
+    load_ws(3, An);  // Ws under the next pair's wait
+    if (tid < RB * 16 * NJ) srbf[tid] = rbv;  // read after the next barrier
+    X2G_TR(2 + 6 * k);
+    // ---- (dq, dskip): dx = (dx_add + dxs * f) + [dq | dskip] [Wq ; Ws]; the gate epilogue of
+    // acc1 runs under these products
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kQSWait) : "memory");
+    __syncthreads();  // every wave's copies landed; (dk, dv) no longer read; srbf written
+    X2G_TR(3 + 6 * k);
+    // reads that must not wait behind the next chunk's copies go out before them
+    doff = tid < nrows * a.RR ? 4 * (r0 * a.RR + tid) : kOOB;
+    dold = bload1(bo, doff, 0);  // drbf += : 0 when not accumulating
+    f4 xa[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const int r = 16 * rb + rl;
+      xa[rb] = bload4(ar, 4 * ((r0 + (r < nrows ? r : 0)) * kCD + c0), 0);
+    }
+    {
+      const bool more = k + 1 < nk;
+      int r1, n1;
+      chunk(more ? k + 1 : k, r1, n1);
+      stage_rows_async<RB>(img_k, a.gr[1].g, a.R, r1, more);
+      stage_rows_async<RB>(img_v, a.gr[2].g, a.R, r1, more);
+      asm volatile("" ::: "memory");
+    }
+    t_copy(0, img_q, r0, nrows);
+    t_copy(3, img_s, r0, nrows);
+    f4 acc[RB], d1[RB];  // d1 = dx_add + dxs * f
+    slice_gemm(img_q, A, acc, rl, g);
+    load_ws(1, A);  // the next chunk's Wk under the second product (once more after the last chunk)
+    f4 wrv;  // drbf's MFMA B operand: lane (j, g) of step e holds W_rbf[c0 + e][j] (zero for j >= NJ)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) wrv[e] = swr[(c0 + e) * NJ + (rl < NJ ? rl : 0)] * (rl < NJ ? 1.0f : 0.0f);
+    float aw[4][NJ];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
-        if (j < a.RR) slab[(c0 + i) * a.RR + j] = sdw[(c0 + i) * NJ + j];
+      for (int j = 0; j < NJ; ++j) aw[i][j] = 0.0f;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const int r = 16 * rb + rl;
+      d1[rb] = xa[rb] + acc1[rb] * gate_filter<NJ>(srbf, swr, r, c0);
+      const f4 df = r < nrows ? acc1[rb] * xv[rb] : zero4();
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) aw[i][j] = fmaf(df[i], srbf[r * NJ + j], aw[i][j]);
+      // the wave's drbf partial of row block rb = df (16 rows x its 16 features) W_rbf slice, on the
+      // matrix pipe: lane (j, g) ends with rows 16 rb + 4 g + i, column j (zero for j >= NJ)
+      f4 pd = zero4();
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pd = __builtin_amdgcn_mfma_f32_16x16x4f32(df[e], wrv[e], pd, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[(w * RB * 16 + 16 * rb + 4 * g + i) * 16 + rl] = pd[i];
+    }
+    // this chunk's dW_rbf partial: the 16 row lanes' sum (in every lane of the row group), added by
+    // all 16 lanes at once (same address, same value: one wave instruction, no branch)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) sdw[(c0 + i) * NJ + j] += row_sum16(aw[i][j]);
+    slice_gemm<RB, false>(img_s, An, acc, rl, g);
+    load_ws(2, An);
+    X2G_TR(4 + 6 * k);
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const int r = 16 * rb + rl;
+      bstore4(dr, d1[rb] + acc[rb], r < nrows ? 4 * ((r0 + r) * kCD + c0) : kOOB);
+    }
+    X2G_TR(5 + 6 * k);
   }
+  __syncthreads();  // red of the last chunk
+  drbf_out();
+  float* slab = a.part_w + static_cast<int64_t>(blockIdx.x) * kCD * a.RR;  // this workgroup's dW_rbf slab
+  for (int i = tid; i < kCD * a.RR; i += kCThreads) slab[i] = sdw[(i / a.RR) * NJ + i % a.RR];
 }
 
 inline bool al16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
@@ -1575,6 +1648,13 @@ X2G_API int x2g_conv_proj_bwd(const x2g_proj_grad* grads, int64_t rows, int32_t 
   return last_launch_status();
 }
 
+
+#ifdef X2G_TRACE
+X2G_API int x2g_trace_fetch(unsigned long long* host, int n) {
+  return static_cast<int>(hipMemcpyFromSymbol(host, HIP_SYMBOL(x2g_trace_buf), sizeof(unsigned long long) * n));
+}
+#endif
+
 X2G_API int32_t x2g_conv_proj_bwd_gate_splits(int64_t rows) { return rows > 0 ? static_cast<int32_t>(proj_grid(rows)) : 0; }
 
 X2G_API size_t x2g_conv_proj_bwd_gate_workspace(int64_t rows, int32_t rbf_dim) {
@@ -1616,10 +1696,17 @@ X2G_API int x2g_conv_proj_bwd_gate(const x2g_proj_grad* grads, int64_t rows, int
   a.drbf_acc = (flags & X2G_GATE_DRBF_ACCUM) ? 1 : 0;
   a.R = rows;
   const unsigned grid = proj_grid(rows);
-  if (rbf_dim <= 6)
-    conv_proj_bwd_gate_kernel<6, kProjRB, kProjWPC><<<grid, kCThreads, 0, st>>>(a);
-  else
-    conv_proj_bwd_gate_kernel<8, kProjRB, kProjWPC><<<grid, kCThreads, 0, st>>>(a);
+  const bool tw = grads[0].wt && grads[1].wt && grads[2].wt && grads[3].wt;
+  if (rbf_dim <= 6) {
+    if (tw)
+      conv_proj_bwd_gate_kernel<6, true><<<grid, kCThreads, 0, st>>>(a);
+    else
+      conv_proj_bwd_gate_kernel<6, false><<<grid, kCThreads, 0, st>>>(a);
+  } else if (tw) {
+    conv_proj_bwd_gate_kernel<8, true><<<grid, kCThreads, 0, st>>>(a);
+  } else {
+    conv_proj_bwd_gate_kernel<8, false><<<grid, kCThreads, 0, st>>>(a);
+  }
   const int rc = last_launch_status();
   if (rc || (flags & X2G_DEFER_SLAB_SUM)) return rc;
   x2g_slab_job sj{a.part_w, nullptr, dw_rbf, nullptr, static_cast<int64_t>(kCD) * rbf_dim, 0,
