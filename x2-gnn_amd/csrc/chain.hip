@@ -303,6 +303,18 @@ __device__ __forceinline__ void chunk_rows(int64_t ch, int64_t nch, int64_t nblk
 // and dropped by the buffer unit
 constexpr int kOOB = static_cast<int>(0x80000000u);
 
+#ifdef X2G_TRACE  // phase timestamps (A/B trace builds only): thread 0 of each workgroup, 100 MHz clock
+__device__ unsigned long long x2g_trace_buf[1024 * 16];
+#define X2G_TR(k)                                                                                 \
+  do {                                                                                            \
+    if (threadIdx.x == 0 && (k) < 16) x2g_trace_buf[blockIdx.x * 16 + (k)] = wall_clock64();     \
+  } while (0)
+#else
+#define X2G_TR(k) \
+  do {            \
+  } while (0)
+#endif
+
 // descriptor over `bytes` bytes at p (0 when off: every store dropped)
 __device__ __forceinline__ rsrc_t rsrc_n(const float* p, int64_t bytes, bool on) {
   const int64_t nr = on ? (bytes < 0x7fffffff ? bytes : 0x7fffffff) : 0;
@@ -613,6 +625,7 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
     }
     int p = 0;
     __syncthreads();  // the previous chunk's images are no longer read
+    X2G_TR(0);
     {
       float held_m, silu_m, dres_acc_m;
       rsrc_t dres_r, dz_r, t_r;
@@ -621,6 +634,7 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
                          rl, g);
     }
     __syncthreads();
+    X2G_TR(1);
     for (int s = n - 1; s >= 0; --s) {
       f4 An[8];
       load_wslice(s > 0 ? s - 1 : n - 1, An);
@@ -654,7 +668,9 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
       }
       p ^= 1;
       pin(An);
+      X2G_TR(2 + 2 * (n - 1 - s));
       __syncthreads();
+      X2G_TR(3 + 2 * (n - 1 - s));
 #pragma unroll
       for (int b = 0; b < 8; ++b) A[b] = An[b];
     }
@@ -1131,18 +1147,6 @@ struct ProjBwdGateArgs {
   int drbf_acc;
   int64_t R;
 };
-
-#ifdef X2G_TRACE  // phase timestamps (A/B trace builds only): thread 0 of each workgroup, 100 MHz clock
-__device__ unsigned long long x2g_trace_buf[1024 * 16];
-#define X2G_TR(k)                                                                                 \
-  do {                                                                                            \
-    if (threadIdx.x == 0 && (k) < 16) x2g_trace_buf[blockIdx.x * 16 + (k)] = wall_clock64();     \
-  } while (0)
-#else
-#define X2G_TR(k) \
-  do {            \
-  } while (0)
-#endif
 
 constexpr int kGateRB = 3;
 
