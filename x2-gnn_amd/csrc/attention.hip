@@ -861,14 +861,37 @@ namespace x2g {
 // per SIMD overlap (the tile-staged dense_fwd_narrow serialised them per workgroup: 3.1 TB/s).
 constexpr int kSPQ = 3;  // 16-wide contraction groups (K = 42 -> 48, zero-padded)
 
+// Round 3: the same wave-independent MFMA product with both HBM streams made line-coalesced (the
+// per-lane form read each 168-byte sbf row as 8-byte pieces and wrote every output row as 64-byte
+// pieces, 3.2 TB/s).  A wave's 16-row sbf block is 2688 contiguous bytes: three buffer_load ... lds
+// instructions land it in the wave's own LDS slot (double-buffered: the next block's copy flies
+// during this block's MFMAs), and each half of the output block goes out through the same slot
+// (the block's rows are in registers by then), swizzled, as 256-byte row runs, 1 KB per store
+// instruction.  No workgroup barrier after the W staging: every LDS slot is private to its wave (LDS
+// operations of a wave execute in order).  16-wave workgroups share one W image: 16 waves per CU
+// (153 KB of LDS), where 8-wave workgroups with private output tiles fitted only 8.
+typedef __amdgpu_buffer_rsrc_t sp_rsrc_t;
+__device__ __forceinline__ sp_rsrc_t sp_rsrc(const float* p, int64_t bytes) {
+  const int64_t nr = bytes <= 0 ? 0 : (bytes < 0x7fffffff ? bytes : 0x7fffffff);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), static_cast<short>(0), static_cast<int>(nr),
+                                           0x00020000);
+}
+
+constexpr int kSPWaves = 16;           // 1024-thread workgroups, one per CU
+constexpr int kSPChunks = 16 * kS / 4;  // 16-byte chunks per 16-row sbf block (168)
+
 template <int NOB>
-__global__ void __launch_bounds__(256) sbf_project_waves(const float* __restrict__ sbf, const float* __restrict__ w,
-                                                         const float* __restrict__ b, int64_t T,
-                                                         float* __restrict__ out) {
+__global__ void __launch_bounds__(kSPWaves * 64) sbf_project_waves(const float* __restrict__ sbf,
+                                                                  const float* __restrict__ w,
+                                                                  const float* __restrict__ b, int64_t T,
+                                                                  float* __restrict__ out) {
   typedef float f4t __attribute__((ext_vector_type(4)));
-  __shared__ f4t Wl[NOB * kSPQ * 64];  // [ob][q][lane]: W[16ob + i][16q + 4g .. +3]
-  __shared__ f4t Bl[NOB * 4];          // [ob][g]: b[16ob + 4g .. +3]
+  __shared__ f4t Wl[NOB * kSPQ * 64];         // [ob][q][lane]: W[16ob + i][16q + 4g .. +3]
+  __shared__ f4t Bl[NOB * 4];                 // [ob][g]: b[16ob + 4g .. +3]
+  __shared__ f4t Xs[kSPWaves][2][16 * 16];    // per wave, two slots: a 16-row sbf block (168 chunks),
+                                              // then 16 rows x 64 output columns, chunk-swizzled
   constexpr int N = 16 * NOB;
+  constexpr int HB = NOB < 4 ? NOB : 4;       // output blocks per half (64 columns)
   for (int idx = threadIdx.x; idx < NOB * kSPQ * 64; idx += blockDim.x) {
     const int l = idx & 63, q = (idx >> 6) % kSPQ, ob = (idx >> 6) / kSPQ;
     const int c = 16 * ob + (l & 15), k = 16 * q + 4 * (l >> 4);
@@ -884,34 +907,46 @@ __global__ void __launch_bounds__(256) sbf_project_waves(const float* __restrict
     Bl[idx] = v;
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
   const int64_t nblk = (T + 15) / 16;
-  const int64_t nw = static_cast<int64_t>(gridDim.x) * 4;
-  auto load_b = [&](int64_t blk, f4t (&B)[kSPQ]) {
-    const int64_t r = blk * 16 + i;
-    const bool rok = r < T;
-    const float* row = sbf + (rok ? r : T - 1) * kS;
+  const int64_t nw = static_cast<int64_t>(gridDim.x) * kSPWaves;
+  int64_t blk = static_cast<int64_t>(blockIdx.x) * kSPWaves + wv;
+  // a block's rows are 2688 contiguous bytes: chunk u * 64 + lane of the block (chunks >= 168 and rows
+  // >= T read as zero through the range check)
+  auto issue = [&](int64_t bk, int slot) {
+    const float* base = sbf + bk * (16 * kS);
+    const sp_rsrc_t r = sp_rsrc(base, (T - bk * 16) * kS * 4);
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(&Xs[wv][slot][64 * u]), 16,
+                                               (64 * u + lane) < kSPChunks ? 16 * (64 * u + lane) : 0x7fffff00, 0, 0,
+                                               0);
+  };
+  int slot = 0;
+  if (blk < nblk) issue(blk, 0);
+  for (; blk < nblk; blk += nw) {
+    const bool more = blk + nw < nblk;
+    if (more) issue(blk + nw, slot ^ 1);
+    asm volatile("" ::: "memory");
+    // this block's copy is done when at most the next block's 3 copies (issued after it) remain;
+    // the previous block's stores went out before those and may still be in flight only if counted
+    if (more)
+      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // B operand: lane (i, g) = row i, k = 16q + 4g + e (row i's floats at 42 i: 8-byte aligned)
+    const float* xr = reinterpret_cast<const float*>(&Xs[wv][slot][0]) + i * kS;
+    f4t B[kSPQ];
 #pragma unroll
     for (int q = 0; q < kSPQ; ++q) {
-      const int k = 16 * q + 4 * g;  // k even: 8-byte aligned pairs
-      const int k0 = k < kS ? k : kS - 2, k1 = k + 2 < kS ? k + 2 : kS - 2;
-      const float2 lo = *reinterpret_cast<const float2*>(row + k0);
-      const float2 hi = *reinterpret_cast<const float2*>(row + k1);
-      const float m0 = (rok && k < kS) ? 1.0f : 0.0f, m1 = (rok && k + 2 < kS) ? 1.0f : 0.0f;
-      B[q] = f4t{lo.x * m0, lo.y * m0, hi.x * m1, hi.y * m1};
+      const int k = 16 * q + 4 * g;
+      const float2 lo = *reinterpret_cast<const float2*>(xr + (k < kS ? k : 0));
+      const float2 hi = *reinterpret_cast<const float2*>(xr + (k + 2 < kS ? k + 2 : 0));
+      B[q] = f4t{k < kS ? lo.x : 0.0f, k < kS ? lo.y : 0.0f, k + 2 < kS ? hi.x : 0.0f, k + 2 < kS ? hi.y : 0.0f};
     }
-  };
-  int64_t blk = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  f4t B[kSPQ];
-  if (blk < nblk) load_b(blk, B);
-  for (; blk < nblk; blk += nw) {
-    f4t Bn[kSPQ];
-    load_b(blk + nw < nblk ? blk + nw : blk, Bn);  // (the last block reloads itself: unused)
-    const int64_t r = blk * 16 + i;
-    float* o = out + (r < T ? r : 0) * N + 4 * g;
-    // output columns in halves of (at most) 4 blocks: 4 accumulators in flight (dependency distance
-    // 4 MFMAs >= the 40-cycle accumulator latency), fewer registers than all 8 at once
-    constexpr int HB = NOB < 4 ? NOB : 4;
+    float* ob = out + blk * 16 * N;
+    const sp_rsrc_t orr = sp_rsrc(ob, (T - blk * 16) * N * 4);
+    float* ys = reinterpret_cast<float*>(&Xs[wv][slot][0]);  // B is in registers: the slot is free
 #pragma unroll
     for (int h0 = 0; h0 < NOB; h0 += HB) {
       f4t acc[HB];
@@ -927,13 +962,19 @@ __global__ void __launch_bounds__(256) sbf_project_waves(const float* __restrict
 #pragma unroll
           for (int j = 0; j < HB; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][e], B[q][e], acc[j], 0, 0, 0);
       }
-      if (r < T) {
+      // D lane (i, g): row i, local columns 16 j + 4 g .. +3 = chunk 4 j + g of the row's 16
 #pragma unroll
-        for (int j = 0; j < HB; ++j) *reinterpret_cast<f4t*>(o + 16 * (h0 + j)) = acc[j];
+      for (int j = 0; j < HB; ++j) *reinterpret_cast<f4t*>(ys + i * 64 + 4 * ((4 * j + g) ^ i)) = acc[j];
+      // row-major out: instruction u covers rows 4u .. 4u + 3, lane = (row 4u + (lane >> 4), chunk lane & 15)
+#pragma unroll
+      for (int u = 0; u < 16 * HB / 16; ++u) {
+        const int r = 4 * u + (lane >> 4), c = lane & 15;
+        const f4t v = *reinterpret_cast<const f4t*>(ys + r * 64 + 4 * (c ^ r));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), orr,
+                                               4 * (r * N + 16 * h0 + 4 * c), 0, 0);
       }
     }
-#pragma unroll
-    for (int q = 0; q < kSPQ; ++q) B[q] = Bn[q];
+    slot ^= 1;
   }
 }
 }  // namespace x2g
@@ -947,17 +988,16 @@ X2G_API int x2g_sbf_project(const float* sbf, int64_t T, int32_t sbf_dim, const 
   if (T == 0) return X2G_OK;
   if (!sbf || !w_sbf || !b_sbf || !sbfproj) return X2G_EINVAL;
   hipStream_t st = as_stream(stream);
-  // wave-independent f32 MFMA kernel (out_dim 128 or 64, 8-byte aligned sbf rows, 16-byte aligned
-  // output rows)
-  if ((out_dim == 128 || out_dim == 64) && reinterpret_cast<uintptr_t>(sbf) % 8 == 0 &&
+  // wave-independent f32 MFMA kernel (out_dim 128 or 64, 16-byte aligned sbf and output)
+  if ((out_dim == 128 || out_dim == 64) && reinterpret_cast<uintptr_t>(sbf) % 16 == 0 &&
       reinterpret_cast<uintptr_t>(sbfproj) % 16 == 0) {
     const int64_t nblk = (T + 15) / 16;
-    int64_t want = (nblk + 3) / 4;
-    want = want < 1280 ? want : 1280;  // ~5 workgroups per CU, each wave looping over its blocks
+    int64_t want = (nblk + kSPWaves - 1) / kSPWaves;
+    want = want < 256 ? want : 256;  // one 1024-thread workgroup per CU, each wave looping over its blocks
     if (out_dim == 128)
-      sbf_project_waves<8><<<static_cast<unsigned>(want), 256, 0, st>>>(sbf, w_sbf, b_sbf, T, sbfproj);
+      sbf_project_waves<8><<<static_cast<unsigned>(want), kSPWaves * 64, 0, st>>>(sbf, w_sbf, b_sbf, T, sbfproj);
     else
-      sbf_project_waves<4><<<static_cast<unsigned>(want), 256, 0, st>>>(sbf, w_sbf, b_sbf, T, sbfproj);
+      sbf_project_waves<4><<<static_cast<unsigned>(want), kSPWaves * 64, 0, st>>>(sbf, w_sbf, b_sbf, T, sbfproj);
     return last_launch_status();
   }
   // f32 MFMA, tiles staged through LDS (dense.hip): that kernel covers N <= 128 output columns
