@@ -1,7 +1,7 @@
 """Interleaved A/B of whole training steps: bench.py --step-only under each variant's environment,
 round-robin for several rounds on one box (box-to-box spread is ~1 %, so steps are compared only
 within one call).  Usage: python scripts/step_ab.py ROUNDS NAME=ENV[;ENV...] ...
-e.g.  python scripts/step_ab.py 3 base= nogate=X2G_PROJ_GATE=0 nopool=X2G_POOL_BATCH=0"""
+e.g.  python scripts/step_ab.py 3 base=X2G_LIB=x2-gnn_amd/lib/ab/libx2g_base.so new="""
 import json
 import os
 import subprocess

@@ -24,6 +24,8 @@
 // MFMAs run and written to LDS after them.
 #include <math.h>
 
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace x2g {
@@ -442,7 +444,7 @@ __device__ __forceinline__ void pipe_sched() {
 // one stage of the v4 forward: in -> out (distinct arrays after inlining)
 __device__ __forceinline__ void fwd4_stage(const ChainFwdArgs& a, int s, const f4* __restrict__ in,
                                            f4* __restrict__ out, const f4* __restrict__ rimg, f4 (&A)[8],
-                                           f4 (&held)[kV2RB], int64_t ch, int64_t wt_groups, int r0, int nrows,
+                                           f4 (&held)[kV2RB], int r0, int nrows,
                                            int w, int rl, int g) {
   const int n = a.n;
   const x2g_chain_stage& S = a.st[s];
@@ -450,13 +452,6 @@ __device__ __forceinline__ void fwd4_stage(const ChainFwdArgs& a, int s, const f
   f4 An[8];
   load_slice<false>(a.st[s + 1 < n ? s + 1 : 0].w, w, rl, g, An);
   const f4 bias = bload4(rsrc(S.b ? S.b : S.w), 4 * (16 * w + 4 * g), 0) * (S.b ? 1.0f : 0.0f);
-  if (S.wt && ch < wt_groups) {
-#pragma unroll
-    for (int b = 0; b < 8; ++b)
-      if (b % wt_groups == ch)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) S.wt[(16 * b + 4 * g + e) * kCD + 16 * w + rl] = A[b][e];
-  }
   if (fl & (X2G_CHAIN_HOLD | X2G_CHAIN_RES_EXT)) {
     const f4* src = (fl & X2G_CHAIN_HOLD) ? in : rimg;
 #pragma unroll
@@ -499,7 +494,13 @@ __device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a) {
   const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
   const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
   const int n = a.n;
-  const int64_t wt_groups = G < 8 ? G : 8;
+  // W^T of every stage for the backward (x2g_chain_stage.wt): each workgroup writes its share, one
+  // element per thread (written by the first 8 chunks, it made those workgroups the launch's tail)
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kCThreads + tid; i < static_cast<int64_t>(n) * kCD * kCD;
+       i += G * kCThreads) {
+    const int s = static_cast<int>(i / (kCD * kCD)), e = static_cast<int>(i % (kCD * kCD));
+    if (a.st[s].wt) a.st[s].wt[e] = a.st[s].w[(e % kCD) * kCD + e / kCD];
+  }
   for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
     int r0, nrows;
     chunk_rows(ch, nch, nblk, a.R, r0, nrows);
@@ -518,8 +519,8 @@ __device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a) {
       store_t_slice(a.in_t, xs, r0, nrows, w, rl, g);
     }
     for (int s = 0; s < n; s += 2) {
-      fwd4_stage(a, s, img0, img1, imgr, A, held, ch, wt_groups, r0, nrows, w, rl, g);
-      if (s + 1 < n) fwd4_stage(a, s + 1, img1, img0, imgr, A, held, ch, wt_groups, r0, nrows, w, rl, g);
+      fwd4_stage(a, s, img0, img1, imgr, A, held, r0, nrows, w, rl, g);
+      if (s + 1 < n) fwd4_stage(a, s + 1, img1, img0, imgr, A, held, r0, nrows, w, rl, g);
     }
   }
 }
@@ -943,6 +944,7 @@ inline int chain_wgrad_splits_of(int64_t ntiles, int stages) {
 // v2 structure: a workgroup's <= 96 rows of x, and of x_src = x * (rbf W_rbf^T) formed in
 // registers, sit in LDS; each wave computes its 16-feature slice of q, k, v and skip.
 constexpr int kRbfMax = 8;
+constexpr int kGateRB = 3;  // row blocks per chunk of the pipelined projection kernels
 
 struct ProjFwdArgs {
   const float* x;
@@ -991,8 +993,12 @@ __device__ __forceinline__ f4 gate_filter(const float* __restrict__ srbf, const 
   return f;
 }
 
-template <int NJ, int RB = kV2RB, int WPC = 1>  // RB row blocks per chunk, WPC workgroups per CU (2 WPC waves / SIMD)
-__global__ void __launch_bounds__(kCThreads, 2 * WPC) conv_proj_fwd_kernel(const ProjFwdArgs a) {
+// (A two-chunk software pipeline as in the gate backward below measured slower here, 51.5 vs
+// 39.6 us at config 2: the products are already most of the launch, and 48-row chunks add a
+// barrier skew per chunk; phase stamps, scripts/trace_proj_fwd.py.)
+template <int NJ>
+__global__ void __launch_bounds__(kCThreads, 2) conv_proj_fwd_kernel(const ProjFwdArgs a) {
+  constexpr int RB = kV2RB;
   __shared__ f4 img[2][RB * 16 * 32];  // x, x_src
   __shared__ float srbf[RB * 16 * NJ];
   __shared__ float swr[kCD * NJ];
@@ -1000,10 +1006,15 @@ __global__ void __launch_bounds__(kCThreads, 2 * WPC) conv_proj_fwd_kernel(const
   const int rl = lane & 15, g = lane >> 4;
   const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
   const int64_t nch = (nblk + RB * G - 1) / (RB * G) * G;
-  const int64_t wt_groups = G < 8 ? G : 8;
   for (int i = tid; i < kCD * NJ; i += kCThreads) {
     const int c = i / NJ, j = i % NJ;
     swr[i] = j < a.RR ? a.wr[c * a.RR + j] : 0.0f;
+  }
+  // W^T for the backward (x2g_proj.wt): every workgroup writes its share, one element per thread
+  // (the first 8 chunks writing it all made those workgroups the launch's tail)
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kCThreads + tid; i < 4 * kCD * kCD; i += G * kCThreads) {
+    const int p = static_cast<int>(i / (kCD * kCD)), e = static_cast<int>(i % (kCD * kCD));
+    if (a.p[p].wt) a.p[p].wt[e] = a.p[p].w[(e % kCD) * kCD + e / kCD];
   }
   for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
     int r0, nrows;
@@ -1033,13 +1044,6 @@ __global__ void __launch_bounds__(kCThreads, 2 * WPC) conv_proj_fwd_kernel(const
       f4 An[8];
       load_slice<false>(a.p[p + 1 < 4 ? p + 1 : 0].w, w, rl, g, An);
       const f4 bias = bload4(rsrc(P.b ? P.b : P.w), 4 * (16 * w + 4 * g), 0) * (P.b ? 1.0f : 0.0f);
-      if (P.wt && ch < wt_groups) {
-#pragma unroll
-        for (int b = 0; b < 8; ++b)
-          if (b % wt_groups == ch)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) P.wt[(16 * b + 4 * g + e) * kCD + 16 * w + rl] = A[b][e];
-      }
       f4 acc[RB];
       slice_gemm(img[(p == 1 || p == 2) ? 1 : 0], A, acc, rl, g);
 #pragma unroll
@@ -1148,7 +1152,6 @@ struct ProjBwdGateArgs {
   int64_t R;
 };
 
-constexpr int kGateRB = 3;
 
 template <int NJ, bool TW>  // TW: every projection's W^T given (else W read transposed)
 __global__ void __launch_bounds__(kCThreads, 2) conv_proj_bwd_gate_kernel(const ProjBwdGateArgs a) {
@@ -1591,16 +1594,9 @@ static inline unsigned v2_grid(int64_t rows) {
   return static_cast<unsigned>(nblk < 256 ? nblk : 256);
 }
 
-// the projection kernels' chunk height (row blocks) and workgroups per CU (compile-time A/B builds)
-#ifndef X2G_PROJ_RB
-#define X2G_PROJ_RB 6
-#endif
-#ifndef X2G_PROJ_WPC
-#define X2G_PROJ_WPC 1
-#endif
-constexpr int kProjRB = X2G_PROJ_RB, kProjWPC = X2G_PROJ_WPC;
+// the projection kernels: one 512-thread workgroup per CU (two waves per SIMD at 256 VGPRs)
 static inline unsigned proj_grid(int64_t rows) {
-  const int64_t nblk = (rows + 15) / 16, cap = 256 * kProjWPC;
+  const int64_t nblk = (rows + 15) / 16, cap = 256;
   return static_cast<unsigned>(nblk < cap ? nblk : cap);
 }
 
@@ -1625,9 +1621,9 @@ X2G_API int x2g_conv_proj_fwd(const float* x, const float* rbf, int32_t rbf_dim,
   }
   if (!al16(x) || !al16(x_t) || !al16(xs_t)) return X2G_EUNSUPPORTED;
   if (rbf_dim <= 6)
-    conv_proj_fwd_kernel<6, kProjRB, kProjWPC><<<proj_grid(rows), kCThreads, 0, as_stream(stream)>>>(a);
+    conv_proj_fwd_kernel<6><<<proj_grid(rows), kCThreads, 0, as_stream(stream)>>>(a);
   else
-    conv_proj_fwd_kernel<8, kProjRB, kProjWPC><<<proj_grid(rows), kCThreads, 0, as_stream(stream)>>>(a);
+    conv_proj_fwd_kernel<8><<<proj_grid(rows), kCThreads, 0, as_stream(stream)>>>(a);
   return last_launch_status();
 }
 
