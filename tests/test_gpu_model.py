@@ -327,6 +327,29 @@ def test_inference_fused_projection_matches_training_path(cuda, monkeypatch):
     assert rel_err(infer.cpu().numpy(), train.cpu().numpy()) < 1e-5
 
 
+@pytest.mark.parametrize("tile", [257, 4096])
+def test_inference_tiled_projection_equals_whole(cuda, monkeypatch, tile):
+    """Grad mode off with more than ops.INFER_TILE triplets: S = lin_sbf(sbf) is projected and
+    consumed per range of destination edges (at most `tile` triplets; odd range starts included)
+    and never exists whole; the energies equal the untiled inference bit for bit (every
+    destination segment is computed by the same kernel code on the same S rows)."""
+    from x2gnn import ops
+
+    z = golden("model_full.npz")
+    m = product_model(z, cuda)
+    b = batch_from_fixture(z).to(cuda)
+    emb = m.emb_block.embedding.weight
+    w0 = emb.detach().clone()  # every forward applies the max_norm renorm in place: same start for both
+    monkeypatch.setattr(ops, "INFER_TILE", 1 << 30)
+    with torch.no_grad():
+        whole = m(b).cpu()
+        emb.copy_(w0)
+    monkeypatch.setattr(ops, "INFER_TILE", tile)
+    with torch.no_grad():
+        tiled = m(b).cpu()
+    assert torch.equal(whole, tiled)
+
+
 def _dense_cluster(n_atoms=72, seed=5):
     """One molecule whose atoms all sit within 5 A of each other (a 2.4 A-radius ball, >= 0.8 A
     apart): every line node has n_atoms - 2 > 64 triplets, past the kernels' 64-id index chunks."""

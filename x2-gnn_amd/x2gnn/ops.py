@@ -21,6 +21,7 @@ import contextlib
 import ctypes
 import os
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -712,6 +713,75 @@ def flush_keyed():
             call("x2g_keyed_row_sum_batch", srcs, outs, n, ptr(part[0][1]), R, D, nk, 0, ptr(ws), wsb, stream_ptr())
 
 
+# Inference (grad mode off) with many triplets: S = lin_sbf(sbf) [T, D] is projected and consumed one
+# range of destination edges at a time (whole destination segments, at most INFER_TILE triplets),
+# so no more than [INFER_TILE, D] of it exists at once (config 5, T = 3.49M: 1.8 GB per layer
+# whole, 256 MB per tile at the default).  Cost at config 5 (bench --workload aid_infer): 9.34 ms
+# per step whole, 9.74 tiled at 2^19 triplets, 10.75 at 2^17 (per-launch ramp and drain; projecting
+# the next tile on a side stream under the current attention measured no better).
+INFER_TILE = int(os.environ.get("X2G_INFER_TILE", str(1 << 19)))
+
+
+def _infer_tiles(lg, tmax):
+    """[(e0, e1, t0, t1)] destination-edge ranges of at most ``tmax`` triplets each (a longer
+    segment gets a range of its own), cached on the line graph.  With the batch's per-molecule
+    counts (``lg.mol_counts``, set by GraphPlan from host metadata) the ranges are whole molecules,
+    found without touching the device, so a captured graph can be recorded from a fresh line
+    graph; otherwise (the drop-in conv API) from the row pointer, read back once."""
+    cache = lg.__dict__.setdefault("_x2g_infer_tiles", {})
+    if tmax in cache:
+        return cache[tmax]
+    counts = getattr(lg, "mol_counts", None)
+    if counts is not None:
+        ec, tc = counts
+        ep = np.concatenate([[0], np.cumsum(ec)])
+        rp = np.concatenate([[0], np.cumsum(tc)])
+    else:
+        rp = lg.trip_rowptr.cpu().numpy().astype("int64")
+        ep = np.arange(lg.E + 1, dtype=np.int64)
+    n = len(rp) - 1
+    tiles, i = [], 0
+    while i < n:
+        j = int(np.searchsorted(rp, rp[i] + tmax, side="right")) - 1  # furthest j with rp[j] - rp[i] <= tmax
+        j = min(max(j, i + 1), n)
+        if ep[j] > ep[i]:
+            tiles.append((int(ep[i]), int(ep[j]), int(rp[i]), int(rp[j])))
+        i = j
+    cache[tmax] = tiles
+    return tiles
+
+
+def _attention_fwd_tiled(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row, heads, channels, tmax):
+    q, k, v, skip = _f32(q), _f32(k), _f32(v), _f32(skip)
+    sbf, w_sbf, b_sbf = _f32(sbf), _f32(w_sbf), _f32(b_sbf)
+    edge = _f32(edge) if edge is not None else None
+    E, T, D, H = q.shape[0], lg.T, heads * channels, heads
+    f32 = dict(dtype=torch.float32, device=q.device)
+    out, alpha = torch.empty(E, D, **f32), torch.empty(T, H, **f32)
+    smax, sden = torch.empty(E, H, **f32), torch.empty(E, H, **f32)
+    tiles = _infer_tiles(lg, tmax)
+    S = torch.empty(max(t1 - (t0 & ~1) for _, _, t0, t1 in tiles), D, **f32)
+    st = stream_ptr()
+    fb, ib = 4, 4  # bytes per float32 / int32 element
+    for e0, e1, t0, t1 in tiles:
+        ta = t0 & ~1  # from an even row: the projection's fast path wants 16-byte aligned sbf blocks
+        call("x2g_sbf_project", sbf.data_ptr() + ta * sbf.shape[1] * fb, t1 - ta, sbf.shape[1], ptr(w_sbf),
+             ptr(b_sbf), D, ptr(S), st)
+        # the kernel reads S at absolute triplet indices t in [t0, t1): hand it the base S - ta rows;
+        # everything per destination edge is offset by e0, everything per triplet / per source edge
+        # is indexed absolutely
+        if edge_mode == EDGE_PER_DST:
+            e_edge = ptr(edge) if edge_row is not None else edge.data_ptr() + e0 * D * fb
+            e_row = edge_row.data_ptr() + e0 * ib if edge_row is not None else None
+        else:
+            e_edge, e_row = ptr(edge), None
+        call("x2g_sbf_attention_fwd", q.data_ptr() + e0 * D * fb, ptr(k), ptr(v), skip.data_ptr() + e0 * D * fb,
+             e_edge, e_row, edge_mode, S.data_ptr() - ta * D * fb, None, None, lg.trip_rowptr.data_ptr() + e0 * ib,
+             ptr(lg.trip_src), e1 - e0, T, heads, channels, D, out.data_ptr() + e0 * D * fb, ptr(alpha),
+             smax.data_ptr() + e0 * H * fb, sden.data_ptr() + e0 * H * fb, st)
+    return out, alpha, smax, sden
+
+
 def sbf_attention(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg: LineGraph, heads: int, channels: int,
                   edge_mode: int = EDGE_PER_TRIPLET, edge_row=None, return_attention=False):
     """Fused SBFTransformerConv message/softmax/aggregate/skip (see csrc/attention.hip).
@@ -726,6 +796,9 @@ def sbf_attention(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg: LineGraph, heads: 
     if _INFER_FUSED and not torch.is_grad_enabled():
         out, alpha, smax, sden = _attention_fwd_fused(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode,
                                                       edge_row, heads, channels)
+    elif not torch.is_grad_enabled() and lg.T > INFER_TILE and q.shape[0] > 0:
+        out, alpha, smax, sden = _attention_fwd_tiled(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode,
+                                                      edge_row, heads, channels, INFER_TILE)
     else:
         out, alpha, smax, sden = _SBFAttention.apply(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row,
                                                  heads, channels)

@@ -63,6 +63,9 @@ class GraphPlan:
                 p.mol_ptr = (torch.arange(2, device=dev, dtype=torch.int32) * p.num_atoms)
             p.dst_type = ops._i32(data.x.index_select(0, p.lg.edge_dst))
         p.atom_rowptr = p.lg.atom_rowptr
+        # per-molecule line-node / triplet counts on the host: whole-molecule ranges of the triplet
+        # stream for the tiled inference attention (ops._infer_tiles), with no device read
+        p.lg.mol_counts = (np.asarray(edges, dtype=np.int64), np.asarray(trips, dtype=np.int64))
         return p
 
     # ------------------------------------------------------------------ from line-graph tensors
