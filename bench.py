@@ -41,9 +41,9 @@ CFG = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embed
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32) peak, MI355X_MICROARCH.md
 # scripts/pmc_traffic.py outputs (rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench), per workload
-TRAFFIC_JSON = {"qm9_u0": os.path.join(ROOT, "profiles", "r3_pmc_traffic.json"),
-                "qm9_allprop": os.path.join(ROOT, "profiles", "r3_pmc_traffic.json"),
-                "aid_infer": os.path.join(ROOT, "profiles", "r3_pmc_traffic_c5.json")}
+TRAFFIC_JSON = {"qm9_u0": os.path.join(ROOT, "profiles", "r3b_pmc_traffic.json"),
+                "qm9_allprop": os.path.join(ROOT, "profiles", "r3b_pmc_traffic.json"),
+                "aid_infer": os.path.join(ROOT, "profiles", "r3b_pmc_traffic_c5.json")}
 # probe name -> the kernel (substring of its symbol) whose PMC bytes it is
 PMC_KERNEL = {"sbf_project": "sbf_project_waves", "attn_fwd": "attn_fwd_batched",
               "attn_bwd_dst": "attn_bwd_dst_g_batched", "attn_bwd_src": "attn_bwd_src_fold_batched",
@@ -248,6 +248,45 @@ def chain_probe(R, reps):
             "chain_wgrad": (_event_time(wgrad, reps), flops)}
 
 
+def proj_probe(R, reps):
+    """The conv projections as the step runs them at this row count: x2g_conv_proj_fwd (lin_rbf
+    gate + q, k, v, skip, the T-layout x / x_src and W^T) and x2g_conv_proj_bwd_gate (dx, the gate's
+    drbf and dW_rbf slab, the four T-layout output gradients), HIP-event timed on the launch stream.
+    FLOPs per launch: 4 * 2 * R * 128 * 128 each."""
+    D, RR = 128, 6
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(6)
+    x = torch.randn(R, D, device=dev, generator=g)
+    rbf = torch.randn(R, RR, device=dev, generator=g)
+    wr = torch.randn(D, RR, device=dev, generator=g)
+    W = [torch.randn(D, D, device=dev, generator=g) / 11.3 for _ in range(4)]
+    B = [torch.randn(D, device=dev, generator=g) for _ in range(4)]
+    out = [torch.empty(R, D, device=dev) for _ in range(4)]
+    grads = [torch.randn(R, D, device=dev, generator=g) for _ in range(4)]
+    WT = [torch.empty(D, D, device=dev) for _ in range(4)]
+    tf = _lib_ws("x2g_chain_t_floats", R, D)
+    x_t, xs_t = torch.empty(tf, device=dev), torch.empty(tf, device=dev)
+    g_t = [torch.empty(tf, device=dev) for _ in range(4)]
+    dx, drbf, dw = torch.zeros(R, D, device=dev), torch.empty(R, RR, device=dev), torch.empty(D, RR, device=dev)
+    wsb = _lib_ws("x2g_conv_proj_bwd_gate_workspace", R, RR)
+    ws = torch.empty(max(wsb, 4), dtype=torch.uint8, device=dev)
+    proj = (ops.Proj * 4)(*[ops.Proj(W[p].data_ptr(), B[p].data_ptr(), out[p].data_ptr(), WT[p].data_ptr())
+                            for p in range(4)])
+    pg = (ops.ProjGrad * 4)(*[ops.ProjGrad(grads[p].data_ptr(), W[p].data_ptr(), WT[p].data_ptr(),
+                                           g_t[p].data_ptr()) for p in range(4)])
+
+    def fwd():
+        call("x2g_conv_proj_fwd", ptr(x), ptr(rbf), RR, ptr(wr), proj, R, D, ptr(x_t), ptr(xs_t), stream_ptr())
+
+    def bwd():  # dx += (the fan-in form the step uses after the first consumer)
+        call("x2g_conv_proj_bwd_gate", pg, R, D, ptr(x), ptr(rbf), RR, ptr(wr), ptr(dx), ptr(dx), ptr(drbf),
+             ptr(dw), 0, ptr(ws), wsb, stream_ptr())
+
+    fwd()
+    flops = 4 * 2.0 * R * D * D
+    return {"conv_proj_fwd": (_event_time(fwd, reps), flops), "conv_proj_bwd_gate": (_event_time(bwd, reps), flops)}
+
+
 def flat_wgrad_probe(reps):
     """The step's largest kernel: every T-layout weight gradient of the backward in one launch
     (x2g_tiled_wgrad_flat, ops._flush_tiled) with the job list the captured step recorded
@@ -323,6 +362,25 @@ def _hbm_entry(name, v, table):
     return {"ms": round(ms, 5), "bytes": int(nbytes), "GBs": round(nbytes / (ms * 1e-3) / 1e9, 1),
             "gathered_bytes": int(gath), "hbm_bytes": hbm,
             "hbm_GBs": None if hbm is None else round(hbm / (ms * 1e-3) / 1e9, 1)}
+
+
+# MFMA probe name -> the kernel (symbol substring) whose PMC bytes it is
+PMC_MFMA_KERNEL = {"conv_proj_fwd": "conv_proj_fwd_kernel", "conv_proj_bwd_gate": "conv_proj_bwd_gate_kernel",
+                   "chain_fwd": "chain_fwd_v4(", "chain_bwd": "chain_bwd_v3_batch",
+                   "tiled_wgrad_flat": "tiled_flat_kernel"}
+
+
+def _mfma_entry(name, v, table):
+    """One MFMA probe in the bench line: time, FLOPs, TF/s and its fraction of the f32 MFMA peak,
+    and the PMC-measured HBM bytes / GB/s of the same kernel in the step (when the summary has it)."""
+    ms, flops = v
+    tfs = flops / (ms * 1e-3) / 1e12
+    e = {"ms": round(ms, 5), "flops": int(flops), "TFs": round(tfs, 2), "mfma_frac": round(tfs / MFMA_F32_PEAK_TFS, 4)}
+    if name in PMC_MFMA_KERNEL:
+        hbm = pmc_traffic([(PMC_MFMA_KERNEL[name], None)], table)
+        e["hbm_bytes"] = hbm
+        e["hbm_GBs"] = None if hbm is None else round(hbm / (ms * 1e-3) / 1e9, 1)
+    return e
 
 
 def _event_time(fn, reps):
@@ -539,6 +597,8 @@ def main():
     sa = scatter_add_probe(plan_lg, args.kernel_reps)
     dense = dense_probe(shape["E"], args.kernel_reps)
     dense.update(chain_probe(shape["E"], args.kernel_reps))
+    if wl["train"]:
+        dense.update(proj_probe(shape["E"], args.kernel_reps))
     # the roofline kernel: the step's largest single kernel in the committed profile
     # (profiles/r2_*_step_kernels.txt) -- the one-launch T-layout weight gradient of the whole
     # backward (x2g_tiled_wgrad_flat), f32 MFMA-bound (sum_j 2 R 128 cols_j FLOP, ~K = R deep)
@@ -604,8 +664,7 @@ def main():
             "roofline": roof,
             "kernels": dict(
                 {k: _hbm_entry(k, v, traffic_table) for k, v in probe.items()},
-                **{k: {"ms": round(v[0], 5), "flops": int(v[1]), "TFs": round(v[1] / (v[0] * 1e-3) / 1e12, 2)}
-                   for k, v in dense.items()}),
+                **{k: _mfma_entry(k, v, traffic_table) for k, v in dense.items()}),
             "roofline_scatter_add": {
                 "kernel": "x2g_segment_sum [T,128]->[E,128]", "bytes_per_launch": sa["bytes"],
                 "warm_GBs": round(sa["bytes"] / (sa["warm_ms"] * 1e-3) / 1e9, 1),
