@@ -806,23 +806,23 @@ struct ChainWgradArgs {
 // lane-linearly, the swizzle applied to the source addresses), two steps in flight ahead of the
 // product; raw s_barrier with counted vmcnt waits so the in-flight copies survive the barriers.
 // One call reduces tiles [t0, t1) of one job into a slab (dW rows 16w + 4g + e, columns 16bk + rl).
-template <int NB, bool SPREAD = true>  // NB LDS buffers: NB - 1 steps in flight ahead of the product;
+template <int NB, bool SPREAD = true, int WT = kWTiles>  // NB LDS buffers: NB - 1 steps in flight ahead of the product;
 // SPREAD: the bias column sums over all eight waves (else waves 0-1 only)
 __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, const float* __restrict__ xin, int64_t t0,
                                               int64_t t1, bool has_b, float* __restrict__ slab,
-                                              float* __restrict__ slab_b, f4 (*Ds)[kWTiles][512],
-                                              f4 (*Xs)[kWTiles][512]) {
+                                              float* __restrict__ slab_b, f4 (*Ds)[WT][512],
+                                              f4 (*Xs)[WT][512]) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int rl = lane & 15, g = lane >> 4;
-  const int nsteps = static_cast<int>((t1 - t0 + kWTiles - 1) / kWTiles);
+  const int nsteps = static_cast<int>((t1 - t0 + WT - 1) / WT);
   // LDS position P = 64w + lane of a tile image holds source chunk (P >> 2) * 4 + ((P & 3) ^ sigma)
   const int P = 64 * w + lane;
   const int src_chunk = (P >> 2) * 4 + ((P & 3) ^ (((P >> 5) & 1) * 3));
   auto issue = [&](int step) {  // the step's tiles into buffer step % NB (tiles past t1: tile t0)
     const int b = step % NB;
 #pragma unroll
-    for (int k = 0; k < kWTiles; ++k) {
-      int64_t t = t0 + static_cast<int64_t>(step) * kWTiles + k;
+    for (int k = 0; k < WT; ++k) {
+      int64_t t = t0 + static_cast<int64_t>(step) * WT + k;
       t = t < t1 ? t : t0;
       __builtin_amdgcn_global_load_lds(dz + t * 2048 + 4 * src_chunk, &Ds[b][k][64 * w], 16, 0, 0);
       __builtin_amdgcn_global_load_lds(xin + t * 2048 + 4 * src_chunk, &Xs[b][k][64 * w], 16, 0, 0);
@@ -835,22 +835,33 @@ __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, cons
 #pragma unroll
   for (int p = 0; p < NB - 1; ++p)
     if (p < nsteps) issue(p);
+#ifdef X2G_TRACE
+  unsigned long long tw = 0, tc = 0, tprev = wall_clock64();
+#endif
   for (int i = 0; i < nsteps; ++i) {
-    // this step's copies are done when at most the later issued steps' 2 * kWTiles each remain
+    // this step's copies are done when at most the later issued steps' 2 * WT each remain
     const int ahead = nsteps - 1 - i < NB - 2 ? nsteps - 1 - i : NB - 2;
     if (ahead >= 2)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * WT) : "memory");
     else if (ahead == 1)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * WT) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave's copies of this step have landed; step i-1 is read
+#ifdef X2G_TRACE
+    {
+      const unsigned long long t = wall_clock64();
+      tc += 0;
+      tw += t - tprev;
+      tprev = t;
+    }
+#endif
     if (i + NB - 1 < nsteps) issue(i + NB - 1);
     const int b = i % NB;
 #pragma unroll
-    for (int k = 0; k < kWTiles; ++k) {
-      if (t0 + static_cast<int64_t>(i) * kWTiles + k >= t1) break;  // wave-uniform
+    for (int k = 0; k < WT; ++k) {
+      if (t0 + static_cast<int64_t>(i) * WT + k >= t1) break;  // wave-uniform
       const f4 av = Ds[b][k][tpos(16 * w + rl, g)];
       f4 bv[8];
 #pragma unroll
@@ -871,7 +882,22 @@ __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, cons
         }
       }
     }
+#ifdef X2G_TRACE
+    {  // (the MFMAs are issued; their results are first needed by the next step's ... at the end)
+      asm volatile("s_nop 0" ::: "memory");
+      const unsigned long long t = wall_clock64();
+      tc += t - tprev;
+      tprev = t;
+    }
+#endif
   }
+#ifdef X2G_TRACE
+  if (threadIdx.x == 0) {
+    x2g_trace_buf[blockIdx.x * 16 + 0] += tw;
+    x2g_trace_buf[blockIdx.x * 16 + 1] += tc;
+    x2g_trace_buf[blockIdx.x * 16 + 2] += nsteps;
+  }
+#endif
 #pragma unroll
   for (int bk = 0; bk < 8; ++bk)
 #pragma unroll
@@ -912,11 +938,11 @@ struct TiledFlatArgs {
   int njobs;
 };
 
-// NB LDS buffers of 2 x 2 tiles (NB x 32 KB): 4 (the default, 128 KB) keeps three steps in flight
-template <int NB, bool SPREAD = true>
+// NB LDS buffers of 2 x WT tiles (NB x WT x 16 KB; NB - 1 steps in flight)
+template <int NB, bool SPREAD = true, int WT = kWTiles>
 __global__ void __launch_bounds__(kCThreads, 1) tiled_flat_kernel(const TiledFlatArgs a) {
-  __shared__ f4 Ds[NB][kWTiles][512];
-  __shared__ f4 Xs[NB][kWTiles][512];
+  __shared__ f4 Ds[NB][WT][512];
+  __shared__ f4 Xs[NB][WT][512];
   const int64_t G = gridDim.x, i = blockIdx.x;
   const int64_t lo = i * a.total / G, hi = (i + 1) * a.total / G;
   for (int64_t j = lo / a.ntiles; j < a.njobs && j * a.ntiles < hi; ++j) {
@@ -925,7 +951,7 @@ __global__ void __launch_bounds__(kCThreads, 1) tiled_flat_kernel(const TiledFla
     if (s0 >= s1) continue;
     __syncthreads();  // a previous segment's last buffers are no longer read
     const int64_t k = i - a.wg_lo[j];
-    tiled_segment<NB, SPREAD>(a.dz_t[j], a.in_t[j], s0 - j * a.ntiles, s1 - j * a.ntiles, a.has_b[j] != 0,
+    tiled_segment<NB, SPREAD, WT>(a.dz_t[j], a.in_t[j], s0 - j * a.ntiles, s1 - j * a.ntiles, a.has_b[j] != 0,
                   a.slab_w[j] + k * kCD * kCD, a.slab_b[j] + k * kCD, Ds, Xs);
   }
 }
@@ -1778,7 +1804,9 @@ X2G_API int x2g_tiled_wgrad_flat(const x2g_tiled_job* jobs, int32_t num_jobs, in
     sj[j] = x2g_slab_job{a.slab_w[j], J.db ? a.slab_b[j] : nullptr, J.dw, J.db, kCD * kCD, J.db ? kCD : 0, n,
                          J.ld, J.cols};
   }
-  tiled_flat_kernel<4, true><<<static_cast<unsigned>(G), kCThreads, 0, as_stream(stream)>>>(a);
+  // two 4-tile (64-row) buffers: one step in flight, half the barriers per row of the r2 form (four
+  // 2-tile buffers, three steps in flight): +0.7 % in the step A/B; 3 x 3 tiles measured -0.3 %
+  tiled_flat_kernel<2, true, 4><<<static_cast<unsigned>(G), kCThreads, 0, as_stream(stream)>>>(a);
   const int rc = last_launch_status();
   if (rc) return rc;
   if (flags & X2G_DEFER_SLAB_SUM) {
