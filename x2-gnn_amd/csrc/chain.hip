@@ -938,9 +938,9 @@ struct TiledFlatArgs {
   int njobs;
 };
 
-// NB LDS buffers of 2 x WT tiles (NB x WT x 16 KB; NB - 1 steps in flight)
-template <int NB, bool SPREAD = true, int WT = kWTiles>
-__global__ void __launch_bounds__(kCThreads, 1) tiled_flat_kernel(const TiledFlatArgs a) {
+// NB LDS buffers of 2 x WT tiles (NB x WT x 16 KB; NB - 1 steps in flight); WPC workgroups per CU
+template <int NB, bool SPREAD = true, int WT = kWTiles, int WPC = 1>
+__global__ void __launch_bounds__(kCThreads, 2 * WPC) tiled_flat_kernel(const TiledFlatArgs a) {
   __shared__ f4 Ds[NB][WT][512];
   __shared__ f4 Xs[NB][WT][512];
   const int64_t G = gridDim.x, i = blockIdx.x;
@@ -1741,8 +1741,11 @@ X2G_API int x2g_conv_proj_bwd_gate(const x2g_proj_grad* grads, int64_t rows, int
 }
 
 // ---- one launch for many jobs (x2g_tiled_wgrad_flat)
+// two 512-thread workgroups per CU (66 KB of LDS and 100 VGPRs each: 4 waves per SIMD)
+constexpr int kFlatWPC = 2;
 static inline unsigned flat_grid(int64_t total) {
-  return static_cast<unsigned>(total < 256 ? (total < 1 ? 1 : total) : 256);  // one workgroup per CU (96 KB LDS)
+  const int64_t cap = 256 * kFlatWPC;
+  return static_cast<unsigned>(total < cap ? (total < 1 ? 1 : total) : cap);
 }
 
 // slabs of job j: the workgroups overlapping its tiles
@@ -1804,9 +1807,11 @@ X2G_API int x2g_tiled_wgrad_flat(const x2g_tiled_job* jobs, int32_t num_jobs, in
     sj[j] = x2g_slab_job{a.slab_w[j], J.db ? a.slab_b[j] : nullptr, J.dw, J.db, kCD * kCD, J.db ? kCD : 0, n,
                          J.ld, J.cols};
   }
-  // two 4-tile (64-row) buffers: one step in flight, half the barriers per row of the r2 form (four
-  // 2-tile buffers, three steps in flight): +0.7 % in the step A/B; 3 x 3 tiles measured -0.3 %
-  tiled_flat_kernel<2, true, 4><<<static_cast<unsigned>(G), kCThreads, 0, as_stream(stream)>>>(a);
+  // two independent workgroups per CU, each with two 2-tile buffers: one workgroup's copy waits and
+  // barriers run under the other's MFMAs (+1.4 % in the step A/B over one workgroup per CU with two
+  // 4-tile buffers, which was +0.7 % over r2's one workgroup with four 2-tile buffers; three 3-tile
+  // buffers: -0.3 %).  Twice the slabs (512 + jobs), summed by the deferred slab pass.
+  tiled_flat_kernel<2, true, 2, kFlatWPC><<<static_cast<unsigned>(G), kCThreads, 0, as_stream(stream)>>>(a);
   const int rc = last_launch_status();
   if (rc) return rc;
   if (flags & X2G_DEFER_SLAB_SUM) {
