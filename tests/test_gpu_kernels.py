@@ -1240,7 +1240,7 @@ def _t_layout(x):
 @pytest.mark.parametrize("R,njobs", [(37, 3), (1000, 11), (21058, 52)])
 def test_tiled_wgrad_flat_vs_torch(cuda, R, njobs):
     """x2g_tiled_wgrad_flat: every job's dW = dy^T x and db = colsum(dy) from T-layout operands,
-    jobs concatenated over one workgroup per CU (a workgroup may span two jobs), partials summed by
+    jobs concatenated over two workgroups per CU (a workgroup may span two jobs), partials summed by
     the returned slab jobs; strided (ld, cols) destinations and bias-less jobs included."""
     import ctypes
     from x2gnn import _lib, ops
