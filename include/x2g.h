@@ -196,6 +196,17 @@ int x2g_sbf_attention_fwd(const float* q, const float* k, const float* v, const 
                           int32_t heads, int32_t channels, int32_t sbf_dim, float* out,
                           float* alpha_raw, float* seg_max, float* seg_den, void* stream);
 
+/* The same forward, also writing row_stats[E, 2] = (mean of out[e, :], sum over c of (out[e, c] -
+ * that mean)^2) per output row: the graph LayerNorm that follows the conv (model.py:46, PyG
+ * LayerNorm(mode='graph')) is then fused into the next kernel's staging (x2g_chain_fwd_ln).
+ * row_stats 8-byte aligned. */
+int x2g_sbf_attention_fwd_stats(const float* q, const float* k, const float* v, const float* skip,
+                                const float* edge, const int32_t* edge_row, int edge_mode, const float* sbf,
+                                const float* w_sbf, const float* b_sbf, const int32_t* trip_rowptr,
+                                const int32_t* trip_src, int64_t num_edges, int64_t num_triplets,
+                                int32_t heads, int32_t channels, int32_t sbf_dim, float* out,
+                                float* alpha_raw, float* seg_max, float* seg_den, float* row_stats, void* stream);
+
 /* Backward, destination-major: dq[E,HC]; d_edge ([E,HC] per destination for EDGE_PER_DST,
  * [T,HC] for EDGE_PER_TRIPLET); dlogit[T,H] (grad of alpha_raw); d_sbfproj[T,HC] (grad of S_t,
  * so dW_sbf = d_sbfproj^T sbf and db_sbf = column sums). */
@@ -296,6 +307,10 @@ size_t x2g_graph_layernorm_bwd_workspace(int64_t num_segments);
 int x2g_graph_layernorm_bwd_ex(const float* out, const float* dout, const float* rstd, const int32_t* rowptr,
                                int64_t num_segments, int64_t dim, float* dx, void* workspace, size_t workspace_bytes,
                                void* stream);
+/* The same backward from per-row sums row_gstats[rows, 2] = (sum_c dout, sum_c dout * out) (as
+ * x2g_chain_bwd_ln leaves them): one apply pass, no stats pass over dout and out. */
+int x2g_graph_layernorm_bwd_rows(const float* out, const float* dout, const float* rstd, const int32_t* rowptr,
+                                 int64_t num_segments, int64_t dim, const float* row_gstats, float* dx, void* stream);
 
 /* ---------------------------------------------------------------- loss
  * F.smooth_l1_loss(pred, target, reduction='mean', beta) of the trainer step (trainer.py:41):
@@ -550,6 +565,19 @@ typedef struct {
 int x2g_chain_fwd(const float* x, const float* res_ext, const x2g_chain_stage* stages, int32_t n_stages,
                   int64_t rows, int32_t dim, float* in_t, void* stream);
 
+/* x2g_chain_fwd on LayerNorm(x): the chain's input is PyG's graph LayerNorm of x (model.py:46,
+ * mode='graph', affine=False: per segment g = rows [seg_rowptr[g], seg_rowptr[g+1]) of the
+ * num_segments molecules covering all rows, out = (x - mean_g) / sqrt(var_g + eps) over every row
+ * and feature of the segment), computed while the input is staged from row_stats [rows, 2] (the
+ * (mean, M2) per row of x2g_sbf_attention_fwd_stats): no separate LayerNorm pass.  Also writes the
+ * normalised rows x_norm [rows, dim] (or NULL) and seg_mean / seg_rstd [num_segments] (or NULL) —
+ * the inputs of x2g_graph_layernorm_bwd_ex, which completes the backward.  The stage weight
+ * gradients see the normalised rows as the chain's input (in_t). */
+int x2g_chain_fwd_ln(const float* x, const float* row_stats, const int32_t* seg_rowptr, int64_t num_segments,
+                     float eps, float* x_norm, float* seg_mean, float* seg_rstd, const float* res_ext,
+                     const x2g_chain_stage* stages, int32_t n_stages, int64_t rows, int32_t dim, float* in_t,
+                     void* stream);
+
 /* Several independent chains over the same row count and stage count in ONE launch (job =
  * blockIdx.y; X2-GNN's readout MLPs, readout.py:25-31 / 55-62: Linear+SiLU, Linear+SiLU on the
  * pooled atom rows of every readout).  Each job's fields mean what x2g_chain_fwd's / _bwd's do. */
@@ -581,6 +609,11 @@ typedef struct {
  * Weight gradients: x2g_chain_wgrad over (in_t, dz_t), or x2g_wgrad_batched over row-major pairs. */
 int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_bwd_stage* stages, int32_t n_stages,
                   int64_t rows, int32_t dim, float* dx, float* d_res_ext, float* dz_t, void* stream);
+/* x2g_chain_bwd for a chain run by x2g_chain_fwd_ln: also writes row_gstats[rows, 2] = (sum_c dx,
+ * sum_c dx * x_norm) per row, the input of x2g_graph_layernorm_bwd_rows (x_norm: x2g_chain_fwd_ln's). */
+int x2g_chain_bwd_ln(const float* dy, const float* dy_add, const x2g_chain_bwd_stage* stages, int32_t n_stages,
+                     int64_t rows, int32_t dim, float* dx, float* d_res_ext, float* dz_t, const float* x_norm,
+                     float* row_gstats, void* stream);
 
 /* x2g_chain_bwd for several chains (x2g_chain_fwd_batch's jobs) in one launch. */
 typedef struct {

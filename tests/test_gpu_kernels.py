@@ -1005,6 +1005,98 @@ def test_row_chain_fwd_bwd_vs_torch(cuda, R, kind):
             assert float((m.bias.grad.double() - b.grad).abs().max()) <= 2e-5 * float(b.grad.abs().max()) + 1e-6
 
 
+def _graph_ln_ref(x, rowptr, eps):
+    """PyG LayerNorm(mode='graph', affine=False) per row segment (two-pass, biased variance)."""
+    out = torch.empty_like(x)
+    rp = rowptr.tolist()
+    for g in range(len(rp) - 1):
+        a, b = rp[g], rp[g + 1]
+        if b > a:
+            xs = x[a:b]
+            xc = xs - xs.mean()
+            out[a:b] = xc / torch.sqrt((xc * xc).mean() + eps)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sizes", ["qm9", "ragged"])
+def test_row_chain_fused_graph_layernorm(cuda, sizes):
+    """ops.row_chain(x, ..., ln=...) (x2g_chain_fwd_ln: the graph LayerNorm of model.py:46 applied
+    while staging, from per-row (mean, M2) statistics) == LayerNorm then row_chain, forward and every
+    gradient, against fp64 torch; segments of 1..400 rows (chunks holding many molecules, molecules
+    spanning several chunks) and empty segments; the row statistics as x2g_sbf_attention_fwd_stats
+    writes them."""
+    from x2gnn import ops
+
+    g = torch.Generator(device="cpu").manual_seed(7)
+    if sizes == "qm9":
+        counts = [165] * 128
+    else:
+        counts = [int(c) for c in torch.randint(0, 40, (60,), generator=g)] + [0, 400, 1, 0, 2, 257]
+    rowptr = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32)
+    R, G, eps = int(rowptr[-1]), len(counts), 1e-8
+    S, H, RH, RE = ops.CHAIN_SILU, ops.CHAIN_HOLD, ops.CHAIN_RES_HELD, ops.CHAIN_RES_EXT
+    flags = [S | H, S | RH, S | RE, S | H, S | RH, S | H, S | RH]
+    gd = torch.Generator(device=cuda).manual_seed(R)
+    lins = [torch.nn.Linear(128, 128).to(cuda) for _ in flags]
+    with torch.no_grad():
+        for m in lins:
+            m.weight.copy_(torch.randn(128, 128, device=cuda, generator=gd) / 11.3)
+            m.bias.copy_(torch.randn(128, device=cuda, generator=gd) * 0.1)
+    x = (torch.randn(R, 128, device=cuda, generator=gd) * 2.0 + 0.7).requires_grad_(True)
+    res = torch.randn(R, 128, device=cuda, generator=gd).requires_grad_(True)
+    xd = x.detach()
+    mu_r = xd.mean(1)
+    stats = torch.stack([mu_r, ((xd - mu_r[:, None]) ** 2).sum(1)], 1).contiguous()
+    y = ops.row_chain(x, res, lins, flags, ln=(stats, rowptr.to(cuda), G, eps))
+    dy = torch.randn(R, 128, device=cuda, generator=gd)
+    y.backward(dy)
+    x64 = x.detach().double().requires_grad_(True)
+    r64 = res.detach().double().requires_grad_(True)
+    wd = [m.weight.detach().double().requires_grad_(True) for m in lins]
+    bd = [m.bias.detach().double().requires_grad_(True) for m in lins]
+    yr = _chain_ref(_graph_ln_ref(x64, rowptr, eps), r64, wd, bd, flags)
+    yr.backward(dy.double())
+    torch.testing.assert_close(y.double(), yr, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(x.grad.double(), x64.grad, rtol=1e-5, atol=1e-5 * float(x64.grad.abs().max()))
+    torch.testing.assert_close(res.grad.double(), r64.grad, rtol=1e-5, atol=1e-5)
+    for m, w, b in zip(lins, wd, bd):
+        assert float((m.weight.grad.double() - w.grad).abs().max()) <= 2e-5 * float(w.grad.abs().max()) + 1e-6
+        assert float((m.bias.grad.double() - b.grad).abs().max()) <= 2e-5 * float(b.grad.abs().max()) + 1e-6
+
+
+@pytest.mark.gpu
+def test_attention_row_stats(cuda):
+    """x2g_sbf_attention_fwd_stats: the same outputs as x2g_sbf_attention_fwd (bitwise) plus per-row
+    (mean, sum of squared deviations) of out, vs torch."""
+    from x2gnn import ops
+    from x2gnn._lib import call, ptr, stream_ptr
+
+    z = golden("triplets.npz")
+    lg = _lg(z["s160_edge_index"], int(z["s160_num_nodes"]), z["s160_trip"].shape[1], cuda)
+    E, T, H, C = lg.E, lg.T, 16, 8
+    D = H * C
+    gd = torch.Generator(device=cuda).manual_seed(5)
+    q, k, v, skip = (torch.randn(E, D, device=cuda, generator=gd) for _ in range(4))
+    table = torch.randn(10, D, device=cuda, generator=gd)
+    erow = torch.randint(0, 10, (E,), device=cuda, generator=gd).to(torch.int32)
+    sp = torch.randn(T, D, device=cuda, generator=gd)
+    outs = []
+    for stats in (None, torch.empty(E, 2, device=cuda)):
+        out, alpha = torch.empty(E, D, device=cuda), torch.empty(T, H, device=cuda)
+        smax, sden = torch.empty(E, H, device=cuda), torch.empty(E, H, device=cuda)
+        name = "x2g_sbf_attention_fwd" if stats is None else "x2g_sbf_attention_fwd_stats"
+        call(name, ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(erow), ops.EDGE_PER_DST, ptr(sp), None, None,
+             ptr(lg.trip_rowptr), ptr(lg.trip_src), E, T, H, C, D, ptr(out), ptr(alpha), ptr(smax), ptr(sden),
+             *((ptr(stats),) if stats is not None else ()), stream_ptr())
+        outs.append((out, alpha, stats))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    o = outs[1][0].double()
+    mu = o.mean(1)
+    torch.testing.assert_close(outs[1][2][:, 0].double(), mu, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(outs[1][2][:, 1].double(), ((o - mu[:, None]) ** 2).sum(1), rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.gpu
 def test_row_chain_rejects_bad_programs(cuda):
     """RES_HELD without a HOLD, two RES_EXT stages, a HOLD..RES_HELD pair spanning the RES_EXT

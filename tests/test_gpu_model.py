@@ -55,6 +55,39 @@ def test_model_energies_and_gradients_vs_reference(cuda, fixture):
             assert np.abs(p.grad.cpu().numpy() - ref).max() <= 2e-3 * np.abs(ref).max() + 1e-6 * scale, n
 
 
+def _fwd_bwd(z, cuda):
+    m = product_model(z, cuda)
+    b = batch_from_fixture(z).to(cuda)
+    res = m(b)
+    torch.nn.functional.smooth_l1_loss(res, b.y).backward()
+    torch.cuda.synchronize()
+    return res.detach().cpu(), [p.grad.detach().cpu().clone() if p.grad is not None else None
+                                for p in m.parameters()]
+
+
+@pytest.mark.parametrize("fixture", ["model_full.npz", "model_aid.npz"])
+@pytest.mark.parametrize("switch", ["_LN_FUSE", "_LN_BWD_ROWS"])
+def test_fused_variants_equal_separate(cuda, monkeypatch, fixture, switch):
+    """_LN_FUSE: the graph LayerNorm fused into the row chain (attention row statistics +
+    x2g_chain_fwd_ln) == the separate LayerNorm kernels; _LN_BWD_ROWS: the fused LayerNorm's backward
+    from the chain backward's per-row sums (x2g_chain_bwd_ln + x2g_graph_layernorm_bwd_rows) == its
+    two-pass backward.  Energies and every gradient to fp32 rounding (other summation orders)."""
+    from x2gnn import ops
+
+    z = golden(fixture)
+    outs = []
+    for on in (True, False):
+        monkeypatch.setattr(ops, switch, on)
+        outs.append(_fwd_bwd(z, cuda))
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-5, atol=1e-6)
+    top = max(float(g.abs().max()) for g in outs[1][1] if g is not None)
+    for a, c in zip(outs[0][1], outs[1][1]):
+        if c is None:
+            assert a is None
+            continue
+        torch.testing.assert_close(a, c, rtol=1e-4, atol=1e-5 * top)
+
+
 def test_model_is_deterministic(cuda):
     z = golden("model_full.npz")
     out = []

@@ -61,6 +61,7 @@ struct AttnArgs {
   float* alpha_out;
   float* smax_out;
   float* sden_out;
+  float2* row_stats;  // fwd: per output row (mean, sum of squared deviations) for a fused graph LayerNorm, or NULL
   float* dq;
   float* d_edge;
   float* dlogit;
@@ -158,6 +159,27 @@ __device__ __forceinline__ void zero_row(float (&r)[CPL]) {
   for (int j = 0; j < CPL; ++j) r[j] = 0.f;
 }
 
+// Per-row statistics of an output row for the graph LayerNorm that follows the conv (model.py:46):
+// rs[e] = (mean over the row's D values, sum of their squared deviations from it).  The consumer
+// (x2g_chain_fwd_ln) combines a molecule's rows exactly (Chan: M2 = sum M2_r + D sum (mean_r -
+// mean)^2), so the LayerNorm needs no pass of its own over the rows.
+template <int CPL>
+__device__ __forceinline__ void store_row_stats(float2* __restrict__ rs, int64_t e, const float (&o)[CPL], bool act,
+                                                int D, int lane) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) s += act ? o[j] : 0.f;
+  const float mu = group_sum<kWave>(s) / static_cast<float>(D);
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const float d = o[j] - mu;
+    q = act ? fmaf(d, d, q) : q;
+  }
+  q = group_sum<kWave>(q);
+  if (lane == 0) rs[e] = make_float2(mu, q);
+}
+
 // Every kernel below takes its pointers as __restrict__ parameters: with them the compiler may
 // serve wave-uniform reads (row pointers, triplet indices, the sbf row) from the scalar cache.
 
@@ -252,7 +274,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(
     const float* __restrict__ sbf, const float* __restrict__ w, const float* __restrict__ b,
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ tsrc, int64_t E, int D, int H, float sqrt_c,
     float* __restrict__ out, float* __restrict__ alpha_out, float* __restrict__ smax_out,
-    float* __restrict__ sden_out) {
+    float* __restrict__ sden_out, float2* __restrict__ row_stats) {
   const int lane = threadIdx.x & 63;
   const bool act = lane * CPL < D;
   const int c0 = act ? lane * CPL : 0;
@@ -294,6 +316,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(
 #pragma unroll
     for (int j = 0; j < CPL; ++j) o[j] = st.acc[j] * inv + sk[j];
     store_row<CPL>(out + e * D + c0, act, o);
+    if (row_stats) store_row_stats<CPL>(row_stats, e, o, act, D, lane);
     if (leader) {
       smax_out[e * H + head] = st.m;
       sden_out[e * H + head] = st.den;
@@ -344,7 +367,7 @@ __global__ void __launch_bounds__(256) attn_fwd_batched(
     const float* __restrict__ skip, const float* __restrict__ edge, const int32_t* __restrict__ edge_row,
     const float* __restrict__ sp, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ tsrc, int64_t E,
     int D, int H, float sqrt_c, float* __restrict__ out, float* __restrict__ alpha_out, float* __restrict__ smax_out,
-    float* __restrict__ sden_out) {
+    float* __restrict__ sden_out, float2* __restrict__ row_stats) {
   const int lane = threadIdx.x & 63;
   const bool act = lane * CPL < D;
   const int c0 = act ? lane * CPL : 0;
@@ -379,6 +402,7 @@ __global__ void __launch_bounds__(256) attn_fwd_batched(
 #pragma unroll
     for (int c = 0; c < CPL; ++c) o[c] = st.acc[c] * inv + sk[c];
     store_row<CPL>(out + e * D + c0, act, o);
+    if (row_stats) store_row_stats<CPL>(row_stats, e, o, act, D, lane);
     if (leader) {
       smax_out[e * H + head] = st.m;
       sden_out[e * H + head] = st.den;
@@ -701,12 +725,12 @@ void launch_pre(Pass pass, const AttnArgs& a, unsigned blocks, hipStream_t st) {
       if (PRE && MODE != X2G_EDGE_PER_TRIPLET) {  // batched: up to 8 triplets' rows in flight per wave
         attn_fwd_batched<CPL, LPH, MODE><<<blocks, 256, 0, st>>>(a.q, a.k, a.v, a.skip, a.edge, a.edge_row, a.sbf,
                                                                  a.rowptr, a.tidx, a.E, a.D, a.H, a.sqrt_c, a.out,
-                                                                 a.alpha_out, a.smax_out, a.sden_out);
+                                                                 a.alpha_out, a.smax_out, a.sden_out, a.row_stats);
         break;
       }
       attn_fwd_kernel<CPL, LPH, MODE, PRE><<<blocks, 256, 0, st>>>(
           a.q, a.k, a.v, a.skip, a.edge, a.edge_row, a.sbf, a.w, a.b, a.rowptr, a.tidx, a.E, a.D, a.H, a.sqrt_c, a.out,
-          a.alpha_out, a.smax_out, a.sden_out);
+          a.alpha_out, a.smax_out, a.sden_out, a.row_stats);
       break;
     case Pass::kBwdDst:
       attn_bwd_dst_kernel<CPL, LPH, MODE, PRE><<<blocks, 256, 0, st>>>(
@@ -806,6 +830,26 @@ X2G_API int x2g_sbf_attention_fwd(const float* q, const float* k, const float* v
   a.q = q; a.k = k; a.v = v; a.skip = skip; a.edge = edge; a.edge_row = edge_row; a.edge_mode = edge_mode;
   a.sbf = sbf; a.w = w_sbf; a.b = b_sbf; a.rowptr = trip_rowptr; a.tidx = trip_src; a.E = E;
   a.out = out; a.alpha_out = alpha_raw; a.smax_out = seg_max; a.sden_out = seg_den;
+  return dispatch(Pass::kFwd, a, heads, channels, sbf_dim, as_stream(stream));
+}
+
+X2G_API int x2g_sbf_attention_fwd_stats(const float* q, const float* k, const float* v, const float* skip,
+                                        const float* edge, const int32_t* edge_row, int edge_mode, const float* sbf,
+                                        const float* w_sbf, const float* b_sbf, const int32_t* trip_rowptr,
+                                        const int32_t* trip_src, int64_t E, int64_t T, int32_t heads,
+                                        int32_t channels, int32_t sbf_dim, float* out, float* alpha_raw,
+                                        float* seg_max, float* seg_den, float* row_stats, void* stream) {
+  if (E > 0 && (!q || !k || !v || !skip || !sbf || (w_sbf && !b_sbf) || !trip_rowptr || !out || !seg_max ||
+                !seg_den || !row_stats))
+    return X2G_EINVAL;
+  if (T > 0 && (!trip_src || !alpha_raw)) return X2G_EINVAL;
+  if (edge_mode != X2G_EDGE_NONE && !edge) return X2G_EINVAL;
+  if (reinterpret_cast<uintptr_t>(row_stats) % 8) return X2G_EUNSUPPORTED;
+  AttnArgs a{};
+  a.q = q; a.k = k; a.v = v; a.skip = skip; a.edge = edge; a.edge_row = edge_row; a.edge_mode = edge_mode;
+  a.sbf = sbf; a.w = w_sbf; a.b = b_sbf; a.rowptr = trip_rowptr; a.tidx = trip_src; a.E = E;
+  a.out = out; a.alpha_out = alpha_raw; a.smax_out = seg_max; a.sden_out = seg_den;
+  a.row_stats = reinterpret_cast<float2*>(row_stats);
   return dispatch(Pass::kFwd, a, heads, channels, sbf_dim, as_stream(stream));
 }
 
@@ -1046,7 +1090,7 @@ void fold_launch_mode(bool dst, const FoldArgs& a, unsigned blocks, hipStream_t 
           a.sqrt_c, a.dq, a.d_edge, a.g_out, a.prob_out, a.rho_out);
   } else {  // source-major pass
     const int C = a.D / a.H;
-    if (a.mode == X2G_EDGE_PER_DST)
+if (a.mode == X2G_EDGE_PER_DST)
       attn_bwd_src_fold_batched<CPL, true><<<blocks, 256, 0, st>>>(
           a.q, a.v, a.edge, a.edge_row, a.edge_rows, a.sp, a.y, a.rowptr, a.tidx, a.tdst, a.prob, a.rho_in, a.g_in,
           a.dout, a.E, a.D, a.H, C, a.dk, a.dv, a.gfold);

@@ -53,6 +53,8 @@ struct ChainBwdArgs {
   float* dx;
   float* dres;
   float* dz_t;    // T-layout dz per stage (or NULL)
+  const float* ln_y;   // the LayerNorm output the chain read (x2g_chain_fwd_ln's x_norm), or NULL
+  float2* ln_gstats;   // with ln_y: per row (sum_c dx, sum_c dx * ln_y) for the LayerNorm backward
   int64_t tf;
   int64_t R;
   int n;
@@ -485,10 +487,87 @@ __device__ __forceinline__ void fwd4_stage(const ChainFwdArgs& a, int s, const f
   for (int b = 0; b < 8; ++b) A[b] = An[b];
 }
 
-__device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a) {
+// Graph LayerNorm (model.py:46, PyG LayerNorm(mode='graph'): per molecule, mean and biased
+// variance over all its rows and features, out = (x - mean) / sqrt(var + eps)) applied while the
+// chain's first input is staged, from per-row statistics the producing kernel left
+// (x2g_sbf_attention_fwd_stats: (mean_r, M2_r) per row): the molecule's statistics are the exact
+// Chan combination mean = sum_r mean_r / n, M2 = sum_r (M2_r + D (mean_r - mean)^2), so the
+// LayerNorm needs no pass of its own over the rows.
+struct ChainLn {
+  const float2* stats;   // [R] (mean_r, M2_r) or NULL: no LayerNorm
+  const int32_t* ptr;    // [G + 1] rows per molecule (CSR)
+  float* out;            // [R, D] the normalised rows (the LayerNorm backward's input), or NULL
+  float* mean;           // [G] or NULL
+  float* rstd;           // [G] or NULL
+  int64_t G;
+  float eps;
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// stage_rows for the chain's first input with the graph LayerNorm applied; lnrow: LDS scratch of
+// RB * 16 (mean, denominator) pairs.  The x rows go to LDS by buffer_load ... lds first (no
+// registers held across the rest), so their latency hides under the statistics; each wave
+// combines the statistics of every 8th molecule that has rows in the chunk (every workgroup that
+// holds rows of a molecule computes the same values, in the same order); the workgroup holding a
+// molecule's first row writes its mean / rstd; then every image element is normalised in place.
+template <int RB = kV2RB>
+__device__ __forceinline__ void stage_rows_ln(f4* __restrict__ img, const float* __restrict__ P, int64_t R,
+                                              const ChainLn& ln, float2* __restrict__ lnrow, int r0, int nrows) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  stage_rows_async<RB>(img, P, R, r0);
+  // first molecule with rows here: (#molecules whose first row <= r0) - 1
+  float cnt = 0.f;
+  for (int64_t k = lane; k <= ln.G; k += 64) cnt += ln.ptr[k] <= r0 ? 1.f : 0.f;
+  const int64_t m0 = static_cast<int64_t>(wave_sum(cnt)) - 1;
+  for (int64_t m = (m0 > 0 ? m0 : 0) + w; m < ln.G; m += kCWaves) {
+    const int p0 = uniform(ln.ptr[m]), p1 = uniform(ln.ptr[m + 1]);
+    if (p0 >= r0 + nrows) break;
+    if (p1 <= p0) continue;
+    const float n = static_cast<float>(p1 - p0);
+    float s = 0.f;
+    for (int r = p0 + lane; r < p1; r += 64) s += ln.stats[r].x;
+    const float mu = wave_sum(s) / n;
+    float q = 0.f;
+    for (int r = p0 + lane; r < p1; r += 64) {
+      const float2 st = ln.stats[r];
+      const float d = st.x - mu;
+      q += fmaf(static_cast<float>(kCD) * d, d, st.y);
+    }
+    const float denom = sqrtf(wave_sum(q) / (n * static_cast<float>(kCD)) + ln.eps);
+    const int lo = p0 > r0 ? p0 : r0, hi = p1 < r0 + nrows ? p1 : r0 + nrows;
+    for (int r = lo + lane; r < hi; r += 64) lnrow[r - r0] = make_float2(mu, denom);
+    if (lane == 0 && p0 >= r0) {
+      if (ln.mean) ln.mean[m] = mu;
+      if (ln.rstd) ln.rstd[m] = 1.0f / denom;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the image copies
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < RB; ++u) {
+    const int q = tid + kCThreads * u, r = q >> 5, c = q & 31;
+    const bool ok = r < nrows;
+    const float2 st = lnrow[ok ? r : 0];
+    const f4 v = img[ipos(r, c)];
+    f4 y;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[e] = ok ? (v[e] - st.x) / st.y : 0.0f;
+    img[ipos(r, c)] = y;
+    if (ln.out && ok) *reinterpret_cast<f4*>(ln.out + (r0 + r) * kCD + 4 * c) = y;
+  }
+}
+
+template <bool LN>
+__device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a, const ChainLn& ln) {
   __shared__ f4 img0[kV2Img];
   __shared__ f4 img1[kV2Img];
   __shared__ f4 imgr[kV2Img];
+  __shared__ float2 lnrow[LN ? kV2RB * 16 : 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int rl = lane & 15, g = lane >> 4;
   const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
@@ -505,7 +584,10 @@ __device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a) {
     int r0, nrows;
     chunk_rows(ch, nch, nblk, a.R, r0, nrows);
     __syncthreads();
-    stage_rows(img0, a.x, nullptr, r0, nrows);
+    if (LN)
+      stage_rows_ln(img0, a.x, a.R, ln, lnrow, r0, nrows);
+    else
+      stage_rows(img0, a.x, nullptr, r0, nrows);
     if (a.res) stage_rows(imgr, a.res, nullptr, r0, nrows);
     f4 A[8], held[kV2RB];
     load_slice<false>(a.st[0].w, w, rl, g, A);
@@ -525,7 +607,16 @@ __device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a) {
   }
 }
 
-__global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4(const ChainFwdArgs a) { chain_fwd_v4_run(a); }
+__global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4(const ChainFwdArgs a) { chain_fwd_v4_run<false>(a, {}); }
+
+// the chain with the graph LayerNorm of its input fused into the staging (x2g_chain_fwd_ln)
+struct ChainFwdLnArgs {
+  ChainFwdArgs a;
+  ChainLn ln;
+};
+__global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4_ln(const ChainFwdLnArgs b) {
+  chain_fwd_v4_run<true>(b.a, b.ln);
+}
 
 // several independent chains over the same row count in one launch (job = blockIdx.y): the
 // readouts' MLPs, whose 2304 atom rows alone would fill a tenth of the chip
@@ -534,13 +625,16 @@ struct ChainFwdBatch {
   ChainFwdArgs a[kChainMaxJobs];
 };
 __global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4_batch(const ChainFwdBatch b) {
-  chain_fwd_v4_run(b.a[blockIdx.y]);
+  chain_fwd_v4_run<false>(b.a[blockIdx.y], {});
 }
 
 // ---- backward v3 (the shipped kernel): the v2 design with stage s-1's elementwise
 // part (residual gradients, dz = g SiLU'(z), the dz stores, the T-layout copy) computed per third of
 // the row blocks and scheduled into the next third's MFMAs, branch-free as the forward v3.
-template <int RB0, int RB1>
+// EXT: the stage has an external residual gradient (d_res_ext read-modify-write) or a row-major dz
+// output; without (6 of the trunk's 7 stages) those loads / stores are not issued at all (as
+// dropped out-of-range buffer operations they still cost the wave 18 memory instructions a stage)
+template <int RB0, int RB1, bool EXT = true>
 __device__ __forceinline__ void bwd_elem(f4 (&gs)[kV2RB], f4 (&dh)[kV2RB], const f4 (&zc)[kV2RB], const f4 (&acc)[kV2RB],
                                          float hold_m, float held_m, float silu_m, float dres_acc_m, rsrc_t dres_r,
                                          rsrc_t dz_r, rsrc_t t_r, f4* __restrict__ out, int r0, int nrows, int w,
@@ -554,13 +648,15 @@ __device__ __forceinline__ void bwd_elem(f4 (&gs)[kV2RB], f4 (&dh)[kV2RB], const
     const int off = r < nrows ? 4 * ((r0 + r) * kCD + col) : kOOB;
     const f4 gv = acc[rb] + dh[rb] * hold_m;  // in_s was also the held residual (stage s HOLD)
     dh[rb] = dh[rb] * (1.0f - hold_m) + gv * held_m;  // stage s-1 adds the held residual
-    const f4 ld = bload4(dres_r, off, 0);  // (out of range / off: 0)
-    const f4 old = dres_acc_m != 0.0f ? ld : zero4();  // select, not a product: a fresh buffer may hold NaN
-    bstore4(dres_r, gv + old, off);
+    if (EXT) {
+      const f4 ld = bload4(dres_r, off, 0);  // (out of range / off: 0)
+      const f4 old = dres_acc_m != 0.0f ? ld : zero4();  // select, not a product: a fresh buffer may hold NaN
+      bstore4(dres_r, gv + old, off);
+    }
     f4 dz;
 #pragma unroll
     for (int e = 0; e < 4; ++e) dz[e] = gv[e] * (silu_m * silu_grad_fast(zc[rb][e]) + (1.0f - silu_m));
-    bstore4(dz_r, dz, off);
+    if (EXT) bstore4(dz_r, dz, off);
     out[ipos(r, 4 * w + g)] = dz;
     gs[rb] = dz;
     f4 t = quad_transpose(dz, j);
@@ -568,6 +664,38 @@ __device__ __forceinline__ void bwd_elem(f4 (&gs)[kV2RB], f4 (&dh)[kV2RB], const
     for (int e = 0; e < 4; ++e) t[e] = 16 * rb + 4 * m + e < nrows ? t[e] : 0.0f;
     bstore4(t_r, t, rb < ntile ? 4 * static_cast<int>((static_cast<int64_t>(r0 >> 4) + rb) * (16 * kCD) + f * 16 + 4 * m)
                                : kOOB);
+  }
+}
+
+// store_img of the chain's input gradient g, plus the per-row sums the graph LayerNorm backward needs
+// (sum_c g, sum_c g y with y the LayerNorm output: PyG LayerNorm(mode='graph') backward,
+// dx = rstd (g - mean(g) - y mean(g y)) per molecule): a row's 32 chunks sit in 32 consecutive
+// lanes, reduced by xor shuffles; the molecule sums are then a pass over these [R, 2] (no second
+// pass over g and y)
+template <int RB = kV2RB>
+__device__ __forceinline__ void store_img_lnstats(float* __restrict__ P, const f4* __restrict__ img,
+                                                  const float* __restrict__ Y, float2* __restrict__ gs, int r0,
+                                                  int nrows) {
+  const int tid = threadIdx.x;
+  f4 yv[RB];
+#pragma unroll
+  for (int u = 0; u < RB; ++u) {
+    const int q = tid + kCThreads * u, r = q >> 5, c = q & 31;
+    yv[u] = *reinterpret_cast<const f4*>(Y + (r0 + (r < nrows ? r : 0)) * kCD + 4 * c);
+  }
+#pragma unroll
+  for (int u = 0; u < RB; ++u) {
+    const int q = tid + kCThreads * u, r = q >> 5, c = q & 31;
+    const f4 g = img[ipos(r, c)];
+    if (r < nrows) *reinterpret_cast<f4*>(P + (r0 + r) * kCD + 4 * c) = g;
+    float s1 = (g[0] + g[1]) + (g[2] + g[3]);
+    float s2 = fmaf(g[0], yv[u][0], fmaf(g[1], yv[u][1], fmaf(g[2], yv[u][2], g[3] * yv[u][3])));
+#pragma unroll
+    for (int off = 1; off < 32; off <<= 1) {
+      s1 += __shfl_xor(s1, off, 64);
+      s2 += __shfl_xor(s2, off, 64);
+    }
+    if (c == 0 && r < nrows) gs[r0 + r] = make_float2(s1, s2);
   }
 }
 
@@ -610,6 +738,12 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
       dz_r = rsrc_n(S.dz ? S.dz : a.dy, a.R * kCD * 4, S.dz != nullptr);
       t_r = rsrc_n(a.dz_t ? a.dz_t + s * a.tf : a.dy, a.tf * 4, a.dz_t != nullptr);
     };
+    // whether stage s's elementwise part stores anything but dz in the T layout (wave-uniform)
+#ifdef X2G_AB_NOEXT  // A/B measurement only (wrong d_res_ext): no stage issues the external loads / stores
+    auto ext_of = [&](int) { return std::false_type{}; };
+#else
+    auto ext_of = [&](int) { return std::true_type{}; };
+#endif
     load_wslice(n - 1, A);
     load_z(n - 1);
     f4 acc0[kV2RB];
@@ -631,8 +765,8 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
       float held_m, silu_m, dres_acc_m;
       rsrc_t dres_r, dz_r, t_r;
       elem_args(n - 1, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r);
-      bwd_elem<0, kV2RB>(gs, dh, zc, acc0, 0.0f, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, img[p], r0, nrows, w,
-                         rl, g);
+      bwd_elem<0, kV2RB, decltype(ext_of(0))::value>(gs, dh, zc, acc0, 0.0f, held_m, silu_m, dres_acc_m, dres_r, dz_r,
+                                                      t_r, img[p], r0, nrows, w, rl, g);
     }
     __syncthreads();
     X2G_TR(1);
@@ -648,20 +782,24 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
         float held_m, silu_m, dres_acc_m;
         rsrc_t dres_r, dz_r, t_r;
         elem_args(s - 1, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r);
-        half_gemm<0, 2>(in, A, acc, rl, g);
-        __builtin_amdgcn_sched_barrier(0);
-        half_gemm<2, 4>(in, A, acc, rl, g);
-        bwd_elem<0, 2>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows, w, rl,
-                       g);
-        interleave_epi_sched();
-        __builtin_amdgcn_sched_barrier(0);
-        half_gemm<4, 6>(in, A, acc, rl, g);
-        bwd_elem<2, 4>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows, w, rl,
-                       g);
-        interleave_epi_sched();
-        __builtin_amdgcn_sched_barrier(0);
-        bwd_elem<4, 6>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows, w, rl,
-                       g);
+        auto body = [&](auto ext) {
+          constexpr bool X = decltype(ext)::value;
+          half_gemm<0, 2>(in, A, acc, rl, g);
+          __builtin_amdgcn_sched_barrier(0);
+          half_gemm<2, 4>(in, A, acc, rl, g);
+          bwd_elem<0, 2, X>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows,
+                            w, rl, g);
+          interleave_epi_sched();
+          __builtin_amdgcn_sched_barrier(0);
+          half_gemm<4, 6>(in, A, acc, rl, g);
+          bwd_elem<2, 4, X>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows,
+                            w, rl, g);
+          interleave_epi_sched();
+          __builtin_amdgcn_sched_barrier(0);
+          bwd_elem<4, 6, X>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows,
+                            w, rl, g);
+        };
+        body(ext_of(s - 1));
       } else {
         slice_gemm(in, A, acc, rl, g);
 #pragma unroll
@@ -675,7 +813,10 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
 #pragma unroll
       for (int b = 0; b < 8; ++b) A[b] = An[b];
     }
-    store_img(a.dx, img[p], r0, nrows);
+    if (a.ln_y)
+      store_img_lnstats(a.dx, img[p], a.ln_y, a.ln_gstats, r0, nrows);
+    else
+      store_img(a.dx, img[p], r0, nrows);
   }
 }
 
@@ -1429,6 +1570,23 @@ X2G_API int x2g_chain_fwd(const float* x, const float* res_ext, const x2g_chain_
   return last_launch_status();
 }
 
+X2G_API int x2g_chain_fwd_ln(const float* x, const float* row_stats, const int32_t* seg_rowptr, int64_t num_segments,
+                             float eps, float* x_norm, float* seg_mean, float* seg_rstd, const float* res_ext,
+                             const x2g_chain_stage* stages, int32_t n_stages, int64_t rows, int32_t dim, float* in_t,
+                             void* stream) {
+  ChainFwdArgs a{};
+  bool empty;
+  if (int rc = chain_fwd_prepare(x, res_ext, stages, n_stages, rows, dim, in_t, a, empty)) return rc;
+  if (num_segments < 0 || (rows > 0 && (!row_stats || !seg_rowptr || num_segments < 1))) return X2G_EINVAL;
+  if (reinterpret_cast<uintptr_t>(row_stats) % 8 || !al16(x_norm)) return X2G_EUNSUPPORTED;
+  if (empty) return X2G_OK;
+  const ChainFwdLnArgs b{a, {reinterpret_cast<const float2*>(row_stats), seg_rowptr, x_norm, seg_mean, seg_rstd,
+                             num_segments, eps}};
+  const int64_t nblk = (rows + 15) / 16;
+  chain_fwd_v4_ln<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, as_stream(stream)>>>(b);
+  return last_launch_status();
+}
+
 static int chain_bwd_prepare(const float* dy, const float* dy_add, const x2g_chain_bwd_stage* stages, int32_t n_stages,
                              int64_t rows, int32_t dim, float* dx, float* d_res_ext, float* dz_t, ChainBwdArgs& a,
                              bool& empty, bool& res_accum) {
@@ -1471,13 +1629,7 @@ static int chain_bwd_prepare(const float* dy, const float* dy_add, const x2g_cha
   return X2G_OK;
 }
 
-X2G_API int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_bwd_stage* stages, int32_t n_stages,
-                          int64_t rows, int32_t dim, float* dx, float* d_res_ext, float* dz_t, void* stream) {
-  ChainBwdArgs a{};
-  bool empty, res_accum;
-  if (int rc = chain_bwd_prepare(dy, dy_add, stages, n_stages, rows, dim, dx, d_res_ext, dz_t, a, empty, res_accum))
-    return rc;
-  if (empty) return X2G_OK;
+static int chain_bwd_launch(const ChainBwdArgs& a, int64_t rows, void* stream) {
   hipStream_t st = as_stream(stream);
   {  // through the batched kernel: a by-value ChainBwdArgs handed to the shared body by reference is
      // copied to scratch (392 B, 79 -> 121 us); a batch entry is not
@@ -1487,6 +1639,31 @@ X2G_API int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_
     chain_bwd_v3_batch<<<dim3(static_cast<unsigned>(nblk < 256 ? nblk : 256), 1), kCThreads, 0, st>>>(b);
   }
   return last_launch_status();
+}
+
+X2G_API int x2g_chain_bwd_ln(const float* dy, const float* dy_add, const x2g_chain_bwd_stage* stages,
+                             int32_t n_stages, int64_t rows, int32_t dim, float* dx, float* d_res_ext, float* dz_t,
+                             const float* x_norm, float* row_gstats, void* stream) {
+  ChainBwdArgs a{};
+  bool empty, res_accum;
+  if (int rc = chain_bwd_prepare(dy, dy_add, stages, n_stages, rows, dim, dx, d_res_ext, dz_t, a, empty, res_accum))
+    return rc;
+  if (rows > 0 && (!x_norm || !row_gstats)) return X2G_EINVAL;
+  if (!al16(x_norm) || reinterpret_cast<uintptr_t>(row_gstats) % 8) return X2G_EUNSUPPORTED;
+  if (empty) return X2G_OK;
+  a.ln_y = x_norm;
+  a.ln_gstats = reinterpret_cast<float2*>(row_gstats);
+  return chain_bwd_launch(a, rows, stream);
+}
+
+X2G_API int x2g_chain_bwd(const float* dy, const float* dy_add, const x2g_chain_bwd_stage* stages, int32_t n_stages,
+                          int64_t rows, int32_t dim, float* dx, float* d_res_ext, float* dz_t, void* stream) {
+  ChainBwdArgs a{};
+  bool empty, res_accum;
+  if (int rc = chain_bwd_prepare(dy, dy_add, stages, n_stages, rows, dim, dx, d_res_ext, dz_t, a, empty, res_accum))
+    return rc;
+  if (empty) return X2G_OK;
+  return chain_bwd_launch(a, rows, stream);
 }
 
 // grid of a batched chain launch: about one workgroup per CU over all jobs, each job's row blocks

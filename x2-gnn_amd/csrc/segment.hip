@@ -546,6 +546,61 @@ __global__ void __launch_bounds__(kLnSplitThreads) graph_ln_bwd_apply(const floa
   }
 }
 
+// The apply pass from per-row sums (x2g_chain_bwd_ln's row_gstats: (sum_c dy, sum_c dy y) per row)
+// instead of a stats pass over dy and y: each of the segment's kLnSplit blocks sums the segment's
+// row pairs in the same fixed order (so every block holds identical molecule totals), then applies.
+__global__ void __launch_bounds__(kLnSplitThreads) graph_ln_bwd_apply_rows(const float4* __restrict__ y,
+                                                                           const float4* __restrict__ dy,
+                                                                           const float* __restrict__ rstd,
+                                                                           const int32_t* __restrict__ rowptr, int64_t D4,
+                                                                           const float2* __restrict__ rows,
+                                                                           float4* __restrict__ dx) {
+  __shared__ float2 lds[kLnSplitThreads / 64];
+  int64_t g, lo, hi, n;
+  ln_split_range(rowptr, D4, g, lo, hi, n);
+  if (n == 0) return;
+  const int64_t r0 = rowptr[g];
+  float s1 = 0.f, s2 = 0.f;
+  for (int64_t r = threadIdx.x; r < n; r += kLnSplitThreads) {
+    const float2 t = rows[r0 + r];
+    s1 += t.x;
+    s2 += t.y;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s1 += __shfl_xor(s1, off, 64);
+    s2 += __shfl_xor(s2, off, 64);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) lds[wave] = make_float2(s1, s2);
+  __syncthreads();
+  float2 t = lds[0];
+#pragma unroll
+  for (int w = 1; w < kLnSplitThreads / 64; ++w) {
+    t.x += lds[w].x;
+    t.y += lds[w].y;
+  }
+  const float norm = static_cast<float>(n * D4 * 4);
+  const float m1 = t.x / norm, m2 = t.y / norm, r = rstd[g];
+  for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += kLnSplitThreads * kLnSplitUnroll) {
+    float4 gv[kLnSplitUnroll], yv[kLnSplitUnroll];
+#pragma unroll
+    for (int u = 0; u < kLnSplitUnroll; ++u) {
+      const int64_t i = i0 + u * kLnSplitThreads;
+      const int64_t ic = i < hi ? i : lo;
+      gv[u] = dy[ic];
+      yv[u] = y[ic];
+    }
+#pragma unroll
+    for (int u = 0; u < kLnSplitUnroll; ++u) {
+      const int64_t i = i0 + u * kLnSplitThreads;
+      if (i < hi)
+        dx[i] = make_float4(r * (gv[u].x - m1 - yv[u].x * m2), r * (gv[u].y - m1 - yv[u].y * m2),
+                            r * (gv[u].z - m1 - yv[u].z * m2), r * (gv[u].w - m1 - yv[u].w * m2));
+    }
+  }
+}
+
 }  // namespace x2g
 
 using namespace x2g;
@@ -771,5 +826,20 @@ X2G_API int x2g_graph_layernorm_bwd_ex(const float* out, const float* dout, cons
   graph_ln_bwd_apply<<<grid, kLnSplitThreads, 0, st>>>(reinterpret_cast<const float4*>(out),
                                                        reinterpret_cast<const float4*>(dout), rstd, rowptr, D / 4, part,
                                                        reinterpret_cast<float4*>(dx));
+  return last_launch_status();
+}
+
+X2G_API int x2g_graph_layernorm_bwd_rows(const float* out, const float* dout, const float* rstd, const int32_t* rowptr,
+                                         int64_t G, int64_t D, const float* row_gstats, float* dx, void* stream) {
+  if (G < 0 || D <= 0) return X2G_EINVAL;
+  if (G == 0) return X2G_OK;
+  if (!out || !dout || !rstd || !rowptr || !row_gstats || !dx) return X2G_EINVAL;
+  if (D % 4 || reinterpret_cast<uintptr_t>(out) % 16 || reinterpret_cast<uintptr_t>(dout) % 16 ||
+      reinterpret_cast<uintptr_t>(dx) % 16 || reinterpret_cast<uintptr_t>(row_gstats) % 8)
+    return X2G_EUNSUPPORTED;
+  const unsigned grid = static_cast<unsigned>(G * kLnSplit);
+  graph_ln_bwd_apply_rows<<<grid, kLnSplitThreads, 0, as_stream(stream)>>>(
+      reinterpret_cast<const float4*>(out), reinterpret_cast<const float4*>(dout), rstd, rowptr, D / 4,
+      reinterpret_cast<const float2*>(row_gstats), reinterpret_cast<float4*>(dx));
   return last_launch_status();
 }

@@ -67,6 +67,8 @@ SIGNATURES = {
     "x2g_sbf_radial_wgrad": [_P, _P, _I64, _I32, _P, _P, ctypes.c_int, _P, _SZ, _P],
     "x2g_sbf_attention_fwd": [_P, _P, _P, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _I64, _I64, _I32, _I32,
                               _I32, _P, _P, _P, _P, _P],
+    "x2g_sbf_attention_fwd_stats": [_P, _P, _P, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _I64, _I64, _I32,
+                                    _I32, _I32, _P, _P, _P, _P, _P, _P],
     "x2g_sbf_attention_bwd_dst": [_P, _P, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64,
                                   _I32, _I32, _I32, _P, _P, _P, _P, _P],
     "x2g_sbf_attention_bwd_src": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I32, _I32, _I32, _P,
@@ -83,6 +85,7 @@ SIGNATURES = {
     "x2g_smooth_l1_mean_bwd": [_P, _P, _I64, _F, _P, _P, _P],
     "x2g_chain_bwd_batch": [_P, _I32, _I32, _I64, _I32, _P],
     "x2g_graph_layernorm_bwd_ex": [_P, _P, _P, _P, _I64, _I64, _P, _P, _SZ, _P],
+    "x2g_graph_layernorm_bwd_rows": [_P, _P, _P, _P, _I64, _I64, _P, _P, _P],
     "x2g_linear_wgrad_workspace": [_I64, _I32, _I32],
     "x2g_linear_wgrad": [_P, _P, _I64, _I32, _I32, _P, _P, _P, _SZ, _P],
     "x2g_dense_fwd": [_P, _P, _P, _I64, _I32, _I32, ctypes.c_int, _P, _P, _P, _P],
@@ -100,7 +103,9 @@ SIGNATURES = {
     "x2g_dense_bwd_ex": [_P, _P, ctypes.c_int, _P, _P, _I64, _I32, _I32, _P, _P, _P, _P, ctypes.c_int, _P, _SZ,
                          _P],
     "x2g_chain_fwd": [_P, _P, _P, _I32, _I64, _I32, _P, _P],
+    "x2g_chain_fwd_ln": [_P, _P, _P, _I64, ctypes.c_float, _P, _P, _P, _P, _P, _I32, _I64, _I32, _P, _P],
     "x2g_chain_bwd": [_P, _P, _P, _I32, _I64, _I32, _P, _P, _P, _P],
+    "x2g_chain_bwd_ln": [_P, _P, _P, _I32, _I64, _I32, _P, _P, _P, _P, _P, _P],
     "x2g_chain_t_floats": [_I64, _I32],
     "x2g_chain_wgrad_workspace": [_I64, _I32, _I32],
     "x2g_chain_wgrad_splits": [_I64, _I32, _I32],

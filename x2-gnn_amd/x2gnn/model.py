@@ -146,8 +146,13 @@ class _Trunk(nn.Module):
             out = self.convs[i](sbf=data.edge_sbf, rbf=data.node_rbf, x=out, edge_index=data._store.get("edge_index"),
                                 edge_attr=edge_attr, line_graph=plan.lg, edge_row=edge_row,
                                 edge_proj=edge_proj[i] if edge_proj is not None else None)
-            out = self.LayerNorm(out, rowptr=plan.line_ptr, num_graphs=plan.num_graphs)
-            out = self._tail(i, out, res0)
+            stats = getattr(out, "_x2g_rowstats", None)
+            if stats is not None and self._ln_fusable(out, i):
+                # the LayerNorm runs inside the tail's row chain, from the conv's per-row statistics
+                out = self._tail(i, out, res0, ln=(stats, plan.line_ptr, plan.num_graphs, self.LayerNorm.eps))
+            else:
+                out = self.LayerNorm(out, rowptr=plan.line_ptr, num_graphs=plan.num_graphs)
+                out = self._tail(i, out, res0)
             if fan:
                 out._x2g_fanin = ops.FanIn()
             readout(i + 1, out)
@@ -201,14 +206,19 @@ class _Trunk(nn.Module):
                 return False
         return True
 
-    def _tail(self, i, out, res0):
+    def _ln_fusable(self, x, i):
+        """True when the graph LayerNorm before layer i's tail can run inside its row chain."""
+        return ops._CHAIN and ops.chain_supported(x, self._tail_linears(i))
+
+    def _tail(self, i, out, res0, ln=None):
         """bf_skip -> SiLU(dense_bf_skip(.)) + res0 -> af_skip (model.py:47-50): one row-chain
-        kernel each way (ops.row_chain, 7 Linear stages) where compiled, else layer by layer."""
+        kernel each way (ops.row_chain, 7 Linear stages) where compiled, else layer by layer.
+        ``ln``: the row chain applies the preceding graph LayerNorm to ``out`` itself."""
         lins = self._tail_linears(i)
         if ops._CHAIN and ops.chain_supported(out, lins):
             S, H, RH, RE = ops.CHAIN_SILU, ops.CHAIN_HOLD, ops.CHAIN_RES_HELD, ops.CHAIN_RES_EXT
             flags = [S | H, S | RH, S | RE, S | H, S | RH, S | H, S | RH]
-            return ops.row_chain(out, res0, lins, flags)
+            return ops.row_chain(out, res0, lins, flags, ln=ln)
         out = self.bf_skip[i](out)
         out = self.dense_bf_skip[i].fused(out, act=ops.ACT_SILU, res=res0)  # SiLU(dense(out)) + res0
         return self.af_skip[i](out)

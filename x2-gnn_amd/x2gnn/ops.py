@@ -225,6 +225,14 @@ def spherical_basis_from_angles(theta, trip_src, rbf_env, num_spherical: int = 7
 
 
 # ---------------------------------------------------------------------------------- attention
+# Graph LayerNorm after the conv (model.py:46) fused: the attention forward leaves per-row (mean, M2)
+# statistics (x2g_sbf_attention_fwd_stats) and the trunk's row chain normalises its input while
+# staging it (x2g_chain_fwd_ln) instead of a LayerNorm pass over the rows.  X2G_LN_FUSE=0: separate.
+_LN_FUSE = os.environ.get("X2G_LN_FUSE", "1") == "1"
+# With the fused LayerNorm, its backward's per-molecule sums come from per-row sums the chain
+# backward leaves (x2g_chain_bwd_ln + x2g_graph_layernorm_bwd_rows): 0 = the two-pass LN backward.
+_LN_BWD_ROWS = os.environ.get("X2G_LN_BWD_ROWS", "1") == "1"
+
 # Factorised lin_sbf backward (csrc/attention_fold.inc): X2G_FOLD_SBF=0 restores the two-pass
 # backward + [T, D] d_sbfproj + T-row weight GEMM (kept for the drop-in conv API, whose sbf is
 # an arbitrary [T, 42] tensor).
@@ -262,9 +270,12 @@ class _SBFAttention(torch.autograd.Function):
         # (sbf pointer = S, weight pointer NULL) instead of re-projecting per triplet
         sproj = torch.empty(T, D, dtype=torch.float32, device=dev)
         call("x2g_sbf_project", ptr(sbf), T, sbf.shape[1], ptr(w_sbf), ptr(b_sbf), D, ptr(sproj), stream_ptr())
-        call("x2g_sbf_attention_fwd", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(edge_row), edge_mode,
-             ptr(sproj), None, None, ptr(lg.trip_rowptr), ptr(lg.trip_src), E, T, heads, channels, D, ptr(out),
-             ptr(alpha), ptr(smax), ptr(sden), stream_ptr())
+        # per-row (mean, M2) of the output for a graph LayerNorm fused into the next row chain
+        rstats = torch.empty(E, 2, dtype=torch.float32, device=dev) if _LN_FUSE and D == 128 else None
+        call("x2g_sbf_attention_fwd_stats" if rstats is not None else "x2g_sbf_attention_fwd", ptr(q), ptr(k), ptr(v),
+             ptr(skip), ptr(edge), ptr(edge_row), edge_mode, ptr(sproj), None, None, ptr(lg.trip_rowptr),
+             ptr(lg.trip_src), E, T, heads, channels, D, ptr(out), ptr(alpha), ptr(smax), ptr(sden),
+             *((ptr(rstats),) if rstats is not None else ()), stream_ptr())
         if factors is not None:  # the factorised backward never reads sbf itself
             ctx.save_for_backward(q, k, v, edge, factors[0], factors[1], sproj, alpha, smax, sden)
         else:
@@ -273,14 +284,15 @@ class _SBFAttention(torch.autograd.Function):
         ctx.w_param, ctx.b_param = w_param, b_param
         ctx.lg, ctx.edge_mode, ctx.edge_row, ctx.heads, ctx.channels = lg, edge_mode, edge_row, heads, channels
         ctx.edge_shape = None if edge is None else edge.shape
-        ctx.mark_non_differentiable(alpha, smax, sden)
+        # (one call: a second mark_non_differentiable replaces the first's set)
+        ctx.mark_non_differentiable(alpha, smax, sden, *((rstats,) if rstats is not None else ()))
         # the logits / max / denominator outputs never receive gradients: do not let autograd
         # materialise zero-filled [T, H] / [E, H] tensors for them (three fill launches per layer)
         ctx.set_materialize_grads(False)
-        return out, alpha, smax, sden
+        return out, alpha, smax, sden, rstats
 
     @staticmethod
-    def backward(ctx, dout, _da=None, _dm=None, _ds=None):
+    def backward(ctx, dout, _da=None, _dm=None, _ds=None, _dr=None):
         q, k, v, edge, sbf, ylm, sproj, alpha, smax, sden = ctx.saved_tensors
         lg, mode, heads, channels = ctx.lg, ctx.edge_mode, ctx.heads, ctx.channels
         dout = _f32(dout)
@@ -388,10 +400,12 @@ def _attention_fwd_fused(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, 
     f32 = dict(dtype=torch.float32, device=q.device)
     out, alpha = torch.empty(E, D, **f32), torch.empty(T, heads, **f32)
     smax, sden = torch.empty(E, heads, **f32), torch.empty(E, heads, **f32)
-    call("x2g_sbf_attention_fwd", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(edge_row), edge_mode,
-         ptr(sbf), ptr(w_sbf), ptr(b_sbf), ptr(lg.trip_rowptr), ptr(lg.trip_src), E, T, heads, channels,
-         sbf.shape[1], ptr(out), ptr(alpha), ptr(smax), ptr(sden), stream_ptr())
-    return out, alpha, smax, sden
+    rstats = torch.empty(E, 2, **f32) if _LN_FUSE and D == 128 else None
+    call("x2g_sbf_attention_fwd_stats" if rstats is not None else "x2g_sbf_attention_fwd", ptr(q), ptr(k), ptr(v),
+         ptr(skip), ptr(edge), ptr(edge_row), edge_mode, ptr(sbf), ptr(w_sbf), ptr(b_sbf), ptr(lg.trip_rowptr),
+         ptr(lg.trip_src), E, T, heads, channels, sbf.shape[1], ptr(out), ptr(alpha), ptr(smax), ptr(sden),
+         *((ptr(rstats),) if rstats is not None else ()), stream_ptr())
+    return out, alpha, smax, sden, rstats
 
 
 class _EmbeddingTable(torch.autograd.Function):
@@ -759,6 +773,7 @@ def _attention_fwd_tiled(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, 
     f32 = dict(dtype=torch.float32, device=q.device)
     out, alpha = torch.empty(E, D, **f32), torch.empty(T, H, **f32)
     smax, sden = torch.empty(E, H, **f32), torch.empty(E, H, **f32)
+    rstats = torch.empty(E, 2, **f32) if _LN_FUSE and D == 128 else None
     tiles = _infer_tiles(lg, tmax)
     S = torch.empty(max(t1 - (t0 & ~1) for _, _, t0, t1 in tiles), D, **f32)
     st = stream_ptr()
@@ -775,11 +790,13 @@ def _attention_fwd_tiled(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, 
             e_row = edge_row.data_ptr() + e0 * ib if edge_row is not None else None
         else:
             e_edge, e_row = ptr(edge), None
-        call("x2g_sbf_attention_fwd", q.data_ptr() + e0 * D * fb, ptr(k), ptr(v), skip.data_ptr() + e0 * D * fb,
+        call("x2g_sbf_attention_fwd_stats" if rstats is not None else "x2g_sbf_attention_fwd",
+             q.data_ptr() + e0 * D * fb, ptr(k), ptr(v), skip.data_ptr() + e0 * D * fb,
              e_edge, e_row, edge_mode, S.data_ptr() - ta * D * fb, None, None, lg.trip_rowptr.data_ptr() + e0 * ib,
              ptr(lg.trip_src), e1 - e0, T, heads, channels, D, out.data_ptr() + e0 * D * fb, ptr(alpha),
-             smax.data_ptr() + e0 * H * fb, sden.data_ptr() + e0 * H * fb, st)
-    return out, alpha, smax, sden
+             smax.data_ptr() + e0 * H * fb, sden.data_ptr() + e0 * H * fb,
+             *((rstats.data_ptr() + e0 * 2 * fb,) if rstats is not None else ()), st)
+    return out, alpha, smax, sden, rstats
 
 
 def sbf_attention(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg: LineGraph, heads: int, channels: int,
@@ -794,14 +811,16 @@ def sbf_attention(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg: LineGraph, heads: 
     if edge_row is not None:
         edge_row = _i32(edge_row)
     if _INFER_FUSED and not torch.is_grad_enabled():
-        out, alpha, smax, sden = _attention_fwd_fused(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode,
-                                                      edge_row, heads, channels)
+        out, alpha, smax, sden, rstats = _attention_fwd_fused(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode,
+                                                              edge_row, heads, channels)
     elif not torch.is_grad_enabled() and lg.T > INFER_TILE and q.shape[0] > 0:
-        out, alpha, smax, sden = _attention_fwd_tiled(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode,
-                                                      edge_row, heads, channels, INFER_TILE)
+        out, alpha, smax, sden, rstats = _attention_fwd_tiled(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode,
+                                                              edge_row, heads, channels, INFER_TILE)
     else:
-        out, alpha, smax, sden = _SBFAttention.apply(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row,
-                                                 heads, channels)
+        out, alpha, smax, sden, rstats = _SBFAttention.apply(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode,
+                                                         edge_row, heads, channels)
+    if rstats is not None:  # for a graph LayerNorm fused into the consumer (ops.row_chain(ln=...))
+        out._x2g_rowstats = rstats
     if not return_attention:
         return out
     dst = lg.trip_dst.long()
@@ -1193,7 +1212,7 @@ class _ChainFn(torch.autograd.Function):
     stage inputs and dz that both kernels leave in the tiled-transposed layout (x2g_chain_wgrad)."""
 
     @staticmethod
-    def forward(ctx, x, res, flags, *params):
+    def forward(ctx, x, res, flags, ln, *params):
         n = len(flags)
         ws, bs = params[0::2], params[1::2]
         x2 = _f32(x)
@@ -1211,9 +1230,20 @@ class _ChainFn(torch.autograd.Function):
         in_t = torch.empty(n, tf, **f32) if grad else None
         st = (ChainStage * n)(*[ChainStage(_dp(W[i]), _dp(B[i]), _dp(zs[i]), _dp(y) if i == n - 1 else None,
                                            None if WT is None else WT[i].data_ptr(), flags[i]) for i in range(n)])
-        call("x2g_chain_fwd", ptr(x2), ptr(r2), st, n, R, D, ptr(in_t), stream_ptr())
+        ctx.ln = ln is not None
+        if ln is None:
+            call("x2g_chain_fwd", ptr(x2), ptr(r2), st, n, R, D, ptr(in_t), stream_ptr())
+            ln_saved = ()
+        else:  # x is the LayerNorm's input: the chain normalises it while staging
+            stats, rowptr, G, eps = ln
+            xn = torch.empty(R, D, **f32) if grad else None
+            rstd = torch.empty(G, **f32) if grad else None
+            call("x2g_chain_fwd_ln", ptr(x2), ptr(stats), ptr(rowptr), G, float(eps), ptr(xn), None, ptr(rstd),
+                 ptr(r2), st, n, R, D, ptr(in_t), stream_ptr())
+            ln_saved = (xn, rstd, rowptr)
+            ctx.ln_segments = G
         if grad:
-            ctx.save_for_backward(*W, *[z if z is not None else x2 for z in zs], WT, in_t)
+            ctx.save_for_backward(*W, *[z if z is not None else x2 for z in zs], WT, in_t, *ln_saved)
         ctx.flags, ctx.params, ctx.has_res = tuple(flags), params, res is not None
         ctx.fan_res = _fan_of(res)
         return y
@@ -1239,13 +1269,34 @@ class _ChainFn(torch.autograd.Function):
         st = (ChainBwdStage * n)(*[ChainBwdStage(_dp(W[i]), WT[i].data_ptr(),
                                                  _dp(zs[i]) if flags[i] & CHAIN_SILU else None, None, bflags[i])
                                    for i in range(n)])
-        call("x2g_chain_bwd", ptr(gy2), None, st, n, R, D, ptr(dx), ptr(dres), ptr(dz_t), stream_ptr())
+        if not ctx.ln:
+            call("x2g_chain_bwd", ptr(gy2), None, st, n, R, D, ptr(dx), ptr(dres), ptr(dz_t), stream_ptr())
+        elif _LN_BWD_ROWS:  # dx is the LayerNorm output's gradient: through its backward to the chain's input,
+            # the per-row sums it needs left by the chain's last store
+            xn, rstd, rowptr = saved[2 * n + 2:2 * n + 5]
+            gst = torch.empty(R, 2, **f32)
+            call("x2g_chain_bwd_ln", ptr(gy2), None, st, n, R, D, ptr(dx), ptr(dres), ptr(dz_t), ptr(xn), ptr(gst),
+                 stream_ptr())
+            dxp = torch.empty(R, D, **f32)
+            call("x2g_graph_layernorm_bwd_rows", ptr(xn), ptr(dx), ptr(rstd), ptr(rowptr), ctx.ln_segments, D, ptr(gst),
+                 ptr(dxp), stream_ptr())
+            dx = dxp
+        else:
+            call("x2g_chain_bwd", ptr(gy2), None, st, n, R, D, ptr(dx), ptr(dres), ptr(dz_t), stream_ptr())
+            xn, rstd, rowptr = saved[2 * n + 2:2 * n + 5]
+            G = ctx.ln_segments
+            dxp = torch.empty(R, D, **f32)
+            wsb = int(_lib.load().x2g_graph_layernorm_bwd_workspace(G))
+            lws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=gy2.device)
+            call("x2g_graph_layernorm_bwd_ex", ptr(xn), ptr(dx), ptr(rstd), ptr(rowptr), G, D, ptr(dxp), ptr(lws), wsb,
+                 stream_ptr())
+            dx = dxp
         ws, bs = ctx.params[0::2], ctx.params[1::2]
         dws, dbs = chain_wgrad(in_t, dz_t, R, ws, bs)
         grads = []
         for i in range(n):
             grads += [dws[i], dbs[i]]
-        return (dx, dres if first else None, None, *grads)
+        return (dx, dres if first else None, None, None, *grads)
 
 
 def chain_supported(x, linears):
@@ -1265,12 +1316,19 @@ def chain_supported(x, linears):
 _CHAIN = os.environ.get("X2G_CHAIN", "1") == "1"
 
 
-def row_chain(x, res, linears, flags):
-    """Apply the chain of ``linears`` (nn.Linear modules, D x D) with per-stage X2G_CHAIN_* flags."""
+def row_chain(x, res, linears, flags, ln=None):
+    """Apply the chain of ``linears`` (nn.Linear modules, D x D) with per-stage X2G_CHAIN_* flags.
+
+    ``ln`` = (row_stats [R, 2], segment rowptr [G + 1] int32, G, eps): the chain's input is the
+    graph LayerNorm of x (model.py:46), computed while staging from the per-row (mean, M2) the
+    attention forward left (``x._x2g_rowstats``); the backward runs the LayerNorm's too."""
     params = []
     for m in linears:
         params += [m.weight, m.bias]
-    return _ChainFn.apply(x, res, tuple(flags), *params)
+    if ln is not None:
+        stats, rowptr, G, eps = ln
+        ln = (_f32(stats), _i32(rowptr), int(G), float(eps))
+    return _ChainFn.apply(x, res, tuple(flags), ln, *params)
 
 
 # ------------------------------------------------------------------------------ small-table chains

@@ -83,7 +83,9 @@ class _XGNNBase(nn.Module):
         """(element table, per-layer lin_edge tables or None).  The embedding Linear, edgenn and every
         conv's lin_edge all act on the <= 10-row element table (xgnn.py:57-58): where compiled they
         run as ONE small-table chain (ops.table_chain, one launch each way); the trunk then reads
-        its lin_edge tables from ``_x2g_edge_proj`` instead of applying edgenn / lin_edge itself."""
+        its lin_edge tables from ``_x2g_edge_proj`` instead of applying edgenn / lin_edge itself.
+        (Run on a second stream under the triplet build / featurisation it measured 0.4 % slower in
+        the step: its workgroup holds a CU the full-chip MFMA kernels then wait for.)"""
         emb = self.emb_block
         rows = emb.element_rows(atomic_num, count_z) if ops._TABLE_CHAIN else None
         trunk_stages = self.fin_model.edge_table_stages() if rows is not None else None
