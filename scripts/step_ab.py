@@ -14,7 +14,7 @@ for spec in sys.argv[2:]:
     env = {}
     for kv in filter(None, envs.split(";")):
         k, _, v = kv.partition("=")
-        env[k] = v
+        env[k] = os.path.expandvars(v)
     variants.append((name, env))
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 res = {name: [] for name, _ in variants}

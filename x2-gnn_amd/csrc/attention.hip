@@ -169,14 +169,14 @@ __device__ __forceinline__ void store_row_stats(float2* __restrict__ rs, int64_t
   float s = 0.f;
 #pragma unroll
   for (int j = 0; j < CPL; ++j) s += act ? o[j] : 0.f;
-  const float mu = group_sum<kWave>(s) / static_cast<float>(D);
+  const float mu = wave64_sum(s) / static_cast<float>(D);
   float q = 0.f;
 #pragma unroll
   for (int j = 0; j < CPL; ++j) {
     const float d = o[j] - mu;
     q = act ? fmaf(d, d, q) : q;
   }
-  q = group_sum<kWave>(q);
+  q = wave64_sum(q);
   if (lane == 0) rs[e] = make_float2(mu, q);
 }
 

@@ -520,25 +520,59 @@ __device__ __forceinline__ void stage_rows_ln(f4* __restrict__ img, const float*
                                               const ChainLn& ln, float2* __restrict__ lnrow, int r0, int nrows) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   stage_rows_async<RB>(img, P, R, r0);
-  // first molecule with rows here: (#molecules whose first row <= r0) - 1
+  // the segment row pointers ptr[k], k = lane + 64 j < 256, in registers (one round of independent
+  // loads); the first molecule with rows here is (#k with ptr[k] <= r0) - 1
+  constexpr int kPW = 4;
+  int pk[kPW];
+#pragma unroll
+  for (int j = 0; j < kPW; ++j) {
+    const int64_t k = lane + 64 * j;
+    pk[j] = ln.ptr[k <= ln.G ? k : ln.G];
+  }
   float cnt = 0.f;
-  for (int64_t k = lane; k <= ln.G; k += 64) cnt += ln.ptr[k] <= r0 ? 1.f : 0.f;
-  const int64_t m0 = static_cast<int64_t>(wave_sum(cnt)) - 1;
+#pragma unroll
+  for (int j = 0; j < kPW; ++j) cnt += (lane + 64 * j <= ln.G && pk[j] <= r0) ? 1.f : 0.f;
+  for (int64_t k = lane + 64 * kPW; k <= ln.G; k += 64) cnt += ln.ptr[k] <= r0 ? 1.f : 0.f;  // G >= 256
+  const int64_t m0 = static_cast<int64_t>(wave64_sum(cnt)) - 1;
+  auto ptr_at = [&](int64_t k) -> int {  // wave-uniform k
+    if (k >= 64 * kPW) return uniform(ln.ptr[k]);
+    const int l = static_cast<int>(k & 63);
+    switch (k >> 6) {
+      case 0: return lane_bcast(pk[0], l);
+      case 1: return lane_bcast(pk[1], l);
+      case 2: return lane_bcast(pk[2], l);
+      default: return lane_bcast(pk[3], l);
+    }
+  };
+  constexpr int kSW = 4;  // molecules of up to 256 rows: their statistics stay in registers
   for (int64_t m = (m0 > 0 ? m0 : 0) + w; m < ln.G; m += kCWaves) {
-    const int p0 = uniform(ln.ptr[m]), p1 = uniform(ln.ptr[m + 1]);
+    const int p0 = ptr_at(m), p1 = ptr_at(m + 1);
     if (p0 >= r0 + nrows) break;
     if (p1 <= p0) continue;
     const float n = static_cast<float>(p1 - p0);
+    float2 sv[kSW];
+#pragma unroll
+    for (int j = 0; j < kSW; ++j) {
+      const int r = p0 + lane + 64 * j;
+      sv[j] = ln.stats[r < p1 ? r : p0];
+    }
     float s = 0.f;
-    for (int r = p0 + lane; r < p1; r += 64) s += ln.stats[r].x;
-    const float mu = wave_sum(s) / n;
+#pragma unroll
+    for (int j = 0; j < kSW; ++j) s += p0 + lane + 64 * j < p1 ? sv[j].x : 0.f;
+    for (int r = p0 + lane + 64 * kSW; r < p1; r += 64) s += ln.stats[r].x;
+    const float mu = wave64_sum(s) / n;
     float q = 0.f;
-    for (int r = p0 + lane; r < p1; r += 64) {
+#pragma unroll
+    for (int j = 0; j < kSW; ++j) {
+      const float d = sv[j].x - mu;
+      q += p0 + lane + 64 * j < p1 ? fmaf(static_cast<float>(kCD) * d, d, sv[j].y) : 0.f;
+    }
+    for (int r = p0 + lane + 64 * kSW; r < p1; r += 64) {
       const float2 st = ln.stats[r];
       const float d = st.x - mu;
       q += fmaf(static_cast<float>(kCD) * d, d, st.y);
     }
-    const float denom = sqrtf(wave_sum(q) / (n * static_cast<float>(kCD)) + ln.eps);
+    const float denom = sqrtf(wave64_sum(q) / (n * static_cast<float>(kCD)) + ln.eps);
     const int lo = p0 > r0 ? p0 : r0, hi = p1 < r0 + nrows ? p1 : r0 + nrows;
     for (int r = lo + lane; r < hi; r += 64) lnrow[r - r0] = make_float2(mu, denom);
     if (lane == 0 && p0 >= r0) {
@@ -631,10 +665,13 @@ __global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4_batch(const ChainFw
 // ---- backward v3 (the shipped kernel): the v2 design with stage s-1's elementwise
 // part (residual gradients, dz = g SiLU'(z), the dz stores, the T-layout copy) computed per third of
 // the row blocks and scheduled into the next third's MFMAs, branch-free as the forward v3.
-// EXT: the stage has an external residual gradient (d_res_ext read-modify-write) or a row-major dz
-// output; without (6 of the trunk's 7 stages) those loads / stores are not issued at all (as
-// dropped out-of-range buffer operations they still cost the wave 18 memory instructions a stage)
-template <int RB0, int RB1, bool EXT = true>
+// A stage that adds its external residual gradient into d_res_ext (X2G_CHAIN_RES_ACCUM): the read
+// of the old value waits (vmcnt) for every older memory operation of the wave — the next stage's
+// weight / z prefetches and all T-layout stores so far — so it is issued, behind a wave-uniform
+// branch, only in the accumulating stage's elementwise part (1 of the trunk's 7; r2 issued it in
+// every stage as a dropped out-of-range load and waited on it there: removing every external access
+// measured +1.3 % in the step, profiles/r3d_ab_chain_noext.log, the bound for this change)
+template <int RB0, int RB1>
 __device__ __forceinline__ void bwd_elem(f4 (&gs)[kV2RB], f4 (&dh)[kV2RB], const f4 (&zc)[kV2RB], const f4 (&acc)[kV2RB],
                                          float hold_m, float held_m, float silu_m, float dres_acc_m, rsrc_t dres_r,
                                          rsrc_t dz_r, rsrc_t t_r, f4* __restrict__ out, int r0, int nrows, int w,
@@ -648,15 +685,15 @@ __device__ __forceinline__ void bwd_elem(f4 (&gs)[kV2RB], f4 (&dh)[kV2RB], const
     const int off = r < nrows ? 4 * ((r0 + r) * kCD + col) : kOOB;
     const f4 gv = acc[rb] + dh[rb] * hold_m;  // in_s was also the held residual (stage s HOLD)
     dh[rb] = dh[rb] * (1.0f - hold_m) + gv * held_m;  // stage s-1 adds the held residual
-    if (EXT) {
-      const f4 ld = bload4(dres_r, off, 0);  // (out of range / off: 0)
-      const f4 old = dres_acc_m != 0.0f ? ld : zero4();  // select, not a product: a fresh buffer may hold NaN
-      bstore4(dres_r, gv + old, off);
+    if (dres_acc_m != 0.0f) {  // wave-uniform: only the accumulating stage reads (and waits)
+      bstore4(dres_r, gv + bload4(dres_r, off, 0), off);
+    } else {
+      bstore4(dres_r, gv, off);
     }
     f4 dz;
 #pragma unroll
     for (int e = 0; e < 4; ++e) dz[e] = gv[e] * (silu_m * silu_grad_fast(zc[rb][e]) + (1.0f - silu_m));
-    if (EXT) bstore4(dz_r, dz, off);
+    bstore4(dz_r, dz, off);
     out[ipos(r, 4 * w + g)] = dz;
     gs[rb] = dz;
     f4 t = quad_transpose(dz, j);
@@ -672,35 +709,28 @@ __device__ __forceinline__ void bwd_elem(f4 (&gs)[kV2RB], f4 (&dh)[kV2RB], const
 // dx = rstd (g - mean(g) - y mean(g y)) per molecule): a row's 32 chunks sit in 32 consecutive
 // lanes, reduced by xor shuffles; the molecule sums are then a pass over these [R, 2] (no second
 // pass over g and y)
+// yimg: the chain input's rows (x2g_chain_fwd_ln's x_norm), copied into LDS by stage_rows_async at the
+// start of the last stage (landed by its barrier)
 template <int RB = kV2RB>
 __device__ __forceinline__ void store_img_lnstats(float* __restrict__ P, const f4* __restrict__ img,
-                                                  const float* __restrict__ Y, float2* __restrict__ gs, int r0,
+                                                  const f4* __restrict__ yimg, float2* __restrict__ gs, int r0,
                                                   int nrows) {
   const int tid = threadIdx.x;
-  f4 yv[RB];
 #pragma unroll
   for (int u = 0; u < RB; ++u) {
     const int q = tid + kCThreads * u, r = q >> 5, c = q & 31;
-    yv[u] = *reinterpret_cast<const f4*>(Y + (r0 + (r < nrows ? r : 0)) * kCD + 4 * c);
-  }
-#pragma unroll
-  for (int u = 0; u < RB; ++u) {
-    const int q = tid + kCThreads * u, r = q >> 5, c = q & 31;
-    const f4 g = img[ipos(r, c)];
+    const f4 g = img[ipos(r, c)], y = yimg[ipos(r, c)];
     if (r < nrows) *reinterpret_cast<f4*>(P + (r0 + r) * kCD + 4 * c) = g;
-    float s1 = (g[0] + g[1]) + (g[2] + g[3]);
-    float s2 = fmaf(g[0], yv[u][0], fmaf(g[1], yv[u][1], fmaf(g[2], yv[u][2], g[3] * yv[u][3])));
-#pragma unroll
-    for (int off = 1; off < 32; off <<= 1) {
-      s1 += __shfl_xor(s1, off, 64);
-      s2 += __shfl_xor(s2, off, 64);
-    }
-    if (c == 0 && r < nrows) gs[r0 + r] = make_float2(s1, s2);
+    // a row's 32 chunks are one aligned half-wave: DPP sums, valid in its upper 16 lanes
+    const float s1 = half32_sum_hi((g[0] + g[1]) + (g[2] + g[3]));
+    const float s2 = half32_sum_hi(fmaf(g[0], y[0], fmaf(g[1], y[1], fmaf(g[2], y[2], g[3] * y[3]))));
+    if (c == 16 && r < nrows) gs[r0 + r] = make_float2(s1, s2);
   }
 }
 
 __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
   __shared__ f4 img[2][kV2Img];
+  __shared__ f4 yimg[kV2Img];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int rl = lane & 15, g = lane >> 4;
   const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
@@ -739,11 +769,9 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
       t_r = rsrc_n(a.dz_t ? a.dz_t + s * a.tf : a.dy, a.tf * 4, a.dz_t != nullptr);
     };
     // whether stage s's elementwise part stores anything but dz in the T layout (wave-uniform)
-#ifdef X2G_AB_NOEXT  // A/B measurement only (wrong d_res_ext): no stage issues the external loads / stores
-    auto ext_of = [&](int) { return std::false_type{}; };
-#else
-    auto ext_of = [&](int) { return std::true_type{}; };
-#endif
+    // the LayerNorm backward's y rows for the final store: an LDS copy in flight with the first loads
+    // (yimg is read only after the last stage's barrier; the first waits below cover it)
+    if (a.ln_y) stage_rows_async<kV2RB>(yimg, a.ln_y, a.R, r0);
     load_wslice(n - 1, A);
     load_z(n - 1);
     f4 acc0[kV2RB];
@@ -765,8 +793,8 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
       float held_m, silu_m, dres_acc_m;
       rsrc_t dres_r, dz_r, t_r;
       elem_args(n - 1, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r);
-      bwd_elem<0, kV2RB, decltype(ext_of(0))::value>(gs, dh, zc, acc0, 0.0f, held_m, silu_m, dres_acc_m, dres_r, dz_r,
-                                                      t_r, img[p], r0, nrows, w, rl, g);
+      bwd_elem<0, kV2RB>(gs, dh, zc, acc0, 0.0f, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, img[p], r0, nrows,
+                              w, rl, g);
     }
     __syncthreads();
     X2G_TR(1);
@@ -782,24 +810,22 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
         float held_m, silu_m, dres_acc_m;
         rsrc_t dres_r, dz_r, t_r;
         elem_args(s - 1, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r);
-        auto body = [&](auto ext) {
-          constexpr bool X = decltype(ext)::value;
+        {
           half_gemm<0, 2>(in, A, acc, rl, g);
           __builtin_amdgcn_sched_barrier(0);
           half_gemm<2, 4>(in, A, acc, rl, g);
-          bwd_elem<0, 2, X>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows,
+          bwd_elem<0, 2>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows,
                             w, rl, g);
           interleave_epi_sched();
           __builtin_amdgcn_sched_barrier(0);
           half_gemm<4, 6>(in, A, acc, rl, g);
-          bwd_elem<2, 4, X>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows,
+          bwd_elem<2, 4>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows,
                             w, rl, g);
           interleave_epi_sched();
           __builtin_amdgcn_sched_barrier(0);
-          bwd_elem<4, 6, X>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows,
+          bwd_elem<4, 6>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows,
                             w, rl, g);
-        };
-        body(ext_of(s - 1));
+        }
       } else {
         slice_gemm(in, A, acc, rl, g);
 #pragma unroll
@@ -814,7 +840,7 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
       for (int b = 0; b < 8; ++b) A[b] = An[b];
     }
     if (a.ln_y)
-      store_img_lnstats(a.dx, img[p], a.ln_y, a.ln_gstats, r0, nrows);
+      store_img_lnstats(a.dx, img[p], yimg, a.ln_gstats, r0, nrows);
     else
       store_img(a.dx, img[p], r0, nrows);
   }
@@ -1636,7 +1662,8 @@ static int chain_bwd_launch(const ChainBwdArgs& a, int64_t rows, void* stream) {
     const int64_t nblk = (rows + 15) / 16;
     ChainBwdBatch b{};
     b.a[0] = a;
-    chain_bwd_v3_batch<<<dim3(static_cast<unsigned>(nblk < 256 ? nblk : 256), 1), kCThreads, 0, st>>>(b);
+    const dim3 grid(static_cast<unsigned>(nblk < 256 ? nblk : 256), 1);
+    chain_bwd_v3_batch<<<grid, kCThreads, 0, st>>>(b);
   }
   return last_launch_status();
 }

@@ -56,6 +56,31 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
+// Cross-lane sums on DPP (no LDS round trips, unlike __shfl_xor's ds_bpermute / ds_swizzle chains).
+template <int CTL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTL, 0xF, 0xF, false));
+}
+// sum over each 16-lane DPP row, in every lane of the row
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_mov<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror
+  v += dpp_mov<0x140>(v);  // row_mirror
+  return v;
+}
+// sum over each aligned 32-lane half of the wave, valid in its upper 16 lanes (16..31, 48..63):
+// row_bcast15 adds lane 15 of rows 0 / 2 to rows 1 / 3
+__device__ __forceinline__ float half32_sum_hi(float v) {
+  v = row16_sum(v);
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xA, 0xF, false));
+}
+// sum over the whole wave, wave-uniform
+__device__ __forceinline__ float wave64_sum(float v) {
+  v = row16_sum(v);
+  return (lane_bcast(v, 0) + lane_bcast(v, 16)) + (lane_bcast(v, 32) + lane_bcast(v, 48));
+}
+
 template <int G>
 __device__ __forceinline__ float group_max(float v) {
 #pragma unroll

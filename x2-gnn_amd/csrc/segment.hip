@@ -566,11 +566,8 @@ __global__ void __launch_bounds__(kLnSplitThreads) graph_ln_bwd_apply_rows(const
     s1 += t.x;
     s2 += t.y;
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    s1 += __shfl_xor(s1, off, 64);
-    s2 += __shfl_xor(s2, off, 64);
-  }
+  s1 = wave64_sum(s1);
+  s2 = wave64_sum(s2);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (lane == 0) lds[wave] = make_float2(s1, s2);
   __syncthreads();
