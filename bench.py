@@ -202,11 +202,14 @@ def dense_probe(R, reps):
     return {"dense_fwd": (_event_time(fwd, reps), 2.0 * R * K * N), "dense_bwd": (_event_time(bwd, reps), 4.0 * R * K * N)}
 
 
-def chain_probe(R, reps):
+def chain_probe(R, reps, mol_rows=165):
     """The trunk tail as the step runs it (ops.row_chain, model.py:47-50: 7 Linear stages per conv
-    layer) at this step's row count: x2g_chain_fwd (with the T-layout stage inputs), x2g_chain_bwd
-    (with the T-layout dz) and x2g_chain_wgrad (slab sums deferred, as in the step), HIP-event
-    timed on the launch stream.  FLOPs per launch: 7 * 2 * R * 128 * 128 each."""
+    layer) at this step's row count: x2g_chain_fwd_ln (the graph LayerNorm of model.py:46 applied
+    while staging, molecules of ``mol_rows`` line nodes, with the T-layout stage inputs),
+    x2g_chain_bwd_ln (T-layout dz, the residual gradient accumulated into the layer input's fan-in
+    buffer as the trunk does, the LayerNorm's per-row sums) and x2g_chain_wgrad (slab sums deferred,
+    as in the step), HIP-event timed on the launch stream.  FLOPs per launch: 7 * 2 * R * 128 * 128
+    each (the LayerNorm's are not counted)."""
     D, n = 128, 7
     S, H, RH, RE = ops.CHAIN_SILU, ops.CHAIN_HOLD, ops.CHAIN_RES_HELD, ops.CHAIN_RES_EXT
     flags = [S | H, S | RH, S | RE, S | H, S | RH, S | H, S | RH]
@@ -216,7 +219,8 @@ def chain_probe(R, reps):
     W = [torch.randn(D, D, device=dev, generator=g) / 11.3 for _ in range(n)]
     B = [0.1 * torch.randn(D, device=dev, generator=g) for _ in range(n)]
     Z = [torch.empty(R, D, device=dev) for _ in range(n)]
-    y, dx, dres = (torch.empty(R, D, device=dev) for _ in range(3))
+    y, dx = (torch.empty(R, D, device=dev) for _ in range(2))
+    dres = torch.zeros(R, D, device=dev)  # accumulated into (RES_ACCUM), as the fan-in buffer is
     WT = torch.empty(n, D, D, device=dev)
     tf = _lib_ws("x2g_chain_t_floats", R, D)
     in_t, dz_t = torch.empty(n, tf, device=dev), torch.empty(n, tf, device=dev)
@@ -225,18 +229,27 @@ def chain_probe(R, reps):
     st = (ops.ChainStage * n)(*[ops.ChainStage(W[i].data_ptr(), B[i].data_ptr(), Z[i].data_ptr(),
                                                y.data_ptr() if i == n - 1 else None, WT[i].data_ptr(), flags[i])
                                 for i in range(n)])
+    bflags = [f | (ops.CHAIN_RES_ACCUM if f & RE else 0) for f in flags]
     bst = (ops.ChainBwdStage * n)(*[ops.ChainBwdStage(W[i].data_ptr(), WT[i].data_ptr(), Z[i].data_ptr(), None,
-                                                      flags[i]) for i in range(n)])
+                                                      bflags[i]) for i in range(n)])
+    ptr_np = np.unique(np.concatenate([np.arange(0, R, mol_rows), [R]])).astype(np.int32)
+    seg = torch.from_numpy(ptr_np).to(dev)
+    G = len(ptr_np) - 1
+    xm = x.mean(1)
+    stats = torch.stack([xm, ((x - xm[:, None]) ** 2).sum(1)], 1).contiguous()
+    xn, rstd, gst = torch.empty(R, D, device=dev), torch.empty(G, device=dev), torch.empty(R, 2, device=dev)
     wsb = _lib_ws("x2g_chain_wgrad_workspace", R, D, n)
     ws = torch.empty(max(wsb, 4), dtype=torch.uint8, device=dev)
     dwa = (ctypes.c_void_p * n)(*[t.data_ptr() for t in DW])
     dba = (ctypes.c_void_p * n)(*[t.data_ptr() for t in DB])
 
     def fwd():
-        call("x2g_chain_fwd", ptr(x), ptr(res), st, n, R, D, ptr(in_t), stream_ptr())
+        call("x2g_chain_fwd_ln", ptr(x), ptr(stats), ptr(seg), G, 1e-8, ptr(xn), None, ptr(rstd), ptr(res), st, n,
+             R, D, ptr(in_t), stream_ptr())
 
     def bwd():
-        call("x2g_chain_bwd", ptr(dy), None, bst, n, R, D, ptr(dx), ptr(dres), ptr(dz_t), stream_ptr())
+        call("x2g_chain_bwd_ln", ptr(dy), None, bst, n, R, D, ptr(dx), ptr(dres), ptr(dz_t), ptr(xn), ptr(gst),
+             stream_ptr())
 
     def wgrad():
         call("x2g_chain_wgrad", ptr(in_t), ptr(dz_t), n, R, D, dwa, dba, ops.DEFER_SLAB_SUM, ptr(ws), wsb, stream_ptr())
@@ -366,7 +379,7 @@ def _hbm_entry(name, v, table):
 
 # MFMA probe name -> the kernel (symbol substring) whose PMC bytes it is
 PMC_MFMA_KERNEL = {"conv_proj_fwd": "conv_proj_fwd_kernel", "conv_proj_bwd_gate": "conv_proj_bwd_gate_kernel",
-                   "chain_fwd": "chain_fwd_v4(", "chain_bwd": "chain_bwd_v3_batch",
+                   "chain_fwd": "chain_fwd_v4_ln(", "chain_bwd": "chain_bwd_v3_batch",
                    "tiled_wgrad_flat": "tiled_flat_kernel"}
 
 
