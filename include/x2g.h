@@ -232,7 +232,9 @@ int x2g_sbf_attention_bwd_src(const float* q, const float* sbf, const float* w_s
  *  (1) x2g_sbf_attention_bwd_dst_g: ONE pass per destination -> dq, d_edge (EDGE_NONE / EDGE_PER_DST
  *      only), g[T,H] = sum over the head's channels of dout (v[src]+edge) S_t (the softmax-output
  *      gradient), prob[T,H] = a_t (the softmax probabilities) and seg_rho[E,H] = sum_t a_t g_t;
- *  (2) x2g_sbf_attention_bwd_src_fold: source-major -> dk, dv (dlogit = a (g - rho) formed here) and
+ *      g_out may be NULL (not written: the source pass then recomputes g, bitwise the same value);
+ *  (2) x2g_sbf_attention_bwd_src_fold: source-major -> dk, dv (dlogit = a (g - rho) formed here; g_in
+ *      NULL: g recomputed from the rows the pass reads anyway, no [T, H] round trip) and
  *      radial_grad[E, 8, HC]: G[s, l, :] = sum_{t: src(t)=s} d_sbfproj[t, :] Y_l(t) (sph_y from
  *      x2g_spherical_basis; slot 7 = sum of d_sbfproj).  EDGE_PER_DST requires edge_row and a table
  *      of edge_rows <= 16 rows (staged in LDS), else X2G_EUNSUPPORTED;

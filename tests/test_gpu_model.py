@@ -66,12 +66,13 @@ def _fwd_bwd(z, cuda):
 
 
 @pytest.mark.parametrize("fixture", ["model_full.npz", "model_aid.npz"])
-@pytest.mark.parametrize("switch", ["_LN_FUSE", "_LN_BWD_ROWS"])
+@pytest.mark.parametrize("switch", ["_LN_FUSE", "_LN_BWD_ROWS", "_SRC_G"])
 def test_fused_variants_equal_separate(cuda, monkeypatch, fixture, switch):
     """_LN_FUSE: the graph LayerNorm fused into the row chain (attention row statistics +
     x2g_chain_fwd_ln) == the separate LayerNorm kernels; _LN_BWD_ROWS: the fused LayerNorm's backward
     from the chain backward's per-row sums (x2g_chain_bwd_ln + x2g_graph_layernorm_bwd_rows) == its
-    two-pass backward.  Energies and every gradient to fp32 rounding (other summation orders)."""
+    two-pass backward; _SRC_G: the source pass recomputing g_t instead of reading the destination
+    pass's g [T, H].  Energies and every gradient to fp32 rounding (other summation orders)."""
     from x2gnn import ops
 
     z = golden(fixture)

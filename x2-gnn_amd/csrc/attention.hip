@@ -1090,14 +1090,17 @@ void fold_launch_mode(bool dst, const FoldArgs& a, unsigned blocks, hipStream_t 
           a.sqrt_c, a.dq, a.d_edge, a.g_out, a.prob_out, a.rho_out);
   } else {  // source-major pass
     const int C = a.D / a.H;
-if (a.mode == X2G_EDGE_PER_DST)
-      attn_bwd_src_fold_batched<CPL, true><<<blocks, 256, 0, st>>>(
-          a.q, a.v, a.edge, a.edge_row, a.edge_rows, a.sp, a.y, a.rowptr, a.tidx, a.tdst, a.prob, a.rho_in, a.g_in,
-          a.dout, a.E, a.D, a.H, C, a.dk, a.dv, a.gfold);
-    else
-      attn_bwd_src_fold_batched<CPL, false><<<blocks, 256, 0, st>>>(
-          a.q, a.v, a.edge, a.edge_row, a.edge_rows, a.sp, a.y, a.rowptr, a.tidx, a.tdst, a.prob, a.rho_in, a.g_in,
-          a.dout, a.E, a.D, a.H, C, a.dk, a.dv, a.gfold);
+#define X2G_SRC_FOLD(TABLE, GIN)                                                                                 \
+  attn_bwd_src_fold_batched<CPL, LPH, TABLE, GIN><<<blocks, 256, 0, st>>>(                                       \
+      a.q, a.v, a.edge, a.edge_row, a.edge_rows, a.sp, a.y, a.rowptr, a.tidx, a.tdst, a.prob, a.rho_in, a.g_in,   \
+      a.dout, a.E, a.D, a.H, C, a.dk, a.dv, a.gfold)
+    const bool gin = a.g_in != nullptr;
+    if (a.mode == X2G_EDGE_PER_DST) {
+      if (gin) X2G_SRC_FOLD(true, true); else X2G_SRC_FOLD(true, false);
+    } else {
+      if (gin) X2G_SRC_FOLD(false, true); else X2G_SRC_FOLD(false, false);
+    }
+#undef X2G_SRC_FOLD
   }
 }
 
@@ -1147,7 +1150,7 @@ X2G_API int x2g_sbf_attention_bwd_dst_g(const float* q, const float* k, const fl
                                         float* g_out, float* prob_out, float* seg_rho, void* stream) {
   if (E > 0 && (!q || !k || !v || !sbfproj || !trip_rowptr || !seg_max || !seg_den || !dout || !dq || !seg_rho))
     return X2G_EINVAL;
-  if (T > 0 && (!trip_src || !alpha_raw || !g_out || !prob_out)) return X2G_EINVAL;
+  if (T > 0 && (!trip_src || !alpha_raw || !prob_out)) return X2G_EINVAL;  // g_out may be NULL
   if (edge_mode != X2G_EDGE_NONE && (!edge || !d_edge)) return X2G_EINVAL;
   FoldArgs a{};
   a.q = q; a.k = k; a.v = v; a.edge = edge; a.edge_row = edge_row; a.mode = edge_mode; a.sp = sbfproj;
@@ -1164,7 +1167,7 @@ X2G_API int x2g_sbf_attention_bwd_src_fold(const float* q, const float* v, const
                                            float* dk, float* dv, float* radial_grad, void* stream) {
   if (E > 0 && (!q || !v || !sbfproj || !src_rowptr || !seg_rho || !dout || !dk || !dv || !radial_grad))
     return X2G_EINVAL;
-  if (T > 0 && (!src_perm || !trip_dst || !prob || !g_in || !sph_y)) return X2G_EINVAL;
+  if (T > 0 && (!src_perm || !trip_dst || !prob || !sph_y)) return X2G_EINVAL;  // g_in may be NULL
   // the source pass reads the edge term from a small table staged in LDS (X2-GNN's element table)
   if (edge_mode == X2G_EDGE_PER_DST && (!edge || !edge_row || edge_rows < 1 || edge_rows > kFoldTableRows))
     return X2G_EUNSUPPORTED;

@@ -232,6 +232,9 @@ _LN_FUSE = os.environ.get("X2G_LN_FUSE", "1") == "1"
 # With the fused LayerNorm, its backward's per-molecule sums come from per-row sums the chain
 # backward leaves (x2g_chain_bwd_ln + x2g_graph_layernorm_bwd_rows): 0 = the two-pass LN backward.
 _LN_BWD_ROWS = os.environ.get("X2G_LN_BWD_ROWS", "1") == "1"
+# The folded source-major pass recomputes g_t = d loss / d a_t (per head) itself — bitwise the value
+# the destination pass computes — so g [T, H] is neither written nor read: 0 = the round trip.
+_SRC_G = os.environ.get("X2G_SRC_G", "1") == "1"
 
 # Factorised lin_sbf backward (csrc/attention_fold.inc): X2G_FOLD_SBF=0 restores the two-pass
 # backward + [T, D] d_sbfproj + T-row weight GEMM (kept for the drop-in conv API, whose sbf is
@@ -336,7 +339,8 @@ class _SBFAttention(torch.autograd.Function):
         lg, mode, heads, channels = ctx.lg, ctx.edge_mode, ctx.heads, ctx.channels
         E, T, D = q.shape[0], lg.T, heads * channels
         dev = q.device
-        g = torch.empty(T, heads, dtype=torch.float32, device=dev)
+        # g[T, H] (d loss / d a_t): the source pass recomputes it from rows it holds anyway (_SRC_G)
+        g = None if _SRC_G else torch.empty(T, heads, dtype=torch.float32, device=dev)
         prob = torch.empty(T, heads, dtype=torch.float32, device=dev)
         rho = torch.empty(E, heads, dtype=torch.float32, device=dev)
         d_edge = torch.empty(E, D, dtype=torch.float32, device=dev) if mode == EDGE_PER_DST else None
