@@ -138,12 +138,13 @@ def attention_probe(model, batch, reps):
     def bwd_dst():  # the factorised backward the model runs (csrc/attention_fold.inc)
         call("x2g_sbf_attention_bwd_dst_g", ptr(q), ptr(k), ptr(v), ptr(table), ptr(row), ops.EDGE_PER_DST,
              ptr(sproj), ptr(lg.trip_rowptr), ptr(lg.trip_src), ptr(alpha), ptr(smax), ptr(sden), ptr(dout), E, T, H,
-             C, ptr(dq), ptr(dedge), ptr(dlogit), ptr(prob), ptr(rho), stream_ptr())
+             C, ptr(dq), ptr(dedge), None if ops._SRC_G else ptr(dlogit), ptr(prob), ptr(rho), stream_ptr())
 
     def bwd_src():
         call("x2g_sbf_attention_bwd_src_fold", ptr(q), ptr(v), ptr(table), ptr(row), table.shape[0],
              ops.EDGE_PER_DST, ptr(sproj), ptr(ylm), ptr(src_rowptr), ptr(src_perm), ptr(lg.trip_dst), ptr(prob),
-             ptr(dlogit), ptr(rho), ptr(dout), E, T, H, C, ptr(dk), ptr(dv), ptr(gfold), stream_ptr())
+             None if ops._SRC_G else ptr(dlogit), ptr(rho), ptr(dout), E, T, H, C, ptr(dk), ptr(dv), ptr(gfold),
+             stream_ptr())
 
     def radial_wgrad():
         call("x2g_sbf_radial_wgrad", ptr(gfold), ptr(radial), E, D, ptr(dwr), ptr(dbr), 0, ptr(ws), ws_bytes,
@@ -160,11 +161,12 @@ def attention_probe(model, batch, reps):
     proj_bytes = T * (4 * S + row_b) + 4 * D * (S + 1)
     fwd_bytes = idx + T * (row_b + 4 * H) + E * (4 + 5 * row_b + 8 * H)  # q k v skip out, S, alpha, max/den
     fwd_gath = idx + T * (3 * row_b + 4 * H) + E * (4 + 3 * row_b + 8 * H)
-    dst_bytes = idx + T * (row_b + 12 * H) + E * (4 + 6 * row_b + 12 * H)  # q k v dout dq d_edge, S, a/g/p
-    dst_gath = idx + T * (3 * row_b + 12 * H) + E * (4 + 4 * row_b + 12 * H)
-    # source-major CSR + trip_dst; S and Y rows, prob, g; q v dout read, dk dv written, G [E, 8, D]
-    src_bytes = idx + 4 * T + T * (row_b + 32 + 8 * H) + E * (4 + 13 * row_b + 4 * H)
-    src_gath = idx + 4 * T + T * (3 * row_b + 32 + 8 * H) + E * (4 + 11 * row_b + 4 * H)
+    gh = 0 if ops._SRC_G else 4 * H  # g [T, H]: written by the destination pass, read by the source pass
+    dst_bytes = idx + T * (row_b + 8 * H + gh) + E * (4 + 6 * row_b + 12 * H)  # q k v dout dq d_edge, S, a/p(/g)
+    dst_gath = idx + T * (3 * row_b + 8 * H + gh) + E * (4 + 4 * row_b + 12 * H)
+    # source-major CSR + trip_dst; S and Y rows, prob (, g); q v dout read, dk dv written, G [E, 8, D]
+    src_bytes = idx + 4 * T + T * (row_b + 32 + 4 * H + gh) + E * (4 + 13 * row_b + 4 * H)
+    src_gath = idx + 4 * T + T * (3 * row_b + 32 + 4 * H + gh) + E * (4 + 11 * row_b + 4 * H)
     radial_bytes = E * (8 * row_b + 4 * S) + 4 * D * (S + 1)
     res = {}
     for name, fn, nbytes, gath in (("sbf_project", proj, proj_bytes, proj_bytes), ("attn_fwd", fwd, fwd_bytes, fwd_gath),

@@ -767,6 +767,13 @@ typedef struct {
  * gradient and dx = dL/dx ([rows, D], may be NULL). */
 int x2g_table_chain_bwd(const x2g_table_bwd_stage* stages, int32_t n_stages, int64_t rows, int32_t dim, float* dx,
                         void* stream);
+/* The same with a workspace (x2g_table_chain_bwd_workspace bytes, 16-byte aligned): a tree with
+ * several leaves (X2-GNN's four lin_edge) runs its leaf stages side by side, one workgroup each,
+ * then the inner stages (two launches; the one-workgroup chain otherwise).  The forward already runs
+ * one workgroup per root-to-leaf path. */
+size_t x2g_table_chain_bwd_workspace(int32_t n_stages);
+int x2g_table_chain_bwd_ex(const x2g_table_bwd_stage* stages, int32_t n_stages, int64_t rows, int32_t dim, float* dx,
+                           void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- line-node featurisation
  * neo_x = SiLU(emb_trans(SiLU(mat_trans(x * env))))  (xgnn.py:49-56 of the reference: mat_trans

@@ -1233,21 +1233,34 @@ def test_conv_projections_fused_vs_layerwise(cuda, R, RR):
         assert float((a - b).abs().max()) <= 2e-5 * scale + 1e-6, i
 
 
+TABLE_TREES = {
+    # X2-GNN's: embedding Linear (SiLU) -> edgenn (Linear, SiLU, Linear) -> four lin_edge (no bias)
+    "x2gnn": ([(-1, 1, True), (0, 1, True), (1, 0, True), (2, 0, False), (2, 0, False), (2, 0, False),
+               (2, 0, False)], (3, 4, 5, 6)),
+    # leaves at several depths (one a child of the input), an inner stage with its own output gradient
+    "mixed": ([(-1, 1, True), (0, 0, True), (-1, 0, False), (1, 1, True), (0, 0, False)], (1, 2, 3, 4)),
+    # a plain chain: one leaf, one workgroup each way
+    "chain": ([(-1, 1, True), (0, 1, True), (1, 0, False)], (2,)),
+}
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("R", [1, 10, 16])
-def test_table_chain_vs_torch(cuda, R):
-    """x2g_table_chain_fwd / _bwd (ops.table_chain): X2-GNN's element-table tree — embedding Linear
-    (SiLU) -> edgenn (Linear, SiLU, Linear) -> four lin_edge (no bias) — outputs and every input /
-    parameter gradient vs fp64 torch, only some outputs receiving a gradient (as in the trunk); plus
-    the bucket-accumulating path (grad_sink) against the returned gradients."""
+@pytest.mark.parametrize("tree", sorted(TABLE_TREES))
+def test_table_chain_vs_torch(cuda, R, tree):
+    """x2g_table_chain_fwd / _bwd_ex (ops.table_chain): a tree of Linear stages on the element table
+    (one workgroup per root-to-leaf path forward; the leaf stages side by side, then the inner ones,
+    backward) — outputs and every input / parameter gradient vs fp64 torch, only some outputs
+    receiving a gradient (as in the trunk); plus the bucket-accumulating path (grad_sink) against the
+    returned gradients."""
     from x2gnn import ops
     from x2gnn.layers import Linear
 
     torch.manual_seed(R)
-    spec = [(-1, 1, True), (0, 1, True), (1, 0, True), (2, 0, False), (2, 0, False), (2, 0, False), (2, 0, False)]
+    spec, graded = TABLE_TREES[tree]
     lins = [Linear(128, 128, bias=hb).to(cuda) for _, _, hb in spec]
     x = (0.5 * torch.randn(R, 128, device=cuda)).requires_grad_(True)
-    gys = {s: torch.randn(R, 128, device=cuda) for s in (3, 4, 5, 6)}
+    gys = {s: torch.randn(R, 128, device=cuda) for s in graded}
     outs = ops.table_chain(x, [(m, a, p) for m, (p, a, _) in zip(lins, spec)])
     torch.autograd.backward([outs[s] for s in gys], [gys[s] for s in gys])
 

@@ -15,7 +15,10 @@
 namespace x2g {
 
 constexpr int kGateRMax = 8;
-constexpr int kGateBwdSplits = 512;
+#ifndef X2G_AB_GATE_SPLITS
+#define X2G_AB_GATE_SPLITS 512
+#endif
+constexpr int kGateBwdSplits = X2G_AB_GATE_SPLITS;
 
 typedef float f4v __attribute__((ext_vector_type(4)));
 

@@ -44,12 +44,30 @@ __device__ __forceinline__ void rows_to_lds(float* __restrict__ dst, const float
                                                      : f4{0.f, 0.f, 0.f, 0.f};
 }
 
+// Stages run by one workgroup (bit s of mask: stage s); own: the stages whose outputs it writes.
+// A tree with several leaves (X2-GNN: emb -> edgenn -> edgenn -> 4 x lin_edge) runs as one
+// workgroup per leaf, each computing the path from the root to its leaf (the shared prefix
+// redundantly: a 16-row stage is latency, not work), so the chain is as deep as the longest path
+// (4 stages) instead of the stage count (7).
 struct TableFwdArgs {
   const float* x;
   x2g_table_stage st[kTMax];
   int n;
   int R;
+  uint32_t mask[kTMax];
+  uint32_t own[kTMax];
 };
+
+// the next stage after s in mask (n when none; s = -1: the first)
+__device__ __forceinline__ int next_in(uint32_t mask, int s, int n) {
+  const uint32_t rest = s + 1 < 32 ? (mask >> (s + 1)) : 0u;
+  return (s >= n || rest == 0) ? n : s + 1 + __builtin_ctz(rest);
+}
+// the stage before s in mask (-1 when none)
+__device__ __forceinline__ int prev_in(uint32_t mask, int s) {
+  const uint32_t below = s > 0 ? (mask & ((1u << s) - 1u)) : 0u;
+  return below == 0 ? -1 : 31 - __builtin_clz(below);
+}
 
 // Stage s + 1's weight slice (the wave's 16 rows of W, 32 VGPRs) and bias are in flight while
 // stage s computes; two register sets alternate (loop unrolled by two, no copies).
@@ -59,7 +77,7 @@ struct FwdPre {
 };
 
 __device__ __forceinline__ void fwd_prefetch(const TableFwdArgs& a, int s, FwdPre& p) {
-  if (s >= a.n) return;
+  if (s < 0 || s >= a.n) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = 16 * w + (lane & 15), g = lane >> 4;
   const float* W = a.st[s].w + c * kTD + 4 * g;
@@ -68,13 +86,14 @@ __device__ __forceinline__ void fwd_prefetch(const TableFwdArgs& a, int s, FwdPr
   p.b = a.st[s].b ? a.st[s].b[c] : 0.0f;
 }
 
-__device__ __forceinline__ void fwd_stage(const TableFwdArgs& a, int s, FwdPre& cur, FwdPre& nxt,
+// stage s of this workgroup's path; pf: the stage after it on the path (prefetched into nxt)
+__device__ __forceinline__ void fwd_stage(const TableFwdArgs& a, int s, int pf, bool own, FwdPre& cur, FwdPre& nxt,
                                           float (*Y)[kTRows * kTS]) {
   const x2g_table_stage& S = a.st[s];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, g = lane >> 4, c = 16 * w + i;
   __syncthreads();  // Y[parent] is complete
-  fwd_prefetch(a, s + 1, nxt);
+  fwd_prefetch(a, pf, nxt);
   const float* in = Y[S.parent + 1] + i * kTS + 4 * g;
   f4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -90,7 +109,7 @@ __device__ __forceinline__ void fwd_stage(const TableFwdArgs& a, int s, FwdPre& 
     const float z = acc[e] + cur.b;
     const float y = S.act ? silu_(z) : z;
     Y[s + 1][r * kTS + c] = y;
-    if (r < R) {
+    if (r < R && own) {
       if (S.z) S.z[r * kTD + c] = z;
       S.y[r * kTD + c] = y;
     }
@@ -99,20 +118,33 @@ __device__ __forceinline__ void fwd_stage(const TableFwdArgs& a, int s, FwdPre& 
 
 __global__ void __launch_bounds__(kTThreads) table_chain_fwd_kernel(const TableFwdArgs a) {
   __shared__ __attribute__((aligned(16))) float Y[kTMax + 1][kTRows * kTS];  // x, then each stage's output
+  const uint32_t mask = a.mask[blockIdx.x], own = a.own[blockIdx.x];
+  const int n = a.n;
   FwdPre p0, p1;
-  fwd_prefetch(a, 0, p0);
+  int s = next_in(mask, -1, n);
+  fwd_prefetch(a, s, p0);
   rows_to_lds(Y[0], a.x, a.R);
-  for (int s = 0; s < a.n; s += 2) {
-    fwd_stage(a, s, p0, p1, Y);
-    if (s + 1 < a.n) fwd_stage(a, s + 1, p1, p0, Y);
+  while (s < n) {  // two register sets alternate (unrolled by two, no copies)
+    const int s1 = next_in(mask, s, n);
+    fwd_stage(a, s, s1, (own >> s) & 1u, p0, p1, Y);
+    if (s1 >= n) break;
+    const int s2 = next_in(mask, s1, n);
+    fwd_stage(a, s1, s2, (own >> s1) & 1u, p1, p0, Y);
+    s = s2;
   }
 }
 
+// Backward with several leaves: launch 1 (leaf pass) runs each leaf stage in its own workgroup and
+// leaves its input-gradient share dy_leaf W_leaf in the workspace (part[leaf]); launch 2 runs the
+// other stages in one workgroup, adding the shares into their parents' gradients in leaf order.
 struct TableBwdArgs {
   x2g_table_bwd_stage st[kTMax];
   float* dx;
   int n;
   int R;
+  uint32_t mask;          // launch 2: the stages it runs (the rest are leaves done by launch 1)
+  int leaf[kTMax];        // launch 1: workgroup b runs stage leaf[b]
+  float* part;            // [n][16][128] the leaves' input-gradient shares (or NULL: one launch)
 };
 
 // Stage s's weight (read transposed: column block 16w, rows 16q + 4g + e), forward input and
@@ -157,7 +189,8 @@ __device__ __forceinline__ void load_old(const TableBwdArgs& a, int s, f4 (&old)
     for (int e = 0; e < 4; ++e) old[t][e] = on ? dw[(16 * w + 4 * g + e) * kTD + 16 * t + i] : 0.0f;
 }
 
-__device__ __forceinline__ void bwd_stage(const TableBwdArgs& a, int s, BwdPre& cur, BwdPre& nxt,
+template <bool LEAF>
+__device__ __forceinline__ void bwd_stage(const TableBwdArgs& a, int s, int pf, BwdPre& cur, BwdPre& nxt,
                                           float (*G)[kTRows * kTS], float* dZ, float* In, f4 (&old)[8]) {
   const x2g_table_bwd_stage& S = a.st[s];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -171,7 +204,7 @@ __device__ __forceinline__ void bwd_stage(const TableBwdArgs& a, int s, BwdPre& 
     dZ[r * kTS + c] = S.act ? gv * silu_grad_(cur.z[e]) : gv;
   }
   __syncthreads();
-  bwd_prefetch(a, s - 1, nxt);
+  bwd_prefetch(a, pf, nxt);
   // dW[n][k] = sum_r dz[r][n] in[r][k]: wave w owns rows n = 16w + ..., all 8 column blocks; the
   // old bucket values (old, loaded at the end of the previous stage) are added at the store
   float ad[4];
@@ -188,7 +221,7 @@ __device__ __forceinline__ void bwd_stage(const TableBwdArgs& a, int s, BwdPre& 
   for (int t = 0; t < 8; ++t)
 #pragma unroll
     for (int e = 0; e < 4; ++e) S.dw[(16 * w + 4 * g + e) * kTD + 16 * t + i] = old[t][e] + dwv[t][e];
-  load_old(a, s - 1, old);  // the next stage's, in flight through its barriers and dz
+  load_old(a, pf, old);  // the next stage's, in flight through its barriers and dz
   if (S.db && tid < kTD) {
     float acc = 0.0f;
     for (int r = 0; r < a.R; ++r) acc += dZ[r * kTS + tid];
@@ -203,11 +236,18 @@ __device__ __forceinline__ void bwd_stage(const TableBwdArgs& a, int s, BwdPre& 
 #pragma unroll
     for (int e = 0; e < 4; ++e) acc = mfma4(av[e], cur.w[q][e], acc);
   }
+  if (LEAF) {  // the share goes to the parent's gradient through the workspace
+    float* pp = a.part + static_cast<int64_t>(s) * kTRows * kTD;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) pp[(4 * g + e) * kTD + c] = acc[e];
+    return;
+  }
   float* gp = G[S.parent + 1];
 #pragma unroll
   for (int e = 0; e < 4; ++e) gp[(4 * g + e) * kTS + c] += acc[e];
 }
 
+template <bool LEAF>
 __global__ void __launch_bounds__(kTThreads) table_chain_bwd_kernel(const TableBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float G[kTMax + 1][kTRows * kTS];  // dL/d(x), dL/d(y_s)
   __shared__ __attribute__((aligned(16))) float dZ[kTRows * kTS];
@@ -215,19 +255,47 @@ __global__ void __launch_bounds__(kTThreads) table_chain_bwd_kernel(const TableB
   const int tid = threadIdx.x;
   const int R = a.R;
   BwdPre p0, p1;
-  bwd_prefetch(a, a.n - 1, p0);
   f4 old[8];
-  load_old(a, a.n - 1, old);
-  for (int s = -1; s < a.n; ++s) {
-    const float* dy = s >= 0 ? a.st[s].dy : nullptr;
+  if (LEAF) {  // launch 1: this workgroup's leaf stage alone
+    const int s = a.leaf[blockIdx.x];
+    bwd_prefetch(a, s, p0);
+    load_old(a, s, old);
+    const float* dy = a.st[s].dy;
     if (dy)
       rows_to_lds(G[s + 1], dy, R);
     else
       *reinterpret_cast<f4*>(G[s + 1] + (tid >> 5) * kTS + 4 * (tid & 31)) = f4{0.f, 0.f, 0.f, 0.f};
+    bwd_stage<true>(a, s, -1, p0, p1, G, dZ, In, old);
+    return;
   }
-  for (int s = a.n - 1; s >= 0; s -= 2) {
-    bwd_stage(a, s, p0, p1, G, dZ, In, old);
-    if (s - 1 >= 0) bwd_stage(a, s - 1, p1, p0, G, dZ, In, old);
+  const uint32_t mask = a.mask;
+  int s = prev_in(mask, a.n);
+  for (int t = -1; t < a.n; ++t) {
+    const float* dy = t >= 0 ? a.st[t].dy : nullptr;
+    if (dy)
+      rows_to_lds(G[t + 1], dy, R);
+    else
+      *reinterpret_cast<f4*>(G[t + 1] + (tid >> 5) * kTS + 4 * (tid & 31)) = f4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (a.part) {  // the leaves' shares, added in stage order (each thread its own elements: no race)
+    const int r = tid >> 5, c4 = 4 * (tid & 31);
+    for (int t = 0; t < a.n; ++t) {
+      if ((mask >> t) & 1u) continue;
+      float* gp = G[a.st[t].parent + 1] + r * kTS + c4;
+      const f4 v = r < R ? *reinterpret_cast<const f4*>(a.part + (static_cast<int64_t>(t) * kTRows + r) * kTD + c4)
+                         : f4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f4*>(gp) = *reinterpret_cast<const f4*>(gp) + v;
+    }
+  }
+  bwd_prefetch(a, s, p0);
+  load_old(a, s, old);
+  while (s >= 0) {  // two register sets alternate (unrolled by two, no copies)
+    const int s1 = prev_in(mask, s);
+    bwd_stage<false>(a, s, s1, p0, p1, G, dZ, In, old);
+    if (s1 < 0) break;
+    const int s2 = prev_in(mask, s1);
+    bwd_stage<false>(a, s1, s2, p1, p0, G, dZ, In, old);
+    s = s2;
   }
   if (a.dx) {
     __syncthreads();
@@ -261,7 +329,22 @@ X2G_API int x2g_table_chain_fwd(const float* x, int64_t rows, int32_t dim, const
   a.x = x;
   a.n = n_stages;
   a.R = static_cast<int>(rows);
-  table_chain_fwd_kernel<<<1, kTThreads, 0, as_stream(stream)>>>(a);
+  // one workgroup per leaf, each running the path root -> leaf; a stage's outputs are written by the
+  // first workgroup whose path holds it
+  uint32_t has_child = 0, owned = 0;
+  for (int s = 0; s < n_stages; ++s)
+    if (stages[s].parent >= 0) has_child |= 1u << stages[s].parent;
+  int nwg = 0;
+  for (int s = 0; s < n_stages; ++s) {
+    if ((has_child >> s) & 1u) continue;
+    uint32_t m = 0;
+    for (int t = s; t >= 0; t = stages[t].parent) m |= 1u << t;
+    a.mask[nwg] = m;
+    a.own[nwg] = m & ~owned;
+    owned |= m;
+    ++nwg;
+  }
+  table_chain_fwd_kernel<<<static_cast<unsigned>(nwg), kTThreads, 0, as_stream(stream)>>>(a);
   return last_launch_status();
 }
 
@@ -281,6 +364,48 @@ X2G_API int x2g_table_chain_bwd(const x2g_table_bwd_stage* stages, int32_t n_sta
   a.dx = dx;
   a.n = n_stages;
   a.R = static_cast<int>(rows);
-  table_chain_bwd_kernel<<<1, kTThreads, 0, as_stream(stream)>>>(a);
+  a.mask = n_stages >= 32 ? ~0u : (1u << n_stages) - 1u;
+  table_chain_bwd_kernel<false><<<1, kTThreads, 0, as_stream(stream)>>>(a);
+  return last_launch_status();
+}
+
+X2G_API size_t x2g_table_chain_bwd_workspace(int32_t n_stages) {
+  return n_stages > 0 ? static_cast<size_t>(n_stages) * kTRows * kTD * sizeof(float) : 0;
+}
+
+X2G_API int x2g_table_chain_bwd_ex(const x2g_table_bwd_stage* stages, int32_t n_stages, int64_t rows, int32_t dim,
+                                   float* dx, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!stages || n_stages < 1 || n_stages > kTMax || rows < 0 || dim <= 0) return X2G_EINVAL;
+  if (dim != kTD || rows > kTRows) return X2G_EUNSUPPORTED;
+  uint32_t has_child = 0;
+  for (int s = 0; s < n_stages; ++s)
+    if (stages[s].parent >= 0 && stages[s].parent < s) has_child |= 1u << stages[s].parent;
+  int nleaf = 0;
+  for (int s = 0; s < n_stages; ++s) nleaf += ((has_child >> s) & 1u) ? 0 : 1;
+  if (nleaf < 2) return x2g_table_chain_bwd(stages, n_stages, rows, dim, dx, stream);
+  if (!workspace || workspace_bytes < x2g_table_chain_bwd_workspace(n_stages)) return X2G_EWORKSPACE;
+  if (!al16(workspace)) return X2G_EUNSUPPORTED;
+  TableBwdArgs a{};
+  for (int s = 0; s < n_stages; ++s) {
+    const x2g_table_bwd_stage& S = stages[s];
+    if (!S.w || !S.in || !S.dw || S.parent < -1 || S.parent >= s || (S.act != 0 && S.act != 1) || (S.act && !S.z))
+      return X2G_EINVAL;
+    if (!al16(S.w) || !al16(S.in) || !al16(S.dy)) return X2G_EUNSUPPORTED;
+    a.st[s] = S;
+  }
+  a.dx = dx;
+  a.n = n_stages;
+  a.R = static_cast<int>(rows);
+  a.part = static_cast<float*>(workspace);
+  int nl = 0;
+  for (int s = 0; s < n_stages; ++s)
+    if (!((has_child >> s) & 1u)) a.leaf[nl++] = s;
+  hipStream_t st = as_stream(stream);
+  // launch 1: the leaves side by side (their dW / db, and their input-gradient shares)
+  table_chain_bwd_kernel<true><<<static_cast<unsigned>(nl), kTThreads, 0, st>>>(a);
+  if (int rc = last_launch_status()) return rc;
+  // launch 2: the inner stages in one workgroup, the shares added into their parents' gradients
+  a.mask = has_child;
+  table_chain_bwd_kernel<false><<<1, kTThreads, 0, st>>>(a);
   return last_launch_status();
 }

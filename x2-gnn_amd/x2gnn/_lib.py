@@ -120,6 +120,8 @@ SIGNATURES = {
     "x2g_tiled_wgrad": [_P, _I32, _I64, _I32, ctypes.c_int, _P, _SZ, _P],
     "x2g_table_chain_fwd": [_P, _I64, _I32, _P, _I32, _P],
     "x2g_table_chain_bwd": [_P, _I32, _I64, _I32, _P, _P],
+    "x2g_table_chain_bwd_workspace": [_I32],
+    "x2g_table_chain_bwd_ex": [_P, _I32, _I64, _I32, _P, _P, _SZ, _P],
     "x2g_tiled_wgrad_flat_workspace": [_I64, _I32, _I32],
     "x2g_tiled_wgrad_flat": [_P, _I32, _I64, _I32, ctypes.c_int, _P, _P, _SZ, _P],
     "x2g_feat_fwd": [_P, _P, _I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
@@ -129,6 +131,7 @@ SIGNATURES = {
     "x2g_wgrad_batched": [_P, _I32, _I64, _I32, ctypes.c_int, _P, _SZ, _P],
 }
 RESTYPES = {"x2g_status_string": ctypes.c_char_p, "x2g_vertex_to_edge_workspace": _SZ,
+            "x2g_table_chain_bwd_workspace": _SZ,
             "x2g_linear_wgrad_workspace": _SZ, "x2g_dense_bwd_workspace": _SZ, "x2g_optimizer_workspace": _SZ,
             "x2g_linear_wgrad_splits": ctypes.c_int32, "x2g_dense_bwd_splits": ctypes.c_int32,
             "x2g_dense_bwd_slab_offset": ctypes.c_int64, "x2g_edge_basis_freq_grad_workspace": _SZ,

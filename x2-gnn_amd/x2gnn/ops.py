@@ -1338,6 +1338,8 @@ def row_chain(x, res, linears, flags, ln=None):
 # ------------------------------------------------------------------------------ small-table chains
 TABLE_MAX_STAGES = 8  # X2G_TABLE_MAX_STAGES
 _TABLE_CHAIN = os.environ.get("X2G_TABLE_CHAIN", "1") == "1"
+# the table chain's backward with its leaf stages side by side (x2g_table_chain_bwd_ex): 0 = one workgroup
+_TABLE_PAR = os.environ.get("X2G_TABLE_PAR", "1") == "1"
 _FEATURIZE = os.environ.get("X2G_FEATURIZE", "1") == "1"
 _FAN_IN = os.environ.get("X2G_FAN_IN", "1") == "1"
 # T-layout weight gradients (chain / projections / featurisation): 1 = their slab sums join the one
@@ -1423,7 +1425,13 @@ class _TableChainFn(torch.autograd.Function):
             stages.append(TableBwdStage(_dp(ws[s]), _dp(src), _dp(zs[s]), _dp(dys[s]), _dp(dw), _dp(db), par, act,
                                         1 if accum else 0))
         dx = torch.empty(R, D, dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None
-        call("x2g_table_chain_bwd", (TableBwdStage * n)(*stages), n, R, D, ptr(dx), stream_ptr())
+        if _TABLE_PAR:  # several leaves (the four lin_edge): leaf stages side by side, then the inner ones
+            wsb = int(_lib.load().x2g_table_chain_bwd_workspace(n))
+            ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+            call("x2g_table_chain_bwd_ex", (TableBwdStage * n)(*stages), n, R, D, ptr(dx), ptr(ws), wsb,
+                 stream_ptr())
+        else:
+            call("x2g_table_chain_bwd", (TableBwdStage * n)(*stages), n, R, D, ptr(dx), stream_ptr())
         return (dx, None, *grads)
 
 
