@@ -19,9 +19,21 @@ __global__ void __launch_bounds__(256) embedding_table_kernel(float* __restrict_
   __shared__ int hist[kEmbMaxRows];
   for (int v = threadIdx.x; v < V; v += blockDim.x) hist[v] = 0;
   __syncthreads();
-  for (int64_t n = threadIdx.x; n < N; n += blockDim.x) {
-    const int64_t v = z[n];
-    if (v >= 0 && v < V) atomicAdd(&hist[v], 1);
+  // the atoms' numbers a batch of kEmbUnroll per thread at a time: every load of the batch in flight
+  // together (a load-then-add loop runs one memory round trip per 256 atoms)
+  constexpr int kEmbUnroll = 16;
+  for (int64_t n0 = threadIdx.x; n0 < N; n0 += static_cast<int64_t>(blockDim.x) * kEmbUnroll) {
+    int64_t zv[kEmbUnroll];
+#pragma unroll
+    for (int u = 0; u < kEmbUnroll; ++u) {
+      const int64_t n = n0 + static_cast<int64_t>(u) * blockDim.x;
+      zv[u] = z[n < N ? n : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < kEmbUnroll; ++u) {
+      const int64_t v = zv[u];
+      if (n0 + static_cast<int64_t>(u) * blockDim.x < N && v >= 0 && v < V) atomicAdd(&hist[v], 1);
+    }
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;

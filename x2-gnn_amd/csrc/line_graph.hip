@@ -223,15 +223,47 @@ __global__ void sort_segments(const int32_t* __restrict__ rowptr, int64_t n_seg,
 constexpr int kScan1Threads = 1024;
 constexpr int64_t kScan1Max = 32768;  // one-workgroup scan up to this many counts (staged in LDS)
 
-// Exclusive scan of n <= kScan1Max int32 counts in ONE workgroup (coalesced loads into LDS, then
-// each thread scans a contiguous run): out[n] = total.  One launch instead of the three-phase
-// scan's three for the line graphs of a training batch.
-__global__ void __launch_bounds__(kScan1Threads) scan_1wg(const int32_t* __restrict__ in, int64_t n,
-                                                         int32_t* __restrict__ out) {
+// count[i] = deg(atom[i]) - 1 for the multi-workgroup scan of larger graphs
+__global__ void degree_count(const int32_t* __restrict__ atom, const int32_t* __restrict__ atom_rowptr, int64_t n,
+                             int32_t* __restrict__ count) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int a = atom[i];
+  const int c = atom_rowptr[a + 1] - atom_rowptr[a] - 1;
+  count[i] = c > 0 ? c : 0;
+}
+
+// Exclusive scan of n <= kScan1Max counts deg(atom[i]) - 1 in ONE workgroup: the counts' gathers
+// (atom[i], then atom_rowptr[a], atom_rowptr[a + 1]) kDegUnroll per thread at a time, every load of
+// a batch in flight together, into LDS; each thread then scans a contiguous run; out[n] = total.
+// One launch instead of a count launch + the three-phase scan for a training batch's line graph
+// (round 3: the counts were a separate grid launch before this one-workgroup scan).
+constexpr int kDegUnroll = 8;
+__global__ void __launch_bounds__(kScan1Threads) degree_scan_1wg(const int32_t* __restrict__ atom,
+                                                                const int32_t* __restrict__ atom_rowptr, int64_t n,
+                                                                int32_t* __restrict__ out) {
   __shared__ int cnt[kScan1Max];
   __shared__ int lds[kScan1Threads / 64];
   const int tid = threadIdx.x;
-  for (int64_t i = tid; i < n; i += kScan1Threads) cnt[i] = in[i];
+  for (int64_t i0 = tid; i0 < n; i0 += static_cast<int64_t>(kScan1Threads) * kDegUnroll) {
+    int a[kDegUnroll], d0[kDegUnroll], d1[kDegUnroll];
+#pragma unroll
+    for (int u = 0; u < kDegUnroll; ++u) {
+      const int64_t i = i0 + static_cast<int64_t>(u) * kScan1Threads;
+      a[u] = atom[i < n ? i : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < kDegUnroll; ++u) {
+      d0[u] = atom_rowptr[a[u]];
+      d1[u] = atom_rowptr[a[u] + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < kDegUnroll; ++u) {
+      const int64_t i = i0 + static_cast<int64_t>(u) * kScan1Threads;
+      const int c = d1[u] - d0[u] - 1;
+      if (i < n) cnt[i] = c > 0 ? c : 0;
+    }
+  }
   __syncthreads();
   const int64_t per = (n + kScan1Threads - 1) / kScan1Threads;
   const int64_t lo = per * tid, hi = lo + per < n ? lo + per : n;
@@ -249,27 +281,17 @@ __global__ void __launch_bounds__(kScan1Threads) scan_1wg(const int32_t* __restr
   if (tid == 0) out[n] = total;
 }
 
-// count[i] = deg(atom[i]) - 1 for the multi-workgroup scan of larger graphs
-__global__ void degree_count(const int32_t* __restrict__ atom, const int32_t* __restrict__ atom_rowptr, int64_t n,
-                             int32_t* __restrict__ count) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int a = atom[i];
-  const int c = atom_rowptr[a + 1] - atom_rowptr[a] - 1;
-  count[i] = c > 0 ? c : 0;
-}
-
-// out = exclusive scan of deg(atom[i]) - 1: the counts by a grid of threads (random gathers need
-// many CUs), the scan by one workgroup when it fits
+// out = exclusive scan of deg(atom[i]) - 1: one workgroup when it fits (counts and scan), else the
+// counts by a grid of threads and the multi-workgroup scan
 int degree_scan(const int32_t* atom, const int32_t* atom_rowptr, int64_t n, int32_t* out, int32_t* count,
                 int32_t* partial, hipStream_t st) {
+  if (n > 0 && n <= kScan1Max) {
+    degree_scan_1wg<<<1, kScan1Threads, 0, st>>>(atom, atom_rowptr, n, out);
+    return last_launch_status();
+  }
   if (n > 0) {
     degree_count<<<blocks_for(n, 256), 256, 0, st>>>(atom, atom_rowptr, n, count);
     if (int rc = last_launch_status()) return rc;
-  }
-  if (n > 0 && n <= kScan1Max) {
-    scan_1wg<<<1, kScan1Threads, 0, st>>>(count, n, out);
-    return last_launch_status();
   }
   return exclusive_scan(count, n, out, partial, st);
 }

@@ -15,10 +15,10 @@
 namespace x2g {
 
 constexpr int kGateRMax = 8;
-#ifndef X2G_AB_GATE_SPLITS
-#define X2G_AB_GATE_SPLITS 512
-#endif
-constexpr int kGateBwdSplits = X2G_AB_GATE_SPLITS;
+// workgroups per job of the pool / gate backward: 128 (about 165 rows each at config 2) amortise each
+// workgroup's weight staging, LDS reduction and slab over 4x the rows of r2's 512 and leave a quarter
+// of the slabs to sum (+0.45 % in the step A/B, profiles/r3e_ab_small_kernels.log)
+constexpr int kGateBwdSplits = 128;
 
 typedef float f4v __attribute__((ext_vector_type(4)));
 
@@ -121,23 +121,36 @@ __global__ void __launch_bounds__(256) rbf_pool_fwd_kernel(const PoolJobs J, con
   GateW<LPR> gw;
   gw.load(sw, R, sub);
   const int nwaves = gridDim.x * 4;
+  // a row's basis values: lane j of each 16-lane DPP row (LPR >= 16, so a data row spans whole DPP
+  // rows) loads value j and row_newbcast hands value j to the row — one load and one register per row
+  // slot instead of kGateRMax of each (occupancy 4 -> 8 waves per SIMD)
+  const int jl = (lane & 15) < R ? (lane & 15) : R - 1;
   for (int64_t g = uniform(blockIdx.x * 4 + (threadIdx.x >> 6)); g < G; g += nwaves) {
     const int r0 = uniform(rowptr[g]), r1 = uniform(rowptr[g + 1]);
     f4v acc = {0.f, 0.f, 0.f, 0.f};
     for (int rb0 = r0; rb0 < r1; rb0 += UNROLL * RPI) {
       f4v v[UNROLL];
-      float rb[UNROLL][kGateRMax];
+      float rv[UNROLL];
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
         const int r = rb0 + u * RPI + slot;
         const int rc = r < r1 ? r : r1 - 1;
         v[u] = x[static_cast<int64_t>(rc) * LPR + sub];
-        load_rbf(rbf, rc, R, rb[u]);
+        rv[u] = rbf[static_cast<int64_t>(rc) * R + jl];
       }
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
         const float ok = rb0 + u * RPI + slot < r1 ? 1.f : 0.f;
-        acc += (v[u] * gw.filter(rb[u])) * ok;
+        float rb[kGateRMax];
+        rb[0] = dpp_mov<0x150>(rv[u]);
+        rb[1] = dpp_mov<0x151>(rv[u]);
+        rb[2] = dpp_mov<0x152>(rv[u]);
+        rb[3] = dpp_mov<0x153>(rv[u]);
+        rb[4] = dpp_mov<0x154>(rv[u]);
+        rb[5] = dpp_mov<0x155>(rv[u]);
+        rb[6] = dpp_mov<0x156>(rv[u]);
+        rb[7] = dpp_mov<0x157>(rv[u]);
+        acc += (v[u] * gw.filter(rb)) * ok;
       }
     }
 #pragma unroll

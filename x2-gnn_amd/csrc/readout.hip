@@ -48,16 +48,31 @@ __global__ void __launch_bounds__(256) readout_head_bwd_kernel(const float* __re
   const int64_t per = (R + gridDim.x - 1) / gridDim.x;
   const int64_t lo = per * blockIdx.x, hi = lo + per < R ? lo + per : R;
   const int splits = gridDim.x;
-  for (int g = 0; g < G; ++g) {
+  {  // job g = blockIdx.y (r2 looped over the jobs in every block: 5 x its row loop's round trips)
+    const int g = blockIdx.y;
     const f4h wv = reinterpret_cast<const f4h*>(b.g[g].w)[sub];
     f4h aw = {0.f, 0.f, 0.f, 0.f};
     float ab = 0.f;
-    for (int64_t r = lo + slot; r < hi; r += RPB) {
-      const float d = dout[r];
-      const f4h hv = reinterpret_cast<const f4h*>(b.g[g].h)[r * LPR + sub];
-      aw += hv * d;
-      ab += d;
-      if (b.g[g].dh) reinterpret_cast<f4h*>(b.g[g].dh)[r * LPR + sub] = wv * d;
+    constexpr int U = 4;  // rows per slot issued together
+    for (int64_t r0 = lo + slot; r0 < hi; r0 += static_cast<int64_t>(RPB) * U) {
+      float dv[U];
+      f4h hv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t r = r0 + static_cast<int64_t>(u) * RPB;
+        const int64_t rc = r < hi ? r : lo;
+        dv[u] = dout[rc];
+        hv[u] = reinterpret_cast<const f4h*>(b.g[g].h)[rc * LPR + sub];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t r = r0 + static_cast<int64_t>(u) * RPB;
+        if (r < hi) {
+          aw += hv[u] * dv[u];
+          ab += dv[u];
+          if (b.g[g].dh) reinterpret_cast<f4h*>(b.g[g].dh)[r * LPR + sub] = wv * dv[u];
+        }
+      }
     }
     red[slot * LPR + sub] = aw;
     if (sub == 0) redb[slot] = ab;
@@ -151,7 +166,7 @@ X2G_API int x2g_readout_head_bwd(const float* dout, const x2g_head_group* groups
   for (int g = 0; g < G; ++g) b.g[g] = groups[g];
   const int splits = head_splits(R);
   float* part = static_cast<float*>(ws);
-  X2G_HEAD_DISPATCH(readout_head_bwd_kernel, splits, dout, b, G, R, part)
+  X2G_HEAD_DISPATCH(readout_head_bwd_kernel, dim3(splits, G), dout, b, G, R, part)
   if (int rc = last_launch_status()) return rc;
   if (flags & X2G_DEFER_SLAB_SUM) return X2G_OK;
   x2g_slab_job jobs[X2G_MAX_GROUPS];
