@@ -49,10 +49,20 @@ __device__ __forceinline__ float lane_bcast(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
 
+template <int CTL>
+__device__ __forceinline__ float dpp_mov(float v);
+
 template <int G>
 __device__ __forceinline__ float group_sum(float v) {
+  // groups of up to 16 lanes on DPP (quad permutes, then row_half_mirror / row_mirror: after the quad
+  // steps every lane of a quad holds the same value, so the partner lane the mirrors pick gives the
+  // same sums, bitwise, as xor 4 / xor 8); wider groups through ds_bpermute
+  if (G >= 2) v += dpp_mov<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+  if (G >= 4) v += dpp_mov<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+  if (G >= 8) v += dpp_mov<0x141>(v);  // row_half_mirror
+  if (G >= 16) v += dpp_mov<0x140>(v); // row_mirror
 #pragma unroll
-  for (int off = 1; off < G; off <<= 1) v += __shfl_xor(v, off, kWave);
+  for (int off = 16; off < G; off <<= 1) v += __shfl_xor(v, off, kWave);
   return v;
 }
 
@@ -81,10 +91,27 @@ __device__ __forceinline__ float wave64_sum(float v) {
   return (lane_bcast(v, 0) + lane_bcast(v, 16)) + (lane_bcast(v, 32) + lane_bcast(v, 48));
 }
 
+// A partner exchange for butterflies over lane bit log2(OFF): xor OFF for OFF 1, 2 and >= 16 (the
+// last through ds_bpermute); OFF 4 / 8 take row_half_mirror / row_mirror, i.e. xor 7 / xor 15 inside
+// a DPP row - the partner still has bit OFF flipped and every higher bit kept, and the masks stay
+// triangular, so a butterfly that visits each bit once still sums every lane exactly once.
+template <int OFF>
+__device__ __forceinline__ float xor_xchg(float v) {
+  if constexpr (OFF == 1) return dpp_mov<0xB1>(v);
+  else if constexpr (OFF == 2) return dpp_mov<0x4E>(v);
+  else if constexpr (OFF == 4) return dpp_mov<0x141>(v);
+  else if constexpr (OFF == 8) return dpp_mov<0x140>(v);
+  else return __shfl_xor(v, OFF, kWave);
+}
+
 template <int G>
 __device__ __forceinline__ float group_max(float v) {
+  if (G >= 2) v = fmaxf(v, xor_xchg<1>(v));
+  if (G >= 4) v = fmaxf(v, xor_xchg<2>(v));
+  if (G >= 8) v = fmaxf(v, xor_xchg<4>(v));
+  if (G >= 16) v = fmaxf(v, xor_xchg<8>(v));
 #pragma unroll
-  for (int off = 1; off < G; off <<= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+  for (int off = 16; off < G; off <<= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
   return v;
 }
 

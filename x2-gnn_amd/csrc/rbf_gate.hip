@@ -164,7 +164,8 @@ __global__ void __launch_bounds__(256) rbf_pool_fwd_kernel(const PoolJobs J, con
 
 // Sum of 8 per-lane values over an aligned group of LPR lanes (LPR in 16..64), as a butterfly
 // that halves the vector at each of the top three levels (4 + 2 + 1 exchanges instead of 8 x 3),
-// then plain xor sums over the remaining lane bits: lane `sub` ends with the group total of
+// then plain sums over the remaining lane bits (partners per xor_xchg: DPP below 16 lanes, so for
+// LPR = 32 only the first level goes through LDS): lane `sub` ends with the group total of
 // element j = 4 [sub & LPR/2] + 2 [sub & LPR/4] + [sub & LPR/8] (returned in j).
 template <int LPR>
 __device__ __forceinline__ float transpose_sum(const float (&p)[kGateRMax], int sub, int& j) {
@@ -174,23 +175,24 @@ __device__ __forceinline__ float transpose_sum(const float (&p)[kGateRMax], int 
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const float send = h1 ? p[k] : p[k + 4];
-    const float recv = __shfl_xor(send, o1, kWave);
+    const float recv = xor_xchg<o1>(send);
     q[k] = (h1 ? p[k + 4] : p[k]) + recv;
   }
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const float send = h2 ? q[k] : q[k + 2];
-    const float recv = __shfl_xor(send, o2, kWave);
+    const float recv = xor_xchg<o2>(send);
     r[k] = (h2 ? q[k + 2] : q[k]) + recv;
   }
   float t;
   {
     const float send = h3 ? r[0] : r[1];
-    const float recv = __shfl_xor(send, o3, kWave);
+    const float recv = xor_xchg<o3>(send);
     t = (h3 ? r[1] : r[0]) + recv;
   }
-#pragma unroll
-  for (int off = o3 / 2; off > 0; off >>= 1) t += __shfl_xor(t, off, kWave);
+  if constexpr (o3 >= 8) t += xor_xchg<4>(t);
+  if constexpr (o3 >= 4) t += xor_xchg<2>(t);
+  if constexpr (o3 >= 2) t += xor_xchg<1>(t);
   j = 4 * h1 + 2 * h2 + h3;
   return t;
 }
