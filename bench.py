@@ -41,9 +41,9 @@ CFG = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embed
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32) peak, MI355X_MICROARCH.md
 # scripts/pmc_traffic.py outputs (rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench), per workload
-TRAFFIC_JSON = {"qm9_u0": os.path.join(ROOT, "profiles", "r3e_pmc_traffic.json"),
-                "qm9_allprop": os.path.join(ROOT, "profiles", "r3e_pmc_traffic.json"),
-                "aid_infer": os.path.join(ROOT, "profiles", "r3e_pmc_traffic_c5.json")}
+TRAFFIC_JSON = {"qm9_u0": os.path.join(ROOT, "profiles", "r3f_pmc_traffic.json"),
+                "qm9_allprop": os.path.join(ROOT, "profiles", "r3f_pmc_traffic.json"),
+                "aid_infer": os.path.join(ROOT, "profiles", "r3f_pmc_traffic_c5.json")}
 # probe name -> the kernel (substring of its symbol) whose PMC bytes it is
 PMC_KERNEL = {"sbf_project": "sbf_project_waves", "attn_fwd": "attn_fwd_batched",
               "attn_bwd_dst": "attn_bwd_dst_g_batched", "attn_bwd_src": "attn_bwd_src_fold_batched",
