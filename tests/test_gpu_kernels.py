@@ -1342,6 +1342,55 @@ def _t_layout(x):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("accum", [0, 1])
+def test_slab_sum_batch_vs_torch(cuda, accum):
+    """x2g_slab_sum_batch over mixed entries: few splits (256-element blocks, 4 waves of slabs) and
+    many (the gate / radial partials: 64-element blocks, 16 split phases), a strided (ld, cols)
+    destination, bias slabs, an element count that is not a multiple of 4 and a misaligned slab
+    base (both scalar-path), more jobs than one launch takes."""
+    from x2gnn import _lib, ops
+    from x2gnn._lib import stream_ptr
+
+    lib = _lib.load()
+    g = torch.Generator(device=cuda).manual_seed(11 + accum)
+    specs = [(5376, 42, 256), (768, 0, 256), (16384, 128, 9), (128 * 128, 0, 40), (1030, 7, 64), (512, 0, 33),
+             (300, 0, 1), (1000, 10, 32)] * 9  # 72 jobs > 60 per launch
+    keep, jobs, refs = [], [], []
+    for j, (nw, nb, splits) in enumerate(specs):
+        pw_all = torch.randn(splits * nw + 1, device=cuda, generator=g)
+        pw = pw_all[1:] if j % 8 == 5 else pw_all[:-1]  # entry 5: base 4 bytes off 16
+        pb = torch.randn(splits, nb, device=cuda, generator=g) if nb else None
+        strided = j % 8 == 3
+        if strided:
+            dw_store = torch.full((128, 300), 2.0, device=cuda)
+            dst_w = dw_store[:, 40:140]
+        else:
+            dw_store = torch.full((nw,), 2.0, device=cuda)
+            dst_w = dw_store
+        db = torch.full((nb,), 3.0, device=cuda) if nb else None
+        keep += [pw_all, pb, dw_store, db]
+        sw = pw.view(splits, nw).double().sum(0)
+        if strided:
+            sw = sw.view(128, 128)[:, :100]
+        refs.append((dst_w, sw + (2.0 if accum else 0.0), db,
+                     pb.double().sum(0) + (3.0 if accum else 0.0) if nb else None))
+        jobs.append(ops.SlabJob(pw.data_ptr(), pb.data_ptr() if nb else None,
+                                dw_store.data_ptr() + (4 * 40 if strided else 0), db.data_ptr() if nb else None,
+                                nw, nb, splits, 300 if strided else 0, 100 if strided else 0))
+    arr = (ops.SlabJob * len(jobs))(*jobs)
+    assert lib.x2g_slab_sum_batch(arr, len(jobs), accum, stream_ptr()) == 0
+    torch.cuda.synchronize()
+    for dst_w, rw, db, rb in refs:
+        assert torch.allclose(dst_w.double(), rw, rtol=1e-5, atol=1e-4)
+        if db is not None:
+            assert torch.allclose(db.double(), rb, rtol=1e-5, atol=1e-4)
+    for j in range(3, len(specs), 8):  # the strided destinations' other columns untouched
+        store = keep[4 * j + 2]
+        assert torch.equal(store[:, :40], torch.full_like(store[:, :40], 2.0))
+        assert torch.equal(store[:, 140:], torch.full_like(store[:, 140:], 2.0))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("R,njobs", [(37, 3), (1000, 11), (21058, 52)])
 def test_tiled_wgrad_flat_vs_torch(cuda, R, njobs):
     """x2g_tiled_wgrad_flat: every job's dW = dy^T x and db = colsum(dy) from T-layout operands,

@@ -237,10 +237,84 @@ __device__ __forceinline__ void sum_slabs_block(const float* __restrict__ part, 
   }
 }
 
+// Many slabs (the per-workgroup partials of the gate, radial and conv weight gradients: up to 256
+// of a few thousand elements): the block above would walk splits / 4 slabs per wave, one memory
+// round trip per 8, and its few blocks became the batch launch's tail.  Here a block takes 64
+// elements and 16 split phases (lane l: float4 l & 15, phase 4 wave + l / 16), so a phase walks
+// splits / 16 slabs and there are 4x as many blocks; the 16 phase sums are added in phase order.
+// Used when the slabs allow 16-byte loads (block-uniform; the host counts blocks by the same rule).
+constexpr int kSlabNarrowElems = 64;
+constexpr int kSlabNarrowMin = 33;  // splits from which a slab set takes the narrow form
+
+__host__ __device__ __forceinline__ bool slab_narrow(const float* part, int64_t n, int splits) {
+  return splits >= kSlabNarrowMin && (n & 3) == 0 && (reinterpret_cast<uintptr_t>(part) & 15) == 0;
+}
+
+__device__ __forceinline__ void sum_slabs_block_narrow(const float* __restrict__ part, int64_t n, int splits,
+                                                       int64_t blk, bool accum, float* __restrict__ out,
+                                                       float4 (*red)[64], int ld, int cols) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane & 15, ph = 4 * wave + (lane >> 4);
+  const int64_t e = blk * kSlabNarrowElems + 4 * q;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e < n) {
+    const float4* p = reinterpret_cast<const float4*>(part + e);
+    const int64_t stride = n / 4;
+#pragma unroll 8
+    for (int k = ph; k < splits; k += 16) {
+      const float4 v = p[static_cast<int64_t>(k) * stride];
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+  }
+  float4* r = &red[0][0];  // [16 phases][16 float4]
+  r[ph * 16 + q] = s;
+  __syncthreads();
+  if (threadIdx.x < 16 && e < n) {
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int h = 0; h < 16; ++h) {
+      const float4 a = r[h * 16 + q];
+      v[0] += a.x;
+      v[1] += a.y;
+      v[2] += a.z;
+      v[3] += a.w;
+    }
+    if (ld > 0) {
+      const int64_t row = e >> 7;
+      const int c0 = static_cast<int>(e & 127);
+      float* o = out + row * ld + c0;
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4)
+        if (c0 + c4 < cols) o[c4] = accum ? o[c4] + v[c4] : v[c4];
+    } else {
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4)
+        if (e + c4 < n) out[e + c4] = accum ? out[e + c4] + v[c4] : v[c4];
+    }
+  }
+}
+
+// blocks of one slab set, and the block body, in the form slab_narrow picks
+__host__ __device__ __forceinline__ int64_t slab_blocks(const float* part, int64_t n, int splits) {
+  const int64_t per = slab_narrow(part, n, splits) ? kSlabNarrowElems : kSlabElems;
+  return n > 0 ? (n + per - 1) / per : 0;
+}
+__device__ __forceinline__ void sum_slabs_any(const float* __restrict__ part, int64_t n, int splits, int64_t blk,
+                                              bool accum, float* __restrict__ out, float4 (*red)[64], int ld = 0,
+                                              int cols = 0) {
+  if (slab_narrow(part, n, splits))
+    sum_slabs_block_narrow(part, n, splits, blk, accum, out, red, ld, cols);
+  else
+    sum_slabs_block(part, n, splits, blk, accum, out, red, ld, cols);
+}
+
 __global__ void __launch_bounds__(256) sum_slabs(const float* __restrict__ part, int64_t n, int splits, int accum,
                                                  float* __restrict__ out) {
   __shared__ float4 red[4][64];
-  sum_slabs_block(part, n, splits, blockIdx.x, accum != 0, out, red);
+  sum_slabs_any(part, n, splits, blockIdx.x, accum != 0, out, red);
 }
 
 // Two slab sets (weight and bias partials) in one launch: blocks [0, nblk_a) take the first.
@@ -248,21 +322,21 @@ __global__ void __launch_bounds__(256) sum_slabs2(const float* __restrict__ part
                                                   const float* __restrict__ part_b, int64_t nb, int splits, int accum,
                                                   float* __restrict__ out_a, float* __restrict__ out_b) {
   __shared__ float4 red[4][64];
-  const int64_t nblk_a = (na + kSlabElems - 1) / kSlabElems;
+  const int64_t nblk_a = slab_blocks(part_a, na, splits);
   if (static_cast<int64_t>(blockIdx.x) < nblk_a)
-    sum_slabs_block(part_a, na, splits, blockIdx.x, accum != 0, out_a, red);
+    sum_slabs_any(part_a, na, splits, blockIdx.x, accum != 0, out_a, red);
   else
-    sum_slabs_block(part_b, nb, splits, blockIdx.x - nblk_a, accum != 0, out_b, red);
+    sum_slabs_any(part_b, nb, splits, blockIdx.x - nblk_a, accum != 0, out_b, red);
 }
 
 // dw (and db when part_b != NULL) from their slabs, one launch; accum: dw += ..., db += ...
 int sum_slabs_launch(const float* part_w, int64_t nw, const float* part_b, int64_t nb, int splits, float* dw,
                      float* db, bool accum, hipStream_t st) {
   if (part_b && db)
-    sum_slabs2<<<blocks_for(nw, kSlabElems) + blocks_for(nb, kSlabElems), 256, 0, st>>>(part_w, nw, part_b, nb,
-                                                                                          splits, accum, dw, db);
+    sum_slabs2<<<static_cast<unsigned>(slab_blocks(part_w, nw, splits) + slab_blocks(part_b, nb, splits)), 256, 0, st>>>(
+        part_w, nw, part_b, nb, splits, accum, dw, db);
   else
-    sum_slabs<<<blocks_for(nw, kSlabElems), 256, 0, st>>>(part_w, nw, splits, accum, dw);
+    sum_slabs<<<static_cast<unsigned>(slab_blocks(part_w, nw, splits)), 256, 0, st>>>(part_w, nw, splits, accum, dw);
   return last_launch_status();
 }
 
@@ -348,7 +422,7 @@ struct SlabBatch {
   float* out[2 * kBatchJobs];
   int32_t n[2 * kBatchJobs];
   int splits[kBatchJobs];
-  int block_end[2 * kBatchJobs];  // exclusive prefix of kSlabElems-element blocks
+  int block_end[2 * kBatchJobs];  // exclusive prefix of the entries' blocks (slab_blocks)
   int ld[kBatchJobs];             // weight entries: strided destination (x2g_slab_job.ld / cols)
   int cols[kBatchJobs];
   int nent;
@@ -368,8 +442,8 @@ __global__ void __launch_bounds__(256) sum_slabs_batch(const SlabBatch b) {
   const int ent = lo;
   const int first = ent ? b.block_end[ent - 1] : 0;
   const bool wgt = (ent & 1) == 0;
-  sum_slabs_block(b.part[ent], b.n[ent], b.splits[ent >> 1], blockIdx.x - first, b.accum != 0, b.out[ent], red,
-                  wgt ? b.ld[ent >> 1] : 0, wgt ? b.cols[ent >> 1] : 0);
+  sum_slabs_any(b.part[ent], b.n[ent], b.splits[ent >> 1], blockIdx.x - first, b.accum != 0, b.out[ent], red,
+                wgt ? b.ld[ent >> 1] : 0, wgt ? b.cols[ent >> 1] : 0);
 }
 
 X2G_API int x2g_slab_sum_batch(const x2g_slab_job* jobs, int32_t njobs, int32_t accum, void* stream) {
@@ -393,12 +467,12 @@ X2G_API int x2g_slab_sum_batch(const x2g_slab_job* jobs, int32_t njobs, int32_t 
       b.part[e0] = jb.part_w;
       b.out[e0] = jb.dw;
       b.n[e0] = static_cast<int32_t>(jb.n_w);
-      blocks += static_cast<int>(blocks_for(jb.n_w, kSlabElems));
+      blocks += static_cast<int>(slab_blocks(jb.part_w, jb.n_w, jb.splits));
       b.block_end[e0] = blocks;
       b.part[e1] = jb.part_b;
       b.out[e1] = jb.db;
       b.n[e1] = (jb.part_b && jb.db) ? jb.n_b : 0;
-      blocks += static_cast<int>(blocks_for(b.n[e1], kSlabElems));
+      blocks += static_cast<int>(slab_blocks(jb.part_b, b.n[e1], jb.splits));
       b.block_end[e1] = blocks;
       b.nent = e1 + 1;
     }
