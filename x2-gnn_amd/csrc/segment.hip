@@ -452,6 +452,7 @@ __global__ void __launch_bounds__(kLnBig) graph_ln_bwd_reg(const float4* __restr
 constexpr int kLnSplit = 4;
 constexpr int kLnSplitThreads = 256;
 constexpr int kLnSplitUnroll = 4;
+constexpr int kLnRowsUnroll = 8;  // graph_ln_bwd_apply_rows: a config-2 split (~41 rows x 32 float4) in one batch
 
 __device__ __forceinline__ void ln_split_range(const int32_t* __restrict__ rowptr, int64_t D4, int64_t& g, int64_t& lo,
                                                int64_t& hi, int64_t& n) {
@@ -559,6 +560,21 @@ __global__ void __launch_bounds__(kLnSplitThreads) graph_ln_bwd_apply_rows(const
   int64_t g, lo, hi, n;
   ln_split_range(rowptr, D4, g, lo, hi, n);
   if (n == 0) return;
+  // the first batch of dy / y rows goes out before the molecule sums (it does not depend on them),
+  // so the sums' round trip and barrier hide under its loads
+  constexpr int U = kLnRowsUnroll;
+  float4 gv[U], yv[U];
+  int64_t i0 = lo + threadIdx.x;
+  auto load_batch = [&](int64_t b) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = b + u * kLnSplitThreads;
+      const int64_t ic = i < hi ? i : lo;  // b < hi, so lo < hi: a valid row of this split
+      gv[u] = dy[ic];
+      yv[u] = y[ic];
+    }
+  };
+  if (i0 < hi) load_batch(i0);
   const int64_t r0 = rowptr[g];
   float s1 = 0.f, s2 = 0.f;
   for (int64_t r = threadIdx.x; r < n; r += kLnSplitThreads) {
@@ -579,22 +595,16 @@ __global__ void __launch_bounds__(kLnSplitThreads) graph_ln_bwd_apply_rows(const
   }
   const float norm = static_cast<float>(n * D4 * 4);
   const float m1 = t.x / norm, m2 = t.y / norm, r = rstd[g];
-  for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += kLnSplitThreads * kLnSplitUnroll) {
-    float4 gv[kLnSplitUnroll], yv[kLnSplitUnroll];
+  while (i0 < hi) {
 #pragma unroll
-    for (int u = 0; u < kLnSplitUnroll; ++u) {
-      const int64_t i = i0 + u * kLnSplitThreads;
-      const int64_t ic = i < hi ? i : lo;
-      gv[u] = dy[ic];
-      yv[u] = y[ic];
-    }
-#pragma unroll
-    for (int u = 0; u < kLnSplitUnroll; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int64_t i = i0 + u * kLnSplitThreads;
       if (i < hi)
         dx[i] = make_float4(r * (gv[u].x - m1 - yv[u].x * m2), r * (gv[u].y - m1 - yv[u].y * m2),
                             r * (gv[u].z - m1 - yv[u].z * m2), r * (gv[u].w - m1 - yv[u].w * m2));
     }
+    i0 += kLnSplitThreads * U;
+    if (i0 < hi) load_batch(i0);
   }
 }
 
@@ -657,21 +667,25 @@ __global__ void __launch_bounds__(256) keyed_row_sum_partial(const KeyedJobs J, 
   constexpr int RPB = 256 / LPR;
   __shared__ float4 acc[RPB * kKeyedMaxKeys * LPR];
   const int sub = threadIdx.x % LPR, slot = threadIdx.x / LPR;
-  for (int i = threadIdx.x; i < RPB * kKeyedMaxKeys * LPR; i += 256) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  __syncthreads();
   const int64_t per = (rows + gridDim.x - 1) / gridDim.x;
   const int64_t lo = per * blockIdx.x, hi = lo + per < rows ? lo + per : rows;
-  float4* mine = acc + slot * kKeyedMaxKeys * LPR + sub;
   constexpr int U = 4;
-  for (int64_t r0 = lo + slot; r0 < hi; r0 += RPB * U) {
-    float4 v[U];
-    int k[U];
+  float4 v[U];
+  int k[U];
+  auto load = [&](int64_t r0) {  // r0 < hi
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t r = r0 + u * RPB, rc = r < hi ? r : hi - 1;
       v[u] = src[rc * LPR + sub];
       k[u] = key[rc];
     }
+  };
+  int64_t r0 = lo + slot;
+  if (r0 < hi) load(r0);  // the first rows fly while the accumulators are cleared
+  for (int i = threadIdx.x; i < RPB * kKeyedMaxKeys * LPR; i += 256) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  float4* mine = acc + slot * kKeyedMaxKeys * LPR + sub;
+  while (r0 < hi) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (r0 + u * RPB < hi) {
@@ -682,6 +696,8 @@ __global__ void __launch_bounds__(256) keyed_row_sum_partial(const KeyedJobs J, 
         a.w += v[u].w;
       }
     }
+    r0 += RPB * U;
+    if (r0 < hi) load(r0);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < nkeys * LPR; i += 256) {
