@@ -42,7 +42,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32) peak, MI355X_MICROARCH.md
 # scripts/pmc_traffic.py outputs (rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench), per workload
 TRAFFIC_JSON = {"qm9_u0": os.path.join(ROOT, "profiles", "r3f_pmc_traffic.json"),
-                "qm9_allprop": os.path.join(ROOT, "profiles", "r3f_pmc_traffic.json"),
+                "qm9_allprop": None,  # no PMC pass at config 3's shapes: its traffic fields stay null
                 "aid_infer": os.path.join(ROOT, "profiles", "r3f_pmc_traffic_c5.json")}
 # probe name -> the kernel (substring of its symbol) whose PMC bytes it is
 PMC_KERNEL = {"sbf_project": "sbf_project_waves", "attn_fwd": "attn_fwd_batched",
@@ -345,7 +345,7 @@ def load_traffic(workload):
     """(path, {"<kernel>|<grid>": {"fetch_bytes", "write_bytes", ...}}) of the committed PMC summary
     for this workload, or (path, None)."""
     path = TRAFFIC_JSON[workload]
-    if not os.path.exists(path):
+    if path is None or not os.path.exists(path):
         return path, None
     return path, json.load(open(path))["kernels"]
 

@@ -239,20 +239,23 @@ __global__ void __launch_bounds__(256) rbf_gate_bwd_kernel(const GateBwdJobs J, 
 #pragma unroll
     for (int j = 0; j < kGateRMax; ++j) aw[i][j] = 0.f;
   }
-  constexpr int UNROLL = 2;
+  constexpr int UNROLL = 3;
   // the drbf element this lane writes (transpose_sum's j); its old value is loaded with the rows
   const int jd = 4 * ((sub & (LPR / 2)) != 0) + 2 * ((sub & (LPR / 4)) != 0) + ((sub & (LPR / 8)) != 0);
   const bool acc_drbf = drbf && drbf_acc && jd < R;
   const int64_t per = (rows + gridDim.x - 1) / gridDim.x;
   const int64_t lo = per * blockIdx.x, hi = lo + per < rows ? lo + per : rows;
+  // a row's basis values: lane j of each 16-lane DPP row loads value j (a data row spans whole DPP
+  // rows, LPR >= 16) and row_newbcast hands value j to the row's lanes — one load per row, not R
+  const int jl = (threadIdx.x & 15) < R ? (threadIdx.x & 15) : R - 1;
   for (int64_t r0 = lo + slot; r0 < hi; r0 += RPB * UNROLL) {
-    float rb[UNROLL][kGateRMax];
+    float rv[UNROLL];
     f4v gv[UNROLL], xv[UNROLL], av[UNROLL];
     float od[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {  // every load of the UNROLL rows first
       const int64_t r = r0 + u * RPB, rc = r < hi ? r : hi - 1;
-      load_rbf(rbf, rc, R, rb[u]);
+      rv[u] = rbf[rc * R + jl];
       od[u] = acc_drbf ? drbf[rc * R + jd] : 0.0f;
       const int64_t o = owner ? owner[rc] : rc;
       gv[u] = g[o * LPR + sub];
@@ -264,8 +267,17 @@ __global__ void __launch_bounds__(256) rbf_gate_bwd_kernel(const GateBwdJobs J, 
       const int64_t r = r0 + u * RPB;
       const bool ok = r < hi;
       const float m = ok ? 1.f : 0.f;
+      float rb[kGateRMax];
+      rb[0] = dpp_mov<0x150>(rv[u]);
+      rb[1] = dpp_mov<0x151>(rv[u]);
+      rb[2] = dpp_mov<0x152>(rv[u]);
+      rb[3] = dpp_mov<0x153>(rv[u]);
+      rb[4] = dpp_mov<0x154>(rv[u]);
+      rb[5] = dpp_mov<0x155>(rv[u]);
+      rb[6] = dpp_mov<0x156>(rv[u]);
+      rb[7] = dpp_mov<0x157>(rv[u]);
       if (dx && ok) {
-        f4v d = gv[u] * gw.filter(rb[u]);
+        f4v d = gv[u] * gw.filter(rb);
         if (dx_add) d += av[u];
         dx[r * LPR + sub] = d;
       }
@@ -274,7 +286,7 @@ __global__ void __launch_bounds__(256) rbf_gate_bwd_kernel(const GateBwdJobs J, 
       for (int i = 0; i < 4; ++i) {
         ab[i] += df[i];
 #pragma unroll
-        for (int j = 0; j < kGateRMax; ++j) aw[i][j] = fmaf(df[i], rb[u][j], aw[i][j]);
+        for (int j = 0; j < kGateRMax; ++j) aw[i][j] = fmaf(df[i], rb[j], aw[i][j]);
       }
       if (drbf) {
         float p[kGateRMax];
