@@ -302,14 +302,14 @@ def proj_probe(R, reps):
     return {"conv_proj_fwd": (_event_time(fwd, reps), flops), "conv_proj_bwd_gate": (_event_time(bwd, reps), flops)}
 
 
-def flat_wgrad_probe(reps):
+def flat_wgrad_probe(flat_launches, reps):
     """The step's largest kernel: every T-layout weight gradient of the backward in one launch
     (x2g_tiled_wgrad_flat, ops._flush_tiled) with the job list the captured step recorded
-    (ops.FLAT_LAUNCHES: rows R, one [128,cols] dW = dz^T x per job, K = R), on synthetic T-layout
+    (Trainer.flat_launches: rows R, one [128,cols] dW = dz^T x per job, K = R), on synthetic T-layout
     operands, HIP-event timed on the launch stream.  FLOPs per launch: sum_j 2 * R * 128 * cols_j."""
-    if not ops.FLAT_LAUNCHES:
+    if not flat_launches:
         return None
-    R, cols = max(ops.FLAT_LAUNCHES, key=lambda rc: rc[0] * sum(rc[1]))
+    R, cols = max(flat_launches, key=lambda rc: rc[0] * sum(rc[1]))
     n, D = len(cols), 128
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(5)
@@ -618,7 +618,7 @@ def main():
     # (profiles/r2_*_step_kernels.txt) -- the one-launch T-layout weight gradient of the whole
     # backward (x2g_tiled_wgrad_flat), f32 MFMA-bound (sum_j 2 R 128 cols_j FLOP, ~K = R deep)
     roof = None
-    flat = flat_wgrad_probe(args.kernel_reps) if wl["train"] else None
+    flat = flat_wgrad_probe(runner.flat_launches, args.kernel_reps) if wl["train"] else None
     if flat is not None:
         f_tfs = flat["flops"] / (flat["ms"] * 1e-3) / 1e12
         traffic = pmc_traffic([("tiled_flat_kernel", None)], traffic_table)  # (the largest launch)

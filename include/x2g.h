@@ -46,6 +46,15 @@ const char* x2g_status_string(int status);
  * Replaces the CSR row pointer scipy builds in edge_graph.py:14 (adj_matrix.tocsr()). */
 int x2g_csr_rowptr(const int32_t* keys, int64_t n, int64_t n_seg, int32_t* rowptr, void* stream);
 
+/* The same row pointer for keys the caller only ASSUMES sorted (the drop-in APIs' sync-free
+ * path, sbftransformer_conv.py:109 propagate over edge_index[1]; model.py:46,53 batch vectors):
+ * rowptr[s] = lower_bound(keys, s) by binary search, so every entry is written and lies in
+ * [0, n] whatever the keys hold, and status[0] is set to 1 (vector store, no host read) when a key
+ * is out of [0, n_seg) or smaller than its predecessor; status[0] is zeroed first.  A violated
+ * contract therefore gives wrong numbers, flagged on the device, never an out-of-range access. */
+int x2g_csr_rowptr_checked(const int32_t* keys, int64_t n, int64_t n_seg, int32_t* rowptr, int32_t* status,
+                           void* stream);
+
 /* Workspace bytes for x2g_vertex_to_edge / x2g_line_graph_transpose. */
 size_t x2g_vertex_to_edge_workspace(int64_t num_edges, int64_t num_nodes);
 
@@ -296,6 +305,26 @@ int x2g_segment_softmax_fwd(const float* src, const int32_t* rowptr, int64_t num
 int x2g_segment_softmax_bwd(const float* out, const float* dout, const int32_t* rowptr,
                             int64_t num_segments, int64_t heads, float* dsrc, void* stream);
 
+/* Index in ANY order (the operator-level drop-ins): the caller stable-sorts the keys on the device
+ * and passes the permutation `perm` (sorted position r -> source row perm[r]) with the CSR row
+ * pointer of the sorted keys; source rows are read in place through perm (no gathered copy).
+ *   x2g_segment_reduce_perm: out[g] = sum (mode X2G_REDUCE_SUM) or mean (X2G_REDUCE_MEAN: / max(count,
+ *     1), empty segments 0) of x[perm[r]], r in segment g — torch_scatter scatter_add / scatter_mean
+ *     (readout.py:37,67-71; model.py:53), summed in the caller's row order;
+ *   x2g_segment_reduce_perm_bwd: out[perm[r]] = g[seg(r)] (/ count for MEAN), its adjoint;
+ *   x2g_segment_softmax_perm_fwd/bwd: PyG utils.softmax(src, index, num_nodes)
+ *     (sbftransformer_conv.py:151) and its backward, written back in the caller's row order. */
+#define X2G_REDUCE_SUM 0
+#define X2G_REDUCE_MEAN 1
+int x2g_segment_reduce_perm(const float* x, const int32_t* perm, const int32_t* rowptr, int64_t num_segments,
+                            int64_t dim, int mode, float* out, void* stream);
+int x2g_segment_reduce_perm_bwd(const float* g, const int32_t* perm, const int32_t* rowptr, int64_t num_segments,
+                                int64_t dim, int mode, float* out, void* stream);
+int x2g_segment_softmax_perm_fwd(const float* src, const int32_t* perm, const int32_t* rowptr,
+                                 int64_t num_segments, int64_t heads, float* out, void* stream);
+int x2g_segment_softmax_perm_bwd(const float* out, const float* dout, const int32_t* perm, const int32_t* rowptr,
+                                 int64_t num_segments, int64_t heads, float* dsrc, void* stream);
+
 /* PyG nn.LayerNorm(mode='graph', affine=False) (model.py:161,183): per segment g of rows,
  * mu = sum x / (n_g*D), var = sum (x-mu)^2 / (n_g*D) (n_g clamped >= 1), out = (x-mu)/sqrt(var+eps).
  * mean/rstd[num_segments] are saved for the backward. */
@@ -514,6 +543,16 @@ int x2g_readout_head_bwd(const float* dout, const x2g_head_group* groups, int32_
 #define X2G_OPT_CLIP 8      /* out: clip coefficient applied */
 #define X2G_OPT_STEP_SIZE 9 /* internal: lr / (1 - beta1^t) */
 #define X2G_OPT_BC2_SQRT 10 /* internal: sqrt(1 - beta2^t) */
+/* Optional on-device LR schedule, LinearWarmupExponentialDecay (scheduler.py:4-31; config.json
+ * warmup_steps 3000, decay_steps 3e6, decay_rate 0.01), evaluated from the device step count so a
+ * captured graph follows it: when X2G_OPT_WARMUP > 0, step t (0-based, the steps taken before it)
+ * uses lr = BASE_LR * min(1/W + t/W, 1) * DECAY_RATE^(t / DECAY_STEPS) (the exponent floored with
+ * STAIRCASE != 0), computed in double as LambdaLR does, and the value used is left in X2G_OPT_LR. */
+#define X2G_OPT_WARMUP 11
+#define X2G_OPT_DECAY_STEPS 12
+#define X2G_OPT_DECAY_RATE 13
+#define X2G_OPT_BASE_LR 14
+#define X2G_OPT_STAIRCASE 15
 
 /* Workspace bytes for x2g_clip_adam_ema. */
 size_t x2g_optimizer_workspace(int64_t n);

@@ -44,6 +44,20 @@ def oracle_model(z):
 
 
 def rel_err(a, b):
+    """max |a - b| / max |b| (one scale for the whole array: outputs other than energies)."""
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def energy_rel_err(a, b, floor=1e-3):
+    """Per-molecule relative error of energies: max_i |a_i - b_i| / |b_i| — the north-star "1e-4
+    relative on fp32 energies" per molecule, not against the batch maximum.  A molecule whose
+    reference energy is below ``floor`` x the batch's largest magnitude is measured against that
+    floor instead (a relative error of a near-zero value is not meaningful)."""
+    a = np.asarray(a, np.float64).reshape(-1)
+    b = np.asarray(b, np.float64).reshape(-1)
+    if b.size == 0:
+        return 0.0
+    scale = np.maximum(np.abs(b), floor * max(np.abs(b).max(), 1e-30))
+    return float((np.abs(a - b) / scale).max())

@@ -126,3 +126,86 @@ def test_two_rank_allreduce_equals_full_batch_gradient(weighted):
     scale = np.abs(ref).max()
     np.testing.assert_allclose(got[0][0], ref, rtol=0, atol=2e-5 * scale)
     assert abs(got[0][1] - float(loss)) <= 1e-5 * max(1.0, abs(float(loss)))
+
+
+def _aid_worker(rank, world, port, idx, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from conftest import GOLDEN
+        from oracle import ref_cpu
+        from x2gnn.dist import collate_shard
+        from x2gnn.synth import molecules_from_geometry_file
+
+        mols = molecules_from_geometry_file(os.path.join(GOLDEN, "aid_geom.npz"), indices=idx)
+        batch, n_local, n_global = collate_shard(mols, world, rank)
+        model = _model()
+        bucket = GradBucket(model.parameters())
+        bucket.zero()
+        res = ref_cpu.run_batch(model, batch)
+        loss = torch.nn.functional.smooth_l1_loss(res, batch.y)
+        loss.backward()
+        bucket.allreduce_mean(local_count=n_local, global_count=n_global)
+        t = loss.detach().clone() * n_local / n_global
+        dist.all_reduce(t)
+        load = int(batch._meta["triplets"].sum())
+        out_q.put((rank, bucket.flat.clone().numpy(), float(t), n_local, load,
+                   batch._store["_x2g_count_z"].numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(400)
+def test_four_rank_aid_mix_sharding_and_allreduce():
+    """Config 4's sharding on an AID-sized mix (66-135-atom molecules, T from ~20k to ~120k each)
+    over 4 gloo ranks: shard_by_triplets partitions the batch with unequal molecule counts and a
+    load imbalance within the LPT bound (one molecule's T), collate_shard hands every rank the
+    global batch's atomic numbers, and the count-weighted all-reduce of the shard gradients equals
+    the single-process gradient of the whole batch (the embedding row excepted: the oracle
+    evaluates scale_grad_by_freq per shard, the product's global-count rule is GPU-tested in
+    tests/test_dist_gpu.py)."""
+    from conftest import GOLDEN
+    from oracle import ref_cpu
+    from x2gnn.synth import molecules_from_geometry_file
+
+    world = 4
+    idx = [1, 3, 12, 0, 5, 16, 13, 2, 9, 17]  # 135, 79, 66, ... atoms: a ragged mix
+    mols = molecules_from_geometry_file(os.path.join(GOLDEN, "aid_geom.npz"), indices=idx)
+    counts = [m["triplet_num"] for m in mols]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_aid_worker, args=(r, world, port, idx, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, flat, loss, n_local, load, count_z = q.get(timeout=360)
+        got[r] = (flat, loss, n_local, load, count_z)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sum(g[2] for g in got.values()) == len(mols) and len({g[2] for g in got.values()}) > 1
+    loads = [g[3] for g in got.values()]
+    assert sum(loads) == sum(counts) and max(loads) - min(loads) <= max(counts)
+    all_z = np.concatenate([m["x"] for m in mols])
+    for r in range(world):
+        np.testing.assert_array_equal(got[r][4], all_z)
+        np.testing.assert_array_equal(got[r][0], got[0][0])
+    model = _model()
+    bucket = GradBucket(model.parameters())
+    bucket.zero()
+    b = collate(mols)
+    res = ref_cpu.run_batch(model, b)
+    loss = torch.nn.functional.smooth_l1_loss(res, b.y)
+    loss.backward()
+    ref = bucket.flat.numpy().copy()
+    emb = model.emb_block.embedding.weight
+    e0 = (emb.grad.data_ptr() - bucket.flat.data_ptr()) // 4
+    mask = np.ones_like(ref, dtype=bool)
+    mask[e0:e0 + emb.numel()] = False
+    scale = np.abs(ref).max()
+    np.testing.assert_allclose(got[0][0][mask], ref[mask], rtol=0, atol=2e-5 * scale)
+    lv = float(loss.detach())
+    assert abs(got[0][1] - lv) <= 1e-5 * max(1.0, abs(lv))

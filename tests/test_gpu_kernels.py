@@ -406,6 +406,127 @@ def test_scatter_add_any_index_order(cuda):
     torch.testing.assert_close(s.grad.cpu(), up.index_select(0, idx), rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("D", [1, 3, 16, 128, 256])
+@pytest.mark.parametrize("order", ["shuffled", "sorted"])
+def test_scatter_mean_any_index_order(cuda, D, order):
+    """ops.scatter_mean == torch_scatter.scatter_mean(src, index, dim=0, dim_size) (readout.py:69):
+    sum / max(count, 1), empty segments 0; any index order; the gradient of src is g[index] / count.
+    (fp64 torch restatement of scatter_mean as the reference, torch_scatter itself not being here.)"""
+    from x2gnn import ops
+
+    g = torch.Generator().manual_seed(9 + D)
+    idx = torch.randint(0, 40, (700,), generator=g)
+    idx[idx == 5] = 6  # an empty segment
+    if order == "sorted":
+        idx = idx.sort().values
+    src = torch.randn(700, D, generator=g) if D > 1 else torch.randn(700, generator=g)
+    s2 = src.double().reshape(700, -1)
+    cnt = torch.zeros(45, dtype=torch.float64).index_add_(0, idx, torch.ones(700, dtype=torch.float64))
+    ref = torch.zeros(45, s2.shape[1], dtype=torch.float64).index_add_(0, idx, s2) / cnt.clamp(min=1)[:, None]
+    s = src.to(cuda).requires_grad_(True)
+    out = ops.scatter_mean(s, idx.to(cuda), 45)
+    assert out.shape == ((45, D) if D > 1 else (45,))
+    torch.testing.assert_close(out.double().cpu().reshape(45, -1), ref, rtol=1e-5, atol=1e-6)
+    assert float(out.reshape(45, -1)[5].abs().max()) == 0.0
+    up = torch.randn(out.shape, generator=g)
+    (out * up.to(cuda)).sum().backward()
+    want = (up.double().reshape(45, -1) / cnt.clamp(min=1)[:, None]).index_select(0, idx)
+    torch.testing.assert_close(s.grad.double().cpu().reshape(700, -1), want, rtol=1e-6, atol=1e-7)
+
+
+def test_softmax_index_form_vs_oracle(cuda):
+    """ops.softmax(src, index, num_nodes) == PyG utils.softmax (sbftransformer_conv.py:151; the
+    oracle's restatement, max shift and + 1e-16) for a shuffled index with empty groups, [R] and
+    [R, H], forward and backward; and equal to the sorted-index (CSR) form row for row."""
+    from x2gnn import ops
+
+    g = torch.Generator().manual_seed(12)
+    idx = torch.randint(0, 60, (1500,), generator=g)
+    idx[idx == 3] = 4
+    for shape in ((1500, 16), (1500,)):
+        src = (3 * torch.randn(*shape, generator=g)).requires_grad_(True)
+        ref = ref_cpu.pyg_softmax(src, idx, 64)
+        up = torch.randn(*shape, generator=g)
+        ref.backward(up)
+        sg = src.detach().to(cuda).requires_grad_(True)
+        out = ops.softmax(sg, idx.to(cuda), num_nodes=64)
+        out.backward(up.to(cuda))
+        np.testing.assert_allclose(out.detach().cpu().numpy(), ref.detach().numpy(), rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(sg.grad.cpu().numpy(), src.grad.numpy(), rtol=1e-4, atol=1e-6)
+    order = torch.argsort(idx, stable=True)
+    srt = idx[order]
+    rp = torch.from_numpy(np.searchsorted(srt.numpy(), np.arange(65)).astype(np.int32)).to(cuda)
+    x = torch.randn(1500, 16, device=cuda)
+    a = ops.softmax(x, idx.to(cuda), num_nodes=64)
+    b = ops.softmax(x[order.to(cuda)], ptr=rp)
+    assert torch.equal(a[order.to(cuda)], b)
+
+
+def test_scatter_ops_are_capture_safe(cuda):
+    """The index-form drop-ins read nothing back from the device: scatter_add / scatter_mean /
+    softmax with a fresh unsorted index record into a HIP graph and replay to the eager values."""
+    from x2gnn import ops
+
+    g = torch.Generator(device=cuda).manual_seed(3)
+    idx = torch.randint(0, 30, (500,), device=cuda, generator=g)
+    src = torch.randn(500, 32, device=cuda, generator=g)
+    eager = (ops.scatter_add(src, idx, 30), ops.scatter_mean(src, idx, 30), ops.softmax(src, idx, num_nodes=30))
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        ops.scatter_add(src, idx, 30)  # (warm-up on a side stream, as torch.cuda.graph asks)
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        outs = (ops.scatter_add(src, idx, 30), ops.scatter_mean(src, idx, 30), ops.softmax(src, idx, num_nodes=30))
+    graph.replay()
+    torch.cuda.synchronize()
+    for a, b in zip(outs, eager):
+        assert torch.equal(a, b)
+
+
+def test_conv_assume_sorted_flags_violation_without_sync(cuda):
+    """assume_sorted=True skips the device sort: on the reference's (sorted) order the output equals
+    the default path's; on a shuffled order the violation is flagged on the line graph's device
+    status (read here, after the fact) and nothing faults."""
+    from x2gnn import ops
+
+    z = golden("conv1.npz")
+    conv = _product_conv(z, cuda)
+    trip = torch.from_numpy(z["trip"].astype(np.int64)).to(cuda)
+    sbf, rbf = torch.from_numpy(z["sbf"]).to(cuda), torch.from_numpy(z["rbf"]).to(cuda)
+    x, ea = torch.from_numpy(z["conv_x"]).to(cuda), torch.from_numpy(z["conv_edge_attr"]).to(cuda)
+    with torch.no_grad():
+        a = conv(sbf, rbf, x, trip, ea)
+        b = conv(sbf, rbf, x, trip, ea, assume_sorted=True)
+    torch.testing.assert_close(a, b, rtol=0, atol=0)
+    lg = ops.LineGraph.from_triplets(trip, x.shape[0])
+    assert not lg.order_violated()
+    perm = torch.from_numpy(np.random.default_rng(2).permutation(trip.shape[1])).to(cuda)
+    bad = ops.LineGraph.from_triplets(trip.index_select(1, perm), x.shape[0])
+    rp = bad.trip_rowptr.cpu().numpy()
+    assert bad.order_violated() and rp.min() >= 0 and rp.max() <= trip.shape[1]
+    with torch.no_grad():
+        out = conv(sbf.index_select(0, perm), rbf, x, trip.index_select(1, perm), ea.index_select(0, perm),
+                   line_graph=bad)
+    torch.cuda.synchronize()
+    assert out.shape == a.shape
+
+
+def test_checked_rowptr_matches_plain(cuda):
+    """x2g_csr_rowptr_checked == x2g_csr_rowptr on sorted keys (empty segments, keys ending early),
+    status 0; an out-of-range key sets the status."""
+    from x2gnn import ops
+
+    keys = torch.tensor([0, 0, 2, 2, 2, 5, 7, 7], dtype=torch.int32, device=cuda)
+    rp, st = ops.csr_rowptr_checked(keys, 10)
+    assert torch.equal(rp, ops.csr_rowptr(keys, 10)) and int(st) == 0
+    _, st = ops.csr_rowptr_checked(torch.tensor([0, 1, 12], dtype=torch.int32, device=cuda), 10)
+    assert int(st) == 1
+    rp, st = ops.csr_rowptr_checked(torch.empty(0, dtype=torch.int32, device=cuda), 4)
+    assert rp.tolist() == [0, 0, 0, 0, 0] and int(st) == 0
+
+
 def test_per_destination_edge_table_equals_per_triplet(cuda):
     """EDGE_PER_DST (table row per destination) == EDGE_PER_TRIPLET with the expanded rows."""
     from x2gnn import ops
@@ -611,6 +732,57 @@ def test_flat_adam_matches_torch(cuda, max_norm):
             for p, m in zip(mine, opt.ema_params()):
                 assert torch.equal(m, p.detach())
     assert float(opt.steps) == 3.0
+
+
+@pytest.mark.parametrize("staircase", [False, True])
+def test_flat_adam_lr_schedule_matches_lambda_lr(cuda, staircase):
+    """FlatAdam.set_schedule (the device-side LinearWarmupExponentialDecay) vs torch Adam driven by
+    LambdaLR with the reference's lr_lambda (scheduler.py:19-26, restated here: the reference cannot
+    be imported on the GPU box), scheduler.step() after every optimizer.step() as trainer.py:44-47
+    does; the update is replayed from ONE captured HIP graph, so the schedule must come from the
+    device step count.  Warmup 3 / decay 4 steps / rate 0.5 so 9 steps cross both regimes."""
+    from x2gnn.dist import GradBucket
+    from x2gnn.optim import FlatAdam
+
+    W, DS, RATE = 3, 4, 0.5
+
+    def lr_lambda(step):
+        warmup = min(1 / W + 1 / W * step, 1)
+        exponent = step / DS
+        if staircase:
+            exponent = int(exponent)
+        return warmup * RATE ** exponent
+
+    g = torch.Generator(device=cuda).manual_seed(12)
+    shapes = [(64, 32), (32,), (5,)]
+    ref = [torch.randn(s, device=cuda, generator=g).requires_grad_(True) for s in shapes]
+    mine = [r.detach().clone().requires_grad_(True) for r in ref]
+    opt_ref = torch.optim.Adam(ref, lr=1e-2)
+    sched = torch.optim.lr_scheduler.LambdaLR(opt_ref, lr_lambda)
+    bucket = GradBucket(mine)
+    opt = FlatAdam(mine, lr=1e-2, max_norm=100.0, ema_decay=None, bucket=bucket)
+    opt.set_schedule(W, DS, RATE, staircase=staircase)
+    grads = [[torch.randn(s, device=cuda, generator=g) for s in shapes] for _ in range(9)]
+    stage = [torch.zeros(s, device=cuda) for s in shapes]
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for m, st in zip(mine, stage):
+            m.grad.copy_(st)
+        opt.step()
+    for step in range(9):
+        lr_used = opt_ref.param_groups[0]["lr"]
+        for r, gr in zip(ref, grads[step]):
+            r.grad = gr.clone()
+        torch.nn.utils.clip_grad_norm_(ref, 100.0)
+        opt_ref.step()
+        sched.step()
+        for st, gr in zip(stage, grads[step]):
+            st.copy_(gr)
+        graph.replay()
+        torch.cuda.synchronize()
+        assert abs(float(opt.lr) - lr_used) <= 1e-7 * lr_used, (step, float(opt.lr), lr_used)
+        for r, m in zip(ref, mine):
+            torch.testing.assert_close(m.detach(), r.detach(), rtol=2e-6, atol=2e-7)
 
 
 @pytest.mark.gpu

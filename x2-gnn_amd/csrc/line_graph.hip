@@ -26,6 +26,27 @@ __global__ void rowptr_kernel(const int32_t* __restrict__ keys, int64_t n, int64
   for (int64_t s = prev + 1; s <= cur; ++s) rowptr[s] = static_cast<int32_t>(i);
 }
 
+// rowptr[s] = lower_bound(keys, s) for s in [0, n_seg] (binary search: every entry written, always in
+// [0, n]); threads i < n also check the keys' contract and flag a violation with a plain vector store
+// of 1 (every writer stores the same value, so the race is benign; no atomics).
+__global__ void rowptr_checked_kernel(const int32_t* __restrict__ keys, int64_t n, int64_t n_seg,
+                                      int32_t* __restrict__ rowptr, int32_t* __restrict__ status) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i <= n_seg) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (keys[mid] < i) lo = mid + 1;
+      else hi = mid;
+    }
+    rowptr[i] = static_cast<int32_t>(lo);
+  }
+  if (i < n) {
+    const int32_t k = keys[i];
+    if (k < 0 || k >= n_seg || (i > 0 && keys[i - 1] > k)) status[0] = 1;
+  }
+}
+
 // ----------------------------------------------------------------------------- exclusive scan
 // Three-phase scan of int32 counts: 1024 elements per 256-thread block, block totals scanned
 // by one block, then offsets added.  out has n+1 entries (out[n] = total).
@@ -342,7 +363,7 @@ __global__ void transpose_sym_kernel(const int32_t* __restrict__ src, const int3
 
 using namespace x2g;
 
-X2G_API int x2g_abi_version(void) { return 10; }
+X2G_API int x2g_abi_version(void) { return 11; }
 
 X2G_API const char* x2g_status_string(int status) {
   switch (status) {
@@ -357,6 +378,18 @@ X2G_API const char* x2g_status_string(int status) {
 X2G_API int x2g_csr_rowptr(const int32_t* keys, int64_t n, int64_t n_seg, int32_t* rowptr, void* stream) {
   if (n < 0 || n_seg < 0 || !rowptr || (n > 0 && !keys)) return X2G_EINVAL;
   rowptr_kernel<<<blocks_for(n + 1, 256), 256, 0, as_stream(stream)>>>(keys, n, n_seg, rowptr);
+  return last_launch_status();
+}
+
+X2G_API int x2g_csr_rowptr_checked(const int32_t* keys, int64_t n, int64_t n_seg, int32_t* rowptr,
+                                   int32_t* status, void* stream) {
+  if (n < 0 || n_seg < 0 || !rowptr || !status || (n > 0 && !keys)) return X2G_EINVAL;
+  if (n_seg + 1 > INT32_MAX || n > INT32_MAX) return X2G_EINVAL;
+  hipStream_t st = as_stream(stream);
+  const hipError_t me = hipMemsetAsync(status, 0, sizeof(int32_t), st);
+  if (me != hipSuccess) return static_cast<int>(me);
+  const int64_t m = n > n_seg + 1 ? n : n_seg + 1;
+  rowptr_checked_kernel<<<blocks_for(m, 256), 256, 0, st>>>(keys, n, n_seg, rowptr, status);
   return last_launch_status();
 }
 

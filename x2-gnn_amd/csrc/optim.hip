@@ -63,6 +63,14 @@ __global__ void __launch_bounds__(kNormThreads) opt_finalize(const float* __rest
     const float coef = max_norm > 0.f ? fminf(max_norm / (norm + 1e-6f), 1.0f) : 1.0f;
     const float step = sc[X2G_OPT_STEP] + 1.0f;
     sc[X2G_OPT_STEP] = step;
+    if (sc[X2G_OPT_WARMUP] > 0.f) {  // LinearWarmupExponentialDecay.lr_lambda(t), t = steps taken before this one
+      const double w = sc[X2G_OPT_WARMUP], t = static_cast<double>(step) - 1.0;
+      const double warm = fmin(1.0 / w + 1.0 / w * t, 1.0);
+      double ex = t / static_cast<double>(sc[X2G_OPT_DECAY_STEPS]);
+      if (sc[X2G_OPT_STAIRCASE] != 0.f) ex = floor(ex);
+      sc[X2G_OPT_LR] = static_cast<float>(static_cast<double>(sc[X2G_OPT_BASE_LR]) * warm *
+                                          pow(static_cast<double>(sc[X2G_OPT_DECAY_RATE]), ex));
+    }
     sc[X2G_OPT_NORM] = norm;
     sc[X2G_OPT_CLIP] = coef;
     // bias corrections as torch.optim.Adam computes them (in double, rounded to float)

@@ -166,31 +166,171 @@ int seg_bcast_launch(const float* g, const float* mul, const int32_t* rowptr, in
   return last_launch_status();
 }
 
+// ------------------------------------------------------------------------------ permuted reductions
+// The same segment walk for an index in ANY order: the caller sorts the keys (a stable sort on the
+// device, no host read) and hands over the permutation; segment g's rows are x[perm[r]] for r in
+// [rowptr[g], rowptr[g+1]), so a [R, D] source is read once in place instead of being gathered
+// into sorted order first.  MEAN divides by max(count, 1) (torch_scatter scatter_mean: empty
+// segments give 0).  The stable sort keeps each segment's rows in the caller's order: the sum is
+// the fixed left-to-right order of a sorted index, bitwise reproducible.
+template <int LPR, bool MEAN>
+__global__ void __launch_bounds__(256) seg_reduce_perm_vec(const float4* __restrict__ x,
+                                                           const int32_t* __restrict__ perm,
+                                                           const int32_t* __restrict__ rowptr, int64_t G,
+                                                           float4* __restrict__ out) {
+  constexpr int RPI = 64 / LPR;
+  constexpr int UNROLL = 8;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane % LPR, slot = lane / LPR;
+  const int nwaves = gridDim.x * kSegWaves;
+  for (int64_t g = uniform(blockIdx.x * kSegWaves + (threadIdx.x >> 6)); g < G; g += nwaves) {
+    const int r0 = uniform(rowptr[g]), r1 = uniform(rowptr[g + 1]);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int rb = r0; rb < r1; rb += UNROLL * RPI) {
+      int src[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const int r = rb + u * RPI + slot;
+        src[u] = perm[r < r1 ? r : r1 - 1];
+      }
+      float4 v[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) v[u] = x[static_cast<int64_t>(src[u]) * LPR + sub];
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const bool ok = rb + u * RPI + slot < r1;
+        acc.x += keep(v[u].x, ok);
+        acc.y += keep(v[u].y, ok);
+        acc.z += keep(v[u].z, ok);
+        acc.w += keep(v[u].w, ok);
+      }
+    }
+#pragma unroll
+    for (int off = LPR; off < 64; off <<= 1) acc = f4_add(acc, f4_shfl_xor(acc, off));
+    if (MEAN) {
+      const float inv = 1.0f / static_cast<float>(r1 - r0 > 1 ? r1 - r0 : 1);
+      acc = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+    }
+    if (slot == 0) out[g * LPR + sub] = acc;
+  }
+}
+
+template <bool MEAN>
+__global__ void seg_reduce_perm_scalar(const float* __restrict__ x, const int32_t* __restrict__ perm,
+                                       const int32_t* __restrict__ rowptr, int64_t G, int64_t D,
+                                       float* __restrict__ out) {
+  const int64_t gid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (gid >= G * D) return;
+  const int64_t g = gid / D, c = gid - g * D;
+  const int64_t r0 = rowptr[g], r1 = rowptr[g + 1];
+  float acc = 0.f;
+  for (int64_t r = r0; r < r1; ++r) acc += x[static_cast<int64_t>(perm[r]) * D + c];
+  out[gid] = MEAN ? acc / static_cast<float>(r1 - r0 > 1 ? r1 - r0 : 1) : acc;
+}
+
+// Adjoint: out[perm[r], :] = g[seg(r), :] (/ count for MEAN).  perm is a permutation, so no output
+// row is written twice; rows outside every segment (keys outside [0, G)) are left as they are.
+template <int LPR, bool MEAN>
+__global__ void __launch_bounds__(256) seg_bcast_perm_vec(const float4* __restrict__ g_in,
+                                                          const int32_t* __restrict__ perm,
+                                                          const int32_t* __restrict__ rowptr, int64_t G,
+                                                          float4* __restrict__ out) {
+  constexpr int RPI = 64 / LPR;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane % LPR, slot = lane / LPR;
+  const int nwaves = gridDim.x * kSegWaves;
+  for (int64_t g = uniform(blockIdx.x * kSegWaves + (threadIdx.x >> 6)); g < G; g += nwaves) {
+    const int r0 = rowptr[g], r1 = rowptr[g + 1];
+    if (r0 >= r1) continue;
+    float4 gv = g_in[g * LPR + sub];
+    if (MEAN) {
+      const float inv = 1.0f / static_cast<float>(r1 - r0);
+      gv = make_float4(gv.x * inv, gv.y * inv, gv.z * inv, gv.w * inv);
+    }
+    for (int r = r0 + slot; r < r1; r += RPI) out[static_cast<int64_t>(perm[r]) * LPR + sub] = gv;
+  }
+}
+
+template <bool MEAN>
+__global__ void seg_bcast_perm_scalar(const float* __restrict__ g_in, const int32_t* __restrict__ perm,
+                                      const int32_t* __restrict__ rowptr, int64_t G, int64_t D,
+                                      float* __restrict__ out) {
+  const int64_t gid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (gid >= G * D) return;
+  const int64_t g = gid / D, c = gid - g * D;
+  const int64_t r0 = rowptr[g], r1 = rowptr[g + 1];
+  if (r0 >= r1) return;
+  const float gv = MEAN ? g_in[gid] / static_cast<float>(r1 - r0) : g_in[gid];
+  for (int64_t r = r0; r < r1; ++r) out[static_cast<int64_t>(perm[r]) * D + c] = gv;
+}
+
+template <bool MEAN, bool BCAST>
+int seg_perm_launch(const float* in, const int32_t* perm, const int32_t* rowptr, int64_t G, int64_t D, float* out,
+                    hipStream_t st) {
+  const auto* iv = reinterpret_cast<const float4*>(in);
+  auto* ov = reinterpret_cast<float4*>(out);
+  const unsigned grid = seg_grid(G);
+  const bool aligned = (reinterpret_cast<uintptr_t>(in) % 16 == 0) && (reinterpret_cast<uintptr_t>(out) % 16 == 0);
+#define X2G_PERM_CASE(W, L)                                                                  \
+  case W:                                                                                    \
+    if (BCAST) seg_bcast_perm_vec<L, MEAN><<<grid, 256, 0, st>>>(iv, perm, rowptr, G, ov);  \
+    else seg_reduce_perm_vec<L, MEAN><<<grid, 256, 0, st>>>(iv, perm, rowptr, G, ov);       \
+    break;
+  switch (aligned ? D : -1) {
+    X2G_PERM_CASE(4, 1)
+    X2G_PERM_CASE(8, 2)
+    X2G_PERM_CASE(16, 4)
+    X2G_PERM_CASE(32, 8)
+    X2G_PERM_CASE(64, 16)
+    X2G_PERM_CASE(128, 32)
+    X2G_PERM_CASE(256, 64)
+    default:
+      if (BCAST) seg_bcast_perm_scalar<MEAN><<<blocks_for(G * D, 256), 256, 0, st>>>(in, perm, rowptr, G, D, out);
+      else seg_reduce_perm_scalar<MEAN><<<blocks_for(G * D, 256), 256, 0, st>>>(in, perm, rowptr, G, D, out);
+      break;
+  }
+#undef X2G_PERM_CASE
+  return last_launch_status();
+}
+
 // ------------------------------------------------------------------------------ segment softmax
-__global__ void seg_softmax_fwd_kernel(const float* __restrict__ src, const int32_t* __restrict__ rowptr,
-                                       int64_t G, int64_t H, float* __restrict__ out) {
+// perm == NULL: rows of segment g are [rowptr[g], rowptr[g+1]); otherwise perm[r] over that range.
+__device__ __forceinline__ int64_t seg_row(const int32_t* perm, int64_t r) { return perm ? perm[r] : r; }
+
+__global__ void seg_softmax_fwd_kernel(const float* __restrict__ src, const int32_t* __restrict__ perm,
+                                       const int32_t* __restrict__ rowptr, int64_t G, int64_t H,
+                                       float* __restrict__ out) {
   const int64_t gid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (gid >= G * H) return;
   const int64_t g = gid / H, h = gid - g * H;
   const int64_t r0 = rowptr[g], r1 = rowptr[g + 1];
   float mx = -INFINITY;
-  for (int64_t r = r0; r < r1; ++r) mx = fmaxf(mx, src[r * H + h]);
+  for (int64_t r = r0; r < r1; ++r) mx = fmaxf(mx, src[seg_row(perm, r) * H + h]);
   float sum = 0.f;
-  for (int64_t r = r0; r < r1; ++r) sum += expf(src[r * H + h] - mx);
+  for (int64_t r = r0; r < r1; ++r) sum += expf(src[seg_row(perm, r) * H + h] - mx);
   const float den = sum + 1e-16f;
-  for (int64_t r = r0; r < r1; ++r) out[r * H + h] = expf(src[r * H + h] - mx) / den;
+  for (int64_t r = r0; r < r1; ++r) {
+    const int64_t i = seg_row(perm, r) * H + h;
+    out[i] = expf(src[i] - mx) / den;
+  }
 }
 
 __global__ void seg_softmax_bwd_kernel(const float* __restrict__ out, const float* __restrict__ dout,
-                                       const int32_t* __restrict__ rowptr, int64_t G, int64_t H,
-                                       float* __restrict__ dsrc) {
+                                       const int32_t* __restrict__ perm, const int32_t* __restrict__ rowptr,
+                                       int64_t G, int64_t H, float* __restrict__ dsrc) {
   const int64_t gid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (gid >= G * H) return;
   const int64_t g = gid / H, h = gid - g * H;
   const int64_t r0 = rowptr[g], r1 = rowptr[g + 1];
   float dot = 0.f;
-  for (int64_t r = r0; r < r1; ++r) dot = fmaf(out[r * H + h], dout[r * H + h], dot);
-  for (int64_t r = r0; r < r1; ++r) dsrc[r * H + h] = out[r * H + h] * (dout[r * H + h] - dot);
+  for (int64_t r = r0; r < r1; ++r) {
+    const int64_t i = seg_row(perm, r) * H + h;
+    dot = fmaf(out[i], dout[i], dot);
+  }
+  for (int64_t r = r0; r < r1; ++r) {
+    const int64_t i = seg_row(perm, r) * H + h;
+    dsrc[i] = out[i] * (dout[i] - dot);
+  }
 }
 
 // ------------------------------------------------------------------------------ graph LayerNorm
@@ -633,7 +773,7 @@ X2G_API int x2g_segment_softmax_fwd(const float* src, const int32_t* rowptr, int
                                     void* stream) {
   if (G < 0 || H <= 0 || (G > 0 && (!src || !rowptr || !out))) return X2G_EINVAL;
   if (G == 0) return X2G_OK;
-  seg_softmax_fwd_kernel<<<blocks_for(G * H, 256), 256, 0, as_stream(stream)>>>(src, rowptr, G, H, out);
+  seg_softmax_fwd_kernel<<<blocks_for(G * H, 256), 256, 0, as_stream(stream)>>>(src, nullptr, rowptr, G, H, out);
   return last_launch_status();
 }
 
@@ -641,7 +781,44 @@ X2G_API int x2g_segment_softmax_bwd(const float* out, const float* dout, const i
                                     int64_t H, float* dsrc, void* stream) {
   if (G < 0 || H <= 0 || (G > 0 && (!out || !dout || !rowptr || !dsrc))) return X2G_EINVAL;
   if (G == 0) return X2G_OK;
-  seg_softmax_bwd_kernel<<<blocks_for(G * H, 256), 256, 0, as_stream(stream)>>>(out, dout, rowptr, G, H, dsrc);
+  seg_softmax_bwd_kernel<<<blocks_for(G * H, 256), 256, 0, as_stream(stream)>>>(out, dout, nullptr, rowptr, G, H,
+                                                                                 dsrc);
+  return last_launch_status();
+}
+
+X2G_API int x2g_segment_reduce_perm(const float* x, const int32_t* perm, const int32_t* rowptr, int64_t G, int64_t D,
+                                    int mode, float* out, void* stream) {
+  if (G < 0 || D <= 0 || (mode != X2G_REDUCE_SUM && mode != X2G_REDUCE_MEAN)) return X2G_EINVAL;
+  if (G > 0 && (!rowptr || !out || !x || !perm)) return X2G_EINVAL;
+  if (G == 0) return X2G_OK;
+  hipStream_t st = as_stream(stream);
+  return mode == X2G_REDUCE_MEAN ? seg_perm_launch<true, false>(x, perm, rowptr, G, D, out, st)
+                                 : seg_perm_launch<false, false>(x, perm, rowptr, G, D, out, st);
+}
+
+X2G_API int x2g_segment_reduce_perm_bwd(const float* g, const int32_t* perm, const int32_t* rowptr, int64_t G,
+                                        int64_t D, int mode, float* out, void* stream) {
+  if (G < 0 || D <= 0 || (mode != X2G_REDUCE_SUM && mode != X2G_REDUCE_MEAN)) return X2G_EINVAL;
+  if (G > 0 && (!rowptr || !out || !g || !perm)) return X2G_EINVAL;
+  if (G == 0) return X2G_OK;
+  hipStream_t st = as_stream(stream);
+  return mode == X2G_REDUCE_MEAN ? seg_perm_launch<true, true>(g, perm, rowptr, G, D, out, st)
+                                 : seg_perm_launch<false, true>(g, perm, rowptr, G, D, out, st);
+}
+
+X2G_API int x2g_segment_softmax_perm_fwd(const float* src, const int32_t* perm, const int32_t* rowptr, int64_t G,
+                                         int64_t H, float* out, void* stream) {
+  if (G < 0 || H <= 0 || (G > 0 && (!src || !perm || !rowptr || !out))) return X2G_EINVAL;
+  if (G == 0) return X2G_OK;
+  seg_softmax_fwd_kernel<<<blocks_for(G * H, 256), 256, 0, as_stream(stream)>>>(src, perm, rowptr, G, H, out);
+  return last_launch_status();
+}
+
+X2G_API int x2g_segment_softmax_perm_bwd(const float* out, const float* dout, const int32_t* perm,
+                                         const int32_t* rowptr, int64_t G, int64_t H, float* dsrc, void* stream) {
+  if (G < 0 || H <= 0 || (G > 0 && (!out || !dout || !perm || !rowptr || !dsrc))) return X2G_EINVAL;
+  if (G == 0) return X2G_OK;
+  seg_softmax_bwd_kernel<<<blocks_for(G * H, 256), 256, 0, as_stream(stream)>>>(out, dout, perm, rowptr, G, H, dsrc);
   return last_launch_status();
 }
 

@@ -77,6 +77,11 @@ SIGNATURES = {
     "x2g_segment_broadcast": [_P, _P, _P, _I64, _I64, _P, _P],
     "x2g_segment_softmax_fwd": [_P, _P, _I64, _I64, _P, _P],
     "x2g_segment_softmax_bwd": [_P, _P, _P, _I64, _I64, _P, _P],
+    "x2g_csr_rowptr_checked": [_P, _I64, _I64, _P, _P, _P],
+    "x2g_segment_reduce_perm": [_P, _P, _P, _I64, _I64, ctypes.c_int, _P, _P],
+    "x2g_segment_reduce_perm_bwd": [_P, _P, _P, _I64, _I64, ctypes.c_int, _P, _P],
+    "x2g_segment_softmax_perm_fwd": [_P, _P, _P, _I64, _I64, _P, _P],
+    "x2g_segment_softmax_perm_bwd": [_P, _P, _P, _P, _I64, _I64, _P, _P],
     "x2g_graph_layernorm_fwd": [_P, _P, _I64, _I64, _F, _P, _P, _P, _P],
     "x2g_graph_layernorm_bwd": [_P, _P, _P, _P, _I64, _I64, _P, _P],
     "x2g_graph_layernorm_bwd_workspace": [_I64],

@@ -76,9 +76,11 @@ class Data:
 
 
 def _meta_from_tensors(data):
-    """Fallback when a Data was built without host metadata: derive it (one device->host copy)."""
+    """Host size metadata of a batch built without it (a Data made elsewhere, or a foreign PyG-style
+    Batch): per-molecule atoms / edges / triplets and whether the directed edge set is symmetric,
+    derived from the tensors (one device->host copy of edge_index and the small count vectors)."""
     ei = data.edge_index.detach().cpu().numpy()
-    n = data.num_nodes
+    n = int(data.x.shape[0])
     if "ptr" in data._store:
         ptr = data.ptr.detach().cpu().numpy()
         nodes = np.diff(ptr)
@@ -94,7 +96,8 @@ def _meta_from_tensors(data):
         trips.append(triplet_count(sub, int(nodes[m])))
         e0 += edges[m]
         a0 += nodes[m]
-    return {"nodes": nodes.astype(np.int64), "edges": edges, "triplets": np.array(trips, dtype=np.int64)}
+    return {"nodes": nodes.astype(np.int64), "edges": edges, "triplets": np.array(trips, dtype=np.int64),
+            "symmetric": _is_symmetric(ei, n)}
 
 
 class Batch(Data):

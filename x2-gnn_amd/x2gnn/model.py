@@ -15,8 +15,6 @@ instead of T (the reference's edge_attr rows are copies of those rows, xgnn.py:5
 """
 from __future__ import annotations
 
-import os
-
 import torch
 import torch.nn as nn
 from torch.nn import ModuleList, Sequential, SiLU
@@ -44,17 +42,6 @@ class LayerNorm(nn.Module):
             num_graphs = int(batch.max()) + 1
             rowptr = ops.csr_rowptr(batch, num_graphs)
         return ops.graph_layer_norm(x, rowptr, num_graphs, self.eps)
-
-
-_SIDE_STREAMS = {}
-
-
-def _side_stream(device):
-    """A second HIP stream per device for the readout branch (see _Trunk._layers)."""
-    s = _SIDE_STREAMS.get(device)
-    if s is None:
-        s = _SIDE_STREAMS[device] = torch.cuda.Stream(device=device)
-    return s
 
 
 def _plan_of(data, edge_index_0, atom_batch):
@@ -99,19 +86,14 @@ class _Trunk(nn.Module):
         edge_attr = run_mlp(self.edgenn, data.edge_attr) if edge_proj is None else None
         edge_row = data.edge_attr_row if per_dst else None
         out = data.x
-        # The readouts (reference model.py:41,50) hang off the layer chain.  With
-        # X2G_READOUT_STREAM=1 they run on a second stream (their backward follows), overlapping the
-        # next layer; off by default: the persistent one-workgroup-per-CU kernels of the main chain
-        # lose more to the shared CUs than the overlap gains (6.30 vs 6.00 ms/step measured).
-        # Results accumulate in layer order either way: deterministic.
-        use_side = out.is_cuda and os.environ.get("X2G_READOUT_STREAM", "0") == "1"
-        side = _side_stream(out.device) if use_side else None
-        main = torch.cuda.current_stream(out.device) if side is not None else None
+        # The readouts (reference model.py:41,50) hang off the layer chain; results accumulate in
+        # layer order (deterministic).  (Run on a second stream, overlapping the next layer, they
+        # measured slower: 6.30 vs 6.00 ms/step — the persistent one-workgroup-per-CU kernels of the
+        # main chain lose more to the shared CUs than the overlap gains; that path is gone.)
         results = None
         # Batched readout MLPs: collect every readout's MLP input, then one batched launch per MLP
         # layer for all readouts (ops.readout_mlps) instead of three launches per readout.
-        grouped = (out.is_cuda and side is None and feature_fn is not None
-                   and os.environ.get("X2G_GROUPED_READOUT", "1") == "1")
+        grouped = out.is_cuda and feature_fn is not None
         feats = []
         # the readouts' edge -> atom pools of every layer output as one launch each way (pool_fn,
         # ops.rbf_pool_batch) after the last layer; per readout where that is unsupported
@@ -125,15 +107,8 @@ class _Trunk(nn.Module):
             if grouped:
                 feats.append(feature_fn(i, x))
                 return
-            if side is None:
-                r = readout_fn(i, x)
-                results = r if results is None else results + r
-                return
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                r = readout_fn(i, x)
-                results = r if results is None else results + r
-            x.record_stream(side)
+            r = readout_fn(i, x)
+            results = r if results is None else results + r
 
         # gradient fan-in in place: the layer inputs and the radial basis feed several fused ops each
         fan = self._fan_in_ok(data, out)
@@ -156,9 +131,6 @@ class _Trunk(nn.Module):
             if fan:
                 out._x2g_fanin = ops.FanIn()
             readout(i + 1, out)
-        if side is not None:
-            main.wait_stream(side)
-            results.record_stream(main)
         if pooled_xs is not None:
             feats = pool_fn(pooled_xs)
             if feats is None:

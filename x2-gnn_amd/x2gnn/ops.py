@@ -19,7 +19,6 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
-import os
 
 import numpy as np
 import torch
@@ -76,6 +75,7 @@ class LineGraph:
         self.atom_k = torch.empty(self.T, **i32)
         self._src_rowptr = None
         self._src_perm = None
+        self.order_status = None  # built here in order: nothing to check
         ws_bytes = int(_lib.load().x2g_vertex_to_edge_workspace(self.E, self.N))
         self._ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         call("x2g_vertex_to_edge_sym" if self.symmetric else "x2g_vertex_to_edge", ptr(edge_src), ptr(edge_dst),
@@ -85,14 +85,17 @@ class LineGraph:
 
     @classmethod
     def from_triplets(cls, triplet_index, num_line_nodes: int):
-        """Wrap an existing triplet index [2, T] (row 1 sorted ascending, as vertex_to_edge_2 emits)."""
+        """Wrap an existing triplet index [2, T] whose row 1 is sorted ascending (as vertex_to_edge_2
+        emits it).  Nothing is read back: the order is checked on the device and a violation is
+        flagged in ``order_status`` (int32 [1]; see ``order_violated``), the row pointer staying in
+        range either way."""
         lg = cls.__new__(cls)
         lg.E, lg.N, lg.T = int(num_line_nodes), None, int(triplet_index.shape[1])
         lg.edge_src = lg.edge_dst = lg.atom_rowptr = None
         lg.atom_i = lg.atom_j = lg.atom_k = None
         lg.trip_src = _i32(triplet_index[0])
         lg.trip_dst = _i32(triplet_index[1])
-        lg.trip_rowptr = csr_rowptr(lg.trip_dst, lg.E)
+        lg.trip_rowptr, lg.order_status = csr_rowptr_checked(lg.trip_dst, lg.E)
         lg._src_rowptr = lg._src_perm = None
         lg.symmetric = False
         ws_bytes = int(_lib.load().x2g_vertex_to_edge_workspace(lg.E, 0))
@@ -113,6 +116,10 @@ class LineGraph:
                      ptr(self._src_perm), ptr(self._ws), self._ws.numel(), stream_ptr())
         return self._src_rowptr, self._src_perm
 
+    def order_violated(self) -> bool:
+        """True when the triplet destinations handed to ``from_triplets`` were not sorted (one sync)."""
+        return self.order_status is not None and bool(self.order_status.item())
+
     def triplet_index(self):
         """int64 [2, T] (row 0 = source line node id(b->k), row 1 = destination id(a->b))."""
         return torch.stack([self.trip_src.long(), self.trip_dst.long()])
@@ -132,6 +139,17 @@ def csr_rowptr(sorted_keys, num_segments: int):
     out = torch.empty(num_segments + 1, dtype=torch.int32, device=keys.device)
     call("x2g_csr_rowptr", ptr(keys), keys.numel(), num_segments, ptr(out), stream_ptr())
     return out
+
+
+def csr_rowptr_checked(keys, num_segments: int):
+    """(rowptr [num_segments + 1], status int32 [1]) for keys assumed sorted and in range: no host
+    read; status is 1 on the device when the assumption fails (x2g_csr_rowptr_checked)."""
+    _need_cuda(keys)
+    k = _i32(keys.reshape(-1))
+    out = torch.empty(num_segments + 1, dtype=torch.int32, device=k.device)
+    status = torch.empty(1, dtype=torch.int32, device=k.device)
+    call("x2g_csr_rowptr_checked", ptr(k), k.numel(), num_segments, ptr(out), ptr(status), stream_ptr())
+    return out, status
 
 
 # ---------------------------------------------------------------------------------- basis
@@ -174,7 +192,7 @@ class _EdgeBasis(torch.autograd.Function):
         dfreq = sink if sink is not None else torch.empty(R, dtype=torch.float32, device=dist.device)
         ws_bytes = int(lib.x2g_edge_basis_freq_grad_workspace(E, R))
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dist.device)
-        defer = sink is not None and _DEFER is not None and E > 0
+        defer = sink is not None and _defer() is not None and E > 0
         flags = (ACCUM_WGRAD if sink is not None else 0) | (DEFER_SLAB_SUM if defer else 0)
         call("x2g_edge_basis_freq_grad", ptr(_f32(grbf)), ptr(dist), ptr(env), ptr(freq), E, R, ctx.cutoff, ptr(dfreq),
              flags, ptr(ws), ws_bytes, stream_ptr())
@@ -227,19 +245,24 @@ def spherical_basis_from_angles(theta, trip_src, rbf_env, num_spherical: int = 7
 # ---------------------------------------------------------------------------------- attention
 # Graph LayerNorm after the conv (model.py:46) fused: the attention forward leaves per-row (mean, M2)
 # statistics (x2g_sbf_attention_fwd_stats) and the trunk's row chain normalises its input while
-# staging it (x2g_chain_fwd_ln) instead of a LayerNorm pass over the rows.  X2G_LN_FUSE=0: separate.
-_LN_FUSE = os.environ.get("X2G_LN_FUSE", "1") == "1"
+# staging it (x2g_chain_fwd_ln) instead of a LayerNorm pass over the rows.  False: separate.
+#
+# The module switches below (_LN_FUSE, _LN_BWD_ROWS, _SRC_G, _FOLD_SBF, _DEFER_KEYED, INFER_TILE,
+# _CHAIN, _FAN_IN, _POOL_BATCH) are constants, not environment reads: each exists because a parity
+# test flips it to check the fused path against the plain one (tests/test_gpu_model.py,
+# tests/test_gpu_kernels.py).  Paths that were measured slower and had no such test are deleted.
+_LN_FUSE = True
 # With the fused LayerNorm, its backward's per-molecule sums come from per-row sums the chain
-# backward leaves (x2g_chain_bwd_ln + x2g_graph_layernorm_bwd_rows): 0 = the two-pass LN backward.
-_LN_BWD_ROWS = os.environ.get("X2G_LN_BWD_ROWS", "1") == "1"
+# backward leaves (x2g_chain_bwd_ln + x2g_graph_layernorm_bwd_rows): False = the two-pass LN backward.
+_LN_BWD_ROWS = True
 # The folded source-major pass recomputes g_t = d loss / d a_t (per head) itself — bitwise the value
-# the destination pass computes — so g [T, H] is neither written nor read: 0 = the round trip.
-_SRC_G = os.environ.get("X2G_SRC_G", "1") == "1"
+# the destination pass computes — so g [T, H] is neither written nor read: False = the round trip.
+_SRC_G = True
 
-# Factorised lin_sbf backward (csrc/attention_fold.inc): X2G_FOLD_SBF=0 restores the two-pass
-# backward + [T, D] d_sbfproj + T-row weight GEMM (kept for the drop-in conv API, whose sbf is
-# an arbitrary [T, 42] tensor).
-_FOLD_SBF = os.environ.get("X2G_FOLD_SBF", "1") == "1"
+# Factorised lin_sbf backward (csrc/attention_fold.inc): False restores the two-pass backward +
+# [T, D] d_sbfproj + T-row weight GEMM (the drop-in conv API takes it anyway: its sbf is an
+# arbitrary [T, 42] tensor).
+_FOLD_SBF = True
 FOLD_BASIS = (7, 6)  # the (num_spherical, num_radial) the folded kernels are compiled for (sbf_dim 42)
 
 
@@ -258,7 +281,9 @@ class _SBFAttention(torch.autograd.Function):
     def forward(ctx, q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row, heads, channels):
         w_param, b_param = w_sbf, b_sbf
         # its gradient is read only by the table chain's backward, which flushes deferred sums first
-        ctx.defer_edge = _DEFER_KEYED and getattr(edge, "_x2g_table_out", False) and ctx.needs_input_grad[4]
+        pending = getattr(edge, "_x2g_keyed_pending", None)
+        ctx.defer_edge = _DEFER_KEYED and pending is not None and ctx.needs_input_grad[4]
+        ctx.keyed_pending = pending
         factors = _sbf_factors(lg, sbf, edge_mode, heads * channels, edge, edge_row)
         q, k, v, skip = _f32(q), _f32(k), _f32(v), _f32(skip)
         sbf, w_sbf, b_sbf = _f32(sbf), _f32(w_sbf), _f32(b_sbf)
@@ -358,7 +383,7 @@ class _SBFAttention(torch.autograd.Function):
             d_edge = None  # (written by the kernel; no consumer: the table's gradient is not wanted)
         elif mode == EDGE_PER_DST and ctx.edge_row is not None:
             if ctx.defer_edge:
-                d_edge = keyed_row_sum_deferred(d_edge, ctx.edge_row, ctx.edge_shape[0])
+                d_edge = keyed_row_sum_deferred(d_edge, ctx.edge_row, ctx.edge_shape[0], ctx.keyed_pending)
             else:
                 d_edge = keyed_row_sum(d_edge, ctx.edge_row, ctx.edge_shape[0])
         gw, gb = grad_sink(ctx.w_param), grad_sink(ctx.b_param)
@@ -381,35 +406,13 @@ def sbf_radial_wgrad(gfold, radial, dw_out=None, db_out=None):
     lib = _lib.load()
     ws_bytes = int(lib.x2g_sbf_radial_wgrad_workspace(E, D))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=gfold.device)
-    defer = accum and _DEFER is not None and E > 0
+    defer = accum and _defer() is not None and E > 0
     flags = (ACCUM_WGRAD if accum else 0) | (DEFER_SLAB_SUM if defer else 0)
     call("x2g_sbf_radial_wgrad", ptr(gfold), ptr(_f32(radial)), E, D, ptr(dw), ptr(db), flags, ptr(ws), ws_bytes,
          stream_ptr())
     if defer:
         _defer_job(ws, 0, int(lib.x2g_sbf_radial_wgrad_splits(E)), D * 42, D, dw, db)
     return (None, None) if accum else (dw, db)
-
-
-# Inference (grad mode off): nothing is saved for a backward, so the [T, D] projection S is not
-# worth materialising; the forward kernel projects each triplet's sbf row itself (W_sbf in
-# registers), reading 4*sbf_dim bytes per triplet instead of writing and re-reading 4*D.
-_INFER_FUSED = os.environ.get("X2G_INFER_SBF", "pre") == "fused"  # measured slower at config 5
-
-
-def _attention_fwd_fused(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row, heads, channels):
-    q, k, v, skip = _f32(q), _f32(k), _f32(v), _f32(skip)
-    sbf, w_sbf, b_sbf = _f32(sbf), _f32(w_sbf), _f32(b_sbf)
-    edge = _f32(edge) if edge is not None else None
-    E, T, D = q.shape[0], lg.T, heads * channels
-    f32 = dict(dtype=torch.float32, device=q.device)
-    out, alpha = torch.empty(E, D, **f32), torch.empty(T, heads, **f32)
-    smax, sden = torch.empty(E, heads, **f32), torch.empty(E, heads, **f32)
-    rstats = torch.empty(E, 2, **f32) if _LN_FUSE and D == 128 else None
-    call("x2g_sbf_attention_fwd_stats" if rstats is not None else "x2g_sbf_attention_fwd", ptr(q), ptr(k), ptr(v),
-         ptr(skip), ptr(edge), ptr(edge_row), edge_mode, ptr(sbf), ptr(w_sbf), ptr(b_sbf), ptr(lg.trip_rowptr),
-         ptr(lg.trip_src), E, T, heads, channels, sbf.shape[1], ptr(out), ptr(alpha), ptr(smax), ptr(sden),
-         *((ptr(rstats),) if rstats is not None else ()), stream_ptr())
-    return out, alpha, smax, sden, rstats
 
 
 class _EmbeddingTable(torch.autograd.Function):
@@ -494,7 +497,7 @@ class _ReadoutMLPs(torch.autograd.Function):
         h2 = [torch.empty(R, D, **f32) for _ in range(G)]
         z2 = [torch.empty(R, D, **f32) for _ in range(G)]
         st = stream_ptr()
-        ctx.chain = _READOUT_CHAIN and _readout_chain_ok(R, D, G, W1, B1, W2, B2)
+        ctx.chain = _readout_chain_ok(R, D, G, W1, B1, W2, B2)
         if ctx.chain:  # both hidden layers of every readout: one x2g_chain_fwd_batch launch
             grad = any(ctx.needs_input_grad)  # inference: no transposed weights, no T-layout inputs
             tf = int(_lib.load().x2g_chain_t_floats(R, D))
@@ -553,7 +556,7 @@ class _ReadoutMLPs(torch.autograd.Function):
                                   for g in range(G)])
         ws_bytes = int(lib.x2g_readout_head_bwd_workspace(R, D, G))
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-        defer = acc3 and _DEFER is not None
+        defer = acc3 and _defer() is not None
         call("x2g_readout_head_bwd", ptr(dout), heads, G, R, D, (ACCUM_WGRAD if acc3 else 0) |
              (DEFER_SLAB_SUM if defer else 0), ptr(ws), ws_bytes, st)
         if defer:
@@ -585,7 +588,7 @@ class _ReadoutMLPs(torch.autograd.Function):
                                                       _dp(dw[g]), _dp(db[g])) for g in range(G)])
             wsz = int(lib.x2g_dense_bwd_workspace(R, D, D))
             ws = torch.empty(max(wsz * G, 1), dtype=torch.uint8, device=dev)
-            defer = acc and _DEFER is not None
+            defer = acc and _defer() is not None
             call("x2g_dense_bwd_batched", grp, G, R, D, D, ACT_SILU, (ACCUM_WGRAD if acc else 0) |
                  (DEFER_SLAB_SUM if defer else 0), ptr(ws), wsz * G, st)
             if defer:
@@ -603,9 +606,8 @@ class _ReadoutMLPs(torch.autograd.Function):
         return (None, *dfeat, *pg)
 
 
-# the readouts' two hidden layers as one batched row-chain launch each way (x2g_chain_*_batch);
-# X2G_READOUT_CHAIN=0: two batched dense launches each way
-_READOUT_CHAIN = os.environ.get("X2G_READOUT_CHAIN", "1") == "1"
+# the readouts' two hidden layers as one batched row-chain launch each way (x2g_chain_*_batch) where
+# compiled; two batched dense launches each way otherwise
 CHAIN_MAX_JOBS = 8  # X2G_CHAIN_MAX_JOBS
 
 
@@ -692,32 +694,34 @@ def keyed_row_sum(src, key, num_keys: int):
 # Keyed row sums whose results are only read by the element-table chain's backward (every conv's
 # per-destination edge gradient -> its lin_edge table rows): queued here and run as ONE batched
 # launch (x2g_keyed_row_sum_batch) when _TableChainFn.backward starts, instead of a partial + a
-# slab-sum launch per layer.  X2G_DEFER_KEYED=0 sums each immediately.
-_DEFER_KEYED = os.environ.get("X2G_DEFER_KEYED", "1") == "1"
-_KEYED_PENDING = []
+# slab-sum launch per layer.  The queue belongs to the table chain's forward (one per model call,
+# ``table_chain``), not to the module: two models, threads or streams never share it.  False sums
+# each immediately.
+_DEFER_KEYED = True
 KEYED_MAX_JOBS = 8  # X2G_KEYED_MAX_JOBS
 
 
-def keyed_row_sum_deferred(src, key, num_keys: int):
-    """keyed_row_sum(src, key, num_keys) into a buffer filled by the next flush_keyed()."""
+def keyed_row_sum_deferred(src, key, num_keys: int, pending: list):
+    """keyed_row_sum(src, key, num_keys) into a buffer filled when ``pending`` (the table chain's
+    queue) is flushed by flush_keyed(pending)."""
     src = _f32(src)
     R, D = src.shape
     if R == 0 or num_keys > 16 or D % 4 or D > 256 or (D // 4) & (D // 4 - 1):
         return keyed_row_sum(src, key, num_keys)
     out = torch.empty(num_keys, D, dtype=torch.float32, device=src.device)
-    _KEYED_PENDING.append((src, _i32(key), int(num_keys), out))
+    pending.append((src, _i32(key), int(num_keys), out))
     return out
 
 
-def flush_keyed():
-    """Run every queued keyed row sum (one partial + one slab-sum launch per group of jobs that
-    share keys and shape)."""
-    if not _KEYED_PENDING:
+def flush_keyed(pending: list):
+    """Run every keyed row sum queued on ``pending`` (one partial + one slab-sum launch per group
+    of jobs that share keys and shape)."""
+    if not pending:
         return
-    pending = list(_KEYED_PENDING)
-    _KEYED_PENDING.clear()
+    items = list(pending)
+    pending.clear()
     groups = {}
-    for src, key, nk, out in pending:
+    for src, key, nk, out in items:
         groups.setdefault((key.data_ptr(), tuple(src.shape), nk), []).append((src, key, nk, out))
     lib = _lib.load()
     for (_, (R, D), nk), items in groups.items():
@@ -737,7 +741,7 @@ def flush_keyed():
 # whole, 256 MB per tile at the default).  Cost at config 5 (bench --workload aid_infer): 9.34 ms
 # per step whole, 9.74 tiled at 2^19 triplets, 10.75 at 2^17 (per-launch ramp and drain; projecting
 # the next tile on a side stream under the current attention measured no better).
-INFER_TILE = int(os.environ.get("X2G_INFER_TILE", str(1 << 19)))
+INFER_TILE = 1 << 19
 
 
 def _infer_tiles(lg, tmax):
@@ -754,7 +758,11 @@ def _infer_tiles(lg, tmax):
         ec, tc = counts
         ep = np.concatenate([[0], np.cumsum(ec)])
         rp = np.concatenate([[0], np.cumsum(tc)])
-    else:
+        # the host metadata must describe this line graph, or a tile could split a destination
+        # segment or run past E / T: otherwise take the row pointer itself (one read-back)
+        if ep[-1] != lg.E or rp[-1] != lg.T or (np.asarray(ec) < 0).any() or (np.asarray(tc) < 0).any():
+            counts = None
+    if counts is None:
         rp = lg.trip_rowptr.cpu().numpy().astype("int64")
         ep = np.arange(lg.E + 1, dtype=np.int64)
     n = len(rp) - 1
@@ -814,10 +822,7 @@ def sbf_attention(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg: LineGraph, heads: 
         edge_mode = EDGE_NONE
     if edge_row is not None:
         edge_row = _i32(edge_row)
-    if _INFER_FUSED and not torch.is_grad_enabled():
-        out, alpha, smax, sden, rstats = _attention_fwd_fused(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode,
-                                                              edge_row, heads, channels)
-    elif not torch.is_grad_enabled() and lg.T > INFER_TILE and q.shape[0] > 0:
+    if not torch.is_grad_enabled() and lg.T > INFER_TILE and q.shape[0] > 0:
         out, alpha, smax, sden, rstats = _attention_fwd_tiled(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode,
                                                               edge_row, heads, channels, INFER_TILE)
     else:
@@ -846,36 +851,49 @@ class SlabJob(ctypes.Structure):
 
 
 class _SlabDeferral:
+    """The state of one ``deferred_wgrad()`` context (one backward): the queued slab sums, the
+    workspaces they read, the T-layout weight-gradient jobs of the flat launch, and — after the
+    context exits — ``flat_launches``: (rows, [cols per job]) of each flat launch it made (bench.py's
+    roofline probe replays the largest)."""
+
     def __init__(self):
         self.jobs = []
         self.keep = []  # workspaces holding the partial slabs until the batched sum is enqueued
         self.tiled = {}  # rows -> [TiledJob]: T-layout weight gradients run as one launch at exit
+        self.flat_launches = []
+
+
+# Open deferrals by HIP stream: autograd runs each backward node on its forward's stream, so a
+# backward finds the context its caller opened on that stream, and two models stepping on two
+# streams (or threads) never see each other's queue.
+_DEFERRALS = {}
+
+
+def _defer():
+    """The deferral open on the current stream, or None."""
+    if not _DEFERRALS:
+        return None
+    return _DEFERRALS.get(torch.cuda.current_stream().cuda_stream)
 
 
 TILED_MAX_JOBS = 64  # X2G_TILED_MAX_JOBS
-# T-layout weight gradients inside deferred_wgrad(): 1 = queued and run as ONE x2g_tiled_wgrad_flat
-# launch at the end of the backward (operands kept alive until then), 0 = one launch per layer
-_FLAT_TILED = os.environ.get("X2G_FLAT_TILED", "1") == "1"
 
 
-def _queue_tiled(R, jobs, keep):
-    """Queue T-layout weight-gradient jobs (x2g_tiled_job, bucket-backed destinations) for the
-    deferred flat launch; ``keep``: tensors the jobs point into."""
-    _DEFER.tiled.setdefault(int(R), []).extend(jobs)
-    _DEFER.keep.extend(keep)
-
-
-FLAT_LAUNCHES = []  # (rows, [cols per job]) of the most recent deferred flush's flat launches (bench.py's probe)
+def _queue_tiled(d, R, jobs, keep):
+    """Queue T-layout weight-gradient jobs (x2g_tiled_job, bucket-backed destinations) on deferral
+    ``d`` for its flat launch; ``keep``: tensors the jobs point into."""
+    d.tiled.setdefault(int(R), []).extend(jobs)
+    d.keep.extend(keep)
 
 
 def _flush_tiled(d):
     lib = _lib.load()
-    FLAT_LAUNCHES.clear()
+    d.flat_launches.clear()
     for R, jobs in d.tiled.items():
         for j0 in range(0, len(jobs), TILED_MAX_JOBS):
             part = jobs[j0:j0 + TILED_MAX_JOBS]
             n = len(part)
-            FLAT_LAUNCHES.append((int(R), [int(j.cols) if j.ld > 0 else 128 for j in part]))
+            d.flat_launches.append((int(R), [int(j.cols) if j.ld > 0 else 128 for j in part]))
             ws_bytes = int(lib.x2g_tiled_wgrad_flat_workspace(R, 128, n))
             ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=torch.device("cuda", torch.cuda.current_device()))
             out = (SlabJob * n)()
@@ -886,42 +904,41 @@ def _flush_tiled(d):
     d.tiled = {}
 
 
-_DEFER = None
-
-
 @contextlib.contextmanager
 def deferred_wgrad():
-    """Within this context, weight gradients that go straight into a gradient bucket
-    (``grad_sink``) leave their per-workgroup partial slabs in place; on exit ONE
-    x2g_slab_sum_batch launch sums every layer's slabs (instead of one small launch per layer)."""
-    global _DEFER
-    prev, _DEFER = _DEFER, _SlabDeferral()
+    """Within this context (on the current stream), weight gradients that go straight into a
+    gradient bucket (``grad_sink``) leave their per-workgroup partial slabs in place and the
+    T-layout ones are queued; on exit ONE flat weight-gradient launch and ONE x2g_slab_sum_batch
+    launch finish every layer's (instead of small launches per layer).  Yields the deferral
+    (``flat_launches`` is filled on exit)."""
+    key = torch.cuda.current_stream().cuda_stream
+    prev = _DEFERRALS.get(key)
+    d = _DEFERRALS[key] = _SlabDeferral()
     try:
-        yield
-        d = _DEFER
+        yield d
         if d.tiled:
             _flush_tiled(d)
         if d.jobs:
             arr = (SlabJob * len(d.jobs))(*d.jobs)
             call("x2g_slab_sum_batch", ctypes.cast(arr, ctypes.c_void_p), len(d.jobs), 1, stream_ptr())
     finally:
-        _DEFER = prev
-        # keyed row sums queued for a table-chain backward that never ran (a partial backward:
-        # frozen embedding / edge tables, autograd.grad on a subset) are dropped here, not kept
-        # alive (and growing) until some later backward
-        _KEYED_PENDING.clear()
+        if prev is None:
+            _DEFERRALS.pop(key, None)
+        else:
+            _DEFERRALS[key] = prev
 
 
-def _defer_job(ws, offset, splits, n_w, n_b, dw, db, ld=0, cols=0, dw_ptr=None, db_ptr=None):
-    """Queue one slab reduction (x2g_slab_job); dw_ptr / db_ptr: raw destinations (a block of a
-    larger weight) instead of the tensors' own pointers."""
+def _defer_job(ws, offset, splits, n_w, n_b, dw, db, ld=0, cols=0, dw_ptr=None, db_ptr=None, d=None):
+    """Queue one slab reduction (x2g_slab_job) on the open deferral; dw_ptr / db_ptr: raw
+    destinations (a block of a larger weight) instead of the tensors' own pointers."""
+    d = d if d is not None else _defer()
     base = ws.data_ptr() + int(offset)
     has_b = db is not None or db_ptr is not None
     part_b = base + 4 * splits * n_w if has_b else None
-    _DEFER.jobs.append(SlabJob(base, part_b, dw_ptr if dw_ptr is not None else dw.data_ptr(),
-                               (db_ptr if db_ptr is not None else db.data_ptr()) if has_b else None, n_w,
-                               n_b if has_b else 0, splits, ld, cols))
-    _DEFER.keep.append(ws)
+    d.jobs.append(SlabJob(base, part_b, dw_ptr if dw_ptr is not None else dw.data_ptr(),
+                          (db_ptr if db_ptr is not None else db.data_ptr()) if has_b else None, n_w,
+                          n_b if has_b else 0, splits, ld, cols))
+    d.keep.append(ws)
 
 
 def grad_sink(param):
@@ -991,7 +1008,7 @@ def linear_wgrad(dy, x, bias=True, dw_out=None, db_out=None):
     db = (db_out if accum else torch.empty(O, dtype=torch.float32, device=dy.device)) if bias else None
     ws_bytes = int(_lib.load().x2g_linear_wgrad_workspace(R, O, I))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dy.device)
-    defer = accum and _DEFER is not None and R > 0
+    defer = accum and _defer() is not None and R > 0
     flags = (ACCUM_WGRAD if accum else 0) | (DEFER_SLAB_SUM if defer else 0)
     call("x2g_linear_wgrad_ex", ptr(dy), ptr(x), R, O, I, ptr(dw), ptr(db), flags, ptr(ws), ws_bytes, stream_ptr())
     if defer:
@@ -1035,7 +1052,7 @@ def _dense_bwd_raw(gy2, z, act, x2, w, w_param, b_param, has_bias, need_dx, dx_a
     lib = _lib.load()
     ws_bytes = int(lib.x2g_dense_bwd_workspace(R, K, N))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-    defer = accum and _DEFER is not None and R > 0
+    defer = accum and _defer() is not None and R > 0
     flags = (ACCUM_WGRAD if accum else 0) | (DEFER_SLAB_SUM if defer else 0)
     call("x2g_dense_bwd_ex", ptr(gy2), ptr(z), act, ptr(x2), ptr(w), R, K, N, ptr(dx), ptr(dx_add), ptr(dw), ptr(db),
          flags, ptr(ws), ws_bytes, stream_ptr())
@@ -1077,9 +1094,6 @@ class _DenseFn(torch.autograd.Function):
         return dx, dw, db, dres, None
 
 
-_FUSED_RESIDUAL = os.environ.get("X2G_FUSED_RESIDUAL", "1") == "1"
-
-
 class _ResidualFn(torch.autograd.Function):
     """ResidualLayer (residual_layer.py:21-27): y = x + SiLU(W1 SiLU(W0 x + b0) + b1), forward as
     two fused dense kernels; the backward's residual term is folded into the second data
@@ -1094,7 +1108,7 @@ class _ResidualFn(torch.autograd.Function):
         B0 = _f32(b0) if b0 is not None else None
         B1 = _f32(b1) if b1 is not None else None
         R = x2.shape[0]
-        if _FUSED_RESIDUAL and W0.shape == (D, D) and W1.shape == (D, D) and D % 4 == 0 and 8 < D <= 128:
+        if W0.shape == (D, D) and W1.shape == (D, D) and D % 4 == 0 and 8 < D <= 128:
             f32 = dict(dtype=torch.float32, device=x2.device)
             h, z0, z1, y = (torch.empty(R, D, **f32) for _ in range(4))
             call("x2g_residual_fwd", ptr(x2), ptr(W0), ptr(B0), ptr(W1), ptr(B1), R, D, ptr(h), ptr(z0), ptr(z1),
@@ -1161,7 +1175,7 @@ def wgrad_batched(dys, xs, weights, biases):
     ws_bytes = int(lib.x2g_wgrad_batched_workspace(R, D, G))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     jobs = (WgradJob * G)(*[WgradJob(_dp(dys[g]), _dp(xs[g]), _dp(dws[g]), _dp(dbs[g])) for g in range(G)])
-    defer = acc and _DEFER is not None
+    defer = acc and _defer() is not None
     call("x2g_wgrad_batched", jobs, G, R, D, (ACCUM_WGRAD if acc else 0) | (DEFER_SLAB_SUM if defer else 0), ptr(ws),
          ws_bytes, stream_ptr())
     if defer:
@@ -1185,9 +1199,10 @@ def chain_wgrad(in_t, dz_t, R, weights, biases):
     bufs, acc = _wgrad_targets(params, [tuple(p.shape) for p in params], dev)
     dws, rest = bufs[:n], iter(bufs[n:])
     dbs = [next(rest) if b is not None else None for b in biases]
-    if acc and _DEFER is not None and _FLAT_TILED:
+    d = _defer() if acc else None
+    if d is not None:
         tf = in_t.shape[1]
-        _queue_tiled(R, [TiledJob(dz_t.data_ptr() + 4 * g * tf, in_t.data_ptr() + 4 * g * tf, _dp(dws[g]), _dp(dbs[g]),
+        _queue_tiled(d, R, [TiledJob(dz_t.data_ptr() + 4 * g * tf, in_t.data_ptr() + 4 * g * tf, _dp(dws[g]), _dp(dbs[g]),
                                   0, 0) for g in range(n)], [in_t, dz_t])
         return [None] * n, [None] * n
     lib = _lib.load()
@@ -1195,14 +1210,8 @@ def chain_wgrad(in_t, dz_t, R, weights, biases):
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     dw_arr = (ctypes.c_void_p * n)(*[_dp(t) for t in dws])
     db_arr = (ctypes.c_void_p * n)(*[_dp(t) for t in dbs])
-    defer = acc and _DEFER is not None and _DEFER_TILED
-    call("x2g_chain_wgrad", ptr(in_t), ptr(dz_t), n, R, D, dw_arr, db_arr,
-         (ACCUM_WGRAD if acc else 0) | (DEFER_SLAB_SUM if defer else 0), ptr(ws), ws_bytes, stream_ptr())
-    if defer:
-        splits = int(lib.x2g_chain_wgrad_splits(R, D, n))
-        per = ws_bytes // n
-        for g in range(n):
-            _defer_job(ws, g * per, splits, D * D, D, dws[g], dbs[g])
+    call("x2g_chain_wgrad", ptr(in_t), ptr(dz_t), n, R, D, dw_arr, db_arr, ACCUM_WGRAD if acc else 0, ptr(ws),
+         ws_bytes, stream_ptr())
     if acc:
         return [None] * n, [None] * n
     return dws, dbs
@@ -1317,7 +1326,7 @@ def chain_supported(x, linears):
     return True
 
 
-_CHAIN = os.environ.get("X2G_CHAIN", "1") == "1"
+_CHAIN = True  # False: layer-by-layer dense kernels (tests/test_gpu_kernels.py flips it)
 
 
 def row_chain(x, res, linears, flags, ln=None):
@@ -1337,14 +1346,7 @@ def row_chain(x, res, linears, flags, ln=None):
 
 # ------------------------------------------------------------------------------ small-table chains
 TABLE_MAX_STAGES = 8  # X2G_TABLE_MAX_STAGES
-_TABLE_CHAIN = os.environ.get("X2G_TABLE_CHAIN", "1") == "1"
-# the table chain's backward with its leaf stages side by side (x2g_table_chain_bwd_ex): 0 = one workgroup
-_TABLE_PAR = os.environ.get("X2G_TABLE_PAR", "1") == "1"
-_FEATURIZE = os.environ.get("X2G_FEATURIZE", "1") == "1"
-_FAN_IN = os.environ.get("X2G_FAN_IN", "1") == "1"
-# T-layout weight gradients (chain / projections / featurisation): 1 = their slab sums join the one
-# deferred batch at the end of the backward, 0 = summed right after each launch (slabs still in MALL)
-_DEFER_TILED = os.environ.get("X2G_DEFER_TILED", "1") == "1"
+_FAN_IN = True  # False: autograd's own fan-in adds (test_fan_in_gradients_match_autograd_adds)
 
 
 class TableStage(ctypes.Structure):
@@ -1379,7 +1381,7 @@ class _TableChainFn(torch.autograd.Function):
     x (parent -1) or an earlier stage's output; one launch per direction for the whole tree."""
 
     @staticmethod
-    def forward(ctx, x, spec, *params):
+    def forward(ctx, x, spec, pending, *params):
         n = len(spec)
         x2 = _f32(x).contiguous()
         R, D = x2.shape
@@ -1393,14 +1395,13 @@ class _TableChainFn(torch.autograd.Function):
                                 for s in range(n)])
         call("x2g_table_chain_fwd", ptr(x2), R, D, st, n, stream_ptr())
         ctx.save_for_backward(x2, *ws, *ys, *zs)
-        ctx.spec = spec
-        ctx.params = params
+        ctx.spec, ctx.params, ctx.pending = spec, params, pending
         ctx.set_materialize_grads(False)
         return tuple(ys)
 
     @staticmethod
     def backward(ctx, *gys):
-        flush_keyed()  # the conv layers' deferred edge-table gradients (keyed_row_sum_deferred)
+        flush_keyed(ctx.pending)  # the conv layers' deferred edge-table gradients (keyed_row_sum_deferred)
         spec, n = ctx.spec, len(ctx.spec)
         saved = ctx.saved_tensors
         x2, ws, ys, zs = saved[0], saved[1:1 + n], saved[1 + n:1 + 2 * n], saved[1 + 2 * n:1 + 3 * n]
@@ -1425,14 +1426,11 @@ class _TableChainFn(torch.autograd.Function):
             stages.append(TableBwdStage(_dp(ws[s]), _dp(src), _dp(zs[s]), _dp(dys[s]), _dp(dw), _dp(db), par, act,
                                         1 if accum else 0))
         dx = torch.empty(R, D, dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None
-        if _TABLE_PAR:  # several leaves (the four lin_edge): leaf stages side by side, then the inner ones
-            wsb = int(_lib.load().x2g_table_chain_bwd_workspace(n))
-            ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
-            call("x2g_table_chain_bwd_ex", (TableBwdStage * n)(*stages), n, R, D, ptr(dx), ptr(ws), wsb,
-                 stream_ptr())
-        else:
-            call("x2g_table_chain_bwd", (TableBwdStage * n)(*stages), n, R, D, ptr(dx), stream_ptr())
-        return (dx, None, *grads)
+        # several leaves (the four lin_edge): leaf stages side by side, then the inner ones
+        wsb = int(_lib.load().x2g_table_chain_bwd_workspace(n))
+        ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+        call("x2g_table_chain_bwd_ex", (TableBwdStage * n)(*stages), n, R, D, ptr(dx), ptr(ws), wsb, stream_ptr())
+        return (dx, None, None, *grads)
 
 
 def table_chain(x, stages):
@@ -1441,9 +1439,10 @@ def table_chain(x, stages):
     for m, act, parent in stages:
         params += [m.weight, m.bias]
         spec.append((int(parent), int(act)))
-    outs = _TableChainFn.apply(x, tuple(spec), *params)
+    pending = []  # keyed row sums consumers queue for this chain's backward (keyed_row_sum_deferred)
+    outs = _TableChainFn.apply(x, tuple(spec), pending, *params)
     for o in outs:
-        o._x2g_table_out = True  # consumers may defer work on its gradient to this chain's backward
+        o._x2g_keyed_pending = pending
     return outs
 
 
@@ -1522,21 +1521,15 @@ class _FeaturizeFn(torch.autograd.Function):
             specs.append((dz2_t.data_ptr(), y1_t.data_ptr() + fb * i * tf, dw2.data_ptr() + fb * i * 128,
                           db2.data_ptr() if (db2 is not None and i == 0) else None, 256, 128))
         n = len(specs)
-        if acc and _DEFER is not None and _FLAT_TILED:
-            _queue_tiled(R, [TiledJob(*sp) for sp in specs], [dz1_t, dz2_t, xs_t, y1_t])
+        d = _defer() if acc else None
+        if d is not None:
+            _queue_tiled(d, R, [TiledJob(*sp) for sp in specs], [dz1_t, dz2_t, xs_t, y1_t])
             return None, None, None, None, None, None
         lib = _lib.load()
         ws_bytes = int(lib.x2g_tiled_wgrad_workspace(R, 128, n))
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
         jobs = (TiledJob * n)(*[TiledJob(*sp) for sp in specs])
-        defer = acc and _DEFER is not None and _DEFER_TILED
-        call("x2g_tiled_wgrad", jobs, n, R, 128, (ACCUM_WGRAD if acc else 0) | (DEFER_SLAB_SUM if defer else 0),
-             ptr(ws), ws_bytes, stream_ptr())
-        if defer:
-            splits = int(lib.x2g_tiled_wgrad_splits(R, 128, n))
-            per = ws_bytes // n
-            for g, (_, _, dwp, dbp, ld, cols) in enumerate(specs):
-                _defer_job(ws, g * per, splits, 128 * 128, 128, None, None, ld=ld, cols=cols, dw_ptr=dwp, db_ptr=dbp)
+        call("x2g_tiled_wgrad", jobs, n, R, 128, ACCUM_WGRAD if acc else 0, ptr(ws), ws_bytes, stream_ptr())
         if acc:
             return None, None, None, None, None, None
         return None, None, dw1, db1, dw2, db2
@@ -1574,22 +1567,16 @@ def tiled_wgrad(dy_ts, x_ts, R, weights, biases):
     bufs, acc = _wgrad_targets(params, [tuple(p.shape) for p in params], dev)
     dws, rest = bufs[:n], iter(bufs[n:])
     dbs = [next(rest) if b is not None else None for b in biases]
-    if acc and _DEFER is not None and _FLAT_TILED:
-        _queue_tiled(R, [TiledJob(_dp(dy_ts[g]), _dp(x_ts[g]), _dp(dws[g]), _dp(dbs[g]), 0, 0) for g in range(n)],
+    d = _defer() if acc else None
+    if d is not None:
+        _queue_tiled(d, R, [TiledJob(_dp(dy_ts[g]), _dp(x_ts[g]), _dp(dws[g]), _dp(dbs[g]), 0, 0) for g in range(n)],
                      list(dy_ts) + list(x_ts))
         return [None] * n, [None] * n
     lib = _lib.load()
     ws_bytes = int(lib.x2g_tiled_wgrad_workspace(R, D, n))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     jobs = (TiledJob * n)(*[TiledJob(_dp(dy_ts[g]), _dp(x_ts[g]), _dp(dws[g]), _dp(dbs[g])) for g in range(n)])
-    defer = acc and _DEFER is not None and _DEFER_TILED
-    call("x2g_tiled_wgrad", jobs, n, R, D, (ACCUM_WGRAD if acc else 0) | (DEFER_SLAB_SUM if defer else 0), ptr(ws),
-         ws_bytes, stream_ptr())
-    if defer:
-        splits = int(lib.x2g_tiled_wgrad_splits(R, D, n))
-        per = ws_bytes // n
-        for g in range(n):
-            _defer_job(ws, g * per, splits, D * D, D, dws[g], dbs[g])
+    call("x2g_tiled_wgrad", jobs, n, R, D, ACCUM_WGRAD if acc else 0, ptr(ws), ws_bytes, stream_ptr())
     if acc:
         return [None] * n, [None] * n
     return dws, dbs
@@ -1607,9 +1594,6 @@ def conv_proj_fused_supported(x, rbf, weights, biases):
     return all(b is None or b.data_ptr() % 16 == 0 for b in biases)
 
 
-_PROJ_GATE = os.environ.get("X2G_PROJ_GATE", "1") == "1"
-
-
 def _conv_proj_bwd_gate(grads, x2, rbf2, Wr, wr, dx, first_x, need_rbf, drbf_out, first_r):
     """x2g_conv_proj_bwd_gate: dx (in place, += when not first_x), drbf, dW_rbf of the projections'
     backward in one launch; returns (dx, drbf, dW_rbf) with None where the gradient went into a
@@ -1625,7 +1609,7 @@ def _conv_proj_bwd_gate(grads, x2, rbf2, Wr, wr, dx, first_x, need_rbf, drbf_out
     lib = _lib.load()
     ws_bytes = int(lib.x2g_conv_proj_bwd_gate_workspace(E, RR))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-    defer = accum and _DEFER is not None and E > 0
+    defer = accum and _defer() is not None and E > 0
     flags = ((ACCUM_WGRAD if accum else 0) | (DEFER_SLAB_SUM if defer else 0)
              | (GATE_DRBF_ACCUM if (need_rbf and not first_r) else 0))
     call("x2g_conv_proj_bwd_gate", grads, E, D, ptr(x2), ptr(rbf2), RR, ptr(Wr), ptr(dx),
@@ -1686,13 +1670,8 @@ class _ConvProjFusedFn(torch.autograd.Function):
         drbf_out = None
         if need_rbf and ctx.fan_r is not None:
             drbf_out, first_r = ctx.fan_r.take(rbf2.shape, x2.device)
-        if _PROJ_GATE:  # the gate's backward inside the projection kernel: dxs stays in registers
-            gx, grbf, dwr = _conv_proj_bwd_gate(grads, x2, rbf2, Wr, wr, dx, first_x, need_rbf, drbf_out, first_r)
-        else:
-            dxs = torch.empty(E, D, **f32)
-            call("x2g_conv_proj_bwd", grads, E, D, ptr(dx), None if first_x else ptr(dx), ptr(dxs), stream_ptr())
-            gx, grbf, dwr, _ = _gate_bwd(dxs, None, x2, rbf2, Wr, None, wr, None, True, need_rbf, dx_add=dx,
-                                         dx_out=dx, drbf_out=drbf_out, drbf_acc=not first_r)
+        # the gate's backward inside the projection kernel: dxs stays in registers
+        gx, grbf, dwr = _conv_proj_bwd_gate(grads, x2, rbf2, Wr, wr, dx, first_x, need_rbf, drbf_out, first_r)
         gx = gx if first_x else None
         grbf = grbf if first_r else None
         dws, dbs = tiled_wgrad([g_t[0], g_t[1], g_t[2], g_t[3]], [x_t, xs_t, xs_t, x_t], E, [wq, wk, wv, ws],
@@ -1791,7 +1770,7 @@ def _gate_bwd(g, owner, x, rbf, w, b, w_param, b_param, need_dx, need_rbf, dx_ad
     lib = _lib.load()
     ws_bytes = int(lib.x2g_rbf_gate_bwd_workspace(rows, D, R))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-    defer = accum and _DEFER is not None and rows > 0
+    defer = accum and _defer() is not None and rows > 0
     flags = (ACCUM_WGRAD if accum else 0) | (DEFER_SLAB_SUM if defer else 0) | (GATE_DRBF_ACCUM if drbf_acc else 0)
     call("x2g_rbf_gate_bwd", ptr(g), ptr(owner), ptr(x), ptr(rbf), ptr(w), ptr(b), rows, D, R, ptr(dx), ptr(dx_add),
          ptr(drbf), ptr(dw), ptr(db), flags, ptr(ws), ws_bytes, stream_ptr())
@@ -1848,7 +1827,7 @@ class GateJob(ctypes.Structure):
 
 GATE_MAX_JOBS = 8  # X2G_GATE_MAX_JOBS
 # the readouts' edge -> atom pools as one launch each way (x2g_rbf_pool_fwd_batch / _gate_bwd_batch)
-_POOL_BATCH = os.environ.get("X2G_POOL_BATCH", "1") == "1"
+_POOL_BATCH = True
 
 
 class _RbfPoolBatchFn(torch.autograd.Function):
@@ -1917,14 +1896,15 @@ class _RbfPoolBatchFn(torch.autograd.Function):
         lib = _lib.load()
         ws_bytes = int(lib.x2g_rbf_gate_bwd_batch_workspace(rows, D, R, n))
         wsb = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-        defer = accum and _DEFER is not None
+        d = _defer() if accum else None
+        defer = d is not None
         flags = (ACCUM_WGRAD if accum else 0) | (DEFER_SLAB_SUM if defer else 0) | (0 if first_r else GATE_DRBF_ACCUM)
         out = (SlabJob * n)()
         call("x2g_rbf_gate_bwd_batch", (GateJob * n)(*jobs), n, ptr(ctx.owner), ptr(rbf2), rows, D, R, ptr(drbf), flags,
              out, ptr(wsb), ws_bytes, stream_ptr())
         if defer:
-            _DEFER.jobs.extend(out)
-            _DEFER.keep.append(wsb)
+            d.jobs.extend(out)
+            d.keep.append(wsb)
         dws = [None if accum else gw for _, gw, _ in sinks]
         dbs = [None if accum else gb for _, _, gb in sinks]
         return (None, drbf if (need_r and first_r) else None, None, None, None, *dx_ret, *dws, *dbs)
@@ -2013,18 +1993,70 @@ def segment_sum(x, rowptr, num_segments: int, mul=None):
     return out.squeeze(1) if squeeze else out
 
 
+class IndexPlan:
+    """A scatter index in any order, prepared on the device without a host read: ``perm`` is the
+    stable sort of the keys (sorted position -> source row; equal keys keep the caller's order) and
+    ``rowptr`` the CSR row pointer of the sorted keys.  Rows whose key lies outside [0, dim_size)
+    belong to no segment (torch_scatter raises for them).  Build once, reuse for every operator
+    over the same index (as MessagePassing reuses edge_index[1])."""
+
+    def __init__(self, index, dim_size: int):
+        _need_cuda(index)
+        idx = _i32(index.reshape(-1))
+        self.n, self.dim_size = int(idx.numel()), int(dim_size)
+        keys, perm = torch.sort(idx, stable=True)
+        self.perm = _i32(perm)
+        self.rowptr, _ = csr_rowptr_checked(keys, self.dim_size)
+
+
+REDUCE_SUM, REDUCE_MEAN = 0, 1  # X2G_REDUCE_*
+
+
+class _ScatterReduce(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, src, plan, mode):
+        x = _f32(src)
+        out = torch.empty(plan.dim_size, x.shape[1], dtype=torch.float32, device=x.device)
+        call("x2g_segment_reduce_perm", ptr(x), ptr(plan.perm), ptr(plan.rowptr), plan.dim_size, x.shape[1], mode,
+             ptr(out), stream_ptr())
+        ctx.plan, ctx.mode, ctx.rows = plan, mode, x.shape[0]
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _f32(g)
+        plan = ctx.plan
+        dx = torch.zeros(ctx.rows, g.shape[1], dtype=torch.float32, device=g.device)
+        call("x2g_segment_reduce_perm_bwd", ptr(g), ptr(plan.perm), ptr(plan.rowptr), plan.dim_size, g.shape[1],
+             ctx.mode, ptr(dx), stream_ptr())
+        return dx, None, None
+
+
+def _scatter(src, index, dim_size, mode):
+    _need_cuda(src, index)
+    if src.shape[0] != index.numel():
+        raise ValueError("scatter: index must hold one key per row of src (dim=0)")
+    plan = index if isinstance(index, IndexPlan) else IndexPlan(index, int(dim_size))
+    squeeze = src.dim() == 1
+    x = src.unsqueeze(1) if squeeze else src.reshape(src.shape[0], -1)
+    out = _ScatterReduce.apply(x, plan, mode)
+    return out.squeeze(1) if squeeze else out.view(plan.dim_size, *src.shape[1:])
+
+
 def scatter_add(src, index, dim_size: int):
     """torch_scatter.scatter_add(src, index, dim=0, dim_size=dim_size) (readout.py:37, model.py:53)
-    for ANY index order: a sorted index is reduced in place through the CSR segment sum; an
-    unsorted one is stably sorted first (its rows gathered in that order), so the per-segment
-    summation order is the caller's row order either way (deterministic, no float atomics)."""
-    _need_cuda(src, index)
-    idx = index.reshape(-1)
-    if idx.numel() > 1 and bool((idx[1:] < idx[:-1]).any()):
-        perm = torch.argsort(idx, stable=True)
-        idx = idx.index_select(0, perm)
-        src = src.index_select(0, perm)
-    return segment_sum(src, csr_rowptr(idx, int(dim_size)), int(dim_size))
+    for ANY index order (or a prebuilt ``IndexPlan``), with no host read (HIP-graph capturable):
+    the keys are stably sorted on the device and the segment sum reads src's rows through the
+    permutation (x2g_segment_reduce_perm), so each segment is summed in the caller's row order —
+    deterministic, no float atomics."""
+    return _scatter(src, index, dim_size, REDUCE_SUM)
+
+
+def scatter_mean(src, index, dim_size: int):
+    """torch_scatter.scatter_mean(src, index, dim=0, dim_size=dim_size) (readout.py:69, MolWise's
+    pool_option='mean'): the segment sum divided by max(count, 1), empty segments 0; any index order,
+    no host read."""
+    return _scatter(src, index, dim_size, REDUCE_MEAN)
 
 
 class _SegmentSoftmax(torch.autograd.Function):
@@ -2052,6 +2084,47 @@ def segment_softmax(src, rowptr, num_segments: int):
     squeeze = src.dim() == 1
     s = src.unsqueeze(1) if squeeze else src
     out = _SegmentSoftmax.apply(s, _i32(rowptr), int(num_segments))
+    return out.squeeze(1) if squeeze else out
+
+
+class _SoftmaxPerm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, src, plan):
+        x = _f32(src)
+        out = torch.empty_like(x)
+        call("x2g_segment_softmax_perm_fwd", ptr(x), ptr(plan.perm), ptr(plan.rowptr), plan.dim_size, x.shape[1],
+             ptr(out), stream_ptr())
+        ctx.save_for_backward(out)
+        ctx.plan = plan
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (out,) = ctx.saved_tensors
+        plan = ctx.plan
+        ds = torch.zeros_like(out)
+        call("x2g_segment_softmax_perm_bwd", ptr(out), ptr(_f32(g)), ptr(plan.perm), ptr(plan.rowptr), plan.dim_size,
+             out.shape[1], ptr(ds), stream_ptr())
+        return ds, None
+
+
+def softmax(src, index=None, ptr=None, num_nodes=None):
+    """torch_geometric.utils.softmax(src, index, ptr, num_nodes) along dim 0
+    (sbftransformer_conv.py:151): exp(src - max) / (sum + 1e-16) per group of rows sharing a key.
+    ``index`` in any order (or an ``IndexPlan``), or a CSR ``ptr`` of contiguous groups.  With
+    neither ``num_nodes`` nor an IndexPlan the group count is ``int(index.max()) + 1`` (a host read,
+    as PyG's maybe_num_nodes makes); otherwise nothing is read back."""
+    if ptr is not None:
+        return segment_softmax(src, ptr, int(ptr.numel()) - 1)
+    if index is None:
+        raise ValueError("softmax needs index or ptr")
+    if not isinstance(index, IndexPlan):
+        _need_cuda(src, index)
+        n = int(num_nodes) if num_nodes is not None else (int(index.max()) + 1 if index.numel() else 0)
+        index = IndexPlan(index, n)
+    squeeze = src.dim() == 1
+    s = src.unsqueeze(1) if squeeze else src
+    out = _SoftmaxPerm.apply(s, index)
     return out.squeeze(1) if squeeze else out
 
 

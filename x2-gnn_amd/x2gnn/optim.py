@@ -15,6 +15,7 @@ from ._lib import call, ptr, stream_ptr
 from .dist import GradBucket, flat_layout
 
 _LR, _B1, _B2, _EPS, _MAXN, _EMAD, _STEP, _NORM, _CLIP = range(9)
+_WARMUP, _DECAY_STEPS, _DECAY_RATE, _BASE_LR, _STAIRCASE = range(11, 16)
 
 
 class FlatAdam:
@@ -55,7 +56,28 @@ class FlatAdam:
              self.ws_bytes, stream_ptr())
 
     def set_lr(self, lr):
+        """A fixed learning rate from the next step on (clears a schedule; e.g. for a host-side
+        ReduceLROnPlateau, train_ema.py:52-53)."""
+        self.scalars[_WARMUP] = 0.0
         self.scalars[_LR] = lr
+
+    def set_schedule(self, warmup_steps, decay_steps, decay_rate, staircase=False, base_lr=None):
+        """LinearWarmupExponentialDecay (scheduler.py:4-31; train_ema.py:50-51) evaluated on the device
+        from the step count at every update, so captured HIP graphs follow it: update t (0-based)
+        uses base_lr * min(1/W + t/W, 1) * decay_rate^(t / decay_steps), as the reference's
+        LambdaLR gives optimizer.step() when scheduler.step() follows every batch (trainer.py:47)."""
+        if decay_rate > 1:
+            raise ValueError("decay_rate must be <= 1 (scheduler.py:16)")
+        base = float(self.scalars[_LR]) if base_lr is None and float(self.scalars[_WARMUP]) <= 0 else base_lr
+        base = float(self.scalars[_BASE_LR]) if base is None else float(base)
+        vals = torch.tensor([max(int(warmup_steps), 1), float(decay_steps), float(decay_rate), base,
+                             1.0 if staircase else 0.0], dtype=torch.float32)
+        self.scalars[_WARMUP:_STAIRCASE + 1] = vals.to(self.scalars.device)
+
+    @property
+    def lr(self):
+        """The learning rate the last update used (device scalar)."""
+        return self.scalars[_LR]
 
     @property
     def grad_norm(self):

@@ -9,12 +9,11 @@ read (and can be captured in a HIP graph).
 from __future__ import annotations
 
 import numpy as np
-import os
-
 import torch
 import torch.nn.functional as F
 
 from . import ops
+from .data import _meta_from_tensors
 
 
 class GraphPlan:
@@ -34,12 +33,26 @@ class GraphPlan:
         self.lg = None
         self.atom_rowptr = self.line_ptr = self.mol_ptr = self.dst_type = None
         self.num_atoms = self.num_lines = self.num_triplets = self.num_graphs = self.out_graphs = 0
+        # int32 [1] device flags of the index contracts checked without a host read (from_line_data)
+        self.order_status = []
+
+    def order_violated(self) -> bool:
+        """True when an index this plan assumed sorted was not (reads the device flags: one sync;
+        call it where a check is wanted, e.g. in tests or after a run)."""
+        return any(bool(s.item()) for s in self.order_status)
 
     # ------------------------------------------------------------------ from an atom batch
     @classmethod
     def from_atom_batch(cls, data):
-        """Plan for ``xgnn_poly.forward(data)`` inputs (edge_index sorted by (src, dst))."""
-        meta = data.host_meta()
+        """Plan for ``xgnn_poly.forward(data)`` inputs (edge_index sorted by (src, dst)).
+
+        ``data`` is x2gnn's collated Batch (host size metadata and the int32 index forms ride
+        along) or any PyG-style batch exposing the keys xgnn.py:38-75 reads (``_store``, ``x``,
+        ``edge_index``, ``edge_num``, ``ptr`` / ``batch``): for a foreign batch the per-molecule
+        sizes are derived from its tensors here (one device->host copy of edge_index, as the
+        reference's own CPU triplet builder makes, xgnn.py:52-53)."""
+        host_meta = getattr(data, "host_meta", None)
+        meta = host_meta() if callable(host_meta) else _meta_from_tensors(data)
         p = cls()
         nodes, edges, trips = meta["nodes"], meta["edges"], meta["triplets"]
         p.num_atoms, p.num_lines, p.num_triplets = int(nodes.sum()), int(edges.sum()), int(trips.sum())
@@ -50,12 +63,12 @@ class GraphPlan:
         ei = data.edge_index
         dev = ei.device
         st = data._store
-        if _HOST_INDICES and "_x2g_edge_src" in st and st["_x2g_edge_src"].device == dev:  # int32 forms (collate)
+        if "_x2g_edge_src" in st and st["_x2g_edge_src"].device == dev:  # int32 forms (collate)
             p.lg = ops.LineGraph(st["_x2g_edge_src"], st["_x2g_edge_dst"], p.num_atoms, p.num_triplets,
                                  st.get("_x2g_symmetric", False))
             p.line_ptr, p.mol_ptr, p.dst_type = st["_x2g_line_ptr"], st["_x2g_mol_ptr"], st["_x2g_dst_type"]
         else:
-            p.lg = ops.vertex_to_edge(ei, p.num_atoms, p.num_triplets)
+            p.lg = ops.vertex_to_edge(ei, p.num_atoms, p.num_triplets, meta.get("symmetric", False))
             p.line_ptr = _ptr_from_counts(data.edge_num, p.num_graphs, dev)
             if "ptr" in st:
                 p.mol_ptr = ops._i32(data.ptr)
@@ -73,27 +86,26 @@ class GraphPlan:
     def from_line_data(cls, data, edge_index_0, atom_batch):
         """Plan for the drop-in ``SBFTransformer.forward(data, edge_index_0, atom_batch)`` API.
 
-        Sizes are read back from the device here (as the reference does with
-        ``int(batch.max())``); the fast path through ``xgnn_poly`` never takes this branch.
+        The molecule count is read back from the device (``int(batch.max()) + 1``, as the reference
+        does at model.py:53 and inside PyG's LayerNorm); nothing else is.  The four index vectors
+        must be sorted ascending, as the reference produces them (vertex_to_edge_2 emits triplets
+        by destination; PyG batches are ordered by molecule; edge_index is source-sorted): their row
+        pointers come from ``ops.csr_rowptr_checked``, which flags a violation on the device
+        (``order_violated()``) instead of syncing per call.  The fast path through ``xgnn_poly``
+        never takes this branch.
         """
         p = cls()
         p.num_lines = int(data.x.shape[0])
         p.num_atoms = int(atom_batch.shape[0])
         p.num_triplets = int(data.edge_index.shape[1])
-        _require_sorted(data.edge_index[1], "line-graph edge_index[1] (triplet destinations)")
-        _require_sorted(edge_index_0, "edge_index_0 (source atom of each line node)")
         p.lg = ops.LineGraph.from_triplets(data.edge_index, p.num_lines)
-        p.atom_rowptr = ops.csr_rowptr(edge_index_0, p.num_atoms)
+        p.atom_rowptr, st_a = ops.csr_rowptr_checked(edge_index_0, p.num_atoms)
         b = data.batch
         p.num_graphs = p.out_graphs = int(b.max()) + 1 if b.numel() else 0
-        _require_sorted(b, "line-graph batch")
-        _require_sorted(atom_batch, "atom_batch")
-        p.line_ptr = ops.csr_rowptr(b, p.num_graphs)
-        p.mol_ptr = ops.csr_rowptr(atom_batch, p.num_graphs)
+        p.line_ptr, st_l = ops.csr_rowptr_checked(b, p.num_graphs)
+        p.mol_ptr, st_m = ops.csr_rowptr_checked(atom_batch, p.num_graphs)
+        p.order_status = [p.lg.order_status, st_a, st_l, st_m]
         return p
-
-
-_HOST_INDICES = os.environ.get("X2G_HOST_INDICES", "1") == "1"
 
 
 def _ptr_from_counts(counts, n, device):
@@ -103,7 +115,3 @@ def _ptr_from_counts(counts, n, device):
         c = torch.full((1,), int(counts), device=device, dtype=torch.int64)
     return F.pad(torch.cumsum(c, 0), (1, 0)).to(torch.int32)
 
-
-def _require_sorted(idx, what):
-    if idx.numel() > 1 and bool((idx[1:] < idx[:-1]).any()):
-        raise ValueError(f"{what} must be sorted ascending (the order the reference produces)")

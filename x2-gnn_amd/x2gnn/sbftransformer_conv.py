@@ -16,9 +16,12 @@ everything else per triplet (gathers, logits, softmax, the weighted sum, the ski
 one destination-major kernel (``ops.sbf_attention``); the backward folds lin_sbf's gradient per
 source line node instead of writing a [T, H*C] gradient (csrc/attention_fold.inc).
 
-Triplets may come in any order (PyG's ``propagate`` accepts any): an ``edge_index[1]`` that is
-not sorted is sorted here (stable) and the per-triplet inputs permuted alike; the attention
-weights, when requested, are returned in the caller's order.
+Triplets may come in any order (PyG's ``propagate`` accepts any).  By default the destinations
+are stably sorted on the device and the per-triplet inputs permuted alike — no host read, so the
+call is HIP-graph capturable; the attention weights, when requested, come back in the caller's
+order.  ``assume_sorted=True`` (the order vertex_to_edge_2 emits, edge_graph.py:12-30) skips the
+sort and its gathers; the order is then checked on the device and a violation is flagged on the
+line graph (``LineGraph.order_violated()``), never an out-of-range access.
 
 Extra keyword-only arguments for the in-framework fast path:
 ``line_graph`` (a prebuilt ``ops.LineGraph``), ``edge_row`` (when ``edge_attr`` is a small
@@ -62,7 +65,8 @@ class SBFTransformerConv(nn.Module):
         self._alpha = None
 
     def forward(self, sbf, rbf, x, edge_index, edge_attr=None, return_attention_weights=None, *,
-                line_graph: Optional[ops.LineGraph] = None, edge_row=None, edge_proj=None):
+                line_graph: Optional[ops.LineGraph] = None, edge_row=None, edge_proj=None,
+                assume_sorted: bool = False):
         H, C = self.heads, self.out_channels
         if self.training and self.dropout > 0:
             raise NotImplementedError("attention dropout is not compiled (X2-GNN uses dropout=0)")
@@ -81,9 +85,9 @@ class SBFTransformerConv(nn.Module):
         perm = None
         if line_graph is None:
             dst = edge_index[1]
-            if dst.numel() > 1 and bool((dst[1:] < dst[:-1]).any()):
-                # CSR by destination needs dst-sorted triplets (vertex_to_edge_2 emits them so; any
-                # other caller order is sorted here, stable, and the per-triplet inputs follow)
+            if not assume_sorted and dst.numel() > 1:
+                # CSR by destination needs dst-sorted triplets: stable device sort, the per-triplet
+                # inputs follow (identity for an already sorted index; no host read either way)
                 perm = torch.argsort(dst, stable=True)
                 edge_index = edge_index.index_select(1, perm)
                 sbf = sbf.index_select(0, perm)

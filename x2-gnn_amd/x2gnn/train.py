@@ -3,7 +3,9 @@ multi-rank (molecule-sharded data parallelism, x2gnn.dist).
 
 ``Trainer.step(batch)`` = forward (xgnn_poly.forward) + smooth-L1 loss (trainer.py:41) +
 backward (trainer.py:42) into one flat gradient bucket + the gradient / loss all-reduce
-(N > 1; §8(e) of SURVEY.md) + clip_grad_norm_(100) + Adam + EMA (trainer.py:44-48).
+(N > 1; §8(e) of SURVEY.md) + clip_grad_norm_(100) + Adam + EMA (trainer.py:44-48), with the
+reference's per-batch LinearWarmupExponentialDecay (scheduler.py, trainer.py:47) when
+``lr_schedule`` is given (evaluated on the device, so captured replays follow it).
 ``capture()`` records the step as two HIP graphs — forward+loss+backward, and the update — with
 the all-reduce eager between them, so a replay enqueues the same kernels as an eager step
 without the ~500 Python-side launches (the eager step is launch-bound).
@@ -38,7 +40,10 @@ class Trainer:
     (host ints from the sharding); None = every rank holds the same count (plain mean)."""
 
     def __init__(self, model, lr=1e-3, max_norm=100.0, ema_decay=0.95, local_count=None, global_count=None,
-                 group=None):
+                 group=None, lr_schedule=None):
+        """``lr_schedule``: None (constant ``lr``) or a dict of LinearWarmupExponentialDecay's
+        arguments — warmup_steps, decay_steps, decay_rate[, staircase] (config.json: 3000, 3e6,
+        0.01) — applied per step from base ``lr`` (FlatAdam.set_schedule)."""
         self.model = model
         self.group = group
         self.multi = _world(group) > 1
@@ -47,6 +52,9 @@ class Trainer:
         # clip_grad_norm_(100) + Adam(1e-3) + EMA(0.95) (config.json) in three launches over the
         # flat parameter / gradient buffers (x2gnn.optim.FlatAdam, csrc/optim.hip)
         self.opt = FlatAdam(model.parameters(), lr=lr, max_norm=max_norm, ema_decay=ema_decay, bucket=self.bucket)
+        if lr_schedule is not None:
+            self.opt.set_schedule(base_lr=lr, **lr_schedule)
+        self.flat_launches = []  # (rows, [cols per job]) of the last backward's flat weight-gradient launches
         self.counts = (local_count, global_count)
         self.graphs = None
         self.loss = None
@@ -59,10 +67,12 @@ class Trainer:
         if not self.grads_zeroed:  # otherwise the previous update zeroed them (FlatAdam.step(zero_grads=True))
             self.bucket.zero()
         self.grads_zeroed = False
+        self.model.train()  # trainer.py:30 (an Inference sharing the model may have left it in eval)
         res = self.model(batch)
         loss = ops.smooth_l1_loss(res, batch.y)  # trainer.py:41, one launch each way
-        with ops.deferred_wgrad():  # all layers' weight-gradient slab sums in one launch
+        with ops.deferred_wgrad() as d:  # all layers' weight-gradient slab sums in one launch
             torch.autograd.backward(loss, self.seed)
+        self.flat_launches = d.flat_launches
         if self.multi:
             self.bucket.extra_view.copy_(loss.detach().reshape(1))
         return loss
@@ -86,6 +96,8 @@ class Trainer:
         self.grads_zeroed = True
 
     def step(self, batch):
+        """One step; returns the (global) loss as a fresh device scalar.  (After ``capture()`` the
+        graph's loss buffer is overwritten by every replay, so it is copied out: one 4-byte copy.)"""
         if self.graphs is None:
             loss = self.forward_backward(batch)
             self.reduce()
@@ -95,7 +107,7 @@ class Trainer:
         self.reduce()
         self.graphs[1].replay()
         self.grads_zeroed = True
-        return self.global_loss(self.loss)
+        return self.global_loss(self.loss).clone()
 
     def replay_forward_backward(self):
         """Replay the captured forward+loss+backward (accumulates into the bucket: zeroed by the
@@ -133,13 +145,18 @@ class Inference:
     MAE, trainer.py:52-58), captured in one HIP graph; ``step`` returns the energies' sum."""
 
     def __init__(self, model):
-        self.model = model.eval()
+        self.model = model
         self.graph = None
         self.out = None
 
     def _fwd(self, batch):
-        with torch.no_grad():
-            return self.model(batch).sum()
+        was = self.model.training  # eval for the forward (trainer.py:54), the caller's mode restored
+        self.model.eval()
+        try:
+            with torch.no_grad():
+                return self.model(batch).sum()
+        finally:
+            self.model.train(was)
 
     def step(self, batch):
         if self.graph is None:

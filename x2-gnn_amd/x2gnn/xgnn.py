@@ -62,7 +62,7 @@ class _XGNNBase(nn.Module):
             env = self.envelop_function(dist).unsqueeze(1)
             node_rbf = self.rbf_layer(dist) * env
             bessel = None
-        fused_feat = ops._FEATURIZE and ops.featurize_supported(data.edge_attr, env, self.mat_trans, self.emb_trans)
+        fused_feat = ops.featurize_supported(data.edge_attr, env, self.mat_trans, self.emb_trans)
         if fused_feat:  # both Linear layers, the envelope scale and SiLUs in one kernel (csrc/feature.hip)
             neo_x = ops.featurize(data.edge_attr, env, self.mat_trans, self.emb_trans)
         else:
@@ -87,7 +87,7 @@ class _XGNNBase(nn.Module):
         (Run on a second stream under the triplet build / featurisation it measured 0.4 % slower in
         the step: its workgroup holds a CU the full-chip MFMA kernels then wait for.)"""
         emb = self.emb_block
-        rows = emb.element_rows(atomic_num, count_z) if ops._TABLE_CHAIN else None
+        rows = emb.element_rows(atomic_num, count_z)
         trunk_stages = self.fin_model.edge_table_stages() if rows is not None else None
         if trunk_stages is not None:
             act = ops.ACT_SILU if emb.activate else ops.ACT_NONE
