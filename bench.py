@@ -141,10 +141,10 @@ def attention_probe(model, batch, reps):
              C, ptr(dq), ptr(dedge), None if ops._SRC_G else ptr(dlogit), ptr(prob), ptr(rho), stream_ptr())
 
     def bwd_src():
-        call("x2g_sbf_attention_bwd_src_fold", ptr(q), ptr(v), ptr(table), ptr(row), table.shape[0],
-             ops.EDGE_PER_DST, ptr(sproj), ptr(ylm), ptr(src_rowptr), ptr(src_perm), ptr(lg.trip_dst), ptr(prob),
-             None if ops._SRC_G else ptr(dlogit), ptr(rho), ptr(dout), E, T, H, C, ptr(dk), ptr(dv), ptr(gfold),
-             stream_ptr())
+        call("x2g_sbf_attention_bwd_src_fold", ptr(q), ptr(v), ptr(table), ptr(row), ptr(lg.src_type),
+             table.shape[0], ops.EDGE_PER_DST, ptr(sproj), ptr(ylm), ptr(src_rowptr), ptr(src_perm), ptr(lg.src_dst),
+             ptr(lg.trip_dst), ptr(prob), None if ops._SRC_G else ptr(dlogit), ptr(rho), ptr(dout), E, T, H, C, ptr(dk),
+             ptr(dv), ptr(gfold), stream_ptr())
 
     def radial_wgrad():
         call("x2g_sbf_radial_wgrad", ptr(gfold), ptr(radial), E, D, ptr(dwr), ptr(dbr), 0, ptr(ws), ws_bytes,
@@ -164,7 +164,7 @@ def attention_probe(model, batch, reps):
     gh = 0 if ops._SRC_G else 4 * H  # g [T, H]: written by the destination pass, read by the source pass
     dst_bytes = idx + T * (row_b + 8 * H + gh) + E * (4 + 6 * row_b + 12 * H)  # q k v dout dq d_edge, S, a/p(/g)
     dst_gath = idx + T * (3 * row_b + 8 * H + gh) + E * (4 + 4 * row_b + 12 * H)
-    # source-major CSR + trip_dst; S and Y rows, prob (, g); q v dout read, dk dv written, G [E, 8, D]
+    # source-major CSR + src_dst; S and Y rows, prob (, g); q v dout read, dk dv written, G [E, 8, D]
     src_bytes = idx + 4 * T + T * (row_b + 32 + 4 * H + gh) + E * (4 + 13 * row_b + 4 * H)
     src_gath = idx + 4 * T + T * (3 * row_b + 32 + 4 * H + gh) + E * (4 + 11 * row_b + 4 * H)
     radial_bytes = E * (8 * row_b + 4 * S) + 4 * D * (S + 1)

@@ -72,11 +72,13 @@ int x2g_vertex_to_edge(const int32_t* edge_src, const int32_t* edge_dst, int64_t
                        void* stream);
 
 /* Triplets regrouped by source line node (the transpose the backward of the k_j / v_j gathers
- * needs): src_rowptr[E+1]; src_perm[T] lists triplet ids of each source in ascending order.
+ * needs): src_rowptr[E+1]; src_perm[T] lists triplet ids of each source in ascending order;
+ * src_dst[T] (optional, NULL = not written; needs trip_dst) = trip_dst[src_perm[p]], the destination of
+ * each source-major position, so the source pass reaches it in one hop.
  * Replaces the atomics of ATen index_add_ behind PyG's index_select backward. */
-int x2g_line_graph_transpose(const int32_t* trip_src, int64_t num_triplets, int64_t num_edges,
-                             int32_t* src_rowptr, int32_t* src_perm, void* workspace,
-                             size_t workspace_bytes, void* stream);
+int x2g_line_graph_transpose(const int32_t* trip_src, const int32_t* trip_dst, int64_t num_triplets,
+                             int64_t num_edges, int32_t* src_rowptr, int32_t* src_perm, int32_t* src_dst,
+                             void* workspace, size_t workspace_bytes, void* stream);
 
 /* The same two operations for a SYMMETRIC edge set (b->a present for every a->b, as every
  * molecular graph: atom_graph.py:42-45 builds it from a symmetric distance test); the caller
@@ -90,7 +92,8 @@ int x2g_vertex_to_edge_sym(const int32_t* edge_src, const int32_t* edge_dst, int
                            size_t workspace_bytes, void* stream);
 int x2g_line_graph_transpose_sym(const int32_t* edge_src, const int32_t* edge_dst, const int32_t* atom_rowptr,
                                  const int32_t* trip_rowptr, int64_t num_edges, int32_t* src_rowptr,
-                                 int32_t* src_perm, void* workspace, size_t workspace_bytes, void* stream);
+                                 int32_t* src_perm, int32_t* src_dst, void* workspace, size_t workspace_bytes,
+                                 void* stream);
 
 /* ---------------------------------------------------------------- basis (featurisation) */
 
@@ -257,12 +260,18 @@ int x2g_sbf_attention_bwd_dst_g(const float* q, const float* k, const float* v, 
                                 const float* seg_max, const float* seg_den, const float* dout, int64_t num_edges,
                                 int64_t num_triplets, int32_t heads, int32_t channels, float* dq, float* d_edge,
                                 float* g_out, float* prob_out, float* seg_rho, void* stream);
+/* Source pass options: src_dst[T] (x2g_line_graph_transpose*'s, may be NULL: then trip_dst[src_perm[p]]
+ * is read, one more dependent hop); src_row[E] (EDGE_PER_DST only, may be NULL) = the edge row of
+ * every triplet with source s, when it depends on s alone — true of the line graph x2g_vertex_to_edge
+ * builds with the per-element table of xgnn.py:57-58 (the triplets of s = (b->k) share middle atom
+ * b: src_row[s] = Z[b]); NULL = edge_row[trip_dst[t]] per triplet. */
 int x2g_sbf_attention_bwd_src_fold(const float* q, const float* v, const float* edge, const int32_t* edge_row,
-                                   int32_t edge_rows, int edge_mode, const float* sbfproj, const float* sph_y,
-                                   const int32_t* src_rowptr, const int32_t* src_perm, const int32_t* trip_dst,
-                                   const float* prob, const float* g_in, const float* seg_rho, const float* dout,
-                                   int64_t num_edges, int64_t num_triplets, int32_t heads, int32_t channels,
-                                   float* dk, float* dv, float* radial_grad, void* stream);
+                                   const int32_t* src_row, int32_t edge_rows, int edge_mode, const float* sbfproj,
+                                   const float* sph_y, const int32_t* src_rowptr, const int32_t* src_perm,
+                                   const int32_t* src_dst, const int32_t* trip_dst, const float* prob,
+                                   const float* g_in, const float* seg_rho, const float* dout, int64_t num_edges,
+                                   int64_t num_triplets, int32_t heads, int32_t channels, float* dk, float* dv,
+                                   float* radial_grad, void* stream);
 int32_t x2g_sbf_radial_wgrad_splits(int64_t num_edges);
 size_t x2g_sbf_radial_wgrad_workspace(int64_t num_edges, int32_t out_dim);
 int x2g_sbf_radial_wgrad(const float* radial_grad, const float* radial, int64_t num_edges, int32_t out_dim,

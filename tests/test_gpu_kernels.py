@@ -103,6 +103,15 @@ def _sym_vs_generic(ei, n, T, cuda):
         assert torch.equal(getattr(gen, name), getattr(sym, name)), name
     for a, b in zip(gen.src_csr(), sym.src_csr()):
         assert torch.equal(a, b)
+    assert torch.equal(gen.src_dst, sym.src_dst)
+    # src_dst = trip_dst[src_perm]; and the source-uniform edge row the fold pass relies on: every
+    # triplet of source s = (b->k) goes into a destination (a->b) whose destination atom is s's source
+    perm = sym.src_csr()[1].long()
+    assert torch.equal(sym.src_dst, sym.trip_dst[perm])
+    if sym.T:
+        rp = sym.src_csr()[0].long()
+        src_of_pos = torch.repeat_interleave(torch.arange(sym.E, device=cuda), rp[1:] - rp[:-1])
+        assert torch.equal(sym.edge_dst.long()[sym.src_dst.long()], sym.edge_src.long()[src_of_pos])
     return sym
 
 

@@ -361,6 +361,17 @@ __device__ __forceinline__ void fwd_batch(int k0, int n, int tb, int sl, FwdStat
   }
 }
 
+// Source ids of one chunk (<= 64 triplets) of a destination segment, lane i <-> triplet t + i (the
+// wave then broadcasts them with v_readlane); an empty chunk loads nothing.
+__device__ __forceinline__ int dst_chunk_src(int t, int n, int lane, const int32_t* __restrict__ tsrc) {
+  if (n <= 0) return 0;  // (wave-uniform)
+  return tsrc[t + (lane < n ? lane : n - 1)];
+}
+
+// Software-pipelined over the wave's destinations: the row pointer two segments ahead, the next
+// segment's source ids and this segment's skip row are requested at the top of the segment, so the
+// dependent index chain (rowptr -> trip_src -> the k / v / S gathers) of the next segment is in flight
+// under this one's gathers and math instead of costing two serial round trips per segment.
 template <int CPL, int LPH, int MODE>
 __global__ void __launch_bounds__(256) attn_fwd_batched(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
@@ -374,30 +385,44 @@ __global__ void __launch_bounds__(256) attn_fwd_batched(
   const int head = lane / LPH;
   const bool leader = act && (lane % LPH) == 0;
   const WaveRange wr_ = xcd_wave_range(E);
-  for (int64_t e = wr_.first; e < wr_.end; e += wr_.stride) {
-    const int t0 = uniform(rowptr[e]), t1 = uniform(rowptr[e + 1]);
+  int64_t e = wr_.first;
+  if (e >= wr_.end) return;
+  const int64_t last = wr_.end - 1;
+  int t0 = uniform(rowptr[e]), t1 = uniform(rowptr[e + 1]);
+  const int64_t e1 = e + wr_.stride < wr_.end ? e + wr_.stride : last;
+  int q0 = uniform(rowptr[e1]), q1 = uniform(rowptr[e1 + 1]);
+  int sl = dst_chunk_src(t0, t1 - t0 < 64 ? t1 - t0 : 64, lane, tsrc);
+  // the edge-table row of the current / next destination (one segment ahead, like the source ids)
+  int er = (MODE == X2G_EDGE_PER_DST && edge_row) ? uniform(edge_row[e]) : static_cast<int>(e);
+  int ern = (MODE == X2G_EDGE_PER_DST && edge_row) ? uniform(edge_row[e1]) : static_cast<int>(e1);
+  for (; e < wr_.end; e += wr_.stride) {
     FwdState<CPL> st;
+    float sk[CPL];
     load_row<CPL>(q + e * D + c0, act, st.qv);
+    load_row<CPL>(skip + e * D + c0, act, sk);
     if (MODE == X2G_EDGE_PER_DST) {
-      const int64_t r = edge_row ? uniform(edge_row[e]) : e;
-      load_row<CPL>(edge + r * D + c0, act, st.ed);
+      load_row<CPL>(edge + static_cast<int64_t>(er) * D + c0, act, st.ed);
     } else {
       zero_row<CPL>(st.ed);
     }
     zero_row<CPL>(st.acc);
     st.m = -INFINITY;
     st.den = 0.f;
+    const int64_t e2r = e + 2 * wr_.stride;
+    const int64_t e2 = e2r < wr_.end ? e2r : last;
+    const int r0 = uniform(rowptr[e2]), r1 = uniform(rowptr[e2 + 1]);
+    const int er2 = (MODE == X2G_EDGE_PER_DST && edge_row) ? uniform(edge_row[e2]) : static_cast<int>(e2);
+    const int sln = dst_chunk_src(q0, q1 - q0 < 64 ? q1 - q0 : 64, lane, tsrc);
     for (int tb = t0; tb < t1; tb += 64) {
       const int n = t1 - tb < 64 ? t1 - tb : 64;
-      const int sl = tsrc[tb + (lane < n ? lane : n - 1)];
+      if (tb != t0) sl = dst_chunk_src(tb, n, lane, tsrc);  // segments longer than 64 triplets
       int k0 = 0;
       for (; n - k0 > 4; k0 += 8)
         fwd_batch<CPL, LPH, MODE, 8>(k0, n, tb, sl, st, k, v, sp, D, H, c0, head, act, leader, sqrt_c, alpha_out);
       if (k0 < n)
         fwd_batch<CPL, LPH, MODE, 4>(k0, n, tb, sl, st, k, v, sp, D, H, c0, head, act, leader, sqrt_c, alpha_out);
     }
-    float sk[CPL], o[CPL];
-    load_row<CPL>(skip + e * D + c0, act, sk);
+    float o[CPL];
     const float inv = 1.0f / (st.den + kSoftmaxEps);
 #pragma unroll
     for (int c = 0; c < CPL; ++c) o[c] = st.acc[c] * inv + sk[c];
@@ -407,6 +432,13 @@ __global__ void __launch_bounds__(256) attn_fwd_batched(
       smax_out[e * H + head] = st.m;
       sden_out[e * H + head] = st.den;
     }
+    t0 = q0;
+    t1 = q1;
+    q0 = r0;
+    q1 = r1;
+    sl = sln;
+    er = ern;
+    ern = er2;
   }
 }
 
@@ -1070,6 +1102,7 @@ struct FoldArgs {
   int mode;
   const float *sp, *y;
   const int32_t *rowptr, *tidx, *tdst;
+  const int32_t *sdst, *src_row;  // source pass: destination per source-major position / edge row per source
   const float *alpha, *smax, *sden, *prob, *rho_in, *g_in, *dout;
   int64_t E;
   int D, H;
@@ -1090,15 +1123,19 @@ void fold_launch_mode(bool dst, const FoldArgs& a, unsigned blocks, hipStream_t 
           a.sqrt_c, a.dq, a.d_edge, a.g_out, a.prob_out, a.rho_out);
   } else {  // source-major pass
     const int C = a.D / a.H;
-#define X2G_SRC_FOLD(TABLE, GIN)                                                                                 \
-  attn_bwd_src_fold_batched<CPL, LPH, TABLE, GIN><<<blocks, 256, 0, st>>>(                                       \
-      a.q, a.v, a.edge, a.edge_row, a.edge_rows, a.sp, a.y, a.rowptr, a.tidx, a.tdst, a.prob, a.rho_in, a.g_in,   \
-      a.dout, a.E, a.D, a.H, C, a.dk, a.dv, a.gfold)
+#define X2G_SRC_FOLD(TABLE, SROW, GIN)                                                                           \
+  attn_bwd_src_fold_batched<CPL, LPH, TABLE, SROW, GIN><<<blocks, 256, 0, st>>>(                                 \
+      a.q, a.v, a.edge, a.edge_row, a.src_row, a.edge_rows, a.sp, a.y, a.rowptr, a.tidx, a.sdst, a.tdst, a.prob,   \
+      a.rho_in, a.g_in, a.dout, a.E, a.D, a.H, C, a.dk, a.dv, a.gfold)
     const bool gin = a.g_in != nullptr;
     if (a.mode == X2G_EDGE_PER_DST) {
-      if (gin) X2G_SRC_FOLD(true, true); else X2G_SRC_FOLD(true, false);
+      if (a.src_row) {
+        if (gin) X2G_SRC_FOLD(true, true, true); else X2G_SRC_FOLD(true, true, false);
+      } else {
+        if (gin) X2G_SRC_FOLD(true, false, true); else X2G_SRC_FOLD(true, false, false);
+      }
     } else {
-      if (gin) X2G_SRC_FOLD(false, true); else X2G_SRC_FOLD(false, false);
+      if (gin) X2G_SRC_FOLD(false, false, true); else X2G_SRC_FOLD(false, false, false);
     }
 #undef X2G_SRC_FOLD
   }
@@ -1160,14 +1197,15 @@ X2G_API int x2g_sbf_attention_bwd_dst_g(const float* q, const float* k, const fl
 }
 
 X2G_API int x2g_sbf_attention_bwd_src_fold(const float* q, const float* v, const float* edge, const int32_t* edge_row,
-                                           int32_t edge_rows, int edge_mode, const float* sbfproj, const float* sph_y,
-                                           const int32_t* src_rowptr, const int32_t* src_perm, const int32_t* trip_dst,
+                                           const int32_t* src_row, int32_t edge_rows, int edge_mode,
+                                           const float* sbfproj, const float* sph_y, const int32_t* src_rowptr,
+                                           const int32_t* src_perm, const int32_t* src_dst, const int32_t* trip_dst,
                                            const float* prob, const float* g_in, const float* seg_rho,
                                            const float* dout, int64_t E, int64_t T, int32_t heads, int32_t channels,
                                            float* dk, float* dv, float* radial_grad, void* stream) {
   if (E > 0 && (!q || !v || !sbfproj || !src_rowptr || !seg_rho || !dout || !dk || !dv || !radial_grad))
     return X2G_EINVAL;
-  if (T > 0 && (!src_perm || !trip_dst || !prob || !sph_y)) return X2G_EINVAL;  // g_in may be NULL
+  if (T > 0 && (!src_perm || (!trip_dst && !src_dst) || !prob || !sph_y)) return X2G_EINVAL;  // g_in may be NULL
   // the source pass reads the edge term from a small table staged in LDS (X2-GNN's element table)
   if (edge_mode == X2G_EDGE_PER_DST && (!edge || !edge_row || edge_rows < 1 || edge_rows > kFoldTableRows))
     return X2G_EUNSUPPORTED;
@@ -1175,6 +1213,7 @@ X2G_API int x2g_sbf_attention_bwd_src_fold(const float* q, const float* v, const
   FoldArgs a{};
   a.q = q; a.v = v; a.edge = edge; a.edge_row = edge_row; a.edge_rows = edge_rows; a.mode = edge_mode;
   a.sp = sbfproj; a.y = sph_y; a.rowptr = src_rowptr; a.tidx = src_perm; a.tdst = trip_dst; a.prob = prob;
+  a.sdst = src_dst; a.src_row = edge_mode == X2G_EDGE_PER_DST ? src_row : nullptr;
   a.rho_in = seg_rho; a.g_in = g_in; a.dout = dout; a.E = E; a.dk = dk; a.dv = dv; a.gfold = radial_grad;
   return fold_dispatch(false, a, heads, channels, as_stream(stream));
 }

@@ -326,7 +326,7 @@ int degree_scan(const int32_t* atom, const int32_t* atom_rowptr, int64_t n, int3
 __global__ void transpose_sym_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
                                      const int32_t* __restrict__ atom_rowptr, const int32_t* __restrict__ trip_rowptr,
                                      const int32_t* __restrict__ src_rowptr, int64_t E,
-                                     int32_t* __restrict__ src_perm) {
+                                     int32_t* __restrict__ src_perm, int32_t* __restrict__ src_dst) {
   const int64_t gtid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int64_t s = gtid / kEmitGroup;
   const int sub = threadIdx.x & (kEmitGroup - 1);
@@ -347,14 +347,17 @@ __global__ void transpose_sym_kernel(const int32_t* __restrict__ src, const int3
     const bool in = valid && idx < hi;
     const int a = in ? dst[idx] : 0;
     const bool keep = in && a != k;
-    int tid_out = 0;
+    int tid_out = 0, e = 0;
     if (keep) {
-      const int e = lower_bound(dst, atom_rowptr[a], atom_rowptr[a + 1], b);  // edge a->b (symmetric graph)
+      e = lower_bound(dst, atom_rowptr[a], atom_rowptr[a + 1], b);  // edge a->b (symmetric graph)
       tid_out = trip_rowptr[e] + rank_k - (idx - lo < rank_k ? 1 : 0);
     }
     const uint64_t ball = __ballot(keep) & group_mask;
     const int q = p + __popcll(ball & ((1ull << lane) - 1));
-    if (keep) src_perm[q] = tid_out;
+    if (keep) {
+      src_perm[q] = tid_out;
+      if (src_dst) src_dst[q] = e;
+    }
     p += __popcll(ball);
   }
 }
@@ -426,9 +429,18 @@ X2G_API int x2g_vertex_to_edge(const int32_t* edge_src, const int32_t* edge_dst,
   return last_launch_status();
 }
 
-X2G_API int x2g_line_graph_transpose(const int32_t* trip_src, int64_t T, int64_t E, int32_t* src_rowptr,
-                                     int32_t* src_perm, void* workspace, size_t workspace_bytes, void* stream) {
+// src_dst[p] = trip_dst[src_perm[p]]: the destination of each source-major position
+__global__ void gather_dst_kernel(const int32_t* __restrict__ perm, const int32_t* __restrict__ tdst, int64_t T,
+                                  int32_t* __restrict__ out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < T) out[i] = tdst[perm[i]];
+}
+
+X2G_API int x2g_line_graph_transpose(const int32_t* trip_src, const int32_t* trip_dst, int64_t T, int64_t E,
+                                     int32_t* src_rowptr, int32_t* src_perm, int32_t* src_dst, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
   if (T < 0 || E < 0 || !src_rowptr || (T > 0 && (!trip_src || !src_perm))) return X2G_EINVAL;
+  if (T > 0 && src_dst && !trip_dst) return X2G_EINVAL;
   if (workspace_bytes < x2g_vertex_to_edge_workspace(E, 0) || !workspace) return X2G_EWORKSPACE;
   hipStream_t st = as_stream(stream);
   int32_t* count = static_cast<int32_t*>(workspace);
@@ -445,6 +457,7 @@ X2G_API int x2g_line_graph_transpose(const int32_t* trip_src, int64_t T, int64_t
   if (T > 0) {
     fill_by_key<<<blocks_for(T, 256), 256, 0, st>>>(trip_src, T, src_rowptr, cursor, src_perm);
     sort_segments<<<blocks_for(E, 256), 256, 0, st>>>(src_rowptr, E, src_perm);
+    if (src_dst) gather_dst_kernel<<<blocks_for(T, 256), 256, 0, st>>>(src_perm, trip_dst, T, src_dst);
   }
   return last_launch_status();
 }
@@ -473,7 +486,8 @@ X2G_API int x2g_vertex_to_edge_sym(const int32_t* edge_src, const int32_t* edge_
 
 X2G_API int x2g_line_graph_transpose_sym(const int32_t* edge_src, const int32_t* edge_dst, const int32_t* atom_rowptr,
                                          const int32_t* trip_rowptr, int64_t E, int32_t* src_rowptr,
-                                         int32_t* src_perm, void* workspace, size_t workspace_bytes, void* stream) {
+                                         int32_t* src_perm, int32_t* src_dst, void* workspace, size_t workspace_bytes,
+                                         void* stream) {
   if (E < 0 || !src_rowptr || (E > 0 && (!edge_src || !edge_dst || !atom_rowptr || !trip_rowptr || !src_perm)))
     return X2G_EINVAL;
   if (workspace_bytes < x2g_vertex_to_edge_workspace(E, 0) || !workspace) return X2G_EWORKSPACE;
@@ -484,6 +498,6 @@ X2G_API int x2g_line_graph_transpose_sym(const int32_t* edge_src, const int32_t*
   if ((rc = degree_scan(edge_src, atom_rowptr, E, src_rowptr, count, partial, st))) return rc;
   if (E > 0)
     transpose_sym_kernel<<<blocks_for(E * kEmitGroup, 256), 256, 0, st>>>(edge_src, edge_dst, atom_rowptr, trip_rowptr,
-                                                                          src_rowptr, E, src_perm);
+                                                                          src_rowptr, E, src_perm, src_dst);
   return last_launch_status();
 }

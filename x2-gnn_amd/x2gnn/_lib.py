@@ -27,7 +27,7 @@ SIGNATURES = {
     "x2g_csr_rowptr": [_P, _I64, _I64, _P, _P],
     "x2g_vertex_to_edge_workspace": [_I64, _I64],
     "x2g_vertex_to_edge": [_P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P],
-    "x2g_line_graph_transpose": [_P, _I64, _I64, _P, _P, _P, _SZ, _P],
+    "x2g_line_graph_transpose": [_P, _P, _I64, _I64, _P, _P, _P, _P, _SZ, _P],
     "x2g_bessel_env": [_P, _I64, _F, _I32, _I32, _P, _P],
     "x2g_edge_basis": [_P, _P, _P, _I64, _F, _P, _I32, _I32, _I32, _P, _P, _P, _P, _P],
     "x2g_edge_basis_freq_grad_workspace": [_I64, _I32],
@@ -48,7 +48,7 @@ SIGNATURES = {
     "x2g_rbf_pool_fwd": [_P, _P, _P, _P, _P, _I64, _I32, _I32, _P, _P],
     "x2g_rbf_gate_bwd_workspace": [_I64, _I32, _I32],
     "x2g_vertex_to_edge_sym": [_P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P],
-    "x2g_line_graph_transpose_sym": [_P, _P, _P, _P, _I64, _P, _P, _P, _SZ, _P],
+    "x2g_line_graph_transpose_sym": [_P, _P, _P, _P, _I64, _P, _P, _P, _P, _SZ, _P],
     "x2g_keyed_row_sum_batch_workspace": [_I64, _I32, _I32, _I32],
     "x2g_keyed_row_sum_batch": [_P, _P, _I32, _P, _I64, _I32, _I32, ctypes.c_int, _P, _SZ, _P],
     "x2g_clip_adam_ema_ex": [_P, _P, _P, _P, _P, _I64, _P, ctypes.c_int, _P, _SZ, _P],
@@ -60,8 +60,8 @@ SIGNATURES = {
     "x2g_spherical_basis": [_P, _P, _P, _P, _P, _P, _P, _I64, _I32, _I32, _P, _P, _P, _P],
     "x2g_sbf_attention_bwd_dst_g": [_P, _P, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I32,
                                     _I32, _P, _P, _P, _P, _P, _P],
-    "x2g_sbf_attention_bwd_src_fold": [_P, _P, _P, _P, _I32, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                                       _I64, _I64, _I32, _I32, _P, _P, _P, _P],
+    "x2g_sbf_attention_bwd_src_fold": [_P, _P, _P, _P, _P, _I32, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                       _P, _I64, _I64, _I32, _I32, _P, _P, _P, _P],
     "x2g_sbf_radial_wgrad_splits": [_I64],
     "x2g_sbf_radial_wgrad_workspace": [_I64, _I32],
     "x2g_sbf_radial_wgrad": [_P, _P, _I64, _I32, _P, _P, ctypes.c_int, _P, _SZ, _P],

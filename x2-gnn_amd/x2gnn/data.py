@@ -151,6 +151,7 @@ def _add_device_indices(b, nodes, edges):
     b._store["_x2g_mol_ptr"] = torch.from_numpy(np.concatenate([[0], np.cumsum(nodes)]).astype(np.int32))
     b._store["_x2g_line_ptr"] = torch.from_numpy(np.concatenate([[0], np.cumsum(edges)]).astype(np.int32))
     b._store["_x2g_dst_type"] = torch.from_numpy(b._store["x"].numpy()[ei_np[1]].astype(np.int32))
+    b._store["_x2g_src_type"] = torch.from_numpy(b._store["x"].numpy()[ei_np[0]].astype(np.int32))
     b._store["_x2g_symmetric"] = _is_symmetric(ei_np, int(nodes.sum()))
 
 

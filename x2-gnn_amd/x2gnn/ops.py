@@ -75,7 +75,12 @@ class LineGraph:
         self.atom_k = torch.empty(self.T, **i32)
         self._src_rowptr = None
         self._src_perm = None
+        self._src_dst = None
         self.order_status = None  # built here in order: nothing to check
+        # per-line-node element rows of the x2g_vertex_to_edge line graph (GraphPlan sets them):
+        # dst_type[e] = Z of e's destination atom = the edge row of every triplet into e, and
+        # src_type[s] = Z of s's source atom = the same row for every triplet out of s
+        self.dst_type = self.src_type = None
         ws_bytes = int(_lib.load().x2g_vertex_to_edge_workspace(self.E, self.N))
         self._ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         call("x2g_vertex_to_edge_sym" if self.symmetric else "x2g_vertex_to_edge", ptr(edge_src), ptr(edge_dst),
@@ -96,25 +101,35 @@ class LineGraph:
         lg.trip_src = _i32(triplet_index[0])
         lg.trip_dst = _i32(triplet_index[1])
         lg.trip_rowptr, lg.order_status = csr_rowptr_checked(lg.trip_dst, lg.E)
-        lg._src_rowptr = lg._src_perm = None
+        lg._src_rowptr = lg._src_perm = lg._src_dst = None
+        lg.dst_type = lg.src_type = None
         lg.symmetric = False
         ws_bytes = int(_lib.load().x2g_vertex_to_edge_workspace(lg.E, 0))
         lg._ws = torch.empty(ws_bytes, dtype=torch.uint8, device=lg.trip_src.device)
         return lg
 
     def src_csr(self):
+        """(src_rowptr [E+1], src_perm [T]): the triplets grouped by source line node; ``src_dst``
+        [T] (each source-major position's destination) is built with them."""
         if self._src_rowptr is None:
             dev = self.trip_src.device
             self._src_rowptr = torch.empty(self.E + 1, dtype=torch.int32, device=dev)
             self._src_perm = torch.empty(self.T, dtype=torch.int32, device=dev)
+            self._src_dst = torch.empty(self.T, dtype=torch.int32, device=dev)
             if self.symmetric:  # lists written in order from the degrees (no atomics, no segment sort)
                 call("x2g_line_graph_transpose_sym", ptr(self.edge_src), ptr(self.edge_dst), ptr(self.atom_rowptr),
-                     ptr(self.trip_rowptr), self.E, ptr(self._src_rowptr), ptr(self._src_perm), ptr(self._ws),
-                     self._ws.numel(), stream_ptr())
+                     ptr(self.trip_rowptr), self.E, ptr(self._src_rowptr), ptr(self._src_perm), ptr(self._src_dst),
+                     ptr(self._ws), self._ws.numel(), stream_ptr())
             else:
-                call("x2g_line_graph_transpose", ptr(self.trip_src), self.T, self.E, ptr(self._src_rowptr),
-                     ptr(self._src_perm), ptr(self._ws), self._ws.numel(), stream_ptr())
+                call("x2g_line_graph_transpose", ptr(self.trip_src), ptr(self.trip_dst), self.T, self.E,
+                     ptr(self._src_rowptr), ptr(self._src_perm), ptr(self._src_dst), ptr(self._ws),
+                     self._ws.numel(), stream_ptr())
         return self._src_rowptr, self._src_perm
+
+    @property
+    def src_dst(self):
+        self.src_csr()
+        return self._src_dst
 
     def order_violated(self) -> bool:
         """True when the triplet destinations handed to ``from_triplets`` were not sorted (one sync)."""
@@ -376,9 +391,12 @@ class _SBFAttention(torch.autograd.Function):
              ptr(dq), ptr(d_edge), ptr(g), ptr(prob), ptr(rho), st)
         src_rowptr, src_perm = lg.src_csr()
         rows = 0 if edge is None else edge.shape[0]
-        call("x2g_sbf_attention_bwd_src_fold", ptr(q), ptr(v), ptr(edge), ptr(ctx.edge_row), rows, mode, ptr(sproj),
-             ptr(ylm), ptr(src_rowptr), ptr(src_perm), ptr(lg.trip_dst), ptr(prob), ptr(g), ptr(rho), ptr(dout), E, T,
-             heads, channels, ptr(dk), ptr(dv), ptr(gfold), st)
+        # the edge row per SOURCE (constant over a source segment) when the rows are the line graph's
+        # own destination elements
+        src_row = lg.src_type if (ctx.edge_row is not None and ctx.edge_row is lg.dst_type) else None
+        call("x2g_sbf_attention_bwd_src_fold", ptr(q), ptr(v), ptr(edge), ptr(ctx.edge_row), ptr(src_row), rows, mode,
+             ptr(sproj), ptr(ylm), ptr(src_rowptr), ptr(src_perm), ptr(lg.src_dst), ptr(lg.trip_dst), ptr(prob),
+             ptr(g), ptr(rho), ptr(dout), E, T, heads, channels, ptr(dk), ptr(dv), ptr(gfold), st)
         if not ctx.needs_input_grad[4]:
             d_edge = None  # (written by the kernel; no consumer: the table's gradient is not wanted)
         elif mode == EDGE_PER_DST and ctx.edge_row is not None:

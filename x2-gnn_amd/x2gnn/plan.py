@@ -67,6 +67,7 @@ class GraphPlan:
             p.lg = ops.LineGraph(st["_x2g_edge_src"], st["_x2g_edge_dst"], p.num_atoms, p.num_triplets,
                                  st.get("_x2g_symmetric", False))
             p.line_ptr, p.mol_ptr, p.dst_type = st["_x2g_line_ptr"], st["_x2g_mol_ptr"], st["_x2g_dst_type"]
+            src_type = st.get("_x2g_src_type")
         else:
             p.lg = ops.vertex_to_edge(ei, p.num_atoms, p.num_triplets, meta.get("symmetric", False))
             p.line_ptr = _ptr_from_counts(data.edge_num, p.num_graphs, dev)
@@ -75,6 +76,10 @@ class GraphPlan:
             else:
                 p.mol_ptr = (torch.arange(2, device=dev, dtype=torch.int32) * p.num_atoms)
             p.dst_type = ops._i32(data.x.index_select(0, p.lg.edge_dst))
+            src_type = None
+        if src_type is None:
+            src_type = ops._i32(data.x.index_select(0, p.lg.edge_src.long()))
+        p.lg.dst_type, p.lg.src_type = p.dst_type, src_type
         p.atom_rowptr = p.lg.atom_rowptr
         # per-molecule line-node / triplet counts on the host: whole-molecule ranges of the triplet
         # stream for the tiled inference attention (ops._infer_tiles), with no device read
