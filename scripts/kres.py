@@ -22,7 +22,7 @@ for line in out.splitlines():
         rows[cur][k] = v
 for name, r in rows.items():
     dem = subprocess.run(["c++filt", name], capture_output=True, text=True).stdout.strip()
-    short = re.sub(r"\(.*", "", dem).replace("x2g::", "").replace("(anonymous namespace)::", "")
+    short = re.sub(r"\(.*", "", dem.replace("(anonymous namespace)::", "")).replace("x2g::", "").replace("void ", "")
     if pat and not pat.search(short):
         continue
     print(f"{short:60s} vgpr {r.get('VGPRs','?'):>4s} agpr {r.get('AGPRs','?'):>3s} spill {r.get('VGPRs Spill','?'):>3s}"

@@ -30,8 +30,13 @@ constexpr int kFN1 = 256;             // mat_trans outputs
 constexpr int kFN2 = 128;             // emb_trans outputs
 constexpr int kFKMax = 384;           // input features, padded: 3 T planes
 constexpr int kFRows = 32;            // rows per tile (two 16-row MFMA blocks)
-constexpr int kFAS = kFKMax + 4;      // LDS row stride of the input tile (== 4 mod 64: conflict-free f4)
-constexpr int kFYS = kFN1 + 4;        // LDS row stride of the hidden tile
+// LDS row strides of the input tile and the hidden tile: == 8 mod 64 floats (2 mod 16 chunks), which
+// makes the MFMA operand read of lane (i, g) — 16 bytes at row i, chunk 4q + g — hit 16 distinct bank
+// quads in each of ds_read_b128's four lane groups ({0-3, 12-15, 20-27}, {4-11, 16-19, 28-31}, ...).
+// The former stride (== 4 mod 64) left 2-way conflicts in those groups: SQ_LDS_BANK_CONFLICT /
+// SQ_LDS_IDX_ACTIVE = 0.49 on the r4d PMC pass.  (scripts: the layout search is in DESIGN.md §3.)
+constexpr int kFAS = kFKMax + 8;
+constexpr int kFYS = kFN1 + 8;
 constexpr int kFThreads = 512;
 
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 acc) {
@@ -271,7 +276,7 @@ struct FeatBwdArgs {
   int64_t tf;
 };
 
-constexpr int kFDS = kFN2 + 4;  // LDS row stride of the dz2 tile
+constexpr int kFDS = kFN2 + 8;  // LDS row stride of the dz2 tile (== 8 mod 64: conflict-free operand reads, as kFAS)
 
 __global__ void __launch_bounds__(kFThreads, 1) feat_bwd_kernel(const FeatBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float DZ[kFRows * kFDS];
