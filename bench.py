@@ -41,9 +41,40 @@ CFG = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embed
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32) peak, MI355X_MICROARCH.md
 # scripts/pmc_traffic.py outputs (rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench), per workload
-TRAFFIC_JSON = {"qm9_u0": os.path.join(ROOT, "profiles", "r3f_pmc_traffic.json"),
-                "qm9_allprop": None,  # no PMC pass at config 3's shapes: its traffic fields stay null
-                "aid_infer": os.path.join(ROOT, "profiles", "r3f_pmc_traffic_c5.json")}
+# the committed PMC summaries (scripts/pmc_traffic.py over rocprofv3 FETCH_SIZE / WRITE_SIZE passes of
+# this bench at the same workload and shape): bytes of each probe's own launch
+TRAFFIC_JSON = {("qm9_u0", "S160"): os.path.join(ROOT, "profiles", "r4_pmc_traffic.json"),
+                ("qm9_u0", "S5A"): os.path.join(ROOT, "profiles", "r4_pmc_traffic_s5a.json"),
+                ("qm9_allprop", "S160"): os.path.join(ROOT, "profiles", "r4_pmc_traffic_c3.json"),
+                ("aid_infer", "S160"): os.path.join(ROOT, "profiles", "r4_pmc_traffic_c5.json")}
+# the config-2 step's per-kernel work table (scripts/step_work.py: PMC HBM bytes, matrix FLOPs, trace time
+# per step) behind `step_roofline`
+STEP_WORK_JSON = os.path.join(ROOT, "profiles", "r4_step_work.json")
+
+
+def step_roofline(ms_per_step, workload, shape):
+    """The step against its own bound: every kernel of the step at its own roofline, back to back —
+    sum_k max(FLOP_k / f32 MFMA peak, HBM bytes_k / HBM peak) — over the measured step time.  FLOP_k are
+    the MFMA kernels' matrix FLOPs, bytes_k the PMC-measured HBM traffic per step (the committed
+    table, scripts/step_work.py); VALU work (attention, elementwise) is priced by its bytes alone."""
+    if workload != "qm9_u0" or shape != "S160" or not os.path.exists(STEP_WORK_JSON):
+        return None
+    tab = json.load(open(STEP_WORK_JSON))
+    rows = []
+    for k, v in tab["kernels"].items():
+        t_f = v["flops"] / (MFMA_F32_PEAK_TFS * 1e12) * 1e3
+        t_b = v["hbm_bytes"] / (HBM_PEAK_GBS * 1e9) * 1e3
+        rows.append((k, max(t_f, t_b), t_f, t_b, v["us"] * 1e-3))
+    bound = sum(r[1] for r in rows)
+    rows.sort(key=lambda r: -(r[4] - r[1]))
+    return {"frac": round(bound / ms_per_step, 4), "bound_ms": round(bound, 4), "ms_per_step": ms_per_step,
+            "mfma_ms": round(sum(r[2] for r in rows), 4), "hbm_ms": round(sum(r[3] for r in rows), 4),
+            "kernel_ms_traced": round(sum(r[4] for r in rows), 4),
+            "largest_gaps": [{"kernel": r[0], "traced_ms": round(r[4], 4), "bound_ms": round(r[1], 4)}
+                             for r in rows[:6]],
+            "source": os.path.relpath(STEP_WORK_JSON, ROOT)}
+
+
 # probe name -> the kernel (substring of its symbol) whose PMC bytes it is
 PMC_KERNEL = {"sbf_project": "sbf_project_waves", "attn_fwd": "attn_fwd_batched",
               "attn_bwd_dst": "attn_bwd_dst_g_batched", "attn_bwd_src": "attn_bwd_src_fold_batched",
@@ -341,10 +372,10 @@ def _lib_ws(name, *args):
     return int(getattr(_lib.load(), name)(*args))
 
 
-def load_traffic(workload):
+def load_traffic(workload, shape="S160"):
     """(path, {"<kernel>|<grid>": {"fetch_bytes", "write_bytes", ...}}) of the committed PMC summary
-    for this workload, or (path, None)."""
-    path = TRAFFIC_JSON[workload]
+    for this workload and shape, or (path, None)."""
+    path = TRAFFIC_JSON.get((workload, shape))
     if path is None or not os.path.exists(path):
         return path, None
     return path, json.load(open(path))["kernels"]
@@ -444,7 +475,7 @@ def scatter_add_probe(lg, reps):
 
 
 # ------------------------------------------------------------------------------------------ cpu
-CALIBRATION_JSON = os.path.join(ROOT, "profiles", "r3_cpu_calibration.json")  # scripts/calibrate_cpu_baseline.py
+CALIBRATION_JSON = os.path.join(ROOT, "profiles", "r4_cpu_calibration.json")  # scripts/calibrate_cpu_baseline.py
 
 
 def host_cores():
@@ -606,7 +637,7 @@ def main():
         return
 
     meta = batch.host_meta()
-    traffic_path, traffic_table = load_traffic(args.workload)
+    traffic_path, traffic_table = load_traffic(args.workload, args.shape)
     probe, shape = attention_probe(model, batch, args.kernel_reps)
     plan_lg = model.line_graph_data(batch)[1].lg
     sa = scatter_add_probe(plan_lg, args.kernel_reps)
@@ -677,6 +708,7 @@ def main():
                        "grad_allreduce": None if world == 1 else (
                            "RCCL" if args.dist_backend == "nccl" else "gloo (rehearsal)")},
             "roofline": roof,
+            "step_roofline": step_roofline(round(1e3 * t_max / args.steps, 4), args.workload, args.shape),
             "kernels": dict(
                 {k: _hbm_entry(k, v, traffic_table) for k, v in probe.items()},
                 **{k: _mfma_entry(k, v, traffic_table) for k, v in dense.items()}),

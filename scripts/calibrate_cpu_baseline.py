@@ -8,7 +8,11 @@ molecules, seed 1000), the same seeded weights, fwd + smooth_l1 + bwd, median of
 1 warm-up, at 8 threads (this container's cores) and 4 (config.json ``num_thread``), and writes
 the reference / restatement rate ratio per thread count:
 
-    python scripts/calibrate_cpu_baseline.py [out.json]   (default profiles/r3_cpu_calibration.json)
+    python scripts/calibrate_cpu_baseline.py [out.json] [seed ...]
+        (default profiles/r4_cpu_calibration.json; seeds default: 1000 = bench.py's batch, 0 = the survey's)
+
+Round 4: the batch seed is a parameter and both the survey's seed-0 batch (BASELINE.md:25, 106.9 mol/s
+at 8 threads) and bench.py's seed-1000 batch are timed, so the two figures can be compared on one host.
 
 bench.py multiplies the restatement's rate on the GPU box's host by this ratio to state a
 reference-equivalent CPU figure beside its own measurement.
@@ -49,10 +53,8 @@ def time_steps(step, reps=5):
     return float(np.median(ts)), [round(t, 4) for t in ts]
 
 
-def main():
-    out_path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "profiles", "r3_cpu_calibration.json")
-    ref = import_reference()
-    mols = synthetic_molecules(128, "S160", seed=1000)  # bench.py's config-2 batch at N = 1
+def calibrate(ref, seed):
+    mols = synthetic_molecules(128, "S160", seed=seed)  # seed 1000: bench.py's config-2 batch at N = 1
     b = collate(mols)
     ref_model = ref.xgnn.xgnn_poly(device="cpu", **CFG)
     port_model = ref_cpu.XGNN(**CFG)
@@ -83,13 +85,27 @@ def main():
         rows[str(threads)] = {"reference_mol_s": round(len(mols) / t_ref, 2), "port_mol_s": round(len(mols) / t_port, 2),
                               "reference_over_port": round(t_port / t_ref, 4), "reference_step_s": ts_ref,
                               "port_step_s": ts_port}
-        print(threads, rows[str(threads)], flush=True)
+        print(seed, threads, rows[str(threads)], flush=True)
+    meta = b.host_meta()
+    return {"batch": f"128 synthetic S160 molecules, seed {seed}",
+            "per_molecule": {"atoms": float(meta["nodes"].mean()), "edges": float(meta["edges"].mean()),
+                             "triplets": float(meta["triplets"].mean())},
+            "energies_max_rel_diff": rel, "threads": rows}
+
+
+def main():
+    out_path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "profiles", "r4_cpu_calibration.json")
+    seeds = [int(x) for x in sys.argv[2:]] or [1000, 0]
+    ref = import_reference()
+    per_seed = {str(s): calibrate(ref, s) for s in seeds}
+    first = per_seed[str(seeds[0])]
     res = {"what": "reference (shimmed import) vs oracle/ref_cpu.py restatement, fwd+smooth_l1+bwd, same batch / "
                    "weights / cores; median of 5 after 1 warm-up",
-           "batch": "128 synthetic S160 molecules, seed 1000 (bench.py config 2, N=1)",
-           "energies_max_rel_diff": rel, "host": {"cpus": os.cpu_count(), "machine": platform.processor() or
-                                                 platform.machine(), "torch": torch.__version__},
-           "threads": rows}
+           "host": {"cpus": os.cpu_count(), "machine": platform.processor() or platform.machine(),
+                    "torch": torch.__version__},
+           # bench.py reads these two (its batch: seed 1000)
+           "batch": first["batch"], "energies_max_rel_diff": first["energies_max_rel_diff"],
+           "threads": first["threads"], "seeds": per_seed}
     json.dump(res, open(out_path, "w"), indent=1)
     print("->", out_path)
 
