@@ -21,22 +21,31 @@ pmc2() {  # pmc2 <name> <bench args...>: FETCH_SIZE pass, WRITE_SIZE pass, summa
   run pmcw_$name 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmcw_${name}_$TAG -o run --output-format csv -- python "$ROOT/bench.py" "$@"
   run sum_$name 120 python scripts/pmc_traffic.py gpurun_out/pmcf_${name}_$TAG gpurun_out/pmcw_${name}_$TAG gpurun_out/pmc_traffic_${name}_$TAG.json
 }
+# PARTS selects the stages (a call is capped at 20 min): pmc (the four PMC summaries), work (step table),
+# bench (the four bench lines)
+PARTS=${PARTS:-pmc work bench}
+has() { [[ " $PARTS " == *" $1 "* ]]; }
 P="--steps 2 --warmup 1 --no-cpu-baseline --kernel-reps 3"
+if has pmc; then
 pmc2 c2 $P
 pmc2 s5a $P --shape S5A
 pmc2 c3 $P --workload qm9_allprop --target 0
 pmc2 c5 $P --workload aid_infer
+cp gpurun_out/pmc_traffic_c2_$TAG.json profiles/r4_pmc_traffic.json
+cp gpurun_out/pmc_traffic_s5a_$TAG.json profiles/r4_pmc_traffic_s5a.json
+cp gpurun_out/pmc_traffic_c3_$TAG.json profiles/r4_pmc_traffic_c3.json
+cp gpurun_out/pmc_traffic_c5_$TAG.json profiles/r4_pmc_traffic_c5.json
+fi
+if has work; then
 # the step's work table: PMC over eager steps, kernel trace over graph-replayed steps
 run pmcf_step 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf_step_$TAG -o run --output-format csv -- python "$ROOT/bench.py" --step-only --eager --steps 3 --warmup 1
 run pmcw_step 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcw_step_$TAG -o run --output-format csv -- python "$ROOT/bench.py" --step-only --eager --steps 3 --warmup 1
 run trace_step 300 rocprofv3 --kernel-trace --stats -d gpurun_out/trace_step_$TAG -o run --output-format csv -- python "$ROOT/bench.py" --step-only --steps 20 --warmup 3
 run work 300 python scripts/step_work.py gpurun_out/pmcf_step_$TAG gpurun_out/pmcw_step_$TAG gpurun_out/trace_step_$TAG gpurun_out/step_work_$TAG.json
-# install the summaries where bench.py reads them (the caller copies them into profiles/ as well)
-cp gpurun_out/pmc_traffic_c2_$TAG.json profiles/r4_pmc_traffic.json
-cp gpurun_out/pmc_traffic_s5a_$TAG.json profiles/r4_pmc_traffic_s5a.json
-cp gpurun_out/pmc_traffic_c3_$TAG.json profiles/r4_pmc_traffic_c3.json
-cp gpurun_out/pmc_traffic_c5_$TAG.json profiles/r4_pmc_traffic_c5.json
 cp gpurun_out/step_work_$TAG.json profiles/r4_step_work.json
+fi
+# the bench lines read the summaries installed above (on this box; the caller copies them into profiles/)
+has bench || exit 0
 run bench_c2 420 python bench.py
 run bench_s5a 420 python bench.py --shape S5A --no-cpu-baseline
 run bench_c3 420 python bench.py --workload qm9_allprop --target 0

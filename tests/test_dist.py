@@ -44,6 +44,54 @@ def _grads(model, mols):
     return loss.detach()
 
 
+def _chunk_worker(rank, world, port, out_q):
+    """One rank's gradient bucket all-reduced once whole and once as 3 asynchronous chunks."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mols = synthetic_molecules(4, "S160", seed=7)
+        model = _model()
+        bucket = GradBucket(model.parameters(), extra=1)
+        bucket.zero()
+        loss = _grads(model, [mols[i] for i in range(rank, 4, world)])
+        bucket.extra_view.copy_(loss.reshape(1))
+        local = bucket.flat.clone()
+        bucket.allreduce_mean(local_count=2, global_count=4)
+        whole = bucket.flat.clone()
+        bucket.flat.copy_(local)
+        bucket.allreduce_mean(local_count=2, global_count=4, chunks=3)
+        out_q.put((rank, whole.numpy(), bucket.flat.clone().numpy(), bucket.chunk_bounds(3), bucket.flat.numel()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_chunked_allreduce_equals_single_collective():
+    """GradBucket.allreduce_mean(chunks=3): three asynchronous collectives over contiguous ranges cut at
+    parameter boundaries (reverse layout order, the loss slot in the first) give the single
+    collective's bucket bit for bit with two ranks."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_chunk_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, whole, chunked, bounds, n = q.get(timeout=240)
+        got[r] = (whole, chunked, bounds, n)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    whole, chunked, bounds, n = got[0]
+    assert len(bounds) == 3 and bounds[0][1] == n and bounds[-1][0] == 0
+    assert all(bounds[i][0] == bounds[i + 1][1] for i in range(len(bounds) - 1))  # contiguous, reversed
+    np.testing.assert_array_equal(chunked, whole)
+    np.testing.assert_array_equal(got[1][1], whole)
+
+
 def _worker(rank, world, port, shards, out_q, weighted=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(2)
@@ -146,11 +194,17 @@ def _aid_worker(rank, world, port, idx, out_q):
         res = ref_cpu.run_batch(model, batch)
         loss = torch.nn.functional.smooth_l1_loss(res, batch.y)
         loss.backward()
+        local = bucket.flat.clone()
         bucket.allreduce_mean(local_count=n_local, global_count=n_global)
+        whole = bucket.flat.clone()
+        bucket.flat.copy_(local)
+        bucket.allreduce_mean(local_count=n_local, global_count=n_global, chunks=4)
+        # four ranks: the ring's per-element summation order may follow the chunk position
+        np.testing.assert_allclose(bucket.flat.numpy(), whole.numpy(), rtol=1e-6, atol=1e-7 * float(whole.abs().max()))
         t = loss.detach().clone() * n_local / n_global
         dist.all_reduce(t)
         load = int(batch._meta["triplets"].sum())
-        out_q.put((rank, bucket.flat.clone().numpy(), float(t), n_local, load,
+        out_q.put((rank, whole.numpy(), float(t), n_local, load,
                    batch._store["_x2g_count_z"].numpy()))
     finally:
         dist.destroy_process_group()

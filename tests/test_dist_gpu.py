@@ -62,7 +62,8 @@ def _worker(rank, world, port, out_q):
         host, n_local, n_global = collate_shard(mols, world, rank)
         assert n_local == len(mine) and n_global == len(mols)
         batch = host.to(dev)
-        tr = Trainer(_model(dev), local_count=n_local, global_count=n_global)
+        # the exchange as 3 asynchronous collectives over contiguous bucket ranges (reverse layout order)
+        tr = Trainer(_model(dev), local_count=n_local, global_count=n_global, exchange_chunks=3)
         # the captured step (what bench.py replays): capture (its 3 warm-up passes run eagerly),
         # zero, replay forward+backward, all-reduce
         tr.capture(batch)
@@ -75,8 +76,15 @@ def _worker(rank, world, port, out_q):
         # after the same >= 4 forwards: each forward re-applies the embedding's max_norm renorm in
         # place, as torch does, and a renormalised row can be renormalised again by an ulp.)
         loss = tr.forward_backward(batch)
+        local = tr.bucket.flat.clone()
         tr.reduce()
         eager = tr.bucket.flat.detach().cpu().numpy().copy()
+        # the chunked exchange equals the single collective bit for bit (two ranks)
+        tr.bucket.flat.copy_(local)
+        tr.exchange_chunks = 1
+        tr.reduce()
+        torch.cuda.synchronize()
+        assert np.array_equal(tr.bucket.flat.detach().cpu().numpy(), eager)
         eager_loss = float(tr.global_loss(loss))
         out_q.put((rank, [int(i) for i in mine], eager, eager_loss, graphed, tr.bucket.num_grad))
     finally:

@@ -78,7 +78,25 @@ class GradBucket:
     def zero(self):
         self.flat.zero_()
 
-    def allreduce_mean(self, group=None, local_count=None, global_count=None):
+    def chunk_bounds(self, chunks: int):
+        """``chunks`` contiguous [lo, hi) ranges of the flat buffer that cover it, cut at parameter
+        boundaries into near-equal byte shares, in REVERSE layout order: the last parameters (the
+        readouts and the last conv layers, whose gradients a backward finishes first) lead.  The
+        trailing ``extra`` floats (the loss slot) ride with the first range issued."""
+        n = self.num_grad
+        chunks = max(1, min(int(chunks), len(self.params)))
+        cuts = [0]
+        for k in range(1, chunks):
+            target = k * n / chunks
+            # the parameter boundary nearest the target, strictly increasing
+            best = min(self.offsets, key=lambda o: abs(o - target))
+            if best > cuts[-1]:
+                cuts.append(best)
+        cuts.append(self.flat.numel())
+        ranges = [(cuts[i], cuts[i + 1]) for i in range(len(cuts) - 1)]
+        return ranges[::-1]
+
+    def allreduce_mean(self, group=None, local_count=None, global_count=None, chunks: int = 1):
         """Turn each rank's gradient of its own mean loss into the gradient of the global-batch
         mean loss (trainer.py:41, smooth_l1 with reduction='mean').
 
@@ -86,17 +104,34 @@ class GradBucket:
         per-rank gradients are averaged.  With ``local_count`` (molecules on this rank) and
         ``global_count`` (molecules over all ranks, known on the host from the sharding), each
         rank's gradient is weighted by local/global before the sum, which is what unequal shards
-        (e.g. ``shard_by_triplets``) need."""
+        (e.g. ``shard_by_triplets``) need.
+
+        ``chunks`` > 1 issues the SUM as that many asynchronous collectives over the contiguous
+        ranges of ``chunk_bounds`` (reverse layout order), all in flight together on the process
+        group's own stream and joined to the current stream before returning — so the optimizer that
+        follows waits for all of them, and RCCL pipelines one range's ring behind another's.  Each
+        element is summed over the same ranks either way; with two ranks the result is bitwise equal
+        to the single collective (tests/test_dist.py), with more the ring's per-element order may
+        differ by chunk position (fp32 reassociation only)."""
         multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
         if local_count is not None:
             if global_count is None or global_count <= 0:
                 raise ValueError("weighted all-reduce needs the global molecule count")
             self.flat.mul_(float(local_count) / float(global_count))
             if multi:
-                dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+                self._sum(group, chunks)
             return
         if multi:
             # SUM then one divide: ReduceOp.AVG would save the divide under RCCL, but it is the one
             # collective option the 1-GPU rehearsal (gloo) cannot exercise before the 8-GPU run
-            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+            self._sum(group, chunks)
             self.flat.div_(dist.get_world_size(group))
+
+    def _sum(self, group, chunks):
+        if chunks <= 1:
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+            return
+        works = [dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM, group=group, async_op=True)
+                 for lo, hi in self.chunk_bounds(chunks)]
+        for w in works:
+            w.wait()

@@ -40,10 +40,12 @@ class Trainer:
     (host ints from the sharding); None = every rank holds the same count (plain mean)."""
 
     def __init__(self, model, lr=1e-3, max_norm=100.0, ema_decay=0.95, local_count=None, global_count=None,
-                 group=None, lr_schedule=None):
+                 group=None, lr_schedule=None, exchange_chunks=1):
         """``lr_schedule``: None (constant ``lr``) or a dict of LinearWarmupExponentialDecay's
         arguments — warmup_steps, decay_steps, decay_rate[, staircase] (config.json: 3000, 3e6,
-        0.01) — applied per step from base ``lr`` (FlatAdam.set_schedule)."""
+        0.01) — applied per step from base ``lr`` (FlatAdam.set_schedule).  ``exchange_chunks``: the
+        gradient all-reduce as that many asynchronous collectives over contiguous bucket ranges
+        (GradBucket.allreduce_mean(chunks=...)), joined before the optimizer."""
         self.model = model
         self.group = group
         self.multi = _world(group) > 1
@@ -56,6 +58,7 @@ class Trainer:
             self.opt.set_schedule(base_lr=lr, **lr_schedule)
         self.flat_launches = []  # (rows, [cols per job]) of the last backward's flat weight-gradient launches
         self.counts = (local_count, global_count)
+        self.exchange_chunks = int(exchange_chunks)
         self.graphs = None
         self.loss = None
         self.grads_zeroed = False  # the bucket starts zeroed too; the first step zeroes it anyway
@@ -83,9 +86,10 @@ class Trainer:
             return
         local, total = self.counts
         if local is None:
-            self.bucket.allreduce_mean(group=self.group)
+            self.bucket.allreduce_mean(group=self.group, chunks=self.exchange_chunks)
         else:
-            self.bucket.allreduce_mean(group=self.group, local_count=local, global_count=total)
+            self.bucket.allreduce_mean(group=self.group, local_count=local, global_count=total,
+                                       chunks=self.exchange_chunks)
 
     def global_loss(self, local_loss):
         """The global-batch mean loss after ``reduce()`` (the shard's loss when single-rank)."""
