@@ -1,6 +1,8 @@
 """Phase timeline of the trunk chain backward (x2g_chain_bwd, 7 stages; A/B trace build only:
 make -C x2-gnn_amd ab AB_NAME=trace AB_FLAGS=-DX2G_TRACE, run with X2G_LIB=.../libx2g_trace.so).
-Thread 0 of every workgroup stamps a 100 MHz clock before / after each stage's barrier."""
+Thread 0 of every workgroup stamps a 100 MHz clock before / after each stage's barrier.
+
+    python scripts/trace_chain.py [rows] [fwd]   (fwd: the forward x2g_chain_fwd instead)"""
 import ctypes
 import os
 import sys
@@ -13,6 +15,7 @@ from x2gnn import _lib, ops  # noqa: E402
 from x2gnn._lib import call, ptr, stream_ptr  # noqa: E402
 
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 21120
+FWD = len(sys.argv) > 2 and sys.argv[2] == "fwd"
 D, n = 128, 7
 S, H, RH, RE = ops.CHAIN_SILU, ops.CHAIN_HOLD, ops.CHAIN_RES_HELD, ops.CHAIN_RES_EXT
 flags = [S | H, S | RH, S | RE, S | H, S | RH, S | H, S | RH]
@@ -37,7 +40,10 @@ lib.x2g_trace_fetch.argtypes = [ctypes.c_void_p, ctypes.c_int]
 for it in range(6):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    call("x2g_chain_bwd", ptr(dy), None, bst, n, R, D, ptr(dx), ptr(dres), ptr(dz_t), stream_ptr())
+    if FWD:
+        call("x2g_chain_fwd", ptr(x), ptr(res), st, n, R, D, ptr(in_t), stream_ptr())
+    else:
+        call("x2g_chain_bwd", ptr(dy), None, bst, n, R, D, ptr(dx), ptr(dres), ptr(dz_t), stream_ptr())
     e1.record()
     torch.cuda.synchronize()
 buf = np.zeros(1024 * 16, dtype=np.uint64)
@@ -45,7 +51,10 @@ assert lib.x2g_trace_fetch(buf.ctypes.data, buf.size) == 0
 grid = min(256, (R + 15) // 16)
 t = buf.reshape(1024, 16)[:grid].astype(np.int64)
 t0 = t[:, 0].min()
-names = ["start", "stage6 elem+bar"] + [f"stage{n - 1 - i} {w}" for i in range(n) for w in ("done", "barrier")]
+if FWD:
+    names = ["start", "staged+bar"] + [f"stage{i} {w}" for i in range(n) for w in ("done", "barrier")]
+else:
+    names = ["start", "stage6 elem+bar"] + [f"stage{n - 1 - i} {w}" for i in range(n) for w in ("done", "barrier")]
 print(f"rows {R} grid {grid} event {e0.elapsed_time(e1) * 1e3:.1f} us; relative to the first stamp (us)")
 for k in range(len(names)):
     rel = (t[:, k] - t0) / 100.0

@@ -37,8 +37,9 @@ e1.record()
 torch.cuda.synchronize()
 buf = np.zeros(1024 * 16, dtype=np.uint64)
 assert lib.x2g_trace_fetch(buf.ctypes.data, buf.size) == 0
-t = buf.reshape(1024, 16)[:256].astype(np.float64)
+t = buf.reshape(1024, 16).astype(np.float64)
+t = t[t[:, 2] > 0]  # the launch's workgroups (two per CU)
 wait, comp, steps = t[:, 0] / 100.0 / reps, t[:, 1] / 100.0 / reps, t[:, 2] / reps
-print(f"{e0.elapsed_time(e1) * 1e3 / reps:.1f} us per launch; per workgroup: steps {np.median(steps):.0f}, "
+print(f"{e0.elapsed_time(e1) * 1e3 / reps:.1f} us per launch; {len(t)} workgroups; per workgroup: steps {np.median(steps):.0f}, "
       f"copies+barrier {np.median(wait):.1f} us (max {wait.max():.1f}), MFMA issue {np.median(comp):.1f} us "
       f"(max {comp.max():.1f}); per step {np.median(wait / steps) * 1e3:.0f} + {np.median(comp / steps) * 1e3:.0f} ns")

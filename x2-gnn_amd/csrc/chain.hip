@@ -481,7 +481,9 @@ __device__ __forceinline__ void fwd4_stage(const ChainFwdArgs& a, int s, const f
   __builtin_amdgcn_sched_barrier(0);
   half_epi<4, 6>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
   pin(An);
+  X2G_TR(2 + 2 * s);
   __syncthreads();
+  X2G_TR(3 + 2 * s);
   if (S.y) store_img(S.y, out, r0, nrows);
 #pragma unroll
   for (int b = 0; b < 8; ++b) A[b] = An[b];
@@ -614,6 +616,10 @@ __device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a, const Ch
     const int s = static_cast<int>(i / (kCD * kCD)), e = static_cast<int>(i % (kCD * kCD));
     if (a.st[s].wt) a.st[s].wt[e] = a.st[s].w[(e % kCD) * kCD + e / kCD];
   }
+#ifdef X2G_STAGGER_FWD  // A/B builds only: odd workgroups start X2G_STAGGER_FWD x 8128 cycles late
+  if (blockIdx.x & 1)
+    for (int i = 0; i < X2G_STAGGER_FWD; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
   for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
     int r0, nrows;
     chunk_rows(ch, nch, nblk, a.R, r0, nrows);
@@ -623,11 +629,13 @@ __device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a, const Ch
     else
       stage_rows(img0, a.x, nullptr, r0, nrows);
     if (a.res) stage_rows(imgr, a.res, nullptr, r0, nrows);
+    X2G_TR(0);
     f4 A[8], held[kV2RB];
     load_slice<false>(a.st[0].w, w, rl, g, A);
 #pragma unroll
     for (int rb = 0; rb < kV2RB; ++rb) held[rb] = zero4();
     __syncthreads();
+    X2G_TR(1);
     if (a.in_t) {
       f4 xs[kV2RB];
 #pragma unroll
@@ -737,6 +745,10 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
   const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
   const int n = a.n;
   const int col = 16 * w + 4 * g;
+#ifdef X2G_STAGGER_BWD  // A/B builds only: odd workgroups start X2G_STAGGER_BWD x 8128 cycles late
+  if (blockIdx.x & 1)
+    for (int i = 0; i < X2G_STAGGER_BWD; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
   for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
     int r0, nrows;
     chunk_rows(ch, nch, nblk, a.R, r0, nrows);

@@ -42,12 +42,36 @@ constexpr int kFThreads = 512;
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 acc) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
 }
-__device__ __forceinline__ float silu_(float z) { return z / (1.0f + expf(-z)); }
+// SiLU and its derivative from the hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32: ~1 ulp each), as
+// the row chains: libm expf and IEEE division are ~25 VALU instructions per element, 24 elements per
+// lane and tile in the forward's epilogues, which run between barriers with no MFMA to hide behind.
+// sigmoid(z) = rcp(1 + 2^(-z log2 e)); z -> -inf gives 0, z -> +inf gives 1, NaN stays NaN.
+__device__ __forceinline__ float sigmoid_(float z) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * z));
+}
+__device__ __forceinline__ float silu_(float z) { return z * sigmoid_(z); }
 __device__ __forceinline__ float silu_grad_(float z) {
-  const float s = 1.0f / (1.0f + expf(-z));
+  const float s = sigmoid_(z);
   return s * (1.0f + z * (1.0f - s));
 }
 __device__ __forceinline__ f4 zero4() { return f4{0.f, 0.f, 0.f, 0.f}; }
+
+// 4 x 4 transpose inside each lane quad (DPP quad permutes, no LDS): lane 4m + j holding v[e] =
+// element (e, j) of its quad's 4 x 4 block ends with v[k] = element (j, k)
+__device__ __forceinline__ f4 quad_t(f4 v, int j) {
+  f4 b, c;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float t = dpp_mov<0xB1>(v[k ^ 1]);
+    b[k] = ((k ^ j) & 1) ? t : v[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float t = dpp_mov<0x4E>(b[k ^ 2]);
+    c[k] = ((k ^ j) & 2) ? t : b[k];
+  }
+  return c;
+}
 
 // T layout: element (r, f) of a [R, 128 P] tensor at plane (f >> 7) * tf + (r >> 4) * 2048 +
 // (f & 127) * 16 + (r & 15); a lane's D block rows 4g..4g+3 at column f are one float4.
@@ -249,17 +273,23 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
       }
     }
     const int c2 = 16 * w + i;
+    // neo_x leaves as 16-byte row pieces: lane (i = 4m + j, g) holds rows 4g + e of column c2, and
+    // after the quad transpose row 4g + j, columns 16w + 4m .. +3 (one store per block, not four)
+    const int qj = i & 3, qm = i >> 2;
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
       const int64_t t16 = r0 / 16 + rb;
       if (t16 * 16 >= R) continue;
-      f4 z;
+      f4 z, y;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int r = 16 * rb + 4 * g + e;
         z[e] = r < nr ? acc2[rb][e] + b2v : 0.0f;
-        if (r < nr) a.y2[(r0 + r) * kFN2 + c2] = silu_(z[e]);
+        y[e] = silu_(z[e]);
       }
+      const f4 yt = quad_t(y, qj);
+      const int ry = 16 * rb + 4 * g + qj;
+      if (ry < nr) *reinterpret_cast<f4*>(a.y2 + (r0 + ry) * kFN2 + 16 * w + 4 * qm) = yt;
       if (a.want_t) *reinterpret_cast<f4*>(a.z2_t + tpos(a.tf, t16, c2, g)) = z;
     }
   }
