@@ -360,20 +360,28 @@ __device__ __forceinline__ void half_epi(f4 (&acc)[kV2RB], const f4 (&held)[kV2R
   for (int rb = RB0; rb < RB1; ++rb) {
     const int r = 16 * rb + rl;
     const f4 z = acc[rb] + bias;
+#ifndef X2G_ABL_NOZ  // (ablation switches: A/B timing builds only, never the shipped library)
     bstore4(zr, z, r < nrows ? 4 * ((r0 + r) * kCD + 16 * w + 4 * g) : kOOB);
+#endif
     f4 y;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
+#ifdef X2G_ABL_NOACT
+      const float sv = z[e];
+#else
       const float sv = silu_fast(z[e]);
+#endif
       y[e] = silu_m * sv + (1.0f - silu_m) * z[e] + res_m * held[rb][e];
     }
     out[ipos(r, 4 * w + g)] = y;
     acc[rb] = y;
+#ifndef X2G_ABL_NOT
     f4 t = quad_transpose(y, j);
 #pragma unroll
     for (int e = 0; e < 4; ++e) t[e] = 16 * rb + 4 * m + e < nrows ? t[e] : 0.0f;
     bstore4(tr, t, rb < ntile ? 4 * static_cast<int>((static_cast<int64_t>(r0 >> 4) + rb) * (16 * kCD) + f * 16 + 4 * m)
                               : kOOB);
+#endif
   }
 }
 
@@ -482,7 +490,9 @@ __device__ __forceinline__ void fwd4_stage(const ChainFwdArgs& a, int s, const f
   half_epi<4, 6>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
   pin(An);
   X2G_TR(2 + 2 * s);
+#ifndef X2G_ABL_NOBAR
   __syncthreads();
+#endif
   X2G_TR(3 + 2 * s);
   if (S.y) store_img(S.y, out, r0, nrows);
 #pragma unroll
@@ -616,10 +626,6 @@ __device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a, const Ch
     const int s = static_cast<int>(i / (kCD * kCD)), e = static_cast<int>(i % (kCD * kCD));
     if (a.st[s].wt) a.st[s].wt[e] = a.st[s].w[(e % kCD) * kCD + e / kCD];
   }
-#ifdef X2G_STAGGER_FWD  // A/B builds only: odd workgroups start X2G_STAGGER_FWD x 8128 cycles late
-  if (blockIdx.x & 1)
-    for (int i = 0; i < X2G_STAGGER_FWD; ++i) __builtin_amdgcn_s_sleep(127);
-#endif
   for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
     int r0, nrows;
     chunk_rows(ch, nch, nblk, a.R, r0, nrows);
@@ -745,10 +751,6 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
   const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
   const int n = a.n;
   const int col = 16 * w + 4 * g;
-#ifdef X2G_STAGGER_BWD  // A/B builds only: odd workgroups start X2G_STAGGER_BWD x 8128 cycles late
-  if (blockIdx.x & 1)
-    for (int i = 0; i < X2G_STAGGER_BWD; ++i) __builtin_amdgcn_s_sleep(127);
-#endif
   for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
     int r0, nrows;
     chunk_rows(ch, nch, nblk, a.R, r0, nrows);
@@ -1020,14 +1022,20 @@ __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, cons
   for (int i = 0; i < nsteps; ++i) {
     // this step's copies are done when at most the later issued steps' 2 * WT each remain
     const int ahead = nsteps - 1 - i < NB - 2 ? nsteps - 1 - i : NB - 2;
+#ifndef X2G_ABL_NOWAIT  // (ablation switches: A/B timing builds only, never the shipped library)
     if (ahead >= 2)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * WT) : "memory");
     else if (ahead == 1)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * WT) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
+    (void)ahead;
+#endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifndef X2G_ABL_FLATNOBAR
     __builtin_amdgcn_s_barrier();  // every wave's copies of this step have landed; step i-1 is read
+#endif
 #ifdef X2G_TRACE
     {
       const unsigned long long t = wall_clock64();
@@ -1049,7 +1057,11 @@ __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, cons
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int bk = 0; bk < 8; ++bk) acc[bk] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[bk][e], acc[bk], 0, 0, 0);
+#ifdef X2G_ABL_NOBIAS
+      if (false) {
+#else
       if (SPREAD && has_b) {  // bias: thread (q, f) sums feature f's row quad q (every wave takes a share)
+#endif
         const f4 v = Ds[b][k][tpos(tid & (kCD - 1), tid >> 7)];
         bsum += (v[0] + v[1]) + (v[2] + v[3]);
       }
@@ -1070,6 +1082,9 @@ __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, cons
     }
 #endif
   }
+#ifdef X2G_ABL_NOWAIT
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
 #ifdef X2G_TRACE
   if (threadIdx.x == 0) {
     x2g_trace_buf[blockIdx.x * 16 + 0] += tw;
