@@ -14,5 +14,9 @@ for rep in 1 2; do
     X2G_LIB=$L/libx2g_$v.so timeout -k 10 120 python scripts/flat_time.py >> gpurun_out/abl_flat_$TAG.txt 2>&1 || exit $?
   done
 done
+if [ -n "${FEAT_TRACE:-}" ]; then
+  X2G_LIB=$L/libx2g_ftrace.so timeout -k 10 120 python scripts/trace_feat.py > gpurun_out/trace_feat_$TAG.txt 2>&1 || exit $?
+  cat gpurun_out/trace_feat_$TAG.txt
+fi
 grep -h "libx2g" gpurun_out/abl_chain_$TAG.txt gpurun_out/abl_flat_$TAG.txt 2>/dev/null
 exit 0
