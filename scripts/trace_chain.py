@@ -61,3 +61,7 @@ for k in range(len(names)):
     d = (t[:, k] - t[:, k - 1]) / 100.0 if k else rel
     print(f"{k:2d} {names[k]:>16s}  at med {np.median(rel):7.2f} max {rel.max():7.2f}   phase med {np.median(d):6.2f} "
           f"max {d.max():6.2f}")
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import clk_report  # noqa: E402
+
+clk_report.report(lib, "chain fwd" if FWD else "chain bwd")

@@ -43,3 +43,7 @@ wait, comp, steps = t[:, 0] / 100.0 / reps, t[:, 1] / 100.0 / reps, t[:, 2] / re
 print(f"{e0.elapsed_time(e1) * 1e3 / reps:.1f} us per launch; {len(t)} workgroups; per workgroup: steps {np.median(steps):.0f}, "
       f"copies+barrier {np.median(wait):.1f} us (max {wait.max():.1f}), MFMA issue {np.median(comp):.1f} us "
       f"(max {comp.max():.1f}); per step {np.median(wait / steps) * 1e3:.0f} + {np.median(comp / steps) * 1e3:.0f} ns")
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import clk_report  # noqa: E402
+
+clk_report.report(lib, "flat")

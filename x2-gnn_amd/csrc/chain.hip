@@ -313,9 +313,22 @@ __device__ unsigned long long x2g_trace_buf[1024 * 16];
   do {                                                                                            \
     if (threadIdx.x == 0 && (k) < 16) x2g_trace_buf[blockIdx.x * 16 + (k)] = wall_clock64();     \
   } while (0)
+// core clock vs the 100 MHz wall clock at a kernel's start (k = 0) and end (k = 1): the SCLK the
+// kernel ran at
+__device__ unsigned long long x2g_clk_buf[1024 * 4];
+#define X2G_CLK(k)                                                          \
+  do {                                                                      \
+    if (threadIdx.x == 0) {                                                 \
+      x2g_clk_buf[blockIdx.x * 4 + 2 * (k)] = clock64();                    \
+      x2g_clk_buf[blockIdx.x * 4 + 2 * (k) + 1] = wall_clock64();           \
+    }                                                                       \
+  } while (0)
 #else
 #define X2G_TR(k) \
   do {            \
+  } while (0)
+#define X2G_CLK(k) \
+  do {             \
   } while (0)
 #endif
 
@@ -626,6 +639,7 @@ __device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a, const Ch
     const int s = static_cast<int>(i / (kCD * kCD)), e = static_cast<int>(i % (kCD * kCD));
     if (a.st[s].wt) a.st[s].wt[e] = a.st[s].w[(e % kCD) * kCD + e / kCD];
   }
+  X2G_CLK(0);
   for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
     int r0, nrows;
     chunk_rows(ch, nch, nblk, a.R, r0, nrows);
@@ -653,6 +667,7 @@ __device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a, const Ch
       if (s + 1 < n) fwd4_stage(a, s + 1, img1, img0, imgr, A, held, r0, nrows, w, rl, g);
     }
   }
+  X2G_CLK(1);
 }
 
 __global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4(const ChainFwdArgs a) { chain_fwd_v4_run<false>(a, {}); }
@@ -751,6 +766,7 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
   const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
   const int n = a.n;
   const int col = 16 * w + 4 * g;
+  X2G_CLK(0);
   for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
     int r0, nrows;
     chunk_rows(ch, nch, nblk, a.R, r0, nrows);
@@ -858,6 +874,7 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
     else
       store_img(a.dx, img[p], r0, nrows);
   }
+  X2G_CLK(1);
 }
 
 struct ChainBwdBatch {
@@ -1046,6 +1063,11 @@ __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, cons
 #endif
     if (i + NB - 1 < nsteps) issue(i + NB - 1);
     const int b = i % NB;
+#ifdef X2G_FLAT_BIAS_EARLY  // (A/B) the step's bias reads issued first, summed after its MFMAs
+    f4 bias_v[WT];
+#pragma unroll
+    for (int k = 0; k < WT; ++k) bias_v[k] = Ds[b][k][tpos(tid & (kCD - 1), tid >> 7)];
+#endif
 #pragma unroll
     for (int k = 0; k < WT; ++k) {
       if (t0 + static_cast<int64_t>(i) * WT + k >= t1) break;  // wave-uniform
@@ -1057,7 +1079,7 @@ __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, cons
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int bk = 0; bk < 8; ++bk) acc[bk] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[bk][e], acc[bk], 0, 0, 0);
-#ifdef X2G_ABL_NOBIAS
+#if defined(X2G_ABL_NOBIAS) || defined(X2G_FLAT_BIAS_EARLY)
       if (false) {
 #else
       if (SPREAD && has_b) {  // bias: thread (q, f) sums feature f's row quad q (every wave takes a share)
@@ -1073,6 +1095,13 @@ __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, cons
         }
       }
     }
+#ifdef X2G_FLAT_BIAS_EARLY
+#pragma unroll
+    for (int k = 0; k < WT; ++k) {
+      const bool ok = SPREAD && has_b && t0 + static_cast<int64_t>(i) * WT + k < t1;
+      bsum += ok ? (bias_v[k][0] + bias_v[k][1]) + (bias_v[k][2] + bias_v[k][3]) : 0.0f;
+    }
+#endif
 #ifdef X2G_TRACE
     {  // (the MFMAs are issued; their results are first needed by the next step's ... at the end)
       asm volatile("s_nop 0" ::: "memory");
@@ -1139,6 +1168,7 @@ __global__ void __launch_bounds__(kCThreads, 2 * WPC) tiled_flat_kernel(const Ti
   __shared__ f4 Xs[NB][WT][512];
   const int64_t G = gridDim.x, i = blockIdx.x;
   const int64_t lo = i * a.total / G, hi = (i + 1) * a.total / G;
+  X2G_CLK(0);
   for (int64_t j = lo / a.ntiles; j < a.njobs && j * a.ntiles < hi; ++j) {
     const int64_t s0 = lo > j * a.ntiles ? lo : j * a.ntiles;
     const int64_t s1 = hi < (j + 1) * a.ntiles ? hi : (j + 1) * a.ntiles;
@@ -1148,6 +1178,7 @@ __global__ void __launch_bounds__(kCThreads, 2 * WPC) tiled_flat_kernel(const Ti
     tiled_segment<NB, SPREAD, WT>(a.dz_t[j], a.in_t[j], s0 - j * a.ntiles, s1 - j * a.ntiles, a.has_b[j] != 0,
                   a.slab_w[j] + k * kCD * kCD, a.slab_b[j] + k * kCD, Ds, Xs);
   }
+  X2G_CLK(1);
 }
 
 inline int chain_wgrad_splits_of(int64_t ntiles, int stages) {
@@ -1909,6 +1940,9 @@ X2G_API int x2g_conv_proj_bwd(const x2g_proj_grad* grads, int64_t rows, int32_t 
 #ifdef X2G_TRACE
 X2G_API int x2g_trace_fetch(unsigned long long* host, int n) {
   return static_cast<int>(hipMemcpyFromSymbol(host, HIP_SYMBOL(x2g_trace_buf), sizeof(unsigned long long) * n));
+}
+X2G_API int x2g_clk_fetch(unsigned long long* host, int n) {
+  return static_cast<int>(hipMemcpyFromSymbol(host, HIP_SYMBOL(x2g_clk_buf), sizeof(unsigned long long) * n));
 }
 #endif
 
