@@ -190,6 +190,14 @@ int x2g_spherical_basis(const float* pos, const int32_t* atom_i, const int32_t* 
 int x2g_sbf_project(const float* sbf, int64_t num_triplets, int32_t sbf_dim, const float* w_sbf,
                     const float* b_sbf, int32_t out_dim, float* sbfproj, void* stream);
 
+/* Every layer's S_l = sbf W_l^T + b_l in one launch (layers 1..X2G_SBF_PROJECT_MAX_LAYERS; the
+ * trunk's lin_sbf of every SBFTransformerConv, sbftransformer_conv.py:142): w_sbf / b_sbf / sbfproj are
+ * HOST arrays of n_layers device pointers.  Each S_l equals x2g_sbf_project's bit for bit. */
+#define X2G_SBF_PROJECT_MAX_LAYERS 8
+int x2g_sbf_project_batch(const float* sbf, int64_t num_triplets, int32_t sbf_dim, const float* const* w_sbf,
+                          const float* const* b_sbf, int32_t n_layers, int32_t out_dim, float* const* sbfproj,
+                          void* stream);
+
 /* In the three attention entry points below, w_sbf == NULL (and b_sbf == NULL) means `sbf` is
  * that precomputed projection S [T, heads*channels] and sbf_dim must equal heads*channels;
  * otherwise `sbf` is the raw basis [T, 42] and the projection is computed per triplet. */

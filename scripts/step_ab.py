@@ -21,7 +21,10 @@ res = {name: [] for name, _ in variants}
 for r in range(rounds):
     for name, env in variants:
         e = dict(os.environ, **env)
-        out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--step-only", "--steps", "200",
+        # AB_ROOT: run that tree's bench.py (and so its x2gnn package), e.g. ab_base/ from
+        # scripts/build_base_tree.sh for a host-side change
+        broot = os.path.join(root, env["AB_ROOT"]) if "AB_ROOT" in env else root
+        out = subprocess.run([sys.executable, os.path.join(broot, "bench.py"), "--step-only", "--steps", "200",
                               "--warmup", "10"], env=e, capture_output=True, text=True, timeout=300)
         line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
         if out.returncode != 0 or not line:

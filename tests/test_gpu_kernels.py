@@ -814,6 +814,30 @@ def test_sbf_project_vs_torch(cuda, T, out_dim):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("T,out_dim,n", [(194060, 128, 4), (37, 128, 3), (1000, 64, 2), (0, 128, 4)])
+def test_sbf_project_batch_equals_per_layer(cuda, T, out_dim, n):
+    """x2g_sbf_project_batch (every layer's lin_sbf in one launch, layer = blockIdx.y; out_dim 64 takes the
+    per-layer fallback) == x2g_sbf_project per layer, bit for bit, and == fp64 torch to rounding."""
+    import ctypes
+
+    from x2gnn._lib import call, ptr, stream_ptr
+
+    g = torch.Generator(device=cuda).manual_seed(T + n)
+    sbf = torch.randn(T, 42, device=cuda, generator=g)
+    ws = [torch.randn(out_dim, 42, device=cuda, generator=g) / 6.5 for _ in range(n)]
+    bs = [torch.randn(out_dim, device=cuda, generator=g) for _ in range(n)]
+    outs = [torch.full((T, out_dim), float("nan"), device=cuda) for _ in range(n)]
+    P = ctypes.c_void_p * n
+    call("x2g_sbf_project_batch", ptr(sbf), T, 42, P(*[w.data_ptr() for w in ws]), P(*[b.data_ptr() for b in bs]), n,
+         out_dim, P(*[o.data_ptr() for o in outs]), stream_ptr())
+    for w, b, o in zip(ws, bs, outs):
+        one = torch.full((T, out_dim), float("nan"), device=cuda)
+        call("x2g_sbf_project", ptr(sbf), T, 42, ptr(w), ptr(b), out_dim, ptr(one), stream_ptr())
+        assert torch.equal(o, one)
+        torch.testing.assert_close(o, (sbf.double() @ w.double().t() + b.double()).float(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
 def test_sbf_project_rows_independent_of_nonfinite_neighbours(cuda):
     """A non-finite sbf row poisons only its own projection (the reference's lin_sbf is row-wise):
     the narrow-K kernel's LDS span has row stride K, so a row's pad columns alias the next row."""

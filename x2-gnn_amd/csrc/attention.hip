@@ -957,10 +957,8 @@ constexpr int kSPWaves = 16;           // 1024-thread workgroups, one per CU
 constexpr int kSPChunks = 16 * kS / 4;  // 16-byte chunks per 16-row sbf block (168)
 
 template <int NOB>
-__global__ void __launch_bounds__(kSPWaves * 64) sbf_project_waves(const float* __restrict__ sbf,
-                                                                  const float* __restrict__ w,
-                                                                  const float* __restrict__ b, int64_t T,
-                                                                  float* __restrict__ out) {
+__device__ __forceinline__ void sbf_project_body(const float* __restrict__ sbf, const float* __restrict__ w,
+                                                 const float* __restrict__ b, int64_t T, float* __restrict__ out) {
   typedef float f4t __attribute__((ext_vector_type(4)));
   __shared__ f4t Wl[NOB * kSPQ * 64];         // [ob][q][lane]: W[16ob + i][16q + 4g .. +3]
   __shared__ f4t Bl[NOB * 4];                 // [ob][g]: b[16ob + 4g .. +3]
@@ -1053,6 +1051,30 @@ __global__ void __launch_bounds__(kSPWaves * 64) sbf_project_waves(const float* 
     slot ^= 1;
   }
 }
+
+template <int NOB>
+__global__ void __launch_bounds__(kSPWaves * 64) sbf_project_waves(const float* __restrict__ sbf,
+                                                                  const float* __restrict__ w,
+                                                                  const float* __restrict__ b, int64_t T,
+                                                                  float* __restrict__ out) {
+  sbf_project_body<NOB>(sbf, w, b, T, out);
+}
+
+// Every layer's S = lin_sbf_l(sbf) in ONE launch (layer = blockIdx.y): one ramp and drain instead of
+// one per layer, and the layers after the first read sbf (33 MB at config 2) from the MALL, which the
+// first layer's pass has just filled, instead of from HBM.
+constexpr int kSPMaxLayers = X2G_SBF_PROJECT_MAX_LAYERS;
+struct SPBatch {
+  const float* w[kSPMaxLayers];
+  const float* b[kSPMaxLayers];
+  float* out[kSPMaxLayers];
+};
+template <int NOB>
+__global__ void __launch_bounds__(kSPWaves * 64) sbf_project_waves_batch(const float* __restrict__ sbf,
+                                                                        const SPBatch a, int64_t T) {
+  const int l = blockIdx.y;
+  sbf_project_body<NOB>(sbf, a.w[l], a.b[l], T, a.out[l]);
+}
 }  // namespace x2g
 
 X2G_API int x2g_sbf_project(const float* sbf, int64_t T, int32_t sbf_dim, const float* w_sbf, const float* b_sbf,
@@ -1089,6 +1111,35 @@ X2G_API int x2g_sbf_project(const float* sbf, int64_t T, int32_t sbf_dim, const 
     case 256: sbf_project_kernel<4><<<blocks, 256, 0, st>>>(sbf, w_sbf, b_sbf, T, out_dim, sbfproj); break;
     default: return X2G_EUNSUPPORTED;
   }
+  return last_launch_status();
+}
+
+X2G_API int x2g_sbf_project_batch(const float* sbf, int64_t T, int32_t sbf_dim, const float* const* w_sbf,
+                                  const float* const* b_sbf, int32_t n_layers, int32_t out_dim, float* const* sbfproj,
+                                  void* stream) {
+  if (T < 0 || out_dim <= 0 || sbf_dim <= 0 || n_layers < 1 || n_layers > kSPMaxLayers || !w_sbf || !b_sbf ||
+      !sbfproj)
+    return X2G_EINVAL;
+  if (T == 0) return X2G_OK;
+  bool fused = sbf_dim == kS && out_dim == 128 && sbf && reinterpret_cast<uintptr_t>(sbf) % 16 == 0;
+  SPBatch a{};
+  for (int l = 0; l < n_layers; ++l) {
+    if (!w_sbf[l] || !b_sbf[l] || !sbfproj[l]) return X2G_EINVAL;
+    fused = fused && reinterpret_cast<uintptr_t>(sbfproj[l]) % 16 == 0;
+    a.w[l] = w_sbf[l];
+    a.b[l] = b_sbf[l];
+    a.out[l] = sbfproj[l];
+  }
+  if (!fused) {  // other shapes / alignments: the single-layer entry per layer (same arithmetic)
+    for (int l = 0; l < n_layers; ++l)
+      if (int rc = x2g_sbf_project(sbf, T, sbf_dim, w_sbf[l], b_sbf[l], out_dim, sbfproj[l], stream)) return rc;
+    return X2G_OK;
+  }
+  const int64_t nblk = (T + 15) / 16;
+  int64_t want = (nblk + kSPWaves - 1) / kSPWaves;
+  want = want < 256 ? want : 256;
+  sbf_project_waves_batch<8><<<dim3(static_cast<unsigned>(want), static_cast<unsigned>(n_layers)), kSPWaves * 64, 0,
+                                as_stream(stream)>>>(sbf, a, T);
   return last_launch_status();
 }
 

@@ -204,20 +204,18 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
     X2G_FTR(kt, 1);
     if (tile + gridDim.x < ntiles) xtile_load(a, tile + gridDim.x, xt);  // in flight during the products
     // x * env in T layout: per 16-row tile and plane, float4 u of the 2048-float block holds
-    // feature u >> 2, rows 4 (u & 3) .. +3.  Thread tid writes float4 u = tid of the six (tile, plane)
-    // blocks, one per iteration of the first product's loop below (the tile image is read-only
-    // there): the 48 KB leave under the MFMAs instead of as a burst of their own before them (3 us
-    // of the 27 us per tile in the phase stamps, profiles/r4abl_trace_feat.txt).
-    auto xs_store = [&](int it) {  // (it wave-uniform)
-      const int rt = it / 3, p = it % 3;
+    // feature u >> 2, rows 4 (u & 3) .. +3.  (Issuing these 48 KB one piece per iteration of the first
+    // product's loop instead measured slower: profiles/r4f_ab_feat.txt, variant fnew vs fw2only.)
+    for (int idx = tid; idx < (a.want_t ? 2 * 3 * 512 : 0); idx += kFThreads) {
+      const int rt = idx / (3 * 512), p = (idx / 512) % 3, u = idx % 512;
       const int64_t t16 = r0 / 16 + rt;
-      if (!a.want_t || t16 * 16 >= R || 128 * p >= K) return;
-      const int f = tid >> 2, rr = 16 * rt + 4 * (tid & 3);
+      if (t16 * 16 >= R || 128 * p >= K) continue;
+      const int f = u >> 2, rr = 16 * rt + 4 * (u & 3);
       f4 v;
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = A[(rr + e) * kFAS + 128 * p + f] * envs[rr + e];
-      *reinterpret_cast<f4*>(a.xs_t + p * a.tf + t16 * 2048 + 4 * tid) = v;
-    };
+      *reinterpret_cast<f4*>(a.xs_t + p * a.tf + t16 * 2048 + 4 * u) = v;
+    }
     X2G_FTR(kt, 2);
     // z1 = env (x W1^T) + b1: wave w -> columns c1a, c1b, both 16-row blocks
     f4 acc[2][2] = {{zero4(), zero4()}, {zero4(), zero4()}};
@@ -245,49 +243,40 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
       a0 = n0;
       a1 = n1;
     };
-#ifdef FEAT_XS_FIRST
-    for (int it = 0; it < 6; ++it) xs_store(it);
-#endif
-#pragma unroll 1
     for (int q = 0; q < KQn; q += 2) {
-#ifndef FEAT_XS_FIRST
-      if (q < 12) xs_store(q >> 1);
-#endif
       group(q, wa0, wb0);
       if (q + 1 < KQn) group(q + 1, wa1, wb1);
     }
-    for (int it = (KQn + 1) / 2; it < 6; ++it) xs_store(it);  // (K <= 160: fewer loop iterations than blocks)
     X2G_FTR(kt, 3);
     f4 wq[3];  // the second product's first two W2 groups, in flight under the epilogue and barrier
     wq[0] = *reinterpret_cast<const f4*>(w2s);
     wq[1] = *reinterpret_cast<const f4*>(w2s + 16);
-    // epilogue 1: SiLU(z1) to LDS; z1 / SiLU(z1) stay in registers and leave in T layout (rows past
-    // R zero) under the second product's MFMAs — as one burst before the barrier they were most of
-    // this phase's 5 us per tile (profiles/r4abl_trace_feat.txt)
-    f4 z1v[2][2], y1v[2][2];
+    // epilogue 1: z1 / SiLU(z1) to T layout (rows past R zero) and SiLU(z1) to LDS.  (Holding z1 / SiLU(z1)
+    // in registers and storing them under the second product's MFMAs measured slower:
+    // profiles/r4f_ab_feat.txt, variant fnew vs fnot1.)
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
+      const int64_t t16 = r0 / 16 + rb;
+      const bool tile_ok = t16 * 16 < R;
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
         const int c = cb ? c1b : c1a;
         const float bias = cb ? b1b : b1a;
+        f4 z, y;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = 16 * rb + 4 * g + e;
           const bool ok = r < nr;
-          z1v[rb][cb][e] = ok ? fmaf(acc[rb][cb][e], envs[r], bias) : 0.0f;  // (x * env) W^T = env (x W^T)
-          y1v[rb][cb][e] = ok ? silu_(z1v[rb][cb][e]) : 0.0f;
-          Y1[r * kFYS + c] = y1v[rb][cb][e];
+          z[e] = ok ? fmaf(acc[rb][cb][e], envs[r], bias) : 0.0f;  // (x * env) W^T = env (x W^T)
+          y[e] = ok ? silu_(z[e]) : 0.0f;
+          Y1[r * kFYS + c] = y[e];
+        }
+        if (tile_ok && a.want_t) {
+          *reinterpret_cast<f4*>(a.z1_t + tpos(a.tf, t16, c, g)) = z;
+          *reinterpret_cast<f4*>(a.y1_t + tpos(a.tf, t16, c, g)) = y;
         }
       }
     }
-    auto t1_store = [&](int k) {  // store k of 8: (block, column block, z or y)
-      const int rb = k >> 2, cb = (k >> 1) & 1, zy = k & 1;
-      const int64_t t16 = r0 / 16 + rb;
-      if (t16 * 16 >= R || !a.want_t) return;
-      const int c = cb ? c1b : c1a;
-      *reinterpret_cast<f4*>((zy ? a.y1_t : a.z1_t) + tpos(a.tf, t16, c, g)) = zy ? y1v[rb][cb] : z1v[rb][cb];
-    };
     __syncthreads();
     X2G_FTR(kt, 4);
     // z2 = SiLU(z1) W2^T + b2: wave w -> columns 16w + i
@@ -297,9 +286,6 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
       f4 y1 = *reinterpret_cast<const f4*>(Y1 + (16 + i) * kFYS + 4 * g);
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-#ifndef FEAT_NO_T1DEFER
-        if (q < 8) t1_store(q);
-#endif
         const int qa = q + 1 < 16 ? q + 1 : q;
         const f4 n0 = *reinterpret_cast<const f4*>(Y1 + i * kFYS + 16 * qa + 4 * g);
         const f4 n1 = *reinterpret_cast<const f4*>(Y1 + (16 + i) * kFYS + 16 * qa + 4 * g);

@@ -366,7 +366,7 @@ __global__ void transpose_sym_kernel(const int32_t* __restrict__ src, const int3
 
 using namespace x2g;
 
-X2G_API int x2g_abi_version(void) { return 11; }
+X2G_API int x2g_abi_version(void) { return 12; }
 
 X2G_API const char* x2g_status_string(int status) {
   switch (status) {

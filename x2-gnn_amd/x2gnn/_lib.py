@@ -104,6 +104,7 @@ SIGNATURES = {
     "x2g_dense_bwd_splits": [_I64, _I32, _I32],
     "x2g_dense_bwd_slab_offset": [_I64, _I32, _I32],
     "x2g_sbf_project": [_P, _I64, _I32, _P, _P, _I32, _P, _P],
+    "x2g_sbf_project_batch": [_P, _I64, _I32, _P, _P, _I32, _I32, _P, _P],
     "x2g_clip_adam_ema": [_P, _P, _P, _P, _P, _I64, _P, _P, _SZ, _P],
     "x2g_dense_bwd_ex": [_P, _P, ctypes.c_int, _P, _P, _I64, _I32, _I32, _P, _P, _P, _P, ctypes.c_int, _P, _SZ,
                          _P],

@@ -116,21 +116,31 @@ class _Trunk(nn.Module):
             data.node_rbf._x2g_fanin = ops.FanIn()
             out._x2g_fanin = ops.FanIn()
         readout(0, out)
-        for i in range(self.conv_layers):
-            res0 = out
-            out = self.convs[i](sbf=data.edge_sbf, rbf=data.node_rbf, x=out, edge_index=data._store.get("edge_index"),
-                                edge_attr=edge_attr, line_graph=plan.lg, edge_row=edge_row,
-                                edge_proj=edge_proj[i] if edge_proj is not None else None)
-            stats = getattr(out, "_x2g_rowstats", None)
-            if stats is not None and self._ln_fusable(out, i):
-                # the LayerNorm runs inside the tail's row chain, from the conv's per-row statistics
-                out = self._tail(i, out, res0, ln=(stats, plan.line_ptr, plan.num_graphs, self.LayerNorm.eps))
-            else:
-                out = self.LayerNorm(out, rowptr=plan.line_ptr, num_graphs=plan.num_graphs)
-                out = self._tail(i, out, res0)
-            if fan:
-                out._x2g_fanin = ops.FanIn()
-            readout(i + 1, out)
+        sbf = data.edge_sbf
+        if sbf is not None and sbf.is_cuda and plan.lg is not None and (torch.is_grad_enabled() or
+                                                                         plan.lg.T <= ops.INFER_TILE):
+            # every layer's S = lin_sbf(sbf) in one launch before the first layer (the layers take theirs)
+            ops.sbf_project_all(sbf, [c.lin_sbf.weight for c in self.convs], [c.lin_sbf.bias for c in self.convs],
+                                plan.lg)
+        try:
+            for i in range(self.conv_layers):
+                res0 = out
+                out = self.convs[i](sbf=sbf, rbf=data.node_rbf, x=out, edge_index=data._store.get("edge_index"),
+                                    edge_attr=edge_attr, line_graph=plan.lg, edge_row=edge_row,
+                                    edge_proj=edge_proj[i] if edge_proj is not None else None)
+                stats = getattr(out, "_x2g_rowstats", None)
+                if stats is not None and self._ln_fusable(out, i):
+                    # the LayerNorm runs inside the tail's row chain, from the conv's per-row statistics
+                    out = self._tail(i, out, res0, ln=(stats, plan.line_ptr, plan.num_graphs, self.LayerNorm.eps))
+                else:
+                    out = self.LayerNorm(out, rowptr=plan.line_ptr, num_graphs=plan.num_graphs)
+                    out = self._tail(i, out, res0)
+                if fan:
+                    out._x2g_fanin = ops.FanIn()
+                readout(i + 1, out)
+        finally:
+            if plan.lg is not None:
+                ops.clear_sproj(plan.lg)
         if pooled_xs is not None:
             feats = pool_fn(pooled_xs)
             if feats is None:

@@ -291,6 +291,53 @@ def _sbf_factors(lg, sbf, edge_mode, D, edge, edge_row):
     return fac[1], fac[2]
 
 
+SBF_PROJECT_MAX_LAYERS = 8  # X2G_SBF_PROJECT_MAX_LAYERS
+
+
+def _sproj_key(sbf, w, b):
+    return (sbf.data_ptr(), w.data_ptr(), b.data_ptr())
+
+
+def sbf_project_all(sbf, weights, biases, lg):
+    """S_l = sbf W_l^T + b_l for every layer's lin_sbf in ONE launch (x2g_sbf_project_batch: one ramp
+    and drain instead of one per layer; the later layers read sbf from the MALL the first one filled),
+    left on the line graph for the layers' attention calls (each S taken once, by the call whose sbf and
+    parameters it was projected from).  The caller clears what is left (``clear_sproj``), so an S
+    projected before a weight update can never be read after it."""
+    sbf = _f32(sbf)
+    T, K = sbf.shape
+    n = len(weights)
+    if n == 0 or n > SBF_PROJECT_MAX_LAYERS or T == 0:
+        return
+    if any(w.dtype != torch.float32 or not w.is_contiguous() for w in weights) or \
+            any(b is None or b.dtype != torch.float32 or not b.is_contiguous() for b in biases):
+        return  # (keys are the parameters' own pointers)
+    D = int(weights[0].shape[0])
+    if any(int(w.shape[0]) != D or int(w.shape[1]) != K for w in weights):
+        return
+    outs = [torch.empty(T, D, dtype=torch.float32, device=sbf.device) for _ in weights]
+    P = ctypes.c_void_p * n
+    call("x2g_sbf_project_batch", ptr(sbf), T, K, P(*[w.data_ptr() for w in weights]),
+         P(*[b.data_ptr() for b in biases]), n, D, P(*[o.data_ptr() for o in outs]), stream_ptr())
+    cache = lg.__dict__.setdefault("_x2g_sproj", {})
+    for w, b, o in zip(weights, biases, outs):
+        cache[_sproj_key(sbf, w, b)] = o
+
+
+def clear_sproj(lg):
+    cache = getattr(lg, "_x2g_sproj", None)
+    if cache:
+        cache.clear()
+
+
+def _take_sproj(lg, sbf, w, b, T, D):
+    cache = getattr(lg, "_x2g_sproj", None)
+    if not cache or b is None:
+        return None
+    s = cache.pop(_sproj_key(sbf, w, b), None)
+    return s if s is not None and tuple(s.shape) == (T, D) else None
+
+
 class _SBFAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row, heads, channels):
@@ -310,9 +357,12 @@ class _SBFAttention(torch.autograd.Function):
         smax = torch.empty(E, heads, dtype=torch.float32, device=dev)
         sden = torch.empty(E, heads, dtype=torch.float32, device=dev)
         # S = lin_sbf(sbf) once per layer [T, D]; the three attention kernels read its rows
-        # (sbf pointer = S, weight pointer NULL) instead of re-projecting per triplet
-        sproj = torch.empty(T, D, dtype=torch.float32, device=dev)
-        call("x2g_sbf_project", ptr(sbf), T, sbf.shape[1], ptr(w_sbf), ptr(b_sbf), D, ptr(sproj), stream_ptr())
+        # (sbf pointer = S, weight pointer NULL) instead of re-projecting per triplet.  The trunk
+        # projects every layer's S in one launch before its first layer (sbf_project_all): take it
+        sproj = _take_sproj(lg, sbf, w_sbf, b_sbf, T, D)
+        if sproj is None:
+            sproj = torch.empty(T, D, dtype=torch.float32, device=dev)
+            call("x2g_sbf_project", ptr(sbf), T, sbf.shape[1], ptr(w_sbf), ptr(b_sbf), D, ptr(sproj), stream_ptr())
         # per-row (mean, M2) of the output for a graph LayerNorm fused into the next row chain
         rstats = torch.empty(E, 2, dtype=torch.float32, device=dev) if _LN_FUSE and D == 128 else None
         call("x2g_sbf_attention_fwd_stats" if rstats is not None else "x2g_sbf_attention_fwd", ptr(q), ptr(k), ptr(v),
