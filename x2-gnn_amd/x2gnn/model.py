@@ -117,11 +117,9 @@ class _Trunk(nn.Module):
             out._x2g_fanin = ops.FanIn()
         readout(0, out)
         sbf = data.edge_sbf
-        if sbf is not None and sbf.is_cuda and plan.lg is not None and (torch.is_grad_enabled() or
-                                                                         plan.lg.T <= ops.INFER_TILE):
-            # every layer's S = lin_sbf(sbf) in one launch before the first layer (the layers take theirs)
-            ops.sbf_project_all(sbf, [c.lin_sbf.weight for c in self.convs], [c.lin_sbf.bias for c in self.convs],
-                                plan.lg)
+        # (every layer's S projected up front in one launch, ops.sbf_project_all, measured 1.2 % slower in
+        # the step A/B, profiles/r4ab1_step_ab_sbatch_feat.log: each layer's S written right before its
+        # attention is still in the MALL when the attention reads it; projected 3 layers early it is not)
         try:
             for i in range(self.conv_layers):
                 res0 = out
