@@ -367,6 +367,10 @@ int x2g_graph_layernorm_bwd_rows(const float* out, const float* dout, const floa
 int x2g_smooth_l1_mean_fwd(const float* pred, const float* target, int64_t n, float beta, float* out, void* stream);
 int x2g_smooth_l1_mean_bwd(const float* pred, const float* target, int64_t n, float beta, const float* gout,
                            float* dpred, void* stream);
+/* The forward that also writes dpred_unit = the backward's dpred for gout[0] = 1 (bit for bit): a
+ * training step whose backward seed is 1 (trainer.py:42, loss.backward()) then needs no backward launch. */
+int x2g_smooth_l1_mean_fwd_grad(const float* pred, const float* target, int64_t n, float beta, float* out,
+                                float* dpred_unit, void* stream);
 
 /* ---------------------------------------------------------------- dense-layer gradients */
 

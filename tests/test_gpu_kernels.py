@@ -1662,3 +1662,27 @@ def test_smooth_l1_mean_vs_torch(cuda, n, beta):
     loss.backward(up)
     ref.backward(up)
     torch.testing.assert_close(pred.grad, ref_pred.grad, rtol=1e-6, atol=1e-8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 128, 1000])
+def test_smooth_l1_unit_seed_gradient_equals_backward_kernel(cuda, n):
+    """ops.smooth_l1_loss(unit_seed=s): the forward launch writes d loss / d pred for the seed s (== 1) and
+    the backward handed s returns it without a launch — bitwise the backward kernel's gradient for a
+    ones seed; any other seed object still takes the kernel (the Trainer's step, train.py)."""
+    from x2gnn import ops
+
+    g = torch.Generator(device=cuda).manual_seed(n + 1)
+    base = 3 * torch.randn(n, device=cuda, generator=g)
+    target = torch.randn(n, device=cuda, generator=g)
+    seed = torch.ones((), device=cuda)
+    p1, p2, p3 = (base.clone().requires_grad_(True) for _ in range(3))
+    l1 = ops.smooth_l1_loss(p1, target, unit_seed=seed)
+    l2 = ops.smooth_l1_loss(p2, target)
+    assert torch.equal(l1, l2)
+    torch.autograd.backward(l1, seed)
+    torch.autograd.backward(l2, torch.ones((), device=cuda))
+    assert torch.equal(p1.grad, p2.grad)
+    l3 = ops.smooth_l1_loss(p3, target, unit_seed=seed)
+    torch.autograd.backward(l3, torch.full((), 0.5, device=cuda))  # not the seed object: the kernel
+    torch.testing.assert_close(p3.grad, 0.5 * p2.grad, rtol=0, atol=0)

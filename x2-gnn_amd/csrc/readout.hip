@@ -186,14 +186,19 @@ namespace x2g {
 namespace {
 constexpr int kLossThreads = 256;
 
+// dpred (optional): the gradient for d loss = 1 (the backward kernel's values for gout = 1, same
+// expression), written by the same pass
 __global__ void __launch_bounds__(kLossThreads) smooth_l1_mean_fwd_kernel(const float* __restrict__ pred,
                                                                           const float* __restrict__ target, int64_t n,
-                                                                          float beta, float* __restrict__ out) {
+                                                                          float beta, float* __restrict__ out,
+                                                                          float* __restrict__ dpred) {
   __shared__ float red[kLossThreads / 64];
   float s = 0.f;
+  const float g = 1.0f / static_cast<float>(n);
   for (int64_t i = threadIdx.x; i < n; i += kLossThreads) {
     const float d = pred[i] - target[i], a = fabsf(d);
     s += a < beta ? 0.5f * d * d / beta : a - 0.5f * beta;
+    if (dpred) dpred[i] = g * (d < -beta ? -1.f : (d > beta ? 1.f : d / beta));
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
@@ -224,7 +229,16 @@ __global__ void __launch_bounds__(kLossThreads) smooth_l1_mean_bwd_kernel(const 
 X2G_API int x2g_smooth_l1_mean_fwd(const float* pred, const float* target, int64_t n, float beta, float* out,
                                    void* stream) {
   if (n <= 0 || !pred || !target || !out || !(beta > 0.f)) return X2G_EINVAL;
-  x2g::smooth_l1_mean_fwd_kernel<<<1, x2g::kLossThreads, 0, as_stream(stream)>>>(pred, target, n, beta, out);
+  x2g::smooth_l1_mean_fwd_kernel<<<1, x2g::kLossThreads, 0, as_stream(stream)>>>(pred, target, n, beta, out,
+                                                                                 nullptr);
+  return last_launch_status();
+}
+
+X2G_API int x2g_smooth_l1_mean_fwd_grad(const float* pred, const float* target, int64_t n, float beta, float* out,
+                                        float* dpred_unit, void* stream) {
+  if (n <= 0 || !pred || !target || !out || !dpred_unit || !(beta > 0.f)) return X2G_EINVAL;
+  x2g::smooth_l1_mean_fwd_kernel<<<1, x2g::kLossThreads, 0, as_stream(stream)>>>(pred, target, n, beta, out,
+                                                                                 dpred_unit);
   return last_launch_status();
 }
 

@@ -87,6 +87,7 @@ SIGNATURES = {
     "x2g_graph_layernorm_bwd_workspace": [_I64],
     "x2g_chain_fwd_batch": [_P, _I32, _I32, _I64, _I32, _P],
     "x2g_smooth_l1_mean_fwd": [_P, _P, _I64, _F, _P, _P],
+    "x2g_smooth_l1_mean_fwd_grad": [_P, _P, _I64, _F, _P, _P, _P],
     "x2g_smooth_l1_mean_bwd": [_P, _P, _I64, _F, _P, _P, _P],
     "x2g_chain_bwd_batch": [_P, _I32, _I32, _I64, _I32, _P],
     "x2g_graph_layernorm_bwd_ex": [_P, _P, _P, _P, _I64, _I64, _P, _P, _SZ, _P],

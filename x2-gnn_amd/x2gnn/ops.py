@@ -2235,26 +2235,39 @@ class _SmoothL1MeanFn(torch.autograd.Function):
     elementwise; the target takes no gradient (the reference's labels)."""
 
     @staticmethod
-    def forward(ctx, pred, target, beta):
+    def forward(ctx, pred, target, beta, unit_seed):
         p, t = _f32(pred).reshape(-1), _f32(target).reshape(-1)
         out = torch.empty((), dtype=torch.float32, device=p.device)
-        call("x2g_smooth_l1_mean_fwd", ptr(p), ptr(t), p.numel(), float(beta), ptr(out), stream_ptr())
+        ctx.unit_seed, ctx.dp_unit = unit_seed, None
+        if unit_seed is not None:  # the gradient for a backward seeded with `unit_seed` (== 1) in the same pass
+            ctx.dp_unit = torch.empty_like(p)
+            call("x2g_smooth_l1_mean_fwd_grad", ptr(p), ptr(t), p.numel(), float(beta), ptr(out), ptr(ctx.dp_unit),
+                 stream_ptr())
+        else:
+            call("x2g_smooth_l1_mean_fwd", ptr(p), ptr(t), p.numel(), float(beta), ptr(out), stream_ptr())
         ctx.save_for_backward(p, t)
         ctx.beta, ctx.shape = float(beta), pred.shape
         return out
 
     @staticmethod
     def backward(ctx, g):
+        if ctx.dp_unit is not None and g is ctx.unit_seed:  # autograd hands the caller's seed object through
+            return ctx.dp_unit.view(ctx.shape), None, None, None
         p, t = ctx.saved_tensors
         dp = torch.empty_like(p)
         call("x2g_smooth_l1_mean_bwd", ptr(p), ptr(t), p.numel(), ctx.beta, ptr(_f32(g).reshape(1)), ptr(dp),
              stream_ptr())
-        return dp.view(ctx.shape), None, None
+        return dp.view(ctx.shape), None, None, None
 
 
-def smooth_l1_loss(pred, target, beta: float = 1.0):
-    """torch.nn.functional.smooth_l1_loss(pred, target, beta=beta) (mean) on the device path."""
+def smooth_l1_loss(pred, target, beta: float = 1.0, unit_seed=None):
+    """torch.nn.functional.smooth_l1_loss(pred, target, beta=beta) (mean) on the device path.
+
+    ``unit_seed``: a persistent ones scalar the caller will pass to ``torch.autograd.backward(loss,
+    unit_seed)`` (x2gnn.train.Trainer's ``seed``): the forward launch then also writes the gradient for
+    that seed, and the backward, handed that very object, returns it without a launch (any other
+    gradient takes the backward kernel, so the result is the same either way, bit for bit)."""
     if (not pred.is_cuda or pred.shape != target.shape or pred.numel() == 0 or target.requires_grad
             or beta <= 0):  # beta <= 0 is torch's L1 branch, not compiled
         return torch.nn.functional.smooth_l1_loss(pred, target, beta=beta)
-    return _SmoothL1MeanFn.apply(pred, target, beta)
+    return _SmoothL1MeanFn.apply(pred, target, beta, unit_seed)

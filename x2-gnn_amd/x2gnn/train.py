@@ -72,7 +72,8 @@ class Trainer:
         self.grads_zeroed = False
         self.model.train()  # trainer.py:30 (an Inference sharing the model may have left it in eval)
         res = self.model(batch)
-        loss = ops.smooth_l1_loss(res, batch.y)  # trainer.py:41, one launch each way
+        # trainer.py:41; the loss launch also writes d loss / d res for the seed (no backward launch)
+        loss = ops.smooth_l1_loss(res, batch.y, unit_seed=self.seed)
         with ops.deferred_wgrad() as d:  # all layers' weight-gradient slab sums in one launch
             torch.autograd.backward(loss, self.seed)
         self.flat_launches = d.flat_launches
