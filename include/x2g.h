@@ -549,6 +549,16 @@ int32_t x2g_readout_head_bwd_splits(int64_t rows);
 int x2g_readout_head_bwd(const float* dout, const x2g_head_group* groups, int32_t num_groups, int64_t rows,
                          int32_t dim, int flags, void* workspace, size_t workspace_bytes, void* stream);
 
+/* The heads with the per-molecule sum fused (AtomWise's per-atom outputs pooled by the global add pool,
+ * model.py:53): out_seg[m] = sum over rows r of segment m (seg_rowptr[m] .. seg_rowptr[m+1]) of
+ * sum_g (h_g[r] . w_g + b_g); and the backward from d out_seg (dh_g[r] = dout_seg[seg(r)] w_g, dw_g / db_g as
+ * x2g_readout_head_bwd, same workspace).  One launch each way instead of head + pool / broadcast + head. */
+int x2g_readout_head_pool_fwd(const x2g_head_group* groups, int32_t num_groups, int64_t rows, int32_t dim,
+                              const int32_t* seg_rowptr, int64_t num_segments, float* out_seg, void* stream);
+int x2g_readout_head_pool_bwd(const float* dout_seg, const int32_t* seg_rowptr, int64_t num_segments,
+                              const x2g_head_group* groups, int32_t num_groups, int64_t rows, int32_t dim, int flags,
+                              void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------- parameter update */
 
 /* float[16] device scalar block of x2g_clip_adam_ema: the caller sets the hyper-parameters,

@@ -1105,6 +1105,39 @@ def test_readout_mlps_batched_vs_separate(cuda, R, G):
             torch.testing.assert_close(p.grad, q.grad, rtol=1e-4, atol=1e-4, msg=n)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("sizes,G", [([18] * 128, 5), ([1], 1), ([5, 0, 40, 1, 3], 3), ([300, 2, 61], 8)])
+def test_readout_heads_pooled_vs_pool_after(cuda, sizes, G):
+    """ops.readout_mlps(pool=(mol_ptr, B)): the heads with the global add pool fused (x2g_readout_head_pool_*,
+    model.py:53) equal the per-row heads followed by ops.segment_sum — values, every feature gradient and
+    every parameter gradient (fp32 reassociation: the pooled sum runs in a different order); segments of
+    0, 1 and > 256 rows."""
+    from x2gnn import ops
+    from x2gnn.layers import _mlp
+
+    R = sum(sizes)
+    torch.manual_seed(R + G)
+    mlps = [_mlp(128, 1, 3).to(cuda) for _ in range(G)]
+    mlps_ref = [_mlp(128, 1, 3).to(cuda) for _ in range(G)]
+    for a, b in zip(mlps, mlps_ref):
+        b.load_state_dict(a.state_dict())
+    ptr = torch.tensor([0] + list(torch.tensor(sizes).cumsum(0)), dtype=torch.int32, device=cuda)
+    feats = [torch.randn(R, 128, device=cuda, requires_grad=True) for _ in range(G)]
+    feats_ref = [f.detach().clone().requires_grad_(True) for f in feats]
+    out = ops.readout_mlps(feats, mlps, pool=(ptr, len(sizes)))
+    ref = ops.segment_sum(ops.readout_mlps(feats_ref, mlps_ref), ptr, len(sizes))
+    assert out.shape == ref.shape == (len(sizes), 1)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+    up = torch.randn(len(sizes), 1, device=cuda)
+    out.backward(up)
+    ref.backward(up)
+    for f, fr in zip(feats, feats_ref):
+        torch.testing.assert_close(f.grad, fr.grad, rtol=1e-5, atol=1e-6)
+    for a, b in zip(mlps, mlps_ref):
+        for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
+            torch.testing.assert_close(p.grad, q.grad, rtol=1e-4, atol=1e-5, msg=n)
+
+
 @pytest.mark.parametrize("R,D", [(1, 128), (33, 128), (21058, 128), (500, 64), (77, 12)])
 def test_fused_residual_layer_vs_torch(cuda, R, D):
     """x2g_residual_fwd (both GEMMs of a ResidualLayer in one kernel) + the layer's backward vs

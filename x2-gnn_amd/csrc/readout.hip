@@ -36,10 +36,56 @@ __global__ void __launch_bounds__(256) readout_head_fwd_kernel(const HeadBatch b
   }
 }
 
-// block k owns rows [k * per, (k + 1) * per); partial slabs: part[g][k][D] and part[g][splits*D + k]
+// The heads with the per-molecule sum fused (model.py:53, the global add pool after AtomWise): one
+// workgroup per segment of rows; wave w takes the segment's rows w*RPW .. in turns, each row's heads
+// summed in job order, then the waves' sums in wave order (fixed order: deterministic).  Replaces the
+// head launch + the pooling launch.
+template <int LPR>
+__global__ void __launch_bounds__(256) readout_head_pool_fwd_kernel(const HeadBatch b, int G,
+                                                                    const int32_t* __restrict__ seg_rowptr,
+                                                                    int64_t n_seg, float* __restrict__ out) {
+  constexpr int RPW = 64 / LPR;
+  __shared__ float red[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, sub = lane % LPR;
+  for (int64_t m = blockIdx.x; m < n_seg; m += gridDim.x) {
+    const int r0 = seg_rowptr[m], r1 = seg_rowptr[m + 1];
+    float acc = 0.f;
+    for (int r = r0 + wv * RPW + lane / LPR; r < r1; r += 4 * RPW) {
+      float rowv = 0.f;
+      for (int g = 0; g < G; ++g) {
+        const f4h hv = reinterpret_cast<const f4h*>(b.g[g].h)[static_cast<int64_t>(r) * LPR + sub];
+        const f4h wv4 = reinterpret_cast<const f4h*>(b.g[g].w)[sub];
+        float d = hv.x * wv4.x + hv.y * wv4.y + hv.z * wv4.z + hv.w * wv4.w;
+        d = group_sum<LPR>(d);
+        rowv += d + (b.g[g].b ? b.g[g].b[0] : 0.f);
+      }
+      acc += sub == 0 ? rowv : 0.f;
+    }
+    acc = wave64_sum(acc);
+    if (lane == 0) red[wv] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) out[m] = ((red[0] + red[1]) + red[2]) + red[3];
+    __syncthreads();
+  }
+}
+
+// the segment of row r: the last s with seg_rowptr[s] <= r (segments cover every row)
+__device__ __forceinline__ int64_t seg_of_row(const int32_t* __restrict__ seg_rowptr, int64_t n_seg, int64_t r) {
+  int64_t lo = 0, hi = n_seg;  // seg_rowptr[lo] <= r < seg_rowptr[hi]
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (seg_rowptr[mid] <= r) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// block k owns rows [k * per, (k + 1) * per); partial slabs: part[g][k][D] and part[g][splits*D + k].
+// seg_rowptr (or NULL): dout is per segment of rows (the fused pool's gradient, broadcast here)
 template <int LPR>
 __global__ void __launch_bounds__(256) readout_head_bwd_kernel(const float* __restrict__ dout, const HeadBatch b, int G,
-                                                               int64_t R, float* __restrict__ part) {
+                                                               int64_t R, float* __restrict__ part,
+                                                               const int32_t* __restrict__ seg_rowptr,
+                                                               int64_t n_seg) {
   constexpr int RPB = 256 / LPR;
   constexpr int D = 4 * LPR;
   __shared__ f4h red[RPB * LPR];
@@ -61,7 +107,7 @@ __global__ void __launch_bounds__(256) readout_head_bwd_kernel(const float* __re
       for (int u = 0; u < U; ++u) {
         const int64_t r = r0 + static_cast<int64_t>(u) * RPB;
         const int64_t rc = r < hi ? r : lo;
-        dv[u] = dout[rc];
+        dv[u] = dout[seg_rowptr ? seg_of_row(seg_rowptr, n_seg, rc) : rc];
         hv[u] = reinterpret_cast<const f4h*>(b.g[g].h)[rc * LPR + sub];
       }
 #pragma unroll
@@ -142,8 +188,8 @@ X2G_API size_t x2g_readout_head_bwd_workspace(int64_t R, int32_t D, int32_t G) {
   return static_cast<size_t>(G) * head_splits(R) * (D + 1) * sizeof(float);
 }
 
-X2G_API int x2g_readout_head_bwd(const float* dout, const x2g_head_group* groups, int32_t G, int64_t R, int32_t D,
-                                 int flags, void* ws, size_t wsb, void* stream) {
+static int head_bwd(const float* dout, const int32_t* seg_rowptr, int64_t n_seg, const x2g_head_group* groups,
+                    int32_t G, int64_t R, int32_t D, int flags, void* ws, size_t wsb, void* stream) {
   if (R < 0 || !groups) return X2G_EINVAL;
   if (!head_ok(groups, G, D)) return X2G_EUNSUPPORTED;
   for (int g = 0; g < G; ++g)
@@ -166,7 +212,7 @@ X2G_API int x2g_readout_head_bwd(const float* dout, const x2g_head_group* groups
   for (int g = 0; g < G; ++g) b.g[g] = groups[g];
   const int splits = head_splits(R);
   float* part = static_cast<float*>(ws);
-  X2G_HEAD_DISPATCH(readout_head_bwd_kernel, dim3(splits, G), dout, b, G, R, part)
+  X2G_HEAD_DISPATCH(readout_head_bwd_kernel, dim3(splits, G), dout, b, G, R, part, seg_rowptr, n_seg)
   if (int rc = last_launch_status()) return rc;
   if (flags & X2G_DEFER_SLAB_SUM) return X2G_OK;
   x2g_slab_job jobs[X2G_MAX_GROUPS];
@@ -176,6 +222,31 @@ X2G_API int x2g_readout_head_bwd(const float* dout, const x2g_head_group* groups
                            groups[g].db, D, groups[g].db ? 1 : 0, splits};
   }
   return x2g_slab_sum_batch(jobs, G, accum ? 1 : 0, stream);
+}
+
+X2G_API int x2g_readout_head_bwd(const float* dout, const x2g_head_group* groups, int32_t G, int64_t R, int32_t D,
+                                 int flags, void* ws, size_t wsb, void* stream) {
+  return head_bwd(dout, nullptr, 0, groups, G, R, D, flags, ws, wsb, stream);
+}
+
+X2G_API int x2g_readout_head_pool_fwd(const x2g_head_group* groups, int32_t G, int64_t R, int32_t D,
+                                      const int32_t* seg_rowptr, int64_t n_seg, float* out_seg, void* stream) {
+  if (R < 0 || n_seg < 0 || !groups || !out_seg || (n_seg > 0 && !seg_rowptr)) return X2G_EINVAL;
+  if (!head_ok(groups, G, D)) return X2G_EUNSUPPORTED;
+  if (n_seg == 0) return X2G_OK;
+  HeadBatch b{};
+  for (int g = 0; g < G; ++g) b.g[g] = groups[g];
+  hipStream_t st = as_stream(stream);
+  const unsigned grid = static_cast<unsigned>(n_seg < 65535 ? n_seg : 65535);
+  X2G_HEAD_DISPATCH(readout_head_pool_fwd_kernel, grid, b, G, seg_rowptr, n_seg, out_seg)
+  return last_launch_status();
+}
+
+X2G_API int x2g_readout_head_pool_bwd(const float* dout_seg, const int32_t* seg_rowptr, int64_t n_seg,
+                                      const x2g_head_group* groups, int32_t G, int64_t R, int32_t D, int flags,
+                                      void* ws, size_t wsb, void* stream) {
+  if (n_seg < 0 || (R > 0 && (n_seg < 1 || !seg_rowptr))) return X2G_EINVAL;
+  return head_bwd(dout_seg, seg_rowptr, n_seg, groups, G, R, D, flags, ws, wsb, stream);
 }
 
 // ---------------------------------------------------------------- loss (trainer.py:41)

@@ -38,6 +38,8 @@ SIGNATURES = {
     "x2g_dense_fwd_batched": [_P, _I32, _I64, _I32, _I32, ctypes.c_int, _P],
     "x2g_dense_bwd_batched": [_P, _I32, _I64, _I32, _I32, ctypes.c_int, ctypes.c_int, _P, _SZ, _P],
     "x2g_readout_head_fwd": [_P, _I32, _I64, _I32, _P, _P],
+    "x2g_readout_head_pool_fwd": [_P, _I32, _I64, _I32, _P, _I64, _P, _P],
+    "x2g_readout_head_pool_bwd": [_P, _P, _I64, _P, _I32, _I64, _I32, ctypes.c_int, _P, _SZ, _P],
     "x2g_readout_head_bwd_workspace": [_I64, _I32, _I32],
     "x2g_readout_head_bwd_splits": [_I64],
     "x2g_readout_head_bwd": [_P, _P, _I32, _I64, _I32, ctypes.c_int, _P, _SZ, _P],

@@ -79,7 +79,9 @@ class _Trunk(nn.Module):
         return ([(mods[0], ops.ACT_SILU, -1), (mods[2], ops.ACT_NONE, 0)]
                 + [(c.lin_edge, ops.ACT_NONE, 1) for c in self.convs])
 
-    def _layers(self, data, plan, readout_fn, feature_fn=None, pool_fn=None):
+    def _layers(self, data, plan, readout_fn, feature_fn=None, pool_fn=None, pool_out=None):
+        """The conv layers with their readouts; ``pool_out = (seg_rowptr, S)``: the batched readout heads
+        may sum the per-atom results per molecule themselves (the result then carries ``_x2g_pooled``)."""
         per_dst = "edge_attr_row" in data._store
         edge_proj = data._store.get("_x2g_edge_proj") if per_dst else None
         # lin_edge tables precomputed by the featurisation's table chain, or edgenn here
@@ -120,25 +122,21 @@ class _Trunk(nn.Module):
         # (every layer's S projected up front in one launch, ops.sbf_project_all, measured 1.2 % slower in
         # the step A/B, profiles/r4ab1_step_ab_sbatch_feat.log: each layer's S written right before its
         # attention is still in the MALL when the attention reads it; projected 3 layers early it is not)
-        try:
-            for i in range(self.conv_layers):
-                res0 = out
-                out = self.convs[i](sbf=sbf, rbf=data.node_rbf, x=out, edge_index=data._store.get("edge_index"),
-                                    edge_attr=edge_attr, line_graph=plan.lg, edge_row=edge_row,
-                                    edge_proj=edge_proj[i] if edge_proj is not None else None)
-                stats = getattr(out, "_x2g_rowstats", None)
-                if stats is not None and self._ln_fusable(out, i):
-                    # the LayerNorm runs inside the tail's row chain, from the conv's per-row statistics
-                    out = self._tail(i, out, res0, ln=(stats, plan.line_ptr, plan.num_graphs, self.LayerNorm.eps))
-                else:
-                    out = self.LayerNorm(out, rowptr=plan.line_ptr, num_graphs=plan.num_graphs)
-                    out = self._tail(i, out, res0)
-                if fan:
-                    out._x2g_fanin = ops.FanIn()
-                readout(i + 1, out)
-        finally:
-            if plan.lg is not None:
-                ops.clear_sproj(plan.lg)
+        for i in range(self.conv_layers):
+            res0 = out
+            out = self.convs[i](sbf=sbf, rbf=data.node_rbf, x=out, edge_index=data._store.get("edge_index"),
+                                edge_attr=edge_attr, line_graph=plan.lg, edge_row=edge_row,
+                                edge_proj=edge_proj[i] if edge_proj is not None else None)
+            stats = getattr(out, "_x2g_rowstats", None)
+            if stats is not None and self._ln_fusable(out, i):
+                # the LayerNorm runs inside the tail's row chain, from the conv's per-row statistics
+                out = self._tail(i, out, res0, ln=(stats, plan.line_ptr, plan.num_graphs, self.LayerNorm.eps))
+            else:
+                out = self.LayerNorm(out, rowptr=plan.line_ptr, num_graphs=plan.num_graphs)
+                out = self._tail(i, out, res0)
+            if fan:
+                out._x2g_fanin = ops.FanIn()
+            readout(i + 1, out)
         if pooled_xs is not None:
             feats = pool_fn(pooled_xs)
             if feats is None:
@@ -146,7 +144,10 @@ class _Trunk(nn.Module):
         if grouped:
             mlps = [r.mlp for r in self.readouts]
             if ops.readout_mlps_supported(feats, mlps):
-                return ops.readout_mlps(feats, mlps)
+                r = ops.readout_mlps(feats, mlps, pool=pool_out)
+                if pool_out is not None:
+                    r._x2g_pooled = True
+                return r
             for m, f in zip(mlps, feats):
                 r = run_mlp(m, f)
                 results = r if results is None else results + r
@@ -226,7 +227,11 @@ class SBFTransformer(_Trunk):
         def pools(xs):
             return self._pool_batch(xs, data.node_rbf, edge_index_0, plan)
 
-        per_atom = self._layers(data, plan, readout, features, pools)
+        # the global add pool (model.py:53) fused into the batched readout heads where they run
+        pool_out = (plan.mol_ptr, plan.out_graphs) if plan.out_graphs == plan.num_graphs else None
+        per_atom = self._layers(data, plan, readout, features, pools, pool_out=pool_out)
+        if getattr(per_atom, "_x2g_pooled", False):
+            return per_atom.view(-1)
         return ops.segment_sum(per_atom, plan.mol_ptr, plan.out_graphs).view(-1)
 
 

@@ -554,10 +554,11 @@ class _ReadoutMLPs(torch.autograd.Function):
     fused into the last one; backward likewise (the weight-gradient slab sums deferred)."""
 
     @staticmethod
-    def forward(ctx, G, *args):
+    def forward(ctx, G, pool, *args):
         feats, params = args[:G], args[G:]
         W1, B1, W2, B2, W3, B3 = (params[i::6] for i in range(6))
         R, D = feats[0].shape
+        ctx.pool = pool
         dev = feats[0].device
         f32 = dict(dtype=torch.float32, device=dev)
         xs = [_f32(f) for f in feats]
@@ -581,10 +582,9 @@ class _ReadoutMLPs(torch.autograd.Function):
             jobs = (ChainFwdJob * G)(*[ChainFwdJob(_dp(xs[g]), None, ctypes.addressof(stages[g]),
                                                    in_t[g].data_ptr() if grad else None) for g in range(G)])
             call("x2g_chain_fwd_batch", jobs, G, 2, R, D, st)
-            out = torch.empty(R, 1, **f32)
             heads = (HeadGroup * G)(*[HeadGroup(_dp(h2[g]), _dp(W3[g]), _dp(B3[g]), None, None, None)
                                       for g in range(G)])
-            call("x2g_readout_head_fwd", heads, G, R, D, ptr(out), st)
+            out = _head_fwd(heads, G, R, D, pool, f32, st)
             if grad:
                 ctx.save_for_backward(*h2, *z1, *z2, WT, in_t)
             ctx.G, ctx.params = G, params
@@ -594,9 +594,8 @@ class _ReadoutMLPs(torch.autograd.Function):
             grp = (DenseFwdGroup * G)(*[DenseFwdGroup(_dp(src[g]), _dp(w[g]), _dp(b[g]), None, _dp(y[g]), _dp(z[g]))
                                         for g in range(G)])
             call("x2g_dense_fwd_batched", grp, G, R, D, D, ACT_SILU, st)
-        out = torch.empty(R, 1, **f32)
         heads = (HeadGroup * G)(*[HeadGroup(_dp(h2[g]), _dp(W3[g]), _dp(B3[g]), None, None, None) for g in range(G)])
-        call("x2g_readout_head_fwd", heads, G, R, D, ptr(out), st)
+        out = _head_fwd(heads, G, R, D, pool, f32, st)
         ctx.save_for_backward(*xs, *h1, *z1, *h2, *z2)
         ctx.G, ctx.params = G, params
         return out
@@ -625,8 +624,13 @@ class _ReadoutMLPs(torch.autograd.Function):
         ws_bytes = int(lib.x2g_readout_head_bwd_workspace(R, D, G))
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
         defer = acc3 and _defer() is not None
-        call("x2g_readout_head_bwd", ptr(dout), heads, G, R, D, (ACCUM_WGRAD if acc3 else 0) |
-             (DEFER_SLAB_SUM if defer else 0), ptr(ws), ws_bytes, st)
+        hflags = (ACCUM_WGRAD if acc3 else 0) | (DEFER_SLAB_SUM if defer else 0)
+        if ctx.pool is not None:  # dout per molecule, broadcast to its rows inside the head kernel
+            seg_rowptr, n_seg = ctx.pool
+            call("x2g_readout_head_pool_bwd", ptr(dout), ptr(seg_rowptr), n_seg, heads, G, R, D, hflags, ptr(ws),
+                 ws_bytes, st)
+        else:
+            call("x2g_readout_head_bwd", ptr(dout), heads, G, R, D, hflags, ptr(ws), ws_bytes, st)
         if defer:
             splits = int(lib.x2g_readout_head_bwd_splits(R))
             for g in range(G):
@@ -645,7 +649,7 @@ class _ReadoutMLPs(torch.autograd.Function):
                 dws, dbs = chain_wgrad(in_t[g], dz_t[g], R, [W1[g], W2[g]], [B1[g], B2[g]])
                 pg += [dws[0], dbs[0], dws[1], dbs[1]]
                 pg += [None if acc3 else dw3[g].view_as(W3[g]), None if acc3 else db3[g]]
-            return (None, *dfeat, *pg)
+            return (None, None, *dfeat, *pg)
         grads = {}
         # layer 2 then layer 1: dz = dy * SiLU'(z), dx = dz W, dW / db
         dy = dh2
@@ -671,7 +675,20 @@ class _ReadoutMLPs(torch.autograd.Function):
             for (dw, db) in (grads[1], grads[2]):
                 pg += [None if dw is None else dw[g], None if db is None else db[g]]
             pg += [None if acc3 else dw3[g].view_as(W3[g]), None if acc3 else db3[g]]
-        return (None, *dfeat, *pg)
+        return (None, None, *dfeat, *pg)
+
+
+def _head_fwd(heads, G, R, D, pool, f32, st):
+    """sum_g head_g(h_g) -> [R, 1] per row, or [n_seg, 1] summed per segment of rows with the pool
+    (x2g_readout_head_pool_fwd: the global add pool fused)."""
+    if pool is None:
+        out = torch.empty(R, 1, **f32)
+        call("x2g_readout_head_fwd", heads, G, R, D, ptr(out), st)
+        return out
+    seg_rowptr, n_seg = pool
+    out = torch.empty(n_seg, 1, **f32)
+    call("x2g_readout_head_pool_fwd", heads, G, R, D, ptr(seg_rowptr), n_seg, ptr(out), st)
+    return out
 
 
 # the readouts' two hidden layers as one batched row-chain launch each way (x2g_chain_*_batch) where
@@ -735,13 +752,17 @@ def readout_mlps_supported(feats, mlps):
     return True
 
 
-def readout_mlps(feats, mlps):
-    """sum_g mlp_g(feats[g]) -> [R, 1] (see _ReadoutMLPs)."""
+def readout_mlps(feats, mlps, pool=None):
+    """sum_g mlp_g(feats[g]) -> [R, 1] (see _ReadoutMLPs); with ``pool = (seg_rowptr int32 [S+1], S)`` the
+    rows' sums per segment -> [S, 1] instead (the global add pool after AtomWise, model.py:53, fused into the
+    head launch each way)."""
     params = []
     for m in mlps:
         mods = list(m)
         params += [mods[0].weight, mods[0].bias, mods[2].weight, mods[2].bias, mods[4].weight, mods[4].bias]
-    return _ReadoutMLPs.apply(len(feats), *feats, *params)
+    if pool is not None:
+        pool = (_i32(pool[0]), int(pool[1]))
+    return _ReadoutMLPs.apply(len(feats), pool, *feats, *params)
 
 
 def keyed_row_sum(src, key, num_keys: int):
