@@ -343,8 +343,8 @@ __device__ __forceinline__ void bstore4(rsrc_t r, f4 v, int voff_bytes) {
                                          voff_bytes, 0, 0);
 }
 
-template <int RB0, int RB1>
-__device__ __forceinline__ void half_gemm(const f4* __restrict__ img, const f4 (&A)[8], f4 (&acc)[kV2RB], int rl,
+template <int RB0, int RB1, int N>
+__device__ __forceinline__ void half_gemm(const f4* __restrict__ img, const f4 (&A)[8], f4 (&acc)[N], int rl,
                                           int g) {
 #pragma unroll
   for (int rb = RB0; rb < RB1; ++rb) acc[rb] = zero4();
@@ -363,8 +363,8 @@ __device__ __forceinline__ void half_gemm(const f4* __restrict__ img, const f4 (
 
 // epilogue of blocks [RB0, RB1): z = acc + bias (stored), y = act(z) (+ residual) -> out image and
 // the T-layout copy; acc[rb] := y
-template <int RB0, int RB1>
-__device__ __forceinline__ void half_epi(f4 (&acc)[kV2RB], const f4 (&held)[kV2RB], f4 bias, float silu_m, float res_m,
+template <int RB0, int RB1, int N>
+__device__ __forceinline__ void half_epi(f4 (&acc)[N], const f4 (&held)[N], f4 bias, float silu_m, float res_m,
                                          rsrc_t zr, rsrc_t tr, f4* __restrict__ out, int r0, int nrows, int w,
                                          int rl, int g) {
   const int j = rl & 3, m = rl >> 2, f = 16 * w + 4 * g + j;
@@ -400,12 +400,13 @@ __device__ __forceinline__ void half_epi(f4 (&acc)[kV2RB], const f4 (&held)[kV2R
 
 // scheduling pattern for one two-block product (8 k-groups x (2 LDS reads + 8 MFMAs)) with an
 // epilogue's instructions threaded between the MFMAs
+template <int BPT = 2>  // blocks per third
 __device__ __forceinline__ void interleave_epi_sched() {
 #pragma unroll
   for (int b = 0; b < 8; ++b) {
-    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+    __builtin_amdgcn_sched_group_barrier(0x100, BPT, 0);  // DS read
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < 4 * BPT; ++k) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
       __builtin_amdgcn_sched_group_barrier(0x006, 3, 0);  // VALU / SALU
       __builtin_amdgcn_sched_group_barrier(0x400, 1, 0);  // transcendental
@@ -427,48 +428,52 @@ __device__ __forceinline__ void interleave_epi_sched() {
 // (The same change to the backward measured 73.7 -> 72.6 us alone but -0.2 % in the step, and a
 // forward with two 256-thread workgroups per CU, so that one workgroup's stage tail overlaps the
 // other's product, measured the same as v4 alone: neither is kept.)
-template <int T>
-__device__ __forceinline__ void frag_load(const f4* __restrict__ img, int b, int rl, int g, f4 (&bo)[2]) {
+template <int T, int BPT = 2>
+__device__ __forceinline__ void frag_load(const f4* __restrict__ img, int b, int rl, int g, f4 (&bo)[BPT]) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) bo[j] = img[(16 * (2 * T + j) + rl) * 32 + ((4 * b + g) ^ rl)];
+  for (int j = 0; j < BPT; ++j) bo[j] = img[(16 * (BPT * T + j) + rl) * 32 + ((4 * b + g) ^ rl)];
 }
 
 // third T's product (blocks 2T, 2T + 1); on entry bo[0] holds its group 0, on exit (T < 2) bo[0]
 // holds third T + 1's group 0
-template <int T>
-__device__ __forceinline__ void third_gemm(const f4* __restrict__ img, const f4 (&A)[8], f4 (&acc)[kV2RB],
-                                           f4 (&bo)[2][2], int rl, int g) {
-  acc[2 * T] = zero4();
-  acc[2 * T + 1] = zero4();
+template <int T, int BPT, int N>
+__device__ __forceinline__ void third_gemm(const f4* __restrict__ img, const f4 (&A)[8], f4 (&acc)[N],
+                                           f4 (&bo)[2][BPT], int rl, int g) {
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) acc[BPT * T + j] = zero4();
 #pragma unroll
   for (int b = 0; b < 8; ++b) {
     const int cur = b & 1;
     if (b + 1 < 8)
-      frag_load<T>(img, b + 1, rl, g, bo[cur ^ 1]);
+      frag_load<T, BPT>(img, b + 1, rl, g, bo[cur ^ 1]);
     else if (T < 2)
-      frag_load<(T < 2 ? T + 1 : T)>(img, 0, rl, g, bo[cur ^ 1]);
+      frag_load<(T < 2 ? T + 1 : T), BPT>(img, 0, rl, g, bo[cur ^ 1]);
 #pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[2 * T + j] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[b][e], bo[cur][j][e], acc[2 * T + j], 0, 0, 0);
+      for (int j = 0; j < BPT; ++j)
+        acc[BPT * T + j] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[b][e], bo[cur][j][e], acc[BPT * T + j], 0, 0, 0);
   }
 }
 
 // a third's product alone: per group its 2 (next-group) LDS reads, then 8 MFMAs
+template <int BPT = 2>
 __device__ __forceinline__ void pipe_sched() {
 #pragma unroll
   for (int b = 0; b < 8; ++b) {
-    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, BPT, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 4 * BPT, 0);
   }
 }
 
-// one stage of the v4 forward: in -> out (distinct arrays after inlining)
+// one stage of the v4 forward: in -> out (distinct arrays after inlining); RB row blocks per chunk (6,
+// or 3 for the small-row batched chains), computed in thirds of RB / 3 blocks
+template <int RB>
 __device__ __forceinline__ void fwd4_stage(const ChainFwdArgs& a, int s, const f4* __restrict__ in,
                                            f4* __restrict__ out, const f4* __restrict__ rimg, f4 (&A)[8],
-                                           f4 (&held)[kV2RB], int r0, int nrows,
+                                           f4 (&held)[RB], int r0, int nrows,
                                            int w, int rl, int g) {
+  constexpr int BPT = RB / 3;
   const int n = a.n;
   const x2g_chain_stage& S = a.st[s];
   const int fl = S.flags;
@@ -478,36 +483,36 @@ __device__ __forceinline__ void fwd4_stage(const ChainFwdArgs& a, int s, const f
   if (fl & (X2G_CHAIN_HOLD | X2G_CHAIN_RES_EXT)) {
     const f4* src = (fl & X2G_CHAIN_HOLD) ? in : rimg;
 #pragma unroll
-    for (int rb = 0; rb < kV2RB; ++rb) held[rb] = src[ipos(16 * rb + rl, 4 * w + g)];
+    for (int rb = 0; rb < RB; ++rb) held[rb] = src[ipos(16 * rb + rl, 4 * w + g)];
   }
   const float silu_m = (fl & X2G_CHAIN_SILU) ? 1.0f : 0.0f;
   const float res_m = (fl & (X2G_CHAIN_RES_HELD | X2G_CHAIN_RES_EXT)) ? 1.0f : 0.0f;
   const rsrc_t zr = rsrc_n(S.z ? S.z : S.w, a.R * kCD * 4, S.z != nullptr);
   const bool t_on = a.in_t && s + 1 < n;
   const rsrc_t tr = rsrc_n(t_on ? a.in_t + (s + 1) * a.tf : S.w, a.tf * 4, t_on);
-  f4 acc[kV2RB];
-  f4 bo[2][2];
-  frag_load<0>(in, 0, rl, g, bo[0]);
+  f4 acc[RB];
+  f4 bo[2][BPT];
+  frag_load<0, BPT>(in, 0, rl, g, bo[0]);
   __builtin_amdgcn_sched_barrier(0);  // the region below: third 0's MFMAs and its next-group reads only
-  third_gemm<0>(in, A, acc, bo, rl, g);
-  pipe_sched();
+  third_gemm<0, BPT>(in, A, acc, bo, rl, g);
+  pipe_sched<BPT>();
   __builtin_amdgcn_sched_barrier(0);
-  third_gemm<1>(in, A, acc, bo, rl, g);
-  half_epi<0, 2>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
-  interleave_epi_sched();
+  third_gemm<1, BPT>(in, A, acc, bo, rl, g);
+  half_epi<0, BPT>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
+  interleave_epi_sched<BPT>();
   __builtin_amdgcn_sched_barrier(0);
-  third_gemm<2>(in, A, acc, bo, rl, g);
-  half_epi<2, 4>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
-  interleave_epi_sched();
+  third_gemm<2, BPT>(in, A, acc, bo, rl, g);
+  half_epi<BPT, 2 * BPT>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
+  interleave_epi_sched<BPT>();
   __builtin_amdgcn_sched_barrier(0);
-  half_epi<4, 6>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
+  half_epi<2 * BPT, 3 * BPT>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
   pin(An);
   X2G_TR(2 + 2 * s);
 #ifndef X2G_ABL_NOBAR
   __syncthreads();
 #endif
   X2G_TR(3 + 2 * s);
-  if (S.y) store_img(S.y, out, r0, nrows);
+  if (S.y) store_img<RB>(S.y, out, r0, nrows);
 #pragma unroll
   for (int b = 0; b < 8; ++b) A[b] = An[b];
 }
@@ -621,16 +626,17 @@ __device__ __forceinline__ void stage_rows_ln(f4* __restrict__ img, const float*
   }
 }
 
-template <bool LN>
+template <bool LN, int RB = kV2RB>
 __device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a, const ChainLn& ln) {
-  __shared__ f4 img0[kV2Img];
-  __shared__ f4 img1[kV2Img];
-  __shared__ f4 imgr[kV2Img];
-  __shared__ float2 lnrow[LN ? kV2RB * 16 : 1];
+  static_assert(RB == 6 || RB == 3, "thirds of 2 or 1 row blocks");
+  __shared__ f4 img0[RB * 16 * 32];
+  __shared__ f4 img1[RB * 16 * 32];
+  __shared__ f4 imgr[RB * 16 * 32];
+  __shared__ float2 lnrow[LN ? RB * 16 : 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int rl = lane & 15, g = lane >> 4;
   const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
-  const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
+  const int64_t nch = (nblk + RB * G - 1) / (RB * G) * G;
   const int n = a.n;
   // W^T of every stage for the backward (x2g_chain_stage.wt): each workgroup writes its share, one
   // element per thread (written by the first 8 chunks, it made those workgroups the launch's tail)
@@ -645,26 +651,26 @@ __device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a, const Ch
     chunk_rows(ch, nch, nblk, a.R, r0, nrows);
     __syncthreads();
     if (LN)
-      stage_rows_ln(img0, a.x, a.R, ln, lnrow, r0, nrows);
+      stage_rows_ln<RB>(img0, a.x, a.R, ln, lnrow, r0, nrows);
     else
-      stage_rows(img0, a.x, nullptr, r0, nrows);
-    if (a.res) stage_rows(imgr, a.res, nullptr, r0, nrows);
+      stage_rows<RB>(img0, a.x, nullptr, r0, nrows);
+    if (a.res) stage_rows<RB>(imgr, a.res, nullptr, r0, nrows);
     X2G_TR(0);
-    f4 A[8], held[kV2RB];
+    f4 A[8], held[RB];
     load_slice<false>(a.st[0].w, w, rl, g, A);
 #pragma unroll
-    for (int rb = 0; rb < kV2RB; ++rb) held[rb] = zero4();
+    for (int rb = 0; rb < RB; ++rb) held[rb] = zero4();
     __syncthreads();
     X2G_TR(1);
     if (a.in_t) {
-      f4 xs[kV2RB];
+      f4 xs[RB];
 #pragma unroll
-      for (int rb = 0; rb < kV2RB; ++rb) xs[rb] = img0[ipos(16 * rb + rl, 4 * w + g)];
+      for (int rb = 0; rb < RB; ++rb) xs[rb] = img0[ipos(16 * rb + rl, 4 * w + g)];
       store_t_slice(a.in_t, xs, r0, nrows, w, rl, g);
     }
     for (int s = 0; s < n; s += 2) {
-      fwd4_stage(a, s, img0, img1, imgr, A, held, r0, nrows, w, rl, g);
-      if (s + 1 < n) fwd4_stage(a, s + 1, img1, img0, imgr, A, held, r0, nrows, w, rl, g);
+      fwd4_stage<RB>(a, s, img0, img1, imgr, A, held, r0, nrows, w, rl, g);
+      if (s + 1 < n) fwd4_stage<RB>(a, s + 1, img1, img0, imgr, A, held, r0, nrows, w, rl, g);
     }
   }
   X2G_CLK(1);
@@ -687,8 +693,11 @@ constexpr int kChainMaxJobs = X2G_CHAIN_MAX_JOBS;
 struct ChainFwdBatch {
   ChainFwdArgs a[kChainMaxJobs];
 };
+// RB = 3 when one chunk of 3 row blocks per workgroup covers a job (the readouts' 2304 rows on 51
+// workgroups each): the products of 6 blocks, half of them padding, would set the stage time
+template <int RB>
 __global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4_batch(const ChainFwdBatch b) {
-  chain_fwd_v4_run<false>(b.a[blockIdx.y], {});
+  chain_fwd_v4_run<false, RB>(b.a[blockIdx.y], {});
 }
 
 // ---- backward v3 (the shipped kernel): the v2 design with stage s-1's elementwise
@@ -700,8 +709,8 @@ __global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4_batch(const ChainFw
 // branch, only in the accumulating stage's elementwise part (1 of the trunk's 7; r2 issued it in
 // every stage as a dropped out-of-range load and waited on it there: removing every external access
 // measured +1.3 % in the step, profiles/r3d_ab_chain_noext.log, the bound for this change)
-template <int RB0, int RB1>
-__device__ __forceinline__ void bwd_elem(f4 (&gs)[kV2RB], f4 (&dh)[kV2RB], const f4 (&zc)[kV2RB], const f4 (&acc)[kV2RB],
+template <int RB0, int RB1, int N>
+__device__ __forceinline__ void bwd_elem(f4 (&gs)[N], f4 (&dh)[N], const f4 (&zc)[N], const f4 (&acc)[N],
                                          float hold_m, float held_m, float silu_m, float dres_acc_m, rsrc_t dres_r,
                                          rsrc_t dz_r, rsrc_t t_r, f4* __restrict__ out, int r0, int nrows, int w,
                                          int rl, int g) {
@@ -757,24 +766,27 @@ __device__ __forceinline__ void store_img_lnstats(float* __restrict__ P, const f
   }
 }
 
+template <int RB = kV2RB>
 __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
-  __shared__ f4 img[2][kV2Img];
-  __shared__ f4 yimg[kV2Img];
+  static_assert(RB == 6 || RB == 3, "thirds of 2 or 1 row blocks");
+  constexpr int BPT = RB / 3;
+  __shared__ f4 img[2][RB * 16 * 32];
+  __shared__ f4 yimg[RB * 16 * 32];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int rl = lane & 15, g = lane >> 4;
   const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
-  const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
+  const int64_t nch = (nblk + RB * G - 1) / (RB * G) * G;
   const int n = a.n;
   const int col = 16 * w + 4 * g;
   X2G_CLK(0);
   for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
     int r0, nrows;
     chunk_rows(ch, nch, nblk, a.R, r0, nrows);
-    f4 A[8], dh[kV2RB], zc[kV2RB], gs[kV2RB];
+    f4 A[8], dh[RB], zc[RB], gs[RB];
     auto load_z = [&](int s) {
       const rsrc_t zr = rsrc((a.st[s].flags & X2G_CHAIN_SILU) ? a.st[s].z : a.dy);
 #pragma unroll
-      for (int rb = 0; rb < kV2RB; ++rb) {
+      for (int rb = 0; rb < RB; ++rb) {
         const int r = 16 * rb + rl;
         zc[rb] = bload4(zr, 4 * ((r0 + (r < nrows ? r : 0)) * kCD + col), 0);
       }
@@ -801,15 +813,15 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
     // whether stage s's elementwise part stores anything but dz in the T layout (wave-uniform)
     // the LayerNorm backward's y rows for the final store: an LDS copy in flight with the first loads
     // (yimg is read only after the last stage's barrier; the first waits below cover it)
-    if (a.ln_y) stage_rows_async<kV2RB>(yimg, a.ln_y, a.R, r0);
+    if (a.ln_y) stage_rows_async<RB>(yimg, a.ln_y, a.R, r0);
     load_wslice(n - 1, A);
     load_z(n - 1);
-    f4 acc0[kV2RB];
+    f4 acc0[RB];
     {
       const rsrc_t yr = rsrc(a.dy), ar = rsrc(a.dy_add ? a.dy_add : a.dy);
       const float am = a.dy_add ? 1.0f : 0.0f;
 #pragma unroll
-      for (int rb = 0; rb < kV2RB; ++rb) {
+      for (int rb = 0; rb < RB; ++rb) {
         const int r = 16 * rb + rl;
         const int vo = 4 * ((r0 + (r < nrows ? r : 0)) * kCD + col);
         acc0[rb] = bload4(yr, vo, 0) + bload4(ar, vo, 0) * am;
@@ -823,7 +835,7 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
       float held_m, silu_m, dres_acc_m;
       rsrc_t dres_r, dz_r, t_r;
       elem_args(n - 1, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r);
-      bwd_elem<0, kV2RB>(gs, dh, zc, acc0, 0.0f, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, img[p], r0, nrows,
+      bwd_elem<0, RB>(gs, dh, zc, acc0, 0.0f, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, img[p], r0, nrows,
                               w, rl, g);
     }
     __syncthreads();
@@ -835,31 +847,31 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
       const float hold_m = (a.st[s].flags & X2G_CHAIN_HOLD) ? 1.0f : 0.0f;
       const f4* in = img[p];
       f4* out = img[p ^ 1];
-      f4 acc[kV2RB];
+      f4 acc[RB];
       if (s > 0) {
         float held_m, silu_m, dres_acc_m;
         rsrc_t dres_r, dz_r, t_r;
         elem_args(s - 1, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r);
         {
-          half_gemm<0, 2>(in, A, acc, rl, g);
+          half_gemm<0, BPT>(in, A, acc, rl, g);
           __builtin_amdgcn_sched_barrier(0);
-          half_gemm<2, 4>(in, A, acc, rl, g);
-          bwd_elem<0, 2>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows,
+          half_gemm<BPT, 2 * BPT>(in, A, acc, rl, g);
+          bwd_elem<0, BPT>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows,
                             w, rl, g);
-          interleave_epi_sched();
+          interleave_epi_sched<BPT>();
           __builtin_amdgcn_sched_barrier(0);
-          half_gemm<4, 6>(in, A, acc, rl, g);
-          bwd_elem<2, 4>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows,
+          half_gemm<2 * BPT, 3 * BPT>(in, A, acc, rl, g);
+          bwd_elem<BPT, 2 * BPT>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows,
                             w, rl, g);
-          interleave_epi_sched();
+          interleave_epi_sched<BPT>();
           __builtin_amdgcn_sched_barrier(0);
-          bwd_elem<4, 6>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows,
+          bwd_elem<2 * BPT, 3 * BPT>(gs, dh, zc, acc, hold_m, held_m, silu_m, dres_acc_m, dres_r, dz_r, t_r, out, r0, nrows,
                             w, rl, g);
         }
       } else {
-        slice_gemm(in, A, acc, rl, g);
+        slice_gemm<RB>(in, A, acc, rl, g);
 #pragma unroll
-        for (int rb = 0; rb < kV2RB; ++rb) out[ipos(16 * rb + rl, 4 * w + g)] = acc[rb] + dh[rb] * hold_m;
+        for (int rb = 0; rb < RB; ++rb) out[ipos(16 * rb + rl, 4 * w + g)] = acc[rb] + dh[rb] * hold_m;
       }
       p ^= 1;
       pin(An);
@@ -870,9 +882,9 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
       for (int b = 0; b < 8; ++b) A[b] = An[b];
     }
     if (a.ln_y)
-      store_img_lnstats(a.dx, img[p], yimg, a.ln_gstats, r0, nrows);
+      store_img_lnstats<RB>(a.dx, img[p], yimg, a.ln_gstats, r0, nrows);
     else
-      store_img(a.dx, img[p], r0, nrows);
+      store_img<RB>(a.dx, img[p], r0, nrows);
   }
   X2G_CLK(1);
 }
@@ -880,8 +892,9 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
 struct ChainBwdBatch {
   ChainBwdArgs a[kChainMaxJobs];
 };
+template <int RB>
 __global__ void __launch_bounds__(kCThreads, 1) chain_bwd_v3_batch(const ChainBwdBatch b) {
-  chain_bwd_v3_run(b.a[blockIdx.y]);
+  chain_bwd_v3_run<RB>(b.a[blockIdx.y]);
 }
 
 
@@ -1721,7 +1734,7 @@ static int chain_bwd_launch(const ChainBwdArgs& a, int64_t rows, void* stream) {
     ChainBwdBatch b{};
     b.a[0] = a;
     const dim3 grid(static_cast<unsigned>(nblk < 256 ? nblk : 256), 1);
-    chain_bwd_v3_batch<<<grid, kCThreads, 0, st>>>(b);
+    chain_bwd_v3_batch<kV2RB><<<grid, kCThreads, 0, st>>>(b);
   }
   return last_launch_status();
 }
@@ -1758,6 +1771,13 @@ static inline unsigned chain_batch_grid(int64_t rows, int n_jobs) {
   return static_cast<unsigned>(nblk < per ? nblk : (per < 1 ? 1 : per));
 }
 
+// one chunk of <= 3 row blocks per workgroup covers the job: the 3-block form (products of 3 blocks
+// instead of 6, half of them padding; at config 2 the readouts' 144 blocks on 51 workgroups)
+static inline bool chain_batch_rb3(int64_t rows, unsigned grid_x) {
+  const int64_t nblk = (rows + 15) / 16;
+  return nblk <= 3 * static_cast<int64_t>(grid_x);
+}
+
 X2G_API int x2g_chain_fwd_batch(const x2g_chain_fwd_job* jobs, int32_t n_jobs, int32_t n_stages, int64_t rows,
                                 int32_t dim, void* stream) {
   if (!jobs || n_jobs < 1 || n_jobs > kChainMaxJobs) return X2G_EINVAL;
@@ -1769,7 +1789,10 @@ X2G_API int x2g_chain_fwd_batch(const x2g_chain_fwd_job* jobs, int32_t n_jobs, i
   }
   if (empty) return X2G_OK;
   const dim3 grid(chain_batch_grid(rows, n_jobs), static_cast<unsigned>(n_jobs));
-  chain_fwd_v4_batch<<<grid, kCThreads, 0, as_stream(stream)>>>(b);
+  if (chain_batch_rb3(rows, grid.x))
+    chain_fwd_v4_batch<3><<<grid, kCThreads, 0, as_stream(stream)>>>(b);
+  else
+    chain_fwd_v4_batch<kV2RB><<<grid, kCThreads, 0, as_stream(stream)>>>(b);
   return last_launch_status();
 }
 
@@ -1786,7 +1809,10 @@ X2G_API int x2g_chain_bwd_batch(const x2g_chain_bwd_job* jobs, int32_t n_jobs, i
   }
   if (empty) return X2G_OK;
   const dim3 grid(chain_batch_grid(rows, n_jobs), static_cast<unsigned>(n_jobs));
-  chain_bwd_v3_batch<<<grid, kCThreads, 0, as_stream(stream)>>>(b);
+  if (chain_batch_rb3(rows, grid.x))
+    chain_bwd_v3_batch<3><<<grid, kCThreads, 0, as_stream(stream)>>>(b);
+  else
+    chain_bwd_v3_batch<kV2RB><<<grid, kCThreads, 0, as_stream(stream)>>>(b);
   return last_launch_status();
 }
 
