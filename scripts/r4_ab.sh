@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-r4ab}
 K=${K:-"featurize or model_energies or config2_trainer or chain or conv_proj or flat"}
-timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py -q -m gpu -x -k "$K" \
+timeout -k 10 600 python -u -m pytest ${FILES:-tests/test_gpu_kernels.py tests/test_gpu_model.py} -q -m gpu -x -k "$K" \
   --timeout 300 --timeout-method thread > gpurun_out/t_$TAG.log 2>&1
 rc=$?; tail -3 gpurun_out/t_$TAG.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 1200 python -u scripts/step_ab.py ${ROUNDS:-3} $AB > gpurun_out/ab_$TAG.log 2>&1

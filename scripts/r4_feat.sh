@@ -15,6 +15,7 @@ for rep in 1 2 3; do
   done
 done
 grep -h libx2g gpurun_out/feat_$TAG.txt
+[ -f $L/libx2g_trace.so ] || exit 0
 X2G_LIB=$L/libx2g_trace.so timeout -k 10 120 python scripts/trace_chain.py 21120 fwd > gpurun_out/clk_$TAG.txt 2>&1 || exit $?
 X2G_LIB=$L/libx2g_trace.so timeout -k 10 120 python scripts/trace_chain.py 21120 >> gpurun_out/clk_$TAG.txt 2>&1 || exit $?
 X2G_LIB=$L/libx2g_trace.so timeout -k 10 120 python scripts/trace_flat.py >> gpurun_out/clk_$TAG.txt 2>&1 || exit $?
