@@ -335,35 +335,42 @@ def proj_probe(R, reps):
 
 def flat_wgrad_probe(flat_launches, reps):
     """The step's largest kernel: every T-layout weight gradient of the backward in one launch
-    (x2g_tiled_wgrad_flat, ops._flush_tiled) with the job list the captured step recorded
-    (Trainer.flat_launches: rows R, one [128,cols] dW = dz^T x per job, K = R), on synthetic T-layout
-    operands, HIP-event timed on the launch stream.  FLOPs per launch: sum_j 2 * R * 128 * cols_j."""
+    (x2g_tiled_wgrad_flat_rows, ops._flush_tiled) with the job list the captured step recorded
+    (Trainer.flat_launches: per job its rows R_j and one [128, cols_j] dW = dz^T x, K = R_j — the trunk's
+    line-node rows and the readout MLPs' atom rows in the same launch), on synthetic T-layout operands,
+    HIP-event timed on the launch stream.  FLOPs per launch: sum_j 2 * R_j * 128 * cols_j."""
     if not flat_launches:
         return None
-    R, cols = max(flat_launches, key=lambda rc: rc[0] * sum(rc[1]))
-    n, D = len(cols), 128
+    launch = max(flat_launches, key=lambda l: sum(R * c for R, c in l))
+    n, D = len(launch), 128
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(5)
-    tf = _lib_ws("x2g_chain_t_floats", R, D)
-    x_t = [torch.randn(tf, device=dev, generator=g) for _ in range(n)]
-    dz_t = [torch.randn(tf, device=dev, generator=g) for _ in range(n)]
+    x_t, dz_t = [], []
+    for R, _ in launch:
+        tf = _lib_ws("x2g_chain_t_floats", R, D)
+        x_t.append(torch.randn(tf, device=dev, generator=g))
+        dz_t.append(torch.randn(tf, device=dev, generator=g))
     dw = [torch.zeros(D, D, device=dev) for _ in range(n)]
     db = [torch.zeros(D, device=dev) for _ in range(n)]
     jobs = (ops.TiledJob * n)(*[ops.TiledJob(dz_t[j].data_ptr(), x_t[j].data_ptr(), dw[j].data_ptr(),
-                                             db[j].data_ptr(), D if cols[j] < D else 0, cols[j] if cols[j] < D else 0)
-                                for j in range(n)])
-    wsb = _lib_ws("x2g_tiled_wgrad_flat_workspace", R, D, n)
+                                             db[j].data_ptr(), D if c < D else 0, c if c < D else 0)
+                                for j, (_, c) in enumerate(launch)])
+    rows = (ctypes.c_int64 * n)(*[R for R, _ in launch])
+    from x2gnn import _lib
+    wsb = int(_lib.load().x2g_tiled_wgrad_flat_rows_workspace(rows, n, D))
     ws = torch.empty(max(wsb, 4), dtype=torch.uint8, device=dev)
     out = (ops.SlabJob * n)()
 
     def run():
-        call("x2g_tiled_wgrad_flat", jobs, n, R, D, ops.ACCUM_WGRAD | ops.DEFER_SLAB_SUM, out, ptr(ws), wsb,
+        call("x2g_tiled_wgrad_flat_rows", jobs, rows, n, D, ops.ACCUM_WGRAD | ops.DEFER_SLAB_SUM, out, ptr(ws), wsb,
              stream_ptr())
 
     run()
     ms = _event_time(run, reps)
-    wgs = min(512, max(1, (R + 15) // 16 * n))  # chain.hip flat_grid: two 512-thread workgroups per CU
-    return {"ms": ms, "flops": float(sum(2.0 * R * D * c for c in cols)), "rows": R, "jobs": n, "grid": wgs * 512}
+    tiles = sum((R + 15) // 16 for R, _ in launch)
+    wgs = min(512, max(1, tiles))  # chain.hip flat_grid: two 512-thread workgroups per CU
+    return {"ms": ms, "flops": float(sum(2.0 * R * D * c for R, c in launch)),
+            "rows": sorted({R for R, _ in launch}), "jobs": n, "grid": wgs * 512}
 
 
 def _lib_ws(name, *args):

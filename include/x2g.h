@@ -793,6 +793,13 @@ typedef struct {
 size_t x2g_tiled_wgrad_flat_workspace(int64_t rows, int32_t dim, int32_t num_jobs);
 int x2g_tiled_wgrad_flat(const x2g_tiled_job* jobs, int32_t num_jobs, int64_t rows, int32_t dim, int flags,
                          x2g_slab_job* slab_jobs, void* workspace, size_t workspace_bytes, void* stream);
+/* The same with a row count per job (job_rows: HOST array of num_jobs): a backward's weight gradients
+ * over the line-node rows and over the atom rows (the readout MLPs) in one launch instead of one per
+ * row count.  Equal row counts reproduce x2g_tiled_wgrad_flat exactly. */
+size_t x2g_tiled_wgrad_flat_rows_workspace(const int64_t* job_rows, int32_t num_jobs, int32_t dim);
+int x2g_tiled_wgrad_flat_rows(const x2g_tiled_job* jobs, const int64_t* job_rows, int32_t num_jobs, int32_t dim,
+                              int flags, x2g_slab_job* slab_jobs, void* workspace, size_t workspace_bytes,
+                              void* stream);
 
 size_t x2g_tiled_wgrad_workspace(int64_t rows, int32_t dim, int32_t num_jobs);
 int32_t x2g_tiled_wgrad_splits(int64_t rows, int32_t dim, int32_t num_jobs);

@@ -62,7 +62,7 @@ def trace(d, last=8):
 def flops_per_step(E, T, N, flat_launches):
     """Matrix FLOPs (2 per multiply-add) per training step of each MFMA kernel at this batch's shape."""
     L = 4
-    flat = sum(2 * R * D * c for R, cols in flat_launches for c in cols)
+    flat = sum(2 * R * D * c for launch in flat_launches for R, c in launch)  # [(rows, cols) per job] per launch
     return {
         "chain_fwd_v4_ln": L * 7 * 2 * E * D * D,           # trunk tail: 7 D x D stages per layer
         "chain_fwd_v4_batch": 5 * 2 * 2 * N * D * D,        # 5 readout MLPs x 2 hidden layers on the atom rows

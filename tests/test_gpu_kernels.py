@@ -1677,6 +1677,59 @@ def test_tiled_wgrad_flat_vs_torch(cuda, R, njobs):
             assert float((dbs[j].double() - 5.0 - rb).abs().max()) <= 2e-5 * float(rb.abs().max()) + 1e-4, j
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows", [[21058] * 52 + [2304] * 10, [37, 1000, 5, 2304], [16, 1], [1000, 1000, 1000]])
+def test_tiled_wgrad_flat_rows_mixed(cuda, rows):
+    """x2g_tiled_wgrad_flat_rows: jobs with their own row counts in one launch (the trunk's line-node
+    rows and the readout MLPs' atom rows, ops._flush_tiled) — every dW / db against fp64 torch, and with
+    equal row counts bit for bit the single-row-count entry x2g_tiled_wgrad_flat."""
+    import ctypes
+    from x2gnn import _lib, ops
+    from x2gnn._lib import ptr, stream_ptr
+
+    lib = _lib.load()
+    n = len(rows)
+    g = torch.Generator(device=cuda).manual_seed(sum(rows) + n)
+    dys = [torch.randn(R, 128, device=cuda, generator=g) for R in rows]
+    xs = [torch.randn(R, 128, device=cuda, generator=g) for R in rows]
+    dy_t = [_t_layout(t)[0].contiguous() for t in dys]
+    x_t = [_t_layout(t)[0].contiguous() for t in xs]
+
+    def run(entry_rows):
+        dws = [torch.zeros(128, 128, device=cuda) for _ in range(n)]
+        dbs = [torch.zeros(128, device=cuda) if j % 2 == 0 else None for j in range(n)]
+        arr = (ops.TiledJob * n)(*[ops.TiledJob(dy_t[j].data_ptr(), x_t[j].data_ptr(), dws[j].data_ptr(),
+                                                dbs[j].data_ptr() if dbs[j] is not None else None, 0, 0)
+                                   for j in range(n)])
+        out = (ops.SlabJob * n)()
+        if entry_rows is None:
+            r = (ctypes.c_int64 * n)(*rows)
+            wsb = int(lib.x2g_tiled_wgrad_flat_rows_workspace(r, n, 128))
+            ws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
+            assert lib.x2g_tiled_wgrad_flat_rows(arr, r, n, 128, ops.ACCUM_WGRAD | ops.DEFER_SLAB_SUM, out, ptr(ws),
+                                                 wsb, stream_ptr()) == 0
+        else:
+            wsb = int(lib.x2g_tiled_wgrad_flat_workspace(entry_rows, 128, n))
+            ws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
+            assert lib.x2g_tiled_wgrad_flat(arr, n, entry_rows, 128, ops.ACCUM_WGRAD | ops.DEFER_SLAB_SUM, out,
+                                            ptr(ws), wsb, stream_ptr()) == 0
+        assert lib.x2g_slab_sum_batch(out, n, 1, stream_ptr()) == 0
+        torch.cuda.synchronize()
+        return dws, dbs
+
+    dws, dbs = run(None)
+    for j in range(n):
+        ref = dys[j].double().t() @ xs[j].double()
+        assert float((dws[j].double() - ref).abs().max()) <= 2e-5 * float(ref.abs().max()), j
+        if dbs[j] is not None:
+            rb = dys[j].double().sum(0)
+            assert float((dbs[j].double() - rb).abs().max()) <= 2e-5 * float(rb.abs().max()) + 1e-4, j
+    if len(set(rows)) == 1:
+        dws1, dbs1 = run(rows[0])
+        assert all(torch.equal(a, b) for a, b in zip(dws, dws1))
+        assert all((a is None and b is None) or torch.equal(a, b) for a, b in zip(dbs, dbs1))
+
+
 @pytest.mark.parametrize("n,beta", [(1, 1.0), (128, 1.0), (1000, 0.5), (3, 2.0)])
 def test_smooth_l1_mean_vs_torch(cuda, n, beta):
     """ops.smooth_l1_loss (x2g_smooth_l1_mean_fwd / _bwd, trainer.py:41) vs F.smooth_l1_loss:

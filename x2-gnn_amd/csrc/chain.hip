@@ -1157,7 +1157,7 @@ __global__ void __launch_bounds__(kCThreads, 1) chain_wgrad_kernel(const ChainWg
 }
 
 // Every T-layout weight gradient of a backward in ONE launch: the jobs' tiles are concatenated
-// (job j owns [j * ntiles, (j + 1) * ntiles)) and workgroup i takes the equal share
+// (job j owns [tile0[j], tile0[j + 1]): jobs may differ in row count) and workgroup i takes the equal share
 // [i * total / G, (i + 1) * total / G), i.e. at most a few job segments; each segment leaves one
 // slab, job j's slabs contiguous from workgroup wg_lo[j] on.  Versus one launch per layer with
 // 256 / jobs splits per job: the same MFMA work, ~256 + jobs slabs in all instead of 256 per
@@ -1169,7 +1169,7 @@ struct TiledFlatArgs {
   float* slab_b[X2G_TILED_MAX_JOBS];  // ... and its bias slab at + k * D
   int wg_lo[X2G_TILED_MAX_JOBS];
   int has_b[X2G_TILED_MAX_JOBS];
-  int64_t ntiles;
+  int64_t tile0[X2G_TILED_MAX_JOBS + 1];  // job j: tiles [tile0[j], tile0[j + 1]) of the concatenation
   int64_t total;
   int njobs;
 };
@@ -1182,13 +1182,15 @@ __global__ void __launch_bounds__(kCThreads, 2 * WPC) tiled_flat_kernel(const Ti
   const int64_t G = gridDim.x, i = blockIdx.x;
   const int64_t lo = i * a.total / G, hi = (i + 1) * a.total / G;
   X2G_CLK(0);
-  for (int64_t j = lo / a.ntiles; j < a.njobs && j * a.ntiles < hi; ++j) {
-    const int64_t s0 = lo > j * a.ntiles ? lo : j * a.ntiles;
-    const int64_t s1 = hi < (j + 1) * a.ntiles ? hi : (j + 1) * a.ntiles;
+  int j0 = 0;
+  while (j0 < a.njobs && a.tile0[j0 + 1] <= lo) ++j0;  // (uniform; <= 64 jobs)
+  for (int j = j0; j < a.njobs && a.tile0[j] < hi; ++j) {
+    const int64_t s0 = lo > a.tile0[j] ? lo : a.tile0[j];
+    const int64_t s1 = hi < a.tile0[j + 1] ? hi : a.tile0[j + 1];
     if (s0 >= s1) continue;
     __syncthreads();  // a previous segment's last buffers are no longer read
     const int64_t k = i - a.wg_lo[j];
-    tiled_segment<NB, SPREAD, WT>(a.dz_t[j], a.in_t[j], s0 - j * a.ntiles, s1 - j * a.ntiles, a.has_b[j] != 0,
+    tiled_segment<NB, SPREAD, WT>(a.dz_t[j], a.in_t[j], s0 - a.tile0[j], s1 - a.tile0[j], a.has_b[j] != 0,
                   a.slab_w[j] + k * kCD * kCD, a.slab_b[j] + k * kCD, Ds, Xs);
   }
   X2G_CLK(1);
@@ -2039,8 +2041,8 @@ static inline unsigned flat_grid(int64_t total) {
   return static_cast<unsigned>(total < cap ? (total < 1 ? 1 : total) : cap);
 }
 
-// slabs of job j: the workgroups overlapping its tiles
-static inline void flat_span(int64_t ntiles, int64_t total, int64_t G, int j, int& lo, int& n) {
+// slabs of job j (tiles [t0, t1) of the concatenation): the workgroups overlapping them
+static inline void flat_span(int64_t t0, int64_t t1, int64_t total, int64_t G, int& lo, int& n) {
   // workgroup i covers [i * total / G, (i + 1) * total / G): the one holding tile t is the largest i
   // with i * total / G <= t
   auto owner = [&](int64_t t) {
@@ -2049,34 +2051,48 @@ static inline void flat_span(int64_t ntiles, int64_t total, int64_t G, int j, in
     while (i > 0 && i * total / G > t) --i;
     return static_cast<int>(i);
   };
-  lo = owner(j * ntiles);
-  n = owner((j + 1) * ntiles - 1) - lo + 1;
+  lo = owner(t0);
+  n = owner(t1 - 1) - lo + 1;
 }
 
-X2G_API size_t x2g_tiled_wgrad_flat_workspace(int64_t rows, int32_t dim, int32_t num_jobs) {
-  if (rows <= 0 || dim != kCD || num_jobs < 1 || num_jobs > X2G_TILED_MAX_JOBS) return 0;
-  const int64_t ntiles = (rows + 15) / 16, total = ntiles * num_jobs, G = flat_grid(total);
+// the concatenation's tile offsets of jobs with rows[j] rows each (0 on a bad row count)
+static inline bool flat_tiles(const int64_t* rows, int num_jobs, int64_t* tile0) {
+  tile0[0] = 0;
+  for (int j = 0; j < num_jobs; ++j) {
+    if (rows[j] <= 0 || rows[j] * kCD * 4 >= (int64_t(1) << 31)) return false;
+    tile0[j + 1] = tile0[j] + (rows[j] + 15) / 16;
+  }
+  return true;
+}
+
+static size_t flat_workspace(const int64_t* rows, int32_t num_jobs, int32_t dim) {
+  if (!rows || dim != kCD || num_jobs < 1 || num_jobs > X2G_TILED_MAX_JOBS) return 0;
+  int64_t tile0[X2G_TILED_MAX_JOBS + 1];
+  if (!flat_tiles(rows, num_jobs, tile0)) return 0;
+  const int64_t total = tile0[num_jobs], G = flat_grid(total);
   int64_t slabs = 0;
   for (int j = 0; j < num_jobs; ++j) {
     int lo, n;
-    flat_span(ntiles, total, G, j, lo, n);
+    flat_span(tile0[j], tile0[j + 1], total, G, lo, n);
     slabs += n;
   }
   return static_cast<size_t>(slabs) * (kCD * kCD + kCD) * sizeof(float);
 }
 
-X2G_API int x2g_tiled_wgrad_flat(const x2g_tiled_job* jobs, int32_t num_jobs, int64_t rows, int32_t dim, int flags,
-                                 x2g_slab_job* slab_jobs, void* workspace, size_t workspace_bytes, void* stream) {
-  if (!jobs || num_jobs < 1 || num_jobs > X2G_TILED_MAX_JOBS || rows <= 0 || dim <= 0 ||
+static int flat_launch(const x2g_tiled_job* jobs, const int64_t* rows, int32_t num_jobs, int32_t dim, int flags,
+                       x2g_slab_job* slab_jobs, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!jobs || !rows || num_jobs < 1 || num_jobs > X2G_TILED_MAX_JOBS || dim <= 0 ||
       (flags & ~(X2G_ACCUM_WGRAD | X2G_DEFER_SLAB_SUM)))
     return X2G_EINVAL;
-  if (dim != kCD || rows * kCD * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
+  for (int j = 0; j < num_jobs; ++j)
+    if (rows[j] <= 0) return X2G_EINVAL;
+  if (dim != kCD) return X2G_EUNSUPPORTED;
   if ((flags & X2G_DEFER_SLAB_SUM) && !slab_jobs) return X2G_EINVAL;
-  const size_t need = x2g_tiled_wgrad_flat_workspace(rows, dim, num_jobs);
-  if (!workspace || workspace_bytes < need) return X2G_EWORKSPACE;
   TiledFlatArgs a{};
-  a.ntiles = (rows + 15) / 16;
-  a.total = a.ntiles * num_jobs;
+  if (!flat_tiles(rows, num_jobs, a.tile0)) return X2G_EUNSUPPORTED;
+  const size_t need = flat_workspace(rows, num_jobs, dim);
+  if (!workspace || workspace_bytes < need) return X2G_EWORKSPACE;
+  a.total = a.tile0[num_jobs];
   a.njobs = num_jobs;
   const int64_t G = flat_grid(a.total);
   x2g_slab_job sj[X2G_TILED_MAX_JOBS];
@@ -2087,7 +2103,7 @@ X2G_API int x2g_tiled_wgrad_flat(const x2g_tiled_job* jobs, int32_t num_jobs, in
     if (!al16(J.dy_t) || !al16(J.x_t)) return X2G_EUNSUPPORTED;
     if (J.ld < 0 || (J.ld > 0 && (J.cols < 1 || J.cols > kCD || J.cols > J.ld))) return X2G_EINVAL;
     int lo, n;
-    flat_span(a.ntiles, a.total, G, j, lo, n);
+    flat_span(a.tile0[j], a.tile0[j + 1], a.total, G, lo, n);
     a.in_t[j] = J.x_t;
     a.dz_t[j] = J.dy_t;
     a.wg_lo[j] = lo;
@@ -2110,6 +2126,31 @@ X2G_API int x2g_tiled_wgrad_flat(const x2g_tiled_job* jobs, int32_t num_jobs, in
     return X2G_OK;
   }
   return x2g_slab_sum_batch(sj, num_jobs, (flags & X2G_ACCUM_WGRAD) ? 1 : 0, stream);
+}
+
+X2G_API size_t x2g_tiled_wgrad_flat_workspace(int64_t rows, int32_t dim, int32_t num_jobs) {
+  if (rows <= 0 || num_jobs < 1 || num_jobs > X2G_TILED_MAX_JOBS) return 0;
+  int64_t r[X2G_TILED_MAX_JOBS];
+  for (int j = 0; j < num_jobs; ++j) r[j] = rows;
+  return flat_workspace(r, num_jobs, dim);
+}
+
+X2G_API int x2g_tiled_wgrad_flat(const x2g_tiled_job* jobs, int32_t num_jobs, int64_t rows, int32_t dim, int flags,
+                                 x2g_slab_job* slab_jobs, void* workspace, size_t workspace_bytes, void* stream) {
+  if (rows <= 0 || num_jobs < 1 || num_jobs > X2G_TILED_MAX_JOBS) return X2G_EINVAL;
+  int64_t r[X2G_TILED_MAX_JOBS];
+  for (int j = 0; j < num_jobs; ++j) r[j] = rows;
+  return flat_launch(jobs, r, num_jobs, dim, flags, slab_jobs, workspace, workspace_bytes, stream);
+}
+
+X2G_API size_t x2g_tiled_wgrad_flat_rows_workspace(const int64_t* job_rows, int32_t num_jobs, int32_t dim) {
+  return flat_workspace(job_rows, num_jobs, dim);
+}
+
+X2G_API int x2g_tiled_wgrad_flat_rows(const x2g_tiled_job* jobs, const int64_t* job_rows, int32_t num_jobs,
+                                      int32_t dim, int flags, x2g_slab_job* slab_jobs, void* workspace,
+                                      size_t workspace_bytes, void* stream) {
+  return flat_launch(jobs, job_rows, num_jobs, dim, flags, slab_jobs, workspace, workspace_bytes, stream);
 }
 
 X2G_API int32_t x2g_tiled_wgrad_splits(int64_t rows, int32_t dim, int32_t num_jobs) {

@@ -942,7 +942,7 @@ class SlabJob(ctypes.Structure):
 class _SlabDeferral:
     """The state of one ``deferred_wgrad()`` context (one backward): the queued slab sums, the
     workspaces they read, the T-layout weight-gradient jobs of the flat launch, and — after the
-    context exits — ``flat_launches``: (rows, [cols per job]) of each flat launch it made (bench.py's
+    context exits — ``flat_launches``: [(rows, cols) per job] of each flat launch it made (bench.py's
     roofline probe replays the largest)."""
 
     def __init__(self):
@@ -976,20 +976,25 @@ def _queue_tiled(d, R, jobs, keep):
 
 
 def _flush_tiled(d):
+    """Every queued T-layout weight gradient, whatever its row count (the line-node rows of the trunk,
+    the atom rows of the readout MLPs), in as few launches as X2G_TILED_MAX_JOBS allows: one at config 2
+    (x2g_tiled_wgrad_flat_rows; one launch per row count before).  ``d.flat_launches`` records each
+    launch as [(rows, cols) per job]."""
     lib = _lib.load()
     d.flat_launches.clear()
-    for R, jobs in d.tiled.items():
-        for j0 in range(0, len(jobs), TILED_MAX_JOBS):
-            part = jobs[j0:j0 + TILED_MAX_JOBS]
-            n = len(part)
-            d.flat_launches.append((int(R), [int(j.cols) if j.ld > 0 else 128 for j in part]))
-            ws_bytes = int(lib.x2g_tiled_wgrad_flat_workspace(R, 128, n))
-            ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=torch.device("cuda", torch.cuda.current_device()))
-            out = (SlabJob * n)()
-            call("x2g_tiled_wgrad_flat", (TiledJob * n)(*part), n, R, 128, ACCUM_WGRAD | DEFER_SLAB_SUM, out, ptr(ws),
-                 ws_bytes, stream_ptr())
-            d.jobs.extend(out)
-            d.keep.append(ws)
+    items = [(int(R), j) for R, jobs in d.tiled.items() for j in jobs]
+    for j0 in range(0, len(items), TILED_MAX_JOBS):
+        part = items[j0:j0 + TILED_MAX_JOBS]
+        n = len(part)
+        d.flat_launches.append([(R, int(j.cols) if j.ld > 0 else 128) for R, j in part])
+        rows = (ctypes.c_int64 * n)(*[R for R, _ in part])
+        ws_bytes = int(lib.x2g_tiled_wgrad_flat_rows_workspace(rows, n, 128))
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=torch.device("cuda", torch.cuda.current_device()))
+        out = (SlabJob * n)()
+        call("x2g_tiled_wgrad_flat_rows", (TiledJob * n)(*[j for _, j in part]), rows, n, 128,
+             ACCUM_WGRAD | DEFER_SLAB_SUM, out, ptr(ws), ws_bytes, stream_ptr())
+        d.jobs.extend(out)
+        d.keep.append(ws)
     d.tiled = {}
 
 

@@ -56,7 +56,7 @@ class Trainer:
         self.opt = FlatAdam(model.parameters(), lr=lr, max_norm=max_norm, ema_decay=ema_decay, bucket=self.bucket)
         if lr_schedule is not None:
             self.opt.set_schedule(base_lr=lr, **lr_schedule)
-        self.flat_launches = []  # (rows, [cols per job]) of the last backward's flat weight-gradient launches
+        self.flat_launches = []  # [(rows, cols) per job] of the last backward's flat weight-gradient launches
         self.counts = (local_count, global_count)
         self.exchange_chunks = int(exchange_chunks)
         self.graphs = None
