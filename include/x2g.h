@@ -94,6 +94,15 @@ int x2g_line_graph_transpose_sym(const int32_t* edge_src, const int32_t* edge_ds
                                  const int32_t* trip_rowptr, int64_t num_edges, int32_t* src_rowptr,
                                  int32_t* src_perm, int32_t* src_dst, void* workspace, size_t workspace_bytes,
                                  void* stream);
+/* Both at once for a training batch (a backward will need the transpose): x2g_vertex_to_edge_sym's
+ * outputs and x2g_line_graph_transpose_sym's (src_rowptr [E+1], src_perm [T], src_dst [T] or NULL) in
+ * three launches instead of five — the source row pointer from the same one-workgroup scan, the
+ * emission and the transpose in one grid.  Outputs equal the two entry points' bit for bit. */
+int x2g_line_graph_sym_build(const int32_t* edge_src, const int32_t* edge_dst, int64_t num_edges, int64_t num_nodes,
+                             int64_t num_triplets, int32_t* atom_rowptr, int32_t* trip_rowptr, int32_t* trip_src,
+                             int32_t* trip_dst, int32_t* atom_j, int32_t* atom_i, int32_t* atom_k,
+                             int32_t* src_rowptr, int32_t* src_perm, int32_t* src_dst, void* workspace,
+                             size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- basis (featurisation) */
 

@@ -92,18 +92,22 @@ def test_vertex_to_edge_edge_cases(cuda):
 
 
 def _sym_vs_generic(ei, n, T, cuda):
-    """x2g_vertex_to_edge_sym / x2g_line_graph_transpose_sym against the generic builder and
-    transpose on the same symmetric graph: every output bit-for-bit."""
+    """x2g_vertex_to_edge_sym / x2g_line_graph_transpose_sym and x2g_line_graph_sym_build against the
+    generic builder and transpose on the same symmetric graph: every output bit-for-bit."""
     from x2gnn import ops
 
     e = torch.from_numpy(ei.astype(np.int64)).to(cuda)
     gen = ops.vertex_to_edge(e, n, T)
-    sym = ops.vertex_to_edge(e, n, T, symmetric=True)
-    for name in ("atom_rowptr", "trip_rowptr", "trip_src", "trip_dst", "atom_j", "atom_i", "atom_k"):
-        assert torch.equal(getattr(gen, name), getattr(sym, name)), name
-    for a, b in zip(gen.src_csr(), sym.src_csr()):
-        assert torch.equal(a, b)
-    assert torch.equal(gen.src_dst, sym.src_dst)
+    ei32 = ops._i32(e)
+    # the two entry points in turn (transpose built on first use) and x2g_line_graph_sym_build (both at once)
+    for wt in (False, True):
+        sym = ops.LineGraph(ei32[0].contiguous(), ei32[1].contiguous(), n, T, symmetric=True, with_transpose=wt)
+        assert (sym._src_rowptr is not None) == wt
+        for name in ("atom_rowptr", "trip_rowptr", "trip_src", "trip_dst", "atom_j", "atom_i", "atom_k"):
+            assert torch.equal(getattr(gen, name), getattr(sym, name)), (name, wt)
+        for a, b in zip(gen.src_csr(), sym.src_csr()):
+            assert torch.equal(a, b), wt
+        assert torch.equal(gen.src_dst, sym.src_dst), wt
     # src_dst = trip_dst[src_perm]; and the source-uniform edge row the fold pass relies on: every
     # triplet of source s = (b->k) goes into a destination (a->b) whose destination atom is s's source
     perm = sym.src_csr()[1].long()

@@ -161,12 +161,12 @@ __global__ void triplet_count_kernel(const int32_t* __restrict__ src, const int3
 // Emit the triplets of 8 destination edges per wave: lane group of 8 walks N_out(b) in
 // chunks of 8, compacts with a ballot so writes of one group are contiguous.
 constexpr int kEmitGroup = 8;
-__global__ void triplet_emit_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
-                                    const int32_t* __restrict__ atom_rowptr,
-                                    const int32_t* __restrict__ trip_rowptr, int64_t E, int64_t T,
-                                    int32_t* __restrict__ trip_src, int32_t* __restrict__ trip_dst,
-                                    int32_t* __restrict__ atom_j, int32_t* __restrict__ atom_i,
-                                    int32_t* __restrict__ atom_k) {
+__device__ __forceinline__ void emit_group(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                                           const int32_t* __restrict__ atom_rowptr,
+                                           const int32_t* __restrict__ trip_rowptr, int64_t E, int64_t T,
+                                           int32_t* __restrict__ trip_src, int32_t* __restrict__ trip_dst,
+                                           int32_t* __restrict__ atom_j, int32_t* __restrict__ atom_i,
+                                           int32_t* __restrict__ atom_k) {
   const int64_t gtid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int64_t e = gtid / kEmitGroup;
   const int sub = threadIdx.x & (kEmitGroup - 1);
@@ -199,6 +199,15 @@ __global__ void triplet_emit_kernel(const int32_t* __restrict__ src, const int32
     }
     p += __popcll(ball);
   }
+}
+
+__global__ void triplet_emit_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                                    const int32_t* __restrict__ atom_rowptr,
+                                    const int32_t* __restrict__ trip_rowptr, int64_t E, int64_t T,
+                                    int32_t* __restrict__ trip_src, int32_t* __restrict__ trip_dst,
+                                    int32_t* __restrict__ atom_j, int32_t* __restrict__ atom_i,
+                                    int32_t* __restrict__ atom_k) {
+  emit_group(src, dst, atom_rowptr, trip_rowptr, E, T, trip_src, trip_dst, atom_j, atom_i, atom_k);
 }
 
 // ----------------------------------------------------------------------------- transpose
@@ -260,9 +269,15 @@ __global__ void degree_count(const int32_t* __restrict__ atom, const int32_t* __
 // One launch instead of a count launch + the three-phase scan for a training batch's line graph
 // (round 3: the counts were a separate grid launch before this one-workgroup scan).
 constexpr int kDegUnroll = 8;
+__device__ __forceinline__ void src_rowptr_sym_body(const int32_t* __restrict__ edge_src,
+                                                    const int32_t* __restrict__ atom_rowptr, int64_t E,
+                                                    int32_t* __restrict__ src_rowptr, int* lds);
+// sym_src (or NULL): also the symmetric graph's src_rowptr from edge_src = sym_src (src_rowptr_sym_body)
 __global__ void __launch_bounds__(kScan1Threads) degree_scan_1wg(const int32_t* __restrict__ atom,
                                                                 const int32_t* __restrict__ atom_rowptr, int64_t n,
-                                                                int32_t* __restrict__ out) {
+                                                                int32_t* __restrict__ out,
+                                                                const int32_t* __restrict__ sym_src = nullptr,
+                                                                int32_t* __restrict__ src_rowptr = nullptr) {
   __shared__ int cnt[kScan1Max];
   __shared__ int lds[kScan1Threads / 64];
   const int tid = threadIdx.x;
@@ -300,6 +315,7 @@ __global__ void __launch_bounds__(kScan1Threads) degree_scan_1wg(const int32_t* 
   __syncthreads();
   for (int64_t i = tid; i < n; i += kScan1Threads) out[i] = cnt[i];  // coalesced stores
   if (tid == 0) out[n] = total;
+  if (src_rowptr) src_rowptr_sym_body(sym_src, atom_rowptr, n, src_rowptr, lds);  // (uniform)
 }
 
 // src_rowptr of a SYMMETRIC edge set from the atoms instead of the edges: source s = (b->k) has
@@ -308,10 +324,9 @@ __global__ void __launch_bounds__(kScan1Threads) degree_scan_1wg(const int32_t* 
 // one scan over the atoms (contiguous atom_rowptr loads) instead of over the edges with two dependent
 // gathers per edge (degree_scan_1wg: 12 us at config 2, this 3-4 us).  The atoms that own edges are
 // 0 .. edge_src[E-1]; thread t takes a contiguous range of them.
-__global__ void __launch_bounds__(kScan1Threads) src_rowptr_sym_1wg(const int32_t* __restrict__ edge_src,
-                                                                   const int32_t* __restrict__ atom_rowptr, int64_t E,
-                                                                   int32_t* __restrict__ src_rowptr) {
-  __shared__ int lds[kScan1Threads / 64];
+__device__ __forceinline__ void src_rowptr_sym_body(const int32_t* __restrict__ edge_src,
+                                                    const int32_t* __restrict__ atom_rowptr, int64_t E,
+                                                    int32_t* __restrict__ src_rowptr, int* lds) {
   const int tid = threadIdx.x;
   const int64_t n = static_cast<int64_t>(edge_src[E - 1]) + 1;  // atoms 0 .. n-1 (the last owns edge E-1)
   const int64_t per = (n + kScan1Threads - 1) / kScan1Threads;
@@ -329,6 +344,13 @@ __global__ void __launch_bounds__(kScan1Threads) src_rowptr_sym_1wg(const int32_
     run += d * c;
   }
   if (tid == 0) src_rowptr[E] = total;
+}
+
+__global__ void __launch_bounds__(kScan1Threads) src_rowptr_sym_1wg(const int32_t* __restrict__ edge_src,
+                                                                   const int32_t* __restrict__ atom_rowptr, int64_t E,
+                                                                   int32_t* __restrict__ src_rowptr) {
+  __shared__ int lds[kScan1Threads / 64];
+  src_rowptr_sym_body(edge_src, atom_rowptr, E, src_rowptr, lds);
 }
 
 // out = exclusive scan of deg(atom[i]) - 1: one workgroup when it fits (counts and scan), else the
@@ -352,10 +374,11 @@ int degree_scan(const int32_t* atom, const int32_t* atom_rowptr, int64_t n, int3
 // id is trip_rowptr[e] plus that; e itself is found in a's sorted out-list.  A group of 8 lanes per
 // source walks b's neighbours 8 at a time (one search each, in parallel) and compacts with a
 // ballot, as the triplet emitter does.
-__global__ void transpose_sym_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
-                                     const int32_t* __restrict__ atom_rowptr, const int32_t* __restrict__ trip_rowptr,
-                                     const int32_t* __restrict__ src_rowptr, int64_t E,
-                                     int32_t* __restrict__ src_perm, int32_t* __restrict__ src_dst) {
+__device__ __forceinline__ void transpose_group(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                                                const int32_t* __restrict__ atom_rowptr,
+                                                const int32_t* __restrict__ trip_rowptr,
+                                                const int32_t* __restrict__ src_rowptr, int64_t E,
+                                                int32_t* __restrict__ src_perm, int32_t* __restrict__ src_dst) {
   const int64_t gtid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int64_t s = gtid / kEmitGroup;
   const int sub = threadIdx.x & (kEmitGroup - 1);
@@ -391,11 +414,32 @@ __global__ void transpose_sym_kernel(const int32_t* __restrict__ src, const int3
   }
 }
 
+__global__ void transpose_sym_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                                     const int32_t* __restrict__ atom_rowptr, const int32_t* __restrict__ trip_rowptr,
+                                     const int32_t* __restrict__ src_rowptr, int64_t E,
+                                     int32_t* __restrict__ src_perm, int32_t* __restrict__ src_dst) {
+  transpose_group(src, dst, atom_rowptr, trip_rowptr, src_rowptr, E, src_perm, src_dst);
+}
+
+// both per-edge passes of a symmetric line graph in one grid: edge g emits its triplets as a
+// destination (emit_group) and lists them as a source (transpose_group, which reads only trip_rowptr)
+__global__ void emit_transpose_sym_kernel(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                                          const int32_t* __restrict__ atom_rowptr,
+                                          const int32_t* __restrict__ trip_rowptr,
+                                          const int32_t* __restrict__ src_rowptr, int64_t E, int64_t T,
+                                          int32_t* __restrict__ trip_src, int32_t* __restrict__ trip_dst,
+                                          int32_t* __restrict__ atom_j, int32_t* __restrict__ atom_i,
+                                          int32_t* __restrict__ atom_k, int32_t* __restrict__ src_perm,
+                                          int32_t* __restrict__ src_dst) {
+  emit_group(src, dst, atom_rowptr, trip_rowptr, E, T, trip_src, trip_dst, atom_j, atom_i, atom_k);
+  transpose_group(src, dst, atom_rowptr, trip_rowptr, src_rowptr, E, src_perm, src_dst);
+}
+
 }  // namespace x2g
 
 using namespace x2g;
 
-X2G_API int x2g_abi_version(void) { return 12; }
+X2G_API int x2g_abi_version(void) { return 13; }
 
 X2G_API const char* x2g_status_string(int status) {
   switch (status) {
@@ -533,5 +577,32 @@ X2G_API int x2g_line_graph_transpose_sym(const int32_t* edge_src, const int32_t*
   if (E > 0)
     transpose_sym_kernel<<<blocks_for(E * kEmitGroup, 256), 256, 0, st>>>(edge_src, edge_dst, atom_rowptr, trip_rowptr,
                                                                           src_rowptr, E, src_perm, src_dst);
+  return last_launch_status();
+}
+
+X2G_API int x2g_line_graph_sym_build(const int32_t* edge_src, const int32_t* edge_dst, int64_t E, int64_t N,
+                                     int64_t T, int32_t* atom_rowptr, int32_t* trip_rowptr, int32_t* trip_src,
+                                     int32_t* trip_dst, int32_t* atom_j, int32_t* atom_i, int32_t* atom_k,
+                                     int32_t* src_rowptr, int32_t* src_perm, int32_t* src_dst, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+  if (E < 0 || N < 0 || T < 0 || !atom_rowptr || !trip_rowptr || !src_rowptr) return X2G_EINVAL;
+  if (E > 0 && (!edge_src || !edge_dst)) return X2G_EINVAL;
+  if (T > 0 && (!trip_src || !trip_dst || !src_perm)) return X2G_EINVAL;
+  if (workspace_bytes < x2g_vertex_to_edge_workspace(E, N) || !workspace) return X2G_EWORKSPACE;
+  if (E == 0 || E > kScan1Max) {  // outside the one-workgroup scan: the two entry points in turn
+    if (int rc = x2g_vertex_to_edge_sym(edge_src, edge_dst, E, N, T, atom_rowptr, trip_rowptr, trip_src, trip_dst,
+                                        atom_j, atom_i, atom_k, workspace, workspace_bytes, stream))
+      return rc;
+    return x2g_line_graph_transpose_sym(edge_src, edge_dst, atom_rowptr, trip_rowptr, E, src_rowptr, src_perm,
+                                        src_dst, workspace, workspace_bytes, stream);
+  }
+  hipStream_t st = as_stream(stream);
+  int rc = x2g_csr_rowptr(edge_src, E, N, atom_rowptr, stream);
+  if (rc) return rc;
+  degree_scan_1wg<<<1, kScan1Threads, 0, st>>>(edge_dst, atom_rowptr, E, trip_rowptr, edge_src, src_rowptr);
+  if ((rc = last_launch_status())) return rc;
+  emit_transpose_sym_kernel<<<blocks_for(E * kEmitGroup, 256), 256, 0, st>>>(
+      edge_src, edge_dst, atom_rowptr, trip_rowptr, src_rowptr, E, T, trip_src, trip_dst, atom_j, atom_i, atom_k,
+      src_perm, src_dst);
   return last_launch_status();
 }

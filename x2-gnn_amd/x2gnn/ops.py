@@ -58,8 +58,13 @@ class LineGraph:
     src_rowptr/src_perm: the same triplets grouped by source line node (built on first use).
     """
 
-    def __init__(self, edge_src, edge_dst, num_nodes, num_triplets, symmetric=False):
+    def __init__(self, edge_src, edge_dst, num_nodes, num_triplets, symmetric=False, with_transpose=None):
+        """``with_transpose`` (default: symmetric and grad enabled, i.e. a backward will ask for
+        ``src_csr``): build the by-source lists with the line graph (x2g_line_graph_sym_build,
+        three launches for both instead of five)."""
         self.symmetric = bool(symmetric)  # caller-asserted: b->a present for every a->b (x2g_*_sym)
+        if with_transpose is None:
+            with_transpose = self.symmetric and torch.is_grad_enabled()
         self.E = int(edge_src.shape[0])
         self.N = int(num_nodes)
         self.T = int(num_triplets)
@@ -83,6 +88,15 @@ class LineGraph:
         self.dst_type = self.src_type = None
         ws_bytes = int(_lib.load().x2g_vertex_to_edge_workspace(self.E, self.N))
         self._ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        if with_transpose and self.symmetric:
+            self._src_rowptr = torch.empty(self.E + 1, **i32)
+            self._src_perm = torch.empty(self.T, **i32)
+            self._src_dst = torch.empty(self.T, **i32)
+            call("x2g_line_graph_sym_build", ptr(edge_src), ptr(edge_dst), self.E, self.N, self.T,
+                 ptr(self.atom_rowptr), ptr(self.trip_rowptr), ptr(self.trip_src), ptr(self.trip_dst),
+                 ptr(self.atom_j), ptr(self.atom_i), ptr(self.atom_k), ptr(self._src_rowptr), ptr(self._src_perm),
+                 ptr(self._src_dst), ptr(self._ws), ws_bytes, stream_ptr())
+            return
         call("x2g_vertex_to_edge_sym" if self.symmetric else "x2g_vertex_to_edge", ptr(edge_src), ptr(edge_dst),
              self.E, self.N, self.T, ptr(self.atom_rowptr), ptr(self.trip_rowptr), ptr(self.trip_src),
              ptr(self.trip_dst), ptr(self.atom_j), ptr(self.atom_i), ptr(self.atom_k), ptr(self._ws), ws_bytes,
