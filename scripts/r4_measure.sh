@@ -22,7 +22,7 @@ pmc2() {  # pmc2 <name> <bench args...>: FETCH_SIZE pass, WRITE_SIZE pass, summa
   run sum_$name 120 python scripts/pmc_traffic.py gpurun_out/pmcf_${name}_$TAG gpurun_out/pmcw_${name}_$TAG gpurun_out/pmc_traffic_${name}_$TAG.json
 }
 # PARTS selects the stages (a call is capped at 20 min): pmc (the four PMC summaries), work (step table),
-# bench (the four bench lines)
+# bench (the four bench lines), prof (config 2's bench command under rocprofv3 --kernel-trace --stats)
 PARTS=${PARTS:-pmc work bench}
 has() { [[ " $PARTS " == *" $1 "* ]]; }
 P="--steps 2 --warmup 1 --no-cpu-baseline --kernel-reps 3"
@@ -47,6 +47,10 @@ fi
 # the bench lines read the summaries installed above (on this box; the caller copies them into profiles/)
 has bench || exit 0
 run bench_c2 420 python bench.py
+# the same command under rocprofv3 (kernel stats: the roofline kernel's average launch must agree)
+if has prof; then
+run prof_c2 420 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2_$TAG -o run --output-format csv -- python "$ROOT/bench.py" --no-cpu-baseline
+fi
 run bench_s5a 420 python bench.py --shape S5A --no-cpu-baseline
 run bench_c3 420 python bench.py --workload qm9_allprop --target 0
 run bench_c5 420 python bench.py --workload aid_infer --steps 50 --warmup 5
