@@ -144,5 +144,6 @@ def test_two_rank_product_ddp_equals_single_process(cuda):
         a, b = dp[off:off + n], ref[off:off + n]
         assert np.abs(a - b).max() <= 1e-4 * np.abs(b).max() + 1e-7 * scale
     # the loss slot holds the global-batch mean loss
-    assert abs(float(dp[ngrad]) - float(loss)) <= 1e-5 * max(1.0, abs(float(loss)))
-    assert abs(got[0][2] - float(loss)) <= 1e-5 * max(1.0, abs(float(loss)))
+    loss = float(loss.detach())
+    assert abs(float(dp[ngrad]) - loss) <= 1e-5 * max(1.0, abs(loss))
+    assert abs(got[0][2] - loss) <= 1e-5 * max(1.0, abs(loss))
