@@ -22,6 +22,7 @@
 //    dlogit[T,H], and d_sbfproj[T,HC] (for dW_sbf = d_sbfproj^T sbf);
 //  * source-major (bwd_src) over the transposed triplet lists: dk and dv, each a fixed-order
 //    segmented sum (the adjoint of the k_j / v_j gathers).
+#include <type_traits>
 #include <math.h>
 
 #include "common.hpp"
@@ -959,22 +960,29 @@ __device__ __forceinline__ sp_rsrc_t sp_rsrc(const float* p, int64_t bytes) {
 constexpr int kSPWaves = 16;           // 1024-thread workgroups, one per CU
 constexpr int kSPChunks = 16 * kS / 4;  // 16-byte chunks per 16-row sbf block (168)
 
+// The two LDS slots of a wave are two NAMED arrays and the loop is unrolled by two, so every slot
+// index is static: with one dynamically indexed array the compiler could not tell the slot a ds_read
+// reads from the slot the next block's buffer_load ... lds is filling and waited for every copy in
+// flight (vmcnt(0)) before the B reads — the prefetch then bought nothing.  The wave index is read
+// through readfirstlane, so block bases and buffer descriptors live in SGPRs (a descriptor the
+// compiler thinks divergent costs a readfirstlane loop around every buffer instruction).
 template <int NOB>
 __device__ __forceinline__ void sbf_project_body(const float* __restrict__ sbf, const float* __restrict__ w,
                                                  const float* __restrict__ b, int64_t T, float* __restrict__ out) {
   typedef float f4t __attribute__((ext_vector_type(4)));
   __shared__ f4t Wl[NOB * kSPQ * 64];         // [ob][q][lane]: W[16ob + i][16q + 4g .. +3]
   __shared__ f4t Bl[NOB * 4];                 // [ob][g]: b[16ob + 4g .. +3]
-  __shared__ f4t Xs[kSPWaves][2][16 * 16];    // per wave, two slots: a 16-row sbf block (168 chunks),
-                                              // then 16 rows x 64 output columns, chunk-swizzled
+  __shared__ f4t XsA[kSPWaves][16 * 16];      // per wave, slot A / slot B: a 16-row sbf block (168
+  __shared__ f4t XsB[kSPWaves][16 * 16];      // chunks), then 16 rows x 64 output columns, swizzled
   constexpr int N = 16 * NOB;
   constexpr int HB = NOB < 4 ? NOB : 4;       // output blocks per half (64 columns)
+  constexpr int kStores = NOB;                // store instructions per block (NOB / HB halves x HB)
   for (int idx = threadIdx.x; idx < NOB * kSPQ * 64; idx += blockDim.x) {
     const int l = idx & 63, q = (idx >> 6) % kSPQ, ob = (idx >> 6) / kSPQ;
-    const int c = 16 * ob + (l & 15), k = 16 * q + 4 * (l >> 4);
+    const int c = 16 * ob + (l & 15), k = 16 * q + (l >> 4);  // element e: contraction index k + 4e
     f4t v;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = k + e < kS ? w[c * kS + k + e] : 0.0f;
+    for (int e = 0; e < 4; ++e) v[e] = k + 4 * e < kS ? w[c * kS + k + 4 * e] : 0.0f;
     Wl[idx] = v;
   }
   for (int idx = threadIdx.x; idx < NOB * 4; idx += blockDim.x) {
@@ -984,46 +992,52 @@ __device__ __forceinline__ void sbf_project_body(const float* __restrict__ sbf, 
     Bl[idx] = v;
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
+  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int64_t nblk = (T + 15) / 16;
   const int64_t nw = static_cast<int64_t>(gridDim.x) * kSPWaves;
-  int64_t blk = static_cast<int64_t>(blockIdx.x) * kSPWaves + wv;
+  f4t* const slotA = &XsA[wv][0];
+  f4t* const slotB = &XsB[wv][0];
   // a block's rows are 2688 contiguous bytes: chunk u * 64 + lane of the block (chunks >= 168 and rows
   // >= T read as zero through the range check)
-  auto issue = [&](int64_t bk, int slot) {
+  auto issue = [&](int64_t bk, f4t* slot) {
     const float* base = sbf + bk * (16 * kS);
     const sp_rsrc_t r = sp_rsrc(base, (T - bk * 16) * kS * 4);
 #pragma unroll
     for (int u = 0; u < 3; ++u)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(&Xs[wv][slot][64 * u]), 16,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(slot + 64 * u), 16,
                                                (64 * u + lane) < kSPChunks ? 16 * (64 * u + lane) : 0x7fffff00, 0, 0,
                                                0);
   };
-  int slot = 0;
-  if (blk < nblk) issue(blk, 0);
-  for (; blk < nblk; blk += nw) {
-    const bool more = blk + nw < nblk;
-    if (more) issue(blk + nw, slot ^ 1);
+  // block bk from `cur` (its copy issued one block earlier); the next block's copy goes to `nxt`
+  auto block = [&](int64_t bk, f4t* cur, f4t* nxt, auto first) {
+    // the next block's copy, unconditionally (past the end its descriptor has no records: zeros land
+    // in the idle slot) — no branch, so the compiler's wait counts stay exact
+    issue(bk + nw, nxt);
     asm volatile("" ::: "memory");
-    // this block's copy is done when at most the next block's 3 copies (issued after it) remain;
-    // the previous block's stores went out before those and may still be in flight only if counted
-    if (more)
+    // this block's copy is done when at most what was issued after it remains: the previous block's
+    // stores and the next block's 3 copies (the stores read registers: nothing waits for them)
+    if constexpr (decltype(first)::value)  // nothing was stored before the first block
       asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // B operand: lane (i, g) = row i, k = 16q + 4g + e (row i's floats at 42 i: 8-byte aligned)
-    const float* xr = reinterpret_cast<const float*>(&Xs[wv][slot][0]) + i * kS;
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kStores + 3) : "memory");
+    // B operand: lane (i, g) = row i, k = 16q + 4e + g (row i's floats at 42 i).  MFMA (q, e) then
+    // contracts the 4 consecutive indices 16q + 4e .. +3, so the all-padding group k = 44..47 is
+    // skipped: 11 MFMAs per output block instead of 12
+    const float* xr = reinterpret_cast<const float*>(cur) + i * kS + g;
     f4t B[kSPQ];
 #pragma unroll
-    for (int q = 0; q < kSPQ; ++q) {
-      const int k = 16 * q + 4 * g;
-      const float2 lo = *reinterpret_cast<const float2*>(xr + (k < kS ? k : 0));
-      const float2 hi = *reinterpret_cast<const float2*>(xr + (k + 2 < kS ? k + 2 : 0));
-      B[q] = f4t{k < kS ? lo.x : 0.0f, k < kS ? lo.y : 0.0f, k + 2 < kS ? hi.x : 0.0f, k + 2 < kS ? hi.y : 0.0f};
-    }
-    float* ob = out + blk * 16 * N;
-    const sp_rsrc_t orr = sp_rsrc(ob, (T - blk * 16) * N * 4);
-    float* ys = reinterpret_cast<float*>(&Xs[wv][slot][0]);  // B is in registers: the slot is free
+    for (int q = 0; q < kSPQ; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k0 = 16 * q + 4 * e;  // + g: padding when >= kS (the read stays inside the slot)
+        if (k0 >= kS) continue;          // (the skipped group)
+        const float xv = xr[k0];
+        B[q][e] = k0 + g < kS ? xv : 0.0f;
+      }
+    float* ob = out + bk * 16 * N;
+    const sp_rsrc_t orr = sp_rsrc(ob, (T - bk * 16) * N * 4);
+    float* ys = reinterpret_cast<float*>(cur);  // B is in registers: the slot is free
 #pragma unroll
     for (int h0 = 0; h0 < NOB; h0 += HB) {
       f4t acc[HB];
@@ -1035,9 +1049,11 @@ __device__ __forceinline__ void sbf_project_body(const float* __restrict__ sbf, 
 #pragma unroll
         for (int j = 0; j < HB; ++j) a[j] = Wl[((h0 + j) * kSPQ + q) * 64 + lane];
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+        for (int e = 0; e < 4; ++e) {
+          if (16 * q + 4 * e >= kS) continue;  // an all-padding contraction group
 #pragma unroll
           for (int j = 0; j < HB; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][e], B[q][e], acc[j], 0, 0, 0);
+        }
       }
       // D lane (i, g): row i, local columns 16 j + 4 g .. +3 = chunk 4 j + g of the row's 16
 #pragma unroll
@@ -1051,7 +1067,19 @@ __device__ __forceinline__ void sbf_project_body(const float* __restrict__ sbf, 
                                                4 * (r * N + 16 * h0 + 4 * c), 0, 0);
       }
     }
-    slot ^= 1;
+  };
+  // the first block peeled (nothing stored before it), then pairs: every block's wait then sees the
+  // same history on all paths into it and the compiler's own count for the slot reads stays exact
+  int64_t blk = static_cast<int64_t>(blockIdx.x) * kSPWaves + wv;
+  if (blk < nblk) {
+    issue(blk, slotA);
+    block(blk, slotA, slotB, std::true_type{});
+    for (blk += nw; blk < nblk; blk += nw) {
+      block(blk, slotB, slotA, std::false_type{});
+      blk += nw;
+      if (blk >= nblk) break;
+      block(blk, slotA, slotB, std::false_type{});
+    }
   }
 }
 
