@@ -331,6 +331,10 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
         const f4 n0 = *reinterpret_cast<const f4*>(Y1 + i * kFYS + 16 * qa + 4 * g);
         const f4 n1 = *reinterpret_cast<const f4*>(Y1 + (16 + i) * kFYS + 16 * qa + 4 * g);
         if (q + 2 < 16) wq[(q + 2) % 3] = *reinterpret_cast<const f4*>(w2s + 16 * (q + 2));
+        // pins the group-(q + 2) load ahead of group q's MFMAs: left alone, the scheduler hoisted the
+        // MFMAs over it, so each load issued one group ahead and was waited for (vmcnt(0)) after only
+        // 8 MFMAs — an L2 round trip not covered
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           acc2[0] = mfma4(y0[e], wq[q % 3][e], acc2[0]);
