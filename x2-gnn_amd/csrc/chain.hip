@@ -1147,6 +1147,95 @@ __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, cons
   }
 }
 
+// NB = 2 with the two buffers as distinct NAMED LDS arrays and the step loop unrolled by two, so every
+// buffer index is static.  With one dynamically indexed [NB] array the compiler could not tell the
+// buffer a step reads from the one the next step's copies are filling, and waited for those copies
+// (vmcnt(0)) before the step's first LDS read: step i + 1's copy never ran under step i's MFMAs.  The
+// next step's copy is issued unconditionally (past the segment's end it re-reads tile t0 into the idle
+// buffer, drained at the end), since a branch around it would merge two wait histories into vmcnt(0).
+template <bool SPREAD, int WT>
+__device__ __forceinline__ void tiled_segment2(const float* __restrict__ dz, const float* __restrict__ xin, int64_t t0,
+                                               int64_t t1, bool has_b, float* __restrict__ slab,
+                                               float* __restrict__ slab_b, f4 (*D0)[512], f4 (*X0)[512],
+                                               f4 (*D1)[512], f4 (*X1)[512]) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rl = lane & 15, g = lane >> 4;
+  const int nsteps = static_cast<int>((t1 - t0 + WT - 1) / WT);
+  const int P = 64 * w + lane;
+  const int src_chunk = (P >> 2) * 4 + ((P & 3) ^ (((P >> 5) & 1) * 3));
+  // buffer_load ... lds over the segment's tiles (global_load_lds carried no LDS memory operand the
+  // compiler could tell apart, so it waited on it before any LDS read even with separate buffers)
+  const int64_t nt = t1 - t0;
+  const int nbytes = static_cast<int>(nt * 8192 < 0x7fffffff ? nt * 8192 : 0x7fffffff);
+  const rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dz + t0 * 2048), static_cast<short>(0), nbytes,
+                                                      0x00020000);
+  const rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xin + t0 * 2048), static_cast<short>(0), nbytes,
+                                                      0x00020000);
+  auto issue = [&](int step, f4 (*Dd)[512], f4 (*Xd)[512]) {  // tiles past t1: tile t0
+#pragma unroll
+    for (int k = 0; k < WT; ++k) {
+      int tt = step * WT + k;
+      tt = tt < nt ? tt : 0;
+      const int vo = tt * 8192 + 16 * src_chunk;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dr, (__attribute__((address_space(3))) void*)(&Dd[k][64 * w]), 16, vo, 0,
+                                               0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(&Xd[k][64 * w]), 16, vo, 0,
+                                               0, 0);
+    }
+  };
+  f4 acc[8];
+#pragma unroll
+  for (int bk = 0; bk < 8; ++bk) acc[bk] = zero4();
+  float bsum = 0.f;
+  auto body = [&](int i, f4 (*Dc)[512], f4 (*Xc)[512], f4 (*Dn)[512], f4 (*Xn)[512]) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this step's copies (the only ones in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's copies of this step have landed; step i - 1 is read
+    issue(i + 1, Dn, Xn);
+#pragma unroll
+    for (int k = 0; k < WT; ++k) {
+      if (t0 + static_cast<int64_t>(i) * WT + k >= t1) break;  // wave-uniform
+      const f4 av = Dc[k][tpos(16 * w + rl, g)];
+      f4 bv[8];
+#pragma unroll
+      for (int bk = 0; bk < 8; ++bk) bv[bk] = Xc[k][tpos(16 * bk + rl, g)];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int bk = 0; bk < 8; ++bk) acc[bk] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[bk][e], acc[bk], 0, 0, 0);
+      if (SPREAD && has_b) {
+        const f4 v = Dc[k][tpos(tid & (kCD - 1), tid >> 7)];
+        bsum += (v[0] + v[1]) + (v[2] + v[3]);
+      }
+      if (!SPREAD && tid < 128) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f4 v = Dc[k][tpos(tid, q)];
+          bsum += (v[0] + v[1]) + (v[2] + v[3]);
+        }
+      }
+    }
+  };
+  if (nsteps > 0) issue(0, D0, X0);
+  for (int i = 0; i < nsteps; i += 2) {
+    body(i, D0, X0, D1, X1);
+    if (i + 1 >= nsteps) break;
+    body(i + 1, D1, X1, D0, X0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the copy issued past the end lands before reuse
+#pragma unroll
+  for (int bk = 0; bk < 8; ++bk)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) slab[(16 * w + 4 * g + e) * kCD + 16 * bk + rl] = acc[bk][e];
+  if (!SPREAD && has_b && tid < 128) slab_b[tid] = bsum;
+  if (SPREAD && has_b) {  // the four row-quad partials of each feature, in quad order
+    __shared__ float bred[4 * kCD];
+    bred[tid] = bsum;
+    __syncthreads();
+    if (tid < kCD) slab_b[tid] = ((bred[tid] + bred[kCD + tid]) + bred[2 * kCD + tid]) + bred[3 * kCD + tid];
+  }
+}
+
 __global__ void __launch_bounds__(kCThreads, 1) chain_wgrad_kernel(const ChainWgradArgs a) {
   __shared__ f4 Ds[3][kWTiles][512];
   __shared__ f4 Xs[3][kWTiles][512];
@@ -1177,8 +1266,11 @@ struct TiledFlatArgs {
 // NB LDS buffers of 2 x WT tiles (NB x WT x 16 KB; NB - 1 steps in flight); WPC workgroups per CU
 template <int NB, bool SPREAD = true, int WT = kWTiles, int WPC = 1>
 __global__ void __launch_bounds__(kCThreads, 2 * WPC) tiled_flat_kernel(const TiledFlatArgs a) {
-  __shared__ f4 Ds[NB][WT][512];
-  __shared__ f4 Xs[NB][WT][512];
+  static_assert(NB == 2, "the flat launch's two named buffers (tiled_segment2)");
+  __shared__ f4 D0[WT][512];
+  __shared__ f4 X0[WT][512];
+  __shared__ f4 D1[WT][512];
+  __shared__ f4 X1[WT][512];
   const int64_t G = gridDim.x, i = blockIdx.x;
   const int64_t lo = i * a.total / G, hi = (i + 1) * a.total / G;
   X2G_CLK(0);
@@ -1190,8 +1282,8 @@ __global__ void __launch_bounds__(kCThreads, 2 * WPC) tiled_flat_kernel(const Ti
     if (s0 >= s1) continue;
     __syncthreads();  // a previous segment's last buffers are no longer read
     const int64_t k = i - a.wg_lo[j];
-    tiled_segment<NB, SPREAD, WT>(a.dz_t[j], a.in_t[j], s0 - a.tile0[j], s1 - a.tile0[j], a.has_b[j] != 0,
-                  a.slab_w[j] + k * kCD * kCD, a.slab_b[j] + k * kCD, Ds, Xs);
+    tiled_segment2<SPREAD, WT>(a.dz_t[j], a.in_t[j], s0 - a.tile0[j], s1 - a.tile0[j], a.has_b[j] != 0,
+                               a.slab_w[j] + k * kCD * kCD, a.slab_b[j] + k * kCD, D0, X0, D1, X1);
   }
   X2G_CLK(1);
 }
