@@ -1186,7 +1186,7 @@ struct FoldArgs {
   const int32_t *rowptr, *tidx, *tdst;
   const int32_t *sdst, *src_row;  // source pass: destination per source-major position / edge row per source
   const float *alpha, *smax, *sden, *prob, *rho_in, *g_in, *dout;
-  int64_t E;
+  int64_t E, T;
   int D, H;
   float sqrt_c;
   float *dq, *d_edge, *g_out, *prob_out, *rho_out, *dk, *dv, *gfold;
@@ -1197,12 +1197,12 @@ void fold_launch_mode(bool dst, const FoldArgs& a, unsigned blocks, hipStream_t 
   if (dst) {  // destination-major pass
     if (a.mode == X2G_EDGE_PER_DST)
       attn_bwd_dst_g_batched<CPL, LPH, X2G_EDGE_PER_DST><<<blocks, 256, 0, st>>>(
-          a.q, a.k, a.v, a.edge, a.edge_row, a.sp, a.rowptr, a.tidx, a.alpha, a.smax, a.sden, a.dout, a.E, a.D, a.H,
-          a.sqrt_c, a.dq, a.d_edge, a.g_out, a.prob_out, a.rho_out);
+          a.q, a.k, a.v, a.edge, a.edge_row, a.sp, a.rowptr, a.tidx, a.alpha, a.smax, a.sden, a.dout, a.E, a.T, a.D,
+          a.H, a.sqrt_c, a.dq, a.d_edge, a.g_out, a.prob_out, a.rho_out);
     else
       attn_bwd_dst_g_batched<CPL, LPH, X2G_EDGE_NONE><<<blocks, 256, 0, st>>>(
-          a.q, a.k, a.v, a.edge, a.edge_row, a.sp, a.rowptr, a.tidx, a.alpha, a.smax, a.sden, a.dout, a.E, a.D, a.H,
-          a.sqrt_c, a.dq, a.d_edge, a.g_out, a.prob_out, a.rho_out);
+          a.q, a.k, a.v, a.edge, a.edge_row, a.sp, a.rowptr, a.tidx, a.alpha, a.smax, a.sden, a.dout, a.E, a.T, a.D,
+          a.H, a.sqrt_c, a.dq, a.d_edge, a.g_out, a.prob_out, a.rho_out);
   } else {  // source-major pass
     const int C = a.D / a.H;
 #define X2G_SRC_FOLD(TABLE, SROW, GIN)                                                                           \
@@ -1274,7 +1274,7 @@ X2G_API int x2g_sbf_attention_bwd_dst_g(const float* q, const float* k, const fl
   FoldArgs a{};
   a.q = q; a.k = k; a.v = v; a.edge = edge; a.edge_row = edge_row; a.mode = edge_mode; a.sp = sbfproj;
   a.rowptr = trip_rowptr; a.tidx = trip_src; a.alpha = alpha_raw; a.smax = seg_max; a.sden = seg_den; a.dout = dout;
-  a.E = E; a.dq = dq; a.d_edge = d_edge; a.g_out = g_out; a.prob_out = prob_out; a.rho_out = seg_rho;
+  a.E = E; a.T = T; a.dq = dq; a.d_edge = d_edge; a.g_out = g_out; a.prob_out = prob_out; a.rho_out = seg_rho;
   return fold_dispatch(true, a, heads, channels, as_stream(stream));
 }
 
