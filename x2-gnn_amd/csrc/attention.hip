@@ -58,6 +58,7 @@ struct AttnArgs {
   const float* dlogit_in;
   const float* dout;
   int64_t E;
+  int64_t T;
   int D;
   int H;
   float sqrt_c;
@@ -365,12 +366,6 @@ __device__ __forceinline__ void fwd_batch(int k0, int n, int tb, int sl, FwdStat
   }
 }
 
-// Source ids of one chunk (<= 64 triplets) of a destination segment, lane i <-> triplet t + i (the
-// wave then broadcasts them with v_readlane); an empty chunk loads nothing.
-__device__ __forceinline__ int dst_chunk_src(int t, int n, int lane, const int32_t* __restrict__ tsrc) {
-  if (n <= 0) return 0;  // (wave-uniform)
-  return tsrc[t + (lane < n ? lane : n - 1)];
-}
 
 // Software-pipelined over the wave's destinations: the row pointer two segments ahead, the next
 // segment's source ids and this segment's skip row are requested at the top of the segment, so the
@@ -381,13 +376,21 @@ __global__ void __launch_bounds__(256) attn_fwd_batched(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v,
     const float* __restrict__ skip, const float* __restrict__ edge, const int32_t* __restrict__ edge_row,
     const float* __restrict__ sp, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ tsrc, int64_t E,
-    int D, int H, float sqrt_c, float* __restrict__ out, float* __restrict__ alpha_out, float* __restrict__ smax_out,
-    float* __restrict__ sden_out, float2* __restrict__ row_stats) {
+    int64_t T, int D, int H, float sqrt_c, float* __restrict__ out, float* __restrict__ alpha_out,
+    float* __restrict__ smax_out, float* __restrict__ sden_out, float2* __restrict__ row_stats) {
   const int lane = threadIdx.x & 63;
   const bool act = lane * CPL < D;
   const int c0 = act ? lane * CPL : 0;
   const int head = lane / LPH;
   const bool leader = act && (lane % LPH) == 0;
+  // source ids through a descriptor: unconditional loads (see attn_bwd_dst_g_batched)
+  const int tbytes = static_cast<int>(T * 4 < 0x7fffffff ? T * 4 : 0x7fffffff);
+  const __amdgpu_buffer_rsrc_t ts_r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(tsrc), static_cast<short>(0), tbytes, 0x00020000);
+  auto chunk_src = [&](int t, int n) {
+    const int idx = t + (lane < n ? lane : (n > 0 ? n - 1 : 0));
+    return static_cast<int>(__builtin_amdgcn_raw_buffer_load_b32(ts_r, n > 0 ? idx * 4 : 0x7ffffff0, 0, 0));
+  };
   const WaveRange wr_ = xcd_wave_range(E);
   int64_t e = wr_.first;
   if (e >= wr_.end) return;
@@ -395,7 +398,7 @@ __global__ void __launch_bounds__(256) attn_fwd_batched(
   int t0 = uniform(rowptr[e]), t1 = uniform(rowptr[e + 1]);
   const int64_t e1 = e + wr_.stride < wr_.end ? e + wr_.stride : last;
   int q0 = uniform(rowptr[e1]), q1 = uniform(rowptr[e1 + 1]);
-  int sl = dst_chunk_src(t0, t1 - t0 < 64 ? t1 - t0 : 64, lane, tsrc);
+  int sl = chunk_src(t0, t1 - t0 < 64 ? t1 - t0 : 64);
   // the edge-table row of the current / next destination (one segment ahead, like the source ids)
   int er = (MODE == X2G_EDGE_PER_DST && edge_row) ? uniform(edge_row[e]) : static_cast<int>(e);
   int ern = (MODE == X2G_EDGE_PER_DST && edge_row) ? uniform(edge_row[e1]) : static_cast<int>(e1);
@@ -416,10 +419,10 @@ __global__ void __launch_bounds__(256) attn_fwd_batched(
     const int64_t e2 = e2r < wr_.end ? e2r : last;
     const int r0 = uniform(rowptr[e2]), r1 = uniform(rowptr[e2 + 1]);
     const int er2 = (MODE == X2G_EDGE_PER_DST && edge_row) ? uniform(edge_row[e2]) : static_cast<int>(e2);
-    const int sln = dst_chunk_src(q0, q1 - q0 < 64 ? q1 - q0 : 64, lane, tsrc);
+    const int sln = chunk_src(q0, q1 - q0 < 64 ? q1 - q0 : 64);
     for (int tb = t0; tb < t1; tb += 64) {
       const int n = t1 - tb < 64 ? t1 - tb : 64;
-      if (tb != t0) sl = dst_chunk_src(tb, n, lane, tsrc);  // segments longer than 64 triplets
+      if (tb != t0) sl = chunk_src(tb, n);  // segments longer than 64 triplets
       int k0 = 0;
       for (; n - k0 > 4; k0 += 8)
         fwd_batch<CPL, LPH, MODE, 8>(k0, n, tb, sl, st, k, v, sp, D, H, c0, head, act, leader, sqrt_c, alpha_out);
@@ -760,7 +763,7 @@ void launch_pre(Pass pass, const AttnArgs& a, unsigned blocks, hipStream_t st) {
     case Pass::kFwd:
       if (PRE && MODE != X2G_EDGE_PER_TRIPLET) {  // batched: up to 8 triplets' rows in flight per wave
         attn_fwd_batched<CPL, LPH, MODE><<<blocks, 256, 0, st>>>(a.q, a.k, a.v, a.skip, a.edge, a.edge_row, a.sbf,
-                                                                 a.rowptr, a.tidx, a.E, a.D, a.H, a.sqrt_c, a.out,
+                                                                 a.rowptr, a.tidx, a.E, a.T, a.D, a.H, a.sqrt_c, a.out,
                                                                  a.alpha_out, a.smax_out, a.sden_out, a.row_stats);
         break;
       }
@@ -864,7 +867,7 @@ X2G_API int x2g_sbf_attention_fwd(const float* q, const float* k, const float* v
   if (edge_mode != X2G_EDGE_NONE && !edge) return X2G_EINVAL;
   AttnArgs a{};
   a.q = q; a.k = k; a.v = v; a.skip = skip; a.edge = edge; a.edge_row = edge_row; a.edge_mode = edge_mode;
-  a.sbf = sbf; a.w = w_sbf; a.b = b_sbf; a.rowptr = trip_rowptr; a.tidx = trip_src; a.E = E;
+  a.sbf = sbf; a.w = w_sbf; a.b = b_sbf; a.rowptr = trip_rowptr; a.tidx = trip_src; a.E = E; a.T = T;
   a.out = out; a.alpha_out = alpha_raw; a.smax_out = seg_max; a.sden_out = seg_den;
   return dispatch(Pass::kFwd, a, heads, channels, sbf_dim, as_stream(stream));
 }
@@ -883,7 +886,7 @@ X2G_API int x2g_sbf_attention_fwd_stats(const float* q, const float* k, const fl
   if (reinterpret_cast<uintptr_t>(row_stats) % 8) return X2G_EUNSUPPORTED;
   AttnArgs a{};
   a.q = q; a.k = k; a.v = v; a.skip = skip; a.edge = edge; a.edge_row = edge_row; a.edge_mode = edge_mode;
-  a.sbf = sbf; a.w = w_sbf; a.b = b_sbf; a.rowptr = trip_rowptr; a.tidx = trip_src; a.E = E;
+  a.sbf = sbf; a.w = w_sbf; a.b = b_sbf; a.rowptr = trip_rowptr; a.tidx = trip_src; a.E = E; a.T = T;
   a.out = out; a.alpha_out = alpha_raw; a.smax_out = seg_max; a.sden_out = seg_den;
   a.row_stats = reinterpret_cast<float2*>(row_stats);
   return dispatch(Pass::kFwd, a, heads, channels, sbf_dim, as_stream(stream));
