@@ -248,6 +248,17 @@ __global__ void __launch_bounds__(256) rbf_gate_bwd_kernel(const GateBwdJobs J, 
   // a row's basis values: lane j of each 16-lane DPP row loads value j (a data row spans whole DPP
   // rows, LPR >= 16) and row_newbcast hands value j to the row's lanes — one load per row, not R
   const int jl = (threadIdx.x & 15) < R ? (threadIdx.x & 15) : R - 1;
+  // the optional operands (owner, the accumulated drbf, dx_add) through descriptors that are empty when
+  // absent: every load is unconditional (a lane that must not read goes out of range and gets zero),
+  // so no branch merges two wait histories into a vmcnt(0) between the owner load and its gather
+  auto desc = [](const void* p, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), static_cast<short>(0),
+                                             static_cast<int>(bytes < 0x7fffffff ? bytes : 0x7fffffff), 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t own_r = desc(owner, owner ? rows * 4 : 0);
+  const __amdgpu_buffer_rsrc_t od_r = desc(drbf, (drbf && drbf_acc) ? rows * R * 4 : 0);
+  const __amdgpu_buffer_rsrc_t add_r = desc(dx_add, dx_add ? rows * LPR * 16 : 0);
+  const bool has_owner = owner != nullptr;
   for (int64_t r0 = lo + slot; r0 < hi; r0 += RPB * UNROLL) {
     float rv[UNROLL];
     f4v gv[UNROLL], xv[UNROLL], av[UNROLL];
@@ -256,11 +267,14 @@ __global__ void __launch_bounds__(256) rbf_gate_bwd_kernel(const GateBwdJobs J, 
     for (int u = 0; u < UNROLL; ++u) {  // every load of the UNROLL rows first
       const int64_t r = r0 + u * RPB, rc = r < hi ? r : hi - 1;
       rv[u] = rbf[rc * R + jl];
-      od[u] = acc_drbf ? drbf[rc * R + jd] : 0.0f;
-      const int64_t o = owner ? owner[rc] : rc;
+      od[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                            od_r, acc_drbf ? static_cast<int>((rc * R + jd) * 4) : 0x7ffffff0, 0, 0));
+      const int ow = static_cast<int>(__builtin_amdgcn_raw_buffer_load_b32(own_r, static_cast<int>(rc * 4), 0, 0));
+      const int64_t o = has_owner ? ow : rc;
       gv[u] = g[o * LPR + sub];
       xv[u] = x[rc * LPR + sub];
-      if (dx_add) av[u] = dx_add[rc * LPR + sub];
+      av[u] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                         add_r, static_cast<int>((rc * LPR + sub) * 16), 0, 0));
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
@@ -402,6 +416,9 @@ X2G_API int x2g_rbf_pool_fwd_batch(const x2g_gate_job* jobs, int32_t n_jobs, con
 
 static int gate_bwd_launch(const GateBwdJobs& J, int n_jobs, const int32_t* owner, const float* rbf, int64_t rows,
                            int D, int R, int drbf_acc, int splits, hipStream_t st) {
+  // (the optional operands go through 32-bit buffer offsets: rows x D floats below 2^31 bytes)
+  if (rows * static_cast<int64_t>(D) * 4 >= (int64_t(1) << 31) || rows * static_cast<int64_t>(R) * 4 >= (int64_t(1) << 31))
+    return X2G_EUNSUPPORTED;
   const dim3 grid(static_cast<unsigned>(splits), static_cast<unsigned>(n_jobs));
   switch (D) {
     case 64: rbf_gate_bwd_kernel<16><<<grid, 256, 0, st>>>(J, owner, rbf, rows, R, drbf_acc); break;
