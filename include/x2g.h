@@ -86,10 +86,14 @@ int x2g_line_graph_transpose(const int32_t* trip_src, const int32_t* trip_dst, i
  * triplets per destination a->b and per source b->k), so count and scan are one launch, and the
  * transposed lists are written in order directly (no atomics, no segment sort).  Outputs equal
  * x2g_vertex_to_edge's / x2g_line_graph_transpose's bit for bit on such graphs. */
+/* edge_rev / rev_trip (both or neither; NULL = not written), for the center-atom attention kernels:
+ * edge_rev[e] = id(b->a) for e = (a->b) (the neighbour vertex_to_edge_2 excludes), and
+ * rev_trip[id(b->a)] = trip_rowptr[e] — per source line node s, where the triplet block of its reverse
+ * edge starts. */
 int x2g_vertex_to_edge_sym(const int32_t* edge_src, const int32_t* edge_dst, int64_t num_edges, int64_t num_nodes,
                            int64_t num_triplets, int32_t* atom_rowptr, int32_t* trip_rowptr, int32_t* trip_src,
-                           int32_t* trip_dst, int32_t* atom_j, int32_t* atom_i, int32_t* atom_k, void* workspace,
-                           size_t workspace_bytes, void* stream);
+                           int32_t* trip_dst, int32_t* atom_j, int32_t* atom_i, int32_t* atom_k, int32_t* edge_rev,
+                           int32_t* rev_trip, void* workspace, size_t workspace_bytes, void* stream);
 int x2g_line_graph_transpose_sym(const int32_t* edge_src, const int32_t* edge_dst, const int32_t* atom_rowptr,
                                  const int32_t* trip_rowptr, int64_t num_edges, int32_t* src_rowptr,
                                  int32_t* src_perm, int32_t* src_dst, void* workspace, size_t workspace_bytes,
@@ -101,8 +105,8 @@ int x2g_line_graph_transpose_sym(const int32_t* edge_src, const int32_t* edge_ds
 int x2g_line_graph_sym_build(const int32_t* edge_src, const int32_t* edge_dst, int64_t num_edges, int64_t num_nodes,
                              int64_t num_triplets, int32_t* atom_rowptr, int32_t* trip_rowptr, int32_t* trip_src,
                              int32_t* trip_dst, int32_t* atom_j, int32_t* atom_i, int32_t* atom_k,
-                             int32_t* src_rowptr, int32_t* src_perm, int32_t* src_dst, void* workspace,
-                             size_t workspace_bytes, void* stream);
+                             int32_t* src_rowptr, int32_t* src_perm, int32_t* src_dst, int32_t* edge_rev,
+                             int32_t* rev_trip, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------- basis (featurisation) */
 
@@ -235,6 +239,46 @@ int x2g_sbf_attention_fwd_stats(const float* q, const float* k, const float* v, 
                                 const int32_t* trip_src, int64_t num_edges, int64_t num_triplets,
                                 int32_t heads, int32_t channels, int32_t sbf_dim, float* out,
                                 float* alpha_raw, float* seg_max, float* seg_den, float* row_stats, void* stream);
+
+/* The forward over a SYMMETRIC line graph grouped by center atom (csrc/attention_center.hip): the
+ * triplets through atom b are the block {(b->k_j) -> (k_i->b) : i != j} over b's n = deg(b) neighbours,
+ * so one workgroup per atom stages the n source rows of k and v (b's out-edges: contiguous line nodes)
+ * in LDS once, coalesced, and destination i = edge_rev[b->k_i] streams its contiguous triplet rows
+ * rev_trip[b->k_i] + 0 .. n-2.  Same outputs as x2g_sbf_attention_fwd(_stats) (row_stats may be NULL)
+ * on such graphs, up to fp32 rounding (per-batch softmax rescale, 4-channel head sums).
+ *   edge_mode X2G_EDGE_NONE or X2G_EDGE_PER_DST; for the latter the edge term of center atom b is row
+ *   src_row[atom_rowptr[b]] of `edge` (X2-GNN: the element-table row of b, the per-source src_type).
+ *   sbfproj: S rows for triplets t_base .. (row t - t_base), covering every triplet of the atoms
+ *   atom0 .. atom0 + n_atoms - 1 (whole molecules: the tiled inference path passes a molecule range).
+ *   max_degree >= every deg(b) of those atoms, <= X2G_CENTER_MAX_DEGREE (sizes the LDS image).
+ * heads * channels = 128 and channels a multiple of 4, 16-byte aligned rows, else X2G_EUNSUPPORTED. */
+#define X2G_CENTER_MAX_DEGREE 64
+int x2g_sbf_attention_fwd_center(const float* q, const float* k, const float* v, const float* skip,
+                                 const float* edge, const int32_t* src_row, int edge_mode, const float* sbfproj,
+                                 int64_t t_base, const int32_t* atom_rowptr, const int32_t* edge_rev,
+                                 const int32_t* rev_trip, int64_t atom0, int64_t n_atoms, int32_t max_degree,
+                                 int64_t num_edges, int64_t num_triplets, int32_t heads, int32_t channels, float* out,
+                                 float* alpha_raw, float* seg_max, float* seg_den, float* row_stats, void* stream);
+
+/* The whole attention backward over a SYMMETRIC line graph in ONE launch, one workgroup per center atom
+ * (csrc/attention_center.hip): the block's rows (k + e of its sources, dout and q of its destinations,
+ * their softmax max / denominator) staged in LDS, then per source j a pass over its triplets' S rows,
+ * alpha and Y (dv, the folded lin_sbf gradient G, the block's (a_t, g_t) tables), rho per destination,
+ * and dk, dq from LDS.  Replaces x2g_sbf_attention_bwd_dst_g + x2g_sbf_attention_bwd_src_fold on such
+ * graphs (same dq, dk, dv, radial_grad = G [E, 8, HC]; fp32 rounding apart), reading S once instead of
+ * twice and no row gathers; d_edge_atom [num_atoms, HC] (or NULL) = the per-CENTER-ATOM gradient of the
+ * edge term (sum over the atom's sources of dk + dv): the element-table gradient is its keyed sum by
+ * atom element.  sph_y [T, 8] as x2g_spherical_basis writes it.  LDS per workgroup:
+ * x2g_sbf_attention_bwd_center_lds(max_degree, heads) bytes (<= 160 KiB, else X2G_EUNSUPPORTED).
+ * heads * channels = 128, channels a multiple of 4, 16-byte aligned rows. */
+size_t x2g_sbf_attention_bwd_center_lds(int32_t max_degree, int32_t heads);
+int x2g_sbf_attention_bwd_center(const float* q, const float* k, const float* v, const float* edge,
+                                 const int32_t* src_row, int edge_mode, const float* sbfproj, const float* sph_y,
+                                 const int32_t* atom_rowptr, const int32_t* edge_rev, const int32_t* rev_trip,
+                                 const float* alpha_raw, const float* seg_max, const float* seg_den, const float* dout,
+                                 int64_t num_atoms, int32_t max_degree, int64_t num_edges, int64_t num_triplets,
+                                 int32_t heads, int32_t channels, float* dq, float* dk, float* dv, float* radial_grad,
+                                 float* d_edge_atom, void* stream);
 
 /* Backward, destination-major: dq[E,HC]; d_edge ([E,HC] per destination for EDGE_PER_DST,
  * [T,HC] for EDGE_PER_TRIPLET); dlogit[T,H] (grad of alpha_raw); d_sbfproj[T,HC] (grad of S_t,

@@ -116,6 +116,14 @@ def _sym_vs_generic(ei, n, T, cuda):
         rp = sym.src_csr()[0].long()
         src_of_pos = torch.repeat_interleave(torch.arange(sym.E, device=cuda), rp[1:] - rp[:-1])
         assert torch.equal(sym.edge_dst.long()[sym.src_dst.long()], sym.edge_src.long()[src_of_pos])
+    # the center-atom outputs: edge_rev[e] is the reverse edge, rev_trip[s] the triplet block start of
+    # s's reverse (trip_rowptr[edge_rev[s]])
+    if sym.E:
+        rev = sym.edge_rev.long()
+        assert torch.equal(sym.edge_src.long()[rev], sym.edge_dst.long())
+        assert torch.equal(sym.edge_dst.long()[rev], sym.edge_src.long())
+        assert torch.equal(rev[rev], torch.arange(sym.E, device=cuda))
+        assert torch.equal(sym.rev_trip, sym.trip_rowptr[rev])
     return sym
 
 
@@ -417,6 +425,32 @@ def test_scatter_add_any_index_order(cuda):
     up = torch.randn(60, 64, generator=g)
     (out * up.to(cuda)).sum().backward()
     torch.testing.assert_close(s.grad.cpu(), up.index_select(0, idx), rtol=0, atol=0)
+
+
+def test_index_plan_reused_across_scatter_and_softmax(cuda):
+    """One prebuilt IndexPlan serves scatter_add, scatter_mean and softmax (as MessagePassing reuses
+    edge_index[1]) with the same results as the raw-index calls; a plan built for another row count is
+    refused before any kernel reads through its permutation."""
+    from x2gnn import ops
+
+    g = torch.Generator().manual_seed(21)
+    idx = torch.randint(0, 30, (500,), generator=g)
+    idx[idx == 11] = 12  # an empty segment
+    src = torch.randn(500, 16, generator=g).to(cuda)
+    ic = idx.to(cuda)
+    plan = ops.IndexPlan(ic, 32)
+    assert torch.equal(ops.scatter_add(src, plan, 32), ops.scatter_add(src, ic, 32))
+    assert torch.equal(ops.scatter_mean(src, plan), ops.scatter_mean(src, ic, 32))
+    assert torch.equal(ops.softmax(src, plan), ops.softmax(src, ic, num_nodes=32))
+    s = src.clone().requires_grad_(True)
+    ops.scatter_add(s, plan, 32).sum().backward()
+    assert float(s.grad.sub(1.0).abs().max()) == 0.0
+    with pytest.raises(ValueError):
+        ops.scatter_add(src[:499], plan, 32)
+    with pytest.raises(ValueError):
+        ops.softmax(src[:499], plan)
+    with pytest.raises(ValueError):
+        ops.scatter_add(src, plan, 31)
 
 
 @pytest.mark.parametrize("D", [1, 3, 16, 128, 256])
@@ -959,6 +993,42 @@ def test_rbf_gate_vs_torch(cuda, rows, D, R, bias):
     call("x2g_rbf_gate_bwd", ptr(gy), None, ptr(x), ptr(rbf), ptr(w), ptr(b), rows, D, R, None, None, None, ptr(dw2),
          ptr(db2), 1, ptr(ws), ws_bytes, stream_ptr())
     torch.testing.assert_close(dw2, wr.grad + 1, rtol=1e-4, atol=1e-3)
+
+
+def test_rbf_gate_bwd_beyond_32bit_offsets(cuda):
+    """The gate backward at rows x D x 4 >= 2^31 bytes (4.2M rows at D = 128): without the optional
+    operands that take 32-bit buffer offsets it runs (dx, dW, db vs an fp64 reduction); with dx_add it
+    refuses (X2G_EUNSUPPORTED) instead of reading wrapped offsets."""
+    from x2gnn import _lib
+    from x2gnn._lib import call, ptr, stream_ptr
+
+    rows, D, R = (1 << 31) // (128 * 4) + 96, 128, 6
+    g = torch.Generator(device=cuda).manual_seed(5)
+    x = torch.randn(rows, D, device=cuda, generator=g)
+    gy = torch.randn(rows, D, device=cuda, generator=g)
+    rbf = torch.randn(rows, R, device=cuda, generator=g)
+    w = 0.3 * torch.randn(D, R, device=cuda, generator=g)
+    b = 0.1 * torch.randn(D, device=cuda, generator=g)
+    dx = torch.empty_like(x)
+    dw, db = torch.empty_like(w), torch.empty_like(b)
+    ws_bytes = int(_lib.load().x2g_rbf_gate_bwd_workspace(rows, D, R))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=cuda)
+    call("x2g_rbf_gate_bwd", ptr(gy), None, ptr(x), ptr(rbf), ptr(w), ptr(b), rows, D, R, ptr(dx), None, None,
+         ptr(dw), ptr(db), 0, ptr(ws), ws_bytes, stream_ptr())
+    tail = slice(rows - 5000, rows)
+    want = gy[tail] * torch.nn.functional.linear(rbf[tail], w, b)
+    torch.testing.assert_close(dx[tail], want, rtol=1e-5, atol=1e-5)
+    gx = (gy * x).double()
+    ref_w = gx.t() @ rbf.double()
+    ref_b = gx.sum(0)
+    del gx
+    scale = float(ref_w.abs().max())
+    assert float((dw.double() - ref_w).abs().max()) <= 1e-5 * scale + 1e-3
+    assert float((db.double() - ref_b).abs().max()) <= 1e-5 * float(ref_b.abs().max()) + 1e-3
+    add = torch.zeros(8, device=cuda)  # present (its size is not what is checked)
+    with pytest.raises(RuntimeError):
+        call("x2g_rbf_gate_bwd", ptr(gy), None, ptr(x), ptr(rbf), ptr(w), ptr(b), rows, D, R, ptr(dx), ptr(add),
+             None, ptr(dw), ptr(db), 0, ptr(ws), ws_bytes, stream_ptr())
 
 
 def test_rbf_pool_vs_torch(cuda):
@@ -1776,3 +1846,218 @@ def test_smooth_l1_unit_seed_gradient_equals_backward_kernel(cuda, n):
     l3 = ops.smooth_l1_loss(p3, target, unit_seed=seed)
     torch.autograd.backward(l3, torch.full((), 0.5, device=cuda))  # not the seed object: the kernel
     torch.testing.assert_close(p3.grad, 0.5 * p2.grad, rtol=0, atol=0)
+
+
+# ------------------------------------------------------------------------------ center-atom attention
+def _sym_lg(ei, n, cuda, with_transpose=False):
+    """Symmetric line graph with the center-atom outputs (edge_rev, rev_trip), its src_type / dst_type
+    element rows from random atom elements, and its max degree."""
+    from x2gnn import ops
+
+    e = torch.from_numpy(ei.astype(np.int64)).to(cuda)
+    T = int(triplets.vertex_to_edge(ei, n)[0].shape[1])
+    ei32 = ops._i32(e)
+    lg = ops.LineGraph(ei32[0].contiguous(), ei32[1].contiguous(), n, T, symmetric=True,
+                       with_transpose=with_transpose)
+    z = torch.randint(0, 10, (n,), generator=torch.Generator().manual_seed(n)).to(cuda)
+    lg.dst_type = ops._i32(z[e[1]])
+    lg.src_type = ops._i32(z[e[0]])
+    lg.max_degree = int(np.bincount(ei[0], minlength=n).max()) if ei.shape[1] else 0
+    return lg
+
+
+def _attn_inputs(lg, cuda, seed, rows=10):
+    g = torch.Generator(device=cuda).manual_seed(seed)
+    E, T = lg.E, lg.T
+    q, k, v, skip = (torch.randn(E, 128, device=cuda, generator=g) for _ in range(4))
+    S = torch.randn(T, 128, device=cuda, generator=g)
+    table = torch.randn(rows, 128, device=cuda, generator=g)
+    return q, k, v, skip, S, table
+
+
+def _fwd_both(lg, q, k, v, skip, S, table, mode, heads, channels, stats=True):
+    """(center outputs, destination-major outputs): out, alpha, smax, sden, row_stats."""
+    from x2gnn import ops
+    from x2gnn._lib import call, ptr, stream_ptr
+
+    E, T, H, D = lg.E, lg.T, heads, heads * channels
+    res = []
+    for center in (True, False):
+        out = torch.full((E, D), float("nan"), device=q.device)
+        alpha = torch.full((T, H), float("nan"), device=q.device)
+        smax, sden = torch.empty(E, H, device=q.device), torch.empty(E, H, device=q.device)
+        rs = torch.empty(E, 2, device=q.device) if stats else None
+        edge = table if mode == ops.EDGE_PER_DST else None
+        if center:
+            call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge),
+                 ptr(lg.src_type) if edge is not None else None, mode, ptr(S), 0, ptr(lg.atom_rowptr),
+                 ptr(lg.edge_rev), ptr(lg.rev_trip), 0, lg.N, lg.max_degree, E, T, heads, channels, ptr(out),
+                 ptr(alpha), ptr(smax), ptr(sden), ptr(rs), stream_ptr())
+        else:
+            call("x2g_sbf_attention_fwd_stats" if stats else "x2g_sbf_attention_fwd", ptr(q), ptr(k), ptr(v),
+                 ptr(skip), ptr(edge), ptr(lg.dst_type) if edge is not None else None, mode, ptr(S), None, None,
+                 ptr(lg.trip_rowptr), ptr(lg.trip_src), E, T, heads, channels, D, ptr(out), ptr(alpha), ptr(smax),
+                 ptr(sden), *((ptr(rs),) if stats else ()), stream_ptr())
+        res.append((out, alpha, smax, sden, rs))
+    return res
+
+
+def _close_fwd(a, b, tol=2e-6):
+    out, alpha, smax, sden, rs = a
+    out2, alpha2, smax2, sden2, rs2 = b
+    assert not torch.isnan(out).any() and not torch.isnan(alpha).any()
+    for x, y in ((out, out2), (alpha, alpha2), (smax, smax2)):
+        torch.testing.assert_close(x, y, rtol=tol, atol=tol)
+    torch.testing.assert_close(sden, sden2, rtol=1e-5, atol=1e-6)
+    if rs is not None:
+        torch.testing.assert_close(rs, rs2, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("heads,channels", [(16, 8), (8, 16), (32, 4)])
+def test_center_forward_equals_destination_major(cuda, heads, channels):
+    """x2g_sbf_attention_fwd_center (one workgroup per center atom, k / v staged in LDS) == the
+    destination-major forward on a config-2 batch (128 S160 molecules), with the element-table edge term
+    and without, with and without the LayerNorm row statistics; fp32 rounding apart (per-batch softmax
+    rescale, 4-channel partial head sums)."""
+    from x2gnn import ops
+    from x2gnn.data import collate
+    from x2gnn.synth import synthetic_molecules
+
+    b = collate(synthetic_molecules(128, "S160", seed=11))
+    lg = _sym_lg(b.edge_index.numpy(), b.num_nodes, cuda)
+    assert lg.max_degree >= 9
+    q, k, v, skip, S, table = _attn_inputs(lg, cuda, 3)
+    for mode in (ops.EDGE_PER_DST, ops.EDGE_NONE):
+        for stats in (True, False):
+            a, r = _fwd_both(lg, q, k, v, skip, S, table, mode, heads, channels, stats)
+            _close_fwd(a, r)
+
+
+def test_center_forward_edge_cases(cuda):
+    """Degree-1 atoms (destinations without triplets: out = skip, max -inf, denominator 0), isolated atoms
+    (no edges), a hub of degree 64 (the LDS bound), and the atom / triplet offsets the tiled inference path
+    hands over (two molecule ranges == the whole)."""
+    from x2gnn import ops
+    from x2gnn._lib import call, ptr, stream_ptr
+
+    # a path a-b-c (degrees 1, 2, 1), an isolated atom, a star of degree 64, a triangle
+    pairs = [(0, 1), (1, 2)] + [(4, 5 + i) for i in range(64)] + [(69, 70), (70, 71), (69, 71)]
+    ed = sorted({(a, b) for a, b in pairs} | {(b, a) for a, b in pairs})
+    ei = np.array(ed, dtype=np.int64).T
+    n = 72
+    lg = _sym_lg(ei, n, cuda)
+    assert lg.max_degree == 64
+    q, k, v, skip, S, table = _attn_inputs(lg, cuda, 4)
+    a, r = _fwd_both(lg, q, k, v, skip, S, table, ops.EDGE_PER_DST, 16, 8)
+    _close_fwd(a, r)
+    d_leaf = int(np.nonzero((ei[0] == 0) & (ei[1] == 1))[0][0])  # (0 -> 1): center 1 has degree 2
+    assert a[2][d_leaf].isfinite().all()
+    d_hub_in = int(np.nonzero((ei[0] == 1) & (ei[1] == 0))[0][0])  # (1 -> 0): center 0 has degree 1
+    torch.testing.assert_close(a[0][d_hub_in], skip[d_hub_in])
+    assert bool((a[2][d_hub_in] == -float("inf")).all()) and float(a[3][d_hub_in].abs().max()) == 0.0
+    # two atom ranges with S handed over from each range's first triplet (the tiled path)
+    split = 4  # atoms 0..3 | 4..71: the ranges' triplets are disjoint and contiguous
+    t_split = int(lg.trip_rowptr[int(lg.atom_rowptr[split])])
+    out = torch.empty_like(q)
+    alpha = torch.empty(lg.T, 16, device=cuda)
+    smax, sden, rs = torch.empty(lg.E, 16, device=cuda), torch.empty(lg.E, 16, device=cuda), torch.empty(lg.E, 2, device=cuda)
+    for a0, a1, t0, t1 in ((0, split, 0, t_split), (split, n, t_split, lg.T)):
+        Sc = S[t0:t1].clone()
+        call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
+             ops.EDGE_PER_DST, ptr(Sc), t0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), a0, a1 - a0,
+             lg.max_degree, lg.E, lg.T, 16, 8, ptr(out), ptr(alpha), ptr(smax), ptr(sden), ptr(rs), stream_ptr())
+    for x, y in zip((out, alpha, smax, sden, rs), a):
+        assert torch.equal(x, y)
+
+
+def _bwd_both(lg, q, k, v, S, table, mode, heads, channels, seed):
+    """(center, destination-major fold) backward outputs on the same forward state: dq, dk, dv, G and the
+    element-table gradient of the edge term (keyed sums in fp64)."""
+    from x2gnn import _lib, ops
+    from x2gnn._lib import call, ptr, stream_ptr
+
+    E, T, H, D = lg.E, lg.T, heads, heads * channels
+    skip = torch.zeros_like(q)
+    (out, alpha, smax, sden, _), _ = _fwd_both(lg, q, k, v, skip, S, table, mode, heads, channels, stats=False)
+    g = torch.Generator(device=q.device).manual_seed(seed)
+    dout = torch.randn(E, D, device=q.device, generator=g)
+    y = torch.randn(T, 8, device=q.device, generator=g)
+    y[:, 7] = 1.0
+    edge = table if mode == ops.EDGE_PER_DST else None
+    rows = table.shape[0]
+    f = dict(device=q.device, dtype=torch.float32)
+    # center
+    dq, dk, dv, G = (torch.full((E, D), float("nan"), **f) for _ in range(3)) + (torch.full((E, 8, D), float("nan"), **f),)
+    de_atom = torch.full((lg.N, D), float("nan"), **f) if edge is not None else None
+    assert int(_lib.load().x2g_sbf_attention_bwd_center_lds(lg.max_degree, heads)) <= 160 * 1024
+    call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(lg.src_type) if edge is not None else None,
+         mode, ptr(S), ptr(y), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(alpha), ptr(smax), ptr(sden),
+         ptr(dout), lg.N, lg.max_degree, E, T, heads, channels, ptr(dq), ptr(dk), ptr(dv), ptr(G), ptr(de_atom),
+         stream_ptr())
+    c = [dq, dk, dv, G]
+    if edge is not None:
+        c.append(torch.zeros(rows, D, dtype=torch.float64, device=q.device).index_add_(0, lg.atom_type.long(), de_atom.double()))
+    # destination-major fold passes
+    dq2, dk2, dv2, G2 = (torch.empty(E, D, **f) for _ in range(3)) + (torch.empty(E, 8, D, **f),)
+    prob, rho = torch.empty(T, H, **f), torch.empty(E, H, **f)
+    de = torch.empty(E, D, **f) if edge is not None else None
+    call("x2g_sbf_attention_bwd_dst_g", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(lg.dst_type) if edge is not None else None,
+         mode, ptr(S), ptr(lg.trip_rowptr), ptr(lg.trip_src), ptr(alpha), ptr(smax), ptr(sden), ptr(dout), E, T, heads,
+         channels, ptr(dq2), ptr(de), None, ptr(prob), ptr(rho), stream_ptr())
+    src_rowptr, src_perm = lg.src_csr()
+    call("x2g_sbf_attention_bwd_src_fold", ptr(q), ptr(v), ptr(edge), ptr(lg.dst_type) if edge is not None else None,
+         ptr(lg.src_type) if edge is not None else None, rows if edge is not None else 0, mode, ptr(S), ptr(y),
+         ptr(src_rowptr), ptr(src_perm), ptr(lg.src_dst), ptr(lg.trip_dst), ptr(prob), None, ptr(rho), ptr(dout), E, T,
+         heads, channels, ptr(dk2), ptr(dv2), ptr(G2), stream_ptr())
+    r = [dq2, dk2, dv2, G2]
+    if edge is not None:
+        r.append(torch.zeros(rows, D, dtype=torch.float64, device=q.device).index_add_(0, lg.dst_type.long(), de.double()))
+    return c, r
+
+
+def _close_bwd(c, r):
+    for name, x, y in zip(("dq", "dk", "dv", "G", "d_edge"), c, r):
+        assert not torch.isnan(x).any(), name
+        scale = float(y.abs().max())
+        err = float((x.double() - y.double()).abs().max())
+        assert err <= 2e-5 * scale + 1e-6, (name, err, scale)
+
+
+@pytest.mark.parametrize("heads,channels", [(16, 8), (8, 16), (32, 4)])
+def test_center_backward_equals_fold_passes(cuda, heads, channels):
+    """x2g_sbf_attention_bwd_center (both backward passes in one launch per center atom) == the
+    destination-major x2g_sbf_attention_bwd_dst_g + source-major x2g_sbf_attention_bwd_src_fold on a
+    config-2 batch: dq, dk, dv, the folded lin_sbf gradient G, and the element-table gradient (per-atom
+    rows keyed by element == per-destination rows keyed by destination element), with and without the
+    edge term; within 2e-5 of each output's max (fp32 reassociation)."""
+    from x2gnn import ops
+    from x2gnn.data import collate
+    from x2gnn.synth import synthetic_molecules
+
+    b = collate(synthetic_molecules(128, "S160", seed=12))
+    lg = _sym_lg(b.edge_index.numpy(), b.num_nodes, cuda, with_transpose=True)
+    lg.atom_type = ops._i32(torch.randint(0, 10, (b.num_nodes,), generator=torch.Generator().manual_seed(b.num_nodes)).to(cuda))
+    lg.src_type = ops._i32(lg.atom_type[lg.edge_src.long()])
+    lg.dst_type = ops._i32(lg.atom_type[lg.edge_dst.long()])
+    q, k, v, _, S, table = _attn_inputs(lg, cuda, 5)
+    for mode in (ops.EDGE_PER_DST, ops.EDGE_NONE):
+        c, r = _bwd_both(lg, q, k, v, S, table, mode, heads, channels, 6)
+        _close_bwd(c, r)
+
+
+def test_center_backward_edge_cases(cuda):
+    """Degree-1 and isolated atoms (zero rows), a hub of degree 40 (LDS tables of 40 x 40 x heads), a
+    triangle; vs the fold passes."""
+    from x2gnn import ops
+
+    pairs = [(0, 1), (1, 2)] + [(4, 5 + i) for i in range(40)] + [(45, 46), (46, 47), (45, 47)]
+    ed = sorted({(a, b) for a, b in pairs} | {(b, a) for a, b in pairs})
+    ei = np.array(ed, dtype=np.int64).T
+    n = 48
+    lg = _sym_lg(ei, n, cuda, with_transpose=True)
+    z = torch.randint(0, 10, (n,), generator=torch.Generator().manual_seed(1)).to(cuda)
+    lg.atom_type = ops._i32(z)
+    lg.src_type, lg.dst_type = ops._i32(z[lg.edge_src.long()]), ops._i32(z[lg.edge_dst.long()])
+    q, k, v, _, S, table = _attn_inputs(lg, cuda, 7)
+    c, r = _bwd_both(lg, q, k, v, S, table, ops.EDGE_PER_DST, 16, 8, 8)
+    _close_bwd(c, r)

@@ -157,6 +157,37 @@ def test_trunk_drop_in_api_vs_fast_path(cuda):
     assert rel_err(slow.cpu().numpy(), fast.cpu().numpy()) < 1e-5
 
 
+@pytest.mark.parametrize("which", ["batch", "atom_batch", "edge_index_0", "triplets"])
+def test_trunk_drop_in_unsorted_index_raises(cuda, which):
+    """The drop-in SBFTransformer.forward assumes sorted indices (as the reference's own batches are);
+    an eager call on a shuffled one raises instead of returning wrong sums."""
+    from x2gnn.data import Data
+
+    z = golden("model_small.npz")
+    m = product_model(z, cuda)
+    b = batch_from_fixture(z).to(cuda)
+    with torch.no_grad():
+        line, plan = m.line_graph_data(b)
+        lg = plan.lg
+        per_trip = line.edge_attr.index_select(0, b.x.index_select(0, lg.atom_j.long()))
+        batch_line = torch.repeat_interleave(torch.arange(b.num_graphs, device=cuda), b.edge_num)
+        trip = lg.triplet_index()
+        ei0, ab = b.edge_index[0], b.batch
+        flip = lambda t: t.flip(0)  # noqa: E731
+        if which == "batch":
+            batch_line = flip(batch_line)
+        elif which == "atom_batch":
+            ab = flip(ab)
+        elif which == "edge_index_0":
+            ei0 = flip(ei0)
+        else:
+            trip = trip.flip(1)
+        d = Data(x=line.x, edge_index=trip, edge_attr=per_trip, batch=batch_line, edge_sbf=line.edge_sbf,
+                 node_rbf=line.node_rbf)
+        with pytest.raises(ValueError, match="not sorted"):
+            m.fin_model(d, edge_index_0=ei0, atom_batch=ab)
+
+
 def _grads_vs_oracle(m, orc, rtol=2e-3):
     """Every parameter gradient of the product model against the oracle's: max |diff| within
     ``rtol`` of the reference gradient's own max (+ 1e-6 of the largest gradient of the model, for

@@ -1,0 +1,493 @@
+// Center-atom SBF-transformer attention (symmetric line graphs: every molecular batch).
+//
+// Reference: SBFTransformerConv.forward / message (sbftransformer_conv.py:93-162) over the triplets
+// vertex_to_edge_2 emits (edge_graph.py:12-30).  A triplet (s -> d) joins destination d = (a -> b) and
+// source s = (b -> k), k != a: every triplet has a middle ("center") atom b, and the triplets through b
+// are the complete bipartite block {(b -> k_j) -> (k_i -> b) : i != j} over b's n = deg(b) neighbours.
+// Grouped by center atom instead of by destination, a workgroup owns one atom b and all of its n (n - 1)
+// triplets:
+//   * the n source rows of k and v are b's out-edges, CONTIGUOUS line nodes atom_rowptr[b] .. +n: loaded
+//     once, coalesced, into LDS (k + e and v + e: X2-GNN's edge term is the element-table row of the
+//     center atom, xgnn.py:57-58, uniform over the block), instead of being gathered from L2 once per
+//     triplet (8 times each at config 2) by one-destination-per-wave kernels;
+//   * destination i = rev(b -> k_i) owns the contiguous triplet rows rev_trip[b -> k_i] + 0 .. n - 2
+//     (vertex_to_edge_2's order: sources ascending, the reverse edge skipped), read as one S stream.
+// A destination is owned by a HALF wave (32 lanes x 4 channels = D = 128, LPH lanes per head), so a
+// 16-byte load moves two destinations' rows per instruction and the per-head softmax arithmetic runs on
+// 2 lanes per head instead of 4.  Both halves walk j = 0 .. n-1 in lockstep (each masks its own j == i),
+// so their LDS row reads are the same address (broadcast).  Online softmax per batch of B triplets (one
+// running-max rescale per batch); fixed order (j ascending), no atomics.
+//
+// Needs x2g_vertex_to_edge_sym's / x2g_line_graph_sym_build's edge_rev and rev_trip.
+#include <math.h>
+
+#include <type_traits>
+
+#include "common.hpp"
+
+namespace x2g {
+namespace {
+
+constexpr int kCD = 128;  // D compiled (H * C)
+constexpr float kCEps = 1e-16f;
+typedef float cf4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ cf4 ld4(const float* p) { return *reinterpret_cast<const cf4*>(p); }
+__device__ __forceinline__ void st4(float* p, cf4 v) { *reinterpret_cast<cf4*>(p) = v; }
+
+// sum over the LPH lanes of a head (aligned groups inside a half wave)
+template <int LPH>
+__device__ __forceinline__ float head_sum(float v) {
+  return group_sum<LPH>(v);
+}
+
+// sum over each aligned 32-lane half, in every lane of that half
+__device__ __forceinline__ float half_sum(float v, int half) {
+  v = half32_sum_hi(v);
+  const float lo = lane_bcast(v, 31), hi = lane_bcast(v, 63);
+  return half ? hi : lo;
+}
+
+struct FwdCenterArgs {
+  const float *q, *k, *v, *skip, *edge;
+  const int32_t* src_row;  // per source line node: its edge-table row (the center atom's element)
+  const float* sp;         // S rows, row t - t_base
+  int64_t t_base;
+  const int32_t *atom_rowptr, *edge_rev, *rev_trip;
+  int64_t atom0, n_atoms;
+  int H;
+  float sqrt_c;
+  float *out, *alpha, *smax, *sden;
+  float2* row_stats;
+};
+
+template <int LPH, int WAVES, int B, bool EDGE>
+__global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_kernel(const FwdCenterArgs a) {
+  extern __shared__ cf4 lds[];  // [n][32] (k + e), then [n][32] (v + e)
+  const int64_t b = a.atom0 + blockIdx.x;
+  const int r0 = uniform(a.atom_rowptr[b]);
+  const int n = uniform(a.atom_rowptr[b + 1]) - r0;
+  if (n <= 0) return;  // (workgroup-uniform: no barrier is skipped by a part of it)
+  cf4* ke = lds;
+  cf4* ve = lds + n * 32;
+  const int tid = threadIdx.x;
+  const int l32 = tid & 31, half = (tid >> 5) & 1, wave = tid >> 6;
+  const int owner = 2 * wave + half;
+  const int head = l32 / LPH;
+  const bool leader = (l32 % LPH) == 0;
+  const int c0 = 4 * l32;
+  // this owner's first destination: its id and triplet block (in flight under the staging)
+  int i = owner;
+  int d = 0, tb = 0;
+  if (i < n) {
+    d = a.edge_rev[r0 + i];
+    tb = a.rev_trip[r0 + i];
+  }
+  // stage k + e, v + e of the n source rows (contiguous line nodes r0 .. r0 + n - 1)
+  cf4 e4 = {0.f, 0.f, 0.f, 0.f};
+  for (int idx = tid; idx < n * 32; idx += 64 * WAVES) {
+    const int j = idx >> 5, c = idx & 31;
+    if (EDGE) e4 = ld4(a.edge + static_cast<int64_t>(uniform(a.src_row[r0])) * kCD + 4 * c);
+    const int64_t row = static_cast<int64_t>(r0 + j) * kCD + 4 * c;
+    ke[idx] = ld4(a.k + row) + e4;
+    ve[idx] = ld4(a.v + row) + e4;
+  }
+  __syncthreads();
+  const int nt = n - 1;  // triplets per destination
+  for (; i < n; i += 2 * WAVES) {
+    if (i != owner) {
+      d = a.edge_rev[r0 + i];
+      tb = a.rev_trip[r0 + i];
+    }
+    const int64_t drow = static_cast<int64_t>(d) * kCD + c0;
+    const cf4 qv = ld4(a.q + drow);
+    const cf4 sk = ld4(a.skip + drow);
+    cf4 acc = {0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, den = 0.f;
+    const float* sbase = a.sp + (static_cast<int64_t>(tb) - a.t_base) * kCD + c0;
+    // one batch of BB consecutive sources j0 .. j0 + BB - 1 (those >= n or == i masked): every S row
+    // of the batch in flight together, then the logits, one rescale, the weighted values
+    auto batch = [&](int j0, auto bb) {
+      constexpr int BB = decltype(bb)::value;
+      cf4 sv[BB];
+#pragma unroll
+      for (int u = 0; u < BB; ++u) {
+        const int j = j0 + u;
+        int jj = j - (j > i ? 1 : 0);
+        jj = jj < nt ? jj : nt - 1;  // clamped (nt >= 1 here): every load unconditional
+        sv[u] = ld4(sbase + static_cast<int64_t>(jj) * kCD);
+      }
+      float lg[BB];
+      float mb = -INFINITY;
+#pragma unroll
+      for (int u = 0; u < BB; ++u) {
+        const int j = j0 + u;
+        const bool ok = j < n && j != i;
+        const cf4 kr = ke[(j < n ? j : n - 1) * 32 + l32];
+        float dot = qv[0] * kr[0];
+        dot = fmaf(qv[1], kr[1], dot);
+        dot = fmaf(qv[2], kr[2], dot);
+        dot = fmaf(qv[3], kr[3], dot);
+        const float logit = head_sum<LPH>(dot) / a.sqrt_c;
+        lg[u] = ok ? logit : -INFINITY;
+        mb = fmaxf(mb, lg[u]);
+        if (ok && leader) a.alpha[(static_cast<int64_t>(tb) + (j - (j > i ? 1 : 0))) * a.H + head] = logit;
+      }
+      const float m_new = fmaxf(m, mb);
+      const float corr = m_new == -INFINITY ? 1.f : expf(m - m_new);
+      den *= corr;
+      acc *= corr;
+#pragma unroll
+      for (int u = 0; u < BB; ++u) {
+        const int j = j0 + u;
+        const float p = lg[u] == -INFINITY ? 0.f : expf(lg[u] - m_new);
+        const cf4 vr = ve[(j < n ? j : n - 1) * 32 + l32];
+        den += p;
+        acc += p * (vr * sv[u]);
+      }
+      m = m_new;
+    };
+    if (nt > 0) {  // (workgroup-uniform)
+      int j0 = 0;
+      for (; n - j0 > B / 2; j0 += B) batch(j0, std::integral_constant<int, B>{});
+      if (j0 < n) batch(j0, std::integral_constant<int, B / 2>{});
+    }
+    const float inv = 1.0f / (den + kCEps);
+    const cf4 o = acc * inv + sk;
+    st4(a.out + drow, o);
+    if (a.row_stats) {
+      const float mu = half_sum(o[0] + o[1] + o[2] + o[3], half) / static_cast<float>(kCD);
+      const cf4 dv = o - mu;
+      const float q2 = half_sum(dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2] + dv[3] * dv[3], half);
+      if (l32 == 0) a.row_stats[d] = make_float2(mu, q2);
+    }
+    if (leader) {
+      a.smax[static_cast<int64_t>(d) * a.H + head] = m;
+      a.sden[static_cast<int64_t>(d) * a.H + head] = den;
+    }
+  }
+}
+
+template <int LPH>
+int fwd_center_launch(const FwdCenterArgs& a, bool edge, int max_degree, hipStream_t st) {
+  constexpr int W = 4, B = 8;
+  const size_t lds = static_cast<size_t>(2) * max_degree * kCD * sizeof(float);
+  const unsigned grid = static_cast<unsigned>(a.n_atoms);
+  if (edge)
+    attn_fwd_center_kernel<LPH, W, B, true><<<grid, 64 * W, lds, st>>>(a);
+  else
+    attn_fwd_center_kernel<LPH, W, B, false><<<grid, 64 * W, lds, st>>>(a);
+  return last_launch_status();
+}
+
+// ------------------------------------------------------------------------------ fused backward
+// One workgroup per center atom b does BOTH backward passes of the destination-major kernels
+// (attention_fold.inc) over b's triplet block, from LDS images of the block's rows:
+//   KE[j] = k_j + e, GO[i] = dout[d_i], QI[i] = q[d_i], per-destination max / 1 / (den + eps);
+// pass 1, one owner per SOURCE j (its S rows t(i, j) = TB[i] + j - [j > i], one 512-byte row each):
+//   at = exp(alpha_t - max_i) / (den_i + eps),  g = sum over the head of go_i (v_j + e) S_t,
+//   dv_j += at go_i S_t,  G_j[l] += at go_i (v_j + e) Y_l(t)  (the folded lin_sbf gradient),
+//   and (at, g) into the block's [i][j][head] tables;
+// then rho_i = sum_j at g (j ascending: the destination pass's order), and pass 2 from LDS alone:
+//   w = at (g - rho_i) / sqrt(C),  dk_j = sum_i w q_i (owner j),  dq_i = sum_j w (k_j + e) (owner i),
+// and, for the element-table gradient, d_edge[b] = sum_j (dk_j + dv_j) (X2-GNN's edge term enters as
+// k_j + e and v_j + e with e the center atom's row: its gradient is the block's sum).  S, alpha and Y
+// are read once per backward (the two destination-major passes read S twice and gather k / v / q /
+// dout rows per triplet from L2); no g, prob or rho tensors leave the kernel.
+struct BwdCenterArgs {
+  const float *q, *k, *v, *edge;
+  const int32_t* src_row;
+  const float *sp, *alpha, *smax, *sden, *dout, *y;
+  const int32_t *atom_rowptr, *edge_rev, *rev_trip;
+  int64_t n_atoms, T;
+  int H;
+  float inv_sqrt_c;
+  float *dq, *dk, *dv, *gfold, *d_edge;
+};
+
+template <int H>
+__host__ __device__ constexpr size_t bwd_center_lds(int n) {
+  return static_cast<size_t>(n) * 3 * kCD * 4           // KE, GO, QI
+         + static_cast<size_t>(n) * n * H * 4 * 2        // AT, GT
+         + static_cast<size_t>(n) * H * 4 * 3            // MX, IV, RHO
+         + static_cast<size_t>(n) * 4 * 2;               // TB, DI
+}
+
+template <int LPH, int WAVES, int B, bool EDGE>
+__global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCenterArgs a) {
+  constexpr int H = 32 / LPH;
+  extern __shared__ cf4 lds[];
+  const int64_t b = blockIdx.x;
+  const int r0 = uniform(a.atom_rowptr[b]);
+  const int n = uniform(a.atom_rowptr[b + 1]) - r0;
+  const int tid = threadIdx.x;
+  const int l32 = tid & 31, half = (tid >> 5) & 1, wave = tid >> 6;
+  const int owner = 2 * wave + half;
+  constexpr int NO = 2 * WAVES;  // owners
+  const int head = l32 / LPH;
+  const bool leader = (l32 % LPH) == 0;
+  const int c0 = 4 * l32;
+  if (n <= 0) {  // an atom without edges: its element-table gradient row is zero
+    if (a.d_edge && tid < 32) st4(a.d_edge + b * kCD + c0, cf4{0.f, 0.f, 0.f, 0.f});
+    return;
+  }
+  cf4* KE = lds;
+  cf4* GO = KE + n * 32;
+  cf4* QI = GO + n * 32;
+  float* AT = reinterpret_cast<float*>(QI + n * 32);
+  float* GT = AT + n * n * H;
+  float* MX = GT + n * n * H;
+  float* IV = MX + n * H;
+  float* RHO = IV + n * H;
+  int* TB = reinterpret_cast<int*>(RHO + n * H);
+  int* DI = TB + n;
+  const int64_t e_row = EDGE ? static_cast<int64_t>(uniform(a.src_row[r0])) * kCD : 0;
+  // ---- staging
+  for (int idx = tid; idx < n * 32; idx += 64 * WAVES) {
+    const int j = idx >> 5, c = idx & 31;
+    const int64_t d = a.edge_rev[r0 + j];
+    const cf4 e4 = EDGE ? ld4(a.edge + e_row + 4 * c) : cf4{0.f, 0.f, 0.f, 0.f};
+    KE[idx] = ld4(a.k + static_cast<int64_t>(r0 + j) * kCD + 4 * c) + e4;
+    GO[idx] = ld4(a.dout + d * kCD + 4 * c);
+    QI[idx] = ld4(a.q + d * kCD + 4 * c);
+  }
+  for (int idx = tid; idx < n * H; idx += 64 * WAVES) {
+    const int i = idx / H, h = idx - i * H;
+    const int64_t d = a.edge_rev[r0 + i];
+    MX[idx] = a.smax[d * H + h];
+    IV[idx] = 1.0f / (a.sden[d * H + h] + kCEps);
+  }
+  for (int idx = tid; idx < n; idx += 64 * WAVES) {
+    TB[idx] = a.rev_trip[r0 + idx];
+    DI[idx] = a.edge_rev[r0 + idx];
+  }
+  __syncthreads();
+  // ---- pass 1: one owner per source j
+  const int nt = n - 1;  // triplets per destination (and per source)
+  auto rsrc = [](const void* p, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), static_cast<short>(0),
+                                             static_cast<int>(bytes < 0x7fffffff ? bytes : 0x7fffffff), 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t sp_r = rsrc(a.sp, a.T * kCD * 4);
+  const __amdgpu_buffer_rsrc_t al_r = rsrc(a.alpha, a.T * H * 4);
+  const __amdgpu_buffer_rsrc_t y_r = rsrc(a.y, a.T * 8 * 4);
+  for (int j = owner; j < n; j += NO) {
+    const int64_t srow = static_cast<int64_t>(r0 + j) * kCD + c0;
+    cf4 ue = ld4(a.v + srow);
+    if (EDGE) ue += ld4(a.edge + e_row + c0);
+    cf4 dv = {0.f, 0.f, 0.f, 0.f};
+    cf4 G[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) G[l] = cf4{0.f, 0.f, 0.f, 0.f};
+    auto batch = [&](int i0, auto bb) {
+      constexpr int BB = decltype(bb)::value;
+      cf4 sv[BB];
+      float al[BB], yv[BB];
+#pragma unroll
+      for (int u = 0; u < BB; ++u) {
+        const int i = i0 + u < n ? i0 + u : n - 1;  // clamped: loads unconditional, masked below
+        int pos = j - (j > i ? 1 : 0);               // (i == j: some row of i's block, unused)
+        pos = pos < nt ? pos : nt - 1;
+        const int t = TB[i] + pos;                   // (32-bit buffer offsets: T * 512 < 2^31, checked)
+        sv[u] = __builtin_bit_cast(cf4, __builtin_amdgcn_raw_buffer_load_b128(sp_r, t * (kCD * 4) + c0 * 4, 0, 0));
+        al[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(al_r, (t * H + head) * 4, 0, 0));
+        yv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(y_r, (t * 8 + (l32 & 7)) * 4, 0, 0));
+      }
+      // per triplet: at, g, the tables, dv; sv[u] becomes dS / S-free: go (v + e) at
+#pragma unroll
+      for (int u = 0; u < BB; ++u) {
+        const int i = i0 + u < n ? i0 + u : n - 1;
+        const bool ok = i0 + u < n && i != j;
+        const float at = ok ? expf(al[u] - MX[i * H + head]) * IV[i * H + head] : 0.f;
+        const cf4 go = GO[i * 32 + l32];
+        const cf4 gu = go * ue;
+        float gp = gu[0] * sv[u][0];
+        gp = fmaf(gu[1], sv[u][1], gp);
+        gp = fmaf(gu[2], sv[u][2], gp);
+        gp = fmaf(gu[3], sv[u][3], gp);
+        const float g = head_sum<LPH>(gp);
+        if (ok && leader) {
+          AT[(i * n + j) * H + head] = at;
+          GT[(i * n + j) * H + head] = g;
+        }
+        dv += at * (go * sv[u]);
+        sv[u] = gu * at;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // G[l] += dS Y_l(t): Y_l handed to the half's lanes by row_newbcast (both 16-lane rows of a half
+      // loaded the same triplet's Y row, one value per lane)
+#pragma unroll
+      for (int u = 0; u < BB; ++u) {
+        float yl[8];
+        yl[0] = dpp_mov<0x150>(yv[u]);
+        yl[1] = dpp_mov<0x151>(yv[u]);
+        yl[2] = dpp_mov<0x152>(yv[u]);
+        yl[3] = dpp_mov<0x153>(yv[u]);
+        yl[4] = dpp_mov<0x154>(yv[u]);
+        yl[5] = dpp_mov<0x155>(yv[u]);
+        yl[6] = dpp_mov<0x156>(yv[u]);
+        yl[7] = dpp_mov<0x157>(yv[u]);
+#pragma unroll
+        for (int l = 0; l < 8; ++l) G[l] += sv[u] * yl[l];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    if (nt > 0) {  // (workgroup-uniform)
+      int i0 = 0;
+      for (; n - i0 > B / 2; i0 += B) batch(i0, std::integral_constant<int, B>{});
+      if (i0 < n) batch(i0, std::integral_constant<int, B / 2>{});
+    }
+    st4(a.dv + srow, dv);
+    float* gf = a.gfold + static_cast<int64_t>(r0 + j) * 8 * kCD + c0;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) st4(gf + l * kCD, G[l]);
+    if (a.d_edge) GO[j * 32 + l32] = dv;  // (GO is read by pass 1 only: after the barrier, dv + dk rows)
+  }
+  __syncthreads();
+  // ---- rho_i = sum_{j != i} at g, j ascending (one owner per destination)
+  for (int i = owner; i < n; i += NO) {
+    float rho = 0.f;
+    for (int j = 0; j < n; ++j)
+      if (j != i) rho = fmaf(AT[(i * n + j) * H + head], GT[(i * n + j) * H + head], rho);
+    if (leader) RHO[i * H + head] = rho;
+  }
+  __syncthreads();
+  // ---- pass 2: dk_j (owner of source j), dq_i (owner of destination i), from LDS
+  for (int o = owner; o < n; o += NO) {
+    cf4 dk = {0.f, 0.f, 0.f, 0.f}, dq = {0.f, 0.f, 0.f, 0.f};
+    for (int x = 0; x < n; ++x) {
+      if (x == o) continue;
+      // source role j = o over destinations i = x
+      const float ws = AT[(x * n + o) * H + head] * (GT[(x * n + o) * H + head] - RHO[x * H + head]) * a.inv_sqrt_c;
+      dk += ws * QI[x * 32 + l32];
+      // destination role i = o over sources j = x
+      const float wd = AT[(o * n + x) * H + head] * (GT[(o * n + x) * H + head] - RHO[o * H + head]) * a.inv_sqrt_c;
+      dq += wd * KE[x * 32 + l32];
+    }
+    st4(a.dk + static_cast<int64_t>(r0 + o) * kCD + c0, dk);
+    st4(a.dq + static_cast<int64_t>(DI[o]) * kCD + c0, dq);
+    if (a.d_edge) GO[o * 32 + l32] += dk;
+  }
+  if (a.d_edge) {  // d_edge[b] = sum_j (dv_j + dk_j), j ascending
+    __syncthreads();
+    if (tid < 32) {
+      cf4 s = GO[l32];
+      for (int j = 1; j < n; ++j) s += GO[j * 32 + l32];
+      st4(a.d_edge + b * kCD + c0, s);
+    }
+  }
+}
+
+template <int LPH>
+int bwd_center_launch(const BwdCenterArgs& a, bool edge, int max_degree, hipStream_t st) {
+  constexpr int W = 4, B = 8;
+  constexpr int H = 32 / LPH;
+  const size_t lds = bwd_center_lds<H>(max_degree);
+  if (lds > 160 * 1024) return X2G_EUNSUPPORTED;
+  const unsigned grid = static_cast<unsigned>(a.n_atoms);
+  auto go = [&](auto kern) {
+    if (lds > 64 * 1024) hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    kern<<<grid, 64 * W, lds, st>>>(a);
+  };
+  if (edge)
+    go(attn_bwd_center_kernel<LPH, W, B, true>);
+  else
+    go(attn_bwd_center_kernel<LPH, W, B, false>);
+  return last_launch_status();
+}
+
+}  // namespace
+}  // namespace x2g
+
+using namespace x2g;
+
+X2G_API size_t x2g_sbf_attention_bwd_center_lds(int32_t max_degree, int32_t heads) {
+  if (max_degree < 0 || heads <= 0) return 0;
+  const int n = max_degree > 0 ? max_degree : 1;
+  return static_cast<size_t>(n) * 3 * kCD * 4 + static_cast<size_t>(n) * n * heads * 8 +
+         static_cast<size_t>(n) * heads * 12 + static_cast<size_t>(n) * 8;
+}
+
+X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const float* v, const float* edge,
+                                         const int32_t* src_row, int edge_mode, const float* sbfproj,
+                                         const float* sph_y, const int32_t* atom_rowptr, const int32_t* edge_rev,
+                                         const int32_t* rev_trip, const float* alpha_raw, const float* seg_max,
+                                         const float* seg_den, const float* dout, int64_t num_atoms,
+                                         int32_t max_degree, int64_t num_edges, int64_t num_triplets, int32_t heads,
+                                         int32_t channels, float* dq, float* dk, float* dv, float* radial_grad,
+                                         float* d_edge_atom, void* stream) {
+  if (num_atoms < 0 || num_edges < 0 || num_triplets < 0 || heads <= 0 || channels <= 0) return X2G_EINVAL;
+  if (edge_mode != X2G_EDGE_NONE && edge_mode != X2G_EDGE_PER_DST) return X2G_EUNSUPPORTED;
+  if (heads * channels != kCD || channels % 4 || max_degree < 0 || max_degree > X2G_CENTER_MAX_DEGREE)
+    return X2G_EUNSUPPORTED;
+  if (x2g_sbf_attention_bwd_center_lds(max_degree, heads) > 160 * 1024) return X2G_EUNSUPPORTED;
+  if (num_triplets * kCD * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;  // 32-bit S offsets
+  if (num_atoms == 0) return X2G_OK;
+  if (num_edges > 0 && (!q || !k || !v || !sbfproj || !sph_y || !atom_rowptr || !edge_rev || !rev_trip ||
+                        !alpha_raw || !seg_max || !seg_den || !dout || !dq || !dk || !dv || !radial_grad))
+    return X2G_EINVAL;
+  if (!atom_rowptr) return X2G_EINVAL;
+  if (edge_mode == X2G_EDGE_PER_DST && (!edge || !src_row)) return X2G_EINVAL;
+  const auto al = [](const void* p, int m) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % m == 0; };
+  if (!al(q, 16) || !al(k, 16) || !al(v, 16) || !al(edge, 16) || !al(sbfproj, 16) || !al(dout, 16) || !al(dq, 16) ||
+      !al(dk, 16) || !al(dv, 16) || !al(radial_grad, 16) || !al(d_edge_atom, 16))
+    return X2G_EUNSUPPORTED;
+  BwdCenterArgs a{};
+  a.q = q; a.k = k; a.v = v; a.edge = edge; a.src_row = src_row; a.sp = sbfproj; a.alpha = alpha_raw;
+  a.smax = seg_max; a.sden = seg_den; a.dout = dout; a.y = sph_y; a.atom_rowptr = atom_rowptr; a.edge_rev = edge_rev;
+  a.rev_trip = rev_trip; a.n_atoms = num_atoms; a.T = num_triplets; a.H = heads;
+  a.inv_sqrt_c = static_cast<float>(1.0 / sqrt(static_cast<double>(channels)));
+  a.dq = dq; a.dk = dk; a.dv = dv; a.gfold = radial_grad; a.d_edge = d_edge_atom;
+  const int md = max_degree > 0 ? max_degree : 1;
+  const bool edge_on = edge_mode == X2G_EDGE_PER_DST;
+  hipStream_t st = as_stream(stream);
+  switch (channels / 4) {
+    case 1: return bwd_center_launch<1>(a, edge_on, md, st);
+    case 2: return bwd_center_launch<2>(a, edge_on, md, st);
+    case 4: return bwd_center_launch<4>(a, edge_on, md, st);
+    case 8: return bwd_center_launch<8>(a, edge_on, md, st);
+    default: return X2G_EUNSUPPORTED;
+  }
+}
+
+X2G_API int x2g_sbf_attention_fwd_center(const float* q, const float* k, const float* v, const float* skip,
+                                         const float* edge, const int32_t* src_row, int edge_mode,
+                                         const float* sbfproj, int64_t t_base, const int32_t* atom_rowptr,
+                                         const int32_t* edge_rev, const int32_t* rev_trip, int64_t atom0,
+                                         int64_t n_atoms, int32_t max_degree, int64_t num_edges,
+                                         int64_t num_triplets, int32_t heads, int32_t channels, float* out,
+                                         float* alpha_raw, float* seg_max, float* seg_den, float* row_stats,
+                                         void* stream) {
+  if (n_atoms < 0 || atom0 < 0 || num_edges < 0 || num_triplets < 0 || heads <= 0 || channels <= 0)
+    return X2G_EINVAL;
+  if (edge_mode != X2G_EDGE_NONE && edge_mode != X2G_EDGE_PER_DST) return X2G_EUNSUPPORTED;
+  if (heads * channels != kCD || channels % 4 || max_degree < 0 || max_degree > X2G_CENTER_MAX_DEGREE)
+    return X2G_EUNSUPPORTED;
+  if (n_atoms == 0 || num_edges == 0) return X2G_OK;
+  if (!q || !k || !v || !skip || !sbfproj || !atom_rowptr || !edge_rev || !rev_trip || !out || !seg_max || !seg_den)
+    return X2G_EINVAL;
+  if (num_triplets > 0 && !alpha_raw) return X2G_EINVAL;
+  if (edge_mode == X2G_EDGE_PER_DST && (!edge || !src_row)) return X2G_EINVAL;
+  // 16-byte rows (float4 per lane), 8-byte row statistics
+  const auto al = [](const void* p, int m) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % m == 0; };
+  if (!al(q, 16) || !al(k, 16) || !al(v, 16) || !al(skip, 16) || !al(edge, 16) || !al(sbfproj, 16) || !al(out, 16) ||
+      !al(row_stats, 8))
+    return X2G_EUNSUPPORTED;
+  FwdCenterArgs a{};
+  a.q = q; a.k = k; a.v = v; a.skip = skip; a.edge = edge; a.src_row = src_row; a.sp = sbfproj; a.t_base = t_base;
+  a.atom_rowptr = atom_rowptr; a.edge_rev = edge_rev; a.rev_trip = rev_trip; a.atom0 = atom0; a.n_atoms = n_atoms;
+  a.H = heads; a.sqrt_c = static_cast<float>(sqrt(static_cast<double>(channels)));
+  a.out = out; a.alpha = alpha_raw; a.smax = seg_max; a.sden = seg_den;
+  a.row_stats = reinterpret_cast<float2*>(row_stats);
+  const int md = max_degree > 0 ? max_degree : 1;
+  const bool edge_on = edge_mode == X2G_EDGE_PER_DST;
+  hipStream_t st = as_stream(stream);
+  switch (channels / 4) {
+    case 1: return fwd_center_launch<1>(a, edge_on, md, st);
+    case 2: return fwd_center_launch<2>(a, edge_on, md, st);
+    case 4: return fwd_center_launch<4>(a, edge_on, md, st);
+    case 8: return fwd_center_launch<8>(a, edge_on, md, st);
+    default: return X2G_EUNSUPPORTED;
+  }
+}

@@ -166,7 +166,8 @@ __device__ __forceinline__ void emit_group(const int32_t* __restrict__ src, cons
                                            const int32_t* __restrict__ trip_rowptr, int64_t E, int64_t T,
                                            int32_t* __restrict__ trip_src, int32_t* __restrict__ trip_dst,
                                            int32_t* __restrict__ atom_j, int32_t* __restrict__ atom_i,
-                                           int32_t* __restrict__ atom_k) {
+                                           int32_t* __restrict__ atom_k, int32_t* __restrict__ edge_rev = nullptr,
+                                           int32_t* __restrict__ rev_trip = nullptr) {
   const int64_t gtid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int64_t e = gtid / kEmitGroup;
   const int sub = threadIdx.x & (kEmitGroup - 1);
@@ -181,12 +182,19 @@ __device__ __forceinline__ void emit_group(const int32_t* __restrict__ src, cons
     hi = atom_rowptr[b + 1];
     p = trip_rowptr[e];
   }
+  const int p0 = p;
   // loop until every group in the wave is done (wave-uniform trip count via __any)
   for (int base = lo; __any(valid && base < hi); base += kEmitGroup) {
     const int idx = base + sub;
     const bool in = valid && idx < hi;
     const int k = in ? dst[idx] : -1;
     const bool keep = in && k != a;
+    // the excluded neighbour k == a is the reverse edge b->a: for the center-atom attention kernels,
+    // edge_rev[e] = id(b->a) and rev_trip[b->a] = trip_rowptr[e] (symmetric graphs: every edge has one)
+    if (edge_rev && in && k == a) {
+      edge_rev[e] = idx;
+      rev_trip[idx] = p0;
+    }
     const uint64_t ball = __ballot(keep) & group_mask;
     const uint64_t below = ball & ((1ull << lane) - 1);
     const int q = p + __popcll(below);
@@ -206,8 +214,9 @@ __global__ void triplet_emit_kernel(const int32_t* __restrict__ src, const int32
                                     const int32_t* __restrict__ trip_rowptr, int64_t E, int64_t T,
                                     int32_t* __restrict__ trip_src, int32_t* __restrict__ trip_dst,
                                     int32_t* __restrict__ atom_j, int32_t* __restrict__ atom_i,
-                                    int32_t* __restrict__ atom_k) {
-  emit_group(src, dst, atom_rowptr, trip_rowptr, E, T, trip_src, trip_dst, atom_j, atom_i, atom_k);
+                                    int32_t* __restrict__ atom_k, int32_t* __restrict__ edge_rev,
+                                    int32_t* __restrict__ rev_trip) {
+  emit_group(src, dst, atom_rowptr, trip_rowptr, E, T, trip_src, trip_dst, atom_j, atom_i, atom_k, edge_rev, rev_trip);
 }
 
 // ----------------------------------------------------------------------------- transpose
@@ -430,8 +439,9 @@ __global__ void emit_transpose_sym_kernel(const int32_t* __restrict__ src, const
                                           int32_t* __restrict__ trip_src, int32_t* __restrict__ trip_dst,
                                           int32_t* __restrict__ atom_j, int32_t* __restrict__ atom_i,
                                           int32_t* __restrict__ atom_k, int32_t* __restrict__ src_perm,
-                                          int32_t* __restrict__ src_dst) {
-  emit_group(src, dst, atom_rowptr, trip_rowptr, E, T, trip_src, trip_dst, atom_j, atom_i, atom_k);
+                                          int32_t* __restrict__ src_dst, int32_t* __restrict__ edge_rev,
+                                          int32_t* __restrict__ rev_trip) {
+  emit_group(src, dst, atom_rowptr, trip_rowptr, E, T, trip_src, trip_dst, atom_j, atom_i, atom_k, edge_rev, rev_trip);
   transpose_group(src, dst, atom_rowptr, trip_rowptr, src_rowptr, E, src_perm, src_dst);
 }
 
@@ -439,7 +449,7 @@ __global__ void emit_transpose_sym_kernel(const int32_t* __restrict__ src, const
 
 using namespace x2g;
 
-X2G_API int x2g_abi_version(void) { return 13; }
+X2G_API int x2g_abi_version(void) { return 14; }
 
 X2G_API const char* x2g_status_string(int status) {
   switch (status) {
@@ -497,7 +507,8 @@ X2G_API int x2g_vertex_to_edge(const int32_t* edge_src, const int32_t* edge_dst,
   if ((rc = exclusive_scan(count, E, trip_rowptr, partial, st))) return rc;
   if (E > 0) {
     triplet_emit_kernel<<<blocks_for(E * kEmitGroup, 256), 256, 0, st>>>(
-        edge_src, edge_dst, atom_rowptr, trip_rowptr, E, T, trip_src, trip_dst, atom_j, atom_i, atom_k);
+        edge_src, edge_dst, atom_rowptr, trip_rowptr, E, T, trip_src, trip_dst, atom_j, atom_i, atom_k, nullptr,
+        nullptr);
   }
   return last_launch_status();
 }
@@ -537,9 +548,10 @@ X2G_API int x2g_line_graph_transpose(const int32_t* trip_src, const int32_t* tri
 
 X2G_API int x2g_vertex_to_edge_sym(const int32_t* edge_src, const int32_t* edge_dst, int64_t E, int64_t N, int64_t T,
                                    int32_t* atom_rowptr, int32_t* trip_rowptr, int32_t* trip_src, int32_t* trip_dst,
-                                   int32_t* atom_j, int32_t* atom_i, int32_t* atom_k, void* workspace,
-                                   size_t workspace_bytes, void* stream) {
+                                   int32_t* atom_j, int32_t* atom_i, int32_t* atom_k, int32_t* edge_rev,
+                                   int32_t* rev_trip, void* workspace, size_t workspace_bytes, void* stream) {
   if (E < 0 || N < 0 || T < 0 || !atom_rowptr || !trip_rowptr) return X2G_EINVAL;
+  if (!edge_rev != !rev_trip) return X2G_EINVAL;
   if (E > 0 && (!edge_src || !edge_dst)) return X2G_EINVAL;
   if (T > 0 && (!trip_src || !trip_dst)) return X2G_EINVAL;
   if (workspace_bytes < x2g_vertex_to_edge_workspace(E, N) || !workspace) return X2G_EWORKSPACE;
@@ -552,7 +564,8 @@ X2G_API int x2g_vertex_to_edge_sym(const int32_t* edge_src, const int32_t* edge_
   if ((rc = degree_scan(edge_dst, atom_rowptr, E, trip_rowptr, count, partial, st))) return rc;
   if (E > 0) {
     triplet_emit_kernel<<<blocks_for(E * kEmitGroup, 256), 256, 0, st>>>(
-        edge_src, edge_dst, atom_rowptr, trip_rowptr, E, T, trip_src, trip_dst, atom_j, atom_i, atom_k);
+        edge_src, edge_dst, atom_rowptr, trip_rowptr, E, T, trip_src, trip_dst, atom_j, atom_i, atom_k, edge_rev,
+        rev_trip);
   }
   return last_launch_status();
 }
@@ -583,15 +596,17 @@ X2G_API int x2g_line_graph_transpose_sym(const int32_t* edge_src, const int32_t*
 X2G_API int x2g_line_graph_sym_build(const int32_t* edge_src, const int32_t* edge_dst, int64_t E, int64_t N,
                                      int64_t T, int32_t* atom_rowptr, int32_t* trip_rowptr, int32_t* trip_src,
                                      int32_t* trip_dst, int32_t* atom_j, int32_t* atom_i, int32_t* atom_k,
-                                     int32_t* src_rowptr, int32_t* src_perm, int32_t* src_dst, void* workspace,
-                                     size_t workspace_bytes, void* stream) {
+                                     int32_t* src_rowptr, int32_t* src_perm, int32_t* src_dst, int32_t* edge_rev,
+                                     int32_t* rev_trip, void* workspace, size_t workspace_bytes, void* stream) {
   if (E < 0 || N < 0 || T < 0 || !atom_rowptr || !trip_rowptr || !src_rowptr) return X2G_EINVAL;
+  if (!edge_rev != !rev_trip) return X2G_EINVAL;
   if (E > 0 && (!edge_src || !edge_dst)) return X2G_EINVAL;
   if (T > 0 && (!trip_src || !trip_dst || !src_perm)) return X2G_EINVAL;
   if (workspace_bytes < x2g_vertex_to_edge_workspace(E, N) || !workspace) return X2G_EWORKSPACE;
   if (E == 0 || E > kScan1Max) {  // outside the one-workgroup scan: the two entry points in turn
     if (int rc = x2g_vertex_to_edge_sym(edge_src, edge_dst, E, N, T, atom_rowptr, trip_rowptr, trip_src, trip_dst,
-                                        atom_j, atom_i, atom_k, workspace, workspace_bytes, stream))
+                                        atom_j, atom_i, atom_k, edge_rev, rev_trip, workspace, workspace_bytes,
+                                        stream))
       return rc;
     return x2g_line_graph_transpose_sym(edge_src, edge_dst, atom_rowptr, trip_rowptr, E, src_rowptr, src_perm,
                                         src_dst, workspace, workspace_bytes, stream);
@@ -603,6 +618,6 @@ X2G_API int x2g_line_graph_sym_build(const int32_t* edge_src, const int32_t* edg
   if ((rc = last_launch_status())) return rc;
   emit_transpose_sym_kernel<<<blocks_for(E * kEmitGroup, 256), 256, 0, st>>>(
       edge_src, edge_dst, atom_rowptr, trip_rowptr, src_rowptr, E, T, trip_src, trip_dst, atom_j, atom_i, atom_k,
-      src_perm, src_dst);
+      src_perm, src_dst, edge_rev, rev_trip);
   return last_launch_status();
 }

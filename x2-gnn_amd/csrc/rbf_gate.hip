@@ -416,8 +416,13 @@ X2G_API int x2g_rbf_pool_fwd_batch(const x2g_gate_job* jobs, int32_t n_jobs, con
 
 static int gate_bwd_launch(const GateBwdJobs& J, int n_jobs, const int32_t* owner, const float* rbf, int64_t rows,
                            int D, int R, int drbf_acc, int splits, hipStream_t st) {
-  // (the optional operands go through 32-bit buffer offsets: rows x D floats below 2^31 bytes)
-  if (rows * static_cast<int64_t>(D) * 4 >= (int64_t(1) << 31) || rows * static_cast<int64_t>(R) * 4 >= (int64_t(1) << 31))
+  // the optional operands go through 32-bit buffer offsets, so each one PRESENT bounds the rows (an
+  // absent one's descriptor is empty: every offset reads zero); g, x, dx, drbf use 64-bit pointers
+  constexpr int64_t kLim = int64_t(1) << 31;
+  bool add = false;
+  for (int j = 0; j < n_jobs; ++j) add = add || J.dx_add[j] != nullptr;
+  if ((owner && rows * 4 >= kLim) || (drbf_acc && rows * static_cast<int64_t>(R) * 4 >= kLim) ||
+      (add && rows * static_cast<int64_t>(D) * 4 >= kLim))
     return X2G_EUNSUPPORTED;
   const dim3 grid(static_cast<unsigned>(splits), static_cast<unsigned>(n_jobs));
   switch (D) {

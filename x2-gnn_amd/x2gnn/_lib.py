@@ -49,9 +49,9 @@ SIGNATURES = {
     "x2g_rbf_gate_fwd": [_P, _P, _P, _P, _I64, _I32, _I32, _P, _P],
     "x2g_rbf_pool_fwd": [_P, _P, _P, _P, _P, _I64, _I32, _I32, _P, _P],
     "x2g_rbf_gate_bwd_workspace": [_I64, _I32, _I32],
-    "x2g_vertex_to_edge_sym": [_P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P],
+    "x2g_vertex_to_edge_sym": [_P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P],
     "x2g_line_graph_transpose_sym": [_P, _P, _P, _P, _I64, _P, _P, _P, _P, _SZ, _P],
-    "x2g_line_graph_sym_build": [_P, _P, _I64, _I64, _I64] + [_P] * 10 + [_P, _SZ, _P],
+    "x2g_line_graph_sym_build": [_P, _P, _I64, _I64, _I64] + [_P] * 12 + [_P, _SZ, _P],
     "x2g_keyed_row_sum_batch_workspace": [_I64, _I32, _I32, _I32],
     "x2g_keyed_row_sum_batch": [_P, _P, _I32, _P, _I64, _I32, _I32, ctypes.c_int, _P, _SZ, _P],
     "x2g_clip_adam_ema_ex": [_P, _P, _P, _P, _P, _I64, _P, ctypes.c_int, _P, _SZ, _P],
@@ -72,6 +72,11 @@ SIGNATURES = {
                               _I32, _P, _P, _P, _P, _P],
     "x2g_sbf_attention_fwd_stats": [_P, _P, _P, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _I64, _I64, _I32,
                                     _I32, _I32, _P, _P, _P, _P, _P, _P],
+    "x2g_sbf_attention_fwd_center": [_P, _P, _P, _P, _P, _P, ctypes.c_int, _P, _I64, _P, _P, _P, _I64, _I64, _I32,
+                                     _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P],
+    "x2g_sbf_attention_bwd_center_lds": [_I32, _I32],
+    "x2g_sbf_attention_bwd_center": [_P, _P, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64,
+                                     _I32, _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P],
     "x2g_sbf_attention_bwd_dst": [_P, _P, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64,
                                   _I32, _I32, _I32, _P, _P, _P, _P, _P],
     "x2g_sbf_attention_bwd_src": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I32, _I32, _I32, _P,
@@ -156,7 +161,8 @@ RESTYPES = {"x2g_status_string": ctypes.c_char_p, "x2g_vertex_to_edge_workspace"
             "x2g_chain_wgrad_splits": ctypes.c_int32, "x2g_tiled_wgrad_workspace": _SZ, "x2g_tiled_wgrad_flat_workspace": _SZ,
             "x2g_tiled_wgrad_flat_rows_workspace": _SZ,
             "x2g_tiled_wgrad_splits": ctypes.c_int32, "x2g_conv_proj_bwd_gate_splits": ctypes.c_int32,
-            "x2g_conv_proj_bwd_gate_workspace": _SZ, "x2g_graph_layernorm_bwd_workspace": _SZ}
+            "x2g_conv_proj_bwd_gate_workspace": _SZ, "x2g_graph_layernorm_bwd_workspace": _SZ,
+            "x2g_sbf_attention_bwd_center_lds": _SZ}
 
 _lib = None
 

@@ -97,7 +97,7 @@ def _meta_from_tensors(data):
         e0 += edges[m]
         a0 += nodes[m]
     return {"nodes": nodes.astype(np.int64), "edges": edges, "triplets": np.array(trips, dtype=np.int64),
-            "symmetric": _is_symmetric(ei, n)}
+            "symmetric": _is_symmetric(ei, n), "max_degree": int(np.bincount(ei[0]).max()) if ei.shape[1] else 0}
 
 
 class Batch(Data):
@@ -152,7 +152,9 @@ def _add_device_indices(b, nodes, edges):
     b._store["_x2g_line_ptr"] = torch.from_numpy(np.concatenate([[0], np.cumsum(edges)]).astype(np.int32))
     b._store["_x2g_dst_type"] = torch.from_numpy(b._store["x"].numpy()[ei_np[1]].astype(np.int32))
     b._store["_x2g_src_type"] = torch.from_numpy(b._store["x"].numpy()[ei_np[0]].astype(np.int32))
+    b._store["_x2g_atom_type"] = torch.from_numpy(b._store["x"].numpy().reshape(-1).astype(np.int32))
     b._store["_x2g_symmetric"] = _is_symmetric(ei_np, int(nodes.sum()))
+    b._store["_x2g_max_degree"] = int(np.bincount(ei_np[0]).max()) if ei_np.shape[1] else 0
 
 
 def _is_symmetric(ei, n):

@@ -119,7 +119,7 @@ class _Trunk(nn.Module):
             out._x2g_fanin = ops.FanIn()
         readout(0, out)
         sbf = data.edge_sbf
-        # (every layer's S projected up front in one launch, ops.sbf_project_all, measured 1.2 % slower in
+        # (every layer's S projected up front in one launch, x2g_sbf_project_batch, measured 1.2 % slower in
         # the step A/B, profiles/r4ab1_step_ab_sbatch_feat.log: each layer's S written right before its
         # attention is still in the MALL when the attention reads it; projected 3 layers early it is not)
         for i in range(self.conv_layers):

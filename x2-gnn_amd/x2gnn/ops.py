@@ -88,6 +88,14 @@ class LineGraph:
         self.dst_type = self.src_type = None
         ws_bytes = int(_lib.load().x2g_vertex_to_edge_workspace(self.E, self.N))
         self._ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        # symmetric graphs: each edge's reverse and where its triplet block starts, for the center-atom
+        # attention kernels (written by the same emission grid)
+        self.edge_rev = torch.empty(self.E, **i32) if self.symmetric else None
+        self.rev_trip = torch.empty(self.E, **i32) if self.symmetric else None
+        # degree bound of the center atoms (host metadata; set by GraphPlan, None = unknown) and each atom's
+        # element row (int32 [N]: the key of the center-atom edge-term gradient)
+        self.max_degree = None
+        self.atom_type = None
         if with_transpose and self.symmetric:
             self._src_rowptr = torch.empty(self.E + 1, **i32)
             self._src_perm = torch.empty(self.T, **i32)
@@ -95,12 +103,16 @@ class LineGraph:
             call("x2g_line_graph_sym_build", ptr(edge_src), ptr(edge_dst), self.E, self.N, self.T,
                  ptr(self.atom_rowptr), ptr(self.trip_rowptr), ptr(self.trip_src), ptr(self.trip_dst),
                  ptr(self.atom_j), ptr(self.atom_i), ptr(self.atom_k), ptr(self._src_rowptr), ptr(self._src_perm),
-                 ptr(self._src_dst), ptr(self._ws), ws_bytes, stream_ptr())
+                 ptr(self._src_dst), ptr(self.edge_rev), ptr(self.rev_trip), ptr(self._ws), ws_bytes, stream_ptr())
             return
-        call("x2g_vertex_to_edge_sym" if self.symmetric else "x2g_vertex_to_edge", ptr(edge_src), ptr(edge_dst),
-             self.E, self.N, self.T, ptr(self.atom_rowptr), ptr(self.trip_rowptr), ptr(self.trip_src),
-             ptr(self.trip_dst), ptr(self.atom_j), ptr(self.atom_i), ptr(self.atom_k), ptr(self._ws), ws_bytes,
-             stream_ptr())
+        if self.symmetric:
+            call("x2g_vertex_to_edge_sym", ptr(edge_src), ptr(edge_dst), self.E, self.N, self.T, ptr(self.atom_rowptr),
+                 ptr(self.trip_rowptr), ptr(self.trip_src), ptr(self.trip_dst), ptr(self.atom_j), ptr(self.atom_i),
+                 ptr(self.atom_k), ptr(self.edge_rev), ptr(self.rev_trip), ptr(self._ws), ws_bytes, stream_ptr())
+            return
+        call("x2g_vertex_to_edge", ptr(edge_src), ptr(edge_dst), self.E, self.N, self.T, ptr(self.atom_rowptr),
+             ptr(self.trip_rowptr), ptr(self.trip_src), ptr(self.trip_dst), ptr(self.atom_j), ptr(self.atom_i),
+             ptr(self.atom_k), ptr(self._ws), ws_bytes, stream_ptr())
 
     @classmethod
     def from_triplets(cls, triplet_index, num_line_nodes: int):
@@ -118,6 +130,7 @@ class LineGraph:
         lg._src_rowptr = lg._src_perm = lg._src_dst = None
         lg.dst_type = lg.src_type = None
         lg.symmetric = False
+        lg.edge_rev = lg.rev_trip = lg.max_degree = lg.atom_type = None
         ws_bytes = int(_lib.load().x2g_vertex_to_edge_workspace(lg.E, 0))
         lg._ws = torch.empty(ws_bytes, dtype=torch.uint8, device=lg.trip_src.device)
         return lg
@@ -305,51 +318,24 @@ def _sbf_factors(lg, sbf, edge_mode, D, edge, edge_row):
     return fac[1], fac[2]
 
 
-SBF_PROJECT_MAX_LAYERS = 8  # X2G_SBF_PROJECT_MAX_LAYERS
+CENTER_MAX_DEGREE = 64  # X2G_CENTER_MAX_DEGREE
+# Center-atom attention kernels (csrc/attention_center.hip) for symmetric line graphs: False = the
+# destination-major kernels everywhere (a parity test flips it).
+_CENTER = True
 
 
-def _sproj_key(sbf, w, b):
-    return (sbf.data_ptr(), w.data_ptr(), b.data_ptr())
-
-
-def sbf_project_all(sbf, weights, biases, lg):
-    """S_l = sbf W_l^T + b_l for every layer's lin_sbf in ONE launch (x2g_sbf_project_batch: one ramp
-    and drain instead of one per layer; the later layers read sbf from the MALL the first one filled),
-    left on the line graph for the layers' attention calls (each S taken once, by the call whose sbf and
-    parameters it was projected from).  The caller clears what is left (``clear_sproj``), so an S
-    projected before a weight update can never be read after it."""
-    sbf = _f32(sbf)
-    T, K = sbf.shape
-    n = len(weights)
-    if n == 0 or n > SBF_PROJECT_MAX_LAYERS or T == 0:
-        return
-    if any(w.dtype != torch.float32 or not w.is_contiguous() for w in weights) or \
-            any(b is None or b.dtype != torch.float32 or not b.is_contiguous() for b in biases):
-        return  # (keys are the parameters' own pointers)
-    D = int(weights[0].shape[0])
-    if any(int(w.shape[0]) != D or int(w.shape[1]) != K for w in weights):
-        return
-    outs = [torch.empty(T, D, dtype=torch.float32, device=sbf.device) for _ in weights]
-    P = ctypes.c_void_p * n
-    call("x2g_sbf_project_batch", ptr(sbf), T, K, P(*[w.data_ptr() for w in weights]),
-         P(*[b.data_ptr() for b in biases]), n, D, P(*[o.data_ptr() for o in outs]), stream_ptr())
-    cache = lg.__dict__.setdefault("_x2g_sproj", {})
-    for w, b, o in zip(weights, biases, outs):
-        cache[_sproj_key(sbf, w, b)] = o
-
-
-def clear_sproj(lg):
-    cache = getattr(lg, "_x2g_sproj", None)
-    if cache:
-        cache.clear()
-
-
-def _take_sproj(lg, sbf, w, b, T, D):
-    cache = getattr(lg, "_x2g_sproj", None)
-    if not cache or b is None:
-        return None
-    s = cache.pop(_sproj_key(sbf, w, b), None)
-    return s if s is not None and tuple(s.shape) == (T, D) else None
+def _center_rows(lg, edge_mode, edge_row, D, channels):
+    """(ok, src_row): whether the center-atom forward applies to this call, and the per-source edge-table
+    row it reads for EDGE_PER_DST (the center atom's element: lg.src_type, valid when the caller's
+    per-destination rows are the line graph's own dst_type)."""
+    if (not _CENTER or getattr(lg, "edge_rev", None) is None or lg.max_degree is None
+            or lg.max_degree > CENTER_MAX_DEGREE or D != 128 or channels % 4 or edge_mode == EDGE_PER_TRIPLET):
+        return False, None
+    if edge_mode == EDGE_PER_DST:
+        if edge_row is None or lg.src_type is None or edge_row is not lg.dst_type:
+            return False, None
+        return True, lg.src_type
+    return True, None
 
 
 class _SBFAttention(torch.autograd.Function):
@@ -370,19 +356,23 @@ class _SBFAttention(torch.autograd.Function):
         alpha = torch.empty(T, heads, dtype=torch.float32, device=dev)
         smax = torch.empty(E, heads, dtype=torch.float32, device=dev)
         sden = torch.empty(E, heads, dtype=torch.float32, device=dev)
-        # S = lin_sbf(sbf) once per layer [T, D]; the three attention kernels read its rows
-        # (sbf pointer = S, weight pointer NULL) instead of re-projecting per triplet.  The trunk
-        # projects every layer's S in one launch before its first layer (sbf_project_all): take it
-        sproj = _take_sproj(lg, sbf, w_sbf, b_sbf, T, D)
-        if sproj is None:
-            sproj = torch.empty(T, D, dtype=torch.float32, device=dev)
-            call("x2g_sbf_project", ptr(sbf), T, sbf.shape[1], ptr(w_sbf), ptr(b_sbf), D, ptr(sproj), stream_ptr())
+        # S = lin_sbf(sbf) once per layer [T, D], right before this layer's attention (so it is still
+        # in the MALL when the three attention kernels read its rows: sbf pointer = S, weight pointer
+        # NULL) instead of re-projecting per triplet
+        sproj = torch.empty(T, D, dtype=torch.float32, device=dev)
+        call("x2g_sbf_project", ptr(sbf), T, sbf.shape[1], ptr(w_sbf), ptr(b_sbf), D, ptr(sproj), stream_ptr())
         # per-row (mean, M2) of the output for a graph LayerNorm fused into the next row chain
         rstats = torch.empty(E, 2, dtype=torch.float32, device=dev) if _LN_FUSE and D == 128 else None
-        call("x2g_sbf_attention_fwd_stats" if rstats is not None else "x2g_sbf_attention_fwd", ptr(q), ptr(k), ptr(v),
-             ptr(skip), ptr(edge), ptr(edge_row), edge_mode, ptr(sproj), None, None, ptr(lg.trip_rowptr),
-             ptr(lg.trip_src), E, T, heads, channels, D, ptr(out), ptr(alpha), ptr(smax), ptr(sden),
-             *((ptr(rstats),) if rstats is not None else ()), stream_ptr())
+        center, src_row = _center_rows(lg, edge_mode, edge_row, D, channels)
+        if center:
+            call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(src_row), edge_mode,
+                 ptr(sproj), 0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), 0, lg.N, lg.max_degree, E, T,
+                 heads, channels, ptr(out), ptr(alpha), ptr(smax), ptr(sden), ptr(rstats), stream_ptr())
+        else:
+            call("x2g_sbf_attention_fwd_stats" if rstats is not None else "x2g_sbf_attention_fwd", ptr(q), ptr(k),
+                 ptr(v), ptr(skip), ptr(edge), ptr(edge_row), edge_mode, ptr(sproj), None, None, ptr(lg.trip_rowptr),
+                 ptr(lg.trip_src), E, T, heads, channels, D, ptr(out), ptr(alpha), ptr(smax), ptr(sden),
+                 *((ptr(rstats),) if rstats is not None else ()), stream_ptr())
         if factors is not None:  # the factorised backward never reads sbf itself
             ctx.save_for_backward(q, k, v, edge, factors[0], factors[1], sproj, alpha, smax, sden)
         else:
@@ -447,9 +437,32 @@ class _SBFAttention(torch.autograd.Function):
         g = None if _SRC_G else torch.empty(T, heads, dtype=torch.float32, device=dev)
         prob = torch.empty(T, heads, dtype=torch.float32, device=dev)
         rho = torch.empty(E, heads, dtype=torch.float32, device=dev)
-        d_edge = torch.empty(E, D, dtype=torch.float32, device=dev) if mode == EDGE_PER_DST else None
         gfold = torch.empty(E, 8, D, dtype=torch.float32, device=dev)
         st = stream_ptr()
+        center, src_row = _center_rows(lg, mode, ctx.edge_row, D, channels)
+        if center and getattr(lg, "atom_type", None) is not None and (
+                _lib.load().x2g_sbf_attention_bwd_center_lds(lg.max_degree, heads) <= 160 * 1024):
+            # one launch for both passes, per center atom (csrc/attention_center.hip); the edge term's
+            # gradient comes per center atom and is summed by the atoms' elements
+            want_edge = mode == EDGE_PER_DST and ctx.needs_input_grad[4]
+            d_edge_atom = torch.empty(lg.N, D, dtype=torch.float32, device=dev) if want_edge else None
+            call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(src_row), mode, ptr(sproj),
+                 ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(alpha), ptr(smax), ptr(sden),
+                 ptr(dout), lg.N, lg.max_degree, E, T, heads, channels, ptr(dq), ptr(dk), ptr(dv), ptr(gfold),
+                 ptr(d_edge_atom), st)
+            d_edge = None
+            if want_edge:
+                if ctx.defer_edge:
+                    d_edge = keyed_row_sum_deferred(d_edge_atom, lg.atom_type, ctx.edge_shape[0], ctx.keyed_pending)
+                else:
+                    d_edge = keyed_row_sum(d_edge_atom, lg.atom_type, ctx.edge_shape[0])
+            gw, gb = grad_sink(ctx.w_param), grad_sink(ctx.b_param)
+            if gw is not None and gb is not None:
+                dw, db = sbf_radial_wgrad(gfold, radial, dw_out=gw, db_out=gb)
+            else:
+                dw, db = sbf_radial_wgrad(gfold, radial)
+            return dq, dk, dv, dout, d_edge, None, dw, db, None, None, None, None, None
+        d_edge = torch.empty(E, D, dtype=torch.float32, device=dev) if mode == EDGE_PER_DST else None
         call("x2g_sbf_attention_bwd_dst_g", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(ctx.edge_row), mode, ptr(sproj),
              ptr(lg.trip_rowptr), ptr(lg.trip_src), ptr(alpha), ptr(smax), ptr(sden), ptr(dout), E, T, heads, channels,
              ptr(dq), ptr(d_edge), ptr(g), ptr(prob), ptr(rho), st)
@@ -857,10 +870,15 @@ def _infer_tiles(lg, tmax):
     if tmax in cache:
         return cache[tmax]
     counts = getattr(lg, "mol_counts", None)
+    ap = None
     if counts is not None:
-        ec, tc = counts
+        ec, tc = counts[0], counts[1]
         ep = np.concatenate([[0], np.cumsum(ec)])
         rp = np.concatenate([[0], np.cumsum(tc)])
+        if len(counts) > 2:  # atoms per molecule: each tile's atom range too (center-atom kernels)
+            ap = np.concatenate([[0], np.cumsum(counts[2])])
+            if ap[-1] != lg.N:
+                ap = None
         # the host metadata must describe this line graph, or a tile could split a destination
         # segment or run past E / T: otherwise take the row pointer itself (one read-back)
         if ep[-1] != lg.E or rp[-1] != lg.T or (np.asarray(ec) < 0).any() or (np.asarray(tc) < 0).any():
@@ -868,13 +886,15 @@ def _infer_tiles(lg, tmax):
     if counts is None:
         rp = lg.trip_rowptr.cpu().numpy().astype("int64")
         ep = np.arange(lg.E + 1, dtype=np.int64)
+        ap = None
     n = len(rp) - 1
     tiles, i = [], 0
     while i < n:
         j = int(np.searchsorted(rp, rp[i] + tmax, side="right")) - 1  # furthest j with rp[j] - rp[i] <= tmax
         j = min(max(j, i + 1), n)
         if ep[j] > ep[i]:
-            tiles.append((int(ep[i]), int(ep[j]), int(rp[i]), int(rp[j])))
+            atoms = (int(ap[i]), int(ap[j])) if ap is not None else None
+            tiles.append((int(ep[i]), int(ep[j]), int(rp[i]), int(rp[j]), atoms))
         i = j
     cache[tmax] = tiles
     return tiles
@@ -890,13 +910,20 @@ def _attention_fwd_tiled(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, 
     smax, sden = torch.empty(E, H, **f32), torch.empty(E, H, **f32)
     rstats = torch.empty(E, 2, **f32) if _LN_FUSE and D == 128 else None
     tiles = _infer_tiles(lg, tmax)
-    S = torch.empty(max(t1 - (t0 & ~1) for _, _, t0, t1 in tiles), D, **f32)
+    S = torch.empty(max(t[3] - (t[2] & ~1) for t in tiles), D, **f32)
     st = stream_ptr()
     fb, ib = 4, 4  # bytes per float32 / int32 element
-    for e0, e1, t0, t1 in tiles:
+    center, src_row = _center_rows(lg, edge_mode, edge_row, D, channels)
+    center = center and all(t[4] is not None for t in tiles)
+    for e0, e1, t0, t1, atoms in tiles:
         ta = t0 & ~1  # from an even row: the projection's fast path wants 16-byte aligned sbf blocks
         call("x2g_sbf_project", sbf.data_ptr() + ta * sbf.shape[1] * fb, t1 - ta, sbf.shape[1], ptr(w_sbf),
              ptr(b_sbf), D, ptr(S), st)
+        if center:  # whole molecules: the tile's atoms own exactly its triplets (S rows t - ta)
+            call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(src_row), edge_mode,
+                 ptr(S), ta, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), atoms[0], atoms[1] - atoms[0],
+                 lg.max_degree, E, T, heads, channels, ptr(out), ptr(alpha), ptr(smax), ptr(sden), ptr(rstats), st)
+            continue
         # the kernel reads S at absolute triplet indices t in [t0, t1): hand it the base S - ta rows;
         # everything per destination edge is offset by e0, everything per triplet / per source edge
         # is indexed absolutely
@@ -2140,18 +2167,33 @@ class _ScatterReduce(torch.autograd.Function):
         return dx, None, None
 
 
+def _plan_rows(src, plan):
+    """A prebuilt IndexPlan's row count must be src's: its permutation addresses src's rows."""
+    _need_cuda(src)
+    if src.shape[0] != plan.n:
+        raise ValueError(f"IndexPlan was built for {plan.n} rows, src has {src.shape[0]}")
+
+
 def _scatter(src, index, dim_size, mode):
-    _need_cuda(src, index)
-    if src.shape[0] != index.numel():
-        raise ValueError("scatter: index must hold one key per row of src (dim=0)")
-    plan = index if isinstance(index, IndexPlan) else IndexPlan(index, int(dim_size))
+    if isinstance(index, IndexPlan):
+        _plan_rows(src, index)
+        if dim_size is not None and int(dim_size) != index.dim_size:
+            raise ValueError(f"dim_size {dim_size} differs from the IndexPlan's {index.dim_size}")
+        plan = index
+    else:
+        _need_cuda(src, index)
+        if src.shape[0] != index.numel():
+            raise ValueError("scatter: index must hold one key per row of src (dim=0)")
+        if dim_size is None:  # torch_scatter's default: index.max() + 1 (a host read)
+            dim_size = int(index.max()) + 1 if index.numel() else 0
+        plan = IndexPlan(index, int(dim_size))
     squeeze = src.dim() == 1
     x = src.unsqueeze(1) if squeeze else src.reshape(src.shape[0], -1)
     out = _ScatterReduce.apply(x, plan, mode)
     return out.squeeze(1) if squeeze else out.view(plan.dim_size, *src.shape[1:])
 
 
-def scatter_add(src, index, dim_size: int):
+def scatter_add(src, index, dim_size: int = None):
     """torch_scatter.scatter_add(src, index, dim=0, dim_size=dim_size) (readout.py:37, model.py:53)
     for ANY index order (or a prebuilt ``IndexPlan``), with no host read (HIP-graph capturable):
     the keys are stably sorted on the device and the segment sum reads src's rows through the
@@ -2160,7 +2202,7 @@ def scatter_add(src, index, dim_size: int):
     return _scatter(src, index, dim_size, REDUCE_SUM)
 
 
-def scatter_mean(src, index, dim_size: int):
+def scatter_mean(src, index, dim_size: int = None):
     """torch_scatter.scatter_mean(src, index, dim=0, dim_size=dim_size) (readout.py:69, MolWise's
     pool_option='mean'): the segment sum divided by max(count, 1), empty segments 0; any index order,
     no host read."""
@@ -2226,8 +2268,12 @@ def softmax(src, index=None, ptr=None, num_nodes=None):
         return segment_softmax(src, ptr, int(ptr.numel()) - 1)
     if index is None:
         raise ValueError("softmax needs index or ptr")
-    if not isinstance(index, IndexPlan):
+    if isinstance(index, IndexPlan):
+        _plan_rows(src, index)
+    else:
         _need_cuda(src, index)
+        if src.shape[0] != index.numel():
+            raise ValueError("softmax: index must hold one key per row of src (dim=0)")
         n = int(num_nodes) if num_nodes is not None else (int(index.max()) + 1 if index.numel() else 0)
         index = IndexPlan(index, n)
     squeeze = src.dim() == 1

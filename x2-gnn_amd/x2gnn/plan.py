@@ -68,6 +68,7 @@ class GraphPlan:
                                  st.get("_x2g_symmetric", False))
             p.line_ptr, p.mol_ptr, p.dst_type = st["_x2g_line_ptr"], st["_x2g_mol_ptr"], st["_x2g_dst_type"]
             src_type = st.get("_x2g_src_type")
+            p.lg.atom_type = st.get("_x2g_atom_type")
         else:
             p.lg = ops.vertex_to_edge(ei, p.num_atoms, p.num_triplets, meta.get("symmetric", False))
             p.line_ptr = _ptr_from_counts(data.edge_num, p.num_graphs, dev)
@@ -79,11 +80,17 @@ class GraphPlan:
             src_type = None
         if src_type is None:
             src_type = ops._i32(data.x.index_select(0, p.lg.edge_src.long()))
+        if p.lg.atom_type is None:
+            p.lg.atom_type = ops._i32(data.x.reshape(-1))
         p.lg.dst_type, p.lg.src_type = p.dst_type, src_type
         p.atom_rowptr = p.lg.atom_rowptr
         # per-molecule line-node / triplet counts on the host: whole-molecule ranges of the triplet
         # stream for the tiled inference attention (ops._infer_tiles), with no device read
-        p.lg.mol_counts = (np.asarray(edges, dtype=np.int64), np.asarray(trips, dtype=np.int64))
+        p.lg.mol_counts = (np.asarray(edges, dtype=np.int64), np.asarray(trips, dtype=np.int64),
+                           np.asarray(nodes, dtype=np.int64))
+        # the largest center-atom degree (host metadata): sizes the center-atom kernels' LDS image
+        md = st.get("_x2g_max_degree", meta.get("max_degree"))
+        p.lg.max_degree = int(md) if md is not None else None
         return p
 
     # ------------------------------------------------------------------ from line-graph tensors
@@ -95,8 +102,10 @@ class GraphPlan:
         does at model.py:53 and inside PyG's LayerNorm); nothing else is.  The four index vectors
         must be sorted ascending, as the reference produces them (vertex_to_edge_2 emits triplets
         by destination; PyG batches are ordered by molecule; edge_index is source-sorted): their row
-        pointers come from ``ops.csr_rowptr_checked``, which flags a violation on the device
-        (``order_violated()``) instead of syncing per call.  The fast path through ``xgnn_poly``
+        pointers come from ``ops.csr_rowptr_checked``, which flags a violation on the device.  In an
+        eager call the flags come back with the molecule count (the same host read) and an unsorted
+        index raises ValueError instead of giving wrong sums; under HIP-graph capture nothing is
+        read and ``order_violated()`` reports it after a replay.  The fast path through ``xgnn_poly``
         never takes this branch.
         """
         p = cls()
@@ -110,6 +119,13 @@ class GraphPlan:
         p.line_ptr, st_l = ops.csr_rowptr_checked(b, p.num_graphs)
         p.mol_ptr, st_m = ops.csr_rowptr_checked(atom_batch, p.num_graphs)
         p.order_status = [p.lg.order_status, st_a, st_l, st_m]
+        if not torch.cuda.is_current_stream_capturing():
+            bad = torch.cat(p.order_status).cpu().tolist()
+            names = ("data.edge_index[1] (triplet destinations)", "edge_index_0", "data.batch", "atom_batch")
+            wrong = [n for n, f in zip(names, bad) if f]
+            if wrong:
+                raise ValueError("SBFTransformer drop-in: index not sorted ascending (or out of range): "
+                                 + ", ".join(wrong))
         return p
 
 
