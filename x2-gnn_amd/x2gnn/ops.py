@@ -320,8 +320,10 @@ def _sbf_factors(lg, sbf, edge_mode, D, edge, edge_row):
 
 CENTER_MAX_DEGREE = 64  # X2G_CENTER_MAX_DEGREE
 # Center-atom attention kernels (csrc/attention_center.hip) for symmetric line graphs: False = the
-# destination-major kernels everywhere (a parity test flips it).
+# destination-major kernels everywhere; _CENTER_BWD False = the center forward with the destination-major
+# backward passes (parity tests flip them).
 _CENTER = True
+_CENTER_BWD = True
 
 
 def _center_rows(lg, edge_mode, edge_row, D, channels):
@@ -440,7 +442,7 @@ class _SBFAttention(torch.autograd.Function):
         gfold = torch.empty(E, 8, D, dtype=torch.float32, device=dev)
         st = stream_ptr()
         center, src_row = _center_rows(lg, mode, ctx.edge_row, D, channels)
-        if center and getattr(lg, "atom_type", None) is not None and (
+        if center and _CENTER_BWD and getattr(lg, "atom_type", None) is not None and (
                 _lib.load().x2g_sbf_attention_bwd_center_lds(lg.max_degree, heads) <= 160 * 1024):
             # one launch for both passes, per center atom (csrc/attention_center.hip); the edge term's
             # gradient comes per center atom and is summed by the atoms' elements
