@@ -385,16 +385,16 @@ int bwd_center_launch(const BwdCenterArgs& a, bool edge, int max_degree, hipStre
   const size_t lds = bwd_center_lds<H>(max_degree);
   if (lds > 160 * 1024) return X2G_EUNSUPPORTED;
   const unsigned grid = static_cast<unsigned>(a.n_atoms);
-  auto go = [&](auto kern) {
-    if (lds > 64 * 1024) hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+  auto go = [&](auto kern) -> int {
+    if (lds > 64 * 1024) {  // above the default dynamic-LDS limit
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+      if (e != hipSuccess) return static_cast<int>(e);
+    }
     kern<<<grid, 64 * W, lds, st>>>(a);
+    return last_launch_status();
   };
-  if (edge)
-    go(attn_bwd_center_kernel<LPH, W, B, true>);
-  else
-    go(attn_bwd_center_kernel<LPH, W, B, false>);
-  return last_launch_status();
+  return edge ? go(attn_bwd_center_kernel<LPH, W, B, true>) : go(attn_bwd_center_kernel<LPH, W, B, false>);
 }
 
 }  // namespace
