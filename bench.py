@@ -76,7 +76,8 @@ def step_roofline(ms_per_step, workload, shape):
 
 
 # probe name -> the kernel (substring of its symbol) whose PMC bytes it is
-PMC_KERNEL = {"sbf_project": "sbf_project_waves", "attn_fwd": "attn_fwd_batched",
+PMC_KERNEL = {"sbf_project": "sbf_project_waves", "attn_fwd": "attn_fwd_center_kernel",
+              "attn_bwd": "attn_bwd_center_kernel",
               "attn_bwd_dst": "attn_bwd_dst_g_batched", "attn_bwd_src": "attn_bwd_src_fold_batched",
               "sbf_radial_wgrad": "sbf_radial_wgrad"}
 METRIC = "molecules/sec (fwd+bwd) on QM9 U0, batch=128, 1/2/4/8 MI355X"
@@ -181,6 +182,21 @@ def attention_probe(model, batch, reps):
         call("x2g_sbf_radial_wgrad", ptr(gfold), ptr(radial), E, D, ptr(dwr), ptr(dbr), 0, ptr(ws), ws_bytes,
              stream_ptr())
 
+    center, src_row = ops._center_rows(lg, ops.EDGE_PER_DST, row, D, C)
+    center_bwd = center and ops._CENTER_BWD and lg.atom_type is not None
+    atom_de = torch.empty(lg.N, D, **f32)
+
+    def fwd_center():  # the model's forward on a symmetric line graph (csrc/attention_center.hip)
+        call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(src_row),
+             ops.EDGE_PER_DST, ptr(sproj), 0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), 0, lg.N,
+             lg.max_degree, E, T, H, C, ptr(out), ptr(alpha), ptr(smax), ptr(sden), None, stream_ptr())
+
+    def bwd_center():  # both backward passes in one launch per center atom
+        call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(table), ptr(src_row), ops.EDGE_PER_DST,
+             ptr(sproj), ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(alpha), ptr(smax),
+             ptr(sden), ptr(dout), lg.N, lg.max_degree, E, T, H, C, ptr(dq), ptr(dk), ptr(dv), ptr(gfold),
+             ptr(atom_de), stream_ptr())
+
     row_b = 4 * D
     # Bytes per launch, two ways.  "bytes" (the roofline's algorithmic figure): every array the
     # kernel needs, each element once -- k / v / q / dout rows count once per LINE NODE however
@@ -199,13 +215,26 @@ def attention_probe(model, batch, reps):
     src_bytes = idx + 4 * T + T * (row_b + 32 + 4 * H + gh) + E * (4 + 13 * row_b + 4 * H)
     src_gath = idx + 4 * T + T * (3 * row_b + 32 + 4 * H + gh) + E * (4 + 11 * row_b + 4 * H)
     radial_bytes = E * (8 * row_b + 4 * S) + 4 * D * (S + 1)
+    # center-atom kernels: every row once (k / v staged per atom, not gathered per triplet); indices are
+    # atom_rowptr, edge_rev, rev_trip and the per-source element row
+    cidx = 4 * (lg.N + 1) + 12 * E
+    cfwd_bytes = cidx + T * (row_b + 4 * H) + E * (5 * row_b + 8 * H)  # k v q skip out, S, alpha, max/den
+    # reads k v q dout, S, alpha, Y, max/den; writes dq dk dv, G [E, 8, D], the per-atom edge gradient
+    cbwd_bytes = cidx + T * (row_b + 4 * H + 32) + E * (4 * row_b + 8 * H) + E * (3 * row_b + 8 * row_b) + lg.N * row_b
+    probes = [("sbf_project", proj, proj_bytes, proj_bytes)]
+    if center:
+        probes.append(("attn_fwd", fwd_center, cfwd_bytes, cfwd_bytes))
+    else:
+        probes.append(("attn_fwd", fwd, fwd_bytes, fwd_gath))
+    if center_bwd:
+        probes.append(("attn_bwd", bwd_center, cbwd_bytes, cbwd_bytes))
+    else:
+        probes += [("attn_bwd_dst", bwd_dst, dst_bytes, dst_gath), ("attn_bwd_src", bwd_src, src_bytes, src_gath)]
+    probes.append(("sbf_radial_wgrad", radial_wgrad, radial_bytes, radial_bytes))
     res = {}
-    for name, fn, nbytes, gath in (("sbf_project", proj, proj_bytes, proj_bytes), ("attn_fwd", fwd, fwd_bytes, fwd_gath),
-                                   ("attn_bwd_dst", bwd_dst, dst_bytes, dst_gath),
-                                   ("attn_bwd_src", bwd_src, src_bytes, src_gath),
-                                   ("sbf_radial_wgrad", radial_wgrad, radial_bytes, radial_bytes)):
+    for name, fn, nbytes, gath in probes:
         res[name] = (_event_time(fn, reps), nbytes, gath)
-    return res, dict(E=E, T=T, D=D)
+    return res, dict(E=E, T=T, D=D, center=center, center_bwd=center_bwd)
 
 
 def dense_probe(R, reps):
@@ -371,6 +400,31 @@ def flat_wgrad_probe(flat_launches, reps):
     wgs = min(512, max(1, tiles))  # chain.hip flat_grid: two 512-thread workgroups per CU
     return {"ms": ms, "flops": float(sum(2.0 * R * D * c for R, c in launch)),
             "rows": sorted({R for R, _ in launch}), "jobs": n, "grid": wgs * 512}
+
+
+def in_step_kernel_ms(runner, batch, name, reps):
+    """The named kernel's duration INSIDE the training step: ``reps`` eager forward+backward passes
+    with HIP events around that launch on its stream (ops.KERNEL_TIMERS: a sleep kernel ahead of the
+    start event keeps the device busy while the host enqueues the launch), median over passes.  The
+    operands are the ones the same backward just wrote (MALL-warm), as in the captured step."""
+    ops.KERNEL_TIMERS[name] = []
+    try:
+        for _ in range(reps):
+            runner.forward_backward(batch)
+        torch.cuda.synchronize()
+        evs = ops.KERNEL_TIMERS[name]
+    finally:
+        ops.KERNEL_TIMERS.pop(name, None)
+    runner.bucket.zero()
+    ms = sorted(a.elapsed_time(b) for a, b in evs)
+    return (ms[len(ms) // 2], len(ms)) if ms else (None, 0)
+
+
+# Core clocks measured under each MFMA kernel's own load (trace builds stamping the shader clock against
+# the 100 MHz wall clock, profiles/r4f_sclk_chain_flat.txt): the f32 MFMA rate they can reach is
+# 157.3 TF/s x sclk / 2.4 GHz
+SCLK_GHZ = {"tiled_wgrad_flat": 1.93, "chain_fwd": 2.08, "chain_bwd": 2.12}
+SCLK_SOURCE = "profiles/r4f_sclk_chain_flat.txt"
 
 
 def _lib_ws(name, *args):
@@ -658,20 +712,35 @@ def main():
     roof = None
     flat = flat_wgrad_probe(runner.flat_launches, args.kernel_reps) if wl["train"] else None
     if flat is not None:
-        f_tfs = flat["flops"] / (flat["ms"] * 1e-3) / 1e12
+        # the launch's duration inside the step (eager passes, HIP events around it on its stream): the
+        # roofline figure; the probe (the same launch back to back on synthetic operands that are not
+        # MALL-resident) beside it
+        in_ms, in_n = in_step_kernel_ms(runner, batch, "tiled_wgrad_flat", max(3, args.kernel_reps // 4))
+        f_ms = in_ms if in_ms is not None else flat["ms"]
+        f_tfs = flat["flops"] / (f_ms * 1e-3) / 1e12
+        p_tfs = flat["flops"] / (flat["ms"] * 1e-3) / 1e12
         traffic = pmc_traffic([("tiled_flat_kernel", None)], traffic_table)  # (the largest launch)
+        sclk = SCLK_GHZ["tiled_wgrad_flat"]
         roof = {"kernel": f"x2g_tiled_wgrad_flat: {flat['jobs']} weight gradients dW = dz^T x over "
                           f"R={flat['rows']} rows in one launch (tiled_flat_kernel)",
                 "bound": "mfma", "achieved": round(f_tfs, 2), "peak": MFMA_F32_PEAK_TFS,
                 "unit": "TFLOP/s", "frac": round(f_tfs / MFMA_F32_PEAK_TFS, 4), "traffic": traffic,
-                "avg_ms": round(flat["ms"], 5), "flops_per_launch": int(flat["flops"]),
+                "avg_ms": round(f_ms, 5), "timing": (f"in-step: median of {in_n} eager training passes, HIP "
+                                                     f"events around the launch on its stream" if in_ms is not None
+                                                     else "probe"),
+                "probe_ms": round(flat["ms"], 5), "probe_frac": round(p_tfs / MFMA_F32_PEAK_TFS, 4),
+                "flops_per_launch": int(flat["flops"]),
+                "sclk_ghz": sclk, "attainable_peak": round(MFMA_F32_PEAK_TFS * sclk / 2.4, 1),
+                "frac_of_attainable": round(f_tfs / (MFMA_F32_PEAK_TFS * sclk / 2.4), 4), "sclk_source": SCLK_SOURCE,
                 "traffic_source": os.path.relpath(traffic_path, ROOT) if traffic else None}
-        dense["tiled_wgrad_flat"] = (flat["ms"], flat["flops"])
+        dense["tiled_wgrad_flat"] = (f_ms, flat["flops"])
     if not wl["train"]:  # inference: no backward; the T-row attention forward dominates
         a_ms, a_bytes, a_gath = probe["attn_fwd"]
         a_gbs = a_bytes / (a_ms * 1e-3) / 1e9
         hbm = _pmc_bytes("attn_fwd", traffic_table)
-        roof = {"kernel": "x2g_sbf_attention_fwd (attn_fwd_batched, S = lin_sbf(sbf) precomputed)",
+        roof = {"kernel": ("x2g_sbf_attention_fwd_center (attn_fwd_center_kernel: one workgroup per center atom, "
+                           "S = lin_sbf(sbf) precomputed)" if shape.get("center") else
+                           "x2g_sbf_attention_fwd (attn_fwd_batched, S = lin_sbf(sbf) precomputed)"),
                 "bound": "hbm", "achieved": round(a_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(a_gbs / HBM_PEAK_GBS, 4), "traffic": hbm, "avg_ms": round(a_ms, 5),
                 "bytes_per_launch": int(a_bytes), "gathered_bytes_per_launch": int(a_gath),

@@ -252,7 +252,7 @@ int x2g_sbf_attention_fwd_stats(const float* q, const float* k, const float* v, 
  *   atom0 .. atom0 + n_atoms - 1 (whole molecules: the tiled inference path passes a molecule range).
  *   max_degree >= every deg(b) of those atoms, <= X2G_CENTER_MAX_DEGREE (sizes the LDS image).
  * heads * channels = 128 and channels a multiple of 4, 16-byte aligned rows, else X2G_EUNSUPPORTED. */
-#define X2G_CENTER_MAX_DEGREE 64
+#define X2G_CENTER_MAX_DEGREE 128
 int x2g_sbf_attention_fwd_center(const float* q, const float* k, const float* v, const float* skip,
                                  const float* edge, const int32_t* src_row, int edge_mode, const float* sbfproj,
                                  int64_t t_base, const int32_t* atom_rowptr, const int32_t* edge_rev,

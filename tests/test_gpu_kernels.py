@@ -1935,18 +1935,19 @@ def test_center_forward_equals_destination_major(cuda, heads, channels):
 
 def test_center_forward_edge_cases(cuda):
     """Degree-1 atoms (destinations without triplets: out = skip, max -inf, denominator 0), isolated atoms
-    (no edges), a hub of degree 64 (the LDS bound), and the atom / triplet offsets the tiled inference path
+    (no edges), a hub of degree 100 (a 100 KB LDS image, above the 64 KB default), and the atom / triplet
+    offsets the tiled inference path
     hands over (two molecule ranges == the whole)."""
     from x2gnn import ops
     from x2gnn._lib import call, ptr, stream_ptr
 
     # a path a-b-c (degrees 1, 2, 1), an isolated atom, a star of degree 64, a triangle
-    pairs = [(0, 1), (1, 2)] + [(4, 5 + i) for i in range(64)] + [(69, 70), (70, 71), (69, 71)]
+    pairs = [(0, 1), (1, 2)] + [(4, 5 + i) for i in range(100)] + [(105, 106), (106, 107), (105, 107)]
     ed = sorted({(a, b) for a, b in pairs} | {(b, a) for a, b in pairs})
     ei = np.array(ed, dtype=np.int64).T
-    n = 72
+    n = 108
     lg = _sym_lg(ei, n, cuda)
-    assert lg.max_degree == 64
+    assert lg.max_degree == 100
     q, k, v, skip, S, table = _attn_inputs(lg, cuda, 4)
     a, r = _fwd_both(lg, q, k, v, skip, S, table, ops.EDGE_PER_DST, 16, 8)
     _close_fwd(a, r)
@@ -1956,7 +1957,7 @@ def test_center_forward_edge_cases(cuda):
     torch.testing.assert_close(a[0][d_hub_in], skip[d_hub_in])
     assert bool((a[2][d_hub_in] == -float("inf")).all()) and float(a[3][d_hub_in].abs().max()) == 0.0
     # two atom ranges with S handed over from each range's first triplet (the tiled path)
-    split = 4  # atoms 0..3 | 4..71: the ranges' triplets are disjoint and contiguous
+    split = 4  # atoms 0..3 | 4..107: the ranges' triplets are disjoint and contiguous
     t_split = int(lg.trip_rowptr[int(lg.atom_rowptr[split])])
     out = torch.empty_like(q)
     alpha = torch.empty(lg.T, 16, device=cuda)
@@ -1987,7 +1988,8 @@ def _bwd_both(lg, q, k, v, S, table, mode, heads, channels, seed):
     rows = table.shape[0]
     f = dict(device=q.device, dtype=torch.float32)
     # center
-    dq, dk, dv, G = (torch.full((E, D), float("nan"), **f) for _ in range(3)) + (torch.full((E, 8, D), float("nan"), **f),)
+    dq, dk, dv = (torch.full((E, D), float("nan"), **f) for _ in range(3))
+    G = torch.full((E, 8, D), float("nan"), **f)
     de_atom = torch.full((lg.N, D), float("nan"), **f) if edge is not None else None
     assert int(_lib.load().x2g_sbf_attention_bwd_center_lds(lg.max_degree, heads)) <= 160 * 1024
     call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(lg.src_type) if edge is not None else None,
@@ -1998,7 +2000,8 @@ def _bwd_both(lg, q, k, v, S, table, mode, heads, channels, seed):
     if edge is not None:
         c.append(torch.zeros(rows, D, dtype=torch.float64, device=q.device).index_add_(0, lg.atom_type.long(), de_atom.double()))
     # destination-major fold passes
-    dq2, dk2, dv2, G2 = (torch.empty(E, D, **f) for _ in range(3)) + (torch.empty(E, 8, D, **f),)
+    dq2, dk2, dv2 = (torch.empty(E, D, **f) for _ in range(3))
+    G2 = torch.empty(E, 8, D, **f)
     prob, rho = torch.empty(T, H, **f), torch.empty(E, H, **f)
     de = torch.empty(E, D, **f) if edge is not None else None
     call("x2g_sbf_attention_bwd_dst_g", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(lg.dst_type) if edge is not None else None,
@@ -2046,14 +2049,15 @@ def test_center_backward_equals_fold_passes(cuda, heads, channels):
 
 
 def test_center_backward_edge_cases(cuda):
-    """Degree-1 and isolated atoms (zero rows), a hub of degree 40 (LDS tables of 40 x 40 x heads), a
-    triangle; vs the fold passes."""
+    """Degree-1 and isolated atoms (zero rows), a hub of degree 24 (LDS tables of 24 x 24 x heads: a
+    111 KB image, above the 64 KB default), a triangle; vs the fold passes.  A degree whose image exceeds
+    the 160 KB of LDS is refused (X2G_EUNSUPPORTED: the host then takes the fold passes)."""
     from x2gnn import ops
 
-    pairs = [(0, 1), (1, 2)] + [(4, 5 + i) for i in range(40)] + [(45, 46), (46, 47), (45, 47)]
+    pairs = [(0, 1), (1, 2)] + [(4, 5 + i) for i in range(24)] + [(29, 30), (30, 31), (29, 31)]
     ed = sorted({(a, b) for a, b in pairs} | {(b, a) for a, b in pairs})
     ei = np.array(ed, dtype=np.int64).T
-    n = 48
+    n = 32
     lg = _sym_lg(ei, n, cuda, with_transpose=True)
     z = torch.randint(0, 10, (n,), generator=torch.Generator().manual_seed(1)).to(cuda)
     lg.atom_type = ops._i32(z)
@@ -2061,3 +2065,10 @@ def test_center_backward_edge_cases(cuda):
     q, k, v, _, S, table = _attn_inputs(lg, cuda, 7)
     c, r = _bwd_both(lg, q, k, v, S, table, ops.EDGE_PER_DST, 16, 8, 8)
     _close_bwd(c, r)
+    from x2gnn import _lib
+
+    assert int(_lib.load().x2g_sbf_attention_bwd_center_lds(40, 16)) > 160 * 1024
+    rc = _lib.load().x2g_sbf_attention_bwd_center(None, None, None, None, None, 0, None, None, None, None, None, None,
+                                                   None, None, None, 1, 40, 1, 1, 16, 8, None, None, None, None, None,
+                                                   None)
+    assert rc == 1002  # X2G_EUNSUPPORTED

@@ -307,6 +307,30 @@ __device__ __forceinline__ void chunk_rows(int64_t ch, int64_t nch, int64_t nblk
 // and dropped by the buffer unit
 constexpr int kOOB = static_cast<int>(0x80000000u);
 
+#ifdef X2G_TRACE  // phase timestamps (A/B trace builds only): thread 0 of each workgroup, 100 MHz clock
+__device__ unsigned long long x2g_trace_buf[1024 * 16];
+#define X2G_TR(k)                                                                                 \
+  do {                                                                                            \
+    if (threadIdx.x == 0 && (k) < 16) x2g_trace_buf[blockIdx.x * 16 + (k)] = wall_clock64();     \
+  } while (0)
+// core clock vs the 100 MHz wall clock at a kernel's start (k = 0) and end (k = 1): the SCLK the
+// kernel ran at
+__device__ unsigned long long x2g_clk_buf[1024 * 4];
+#define X2G_CLK(k)                                                          \
+  do {                                                                      \
+    if (threadIdx.x == 0) {                                                 \
+      x2g_clk_buf[blockIdx.x * 4 + 2 * (k)] = clock64();                    \
+      x2g_clk_buf[blockIdx.x * 4 + 2 * (k) + 1] = wall_clock64();           \
+    }                                                                       \
+  } while (0)
+#else
+#define X2G_TR(k) \
+  do {            \
+  } while (0)
+#define X2G_CLK(k) \
+  do {             \
+  } while (0)
+#endif
 
 // descriptor over `bytes` bytes at p (0 when off: every store dropped)
 __device__ __forceinline__ rsrc_t rsrc_n(const float* p, int64_t bytes, bool on) {
@@ -349,20 +373,28 @@ __device__ __forceinline__ void half_epi(f4 (&acc)[N], const f4 (&held)[N], f4 b
   for (int rb = RB0; rb < RB1; ++rb) {
     const int r = 16 * rb + rl;
     const f4 z = acc[rb] + bias;
+#ifndef X2G_ABL_NOZ  // (ablation switches: A/B timing builds only, never the shipped library)
     bstore4(zr, z, r < nrows ? 4 * ((r0 + r) * kCD + 16 * w + 4 * g) : kOOB);
+#endif
     f4 y;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
+#ifdef X2G_ABL_NOACT
+      const float sv = z[e];
+#else
       const float sv = silu_fast(z[e]);
+#endif
       y[e] = silu_m * sv + (1.0f - silu_m) * z[e] + res_m * held[rb][e];
     }
     out[ipos(r, 4 * w + g)] = y;
     acc[rb] = y;
+#ifndef X2G_ABL_NOT
     f4 t = quad_transpose(y, j);
 #pragma unroll
     for (int e = 0; e < 4; ++e) t[e] = 16 * rb + 4 * m + e < nrows ? t[e] : 0.0f;
     bstore4(tr, t, rb < ntile ? 4 * static_cast<int>((static_cast<int64_t>(r0 >> 4) + rb) * (16 * kCD) + f * 16 + 4 * m)
                               : kOOB);
+#endif
   }
 }
 
@@ -475,7 +507,11 @@ __device__ __forceinline__ void fwd4_stage(const ChainFwdArgs& a, int s, const f
   __builtin_amdgcn_sched_barrier(0);
   half_epi<2 * BPT, 3 * BPT>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
   pin(An);
+  X2G_TR(2 + 2 * s);
+#ifndef X2G_ABL_NOBAR
   __syncthreads();
+#endif
+  X2G_TR(3 + 2 * s);
   if (S.y) store_img<RB>(S.y, out, r0, nrows);
 #pragma unroll
   for (int b = 0; b < 8; ++b) A[b] = An[b];
@@ -609,6 +645,7 @@ __device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a, const Ch
     const int s = static_cast<int>(i / (kCD * kCD)), e = static_cast<int>(i % (kCD * kCD));
     if (a.st[s].wt) a.st[s].wt[e] = a.st[s].w[(e % kCD) * kCD + e / kCD];
   }
+  X2G_CLK(0);
   for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
     int r0, nrows;
     chunk_rows(ch, nch, nblk, a.R, r0, nrows);
@@ -618,11 +655,13 @@ __device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a, const Ch
     else
       stage_rows<RB>(img0, a.x, nullptr, r0, nrows);
     if (a.res) stage_rows<RB>(imgr, a.res, nullptr, r0, nrows);
+    X2G_TR(0);
     f4 A[8], held[RB];
     load_slice<false>(a.st[0].w, w, rl, g, A);
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) held[rb] = zero4();
     __syncthreads();
+    X2G_TR(1);
     if (a.in_t) {
       f4 xs[RB];
 #pragma unroll
@@ -634,6 +673,7 @@ __device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a, const Ch
       if (s + 1 < n) fwd4_stage<RB>(a, s + 1, img1, img0, imgr, A, held, r0, nrows, w, rl, g);
     }
   }
+  X2G_CLK(1);
 }
 
 __global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4(const ChainFwdArgs a) { chain_fwd_v4_run<false>(a, {}); }
@@ -738,6 +778,7 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
   const int64_t nch = (nblk + RB * G - 1) / (RB * G) * G;
   const int n = a.n;
   const int col = 16 * w + 4 * g;
+  X2G_CLK(0);
   for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
     int r0, nrows;
     chunk_rows(ch, nch, nblk, a.R, r0, nrows);
@@ -789,6 +830,7 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
     }
     int p = 0;
     __syncthreads();  // the previous chunk's images are no longer read
+    X2G_TR(0);
     {
       float held_m, silu_m, dres_acc_m;
       rsrc_t dres_r, dz_r, t_r;
@@ -797,6 +839,7 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
                               w, rl, g);
     }
     __syncthreads();
+    X2G_TR(1);
     for (int s = n - 1; s >= 0; --s) {
       f4 An[8];
       load_wslice(s > 0 ? s - 1 : n - 1, An);
@@ -832,7 +875,9 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
       }
       p ^= 1;
       pin(An);
+      X2G_TR(2 + 2 * (n - 1 - s));
       __syncthreads();
+      X2G_TR(3 + 2 * (n - 1 - s));
 #pragma unroll
       for (int b = 0; b < 8; ++b) A[b] = An[b];
     }
@@ -841,6 +886,7 @@ __device__ __forceinline__ void chain_bwd_v3_run(const ChainBwdArgs& a) {
     else
       store_img<RB>(a.dx, img[p], r0, nrows);
   }
+  X2G_CLK(1);
 }
 
 struct ChainBwdBatch {
@@ -1000,19 +1046,41 @@ __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, cons
 #pragma unroll
   for (int p = 0; p < NB - 1; ++p)
     if (p < nsteps) issue(p);
+#ifdef X2G_TRACE
+  unsigned long long tw = 0, tc = 0, tprev = wall_clock64();
+#endif
   for (int i = 0; i < nsteps; ++i) {
     // this step's copies are done when at most the later issued steps' 2 * WT each remain
     const int ahead = nsteps - 1 - i < NB - 2 ? nsteps - 1 - i : NB - 2;
+#ifndef X2G_ABL_NOWAIT  // (ablation switches: A/B timing builds only, never the shipped library)
     if (ahead >= 2)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * WT) : "memory");
     else if (ahead == 1)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * WT) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
+    (void)ahead;
+#endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifndef X2G_ABL_FLATNOBAR
     __builtin_amdgcn_s_barrier();  // every wave's copies of this step have landed; step i-1 is read
+#endif
+#ifdef X2G_TRACE
+    {
+      const unsigned long long t = wall_clock64();
+      tc += 0;
+      tw += t - tprev;
+      tprev = t;
+    }
+#endif
     if (i + NB - 1 < nsteps) issue(i + NB - 1);
     const int b = i % NB;
+#ifdef X2G_FLAT_BIAS_EARLY  // (A/B) the step's bias reads issued first, summed after its MFMAs
+    f4 bias_v[WT];
+#pragma unroll
+    for (int k = 0; k < WT; ++k) bias_v[k] = Ds[b][k][tpos(tid & (kCD - 1), tid >> 7)];
+#endif
 #pragma unroll
     for (int k = 0; k < WT; ++k) {
       if (t0 + static_cast<int64_t>(i) * WT + k >= t1) break;  // wave-uniform
@@ -1024,7 +1092,11 @@ __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, cons
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int bk = 0; bk < 8; ++bk) acc[bk] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[bk][e], acc[bk], 0, 0, 0);
+#if defined(X2G_ABL_NOBIAS) || defined(X2G_FLAT_BIAS_EARLY)
+      if (false) {
+#else
       if (SPREAD && has_b) {  // bias: thread (q, f) sums feature f's row quad q (every wave takes a share)
+#endif
         const f4 v = Ds[b][k][tpos(tid & (kCD - 1), tid >> 7)];
         bsum += (v[0] + v[1]) + (v[2] + v[3]);
       }
@@ -1036,7 +1108,32 @@ __device__ __forceinline__ void tiled_segment(const float* __restrict__ dz, cons
         }
       }
     }
+#ifdef X2G_FLAT_BIAS_EARLY
+#pragma unroll
+    for (int k = 0; k < WT; ++k) {
+      const bool ok = SPREAD && has_b && t0 + static_cast<int64_t>(i) * WT + k < t1;
+      bsum += ok ? (bias_v[k][0] + bias_v[k][1]) + (bias_v[k][2] + bias_v[k][3]) : 0.0f;
+    }
+#endif
+#ifdef X2G_TRACE
+    {  // (the MFMAs are issued; their results are first needed by the next step's ... at the end)
+      asm volatile("s_nop 0" ::: "memory");
+      const unsigned long long t = wall_clock64();
+      tc += t - tprev;
+      tprev = t;
+    }
+#endif
   }
+#ifdef X2G_ABL_NOWAIT
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+#ifdef X2G_TRACE
+  if (threadIdx.x == 0) {
+    x2g_trace_buf[blockIdx.x * 16 + 0] += tw;
+    x2g_trace_buf[blockIdx.x * 16 + 1] += tc;
+    x2g_trace_buf[blockIdx.x * 16 + 2] += nsteps;
+  }
+#endif
 #pragma unroll
   for (int bk = 0; bk < 8; ++bk)
 #pragma unroll
@@ -1176,6 +1273,7 @@ __global__ void __launch_bounds__(kCThreads, 2 * WPC) tiled_flat_kernel(const Ti
   __shared__ f4 X1[WT][512];
   const int64_t G = gridDim.x, i = blockIdx.x;
   const int64_t lo = i * a.total / G, hi = (i + 1) * a.total / G;
+  X2G_CLK(0);
   int j0 = 0;
   while (j0 < a.njobs && a.tile0[j0 + 1] <= lo) ++j0;  // (uniform; <= 64 jobs)
   for (int j = j0; j < a.njobs && a.tile0[j] < hi; ++j) {
@@ -1187,6 +1285,7 @@ __global__ void __launch_bounds__(kCThreads, 2 * WPC) tiled_flat_kernel(const Ti
     tiled_segment2<SPREAD, WT>(a.dz_t[j], a.in_t[j], s0 - a.tile0[j], s1 - a.tile0[j], a.has_b[j] != 0,
                                a.slab_w[j] + k * kCD * kCD, a.slab_b[j] + k * kCD, D0, X0, D1, X1);
   }
+  X2G_CLK(1);
 }
 
 inline int chain_wgrad_splits_of(int64_t ntiles, int stages) {
@@ -1430,6 +1529,7 @@ __global__ void __launch_bounds__(kCThreads, 2) conv_proj_bwd_gate_kernel(const 
   const int64_t nch = (nblk + RB * G - 1) / (RB * G) * G;  // a multiple of G: every workgroup nk chunks
   const int nk = static_cast<int>(nch / G);
   const int c0 = 16 * w + 4 * g;
+  X2G_TR(0);
   for (int i = tid; i < kCD * NJ; i += kCThreads) {
     const int c = i / NJ, j = i % NJ;
     swr[i] = j < a.RR ? a.wr[c * a.RR + j] : 0.0f;
@@ -1492,6 +1592,7 @@ __global__ void __launch_bounds__(kCThreads, 2) conv_proj_bwd_gate_kernel(const 
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // every wave's copies landed; the previous chunk's (dq, dskip), srbf and red read
+    X2G_TR(1 + 6 * k);
     drbf_out();
     stage_rows_async<RB>(img_q, a.gr[0].g, a.R, r0);
     stage_rows_async<RB>(img_s, a.gr[3].g, a.R, r0);
@@ -1515,10 +1616,12 @@ __global__ void __launch_bounds__(kCThreads, 2) conv_proj_bwd_gate_kernel(const 
     slice_gemm<RB, false>(img_v, An, acc1, rl, g);
     load_ws(3, An);  // Ws under the next pair's wait
     if (tid < RB * 16 * NJ) srbf[tid] = rbv;  // read after the next barrier
+    X2G_TR(2 + 6 * k);
     // ---- (dq, dskip): dx = (dx_add + dxs * f) + [dq | dskip] [Wq ; Ws]; the gate epilogue of
     // acc1 runs under these products
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kQSWait) : "memory");
     __syncthreads();  // every wave's copies landed; (dk, dv) no longer read; srbf written
+    X2G_TR(3 + 6 * k);
     // reads that must not wait behind the next chunk's copies go out before them
     doff = tid < nrows * a.RR ? 4 * (r0 * a.RR + tid) : kOOB;
     dold = bload1(bo, doff, 0);  // drbf += : 0 when not accumulating
@@ -1574,11 +1677,13 @@ __global__ void __launch_bounds__(kCThreads, 2) conv_proj_bwd_gate_kernel(const 
       for (int j = 0; j < NJ; ++j) sdw[(c0 + i) * NJ + j] += row_sum16(aw[i][j]);
     slice_gemm<RB, false>(img_s, An, acc, rl, g);
     load_ws(2, An);
+    X2G_TR(4 + 6 * k);
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
       const int r = 16 * rb + rl;
       bstore4(dr, d1[rb] + acc[rb], r < nrows ? 4 * ((r0 + r) * kCD + c0) : kOOB);
     }
+    X2G_TR(5 + 6 * k);
   }
   __syncthreads();  // red of the last chunk
   drbf_out();
@@ -1952,6 +2057,14 @@ X2G_API int x2g_conv_proj_bwd(const x2g_proj_grad* grads, int64_t rows, int32_t 
 }
 
 
+#ifdef X2G_TRACE
+X2G_API int x2g_trace_fetch(unsigned long long* host, int n) {
+  return static_cast<int>(hipMemcpyFromSymbol(host, HIP_SYMBOL(x2g_trace_buf), sizeof(unsigned long long) * n));
+}
+X2G_API int x2g_clk_fetch(unsigned long long* host, int n) {
+  return static_cast<int>(hipMemcpyFromSymbol(host, HIP_SYMBOL(x2g_clk_buf), sizeof(unsigned long long) * n));
+}
+#endif
 
 X2G_API int32_t x2g_conv_proj_bwd_gate_splits(int64_t rows) { return rows > 0 ? static_cast<int32_t>(proj_grid(rows)) : 0; }
 

@@ -110,9 +110,17 @@ __device__ __forceinline__ f4 w1_frag(const float* __restrict__ w1, int K, int c
 
 constexpr int kFX4 = (kFRows * kFKMax / 4 + kFThreads - 1) / kFThreads;  // staged float4 per thread
 
+#ifdef X2G_TRACE  // phase timestamps (A/B trace builds only): thread 0 of each workgroup, its first two tiles
+__device__ unsigned long long x2g_feat_trace_buf[1024 * 16];
+#define X2G_FTR(k, p)                                                                                            \
+  do {                                                                                                           \
+    if (threadIdx.x == 0 && (k) < 2) x2g_feat_trace_buf[blockIdx.x * 16 + 7 * (k) + (p)] = wall_clock64();     \
+  } while (0)
+#else
 #define X2G_FTR(k, p) \
   do {                \
   } while (0)
+#endif
 
 // The tile's span x[r0 .. r0 + nr) is contiguous and 16-byte aligned (r0 * K * 4 is a multiple of
 // 16): thread t holds float4 t + 512 u in registers (the next tile's are loaded during the current
@@ -167,6 +175,18 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
   const int64_t ntiles = (R + kFRows - 1) / kFRows;
   XTile xt;
   if (static_cast<int64_t>(blockIdx.x) < ntiles) xtile_load(a, blockIdx.x, xt);
+#ifdef FEAT_T1_NEXT
+  // (A/B) the previous tile's z1 / SiLU(z1) blocks, stored under this tile's first product
+  f4 z1p[2][2], y1p[2][2];
+  int64_t prev_r0 = -1;
+  auto t1_prev_store = [&](int k) {  // store k of 8: (block, column block, z or y); prev_r0 uniform
+    const int rb = k >> 2, cb = (k >> 1) & 1, zy = k & 1;
+    const int64_t t16 = prev_r0 / 16 + rb;
+    if (prev_r0 < 0 || t16 * 16 >= R || !a.want_t) return;
+    *reinterpret_cast<f4*>((zy ? a.y1_t : a.z1_t) + tpos(a.tf, t16, cb ? c1b : c1a, g)) =
+        zy ? y1p[rb][cb] : z1p[rb][cb];
+  };
+#endif
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t r0 = tile * kFRows;
     const int nr = R - r0 < kFRows ? static_cast<int>(R - r0) : kFRows;
@@ -208,7 +228,9 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
       for (int e = 0; e < 4; ++e) v[e] = A[(rr + e) * kFAS + 128 * p + f] * envs[rr + e];
       *reinterpret_cast<f4*>(a.xs_t + p * a.tf + t16 * 2048 + 4 * tid) = v;
     };
+#ifndef FEAT_XS_IL
     for (int it = 0; it < 6; ++it) xs_store(it);
+#endif
     X2G_FTR(kt, 2);
     // z1 = env (x W1^T) + b1: wave w -> columns c1a, c1b, both 16-row blocks
     f4 acc[2][2] = {{zero4(), zero4()}, {zero4(), zero4()}};
@@ -237,6 +259,22 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
       a1 = n1;
     };
     int q = 0;
+#if defined(FEAT_XS_IL) || defined(FEAT_T1_NEXT)
+    // the first six iterations each carry one T-layout block of x * env and / or of the previous tile's
+    // z1 / SiLU(z1) (A/B variants)
+#pragma unroll 1
+    for (int it = 0; it < 6; ++it, q += 2) {
+#ifdef FEAT_XS_IL
+      xs_store(it);
+#endif
+#ifdef FEAT_T1_NEXT
+      t1_prev_store(it);
+      if (it < 2) t1_prev_store(it + 6);
+#endif
+      if (q < KQn) group(q, wa0, wb0);
+      if (q + 1 < KQn) group(q + 1, wa1, wb1);
+    }
+#endif
     for (; q < KQn; q += 2) {
       group(q, wa0, wb0);
       if (q + 1 < KQn) group(q + 1, wa1, wb1);
@@ -265,12 +303,21 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
           y[e] = ok ? silu_(z[e]) : 0.0f;
           Y1[r * kFYS + c] = y[e];
         }
+#ifdef FEAT_T1_NEXT
+        z1p[rb][cb] = z;
+        y1p[rb][cb] = y;
+        (void)tile_ok;
+#else
         if (tile_ok && a.want_t) {
           *reinterpret_cast<f4*>(a.z1_t + tpos(a.tf, t16, c, g)) = z;
           *reinterpret_cast<f4*>(a.y1_t + tpos(a.tf, t16, c, g)) = y;
         }
+#endif
       }
     }
+#ifdef FEAT_T1_NEXT
+    prev_r0 = r0;
+#endif
     __syncthreads();
     X2G_FTR(kt, 4);
     // z2 = SiLU(z1) W2^T + b2: wave w -> columns 16w + i
@@ -320,6 +367,9 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
     }
     X2G_FTR(kt, 6);
   }
+#ifdef FEAT_T1_NEXT
+  for (int k = 0; k < 8; ++k) t1_prev_store(k);  // the last tile's
+#endif
 }
 
 struct FeatBwdArgs {
@@ -448,3 +498,8 @@ X2G_API int x2g_feat_bwd(const float* dy, const float* z2_t, const float* z1_t, 
   return last_launch_status();
 }
 
+#ifdef X2G_TRACE
+X2G_API int x2g_feat_trace_fetch(unsigned long long* host, int n) {
+  return static_cast<int>(hipMemcpyFromSymbol(host, HIP_SYMBOL(x2g_feat_trace_buf), sizeof(unsigned long long) * n));
+}
+#endif

@@ -32,10 +32,8 @@ namespace x2g {
 constexpr int kS = 42;           // sbf_dim compiled in (7 spherical x 6 radial)
 constexpr int kSph = 7;
 constexpr int kAttnWaves = 4;    // waves per 256-thread block
-#ifndef X2G_ATTN_MAX_BLOCKS
-#define X2G_ATTN_MAX_BLOCKS 2048
-#endif
-constexpr int kMaxBlocks = X2G_ATTN_MAX_BLOCKS;  // persistent-ish grid: waves grid-stride over line nodes
+// persistent-ish grid: waves grid-stride over line nodes (round 4 A/B of 1024 / 2048 / 4096 / 8192: 2048)
+constexpr int kMaxBlocks = 2048;
 constexpr float kSoftmaxEps = 1e-16f;
 
 struct AttnArgs {

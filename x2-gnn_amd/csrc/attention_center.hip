@@ -173,11 +173,16 @@ int fwd_center_launch(const FwdCenterArgs& a, bool edge, int max_degree, hipStre
   constexpr int W = 4, B = 8;
   const size_t lds = static_cast<size_t>(2) * max_degree * kCD * sizeof(float);
   const unsigned grid = static_cast<unsigned>(a.n_atoms);
-  if (edge)
-    attn_fwd_center_kernel<LPH, W, B, true><<<grid, 64 * W, lds, st>>>(a);
-  else
-    attn_fwd_center_kernel<LPH, W, B, false><<<grid, 64 * W, lds, st>>>(a);
-  return last_launch_status();
+  auto go = [&](auto kern) -> int {
+    if (lds > 64 * 1024) {  // above the default dynamic-LDS limit (degrees > 64)
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+      if (e != hipSuccess) return static_cast<int>(e);
+    }
+    kern<<<grid, 64 * W, lds, st>>>(a);
+    return last_launch_status();
+  };
+  return edge ? go(attn_fwd_center_kernel<LPH, W, B, true>) : go(attn_fwd_center_kernel<LPH, W, B, false>);
 }
 
 // ------------------------------------------------------------------------------ fused backward
@@ -341,7 +346,6 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
     float* gf = a.gfold + static_cast<int64_t>(r0 + j) * 8 * kCD + c0;
 #pragma unroll
     for (int l = 0; l < 8; ++l) st4(gf + l * kCD, G[l]);
-    if (a.d_edge) GO[j * 32 + l32] = dv;  // (GO is read by pass 1 only: after the barrier, dv + dk rows)
   }
   __syncthreads();
   // ---- rho_i = sum_{j != i} at g, j ascending (one owner per destination)
@@ -366,7 +370,9 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
     }
     st4(a.dk + static_cast<int64_t>(r0 + o) * kCD + c0, dk);
     st4(a.dq + static_cast<int64_t>(DI[o]) * kCD + c0, dq);
-    if (a.d_edge) GO[o * 32 + l32] += dk;
+    // GO is free after pass 1 (other owners read it until the barrier): dv + dk rows for the edge term;
+    // this lane's own dv store of pass 1 is read back (program order)
+    if (a.d_edge) GO[o * 32 + l32] = dk + ld4(a.dv + static_cast<int64_t>(r0 + o) * kCD + c0);
   }
   if (a.d_edge) {  // d_edge[b] = sum_j (dv_j + dk_j), j ascending
     __syncthreads();

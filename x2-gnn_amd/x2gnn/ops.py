@@ -318,7 +318,7 @@ def _sbf_factors(lg, sbf, edge_mode, D, edge, edge_row):
     return fac[1], fac[2]
 
 
-CENTER_MAX_DEGREE = 64  # X2G_CENTER_MAX_DEGREE
+CENTER_MAX_DEGREE = 128  # X2G_CENTER_MAX_DEGREE
 # Center-atom attention kernels (csrc/attention_center.hip) for symmetric line graphs: False = the
 # destination-major kernels everywhere; _CENTER_BWD False = the center forward with the destination-major
 # backward passes (parity tests flip them).
@@ -1010,6 +1010,27 @@ def _defer():
 
 TILED_MAX_JOBS = 64  # X2G_TILED_MAX_JOBS
 
+# In-step kernel timing for bench.py's roofline line: while a name is a key here, an EAGER (not captured)
+# pass appends (start, end) HIP events recorded around that kernel's launch on its stream.  A sleep kernel
+# ahead of the start event keeps the device busy while the host enqueues the launch, so the events bracket
+# the kernel alone, in the step's own cache state (its operands were just written by the same backward).
+KERNEL_TIMERS = {}
+
+
+@contextlib.contextmanager
+def _timed(name):
+    evs = KERNEL_TIMERS.get(name)
+    if evs is None or torch.cuda.is_current_stream_capturing():
+        yield
+        return
+    st = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda._sleep(200_000)  # ~0.1 ms of device time: the host enqueues the launch meanwhile
+    a.record(st)
+    yield
+    b.record(st)
+    evs.append((a, b))
+
 
 def _queue_tiled(d, R, jobs, keep):
     """Queue T-layout weight-gradient jobs (x2g_tiled_job, bucket-backed destinations) on deferral
@@ -1034,8 +1055,9 @@ def _flush_tiled(d):
         ws_bytes = int(lib.x2g_tiled_wgrad_flat_rows_workspace(rows, n, 128))
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=torch.device("cuda", torch.cuda.current_device()))
         out = (SlabJob * n)()
-        call("x2g_tiled_wgrad_flat_rows", (TiledJob * n)(*[j for _, j in part]), rows, n, 128,
-             ACCUM_WGRAD | DEFER_SLAB_SUM, out, ptr(ws), ws_bytes, stream_ptr())
+        with _timed("tiled_wgrad_flat"):
+            call("x2g_tiled_wgrad_flat_rows", (TiledJob * n)(*[j for _, j in part]), rows, n, 128,
+                 ACCUM_WGRAD | DEFER_SLAB_SUM, out, ptr(ws), ws_bytes, stream_ptr())
         d.jobs.extend(out)
         d.keep.append(ws)
     d.tiled = {}
