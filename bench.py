@@ -185,6 +185,7 @@ def attention_probe(model, batch, reps):
     center, src_row = ops._center_rows(lg, ops.EDGE_PER_DST, row, D, C)
     center_bwd = center and ops._CENTER_BWD and lg.atom_type is not None
     atom_de = torch.empty(lg.N, D, **f32)
+    g_work = torch.empty(T, H, **f32)
 
     def fwd_center():  # the model's forward on a symmetric line graph (csrc/attention_center.hip)
         call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(src_row),
@@ -195,7 +196,7 @@ def attention_probe(model, batch, reps):
         call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(table), ptr(src_row), ops.EDGE_PER_DST,
              ptr(sproj), ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(alpha), ptr(smax),
              ptr(sden), ptr(dout), lg.N, lg.max_degree, E, T, H, C, ptr(dq), ptr(dk), ptr(dv), ptr(gfold),
-             ptr(atom_de), stream_ptr())
+             ptr(atom_de), ptr(g_work), stream_ptr())
 
     row_b = 4 * D
     # Bytes per launch, two ways.  "bytes" (the roofline's algorithmic figure): every array the
@@ -220,7 +221,9 @@ def attention_probe(model, batch, reps):
     cidx = 4 * (lg.N + 1) + 12 * E
     cfwd_bytes = cidx + T * (row_b + 4 * H) + E * (5 * row_b + 8 * H)  # k v q skip out, S, alpha, max/den
     # reads k v q dout, S, alpha, Y, max/den; writes dq dk dv, G [E, 8, D], the per-atom edge gradient
-    cbwd_bytes = cidx + T * (row_b + 4 * H + 32) + E * (4 * row_b + 8 * H) + E * (3 * row_b + 8 * row_b) + lg.N * row_b
+    # (+ the g_t [T, H] scratch: written once, read back from L2 by the same workgroup)
+    cbwd_bytes = (cidx + T * (row_b + 4 * H + 32) + E * (4 * row_b + 8 * H) + E * (3 * row_b + 8 * row_b)
+                  + lg.N * row_b + T * 4 * H)
     probes = [("sbf_project", proj, proj_bytes, proj_bytes)]
     if center:
         probes.append(("attn_fwd", fwd_center, cfwd_bytes, cfwd_bytes))
@@ -640,7 +643,10 @@ def main():
         all_mols = molecules_from_geometry_file(AID_GEOM, indices=[i % n_aid for i in range(global_batch)], seed=0)
     else:
         all_mols = synthetic_molecules(global_batch, args.shape, seed=1000)
-    mols = [all_mols[i] for i in shard_by_triplets([m["triplet_num"] for m in all_mols], world)[rank]]
+    shards = shard_by_triplets([m["triplet_num"] for m in all_mols], world)
+    mols = [all_mols[i] for i in shards[rank]]
+    # the shards' triplet totals: the straggler bound of the step (every rank waits for the largest)
+    shard_t = [int(sum(all_mols[i]["triplet_num"] for i in s)) for s in shards]
     host_batch, n_local, _ = collate_shard(all_mols, world, rank)
     batch = host_batch.to(dev)
     # the per-batch host cost a data loader has to hide under the step (side fields, not `value`):
@@ -779,6 +785,9 @@ def main():
             "config": {"workload": work,
                        "per_gpu_batch": len(mols), "global_batch": global_batch,
                        "sharding": "one global batch, shard_by_triplets (sum-T balanced)" if world > 1 else None,
+                       "shard_triplets": shard_t if world > 1 else None,
+                       "imbalance_max_over_mean": (round(max(shard_t) / (sum(shard_t) / world), 5)
+                                                   if world > 1 else None),
                        "line_nodes_per_gpu": shape["E"], "triplets_per_gpu": shape["T"],
                        "parallelism": f"dp{world}", "hip_graph": graphed,
                        "grad_allreduce": None if world == 1 else (

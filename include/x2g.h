@@ -108,6 +108,17 @@ int x2g_line_graph_sym_build(const int32_t* edge_src, const int32_t* edge_dst, i
                              int32_t* src_rowptr, int32_t* src_perm, int32_t* src_dst, int32_t* edge_rev,
                              int32_t* rev_trip, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Size metadata of a PyG-style batch from its tensors, on the device (for a Batch made elsewhere, e.g.
+ * by the reference trainer's DataLoader, trainer.py:25-27,37-40, which carries no triplet counts;
+ * xgnn.py:41-52): edge_src / edge_dst (int32 [E]) from edge_index (int64 [2, E], PyG), atom_rowptr
+ * [N+1] of edge_src, mol_triplets[g] (int64 [num_graphs]) = sum over molecule g's edges e = (a->b) of
+ * |N_out(b) \ {a}| (the molecule of e is batch[a]; batch may be NULL: one molecule), and flags (int32
+ * [3]): [0] edges whose reverse is missing (0 = a symmetric edge set), [1] the largest out-degree,
+ * [2] edges out of (src, dst) order, repeated or out of range.  Integer atomics only: exact. */
+int x2g_batch_meta(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes, const int64_t* batch,
+                   int64_t num_graphs, int32_t* edge_src, int32_t* edge_dst, int32_t* atom_rowptr,
+                   int64_t* mol_triplets, int32_t* flags, void* stream);
+
 /* ---------------------------------------------------------------- basis (featurisation) */
 
 /* rbf_env[e, l*R+n] = env(d_e) * N_ln j_l(z_ln d_e/cutoff)   (l < num_spherical, n < R = num_radial)
@@ -263,8 +274,8 @@ int x2g_sbf_attention_fwd_center(const float* q, const float* k, const float* v,
 /* The whole attention backward over a SYMMETRIC line graph in ONE launch, one workgroup per center atom
  * (csrc/attention_center.hip): the block's rows (k + e of its sources, dout and q of its destinations,
  * their softmax max / denominator) staged in LDS, then per source j a pass over its triplets' S rows,
- * alpha and Y (dv, the folded lin_sbf gradient G, the block's (a_t, g_t) tables), rho per destination,
- * and dk, dq from LDS.  Replaces x2g_sbf_attention_bwd_dst_g + x2g_sbf_attention_bwd_src_fold on such
+ * alpha and Y (dv, the folded lin_sbf gradient G, g_t into the g_work [T, heads] scratch), rho per
+ * destination, and dk, dq.  Replaces x2g_sbf_attention_bwd_dst_g + x2g_sbf_attention_bwd_src_fold on such
  * graphs (same dq, dk, dv, radial_grad = G [E, 8, HC]; fp32 rounding apart), reading S once instead of
  * twice and no row gathers; d_edge_atom [num_atoms, HC] (or NULL) = the per-CENTER-ATOM gradient of the
  * edge term (sum over the atom's sources of dk + dv): the element-table gradient is its keyed sum by
@@ -278,7 +289,7 @@ int x2g_sbf_attention_bwd_center(const float* q, const float* k, const float* v,
                                  const float* alpha_raw, const float* seg_max, const float* seg_den, const float* dout,
                                  int64_t num_atoms, int32_t max_degree, int64_t num_edges, int64_t num_triplets,
                                  int32_t heads, int32_t channels, float* dq, float* dk, float* dv, float* radial_grad,
-                                 float* d_edge_atom, void* stream);
+                                 float* d_edge_atom, float* g_work, void* stream);
 
 /* Backward, destination-major: dq[E,HC]; d_edge ([E,HC] per destination for EDGE_PER_DST,
  * [T,HC] for EDGE_PER_TRIPLET); dlogit[T,H] (grad of alpha_raw); d_sbfproj[T,HC] (grad of S_t,

@@ -1995,7 +1995,7 @@ def _bwd_both(lg, q, k, v, S, table, mode, heads, channels, seed):
     call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(lg.src_type) if edge is not None else None,
          mode, ptr(S), ptr(y), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(alpha), ptr(smax), ptr(sden),
          ptr(dout), lg.N, lg.max_degree, E, T, heads, channels, ptr(dq), ptr(dk), ptr(dv), ptr(G), ptr(de_atom),
-         stream_ptr())
+         ptr(torch.empty(T, H, **f)), stream_ptr())
     c = [dq, dk, dv, G]
     if edge is not None:
         c.append(torch.zeros(rows, D, dtype=torch.float64, device=q.device).index_add_(0, lg.atom_type.long(), de_atom.double()))
@@ -2049,9 +2049,9 @@ def test_center_backward_equals_fold_passes(cuda, heads, channels):
 
 
 def test_center_backward_edge_cases(cuda):
-    """Degree-1 and isolated atoms (zero rows), a hub of degree 24 (LDS tables of 24 x 24 x heads: a
-    111 KB image, above the 64 KB default), a triangle; vs the fold passes.  A degree whose image exceeds
-    the 160 KB of LDS is refused (X2G_EUNSUPPORTED: the host then takes the fold passes)."""
+    """Degree-1 and isolated atoms (zero rows), a hub of degree 24, a triangle; vs the fold passes.  A
+    degree above X2G_CENTER_MAX_DEGREE is refused (X2G_EUNSUPPORTED: the host then takes the fold
+    passes)."""
     from x2gnn import ops
 
     pairs = [(0, 1), (1, 2)] + [(4, 5 + i) for i in range(24)] + [(29, 30), (30, 31), (29, 31)]
@@ -2067,8 +2067,8 @@ def test_center_backward_edge_cases(cuda):
     _close_bwd(c, r)
     from x2gnn import _lib
 
-    assert int(_lib.load().x2g_sbf_attention_bwd_center_lds(40, 16)) > 160 * 1024
+    assert int(_lib.load().x2g_sbf_attention_bwd_center_lds(130, 16)) > 160 * 1024 or 130 > ops.CENTER_MAX_DEGREE
     rc = _lib.load().x2g_sbf_attention_bwd_center(None, None, None, None, None, 0, None, None, None, None, None, None,
-                                                   None, None, None, 1, 40, 1, 1, 16, 8, None, None, None, None, None,
-                                                   None)
+                                                   None, None, None, 1, 130, 1, 1, 16, 8, None, None, None, None, None,
+                                                   None, None)
     assert rc == 1002  # X2G_EUNSUPPORTED

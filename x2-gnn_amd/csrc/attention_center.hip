@@ -190,15 +190,17 @@ int fwd_center_launch(const FwdCenterArgs& a, bool edge, int max_degree, hipStre
 // (attention_fold.inc) over b's triplet block, from LDS images of the block's rows:
 //   KE[j] = k_j + e, GO[i] = dout[d_i], QI[i] = q[d_i], per-destination max / 1 / (den + eps);
 // pass 1, one owner per SOURCE j (its S rows t(i, j) = TB[i] + j - [j > i], one 512-byte row each):
-//   at = exp(alpha_t - max_i) / (den_i + eps),  g = sum over the head of go_i (v_j + e) S_t,
+//   at = exp(alpha_t - max_i) / (den_i + eps),  g_t = sum over the head of go_i (v_j + e) S_t,
 //   dv_j += at go_i S_t,  G_j[l] += at go_i (v_j + e) Y_l(t)  (the folded lin_sbf gradient),
-//   and (at, g) into the block's [i][j][head] tables;
-// then rho_i = sum_j at g (j ascending: the destination pass's order), and pass 2 from LDS alone:
+//   g_t into a [T, H] scratch (L2-resident until the same workgroup reads it back);
+// then rho_i = sum_j at g (j ascending: the destination pass's order) over destination i's contiguous
+// block, and pass 2 (at recomputed from alpha, g from the scratch, rows from LDS):
 //   w = at (g - rho_i) / sqrt(C),  dk_j = sum_i w q_i (owner j),  dq_i = sum_j w (k_j + e) (owner i),
 // and, for the element-table gradient, d_edge[b] = sum_j (dk_j + dv_j) (X2-GNN's edge term enters as
-// k_j + e and v_j + e with e the center atom's row: its gradient is the block's sum).  S, alpha and Y
-// are read once per backward (the two destination-major passes read S twice and gather k / v / q /
-// dout rows per triplet from L2); no g, prob or rho tensors leave the kernel.
+// k_j + e and v_j + e with e the center atom's row: its gradient is the block's sum).  S and Y are read
+// once per backward (the two destination-major passes read S twice and gather k / v / q / dout rows per
+// triplet from L2).  LDS holds only the block's rows (3 n x 512 B + n x 200 B), so at config 2's
+// largest degree (17) four workgroups share a CU.
 struct BwdCenterArgs {
   const float *q, *k, *v, *edge;
   const int32_t* src_row;
@@ -207,15 +209,14 @@ struct BwdCenterArgs {
   int64_t n_atoms, T;
   int H;
   float inv_sqrt_c;
-  float *dq, *dk, *dv, *gfold, *d_edge;
+  float *dq, *dk, *dv, *gfold, *d_edge, *gw;
 };
 
 template <int H>
 __host__ __device__ constexpr size_t bwd_center_lds(int n) {
-  return static_cast<size_t>(n) * 3 * kCD * 4           // KE, GO, QI
-         + static_cast<size_t>(n) * n * H * 4 * 2        // AT, GT
-         + static_cast<size_t>(n) * H * 4 * 3            // MX, IV, RHO
-         + static_cast<size_t>(n) * 4 * 2;               // TB, DI
+  return static_cast<size_t>(n) * 3 * kCD * 4  // KE, GO, QI
+         + static_cast<size_t>(n) * H * 4 * 3  // MX, IV, RHO
+         + static_cast<size_t>(n) * 4 * 2;     // TB, DI
 }
 
 template <int LPH, int WAVES, int B, bool EDGE>
@@ -239,9 +240,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
   cf4* KE = lds;
   cf4* GO = KE + n * 32;
   cf4* QI = GO + n * 32;
-  float* AT = reinterpret_cast<float*>(QI + n * 32);
-  float* GT = AT + n * n * H;
-  float* MX = GT + n * n * H;
+  float* MX = reinterpret_cast<float*>(QI + n * 32);
   float* IV = MX + n * H;
   float* RHO = IV + n * H;
   int* TB = reinterpret_cast<int*>(RHO + n * H);
@@ -276,6 +275,10 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
   const __amdgpu_buffer_rsrc_t sp_r = rsrc(a.sp, a.T * kCD * 4);
   const __amdgpu_buffer_rsrc_t al_r = rsrc(a.alpha, a.T * H * 4);
   const __amdgpu_buffer_rsrc_t y_r = rsrc(a.y, a.T * 8 * 4);
+  const __amdgpu_buffer_rsrc_t g_r = rsrc(a.gw, a.T * H * 4);
+  auto ldf = [](__amdgpu_buffer_rsrc_t r, int off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+  };
   for (int j = owner; j < n; j += NO) {
     const int64_t srow = static_cast<int64_t>(r0 + j) * kCD + c0;
     cf4 ue = ld4(a.v + srow);
@@ -288,17 +291,19 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
       constexpr int BB = decltype(bb)::value;
       cf4 sv[BB];
       float al[BB], yv[BB];
+      int tt[BB];
 #pragma unroll
       for (int u = 0; u < BB; ++u) {
         const int i = i0 + u < n ? i0 + u : n - 1;  // clamped: loads unconditional, masked below
         int pos = j - (j > i ? 1 : 0);               // (i == j: some row of i's block, unused)
         pos = pos < nt ? pos : nt - 1;
         const int t = TB[i] + pos;                   // (32-bit buffer offsets: T * 512 < 2^31, checked)
+        tt[u] = t;
         sv[u] = __builtin_bit_cast(cf4, __builtin_amdgcn_raw_buffer_load_b128(sp_r, t * (kCD * 4) + c0 * 4, 0, 0));
-        al[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(al_r, (t * H + head) * 4, 0, 0));
-        yv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(y_r, (t * 8 + (l32 & 7)) * 4, 0, 0));
+        al[u] = ldf(al_r, (t * H + head) * 4);
+        yv[u] = ldf(y_r, (t * 8 + (l32 & 7)) * 4);
       }
-      // per triplet: at, g, the tables, dv; sv[u] becomes dS / S-free: go (v + e) at
+      // per triplet: at, g (to the scratch), dv; sv[u] becomes dS = go (v + e) at
 #pragma unroll
       for (int u = 0; u < BB; ++u) {
         const int i = i0 + u < n ? i0 + u : n - 1;
@@ -311,10 +316,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
         gp = fmaf(gu[2], sv[u][2], gp);
         gp = fmaf(gu[3], sv[u][3], gp);
         const float g = head_sum<LPH>(gp);
-        if (ok && leader) {
-          AT[(i * n + j) * H + head] = at;
-          GT[(i * n + j) * H + head] = g;
-        }
+        if (ok && leader) a.gw[static_cast<int64_t>(tt[u]) * H + head] = g;
         dv += at * (go * sv[u]);
         sv[u] = gu * at;
         __builtin_amdgcn_sched_barrier(0);
@@ -347,26 +349,54 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
 #pragma unroll
     for (int l = 0; l < 8; ++l) st4(gf + l * kCD, G[l]);
   }
+  // the g scratch written by every owner is read by others below: workgroup-scope release / acquire
+  __threadfence_block();
   __syncthreads();
-  // ---- rho_i = sum_{j != i} at g, j ascending (one owner per destination)
+  // at of triplet t for destination i (recomputed, as pass 1 did) and g_t, from global (L2) in batches
+  auto atg = [&](int i, int t, float& at, float& g) {
+    at = expf(ldf(al_r, (t * H + head) * 4) - MX[i * H + head]) * IV[i * H + head];
+    g = ldf(g_r, (t * H + head) * 4);
+  };
+  // ---- rho_i = sum_{j != i} at g over i's contiguous block, j ascending (one owner per destination)
   for (int i = owner; i < n; i += NO) {
     float rho = 0.f;
-    for (int j = 0; j < n; ++j)
-      if (j != i) rho = fmaf(AT[(i * n + j) * H + head], GT[(i * n + j) * H + head], rho);
+    for (int p0 = 0; p0 < nt; p0 += 8) {
+      float at[8], g[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) atg(i, TB[i] + (p0 + u < nt ? p0 + u : nt - 1), at[u], g[u]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (p0 + u < nt) rho = fmaf(at[u], g[u], rho);
+    }
     if (leader) RHO[i * H + head] = rho;
   }
   __syncthreads();
-  // ---- pass 2: dk_j (owner of source j), dq_i (owner of destination i), from LDS
+  // ---- pass 2: dk_j (owner of source j), dq_i (owner of destination i); x over the other n - 1
   for (int o = owner; o < n; o += NO) {
     cf4 dk = {0.f, 0.f, 0.f, 0.f}, dq = {0.f, 0.f, 0.f, 0.f};
-    for (int x = 0; x < n; ++x) {
-      if (x == o) continue;
-      // source role j = o over destinations i = x
-      const float ws = AT[(x * n + o) * H + head] * (GT[(x * n + o) * H + head] - RHO[x * H + head]) * a.inv_sqrt_c;
-      dk += ws * QI[x * 32 + l32];
-      // destination role i = o over sources j = x
-      const float wd = AT[(o * n + x) * H + head] * (GT[(o * n + x) * H + head] - RHO[o * H + head]) * a.inv_sqrt_c;
-      dq += wd * KE[x * 32 + l32];
+    const float rho_o = RHO[o * H + head];
+    for (int x0 = 0; x0 < n; x0 += 8) {
+      float ats[8], gs[8], atd[8], gd[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int x = x0 + u < n ? x0 + u : n - 1;
+        // source role (j = o, i = x): triplet TB[x] + o - [o > x]; destination role (i = o, j = x)
+        int ps = o - (o > x ? 1 : 0), pd = x - (x > o ? 1 : 0);
+        ps = ps < nt ? ps : nt - 1;
+        pd = pd < nt ? pd : nt - 1;
+        atg(x, TB[x] + ps, ats[u], gs[u]);
+        atg(o, TB[o] + pd, atd[u], gd[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int x = x0 + u;
+        if (x >= n) break;  // (workgroup-uniform)
+        if (x == o) continue;
+        const float ws = ats[u] * (gs[u] - RHO[x * H + head]) * a.inv_sqrt_c;
+        dk += ws * QI[x * 32 + l32];
+        const float wd = atd[u] * (gd[u] - rho_o) * a.inv_sqrt_c;
+        dq += wd * KE[x * 32 + l32];
+      }
     }
     st4(a.dk + static_cast<int64_t>(r0 + o) * kCD + c0, dk);
     st4(a.dq + static_cast<int64_t>(DI[o]) * kCD + c0, dq);
@@ -386,7 +416,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
 
 template <int LPH>
 int bwd_center_launch(const BwdCenterArgs& a, bool edge, int max_degree, hipStream_t st) {
-  constexpr int W = 4, B = 8;
+  constexpr int W = 4, B = 4;
   constexpr int H = 32 / LPH;
   const size_t lds = bwd_center_lds<H>(max_degree);
   if (lds > 160 * 1024) return X2G_EUNSUPPORTED;
@@ -411,8 +441,7 @@ using namespace x2g;
 X2G_API size_t x2g_sbf_attention_bwd_center_lds(int32_t max_degree, int32_t heads) {
   if (max_degree < 0 || heads <= 0) return 0;
   const int n = max_degree > 0 ? max_degree : 1;
-  return static_cast<size_t>(n) * 3 * kCD * 4 + static_cast<size_t>(n) * n * heads * 8 +
-         static_cast<size_t>(n) * heads * 12 + static_cast<size_t>(n) * 8;
+  return static_cast<size_t>(n) * 3 * kCD * 4 + static_cast<size_t>(n) * heads * 12 + static_cast<size_t>(n) * 8;
 }
 
 X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const float* v, const float* edge,
@@ -422,7 +451,7 @@ X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const f
                                          const float* seg_den, const float* dout, int64_t num_atoms,
                                          int32_t max_degree, int64_t num_edges, int64_t num_triplets, int32_t heads,
                                          int32_t channels, float* dq, float* dk, float* dv, float* radial_grad,
-                                         float* d_edge_atom, void* stream) {
+                                         float* d_edge_atom, float* g_work, void* stream) {
   if (num_atoms < 0 || num_edges < 0 || num_triplets < 0 || heads <= 0 || channels <= 0) return X2G_EINVAL;
   if (edge_mode != X2G_EDGE_NONE && edge_mode != X2G_EDGE_PER_DST) return X2G_EUNSUPPORTED;
   if (heads * channels != kCD || channels % 4 || max_degree < 0 || max_degree > X2G_CENTER_MAX_DEGREE)
@@ -431,7 +460,8 @@ X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const f
   if (num_triplets * kCD * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;  // 32-bit S offsets
   if (num_atoms == 0) return X2G_OK;
   if (num_edges > 0 && (!q || !k || !v || !sbfproj || !sph_y || !atom_rowptr || !edge_rev || !rev_trip ||
-                        !alpha_raw || !seg_max || !seg_den || !dout || !dq || !dk || !dv || !radial_grad))
+                        !alpha_raw || !seg_max || !seg_den || !dout || !dq || !dk || !dv || !radial_grad ||
+                        (num_triplets > 0 && !g_work)))
     return X2G_EINVAL;
   if (!atom_rowptr) return X2G_EINVAL;
   if (edge_mode == X2G_EDGE_PER_DST && (!edge || !src_row)) return X2G_EINVAL;
@@ -444,7 +474,7 @@ X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const f
   a.smax = seg_max; a.sden = seg_den; a.dout = dout; a.y = sph_y; a.atom_rowptr = atom_rowptr; a.edge_rev = edge_rev;
   a.rev_trip = rev_trip; a.n_atoms = num_atoms; a.T = num_triplets; a.H = heads;
   a.inv_sqrt_c = static_cast<float>(1.0 / sqrt(static_cast<double>(channels)));
-  a.dq = dq; a.dk = dk; a.dv = dv; a.gfold = radial_grad; a.d_edge = d_edge_atom;
+  a.dq = dq; a.dk = dk; a.dv = dv; a.gfold = radial_grad; a.d_edge = d_edge_atom; a.gw = g_work;
   const int md = max_degree > 0 ? max_degree : 1;
   const bool edge_on = edge_mode == X2G_EDGE_PER_DST;
   hipStream_t st = as_stream(stream);

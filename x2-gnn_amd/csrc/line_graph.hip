@@ -445,9 +445,72 @@ __global__ void emit_transpose_sym_kernel(const int32_t* __restrict__ src, const
   transpose_group(src, dst, atom_rowptr, trip_rowptr, src_rowptr, E, src_perm, src_dst);
 }
 
+// ----------------------------------------------------------------------------- batch metadata
+// A PyG-style batch made elsewhere (the drop-in's real caller, trainer.py:37-40: a DataLoader Batch of
+// xgnn.py:41-52's keys) carries no per-molecule triplet counts.  They come from the device: int32 copies
+// of edge_index (int64, PyG), then per edge e = (a->b) its triplet count deg(b) - [b->a exists] (the
+// reverse found by binary search in b's sorted out-list) summed into its molecule batch[a] (integer
+// atomics: exact, order-independent), and flags: [0] edges without a reverse (0 = symmetric), [1] the
+// largest out-degree, [2] edges out of (src, dst) order or repeated (the builders need a sorted simple
+// edge list).
+__global__ void batch_meta_cast(const int64_t* __restrict__ ei, int64_t E, int32_t* __restrict__ src,
+                                int32_t* __restrict__ dst) {
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  src[e] = static_cast<int32_t>(ei[e]);
+  dst[e] = static_cast<int32_t>(ei[E + e]);
+}
+
+__global__ void batch_meta_count(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                                 const int32_t* __restrict__ atom_rowptr, const int64_t* __restrict__ batch,
+                                 int64_t E, int64_t N, int64_t B, unsigned long long* __restrict__ mol_trip,
+                                 int32_t* __restrict__ flags) {
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  const int a = src[e], b = dst[e];
+  if (a < 0 || a >= N || b < 0 || b >= N) {
+    atomicAdd(&flags[2], 1);
+    return;
+  }
+  const int lo = atom_rowptr[b], hi = atom_rowptr[b + 1];
+  const int p = lower_bound(dst, lo, hi, a);
+  const int has_rev = (p < hi && dst[p] == a) ? 1 : 0;
+  if (!has_rev) atomicAdd(&flags[0], 1);
+  if (e > 0) {
+    const int pa = src[e - 1], pb = dst[e - 1];
+    if (pa > a || (pa == a && pb >= b)) atomicAdd(&flags[2], 1);
+  }
+  if (e == atom_rowptr[a]) atomicMax(&flags[1], atom_rowptr[a + 1] - atom_rowptr[a]);
+  const int64_t m = batch ? batch[a] : 0;
+  if (m >= 0 && m < B) atomicAdd(&mol_trip[m], static_cast<unsigned long long>(hi - lo - has_rev));
+}
+
 }  // namespace x2g
 
 using namespace x2g;
+
+X2G_API int x2g_batch_meta(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes, const int64_t* batch,
+                           int64_t num_graphs, int32_t* edge_src, int32_t* edge_dst, int32_t* atom_rowptr,
+                           int64_t* mol_triplets, int32_t* flags, void* stream) {
+  if (num_edges < 0 || num_nodes < 0 || num_graphs < 0 || !atom_rowptr || !flags || (num_graphs > 0 && !mol_triplets))
+    return X2G_EINVAL;
+  if (num_edges > 0 && (!edge_index || !edge_src || !edge_dst)) return X2G_EINVAL;
+  if (num_edges > 0x7fffffff || num_nodes > 0x7fffffff) return X2G_EUNSUPPORTED;
+  hipStream_t st = as_stream(stream);
+  hipError_t he = hipMemsetAsync(flags, 0, 3 * sizeof(int32_t), st);
+  if (he == hipSuccess && num_graphs > 0) he = hipMemsetAsync(mol_triplets, 0, num_graphs * sizeof(int64_t), st);
+  if (he != hipSuccess) return static_cast<int>(he);
+  if (num_edges > 0) {
+    batch_meta_cast<<<blocks_for(num_edges, 256), 256, 0, st>>>(edge_index, num_edges, edge_src, edge_dst);
+    if (int rc = last_launch_status()) return rc;
+  }
+  if (int rc = x2g_csr_rowptr(edge_src, num_edges, num_nodes, atom_rowptr, stream)) return rc;
+  if (num_edges > 0)
+    batch_meta_count<<<blocks_for(num_edges, 256), 256, 0, st>>>(
+        edge_src, edge_dst, atom_rowptr, batch, num_edges, num_nodes, num_graphs,
+        reinterpret_cast<unsigned long long*>(mol_triplets), flags);
+  return last_launch_status();
+}
 
 X2G_API int x2g_abi_version(void) { return 14; }
 

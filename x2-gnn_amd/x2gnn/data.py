@@ -77,8 +77,12 @@ class Data:
 
 def _meta_from_tensors(data):
     """Host size metadata of a batch built without it (a Data made elsewhere, or a foreign PyG-style
-    Batch): per-molecule atoms / edges / triplets and whether the directed edge set is symmetric,
-    derived from the tensors (one device->host copy of edge_index and the small count vectors)."""
+    Batch): per-molecule atoms / edges / triplets, whether the directed edge set is symmetric, and the
+    largest out-degree.  On the device (x2g_batch_meta: one pass over the edges, then ONE small
+    device->host copy of the per-molecule vectors; the reference itself copies edge_index to the host,
+    xgnn.py:52); a batch on the host is counted with numpy."""
+    if data.edge_index.is_cuda:
+        return _meta_on_device(data)
     ei = data.edge_index.detach().cpu().numpy()
     n = int(data.x.shape[0])
     if "ptr" in data._store:
@@ -98,6 +102,44 @@ def _meta_from_tensors(data):
         a0 += nodes[m]
     return {"nodes": nodes.astype(np.int64), "edges": edges, "triplets": np.array(trips, dtype=np.int64),
             "symmetric": _is_symmetric(ei, n), "max_degree": int(np.bincount(ei[0]).max()) if ei.shape[1] else 0}
+
+
+def _meta_on_device(data):
+    from . import _lib
+    from ._lib import call, ptr, stream_ptr
+
+    ei = data.edge_index
+    if ei.dtype != torch.int64:
+        ei = ei.to(torch.int64)
+    ei = ei.contiguous()
+    dev = ei.device
+    E, n = int(ei.shape[1]), int(data.x.shape[0])
+    st = data._store
+    batch = st["batch"].to(torch.int64).contiguous() if "batch" in st else None
+    B = int(data.num_graphs) if batch is not None else 1
+    i32 = dict(dtype=torch.int32, device=dev)
+    src, dst, rowptr = torch.empty(E, **i32), torch.empty(E, **i32), torch.empty(n + 1, **i32)
+    trips = torch.empty(B, dtype=torch.int64, device=dev)
+    flags = torch.empty(3, **i32)
+    _lib.load()
+    call("x2g_batch_meta", ptr(ei), E, n, ptr(batch), B, ptr(src), ptr(dst), ptr(rowptr), ptr(trips), ptr(flags),
+         stream_ptr())
+    if "ptr" in st:
+        nodes = torch.diff(st["ptr"].to(torch.int64).reshape(-1))
+    else:
+        nodes = torch.full((1,), n, dtype=torch.int64, device=dev)
+    en = data.edge_num
+    edges = (en.reshape(-1).to(device=dev, dtype=torch.int64) if torch.is_tensor(en)
+             else torch.full((1,), int(en), dtype=torch.int64, device=dev))
+    # one device->host copy of everything the plan needs
+    host = torch.cat([nodes, edges, trips, flags.to(torch.int64)]).cpu().numpy()
+    nb, ne = len(nodes), len(edges)
+    fl = host[nb + ne + B:]
+    if fl[2]:
+        raise ValueError("edge_index must list each directed edge once, sorted by (source, destination) "
+                         "(the order the reference's radius graph emits, atom_graph.py:42-45)")
+    return {"nodes": host[:nb], "edges": host[nb:nb + ne], "triplets": host[nb + ne:nb + ne + B],
+            "symmetric": bool(fl[0] == 0), "max_degree": int(fl[1])}
 
 
 class Batch(Data):
