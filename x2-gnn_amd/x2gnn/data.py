@@ -105,6 +105,8 @@ def _meta_from_tensors(data):
 
 
 def _meta_on_device(data):
+    """x2g_batch_meta over a CUDA batch: the metadata dict of ``host_meta`` plus, under "index", the int32
+    index forms GraphPlan reads (the ones collate makes on the host for x2gnn's own batches)."""
     from . import _lib
     from ._lib import call, ptr, stream_ptr
 
@@ -113,33 +115,33 @@ def _meta_on_device(data):
         ei = ei.to(torch.int64)
     ei = ei.contiguous()
     dev = ei.device
-    E, n = int(ei.shape[1]), int(data.x.shape[0])
+    x = data.x.reshape(-1)
+    x = (x if x.dtype == torch.int64 else x.to(torch.int64)).contiguous()
+    E, n = int(ei.shape[1]), int(x.shape[0])
     st = data._store
     batch = st["batch"].to(torch.int64).contiguous() if "batch" in st else None
     B = int(data.num_graphs) if batch is not None else 1
     i32 = dict(dtype=torch.int32, device=dev)
-    src, dst, rowptr = torch.empty(E, **i32), torch.empty(E, **i32), torch.empty(n + 1, **i32)
+    src, dst, src_t, dst_t = (torch.empty(E, **i32) for _ in range(4))
+    atom_t, rowptr = torch.empty(n, **i32), torch.empty(n + 1, **i32)
+    line_ptr, mol_ptr = torch.empty(B + 1, **i32), torch.empty(B + 1, **i32)
     trips = torch.empty(B, dtype=torch.int64, device=dev)
     flags = torch.empty(3, **i32)
     _lib.load()
-    call("x2g_batch_meta", ptr(ei), E, n, ptr(batch), B, ptr(src), ptr(dst), ptr(rowptr), ptr(trips), ptr(flags),
-         stream_ptr())
-    if "ptr" in st:
-        nodes = torch.diff(st["ptr"].to(torch.int64).reshape(-1))
-    else:
-        nodes = torch.full((1,), n, dtype=torch.int64, device=dev)
-    en = data.edge_num
-    edges = (en.reshape(-1).to(device=dev, dtype=torch.int64) if torch.is_tensor(en)
-             else torch.full((1,), int(en), dtype=torch.int64, device=dev))
-    # one device->host copy of everything the plan needs
-    host = torch.cat([nodes, edges, trips, flags.to(torch.int64)]).cpu().numpy()
-    nb, ne = len(nodes), len(edges)
-    fl = host[nb + ne + B:]
+    call("x2g_batch_meta", ptr(ei), ptr(x), ptr(batch), E, n, B, ptr(src), ptr(dst), ptr(src_t), ptr(dst_t),
+         ptr(atom_t), ptr(line_ptr), ptr(mol_ptr), ptr(rowptr), ptr(trips), ptr(flags), stream_ptr())
+    # one device->host copy of the per-molecule sizes and the flags
+    host = torch.cat([mol_ptr, line_ptr, flags]).to(torch.int64)
+    host = torch.cat([host, trips]).cpu().numpy()
+    mp_, lp, fl, tr = host[:B + 1], host[B + 1:2 * B + 2], host[2 * B + 2:2 * B + 5], host[2 * B + 5:]
     if fl[2]:
         raise ValueError("edge_index must list each directed edge once, sorted by (source, destination) "
                          "(the order the reference's radius graph emits, atom_graph.py:42-45)")
-    return {"nodes": host[:nb], "edges": host[nb:nb + ne], "triplets": host[nb + ne:nb + ne + B],
-            "symmetric": bool(fl[0] == 0), "max_degree": int(fl[1])}
+    index = {"_x2g_edge_src": src, "_x2g_edge_dst": dst, "_x2g_src_type": src_t, "_x2g_dst_type": dst_t,
+             "_x2g_atom_type": atom_t, "_x2g_line_ptr": line_ptr, "_x2g_mol_ptr": mol_ptr,
+             "_x2g_symmetric": bool(fl[0] == 0), "_x2g_max_degree": int(fl[1])}
+    return {"nodes": np.diff(mp_), "edges": np.diff(lp), "triplets": tr, "symmetric": bool(fl[0] == 0),
+            "max_degree": int(fl[1]), "index": index}
 
 
 class Batch(Data):

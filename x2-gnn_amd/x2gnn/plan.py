@@ -62,8 +62,9 @@ class GraphPlan:
         p.out_graphs = int(nz[-1]) + 1 if len(nz) else 0
         ei = data.edge_index
         dev = ei.device
-        st = data._store
-        if "_x2g_edge_src" in st and st["_x2g_edge_src"].device == dev:  # int32 forms (collate)
+        # the int32 index forms: collate's (x2gnn's own batches) or x2g_batch_meta's (a foreign batch)
+        st = meta.get("index") or data._store
+        if "_x2g_edge_src" in st and st["_x2g_edge_src"].device == dev:
             p.lg = ops.LineGraph(st["_x2g_edge_src"], st["_x2g_edge_dst"], p.num_atoms, p.num_triplets,
                                  st.get("_x2g_symmetric", False))
             p.line_ptr, p.mol_ptr, p.dst_type = st["_x2g_line_ptr"], st["_x2g_mol_ptr"], st["_x2g_dst_type"]
