@@ -113,15 +113,16 @@ int x2g_line_graph_sym_build(const int32_t* edge_src, const int32_t* edge_dst, i
  * triplet counts; xgnn.py:41-52), in one pass and no host loop: from edge_index (int64 [2, E], PyG), x
  * (int64 [N], atomic numbers) and batch (int64 [N], the molecule of each atom; NULL = one molecule):
  * edge_src / edge_dst (int32 [E]), their elements src_type / dst_type (int32 [E]), atom_type (int32 [N]),
- * the molecules' edge and atom row pointers line_ptr / mol_ptr (int32 [num_graphs + 1]), atom_rowptr
- * [N+1] of edge_src, mol_triplets[g] (int64 [num_graphs]) = sum over molecule g's edges e = (a->b) of
- * |N_out(b) \ {a}|, and flags (int32 [3]): [0] edges whose reverse is missing (0 = a symmetric edge
- * set), [1] the largest out-degree, [2] edges out of (src, dst) order, repeated or out of range.
- * Integer atomics only: exact. */
+ * the molecules' atom and edge row pointers mol_ptr / line_ptr (int32 [num_graphs + 1]), atom_rowptr
+ * [N+1] of edge_src, and everything the host needs in one int64 block (one copy back):
+ * info = [mol_ptr (B+1) | line_ptr (B+1) | triplets (B) | flags (3)], B = num_graphs, where triplets[g] =
+ * sum over molecule g's edges e = (a->b) of |N_out(b) \ {a}| and flags = [edges whose reverse is missing
+ * (0 = a symmetric edge set), the largest out-degree, edges out of (src, dst) order / repeated / out of
+ * range].  Integer atomics only: exact. */
 int x2g_batch_meta(const int64_t* edge_index, const int64_t* x, const int64_t* batch, int64_t num_edges,
                    int64_t num_nodes, int64_t num_graphs, int32_t* edge_src, int32_t* edge_dst, int32_t* src_type,
                    int32_t* dst_type, int32_t* atom_type, int32_t* line_ptr, int32_t* mol_ptr, int32_t* atom_rowptr,
-                   int64_t* mol_triplets, int32_t* flags, void* stream);
+                   int64_t* info, void* stream);
 
 /* ---------------------------------------------------------------- basis (featurisation) */
 

@@ -448,30 +448,52 @@ __global__ void emit_transpose_sym_kernel(const int32_t* __restrict__ src, const
 // ----------------------------------------------------------------------------- batch metadata
 // A PyG-style batch made elsewhere (the drop-in's real caller, trainer.py:37-40: a DataLoader Batch of
 // xgnn.py:41-52's keys) carries neither per-molecule triplet counts nor x2gnn's int32 index forms.  Both
-// come from the device in one pass: per edge e = (a->b) the int32 endpoints, the endpoint elements, its
-// triplet count deg(b) - [b->a exists] (the reverse found by binary search in b's sorted out-list) summed
-// into its molecule batch[a] (integer atomics: exact, order-independent); per atom its element; the
-// molecule row pointers of the atoms and of the edges (CSR of batch[] and of batch[src[]], by the row
-// pointer rule of rowptr_kernel); and flags: [0] edges without a reverse (0 = symmetric), [1] the largest
-// out-degree, [2] edges out of (src, dst) order, repeated or out of range (the builders need a sorted
-// simple edge list).
+// come from the device in one pass: per atom its element and the molecules' atom row pointer (CSR of
+// batch[], the rowptr_kernel rule); per edge e = (a->b) the int32 endpoints, their elements and the
+// molecules' edge row pointer (CSR of batch[src[]]); then per edge its triplet count deg(b) - [b->a
+// exists] (the reverse found by binary search in b's sorted out-list) summed into its molecule batch[a]
+// (integer atomics: exact, order-independent).  Everything the host needs lands in one int64 block
+// info = [mol_ptr (B+1) | line_ptr (B+1) | triplets (B) | flags (3)], read back with one copy; flags:
+// [0] edges without a reverse (0 = symmetric), [1] the largest out-degree, [2] edges out of (src, dst)
+// order, repeated or out of range (the builders need a sorted simple edge list).
 __device__ __forceinline__ void ptr_fill(int64_t prev, int64_t cur, int64_t n_seg, int32_t val,
-                                         int32_t* __restrict__ rowptr) {
+                                         int32_t* __restrict__ rowptr, int64_t* __restrict__ rowptr64) {
   if (prev < -1) prev = -1;
   if (cur > n_seg) cur = n_seg;
-  for (int64_t s = prev + 1; s <= cur; ++s) rowptr[s] = val;
+  for (int64_t s = prev + 1; s <= cur; ++s) {
+    rowptr[s] = val;
+    rowptr64[s] = val;
+  }
+}
+
+// (launched first: also zeroes the triplet counts and flags the later kernels add into)
+__global__ void batch_meta_atoms(const int64_t* __restrict__ x, const int64_t* __restrict__ batch, int64_t N,
+                                 int64_t B, int32_t* __restrict__ atom_type, int32_t* __restrict__ mol_ptr,
+                                 int64_t* __restrict__ info) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < B + 3) info[2 * (B + 1) + i] = 0;
+  if (i > N) return;
+  auto mol_of = [&](int64_t a) -> int64_t { return batch ? batch[a] : 0; };
+  if (i == N) {
+    ptr_fill(N > 0 ? mol_of(N - 1) : -1, B, B, static_cast<int32_t>(N), mol_ptr, info);
+    return;
+  }
+  atom_type[i] = static_cast<int32_t>(x[i]);
+  ptr_fill(i > 0 ? mol_of(i - 1) : -1, mol_of(i), B, static_cast<int32_t>(i), mol_ptr, info);
 }
 
 __global__ void batch_meta_edges(const int64_t* __restrict__ ei, const int64_t* __restrict__ x,
                                  const int64_t* __restrict__ batch, int64_t E, int64_t N, int64_t B,
                                  int32_t* __restrict__ src, int32_t* __restrict__ dst, int32_t* __restrict__ src_type,
                                  int32_t* __restrict__ dst_type, int32_t* __restrict__ line_ptr,
-                                 int32_t* __restrict__ flags) {
+                                 int64_t* __restrict__ info) {
   const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (e > E) return;
+  unsigned long long* flags = reinterpret_cast<unsigned long long*>(info + 3 * B + 2);
+  int64_t* lp64 = info + (B + 1);
   auto mol_of = [&](int64_t a) -> int64_t { return (batch && a >= 0 && a < N) ? batch[a] : 0; };
   if (e == E) {  // the edge row pointer's tail
-    ptr_fill(E > 0 ? mol_of(ei[E - 1]) : -1, B, B, static_cast<int32_t>(E), line_ptr);
+    ptr_fill(E > 0 ? mol_of(ei[E - 1]) : -1, B, B, static_cast<int32_t>(E), line_ptr, lp64);
     return;
   }
   const int64_t a = ei[e], b = ei[E + e];
@@ -480,42 +502,30 @@ __global__ void batch_meta_edges(const int64_t* __restrict__ ei, const int64_t* 
   const bool ok = a >= 0 && a < N && b >= 0 && b < N;
   src_type[e] = ok ? static_cast<int32_t>(x[a]) : 0;
   dst_type[e] = ok ? static_cast<int32_t>(x[b]) : 0;
-  if (!ok) atomicAdd(&flags[2], 1);
+  if (!ok) atomicAdd(&flags[2], 1ull);
   if (e > 0) {
     const int64_t pa = ei[e - 1], pb = ei[E + e - 1];
-    if (pa > a || (pa == a && pb >= b)) atomicAdd(&flags[2], 1);
+    if (pa > a || (pa == a && pb >= b)) atomicAdd(&flags[2], 1ull);
   }
-  ptr_fill(e > 0 ? mol_of(ei[e - 1]) : -1, mol_of(a), B, static_cast<int32_t>(e), line_ptr);
-}
-
-__global__ void batch_meta_atoms(const int64_t* __restrict__ x, const int64_t* __restrict__ batch, int64_t N,
-                                 int64_t B, int32_t* __restrict__ atom_type, int32_t* __restrict__ mol_ptr) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i > N) return;
-  auto mol_of = [&](int64_t a) -> int64_t { return batch ? batch[a] : 0; };
-  if (i == N) {
-    ptr_fill(N > 0 ? mol_of(N - 1) : -1, B, B, static_cast<int32_t>(N), mol_ptr);
-    return;
-  }
-  atom_type[i] = static_cast<int32_t>(x[i]);
-  ptr_fill(i > 0 ? mol_of(i - 1) : -1, mol_of(i), B, static_cast<int32_t>(i), mol_ptr);
+  ptr_fill(e > 0 ? mol_of(ei[e - 1]) : -1, mol_of(a), B, static_cast<int32_t>(e), line_ptr, lp64);
 }
 
 __global__ void batch_meta_count(const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
                                  const int32_t* __restrict__ atom_rowptr, const int64_t* __restrict__ batch,
-                                 int64_t E, int64_t N, int64_t B, unsigned long long* __restrict__ mol_trip,
-                                 int32_t* __restrict__ flags) {
+                                 int64_t E, int64_t N, int64_t B, int64_t* __restrict__ info) {
   const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (e >= E) return;
+  unsigned long long* trips = reinterpret_cast<unsigned long long*>(info + 2 * (B + 1));
+  unsigned long long* flags = trips + B;
   const int a = src[e], b = dst[e];
   if (a < 0 || a >= N || b < 0 || b >= N) return;  // (flagged by batch_meta_edges)
   const int lo = atom_rowptr[b], hi = atom_rowptr[b + 1];
   const int p = lower_bound(dst, lo, hi, a);
   const int has_rev = (p < hi && dst[p] == a) ? 1 : 0;
-  if (!has_rev) atomicAdd(&flags[0], 1);
-  if (e == atom_rowptr[a]) atomicMax(&flags[1], atom_rowptr[a + 1] - atom_rowptr[a]);
+  if (!has_rev) atomicAdd(&flags[0], 1ull);
+  if (e == atom_rowptr[a]) atomicMax(&flags[1], static_cast<unsigned long long>(atom_rowptr[a + 1] - atom_rowptr[a]));
   const int64_t m = batch ? batch[a] : 0;
-  if (m >= 0 && m < B) atomicAdd(&mol_trip[m], static_cast<unsigned long long>(hi - lo - has_rev));
+  if (m >= 0 && m < B) atomicAdd(&trips[m], static_cast<unsigned long long>(hi - lo - has_rev));
 }
 
 }  // namespace x2g
@@ -525,29 +535,24 @@ using namespace x2g;
 X2G_API int x2g_batch_meta(const int64_t* edge_index, const int64_t* x, const int64_t* batch, int64_t num_edges,
                            int64_t num_nodes, int64_t num_graphs, int32_t* edge_src, int32_t* edge_dst,
                            int32_t* src_type, int32_t* dst_type, int32_t* atom_type, int32_t* line_ptr,
-                           int32_t* mol_ptr, int32_t* atom_rowptr, int64_t* mol_triplets, int32_t* flags,
-                           void* stream) {
-  if (num_edges < 0 || num_nodes < 0 || num_graphs < 0 || !atom_rowptr || !flags || !line_ptr || !mol_ptr ||
-      (num_graphs > 0 && !mol_triplets) || (num_nodes > 0 && (!x || !atom_type)))
+                           int32_t* mol_ptr, int32_t* atom_rowptr, int64_t* info, void* stream) {
+  if (num_edges < 0 || num_nodes < 0 || num_graphs < 0 || !atom_rowptr || !info || !line_ptr || !mol_ptr ||
+      (num_nodes > 0 && (!x || !atom_type)))
     return X2G_EINVAL;
   if (num_edges > 0 && (!edge_index || !edge_src || !edge_dst || !src_type || !dst_type)) return X2G_EINVAL;
   if (num_edges > 0x7fffffff || num_nodes > 0x7fffffff) return X2G_EUNSUPPORTED;
   hipStream_t st = as_stream(stream);
-  hipError_t he = hipMemsetAsync(flags, 0, 3 * sizeof(int32_t), st);
-  if (he == hipSuccess && num_graphs > 0) he = hipMemsetAsync(mol_triplets, 0, num_graphs * sizeof(int64_t), st);
-  if (he != hipSuccess) return static_cast<int>(he);
+  const int64_t na = (num_nodes + 1 > num_graphs + 3 ? num_nodes + 1 : num_graphs + 3);
+  batch_meta_atoms<<<blocks_for(na, 256), 256, 0, st>>>(x, batch, num_nodes, num_graphs, atom_type, mol_ptr, info);
+  if (int rc = last_launch_status()) return rc;
   batch_meta_edges<<<blocks_for(num_edges + 1, 256), 256, 0, st>>>(edge_index, x, batch, num_edges, num_nodes,
                                                                    num_graphs, edge_src, edge_dst, src_type, dst_type,
-                                                                   line_ptr, flags);
-  if (int rc = last_launch_status()) return rc;
-  batch_meta_atoms<<<blocks_for(num_nodes + 1, 256), 256, 0, st>>>(x, batch, num_nodes, num_graphs, atom_type,
-                                                                   mol_ptr);
+                                                                   line_ptr, info);
   if (int rc = last_launch_status()) return rc;
   if (int rc = x2g_csr_rowptr(edge_src, num_edges, num_nodes, atom_rowptr, stream)) return rc;
   if (num_edges > 0)
-    batch_meta_count<<<blocks_for(num_edges, 256), 256, 0, st>>>(
-        edge_src, edge_dst, atom_rowptr, batch, num_edges, num_nodes, num_graphs,
-        reinterpret_cast<unsigned long long*>(mol_triplets), flags);
+    batch_meta_count<<<blocks_for(num_edges, 256), 256, 0, st>>>(edge_src, edge_dst, atom_rowptr, batch, num_edges,
+                                                                 num_nodes, num_graphs, info);
   return last_launch_status();
 }
 

@@ -49,7 +49,7 @@ SIGNATURES = {
     "x2g_rbf_gate_fwd": [_P, _P, _P, _P, _I64, _I32, _I32, _P, _P],
     "x2g_rbf_pool_fwd": [_P, _P, _P, _P, _P, _I64, _I32, _I32, _P, _P],
     "x2g_rbf_gate_bwd_workspace": [_I64, _I32, _I32],
-    "x2g_batch_meta": [_P, _P, _P, _I64, _I64, _I64] + [_P] * 10 + [_P],
+    "x2g_batch_meta": [_P, _P, _P, _I64, _I64, _I64] + [_P] * 9 + [_P],
     "x2g_vertex_to_edge_sym": [_P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P],
     "x2g_line_graph_transpose_sym": [_P, _P, _P, _P, _I64, _P, _P, _P, _P, _SZ, _P],
     "x2g_line_graph_sym_build": [_P, _P, _I64, _I64, _I64] + [_P] * 12 + [_P, _SZ, _P],

@@ -125,15 +125,12 @@ def _meta_on_device(data):
     src, dst, src_t, dst_t = (torch.empty(E, **i32) for _ in range(4))
     atom_t, rowptr = torch.empty(n, **i32), torch.empty(n + 1, **i32)
     line_ptr, mol_ptr = torch.empty(B + 1, **i32), torch.empty(B + 1, **i32)
-    trips = torch.empty(B, dtype=torch.int64, device=dev)
-    flags = torch.empty(3, **i32)
+    info = torch.empty(3 * B + 5, dtype=torch.int64, device=dev)
     _lib.load()
     call("x2g_batch_meta", ptr(ei), ptr(x), ptr(batch), E, n, B, ptr(src), ptr(dst), ptr(src_t), ptr(dst_t),
-         ptr(atom_t), ptr(line_ptr), ptr(mol_ptr), ptr(rowptr), ptr(trips), ptr(flags), stream_ptr())
-    # one device->host copy of the per-molecule sizes and the flags
-    host = torch.cat([mol_ptr, line_ptr, flags]).to(torch.int64)
-    host = torch.cat([host, trips]).cpu().numpy()
-    mp_, lp, fl, tr = host[:B + 1], host[B + 1:2 * B + 2], host[2 * B + 2:2 * B + 5], host[2 * B + 5:]
+         ptr(atom_t), ptr(line_ptr), ptr(mol_ptr), ptr(rowptr), ptr(info), stream_ptr())
+    host = info.cpu().numpy()  # the one device->host copy: sizes per molecule and the flags
+    mp_, lp, tr, fl = host[:B + 1], host[B + 1:2 * B + 2], host[2 * B + 2:3 * B + 2], host[3 * B + 2:]
     if fl[2]:
         raise ValueError("edge_index must list each directed edge once, sorted by (source, destination) "
                          "(the order the reference's radius graph emits, atom_graph.py:42-45)")
