@@ -486,12 +486,17 @@ __global__ void batch_meta_edges(const int64_t* __restrict__ ei, const int64_t* 
                                  const int64_t* __restrict__ batch, int64_t E, int64_t N, int64_t B,
                                  int32_t* __restrict__ src, int32_t* __restrict__ dst, int32_t* __restrict__ src_type,
                                  int32_t* __restrict__ dst_type, int32_t* __restrict__ line_ptr,
-                                 int64_t* __restrict__ info) {
+                                 int32_t* __restrict__ atom_rowptr, int64_t* __restrict__ info) {
   const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (e > E) return;
   unsigned long long* flags = reinterpret_cast<unsigned long long*>(info + 3 * B + 2);
   int64_t* lp64 = info + (B + 1);
   auto mol_of = [&](int64_t a) -> int64_t { return (batch && a >= 0 && a < N) ? batch[a] : 0; };
+  // the source-atom row pointer of the edges (rowptr_kernel's rule over src, clamped to [0, N])
+  {
+    const int64_t prev = e > 0 ? ei[e - 1] : -1, cur = e < E ? ei[e] : N;
+    for (int64_t s = (prev < -1 ? -1 : prev) + 1; s <= (cur > N ? N : cur); ++s) atom_rowptr[s] = static_cast<int32_t>(e);
+  }
   if (e == E) {  // the edge row pointer's tail
     ptr_fill(E > 0 ? mol_of(ei[E - 1]) : -1, B, B, static_cast<int32_t>(E), line_ptr, lp64);
     return;
@@ -547,9 +552,8 @@ X2G_API int x2g_batch_meta(const int64_t* edge_index, const int64_t* x, const in
   if (int rc = last_launch_status()) return rc;
   batch_meta_edges<<<blocks_for(num_edges + 1, 256), 256, 0, st>>>(edge_index, x, batch, num_edges, num_nodes,
                                                                    num_graphs, edge_src, edge_dst, src_type, dst_type,
-                                                                   line_ptr, info);
+                                                                   line_ptr, atom_rowptr, info);
   if (int rc = last_launch_status()) return rc;
-  if (int rc = x2g_csr_rowptr(edge_src, num_edges, num_nodes, atom_rowptr, stream)) return rc;
   if (num_edges > 0)
     batch_meta_count<<<blocks_for(num_edges, 256), 256, 0, st>>>(edge_src, edge_dst, atom_rowptr, batch, num_edges,
                                                                  num_nodes, num_graphs, info);

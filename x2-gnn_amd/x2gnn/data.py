@@ -121,10 +121,10 @@ def _meta_on_device(data):
     st = data._store
     batch = st["batch"].to(torch.int64).contiguous() if "batch" in st else None
     B = int(data.num_graphs) if batch is not None else 1
-    i32 = dict(dtype=torch.int32, device=dev)
-    src, dst, src_t, dst_t = (torch.empty(E, **i32) for _ in range(4))
-    atom_t, rowptr = torch.empty(n, **i32), torch.empty(n + 1, **i32)
-    line_ptr, mol_ptr = torch.empty(B + 1, **i32), torch.empty(B + 1, **i32)
+    # every int32 output in one allocation (views), the host block in another
+    buf = torch.empty(4 * E + 2 * n + 1 + 2 * (B + 1), dtype=torch.int32, device=dev)
+    src, dst, src_t, dst_t, atom_t, rowptr, line_ptr, mol_ptr = torch.split(
+        buf, [E, E, E, E, n, n + 1, B + 1, B + 1])
     info = torch.empty(3 * B + 5, dtype=torch.int64, device=dev)
     _lib.load()
     call("x2g_batch_meta", ptr(ei), ptr(x), ptr(batch), E, n, B, ptr(src), ptr(dst), ptr(src_t), ptr(dst_t),
