@@ -203,7 +203,8 @@ int x2g_rbf_gate_bwd(const float* g, const int32_t* owner, const float* x, const
  * (F_B_2D.forward(d, Angles, edge_index_1) signature; pos/atom_* may then be NULL).
  * cos_theta[T] (optional, may be NULL) receives cos(theta).  sph_y[T, 8] (optional, 16-byte
  * aligned) receives Y_0..Y_6 (theta_t) and a 1: the angular factor of sbf, which the factorised
- * lin_sbf backward (x2g_sbf_attention_bwd_src_fold) folds per triplet. */
+ * lin_sbf backward (x2g_sbf_attention_bwd_src_fold) folds per triplet.  sbf may be NULL when sph_y is
+ * given (the factors alone: the center-atom forward rebuilds lin_sbf(sbf) from them). */
 int x2g_spherical_basis(const float* pos, const int32_t* atom_i, const int32_t* atom_j,
                         const int32_t* atom_k, const float* theta, const int32_t* trip_src,
                         const float* rbf_env, int64_t num_triplets, int32_t num_spherical, int32_t num_radial,
@@ -275,6 +276,22 @@ int x2g_sbf_attention_fwd_center(const float* q, const float* k, const float* v,
                                  const int32_t* rev_trip, int64_t atom0, int64_t n_atoms, int32_t max_degree,
                                  int64_t num_edges, int64_t num_triplets, int32_t heads, int32_t channels, float* out,
                                  float* alpha_raw, float* seg_max, float* seg_den, float* row_stats, void* stream);
+
+/* The center-atom forward with lin_sbf fused (no S to read): X2-GNN's sbf row factorises as
+ * sbf[t, 6l+n] = R[s, 6l+n] Y_l(t) (angular_basis_layer.py:87-91; R = rbf_env [E, 42] of the triplet's
+ * source s, Y = sph_y [T, 8] from x2g_spherical_basis), so S_t = b + sum_l Y_l(t) P_s[l] with
+ * P_s[l][c] = sum_n W[c, 6l+n] R[s, 6l+n], formed per source in LDS for each center atom's block
+ * (w_sbf [128, 42], b_sbf [128]).  Outputs as x2g_sbf_attention_fwd_center; sbfproj_out [T, 128] (or
+ * NULL) receives every S_t row for a backward that reads them.  LDS per workgroup 4.5 KB x max_degree
+ * (<= 160 KiB, else X2G_EUNSUPPORTED); no atom0 / t_base tiling is needed (nothing T x 128 is read). */
+int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, const float* v, const float* skip,
+                                    const float* edge, const int32_t* src_row, int edge_mode, const float* radial,
+                                    const float* sph_y, const float* w_sbf, const float* b_sbf,
+                                    const int32_t* atom_rowptr, const int32_t* edge_rev, const int32_t* rev_trip,
+                                    int64_t atom0, int64_t n_atoms, int32_t max_degree, int64_t num_edges,
+                                    int64_t num_triplets, int32_t heads, int32_t channels, float* out,
+                                    float* alpha_raw, float* seg_max, float* seg_den, float* row_stats,
+                                    float* sbfproj_out, void* stream);
 
 /* The whole attention backward over a SYMMETRIC line graph in ONE launch, one workgroup per center atom
  * (csrc/attention_center.hip): the block's rows (k + e of its sources, dout and q of its destinations,

@@ -2072,3 +2072,46 @@ def test_center_backward_edge_cases(cuda):
                                                    None, None, None, 1, 130, 1, 1, 16, 8, None, None, None, None, None,
                                                    None, None)
     assert rc == 1002  # X2G_EUNSUPPORTED
+
+
+def test_center_forward_fused_projection_equals_projected(cuda):
+    """x2g_sbf_attention_fwd_center_sf (S_t = b + sum_l Y_l(t) P_s[l] rebuilt per center atom from the sbf
+    factors, no S read) == x2g_sbf_project + x2g_sbf_attention_fwd_center on a config-2 batch: outputs,
+    logits, softmax statistics, row statistics, and the S rows it stores for the backward; and without the
+    S store (inference) the same outputs.  fp32 reassociation of the 42-term projection: 1e-5."""
+    from x2gnn import ops
+    from x2gnn._lib import call, ptr, stream_ptr
+    from x2gnn.data import collate
+    from x2gnn.synth import synthetic_molecules
+
+    b = collate(synthetic_molecules(128, "S160", seed=13))
+    lg = _sym_lg(b.edge_index.numpy(), b.num_nodes, cuda)
+    E, T, H, C, D = lg.E, lg.T, 16, 8, 128
+    g = torch.Generator(device=cuda).manual_seed(14)
+    q, k, v, skip = (torch.randn(E, D, device=cuda, generator=g) for _ in range(4))
+    table = torch.randn(10, D, device=cuda, generator=g)
+    radial = torch.randn(E, 42, device=cuda, generator=g)
+    y = torch.randn(T, 8, device=cuda, generator=g)
+    y[:, 7] = 1.0
+    sbf = (radial[lg.trip_src.long()].view(T, 7, 6) * y[:, :7, None]).reshape(T, 42).contiguous()
+    W = 0.2 * torch.randn(D, 42, device=cuda, generator=g)
+    bias = 0.1 * torch.randn(D, device=cuda, generator=g)
+    f = dict(device=cuda, dtype=torch.float32)
+    S = torch.empty(T, D, **f)
+    call("x2g_sbf_project", ptr(sbf), T, 42, ptr(W), ptr(bias), D, ptr(S), stream_ptr())
+    ref = [torch.empty(E, D, **f), torch.empty(T, H, **f), torch.empty(E, H, **f), torch.empty(E, H, **f),
+           torch.empty(E, 2, **f)]
+    call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
+         ops.EDGE_PER_DST, ptr(S), 0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), 0, lg.N, lg.max_degree,
+         E, T, H, C, *[ptr(t) for t in ref], stream_ptr())
+    for store in (True, False):
+        got = [torch.full_like(t, float("nan")) for t in ref]
+        S2 = torch.full((T, D), float("nan"), **f) if store else None
+        call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
+             ops.EDGE_PER_DST, ptr(radial), ptr(y), ptr(W), ptr(bias), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
+             ptr(lg.rev_trip), 0, lg.N, lg.max_degree, E, T, H, C, *[ptr(t) for t in got], ptr(S2), stream_ptr())
+        for name, a, r in zip(("out", "alpha", "smax", "sden", "row_stats"), got, ref):
+            assert not torch.isnan(a).any(), name
+            torch.testing.assert_close(a, r, rtol=1e-5, atol=1e-5, msg=name)
+        if store:
+            torch.testing.assert_close(S2, S, rtol=1e-5, atol=1e-5)

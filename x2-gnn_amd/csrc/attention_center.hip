@@ -168,6 +168,204 @@ __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_kernel(const FwdCe
   }
 }
 
+// ------------------------------------------------------------------------------ forward, fused projection
+// The same forward without a materialised S = lin_sbf(sbf) to read: X2-GNN's sbf row is the per-SOURCE
+// radial factor times the per-triplet angular one (angular_basis_layer.py:87-91: sbf[t, 6l+n] =
+// R[s, 6l+n] Y_l(t)), so
+//     S_t[c] = b[c] + sum_l Y_l(t) P_s[l][c],   P_s[l][c] = sum_n W[c][6l+n] R[s, 6l+n],
+// and a center atom's block needs P only for its n sources (7 rows of 128 per source, staged in LDS with
+// k + e and v + e: 4.5 KB per source), then 7 FMAs per channel per triplet from the triplet's 8-float
+// Y row instead of a 512-byte S row.  The separate projection launch (which read sbf [T, 42] and wrote S
+// [T, 128]) and this kernel's S reads disappear; when a backward will need S (training), each triplet's
+// S row is stored as it is formed (the same 512-byte writes the projection made).
+struct FwdSfArgs {
+  const float *q, *k, *v, *skip, *edge;
+  const int32_t* src_row;
+  const float *radial, *y, *w, *bias;  // rbf_env [E, 42], Y [T, 8], lin_sbf weight [128, 42] and bias [128]
+  const int32_t *atom_rowptr, *edge_rev, *rev_trip;
+  int64_t atom0, n_atoms;
+  int H;
+  float sqrt_c;
+  float *out, *alpha, *smax, *sden, *sp;  // sp: S [T, 128] out (NULL: not stored)
+  float2* row_stats;
+};
+
+constexpr int kSfL = 7;                  // angular orders (sbf_dim 42 = 7 x 6)
+constexpr int kSfR = 6;                  // radial functions per order
+constexpr int kSfK = kSfL * kSfR;        // 42
+
+template <int LPH, int WAVES, int B, bool EDGE>
+__global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const FwdSfArgs a) {
+  extern __shared__ cf4 lds[];  // [n][32] (k + e), [n][32] (v + e), [n][7][32] P
+  const int64_t b = a.atom0 + blockIdx.x;
+  const int r0 = uniform(a.atom_rowptr[b]);
+  const int n = uniform(a.atom_rowptr[b + 1]) - r0;
+  if (n <= 0) return;  // (workgroup-uniform)
+  cf4* KE = lds;
+  cf4* VE = lds + n * 32;
+  cf4* P = VE + n * 32;
+  constexpr int NT = 64 * WAVES;
+  const int tid = threadIdx.x;
+  const int l32 = tid & 31, half = (tid >> 5) & 1, wave = tid >> 6;
+  const int owner = 2 * wave + half;
+  const int head = l32 / LPH;
+  const bool leader = (l32 % LPH) == 0;
+  const int c0 = 4 * l32;
+  int i = owner;
+  int d = 0, tb = 0;
+  if (i < n) {
+    d = a.edge_rev[r0 + i];
+    tb = a.rev_trip[r0 + i];
+  }
+  cf4 e4 = {0.f, 0.f, 0.f, 0.f};
+  for (int idx = tid; idx < n * 32; idx += NT) {
+    const int j = idx >> 5, c = idx & 31;
+    if (EDGE) e4 = ld4(a.edge + static_cast<int64_t>(uniform(a.src_row[r0])) * kCD + 4 * c);
+    const int64_t row = static_cast<int64_t>(r0 + j) * kCD + 4 * c;
+    KE[idx] = ld4(a.k + row) + e4;
+    VE[idx] = ld4(a.v + row) + e4;
+  }
+  // P[j][l][c] for the block's sources: thread (group g, order l, channels 4 c4 .. +3) keeps its 4 x 6
+  // weights in registers and walks sources j = g, g + NG, ...
+  {
+    constexpr int NG = NT / 256;  // thread groups of 7 x 32 (the last 32 threads of each 256 idle)
+    const int g = tid / 256, rest = tid % 256;
+    if (rest < kSfL * 32) {
+      const int l = rest >> 5, c4 = rest & 31;
+      float wv[4][kSfR];
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+        for (int r = 0; r < kSfR; ++r) wv[cc][r] = a.w[(4 * c4 + cc) * kSfK + kSfR * l + r];
+      for (int j = g; j < n; j += NG) {
+        const float* rr = a.radial + static_cast<int64_t>(r0 + j) * kSfK + kSfR * l;
+        float rv[kSfR];
+#pragma unroll
+        for (int r = 0; r < kSfR; ++r) rv[r] = rr[r];
+        cf4 p;
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+          float acc = wv[cc][0] * rv[0];
+#pragma unroll
+          for (int r = 1; r < kSfR; ++r) acc = fmaf(wv[cc][r], rv[r], acc);
+          p[cc] = acc;
+        }
+        P[(j * kSfL + l) * 32 + c4] = p;
+      }
+    }
+  }
+  const cf4 bias4 = ld4(a.bias + c0);
+  __syncthreads();
+  const int nt = n - 1;
+  for (; i < n; i += 2 * WAVES) {
+    if (i != owner) {
+      d = a.edge_rev[r0 + i];
+      tb = a.rev_trip[r0 + i];
+    }
+    const int64_t drow = static_cast<int64_t>(d) * kCD + c0;
+    const cf4 qv = ld4(a.q + drow);
+    const cf4 sk = ld4(a.skip + drow);
+    cf4 acc = {0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, den = 0.f;
+    auto batch = [&](int j0, auto bb) {
+      constexpr int BB = decltype(bb)::value;
+      float yv[BB];
+      int tt[BB];
+#pragma unroll
+      for (int u = 0; u < BB; ++u) {
+        const int j = j0 + u;
+        int jj = j - (j > i ? 1 : 0);
+        jj = jj < nt ? jj : nt - 1;  // clamped (nt >= 1 here): every load unconditional
+        tt[u] = tb + jj;
+        yv[u] = a.y[static_cast<int64_t>(tt[u]) * 8 + (l32 & 7)];
+      }
+      cf4 sv[BB];
+      float lg[BB];
+      float mb = -INFINITY;
+#pragma unroll
+      for (int u = 0; u < BB; ++u) {
+        const int j = j0 + u;
+        const bool ok = j < n && j != i;
+        const int jc = j < n ? j : n - 1;
+        // S_t = b + sum_l Y_l(t) P_j[l]: Y_l handed to the half's lanes by row_newbcast (both 16-lane rows
+        // of a half loaded the same triplet's Y row, one value per lane)
+        float yl[kSfL];
+        yl[0] = dpp_mov<0x150>(yv[u]);
+        yl[1] = dpp_mov<0x151>(yv[u]);
+        yl[2] = dpp_mov<0x152>(yv[u]);
+        yl[3] = dpp_mov<0x153>(yv[u]);
+        yl[4] = dpp_mov<0x154>(yv[u]);
+        yl[5] = dpp_mov<0x155>(yv[u]);
+        yl[6] = dpp_mov<0x156>(yv[u]);
+        cf4 s4 = bias4;
+#pragma unroll
+        for (int l = 0; l < kSfL; ++l) s4 += yl[l] * P[(jc * kSfL + l) * 32 + l32];
+        sv[u] = s4;
+        if (a.sp && ok) st4(a.sp + static_cast<int64_t>(tt[u]) * kCD + c0, s4);
+        const cf4 kr = KE[jc * 32 + l32];
+        float dot = qv[0] * kr[0];
+        dot = fmaf(qv[1], kr[1], dot);
+        dot = fmaf(qv[2], kr[2], dot);
+        dot = fmaf(qv[3], kr[3], dot);
+        const float logit = head_sum<LPH>(dot) / a.sqrt_c;
+        lg[u] = ok ? logit : -INFINITY;
+        mb = fmaxf(mb, lg[u]);
+        if (ok && leader) a.alpha[static_cast<int64_t>(tt[u]) * a.H + head] = logit;
+      }
+      const float m_new = fmaxf(m, mb);
+      const float corr = m_new == -INFINITY ? 1.f : expf(m - m_new);
+      den *= corr;
+      acc *= corr;
+#pragma unroll
+      for (int u = 0; u < BB; ++u) {
+        const int j = j0 + u;
+        const float p = lg[u] == -INFINITY ? 0.f : expf(lg[u] - m_new);
+        const cf4 vr = VE[(j < n ? j : n - 1) * 32 + l32];
+        den += p;
+        acc += p * (vr * sv[u]);
+      }
+      m = m_new;
+    };
+    if (nt > 0) {  // (workgroup-uniform)
+      int j0 = 0;
+      for (; n - j0 > B / 2; j0 += B) batch(j0, std::integral_constant<int, B>{});
+      if (j0 < n) batch(j0, std::integral_constant<int, B / 2>{});
+    }
+    const float inv = 1.0f / (den + kCEps);
+    const cf4 o = acc * inv + sk;
+    st4(a.out + drow, o);
+    if (a.row_stats) {
+      const float mu = half_sum(o[0] + o[1] + o[2] + o[3], half) / static_cast<float>(kCD);
+      const cf4 dv = o - mu;
+      const float q2 = half_sum(dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2] + dv[3] * dv[3], half);
+      if (l32 == 0) a.row_stats[d] = make_float2(mu, q2);
+    }
+    if (leader) {
+      a.smax[static_cast<int64_t>(d) * a.H + head] = m;
+      a.sden[static_cast<int64_t>(d) * a.H + head] = den;
+    }
+  }
+}
+
+constexpr size_t fwd_sf_lds(int n) { return static_cast<size_t>(n) * (2 + kSfL) * kCD * 4; }
+
+template <int LPH>
+int fwd_sf_launch(const FwdSfArgs& a, bool edge, int max_degree, hipStream_t st) {
+  constexpr int W = 8, B = 8;
+  const size_t lds = fwd_sf_lds(max_degree);
+  const unsigned grid = static_cast<unsigned>(a.n_atoms);
+  auto go = [&](auto kern) -> int {
+    if (lds > 64 * 1024) {
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+      if (e != hipSuccess) return static_cast<int>(e);
+    }
+    kern<<<grid, 64 * W, lds, st>>>(a);
+    return last_launch_status();
+  };
+  return edge ? go(attn_fwd_center_sf_kernel<LPH, W, B, true>) : go(attn_fwd_center_sf_kernel<LPH, W, B, false>);
+}
+
 template <int LPH>
 int fwd_center_launch(const FwdCenterArgs& a, bool edge, int max_degree, hipStream_t st) {
   constexpr int W = 4, B = 8;
@@ -524,6 +722,49 @@ X2G_API int x2g_sbf_attention_fwd_center(const float* q, const float* k, const f
     case 2: return fwd_center_launch<2>(a, edge_on, md, st);
     case 4: return fwd_center_launch<4>(a, edge_on, md, st);
     case 8: return fwd_center_launch<8>(a, edge_on, md, st);
+    default: return X2G_EUNSUPPORTED;
+  }
+}
+
+X2G_API int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, const float* v, const float* skip,
+                                            const float* edge, const int32_t* src_row, int edge_mode,
+                                            const float* radial, const float* sph_y, const float* w_sbf,
+                                            const float* b_sbf, const int32_t* atom_rowptr, const int32_t* edge_rev,
+                                            const int32_t* rev_trip, int64_t atom0, int64_t n_atoms,
+                                            int32_t max_degree, int64_t num_edges, int64_t num_triplets, int32_t heads,
+                                            int32_t channels, float* out, float* alpha_raw, float* seg_max,
+                                            float* seg_den, float* row_stats, float* sbfproj_out, void* stream) {
+  if (n_atoms < 0 || atom0 < 0 || num_edges < 0 || num_triplets < 0 || heads <= 0 || channels <= 0)
+    return X2G_EINVAL;
+  if (edge_mode != X2G_EDGE_NONE && edge_mode != X2G_EDGE_PER_DST) return X2G_EUNSUPPORTED;
+  if (heads * channels != kCD || channels % 4 || max_degree < 0 ||
+      fwd_sf_lds(max_degree > 0 ? max_degree : 1) > 160 * 1024)
+    return X2G_EUNSUPPORTED;
+  if (n_atoms == 0 || num_edges == 0) return X2G_OK;
+  if (!q || !k || !v || !skip || !radial || !sph_y || !w_sbf || !b_sbf || !atom_rowptr || !edge_rev || !rev_trip ||
+      !out || !seg_max || !seg_den)
+    return X2G_EINVAL;
+  if (num_triplets > 0 && !alpha_raw) return X2G_EINVAL;
+  if (edge_mode == X2G_EDGE_PER_DST && (!edge || !src_row)) return X2G_EINVAL;
+  const auto al = [](const void* p, int m) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % m == 0; };
+  if (!al(q, 16) || !al(k, 16) || !al(v, 16) || !al(skip, 16) || !al(edge, 16) || !al(out, 16) || !al(b_sbf, 16) ||
+      !al(sbfproj_out, 16) || !al(row_stats, 8))
+    return X2G_EUNSUPPORTED;
+  FwdSfArgs a{};
+  a.q = q; a.k = k; a.v = v; a.skip = skip; a.edge = edge; a.src_row = src_row; a.radial = radial; a.y = sph_y;
+  a.w = w_sbf; a.bias = b_sbf; a.atom_rowptr = atom_rowptr; a.edge_rev = edge_rev; a.rev_trip = rev_trip;
+  a.atom0 = atom0; a.n_atoms = n_atoms; a.H = heads;
+  a.sqrt_c = static_cast<float>(sqrt(static_cast<double>(channels)));
+  a.out = out; a.alpha = alpha_raw; a.smax = seg_max; a.sden = seg_den; a.sp = sbfproj_out;
+  a.row_stats = reinterpret_cast<float2*>(row_stats);
+  const int md = max_degree > 0 ? max_degree : 1;
+  const bool edge_on = edge_mode == X2G_EDGE_PER_DST;
+  hipStream_t st = as_stream(stream);
+  switch (channels / 4) {
+    case 1: return fwd_sf_launch<1>(a, edge_on, md, st);
+    case 2: return fwd_sf_launch<2>(a, edge_on, md, st);
+    case 4: return fwd_sf_launch<4>(a, edge_on, md, st);
+    case 8: return fwd_sf_launch<8>(a, edge_on, md, st);
     default: return X2G_EUNSUPPORTED;
   }
 }

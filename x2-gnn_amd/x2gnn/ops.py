@@ -265,7 +265,10 @@ def spherical_basis(pos, lg: LineGraph, rbf_env, want_cos=False, num_spherical: 
     S = num_spherical * num_radial
     out = torch.empty(lg.T, S, dtype=torch.float32, device=pos.device)
     cos_t = torch.empty(lg.T, dtype=torch.float32, device=pos.device) if want_cos else None
-    fold = _FOLD_SBF and torch.is_grad_enabled() and (num_spherical, num_radial) == FOLD_BASIS
+    # the factors are kept for the factorised backward and for the fused-projection center forward (which
+    # also runs without grad, in inference, when its LDS image fits the batch's largest degree)
+    sf_fits = getattr(lg, "max_degree", None) is not None and 4608 * max(lg.max_degree, 1) <= 160 * 1024
+    fold = _FOLD_SBF and (num_spherical, num_radial) == FOLD_BASIS and (torch.is_grad_enabled() or sf_fits)
     ylm = torch.empty(lg.T, 8, dtype=torch.float32, device=pos.device) if fold else None
     call("x2g_spherical_basis", ptr(pos), ptr(lg.atom_i), ptr(lg.atom_j), ptr(lg.atom_k), None, ptr(lg.trip_src),
          ptr(rbf_env), lg.T, num_spherical, num_radial, ptr(out), ptr(cos_t), ptr(ylm), stream_ptr())
@@ -324,6 +327,17 @@ CENTER_MAX_DEGREE = 128  # X2G_CENTER_MAX_DEGREE
 # backward passes (parity tests flip them).
 _CENTER = True
 _CENTER_BWD = True
+# The center forward with lin_sbf fused (x2g_sbf_attention_fwd_center_sf: S_t rebuilt from the sbf factors
+# per center atom, no projection launch, no S read; S rows stored only for a backward): False = project S
+# first and read it (x2g_sbf_project + x2g_sbf_attention_fwd_center).
+_CENTER_SF = True
+
+
+def _center_sf_ok(lg, factors, D):
+    """Whether the fused-projection center forward applies: the sbf factors are this call's, and the
+    block's LDS image (k + e, v + e and 7 P rows per source: 4.5 KB x max degree) fits."""
+    return (_CENTER_SF and factors is not None and factors[1] is not None and D == 128
+            and lg.max_degree is not None and 4608 * max(lg.max_degree, 1) <= 160 * 1024)
 
 
 def _center_rows(lg, edge_mode, edge_row, D, channels):
@@ -358,23 +372,33 @@ class _SBFAttention(torch.autograd.Function):
         alpha = torch.empty(T, heads, dtype=torch.float32, device=dev)
         smax = torch.empty(E, heads, dtype=torch.float32, device=dev)
         sden = torch.empty(E, heads, dtype=torch.float32, device=dev)
-        # S = lin_sbf(sbf) once per layer [T, D], right before this layer's attention (so it is still
-        # in the MALL when the three attention kernels read its rows: sbf pointer = S, weight pointer
-        # NULL) instead of re-projecting per triplet
-        sproj = torch.empty(T, D, dtype=torch.float32, device=dev)
-        call("x2g_sbf_project", ptr(sbf), T, sbf.shape[1], ptr(w_sbf), ptr(b_sbf), D, ptr(sproj), stream_ptr())
         # per-row (mean, M2) of the output for a graph LayerNorm fused into the next row chain
         rstats = torch.empty(E, 2, dtype=torch.float32, device=dev) if _LN_FUSE and D == 128 else None
         center, src_row = _center_rows(lg, edge_mode, edge_row, D, channels)
-        if center:
-            call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(src_row), edge_mode,
-                 ptr(sproj), 0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), 0, lg.N, lg.max_degree, E, T,
-                 heads, channels, ptr(out), ptr(alpha), ptr(smax), ptr(sden), ptr(rstats), stream_ptr())
+        if center and _center_sf_ok(lg, factors, D):
+            # lin_sbf fused into the center forward: S_t rebuilt per center atom from the sbf factors; its
+            # rows stored only when a backward will read them
+            sproj = torch.empty(T, D, dtype=torch.float32, device=dev) if any(ctx.needs_input_grad) else None
+            call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(src_row),
+                 edge_mode, ptr(factors[0]), ptr(factors[1]), ptr(w_sbf), ptr(b_sbf), ptr(lg.atom_rowptr),
+                 ptr(lg.edge_rev), ptr(lg.rev_trip), 0, lg.N, lg.max_degree, E, T, heads, channels, ptr(out),
+                 ptr(alpha), ptr(smax), ptr(sden), ptr(rstats), ptr(sproj), stream_ptr())
         else:
-            call("x2g_sbf_attention_fwd_stats" if rstats is not None else "x2g_sbf_attention_fwd", ptr(q), ptr(k),
-                 ptr(v), ptr(skip), ptr(edge), ptr(edge_row), edge_mode, ptr(sproj), None, None, ptr(lg.trip_rowptr),
-                 ptr(lg.trip_src), E, T, heads, channels, D, ptr(out), ptr(alpha), ptr(smax), ptr(sden),
-                 *((ptr(rstats),) if rstats is not None else ()), stream_ptr())
+            # S = lin_sbf(sbf) once per layer [T, D], right before this layer's attention (so it is still
+            # in the MALL when the attention kernels read its rows: sbf pointer = S, weight pointer NULL)
+            # instead of re-projecting per triplet
+            sproj = torch.empty(T, D, dtype=torch.float32, device=dev)
+            call("x2g_sbf_project", ptr(sbf), T, sbf.shape[1], ptr(w_sbf), ptr(b_sbf), D, ptr(sproj), stream_ptr())
+            if center:
+                call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(src_row),
+                     edge_mode, ptr(sproj), 0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), 0, lg.N,
+                     lg.max_degree, E, T, heads, channels, ptr(out), ptr(alpha), ptr(smax), ptr(sden), ptr(rstats),
+                     stream_ptr())
+            else:
+                call("x2g_sbf_attention_fwd_stats" if rstats is not None else "x2g_sbf_attention_fwd", ptr(q),
+                     ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(edge_row), edge_mode, ptr(sproj), None, None,
+                     ptr(lg.trip_rowptr), ptr(lg.trip_src), E, T, heads, channels, D, ptr(out), ptr(alpha),
+                     ptr(smax), ptr(sden), *((ptr(rstats),) if rstats is not None else ()), stream_ptr())
         if factors is not None:  # the factorised backward never reads sbf itself
             ctx.save_for_backward(q, k, v, edge, factors[0], factors[1], sproj, alpha, smax, sden)
         else:
@@ -955,7 +979,9 @@ def sbf_attention(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg: LineGraph, heads: 
         edge_mode = EDGE_NONE
     if edge_row is not None:
         edge_row = _i32(edge_row)
-    if not torch.is_grad_enabled() and lg.T > INFER_TILE and q.shape[0] > 0:
+    sf = (_center_rows(lg, edge_mode, edge_row, heads * channels, channels)[0]
+          and _center_sf_ok(lg, _sbf_factors(lg, sbf, edge_mode, heads * channels, edge, edge_row), heads * channels))
+    if not torch.is_grad_enabled() and lg.T > INFER_TILE and q.shape[0] > 0 and not sf:  # (sf: no S at all)
         out, alpha, smax, sden, rstats = _attention_fwd_tiled(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode,
                                                               edge_row, heads, channels, INFER_TILE)
     else:
