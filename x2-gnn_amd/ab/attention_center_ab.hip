@@ -25,6 +25,20 @@
 
 #include "common.hpp"
 
+// A/B trace build (-DX2G_TRACE): thread 0 of every backward workgroup stamps the 100 MHz wall clock at its
+// phase boundaries into x2g_ctrace[block][8] (x2g_ctrace_fetch copies them out)
+#ifdef X2G_TRACE
+__device__ unsigned long long x2g_ctrace[8192 * 8];
+#define CTR(k)                                                                           \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < 8192) x2g_ctrace[blockIdx.x * 8 + (k)] = wall_clock64(); \
+  } while (0)
+#else
+#define CTR(k) \
+  do {         \
+  } while (0)
+#endif
+
 namespace x2g {
 namespace {
 
@@ -196,7 +210,7 @@ constexpr int kSfK = kSfL * kSfR;        // 42
 
 template <int LPH, int WAVES, int B, bool EDGE>
 __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const FwdSfArgs a) {
-  extern __shared__ cf4 lds[];  // [n][32] (k + e), [n][32] (v + e), [n][7][32] P, [n][42] R
+  extern __shared__ cf4 lds[];  // [n][32] (k + e), [n][32] (v + e), [n][7][32] P
   const int64_t b = a.atom0 + blockIdx.x;
   const int r0 = uniform(a.atom_rowptr[b]);
   const int n = uniform(a.atom_rowptr[b + 1]) - r0;
@@ -204,7 +218,6 @@ __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const Fw
   cf4* KE = lds;
   cf4* VE = lds + n * 32;
   cf4* P = VE + n * 32;
-  float* RS = reinterpret_cast<float*>(P + n * kSfL * 32);
   constexpr int NT = 64 * WAVES;
   const int tid = threadIdx.x;
   const int l32 = tid & 31, half = (tid >> 5) & 1, wave = tid >> 6;
@@ -226,26 +239,20 @@ __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const Fw
     KE[idx] = ld4(a.k + row) + e4;
     VE[idx] = ld4(a.v + row) + e4;
   }
-  // the block's radial rows (n x 42 contiguous floats) staged too: the P loop below then reads LDS instead
-  // of one dependent global round trip per source
-  for (int idx = tid; idx < n * kSfK; idx += NT) RS[idx] = a.radial[static_cast<int64_t>(r0) * kSfK + idx];
   // P[j][l][c] for the block's sources: thread (group g, order l, channels 4 c4 .. +3) keeps its 4 x 6
-  // weights in registers (loaded before the barrier) and walks sources j = g, g + NG, ...
-  constexpr int NG = NT / 256;  // thread groups of 7 x 32 (the last 32 threads of each 256 idle)
-  const int pg = tid / 256, prest = tid % 256;
-  const bool pthr = prest < kSfL * 32;
-  const int pl = pthr ? prest >> 5 : 0, pc4 = prest & 31;
-  float wv[4][kSfR];
-#pragma unroll
-  for (int cc = 0; cc < 4; ++cc)
-#pragma unroll
-    for (int r = 0; r < kSfR; ++r) wv[cc][r] = a.w[(4 * pc4 + cc) * kSfK + kSfR * pl + r];
-  __syncthreads();
+  // weights in registers and walks sources j = g, g + NG, ...
   {
-    if (pthr) {
-      const int l = pl, c4 = pc4;
-      for (int j = pg; j < n; j += NG) {
-        const float* rr = RS + j * kSfK + kSfR * l;
+    constexpr int NG = NT / 256;  // thread groups of 7 x 32 (the last 32 threads of each 256 idle)
+    const int g = tid / 256, rest = tid % 256;
+    if (rest < kSfL * 32) {
+      const int l = rest >> 5, c4 = rest & 31;
+      float wv[4][kSfR];
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+        for (int r = 0; r < kSfR; ++r) wv[cc][r] = a.w[(4 * c4 + cc) * kSfK + kSfR * l + r];
+      for (int j = g; j < n; j += NG) {
+        const float* rr = a.radial + static_cast<int64_t>(r0 + j) * kSfK + kSfR * l;
         float rv[kSfR];
 #pragma unroll
         for (int r = 0; r < kSfR; ++r) rv[r] = rr[r];
@@ -354,7 +361,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const Fw
   }
 }
 
-constexpr size_t fwd_sf_lds(int n) { return static_cast<size_t>(n) * ((2 + kSfL) * kCD + kSfK) * 4; }
+constexpr size_t fwd_sf_lds(int n) { return static_cast<size_t>(n) * (2 + kSfL) * kCD * 4; }
 
 template <int LPH>
 int fwd_sf_launch(const FwdSfArgs& a, bool edge, int max_degree, hipStream_t st) {
@@ -426,6 +433,7 @@ __host__ __device__ constexpr size_t bwd_center_lds(int n) {
 
 template <int LPH, int WAVES, int B, bool EDGE>
 __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCenterArgs a) {
+  CTR(0);
   constexpr int H = 32 / LPH;
   extern __shared__ cf4 lds[];
   const int64_t b = blockIdx.x;
@@ -471,6 +479,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
     DI[idx] = a.edge_rev[r0 + idx];
   }
   __syncthreads();
+  CTR(1);
   // ---- pass 1: one owner per source j
   const int nt = n - 1;  // triplets per destination (and per source)
   auto rsrc = [](const void* p, int64_t bytes) {
@@ -554,9 +563,11 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
 #pragma unroll
     for (int l = 0; l < 8; ++l) st4(gf + l * kCD, G[l]);
   }
+  CTR(2);
   // the g scratch written by every owner is read by others below: workgroup-scope release / acquire
   __threadfence_block();
   __syncthreads();
+  CTR(3);
   // at of triplet t for destination i (recomputed, as pass 1 did) and g_t, from global (L2) in batches
   auto atg = [&](int i, int t, float& at, float& g) {
     at = expf(ldf(al_r, (t * H + head) * 4) - MX[i * H + head]) * IV[i * H + head];
@@ -576,6 +587,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
     if (leader) RHO[i * H + head] = rho;
   }
   __syncthreads();
+  CTR(4);
   // ---- pass 2: dk_j (owner of source j), dq_i (owner of destination i); x over the other n - 1
   for (int o = owner; o < n; o += NO) {
     cf4 dk = {0.f, 0.f, 0.f, 0.f}, dq = {0.f, 0.f, 0.f, 0.f};
@@ -609,6 +621,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
     // this lane's own dv store of pass 1 is read back (program order)
     if (a.d_edge) GO[o * 32 + l32] = dk + ld4(a.dv + static_cast<int64_t>(r0 + o) * kCD + c0);
   }
+  CTR(5);
   if (a.d_edge) {  // d_edge[b] = sum_j (dv_j + dk_j), j ascending
     __syncthreads();
     if (tid < 32) {
@@ -617,6 +630,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
       st4(a.d_edge + b * kCD + c0, s);
     }
   }
+  CTR(6);
 }
 
 template <int LPH>
@@ -775,3 +789,9 @@ X2G_API int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, cons
     default: return X2G_EUNSUPPORTED;
   }
 }
+
+#ifdef X2G_TRACE
+X2G_API int x2g_ctrace_fetch(unsigned long long* host, int n) {
+  return static_cast<int>(hipMemcpyFromSymbol(host, HIP_SYMBOL(x2g_ctrace), sizeof(unsigned long long) * n));
+}
+#endif

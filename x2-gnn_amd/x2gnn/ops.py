@@ -267,7 +267,7 @@ def spherical_basis(pos, lg: LineGraph, rbf_env, want_cos=False, num_spherical: 
     cos_t = torch.empty(lg.T, dtype=torch.float32, device=pos.device) if want_cos else None
     # the factors are kept for the factorised backward and for the fused-projection center forward (which
     # also runs without grad, in inference, when its LDS image fits the batch's largest degree)
-    sf_fits = getattr(lg, "max_degree", None) is not None and 4608 * max(lg.max_degree, 1) <= 160 * 1024
+    sf_fits = getattr(lg, "max_degree", None) is not None and 4776 * max(lg.max_degree, 1) <= 160 * 1024
     fold = _FOLD_SBF and (num_spherical, num_radial) == FOLD_BASIS and (torch.is_grad_enabled() or sf_fits)
     ylm = torch.empty(lg.T, 8, dtype=torch.float32, device=pos.device) if fold else None
     call("x2g_spherical_basis", ptr(pos), ptr(lg.atom_i), ptr(lg.atom_j), ptr(lg.atom_k), None, ptr(lg.trip_src),
@@ -335,9 +335,9 @@ _CENTER_SF = True
 
 def _center_sf_ok(lg, factors, D):
     """Whether the fused-projection center forward applies: the sbf factors are this call's, and the
-    block's LDS image (k + e, v + e and 7 P rows per source: 4.5 KB x max degree) fits."""
+    block's LDS image (k + e, v + e, 7 P rows and the radial row per source: 4.66 KB x max degree) fits."""
     return (_CENTER_SF and factors is not None and factors[1] is not None and D == 128
-            and lg.max_degree is not None and 4608 * max(lg.max_degree, 1) <= 160 * 1024)
+            and lg.max_degree is not None and 4776 * max(lg.max_degree, 1) <= 160 * 1024)
 
 
 def _center_rows(lg, edge_mode, edge_row, D, channels):
