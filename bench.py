@@ -76,7 +76,7 @@ def step_roofline(ms_per_step, workload, shape):
 
 
 # probe name -> the kernel (substring of its symbol) whose PMC bytes it is
-PMC_KERNEL = {"sbf_project": "sbf_project_waves", "attn_fwd": "attn_fwd_center_kernel",
+PMC_KERNEL = {"sbf_project": "sbf_project_waves", "attn_fwd": "attn_fwd_center",
               "attn_bwd": "attn_bwd_center_kernel",
               "attn_bwd_dst": "attn_bwd_dst_g_batched", "attn_bwd_src": "attn_bwd_src_fold_batched",
               "sbf_radial_wgrad": "sbf_radial_wgrad"}
@@ -189,13 +189,22 @@ def attention_probe(model, batch, reps):
 
     def fwd_center():  # the model's forward on a symmetric line graph (csrc/attention_center.hip)
         call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(src_row),
-             ops.EDGE_PER_DST, ptr(sproj), 0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), 0, lg.N,
-             lg.max_degree, E, T, H, C, ptr(out), ptr(alpha), ptr(smax), ptr(sden), None, stream_ptr())
+             ops.EDGE_PER_DST, ptr(sproj), 0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip),
+             ptr(lg.center_order), 0, lg.N, lg.max_degree, E, T, H, C, ptr(out), ptr(alpha), ptr(smax), ptr(sden),
+             None, stream_ptr())
+
+    sf = center and ops._center_sf_ok(lg, (radial, ylm), D)
+
+    def fwd_sf():  # the model's forward with lin_sbf fused (S rebuilt per center atom; S rows stored)
+        call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(src_row),
+             ops.EDGE_PER_DST, ptr(radial), ptr(ylm), ptr(W), ptr(bsb), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
+             ptr(lg.rev_trip), ptr(lg.center_order), 0, lg.N, lg.max_degree, E, T, H, C, ptr(out), ptr(alpha),
+             ptr(smax), ptr(sden), None, ptr(sproj), stream_ptr())
 
     def bwd_center():  # both backward passes in one launch per center atom
         call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(table), ptr(src_row), ops.EDGE_PER_DST,
-             ptr(sproj), ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(alpha), ptr(smax),
-             ptr(sden), ptr(dout), lg.N, lg.max_degree, E, T, H, C, ptr(dq), ptr(dk), ptr(dv), ptr(gfold),
+             ptr(sproj), ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order),
+             ptr(alpha), ptr(smax), ptr(sden), ptr(dout), lg.N, lg.max_degree, E, T, H, C, ptr(dq), ptr(dk), ptr(dv), ptr(gfold),
              ptr(atom_de), ptr(g_work), stream_ptr())
 
     row_b = 4 * D
@@ -224,8 +233,12 @@ def attention_probe(model, batch, reps):
     # (+ the g_t [T, H] scratch: written once, read back from L2 by the same workgroup)
     cbwd_bytes = (cidx + T * (row_b + 4 * H + 32) + E * (4 * row_b + 8 * H) + E * (3 * row_b + 8 * row_b)
                   + lg.N * row_b + T * 4 * H)
-    probes = [("sbf_project", proj, proj_bytes, proj_bytes)]
-    if center:
+    # fused projection: k v q skip out rows, the radial rows and the weight, Y, alpha, max/den, S rows written
+    sf_bytes = cidx + T * (row_b + 4 * H + 32) + E * (5 * row_b + 8 * H + 4 * S) + 4 * D * (S + 1)
+    probes = [] if sf else [("sbf_project", proj, proj_bytes, proj_bytes)]
+    if sf:
+        probes.append(("attn_fwd", fwd_sf, sf_bytes, sf_bytes))
+    elif center:
         probes.append(("attn_fwd", fwd_center, cfwd_bytes, cfwd_bytes))
     else:
         probes.append(("attn_fwd", fwd, fwd_bytes, fwd_gath))
@@ -237,7 +250,7 @@ def attention_probe(model, batch, reps):
     res = {}
     for name, fn, nbytes, gath in probes:
         res[name] = (_event_time(fn, reps), nbytes, gath)
-    return res, dict(E=E, T=T, D=D, center=center, center_bwd=center_bwd)
+    return res, dict(E=E, T=T, D=D, center=center, center_bwd=center_bwd, sf=sf)
 
 
 def dense_probe(R, reps):

@@ -268,12 +268,15 @@ int x2g_sbf_attention_fwd_stats(const float* q, const float* k, const float* v, 
  *   sbfproj: S rows for triplets t_base .. (row t - t_base), covering every triplet of the atoms
  *   atom0 .. atom0 + n_atoms - 1 (whole molecules: the tiled inference path passes a molecule range).
  *   max_degree >= every deg(b) of those atoms, <= X2G_CENTER_MAX_DEGREE (sizes the LDS image).
+ *   atom_order (or NULL): workgroup w takes center atom atom_order[atom0 + w] (a permutation of the range;
+ *   x2gnn passes the atoms by decreasing degree, so the longest blocks start first).
  * heads * channels = 128 and channels a multiple of 4, 16-byte aligned rows, else X2G_EUNSUPPORTED. */
 #define X2G_CENTER_MAX_DEGREE 128
 int x2g_sbf_attention_fwd_center(const float* q, const float* k, const float* v, const float* skip,
                                  const float* edge, const int32_t* src_row, int edge_mode, const float* sbfproj,
                                  int64_t t_base, const int32_t* atom_rowptr, const int32_t* edge_rev,
-                                 const int32_t* rev_trip, int64_t atom0, int64_t n_atoms, int32_t max_degree,
+                                 const int32_t* rev_trip, const int32_t* atom_order, int64_t atom0, int64_t n_atoms,
+                                 int32_t max_degree,
                                  int64_t num_edges, int64_t num_triplets, int32_t heads, int32_t channels, float* out,
                                  float* alpha_raw, float* seg_max, float* seg_den, float* row_stats, void* stream);
 
@@ -288,7 +291,8 @@ int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, const float*
                                     const float* edge, const int32_t* src_row, int edge_mode, const float* radial,
                                     const float* sph_y, const float* w_sbf, const float* b_sbf,
                                     const int32_t* atom_rowptr, const int32_t* edge_rev, const int32_t* rev_trip,
-                                    int64_t atom0, int64_t n_atoms, int32_t max_degree, int64_t num_edges,
+                                    const int32_t* atom_order, int64_t atom0, int64_t n_atoms, int32_t max_degree,
+                                    int64_t num_edges,
                                     int64_t num_triplets, int32_t heads, int32_t channels, float* out,
                                     float* alpha_raw, float* seg_max, float* seg_den, float* row_stats,
                                     float* sbfproj_out, void* stream);
@@ -308,7 +312,8 @@ size_t x2g_sbf_attention_bwd_center_lds(int32_t max_degree, int32_t heads);
 int x2g_sbf_attention_bwd_center(const float* q, const float* k, const float* v, const float* edge,
                                  const int32_t* src_row, int edge_mode, const float* sbfproj, const float* sph_y,
                                  const int32_t* atom_rowptr, const int32_t* edge_rev, const int32_t* rev_trip,
-                                 const float* alpha_raw, const float* seg_max, const float* seg_den, const float* dout,
+                                 const int32_t* atom_order, const float* alpha_raw, const float* seg_max,
+                                 const float* seg_den, const float* dout,
                                  int64_t num_atoms, int32_t max_degree, int64_t num_edges, int64_t num_triplets,
                                  int32_t heads, int32_t channels, float* dq, float* dk, float* dv, float* radial_grad,
                                  float* d_edge_atom, float* g_work, void* stream);

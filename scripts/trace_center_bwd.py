@@ -4,7 +4,7 @@ X2G_LIB=.../libx2g_ctrace.so).  Thread 0 of every workgroup (one per center atom
 its phase boundaries: start, staging done, pass 1 done (its own), fence + barrier, rho + barrier, pass 2
 done, end.  Prints per-phase medians / p90 over the workgroups and how the workgroups overlap in time.
 
-    python scripts/trace_center_bwd.py [molecules]"""
+    python scripts/trace_center_bwd.py [molecules] [ident]"""
 import ctypes
 import os
 import sys
@@ -29,7 +29,11 @@ e32 = ops._i32(ei)
 lg = ops.LineGraph(e32[0].contiguous(), e32[1].contiguous(), n, T, symmetric=True)
 z = b.x.to(dev)
 lg.src_type, lg.dst_type, lg.atom_type = ops._i32(z[ei[0]]), ops._i32(z[ei[1]]), ops._i32(z)
-md = int(np.bincount(b.edge_index[0].numpy()).max())
+deg_all = np.bincount(b.edge_index[0].numpy(), minlength=n)
+md = int(deg_all.max())
+# launch order: by decreasing degree (the model's), or the identity with "ident" as the second argument
+order = None if (len(sys.argv) > 2 and sys.argv[2] == "ident") else \
+    torch.from_numpy(np.argsort(-deg_all, kind="stable").astype(np.int32)).to(dev)
 E, H, C, D = lg.E, 16, 8, 128
 g = torch.Generator(device=dev).manual_seed(3)
 q, k, v, skip, dout = (torch.randn(E, D, device=dev, generator=g) for _ in range(5))
@@ -40,7 +44,8 @@ f = dict(device=dev, dtype=torch.float32)
 out, alpha = torch.empty(E, D, **f), torch.empty(T, H, **f)
 smax, sden = torch.empty(E, H, **f), torch.empty(E, H, **f)
 call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
-     ops.EDGE_PER_DST, ptr(S), 0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), 0, n, md, E, T, H, C,
+     ops.EDGE_PER_DST, ptr(S), 0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(order), 0, n, md, E, T,
+     H, C,
      ptr(out), ptr(alpha), ptr(smax), ptr(sden), None, stream_ptr())
 dq, dk, dv = (torch.empty(E, D, **f) for _ in range(3))
 G, de, gw = torch.empty(E, 8, D, **f), torch.empty(n, D, **f), torch.empty(T, H, **f)
@@ -51,7 +56,8 @@ for it in range(6):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(table), ptr(lg.src_type), ops.EDGE_PER_DST,
-         ptr(S), ptr(y), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(alpha), ptr(smax), ptr(sden),
+         ptr(S), ptr(y), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(order), ptr(alpha), ptr(smax),
+         ptr(sden),
          ptr(dout), n, md, E, T, H, C, ptr(dq), ptr(dk), ptr(dv), ptr(G), ptr(de), ptr(gw), stream_ptr())
     e1.record()
     torch.cuda.synchronize()
@@ -59,7 +65,8 @@ for it in range(6):
 buf = np.zeros(8192 * 8, dtype=np.uint64)
 assert lib.x2g_ctrace_fetch(buf.ctypes.data, buf.size) == 0
 t = buf.reshape(8192, 8)[:n].astype(np.int64)
-deg = np.diff(lg.atom_rowptr.cpu().numpy())
+# stamps are per workgroup: workgroup w ran atom order[w]
+deg = deg_all[order.cpu().numpy()] if order is not None else deg_all
 live = deg > 0
 t, deg = t[live], deg[live]
 t0 = t[:, 0].min()

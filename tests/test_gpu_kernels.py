@@ -1862,7 +1862,9 @@ def _sym_lg(ei, n, cuda, with_transpose=False):
     z = torch.randint(0, 10, (n,), generator=torch.Generator().manual_seed(n)).to(cuda)
     lg.dst_type = ops._i32(z[e[1]])
     lg.src_type = ops._i32(z[e[0]])
-    lg.max_degree = int(np.bincount(ei[0], minlength=n).max()) if ei.shape[1] else 0
+    deg = np.bincount(ei[0], minlength=n)
+    lg.max_degree = int(deg.max()) if ei.shape[1] else 0
+    lg.center_order = torch.from_numpy(np.argsort(-deg, kind="stable").astype(np.int32)).to(cuda)
     return lg
 
 
@@ -1875,8 +1877,9 @@ def _attn_inputs(lg, cuda, seed, rows=10):
     return q, k, v, skip, S, table
 
 
-def _fwd_both(lg, q, k, v, skip, S, table, mode, heads, channels, stats=True):
-    """(center outputs, destination-major outputs): out, alpha, smax, sden, row_stats."""
+def _fwd_both(lg, q, k, v, skip, S, table, mode, heads, channels, stats=True, order=None):
+    """(center outputs, destination-major outputs): out, alpha, smax, sden, row_stats; ``order``: the center
+    kernel's workgroup -> atom order (None: identity)."""
     from x2gnn import ops
     from x2gnn._lib import call, ptr, stream_ptr
 
@@ -1891,7 +1894,7 @@ def _fwd_both(lg, q, k, v, skip, S, table, mode, heads, channels, stats=True):
         if center:
             call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge),
                  ptr(lg.src_type) if edge is not None else None, mode, ptr(S), 0, ptr(lg.atom_rowptr),
-                 ptr(lg.edge_rev), ptr(lg.rev_trip), 0, lg.N, lg.max_degree, E, T, heads, channels, ptr(out),
+                 ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(order), 0, lg.N, lg.max_degree, E, T, heads, channels, ptr(out),
                  ptr(alpha), ptr(smax), ptr(sden), ptr(rs), stream_ptr())
         else:
             call("x2g_sbf_attention_fwd_stats" if stats else "x2g_sbf_attention_fwd", ptr(q), ptr(k), ptr(v),
@@ -1928,8 +1931,9 @@ def test_center_forward_equals_destination_major(cuda, heads, channels):
     assert lg.max_degree >= 9
     q, k, v, skip, S, table = _attn_inputs(lg, cuda, 3)
     for mode in (ops.EDGE_PER_DST, ops.EDGE_NONE):
-        for stats in (True, False):
-            a, r = _fwd_both(lg, q, k, v, skip, S, table, mode, heads, channels, stats)
+        for stats in (True, False):  # (with stats: atoms launched by decreasing degree, as the model does)
+            a, r = _fwd_both(lg, q, k, v, skip, S, table, mode, heads, channels, stats,
+                             order=lg.center_order if stats else None)
             _close_fwd(a, r)
 
 
@@ -1965,7 +1969,7 @@ def test_center_forward_edge_cases(cuda):
     for a0, a1, t0, t1 in ((0, split, 0, t_split), (split, n, t_split, lg.T)):
         Sc = S[t0:t1].clone()
         call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
-             ops.EDGE_PER_DST, ptr(Sc), t0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), a0, a1 - a0,
+             ops.EDGE_PER_DST, ptr(Sc), t0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), None, a0, a1 - a0,
              lg.max_degree, lg.E, lg.T, 16, 8, ptr(out), ptr(alpha), ptr(smax), ptr(sden), ptr(rs), stream_ptr())
     for x, y in zip((out, alpha, smax, sden, rs), a):
         assert torch.equal(x, y)
@@ -1993,7 +1997,8 @@ def _bwd_both(lg, q, k, v, S, table, mode, heads, channels, seed):
     de_atom = torch.full((lg.N, D), float("nan"), **f) if edge is not None else None
     assert int(_lib.load().x2g_sbf_attention_bwd_center_lds(lg.max_degree, heads)) <= 160 * 1024
     call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(lg.src_type) if edge is not None else None,
-         mode, ptr(S), ptr(y), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(alpha), ptr(smax), ptr(sden),
+         mode, ptr(S), ptr(y), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order), ptr(alpha),
+         ptr(smax), ptr(sden),
          ptr(dout), lg.N, lg.max_degree, E, T, heads, channels, ptr(dq), ptr(dk), ptr(dv), ptr(G), ptr(de_atom),
          ptr(torch.empty(T, H, **f)), stream_ptr())
     c = [dq, dk, dv, G]
@@ -2069,8 +2074,8 @@ def test_center_backward_edge_cases(cuda):
 
     assert int(_lib.load().x2g_sbf_attention_bwd_center_lds(130, 16)) > 160 * 1024 or 130 > ops.CENTER_MAX_DEGREE
     rc = _lib.load().x2g_sbf_attention_bwd_center(None, None, None, None, None, 0, None, None, None, None, None, None,
-                                                   None, None, None, 1, 130, 1, 1, 16, 8, None, None, None, None, None,
-                                                   None, None)
+                                                   None, None, None, None, 1, 130, 1, 1, 16, 8, None, None, None, None,
+                                                   None, None, None)
     assert rc == 1002  # X2G_EUNSUPPORTED
 
 
@@ -2102,14 +2107,15 @@ def test_center_forward_fused_projection_equals_projected(cuda):
     ref = [torch.empty(E, D, **f), torch.empty(T, H, **f), torch.empty(E, H, **f), torch.empty(E, H, **f),
            torch.empty(E, 2, **f)]
     call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
-         ops.EDGE_PER_DST, ptr(S), 0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), 0, lg.N, lg.max_degree,
-         E, T, H, C, *[ptr(t) for t in ref], stream_ptr())
+         ops.EDGE_PER_DST, ptr(S), 0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order), 0,
+         lg.N, lg.max_degree, E, T, H, C, *[ptr(t) for t in ref], stream_ptr())
     for store in (True, False):
         got = [torch.full_like(t, float("nan")) for t in ref]
         S2 = torch.full((T, D), float("nan"), **f) if store else None
         call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
              ops.EDGE_PER_DST, ptr(radial), ptr(y), ptr(W), ptr(bias), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
-             ptr(lg.rev_trip), 0, lg.N, lg.max_degree, E, T, H, C, *[ptr(t) for t in got], ptr(S2), stream_ptr())
+             ptr(lg.rev_trip), None if store else ptr(lg.center_order), 0, lg.N, lg.max_degree, E, T, H, C,
+             *[ptr(t) for t in got], ptr(S2), stream_ptr())
         for name, a, r in zip(("out", "alpha", "smax", "sden", "row_stats"), got, ref):
             assert not torch.isnan(a).any(), name
             torch.testing.assert_close(a, r, rtol=1e-5, atol=1e-5, msg=name)

@@ -29,9 +29,9 @@
 // phase boundaries into x2g_ctrace[block][8] (x2g_ctrace_fetch copies them out)
 #ifdef X2G_TRACE
 __device__ unsigned long long x2g_ctrace[8192 * 8];
-#define CTR(k)                                                                           \
-  do {                                                                                   \
-    if (threadIdx.x == 0 && blockIdx.x < 8192) x2g_ctrace[blockIdx.x * 8 + (k)] = wall_clock64(); \
+#define CTR(k)                                                                                          \
+  do {                                                                                                  \
+    if (threadIdx.x == 0 && blockIdx.x < 8192) x2g_ctrace[blockIdx.x * 8 + (k)] = wall_clock64();     \
   } while (0)
 #else
 #define CTR(k) \
@@ -68,6 +68,7 @@ struct FwdCenterArgs {
   const float* sp;         // S rows, row t - t_base
   int64_t t_base;
   const int32_t *atom_rowptr, *edge_rev, *rev_trip;
+  const int32_t* order;  // workgroup -> center atom (NULL: atom0 + blockIdx.x)
   int64_t atom0, n_atoms;
   int H;
   float sqrt_c;
@@ -78,7 +79,9 @@ struct FwdCenterArgs {
 template <int LPH, int WAVES, int B, bool EDGE>
 __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_kernel(const FwdCenterArgs a) {
   extern __shared__ cf4 lds[];  // [n][32] (k + e), then [n][32] (v + e)
-  const int64_t b = a.atom0 + blockIdx.x;
+  // (the host orders the atoms by decreasing degree: the longest blocks start first, the short ones fill the
+  // tail of the launch)
+  const int64_t b = a.order ? static_cast<int64_t>(a.order[a.atom0 + blockIdx.x]) : a.atom0 + blockIdx.x;
   const int r0 = uniform(a.atom_rowptr[b]);
   const int n = uniform(a.atom_rowptr[b + 1]) - r0;
   if (n <= 0) return;  // (workgroup-uniform: no barrier is skipped by a part of it)
@@ -197,6 +200,7 @@ struct FwdSfArgs {
   const int32_t* src_row;
   const float *radial, *y, *w, *bias;  // rbf_env [E, 42], Y [T, 8], lin_sbf weight [128, 42] and bias [128]
   const int32_t *atom_rowptr, *edge_rev, *rev_trip;
+  const int32_t* order;  // workgroup -> center atom (NULL: atom0 + blockIdx.x)
   int64_t atom0, n_atoms;
   int H;
   float sqrt_c;
@@ -210,14 +214,17 @@ constexpr int kSfK = kSfL * kSfR;        // 42
 
 template <int LPH, int WAVES, int B, bool EDGE>
 __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const FwdSfArgs a) {
-  extern __shared__ cf4 lds[];  // [n][32] (k + e), [n][32] (v + e), [n][7][32] P
-  const int64_t b = a.atom0 + blockIdx.x;
+  extern __shared__ cf4 lds[];  // [n][32] (k + e), [n][32] (v + e), [n][7][32] P, [n][42] R
+  // (the host orders the atoms by decreasing degree: the longest blocks start first, the short ones fill the
+  // tail of the launch)
+  const int64_t b = a.order ? static_cast<int64_t>(a.order[a.atom0 + blockIdx.x]) : a.atom0 + blockIdx.x;
   const int r0 = uniform(a.atom_rowptr[b]);
   const int n = uniform(a.atom_rowptr[b + 1]) - r0;
   if (n <= 0) return;  // (workgroup-uniform)
   cf4* KE = lds;
   cf4* VE = lds + n * 32;
   cf4* P = VE + n * 32;
+  float* RS = reinterpret_cast<float*>(P + n * kSfL * 32);
   constexpr int NT = 64 * WAVES;
   const int tid = threadIdx.x;
   const int l32 = tid & 31, half = (tid >> 5) & 1, wave = tid >> 6;
@@ -239,20 +246,26 @@ __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const Fw
     KE[idx] = ld4(a.k + row) + e4;
     VE[idx] = ld4(a.v + row) + e4;
   }
+  // the block's radial rows (n x 42 contiguous floats) staged too: the P loop below then reads LDS instead
+  // of one dependent global round trip per source
+  for (int idx = tid; idx < n * kSfK; idx += NT) RS[idx] = a.radial[static_cast<int64_t>(r0) * kSfK + idx];
   // P[j][l][c] for the block's sources: thread (group g, order l, channels 4 c4 .. +3) keeps its 4 x 6
-  // weights in registers and walks sources j = g, g + NG, ...
+  // weights in registers (loaded before the barrier) and walks sources j = g, g + NG, ...
+  constexpr int NG = NT / 256;  // thread groups of 7 x 32 (the last 32 threads of each 256 idle)
+  const int pg = tid / 256, prest = tid % 256;
+  const bool pthr = prest < kSfL * 32;
+  const int pl = pthr ? prest >> 5 : 0, pc4 = prest & 31;
+  float wv[4][kSfR];
+#pragma unroll
+  for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+    for (int r = 0; r < kSfR; ++r) wv[cc][r] = a.w[(4 * pc4 + cc) * kSfK + kSfR * pl + r];
+  __syncthreads();
   {
-    constexpr int NG = NT / 256;  // thread groups of 7 x 32 (the last 32 threads of each 256 idle)
-    const int g = tid / 256, rest = tid % 256;
-    if (rest < kSfL * 32) {
-      const int l = rest >> 5, c4 = rest & 31;
-      float wv[4][kSfR];
-#pragma unroll
-      for (int cc = 0; cc < 4; ++cc)
-#pragma unroll
-        for (int r = 0; r < kSfR; ++r) wv[cc][r] = a.w[(4 * c4 + cc) * kSfK + kSfR * l + r];
-      for (int j = g; j < n; j += NG) {
-        const float* rr = a.radial + static_cast<int64_t>(r0 + j) * kSfK + kSfR * l;
+    if (pthr) {
+      const int l = pl, c4 = pc4;
+      for (int j = pg; j < n; j += NG) {
+        const float* rr = RS + j * kSfK + kSfR * l;
         float rv[kSfR];
 #pragma unroll
         for (int r = 0; r < kSfR; ++r) rv[r] = rr[r];
@@ -361,7 +374,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const Fw
   }
 }
 
-constexpr size_t fwd_sf_lds(int n) { return static_cast<size_t>(n) * (2 + kSfL) * kCD * 4; }
+constexpr size_t fwd_sf_lds(int n) { return static_cast<size_t>(n) * ((2 + kSfL) * kCD + kSfK) * 4; }
 
 template <int LPH>
 int fwd_sf_launch(const FwdSfArgs& a, bool edge, int max_degree, hipStream_t st) {
@@ -418,6 +431,7 @@ struct BwdCenterArgs {
   const int32_t* src_row;
   const float *sp, *alpha, *smax, *sden, *dout, *y;
   const int32_t *atom_rowptr, *edge_rev, *rev_trip;
+  const int32_t* order;  // workgroup -> center atom (NULL: blockIdx.x)
   int64_t n_atoms, T;
   int H;
   float inv_sqrt_c;
@@ -436,7 +450,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
   CTR(0);
   constexpr int H = 32 / LPH;
   extern __shared__ cf4 lds[];
-  const int64_t b = blockIdx.x;
+  const int64_t b = a.order ? static_cast<int64_t>(a.order[blockIdx.x]) : static_cast<int64_t>(blockIdx.x);
   const int r0 = uniform(a.atom_rowptr[b]);
   const int n = uniform(a.atom_rowptr[b + 1]) - r0;
   const int tid = threadIdx.x;
@@ -666,7 +680,8 @@ X2G_API size_t x2g_sbf_attention_bwd_center_lds(int32_t max_degree, int32_t head
 X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const float* v, const float* edge,
                                          const int32_t* src_row, int edge_mode, const float* sbfproj,
                                          const float* sph_y, const int32_t* atom_rowptr, const int32_t* edge_rev,
-                                         const int32_t* rev_trip, const float* alpha_raw, const float* seg_max,
+                                         const int32_t* rev_trip, const int32_t* atom_order, const float* alpha_raw,
+                                         const float* seg_max,
                                          const float* seg_den, const float* dout, int64_t num_atoms,
                                          int32_t max_degree, int64_t num_edges, int64_t num_triplets, int32_t heads,
                                          int32_t channels, float* dq, float* dk, float* dv, float* radial_grad,
@@ -691,7 +706,7 @@ X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const f
   BwdCenterArgs a{};
   a.q = q; a.k = k; a.v = v; a.edge = edge; a.src_row = src_row; a.sp = sbfproj; a.alpha = alpha_raw;
   a.smax = seg_max; a.sden = seg_den; a.dout = dout; a.y = sph_y; a.atom_rowptr = atom_rowptr; a.edge_rev = edge_rev;
-  a.rev_trip = rev_trip; a.n_atoms = num_atoms; a.T = num_triplets; a.H = heads;
+  a.rev_trip = rev_trip; a.order = atom_order; a.n_atoms = num_atoms; a.T = num_triplets; a.H = heads;
   a.inv_sqrt_c = static_cast<float>(1.0 / sqrt(static_cast<double>(channels)));
   a.dq = dq; a.dk = dk; a.dv = dv; a.gfold = radial_grad; a.d_edge = d_edge_atom; a.gw = g_work;
   const int md = max_degree > 0 ? max_degree : 1;
@@ -709,7 +724,8 @@ X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const f
 X2G_API int x2g_sbf_attention_fwd_center(const float* q, const float* k, const float* v, const float* skip,
                                          const float* edge, const int32_t* src_row, int edge_mode,
                                          const float* sbfproj, int64_t t_base, const int32_t* atom_rowptr,
-                                         const int32_t* edge_rev, const int32_t* rev_trip, int64_t atom0,
+                                         const int32_t* edge_rev, const int32_t* rev_trip, const int32_t* atom_order,
+                                         int64_t atom0,
                                          int64_t n_atoms, int32_t max_degree, int64_t num_edges,
                                          int64_t num_triplets, int32_t heads, int32_t channels, float* out,
                                          float* alpha_raw, float* seg_max, float* seg_den, float* row_stats,
@@ -731,8 +747,8 @@ X2G_API int x2g_sbf_attention_fwd_center(const float* q, const float* k, const f
     return X2G_EUNSUPPORTED;
   FwdCenterArgs a{};
   a.q = q; a.k = k; a.v = v; a.skip = skip; a.edge = edge; a.src_row = src_row; a.sp = sbfproj; a.t_base = t_base;
-  a.atom_rowptr = atom_rowptr; a.edge_rev = edge_rev; a.rev_trip = rev_trip; a.atom0 = atom0; a.n_atoms = n_atoms;
-  a.H = heads; a.sqrt_c = static_cast<float>(sqrt(static_cast<double>(channels)));
+  a.atom_rowptr = atom_rowptr; a.edge_rev = edge_rev; a.rev_trip = rev_trip; a.order = atom_order; a.atom0 = atom0;
+  a.n_atoms = n_atoms; a.H = heads; a.sqrt_c = static_cast<float>(sqrt(static_cast<double>(channels)));
   a.out = out; a.alpha = alpha_raw; a.smax = seg_max; a.sden = seg_den;
   a.row_stats = reinterpret_cast<float2*>(row_stats);
   const int md = max_degree > 0 ? max_degree : 1;
@@ -751,7 +767,8 @@ X2G_API int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, cons
                                             const float* edge, const int32_t* src_row, int edge_mode,
                                             const float* radial, const float* sph_y, const float* w_sbf,
                                             const float* b_sbf, const int32_t* atom_rowptr, const int32_t* edge_rev,
-                                            const int32_t* rev_trip, int64_t atom0, int64_t n_atoms,
+                                            const int32_t* rev_trip, const int32_t* atom_order, int64_t atom0,
+                                            int64_t n_atoms,
                                             int32_t max_degree, int64_t num_edges, int64_t num_triplets, int32_t heads,
                                             int32_t channels, float* out, float* alpha_raw, float* seg_max,
                                             float* seg_den, float* row_stats, float* sbfproj_out, void* stream) {
@@ -774,7 +791,7 @@ X2G_API int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, cons
   FwdSfArgs a{};
   a.q = q; a.k = k; a.v = v; a.skip = skip; a.edge = edge; a.src_row = src_row; a.radial = radial; a.y = sph_y;
   a.w = w_sbf; a.bias = b_sbf; a.atom_rowptr = atom_rowptr; a.edge_rev = edge_rev; a.rev_trip = rev_trip;
-  a.atom0 = atom0; a.n_atoms = n_atoms; a.H = heads;
+  a.order = atom_order; a.atom0 = atom0; a.n_atoms = n_atoms; a.H = heads;
   a.sqrt_c = static_cast<float>(sqrt(static_cast<double>(channels)));
   a.out = out; a.alpha = alpha_raw; a.smax = seg_max; a.sden = seg_den; a.sp = sbfproj_out;
   a.row_stats = reinterpret_cast<float2*>(row_stats);

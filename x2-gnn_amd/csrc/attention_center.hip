@@ -54,6 +54,7 @@ struct FwdCenterArgs {
   const float* sp;         // S rows, row t - t_base
   int64_t t_base;
   const int32_t *atom_rowptr, *edge_rev, *rev_trip;
+  const int32_t* order;  // workgroup -> center atom (NULL: atom0 + blockIdx.x)
   int64_t atom0, n_atoms;
   int H;
   float sqrt_c;
@@ -64,7 +65,9 @@ struct FwdCenterArgs {
 template <int LPH, int WAVES, int B, bool EDGE>
 __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_kernel(const FwdCenterArgs a) {
   extern __shared__ cf4 lds[];  // [n][32] (k + e), then [n][32] (v + e)
-  const int64_t b = a.atom0 + blockIdx.x;
+  // (the host orders the atoms by decreasing degree: the longest blocks start first, the short ones fill the
+  // tail of the launch)
+  const int64_t b = a.order ? static_cast<int64_t>(a.order[a.atom0 + blockIdx.x]) : a.atom0 + blockIdx.x;
   const int r0 = uniform(a.atom_rowptr[b]);
   const int n = uniform(a.atom_rowptr[b + 1]) - r0;
   if (n <= 0) return;  // (workgroup-uniform: no barrier is skipped by a part of it)
@@ -183,6 +186,7 @@ struct FwdSfArgs {
   const int32_t* src_row;
   const float *radial, *y, *w, *bias;  // rbf_env [E, 42], Y [T, 8], lin_sbf weight [128, 42] and bias [128]
   const int32_t *atom_rowptr, *edge_rev, *rev_trip;
+  const int32_t* order;  // workgroup -> center atom (NULL: atom0 + blockIdx.x)
   int64_t atom0, n_atoms;
   int H;
   float sqrt_c;
@@ -197,7 +201,9 @@ constexpr int kSfK = kSfL * kSfR;        // 42
 template <int LPH, int WAVES, int B, bool EDGE>
 __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const FwdSfArgs a) {
   extern __shared__ cf4 lds[];  // [n][32] (k + e), [n][32] (v + e), [n][7][32] P, [n][42] R
-  const int64_t b = a.atom0 + blockIdx.x;
+  // (the host orders the atoms by decreasing degree: the longest blocks start first, the short ones fill the
+  // tail of the launch)
+  const int64_t b = a.order ? static_cast<int64_t>(a.order[a.atom0 + blockIdx.x]) : a.atom0 + blockIdx.x;
   const int r0 = uniform(a.atom_rowptr[b]);
   const int n = uniform(a.atom_rowptr[b + 1]) - r0;
   if (n <= 0) return;  // (workgroup-uniform)
@@ -411,6 +417,7 @@ struct BwdCenterArgs {
   const int32_t* src_row;
   const float *sp, *alpha, *smax, *sden, *dout, *y;
   const int32_t *atom_rowptr, *edge_rev, *rev_trip;
+  const int32_t* order;  // workgroup -> center atom (NULL: blockIdx.x)
   int64_t n_atoms, T;
   int H;
   float inv_sqrt_c;
@@ -428,7 +435,7 @@ template <int LPH, int WAVES, int B, bool EDGE>
 __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCenterArgs a) {
   constexpr int H = 32 / LPH;
   extern __shared__ cf4 lds[];
-  const int64_t b = blockIdx.x;
+  const int64_t b = a.order ? static_cast<int64_t>(a.order[blockIdx.x]) : static_cast<int64_t>(blockIdx.x);
   const int r0 = uniform(a.atom_rowptr[b]);
   const int n = uniform(a.atom_rowptr[b + 1]) - r0;
   const int tid = threadIdx.x;
@@ -652,7 +659,8 @@ X2G_API size_t x2g_sbf_attention_bwd_center_lds(int32_t max_degree, int32_t head
 X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const float* v, const float* edge,
                                          const int32_t* src_row, int edge_mode, const float* sbfproj,
                                          const float* sph_y, const int32_t* atom_rowptr, const int32_t* edge_rev,
-                                         const int32_t* rev_trip, const float* alpha_raw, const float* seg_max,
+                                         const int32_t* rev_trip, const int32_t* atom_order, const float* alpha_raw,
+                                         const float* seg_max,
                                          const float* seg_den, const float* dout, int64_t num_atoms,
                                          int32_t max_degree, int64_t num_edges, int64_t num_triplets, int32_t heads,
                                          int32_t channels, float* dq, float* dk, float* dv, float* radial_grad,
@@ -677,7 +685,7 @@ X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const f
   BwdCenterArgs a{};
   a.q = q; a.k = k; a.v = v; a.edge = edge; a.src_row = src_row; a.sp = sbfproj; a.alpha = alpha_raw;
   a.smax = seg_max; a.sden = seg_den; a.dout = dout; a.y = sph_y; a.atom_rowptr = atom_rowptr; a.edge_rev = edge_rev;
-  a.rev_trip = rev_trip; a.n_atoms = num_atoms; a.T = num_triplets; a.H = heads;
+  a.rev_trip = rev_trip; a.order = atom_order; a.n_atoms = num_atoms; a.T = num_triplets; a.H = heads;
   a.inv_sqrt_c = static_cast<float>(1.0 / sqrt(static_cast<double>(channels)));
   a.dq = dq; a.dk = dk; a.dv = dv; a.gfold = radial_grad; a.d_edge = d_edge_atom; a.gw = g_work;
   const int md = max_degree > 0 ? max_degree : 1;
@@ -695,7 +703,8 @@ X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const f
 X2G_API int x2g_sbf_attention_fwd_center(const float* q, const float* k, const float* v, const float* skip,
                                          const float* edge, const int32_t* src_row, int edge_mode,
                                          const float* sbfproj, int64_t t_base, const int32_t* atom_rowptr,
-                                         const int32_t* edge_rev, const int32_t* rev_trip, int64_t atom0,
+                                         const int32_t* edge_rev, const int32_t* rev_trip, const int32_t* atom_order,
+                                         int64_t atom0,
                                          int64_t n_atoms, int32_t max_degree, int64_t num_edges,
                                          int64_t num_triplets, int32_t heads, int32_t channels, float* out,
                                          float* alpha_raw, float* seg_max, float* seg_den, float* row_stats,
@@ -717,8 +726,8 @@ X2G_API int x2g_sbf_attention_fwd_center(const float* q, const float* k, const f
     return X2G_EUNSUPPORTED;
   FwdCenterArgs a{};
   a.q = q; a.k = k; a.v = v; a.skip = skip; a.edge = edge; a.src_row = src_row; a.sp = sbfproj; a.t_base = t_base;
-  a.atom_rowptr = atom_rowptr; a.edge_rev = edge_rev; a.rev_trip = rev_trip; a.atom0 = atom0; a.n_atoms = n_atoms;
-  a.H = heads; a.sqrt_c = static_cast<float>(sqrt(static_cast<double>(channels)));
+  a.atom_rowptr = atom_rowptr; a.edge_rev = edge_rev; a.rev_trip = rev_trip; a.order = atom_order; a.atom0 = atom0;
+  a.n_atoms = n_atoms; a.H = heads; a.sqrt_c = static_cast<float>(sqrt(static_cast<double>(channels)));
   a.out = out; a.alpha = alpha_raw; a.smax = seg_max; a.sden = seg_den;
   a.row_stats = reinterpret_cast<float2*>(row_stats);
   const int md = max_degree > 0 ? max_degree : 1;
@@ -737,7 +746,8 @@ X2G_API int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, cons
                                             const float* edge, const int32_t* src_row, int edge_mode,
                                             const float* radial, const float* sph_y, const float* w_sbf,
                                             const float* b_sbf, const int32_t* atom_rowptr, const int32_t* edge_rev,
-                                            const int32_t* rev_trip, int64_t atom0, int64_t n_atoms,
+                                            const int32_t* rev_trip, const int32_t* atom_order, int64_t atom0,
+                                            int64_t n_atoms,
                                             int32_t max_degree, int64_t num_edges, int64_t num_triplets, int32_t heads,
                                             int32_t channels, float* out, float* alpha_raw, float* seg_max,
                                             float* seg_den, float* row_stats, float* sbfproj_out, void* stream) {
@@ -760,7 +770,7 @@ X2G_API int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, cons
   FwdSfArgs a{};
   a.q = q; a.k = k; a.v = v; a.skip = skip; a.edge = edge; a.src_row = src_row; a.radial = radial; a.y = sph_y;
   a.w = w_sbf; a.bias = b_sbf; a.atom_rowptr = atom_rowptr; a.edge_rev = edge_rev; a.rev_trip = rev_trip;
-  a.atom0 = atom0; a.n_atoms = n_atoms; a.H = heads;
+  a.order = atom_order; a.atom0 = atom0; a.n_atoms = n_atoms; a.H = heads;
   a.sqrt_c = static_cast<float>(sqrt(static_cast<double>(channels)));
   a.out = out; a.alpha = alpha_raw; a.smax = seg_max; a.sden = seg_den; a.sp = sbfproj_out;
   a.row_stats = reinterpret_cast<float2*>(row_stats);

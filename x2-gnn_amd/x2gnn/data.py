@@ -195,7 +195,10 @@ def _add_device_indices(b, nodes, edges):
     b._store["_x2g_src_type"] = torch.from_numpy(b._store["x"].numpy()[ei_np[0]].astype(np.int32))
     b._store["_x2g_atom_type"] = torch.from_numpy(b._store["x"].numpy().reshape(-1).astype(np.int32))
     b._store["_x2g_symmetric"] = _is_symmetric(ei_np, int(nodes.sum()))
-    b._store["_x2g_max_degree"] = int(np.bincount(ei_np[0]).max()) if ei_np.shape[1] else 0
+    deg = np.bincount(ei_np[0], minlength=int(nodes.sum()))
+    b._store["_x2g_max_degree"] = int(deg.max()) if deg.size else 0
+    # the center-atom kernels' launch order: atoms by decreasing degree (the longest blocks first)
+    b._store["_x2g_center_order"] = torch.from_numpy(np.argsort(-deg, kind="stable").astype(np.int32))
 
 
 def _is_symmetric(ei, n):

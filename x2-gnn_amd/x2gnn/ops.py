@@ -96,6 +96,7 @@ class LineGraph:
         # element row (int32 [N]: the key of the center-atom edge-term gradient)
         self.max_degree = None
         self.atom_type = None
+        self.center_order = None  # int32 [N]: atoms by decreasing degree (the center kernels' launch order)
         if with_transpose and self.symmetric:
             self._src_rowptr = torch.empty(self.E + 1, **i32)
             self._src_perm = torch.empty(self.T, **i32)
@@ -130,7 +131,7 @@ class LineGraph:
         lg._src_rowptr = lg._src_perm = lg._src_dst = None
         lg.dst_type = lg.src_type = None
         lg.symmetric = False
-        lg.edge_rev = lg.rev_trip = lg.max_degree = lg.atom_type = None
+        lg.edge_rev = lg.rev_trip = lg.max_degree = lg.atom_type = lg.center_order = None
         ws_bytes = int(_lib.load().x2g_vertex_to_edge_workspace(lg.E, 0))
         lg._ws = torch.empty(ws_bytes, dtype=torch.uint8, device=lg.trip_src.device)
         return lg
@@ -381,8 +382,8 @@ class _SBFAttention(torch.autograd.Function):
             sproj = torch.empty(T, D, dtype=torch.float32, device=dev) if any(ctx.needs_input_grad) else None
             call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(src_row),
                  edge_mode, ptr(factors[0]), ptr(factors[1]), ptr(w_sbf), ptr(b_sbf), ptr(lg.atom_rowptr),
-                 ptr(lg.edge_rev), ptr(lg.rev_trip), 0, lg.N, lg.max_degree, E, T, heads, channels, ptr(out),
-                 ptr(alpha), ptr(smax), ptr(sden), ptr(rstats), ptr(sproj), stream_ptr())
+                 ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order), 0, lg.N, lg.max_degree, E, T, heads,
+                 channels, ptr(out), ptr(alpha), ptr(smax), ptr(sden), ptr(rstats), ptr(sproj), stream_ptr())
         else:
             # S = lin_sbf(sbf) once per layer [T, D], right before this layer's attention (so it is still
             # in the MALL when the attention kernels read its rows: sbf pointer = S, weight pointer NULL)
@@ -391,9 +392,9 @@ class _SBFAttention(torch.autograd.Function):
             call("x2g_sbf_project", ptr(sbf), T, sbf.shape[1], ptr(w_sbf), ptr(b_sbf), D, ptr(sproj), stream_ptr())
             if center:
                 call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(src_row),
-                     edge_mode, ptr(sproj), 0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), 0, lg.N,
-                     lg.max_degree, E, T, heads, channels, ptr(out), ptr(alpha), ptr(smax), ptr(sden), ptr(rstats),
-                     stream_ptr())
+                     edge_mode, ptr(sproj), 0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip),
+                     ptr(lg.center_order), 0, lg.N, lg.max_degree, E, T, heads, channels, ptr(out), ptr(alpha),
+                     ptr(smax), ptr(sden), ptr(rstats), stream_ptr())
             else:
                 call("x2g_sbf_attention_fwd_stats" if rstats is not None else "x2g_sbf_attention_fwd", ptr(q),
                      ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(edge_row), edge_mode, ptr(sproj), None, None,
@@ -474,7 +475,8 @@ class _SBFAttention(torch.autograd.Function):
             d_edge_atom = torch.empty(lg.N, D, dtype=torch.float32, device=dev) if want_edge else None
             g_work = torch.empty(T, heads, dtype=torch.float32, device=dev)
             call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(src_row), mode, ptr(sproj),
-                 ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(alpha), ptr(smax), ptr(sden),
+                 ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order), ptr(alpha),
+                 ptr(smax), ptr(sden),
                  ptr(dout), lg.N, lg.max_degree, E, T, heads, channels, ptr(dq), ptr(dk), ptr(dv), ptr(gfold),
                  ptr(d_edge_atom), ptr(g_work), st)
             d_edge = None
@@ -948,7 +950,7 @@ def _attention_fwd_tiled(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, 
              ptr(b_sbf), D, ptr(S), st)
         if center:  # whole molecules: the tile's atoms own exactly its triplets (S rows t - ta)
             call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(src_row), edge_mode,
-                 ptr(S), ta, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), atoms[0], atoms[1] - atoms[0],
+                 ptr(S), ta, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), None, atoms[0], atoms[1] - atoms[0],
                  lg.max_degree, E, T, heads, channels, ptr(out), ptr(alpha), ptr(smax), ptr(sden), ptr(rstats), st)
             continue
         # the kernel reads S at absolute triplet indices t in [t0, t1): hand it the base S - ta rows;

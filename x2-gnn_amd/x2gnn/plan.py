@@ -70,6 +70,7 @@ class GraphPlan:
             p.line_ptr, p.mol_ptr, p.dst_type = st["_x2g_line_ptr"], st["_x2g_mol_ptr"], st["_x2g_dst_type"]
             src_type = st.get("_x2g_src_type")
             p.lg.atom_type = st.get("_x2g_atom_type")
+            p.lg.center_order = st.get("_x2g_center_order")
         else:
             p.lg = ops.vertex_to_edge(ei, p.num_atoms, p.num_triplets, meta.get("symmetric", False))
             p.line_ptr = _ptr_from_counts(data.edge_num, p.num_graphs, dev)
