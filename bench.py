@@ -185,7 +185,7 @@ def attention_probe(model, batch, reps):
     center, src_row = ops._center_rows(lg, ops.EDGE_PER_DST, row, D, C)
     center_bwd = center and ops._CENTER_BWD and lg.atom_type is not None
     atom_de = torch.empty(lg.N, D, **f32)
-    g_work = torch.empty(T, H, **f32)
+    g_work = torch.empty(2, T, H, **f32)
 
     def fwd_center():  # the model's forward on a symmetric line graph (csrc/attention_center.hip)
         call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(src_row),

@@ -300,8 +300,8 @@ int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, const float*
 /* The whole attention backward over a SYMMETRIC line graph in ONE launch, one workgroup per center atom
  * (csrc/attention_center.hip): the block's rows (k + e of its sources, dout and q of its destinations,
  * their softmax max / denominator) staged in LDS, then per source j a pass over its triplets' S rows,
- * alpha and Y (dv, the folded lin_sbf gradient G, g_t into the g_work [T, heads] scratch), rho per
- * destination, and dk, dq.  Replaces x2g_sbf_attention_bwd_dst_g + x2g_sbf_attention_bwd_src_fold on such
+ * alpha (dv, and a_t, g_t into the g_work [2, T, heads] scratch), rho per destination, and per source /
+ * destination dk, the folded lin_sbf gradient G (from Y) and dq.  Replaces x2g_sbf_attention_bwd_dst_g + x2g_sbf_attention_bwd_src_fold on such
  * graphs (same dq, dk, dv, radial_grad = G [E, 8, HC]; fp32 rounding apart), reading S once instead of
  * twice and no row gathers; d_edge_atom [num_atoms, HC] (or NULL) = the per-CENTER-ATOM gradient of the
  * edge term (sum over the atom's sources of dk + dv): the element-table gradient is its keyed sum by

@@ -48,7 +48,7 @@ call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(tabl
      H, C,
      ptr(out), ptr(alpha), ptr(smax), ptr(sden), None, stream_ptr())
 dq, dk, dv = (torch.empty(E, D, **f) for _ in range(3))
-G, de, gw = torch.empty(E, 8, D, **f), torch.empty(n, D, **f), torch.empty(T, H, **f)
+G, de, gw = torch.empty(E, 8, D, **f), torch.empty(n, D, **f), torch.empty(2, T, H, **f)
 lib = _lib.load()
 lib.x2g_ctrace_fetch.argtypes = [ctypes.c_void_p, ctypes.c_int]
 ev = []

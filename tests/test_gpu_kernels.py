@@ -2000,7 +2000,7 @@ def _bwd_both(lg, q, k, v, S, table, mode, heads, channels, seed):
          mode, ptr(S), ptr(y), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order), ptr(alpha),
          ptr(smax), ptr(sden),
          ptr(dout), lg.N, lg.max_degree, E, T, heads, channels, ptr(dq), ptr(dk), ptr(dv), ptr(G), ptr(de_atom),
-         ptr(torch.empty(T, H, **f)), stream_ptr())
+         ptr(torch.empty(2, T, H, **f)), stream_ptr())
     c = [dq, dk, dv, G]
     if edge is not None:
         c.append(torch.zeros(rows, D, dtype=torch.float64, device=q.device).index_add_(0, lg.atom_type.long(), de_atom.double()))

@@ -473,7 +473,7 @@ class _SBFAttention(torch.autograd.Function):
             # gradient comes per center atom and is summed by the atoms' elements
             want_edge = mode == EDGE_PER_DST and ctx.needs_input_grad[4]
             d_edge_atom = torch.empty(lg.N, D, dtype=torch.float32, device=dev) if want_edge else None
-            g_work = torch.empty(T, heads, dtype=torch.float32, device=dev)
+            g_work = torch.empty(2, T, heads, dtype=torch.float32, device=dev)
             call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(src_row), mode, ptr(sproj),
                  ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order), ptr(alpha),
                  ptr(smax), ptr(sden),
