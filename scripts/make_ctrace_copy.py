@@ -33,10 +33,9 @@ def after(s, start, marker, text):
     return s[:j] + text + s[j:]
 
 
-s = after(s, i, "  __syncthreads();\n  // ---- pass 1", "")
-j = s.index("  __syncthreads();\n  // ---- pass 1", i)
-s = s[:j] + "  __syncthreads();\n  CTR(1);\n  // ---- pass 1" + s[j + len("  __syncthreads();\n  // ---- pass 1"):]
-j = s.index("  // the g scratch written by every owner is read by others below", i)
+s = after(s, i, "  __syncthreads();\n  const int nt = n - 1;  // triplets per destination (and per source)\n",
+          "  CTR(1);\n")
+j = s.index("  // the scratch written by every owner is read by others below", i)
 s = s[:j] + "  CTR(2);\n" + s[j:]
 s = after(s, i, "  __threadfence_block();\n  __syncthreads();\n", "  CTR(3);\n")
 s = after(s, i, "    if (leader) RHO[i * H + head] = rho;\n  }\n  __syncthreads();\n", "  CTR(4);\n")
