@@ -416,16 +416,17 @@ int fwd_center_launch(const FwdCenterArgs& a, bool edge, int max_degree, hipStre
 //   KE[j] = k_j + e, GO[i] = dout[d_i], QI[i] = q[d_i], per-destination max / 1 / (den + eps);
 // pass 1, one owner per SOURCE j (its S rows t(i, j) = TB[i] + j - [j > i], one 512-byte row each):
 //   at = exp(alpha_t - max_i) / (den_i + eps),  g_t = sum over the head of go_i (v_j + e) S_t,
-//   dv_j += at go_i S_t,  G_j[l] += at go_i (v_j + e) Y_l(t)  (the folded lin_sbf gradient),
-//   g_t into a [T, H] scratch (L2-resident until the same workgroup reads it back);
+//   dv_j += at go_i S_t,  and (at, g_t) into a [2, T, H] scratch (L2-resident until the same workgroup
+//   reads it back);
 // then rho_i = sum_j at g (j ascending: the destination pass's order) over destination i's contiguous
-// block, and pass 2 (at recomputed from alpha, g from the scratch, rows from LDS):
-//   w = at (g - rho_i) / sqrt(C),  dk_j = sum_i w q_i (owner j),  dq_i = sum_j w (k_j + e) (owner i),
+// block, and pass 2 (at, g from the scratch, Y_t, rows from LDS), per owner both roles:
+//   w = at (g - rho_i) / sqrt(C),  dk_j = sum_i w q_i,  G_j[l] = sum_i at go_i (v_j + e) Y_l(t)  (source j:
+//   the folded lin_sbf gradient),  dq_i = sum_j w (k_j + e)  (destination i),
 // and, for the element-table gradient, d_edge[b] = sum_j (dk_j + dv_j) (X2-GNN's edge term enters as
-// k_j + e and v_j + e with e the center atom's row: its gradient is the block's sum).  S and Y are read
-// once per backward (the two destination-major passes read S twice and gather k / v / q / dout rows per
-// triplet from L2).  LDS holds only the block's rows (3 n x 512 B + n x 200 B), so at config 2's
-// largest degree (17) four workgroups share a CU.
+// k_j + e and v_j + e with e the center atom's row: its gradient is the block's sum).  S is read once per
+// backward (the two destination-major passes read S twice and gather k / v / q / dout rows per triplet
+// from L2), only pass 1 holds S rows and only pass 2 the 32 G accumulators, so both take 8 triplets per
+// memory round trip within 128 VGPRs.
 struct BwdCenterArgs {
   const float *q, *k, *v, *edge;
   const int32_t* src_row;
@@ -435,12 +436,12 @@ struct BwdCenterArgs {
   int64_t n_atoms, T;
   int H;
   float inv_sqrt_c;
-  float *dq, *dk, *dv, *gfold, *d_edge, *gw;
+  float *dq, *dk, *dv, *gfold, *d_edge, *gw;  // gw: [2, T, H] scratch (g, then a)
 };
 
 template <int H>
 __host__ __device__ constexpr size_t bwd_center_lds(int n) {
-  return static_cast<size_t>(n) * 3 * kCD * 4  // KE, GO, QI
+  return static_cast<size_t>(n) * 4 * kCD * 4  // KE, GO, QI, DE
          + static_cast<size_t>(n) * H * 4 * 3  // MX, IV, RHO
          + static_cast<size_t>(n) * 4 * 2;     // TB, DI
 }
@@ -467,7 +468,8 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
   cf4* KE = lds;
   cf4* GO = KE + n * 32;
   cf4* QI = GO + n * 32;
-  float* MX = reinterpret_cast<float*>(QI + n * 32);
+  cf4* DE = QI + n * 32;
+  float* MX = reinterpret_cast<float*>(DE + n * 32);
   float* IV = MX + n * H;
   float* RHO = IV + n * H;
   int* TB = reinterpret_cast<int*>(RHO + n * H);
@@ -493,9 +495,8 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
     DI[idx] = a.edge_rev[r0 + idx];
   }
   __syncthreads();
-  CTR(1);
-  // ---- pass 1: one owner per source j
   const int nt = n - 1;  // triplets per destination (and per source)
+  CTR(1);
   auto rsrc = [](const void* p, int64_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), static_cast<short>(0),
                                              static_cast<int>(bytes < 0x7fffffff ? bytes : 0x7fffffff), 0x00020000);
@@ -504,34 +505,35 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
   const __amdgpu_buffer_rsrc_t al_r = rsrc(a.alpha, a.T * H * 4);
   const __amdgpu_buffer_rsrc_t y_r = rsrc(a.y, a.T * 8 * 4);
   const __amdgpu_buffer_rsrc_t g_r = rsrc(a.gw, a.T * H * 4);
+  const __amdgpu_buffer_rsrc_t at_r = rsrc(a.gw + a.T * H, a.T * H * 4);
+  float* const aw = a.gw + a.T * H;
   auto ldf = [](__amdgpu_buffer_rsrc_t r, int off) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
   };
+  // the triplet of destination i and source j (i != j; i == j gives some row of i's block, unused)
+  auto trip = [&](int i, int j) {
+    int pos = j - (j > i ? 1 : 0);
+    pos = pos < nt ? pos : nt - 1;
+    return TB[i] + pos;  // (32-bit offsets below: T * 512 < 2^31, checked)
+  };
+  // ---- pass 1: one owner per source j: at, g (to the scratch), dv
   for (int j = owner; j < n; j += NO) {
     const int64_t srow = static_cast<int64_t>(r0 + j) * kCD + c0;
     cf4 ue = ld4(a.v + srow);
     if (EDGE) ue += ld4(a.edge + e_row + c0);
     cf4 dv = {0.f, 0.f, 0.f, 0.f};
-    cf4 G[8];
-#pragma unroll
-    for (int l = 0; l < 8; ++l) G[l] = cf4{0.f, 0.f, 0.f, 0.f};
     auto batch = [&](int i0, auto bb) {
       constexpr int BB = decltype(bb)::value;
       cf4 sv[BB];
-      float al[BB], yv[BB];
+      float al[BB];
       int tt[BB];
 #pragma unroll
       for (int u = 0; u < BB; ++u) {
         const int i = i0 + u < n ? i0 + u : n - 1;  // clamped: loads unconditional, masked below
-        int pos = j - (j > i ? 1 : 0);               // (i == j: some row of i's block, unused)
-        pos = pos < nt ? pos : nt - 1;
-        const int t = TB[i] + pos;                   // (32-bit buffer offsets: T * 512 < 2^31, checked)
-        tt[u] = t;
-        sv[u] = __builtin_bit_cast(cf4, __builtin_amdgcn_raw_buffer_load_b128(sp_r, t * (kCD * 4) + c0 * 4, 0, 0));
-        al[u] = ldf(al_r, (t * H + head) * 4);
-        yv[u] = ldf(y_r, (t * 8 + (l32 & 7)) * 4);
+        tt[u] = trip(i, j);
+        sv[u] = __builtin_bit_cast(cf4, __builtin_amdgcn_raw_buffer_load_b128(sp_r, tt[u] * (kCD * 4) + c0 * 4, 0, 0));
+        al[u] = ldf(al_r, (tt[u] * H + head) * 4);
       }
-      // per triplet: at, g (to the scratch), dv; sv[u] becomes dS = go (v + e) at
 #pragma unroll
       for (int u = 0; u < BB; ++u) {
         const int i = i0 + u < n ? i0 + u : n - 1;
@@ -544,15 +546,79 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
         gp = fmaf(gu[2], sv[u][2], gp);
         gp = fmaf(gu[3], sv[u][3], gp);
         const float g = head_sum<LPH>(gp);
-        if (ok && leader) a.gw[static_cast<int64_t>(tt[u]) * H + head] = g;
+        if (ok && leader) {
+          a.gw[static_cast<int64_t>(tt[u]) * H + head] = g;
+          aw[static_cast<int64_t>(tt[u]) * H + head] = at;
+        }
         dv += at * (go * sv[u]);
-        sv[u] = gu * at;
-        __builtin_amdgcn_sched_barrier(0);
       }
-      // G[l] += dS Y_l(t): Y_l handed to the half's lanes by row_newbcast (both 16-lane rows of a half
-      // loaded the same triplet's Y row, one value per lane)
+    };
+    if (nt > 0) {  // (workgroup-uniform)
+      int i0 = 0;
+      for (; n - i0 > B / 2; i0 += B) batch(i0, std::integral_constant<int, B>{});
+      if (i0 < n) batch(i0, std::integral_constant<int, B / 2>{});
+    }
+    st4(a.dv + srow, dv);
+    DE[j * 32 + l32] = dv;  // (the edge term's gradient: dk added in pass 2)
+  }
+  CTR(2);
+  // the scratch written by every owner is read by others below: workgroup-scope release / acquire
+  __threadfence_block();
+  __syncthreads();
+  CTR(3);
+  // ---- rho_i = sum_{j != i} at g over i's contiguous block, j ascending (one owner per destination)
+  for (int i = owner; i < n; i += NO) {
+    float rho = 0.f;
+    for (int p0 = 0; p0 < nt; p0 += 8) {
+      float at[8], g[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int t = TB[i] + (p0 + u < nt ? p0 + u : nt - 1);
+        at[u] = ldf(at_r, (t * H + head) * 4);
+        g[u] = ldf(g_r, (t * H + head) * 4);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (p0 + u < nt) rho = fmaf(at[u], g[u], rho);
+    }
+    if (leader) RHO[i * H + head] = rho;
+  }
+  __syncthreads();
+  CTR(4);
+  // ---- pass 2, owner o in both roles, x over the other n - 1:
+  //   source j = o (destinations i = x): dk_o, G_o;  destination i = o (sources j = x): dq_o
+  for (int o = owner; o < n; o += NO) {
+    const int64_t srow = static_cast<int64_t>(r0 + o) * kCD + c0;
+    cf4 ue = ld4(a.v + srow);
+    if (EDGE) ue += ld4(a.edge + e_row + c0);
+    cf4 dk = {0.f, 0.f, 0.f, 0.f}, dq = {0.f, 0.f, 0.f, 0.f};
+    cf4 G[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) G[l] = cf4{0.f, 0.f, 0.f, 0.f};
+    const float rho_o = RHO[o * H + head];
+    auto batch = [&](int x0, auto bb) {
+      constexpr int BB = decltype(bb)::value;
+      float ats[BB], gs[BB], yv[BB], atd[BB], gd[BB];
 #pragma unroll
       for (int u = 0; u < BB; ++u) {
+        const int x = x0 + u < n ? x0 + u : n - 1;
+        const int ts = trip(x, o), td = trip(o, x);
+        ats[u] = ldf(at_r, (ts * H + head) * 4);
+        gs[u] = ldf(g_r, (ts * H + head) * 4);
+        yv[u] = ldf(y_r, (ts * 8 + (l32 & 7)) * 4);
+        atd[u] = ldf(at_r, (td * H + head) * 4);
+        gd[u] = ldf(g_r, (td * H + head) * 4);
+      }
+#pragma unroll
+      for (int u = 0; u < BB; ++u) {
+        const int x = x0 + u < n ? x0 + u : n - 1;
+        const bool ok = x0 + u < n && x != o;
+        const float as = ok ? ats[u] : 0.f, ad = ok ? atd[u] : 0.f;
+        const float ws = as * (gs[u] - RHO[x * H + head]) * a.inv_sqrt_c;
+        dk += ws * QI[x * 32 + l32];
+        const float wd = ad * (gd[u] - rho_o) * a.inv_sqrt_c;
+        dq += wd * KE[x * 32 + l32];
+        const cf4 ds = (GO[x * 32 + l32] * ue) * as;
         float yl[8];
         yl[0] = dpp_mov<0x150>(yv[u]);
         yl[1] = dpp_mov<0x151>(yv[u]);
@@ -563,84 +629,27 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
         yl[6] = dpp_mov<0x156>(yv[u]);
         yl[7] = dpp_mov<0x157>(yv[u]);
 #pragma unroll
-        for (int l = 0; l < 8; ++l) G[l] += sv[u] * yl[l];
-        __builtin_amdgcn_sched_barrier(0);
+        for (int l = 0; l < 8; ++l) G[l] += ds * yl[l];
       }
     };
-    if (nt > 0) {  // (workgroup-uniform)
-      int i0 = 0;
-      for (; n - i0 > B / 2; i0 += B) batch(i0, std::integral_constant<int, B>{});
-      if (i0 < n) batch(i0, std::integral_constant<int, B / 2>{});
+    if (nt > 0) {
+      int x0 = 0;
+      for (; n - x0 > B / 2; x0 += B) batch(x0, std::integral_constant<int, B>{});
+      if (x0 < n) batch(x0, std::integral_constant<int, B / 2>{});
     }
-    st4(a.dv + srow, dv);
-    float* gf = a.gfold + static_cast<int64_t>(r0 + j) * 8 * kCD + c0;
+    st4(a.dk + srow, dk);
+    st4(a.dq + static_cast<int64_t>(DI[o]) * kCD + c0, dq);
+    float* gf = a.gfold + static_cast<int64_t>(r0 + o) * 8 * kCD + c0;
 #pragma unroll
     for (int l = 0; l < 8; ++l) st4(gf + l * kCD, G[l]);
-  }
-  CTR(2);
-  // the g scratch written by every owner is read by others below: workgroup-scope release / acquire
-  __threadfence_block();
-  __syncthreads();
-  CTR(3);
-  // at of triplet t for destination i (recomputed, as pass 1 did) and g_t, from global (L2) in batches
-  auto atg = [&](int i, int t, float& at, float& g) {
-    at = expf(ldf(al_r, (t * H + head) * 4) - MX[i * H + head]) * IV[i * H + head];
-    g = ldf(g_r, (t * H + head) * 4);
-  };
-  // ---- rho_i = sum_{j != i} at g over i's contiguous block, j ascending (one owner per destination)
-  for (int i = owner; i < n; i += NO) {
-    float rho = 0.f;
-    for (int p0 = 0; p0 < nt; p0 += 8) {
-      float at[8], g[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) atg(i, TB[i] + (p0 + u < nt ? p0 + u : nt - 1), at[u], g[u]);
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (p0 + u < nt) rho = fmaf(at[u], g[u], rho);
-    }
-    if (leader) RHO[i * H + head] = rho;
-  }
-  __syncthreads();
-  CTR(4);
-  // ---- pass 2: dk_j (owner of source j), dq_i (owner of destination i); x over the other n - 1
-  for (int o = owner; o < n; o += NO) {
-    cf4 dk = {0.f, 0.f, 0.f, 0.f}, dq = {0.f, 0.f, 0.f, 0.f};
-    const float rho_o = RHO[o * H + head];
-    for (int x0 = 0; x0 < n; x0 += 8) {
-      float ats[8], gs[8], atd[8], gd[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int x = x0 + u < n ? x0 + u : n - 1;
-        // source role (j = o, i = x): triplet TB[x] + o - [o > x]; destination role (i = o, j = x)
-        int ps = o - (o > x ? 1 : 0), pd = x - (x > o ? 1 : 0);
-        ps = ps < nt ? ps : nt - 1;
-        pd = pd < nt ? pd : nt - 1;
-        atg(x, TB[x] + ps, ats[u], gs[u]);
-        atg(o, TB[o] + pd, atd[u], gd[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int x = x0 + u;
-        if (x >= n) break;  // (workgroup-uniform)
-        if (x == o) continue;
-        const float ws = ats[u] * (gs[u] - RHO[x * H + head]) * a.inv_sqrt_c;
-        dk += ws * QI[x * 32 + l32];
-        const float wd = atd[u] * (gd[u] - rho_o) * a.inv_sqrt_c;
-        dq += wd * KE[x * 32 + l32];
-      }
-    }
-    st4(a.dk + static_cast<int64_t>(r0 + o) * kCD + c0, dk);
-    st4(a.dq + static_cast<int64_t>(DI[o]) * kCD + c0, dq);
-    // GO is free after pass 1 (other owners read it until the barrier): dv + dk rows for the edge term;
-    // this lane's own dv store of pass 1 is read back (program order)
-    if (a.d_edge) GO[o * 32 + l32] = dk + ld4(a.dv + static_cast<int64_t>(r0 + o) * kCD + c0);
+    DE[o * 32 + l32] += dk;  // (this owner's own dv row of pass 1)
   }
   CTR(5);
   if (a.d_edge) {  // d_edge[b] = sum_j (dv_j + dk_j), j ascending
     __syncthreads();
     if (tid < 32) {
-      cf4 s = GO[l32];
-      for (int j = 1; j < n; ++j) s += GO[j * 32 + l32];
+      cf4 s = DE[l32];
+      for (int j = 1; j < n; ++j) s += DE[j * 32 + l32];
       st4(a.d_edge + b * kCD + c0, s);
     }
   }
@@ -649,7 +658,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
 
 template <int LPH>
 int bwd_center_launch(const BwdCenterArgs& a, bool edge, int max_degree, hipStream_t st) {
-  constexpr int W = 4, B = 4;
+  constexpr int W = 4, B = 8;
   constexpr int H = 32 / LPH;
   const size_t lds = bwd_center_lds<H>(max_degree);
   if (lds > 160 * 1024) return X2G_EUNSUPPORTED;
@@ -674,7 +683,7 @@ using namespace x2g;
 X2G_API size_t x2g_sbf_attention_bwd_center_lds(int32_t max_degree, int32_t heads) {
   if (max_degree < 0 || heads <= 0) return 0;
   const int n = max_degree > 0 ? max_degree : 1;
-  return static_cast<size_t>(n) * 3 * kCD * 4 + static_cast<size_t>(n) * heads * 12 + static_cast<size_t>(n) * 8;
+  return static_cast<size_t>(n) * 4 * kCD * 4 + static_cast<size_t>(n) * heads * 12 + static_cast<size_t>(n) * 8;
 }
 
 X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const float* v, const float* edge,
