@@ -33,7 +33,7 @@ for k in sorted(set(fetch) | set(write)):
     out[k] = {"fetch_bytes": None if f[0] is None else round(2 * 1024 * f[0]),
               "write_bytes": None if w[0] is None else round(1024 * w[0]),
               "dispatches": [f[1], w[1]]}
-meta = {"source": [sys.argv[1], sys.argv[2]], "correction": "FETCH_SIZE x2 (gfx950), KiB -> bytes",
+meta = {"commit": os.environ.get("X2G_COMMIT"), "source": [sys.argv[1], sys.argv[2]], "correction": "FETCH_SIZE x2 (gfx950), KiB -> bytes",
         "per_dispatch": "max over the key's dispatches (the probes' launches)"}
 json.dump({"meta": meta, "kernels": out}, open(sys.argv[3], "w"), indent=1)
 print(f"{len(out)} kernel/grid entries -> {sys.argv[3]}")
