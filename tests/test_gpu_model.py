@@ -481,8 +481,8 @@ def _dense_cluster(n_atoms=72, seed=5):
 def test_factorised_sbf_backward_equals_two_pass(cuda, monkeypatch, shape):
     """The folded lin_sbf backward (one destination pass, dS folded per source line node into
     G[E, 8, D], dW_sbf = sum_s R_s G_s; csrc/attention_fold.inc) against the two-pass backward with the
-    materialised d_sbfproj [T, D] and its T-row weight GEMM: same energies, every parameter
-    gradient within fp32 reassociation error.  "dense": segments longer than 64 triplets."""
+    materialised d_sbfproj [T, D] and its T-row weight GEMM: energies and every parameter gradient
+    within fp32 reassociation error.  "dense": segments longer than 64 triplets."""
     import x2gnn
     from x2gnn import ops
     from x2gnn.data import collate
@@ -506,7 +506,9 @@ def test_factorised_sbf_backward_equals_two_pass(cuda, monkeypatch, shape):
     assert len(calls) == 4  # one folded weight gradient per conv layer in the folded run
     ref_res, ref_grads = runs[-1]
     for res, grads in runs[:-1]:
-        assert torch.equal(res, ref_res)
+        # (the folded run's forward forms S from the sbf factors inside the center-atom kernel, the plain
+        # run projects S with the MFMA kernel: equal up to fp32 reassociation, not bitwise)
+        assert float((res - ref_res).abs().max()) <= 1e-5 * float(ref_res.abs().max())
         assert grads.keys() == ref_grads.keys()
         for n, g in grads.items():
             ref = ref_grads[n]
