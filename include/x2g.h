@@ -280,42 +280,52 @@ int x2g_sbf_attention_fwd_center(const float* q, const float* k, const float* v,
                                  int64_t num_edges, int64_t num_triplets, int32_t heads, int32_t channels, float* out,
                                  float* alpha_raw, float* seg_max, float* seg_den, float* row_stats, void* stream);
 
-/* The center-atom forward with lin_sbf fused (no S to read): X2-GNN's sbf row factorises as
+/* Workgroup UNITS of the two whole-batch center kernels below: with pack_ptr (int32 [units + 1], or NULL)
+ * unit u is the PACK of center atoms atom_order[pack_ptr[u]] .. atom_order[pack_ptr[u + 1] - 1] (at most
+ * 64 atoms; every atom of the batch in exactly one pack, atoms without edges included), processed side by
+ * side by one workgroup (its 16 half-wave owners take the rows of all of them: x2gnn packs the atoms
+ * best-fit-decreasing by degree into units of <= 16 rows, data.center_packs); without it unit u is atom
+ * atom_order[u] (or u when atom_order is NULL).  max_rows >= the row count sum(deg) of every unit (the
+ * largest degree without packs), <= X2G_CENTER_MAX_DEGREE: it sizes the LDS image.  Packing changes no
+ * bit of any output (every sum keeps its order within an atom's block).
+ *
+ * The center-atom forward with lin_sbf fused (no S to read): X2-GNN's sbf row factorises as
  * sbf[t, 6l+n] = R[s, 6l+n] Y_l(t) (angular_basis_layer.py:87-91; R = rbf_env [E, 42] of the triplet's
  * source s, Y = sph_y [T, 8] from x2g_spherical_basis), so S_t = b + sum_l Y_l(t) P_s[l] with
  * P_s[l][c] = sum_n W[c, 6l+n] R[s, 6l+n], formed per source in LDS for each center atom's block
  * (w_sbf [128, 42], b_sbf [128]).  Outputs as x2g_sbf_attention_fwd_center; sbfproj_out [T, 128] (or
- * NULL) receives every S_t row for a backward that reads them.  LDS per workgroup 4.5 KB x max_degree
- * (<= 160 KiB, else X2G_EUNSUPPORTED); no atom0 / t_base tiling is needed (nothing T x 128 is read). */
+ * NULL) receives every S_t row for a backward that reads them.  Units unit0 .. unit0 + n_units - 1.  LDS
+ * per workgroup 4.7 KB x max_rows (<= 160 KiB, else X2G_EUNSUPPORTED); no t_base tiling is needed
+ * (nothing T x 128 is read). */
 int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, const float* v, const float* skip,
                                     const float* edge, const int32_t* src_row, int edge_mode, const float* radial,
                                     const float* sph_y, const float* w_sbf, const float* b_sbf,
                                     const int32_t* atom_rowptr, const int32_t* edge_rev, const int32_t* rev_trip,
-                                    const int32_t* atom_order, int64_t atom0, int64_t n_atoms, int32_t max_degree,
-                                    int64_t num_edges,
-                                    int64_t num_triplets, int32_t heads, int32_t channels, float* out,
-                                    float* alpha_raw, float* seg_max, float* seg_den, float* row_stats,
-                                    float* sbfproj_out, void* stream);
+                                    const int32_t* atom_order, const int32_t* pack_ptr, int64_t unit0,
+                                    int64_t n_units, int32_t max_rows, int64_t num_edges, int64_t num_triplets,
+                                    int32_t heads, int32_t channels, float* out, float* alpha_raw, float* seg_max,
+                                    float* seg_den, float* row_stats, float* sbfproj_out, void* stream);
 
-/* The whole attention backward over a SYMMETRIC line graph in ONE launch, one workgroup per center atom
- * (csrc/attention_center.hip): the block's rows (k + e of its sources, dout and q of its destinations,
- * their softmax max / denominator) staged in LDS, then per source j a pass over its triplets' S rows,
- * alpha (dv, and a_t, g_t into the g_work [2, T, heads] scratch), rho per destination, and per source /
- * destination dk, the folded lin_sbf gradient G (from Y) and dq.  Replaces x2g_sbf_attention_bwd_dst_g + x2g_sbf_attention_bwd_src_fold on such
- * graphs (same dq, dk, dv, radial_grad = G [E, 8, HC]; fp32 rounding apart), reading S once instead of
- * twice and no row gathers; d_edge_atom [num_atoms, HC] (or NULL) = the per-CENTER-ATOM gradient of the
- * edge term (sum over the atom's sources of dk + dv): the element-table gradient is its keyed sum by
+/* The whole attention backward over a SYMMETRIC line graph in ONE launch, one workgroup per unit (center
+ * atom or pack, above; csrc/attention_center.hip): the block's rows (k + e of its sources, dout and q of
+ * its destinations, their softmax max / denominator) staged in LDS, then per source j a pass over its
+ * triplets' S rows, alpha (dv, and a_t, g_t into the g_work [2, T, heads] scratch), rho per destination,
+ * and per source / destination dk, the folded lin_sbf gradient G (from Y) and dq.  Replaces
+ * x2g_sbf_attention_bwd_dst_g + x2g_sbf_attention_bwd_src_fold on such graphs (same dq, dk, dv,
+ * radial_grad = G [E, 8, HC]; fp32 rounding apart), reading S once instead of twice and no row gathers;
+ * d_edge_atom [N, HC] (or NULL) = the per-CENTER-ATOM gradient of the edge term (sum over the atom's
+ * sources of dk + dv; zero for an atom without edges): the element-table gradient is its keyed sum by
  * atom element.  sph_y [T, 8] as x2g_spherical_basis writes it.  LDS per workgroup:
- * x2g_sbf_attention_bwd_center_lds(max_degree, heads) bytes (<= 160 KiB, else X2G_EUNSUPPORTED).
- * heads * channels = 128, channels a multiple of 4, 16-byte aligned rows. */
-size_t x2g_sbf_attention_bwd_center_lds(int32_t max_degree, int32_t heads);
+ * x2g_sbf_attention_bwd_center_lds(max_rows, heads) bytes (<= 160 KiB, else X2G_EUNSUPPORTED).
+ * heads * channels = 128, channels a multiple of 4, 16-byte aligned rows, T * 512 < 2^31. */
+size_t x2g_sbf_attention_bwd_center_lds(int32_t max_rows, int32_t heads);
 int x2g_sbf_attention_bwd_center(const float* q, const float* k, const float* v, const float* edge,
                                  const int32_t* src_row, int edge_mode, const float* sbfproj, const float* sph_y,
                                  const int32_t* atom_rowptr, const int32_t* edge_rev, const int32_t* rev_trip,
-                                 const int32_t* atom_order, const float* alpha_raw, const float* seg_max,
-                                 const float* seg_den, const float* dout,
-                                 int64_t num_atoms, int32_t max_degree, int64_t num_edges, int64_t num_triplets,
-                                 int32_t heads, int32_t channels, float* dq, float* dk, float* dv, float* radial_grad,
+                                 const int32_t* atom_order, const int32_t* pack_ptr, const float* alpha_raw,
+                                 const float* seg_max, const float* seg_den, const float* dout, int64_t num_units,
+                                 int32_t max_rows, int64_t num_edges, int64_t num_triplets, int32_t heads,
+                                 int32_t channels, float* dq, float* dk, float* dv, float* radial_grad,
                                  float* d_edge_atom, float* g_work, void* stream);
 
 /* Backward, destination-major: dq[E,HC]; d_edge ([E,HC] per destination for EDGE_PER_DST,

@@ -18,7 +18,7 @@ if [ -n "${K:-}" ]; then
   rc=$?; tail -3 gpurun_out/t_$TAG.log; [ $rc -eq 0 ] || exit $rc
 fi
 if [ "${ROUNDS:-3}" != "0" ]; then
-  timeout -k 10 900 python -u scripts/step_ab.py ${ROUNDS:-3} base=AB_ROOT=ab_base new= > gpurun_out/ab_$TAG.log 2>&1
+  timeout -k 10 900 python -u scripts/step_ab.py ${ROUNDS:-3} base=AB_ROOT=ab_base new= ${AB_EXTRA:-} > gpurun_out/ab_$TAG.log 2>&1
   rc=$?; tail -3 gpurun_out/ab_$TAG.log; [ $rc -eq 0 ] || exit $rc
 fi
 if [ "${TRACE:-1}" != "0" ]; then

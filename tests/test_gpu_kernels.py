@@ -1865,6 +1865,11 @@ def _sym_lg(ei, n, cuda, with_transpose=False):
     deg = np.bincount(ei[0], minlength=n)
     lg.max_degree = int(deg.max()) if ei.shape[1] else 0
     lg.center_order = torch.from_numpy(np.argsort(-deg, kind="stable").astype(np.int32)).to(cuda)
+    # the workgroup packs the model's batches carry (data.center_packs): (order, pack_ptr, max rows)
+    from x2gnn.data import center_packs
+
+    po, pp, pr = center_packs(deg)
+    lg.packed = (torch.from_numpy(po).to(cuda), torch.from_numpy(pp).to(cuda), pr)
     return lg
 
 
@@ -1975,9 +1980,10 @@ def test_center_forward_edge_cases(cuda):
         assert torch.equal(x, y)
 
 
-def _bwd_both(lg, q, k, v, S, table, mode, heads, channels, seed):
+def _bwd_both(lg, q, k, v, S, table, mode, heads, channels, seed, packed=False):
     """(center, destination-major fold) backward outputs on the same forward state: dq, dk, dv, G and the
-    element-table gradient of the edge term (keyed sums in fp64)."""
+    element-table gradient of the edge term (keyed sums in fp64); ``packed``: the center kernel over the
+    batch's workgroup packs (data.center_packs), and its per-atom edge-term rows appended raw."""
     from x2gnn import _lib, ops
     from x2gnn._lib import call, ptr, stream_ptr
 
@@ -1995,15 +2001,20 @@ def _bwd_both(lg, q, k, v, S, table, mode, heads, channels, seed):
     dq, dk, dv = (torch.full((E, D), float("nan"), **f) for _ in range(3))
     G = torch.full((E, 8, D), float("nan"), **f)
     de_atom = torch.full((lg.N, D), float("nan"), **f) if edge is not None else None
-    assert int(_lib.load().x2g_sbf_attention_bwd_center_lds(lg.max_degree, heads)) <= 160 * 1024
+    order, packs, units, max_rows = lg.center_order, None, lg.N, lg.max_degree
+    if packed:
+        order, packs, max_rows = lg.packed
+        units = int(packs.shape[0]) - 1
+    assert int(_lib.load().x2g_sbf_attention_bwd_center_lds(max_rows, heads)) <= 160 * 1024
     call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(lg.src_type) if edge is not None else None,
-         mode, ptr(S), ptr(y), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order), ptr(alpha),
-         ptr(smax), ptr(sden),
-         ptr(dout), lg.N, lg.max_degree, E, T, heads, channels, ptr(dq), ptr(dk), ptr(dv), ptr(G), ptr(de_atom),
-         ptr(torch.empty(2, T, H, **f)), stream_ptr())
+         mode, ptr(S), ptr(y), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(order), ptr(packs),
+         ptr(alpha), ptr(smax), ptr(sden), ptr(dout), units, max_rows, E, T, heads, channels, ptr(dq), ptr(dk),
+         ptr(dv), ptr(G), ptr(de_atom), ptr(torch.empty(2, T, H, **f)), stream_ptr())
     c = [dq, dk, dv, G]
     if edge is not None:
         c.append(torch.zeros(rows, D, dtype=torch.float64, device=q.device).index_add_(0, lg.atom_type.long(), de_atom.double()))
+        if packed:
+            c.append(de_atom)
     # destination-major fold passes
     dq2, dk2, dv2 = (torch.empty(E, D, **f) for _ in range(3))
     G2 = torch.empty(E, 8, D, **f)
@@ -2051,6 +2062,10 @@ def test_center_backward_equals_fold_passes(cuda, heads, channels):
     for mode in (ops.EDGE_PER_DST, ops.EDGE_NONE):
         c, r = _bwd_both(lg, q, k, v, S, table, mode, heads, channels, 6)
         _close_bwd(c, r)
+        # the model's launch: atoms packed into workgroups of <= 16 rows -- the same bits
+        cp, _ = _bwd_both(lg, q, k, v, S, table, mode, heads, channels, 6, packed=True)
+        for x, y in zip(cp, c):
+            assert torch.equal(x, y)
 
 
 def test_center_backward_edge_cases(cuda):
@@ -2070,12 +2085,17 @@ def test_center_backward_edge_cases(cuda):
     q, k, v, _, S, table = _attn_inputs(lg, cuda, 7)
     c, r = _bwd_both(lg, q, k, v, S, table, ops.EDGE_PER_DST, 16, 8, 8)
     _close_bwd(c, r)
+    # packed: the isolated atom shares a unit with others (its edge-term row zero), the hub is alone
+    cp, _ = _bwd_both(lg, q, k, v, S, table, ops.EDGE_PER_DST, 16, 8, 8, packed=True)
+    for x, y in zip(cp, c):
+        assert torch.equal(x, y)
+    assert float(cp[-1][3].abs().max()) == 0.0  # atom 3: no edges
     from x2gnn import _lib
 
     assert int(_lib.load().x2g_sbf_attention_bwd_center_lds(130, 16)) > 160 * 1024 or 130 > ops.CENTER_MAX_DEGREE
     rc = _lib.load().x2g_sbf_attention_bwd_center(None, None, None, None, None, 0, None, None, None, None, None, None,
-                                                   None, None, None, None, 1, 130, 1, 1, 16, 8, None, None, None, None,
-                                                   None, None, None)
+                                                   None, None, None, None, None, 1, 130, 1, 1, 16, 8, None, None, None,
+                                                   None, None, None, None)
     assert rc == 1002  # X2G_EUNSUPPORTED
 
 
@@ -2109,15 +2129,75 @@ def test_center_forward_fused_projection_equals_projected(cuda):
     call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
          ops.EDGE_PER_DST, ptr(S), 0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order), 0,
          lg.N, lg.max_degree, E, T, H, C, *[ptr(t) for t in ref], stream_ptr())
-    for store in (True, False):
+    po, pp, pr = lg.packed
+    runs = []
+    for store, packed in ((True, False), (False, False), (True, True), (False, True)):
         got = [torch.full_like(t, float("nan")) for t in ref]
         S2 = torch.full((T, D), float("nan"), **f) if store else None
+        # unpacked: identity order with the S store, the degree order without; packed: the model's units
+        order, packs, units, rows = (po, pp, int(pp.shape[0]) - 1, pr) if packed else \
+            (None if store else lg.center_order, None, lg.N, lg.max_degree)
         call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
              ops.EDGE_PER_DST, ptr(radial), ptr(y), ptr(W), ptr(bias), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
-             ptr(lg.rev_trip), None if store else ptr(lg.center_order), 0, lg.N, lg.max_degree, E, T, H, C,
+             ptr(lg.rev_trip), ptr(order), ptr(packs), 0, units, rows, E, T, H, C,
              *[ptr(t) for t in got], ptr(S2), stream_ptr())
         for name, a, r in zip(("out", "alpha", "smax", "sden", "row_stats"), got, ref):
             assert not torch.isnan(a).any(), name
             torch.testing.assert_close(a, r, rtol=1e-5, atol=1e-5, msg=name)
         if store:
             torch.testing.assert_close(S2, S, rtol=1e-5, atol=1e-5)
+        runs.append(got + ([S2] if store else []))
+    for a, b in zip(runs[:2], runs[2:]):  # packing changes no bit
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+
+
+def test_center_fused_projection_packed_edge_cases(cuda):
+    """The fused-projection forward over workgroup packs on a graph with degree-1 atoms, isolated atoms (in
+    a unit of their own: no rows), a hub of degree 20 (above the 16-row pack capacity: alone) and small
+    atoms sharing units: == the one-atom-per-workgroup launch, bitwise, and == projection + center
+    forward within fp32 reassociation."""
+    from x2gnn import ops
+    from x2gnn._lib import call, ptr, stream_ptr
+
+    pairs = [(0, 1), (1, 2)] + [(4, 5 + i) for i in range(20)] + [(25, 26), (26, 27), (25, 27)] + \
+        [(28 + i, 29 + i) for i in range(6)]
+    ed = sorted({(a, b) for a, b in pairs} | {(b, a) for a, b in pairs})
+    ei = np.array(ed, dtype=np.int64).T
+    n = 36  # atoms 3 and 35 have no edges
+    lg = _sym_lg(ei, n, cuda)
+    po, pp, pr = lg.packed
+    assert pr == 20 and int(pp.shape[0]) - 1 < n
+    E, T, H, C, D = lg.E, lg.T, 16, 8, 128
+    g = torch.Generator(device=cuda).manual_seed(15)
+    q, k, v, skip = (torch.randn(E, D, device=cuda, generator=g) for _ in range(4))
+    table = torch.randn(10, D, device=cuda, generator=g)
+    radial = torch.randn(E, 42, device=cuda, generator=g)
+    y = torch.randn(T, 8, device=cuda, generator=g)
+    y[:, 7] = 1.0
+    sbf = (radial[lg.trip_src.long()].view(T, 7, 6) * y[:, :7, None]).reshape(T, 42).contiguous()
+    W = 0.2 * torch.randn(D, 42, device=cuda, generator=g)
+    bias = 0.1 * torch.randn(D, device=cuda, generator=g)
+    f = dict(device=cuda, dtype=torch.float32)
+    S = torch.empty(T, D, **f)
+    call("x2g_sbf_project", ptr(sbf), T, 42, ptr(W), ptr(bias), D, ptr(S), stream_ptr())
+    ref = [torch.empty(E, D, **f), torch.empty(T, H, **f), torch.empty(E, H, **f), torch.empty(E, H, **f),
+           torch.empty(E, 2, **f)]
+    call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
+         ops.EDGE_PER_DST, ptr(S), 0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), None, 0,
+         lg.N, lg.max_degree, E, T, H, C, *[ptr(t) for t in ref], stream_ptr())
+    runs = []
+    for packed in (False, True):
+        got = [torch.full_like(t, float("nan")) for t in ref]
+        S2 = torch.full((T, D), float("nan"), **f)
+        order, packs, units, rows = (po, pp, int(pp.shape[0]) - 1, pr) if packed else (None, None, lg.N, lg.max_degree)
+        call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
+             ops.EDGE_PER_DST, ptr(radial), ptr(y), ptr(W), ptr(bias), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
+             ptr(lg.rev_trip), ptr(order), ptr(packs), 0, units, rows, E, T, H, C, *[ptr(t) for t in got], ptr(S2),
+             stream_ptr())
+        for name, a, r in zip(("out", "alpha", "smax", "sden", "row_stats"), got, ref):
+            torch.testing.assert_close(a, r, rtol=1e-5, atol=1e-5, msg=name, equal_nan=False)
+        torch.testing.assert_close(S2, S, rtol=1e-5, atol=1e-5)
+        runs.append(got + [S2])
+    for x, yy in zip(*runs):
+        assert torch.equal(x, yy)

@@ -560,7 +560,7 @@ X2G_API int x2g_batch_meta(const int64_t* edge_index, const int64_t* x, const in
   return last_launch_status();
 }
 
-X2G_API int x2g_abi_version(void) { return 14; }
+X2G_API int x2g_abi_version(void) { return 15; }
 
 X2G_API const char* x2g_status_string(int status) {
   switch (status) {

@@ -197,8 +197,54 @@ def _add_device_indices(b, nodes, edges):
     b._store["_x2g_symmetric"] = _is_symmetric(ei_np, int(nodes.sum()))
     deg = np.bincount(ei_np[0], minlength=int(nodes.sum()))
     b._store["_x2g_max_degree"] = int(deg.max()) if deg.size else 0
-    # the center-atom kernels' launch order: atoms by decreasing degree (the longest blocks first)
-    b._store["_x2g_center_order"] = torch.from_numpy(np.argsort(-deg, kind="stable").astype(np.int32))
+    # the center-atom kernels' workgroup units: atoms packed by degree, the longest units first
+    order, packs, rows = center_packs(deg)
+    b._store["_x2g_center_order"] = torch.from_numpy(order)
+    b._store["_x2g_center_packs"] = torch.from_numpy(packs)
+    b._store["_x2g_center_rows"] = rows
+
+
+CENTER_PACK_ROWS = 16  # the center kernels' half-wave owners per workgroup (csrc/attention_center.hip)
+CENTER_PACK_MEMBERS = 16
+
+
+def center_packs(deg, cap=CENTER_PACK_ROWS, max_members=CENTER_PACK_MEMBERS):
+    """Workgroup units of the center-atom attention kernels (x2g_sbf_attention_fwd_center_sf / _bwd_center
+    pack_ptr): the atoms packed best-fit-decreasing by degree into units of at most ``cap`` rows (a unit's
+    rows are its atoms' out-edges; one workgroup's 16 half-wave owners take one row each), an atom of
+    degree >= cap alone, atoms without edges ``max_members`` to a unit.  One atom per workgroup keeps only
+    57 % of the owners busy at config 2 (degrees 2-17); these units keep 90 %.  Returns (order int32 [N]:
+    the atoms unit by unit, packs int32 [P + 1]: unit p = order[packs[p] .. packs[p + 1]), max_rows: the
+    largest unit's row count), the units in decreasing order of their largest degree (the longest
+    workgroups start first)."""
+    deg = np.asarray(deg, dtype=np.int64)
+    units, rows, free = [], [], [[] for _ in range(cap)]  # free[r]: open units with r rows left
+    for a in np.argsort(-deg, kind="stable").tolist():
+        d = int(deg[a])
+        if d == 0:
+            break  # (sorted: the rest have no edges either)
+        if d < cap:
+            for r in range(d, cap):  # best fit: the fullest open unit that takes it
+                if free[r]:
+                    u = free[r].pop()
+                    units[u].append(a)
+                    rows[u] += d
+                    if len(units[u]) < max_members:
+                        free[r - d].append(u)
+                    break
+            else:
+                free[cap - d].append(len(units))
+                units.append([a])
+                rows.append(d)
+            continue
+        units.append([a])
+        rows.append(d)
+    zero = np.flatnonzero(deg == 0).tolist()
+    units += [zero[i:i + max_members] for i in range(0, len(zero), max_members)]
+    rows += [0] * ((len(zero) + max_members - 1) // max_members)
+    order = np.fromiter((a for u in units for a in u), dtype=np.int32, count=len(deg))
+    packs = np.concatenate([[0], np.cumsum([len(u) for u in units])]).astype(np.int32)
+    return order, packs, int(max(rows, default=0))
 
 
 def _is_symmetric(ei, n):

@@ -96,7 +96,9 @@ class LineGraph:
         # element row (int32 [N]: the key of the center-atom edge-term gradient)
         self.max_degree = None
         self.atom_type = None
-        self.center_order = None  # int32 [N]: atoms by decreasing degree (the center kernels' launch order)
+        # the center kernels' workgroup units (data.center_packs; None: one atom per workgroup): int32 [N] the
+        # atoms unit by unit, int32 [P + 1] the units' bounds in it, and the largest unit's row count
+        self.center_order = self.center_packs = self.center_rows = None
         if with_transpose and self.symmetric:
             self._src_rowptr = torch.empty(self.E + 1, **i32)
             self._src_perm = torch.empty(self.T, **i32)
@@ -131,7 +133,8 @@ class LineGraph:
         lg._src_rowptr = lg._src_perm = lg._src_dst = None
         lg.dst_type = lg.src_type = None
         lg.symmetric = False
-        lg.edge_rev = lg.rev_trip = lg.max_degree = lg.atom_type = lg.center_order = None
+        lg.edge_rev = lg.rev_trip = lg.max_degree = lg.atom_type = None
+        lg.center_order = lg.center_packs = lg.center_rows = None
         ws_bytes = int(_lib.load().x2g_vertex_to_edge_workspace(lg.E, 0))
         lg._ws = torch.empty(ws_bytes, dtype=torch.uint8, device=lg.trip_src.device)
         return lg
@@ -334,11 +337,26 @@ _CENTER_BWD = True
 _CENTER_SF = True
 
 
+def _center_units(lg):
+    """(pack_ptr or None, units, max_rows) of the whole-batch center kernels: the batch's packs of atoms
+    (data.center_packs) when it has them, else one atom per workgroup."""
+    packs = getattr(lg, "center_packs", None)
+    if packs is not None and lg.center_order is not None and lg.center_rows is not None:
+        return packs, int(packs.shape[0]) - 1, max(int(lg.center_rows), 1)
+    return None, lg.N, max(int(lg.max_degree), 1)
+
+
+def _unit_rows_lds(rows):  # csrc/attention_center.hip unit_rows_lds
+    return ((2 * rows + 2 * 64 + 4) * 4 + 15) // 16 * 16
+
+
 def _center_sf_ok(lg, factors, D):
     """Whether the fused-projection center forward applies: the sbf factors are this call's, and the
-    block's LDS image (k + e, v + e, 7 P rows and the radial row per source: 4.66 KB x max degree) fits."""
-    return (_CENTER_SF and factors is not None and factors[1] is not None and D == 128
-            and lg.max_degree is not None and 4776 * max(lg.max_degree, 1) <= 160 * 1024)
+    unit's LDS image (k + e, v + e, 7 P rows and the radial row per source row: 4.66 KB x rows) fits."""
+    if not (_CENTER_SF and factors is not None and factors[1] is not None and D == 128 and lg.max_degree is not None):
+        return False
+    rows = _center_units(lg)[2]
+    return _unit_rows_lds(rows) + 4776 * rows <= 160 * 1024
 
 
 def _center_rows(lg, edge_mode, edge_row, D, channels):
@@ -380,9 +398,10 @@ class _SBFAttention(torch.autograd.Function):
             # lin_sbf fused into the center forward: S_t rebuilt per center atom from the sbf factors; its
             # rows stored only when a backward will read them
             sproj = torch.empty(T, D, dtype=torch.float32, device=dev) if any(ctx.needs_input_grad) else None
+            packs, units, rows = _center_units(lg)
             call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(src_row),
                  edge_mode, ptr(factors[0]), ptr(factors[1]), ptr(w_sbf), ptr(b_sbf), ptr(lg.atom_rowptr),
-                 ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order), 0, lg.N, lg.max_degree, E, T, heads,
+                 ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order), ptr(packs), 0, units, rows, E, T, heads,
                  channels, ptr(out), ptr(alpha), ptr(smax), ptr(sden), ptr(rstats), ptr(sproj), stream_ptr())
         else:
             # S = lin_sbf(sbf) once per layer [T, D], right before this layer's attention (so it is still
@@ -467,18 +486,18 @@ class _SBFAttention(torch.autograd.Function):
         gfold = torch.empty(E, 8, D, dtype=torch.float32, device=dev)
         st = stream_ptr()
         center, src_row = _center_rows(lg, mode, ctx.edge_row, D, channels)
+        packs, units, rows = _center_units(lg) if center else (None, 0, 0)
         if center and _CENTER_BWD and getattr(lg, "atom_type", None) is not None and (
-                _lib.load().x2g_sbf_attention_bwd_center_lds(lg.max_degree, heads) <= 160 * 1024):
+                _lib.load().x2g_sbf_attention_bwd_center_lds(rows, heads) <= 160 * 1024):
             # one launch for both passes, per center atom (csrc/attention_center.hip); the edge term's
             # gradient comes per center atom and is summed by the atoms' elements
             want_edge = mode == EDGE_PER_DST and ctx.needs_input_grad[4]
             d_edge_atom = torch.empty(lg.N, D, dtype=torch.float32, device=dev) if want_edge else None
             g_work = torch.empty(2, T, heads, dtype=torch.float32, device=dev)
             call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(src_row), mode, ptr(sproj),
-                 ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order), ptr(alpha),
-                 ptr(smax), ptr(sden),
-                 ptr(dout), lg.N, lg.max_degree, E, T, heads, channels, ptr(dq), ptr(dk), ptr(dv), ptr(gfold),
-                 ptr(d_edge_atom), ptr(g_work), st)
+                 ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order), ptr(packs),
+                 ptr(alpha), ptr(smax), ptr(sden), ptr(dout), units, rows, E, T, heads, channels, ptr(dq), ptr(dk),
+                 ptr(dv), ptr(gfold), ptr(d_edge_atom), ptr(g_work), st)
             d_edge = None
             if want_edge:
                 if ctx.defer_edge:

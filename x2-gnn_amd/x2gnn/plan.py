@@ -71,6 +71,8 @@ class GraphPlan:
             src_type = st.get("_x2g_src_type")
             p.lg.atom_type = st.get("_x2g_atom_type")
             p.lg.center_order = st.get("_x2g_center_order")
+            p.lg.center_packs = st.get("_x2g_center_packs")
+            p.lg.center_rows = st.get("_x2g_center_rows")
         else:
             p.lg = ops.vertex_to_edge(ei, p.num_atoms, p.num_triplets, meta.get("symmetric", False))
             p.line_ptr = _ptr_from_counts(data.edge_num, p.num_graphs, dev)
