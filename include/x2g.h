@@ -282,7 +282,7 @@ int x2g_sbf_attention_fwd_center(const float* q, const float* k, const float* v,
 
 /* Workgroup UNITS of the two whole-batch center kernels below: with pack_ptr (int32 [units + 1], or NULL)
  * unit u is the PACK of center atoms atom_order[pack_ptr[u]] .. atom_order[pack_ptr[u + 1] - 1] (at most
- * 64 atoms; every atom of the batch in exactly one pack, atoms without edges included), processed side by
+ * 32 atoms; every atom of the batch in exactly one pack, atoms without edges included), processed side by
  * side by one workgroup (its 16 half-wave owners take the rows of all of them: x2gnn packs the atoms
  * best-fit-decreasing by degree into units of <= 16 rows, data.center_packs); without it unit u is atom
  * atom_order[u] (or u when atom_order is NULL).  max_rows >= the row count sum(deg) of every unit (the

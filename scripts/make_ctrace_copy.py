@@ -17,7 +17,16 @@ __device__ unsigned long long x2g_ctrace[8192 * 8];
   do {                                                                                                  \\
     if (threadIdx.x == 0 && blockIdx.x < 8192) x2g_ctrace[blockIdx.x * 8 + (k)] = wall_clock64();     \\
   } while (0)
+// the fused-projection forward's: start, tables, staging, P products, end (x2g_ftrace_fetch)
+__device__ unsigned long long x2g_ftrace[8192 * 8];
+#define FTR(k)                                                                                          \\
+  do {                                                                                                  \\
+    if (threadIdx.x == 0 && blockIdx.x < 8192) x2g_ftrace[blockIdx.x * 8 + (k)] = wall_clock64();     \\
+  } while (0)
 #else
+#define FTR(k) \\
+  do {         \\
+  } while (0)
 #define CTR(k) \\
   do {         \\
   } while (0)
@@ -42,6 +51,24 @@ s = after(s, i, "    st4(a.dq + static_cast<int64_t>(DI[gr]) * kCD + c0, dq);\n 
 j = s.index("  if (a.d_edge) {  // d_edge[b] = sum_j (dv_j + dk_j), j ascending", i)
 s = s[:j] + "  CTR(5);\n" + s[j:]
 s = after(s, i, "      st4(a.d_edge + static_cast<int64_t>(u.MA[m]) * kCD + c0, s);\n    }\n  }\n", "  CTR(6);\n")
+# the fused-projection forward
+i = s.index("attn_fwd_center_sf_kernel(const FwdSfArgs a) {")
+s = s[:i] + s[i:].replace("{", "{\n  FTR(0);", 1)
+s = after(s, i, "  if (n_rows <= 0) return;  // (workgroup-uniform)\n", "  FTR(1);\n")
+j = s.index("  __syncthreads();\n  {\n    if (pthr) {", i) + len("  __syncthreads();\n")
+s = s[:j] + "  FTR(2);\n" + s[j:]
+j = s.index("  __syncthreads();\n  for (; g < n_rows; g += 2 * WAVES) {", i) + len("  __syncthreads();\n")
+s = s[:j] + "  FTR(3);\n" + s[j:]
+j = s.index("\nconstexpr size_t fwd_sf_lds(int rows)", i)
+j = s.rindex("}\n", i, j)
+s = s[:j] + "  __syncthreads();  // (trace build only: the workgroup's end)\n  FTR(4);\n" + s[j:]
+s += '''
+#ifdef X2G_TRACE
+X2G_API int x2g_ftrace_fetch(unsigned long long* host, int n) {
+  return static_cast<int>(hipMemcpyFromSymbol(host, HIP_SYMBOL(x2g_ftrace), sizeof(unsigned long long) * n));
+}
+#endif
+'''
 s += '''
 #ifdef X2G_TRACE
 X2G_API int x2g_ctrace_fetch(unsigned long long* host, int n) {
@@ -49,6 +76,6 @@ X2G_API int x2g_ctrace_fetch(unsigned long long* host, int n) {
 }
 #endif
 '''
-assert s.count("CTR(") == 9, s.count("CTR(")
+assert s.count("CTR(") == 9 and s.count("FTR(") == 7, (s.count("CTR("), s.count("FTR("))
 open(os.path.join(ROOT, "x2-gnn_amd", "ab", "attention_center_ab.hip"), "w").write(s)
 print("ok")

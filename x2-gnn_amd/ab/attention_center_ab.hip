@@ -33,7 +33,16 @@ __device__ unsigned long long x2g_ctrace[8192 * 8];
   do {                                                                                                  \
     if (threadIdx.x == 0 && blockIdx.x < 8192) x2g_ctrace[blockIdx.x * 8 + (k)] = wall_clock64();     \
   } while (0)
+// the fused-projection forward's: start, tables, staging, P products, end (x2g_ftrace_fetch)
+__device__ unsigned long long x2g_ftrace[8192 * 8];
+#define FTR(k)                                                                                          \
+  do {                                                                                                  \
+    if (threadIdx.x == 0 && blockIdx.x < 8192) x2g_ftrace[blockIdx.x * 8 + (k)] = wall_clock64();     \
+  } while (0)
 #else
+#define FTR(k) \
+  do {         \
+  } while (0)
 #define CTR(k) \
   do {         \
   } while (0)
@@ -70,20 +79,22 @@ __device__ __forceinline__ float half_sum(float v, int half) {
 // of the owner count (config 2: degrees 2-17 on 16 owners, 57 % busy); packs of total degree <= 16
 // (the host's best-fit decreasing, data.center_packs) keep 90 % of them busy.  Row g of the workgroup
 // is line node LN[g] = r0_m + (g - base_m) of member m, whose block is rows base_m .. base_m + n_m - 1:
-// RI[g] = base_m | n_m << 16.  Every sum keeps its order (sources / destinations ascending within a
-// block), so packed and unpacked launches give the same bits.
-constexpr int kMaxMembers = 64;  // atoms per pack (one wave builds the tables)
+// RI[g] = base_m | n_m << 16, ER[g] = the member's edge-table row (src_row of its first out-edge: the center
+// atom's element).  Every sum keeps its order (sources / destinations ascending within a block), so packed
+// and unpacked launches give the same bits.
+constexpr int kMaxMembers = 32;  // atoms per pack (wave 0 builds the tables, one lane per member)
 
 struct UnitRows {
-  int* LN;  // [rows] line node
-  int* RI;  // [rows] base | n << 16
-  int* MA;  // [kMaxMembers] member atom (NULL: not kept)
-  int* MI;  // [kMaxMembers] member base | n << 16
+  int* LN;   // [rows] line node
+  int* RI;   // [rows] base | n << 16
+  int* ER;   // [rows] edge-table row
+  int* MA;   // [kMaxMembers] member atom
+  int* MI;   // [kMaxMembers] member base | n << 16
   int* NRS;  // [2] rows, members
 };
 
 __host__ __device__ constexpr size_t unit_rows_lds(int rows) {  // (a multiple of 16 bytes)
-  return ((static_cast<size_t>(2) * rows + 2 * kMaxMembers + 4) * 4 + 15) / 16 * 16;
+  return ((static_cast<size_t>(3) * rows + 2 * kMaxMembers + 4) * 4 + 15) / 16 * 16;
 }
 
 __device__ __forceinline__ UnitRows unit_rows_carve(int* p, int max_rows) {
@@ -93,13 +104,15 @@ __device__ __forceinline__ UnitRows unit_rows_carve(int* p, int max_rows) {
   u.MI = u.MA + kMaxMembers;
   u.LN = u.MI + kMaxMembers;
   u.RI = u.LN + max_rows;
+  u.ER = u.RI + max_rows;
   return u;
 }
 
-// wave 0 fills the tables (the caller synchronises before reading them)
+// wave 0 fills the tables (the caller synchronises before reading them); src_row may be NULL (ER = 0)
 __device__ __forceinline__ void unit_rows_build(const UnitRows& u, const int32_t* __restrict__ order,
                                                 const int32_t* __restrict__ packs, int64_t unit,
-                                                const int32_t* __restrict__ rowptr) {
+                                                const int32_t* __restrict__ rowptr,
+                                                const int32_t* __restrict__ src_row) {
   if (threadIdx.x >= 64) return;
   const int lane = threadIdx.x;
   int64_t m0 = unit, m1 = unit + 1;
@@ -114,6 +127,7 @@ __device__ __forceinline__ void unit_rows_build(const UnitRows& u, const int32_t
     r0 = rowptr[b];
     n = rowptr[b + 1] - r0;
   }
+  const int er = (src_row && n > 0) ? src_row[r0] : 0;
   int inc = n;  // inclusive prefix over the members
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -127,6 +141,7 @@ __device__ __forceinline__ void unit_rows_build(const UnitRows& u, const int32_t
     for (int r = 0; r < n; ++r) {
       u.LN[base + r] = r0 + r;
       u.RI[base + r] = base | n << 16;
+      u.ER[base + r] = er;
     }
   }
   if (lane == 63) {
@@ -289,14 +304,16 @@ constexpr int kSfK = kSfL * kSfR;        // 42
 
 template <int LPH, int WAVES, int B, bool EDGE>
 __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const FwdSfArgs a) {
+  FTR(0);
   // [tables] then [rows][32] (k + e), [rows][32] (v + e), [rows][7][32] P, [rows][42] R
   extern __shared__ cf4 lds[];
   const UnitRows u = unit_rows_carve(reinterpret_cast<int*>(lds), a.max_rows);
   // (the host orders the units by decreasing work: the longest start first, the short ones fill the tail)
-  unit_rows_build(u, a.order, a.packs, a.atom0 + blockIdx.x, a.atom_rowptr);
+  unit_rows_build(u, a.order, a.packs, a.atom0 + blockIdx.x, a.atom_rowptr, EDGE ? a.src_row : nullptr);
   __syncthreads();
   const int n_rows = uniform(u.NRS[0]);
   if (n_rows <= 0) return;  // (workgroup-uniform)
+  FTR(1);
   cf4* KE = lds + unit_rows_lds(a.max_rows) / 16;
   cf4* VE = KE + n_rows * 32;
   cf4* P = VE + n_rows * 32;
@@ -318,7 +335,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const Fw
   for (int idx = tid; idx < n_rows * 32; idx += NT) {
     const int r = idx >> 5, c = idx & 31;
     const int64_t ln = u.LN[r];
-    const cf4 e4 = EDGE ? ld4(a.edge + static_cast<int64_t>(a.src_row[ln]) * kCD + 4 * c) : cf4{0.f, 0.f, 0.f, 0.f};
+    const cf4 e4 = EDGE ? ld4(a.edge + static_cast<int64_t>(u.ER[r]) * kCD + 4 * c) : cf4{0.f, 0.f, 0.f, 0.f};
     const int64_t row = ln * kCD + 4 * c;
     KE[idx] = ld4(a.k + row) + e4;
     VE[idx] = ld4(a.v + row) + e4;
@@ -341,6 +358,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const Fw
 #pragma unroll
     for (int r = 0; r < kSfR; ++r) wv[cc][r] = a.w[(4 * pc4 + cc) * kSfK + kSfR * pl + r];
   __syncthreads();
+  FTR(2);
   {
     if (pthr) {
       const int l = pl, c4 = pc4;
@@ -362,7 +380,14 @@ __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const Fw
     }
   }
   const cf4 bias4 = ld4(a.bias + c0);
+  // the first destination row's q and skip rows in flight under the P products
+  cf4 qv = {0.f, 0.f, 0.f, 0.f}, sk = {0.f, 0.f, 0.f, 0.f};
+  if (g < n_rows) {
+    qv = ld4(a.q + static_cast<int64_t>(d) * kCD + c0);
+    sk = ld4(a.skip + static_cast<int64_t>(d) * kCD + c0);
+  }
   __syncthreads();
+  FTR(3);
   for (; g < n_rows; g += 2 * WAVES) {
     const int ri = u.RI[g];
     const int base = ri & 0xffff, n = ri >> 16;  // this destination's block: rows base .. base + n - 1
@@ -370,11 +395,11 @@ __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const Fw
     if (g != owner) {
       d = a.edge_rev[u.LN[g]];
       tb = a.rev_trip[u.LN[g]];
+      qv = ld4(a.q + static_cast<int64_t>(d) * kCD + c0);
+      sk = ld4(a.skip + static_cast<int64_t>(d) * kCD + c0);
     }
     const int nt = n - 1;  // triplets per destination
     const int64_t drow = static_cast<int64_t>(d) * kCD + c0;
-    const cf4 qv = ld4(a.q + drow);
-    const cf4 sk = ld4(a.skip + drow);
     cf4 acc = {0.f, 0.f, 0.f, 0.f};
     float m = -INFINITY, den = 0.f;
     auto batch = [&](int j0, auto bb) {
@@ -455,6 +480,8 @@ __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const Fw
       a.sden[static_cast<int64_t>(d) * a.H + head] = den;
     }
   }
+  __syncthreads();  // (trace build only: the workgroup's end)
+  FTR(4);
 }
 
 constexpr size_t fwd_sf_lds(int rows) {
@@ -543,7 +570,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const Bw
   constexpr int H = 32 / LPH;
   extern __shared__ cf4 lds[];
   const UnitRows u = unit_rows_carve(reinterpret_cast<int*>(lds), a.max_rows);
-  unit_rows_build(u, a.order, a.packs, blockIdx.x, a.atom_rowptr);
+  unit_rows_build(u, a.order, a.packs, blockIdx.x, a.atom_rowptr, EDGE ? a.src_row : nullptr);
   __syncthreads();
   const int n_rows = uniform(u.NRS[0]), n_mem = uniform(u.NRS[1]);
   const int tid = threadIdx.x;
@@ -562,25 +589,26 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const Bw
   float* RHO = IV + n_rows * H;
   int* TB = reinterpret_cast<int*>(RHO + n_rows * H);
   int* DI = TB + n_rows;
-  // ---- staging
+  // ---- staging: each row's destination and triplet block first (one round trip), then every row load
+  // from addresses in LDS (one more)
+  for (int idx = tid; idx < n_rows; idx += 64 * WAVES) {
+    TB[idx] = a.rev_trip[u.LN[idx]];
+    DI[idx] = a.edge_rev[u.LN[idx]];
+  }
+  __syncthreads();
   for (int idx = tid; idx < n_rows * 32; idx += 64 * WAVES) {
     const int r = idx >> 5, c = idx & 31;
-    const int ln = u.LN[r];
-    const int64_t d = a.edge_rev[ln];
-    const cf4 e4 = EDGE ? ld4(a.edge + static_cast<int64_t>(a.src_row[ln]) * kCD + 4 * c) : cf4{0.f, 0.f, 0.f, 0.f};
-    KE[idx] = ld4(a.k + static_cast<int64_t>(ln) * kCD + 4 * c) + e4;
+    const int64_t d = DI[r];
+    const cf4 e4 = EDGE ? ld4(a.edge + static_cast<int64_t>(u.ER[r]) * kCD + 4 * c) : cf4{0.f, 0.f, 0.f, 0.f};
+    KE[idx] = ld4(a.k + static_cast<int64_t>(u.LN[r]) * kCD + 4 * c) + e4;
     GO[idx] = ld4(a.dout + d * kCD + 4 * c);
     QI[idx] = ld4(a.q + d * kCD + 4 * c);
   }
   for (int idx = tid; idx < n_rows * H; idx += 64 * WAVES) {
     const int r = idx / H, h = idx - r * H;
-    const int64_t d = a.edge_rev[u.LN[r]];
+    const int64_t d = DI[r];
     MX[idx] = a.smax[d * H + h];
     IV[idx] = 1.0f / (a.sden[d * H + h] + kCEps);
-  }
-  for (int idx = tid; idx < n_rows; idx += 64 * WAVES) {
-    TB[idx] = a.rev_trip[u.LN[idx]];
-    DI[idx] = a.edge_rev[u.LN[idx]];
   }
   __syncthreads();
   CTR(1);
@@ -611,7 +639,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const Bw
     const int ln = u.LN[gr];
     const int64_t srow = static_cast<int64_t>(ln) * kCD + c0;
     cf4 ue = ld4(a.v + srow);
-    if (EDGE) ue += ld4(a.edge + static_cast<int64_t>(a.src_row[ln]) * kCD + c0);
+    if (EDGE) ue += ld4(a.edge + static_cast<int64_t>(u.ER[gr]) * kCD + c0);
     cf4 dv = {0.f, 0.f, 0.f, 0.f};
     auto batch = [&](int i0, auto bb) {
       constexpr int BB = decltype(bb)::value;
@@ -713,7 +741,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const Bw
     const int ln = u.LN[gr];
     const int64_t srow = static_cast<int64_t>(ln) * kCD + c0;
     cf4 ue = ld4(a.v + srow);
-    if (EDGE) ue += ld4(a.edge + static_cast<int64_t>(a.src_row[ln]) * kCD + c0);
+    if (EDGE) ue += ld4(a.edge + static_cast<int64_t>(u.ER[gr]) * kCD + c0);
     cf4 dk = {0.f, 0.f, 0.f, 0.f};
     cf4 G[8];
 #pragma unroll
@@ -937,6 +965,12 @@ X2G_API int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, cons
     default: return X2G_EUNSUPPORTED;
   }
 }
+
+#ifdef X2G_TRACE
+X2G_API int x2g_ftrace_fetch(unsigned long long* host, int n) {
+  return static_cast<int>(hipMemcpyFromSymbol(host, HIP_SYMBOL(x2g_ftrace), sizeof(unsigned long long) * n));
+}
+#endif
 
 #ifdef X2G_TRACE
 X2G_API int x2g_ctrace_fetch(unsigned long long* host, int n) {

@@ -56,20 +56,22 @@ __device__ __forceinline__ float half_sum(float v, int half) {
 // of the owner count (config 2: degrees 2-17 on 16 owners, 57 % busy); packs of total degree <= 16
 // (the host's best-fit decreasing, data.center_packs) keep 90 % of them busy.  Row g of the workgroup
 // is line node LN[g] = r0_m + (g - base_m) of member m, whose block is rows base_m .. base_m + n_m - 1:
-// RI[g] = base_m | n_m << 16.  Every sum keeps its order (sources / destinations ascending within a
-// block), so packed and unpacked launches give the same bits.
-constexpr int kMaxMembers = 64;  // atoms per pack (one wave builds the tables)
+// RI[g] = base_m | n_m << 16, ER[g] = the member's edge-table row (src_row of its first out-edge: the center
+// atom's element).  Every sum keeps its order (sources / destinations ascending within a block), so packed
+// and unpacked launches give the same bits.
+constexpr int kMaxMembers = 32;  // atoms per pack (wave 0 builds the tables, one lane per member)
 
 struct UnitRows {
-  int* LN;  // [rows] line node
-  int* RI;  // [rows] base | n << 16
-  int* MA;  // [kMaxMembers] member atom (NULL: not kept)
-  int* MI;  // [kMaxMembers] member base | n << 16
+  int* LN;   // [rows] line node
+  int* RI;   // [rows] base | n << 16
+  int* ER;   // [rows] edge-table row
+  int* MA;   // [kMaxMembers] member atom
+  int* MI;   // [kMaxMembers] member base | n << 16
   int* NRS;  // [2] rows, members
 };
 
 __host__ __device__ constexpr size_t unit_rows_lds(int rows) {  // (a multiple of 16 bytes)
-  return ((static_cast<size_t>(2) * rows + 2 * kMaxMembers + 4) * 4 + 15) / 16 * 16;
+  return ((static_cast<size_t>(3) * rows + 2 * kMaxMembers + 4) * 4 + 15) / 16 * 16;
 }
 
 __device__ __forceinline__ UnitRows unit_rows_carve(int* p, int max_rows) {
@@ -79,13 +81,15 @@ __device__ __forceinline__ UnitRows unit_rows_carve(int* p, int max_rows) {
   u.MI = u.MA + kMaxMembers;
   u.LN = u.MI + kMaxMembers;
   u.RI = u.LN + max_rows;
+  u.ER = u.RI + max_rows;
   return u;
 }
 
-// wave 0 fills the tables (the caller synchronises before reading them)
+// wave 0 fills the tables (the caller synchronises before reading them); src_row may be NULL (ER = 0)
 __device__ __forceinline__ void unit_rows_build(const UnitRows& u, const int32_t* __restrict__ order,
                                                 const int32_t* __restrict__ packs, int64_t unit,
-                                                const int32_t* __restrict__ rowptr) {
+                                                const int32_t* __restrict__ rowptr,
+                                                const int32_t* __restrict__ src_row) {
   if (threadIdx.x >= 64) return;
   const int lane = threadIdx.x;
   int64_t m0 = unit, m1 = unit + 1;
@@ -100,6 +104,7 @@ __device__ __forceinline__ void unit_rows_build(const UnitRows& u, const int32_t
     r0 = rowptr[b];
     n = rowptr[b + 1] - r0;
   }
+  const int er = (src_row && n > 0) ? src_row[r0] : 0;
   int inc = n;  // inclusive prefix over the members
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -113,6 +118,7 @@ __device__ __forceinline__ void unit_rows_build(const UnitRows& u, const int32_t
     for (int r = 0; r < n; ++r) {
       u.LN[base + r] = r0 + r;
       u.RI[base + r] = base | n << 16;
+      u.ER[base + r] = er;
     }
   }
   if (lane == 63) {
@@ -279,7 +285,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const Fw
   extern __shared__ cf4 lds[];
   const UnitRows u = unit_rows_carve(reinterpret_cast<int*>(lds), a.max_rows);
   // (the host orders the units by decreasing work: the longest start first, the short ones fill the tail)
-  unit_rows_build(u, a.order, a.packs, a.atom0 + blockIdx.x, a.atom_rowptr);
+  unit_rows_build(u, a.order, a.packs, a.atom0 + blockIdx.x, a.atom_rowptr, EDGE ? a.src_row : nullptr);
   __syncthreads();
   const int n_rows = uniform(u.NRS[0]);
   if (n_rows <= 0) return;  // (workgroup-uniform)
@@ -304,7 +310,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const Fw
   for (int idx = tid; idx < n_rows * 32; idx += NT) {
     const int r = idx >> 5, c = idx & 31;
     const int64_t ln = u.LN[r];
-    const cf4 e4 = EDGE ? ld4(a.edge + static_cast<int64_t>(a.src_row[ln]) * kCD + 4 * c) : cf4{0.f, 0.f, 0.f, 0.f};
+    const cf4 e4 = EDGE ? ld4(a.edge + static_cast<int64_t>(u.ER[r]) * kCD + 4 * c) : cf4{0.f, 0.f, 0.f, 0.f};
     const int64_t row = ln * kCD + 4 * c;
     KE[idx] = ld4(a.k + row) + e4;
     VE[idx] = ld4(a.v + row) + e4;
@@ -348,6 +354,12 @@ __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const Fw
     }
   }
   const cf4 bias4 = ld4(a.bias + c0);
+  // the first destination row's q and skip rows in flight under the P products
+  cf4 qv = {0.f, 0.f, 0.f, 0.f}, sk = {0.f, 0.f, 0.f, 0.f};
+  if (g < n_rows) {
+    qv = ld4(a.q + static_cast<int64_t>(d) * kCD + c0);
+    sk = ld4(a.skip + static_cast<int64_t>(d) * kCD + c0);
+  }
   __syncthreads();
   for (; g < n_rows; g += 2 * WAVES) {
     const int ri = u.RI[g];
@@ -356,11 +368,11 @@ __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const Fw
     if (g != owner) {
       d = a.edge_rev[u.LN[g]];
       tb = a.rev_trip[u.LN[g]];
+      qv = ld4(a.q + static_cast<int64_t>(d) * kCD + c0);
+      sk = ld4(a.skip + static_cast<int64_t>(d) * kCD + c0);
     }
     const int nt = n - 1;  // triplets per destination
     const int64_t drow = static_cast<int64_t>(d) * kCD + c0;
-    const cf4 qv = ld4(a.q + drow);
-    const cf4 sk = ld4(a.skip + drow);
     cf4 acc = {0.f, 0.f, 0.f, 0.f};
     float m = -INFINITY, den = 0.f;
     auto batch = [&](int j0, auto bb) {
@@ -528,7 +540,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const Bw
   constexpr int H = 32 / LPH;
   extern __shared__ cf4 lds[];
   const UnitRows u = unit_rows_carve(reinterpret_cast<int*>(lds), a.max_rows);
-  unit_rows_build(u, a.order, a.packs, blockIdx.x, a.atom_rowptr);
+  unit_rows_build(u, a.order, a.packs, blockIdx.x, a.atom_rowptr, EDGE ? a.src_row : nullptr);
   __syncthreads();
   const int n_rows = uniform(u.NRS[0]), n_mem = uniform(u.NRS[1]);
   const int tid = threadIdx.x;
@@ -547,25 +559,26 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const Bw
   float* RHO = IV + n_rows * H;
   int* TB = reinterpret_cast<int*>(RHO + n_rows * H);
   int* DI = TB + n_rows;
-  // ---- staging
+  // ---- staging: each row's destination and triplet block first (one round trip), then every row load
+  // from addresses in LDS (one more)
+  for (int idx = tid; idx < n_rows; idx += 64 * WAVES) {
+    TB[idx] = a.rev_trip[u.LN[idx]];
+    DI[idx] = a.edge_rev[u.LN[idx]];
+  }
+  __syncthreads();
   for (int idx = tid; idx < n_rows * 32; idx += 64 * WAVES) {
     const int r = idx >> 5, c = idx & 31;
-    const int ln = u.LN[r];
-    const int64_t d = a.edge_rev[ln];
-    const cf4 e4 = EDGE ? ld4(a.edge + static_cast<int64_t>(a.src_row[ln]) * kCD + 4 * c) : cf4{0.f, 0.f, 0.f, 0.f};
-    KE[idx] = ld4(a.k + static_cast<int64_t>(ln) * kCD + 4 * c) + e4;
+    const int64_t d = DI[r];
+    const cf4 e4 = EDGE ? ld4(a.edge + static_cast<int64_t>(u.ER[r]) * kCD + 4 * c) : cf4{0.f, 0.f, 0.f, 0.f};
+    KE[idx] = ld4(a.k + static_cast<int64_t>(u.LN[r]) * kCD + 4 * c) + e4;
     GO[idx] = ld4(a.dout + d * kCD + 4 * c);
     QI[idx] = ld4(a.q + d * kCD + 4 * c);
   }
   for (int idx = tid; idx < n_rows * H; idx += 64 * WAVES) {
     const int r = idx / H, h = idx - r * H;
-    const int64_t d = a.edge_rev[u.LN[r]];
+    const int64_t d = DI[r];
     MX[idx] = a.smax[d * H + h];
     IV[idx] = 1.0f / (a.sden[d * H + h] + kCEps);
-  }
-  for (int idx = tid; idx < n_rows; idx += 64 * WAVES) {
-    TB[idx] = a.rev_trip[u.LN[idx]];
-    DI[idx] = a.edge_rev[u.LN[idx]];
   }
   __syncthreads();
   auto rsrc = [](const void* p, int64_t bytes) {
@@ -595,7 +608,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const Bw
     const int ln = u.LN[gr];
     const int64_t srow = static_cast<int64_t>(ln) * kCD + c0;
     cf4 ue = ld4(a.v + srow);
-    if (EDGE) ue += ld4(a.edge + static_cast<int64_t>(a.src_row[ln]) * kCD + c0);
+    if (EDGE) ue += ld4(a.edge + static_cast<int64_t>(u.ER[gr]) * kCD + c0);
     cf4 dv = {0.f, 0.f, 0.f, 0.f};
     auto batch = [&](int i0, auto bb) {
       constexpr int BB = decltype(bb)::value;
@@ -694,7 +707,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const Bw
     const int ln = u.LN[gr];
     const int64_t srow = static_cast<int64_t>(ln) * kCD + c0;
     cf4 ue = ld4(a.v + srow);
-    if (EDGE) ue += ld4(a.edge + static_cast<int64_t>(a.src_row[ln]) * kCD + c0);
+    if (EDGE) ue += ld4(a.edge + static_cast<int64_t>(u.ER[gr]) * kCD + c0);
     cf4 dk = {0.f, 0.f, 0.f, 0.f};
     cf4 G[8];
 #pragma unroll

@@ -347,7 +347,7 @@ def _center_units(lg):
 
 
 def _unit_rows_lds(rows):  # csrc/attention_center.hip unit_rows_lds
-    return ((2 * rows + 2 * 64 + 4) * 4 + 15) // 16 * 16
+    return ((3 * rows + 2 * 32 + 4) * 4 + 15) // 16 * 16
 
 
 def _center_sf_ok(lg, factors, D):
