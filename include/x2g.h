@@ -98,6 +98,20 @@ int x2g_line_graph_transpose_sym(const int32_t* edge_src, const int32_t* edge_ds
                                  const int32_t* trip_rowptr, int64_t num_edges, int32_t* src_rowptr,
                                  int32_t* src_perm, int32_t* src_dst, void* workspace, size_t workspace_bytes,
                                  void* stream);
+/* x2g_vertex_to_edge_sym for a BATCH OF MOLECULES (every edge joins two atoms of one molecule, as in a
+ * PyG batch): the atom and triplet row pointers one workgroup per molecule (its atoms mol_ptr[m] ..
+ * mol_ptr[m+1]-1 own its edges line_ptr[m] .. line_ptr[m+1]-1; the triplets before it sum_{m'<m}
+ * mol_trips[m'], int64 [num_mols]: the host's per-molecule counts or x2g_batch_meta's), then the same
+ * emission: two launches, no scan over the whole batch, no workspace; outputs equal x2g_vertex_to_edge_sym's
+ * bit for bit.  max_mol_atoms >= every molecule's atom count (<= 16384: it sizes a degree histogram in
+ * LDS), T < 2^31, else X2G_EUNSUPPORTED.  The transpose, when a backward needs it, comes from
+ * x2g_line_graph_transpose_sym. */
+int x2g_vertex_to_edge_sym_mol(const int32_t* edge_src, const int32_t* edge_dst, int64_t num_edges,
+                               int64_t num_nodes, int64_t num_triplets, const int32_t* mol_ptr,
+                               const int32_t* line_ptr, const int64_t* mol_trips, int64_t num_mols,
+                               int32_t max_mol_atoms, int32_t* atom_rowptr, int32_t* trip_rowptr, int32_t* trip_src,
+                               int32_t* trip_dst, int32_t* atom_j, int32_t* atom_i, int32_t* atom_k,
+                               int32_t* edge_rev, int32_t* rev_trip, void* stream);
 /* Both at once for a training batch (a backward will need the transpose): x2g_vertex_to_edge_sym's
  * outputs and x2g_line_graph_transpose_sym's (src_rowptr [E+1], src_perm [T], src_dst [T] or NULL) in
  * three launches instead of five — the source row pointer from the same one-workgroup scan, the
@@ -115,10 +129,11 @@ int x2g_line_graph_sym_build(const int32_t* edge_src, const int32_t* edge_dst, i
  * edge_src / edge_dst (int32 [E]), their elements src_type / dst_type (int32 [E]), atom_type (int32 [N]),
  * the molecules' atom and edge row pointers mol_ptr / line_ptr (int32 [num_graphs + 1]), atom_rowptr
  * [N+1] of edge_src, and everything the host needs in one int64 block (one copy back):
- * info = [mol_ptr (B+1) | line_ptr (B+1) | triplets (B) | flags (3)], B = num_graphs, where triplets[g] =
+ * info = [mol_ptr (B+1) | line_ptr (B+1) | triplets (B) | flags (4)], B = num_graphs, where triplets[g] =
  * sum over molecule g's edges e = (a->b) of |N_out(b) \ {a}| and flags = [edges whose reverse is missing
  * (0 = a symmetric edge set), the largest out-degree, edges out of (src, dst) order / repeated / out of
- * range].  Integer atomics only: exact. */
+ * range, edges joining two molecules (0 = x2g_vertex_to_edge_sym_mol applies)].  Integer atomics only:
+ * exact. */
 int x2g_batch_meta(const int64_t* edge_index, const int64_t* x, const int64_t* batch, int64_t num_edges,
                    int64_t num_nodes, int64_t num_graphs, int32_t* edge_src, int32_t* edge_dst, int32_t* src_type,
                    int32_t* dst_type, int32_t* atom_type, int32_t* line_ptr, int32_t* mol_ptr, int32_t* atom_rowptr,

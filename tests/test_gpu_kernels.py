@@ -153,6 +153,36 @@ def test_symmetric_builder_and_transpose_equal_generic(cuda):
     _sym_vs_generic(big.edge_index.numpy(), big.num_nodes, int(big._meta["triplets"].sum()), cuda)
 
 
+def test_per_molecule_builder_equals_whole_batch(cuda):
+    """x2g_vertex_to_edge_sym_mol (row pointers one workgroup per molecule, from the molecules' atom / edge
+    pointers and triplet counts) == x2g_vertex_to_edge_sym over the whole batch, every output bit for bit,
+    and the transpose it leaves to src_csr too: a config-2 batch, one larger than the one-workgroup scan,
+    and a batch with one-atom and two-atom molecules (no triplets) between ordinary ones, first and last."""
+    from x2gnn import ops
+    from x2gnn.data import collate
+    from x2gnn.synth import molecule_from_geometry, synthetic_molecules
+
+    rng = np.random.default_rng(0)
+    lone = molecule_from_geometry(np.array([6]), np.zeros((1, 3)), feat_rng=rng, y=0.0)
+    pair = molecule_from_geometry(np.array([1, 1]), np.array([[0.0, 0, 0], [0.74, 0, 0]]), feat_rng=rng, y=0.0)
+    cases = [synthetic_molecules(128, "S160", seed=21), synthetic_molecules(1800, "S160", seed=22),
+             [lone, pair] + synthetic_molecules(5, "S160", seed=23) + [pair, lone]]
+    for mols in cases:
+        b = collate(mols).to(cuda)
+        st = b._store
+        n, T = b.num_nodes, int(b._meta["triplets"].sum())
+        ref = ops.LineGraph(st["_x2g_edge_src"], st["_x2g_edge_dst"], n, T, symmetric=True, with_transpose=False)
+        mol = ops.LineGraph(st["_x2g_edge_src"], st["_x2g_edge_dst"], n, T, symmetric=True,
+                            molecules=(st["_x2g_mol_ptr"], st["_x2g_line_ptr"], st["_x2g_mol_trips"],
+                                       st["_x2g_max_mol_atoms"]))
+        assert mol._src_rowptr is None  # (the center-atom backward never reads the transpose)
+        for name in ("atom_rowptr", "trip_rowptr", "trip_src", "trip_dst", "atom_j", "atom_i", "atom_k", "edge_rev",
+                     "rev_trip"):
+            assert torch.equal(getattr(ref, name), getattr(mol, name)), name
+        for x, y in zip(ref.src_csr(), mol.src_csr()):
+            assert torch.equal(x, y)
+
+
 def test_csr_rowptr(cuda):
     from x2gnn import ops
 

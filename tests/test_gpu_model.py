@@ -759,6 +759,15 @@ def test_foreign_batch_meta_on_device_and_forward_time(cuda):
     for k in ("nodes", "edges", "triplets"):
         np.testing.assert_array_equal(got[k], meta[k])
     assert got["symmetric"] and got["max_degree"] == int(np.bincount(b.edge_index[0].numpy()).max())
+    # every edge inside its molecule: the per-molecule line-graph builder's inputs (counts on the device)
+    assert torch.equal(got["index"]["_x2g_mol_trips"].cpu(), torch.from_numpy(meta["triplets"]))
+    assert got["index"]["_x2g_max_mol_atoms"] == int(meta["nodes"].max())
+    # the last atom of molecule 0 moved into molecule 1: its edges now join two molecules -> not offered
+    moved = _ForeignBatch(**dict(fb._store))
+    bv = fb._store["batch"].clone()
+    bv[int(meta["nodes"][0]) - 1] = 1
+    moved.batch = bv
+    assert "_x2g_mol_trips" not in _meta_on_device(moved)["index"]
     bad = _ForeignBatch(**dict(fb._store))
     bad.edge_index = fb.edge_index.flip(1).contiguous()
     with pytest.raises(ValueError, match="sorted"):

@@ -445,6 +445,68 @@ __global__ void emit_transpose_sym_kernel(const int32_t* __restrict__ src, const
   transpose_group(src, dst, atom_rowptr, trip_rowptr, src_rowptr, E, src_perm, src_dst);
 }
 
+// ----------------------------------------------------------------------------- per-molecule row pointers
+// The row pointers of a SYMMETRIC line graph of a batch of molecules (every edge joins two atoms of one
+// molecule: a PyG batch), one workgroup per molecule m, nothing shared between workgroups: its atoms
+// a0 .. a1 - 1 (mol_ptr) own its edges E0 .. E1 - 1 (line_ptr), so
+//   atom_rowptr[b] = E0 + #{e in molecule : src e < b}       (a histogram of the molecule's sources in LDS),
+//   trip_rowptr[e] = T0 + sum_{e' in [E0, e)} (deg(dst e') - 1),   T0 = sum_{m' < m} mol_trips[m'],
+// the degrees read from the same LDS histogram and T0 from the host's (or x2g_batch_meta's) per-molecule
+// triplet counts.  Replaces the row-pointer grid and the one-workgroup scan over all E edges (24.6 us at
+// config 2 on one CU) with one launch of B short workgroups.
+constexpr int kMolThreads = 256;
+
+__global__ void __launch_bounds__(kMolThreads) mol_rowptr_sym_kernel(
+    const int32_t* __restrict__ edge_src, const int32_t* __restrict__ edge_dst, const int32_t* __restrict__ mol_ptr,
+    const int32_t* __restrict__ line_ptr, const int64_t* __restrict__ mol_trips, int64_t B, int64_t E, int64_t N,
+    int64_t T, int32_t* __restrict__ atom_rowptr, int32_t* __restrict__ trip_rowptr) {
+  extern __shared__ int deg[];  // [a1 - a0]
+  __shared__ int lds[kMolThreads / 64];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  const int a0 = mol_ptr[m], a1 = mol_ptr[m + 1], e0 = line_ptr[m], e1 = line_ptr[m + 1];
+  const int na = a1 - a0;
+  for (int i = tid; i < na; i += kMolThreads) deg[i] = 0;
+  // T0: the triplets of the molecules before this one
+  int64_t part = 0;
+  for (int64_t i = tid; i < m; i += kMolThreads) part += mol_trips[i];
+  int t0;
+  block_exclusive_scan(static_cast<int>(part), lds, &t0);  // (its barriers also order the zeroing)
+  for (int e = e0 + tid; e < e1; e += kMolThreads) {
+    const int b = edge_src[e] - a0;
+    if (b >= 0 && b < na) atomicAdd(&deg[b], 1);  // (a molecule's edges join its own atoms: host contract)
+  }
+  __syncthreads();
+  // atom_rowptr over the molecule's atoms, chunk by chunk with a carry
+  int carry = e0;
+  for (int c = 0; c < na; c += kMolThreads) {
+    const int i = c + tid;
+    const int d = i < na ? deg[i] : 0;
+    int tot;
+    const int pre = block_exclusive_scan(d, lds, &tot);
+    if (i < na) atom_rowptr[a0 + i] = carry + pre;
+    carry += tot;
+  }
+  // trip_rowptr over the molecule's edges
+  carry = t0;
+  for (int c = e0; c < e1; c += kMolThreads) {
+    const int e = c + tid;
+    int cnt = 0;
+    if (e < e1) {
+      const int b = edge_dst[e] - a0;
+      cnt = (b >= 0 && b < na) ? deg[b] - 1 : 0;
+      cnt = cnt > 0 ? cnt : 0;
+    }
+    int tot;
+    const int pre = block_exclusive_scan(cnt, lds, &tot);
+    if (e < e1) trip_rowptr[e] = carry + pre;
+    carry += tot;
+  }
+  if (m == B - 1 && tid == 0) {
+    atom_rowptr[N] = static_cast<int32_t>(E);
+    trip_rowptr[E] = static_cast<int32_t>(T);
+  }
+}
+
 // ----------------------------------------------------------------------------- batch metadata
 // A PyG-style batch made elsewhere (the drop-in's real caller, trainer.py:37-40: a DataLoader Batch of
 // xgnn.py:41-52's keys) carries neither per-molecule triplet counts nor x2gnn's int32 index forms.  Both
@@ -453,9 +515,10 @@ __global__ void emit_transpose_sym_kernel(const int32_t* __restrict__ src, const
 // molecules' edge row pointer (CSR of batch[src[]]); then per edge its triplet count deg(b) - [b->a
 // exists] (the reverse found by binary search in b's sorted out-list) summed into its molecule batch[a]
 // (integer atomics: exact, order-independent).  Everything the host needs lands in one int64 block
-// info = [mol_ptr (B+1) | line_ptr (B+1) | triplets (B) | flags (3)], read back with one copy; flags:
+// info = [mol_ptr (B+1) | line_ptr (B+1) | triplets (B) | flags (4)], read back with one copy; flags:
 // [0] edges without a reverse (0 = symmetric), [1] the largest out-degree, [2] edges out of (src, dst)
-// order, repeated or out of range (the builders need a sorted simple edge list).
+// order, repeated or out of range (the builders need a sorted simple edge list), [3] edges joining two
+// molecules (0: the per-molecule builder x2g_vertex_to_edge_sym_mol applies).
 __device__ __forceinline__ void ptr_fill(int64_t prev, int64_t cur, int64_t n_seg, int32_t val,
                                          int32_t* __restrict__ rowptr, int64_t* __restrict__ rowptr64) {
   if (prev < -1) prev = -1;
@@ -471,7 +534,7 @@ __global__ void batch_meta_atoms(const int64_t* __restrict__ x, const int64_t* _
                                  int64_t B, int32_t* __restrict__ atom_type, int32_t* __restrict__ mol_ptr,
                                  int64_t* __restrict__ info) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i < B + 3) info[2 * (B + 1) + i] = 0;
+  if (i < B + 4) info[2 * (B + 1) + i] = 0;
   if (i > N) return;
   auto mol_of = [&](int64_t a) -> int64_t { return batch ? batch[a] : 0; };
   if (i == N) {
@@ -508,6 +571,7 @@ __global__ void batch_meta_edges(const int64_t* __restrict__ ei, const int64_t* 
   src_type[e] = ok ? static_cast<int32_t>(x[a]) : 0;
   dst_type[e] = ok ? static_cast<int32_t>(x[b]) : 0;
   if (!ok) atomicAdd(&flags[2], 1ull);
+  if (ok && mol_of(a) != mol_of(b)) atomicAdd(&flags[3], 1ull);  // an edge between two molecules
   if (e > 0) {
     const int64_t pa = ei[e - 1], pb = ei[E + e - 1];
     if (pa > a || (pa == a && pb >= b)) atomicAdd(&flags[2], 1ull);
@@ -673,6 +737,33 @@ X2G_API int x2g_vertex_to_edge_sym(const int32_t* edge_src, const int32_t* edge_
   int rc = x2g_csr_rowptr(edge_src, E, N, atom_rowptr, stream);
   if (rc) return rc;
   if ((rc = degree_scan(edge_dst, atom_rowptr, E, trip_rowptr, count, partial, st))) return rc;
+  if (E > 0) {
+    triplet_emit_kernel<<<blocks_for(E * kEmitGroup, 256), 256, 0, st>>>(
+        edge_src, edge_dst, atom_rowptr, trip_rowptr, E, T, trip_src, trip_dst, atom_j, atom_i, atom_k, edge_rev,
+        rev_trip);
+  }
+  return last_launch_status();
+}
+
+X2G_API int x2g_vertex_to_edge_sym_mol(const int32_t* edge_src, const int32_t* edge_dst, int64_t E, int64_t N,
+                                       int64_t T, const int32_t* mol_ptr, const int32_t* line_ptr,
+                                       const int64_t* mol_trips, int64_t num_mols, int32_t max_mol_atoms,
+                                       int32_t* atom_rowptr, int32_t* trip_rowptr, int32_t* trip_src,
+                                       int32_t* trip_dst, int32_t* atom_j, int32_t* atom_i, int32_t* atom_k,
+                                       int32_t* edge_rev, int32_t* rev_trip, void* stream) {
+  if (E < 0 || N < 0 || T < 0 || num_mols <= 0 || max_mol_atoms < 0 || !atom_rowptr || !trip_rowptr || !mol_ptr ||
+      !line_ptr || !mol_trips)
+    return X2G_EINVAL;
+  if (!edge_rev != !rev_trip) return X2G_EINVAL;
+  if (E > 0 && (!edge_src || !edge_dst)) return X2G_EINVAL;
+  if (T > 0 && (!trip_src || !trip_dst)) return X2G_EINVAL;
+  if (T >= (int64_t(1) << 31) || E >= (int64_t(1) << 31) || num_mols >= (int64_t(1) << 31) ||
+      static_cast<size_t>(max_mol_atoms) * 4 > 64 * 1024)
+    return X2G_EUNSUPPORTED;
+  hipStream_t st = as_stream(stream);
+  mol_rowptr_sym_kernel<<<static_cast<unsigned>(num_mols), kMolThreads, static_cast<size_t>(max_mol_atoms) * 4, st>>>(
+      edge_src, edge_dst, mol_ptr, line_ptr, mol_trips, num_mols, E, N, T, atom_rowptr, trip_rowptr);
+  if (int rc = last_launch_status()) return rc;
   if (E > 0) {
     triplet_emit_kernel<<<blocks_for(E * kEmitGroup, 256), 256, 0, st>>>(
         edge_src, edge_dst, atom_rowptr, trip_rowptr, E, T, trip_src, trip_dst, atom_j, atom_i, atom_k, edge_rev,

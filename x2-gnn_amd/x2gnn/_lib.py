@@ -53,6 +53,7 @@ SIGNATURES = {
     "x2g_vertex_to_edge_sym": [_P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P],
     "x2g_line_graph_transpose_sym": [_P, _P, _P, _P, _I64, _P, _P, _P, _P, _SZ, _P],
     "x2g_line_graph_sym_build": [_P, _P, _I64, _I64, _I64] + [_P] * 12 + [_P, _SZ, _P],
+    "x2g_vertex_to_edge_sym_mol": [_P, _P, _I64, _I64, _I64, _P, _P, _P, _I64, _I32] + [_P] * 9 + [_P],
     "x2g_keyed_row_sum_batch_workspace": [_I64, _I32, _I32, _I32],
     "x2g_keyed_row_sum_batch": [_P, _P, _I32, _P, _I64, _I32, _I32, ctypes.c_int, _P, _SZ, _P],
     "x2g_clip_adam_ema_ex": [_P, _P, _P, _P, _P, _I64, _P, ctypes.c_int, _P, _SZ, _P],

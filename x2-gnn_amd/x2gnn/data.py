@@ -125,7 +125,7 @@ def _meta_on_device(data):
     buf = torch.empty(4 * E + 2 * n + 1 + 2 * (B + 1), dtype=torch.int32, device=dev)
     src, dst, src_t, dst_t, atom_t, rowptr, line_ptr, mol_ptr = torch.split(
         buf, [E, E, E, E, n, n + 1, B + 1, B + 1])
-    info = torch.empty(3 * B + 5, dtype=torch.int64, device=dev)
+    info = torch.empty(3 * B + 6, dtype=torch.int64, device=dev)
     _lib.load()
     call("x2g_batch_meta", ptr(ei), ptr(x), ptr(batch), E, n, B, ptr(src), ptr(dst), ptr(src_t), ptr(dst_t),
          ptr(atom_t), ptr(line_ptr), ptr(mol_ptr), ptr(rowptr), ptr(info), stream_ptr())
@@ -137,6 +137,9 @@ def _meta_on_device(data):
     index = {"_x2g_edge_src": src, "_x2g_edge_dst": dst, "_x2g_src_type": src_t, "_x2g_dst_type": dst_t,
              "_x2g_atom_type": atom_t, "_x2g_line_ptr": line_ptr, "_x2g_mol_ptr": mol_ptr,
              "_x2g_symmetric": bool(fl[0] == 0), "_x2g_max_degree": int(fl[1])}
+    if fl[3] == 0 and B > 0:  # every edge inside its molecule: the per-molecule line-graph builder
+        index["_x2g_mol_trips"] = info[2 * B + 2:3 * B + 2]  # (a view of the device block: no copy)
+        index["_x2g_max_mol_atoms"] = int(np.diff(mp_).max())
     return {"nodes": np.diff(mp_), "edges": np.diff(lp), "triplets": tr, "symmetric": bool(fl[0] == 0),
             "max_degree": int(fl[1]), "index": index}
 
@@ -195,6 +198,12 @@ def _add_device_indices(b, nodes, edges):
     b._store["_x2g_src_type"] = torch.from_numpy(b._store["x"].numpy()[ei_np[0]].astype(np.int32))
     b._store["_x2g_atom_type"] = torch.from_numpy(b._store["x"].numpy().reshape(-1).astype(np.int32))
     b._store["_x2g_symmetric"] = _is_symmetric(ei_np, int(nodes.sum()))
+    # per-molecule triplet counts for the per-molecule line-graph builder (x2g_vertex_to_edge_sym_mol); the
+    # molecules' edges stay inside them by construction (each collated from its own graph)
+    trips = b._meta.get("triplets") if b._meta is not None else None
+    if trips is not None and len(trips) == len(nodes):
+        b._store["_x2g_mol_trips"] = torch.from_numpy(np.ascontiguousarray(trips, dtype=np.int64))
+        b._store["_x2g_max_mol_atoms"] = int(nodes.max()) if len(nodes) else 0
     deg = np.bincount(ei_np[0], minlength=int(nodes.sum()))
     b._store["_x2g_max_degree"] = int(deg.max()) if deg.size else 0
     # the center-atom kernels' workgroup units: atoms packed by degree, the longest units first

@@ -50,6 +50,9 @@ def _i32(t):
 
 
 # ---------------------------------------------------------------------------------- line graph
+MOL_ROWPTR_MAX_ATOMS = 16384  # x2g_vertex_to_edge_sym_mol's per-molecule degree histogram (64 KB of LDS)
+
+
 class LineGraph:
     """Triplet structure of one collated batch (all int32, on the device).
 
@@ -58,13 +61,21 @@ class LineGraph:
     src_rowptr/src_perm: the same triplets grouped by source line node (built on first use).
     """
 
-    def __init__(self, edge_src, edge_dst, num_nodes, num_triplets, symmetric=False, with_transpose=None):
+    def __init__(self, edge_src, edge_dst, num_nodes, num_triplets, symmetric=False, with_transpose=None,
+                 molecules=None):
         """``with_transpose`` (default: symmetric and grad enabled, i.e. a backward will ask for
         ``src_csr``): build the by-source lists with the line graph (x2g_line_graph_sym_build,
-        three launches for both instead of five)."""
+        three launches for both instead of five).  ``molecules`` = (mol_ptr int32 [B+1], line_ptr int32
+        [B+1], triplets per molecule int64 [B], largest molecule's atom count) of a symmetric batch whose
+        edges stay inside their molecules: the row pointers one workgroup per molecule
+        (x2g_vertex_to_edge_sym_mol, two launches), the transpose left to ``src_csr`` (the center-atom
+        backward never reads it)."""
         self.symmetric = bool(symmetric)  # caller-asserted: b->a present for every a->b (x2g_*_sym)
+        if molecules is not None and (not self.symmetric or int(molecules[3]) > MOL_ROWPTR_MAX_ATOMS
+                                      or int(molecules[2].shape[0]) < 1):
+            molecules = None
         if with_transpose is None:
-            with_transpose = self.symmetric and torch.is_grad_enabled()
+            with_transpose = self.symmetric and torch.is_grad_enabled() and molecules is None
         self.E = int(edge_src.shape[0])
         self.N = int(num_nodes)
         self.T = int(num_triplets)
@@ -99,6 +110,13 @@ class LineGraph:
         # the center kernels' workgroup units (data.center_packs; None: one atom per workgroup): int32 [N] the
         # atoms unit by unit, int32 [P + 1] the units' bounds in it, and the largest unit's row count
         self.center_order = self.center_packs = self.center_rows = None
+        if molecules is not None:
+            mol_ptr, line_ptr, trips, max_atoms = molecules
+            call("x2g_vertex_to_edge_sym_mol", ptr(edge_src), ptr(edge_dst), self.E, self.N, self.T, ptr(mol_ptr),
+                 ptr(line_ptr), ptr(trips), int(trips.shape[0]), int(max_atoms), ptr(self.atom_rowptr),
+                 ptr(self.trip_rowptr), ptr(self.trip_src), ptr(self.trip_dst), ptr(self.atom_j), ptr(self.atom_i),
+                 ptr(self.atom_k), ptr(self.edge_rev), ptr(self.rev_trip), stream_ptr())
+            return
         if with_transpose and self.symmetric:
             self._src_rowptr = torch.empty(self.E + 1, **i32)
             self._src_perm = torch.empty(self.T, **i32)

@@ -65,8 +65,11 @@ class GraphPlan:
         # the int32 index forms: collate's (x2gnn's own batches) or x2g_batch_meta's (a foreign batch)
         st = meta.get("index") or data._store
         if "_x2g_edge_src" in st and st["_x2g_edge_src"].device == dev:
+            mols = None
+            if st.get("_x2g_mol_trips") is not None and st["_x2g_mol_trips"].device == dev:
+                mols = (st["_x2g_mol_ptr"], st["_x2g_line_ptr"], st["_x2g_mol_trips"], st["_x2g_max_mol_atoms"])
             p.lg = ops.LineGraph(st["_x2g_edge_src"], st["_x2g_edge_dst"], p.num_atoms, p.num_triplets,
-                                 st.get("_x2g_symmetric", False))
+                                 st.get("_x2g_symmetric", False), molecules=mols)
             p.line_ptr, p.mol_ptr, p.dst_type = st["_x2g_line_ptr"], st["_x2g_mol_ptr"], st["_x2g_dst_type"]
             src_type = st.get("_x2g_src_type")
             p.lg.atom_type = st.get("_x2g_atom_type")
