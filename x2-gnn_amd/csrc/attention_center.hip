@@ -279,8 +279,9 @@ constexpr int kSfL = 7;                  // angular orders (sbf_dim 42 = 7 x 6)
 constexpr int kSfR = 6;                  // radial functions per order
 constexpr int kSfK = kSfL * kSfR;        // 42
 
+// (4 waves per SIMD, two 8-wave workgroups per CU: at most 128 VGPRs)
 template <int LPH, int WAVES, int B, bool EDGE>
-__global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_sf_kernel(const FwdSfArgs a) {
+__global__ void __launch_bounds__(64 * WAVES, 4) attn_fwd_center_sf_kernel(const FwdSfArgs a) {
   // [tables] then [rows][32] (k + e), [rows][32] (v + e), [rows][7][32] P, [rows][42] R
   extern __shared__ cf4 lds[];
   const UnitRows u = unit_rows_carve(reinterpret_cast<int*>(lds), a.max_rows);
@@ -769,23 +770,27 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const Bw
   }
 }
 
+// packs (<= 16 rows) on 8 waves, one atom per workgroup on 4 (its degree's rows in 1-2 rounds of 8 owners:
+// every owner of a workgroup walks a block of the same size, so the phase barriers wait for no straggler)
 template <int LPH>
 int bwd_center_launch(const BwdCenterArgs& a, bool edge, hipStream_t st) {
-  constexpr int W = 8, B = 8;
+  constexpr int B = 8;
   constexpr int H = 32 / LPH;
   const size_t lds = bwd_center_lds<H>(a.max_rows);
   if (lds > 160 * 1024) return X2G_EUNSUPPORTED;
   const unsigned grid = static_cast<unsigned>(a.n_units);
-  auto go = [&](auto kern) -> int {
+  auto go = [&](auto kern, int waves) -> int {
     if (lds > 64 * 1024) {  // above the default dynamic-LDS limit
       const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
       if (e != hipSuccess) return static_cast<int>(e);
     }
-    kern<<<grid, 64 * W, lds, st>>>(a);
+    kern<<<grid, 64 * waves, lds, st>>>(a);
     return last_launch_status();
   };
-  return edge ? go(attn_bwd_center_kernel<LPH, W, B, true>) : go(attn_bwd_center_kernel<LPH, W, B, false>);
+  if (a.packs)
+    return edge ? go(attn_bwd_center_kernel<LPH, 8, B, true>, 8) : go(attn_bwd_center_kernel<LPH, 8, B, false>, 8);
+  return edge ? go(attn_bwd_center_kernel<LPH, 4, B, true>, 4) : go(attn_bwd_center_kernel<LPH, 4, B, false>, 4);
 }
 
 }  // namespace

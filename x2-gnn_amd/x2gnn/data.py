@@ -206,9 +206,11 @@ def _add_device_indices(b, nodes, edges):
         b._store["_x2g_max_mol_atoms"] = int(nodes.max()) if len(nodes) else 0
     deg = np.bincount(ei_np[0], minlength=int(nodes.sum()))
     b._store["_x2g_max_degree"] = int(deg.max()) if deg.size else 0
-    # the center-atom kernels' workgroup units: atoms packed by degree, the longest units first
+    # the center-atom kernels' workgroups: one atom each by decreasing degree (the longest blocks first), and
+    # the fused forward's units of atoms packed by degree (the longest units first)
+    b._store["_x2g_center_order"] = torch.from_numpy(np.argsort(-deg, kind="stable").astype(np.int32))
     order, packs, rows = center_packs(deg)
-    b._store["_x2g_center_order"] = torch.from_numpy(order)
+    b._store["_x2g_pack_order"] = torch.from_numpy(order)
     b._store["_x2g_center_packs"] = torch.from_numpy(packs)
     b._store["_x2g_center_rows"] = rows
 

@@ -107,9 +107,10 @@ class LineGraph:
         # element row (int32 [N]: the key of the center-atom edge-term gradient)
         self.max_degree = None
         self.atom_type = None
-        # the center kernels' workgroup units (data.center_packs; None: one atom per workgroup): int32 [N] the
-        # atoms unit by unit, int32 [P + 1] the units' bounds in it, and the largest unit's row count
-        self.center_order = self.center_packs = self.center_rows = None
+        # the center kernels' workgroups (collate's; None: the identity): int32 [N] the atoms by decreasing
+        # degree (one per workgroup), and the fused forward's packs (data.center_packs): int32 [N] the atoms
+        # unit by unit, int32 [P + 1] the units' bounds in it, the largest unit's row count
+        self.center_order = self.pack_order = self.center_packs = self.center_rows = None
         if molecules is not None:
             mol_ptr, line_ptr, trips, max_atoms = molecules
             call("x2g_vertex_to_edge_sym_mol", ptr(edge_src), ptr(edge_dst), self.E, self.N, self.T, ptr(mol_ptr),
@@ -152,7 +153,7 @@ class LineGraph:
         lg.dst_type = lg.src_type = None
         lg.symmetric = False
         lg.edge_rev = lg.rev_trip = lg.max_degree = lg.atom_type = None
-        lg.center_order = lg.center_packs = lg.center_rows = None
+        lg.center_order = lg.pack_order = lg.center_packs = lg.center_rows = None
         ws_bytes = int(_lib.load().x2g_vertex_to_edge_workspace(lg.E, 0))
         lg._ws = torch.empty(ws_bytes, dtype=torch.uint8, device=lg.trip_src.device)
         return lg
@@ -355,13 +356,22 @@ _CENTER_BWD = True
 _CENTER_SF = True
 
 
-def _center_units(lg):
-    """(pack_ptr or None, units, max_rows) of the whole-batch center kernels: the batch's packs of atoms
-    (data.center_packs) when it has them, else one atom per workgroup."""
+def _center_units(lg, packed):
+    """(order, pack_ptr or None, units, max_rows) of a whole-batch center kernel: with ``packed`` the
+    batch's packs of atoms (data.center_packs) when it has them, else one atom per workgroup by
+    decreasing degree."""
     packs = getattr(lg, "center_packs", None)
-    if packs is not None and lg.center_order is not None and lg.center_rows is not None:
-        return packs, int(packs.shape[0]) - 1, max(int(lg.center_rows), 1)
-    return None, lg.N, max(int(lg.max_degree), 1)
+    if packed and packs is not None and lg.pack_order is not None and lg.center_rows is not None:
+        return lg.pack_order, packs, int(packs.shape[0]) - 1, max(int(lg.center_rows), 1)
+    return lg.center_order, None, lg.N, max(int(lg.max_degree), 1)
+
+
+# Workgroup packs (data.center_packs) in the fused forward: 16 owners per workgroup keep 90 % instead of
+# 57 % of them busy, and its owners never wait for one another (no barrier after the P products).  The
+# backward runs one atom per workgroup on 4 waves: with packs its five phase barriers wait for the
+# longest member's owners, and it measured 4 % slower (profiles/r5k_*).
+_PACK_FWD = True
+_PACK_BWD = False
 
 
 def _unit_rows_lds(rows):  # csrc/attention_center.hip unit_rows_lds
@@ -373,7 +383,7 @@ def _center_sf_ok(lg, factors, D):
     unit's LDS image (k + e, v + e, 7 P rows and the radial row per source row: 4.66 KB x rows) fits."""
     if not (_CENTER_SF and factors is not None and factors[1] is not None and D == 128 and lg.max_degree is not None):
         return False
-    rows = _center_units(lg)[2]
+    rows = _center_units(lg, _PACK_FWD)[3]
     return _unit_rows_lds(rows) + 4776 * rows <= 160 * 1024
 
 
@@ -416,10 +426,10 @@ class _SBFAttention(torch.autograd.Function):
             # lin_sbf fused into the center forward: S_t rebuilt per center atom from the sbf factors; its
             # rows stored only when a backward will read them
             sproj = torch.empty(T, D, dtype=torch.float32, device=dev) if any(ctx.needs_input_grad) else None
-            packs, units, rows = _center_units(lg)
+            order, packs, units, rows = _center_units(lg, _PACK_FWD)
             call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(src_row),
                  edge_mode, ptr(factors[0]), ptr(factors[1]), ptr(w_sbf), ptr(b_sbf), ptr(lg.atom_rowptr),
-                 ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order), ptr(packs), 0, units, rows, E, T, heads,
+                 ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(order), ptr(packs), 0, units, rows, E, T, heads,
                  channels, ptr(out), ptr(alpha), ptr(smax), ptr(sden), ptr(rstats), ptr(sproj), stream_ptr())
         else:
             # S = lin_sbf(sbf) once per layer [T, D], right before this layer's attention (so it is still
@@ -504,7 +514,7 @@ class _SBFAttention(torch.autograd.Function):
         gfold = torch.empty(E, 8, D, dtype=torch.float32, device=dev)
         st = stream_ptr()
         center, src_row = _center_rows(lg, mode, ctx.edge_row, D, channels)
-        packs, units, rows = _center_units(lg) if center else (None, 0, 0)
+        order, packs, units, rows = _center_units(lg, _PACK_BWD) if center else (None, None, 0, 0)
         if center and _CENTER_BWD and getattr(lg, "atom_type", None) is not None and (
                 _lib.load().x2g_sbf_attention_bwd_center_lds(rows, heads) <= 160 * 1024):
             # one launch for both passes, per center atom (csrc/attention_center.hip); the edge term's
@@ -513,7 +523,7 @@ class _SBFAttention(torch.autograd.Function):
             d_edge_atom = torch.empty(lg.N, D, dtype=torch.float32, device=dev) if want_edge else None
             g_work = torch.empty(2, T, heads, dtype=torch.float32, device=dev)
             call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(src_row), mode, ptr(sproj),
-                 ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order), ptr(packs),
+                 ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(order), ptr(packs),
                  ptr(alpha), ptr(smax), ptr(sden), ptr(dout), units, rows, E, T, heads, channels, ptr(dq), ptr(dk),
                  ptr(dv), ptr(gfold), ptr(d_edge_atom), ptr(g_work), st)
             d_edge = None

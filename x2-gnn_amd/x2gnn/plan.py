@@ -74,6 +74,7 @@ class GraphPlan:
             src_type = st.get("_x2g_src_type")
             p.lg.atom_type = st.get("_x2g_atom_type")
             p.lg.center_order = st.get("_x2g_center_order")
+            p.lg.pack_order = st.get("_x2g_pack_order")
             p.lg.center_packs = st.get("_x2g_center_packs")
             p.lg.center_rows = st.get("_x2g_center_rows")
         else:
