@@ -196,7 +196,6 @@ def attention_probe(model, batch, reps):
     sf = center and ops._center_sf_ok(lg, (radial, ylm), D)
 
     order, packs, units, rows = ops._center_units(lg, ops._PACK_FWD) if center else (None, None, 0, 0)
-    border, bpacks, bunits, brows = ops._center_units(lg, ops._PACK_BWD) if center else (None, None, 0, 0)
 
     def fwd_sf():  # the model's forward with lin_sbf fused (S rebuilt per workgroup unit; S rows stored)
         call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(src_row),
@@ -204,10 +203,10 @@ def attention_probe(model, batch, reps):
              ptr(lg.rev_trip), ptr(order), ptr(packs), 0, units, rows, E, T, H, C, ptr(out), ptr(alpha),
              ptr(smax), ptr(sden), None, ptr(sproj), stream_ptr())
 
-    def bwd_center():  # both backward passes in one launch per workgroup unit (center atom or pack)
+    def bwd_center():  # both backward passes in one launch per center atom
         call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(table), ptr(src_row), ops.EDGE_PER_DST,
-             ptr(sproj), ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(border),
-             ptr(bpacks), ptr(alpha), ptr(smax), ptr(sden), ptr(dout), bunits, brows, E, T, H, C, ptr(dq), ptr(dk),
+             ptr(sproj), ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order),
+             ptr(alpha), ptr(smax), ptr(sden), ptr(dout), lg.N, lg.max_degree, E, T, H, C, ptr(dq), ptr(dk),
              ptr(dv), ptr(gfold), ptr(atom_de), ptr(g_work), stream_ptr())
 
     row_b = 4 * D

@@ -295,7 +295,7 @@ int x2g_sbf_attention_fwd_center(const float* q, const float* k, const float* v,
                                  int64_t num_edges, int64_t num_triplets, int32_t heads, int32_t channels, float* out,
                                  float* alpha_raw, float* seg_max, float* seg_den, float* row_stats, void* stream);
 
-/* Workgroup UNITS of the two whole-batch center kernels below: with pack_ptr (int32 [units + 1], or NULL)
+/* Workgroup UNITS of the fused-projection center forward below: with pack_ptr (int32 [units + 1], or NULL)
  * unit u is the PACK of center atoms atom_order[pack_ptr[u]] .. atom_order[pack_ptr[u + 1] - 1] (at most
  * 32 atoms; every atom of the batch in exactly one pack, atoms without edges included), processed side by
  * side by one workgroup (its 16 half-wave owners take the rows of all of them: x2gnn packs the atoms
@@ -321,26 +321,26 @@ int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, const float*
                                     int32_t heads, int32_t channels, float* out, float* alpha_raw, float* seg_max,
                                     float* seg_den, float* row_stats, float* sbfproj_out, void* stream);
 
-/* The whole attention backward over a SYMMETRIC line graph in ONE launch, one workgroup per unit (center
- * atom or pack, above; csrc/attention_center.hip): the block's rows (k + e of its sources, dout and q of
- * its destinations, their softmax max / denominator) staged in LDS, then per source j a pass over its
- * triplets' S rows, alpha (dv, and a_t, g_t into the g_work [2, T, heads] scratch), rho per destination,
- * and per source / destination dk, the folded lin_sbf gradient G (from Y) and dq.  Replaces
- * x2g_sbf_attention_bwd_dst_g + x2g_sbf_attention_bwd_src_fold on such graphs (same dq, dk, dv,
- * radial_grad = G [E, 8, HC]; fp32 rounding apart), reading S once instead of twice and no row gathers;
- * d_edge_atom [N, HC] (or NULL) = the per-CENTER-ATOM gradient of the edge term (sum over the atom's
- * sources of dk + dv; zero for an atom without edges): the element-table gradient is its keyed sum by
- * atom element.  sph_y [T, 8] as x2g_spherical_basis writes it.  LDS per workgroup:
- * x2g_sbf_attention_bwd_center_lds(max_rows, heads) bytes (<= 160 KiB, else X2G_EUNSUPPORTED).
- * heads * channels = 128, channels a multiple of 4, 16-byte aligned rows, T * 512 < 2^31. */
-size_t x2g_sbf_attention_bwd_center_lds(int32_t max_rows, int32_t heads);
+/* The whole attention backward over a SYMMETRIC line graph in ONE launch, one workgroup per center atom
+ * (csrc/attention_center.hip): the block's rows (k + e of its sources, dout and q of its destinations,
+ * their softmax max / denominator) staged in LDS, then per source j a pass over its triplets' S rows,
+ * alpha (dv, and a_t, g_t into the g_work [2, T, heads] scratch), rho per destination, and per source /
+ * destination dk, the folded lin_sbf gradient G (from Y) and dq.  Replaces x2g_sbf_attention_bwd_dst_g + x2g_sbf_attention_bwd_src_fold on such
+ * graphs (same dq, dk, dv, radial_grad = G [E, 8, HC]; fp32 rounding apart), reading S once instead of
+ * twice and no row gathers; d_edge_atom [num_atoms, HC] (or NULL) = the per-CENTER-ATOM gradient of the
+ * edge term (sum over the atom's sources of dk + dv): the element-table gradient is its keyed sum by
+ * atom element.  atom_order (or NULL): workgroup w takes atom atom_order[w] (x2gnn: by decreasing degree).
+ * sph_y [T, 8] as x2g_spherical_basis writes it.  LDS per workgroup:
+ * x2g_sbf_attention_bwd_center_lds(max_degree, heads) bytes (<= 160 KiB, else X2G_EUNSUPPORTED).
+ * heads * channels = 128, channels a multiple of 4, 16-byte aligned rows. */
+size_t x2g_sbf_attention_bwd_center_lds(int32_t max_degree, int32_t heads);
 int x2g_sbf_attention_bwd_center(const float* q, const float* k, const float* v, const float* edge,
                                  const int32_t* src_row, int edge_mode, const float* sbfproj, const float* sph_y,
                                  const int32_t* atom_rowptr, const int32_t* edge_rev, const int32_t* rev_trip,
-                                 const int32_t* atom_order, const int32_t* pack_ptr, const float* alpha_raw,
-                                 const float* seg_max, const float* seg_den, const float* dout, int64_t num_units,
-                                 int32_t max_rows, int64_t num_edges, int64_t num_triplets, int32_t heads,
-                                 int32_t channels, float* dq, float* dk, float* dv, float* radial_grad,
+                                 const int32_t* atom_order, const float* alpha_raw, const float* seg_max,
+                                 const float* seg_den, const float* dout,
+                                 int64_t num_atoms, int32_t max_degree, int64_t num_edges, int64_t num_triplets,
+                                 int32_t heads, int32_t channels, float* dq, float* dk, float* dv, float* radial_grad,
                                  float* d_edge_atom, float* g_work, void* stream);
 
 /* Backward, destination-major: dq[E,HC]; d_edge ([E,HC] per destination for EDGE_PER_DST,

@@ -1,6 +1,6 @@
 """Regenerate x2-gnn_amd/ab/attention_center_ab.hip from csrc/attention_center.hip with the phase stamps of the
 center backward (scripts/trace_center_bwd.py reads them): thread 0 of each workgroup stamps the 100 MHz wall
-clock at kernel start, after staging, after its pass 1, after the fence barrier, after rho + dq, after pass 2 and
+clock at kernel start, after staging, after its pass 1, after the fence barrier, after rho, after pass 2 and
 at the end (CTR(0..6), compiled only with -DX2G_TRACE).  Then:
     make -C x2-gnn_amd ab AB_UNIT=attention_center AB_NAME=ctrace AB_FLAGS=-DX2G_TRACE"""
 import os
@@ -42,15 +42,15 @@ def after(s, start, marker, text):
     return s[:j] + text + s[j:]
 
 
-j = s.index("  __syncthreads();\n  auto rsrc", i) + len("  __syncthreads();\n")
-s = s[:j] + "  CTR(1);\n" + s[j:]
+s = after(s, i, "  __syncthreads();\n  const int nt = n - 1;  // triplets per destination (and per source)\n",
+          "  CTR(1);\n")
 j = s.index("  // the scratch written by every owner is read by others below", i)
 s = s[:j] + "  CTR(2);\n" + s[j:]
 s = after(s, i, "  __threadfence_block();\n  __syncthreads();\n", "  CTR(3);\n")
-s = after(s, i, "    st4(a.dq + static_cast<int64_t>(DI[gr]) * kCD + c0, dq);\n  }\n  __syncthreads();\n", "  CTR(4);\n")
+s = after(s, i, "    if (leader) RHO[i * H + head] = rho;\n  }\n  __syncthreads();\n", "  CTR(4);\n")
 j = s.index("  if (a.d_edge) {  // d_edge[b] = sum_j (dv_j + dk_j), j ascending", i)
 s = s[:j] + "  CTR(5);\n" + s[j:]
-s = after(s, i, "      st4(a.d_edge + static_cast<int64_t>(u.MA[m]) * kCD + c0, s);\n    }\n  }\n", "  CTR(6);\n")
+s = after(s, i, "      st4(a.d_edge + b * kCD + c0, s);\n    }\n  }\n", "  CTR(6);\n")
 # the fused-projection forward
 i = s.index("attn_fwd_center_sf_kernel(const FwdSfArgs a) {")
 s = s[:i] + s[i:].replace("{", "{\n  FTR(0);", 1)

@@ -1,10 +1,10 @@
 """Phase timeline of the center-atom attention backward (x2g_sbf_attention_bwd_center; A/B trace build
 only: make -C x2-gnn_amd ab AB_UNIT=attention_center AB_NAME=ctrace AB_FLAGS=-DX2G_TRACE, run with
-X2G_LIB=.../libx2g_ctrace.so).  Thread 0 of every workgroup (one per unit: a center atom or a pack) stamps a 100 MHz clock at
+X2G_LIB=.../libx2g_ctrace.so).  Thread 0 of every workgroup (one per center atom) stamps a 100 MHz clock at
 its phase boundaries: start, staging done, pass 1 done (its own), fence + barrier, rho + barrier, pass 2
 done, end.  Prints per-phase medians / p90 over the workgroups and how the workgroups overlap in time.
 
-    python scripts/trace_center_bwd.py [molecules] [packs|degree|ident]"""
+    python scripts/trace_center_bwd.py [molecules] [degree|ident]"""
 import ctypes
 import os
 import sys
@@ -31,24 +31,12 @@ z = b.x.to(dev)
 lg.src_type, lg.dst_type, lg.atom_type = ops._i32(z[ei[0]]), ops._i32(z[ei[1]]), ops._i32(z)
 deg_all = np.bincount(b.edge_index[0].numpy(), minlength=n)
 md = int(deg_all.max())
-# workgroup units: the model's packs (data.center_packs); "ident": one atom per workgroup, identity order;
-# "degree": one atom per workgroup, by decreasing degree
-mode = sys.argv[2] if len(sys.argv) > 2 else "packs"
-packs = None
-if mode == "packs":
-    from x2gnn.data import center_packs
-
-    po, pp, rows = center_packs(deg_all)
-    order = torch.from_numpy(po).to(dev)
-    packs = torch.from_numpy(pp).to(dev)
-    units = len(pp) - 1
-    unit_rows = np.array([deg_all[po[pp[u]:pp[u + 1]]].sum() for u in range(units)])
-    unit_maxdeg = np.array([deg_all[po[pp[u]:pp[u + 1]]].max() for u in range(units)])
-else:
-    rows, units = md, n
-    order = None if mode == "ident" else torch.from_numpy(np.argsort(-deg_all, kind="stable").astype(np.int32)).to(dev)
-    ordn = order.cpu().numpy() if order is not None else np.arange(n)
-    unit_rows = unit_maxdeg = deg_all[ordn]
+# launch order: by decreasing degree (the model's), or the identity with "ident" as the second argument
+mode = sys.argv[2] if len(sys.argv) > 2 else "degree"
+rows, units = md, n
+order = None if mode == "ident" else torch.from_numpy(np.argsort(-deg_all, kind="stable").astype(np.int32)).to(dev)
+ordn = order.cpu().numpy() if order is not None else np.arange(n)
+unit_rows = unit_maxdeg = deg_all[ordn]
 E, H, C, D = lg.E, 16, 8, 128
 g = torch.Generator(device=dev).manual_seed(3)
 q, k, v, skip, dout = (torch.randn(E, D, device=dev, generator=g) for _ in range(5))
@@ -70,7 +58,7 @@ for it in range(6):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(table), ptr(lg.src_type), ops.EDGE_PER_DST,
-         ptr(S), ptr(y), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(order), ptr(packs), ptr(alpha),
+         ptr(S), ptr(y), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(order), ptr(alpha),
          ptr(smax), ptr(sden), ptr(dout), units, rows, E, T, H, C, ptr(dq), ptr(dk), ptr(dv), ptr(G), ptr(de), ptr(gw),
          stream_ptr())
     e1.record()
@@ -87,7 +75,7 @@ t0 = t[:, 0].min()
 print(f"{mode}: atoms {n}, workgroups {units} (with rows {live.sum()}), E {E}, T {T}, max degree {md}, max rows {rows}; "
       f"kernel (events) "
       f"{np.median(ev):.1f} us; span of the stamps {(t[:, 6].max() - t0) / 100:.1f} us")
-names = ["staging", "pass 1 (own)", "fence + barrier", "rho + dq + barrier", "pass 2", "d_edge + end"]
+names = ["staging", "pass 1 (own)", "fence + barrier", "rho + barrier", "pass 2", "d_edge + end"]
 for kk, name in enumerate(names):
     d = (t[:, kk + 1] - t[:, kk]) / 100.0
     print(f"  {name:16s} median {np.median(d):7.2f} us  p90 {np.percentile(d, 90):7.2f}  max {d.max():7.2f}")

@@ -2010,10 +2010,10 @@ def test_center_forward_edge_cases(cuda):
         assert torch.equal(x, y)
 
 
-def _bwd_both(lg, q, k, v, S, table, mode, heads, channels, seed, packed=False):
+def _bwd_both(lg, q, k, v, S, table, mode, heads, channels, seed):
     """(center, destination-major fold) backward outputs on the same forward state: dq, dk, dv, G and the
-    element-table gradient of the edge term (keyed sums in fp64); ``packed``: the center kernel over the
-    batch's workgroup packs (data.center_packs), and its per-atom edge-term rows appended raw."""
+    element-table gradient of the edge term (keyed sums in fp64), then the center kernel's per-atom
+    edge-term rows raw."""
     from x2gnn import _lib, ops
     from x2gnn._lib import call, ptr, stream_ptr
 
@@ -2031,20 +2031,14 @@ def _bwd_both(lg, q, k, v, S, table, mode, heads, channels, seed, packed=False):
     dq, dk, dv = (torch.full((E, D), float("nan"), **f) for _ in range(3))
     G = torch.full((E, 8, D), float("nan"), **f)
     de_atom = torch.full((lg.N, D), float("nan"), **f) if edge is not None else None
-    order, packs, units, max_rows = lg.center_order, None, lg.N, lg.max_degree
-    if packed:
-        order, packs, max_rows = lg.packed
-        units = int(packs.shape[0]) - 1
-    assert int(_lib.load().x2g_sbf_attention_bwd_center_lds(max_rows, heads)) <= 160 * 1024
+    assert int(_lib.load().x2g_sbf_attention_bwd_center_lds(lg.max_degree, heads)) <= 160 * 1024
     call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(lg.src_type) if edge is not None else None,
-         mode, ptr(S), ptr(y), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(order), ptr(packs),
-         ptr(alpha), ptr(smax), ptr(sden), ptr(dout), units, max_rows, E, T, heads, channels, ptr(dq), ptr(dk),
+         mode, ptr(S), ptr(y), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order),
+         ptr(alpha), ptr(smax), ptr(sden), ptr(dout), lg.N, lg.max_degree, E, T, heads, channels, ptr(dq), ptr(dk),
          ptr(dv), ptr(G), ptr(de_atom), ptr(torch.empty(2, T, H, **f)), stream_ptr())
     c = [dq, dk, dv, G]
     if edge is not None:
         c.append(torch.zeros(rows, D, dtype=torch.float64, device=q.device).index_add_(0, lg.atom_type.long(), de_atom.double()))
-        if packed:
-            c.append(de_atom)
     # destination-major fold passes
     dq2, dk2, dv2 = (torch.empty(E, D, **f) for _ in range(3))
     G2 = torch.empty(E, 8, D, **f)
@@ -2092,10 +2086,6 @@ def test_center_backward_equals_fold_passes(cuda, heads, channels):
     for mode in (ops.EDGE_PER_DST, ops.EDGE_NONE):
         c, r = _bwd_both(lg, q, k, v, S, table, mode, heads, channels, 6)
         _close_bwd(c, r)
-        # the model's launch: atoms packed into workgroups of <= 16 rows -- the same bits
-        cp, _ = _bwd_both(lg, q, k, v, S, table, mode, heads, channels, 6, packed=True)
-        for x, y in zip(cp, c):
-            assert torch.equal(x, y)
 
 
 def test_center_backward_edge_cases(cuda):
@@ -2115,17 +2105,12 @@ def test_center_backward_edge_cases(cuda):
     q, k, v, _, S, table = _attn_inputs(lg, cuda, 7)
     c, r = _bwd_both(lg, q, k, v, S, table, ops.EDGE_PER_DST, 16, 8, 8)
     _close_bwd(c, r)
-    # packed: the isolated atom shares a unit with others (its edge-term row zero), the hub is alone
-    cp, _ = _bwd_both(lg, q, k, v, S, table, ops.EDGE_PER_DST, 16, 8, 8, packed=True)
-    for x, y in zip(cp, c):
-        assert torch.equal(x, y)
-    assert float(cp[-1][3].abs().max()) == 0.0  # atom 3: no edges
     from x2gnn import _lib
 
     assert int(_lib.load().x2g_sbf_attention_bwd_center_lds(130, 16)) > 160 * 1024 or 130 > ops.CENTER_MAX_DEGREE
     rc = _lib.load().x2g_sbf_attention_bwd_center(None, None, None, None, None, 0, None, None, None, None, None, None,
-                                                   None, None, None, None, None, 1, 130, 1, 1, 16, 8, None, None, None,
-                                                   None, None, None, None)
+                                                   None, None, None, None, 1, 130, 1, 1, 16, 8, None, None, None, None,
+                                                   None, None, None)
     assert rc == 1002  # X2G_EUNSUPPORTED
 
 

@@ -495,55 +495,48 @@ int fwd_center_launch(const FwdCenterArgs& a, bool edge, int max_degree, hipStre
 }
 
 // ------------------------------------------------------------------------------ fused backward
-// One workgroup per unit (a center atom b, or a pack of them: its 16 half-wave owners take the blocks' rows)
-// does BOTH backward passes of the destination-major kernels (attention_fold.inc) over its triplet blocks,
-// from LDS images of the blocks' rows:
+// One workgroup per center atom b does BOTH backward passes of the destination-major kernels
+// (attention_fold.inc) over b's triplet block, from LDS images of the block's rows:
 //   KE[j] = k_j + e, GO[i] = dout[d_i], QI[i] = q[d_i], per-destination max / 1 / (den + eps);
-// pass 1, one owner per SOURCE row j (its S rows t(i, j) = TB[i] + j - [j > i], one 512-byte row each):
+// pass 1, one owner per SOURCE j (its S rows t(i, j) = TB[i] + j - [j > i], one 512-byte row each):
 //   at = exp(alpha_t - max_i) / (den_i + eps),  g_t = sum over the head of go_i (v_j + e) S_t,
 //   dv_j += at go_i S_t,  and (at, g_t) into a [2, T, H] scratch (L2-resident until the same workgroup
 //   reads it back);
-// then per DESTINATION row i, over its contiguous triplets (j ascending: the destination pass's order):
-//   rho_i = sum_j at g,  dq_i = sum_j at (g - rho_i) / sqrt(C) (k_j + e);
-// and pass 2 per SOURCE row j (at, g from the scratch, Y_t, rows from LDS):
-//   w = at (g - rho_i) / sqrt(C),  dk_j = sum_i w q_i,  G_j[l] = sum_i at go_i (v_j + e) Y_l(t)  (the folded
-//   lin_sbf gradient),
+// then rho_i = sum_j at g (j ascending: the destination pass's order) over destination i's contiguous
+// block, and pass 2 (at, g from the scratch, Y_t, rows from LDS), per owner both roles:
+//   w = at (g - rho_i) / sqrt(C),  dk_j = sum_i w q_i,  G_j[l] = sum_i at go_i (v_j + e) Y_l(t)  (source j:
+//   the folded lin_sbf gradient),  dq_i = sum_j w (k_j + e)  (destination i),
 // and, for the element-table gradient, d_edge[b] = sum_j (dk_j + dv_j) (X2-GNN's edge term enters as
 // k_j + e and v_j + e with e the center atom's row: its gradient is the block's sum).  S is read once per
 // backward (the two destination-major passes read S twice and gather k / v / q / dout rows per triplet
-// from L2); only pass 1 holds S rows and only pass 2 the 32 G accumulators, so every loop takes 8
-// triplets per memory round trip within the 128 VGPRs of 4 waves per SIMD.
+// from L2), only pass 1 holds S rows and only pass 2 the 32 G accumulators, so both take 8 triplets per
+// memory round trip within 128 VGPRs.
 struct BwdCenterArgs {
   const float *q, *k, *v, *edge;
   const int32_t* src_row;
   const float *sp, *alpha, *smax, *sden, *dout, *y;
   const int32_t *atom_rowptr, *edge_rev, *rev_trip;
-  const int32_t* order;  // unit -> center atom(s) (NULL: the identity)
-  const int32_t* packs;  // unit u = atoms order[packs[u]] .. order[packs[u + 1] - 1] (NULL: one atom per unit)
-  int64_t n_units, T;
-  int max_rows;
+  const int32_t* order;  // workgroup -> center atom (NULL: blockIdx.x)
+  int64_t n_atoms, T;
   int H;
   float inv_sqrt_c;
   float *dq, *dk, *dv, *gfold, *d_edge, *gw;  // gw: [2, T, H] scratch (g, then a)
 };
 
 template <int H>
-__host__ __device__ constexpr size_t bwd_center_lds(int rows) {
-  return unit_rows_lds(rows)                       // row / member tables
-         + static_cast<size_t>(rows) * 4 * kCD * 4  // KE, GO, QI, DE
-         + static_cast<size_t>(rows) * H * 4 * 3    // MX, IV, RHO
-         + static_cast<size_t>(rows) * 4 * 2;       // TB, DI
+__host__ __device__ constexpr size_t bwd_center_lds(int n) {
+  return static_cast<size_t>(n) * 4 * kCD * 4  // KE, GO, QI, DE
+         + static_cast<size_t>(n) * H * 4 * 3  // MX, IV, RHO
+         + static_cast<size_t>(n) * 4 * 2;     // TB, DI
 }
 
-// (4 waves per SIMD: at most 128 VGPRs; left to itself the compiler takes 179 for a 512-thread workgroup)
 template <int LPH, int WAVES, int B, bool EDGE>
-__global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const BwdCenterArgs a) {
+__global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCenterArgs a) {
   constexpr int H = 32 / LPH;
   extern __shared__ cf4 lds[];
-  const UnitRows u = unit_rows_carve(reinterpret_cast<int*>(lds), a.max_rows);
-  unit_rows_build(u, a.order, a.packs, blockIdx.x, a.atom_rowptr, EDGE ? a.src_row : nullptr);
-  __syncthreads();
-  const int n_rows = uniform(u.NRS[0]), n_mem = uniform(u.NRS[1]);
+  const int64_t b = a.order ? static_cast<int64_t>(a.order[blockIdx.x]) : static_cast<int64_t>(blockIdx.x);
+  const int r0 = uniform(a.atom_rowptr[b]);
+  const int n = uniform(a.atom_rowptr[b + 1]) - r0;
   const int tid = threadIdx.x;
   const int l32 = tid & 31, half = (tid >> 5) & 1, wave = tid >> 6;
   const int owner = 2 * wave + half;
@@ -551,37 +544,41 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const Bw
   const int head = l32 / LPH;
   const bool leader = (l32 % LPH) == 0;
   const int c0 = 4 * l32;
-  cf4* KE = lds + unit_rows_lds(a.max_rows) / 16;
-  cf4* GO = KE + n_rows * 32;
-  cf4* QI = GO + n_rows * 32;
-  cf4* DE = QI + n_rows * 32;
-  float* MX = reinterpret_cast<float*>(DE + n_rows * 32);
-  float* IV = MX + n_rows * H;
-  float* RHO = IV + n_rows * H;
-  int* TB = reinterpret_cast<int*>(RHO + n_rows * H);
-  int* DI = TB + n_rows;
-  // ---- staging: each row's destination and triplet block first (one round trip), then every row load
-  // from addresses in LDS (one more)
-  for (int idx = tid; idx < n_rows; idx += 64 * WAVES) {
-    TB[idx] = a.rev_trip[u.LN[idx]];
-    DI[idx] = a.edge_rev[u.LN[idx]];
+  if (n <= 0) {  // an atom without edges: its element-table gradient row is zero
+    if (a.d_edge && tid < 32) st4(a.d_edge + b * kCD + c0, cf4{0.f, 0.f, 0.f, 0.f});
+    return;
   }
-  __syncthreads();
-  for (int idx = tid; idx < n_rows * 32; idx += 64 * WAVES) {
-    const int r = idx >> 5, c = idx & 31;
-    const int64_t d = DI[r];
-    const cf4 e4 = EDGE ? ld4(a.edge + static_cast<int64_t>(u.ER[r]) * kCD + 4 * c) : cf4{0.f, 0.f, 0.f, 0.f};
-    KE[idx] = ld4(a.k + static_cast<int64_t>(u.LN[r]) * kCD + 4 * c) + e4;
+  cf4* KE = lds;
+  cf4* GO = KE + n * 32;
+  cf4* QI = GO + n * 32;
+  cf4* DE = QI + n * 32;
+  float* MX = reinterpret_cast<float*>(DE + n * 32);
+  float* IV = MX + n * H;
+  float* RHO = IV + n * H;
+  int* TB = reinterpret_cast<int*>(RHO + n * H);
+  int* DI = TB + n;
+  const int64_t e_row = EDGE ? static_cast<int64_t>(uniform(a.src_row[r0])) * kCD : 0;
+  // ---- staging
+  for (int idx = tid; idx < n * 32; idx += 64 * WAVES) {
+    const int j = idx >> 5, c = idx & 31;
+    const int64_t d = a.edge_rev[r0 + j];
+    const cf4 e4 = EDGE ? ld4(a.edge + e_row + 4 * c) : cf4{0.f, 0.f, 0.f, 0.f};
+    KE[idx] = ld4(a.k + static_cast<int64_t>(r0 + j) * kCD + 4 * c) + e4;
     GO[idx] = ld4(a.dout + d * kCD + 4 * c);
     QI[idx] = ld4(a.q + d * kCD + 4 * c);
   }
-  for (int idx = tid; idx < n_rows * H; idx += 64 * WAVES) {
-    const int r = idx / H, h = idx - r * H;
-    const int64_t d = DI[r];
+  for (int idx = tid; idx < n * H; idx += 64 * WAVES) {
+    const int i = idx / H, h = idx - i * H;
+    const int64_t d = a.edge_rev[r0 + i];
     MX[idx] = a.smax[d * H + h];
     IV[idx] = 1.0f / (a.sden[d * H + h] + kCEps);
   }
+  for (int idx = tid; idx < n; idx += 64 * WAVES) {
+    TB[idx] = a.rev_trip[r0 + idx];
+    DI[idx] = a.edge_rev[r0 + idx];
+  }
   __syncthreads();
+  const int nt = n - 1;  // triplets per destination (and per source)
   auto rsrc = [](const void* p, int64_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), static_cast<short>(0),
                                              static_cast<int>(bytes < 0x7fffffff ? bytes : 0x7fffffff), 0x00020000);
@@ -595,21 +592,17 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const Bw
   auto ldf = [](__amdgpu_buffer_rsrc_t r, int off) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
   };
-  // ---- pass 1: one owner per source row: at, g (to the scratch), dv
-  for (int gr = owner; gr < n_rows; gr += NO) {
-    const int ri = u.RI[gr];
-    const int base = ri & 0xffff, n = ri >> 16, nt = n - 1;  // the source's block: rows base .. base + n - 1
-    const int j = gr - base;
-    // the triplet of destination row base + i and source j (i != j; i == j gives some row of i's block)
-    auto trip = [&](int i) {
-      int pos = j - (j > i ? 1 : 0);
-      pos = pos < nt ? pos : nt - 1;
-      return TB[base + i] + pos;  // (32-bit offsets below: T * 512 < 2^31, checked)
-    };
-    const int ln = u.LN[gr];
-    const int64_t srow = static_cast<int64_t>(ln) * kCD + c0;
+  // the triplet of destination i and source j (i != j; i == j gives some row of i's block, unused)
+  auto trip = [&](int i, int j) {
+    int pos = j - (j > i ? 1 : 0);
+    pos = pos < nt ? pos : nt - 1;
+    return TB[i] + pos;  // (32-bit offsets below: T * 512 < 2^31, checked)
+  };
+  // ---- pass 1: one owner per source j: at, g (to the scratch), dv
+  for (int j = owner; j < n; j += NO) {
+    const int64_t srow = static_cast<int64_t>(r0 + j) * kCD + c0;
     cf4 ue = ld4(a.v + srow);
-    if (EDGE) ue += ld4(a.edge + static_cast<int64_t>(u.ER[gr]) * kCD + c0);
+    if (EDGE) ue += ld4(a.edge + e_row + c0);
     cf4 dv = {0.f, 0.f, 0.f, 0.f};
     auto batch = [&](int i0, auto bb) {
       constexpr int BB = decltype(bb)::value;
@@ -617,131 +610,103 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const Bw
       float al[BB];
       int tt[BB];
 #pragma unroll
-      for (int uu = 0; uu < BB; ++uu) {
-        const int i = i0 + uu < n ? i0 + uu : n - 1;  // clamped: loads unconditional, masked below
-        tt[uu] = trip(i);
-        sv[uu] = __builtin_bit_cast(cf4, __builtin_amdgcn_raw_buffer_load_b128(sp_r, tt[uu] * (kCD * 4) + c0 * 4, 0, 0));
-        al[uu] = ldf(al_r, (tt[uu] * H + head) * 4);
+      for (int u = 0; u < BB; ++u) {
+        const int i = i0 + u < n ? i0 + u : n - 1;  // clamped: loads unconditional, masked below
+        tt[u] = trip(i, j);
+        sv[u] = __builtin_bit_cast(cf4, __builtin_amdgcn_raw_buffer_load_b128(sp_r, tt[u] * (kCD * 4) + c0 * 4, 0, 0));
+        al[u] = ldf(al_r, (tt[u] * H + head) * 4);
       }
 #pragma unroll
-      for (int uu = 0; uu < BB; ++uu) {
-        const int i = i0 + uu < n ? i0 + uu : n - 1;
-        const bool ok = i0 + uu < n && i != j;
-        const int ir = base + i;
-        const float at = ok ? expf(al[uu] - MX[ir * H + head]) * IV[ir * H + head] : 0.f;
-        const cf4 go = GO[ir * 32 + l32];
+      for (int u = 0; u < BB; ++u) {
+        const int i = i0 + u < n ? i0 + u : n - 1;
+        const bool ok = i0 + u < n && i != j;
+        const float at = ok ? expf(al[u] - MX[i * H + head]) * IV[i * H + head] : 0.f;
+        const cf4 go = GO[i * 32 + l32];
         const cf4 gu = go * ue;
-        float gp = gu[0] * sv[uu][0];
-        gp = fmaf(gu[1], sv[uu][1], gp);
-        gp = fmaf(gu[2], sv[uu][2], gp);
-        gp = fmaf(gu[3], sv[uu][3], gp);
+        float gp = gu[0] * sv[u][0];
+        gp = fmaf(gu[1], sv[u][1], gp);
+        gp = fmaf(gu[2], sv[u][2], gp);
+        gp = fmaf(gu[3], sv[u][3], gp);
         const float g = head_sum<LPH>(gp);
         if (ok && leader) {
-          a.gw[static_cast<int64_t>(tt[uu]) * H + head] = g;
-          aw[static_cast<int64_t>(tt[uu]) * H + head] = at;
+          a.gw[static_cast<int64_t>(tt[u]) * H + head] = g;
+          aw[static_cast<int64_t>(tt[u]) * H + head] = at;
         }
-        dv += at * (go * sv[uu]);
+        dv += at * (go * sv[u]);
       }
     };
-    if (nt > 0) {  // (per owner: the two halves of a wave may hold blocks of different atoms)
+    if (nt > 0) {  // (workgroup-uniform)
       int i0 = 0;
       for (; n - i0 > B / 2; i0 += B) batch(i0, std::integral_constant<int, B>{});
       if (i0 < n) batch(i0, std::integral_constant<int, B / 2>{});
     }
     st4(a.dv + srow, dv);
-    DE[gr * 32 + l32] = dv;  // (the edge term's gradient: dk added in pass 2)
+    DE[j * 32 + l32] = dv;  // (the edge term's gradient: dk added in pass 2)
   }
   // the scratch written by every owner is read by others below: workgroup-scope release / acquire
   __threadfence_block();
   __syncthreads();
-  // ---- per destination row i: rho_i = sum_{j != i} at g over its contiguous triplets (j ascending), then
-  // dq_i = sum_j at (g - rho_i) / sqrt(C) (k_j + e) over the same triplets (their (at, g) read again)
-  for (int gr = owner; gr < n_rows; gr += NO) {
-    const int ri = u.RI[gr];
-    const int base = ri & 0xffff, nt = (ri >> 16) - 1;
-    const int i = gr - base;
+  // ---- rho_i = sum_{j != i} at g over i's contiguous block, j ascending (one owner per destination)
+  for (int i = owner; i < n; i += NO) {
     float rho = 0.f;
     for (int p0 = 0; p0 < nt; p0 += 8) {
       float at[8], g[8];
 #pragma unroll
-      for (int uu = 0; uu < 8; ++uu) {
-        const int t = TB[gr] + (p0 + uu < nt ? p0 + uu : nt - 1);
-        at[uu] = ldf(at_r, (t * H + head) * 4);
-        g[uu] = ldf(g_r, (t * H + head) * 4);
+      for (int u = 0; u < 8; ++u) {
+        const int t = TB[i] + (p0 + u < nt ? p0 + u : nt - 1);
+        at[u] = ldf(at_r, (t * H + head) * 4);
+        g[u] = ldf(g_r, (t * H + head) * 4);
       }
 #pragma unroll
-      for (int uu = 0; uu < 8; ++uu)
-        if (p0 + uu < nt) rho = fmaf(at[uu], g[uu], rho);
+      for (int u = 0; u < 8; ++u)
+        if (p0 + u < nt) rho = fmaf(at[u], g[u], rho);
     }
-    if (leader) RHO[gr * H + head] = rho;
-    cf4 dq = {0.f, 0.f, 0.f, 0.f};
-    for (int p0 = 0; p0 < nt; p0 += 8) {
-      float at[8], g[8];
-#pragma unroll
-      for (int uu = 0; uu < 8; ++uu) {
-        const int t = TB[gr] + (p0 + uu < nt ? p0 + uu : nt - 1);
-        at[uu] = ldf(at_r, (t * H + head) * 4);
-        g[uu] = ldf(g_r, (t * H + head) * 4);
-      }
-#pragma unroll
-      for (int uu = 0; uu < 8; ++uu) {
-        const int p = p0 + uu;
-        const int jr = base + p + (p >= i ? 1 : 0);  // the source of triplet p (clamped below)
-        const float ad = p < nt ? at[uu] : 0.f;
-        const float wd = ad * (g[uu] - rho) * a.inv_sqrt_c;
-        dq += wd * KE[(p < nt ? jr : base) * 32 + l32];
-      }
-    }
-    st4(a.dq + static_cast<int64_t>(DI[gr]) * kCD + c0, dq);
+    if (leader) RHO[i * H + head] = rho;
   }
   __syncthreads();
-  // ---- pass 2, per source row o (destinations x: the other n - 1 rows of its block): dk_o, G_o
-  for (int gr = owner; gr < n_rows; gr += NO) {
-    const int ri = u.RI[gr];
-    const int base = ri & 0xffff, n = ri >> 16, nt = n - 1;
-    const int o = gr - base;
-    auto trip = [&](int i) {  // the triplet of destination row base + i and source o
-      int pos = o - (o > i ? 1 : 0);
-      pos = pos < nt ? pos : nt - 1;
-      return TB[base + i] + pos;
-    };
-    const int ln = u.LN[gr];
-    const int64_t srow = static_cast<int64_t>(ln) * kCD + c0;
+  // ---- pass 2, owner o in both roles, x over the other n - 1:
+  //   source j = o (destinations i = x): dk_o, G_o;  destination i = o (sources j = x): dq_o
+  for (int o = owner; o < n; o += NO) {
+    const int64_t srow = static_cast<int64_t>(r0 + o) * kCD + c0;
     cf4 ue = ld4(a.v + srow);
-    if (EDGE) ue += ld4(a.edge + static_cast<int64_t>(u.ER[gr]) * kCD + c0);
-    cf4 dk = {0.f, 0.f, 0.f, 0.f};
+    if (EDGE) ue += ld4(a.edge + e_row + c0);
+    cf4 dk = {0.f, 0.f, 0.f, 0.f}, dq = {0.f, 0.f, 0.f, 0.f};
     cf4 G[8];
 #pragma unroll
     for (int l = 0; l < 8; ++l) G[l] = cf4{0.f, 0.f, 0.f, 0.f};
+    const float rho_o = RHO[o * H + head];
     auto batch = [&](int x0, auto bb) {
       constexpr int BB = decltype(bb)::value;
-      float ats[BB], gs[BB], yv[BB];
+      float ats[BB], gs[BB], yv[BB], atd[BB], gd[BB];
 #pragma unroll
-      for (int uu = 0; uu < BB; ++uu) {
-        const int x = x0 + uu < n ? x0 + uu : n - 1;
-        const int ts = trip(x);
-        ats[uu] = ldf(at_r, (ts * H + head) * 4);
-        gs[uu] = ldf(g_r, (ts * H + head) * 4);
-        yv[uu] = ldf(y_r, (ts * 8 + (l32 & 7)) * 4);
+      for (int u = 0; u < BB; ++u) {
+        const int x = x0 + u < n ? x0 + u : n - 1;
+        const int ts = trip(x, o), td = trip(o, x);
+        ats[u] = ldf(at_r, (ts * H + head) * 4);
+        gs[u] = ldf(g_r, (ts * H + head) * 4);
+        yv[u] = ldf(y_r, (ts * 8 + (l32 & 7)) * 4);
+        atd[u] = ldf(at_r, (td * H + head) * 4);
+        gd[u] = ldf(g_r, (td * H + head) * 4);
       }
 #pragma unroll
-      for (int uu = 0; uu < BB; ++uu) {
-        const int x = x0 + uu < n ? x0 + uu : n - 1;
-        const bool ok = x0 + uu < n && x != o;
-        const int xr = base + x;
-        const float as = ok ? ats[uu] : 0.f;
-        const float ws = as * (gs[uu] - RHO[xr * H + head]) * a.inv_sqrt_c;
-        dk += ws * QI[xr * 32 + l32];
-        const cf4 ds = (GO[xr * 32 + l32] * ue) * as;
+      for (int u = 0; u < BB; ++u) {
+        const int x = x0 + u < n ? x0 + u : n - 1;
+        const bool ok = x0 + u < n && x != o;
+        const float as = ok ? ats[u] : 0.f, ad = ok ? atd[u] : 0.f;
+        const float ws = as * (gs[u] - RHO[x * H + head]) * a.inv_sqrt_c;
+        dk += ws * QI[x * 32 + l32];
+        const float wd = ad * (gd[u] - rho_o) * a.inv_sqrt_c;
+        dq += wd * KE[x * 32 + l32];
+        const cf4 ds = (GO[x * 32 + l32] * ue) * as;
         float yl[8];
-        yl[0] = dpp_mov<0x150>(yv[uu]);
-        yl[1] = dpp_mov<0x151>(yv[uu]);
-        yl[2] = dpp_mov<0x152>(yv[uu]);
-        yl[3] = dpp_mov<0x153>(yv[uu]);
-        yl[4] = dpp_mov<0x154>(yv[uu]);
-        yl[5] = dpp_mov<0x155>(yv[uu]);
-        yl[6] = dpp_mov<0x156>(yv[uu]);
-        yl[7] = dpp_mov<0x157>(yv[uu]);
+        yl[0] = dpp_mov<0x150>(yv[u]);
+        yl[1] = dpp_mov<0x151>(yv[u]);
+        yl[2] = dpp_mov<0x152>(yv[u]);
+        yl[3] = dpp_mov<0x153>(yv[u]);
+        yl[4] = dpp_mov<0x154>(yv[u]);
+        yl[5] = dpp_mov<0x155>(yv[u]);
+        yl[6] = dpp_mov<0x156>(yv[u]);
+        yl[7] = dpp_mov<0x157>(yv[u]);
 #pragma unroll
         for (int l = 0; l < 8; ++l) G[l] += ds * yl[l];
       }
@@ -752,45 +717,39 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const Bw
       if (x0 < n) batch(x0, std::integral_constant<int, B / 2>{});
     }
     st4(a.dk + srow, dk);
-    float* gf = a.gfold + static_cast<int64_t>(ln) * 8 * kCD + c0;
+    st4(a.dq + static_cast<int64_t>(DI[o]) * kCD + c0, dq);
+    float* gf = a.gfold + static_cast<int64_t>(r0 + o) * 8 * kCD + c0;
 #pragma unroll
     for (int l = 0; l < 8; ++l) st4(gf + l * kCD, G[l]);
-    DE[gr * 32 + l32] += dk;  // (this owner's own dv row of pass 1)
+    DE[o * 32 + l32] += dk;  // (this owner's own dv row of pass 1)
   }
-  if (a.d_edge) {  // d_edge[b] = sum_j (dv_j + dk_j), j ascending, per member atom b (zero without edges)
+  if (a.d_edge) {  // d_edge[b] = sum_j (dv_j + dk_j), j ascending
     __syncthreads();
-    for (int m = owner; m < n_mem; m += NO) {
-      const int mi = u.MI[m];
-      const int base = mi & 0xffff, n = mi >> 16;
-      cf4 s = {0.f, 0.f, 0.f, 0.f};
-      if (n > 0) s = DE[base * 32 + l32];
-      for (int j = 1; j < n; ++j) s += DE[(base + j) * 32 + l32];
-      st4(a.d_edge + static_cast<int64_t>(u.MA[m]) * kCD + c0, s);
+    if (tid < 32) {
+      cf4 s = DE[l32];
+      for (int j = 1; j < n; ++j) s += DE[j * 32 + l32];
+      st4(a.d_edge + b * kCD + c0, s);
     }
   }
 }
 
-// packs (<= 16 rows) on 8 waves, one atom per workgroup on 4 (its degree's rows in 1-2 rounds of 8 owners:
-// every owner of a workgroup walks a block of the same size, so the phase barriers wait for no straggler)
 template <int LPH>
-int bwd_center_launch(const BwdCenterArgs& a, bool edge, hipStream_t st) {
-  constexpr int B = 8;
+int bwd_center_launch(const BwdCenterArgs& a, bool edge, int max_degree, hipStream_t st) {
+  constexpr int W = 4, B = 8;
   constexpr int H = 32 / LPH;
-  const size_t lds = bwd_center_lds<H>(a.max_rows);
+  const size_t lds = bwd_center_lds<H>(max_degree);
   if (lds > 160 * 1024) return X2G_EUNSUPPORTED;
-  const unsigned grid = static_cast<unsigned>(a.n_units);
-  auto go = [&](auto kern, int waves) -> int {
+  const unsigned grid = static_cast<unsigned>(a.n_atoms);
+  auto go = [&](auto kern) -> int {
     if (lds > 64 * 1024) {  // above the default dynamic-LDS limit
       const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
       if (e != hipSuccess) return static_cast<int>(e);
     }
-    kern<<<grid, 64 * waves, lds, st>>>(a);
+    kern<<<grid, 64 * W, lds, st>>>(a);
     return last_launch_status();
   };
-  if (a.packs)
-    return edge ? go(attn_bwd_center_kernel<LPH, 8, B, true>, 8) : go(attn_bwd_center_kernel<LPH, 8, B, false>, 8);
-  return edge ? go(attn_bwd_center_kernel<LPH, 4, B, true>, 4) : go(attn_bwd_center_kernel<LPH, 4, B, false>, 4);
+  return edge ? go(attn_bwd_center_kernel<LPH, W, B, true>) : go(attn_bwd_center_kernel<LPH, W, B, false>);
 }
 
 }  // namespace
@@ -798,34 +757,33 @@ int bwd_center_launch(const BwdCenterArgs& a, bool edge, hipStream_t st) {
 
 using namespace x2g;
 
-X2G_API size_t x2g_sbf_attention_bwd_center_lds(int32_t max_rows, int32_t heads) {
-  if (max_rows < 0 || heads <= 0) return 0;
-  const int n = max_rows > 0 ? max_rows : 1;
-  return unit_rows_lds(n) + static_cast<size_t>(n) * 4 * kCD * 4 + static_cast<size_t>(n) * heads * 12 +
-         static_cast<size_t>(n) * 8;
+X2G_API size_t x2g_sbf_attention_bwd_center_lds(int32_t max_degree, int32_t heads) {
+  if (max_degree < 0 || heads <= 0) return 0;
+  const int n = max_degree > 0 ? max_degree : 1;
+  return static_cast<size_t>(n) * 4 * kCD * 4 + static_cast<size_t>(n) * heads * 12 + static_cast<size_t>(n) * 8;
 }
 
 X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const float* v, const float* edge,
                                          const int32_t* src_row, int edge_mode, const float* sbfproj,
                                          const float* sph_y, const int32_t* atom_rowptr, const int32_t* edge_rev,
-                                         const int32_t* rev_trip, const int32_t* atom_order, const int32_t* pack_ptr,
-                                         const float* alpha_raw, const float* seg_max, const float* seg_den,
-                                         const float* dout, int64_t num_units, int32_t max_rows, int64_t num_edges,
-                                         int64_t num_triplets, int32_t heads, int32_t channels, float* dq, float* dk,
-                                         float* dv, float* radial_grad, float* d_edge_atom, float* g_work,
-                                         void* stream) {
-  if (num_units < 0 || num_edges < 0 || num_triplets < 0 || heads <= 0 || channels <= 0) return X2G_EINVAL;
+                                         const int32_t* rev_trip, const int32_t* atom_order, const float* alpha_raw,
+                                         const float* seg_max,
+                                         const float* seg_den, const float* dout, int64_t num_atoms,
+                                         int32_t max_degree, int64_t num_edges, int64_t num_triplets, int32_t heads,
+                                         int32_t channels, float* dq, float* dk, float* dv, float* radial_grad,
+                                         float* d_edge_atom, float* g_work, void* stream) {
+  if (num_atoms < 0 || num_edges < 0 || num_triplets < 0 || heads <= 0 || channels <= 0) return X2G_EINVAL;
   if (edge_mode != X2G_EDGE_NONE && edge_mode != X2G_EDGE_PER_DST) return X2G_EUNSUPPORTED;
-  if (heads * channels != kCD || channels % 4 || max_rows < 0 || max_rows > X2G_CENTER_MAX_DEGREE)
+  if (heads * channels != kCD || channels % 4 || max_degree < 0 || max_degree > X2G_CENTER_MAX_DEGREE)
     return X2G_EUNSUPPORTED;
-  if (x2g_sbf_attention_bwd_center_lds(max_rows, heads) > 160 * 1024) return X2G_EUNSUPPORTED;
+  if (x2g_sbf_attention_bwd_center_lds(max_degree, heads) > 160 * 1024) return X2G_EUNSUPPORTED;
   if (num_triplets * kCD * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;  // 32-bit S offsets
-  if (num_units == 0) return X2G_OK;
+  if (num_atoms == 0) return X2G_OK;
   if (num_edges > 0 && (!q || !k || !v || !sbfproj || !sph_y || !atom_rowptr || !edge_rev || !rev_trip ||
                         !alpha_raw || !seg_max || !seg_den || !dout || !dq || !dk || !dv || !radial_grad ||
                         (num_triplets > 0 && !g_work)))
     return X2G_EINVAL;
-  if (!atom_rowptr || (pack_ptr && !atom_order)) return X2G_EINVAL;
+  if (!atom_rowptr) return X2G_EINVAL;
   if (edge_mode == X2G_EDGE_PER_DST && (!edge || !src_row)) return X2G_EINVAL;
   const auto al = [](const void* p, int m) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % m == 0; };
   if (!al(q, 16) || !al(k, 16) || !al(v, 16) || !al(edge, 16) || !al(sbfproj, 16) || !al(dout, 16) || !al(dq, 16) ||
@@ -834,17 +792,17 @@ X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const f
   BwdCenterArgs a{};
   a.q = q; a.k = k; a.v = v; a.edge = edge; a.src_row = src_row; a.sp = sbfproj; a.alpha = alpha_raw;
   a.smax = seg_max; a.sden = seg_den; a.dout = dout; a.y = sph_y; a.atom_rowptr = atom_rowptr; a.edge_rev = edge_rev;
-  a.rev_trip = rev_trip; a.order = atom_order; a.packs = pack_ptr; a.n_units = num_units; a.T = num_triplets;
-  a.max_rows = max_rows > 0 ? max_rows : 1; a.H = heads;
+  a.rev_trip = rev_trip; a.order = atom_order; a.n_atoms = num_atoms; a.T = num_triplets; a.H = heads;
   a.inv_sqrt_c = static_cast<float>(1.0 / sqrt(static_cast<double>(channels)));
   a.dq = dq; a.dk = dk; a.dv = dv; a.gfold = radial_grad; a.d_edge = d_edge_atom; a.gw = g_work;
+  const int md = max_degree > 0 ? max_degree : 1;
   const bool edge_on = edge_mode == X2G_EDGE_PER_DST;
   hipStream_t st = as_stream(stream);
   switch (channels / 4) {
-    case 1: return bwd_center_launch<1>(a, edge_on, st);
-    case 2: return bwd_center_launch<2>(a, edge_on, st);
-    case 4: return bwd_center_launch<4>(a, edge_on, st);
-    case 8: return bwd_center_launch<8>(a, edge_on, st);
+    case 1: return bwd_center_launch<1>(a, edge_on, md, st);
+    case 2: return bwd_center_launch<2>(a, edge_on, md, st);
+    case 4: return bwd_center_launch<4>(a, edge_on, md, st);
+    case 8: return bwd_center_launch<8>(a, edge_on, md, st);
     default: return X2G_EUNSUPPORTED;
   }
 }

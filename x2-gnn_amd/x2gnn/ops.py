@@ -368,10 +368,9 @@ def _center_units(lg, packed):
 
 # Workgroup packs (data.center_packs) in the fused forward: 16 owners per workgroup keep 90 % instead of
 # 57 % of them busy, and its owners never wait for one another (no barrier after the P products).  The
-# backward runs one atom per workgroup on 4 waves: with packs its five phase barriers wait for the
-# longest member's owners, and it measured 4 % slower (profiles/r5k_*).
+# backward stays one atom per workgroup on 4 waves: with packs (8 waves) its phase barriers waited for
+# the longest member's owners and it measured 4 % slower (profiles/r5k_*); the packed backward was removed.
 _PACK_FWD = True
-_PACK_BWD = False
 
 
 def _unit_rows_lds(rows):  # csrc/attention_center.hip unit_rows_lds
@@ -514,18 +513,17 @@ class _SBFAttention(torch.autograd.Function):
         gfold = torch.empty(E, 8, D, dtype=torch.float32, device=dev)
         st = stream_ptr()
         center, src_row = _center_rows(lg, mode, ctx.edge_row, D, channels)
-        order, packs, units, rows = _center_units(lg, _PACK_BWD) if center else (None, None, 0, 0)
         if center and _CENTER_BWD and getattr(lg, "atom_type", None) is not None and (
-                _lib.load().x2g_sbf_attention_bwd_center_lds(rows, heads) <= 160 * 1024):
+                _lib.load().x2g_sbf_attention_bwd_center_lds(lg.max_degree, heads) <= 160 * 1024):
             # one launch for both passes, per center atom (csrc/attention_center.hip); the edge term's
             # gradient comes per center atom and is summed by the atoms' elements
             want_edge = mode == EDGE_PER_DST and ctx.needs_input_grad[4]
             d_edge_atom = torch.empty(lg.N, D, dtype=torch.float32, device=dev) if want_edge else None
             g_work = torch.empty(2, T, heads, dtype=torch.float32, device=dev)
             call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(src_row), mode, ptr(sproj),
-                 ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(order), ptr(packs),
-                 ptr(alpha), ptr(smax), ptr(sden), ptr(dout), units, rows, E, T, heads, channels, ptr(dq), ptr(dk),
-                 ptr(dv), ptr(gfold), ptr(d_edge_atom), ptr(g_work), st)
+                 ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order),
+                 ptr(alpha), ptr(smax), ptr(sden), ptr(dout), lg.N, lg.max_degree, E, T, heads, channels, ptr(dq),
+                 ptr(dk), ptr(dv), ptr(gfold), ptr(d_edge_atom), ptr(g_work), st)
             d_edge = None
             if want_edge:
                 if ctx.defer_edge:
