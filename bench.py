@@ -201,11 +201,12 @@ def attention_probe(model, batch, reps):
         call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(src_row),
              ops.EDGE_PER_DST, ptr(radial), ptr(ylm), ptr(W), ptr(bsb), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
              ptr(lg.rev_trip), ptr(order), ptr(packs), 0, units, rows, E, T, H, C, ptr(out), ptr(alpha),
-             ptr(smax), ptr(sden), None, ptr(sproj), stream_ptr())
+             ptr(smax), ptr(sden), None, ptr(sproj), None, stream_ptr())
 
     def bwd_center():  # both backward passes in one launch per center atom
         call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(table), ptr(src_row), ops.EDGE_PER_DST,
-             ptr(sproj), ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order),
+             ptr(sproj), None, None, ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip),
+             ptr(lg.center_order),
              ptr(alpha), ptr(smax), ptr(sden), ptr(dout), lg.N, lg.max_degree, E, T, H, C, ptr(dq), ptr(dk),
              ptr(dv), ptr(gfold), ptr(atom_de), ptr(g_work), stream_ptr())
 

@@ -308,8 +308,10 @@ int x2g_sbf_attention_fwd_center(const float* q, const float* k, const float* v,
  * sbf[t, 6l+n] = R[s, 6l+n] Y_l(t) (angular_basis_layer.py:87-91; R = rbf_env [E, 42] of the triplet's
  * source s, Y = sph_y [T, 8] from x2g_spherical_basis), so S_t = b + sum_l Y_l(t) P_s[l] with
  * P_s[l][c] = sum_n W[c, 6l+n] R[s, 6l+n], formed per source in LDS for each center atom's block
- * (w_sbf [128, 42], b_sbf [128]).  Outputs as x2g_sbf_attention_fwd_center; sbfproj_out [T, 128] (or
- * NULL) receives every S_t row for a backward that reads them.  Units unit0 .. unit0 + n_units - 1.  LDS
+ * (w_sbf [128, 42], b_sbf [128]).  Outputs as x2g_sbf_attention_fwd_center; for a backward, either
+ * sbfproj_out [T, 128] receives every S_t row, or sbf_p_out [E, 7, 128] every source's P rows (3.5 KB per
+ * line node instead of 512 B per triplet: x2g_sbf_attention_bwd_center rebuilds S_t from them bit for
+ * bit); either may be NULL.  Units unit0 .. unit0 + n_units - 1.  LDS
  * per workgroup 4.7 KB x max_rows (<= 160 KiB, else X2G_EUNSUPPORTED); no t_base tiling is needed
  * (nothing T x 128 is read). */
 int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, const float* v, const float* skip,
@@ -319,23 +321,27 @@ int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, const float*
                                     const int32_t* atom_order, const int32_t* pack_ptr, int64_t unit0,
                                     int64_t n_units, int32_t max_rows, int64_t num_edges, int64_t num_triplets,
                                     int32_t heads, int32_t channels, float* out, float* alpha_raw, float* seg_max,
-                                    float* seg_den, float* row_stats, float* sbfproj_out, void* stream);
+                                    float* seg_den, float* row_stats, float* sbfproj_out, float* sbf_p_out,
+                                    void* stream);
 
 /* The whole attention backward over a SYMMETRIC line graph in ONE launch, one workgroup per center atom
  * (csrc/attention_center.hip): the block's rows (k + e of its sources, dout and q of its destinations,
  * their softmax max / denominator) staged in LDS, then per source j a pass over its triplets' S rows,
- * alpha (dv, and a_t, g_t into the g_work [2, T, heads] scratch), rho per destination, and per source /
+ * alpha (dv, and (g_t, a_t) pairs into the g_work scratch of 2 T heads floats), rho per destination, and per source /
  * destination dk, the folded lin_sbf gradient G (from Y) and dq.  Replaces x2g_sbf_attention_bwd_dst_g + x2g_sbf_attention_bwd_src_fold on such
  * graphs (same dq, dk, dv, radial_grad = G [E, 8, HC]; fp32 rounding apart), reading S once instead of
  * twice and no row gathers; d_edge_atom [num_atoms, HC] (or NULL) = the per-CENTER-ATOM gradient of the
  * edge term (sum over the atom's sources of dk + dv): the element-table gradient is its keyed sum by
  * atom element.  atom_order (or NULL): workgroup w takes atom atom_order[w] (x2gnn: by decreasing degree).
+ * S_t comes from sbfproj [T, 128] rows, or (sbfproj NULL) from the fused forward's sbf_p [E, 7, 128] and
+ * b_sbf [128] as S_t = b + sum_l Y_l(t) P_s[l] (exactly one of the two forms).
  * sph_y [T, 8] as x2g_spherical_basis writes it.  LDS per workgroup:
  * x2g_sbf_attention_bwd_center_lds(max_degree, heads) bytes (<= 160 KiB, else X2G_EUNSUPPORTED).
  * heads * channels = 128, channels a multiple of 4, 16-byte aligned rows. */
 size_t x2g_sbf_attention_bwd_center_lds(int32_t max_degree, int32_t heads);
 int x2g_sbf_attention_bwd_center(const float* q, const float* k, const float* v, const float* edge,
-                                 const int32_t* src_row, int edge_mode, const float* sbfproj, const float* sph_y,
+                                 const int32_t* src_row, int edge_mode, const float* sbfproj, const float* sbf_p,
+                                 const float* b_sbf, const float* sph_y,
                                  const int32_t* atom_rowptr, const int32_t* edge_rev, const int32_t* rev_trip,
                                  const int32_t* atom_order, const float* alpha_raw, const float* seg_max,
                                  const float* seg_den, const float* dout,

@@ -58,7 +58,7 @@ for it in range(6):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(table), ptr(lg.src_type), ops.EDGE_PER_DST,
-         ptr(S), ptr(y), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(order), ptr(alpha),
+         ptr(S), None, None, ptr(y), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(order), ptr(alpha),
          ptr(smax), ptr(sden), ptr(dout), units, rows, E, T, H, C, ptr(dq), ptr(dk), ptr(dv), ptr(G), ptr(de), ptr(gw),
          stream_ptr())
     e1.record()

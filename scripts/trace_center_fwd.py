@@ -53,17 +53,24 @@ out, alpha, S = torch.empty(E, D, **f), torch.empty(T, H, **f), torch.empty(T, D
 smax, sden, rs = torch.empty(E, H, **f), torch.empty(E, H, **f), torch.empty(E, 2, **f)
 lib = _lib.load()
 lib.x2g_ftrace_fetch.argtypes = [ctypes.c_void_p, ctypes.c_int]
-ev = []
-for it in range(6):
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
-         ops.EDGE_PER_DST, ptr(radial), ptr(y), ptr(W), ptr(bias), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
-         ptr(lg.rev_trip), ptr(order), ptr(packs), 0, units, rows, E, T, H, C, ptr(out), ptr(alpha), ptr(smax),
-         ptr(sden), ptr(rs), ptr(S), stream_ptr())
-    e1.record()
-    torch.cuda.synchronize()
-    ev.append(e0.elapsed_time(e1) * 1e3)
+def run(store):
+    ev = []
+    for it in range(6):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
+             ops.EDGE_PER_DST, ptr(radial), ptr(y), ptr(W), ptr(bias), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
+             ptr(lg.rev_trip), ptr(order), ptr(packs), 0, units, rows, E, T, H, C, ptr(out), ptr(alpha), ptr(smax),
+             ptr(sden), ptr(rs), ptr(S) if store else None, None, stream_ptr())
+        e1.record()
+        torch.cuda.synchronize()
+        ev.append(e0.elapsed_time(e1) * 1e3)
+    return ev
+
+
+# without the S rows a backward reads (inference) first, for the comparison; the stamps are the training form's
+print(f"kernel (events) without the S store: {np.median(run(False)):.1f} us")
+ev = run(True)
 buf = np.zeros(8192 * 8, dtype=np.uint64)
 assert lib.x2g_ftrace_fetch(buf.ctypes.data, buf.size) == 0
 t = buf.reshape(8192, 8)[:units].astype(np.int64)

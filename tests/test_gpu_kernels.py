@@ -2033,7 +2033,7 @@ def _bwd_both(lg, q, k, v, S, table, mode, heads, channels, seed):
     de_atom = torch.full((lg.N, D), float("nan"), **f) if edge is not None else None
     assert int(_lib.load().x2g_sbf_attention_bwd_center_lds(lg.max_degree, heads)) <= 160 * 1024
     call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(lg.src_type) if edge is not None else None,
-         mode, ptr(S), ptr(y), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order),
+         mode, ptr(S), None, None, ptr(y), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order),
          ptr(alpha), ptr(smax), ptr(sden), ptr(dout), lg.N, lg.max_degree, E, T, heads, channels, ptr(dq), ptr(dk),
          ptr(dv), ptr(G), ptr(de_atom), ptr(torch.empty(2, T, H, **f)), stream_ptr())
     c = [dq, dk, dv, G]
@@ -2109,8 +2109,8 @@ def test_center_backward_edge_cases(cuda):
 
     assert int(_lib.load().x2g_sbf_attention_bwd_center_lds(130, 16)) > 160 * 1024 or 130 > ops.CENTER_MAX_DEGREE
     rc = _lib.load().x2g_sbf_attention_bwd_center(None, None, None, None, None, 0, None, None, None, None, None, None,
-                                                   None, None, None, None, 1, 130, 1, 1, 16, 8, None, None, None, None,
-                                                   None, None, None)
+                                                   None, None, None, None, None, None, 1, 130, 1, 1, 16, 8, None, None,
+                                                   None, None, None, None, None)
     assert rc == 1002  # X2G_EUNSUPPORTED
 
 
@@ -2155,7 +2155,7 @@ def test_center_forward_fused_projection_equals_projected(cuda):
         call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
              ops.EDGE_PER_DST, ptr(radial), ptr(y), ptr(W), ptr(bias), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
              ptr(lg.rev_trip), ptr(order), ptr(packs), 0, units, rows, E, T, H, C,
-             *[ptr(t) for t in got], ptr(S2), stream_ptr())
+             *[ptr(t) for t in got], ptr(S2), None, stream_ptr())
         for name, a, r in zip(("out", "alpha", "smax", "sden", "row_stats"), got, ref):
             assert not torch.isnan(a).any(), name
             torch.testing.assert_close(a, r, rtol=1e-5, atol=1e-5, msg=name)
@@ -2209,10 +2209,65 @@ def test_center_fused_projection_packed_edge_cases(cuda):
         call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
              ops.EDGE_PER_DST, ptr(radial), ptr(y), ptr(W), ptr(bias), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
              ptr(lg.rev_trip), ptr(order), ptr(packs), 0, units, rows, E, T, H, C, *[ptr(t) for t in got], ptr(S2),
-             stream_ptr())
+             None, stream_ptr())
         for name, a, r in zip(("out", "alpha", "smax", "sden", "row_stats"), got, ref):
             torch.testing.assert_close(a, r, rtol=1e-5, atol=1e-5, msg=name, equal_nan=False)
         torch.testing.assert_close(S2, S, rtol=1e-5, atol=1e-5)
         runs.append(got + [S2])
     for x, yy in zip(*runs):
         assert torch.equal(x, yy)
+
+
+def test_center_backward_from_p_rows_equals_s_rows(cuda):
+    """The fused forward's P rows (sbf_p_out [E, 7, 128]: 3.5 KB per source instead of 512 B per triplet)
+    feed the center backward, which rebuilds S_t = b + sum_l Y_l(t) P_s[l] in the forward's own arithmetic:
+    every backward output equals the one from the S rows the same forward stores, bit for bit, with and
+    without the edge term; and the P rows equal W R_s per source (fp32)."""
+    from x2gnn import ops
+    from x2gnn._lib import call, ptr, stream_ptr
+    from x2gnn.data import collate
+    from x2gnn.synth import synthetic_molecules
+
+    b = collate(synthetic_molecules(128, "S160", seed=16))
+    lg = _sym_lg(b.edge_index.numpy(), b.num_nodes, cuda)
+    z = torch.randint(0, 10, (b.num_nodes,), generator=torch.Generator().manual_seed(2)).to(cuda)
+    lg.atom_type = ops._i32(z)
+    lg.src_type, lg.dst_type = ops._i32(z[lg.edge_src.long()]), ops._i32(z[lg.edge_dst.long()])
+    E, T, H, C, D = lg.E, lg.T, 16, 8, 128
+    g = torch.Generator(device=cuda).manual_seed(17)
+    q, k, v, skip, dout = (torch.randn(E, D, device=cuda, generator=g) for _ in range(5))
+    table = torch.randn(10, D, device=cuda, generator=g)
+    radial = torch.randn(E, 42, device=cuda, generator=g)
+    y = torch.randn(T, 8, device=cuda, generator=g)
+    y[:, 7] = 1.0
+    W = 0.2 * torch.randn(D, 42, device=cuda, generator=g)
+    bias = 0.1 * torch.randn(D, device=cuda, generator=g)
+    f = dict(device=cuda, dtype=torch.float32)
+    po, pp, pr = lg.packed
+    fw = [torch.empty(E, D, **f), torch.empty(T, H, **f), torch.empty(E, H, **f), torch.empty(E, H, **f),
+          torch.empty(E, 2, **f)]
+    S, P = torch.full((T, D), float("nan"), **f), torch.full((E, 7, D), float("nan"), **f)
+    call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
+         ops.EDGE_PER_DST, ptr(radial), ptr(y), ptr(W), ptr(bias), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
+         ptr(lg.rev_trip), ptr(po), ptr(pp), 0, int(pp.shape[0]) - 1, pr, E, T, H, C, *[ptr(t) for t in fw], ptr(S),
+         ptr(P), stream_ptr())
+    ref_p = torch.einsum("clk,elk->elc", W.view(D, 7, 6), radial.view(E, 7, 6))
+    torch.testing.assert_close(P, ref_p, rtol=1e-5, atol=1e-5)
+    alpha, smax, sden = fw[1], fw[2], fw[3]
+    for mode in (ops.EDGE_PER_DST, ops.EDGE_NONE):
+        edge = table if mode == ops.EDGE_PER_DST else None
+        outs = []
+        for from_p in (False, True):
+            dq, dk, dv = (torch.full((E, D), float("nan"), **f) for _ in range(3))
+            G = torch.full((E, 8, D), float("nan"), **f)
+            de = torch.full((lg.N, D), float("nan"), **f) if edge is not None else None
+            call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(edge),
+                 ptr(lg.src_type) if edge is not None else None, mode, None if from_p else ptr(S),
+                 ptr(P) if from_p else None, ptr(bias) if from_p else None, ptr(y), ptr(lg.atom_rowptr),
+                 ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order), ptr(alpha), ptr(smax), ptr(sden), ptr(dout),
+                 lg.N, lg.max_degree, E, T, H, C, ptr(dq), ptr(dk), ptr(dv), ptr(G), ptr(de),
+                 ptr(torch.empty(2, T, H, **f)), stream_ptr())
+            outs.append([t for t in (dq, dk, dv, G, de) if t is not None])
+        for a, r in zip(*outs):
+            assert not torch.isnan(a).any()
+            assert torch.equal(a, r)

@@ -48,6 +48,16 @@ __device__ __forceinline__ float half_sum(float v, int half) {
   return half ? hi : lo;
 }
 
+#ifndef X2G_B1
+#define X2G_B1 6
+#endif
+// triplets per round trip of the backward's pass 1 when it rebuilds S_t from the P rows (their 28 VGPRs
+// live through the source's batches)
+constexpr int kFactBatch = X2G_B1;
+constexpr int kSfL = 7;                  // angular orders (sbf_dim 42 = 7 x 6)
+constexpr int kSfR = 6;                  // radial functions per order
+constexpr int kSfK = kSfL * kSfR;        // 42
+
 // ------------------------------------------------------------------------------ workgroup rows
 // A workgroup runs one UNIT: one center atom, or (pack_ptr given) a PACK of center atoms
 // order[pack_ptr[u]] .. order[pack_ptr[u + 1] - 1] whose blocks it processes side by side.  A block has
@@ -272,12 +282,9 @@ struct FwdSfArgs {
   int H;
   float sqrt_c;
   float *out, *alpha, *smax, *sden, *sp;  // sp: S [T, 128] out (NULL: not stored)
+  float* pp;  // P [E, 7, 128] out (NULL: not stored): the backward's S_t = b + sum_l Y_l(t) P_s[l]
   float2* row_stats;
 };
-
-constexpr int kSfL = 7;                  // angular orders (sbf_dim 42 = 7 x 6)
-constexpr int kSfR = 6;                  // radial functions per order
-constexpr int kSfK = kSfL * kSfR;        // 42
 
 // (4 waves per SIMD, two 8-wave workgroups per CU: at most 128 VGPRs)
 template <int LPH, int WAVES, int B, bool EDGE>
@@ -454,6 +461,15 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_fwd_center_sf_kernel(const
       a.sden[static_cast<int64_t>(d) * a.H + head] = den;
     }
   }
+  // P rows out for the backward (instead of every S row: 3.5 KB per source line node against 512 B per
+  // triplet), issued last so that no load above waits behind these stores
+  if (a.pp) {
+    cf4* pout = reinterpret_cast<cf4*>(a.pp);
+    for (int idx = tid; idx < n_rows * kSfL * 32; idx += NT) {
+      const int r = idx / (kSfL * 32);
+      pout[static_cast<int64_t>(u.LN[r]) * (kSfL * 32) + (idx - r * (kSfL * 32))] = P[idx];
+    }
+  }
 }
 
 constexpr size_t fwd_sf_lds(int rows) {
@@ -500,7 +516,7 @@ int fwd_center_launch(const FwdCenterArgs& a, bool edge, int max_degree, hipStre
 //   KE[j] = k_j + e, GO[i] = dout[d_i], QI[i] = q[d_i], per-destination max / 1 / (den + eps);
 // pass 1, one owner per SOURCE j (its S rows t(i, j) = TB[i] + j - [j > i], one 512-byte row each):
 //   at = exp(alpha_t - max_i) / (den_i + eps),  g_t = sum over the head of go_i (v_j + e) S_t,
-//   dv_j += at go_i S_t,  and (at, g_t) into a [2, T, H] scratch (L2-resident until the same workgroup
+//   dv_j += at go_i S_t,  and (g_t, at) pairs into a [T, H] scratch (L2-resident until the same workgroup
 //   reads it back);
 // then rho_i = sum_j at g (j ascending: the destination pass's order) over destination i's contiguous
 // block, and pass 2 (at, g from the scratch, Y_t, rows from LDS), per owner both roles:
@@ -515,12 +531,13 @@ struct BwdCenterArgs {
   const float *q, *k, *v, *edge;
   const int32_t* src_row;
   const float *sp, *alpha, *smax, *sden, *dout, *y;
+  const float *pp, *bias;  // FACT: S_t = bias + sum_l Y_l(t) P_s[l] from pp [E, 7, 128] instead of sp rows
   const int32_t *atom_rowptr, *edge_rev, *rev_trip;
   const int32_t* order;  // workgroup -> center atom (NULL: blockIdx.x)
   int64_t n_atoms, T;
   int H;
   float inv_sqrt_c;
-  float *dq, *dk, *dv, *gfold, *d_edge, *gw;  // gw: [2, T, H] scratch (g, then a)
+  float *dq, *dk, *dv, *gfold, *d_edge, *gw;  // gw: [T, H] (g, a) pairs of scratch
 };
 
 template <int H>
@@ -530,8 +547,8 @@ __host__ __device__ constexpr size_t bwd_center_lds(int n) {
          + static_cast<size_t>(n) * 4 * 2;     // TB, DI
 }
 
-template <int LPH, int WAVES, int B, bool EDGE>
-__global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCenterArgs a) {
+template <int LPH, int WAVES, int B, bool EDGE, bool FACT>
+__global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const BwdCenterArgs a) {
   constexpr int H = 32 / LPH;
   extern __shared__ cf4 lds[];
   const int64_t b = a.order ? static_cast<int64_t>(a.order[blockIdx.x]) : static_cast<int64_t>(blockIdx.x);
@@ -558,10 +575,16 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
   int* TB = reinterpret_cast<int*>(RHO + n * H);
   int* DI = TB + n;
   const int64_t e_row = EDGE ? static_cast<int64_t>(uniform(a.src_row[r0])) * kCD : 0;
-  // ---- staging
+  // ---- staging: the destinations and triplet blocks first, then every row load from addresses in LDS
+  // (two dependent round trips instead of an index load in front of each row load)
+  for (int idx = tid; idx < n; idx += 64 * WAVES) {
+    TB[idx] = a.rev_trip[r0 + idx];
+    DI[idx] = a.edge_rev[r0 + idx];
+  }
+  __syncthreads();
   for (int idx = tid; idx < n * 32; idx += 64 * WAVES) {
     const int j = idx >> 5, c = idx & 31;
-    const int64_t d = a.edge_rev[r0 + j];
+    const int64_t d = DI[j];
     const cf4 e4 = EDGE ? ld4(a.edge + e_row + 4 * c) : cf4{0.f, 0.f, 0.f, 0.f};
     KE[idx] = ld4(a.k + static_cast<int64_t>(r0 + j) * kCD + 4 * c) + e4;
     GO[idx] = ld4(a.dout + d * kCD + 4 * c);
@@ -569,13 +592,9 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
   }
   for (int idx = tid; idx < n * H; idx += 64 * WAVES) {
     const int i = idx / H, h = idx - i * H;
-    const int64_t d = a.edge_rev[r0 + i];
+    const int64_t d = DI[i];
     MX[idx] = a.smax[d * H + h];
     IV[idx] = 1.0f / (a.sden[d * H + h] + kCEps);
-  }
-  for (int idx = tid; idx < n; idx += 64 * WAVES) {
-    TB[idx] = a.rev_trip[r0 + idx];
-    DI[idx] = a.edge_rev[r0 + idx];
   }
   __syncthreads();
   const int nt = n - 1;  // triplets per destination (and per source)
@@ -586,11 +605,14 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
   const __amdgpu_buffer_rsrc_t sp_r = rsrc(a.sp, a.T * kCD * 4);
   const __amdgpu_buffer_rsrc_t al_r = rsrc(a.alpha, a.T * H * 4);
   const __amdgpu_buffer_rsrc_t y_r = rsrc(a.y, a.T * 8 * 4);
-  const __amdgpu_buffer_rsrc_t g_r = rsrc(a.gw, a.T * H * 4);
-  const __amdgpu_buffer_rsrc_t at_r = rsrc(a.gw + a.T * H, a.T * H * 4);
-  float* const aw = a.gw + a.T * H;
+  // the scratch holds (g_t, a_t) pairs per (triplet, head): one 8-byte store in pass 1, one 8-byte load
+  // per use below
+  const __amdgpu_buffer_rsrc_t ag_r = rsrc(a.gw, a.T * H * 8);
   auto ldf = [](__amdgpu_buffer_rsrc_t r, int off) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+  };
+  auto ldag = [&](int t) {  // (g, a) of triplet t, this lane's head
+    return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(ag_r, (t * H + head) * 8, 0, 0));
   };
   // the triplet of destination i and source j (i != j; i == j gives some row of i's block, unused)
   auto trip = [&](int i, int j) {
@@ -604,41 +626,66 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
     cf4 ue = ld4(a.v + srow);
     if (EDGE) ue += ld4(a.edge + e_row + c0);
     cf4 dv = {0.f, 0.f, 0.f, 0.f};
+    // FACT: this source's 7 P rows (the forward's own, so S_t below is the forward's S_t bit for bit)
+    cf4 pj[FACT ? kSfL : 1], bias4 = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (FACT) {
+#pragma unroll
+      for (int l = 0; l < kSfL; ++l) pj[l] = ld4(a.pp + (static_cast<int64_t>(r0 + j) * kSfL + l) * kCD + c0);
+      bias4 = ld4(a.bias + c0);
+    }
     auto batch = [&](int i0, auto bb) {
       constexpr int BB = decltype(bb)::value;
-      cf4 sv[BB];
+      cf4 sv[FACT ? 1 : BB];
+      float yv[FACT ? BB : 1];
       float al[BB];
       int tt[BB];
 #pragma unroll
       for (int u = 0; u < BB; ++u) {
         const int i = i0 + u < n ? i0 + u : n - 1;  // clamped: loads unconditional, masked below
         tt[u] = trip(i, j);
-        sv[u] = __builtin_bit_cast(cf4, __builtin_amdgcn_raw_buffer_load_b128(sp_r, tt[u] * (kCD * 4) + c0 * 4, 0, 0));
+        if constexpr (FACT)
+          yv[u] = ldf(y_r, (tt[u] * 8 + (l32 & 7)) * 4);
+        else
+          sv[u] = __builtin_bit_cast(cf4, __builtin_amdgcn_raw_buffer_load_b128(sp_r, tt[u] * (kCD * 4) + c0 * 4, 0, 0));
         al[u] = ldf(al_r, (tt[u] * H + head) * 4);
       }
 #pragma unroll
       for (int u = 0; u < BB; ++u) {
         const int i = i0 + u < n ? i0 + u : n - 1;
         const bool ok = i0 + u < n && i != j;
+        cf4 st;
+        if constexpr (FACT) {  // S_t = b + sum_l Y_l(t) P_j[l], the forward's arithmetic in its order
+          float yl[kSfL];
+          yl[0] = dpp_mov<0x150>(yv[u]);
+          yl[1] = dpp_mov<0x151>(yv[u]);
+          yl[2] = dpp_mov<0x152>(yv[u]);
+          yl[3] = dpp_mov<0x153>(yv[u]);
+          yl[4] = dpp_mov<0x154>(yv[u]);
+          yl[5] = dpp_mov<0x155>(yv[u]);
+          yl[6] = dpp_mov<0x156>(yv[u]);
+          st = bias4;
+#pragma unroll
+          for (int l = 0; l < kSfL; ++l) st += yl[l] * pj[l];
+        } else {
+          st = sv[u];
+        }
         const float at = ok ? expf(al[u] - MX[i * H + head]) * IV[i * H + head] : 0.f;
         const cf4 go = GO[i * 32 + l32];
         const cf4 gu = go * ue;
-        float gp = gu[0] * sv[u][0];
-        gp = fmaf(gu[1], sv[u][1], gp);
-        gp = fmaf(gu[2], sv[u][2], gp);
-        gp = fmaf(gu[3], sv[u][3], gp);
+        float gp = gu[0] * st[0];
+        gp = fmaf(gu[1], st[1], gp);
+        gp = fmaf(gu[2], st[2], gp);
+        gp = fmaf(gu[3], st[3], gp);
         const float g = head_sum<LPH>(gp);
-        if (ok && leader) {
-          a.gw[static_cast<int64_t>(tt[u]) * H + head] = g;
-          aw[static_cast<int64_t>(tt[u]) * H + head] = at;
-        }
-        dv += at * (go * sv[u]);
+        if (ok && leader) *reinterpret_cast<float2*>(a.gw + (static_cast<int64_t>(tt[u]) * H + head) * 2) = make_float2(g, at);
+        dv += at * (go * st);
       }
     };
     if (nt > 0) {  // (workgroup-uniform)
+      constexpr int B1 = FACT ? kFactBatch : B;
       int i0 = 0;
-      for (; n - i0 > B / 2; i0 += B) batch(i0, std::integral_constant<int, B>{});
-      if (i0 < n) batch(i0, std::integral_constant<int, B / 2>{});
+      for (; n - i0 > B1 / 2; i0 += B1) batch(i0, std::integral_constant<int, B1>{});
+      if (i0 < n) batch(i0, std::integral_constant<int, B1 / 2>{});
     }
     st4(a.dv + srow, dv);
     DE[j * 32 + l32] = dv;  // (the edge term's gradient: dk added in pass 2)
@@ -653,9 +700,9 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
       float at[8], g[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int t = TB[i] + (p0 + u < nt ? p0 + u : nt - 1);
-        at[u] = ldf(at_r, (t * H + head) * 4);
-        g[u] = ldf(g_r, (t * H + head) * 4);
+        const float2 ag = ldag(TB[i] + (p0 + u < nt ? p0 + u : nt - 1));
+        g[u] = ag.x;
+        at[u] = ag.y;
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u)
@@ -682,11 +729,12 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_center_kernel(const BwdCe
       for (int u = 0; u < BB; ++u) {
         const int x = x0 + u < n ? x0 + u : n - 1;
         const int ts = trip(x, o), td = trip(o, x);
-        ats[u] = ldf(at_r, (ts * H + head) * 4);
-        gs[u] = ldf(g_r, (ts * H + head) * 4);
+        const float2 ags = ldag(ts), agd = ldag(td);
+        gs[u] = ags.x;
+        ats[u] = ags.y;
         yv[u] = ldf(y_r, (ts * 8 + (l32 & 7)) * 4);
-        atd[u] = ldf(at_r, (td * H + head) * 4);
-        gd[u] = ldf(g_r, (td * H + head) * 4);
+        gd[u] = agd.x;
+        atd[u] = agd.y;
       }
 #pragma unroll
       for (int u = 0; u < BB; ++u) {
@@ -749,7 +797,9 @@ int bwd_center_launch(const BwdCenterArgs& a, bool edge, int max_degree, hipStre
     kern<<<grid, 64 * W, lds, st>>>(a);
     return last_launch_status();
   };
-  return edge ? go(attn_bwd_center_kernel<LPH, W, B, true>) : go(attn_bwd_center_kernel<LPH, W, B, false>);
+  if (a.pp)
+    return edge ? go(attn_bwd_center_kernel<LPH, W, B, true, true>) : go(attn_bwd_center_kernel<LPH, W, B, false, true>);
+  return edge ? go(attn_bwd_center_kernel<LPH, W, B, true, false>) : go(attn_bwd_center_kernel<LPH, W, B, false, false>);
 }
 
 }  // namespace
@@ -765,6 +815,7 @@ X2G_API size_t x2g_sbf_attention_bwd_center_lds(int32_t max_degree, int32_t head
 
 X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const float* v, const float* edge,
                                          const int32_t* src_row, int edge_mode, const float* sbfproj,
+                                         const float* sbf_p, const float* b_sbf,
                                          const float* sph_y, const int32_t* atom_rowptr, const int32_t* edge_rev,
                                          const int32_t* rev_trip, const int32_t* atom_order, const float* alpha_raw,
                                          const float* seg_max,
@@ -779,7 +830,8 @@ X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const f
   if (x2g_sbf_attention_bwd_center_lds(max_degree, heads) > 160 * 1024) return X2G_EUNSUPPORTED;
   if (num_triplets * kCD * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;  // 32-bit S offsets
   if (num_atoms == 0) return X2G_OK;
-  if (num_edges > 0 && (!q || !k || !v || !sbfproj || !sph_y || !atom_rowptr || !edge_rev || !rev_trip ||
+  if (!sbfproj == !sbf_p || (sbf_p && !b_sbf)) return X2G_EINVAL;  // S rows, or the P rows and the bias
+  if (num_edges > 0 && (!q || !k || !v || !sph_y || !atom_rowptr || !edge_rev || !rev_trip ||
                         !alpha_raw || !seg_max || !seg_den || !dout || !dq || !dk || !dv || !radial_grad ||
                         (num_triplets > 0 && !g_work)))
     return X2G_EINVAL;
@@ -787,9 +839,10 @@ X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const f
   if (edge_mode == X2G_EDGE_PER_DST && (!edge || !src_row)) return X2G_EINVAL;
   const auto al = [](const void* p, int m) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % m == 0; };
   if (!al(q, 16) || !al(k, 16) || !al(v, 16) || !al(edge, 16) || !al(sbfproj, 16) || !al(dout, 16) || !al(dq, 16) ||
-      !al(dk, 16) || !al(dv, 16) || !al(radial_grad, 16) || !al(d_edge_atom, 16))
+      !al(dk, 16) || !al(dv, 16) || !al(radial_grad, 16) || !al(d_edge_atom, 16) || !al(sbf_p, 16) || !al(b_sbf, 16))
     return X2G_EUNSUPPORTED;
   BwdCenterArgs a{};
+  a.pp = sbf_p; a.bias = b_sbf;
   a.q = q; a.k = k; a.v = v; a.edge = edge; a.src_row = src_row; a.sp = sbfproj; a.alpha = alpha_raw;
   a.smax = seg_max; a.sden = seg_den; a.dout = dout; a.y = sph_y; a.atom_rowptr = atom_rowptr; a.edge_rev = edge_rev;
   a.rev_trip = rev_trip; a.order = atom_order; a.n_atoms = num_atoms; a.T = num_triplets; a.H = heads;
@@ -857,7 +910,8 @@ X2G_API int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, cons
                                             const int32_t* pack_ptr, int64_t unit0, int64_t n_units,
                                             int32_t max_rows, int64_t num_edges, int64_t num_triplets, int32_t heads,
                                             int32_t channels, float* out, float* alpha_raw, float* seg_max,
-                                            float* seg_den, float* row_stats, float* sbfproj_out, void* stream) {
+                                            float* seg_den, float* row_stats, float* sbfproj_out, float* sbf_p_out,
+                                            void* stream) {
   if (n_units < 0 || unit0 < 0 || num_edges < 0 || num_triplets < 0 || heads <= 0 || channels <= 0)
     return X2G_EINVAL;
   if (edge_mode != X2G_EDGE_NONE && edge_mode != X2G_EDGE_PER_DST) return X2G_EUNSUPPORTED;
@@ -872,9 +926,10 @@ X2G_API int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, cons
   if (edge_mode == X2G_EDGE_PER_DST && (!edge || !src_row)) return X2G_EINVAL;
   const auto al = [](const void* p, int m) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % m == 0; };
   if (!al(q, 16) || !al(k, 16) || !al(v, 16) || !al(skip, 16) || !al(edge, 16) || !al(out, 16) || !al(b_sbf, 16) ||
-      !al(sbfproj_out, 16) || !al(row_stats, 8))
+      !al(sbfproj_out, 16) || !al(sbf_p_out, 16) || !al(row_stats, 8))
     return X2G_EUNSUPPORTED;
   FwdSfArgs a{};
+  a.pp = sbf_p_out;
   a.q = q; a.k = k; a.v = v; a.skip = skip; a.edge = edge; a.src_row = src_row; a.radial = radial; a.y = sph_y;
   a.w = w_sbf; a.bias = b_sbf; a.atom_rowptr = atom_rowptr; a.edge_rev = edge_rev; a.rev_trip = rev_trip;
   a.order = atom_order; a.packs = pack_ptr; a.atom0 = unit0; a.n_atoms = n_units;

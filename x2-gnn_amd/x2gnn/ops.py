@@ -371,6 +371,9 @@ def _center_units(lg, packed):
 # backward stays one atom per workgroup on 4 waves: with packs (8 waves) its phase barriers waited for
 # the longest member's owners and it measured 4 % slower (profiles/r5k_*); the packed backward was removed.
 _PACK_FWD = True
+# The fused forward hands the center backward each source's P rows (E x 3.5 KB) instead of every S row
+# (T x 512 B), and the backward rebuilds S_t = b + sum_l Y_l(t) P_s[l] bit for bit: False = S rows.
+_CENTER_P = True
 
 
 def _unit_rows_lds(rows):  # csrc/attention_center.hip unit_rows_lds
@@ -384,6 +387,13 @@ def _center_sf_ok(lg, factors, D):
         return False
     rows = _center_units(lg, _PACK_FWD)[3]
     return _unit_rows_lds(rows) + 4776 * rows <= 160 * 1024
+
+
+def _center_bwd_ok(lg, heads):
+    """Whether the center-atom backward takes this line graph (its element rows known, the LDS image of the
+    largest atom's block within 160 KB)."""
+    return (_CENTER_BWD and getattr(lg, "atom_type", None) is not None and lg.max_degree is not None and
+            _lib.load().x2g_sbf_attention_bwd_center_lds(lg.max_degree, heads) <= 160 * 1024)
 
 
 def _center_rows(lg, edge_mode, edge_row, D, channels):
@@ -421,15 +431,22 @@ class _SBFAttention(torch.autograd.Function):
         # per-row (mean, M2) of the output for a graph LayerNorm fused into the next row chain
         rstats = torch.empty(E, 2, dtype=torch.float32, device=dev) if _LN_FUSE and D == 128 else None
         center, src_row = _center_rows(lg, edge_mode, edge_row, D, channels)
+        sbf_p = None
         if center and _center_sf_ok(lg, factors, D):
-            # lin_sbf fused into the center forward: S_t rebuilt per center atom from the sbf factors; its
-            # rows stored only when a backward will read them
-            sproj = torch.empty(T, D, dtype=torch.float32, device=dev) if any(ctx.needs_input_grad) else None
+            # lin_sbf fused into the center forward: S_t rebuilt per center atom from the sbf factors; for a
+            # backward, the sources' P rows (the center backward rebuilds S_t from them) or the S rows
+            sproj = None
+            if any(ctx.needs_input_grad):
+                if _CENTER_P and _center_bwd_ok(lg, heads):
+                    sbf_p = torch.empty(E, 7, D, dtype=torch.float32, device=dev)
+                else:
+                    sproj = torch.empty(T, D, dtype=torch.float32, device=dev)
             order, packs, units, rows = _center_units(lg, _PACK_FWD)
             call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(src_row),
                  edge_mode, ptr(factors[0]), ptr(factors[1]), ptr(w_sbf), ptr(b_sbf), ptr(lg.atom_rowptr),
                  ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(order), ptr(packs), 0, units, rows, E, T, heads,
-                 channels, ptr(out), ptr(alpha), ptr(smax), ptr(sden), ptr(rstats), ptr(sproj), stream_ptr())
+                 channels, ptr(out), ptr(alpha), ptr(smax), ptr(sden), ptr(rstats), ptr(sproj), ptr(sbf_p),
+                 stream_ptr())
         else:
             # S = lin_sbf(sbf) once per layer [T, D], right before this layer's attention (so it is still
             # in the MALL when the attention kernels read its rows: sbf pointer = S, weight pointer NULL)
@@ -447,9 +464,10 @@ class _SBFAttention(torch.autograd.Function):
                      ptr(lg.trip_rowptr), ptr(lg.trip_src), E, T, heads, channels, D, ptr(out), ptr(alpha),
                      ptr(smax), ptr(sden), *((ptr(rstats),) if rstats is not None else ()), stream_ptr())
         if factors is not None:  # the factorised backward never reads sbf itself
-            ctx.save_for_backward(q, k, v, edge, factors[0], factors[1], sproj, alpha, smax, sden)
+            ctx.save_for_backward(q, k, v, edge, factors[0], factors[1], sproj, alpha, smax, sden, sbf_p,
+                                  b_sbf if sbf_p is not None else None)
         else:
-            ctx.save_for_backward(q, k, v, edge, sbf, None, sproj, alpha, smax, sden)
+            ctx.save_for_backward(q, k, v, edge, sbf, None, sproj, alpha, smax, sden, None, None)
         ctx.fold = factors is not None
         ctx.w_param, ctx.b_param = w_param, b_param
         ctx.lg, ctx.edge_mode, ctx.edge_row, ctx.heads, ctx.channels = lg, edge_mode, edge_row, heads, channels
@@ -463,7 +481,7 @@ class _SBFAttention(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout, _da=None, _dm=None, _ds=None, _dr=None):
-        q, k, v, edge, sbf, ylm, sproj, alpha, smax, sden = ctx.saved_tensors
+        q, k, v, edge, sbf, ylm, sproj, alpha, smax, sden, sbf_p, b_sbf = ctx.saved_tensors
         lg, mode, heads, channels = ctx.lg, ctx.edge_mode, ctx.heads, ctx.channels
         dout = _f32(dout)
         E, T, D = q.shape[0], lg.T, heads * channels
@@ -472,7 +490,8 @@ class _SBFAttention(torch.autograd.Function):
         dk = torch.empty_like(dq)
         dv = torch.empty_like(dq)
         if ctx.fold:  # sbf here is the radial factor rbf_env [E, 42]
-            return _SBFAttention._backward_fold(ctx, dout, q, k, v, edge, sbf, ylm, sproj, alpha, smax, sden, dq, dk, dv)
+            return _SBFAttention._backward_fold(ctx, dout, q, k, v, edge, sbf, ylm, sproj, alpha, smax, sden, dq, dk, dv,
+                                                sbf_p, b_sbf)
         dlogit = torch.empty(T, heads, dtype=torch.float32, device=dev)
         dproj = torch.empty(T, D, dtype=torch.float32, device=dev)
         if mode == EDGE_PER_TRIPLET:
@@ -502,7 +521,8 @@ class _SBFAttention(torch.autograd.Function):
         return dq, dk, dv, dout, d_edge, None, dw, db, None, None, None, None, None
 
     @staticmethod
-    def _backward_fold(ctx, dout, q, k, v, edge, radial, ylm, sproj, alpha, smax, sden, dq, dk, dv):
+    def _backward_fold(ctx, dout, q, k, v, edge, radial, ylm, sproj, alpha, smax, sden, dq, dk, dv, sbf_p=None,
+                       b_sbf=None):
         lg, mode, heads, channels = ctx.lg, ctx.edge_mode, ctx.heads, ctx.channels
         E, T, D = q.shape[0], lg.T, heads * channels
         dev = q.device
@@ -513,15 +533,14 @@ class _SBFAttention(torch.autograd.Function):
         gfold = torch.empty(E, 8, D, dtype=torch.float32, device=dev)
         st = stream_ptr()
         center, src_row = _center_rows(lg, mode, ctx.edge_row, D, channels)
-        if center and _CENTER_BWD and getattr(lg, "atom_type", None) is not None and (
-                _lib.load().x2g_sbf_attention_bwd_center_lds(lg.max_degree, heads) <= 160 * 1024):
+        if sbf_p is not None or (center and _center_bwd_ok(lg, heads)):
             # one launch for both passes, per center atom (csrc/attention_center.hip); the edge term's
             # gradient comes per center atom and is summed by the atoms' elements
             want_edge = mode == EDGE_PER_DST and ctx.needs_input_grad[4]
             d_edge_atom = torch.empty(lg.N, D, dtype=torch.float32, device=dev) if want_edge else None
             g_work = torch.empty(2, T, heads, dtype=torch.float32, device=dev)
             call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(src_row), mode, ptr(sproj),
-                 ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order),
+                 ptr(sbf_p), ptr(b_sbf), ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order),
                  ptr(alpha), ptr(smax), ptr(sden), ptr(dout), lg.N, lg.max_degree, E, T, heads, channels, ptr(dq),
                  ptr(dk), ptr(dv), ptr(gfold), ptr(d_edge_atom), ptr(g_work), st)
             d_edge = None
