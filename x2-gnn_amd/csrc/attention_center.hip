@@ -48,12 +48,10 @@ __device__ __forceinline__ float half_sum(float v, int half) {
   return half ? hi : lo;
 }
 
-#ifndef X2G_B1
-#define X2G_B1 6
-#endif
 // triplets per round trip of the backward's pass 1 when it rebuilds S_t from the P rows (their 28 VGPRs
-// live through the source's batches)
-constexpr int kFactBatch = X2G_B1;
+// live through the source's batches: 8 spills 21 VGPRs, 6 spills 7; 4 spills none and measured best,
+// r5q: 55.66k vs 55.46k mol/s at 6)
+constexpr int kFactBatch = 4;
 constexpr int kSfL = 7;                  // angular orders (sbf_dim 42 = 7 x 6)
 constexpr int kSfR = 6;                  // radial functions per order
 constexpr int kSfK = kSfL * kSfR;        // 42
