@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 ROOT=$(pwd)
 TAG=${TAG:-r4}
-KRE=${KRE:-'chain_fwd_v4_ln|chain_bwd_v3|conv_proj_fwd|conv_proj_bwd_gate|feat_fwd|tiled_flat|attn_fwd_batched|attn_bwd_dst_g|attn_bwd_src_fold|sbf_project'}
+KRE=${KRE:-'chain_fwd_v4_ln|chain_bwd_v3|conv_proj_fwd|conv_proj_bwd_gate|feat_fwd|tiled_flat|attn_fwd_center_sf|attn_bwd_center|sbf_radial_wgrad'}
 if [ "${1:-}" = "list" ]; then
   timeout -s KILL 120 rocprofv3 -L > gpurun_out/counters_$TAG.txt 2>&1
   echo "list rc=$?"
