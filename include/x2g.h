@@ -496,16 +496,9 @@ int x2g_smooth_l1_mean_fwd_grad(const float* pred, const float* target, int64_t 
 
 /* ---------------------------------------------------------------- dense-layer gradients */
 
-/* Workspace bytes for x2g_linear_wgrad (row-split partial slabs). */
+/* Workspace bytes for x2g_linear_wgrad_ex (row-split partial slabs). */
 size_t x2g_linear_wgrad_workspace(int64_t rows, int32_t out_features, int32_t in_features);
 
-/* dW[O,I] = dy[R,O]^T x[R,I] and db[O] = column sums of dy (db may be NULL): the weight/bias
- * gradient of every nn.Linear the reference applies row-wise (residual_layer.py, model.py:39,48,
- * readout.py, sbftransformer_conv.py:99-148, xgnn.py:54-70), split over rows with f32 MFMA and
- * summed in a fixed order (deterministic; replaces ATen's addmm backward through hipBLASLt). */
-int x2g_linear_wgrad(const float* dy, const float* x, int64_t rows, int32_t out_features,
-                     int32_t in_features, float* dw, float* db, void* workspace, size_t workspace_bytes,
-                     void* stream);
 
 /* flags of the *_ex gradient entry points */
 #define X2G_ACCUM_WGRAD 1 /* dw += ..., db += ... (write straight into a gradient buffer that already
@@ -567,7 +560,11 @@ int32_t x2g_dense_bwd_splits(int64_t rows, int32_t in_features, int32_t out_feat
  * x2g_linear_wgrad_ex's slabs start at its workspace). */
 int64_t x2g_dense_bwd_slab_offset(int64_t rows, int32_t in_features, int32_t out_features);
 
-/* x2g_linear_wgrad with flags (X2G_ACCUM_WGRAD). */
+/* dW[O,I] = dy[R,O]^T x[R,I] and db[O] = column sums of dy (db may be NULL): the weight/bias
+ * gradient of every nn.Linear the reference applies row-wise (residual_layer.py, model.py:39,48,
+ * readout.py, sbftransformer_conv.py:99-148, xgnn.py:54-70), split over rows with f32 MFMA and
+ * summed in a fixed order (deterministic; replaces ATen's addmm backward through hipBLASLt);
+ * flags X2G_ACCUM_WGRAD / X2G_DEFER_SLAB_SUM. */
 int x2g_linear_wgrad_ex(const float* dy, const float* x, int64_t rows, int32_t out_features,
                         int32_t in_features, float* dw, float* db, int flags, void* workspace,
                         size_t workspace_bytes, void* stream);
@@ -581,11 +578,6 @@ int x2g_linear_wgrad_ex(const float* dy, const float* x, int64_t rows, int32_t o
  * xgnn.py:54-55,70 and the projections of sbftransformer_conv.py:99-107,127.  b, res, z may be NULL. */
 int x2g_dense_fwd(const float* x, const float* w, const float* b, int64_t rows, int32_t in_features,
                   int32_t out_features, int act, const float* res, float* y, float* z, void* stream);
-
-/* Data gradient of x2g_dense_fwd: dz = dy * act'(z) (written to dz when non-NULL), dx = dz w.
- * dy, z, dz: [R, N]; w: [N, K]; dx: [R, K]. */
-int x2g_dense_bwd_data(const float* dy, const float* z, int act, const float* w, int64_t rows,
-                       int32_t in_features, int32_t out_features, float* dx, float* dz, void* stream);
 
 /* Workspace bytes for x2g_dense_bwd. */
 size_t x2g_dense_bwd_workspace(int64_t rows, int32_t in_features, int32_t out_features);
@@ -827,7 +819,6 @@ int x2g_chain_bwd_batch(const x2g_chain_bwd_job* jobs, int32_t num_jobs, int32_t
  * in a fixed order; flags and slab layout as x2g_wgrad_batched (stage s's slabs at byte
  * s * (workspace / n_stages)). */
 size_t x2g_chain_wgrad_workspace(int64_t rows, int32_t dim, int32_t n_stages);
-int32_t x2g_chain_wgrad_splits(int64_t rows, int32_t dim, int32_t n_stages);
 int x2g_chain_wgrad(const float* in_t, const float* dz_t, int32_t n_stages, int64_t rows, int32_t dim,
                     float* const* dw, float* const* db, int flags, void* workspace, size_t workspace_bytes,
                     void* stream);
@@ -856,7 +847,7 @@ int x2g_wgrad_batched(const x2g_wgrad_job* jobs, int32_t num_jobs, int64_t rows,
  * q = lin_query(x), k = lin_key(x_src), v = lin_value(x_src), skip = lin_skip(x) — one kernel with
  * each CU's rows of x and x_src held in LDS (the row-chain v2 structure), D = 128, rbf_dim <= 8.
  * proj[0..3] = query, key, value, skip: w [D, D], b [D] or NULL, out [rows, D], wt (optional out:
- * w transposed, for x2g_conv_proj_bwd).  x_t / xs_t (optional): x and x_src in the T layout (the
+ * w transposed, for the backward).  x_t / xs_t (optional): x and x_src in the T layout (the
  * weight gradient's operands).  */
 typedef struct {
   const float* w;
@@ -868,10 +859,10 @@ typedef struct {
 int x2g_conv_proj_fwd(const float* x, const float* rbf, int32_t rbf_dim, const float* w_rbf, const x2g_proj* proj,
                       int64_t rows, int32_t dim, float* x_t, float* xs_t, void* stream);
 
-/* Data-gradient products of x2g_conv_proj_fwd's backward: grads[0..3] = dL/d(q, k, v, skip) with
- * their weights (w, or wt when given) and optional T-layout copies g_t for the weight gradient
+/* The gradients x2g_conv_proj_fwd's backward takes: grads[0..3] = dL/d(q, k, v, skip) with their
+ * weights (w, or wt when given) and optional T-layout copies g_t for the weight gradient
  * (x2g_tiled_wgrad):  dx = dq Wq + dskip Ws (+ dx_add; dx may alias dx_add),  dxs = dk Wk + dv Wv
- * = dL/d x_src.  The gate's share (dx += dxs * f, drbf, dW_rbf) is x2g_rbf_gate_bwd(dxs, ...). */
+ * = dL/d x_src. */
 typedef struct {
   const float* g;
   const float* w;
@@ -879,10 +870,7 @@ typedef struct {
   float* g_t;
 } x2g_proj_grad;
 
-int x2g_conv_proj_bwd(const x2g_proj_grad* grads, int64_t rows, int32_t dim, float* dx, const float* dx_add,
-                      float* dxs, void* stream);
-
-/* x2g_conv_proj_bwd with the gate's backward (x2g_rbf_gate_bwd on dxs) folded in, dxs kept in
+/* The projections' data gradient with the gate's backward folded in, dxs kept in
  * registers: dx = dq Wq + dskip Ws (+ dx_add) + dxs * f with f = rbf W_rbf^T; drbf (optional,
  * [rows, rbf_dim]) = (dxs * x) W_rbf, added to its contents with X2G_GATE_DRBF_ACCUM; dw_rbf
  * [dim, rbf_dim] (+)= (dxs * x)^T rbf from one slab per workgroup (flags X2G_ACCUM_WGRAD,
@@ -924,7 +912,6 @@ int x2g_tiled_wgrad_flat_rows(const x2g_tiled_job* jobs, const int64_t* job_rows
                               void* stream);
 
 size_t x2g_tiled_wgrad_workspace(int64_t rows, int32_t dim, int32_t num_jobs);
-int32_t x2g_tiled_wgrad_splits(int64_t rows, int32_t dim, int32_t num_jobs);
 int x2g_tiled_wgrad(const x2g_tiled_job* jobs, int32_t num_jobs, int64_t rows, int32_t dim, int flags,
                     void* workspace, size_t workspace_bytes, void* stream);
 
@@ -963,10 +950,8 @@ typedef struct {
 } x2g_table_bwd_stage;
 
 /* Backward of x2g_table_chain_fwd (stages in the forward's order): every stage's weight / bias
- * gradient and dx = dL/dx ([rows, D], may be NULL). */
-int x2g_table_chain_bwd(const x2g_table_bwd_stage* stages, int32_t n_stages, int64_t rows, int32_t dim, float* dx,
-                        void* stream);
-/* The same with a workspace (x2g_table_chain_bwd_workspace bytes, 16-byte aligned): a tree with
+ * gradient and dx = dL/dx ([rows, D], may be NULL), with a workspace (x2g_table_chain_bwd_workspace
+ * bytes, 16-byte aligned): a tree with
  * several leaves (X2-GNN's four lin_edge) runs its leaf stages side by side, one workgroup each,
  * then the inner stages (two launches; the one-workgroup chain otherwise).  The forward already runs
  * one workgroup per root-to-leaf path. */

@@ -92,7 +92,6 @@ __device__ __forceinline__ float silu_grad_fast(float z) {
 // residual rows.  Backward likewise with the weight slice read transposed (dx = dz W) and dz
 // formed in LDS before the product.
 constexpr int kV2RB = 6;                 // row blocks (16 rows) per workgroup chunk
-constexpr int kV2Img = kV2RB * 16 * 32;  // 16-byte chunks per image (48 KB)
 
 __device__ __forceinline__ int ipos(int r, int c) { return r * 32 + (c ^ (r & 15)); }
 
@@ -1317,70 +1316,7 @@ __global__ void __launch_bounds__(kCThreads, 2) conv_proj_fwd_kernel(const ProjF
   }
 }
 
-struct ProjBwdArgs {
-  x2g_proj_grad gr[4];
-  const float* dx_add;
-  float* dx;
-  float* dxs;
-  int64_t R;
-};
-
-// dxs = dk Wk + dv Wv, dx = dq Wq + dskip Ws (+ dx_add): the four gradients staged two at a time
-__global__ void __launch_bounds__(kCThreads, 1) conv_proj_bwd_kernel(const ProjBwdArgs a) {
-  __shared__ f4 img[2][kV2Img];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int rl = lane & 15, g = lane >> 4;
-  const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
-  const int64_t nch = (nblk + kV2RB * G - 1) / (kV2RB * G) * G;
-  const int c0 = 16 * w + 4 * g;
-  auto load_ws = [&](int p, f4 (&dst)[8]) {
-    if (a.gr[p].wt)
-      load_slice<false>(a.gr[p].wt, w, rl, g, dst);
-    else
-      load_slice<true>(a.gr[p].w, w, rl, g, dst);
-  };
-  auto t_copy = [&](int p, const f4* im, int r0, int nrows) {  // the weight gradient's dy operand
-    if (!a.gr[p].g_t) return;
-    f4 v[kV2RB];
-#pragma unroll
-    for (int rb = 0; rb < kV2RB; ++rb) v[rb] = im[ipos(16 * rb + rl, 4 * w + g)];
-    store_t_slice(a.gr[p].g_t, v, r0, nrows, w, rl, g);
-  };
-  for (int64_t ch = blockIdx.x; ch < nch; ch += G) {
-    int r0, nrows;
-    chunk_rows(ch, nch, nblk, a.R, r0, nrows);
-#pragma unroll 1
-    for (int half = 0; half < 2; ++half) {  // (dk, dv) -> dxs, then (dq, dskip) -> dx
-      const int p0 = half ? 0 : 1, p1 = half ? 3 : 2;
-      __syncthreads();  // the images are no longer read
-      stage_rows(img[0], a.gr[p0].g, nullptr, r0, nrows);
-      stage_rows(img[1], a.gr[p1].g, nullptr, r0, nrows);
-      f4 A[8], An[8];
-      load_ws(p0, A);
-      load_ws(p1, An);
-      __syncthreads();
-      t_copy(p0, img[0], r0, nrows);
-      t_copy(p1, img[1], r0, nrows);
-      f4 acc[kV2RB], t[kV2RB];
-      slice_gemm(img[0], A, acc, rl, g);
-      slice_gemm(img[1], An, t, rl, g);
-      float* out = half ? a.dx : a.dxs;
-      const float* add = half ? a.dx_add : nullptr;
-      const rsrc_t ar = rsrc(add ? add : a.gr[0].g);
-      const float am = add ? 1.0f : 0.0f;
-#pragma unroll
-      for (int rb = 0; rb < kV2RB; ++rb) {
-        const int r = 16 * rb + rl;
-        if (r < nrows) {
-          const int off = (r0 + r) * kCD + c0;
-          *reinterpret_cast<f4*>(out + off) = acc[rb] + t[rb] + bload4(ar, 4 * off, 0) * am;
-        }
-      }
-    }
-  }
-}
-
-// conv_proj_bwd_kernel with the rbf gate's backward folded into the dxs epilogue (what
+// The projections' backward with the rbf gate's backward folded into the dxs epilogue (what
 // x2g_rbf_gate_bwd did as a separate pass over dxs, x, rbf and dx): dxs never leaves registers.
 //   dx   = (dx_add + dxs * f) + (dq Wq + dskip Ws)       f = rbf W_rbf^T (the forward's filter)
 //   (dx_add is read only when given: an uninitialised dx never meets a 0 * NaN)
@@ -1846,13 +1782,13 @@ X2G_API int x2g_wgrad_batched(const x2g_wgrad_job* jobs, int32_t num_jobs, int64
   return x2g_slab_sum_batch(sj, num_jobs, (flags & X2G_ACCUM_WGRAD) ? 1 : 0, stream);
 }
 
-X2G_API int32_t x2g_chain_wgrad_splits(int64_t rows, int32_t dim, int32_t n_stages) {
+static int32_t chain_wgrad_splits(int64_t rows, int32_t dim, int32_t n_stages) {
   if (rows <= 0 || dim != kCD || n_stages < 1 || n_stages > X2G_CHAIN_MAX_STAGES) return 0;
   return chain_wgrad_splits_of((rows + 15) / 16, n_stages);
 }
 
 X2G_API size_t x2g_chain_wgrad_workspace(int64_t rows, int32_t dim, int32_t n_stages) {
-  const int32_t splits = x2g_chain_wgrad_splits(rows, dim, n_stages);
+  const int32_t splits = chain_wgrad_splits(rows, dim, n_stages);
   return static_cast<size_t>(splits > 0 ? n_stages : 0) * splits * (kCD * kCD + kCD) * sizeof(float);
 }
 
@@ -1873,7 +1809,7 @@ X2G_API int x2g_chain_wgrad(const float* in_t, const float* dz_t, int32_t n_stag
     a.dz_t[j] = dz_t + j * tf;
   }
   a.ntiles = (rows + 15) / 16;
-  a.splits = x2g_chain_wgrad_splits(rows, dim, n_stages);
+  a.splits = chain_wgrad_splits(rows, dim, n_stages);
   const size_t per = need / n_stages;
   x2g_slab_job sj[X2G_CHAIN_MAX_STAGES];
   for (int j = 0; j < n_stages; ++j) {
@@ -1929,29 +1865,6 @@ X2G_API int x2g_conv_proj_fwd(const float* x, const float* rbf, int32_t rbf_dim,
     conv_proj_fwd_kernel<8><<<proj_grid(rows), kCThreads, 0, as_stream(stream)>>>(a);
   return last_launch_status();
 }
-
-X2G_API int x2g_conv_proj_bwd(const x2g_proj_grad* grads, int64_t rows, int32_t dim, float* dx, const float* dx_add,
-                              float* dxs, void* stream) {
-  if (!grads || rows < 0 || dim <= 0) return X2G_EINVAL;
-  if (dim != kCD || rows * kCD * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
-  if (rows == 0) return X2G_OK;
-  if (!dx || !dxs) return X2G_EINVAL;
-  ProjBwdArgs a{};
-  for (int p = 0; p < 4; ++p) {
-    if (!grads[p].g || !grads[p].w) return X2G_EINVAL;
-    if (!al16(grads[p].g) || !al16(grads[p].w) || !al16(grads[p].wt) || !al16(grads[p].g_t)) return X2G_EUNSUPPORTED;
-    a.gr[p] = grads[p];
-  }
-  if (!al16(dx) || !al16(dx_add) || !al16(dxs)) return X2G_EUNSUPPORTED;
-  a.dx_add = dx_add;
-  a.dx = dx;
-  a.dxs = dxs;
-  a.R = rows;
-  conv_proj_bwd_kernel<<<v2_grid(rows), kCThreads, 0, as_stream(stream)>>>(a);
-  return last_launch_status();
-}
-
-
 
 X2G_API int32_t x2g_conv_proj_bwd_gate_splits(int64_t rows) { return rows > 0 ? static_cast<int32_t>(proj_grid(rows)) : 0; }
 
@@ -2132,10 +2045,6 @@ X2G_API int x2g_tiled_wgrad_flat_rows(const x2g_tiled_job* jobs, const int64_t* 
   return flat_launch(jobs, job_rows, num_jobs, dim, flags, slab_jobs, workspace, workspace_bytes, stream);
 }
 
-X2G_API int32_t x2g_tiled_wgrad_splits(int64_t rows, int32_t dim, int32_t num_jobs) {
-  return x2g_chain_wgrad_splits(rows, dim, num_jobs);
-}
-
 X2G_API size_t x2g_tiled_wgrad_workspace(int64_t rows, int32_t dim, int32_t num_jobs) {
   return x2g_chain_wgrad_workspace(rows, dim, num_jobs);
 }
@@ -2150,7 +2059,7 @@ X2G_API int x2g_tiled_wgrad(const x2g_tiled_job* jobs, int32_t num_jobs, int64_t
   if (!workspace || workspace_bytes < need) return X2G_EWORKSPACE;
   ChainWgradArgs a{};
   a.ntiles = (rows + 15) / 16;
-  a.splits = x2g_tiled_wgrad_splits(rows, dim, num_jobs);
+  a.splits = chain_wgrad_splits(rows, dim, num_jobs);
   const size_t per = need / num_jobs;
   x2g_slab_job sj[X2G_CHAIN_MAX_STAGES];
   for (int j = 0; j < num_jobs; ++j) {

@@ -1431,23 +1431,12 @@ static int dense_bwd_data_impl(const float* dy, const float* z, int act, const f
   return last_launch_status();
 }
 
-X2G_API int x2g_dense_bwd_data(const float* dy, const float* z, int act, const float* w, int64_t R, int32_t K,
-                               int32_t N, float* dx, float* dz, void* stream) {
-  // dy, z: [R, N]; w: [N, K]; dx: [R, K]; dz (optional, [R, N]) receives dy * act'(z)
-  if (R < 0 || K <= 0 || N <= 0 || (act != kActNone && act != kActSilu)) return X2G_EINVAL;
-  if (R == 0) return X2G_OK;
-  if (!dy || !w || !dx || (act == kActSilu && !z)) return X2G_EINVAL;
-  return dense_bwd_data_impl(dy, z, act, w, R, K, N, dx, nullptr, dz, as_stream(stream));
-}
-
 namespace x2g {  // slab sums come from linear.hip
 int sum_slabs_launch(const float* part_w, int64_t nw, const float* part_b, int64_t nb, int splits, float* dw,
                      float* db, bool accum, hipStream_t st);
 }  // namespace x2g
 
 X2G_API size_t x2g_linear_wgrad_workspace(int64_t R, int32_t O, int32_t I);
-X2G_API int x2g_linear_wgrad(const float* dy, const float* x, int64_t R, int32_t O, int32_t I, float* dw, float* db,
-                             void* workspace, size_t workspace_bytes, void* stream);
 
 // Backward grid: the fewest workgroups that keep the busiest one at ceil(tiles / 256) tiles —
 // every workgroup writes a full weight-gradient slab, so idle-making extra workgroups would only

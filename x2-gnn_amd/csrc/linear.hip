@@ -484,7 +484,4 @@ X2G_API int x2g_slab_sum_batch(const x2g_slab_job* jobs, int32_t njobs, int32_t 
   return X2G_OK;
 }
 
-X2G_API int x2g_linear_wgrad(const float* dy, const float* x, int64_t R, int32_t O, int32_t I, float* dw, float* db,
-                             void* workspace, size_t workspace_bytes, void* stream) {
-  return x2g_linear_wgrad_ex(dy, x, R, O, I, dw, db, 0, workspace, workspace_bytes, stream);
-}
+

@@ -348,10 +348,9 @@ X2G_API int x2g_table_chain_fwd(const float* x, int64_t rows, int32_t dim, const
   return last_launch_status();
 }
 
-X2G_API int x2g_table_chain_bwd(const x2g_table_bwd_stage* stages, int32_t n_stages, int64_t rows, int32_t dim,
-                                float* dx, void* stream) {
-  if (!stages || n_stages < 1 || n_stages > kTMax || rows < 0 || dim <= 0) return X2G_EINVAL;
-  if (dim != kTD || rows > kTRows) return X2G_EUNSUPPORTED;
+// the one-workgroup chain (a tree with one leaf)
+static int table_chain_bwd_1wg(const x2g_table_bwd_stage* stages, int32_t n_stages, int64_t rows, float* dx,
+                               hipStream_t st) {
   TableBwdArgs a{};
   for (int s = 0; s < n_stages; ++s) {
     const x2g_table_bwd_stage& S = stages[s];
@@ -365,7 +364,7 @@ X2G_API int x2g_table_chain_bwd(const x2g_table_bwd_stage* stages, int32_t n_sta
   a.n = n_stages;
   a.R = static_cast<int>(rows);
   a.mask = n_stages >= 32 ? ~0u : (1u << n_stages) - 1u;
-  table_chain_bwd_kernel<false><<<1, kTThreads, 0, as_stream(stream)>>>(a);
+  table_chain_bwd_kernel<false><<<1, kTThreads, 0, st>>>(a);
   return last_launch_status();
 }
 
@@ -382,7 +381,7 @@ X2G_API int x2g_table_chain_bwd_ex(const x2g_table_bwd_stage* stages, int32_t n_
     if (stages[s].parent >= 0 && stages[s].parent < s) has_child |= 1u << stages[s].parent;
   int nleaf = 0;
   for (int s = 0; s < n_stages; ++s) nleaf += ((has_child >> s) & 1u) ? 0 : 1;
-  if (nleaf < 2) return x2g_table_chain_bwd(stages, n_stages, rows, dim, dx, stream);
+  if (nleaf < 2) return table_chain_bwd_1wg(stages, n_stages, rows, dx, as_stream(stream));
   if (!workspace || workspace_bytes < x2g_table_chain_bwd_workspace(n_stages)) return X2G_EWORKSPACE;
   if (!al16(workspace)) return X2G_EUNSUPPORTED;
   TableBwdArgs a{};
