@@ -699,8 +699,7 @@ int x2g_readout_head_pool_bwd(const float* dout_seg, const int32_t* seg_rowptr, 
 #define X2G_OPT_BASE_LR 14
 #define X2G_OPT_STAIRCASE 15
 
-/* Workspace bytes for x2g_clip_adam_ema: zero-filled before the first call (it ends in an arrival
- * counter that every call leaves zero again). */
+/* Workspace bytes for x2g_clip_adam_ema. */
 size_t x2g_optimizer_workspace(int64_t n);
 
 /* The reference trainer's update (trainer.py:43-48, train_ema.py:45-48) over one flat fp32

@@ -1,11 +1,10 @@
 // The reference trainer's parameter update (trainer.py:39-48, train_ema.py:45-48) over ONE flat
 // fp32 parameter buffer: clip_grad_norm_(max_norm) -> Adam(amsgrad=False) -> EMA
 // (AveragedModel with avg_fn = d*avg + (1-d)*p).  torch's capturable Adam issues a few kernels
-// per parameter tensor (~300 launches for X2-GNN's 155 tensors); here it is two launches:
-//   1. per-block partial sums of g^2 over contiguous chunks (fixed order); the block that finishes
-//      last (an integer arrival counter in the workspace) sums the partials in a fixed order: total
-//      norm, clip coefficient, step count + bias corrections -> scalars,
-//   2. elementwise Adam + EMA (a copy of the parameters at step 1, as AveragedModel does).
+// per parameter tensor (~300 launches for X2-GNN's 155 tensors); here it is three launches:
+//   1. per-block partial sums of g^2 over contiguous chunks (fixed order),
+//   2. one block: total norm, clip coefficient, step count + bias corrections -> scalars,
+//   3. elementwise Adam + EMA (a copy of the parameters at step 1, as AveragedModel does).
 // Every value the update depends on that changes between steps (step count, norm, clip scale)
 // lives in device memory, so a captured HIP graph replays correctly; the hyper-parameters
 // (lr, betas, eps, max_norm, ema decay) are read from the same device scalar block so a
@@ -19,12 +18,38 @@ namespace x2g {
 constexpr int kNormBlocks = 1024;
 constexpr int kNormThreads = 256;
 
-// the total norm and the step's scalars from the partial sums (one block, fixed order)
-__device__ void opt_finalize_block(const float* partial, int nparts, float* __restrict__ sc, float* red) {
+// scalars layout (float[16]); see x2g.h X2G_OPT_*
+__global__ void __launch_bounds__(kNormThreads) grad_sq_partial(const float4* __restrict__ g4,
+                                                                const float* __restrict__ g, int64_t n,
+                                                                float* __restrict__ partial) {
+  __shared__ float red[kNormThreads];
+  const int64_t n4 = n >> 2;
+  const int64_t per = (n4 + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = per * blockIdx.x, hi = lo + per < n4 ? lo + per : n4;
   float s = 0.f;
-  // (device-coherent loads: the partials were written by other CUs in this launch)
-  for (int i = threadIdx.x; i < nparts; i += kNormThreads)
-    s += __hip_atomic_load(partial + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kNormThreads) {
+    const float4 v = g4[i];
+    s = fmaf(v.x, v.x, s);
+    s = fmaf(v.y, v.y, s);
+    s = fmaf(v.z, v.z, s);
+    s = fmaf(v.w, v.w, s);
+  }
+  if (blockIdx.x == 0)  // the n % 4 tail
+    for (int64_t i = 4 * n4 + threadIdx.x; i < n; i += kNormThreads) s = fmaf(g[i], g[i], s);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = kNormThreads / 2; off > 0; off >>= 1) {
+    if (static_cast<int>(threadIdx.x) < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(kNormThreads) opt_finalize(const float* __restrict__ partial, int nparts,
+                                                             float* __restrict__ sc) {
+  __shared__ float red[kNormThreads];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += kNormThreads) s += partial[i];
   red[threadIdx.x] = s;
   __syncthreads();
   for (int off = kNormThreads / 2; off > 0; off >>= 1) {
@@ -55,44 +80,6 @@ __device__ void opt_finalize_block(const float* partial, int nparts, float* __re
     sc[X2G_OPT_STEP_SIZE] = static_cast<float>(sc[X2G_OPT_LR] / bc1);
     sc[X2G_OPT_BC2_SQRT] = static_cast<float>(sqrt(bc2));
   }
-}
-
-// scalars layout (float[16]); see x2g.h X2G_OPT_*
-__global__ void __launch_bounds__(kNormThreads) grad_sq_partial(const float4* __restrict__ g4,
-                                                                const float* __restrict__ g, int64_t n,
-                                                                float* __restrict__ partial,
-                                                                unsigned* __restrict__ arrived, float* __restrict__ sc) {
-  __shared__ float red[kNormThreads];
-  __shared__ int last;
-  const int64_t n4 = n >> 2;
-  const int64_t per = (n4 + gridDim.x - 1) / gridDim.x;
-  const int64_t lo = per * blockIdx.x, hi = lo + per < n4 ? lo + per : n4;
-  float s = 0.f;
-  for (int64_t i = lo + threadIdx.x; i < hi; i += kNormThreads) {
-    const float4 v = g4[i];
-    s = fmaf(v.x, v.x, s);
-    s = fmaf(v.y, v.y, s);
-    s = fmaf(v.z, v.z, s);
-    s = fmaf(v.w, v.w, s);
-  }
-  if (blockIdx.x == 0)  // the n % 4 tail
-    for (int64_t i = 4 * n4 + threadIdx.x; i < n; i += kNormThreads) s = fmaf(g[i], g[i], s);
-  red[threadIdx.x] = s;
-  __syncthreads();
-  for (int off = kNormThreads / 2; off > 0; off >>= 1) {
-    if (static_cast<int>(threadIdx.x) < off) red[threadIdx.x] += red[threadIdx.x + off];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    partial[blockIdx.x] = red[0];
-    __threadfence();  // the partial is visible before the arrival is
-    last = atomicAdd(arrived, 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!last) return;  // (block-uniform)
-  __threadfence();
-  opt_finalize_block(partial, gridDim.x, sc, red);
-  if (threadIdx.x == 0) *arrived = 0u;  // ready for the next call (a captured graph's next replay)
 }
 
 __global__ void __launch_bounds__(256) adam_ema(float* __restrict__ p, float* __restrict__ g,
@@ -127,8 +114,7 @@ __global__ void __launch_bounds__(256) adam_ema(float* __restrict__ p, float* __
 
 using namespace x2g;
 
-// the partial sums, then the arrival counter (zero before the first call; every call leaves it zero)
-X2G_API size_t x2g_optimizer_workspace(int64_t n) { return n > 0 ? (kNormBlocks + 4) * sizeof(float) : 0; }
+X2G_API size_t x2g_optimizer_workspace(int64_t n) { return n > 0 ? kNormBlocks * sizeof(float) : 0; }
 
 static int clip_adam_ema(float* params, float* grads, float* exp_avg, float* exp_avg_sq, float* ema, int64_t n,
                          float* scalars, int zero_grads, void* workspace, size_t workspace_bytes, void* stream) {
@@ -139,8 +125,8 @@ static int clip_adam_ema(float* params, float* grads, float* exp_avg, float* exp
   if (reinterpret_cast<uintptr_t>(grads) % 16) return X2G_EINVAL;
   hipStream_t st = as_stream(stream);
   float* partial = static_cast<float*>(workspace);
-  grad_sq_partial<<<kNormBlocks, kNormThreads, 0, st>>>(reinterpret_cast<const float4*>(grads), grads, n, partial,
-                                                        reinterpret_cast<unsigned*>(partial + kNormBlocks), scalars);
+  grad_sq_partial<<<kNormBlocks, kNormThreads, 0, st>>>(reinterpret_cast<const float4*>(grads), grads, n, partial);
+  opt_finalize<<<1, kNormThreads, 0, st>>>(partial, kNormBlocks, scalars);
   const int64_t want = (n + 255) / 256;
   adam_ema<<<static_cast<unsigned>(want < 4096 ? want : 4096), 256, 0, st>>>(params, grads, exp_avg, exp_avg_sq, ema,
                                                                               n, scalars, zero_grads);

@@ -46,7 +46,7 @@ class FlatAdam:
             [lr, betas[0], betas[1], eps, max_norm if max_norm else 0.0, ema_decay or 0.0], dtype=torch.float32)
         self.scalars = sc.to(dev)
         self.ws_bytes = int(_lib.load().x2g_optimizer_workspace(n))
-        self.ws = torch.zeros(max(self.ws_bytes, 4), dtype=torch.uint8, device=dev)  # (an arrival counter: zero)
+        self.ws = torch.empty(max(self.ws_bytes, 4), dtype=torch.uint8, device=dev)
 
     def step(self, zero_grads=False):
         """One update; ``zero_grads``: also zero the gradient bucket as it is read (zero_grad()
