@@ -197,16 +197,21 @@ def attention_probe(model, batch, reps):
 
     order, packs, units, rows = ops._center_units(lg, ops._PACK_FWD) if center else (None, None, 0, 0)
 
-    def fwd_sf():  # the model's forward with lin_sbf fused (S rebuilt per workgroup unit; S rows stored)
+    # as the model: with the fused forward feeding the center backward, P rows [E, 7, D] pass between them
+    # instead of S rows [T, D] (ops._CENTER_P)
+    use_p = sf and center_bwd and ops._CENTER_P
+    pbuf = torch.empty(E, 7, D, **f32) if use_p else None
+
+    def fwd_sf():  # the model's forward with lin_sbf fused (S rebuilt per workgroup unit; P or S rows stored)
         call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(src_row),
              ops.EDGE_PER_DST, ptr(radial), ptr(ylm), ptr(W), ptr(bsb), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
              ptr(lg.rev_trip), ptr(order), ptr(packs), 0, units, rows, E, T, H, C, ptr(out), ptr(alpha),
-             ptr(smax), ptr(sden), None, ptr(sproj), None, stream_ptr())
+             ptr(smax), ptr(sden), None, None if use_p else ptr(sproj), ptr(pbuf), stream_ptr())
 
     def bwd_center():  # both backward passes in one launch per center atom
         call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(table), ptr(src_row), ops.EDGE_PER_DST,
-             ptr(sproj), None, None, ptr(ylm), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip),
-             ptr(lg.center_order),
+             None if use_p else ptr(sproj), ptr(pbuf), ptr(bsb) if use_p else None, ptr(ylm), ptr(lg.atom_rowptr),
+             ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order),
              ptr(alpha), ptr(smax), ptr(sden), ptr(dout), lg.N, lg.max_degree, E, T, H, C, ptr(dq), ptr(dk),
              ptr(dv), ptr(gfold), ptr(atom_de), ptr(g_work), stream_ptr())
 
@@ -232,12 +237,15 @@ def attention_probe(model, batch, reps):
     # atom_rowptr, edge_rev, rev_trip and the per-source element row
     cidx = 4 * (lg.N + 1) + 12 * E
     cfwd_bytes = cidx + T * (row_b + 4 * H) + E * (5 * row_b + 8 * H)  # k v q skip out, S, alpha, max/den
-    # reads k v q dout, S, alpha, Y, max/den; writes dq dk dv, G [E, 8, D], the per-atom edge gradient
-    # (+ the g_t [T, H] scratch: written once, read back from L2 by the same workgroup)
-    cbwd_bytes = (cidx + T * (row_b + 4 * H + 32) + E * (4 * row_b + 8 * H) + E * (3 * row_b + 8 * row_b)
-                  + lg.N * row_b + T * 4 * H)
-    # fused projection: k v q skip out rows, the radial rows and the weight, Y, alpha, max/den, S rows written
-    sf_bytes = cidx + T * (row_b + 4 * H + 32) + E * (5 * row_b + 8 * H + 4 * S) + 4 * D * (S + 1)
+    # reads k v q dout, S rows (or the P rows), alpha, Y, max/den; writes dq dk dv, G [E, 8, D], the per-atom
+    # edge gradient (the (g, a) scratch, written once and read back from L2 by the same workgroup, not counted)
+    s_or_p = E * 7 * row_b + 4 * D if use_p else T * row_b
+    cbwd_bytes = (cidx + T * (4 * H + 32) + s_or_p + E * (4 * row_b + 8 * H) + E * (3 * row_b + 8 * row_b)
+                  + lg.N * row_b)
+    # fused projection: k v q skip out rows, the radial rows and the weight, Y, alpha, max/den, S (or P) rows
+    # written
+    sf_bytes = cidx + T * (4 * H + 32) + (E * 7 * row_b if use_p else T * row_b) + E * (5 * row_b + 8 * H + 4 * S) \
+        + 4 * D * (S + 1)
     probes = [] if sf else [("sbf_project", proj, proj_bytes, proj_bytes)]
     if sf:
         probes.append(("attn_fwd", fwd_sf, sf_bytes, sf_bytes))
