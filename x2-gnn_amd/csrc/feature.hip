@@ -110,10 +110,6 @@ __device__ __forceinline__ f4 w1_frag(const float* __restrict__ w1, int K, int c
 
 constexpr int kFX4 = (kFRows * kFKMax / 4 + kFThreads - 1) / kFThreads;  // staged float4 per thread
 
-#define X2G_FTR(k, p) \
-  do {                \
-  } while (0)
-
 // The tile's span x[r0 .. r0 + nr) is contiguous and 16-byte aligned (r0 * K * 4 is a multiple of
 // 16): thread t holds float4 t + 512 u in registers (the next tile's are loaded during the current
 // tile's products); env of the tile's rows rides along in threads 0..31.
@@ -170,10 +166,7 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t r0 = tile * kFRows;
     const int nr = R - r0 < kFRows ? static_cast<int>(R - r0) : kFRows;
-    const int kt = static_cast<int>((tile - blockIdx.x) / gridDim.x);
-    (void)kt;
     __syncthreads();  // the previous tile's products no longer read A / Y1 / envs
-    X2G_FTR(kt, 0);
     {  // scatter the staged span into 388-float rows (rows past nr: zero)
       const int n = nr * K;
 #pragma unroll
@@ -193,7 +186,6 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
       if (tid < kFRows) envs[tid] = xt.env;
     }
     __syncthreads();
-    X2G_FTR(kt, 1);
     if (tile + gridDim.x < ntiles) xtile_load(a, tile + gridDim.x, xt);  // in flight during the products
     // x * env in T layout: per 16-row tile and plane, float4 u of the 2048-float block holds
     // feature u >> 2, rows 4 (u & 3) .. +3.  (Issuing these 48 KB one piece per iteration of the first
@@ -209,7 +201,6 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
       *reinterpret_cast<f4*>(a.xs_t + p * a.tf + t16 * 2048 + 4 * tid) = v;
     };
     for (int it = 0; it < 6; ++it) xs_store(it);
-    X2G_FTR(kt, 2);
     // z1 = env (x W1^T) + b1: wave w -> columns c1a, c1b, both 16-row blocks
     f4 acc[2][2] = {{zero4(), zero4()}, {zero4(), zero4()}};
     // W1 operands two groups ahead (set 0: even groups, set 1: odd; a set is reloaded right after
@@ -241,7 +232,6 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
       group(q, wa0, wb0);
       if (q + 1 < KQn) group(q + 1, wa1, wb1);
     }
-    X2G_FTR(kt, 3);
     f4 wq[3];  // the second product's first two W2 groups, in flight under the epilogue and barrier
     wq[0] = *reinterpret_cast<const f4*>(w2s);
     wq[1] = *reinterpret_cast<const f4*>(w2s + 16);
@@ -272,7 +262,6 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
       }
     }
     __syncthreads();
-    X2G_FTR(kt, 4);
     // z2 = SiLU(z1) W2^T + b2: wave w -> columns 16w + i
     f4 acc2[2] = {zero4(), zero4()};
     {
@@ -297,7 +286,6 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
         y1 = n1;
       }
     }
-    X2G_FTR(kt, 5);
     const int c2 = 16 * w + i;
     // neo_x leaves as 16-byte row pieces: lane (i = 4m + j, g) holds rows 4g + e of column c2, and
     // after the quad transpose row 4g + j, columns 16w + 4m .. +3 (one store per block, not four)
@@ -318,7 +306,6 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
       if (ry < nr) *reinterpret_cast<f4*>(a.y2 + (r0 + ry) * kFN2 + 16 * w + 4 * qm) = yt;
       if (a.want_t) *reinterpret_cast<f4*>(a.z2_t + tpos(a.tf, t16, c2, g)) = z;
     }
-    X2G_FTR(kt, 6);
   }
 }
 
