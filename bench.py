@@ -195,7 +195,7 @@ def attention_probe(model, batch, reps):
 
     sf = center and ops._center_sf_ok(lg, (radial, ylm), D)
 
-    order, packs, units, rows = ops._center_units(lg, ops._PACK_FWD) if center else (None, None, 0, 0)
+    order, packs, units, rows, info = ops._center_units(lg, ops._PACK_FWD) if center else (None, None, 0, 0, None)
 
     # as the model: with the fused forward feeding the center backward, P rows [E, 7, D] pass between them
     # instead of S rows [T, D] (ops._CENTER_P)
@@ -205,7 +205,7 @@ def attention_probe(model, batch, reps):
     def fwd_sf():  # the model's forward with lin_sbf fused (S rebuilt per workgroup unit; P or S rows stored)
         call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(src_row),
              ops.EDGE_PER_DST, ptr(radial), ptr(ylm), ptr(W), ptr(bsb), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
-             ptr(lg.rev_trip), ptr(order), ptr(packs), 0, units, rows, E, T, H, C, ptr(out), ptr(alpha),
+             ptr(lg.rev_trip), ptr(order), ptr(packs), ptr(info), 0, units, rows, E, T, H, C, ptr(out), ptr(alpha),
              ptr(smax), ptr(sden), None, None if use_p else ptr(sproj), ptr(pbuf), stream_ptr())
 
     def bwd_center():  # both backward passes in one launch per center atom

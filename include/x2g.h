@@ -302,7 +302,10 @@ int x2g_sbf_attention_fwd_center(const float* q, const float* k, const float* v,
  * best-fit-decreasing by degree into units of <= 16 rows, data.center_packs); without it unit u is atom
  * atom_order[u] (or u when atom_order is NULL).  max_rows >= the row count sum(deg) of every unit (the
  * largest degree without packs), <= X2G_CENTER_MAX_DEGREE: it sizes the LDS image.  Packing changes no
- * bit of any output (every sum keeps its order within an atom's block).
+ * bit of any output (every sum keeps its order within an atom's block).  atom_info (or NULL): int32
+ * [N, 4], 16-byte aligned, per position p of atom_order: (atom_order[p], atom_rowptr of it, its degree,
+ * src_row of its first out-edge) — the workgroup then reads its atoms' row ranges with one load instead
+ * of three dependent ones (x2gnn makes it at collate time).
  *
  * The center-atom forward with lin_sbf fused (no S to read): X2-GNN's sbf row factorises as
  * sbf[t, 6l+n] = R[s, 6l+n] Y_l(t) (angular_basis_layer.py:87-91; R = rbf_env [E, 42] of the triplet's
@@ -318,8 +321,8 @@ int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, const float*
                                     const float* edge, const int32_t* src_row, int edge_mode, const float* radial,
                                     const float* sph_y, const float* w_sbf, const float* b_sbf,
                                     const int32_t* atom_rowptr, const int32_t* edge_rev, const int32_t* rev_trip,
-                                    const int32_t* atom_order, const int32_t* pack_ptr, int64_t unit0,
-                                    int64_t n_units, int32_t max_rows, int64_t num_edges, int64_t num_triplets,
+                                    const int32_t* atom_order, const int32_t* pack_ptr, const int32_t* atom_info,
+                                    int64_t unit0, int64_t n_units, int32_t max_rows, int64_t num_edges, int64_t num_triplets,
                                     int32_t heads, int32_t channels, float* out, float* alpha_raw, float* seg_max,
                                     float* seg_den, float* row_stats, float* sbfproj_out, float* sbf_p_out,
                                     void* stream);

@@ -35,10 +35,11 @@ md = int(deg_all.max())
 if mode == "packs":
     po, pp, rows = center_packs(deg_all)
     order, packs, units = torch.from_numpy(po).to(dev), torch.from_numpy(pp).to(dev), len(pp) - 1
+    info = b._store["_x2g_pack_info"].to(dev)  # (collate's: the same packs)
     unit_rows = np.array([deg_all[po[pp[u]:pp[u + 1]]].sum() for u in range(units)])
 else:
     po = np.argsort(-deg_all, kind="stable").astype(np.int32)
-    order, packs, units, rows = torch.from_numpy(po).to(dev), None, n, md
+    order, packs, units, rows, info = torch.from_numpy(po).to(dev), None, n, md, None
     unit_rows = deg_all[po]
 E, H, C, D = lg.E, 16, 8, 128
 g = torch.Generator(device=dev).manual_seed(3)
@@ -60,7 +61,7 @@ def run(store):
         e0.record()
         call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
              ops.EDGE_PER_DST, ptr(radial), ptr(y), ptr(W), ptr(bias), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
-             ptr(lg.rev_trip), ptr(order), ptr(packs), 0, units, rows, E, T, H, C, ptr(out), ptr(alpha), ptr(smax),
+             ptr(lg.rev_trip), ptr(order), ptr(packs), ptr(info), 0, units, rows, E, T, H, C, ptr(out), ptr(alpha), ptr(smax),
              ptr(sden), ptr(rs), ptr(S) if store else None, None, stream_ptr())
         e1.record()
         torch.cuda.synchronize()

@@ -1903,6 +1903,16 @@ def _sym_lg(ei, n, cuda, with_transpose=False):
     return lg
 
 
+def _pack_info(lg, order):
+    """The fused forward's atom_info for the atoms in ``order``: (atom, first out-edge, degree, element row of
+    its out-edges) per position, int32 [N * 4], from the line graph's own arrays (as collate makes it)."""
+    o = order.long()
+    rp = lg.atom_rowptr.long()
+    first, deg = rp[o], rp[o + 1] - rp[o]
+    er = lg.src_type.long()[first.clamp(max=max(lg.E - 1, 0))] if lg.E else torch.zeros_like(first)
+    return torch.stack([o, first, deg, torch.where(deg > 0, er, 0)], 1).to(torch.int32).contiguous().reshape(-1)
+
+
 def _attn_inputs(lg, cuda, seed, rows=10):
     g = torch.Generator(device=cuda).manual_seed(seed)
     E, T = lg.E, lg.T
@@ -2152,9 +2162,11 @@ def test_center_forward_fused_projection_equals_projected(cuda):
         # unpacked: identity order with the S store, the degree order without; packed: the model's units
         order, packs, units, rows = (po, pp, int(pp.shape[0]) - 1, pr) if packed else \
             (None if store else lg.center_order, None, lg.N, lg.max_degree)
+        # packed with the S store: the row ranges from atom_info (the model's launch); without: derived
+        info = _pack_info(lg, po) if packed and store else None
         call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
              ops.EDGE_PER_DST, ptr(radial), ptr(y), ptr(W), ptr(bias), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
-             ptr(lg.rev_trip), ptr(order), ptr(packs), 0, units, rows, E, T, H, C,
+             ptr(lg.rev_trip), ptr(order), ptr(packs), ptr(info), 0, units, rows, E, T, H, C,
              *[ptr(t) for t in got], ptr(S2), None, stream_ptr())
         for name, a, r in zip(("out", "alpha", "smax", "sden", "row_stats"), got, ref):
             assert not torch.isnan(a).any(), name
@@ -2206,9 +2218,10 @@ def test_center_fused_projection_packed_edge_cases(cuda):
         got = [torch.full_like(t, float("nan")) for t in ref]
         S2 = torch.full((T, D), float("nan"), **f)
         order, packs, units, rows = (po, pp, int(pp.shape[0]) - 1, pr) if packed else (None, None, lg.N, lg.max_degree)
+        info = _pack_info(lg, po) if packed else None
         call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
              ops.EDGE_PER_DST, ptr(radial), ptr(y), ptr(W), ptr(bias), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
-             ptr(lg.rev_trip), ptr(order), ptr(packs), 0, units, rows, E, T, H, C, *[ptr(t) for t in got], ptr(S2),
+             ptr(lg.rev_trip), ptr(order), ptr(packs), ptr(info), 0, units, rows, E, T, H, C, *[ptr(t) for t in got], ptr(S2),
              None, stream_ptr())
         for name, a, r in zip(("out", "alpha", "smax", "sden", "row_stats"), got, ref):
             torch.testing.assert_close(a, r, rtol=1e-5, atol=1e-5, msg=name, equal_nan=False)
@@ -2249,7 +2262,8 @@ def test_center_backward_from_p_rows_equals_s_rows(cuda):
     S, P = torch.full((T, D), float("nan"), **f), torch.full((E, 7, D), float("nan"), **f)
     call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
          ops.EDGE_PER_DST, ptr(radial), ptr(y), ptr(W), ptr(bias), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
-         ptr(lg.rev_trip), ptr(po), ptr(pp), 0, int(pp.shape[0]) - 1, pr, E, T, H, C, *[ptr(t) for t in fw], ptr(S),
+         ptr(lg.rev_trip), ptr(po), ptr(pp), ptr(_pack_info(lg, po)), 0, int(pp.shape[0]) - 1, pr, E, T, H, C,
+         *[ptr(t) for t in fw], ptr(S),
          ptr(P), stream_ptr())
     ref_p = torch.einsum("clk,elk->elc", W.view(D, 7, 6), radial.view(E, 7, 6))
     torch.testing.assert_close(P, ref_p, rtol=1e-5, atol=1e-5)

@@ -114,3 +114,37 @@ def test_device_ops_refuse_cpu_tensors():
         ops.segment_sum(x, torch.zeros(3, dtype=torch.int32), 2)
     with pytest.raises(RuntimeError, match="GPU"):
         ops.vertex_to_edge(torch.zeros(2, 3, dtype=torch.int64), 3, 0)
+
+
+def test_center_packs_and_atom_info():
+    """data.center_packs (the fused forward's workgroup units): every atom in exactly one unit, no unit
+    above 16 rows unless it is one atom of larger degree, atoms without edges in units of their own, the
+    units in decreasing order of their largest degree, 90 % of the owners busy at config 2; and
+    collate's atom_info rows = (atom, first out-edge, degree, element) in the same order."""
+    import numpy as np
+
+    from x2gnn.data import center_packs, collate
+    from x2gnn.synth import synthetic_molecules
+
+    b = collate(synthetic_molecules(128, "S160", seed=1000))
+    n = b.num_nodes
+    deg = np.bincount(b.edge_index[0].numpy(), minlength=n)
+    order, packs, rows = center_packs(deg)
+    assert sorted(order.tolist()) == list(range(n))
+    units = [order[packs[u]:packs[u + 1]] for u in range(len(packs) - 1)]
+    sums = np.array([deg[u].sum() for u in units])
+    assert all(s <= 16 or len(u) == 1 for s, u in zip(sums, units))
+    assert rows == sums.max() and all(len(u) <= 16 for u in units)
+    big = np.array([deg[u].max() for u in units])
+    assert (np.diff(big) <= 0).all()
+    assert sums.sum() / (16 * np.ceil(sums / 16)).sum() > 0.88
+    st = b._store
+    assert np.array_equal(st["_x2g_pack_order"].numpy(), order)
+    info = st["_x2g_pack_info"].numpy().reshape(-1, 4)
+    first = np.concatenate([[0], np.cumsum(deg)[:-1]])
+    z = st["x"].numpy().reshape(-1)
+    assert np.array_equal(info, np.stack([order, first[order], deg[order], z[order]], 1))
+    # atoms without edges: a unit of their own (no rows)
+    o2, p2, r2 = center_packs(np.array([0, 3, 0, 20, 5, 16, 1]))
+    u2 = [o2[p2[u]:p2[u + 1]].tolist() for u in range(len(p2) - 1)]
+    assert u2[-1] == [0, 2] and [3] in u2 and [5] in u2 and r2 == 20

@@ -93,11 +93,15 @@ __device__ __forceinline__ UnitRows unit_rows_carve(int* p, int max_rows) {
   return u;
 }
 
-// wave 0 fills the tables (the caller synchronises before reading them); src_row may be NULL (ER = 0)
+// wave 0 fills the tables (the caller synchronises before reading them); src_row may be NULL (ER = 0).
+// With info (int32 [.., 4] per atom in the order's positions: atom, first out-edge, degree, edge-table
+// row; the host's, data.center_packs) a member's row range is one load instead of three dependent ones
+// (order -> rowptr -> src_row).
 __device__ __forceinline__ void unit_rows_build(const UnitRows& u, const int32_t* __restrict__ order,
                                                 const int32_t* __restrict__ packs, int64_t unit,
                                                 const int32_t* __restrict__ rowptr,
-                                                const int32_t* __restrict__ src_row) {
+                                                const int32_t* __restrict__ src_row,
+                                                const int4* __restrict__ info) {
   if (threadIdx.x >= 64) return;
   const int lane = threadIdx.x;
   int64_t m0 = unit, m1 = unit + 1;
@@ -106,13 +110,23 @@ __device__ __forceinline__ void unit_rows_build(const UnitRows& u, const int32_t
     m1 = packs[unit + 1];
   }
   const int M = static_cast<int>(m1 - m0);  // <= kMaxMembers (host contract)
-  int b = 0, r0 = 0, n = 0;
-  if (lane < M) {
-    b = order ? order[m0 + lane] : static_cast<int>(m0 + lane);
-    r0 = rowptr[b];
-    n = rowptr[b + 1] - r0;
+  int b = 0, r0 = 0, n = 0, er = 0;
+  if (info) {
+    if (lane < M) {
+      const int4 v = info[m0 + lane];
+      b = v.x;
+      r0 = v.y;
+      n = v.z;
+      er = src_row ? v.w : 0;
+    }
+  } else {
+    if (lane < M) {
+      b = order ? order[m0 + lane] : static_cast<int>(m0 + lane);
+      r0 = rowptr[b];
+      n = rowptr[b + 1] - r0;
+    }
+    er = (src_row && n > 0) ? src_row[r0] : 0;
   }
-  const int er = (src_row && n > 0) ? src_row[r0] : 0;
   int inc = n;  // inclusive prefix over the members
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -275,6 +289,7 @@ struct FwdSfArgs {
   const int32_t *atom_rowptr, *edge_rev, *rev_trip;
   const int32_t* order;  // unit -> center atom(s) (NULL: the identity)
   const int32_t* packs;  // unit u = atoms order[packs[u]] .. order[packs[u + 1] - 1] (NULL: one atom per unit)
+  const int4* info;      // per order position: atom, first out-edge, degree, edge-table row (NULL: derived)
   int64_t atom0, n_atoms;  // units atom0 .. atom0 + n_atoms - 1
   int max_rows;            // rows of the largest unit (the LDS image is sized for it)
   int H;
@@ -291,7 +306,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_fwd_center_sf_kernel(const
   extern __shared__ cf4 lds[];
   const UnitRows u = unit_rows_carve(reinterpret_cast<int*>(lds), a.max_rows);
   // (the host orders the units by decreasing work: the longest start first, the short ones fill the tail)
-  unit_rows_build(u, a.order, a.packs, a.atom0 + blockIdx.x, a.atom_rowptr, EDGE ? a.src_row : nullptr);
+  unit_rows_build(u, a.order, a.packs, a.atom0 + blockIdx.x, a.atom_rowptr, EDGE ? a.src_row : nullptr, a.info);
   __syncthreads();
   const int n_rows = uniform(u.NRS[0]);
   if (n_rows <= 0) return;  // (workgroup-uniform)
@@ -905,7 +920,8 @@ X2G_API int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, cons
                                             const float* radial, const float* sph_y, const float* w_sbf,
                                             const float* b_sbf, const int32_t* atom_rowptr, const int32_t* edge_rev,
                                             const int32_t* rev_trip, const int32_t* atom_order,
-                                            const int32_t* pack_ptr, int64_t unit0, int64_t n_units,
+                                            const int32_t* pack_ptr, const int32_t* atom_info, int64_t unit0,
+                                            int64_t n_units,
                                             int32_t max_rows, int64_t num_edges, int64_t num_triplets, int32_t heads,
                                             int32_t channels, float* out, float* alpha_raw, float* seg_max,
                                             float* seg_den, float* row_stats, float* sbfproj_out, float* sbf_p_out,
@@ -924,9 +940,10 @@ X2G_API int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, cons
   if (edge_mode == X2G_EDGE_PER_DST && (!edge || !src_row)) return X2G_EINVAL;
   const auto al = [](const void* p, int m) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % m == 0; };
   if (!al(q, 16) || !al(k, 16) || !al(v, 16) || !al(skip, 16) || !al(edge, 16) || !al(out, 16) || !al(b_sbf, 16) ||
-      !al(sbfproj_out, 16) || !al(sbf_p_out, 16) || !al(row_stats, 8))
+      !al(sbfproj_out, 16) || !al(sbf_p_out, 16) || !al(row_stats, 8) || !al(atom_info, 16))
     return X2G_EUNSUPPORTED;
   FwdSfArgs a{};
+  a.info = reinterpret_cast<const int4*>(atom_info);
   a.pp = sbf_p_out;
   a.q = q; a.k = k; a.v = v; a.skip = skip; a.edge = edge; a.src_row = src_row; a.radial = radial; a.y = sph_y;
   a.w = w_sbf; a.bias = b_sbf; a.atom_rowptr = atom_rowptr; a.edge_rev = edge_rev; a.rev_trip = rev_trip;

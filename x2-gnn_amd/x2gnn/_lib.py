@@ -76,8 +76,8 @@ SIGNATURES = {
                                     _I32, _I32, _P, _P, _P, _P, _P, _P],
     "x2g_sbf_attention_fwd_center": [_P, _P, _P, _P, _P, _P, ctypes.c_int, _P, _I64, _P, _P, _P, _P, _I64, _I64, _I32,
                                      _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P],
-    "x2g_sbf_attention_fwd_center_sf": [_P] * 6 + [ctypes.c_int] + [_P] * 9 + [_I64, _I64, _I32, _I64, _I64, _I32,
-                                                                               _I32] + [_P] * 8,
+    "x2g_sbf_attention_fwd_center_sf": [_P] * 6 + [ctypes.c_int] + [_P] * 10 + [_I64, _I64, _I32, _I64, _I64, _I32,
+                                                                                _I32] + [_P] * 8,
     "x2g_sbf_attention_bwd_center_lds": [_I32, _I32],
     "x2g_sbf_attention_bwd_center": [_P] * 5 + [ctypes.c_int] + [_P] * 12 + [_I64, _I32, _I64, _I64, _I32, _I32] +
                                     [_P] * 7,

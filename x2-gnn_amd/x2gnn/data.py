@@ -213,6 +213,12 @@ def _add_device_indices(b, nodes, edges):
     b._store["_x2g_pack_order"] = torch.from_numpy(order)
     b._store["_x2g_center_packs"] = torch.from_numpy(packs)
     b._store["_x2g_center_rows"] = rows
+    # per pack-order position: (atom, first out-edge, degree, element): the fused forward's row tables in one
+    # load per atom (x2g_sbf_attention_fwd_center_sf atom_info)
+    first = np.concatenate([[0], np.cumsum(deg)[:-1]]) if deg.size else deg
+    z = b._store["x"].numpy().reshape(-1)
+    info = np.stack([order, first[order], deg[order], z[order]], axis=1).astype(np.int32)
+    b._store["_x2g_pack_info"] = torch.from_numpy(np.ascontiguousarray(info).reshape(-1))
 
 
 CENTER_PACK_ROWS = 16  # the center kernels' half-wave owners per workgroup (csrc/attention_center.hip)

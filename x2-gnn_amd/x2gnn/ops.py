@@ -110,7 +110,7 @@ class LineGraph:
         # the center kernels' workgroups (collate's; None: the identity): int32 [N] the atoms by decreasing
         # degree (one per workgroup), and the fused forward's packs (data.center_packs): int32 [N] the atoms
         # unit by unit, int32 [P + 1] the units' bounds in it, the largest unit's row count
-        self.center_order = self.pack_order = self.center_packs = self.center_rows = None
+        self.center_order = self.pack_order = self.center_packs = self.center_rows = self.pack_info = None
         if molecules is not None:
             mol_ptr, line_ptr, trips, max_atoms = molecules
             call("x2g_vertex_to_edge_sym_mol", ptr(edge_src), ptr(edge_dst), self.E, self.N, self.T, ptr(mol_ptr),
@@ -153,7 +153,7 @@ class LineGraph:
         lg.dst_type = lg.src_type = None
         lg.symmetric = False
         lg.edge_rev = lg.rev_trip = lg.max_degree = lg.atom_type = None
-        lg.center_order = lg.pack_order = lg.center_packs = lg.center_rows = None
+        lg.center_order = lg.pack_order = lg.center_packs = lg.center_rows = lg.pack_info = None
         ws_bytes = int(_lib.load().x2g_vertex_to_edge_workspace(lg.E, 0))
         lg._ws = torch.empty(ws_bytes, dtype=torch.uint8, device=lg.trip_src.device)
         return lg
@@ -357,13 +357,14 @@ _CENTER_SF = True
 
 
 def _center_units(lg, packed):
-    """(order, pack_ptr or None, units, max_rows) of a whole-batch center kernel: with ``packed`` the
-    batch's packs of atoms (data.center_packs) when it has them, else one atom per workgroup by
-    decreasing degree."""
+    """(order, pack_ptr or None, units, max_rows, atom_info or None) of a whole-batch center kernel: with
+    ``packed`` the batch's packs of atoms (data.center_packs) when it has them, else one atom per
+    workgroup by decreasing degree."""
     packs = getattr(lg, "center_packs", None)
     if packed and packs is not None and lg.pack_order is not None and lg.center_rows is not None:
-        return lg.pack_order, packs, int(packs.shape[0]) - 1, max(int(lg.center_rows), 1)
-    return lg.center_order, None, lg.N, max(int(lg.max_degree), 1)
+        return lg.pack_order, packs, int(packs.shape[0]) - 1, max(int(lg.center_rows), 1), \
+            getattr(lg, "pack_info", None)
+    return lg.center_order, None, lg.N, max(int(lg.max_degree), 1), None
 
 
 # Workgroup packs (data.center_packs) in the fused forward: 16 owners per workgroup keep 90 % instead of
@@ -441,10 +442,10 @@ class _SBFAttention(torch.autograd.Function):
                     sbf_p = torch.empty(E, 7, D, dtype=torch.float32, device=dev)
                 else:
                     sproj = torch.empty(T, D, dtype=torch.float32, device=dev)
-            order, packs, units, rows = _center_units(lg, _PACK_FWD)
+            order, packs, units, rows, info = _center_units(lg, _PACK_FWD)
             call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(src_row),
                  edge_mode, ptr(factors[0]), ptr(factors[1]), ptr(w_sbf), ptr(b_sbf), ptr(lg.atom_rowptr),
-                 ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(order), ptr(packs), 0, units, rows, E, T, heads,
+                 ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(order), ptr(packs), ptr(info), 0, units, rows, E, T, heads,
                  channels, ptr(out), ptr(alpha), ptr(smax), ptr(sden), ptr(rstats), ptr(sproj), ptr(sbf_p),
                  stream_ptr())
         else:

@@ -77,6 +77,7 @@ class GraphPlan:
             p.lg.pack_order = st.get("_x2g_pack_order")
             p.lg.center_packs = st.get("_x2g_center_packs")
             p.lg.center_rows = st.get("_x2g_center_rows")
+            p.lg.pack_info = st.get("_x2g_pack_info")
         else:
             p.lg = ops.vertex_to_edge(ei, p.num_atoms, p.num_triplets, meta.get("symmetric", False))
             p.line_ptr = _ptr_from_counts(data.edge_num, p.num_graphs, dev)
