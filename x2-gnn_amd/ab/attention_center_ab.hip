@@ -625,19 +625,52 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const Bw
     DI[idx] = a.edge_rev[r0 + idx];
   }
   __syncthreads();
-  for (int idx = tid; idx < n * 32; idx += 64 * WAVES) {
-    const int j = idx >> 5, c = idx & 31;
-    const int64_t d = DI[j];
+  constexpr int NT = 64 * WAVES;
+  if (n * 32 <= 2 * NT && n * H <= NT) {  // (workgroup-uniform) every staging load in flight together
+    cf4 kk[2], gg[2], qq[2];
+    const int c = tid & 31;  // (the same column in both slots: NT is a multiple of 32)
     const cf4 e4 = EDGE ? ld4(a.edge + e_row + 4 * c) : cf4{0.f, 0.f, 0.f, 0.f};
-    KE[idx] = ld4(a.k + static_cast<int64_t>(r0 + j) * kCD + 4 * c) + e4;
-    GO[idx] = ld4(a.dout + d * kCD + 4 * c);
-    QI[idx] = ld4(a.q + d * kCD + 4 * c);
-  }
-  for (int idx = tid; idx < n * H; idx += 64 * WAVES) {
-    const int i = idx / H, h = idx - i * H;
-    const int64_t d = DI[i];
-    MX[idx] = a.smax[d * H + h];
-    IV[idx] = 1.0f / (a.sden[d * H + h] + kCEps);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      int j = (tid + u * NT) >> 5;
+      j = j < n ? j : n - 1;  // clamped: loads unconditional, stores masked below
+      const int64_t d = DI[j];
+      kk[u] = ld4(a.k + static_cast<int64_t>(r0 + j) * kCD + 4 * c);
+      gg[u] = ld4(a.dout + d * kCD + 4 * c);
+      qq[u] = ld4(a.q + d * kCD + 4 * c);
+    }
+    const int sidx = tid < n * H ? tid : 0;
+    const int si = sidx / H, sh = sidx - si * H;
+    const int64_t sd = DI[si];
+    const float mx = a.smax[sd * H + sh], dn = a.sden[sd * H + sh];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int idx = tid + u * NT;
+      if (idx < n * 32) {
+        KE[idx] = kk[u] + e4;
+        GO[idx] = gg[u];
+        QI[idx] = qq[u];
+      }
+    }
+    if (tid < n * H) {
+      MX[tid] = mx;
+      IV[tid] = 1.0f / (dn + kCEps);
+    }
+  } else {
+    for (int idx = tid; idx < n * 32; idx += NT) {
+      const int j = idx >> 5, c = idx & 31;
+      const int64_t d = DI[j];
+      const cf4 e4 = EDGE ? ld4(a.edge + e_row + 4 * c) : cf4{0.f, 0.f, 0.f, 0.f};
+      KE[idx] = ld4(a.k + static_cast<int64_t>(r0 + j) * kCD + 4 * c) + e4;
+      GO[idx] = ld4(a.dout + d * kCD + 4 * c);
+      QI[idx] = ld4(a.q + d * kCD + 4 * c);
+    }
+    for (int idx = tid; idx < n * H; idx += NT) {
+      const int i = idx / H, h = idx - i * H;
+      const int64_t d = DI[i];
+      MX[idx] = a.smax[d * H + h];
+      IV[idx] = 1.0f / (a.sden[d * H + h] + kCEps);
+    }
   }
   __syncthreads();
   const int nt = n - 1;  // triplets per destination (and per source)

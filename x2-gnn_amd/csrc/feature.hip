@@ -340,6 +340,29 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_bwd_kernel(const FeatBwdArg
     }
   const int c2 = 16 * w + i;
   const int64_t ntiles = (R + kFRows - 1) / kFRows;
+  // a tile's inputs: z2 (T layout) and dy of column c2 for both row blocks, and z1 of the wave's two
+  // column blocks.  z2 / dy of the NEXT tile and z1 of this one are issued before this tile's barrier and
+  // products, so they arrive under the MFMAs (one memory round trip per tile instead of three)
+  struct In {
+    f4 z2[2];
+    float dy[2][4];
+  };
+  auto load_in = [&](int64_t tile, In& in) {
+    const int64_t r0 = tile * kFRows;
+    const int nr = R - r0 < kFRows ? static_cast<int>(R - r0) : kFRows;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int64_t t16 = r0 / 16 + rb;
+      in.z2[rb] = t16 * 16 < R ? *reinterpret_cast<const f4*>(a.z2_t + tpos(a.tf, t16, c2, g)) : zero4();
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = 16 * rb + 4 * g + e;
+        in.dy[rb][e] = r < nr ? a.dy[(r0 + r) * kFN2 + c2] : 0.0f;
+      }
+    }
+  };
+  In cur;
+  if (static_cast<int64_t>(blockIdx.x) < ntiles) load_in(blockIdx.x, cur);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t r0 = tile * kFRows;
     const int nr = R - r0 < kFRows ? static_cast<int>(R - r0) : kFRows;
@@ -349,16 +372,24 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_bwd_kernel(const FeatBwdArg
     for (int rb = 0; rb < 2; ++rb) {
       const int64_t t16 = r0 / 16 + rb;
       const bool tile_ok = t16 * 16 < R;
-      const f4 z = tile_ok ? *reinterpret_cast<const f4*>(a.z2_t + tpos(a.tf, t16, c2, g)) : zero4();
       f4 d;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int r = 16 * rb + 4 * g + e;
-        d[e] = r < nr ? a.dy[(r0 + r) * kFN2 + c2] * silu_grad_(z[e]) : 0.0f;
+        d[e] = r < nr ? cur.dy[rb][e] * silu_grad_(cur.z2[rb][e]) : 0.0f;
         DZ[r * kFDS + c2] = d[e];
       }
       if (tile_ok) *reinterpret_cast<f4*>(a.dz2_t + tpos(a.tf, t16, c2, g)) = d;
     }
+    f4 z1v[2][2];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int64_t t16 = r0 / 16 + rb;
+      const int64_t tt = t16 * 16 < R ? t16 : r0 / 16;  // (a past-the-end block reads a valid one, unused)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) z1v[rb][k] = *reinterpret_cast<const f4*>(a.z1_t + tpos(a.tf, tt, k ? cb : ca, g));
+    }
+    if (tile + gridDim.x < ntiles) load_in(tile + gridDim.x, cur);
     __syncthreads();
     f4 acc[2][2] = {{zero4(), zero4()}, {zero4(), zero4()}};
 #pragma unroll
@@ -381,10 +412,9 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_bwd_kernel(const FeatBwdArg
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         const int c = k ? cb : ca;
-        const f4 z = *reinterpret_cast<const f4*>(a.z1_t + tpos(a.tf, t16, c, g));
         f4 d;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) d[e] = acc[rb][k][e] * silu_grad_(z[e]);
+        for (int e = 0; e < 4; ++e) d[e] = acc[rb][k][e] * silu_grad_(z1v[rb][k][e]);
         *reinterpret_cast<f4*>(a.dz1_t + tpos(a.tf, t16, c, g)) = d;
       }
     }
