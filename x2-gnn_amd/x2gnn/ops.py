@@ -947,11 +947,11 @@ def flush_keyed(pending: list):
 
 # Inference (grad mode off) with many triplets: S = lin_sbf(sbf) [T, D] is projected and consumed one
 # range of destination edges at a time (whole destination segments, at most INFER_TILE triplets),
-# so no more than [INFER_TILE, D] of it exists at once (config 5, T = 3.49M: 1.8 GB per layer
-# whole, 256 MB per tile at the default).  Cost at config 5 (bench --workload aid_infer): 9.34 ms
-# per step whole, 9.74 tiled at 2^19 triplets, 10.75 at 2^17 (per-launch ramp and drain; projecting
-# the next tile on a side stream under the current attention measured no better).
-INFER_TILE = 1 << 19
+# so no more than [INFER_TILE, D] of it exists at once.  Sized for 288 GB of HBM: 2^24 triplets are an
+# 8.6 GB tile, so config 5 (T = 3.49M, S 1.8 GB per layer) runs whole — one projection and one center
+# forward per layer: 8.00 ms per step against 9.11 tiled at 2^19 (seven tiles, 14 launches per layer
+# with their ramps and drains; profiles/r5ab_c5_tile.log) and 10.75 at 2^17 (round 4).
+INFER_TILE = 1 << 24
 
 
 def _infer_tiles(lg, tmax):
