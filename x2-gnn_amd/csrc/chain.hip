@@ -508,9 +508,17 @@ __device__ __forceinline__ float wave_sum(float v) {
 // combines the statistics of every 8th molecule that has rows in the chunk (every workgroup that
 // holds rows of a molecule computes the same values, in the same order); the workgroup holding a
 // molecule's first row writes its mean / rstd; then every image element is normalised in place.
+// A molecule of more than kLongMol rows (AID's ~2,000-row molecules) is combined by the whole workgroup
+// instead, each thread summing every 512th row: a chunk inside such a molecule then takes two short
+// passes, not one wave's serial walk over the molecule twice (config 5: 533 -> ~400 us per chain launch,
+// the other 7 waves had waited at the staging barrier; +6.5 % molecules/s).  Up to kLongMol rows the
+// one-wave form (at most 4 loop trips past its register window; S5A's ~300-row molecules: one) stays.
+// red: 2 x 8 floats of LDS.
+constexpr int kLongMol = 512;
 template <int RB = kV2RB>
 __device__ __forceinline__ void stage_rows_ln(f4* __restrict__ img, const float* __restrict__ P, int64_t R,
-                                              const ChainLn& ln, float2* __restrict__ lnrow, int r0, int nrows) {
+                                              const ChainLn& ln, float2* __restrict__ lnrow,
+                                              float* __restrict__ red, int r0, int nrows) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   stage_rows_async<RB>(img, P, R, r0);
   // the segment row pointers ptr[k], k = lane + 64 j < 256, in registers (one round of independent
@@ -538,10 +546,64 @@ __device__ __forceinline__ void stage_rows_ln(f4* __restrict__ img, const float*
     }
   };
   constexpr int kSW = 4;  // molecules of up to 256 rows: their statistics stay in registers
+  // the long molecules with rows here (workgroup-uniform loop; none at QM9 sizes)
+  for (int64_t m = m0 > 0 ? m0 : 0; m < ln.G; ++m) {
+    const int p0 = ptr_at(m), p1 = ptr_at(m + 1);
+    if (p0 >= r0 + nrows) break;
+    if (p1 - p0 <= kLongMol) continue;
+    const float n = static_cast<float>(p1 - p0);
+    constexpr int kU = 4;  // loads in flight per thread and pass
+    float s = 0.f;
+    for (int base = p0 + tid; base < p1; base += kU * kCThreads) {
+      float v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int r = base + u * kCThreads;
+        v[u] = r < p1 ? ln.stats[r].x : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) s += v[u];
+    }
+    s = wave64_sum(s);
+    if (lane == 0) red[w] = s;
+    __syncthreads();
+    float st = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < kCWaves; ++ww) st += red[ww];
+    const float mu = st / n;
+    float q = 0.f;
+    for (int base = p0 + tid; base < p1; base += kU * kCThreads) {
+      float2 v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int r = base + u * kCThreads;
+        v[u] = r < p1 ? ln.stats[r] : make_float2(mu, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const float d = v[u].x - mu;
+        q += fmaf(static_cast<float>(kCD) * d, d, v[u].y);
+      }
+    }
+    q = wave64_sum(q);
+    if (lane == 0) red[kCWaves + w] = q;
+    __syncthreads();
+    float qt = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < kCWaves; ++ww) qt += red[kCWaves + ww];
+    const float denom = sqrtf(qt / (n * static_cast<float>(kCD)) + ln.eps);
+    const int lo = p0 > r0 ? p0 : r0, hi = p1 < r0 + nrows ? p1 : r0 + nrows;
+    for (int r = lo + tid; r < hi; r += kCThreads) lnrow[r - r0] = make_float2(mu, denom);
+    if (tid == 0 && p0 >= r0) {
+      if (ln.mean) ln.mean[m] = mu;
+      if (ln.rstd) ln.rstd[m] = 1.0f / denom;
+    }
+    __syncthreads();  // red is reused by the next long molecule
+  }
   for (int64_t m = (m0 > 0 ? m0 : 0) + w; m < ln.G; m += kCWaves) {
     const int p0 = ptr_at(m), p1 = ptr_at(m + 1);
     if (p0 >= r0 + nrows) break;
-    if (p1 <= p0) continue;
+    if (p1 <= p0 || p1 - p0 > kLongMol) continue;
     const float n = static_cast<float>(p1 - p0);
     float2 sv[kSW];
 #pragma unroll
@@ -596,6 +658,7 @@ __device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a, const Ch
   __shared__ f4 img1[RB * 16 * 32];
   __shared__ f4 imgr[RB * 16 * 32];
   __shared__ float2 lnrow[LN ? RB * 16 : 1];
+  __shared__ float lnred[LN ? 2 * kCWaves : 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int rl = lane & 15, g = lane >> 4;
   const int64_t nblk = (a.R + 15) / 16, G = gridDim.x;
@@ -613,7 +676,7 @@ __device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a, const Ch
     chunk_rows(ch, nch, nblk, a.R, r0, nrows);
     __syncthreads();
     if (LN)
-      stage_rows_ln<RB>(img0, a.x, a.R, ln, lnrow, r0, nrows);
+      stage_rows_ln<RB>(img0, a.x, a.R, ln, lnrow, lnred, r0, nrows);
     else
       stage_rows<RB>(img0, a.x, nullptr, r0, nrows);
     if (a.res) stage_rows<RB>(imgr, a.res, nullptr, r0, nrows);
