@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -1126,11 +1127,19 @@ def _timed(name):
     evs.append((a, b))
 
 
+# FLAT_SPLIT > 0: the queued T-layout weight gradients are launched as soon as that many are queued (the
+# last layers' group mid-backward, the rest at exit) — the split an exchange overlap needs, so that the
+# first group's gradients exist before the backward ends.  0: one flat launch at exit (the default).
+FLAT_SPLIT = int(os.environ.get("X2G_FLAT_SPLIT", "0"))
+
+
 def _queue_tiled(d, R, jobs, keep):
     """Queue T-layout weight-gradient jobs (x2g_tiled_job, bucket-backed destinations) on deferral
     ``d`` for its flat launch; ``keep``: tensors the jobs point into."""
     d.tiled.setdefault(int(R), []).extend(jobs)
     d.keep.extend(keep)
+    if FLAT_SPLIT > 0 and not d.flat_launches and sum(len(j) for j in d.tiled.values()) >= FLAT_SPLIT:
+        _flush_tiled(d)
 
 
 def _flush_tiled(d):
@@ -1139,7 +1148,6 @@ def _flush_tiled(d):
     (x2g_tiled_wgrad_flat_rows; one launch per row count before).  ``d.flat_launches`` records each
     launch as [(rows, cols) per job]."""
     lib = _lib.load()
-    d.flat_launches.clear()
     items = [(int(R), j) for R, jobs in d.tiled.items() for j in jobs]
     for j0 in range(0, len(items), TILED_MAX_JOBS):
         part = items[j0:j0 + TILED_MAX_JOBS]
