@@ -285,6 +285,7 @@ int x2g_sbf_attention_fwd_stats(const float* q, const float* k, const float* v, 
  *   max_degree >= every deg(b) of those atoms, <= X2G_CENTER_MAX_DEGREE (sizes the LDS image).
  *   atom_order (or NULL): workgroup w takes center atom atom_order[atom0 + w] (a permutation of the range;
  *   x2gnn passes the atoms by decreasing degree, so the longest blocks start first).
+ *   alpha_raw may be NULL (inference without attention weights): the logits are then not stored.
  * heads * channels = 128 and channels a multiple of 4, 16-byte aligned rows, else X2G_EUNSUPPORTED. */
 #define X2G_CENTER_MAX_DEGREE 128
 int x2g_sbf_attention_fwd_center(const float* q, const float* k, const float* v, const float* skip,
@@ -314,7 +315,8 @@ int x2g_sbf_attention_fwd_center(const float* q, const float* k, const float* v,
  * (w_sbf [128, 42], b_sbf [128]).  Outputs as x2g_sbf_attention_fwd_center; for a backward, either
  * sbfproj_out [T, 128] receives every S_t row, or sbf_p_out [E, 7, 128] every source's P rows (3.5 KB per
  * line node instead of 512 B per triplet: x2g_sbf_attention_bwd_center rebuilds S_t from them bit for
- * bit); either may be NULL.  Units unit0 .. unit0 + n_units - 1.  LDS
+ * bit); either may be NULL, and so may alpha_raw (inference: no logits stored).  Units unit0 .. unit0 +
+ * n_units - 1.  LDS
  * per workgroup 4.7 KB x max_rows (<= 160 KiB, else X2G_EUNSUPPORTED); no t_base tiling is needed
  * (nothing T x 128 is read). */
 int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, const float* v, const float* skip,

@@ -235,7 +235,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_kernel(const FwdCe
         const float logit = head_sum<LPH>(dot) / a.sqrt_c;
         lg[u] = ok ? logit : -INFINITY;
         mb = fmaxf(mb, lg[u]);
-        if (ok && leader) a.alpha[(static_cast<int64_t>(tb) + (j - (j > i ? 1 : 0))) * a.H + head] = logit;
+        if (a.alpha && ok && leader) a.alpha[(static_cast<int64_t>(tb) + (j - (j > i ? 1 : 0))) * a.H + head] = logit;
       }
       const float m_new = fmaxf(m, mb);
       const float corr = m_new == -INFINITY ? 1.f : expf(m - m_new);
@@ -439,7 +439,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_fwd_center_sf_kernel(const
         const float logit = head_sum<LPH>(dot) / a.sqrt_c;
         lg[uu] = ok ? logit : -INFINITY;
         mb = fmaxf(mb, lg[uu]);
-        if (ok && leader) a.alpha[static_cast<int64_t>(tt[uu]) * a.H + head] = logit;
+        if (a.alpha && ok && leader) a.alpha[static_cast<int64_t>(tt[uu]) * a.H + head] = logit;
       }
       const float m_new = fmaxf(m, mb);
       const float corr = m_new == -INFINITY ? 1.f : expf(m - m_new);
@@ -923,7 +923,7 @@ X2G_API int x2g_sbf_attention_fwd_center(const float* q, const float* k, const f
   if (n_atoms == 0 || num_edges == 0) return X2G_OK;
   if (!q || !k || !v || !skip || !sbfproj || !atom_rowptr || !edge_rev || !rev_trip || !out || !seg_max || !seg_den)
     return X2G_EINVAL;
-  if (num_triplets > 0 && !alpha_raw) return X2G_EINVAL;
+  // (alpha_raw NULL: the logits are not stored — inference)
   if (edge_mode == X2G_EDGE_PER_DST && (!edge || !src_row)) return X2G_EINVAL;
   // 16-byte rows (float4 per lane), 8-byte row statistics
   const auto al = [](const void* p, int m) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % m == 0; };
@@ -969,7 +969,7 @@ X2G_API int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, cons
   if (!q || !k || !v || !skip || !radial || !sph_y || !w_sbf || !b_sbf || !atom_rowptr || !edge_rev || !rev_trip ||
       !out || !seg_max || !seg_den || (pack_ptr && !atom_order))
     return X2G_EINVAL;
-  if (num_triplets > 0 && !alpha_raw) return X2G_EINVAL;
+  // (alpha_raw NULL: the logits are not stored — inference)
   if (edge_mode == X2G_EDGE_PER_DST && (!edge || !src_row)) return X2G_EINVAL;
   const auto al = [](const void* p, int m) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % m == 0; };
   if (!al(q, 16) || !al(k, 16) || !al(v, 16) || !al(skip, 16) || !al(edge, 16) || !al(out, 16) || !al(b_sbf, 16) ||

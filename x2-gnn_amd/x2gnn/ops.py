@@ -414,7 +414,8 @@ def _center_rows(lg, edge_mode, edge_row, D, channels):
 
 class _SBFAttention(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row, heads, channels):
+    def forward(ctx, q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row, heads, channels,
+                keep_alpha=True):
         w_param, b_param = w_sbf, b_sbf
         # its gradient is read only by the table chain's backward, which flushes deferred sums first
         pending = getattr(edge, "_x2g_keyed_pending", None)
@@ -427,12 +428,15 @@ class _SBFAttention(torch.autograd.Function):
         E, T, D = q.shape[0], lg.T, heads * channels
         dev = q.device
         out = torch.empty(E, D, dtype=torch.float32, device=dev)
-        alpha = torch.empty(T, heads, dtype=torch.float32, device=dev)
+        center, src_row = _center_rows(lg, edge_mode, edge_row, D, channels)
+        # the logits [T, H] are read by a backward or for the attention weights; the center forwards skip
+        # the store otherwise (inference: 223 MB per layer at config 5)
+        alpha = (torch.empty(T, heads, dtype=torch.float32, device=dev)
+                 if keep_alpha or any(ctx.needs_input_grad) or not center else None)
         smax = torch.empty(E, heads, dtype=torch.float32, device=dev)
         sden = torch.empty(E, heads, dtype=torch.float32, device=dev)
         # per-row (mean, M2) of the output for a graph LayerNorm fused into the next row chain
         rstats = torch.empty(E, 2, dtype=torch.float32, device=dev) if _LN_FUSE and D == 128 else None
-        center, src_row = _center_rows(lg, edge_mode, edge_row, D, channels)
         sbf_p = None
         if center and _center_sf_ok(lg, factors, D):
             # lin_sbf fused into the center forward: S_t rebuilt per center atom from the sbf factors; for a
@@ -520,7 +524,7 @@ class _SBFAttention(torch.autograd.Function):
             dw, db = linear_wgrad(dproj, sbf, dw_out=gw, db_out=gb)  # summed into the bucket: None
         else:
             dw, db = linear_wgrad(dproj, sbf)
-        return dq, dk, dv, dout, d_edge, None, dw, db, None, None, None, None, None
+        return dq, dk, dv, dout, d_edge, None, dw, db, None, None, None, None, None, None
 
     @staticmethod
     def _backward_fold(ctx, dout, q, k, v, edge, radial, ylm, sproj, alpha, smax, sden, dq, dk, dv, sbf_p=None,
@@ -556,7 +560,7 @@ class _SBFAttention(torch.autograd.Function):
                 dw, db = sbf_radial_wgrad(gfold, radial, dw_out=gw, db_out=gb)
             else:
                 dw, db = sbf_radial_wgrad(gfold, radial)
-            return dq, dk, dv, dout, d_edge, None, dw, db, None, None, None, None, None
+            return dq, dk, dv, dout, d_edge, None, dw, db, None, None, None, None, None, None
         d_edge = torch.empty(E, D, dtype=torch.float32, device=dev) if mode == EDGE_PER_DST else None
         call("x2g_sbf_attention_bwd_dst_g", ptr(q), ptr(k), ptr(v), ptr(edge), ptr(ctx.edge_row), mode, ptr(sproj),
              ptr(lg.trip_rowptr), ptr(lg.trip_src), ptr(alpha), ptr(smax), ptr(sden), ptr(dout), E, T, heads, channels,
@@ -581,7 +585,7 @@ class _SBFAttention(torch.autograd.Function):
             dw, db = sbf_radial_wgrad(gfold, radial, dw_out=gw, db_out=gb)
         else:
             dw, db = sbf_radial_wgrad(gfold, radial)
-        return dq, dk, dv, dout, d_edge, None, dw, db, None, None, None, None, None
+        return dq, dk, dv, dout, d_edge, None, dw, db, None, None, None, None, None, None
 
 
 def sbf_radial_wgrad(gfold, radial, dw_out=None, db_out=None):
@@ -995,13 +999,14 @@ def _infer_tiles(lg, tmax):
     return tiles
 
 
-def _attention_fwd_tiled(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row, heads, channels, tmax):
+def _attention_fwd_tiled(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, edge_row, heads, channels, tmax,
+                         keep_alpha=True):
     q, k, v, skip = _f32(q), _f32(k), _f32(v), _f32(skip)
     sbf, w_sbf, b_sbf = _f32(sbf), _f32(w_sbf), _f32(b_sbf)
     edge = _f32(edge) if edge is not None else None
     E, T, D, H = q.shape[0], lg.T, heads * channels, heads
     f32 = dict(dtype=torch.float32, device=q.device)
-    out, alpha = torch.empty(E, D, **f32), torch.empty(T, H, **f32)
+    out = torch.empty(E, D, **f32)
     smax, sden = torch.empty(E, H, **f32), torch.empty(E, H, **f32)
     rstats = torch.empty(E, 2, **f32) if _LN_FUSE and D == 128 else None
     tiles = _infer_tiles(lg, tmax)
@@ -1010,6 +1015,7 @@ def _attention_fwd_tiled(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, 
     fb, ib = 4, 4  # bytes per float32 / int32 element
     center, src_row = _center_rows(lg, edge_mode, edge_row, D, channels)
     center = center and all(t[4] is not None for t in tiles)
+    alpha = torch.empty(T, H, **f32) if keep_alpha or not center else None  # (the center forward may skip it)
     for e0, e1, t0, t1, atoms in tiles:
         ta = t0 & ~1  # from an even row: the projection's fast path wants 16-byte aligned sbf blocks
         call("x2g_sbf_project", sbf.data_ptr() + ta * sbf.shape[1] * fb, t1 - ta, sbf.shape[1], ptr(w_sbf),
@@ -1051,10 +1057,10 @@ def sbf_attention(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg: LineGraph, heads: 
           and _center_sf_ok(lg, _sbf_factors(lg, sbf, edge_mode, heads * channels, edge, edge_row), heads * channels))
     if not torch.is_grad_enabled() and lg.T > INFER_TILE and q.shape[0] > 0 and not sf:  # (sf: no S at all)
         out, alpha, smax, sden, rstats = _attention_fwd_tiled(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode,
-                                                              edge_row, heads, channels, INFER_TILE)
+                                                              edge_row, heads, channels, INFER_TILE, return_attention)
     else:
         out, alpha, smax, sden, rstats = _SBFAttention.apply(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode,
-                                                         edge_row, heads, channels)
+                                                         edge_row, heads, channels, return_attention)
     if rstats is not None:  # for a graph LayerNorm fused into the consumer (ops.row_chain(ln=...))
         out._x2g_rowstats = rstats
     if not return_attention:
