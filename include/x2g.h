@@ -342,7 +342,9 @@ int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, const float*
  * b_sbf [128] as S_t = b + sum_l Y_l(t) P_s[l] (exactly one of the two forms).
  * sph_y [T, 8] as x2g_spherical_basis writes it.  LDS per workgroup:
  * x2g_sbf_attention_bwd_center_lds(max_degree, heads) bytes (<= 160 KiB, else X2G_EUNSUPPORTED).
- * heads * channels = 128, channels a multiple of 4, 16-byte aligned rows. */
+ * heads * channels = 128, channels a multiple of 4, 16-byte aligned rows.  T-row arrays are addressed with
+ * 32-bit offsets: T * 512 < 2^31 with sbfproj, T * heads * 8 < 2^31 with sbf_p, else X2G_EUNSUPPORTED
+ * (x2gnn then takes the destination-major passes). */
 size_t x2g_sbf_attention_bwd_center_lds(int32_t max_degree, int32_t heads);
 int x2g_sbf_attention_bwd_center(const float* q, const float* k, const float* v, const float* edge,
                                  const int32_t* src_row, int edge_mode, const float* sbfproj, const float* sbf_p,

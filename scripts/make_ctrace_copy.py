@@ -1,4 +1,4 @@
-"""Regenerate x2-gnn_amd/ab/attention_center_ab.hip from csrc/attention_center.hip with the phase stamps of the
+"""Generate x2-gnn_amd/build/ab_src/attention_center_ab.hip (untracked) from csrc/attention_center.hip with the phase stamps of the
 center backward (scripts/trace_center_bwd.py reads them): thread 0 of each workgroup stamps the 100 MHz wall
 clock at kernel start, after staging, after its pass 1, after the fence barrier, after rho, after pass 2 and
 at the end (CTR(0..6), compiled only with -DX2G_TRACE).  Then:
@@ -77,5 +77,7 @@ X2G_API int x2g_ctrace_fetch(unsigned long long* host, int n) {
 #endif
 '''
 assert s.count("CTR(") == 9 and s.count("FTR(") == 7, (s.count("CTR("), s.count("FTR("))
-open(os.path.join(ROOT, "x2-gnn_amd", "ab", "attention_center_ab.hip"), "w").write(s)
+dst = os.path.join(ROOT, "x2-gnn_amd", "build", "ab_src", "attention_center_ab.hip")
+os.makedirs(os.path.dirname(dst), exist_ok=True)
+open(dst, "w").write(s)
 print("ok")

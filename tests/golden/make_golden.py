@@ -286,6 +286,9 @@ FULL = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embe
 SEL = ["fin_model.convs.0.lin_sbf.weight", "fin_model.convs.3.lin_query.weight",
        "fin_model.convs.1.lin_edge.weight", "emb_block.embedding.weight", "rbf_layer.frequencies",
        "fin_model.readouts.2.lin_rbf.weight", "fin_model.edgenn.0.weight", "mat_trans.weight"]
+SEL_CONV = [f"fin_model.convs.{i}.{lin}.{p}" for i in (0, 3)
+            for lin in ("lin_key", "lin_value", "lin_query", "lin_skip", "lin_sbf", "lin_edge", "lin_rbf")
+            for p in ("weight", "bias")]
 
 
 def aid_molecules(k, seed=0):
@@ -315,6 +318,11 @@ GENERATORS = {
     # config 5: real AID geometry (the two smallest molecules), full width
     "model_aid": lambda ref: gen_model(ref, "model_aid.npz", "poly", FULL, n_mol=1, seed_mol=0, seed_w=206,
                                        grads=SEL, mols=aid_molecules(2)),
+    # config-2 width on the physical 5 A geometry (degrees up to 17): the shipped center-atom attention
+    # kernels (D = 128 only) against the reference with per-element gradients of every conv projection
+    # of two layers (lin_key / lin_value / lin_sbf / lin_rbf carry the center backward's dk, dv, G)
+    "model_s5a_full": lambda ref: gen_model(ref, "model_s5a_full.npz", "poly", FULL, n_mol=2, seed_mol=46,
+                                            seed_w=207, shape="S5A", grads=SEL + SEL_CONV),
     "aid_geom": lambda ref: gen_aid_geometry(ref),
     "xyz_ref": lambda ref: gen_xyz_ref(ref),
 }

@@ -6,9 +6,13 @@ from conftest import golden  # noqa: F401
 from weights import load_seeded
 
 
-def batch_from_fixture(z, prefix=""):
-    """Collated x2gnn Batch (host) from a fixture's stored inputs."""
-    from x2gnn.data import Batch, Data
+def batch_from_fixture(z, prefix="", shipped=True):
+    """Collated x2gnn Batch (host) from a fixture's stored inputs.  ``shipped``: with the index forms
+    collate attaches (symmetric flag, largest degree, center order / packs / atom_info, per-molecule
+    triplet counts), so a model runs the path a training batch takes (the center-atom attention kernels
+    at D = 128); False: the bare tensors, which take the generic line-graph build and the
+    destination-major attention kernels."""
+    from x2gnn.data import Batch, Data, _add_device_indices
 
     nodes, edges, trips = z[prefix + "nodes"], z[prefix + "edges"], z[prefix + "triplets"]
     b = Batch()
@@ -22,6 +26,8 @@ def batch_from_fixture(z, prefix=""):
     b._store["ptr"] = torch.from_numpy(np.concatenate([[0], np.cumsum(nodes)]).astype(np.int64))
     object.__setattr__(b, "_meta", {"nodes": nodes.astype(np.int64), "edges": edges.astype(np.int64),
                                     "triplets": trips.astype(np.int64)})
+    if shipped:
+        _add_device_indices(b, nodes.astype(np.int64), edges.astype(np.int64))
     assert isinstance(b, Data)
     return b
 

@@ -31,21 +31,31 @@ def grad_scale(z, names):
     return max(float(z["gnorm." + n]) for n in names)
 
 
-@pytest.mark.parametrize("fixture", ["model_small.npz", "model_full.npz", "model_global.npz", "model_s5a.npz",
-                                     "model_global_add.npz", "model_aid.npz"])
-def test_model_energies_and_gradients_vs_reference(cuda, fixture):
-    z = golden(fixture)
-    m = product_model(z, cuda)
-    b = batch_from_fixture(z).to(cuda)
-    res = m(b)
+def record_calls(monkeypatch):
+    """Every C-ABI entry the host layer calls from here on: [(name, args)] (ops.call wrapped)."""
+    from x2gnn import ops
+
+    seen, inner = [], ops.call
+
+    def rec(name, *args):
+        seen.append((name, args))
+        return inner(name, *args)
+
+    monkeypatch.setattr(ops, "call", rec)
+    return seen
+
+
+def check_vs_fixture(m, z, res, y):
+    """Energies within ENERGY_RTOL per molecule, the embedding after max_norm, every parameter
+    gradient's norm and the per-element gradients the fixture holds."""
     assert res.shape == z["energies"].shape
     assert energy_rel_err(res.detach().cpu().numpy(), z["energies"]) < ENERGY_RTOL
-    loss = torch.nn.functional.smooth_l1_loss(res, b.y)
-    loss.backward()
+    torch.nn.functional.smooth_l1_loss(res, y).backward()
     np.testing.assert_allclose(m.emb_block.embedding.weight.detach().cpu().numpy(), z["emb_after"], rtol=1e-6,
                                atol=1e-7)
     names = [n for n, _ in m.named_parameters()]
     scale = grad_scale(z, names)
+    checked = 0
     for n, p in m.named_parameters():
         ref_norm = float(z["gnorm." + n])
         got = 0.0 if p.grad is None else float(p.grad.double().norm())
@@ -53,6 +63,48 @@ def test_model_energies_and_gradients_vs_reference(cuda, fixture):
         if "grad." + n in z.files:
             ref = z["grad." + n]
             assert np.abs(p.grad.cpu().numpy() - ref).max() <= 2e-3 * np.abs(ref).max() + 1e-6 * scale, n
+            checked += 1
+    return checked
+
+
+def max_degree(z):
+    return int(np.bincount(z["edge_index"][0]).max())
+
+
+MODEL_FIXTURES = ["model_small.npz", "model_full.npz", "model_global.npz", "model_s5a.npz", "model_global_add.npz",
+                  "model_aid.npz", "model_s5a_full.npz"]
+
+
+@pytest.mark.parametrize("path", ["shipped", "dst_major"])
+@pytest.mark.parametrize("fixture", MODEL_FIXTURES)
+def test_model_energies_and_gradients_vs_reference(cuda, monkeypatch, fixture, path):
+    """The reference's own energies and gradients (fixtures written by running it) through the path a
+    collated training batch takes (``shipped``: symmetric line graph, center-atom attention kernels with
+    packs, atom_info and P rows at D = 128 — asserted from the calls made) and through the
+    destination-major fallback kernels (a batch without collate's index forms)."""
+    z = golden(fixture)
+    m = product_model(z, cuda)
+    b = batch_from_fixture(z, shipped=path == "shipped").to(cuda)
+    seen = record_calls(monkeypatch)
+    res = m(b)
+    check_vs_fixture(m, z, res, b.y)
+    names = [n for n, _ in seen]
+    wide = model_cfg(z)["in_channels"] == 128
+    if path == "shipped" and wide:
+        layers = model_cfg(z)["conv_layers"]
+        fwd = [(n, a) for n, a in seen if n.startswith("x2g_sbf_attention_fwd_center")]
+        assert len(fwd) == layers
+        # the fused-projection form with pack_ptr and atom_info handed over (or, for atoms whose LDS image
+        # does not fit it, the S-reading center forward)
+        assert all(a[15] and a[16] for n, a in fwd if n == "x2g_sbf_attention_fwd_center_sf")
+        if max_degree(z) <= 33:
+            assert all(n == "x2g_sbf_attention_fwd_center_sf" for n, _ in fwd)
+            assert "x2g_sbf_project" not in names
+        assert names.count("x2g_sbf_attention_bwd_center") == layers
+        assert "x2g_sbf_attention_bwd_dst_g" not in names
+    else:
+        assert not any(n.startswith("x2g_sbf_attention_fwd_center") or n == "x2g_sbf_attention_bwd_center"
+                       for n in names)
 
 
 def _fwd_bwd(z, cuda):
@@ -450,7 +502,7 @@ def test_inference_tiled_projection_equals_whole(cuda, monkeypatch, tile):
 
     z = golden("model_full.npz")
     m = product_model(z, cuda)
-    b = batch_from_fixture(z).to(cuda)
+    b = batch_from_fixture(z, shipped=False).to(cuda)  # (a collated batch runs the fused form: no S at all)
     emb = m.emb_block.embedding.weight
     w0 = emb.detach().clone()  # every forward applies the max_norm renorm in place: same start for both
     monkeypatch.setattr(ops, "INFER_TILE", 1 << 30)
@@ -717,25 +769,24 @@ class _ForeignBatch:
         return int(self._store["x"].shape[0])
 
 
-@pytest.mark.parametrize("fixture", ["model_full.npz", "model_global.npz"])
-def test_foreign_pyg_style_batch_vs_reference(cuda, fixture):
+@pytest.mark.parametrize("fixture", ["model_full.npz", "model_global.npz", "model_s5a_full.npz", "model_aid.npz"])
+def test_foreign_pyg_style_batch_vs_reference(cuda, monkeypatch, fixture):
     """xgnn_poly.forward(data) on a duck-typed PyG-style batch (the drop-in's real caller): the
-    plan derives the per-molecule sizes from the tensors; energies and gradients equal the
-    reference fixture as for x2gnn's own Batch."""
+    plan derives the per-molecule sizes and the center-atom schedule from the tensors on the device;
+    energies, gradient norms and the fixture's per-element gradients equal the reference's as for
+    x2gnn's own Batch, through the center-atom kernels at D = 128."""
     z = golden(fixture)
-    own = batch_from_fixture(z)
+    own = batch_from_fixture(z, shipped=False)
     fb = _ForeignBatch(**{k: v.to(cuda) for k, v in own._store.items() if not k.startswith("_x2g")})
     assert not hasattr(fb, "host_meta")
     m = product_model(z, cuda)
+    seen = record_calls(monkeypatch)
     res = m(fb)
-    assert energy_rel_err(res.detach().cpu().numpy(), z["energies"]) < ENERGY_RTOL
-    torch.nn.functional.smooth_l1_loss(res, fb.y).backward()
-    names = [n for n, _ in m.named_parameters()]
-    scale = grad_scale(z, names)
-    for n, p in m.named_parameters():
-        ref_norm = float(z["gnorm." + n])
-        got = 0.0 if p.grad is None else float(p.grad.double().norm())
-        assert abs(got - ref_norm) <= 2e-3 * ref_norm + 1e-6 * scale, (n, got, ref_norm)
+    assert check_vs_fixture(m, z, res, fb.y) >= 5
+    if model_cfg(z)["in_channels"] == 128:
+        names = [n for n, _ in seen]
+        assert sum(n.startswith("x2g_sbf_attention_fwd_center") for n in names) == model_cfg(z)["conv_layers"]
+        assert names.count("x2g_sbf_attention_bwd_center") == model_cfg(z)["conv_layers"]
 
 
 def test_foreign_batch_meta_on_device_and_forward_time(cuda):

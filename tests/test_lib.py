@@ -80,3 +80,27 @@ def test_attention_rejects_uncompiled_shapes():
     assert rc == 1002
     rc = lib.x2g_sbf_attention_fwd(p, p, p, p, None, None, 0, p, p, p, p, p, 4, 0, 16, 8, 40, p, p, p, p, None)
     assert rc == 1002
+
+
+def test_center_backward_refuses_32bit_overflow_and_host_falls_back():
+    """The center backward addresses its T-row arrays with 32-bit buffer offsets: T * 512 B for S rows,
+    T * heads * 8 B (the (g, a) scratch) for P rows; beyond that it returns X2G_EUNSUPPORTED before
+    touching anything, and the host's predicate routes such a batch to the destination-major passes
+    (which the forward then feeds with S rows) instead of failing in the backward."""
+    import types
+
+    from x2gnn import _lib, ops
+
+    lib = _lib.load()
+    p = ctypes.c_void_p(16)  # never dereferenced: the size check fails first
+    big = (1 << 31) // 512  # the first T whose S rows overflow
+    args = lambda sp, pp, T: (p, p, p, None, None, 0, sp, pp, p, p, p, p, p, p, p, p, p, p, 4, 16, 64, T, 16, 8,  # noqa: E731
+                              p, p, p, p, None, p, None)
+    assert lib.x2g_sbf_attention_bwd_center(*args(p, None, big)) == 1002
+    assert lib.x2g_sbf_attention_bwd_center(*args(None, p, (1 << 31) // 128)) == 1002
+    lg = types.SimpleNamespace(atom_type=object(), max_degree=16, T=big - 1)
+    assert ops._center_bwd_ok(lg, 16) and ops._center_bwd_ok(lg, 16, s_rows=True)
+    lg.T = big
+    assert ops._center_bwd_ok(lg, 16) and not ops._center_bwd_ok(lg, 16, s_rows=True)
+    lg.T = (1 << 31) // 128
+    assert not ops._center_bwd_ok(lg, 16)

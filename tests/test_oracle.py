@@ -87,7 +87,7 @@ def test_conv_layer_vs_reference():
 
 
 @pytest.mark.parametrize("fixture", ["model_small.npz", "model_full.npz", "model_global.npz", "model_s5a.npz",
-                                     "model_global_add.npz", "model_aid.npz"])
+                                     "model_global_add.npz", "model_aid.npz", "model_s5a_full.npz"])
 def test_model_vs_reference(fixture):
     z = golden(fixture)
     m = oracle_model(z)

@@ -874,7 +874,9 @@ X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const f
   if (heads * channels != kCD || channels % 4 || max_degree < 0 || max_degree > X2G_CENTER_MAX_DEGREE)
     return X2G_EUNSUPPORTED;
   if (x2g_sbf_attention_bwd_center_lds(max_degree, heads) > 160 * 1024) return X2G_EUNSUPPORTED;
-  if (num_triplets * kCD * 4 >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;  // 32-bit S offsets
+  // 32-bit buffer offsets: the S rows (T x 512 B), or with P rows the (g, a) scratch (T x H x 8 B, the
+  // largest T-row array then: logits T x H x 4, Y rows T x 32)
+  if (num_triplets * (sbf_p ? int64_t(heads) * 8 : int64_t(kCD) * 4) >= (int64_t(1) << 31)) return X2G_EUNSUPPORTED;
   if (num_atoms == 0) return X2G_OK;
   if (!sbfproj == !sbf_p || (sbf_p && !b_sbf)) return X2G_EINVAL;  // S rows, or the P rows and the bias
   if (num_edges > 0 && (!q || !k || !v || !sph_y || !atom_rowptr || !edge_rev || !rev_trip ||

@@ -611,7 +611,8 @@ X2G_API int x2g_batch_meta(const int64_t* edge_index, const int64_t* x, const in
   if (num_edges > 0 && (!edge_index || !edge_src || !edge_dst || !src_type || !dst_type)) return X2G_EINVAL;
   if (num_edges > 0x7fffffff || num_nodes > 0x7fffffff) return X2G_EUNSUPPORTED;
   hipStream_t st = as_stream(stream);
-  const int64_t na = (num_nodes + 1 > num_graphs + 3 ? num_nodes + 1 : num_graphs + 3);
+  // threads: N + 1 atom slots, and B + 4 to zero the triplet counts and the four flags
+  const int64_t na = (num_nodes + 1 > num_graphs + 4 ? num_nodes + 1 : num_graphs + 4);
   batch_meta_atoms<<<blocks_for(na, 256), 256, 0, st>>>(x, batch, num_nodes, num_graphs, atom_type, mol_ptr, info);
   if (int rc = last_launch_status()) return rc;
   batch_meta_edges<<<blocks_for(num_edges + 1, 256), 256, 0, st>>>(edge_index, x, batch, num_edges, num_nodes,

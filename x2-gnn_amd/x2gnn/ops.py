@@ -19,7 +19,6 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
-import os
 
 import numpy as np
 import torch
@@ -391,10 +390,13 @@ def _center_sf_ok(lg, factors, D):
     return _unit_rows_lds(rows) + 4776 * rows <= 160 * 1024
 
 
-def _center_bwd_ok(lg, heads):
+def _center_bwd_ok(lg, heads, s_rows=False):
     """Whether the center-atom backward takes this line graph (its element rows known, the LDS image of the
-    largest atom's block within 160 KB)."""
+    largest atom's block within 160 KB, and its T-row arrays within the kernel's 32-bit buffer offsets:
+    the S rows T x 512 B when ``s_rows``, else the P-row form's (g, a) scratch T x heads x 8 B)."""
+    row_bytes = 128 * 4 if s_rows else heads * 8
     return (_CENTER_BWD and getattr(lg, "atom_type", None) is not None and lg.max_degree is not None and
+            lg.T * row_bytes < 2 ** 31 and
             _lib.load().x2g_sbf_attention_bwd_center_lds(lg.max_degree, heads) <= 160 * 1024)
 
 
@@ -539,7 +541,7 @@ class _SBFAttention(torch.autograd.Function):
         gfold = torch.empty(E, 8, D, dtype=torch.float32, device=dev)
         st = stream_ptr()
         center, src_row = _center_rows(lg, mode, ctx.edge_row, D, channels)
-        if sbf_p is not None or (center and _center_bwd_ok(lg, heads)):
+        if sbf_p is not None or (center and _center_bwd_ok(lg, heads, s_rows=True)):
             # one launch for both passes, per center atom (csrc/attention_center.hip); the edge term's
             # gradient comes per center atom and is summed by the atoms' elements
             want_edge = mode == EDGE_PER_DST and ctx.needs_input_grad[4]
@@ -1135,8 +1137,9 @@ def _timed(name):
 
 # FLAT_SPLIT > 0: the queued T-layout weight gradients are launched as soon as that many are queued (the
 # last layers' group mid-backward, the rest at exit) — the split an exchange overlap needs, so that the
-# first group's gradients exist before the backward ends.  0: one flat launch at exit (the default).
-FLAT_SPLIT = int(os.environ.get("X2G_FLAT_SPLIT", "0"))
+# first group's gradients exist before the backward ends.  0: one flat launch at exit (the default).  A
+# constant like the switches above (set explicitly by an A/B script or a test, never from the environment).
+FLAT_SPLIT = 0
 
 
 def _queue_tiled(d, R, jobs, keep):

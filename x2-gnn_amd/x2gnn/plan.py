@@ -64,10 +64,12 @@ class GraphPlan:
         dev = ei.device
         # the int32 index forms: collate's (x2gnn's own batches) or x2g_batch_meta's (a foreign batch)
         st = meta.get("index") or data._store
+        within = False  # every edge known to stay inside its molecule (collate's batches; x2g_batch_meta flag 3)
         if "_x2g_edge_src" in st and st["_x2g_edge_src"].device == dev:
             mols = None
             if st.get("_x2g_mol_trips") is not None and st["_x2g_mol_trips"].device == dev:
                 mols = (st["_x2g_mol_ptr"], st["_x2g_line_ptr"], st["_x2g_mol_trips"], st["_x2g_max_mol_atoms"])
+                within = True
             p.lg = ops.LineGraph(st["_x2g_edge_src"], st["_x2g_edge_dst"], p.num_atoms, p.num_triplets,
                                  st.get("_x2g_symmetric", False), molecules=mols)
             p.line_ptr, p.mol_ptr, p.dst_type = st["_x2g_line_ptr"], st["_x2g_mol_ptr"], st["_x2g_dst_type"]
@@ -94,9 +96,11 @@ class GraphPlan:
         p.lg.dst_type, p.lg.src_type = p.dst_type, src_type
         p.atom_rowptr = p.lg.atom_rowptr
         # per-molecule line-node / triplet counts on the host: whole-molecule ranges of the triplet
-        # stream for the tiled inference attention (ops._infer_tiles), with no device read
-        p.lg.mol_counts = (np.asarray(edges, dtype=np.int64), np.asarray(trips, dtype=np.int64),
-                           np.asarray(nodes, dtype=np.int64))
+        # stream for the tiled inference attention (ops._infer_tiles), with no device read; the atoms
+        # per molecule only when no edge joins two molecules (the tiled center forward assumes a tile's
+        # atoms own exactly its triplets: otherwise the destination-major tiles)
+        p.lg.mol_counts = (np.asarray(edges, dtype=np.int64), np.asarray(trips, dtype=np.int64)) + (
+            (np.asarray(nodes, dtype=np.int64),) if within else ())
         # the largest center-atom degree (host metadata): sizes the center-atom kernels' LDS image
         md = st.get("_x2g_max_degree", meta.get("max_degree"))
         p.lg.max_degree = int(md) if md is not None else None
