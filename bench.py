@@ -52,14 +52,37 @@ TRAFFIC_JSON = {("qm9_u0", "S160"): os.path.join(ROOT, "profiles", "r5_pmc_traff
 STEP_WORK_JSON = os.path.join(ROOT, "profiles", "r5_step_work.json")
 
 
+def product_digest():
+    """sha256 over the product sources (x2-gnn_amd/csrc/* and x2-gnn_amd/x2gnn/*.py, sorted by name): what a
+    committed measurement table was taken on (.git does not travel to the GPU box, so the commit alone
+    cannot be checked there)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    pkg = os.path.join(ROOT, "x2-gnn_amd")
+    for sub, ext in (("csrc", ""), ("x2gnn", ".py")):
+        d = os.path.join(pkg, sub)
+        for f in sorted(os.listdir(d)):
+            if f.endswith(ext) and os.path.isfile(os.path.join(d, f)):
+                h.update(f"{sub}/{f}\0".encode())
+                h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()
+
+
 def step_roofline(ms_per_step, workload, shape):
     """The step against its own bound: every kernel of the step at its own roofline, back to back —
     sum_k max(FLOP_k / f32 MFMA peak, HBM bytes_k / HBM peak) — over the measured step time.  FLOP_k are
     the MFMA kernels' matrix FLOPs, bytes_k the PMC-measured HBM traffic per step (the committed
-    table, scripts/step_work.py); VALU work (attention, elementwise) is priced by its bytes alone."""
+    table, scripts/step_work.py); VALU work (attention, elementwise) is priced by its bytes alone.  The
+    table is used only when it was measured on these product sources (its digest equals
+    product_digest()): a table from older sources gives {"stale": ...} instead of a fraction."""
     if workload != "qm9_u0" or shape != "S160" or not os.path.exists(STEP_WORK_JSON):
         return None
     tab = json.load(open(STEP_WORK_JSON))
+    src = os.path.relpath(STEP_WORK_JSON, ROOT)
+    if tab["meta"].get("digest") != product_digest():
+        return {"frac": None, "stale": f"{src} was measured on other product sources (commit "
+                                       f"{tab['meta'].get('commit')}): not stated", "source": src}
     rows = []
     for k, v in tab["kernels"].items():
         t_f = v["flops"] / (MFMA_F32_PEAK_TFS * 1e12) * 1e3
@@ -72,7 +95,7 @@ def step_roofline(ms_per_step, workload, shape):
             "kernel_ms_traced": round(sum(r[4] for r in rows), 4),
             "largest_gaps": [{"kernel": r[0], "traced_ms": round(r[4], 4), "bound_ms": round(r[1], 4)}
                              for r in rows[:6]],
-            "source": os.path.relpath(STEP_WORK_JSON, ROOT), "commit": tab["meta"].get("commit")}
+            "source": src, "commit": tab["meta"].get("commit"), "digest": tab["meta"]["digest"][:12]}
 
 
 # probe name -> the kernel (substring of its symbol) whose PMC bytes it is
@@ -447,13 +470,6 @@ def in_step_kernel_ms(runner, batch, name, reps):
     return (ms[len(ms) // 2], len(ms)) if ms else (None, 0)
 
 
-# Core clocks measured under each MFMA kernel's own load (trace builds stamping the shader clock against
-# the 100 MHz wall clock, profiles/r4f_sclk_chain_flat.txt): the f32 MFMA rate they can reach is
-# 157.3 TF/s x sclk / 2.4 GHz
-SCLK_GHZ = {"tiled_wgrad_flat": 1.93, "chain_fwd": 2.08, "chain_bwd": 2.12}
-SCLK_SOURCE = "profiles/r4f_sclk_chain_flat.txt"
-
-
 def _lib_ws(name, *args):
     from x2gnn import _lib
 
@@ -750,9 +766,6 @@ def main():
         f_tfs = flat["flops"] / (f_ms * 1e-3) / 1e12
         p_tfs = flat["flops"] / (flat["ms"] * 1e-3) / 1e12
         traffic = pmc_traffic([("tiled_flat_kernel", None)], traffic_table)  # (the largest launch)
-        # the clock was measured under config 2's S160 launch: the attainable fraction is stated for that
-        # shape only (the S5A / config-3 launches run at their own, unmeasured clocks)
-        sclk = SCLK_GHZ["tiled_wgrad_flat"] if (args.workload, args.shape) == ("qm9_u0", "S160") else None
         roof = {"kernel": f"x2g_tiled_wgrad_flat: {flat['jobs']} weight gradients dW = dz^T x over "
                           f"R={flat['rows']} rows in one launch (tiled_flat_kernel)",
                 "bound": "mfma", "achieved": round(f_tfs, 2), "peak": MFMA_F32_PEAK_TFS,
@@ -762,9 +775,6 @@ def main():
                                                      else "probe"),
                 "probe_ms": round(flat["ms"], 5), "probe_frac": round(p_tfs / MFMA_F32_PEAK_TFS, 4),
                 "flops_per_launch": int(flat["flops"]),
-                "sclk_ghz": sclk, "attainable_peak": round(MFMA_F32_PEAK_TFS * sclk / 2.4, 1) if sclk else None,
-                "frac_of_attainable": round(f_tfs / (MFMA_F32_PEAK_TFS * sclk / 2.4), 4) if sclk else None,
-                "sclk_source": SCLK_SOURCE if sclk else "not measured at this workload / shape",
                 "traffic_source": os.path.relpath(traffic_path, ROOT) if traffic else None}
         dense["tiled_wgrad_flat"] = (f_ms, flat["flops"])
     if not wl["train"]:  # inference: no backward; the T-row attention forward dominates

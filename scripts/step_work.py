@@ -106,7 +106,10 @@ def main():
         b = 2 * 1024 * fetch.get(k, 0.0) / sf + 1024 * write.get(k, 0.0) / sw
         kernels[k] = {"hbm_bytes": int(b), "flops": int(fl.get(k, 0)), "us": round(t_us.get(k, 0.0), 2),
                       "launches": round(t_cnt.get(k, 0), 2)}
+    from bench import product_digest
+
     json.dump({"meta": {"commit": os.environ.get("X2G_COMMIT"),  # the tree measured (.git does not travel to the box)
+                        "digest": product_digest(),  # bench.py states step_roofline only on these sources
                         "shape": {"E": E, "T": T, "N": N, "B": 128}, "steps": {"fetch": sf, "write": sw, "trace": st},
                         "sources": [fetch_d, write_d, trace_d],
                         "note": "HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB) per step; flops = matrix FLOPs per "
