@@ -146,9 +146,10 @@ def parse():
 
 
 # ------------------------------------------------------------------------------------------ kernels
-def attention_probe(model, batch, reps):
+def attention_probe(model, batch, reps, train=True):
     """Time the fused attention kernels of conv layer 0 on this step's real inputs with HIP
-    events on the launch stream; returns {kernel: (avg_ms, algorithmic_bytes_per_launch)}."""
+    events on the launch stream; returns {kernel: (avg_ms, algorithmic_bytes_per_launch)}.  ``train``
+    False: the forward as inference runs it (no logits, no S / P rows stored)."""
     conv = model.fin_model.convs[0]
     line, plan = model.line_graph_data(batch)  # grad mode on: keeps the sbf factors (rbf_env, Y)
     lg = plan.lg
@@ -218,7 +219,9 @@ def attention_probe(model, batch, reps):
 
     sf = center and ops._center_sf_ok(lg, (radial, ylm), D)
 
-    order, packs, units, rows, info = ops._center_units(lg, ops._PACK_FWD) if center else (None, None, 0, 0, None)
+    # the model's units: the leading hub units (atoms beyond the fused forward's LDS image) source-tiled, the rest
+    # untiled (ops._center_split)
+    order, packs, info, launches = ops._center_split(lg) if center else (None, None, None, [])
 
     # as the model: with the fused forward feeding the center backward, P rows [E, 7, D] pass between them
     # instead of S rows [T, D] (ops._CENTER_P)
@@ -226,10 +229,15 @@ def attention_probe(model, batch, reps):
     pbuf = torch.empty(E, 7, D, **f32) if use_p else None
 
     def fwd_sf():  # the model's forward with lin_sbf fused (S rebuilt per workgroup unit; P or S rows stored)
-        call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(src_row),
-             ops.EDGE_PER_DST, ptr(radial), ptr(ylm), ptr(W), ptr(bsb), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
-             ptr(lg.rev_trip), ptr(order), ptr(packs), ptr(info), 0, units, rows, E, T, H, C, ptr(out), ptr(alpha),
-             ptr(smax), ptr(sden), None, None if use_p else ptr(sproj), ptr(pbuf), stream_ptr())
+        common = (ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(src_row), ops.EDGE_PER_DST, ptr(radial), ptr(ylm),
+                  ptr(W), ptr(bsb), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(order), ptr(packs),
+                  ptr(info))
+        if train:
+            outs = (E, T, H, C, ptr(out), ptr(alpha), ptr(smax), ptr(sden), None, None if use_p else ptr(sproj),
+                    ptr(pbuf), stream_ptr())
+        else:  # inference (ops.sbf_attention without attention weights): nothing for a backward
+            outs = (E, T, H, C, ptr(out), None, ptr(smax), ptr(sden), None, None, None, stream_ptr())
+        ops._center_launch(launches, common, outs)
 
     def bwd_center():  # both backward passes in one launch per center atom
         call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(table), ptr(src_row), ops.EDGE_PER_DST,
@@ -269,6 +277,8 @@ def attention_probe(model, batch, reps):
     # written
     sf_bytes = cidx + T * (4 * H + 32) + (E * 7 * row_b if use_p else T * row_b) + E * (5 * row_b + 8 * H + 4 * S) \
         + 4 * D * (S + 1)
+    if not train:  # Y rows in, out / max / den out: no logits, no S or P rows
+        sf_bytes = cidx + T * 32 + E * (5 * row_b + 8 * H + 4 * S) + 4 * D * (S + 1)
     probes = [] if sf else [("sbf_project", proj, proj_bytes, proj_bytes)]
     if sf:
         probes.append(("attn_fwd", fwd_sf, sf_bytes, sf_bytes))
@@ -745,7 +755,7 @@ def main():
 
     meta = batch.host_meta()
     traffic_path, traffic_table = load_traffic(args.workload, args.shape)
-    probe, shape = attention_probe(model, batch, args.kernel_reps)
+    probe, shape = attention_probe(model, batch, args.kernel_reps, train=wl["train"])
     plan_lg = model.line_graph_data(batch)[1].lg
     sa = scatter_add_probe(plan_lg, args.kernel_reps)
     dense = dense_probe(shape["E"], args.kernel_reps)
@@ -781,7 +791,11 @@ def main():
         a_ms, a_bytes, a_gath = probe["attn_fwd"]
         a_gbs = a_bytes / (a_ms * 1e-3) / 1e9
         hbm = _pmc_bytes("attn_fwd", traffic_table)
-        roof = {"kernel": ("x2g_sbf_attention_fwd_center (attn_fwd_center_kernel: one workgroup per center atom, "
+        roof = {"kernel": ("x2g_sbf_attention_fwd_center_sf_tiled + _sf (attn_fwd_center_sf_tiled_kernel / "
+                           "attn_fwd_center_sf_kernel: lin_sbf fused, one workgroup per center atom (sources in tiles "
+                           "of 16 for degrees > 17) or per pack of small atoms; no S = lin_sbf(sbf) exists)"
+                           if shape.get("sf") else
+                           "x2g_sbf_attention_fwd_center (attn_fwd_center_kernel: one workgroup per center atom, "
                            "S = lin_sbf(sbf) precomputed)" if shape.get("center") else
                            "x2g_sbf_attention_fwd (attn_fwd_batched, S = lin_sbf(sbf) precomputed)"),
                 "bound": "hbm", "achieved": round(a_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

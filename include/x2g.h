@@ -296,6 +296,25 @@ int x2g_sbf_attention_fwd_center(const float* q, const float* k, const float* v,
                                  int64_t num_edges, int64_t num_triplets, int32_t heads, int32_t channels, float* out,
                                  float* alpha_raw, float* seg_max, float* seg_den, float* row_stats, void* stream);
 
+/* The center-atom kernels' schedule made on the device, for a batch that does not carry collate's
+ * (data.center_packs; the reference trainer's PyG batch, trainer.py:25-27,37-40): from the atoms' out-edge
+ * row pointer atom_rowptr [N + 1], the molecules' atom row pointer mol_ptr [B + 1] (atoms of molecule m:
+ * mol_ptr[m] .. mol_ptr[m + 1] - 1, covering 0 .. N - 1) and src_row [E] (or NULL), writes
+ *   center_order [N]: every atom by decreasing degree (the center backward's workgroups);
+ *   pack_order [N], pack_ptr [N + 1], atom_info [N, 4] (16-byte aligned): the fused forward's units, per
+ *   molecule its atoms by decreasing degree packed best-fit into units of <= 16 rows and <= 16 atoms (an atom
+ *   of degree >= 16 alone; one atom per unit in a molecule of more than 64 atoms), unit slots = the
+ *   molecule's atom slots, unused slots empty (pack_ptr[s] == pack_ptr[s + 1]): launch the fused forwards over
+ *   all N units (x2g_sbf_attention_fwd_center_sf with max_rows 17 leaves out the units of more rows,
+ *   x2g_sbf_attention_fwd_center_sf_tiled with skip_rows 17 takes exactly those).
+ * workspace: x2g_center_schedule_workspace() bytes.  Two launches and a memset on the stream, no host read.
+ * The order among atoms of equal degree follows integer atomics; no output of the center kernels depends on
+ * it. */
+size_t x2g_center_schedule_workspace(void);
+int x2g_center_schedule(const int32_t* atom_rowptr, const int32_t* mol_ptr, const int32_t* src_row,
+                        int64_t num_atoms, int64_t num_graphs, int32_t* center_order, int32_t* pack_order,
+                        int32_t* pack_ptr, int32_t* atom_info, void* workspace, size_t ws_bytes, void* stream);
+
 /* Workgroup UNITS of the fused-projection center forward below: with pack_ptr (int32 [units + 1], or NULL)
  * unit u is the PACK of center atoms atom_order[pack_ptr[u]] .. atom_order[pack_ptr[u + 1] - 1] (at most
  * 32 atoms; every atom of the batch in exactly one pack, atoms without edges included), processed side by
@@ -328,6 +347,29 @@ int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, const float*
                                     int32_t heads, int32_t channels, float* out, float* alpha_raw, float* seg_max,
                                     float* seg_den, float* row_stats, float* sbfproj_out, float* sbf_p_out,
                                     void* stream);
+
+/* The fused-projection center forward for atoms whose block exceeds that LDS image (config 5's AID atoms:
+ * degrees up to 61; replaces the S = lin_sbf(sbf) projection + S-reading forward those took; reference
+ * sbftransformer_conv.py:138-162, angular_basis_layer.py:86-93): one workgroup per unit, each unit a SINGLE
+ * atom (atom_order[pack_ptr[u]], or atom_order[u] / u as above; atom_info as above), its sources staged 16 at
+ * a time (k + e, v + e, radial rows, P rows in LDS: x2g_sbf_attention_fwd_center_sf_tiled_lds() bytes), the
+ * 16 owners' destination rows d = owner + 16 r carrying their online-softmax state across the tiles; sources
+ * in the same order, batches of 4 (equal to the untiled form to fp32 rounding).  max_degree >= every unit's
+ * degree, <= X2G_CENTER_MAX_DEGREE.  skip_rows >= 0: units whose (first) atom has at most that many rows are
+ * left to the untiled form (a list made by x2g_center_schedule mixes both kinds; x2gnn passes 17, the untiled
+ * form's max_rows, which in turn leaves out every unit of more rows than its max_rows).  Outputs,
+ * sbfproj_out / sbf_p_out and alpha_raw as the untiled form. */
+size_t x2g_sbf_attention_fwd_center_sf_tiled_lds(void);
+int x2g_sbf_attention_fwd_center_sf_tiled(const float* q, const float* k, const float* v, const float* skip,
+                                          const float* edge, const int32_t* src_row, int edge_mode,
+                                          const float* radial, const float* sph_y, const float* w_sbf,
+                                          const float* b_sbf, const int32_t* atom_rowptr, const int32_t* edge_rev,
+                                          const int32_t* rev_trip, const int32_t* atom_order,
+                                          const int32_t* pack_ptr, const int32_t* atom_info, int64_t unit0,
+                                          int64_t n_units, int32_t max_degree, int32_t skip_rows, int64_t num_edges,
+                                          int64_t num_triplets, int32_t heads, int32_t channels, float* out,
+                                          float* alpha_raw, float* seg_max, float* seg_den, float* row_stats,
+                                          float* sbfproj_out, float* sbf_p_out, void* stream);
 
 /* The whole attention backward over a SYMMETRIC line graph in ONE launch, one workgroup per center atom
  * (csrc/attention_center.hip): the block's rows (k + e of its sources, dout and q of its destinations,

@@ -2,12 +2,13 @@
 CPU oracle on the same seeded inputs (integer work bit-exact, float work within stated
 tolerances)."""
 import math
+import os
 
 import numpy as np
 import pytest
 import torch
 
-from conftest import golden
+from conftest import GOLDEN, golden
 from helpers import rel_err
 
 from oracle import ref_cpu, triplets
@@ -2285,3 +2286,161 @@ def test_center_backward_from_p_rows_equals_s_rows(cuda):
         for a, r in zip(*outs):
             assert not torch.isnan(a).any()
             assert torch.equal(a, r)
+
+
+@pytest.mark.parametrize("graph", ["aid", "hub100"])
+def test_center_fused_source_tiles_equal_projected(cuda, graph):
+    """x2g_sbf_attention_fwd_center_sf_tiled (atoms beyond the fused forward's LDS image: sources staged 16 at
+    a time, each owner's destinations carrying their online-softmax state across the tiles) == projection +
+    the S-reading center forward on AID_kcal molecules (config 5's geometry: degrees up to ~50, RMAX 4) and on
+    a graph with a degree-100 hub (RMAX 8), degree-1 and isolated atoms: outputs, logits, softmax and row
+    statistics, the S rows and P rows it stores; the model's split launch (the leading hub units tiled, the
+    packed rest untiled: data.center_hubs) gives the same outputs as all atoms tiled."""
+    from x2gnn import ops
+    from x2gnn._lib import call, ptr, stream_ptr
+    from x2gnn.data import center_hubs
+    from x2gnn.synth import molecules_from_geometry_file
+
+    if graph == "aid":
+        from x2gnn.data import collate
+
+        b = collate(molecules_from_geometry_file(os.path.join(GOLDEN, "aid_geom.npz"), indices=[0, 5, 9], seed=0))
+        ei, n = b.edge_index.numpy(), b.num_nodes
+    else:
+        pairs = [(0, 1), (1, 2)] + [(4, 5 + i) for i in range(100)] + [(110, 111), (111, 112), (110, 112)] + \
+            [(5 + i, 6 + i) for i in range(30)]
+        ed = sorted({(a, c) for a, c in pairs} | {(c, a) for a, c in pairs})
+        ei, n = np.array(ed, dtype=np.int64).T, 114  # atoms 3 and 113 have no edges
+    lg = _sym_lg(ei, n, cuda)
+    deg = np.bincount(ei[0], minlength=n)
+    assert lg.max_degree > 33
+    E, T, H, C, D = lg.E, lg.T, 16, 8, 128
+    g = torch.Generator(device=cuda).manual_seed(18)
+    q, k, v, skip = (torch.randn(E, D, device=cuda, generator=g) for _ in range(4))
+    table = torch.randn(10, D, device=cuda, generator=g)
+    radial = torch.randn(E, 42, device=cuda, generator=g)
+    y = torch.randn(T, 8, device=cuda, generator=g)
+    y[:, 7] = 1.0
+    sbf = (radial[lg.trip_src.long()].view(T, 7, 6) * y[:, :7, None]).reshape(T, 42).contiguous()
+    W = 0.2 * torch.randn(D, 42, device=cuda, generator=g)
+    bias = 0.1 * torch.randn(D, device=cuda, generator=g)
+    f = dict(device=cuda, dtype=torch.float32)
+    S = torch.empty(T, D, **f)
+    call("x2g_sbf_project", ptr(sbf), T, 42, ptr(W), ptr(bias), D, ptr(S), stream_ptr())
+    ref = [torch.empty(E, D, **f), torch.empty(T, H, **f), torch.empty(E, H, **f), torch.empty(E, H, **f),
+           torch.empty(E, 2, **f)]
+    call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
+         ops.EDGE_PER_DST, ptr(S), 0, ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), None, 0,
+         lg.N, lg.max_degree, E, T, H, C, *[ptr(t) for t in ref], stream_ptr())
+    ref_p = torch.einsum("clk,elk->elc", W.view(D, 7, 6), radial.view(E, 7, 6))
+    po, pp, pr = lg.packed
+    hubs, rows = center_hubs(deg, po.cpu().numpy(), pp.cpu().numpy())
+    assert 0 < hubs < int(pp.shape[0]) - 1 and rows <= 17
+    info = _pack_info(lg, po)
+    runs = []
+    for split in (False, True):
+        got = [torch.full_like(t, float("nan")) for t in ref]
+        S2 = torch.full((T, D), float("nan"), **f)
+        P2 = torch.full((E, 7, D), float("nan"), **f)
+        common = (ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type), ops.EDGE_PER_DST, ptr(radial),
+                  ptr(y), ptr(W), ptr(bias), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip))
+        outs = (E, T, H, C, *[ptr(t) for t in got], ptr(S2), ptr(P2), stream_ptr())
+        if split:  # the model's launches
+            call("x2g_sbf_attention_fwd_center_sf_tiled", *common, ptr(po), ptr(pp), ptr(info), 0, hubs,
+                 lg.max_degree, 0, *outs)
+            call("x2g_sbf_attention_fwd_center_sf", *common, ptr(po), ptr(pp), ptr(info), hubs,
+                 int(pp.shape[0]) - 1 - hubs, rows, *outs)
+        else:  # every atom tiled, by decreasing degree, row ranges derived
+            call("x2g_sbf_attention_fwd_center_sf_tiled", *common, ptr(lg.center_order), None, None, 0, lg.N,
+                 lg.max_degree, 0, *outs)
+        for name, a, r in zip(("out", "alpha", "smax", "sden", "row_stats"), got, ref):
+            assert not torch.isnan(a).any(), name
+            torch.testing.assert_close(a, r, rtol=1e-5, atol=1e-5, msg=name)
+        torch.testing.assert_close(S2, S, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(P2, ref_p, rtol=1e-5, atol=1e-5)
+        runs.append(got)
+    for a, r in zip(*runs):  # the hubs are computed by the same kernel either way; the rest to fp32 rounding
+        torch.testing.assert_close(a, r, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("graph", ["s160", "aid"])
+def test_device_center_schedule(cuda, graph):
+    """x2g_center_schedule (the center kernels' schedule made on the device, for batches without collate's):
+    center_order is a permutation by non-increasing degree; every atom sits in exactly one unit, a unit of
+    several atoms holds <= 16 rows and <= 16 atoms, units stay inside their molecule's slots; atom_info
+    matches the line graph; and the fused forward over it (both forms over all unit slots, each leaving out
+    the other's units) equals the forward over collate's host schedule bit for bit."""
+    from x2gnn import ops
+    from x2gnn._lib import call, ptr, stream_ptr
+    from x2gnn.data import center_hubs, collate
+    from x2gnn.synth import molecules_from_geometry_file, synthetic_molecules
+
+    if graph == "s160":
+        b = collate(synthetic_molecules(128, "S160", seed=21))
+    else:  # degrees up to ~50; a molecule of > 64 atoms takes the one-atom-per-unit layout
+        b = collate(molecules_from_geometry_file(os.path.join(GOLDEN, "aid_geom.npz"), indices=[0, 5, 9, 30], seed=0))
+    ei, n, B = b.edge_index.numpy(), b.num_nodes, b.num_graphs
+    lg = _sym_lg(ei, n, cuda)
+    deg = np.bincount(ei[0], minlength=n)
+    mol_ptr = torch.from_numpy(np.concatenate([[0], np.cumsum(b._meta["nodes"])]).astype(np.int32)).to(cuda)
+    i32 = dict(dtype=torch.int32, device=cuda)
+    c_order, p_order, p_ptr = torch.full((n,), -1, **i32), torch.full((n,), -1, **i32), torch.full((n + 1,), -1, **i32)
+    info = torch.full((4 * n,), -1, **i32)
+    ws_b = int(_lib_mod().x2g_center_schedule_workspace())
+    ws = torch.empty(ws_b, dtype=torch.uint8, device=cuda)
+    call("x2g_center_schedule", ptr(lg.atom_rowptr), ptr(mol_ptr), ptr(lg.src_type), n, B, ptr(c_order), ptr(p_order),
+         ptr(p_ptr), ptr(info), ptr(ws), ws_b, stream_ptr())
+    co, po, pp = c_order.cpu().numpy(), p_order.cpu().numpy(), p_ptr.cpu().numpy()
+    assert np.array_equal(np.sort(co), np.arange(n)) and (np.diff(deg[co]) <= 0).all()
+    assert np.array_equal(np.sort(po), np.arange(n)) and pp[0] == 0 and pp[n] == n and (np.diff(pp) >= 0).all()
+    mp = mol_ptr.cpu().numpy()
+    for m in range(B):
+        for s in range(mp[m], mp[m + 1]):
+            mem = po[pp[s]:pp[s + 1]]
+            assert ((mem >= mp[m]) & (mem < mp[m + 1])).all()
+            if len(mem) > 1:
+                assert deg[mem].sum() <= 16 and len(mem) <= 16
+    inf = info.cpu().numpy().reshape(n, 4)
+    rp = lg.atom_rowptr.cpu().numpy()
+    st = lg.src_type.cpu().numpy()
+    assert np.array_equal(inf[:, 0], po) and np.array_equal(inf[:, 1], rp[po]) and np.array_equal(inf[:, 2], deg[po])
+    assert np.array_equal(inf[:, 3], np.where(deg[po] > 0, st[np.minimum(rp[po], len(st) - 1)], 0))
+    # the fused forward over the device schedule == over the host schedule
+    E, T, H, C, D = lg.E, lg.T, 16, 8, 128
+    g = torch.Generator(device=cuda).manual_seed(22)
+    q, k, v, skip = (torch.randn(E, D, device=cuda, generator=g) for _ in range(4))
+    table = torch.randn(10, D, device=cuda, generator=g)
+    radial = torch.randn(E, 42, device=cuda, generator=g)
+    y = torch.randn(T, 8, device=cuda, generator=g)
+    y[:, 7] = 1.0
+    W = 0.2 * torch.randn(D, 42, device=cuda, generator=g)
+    bias = 0.1 * torch.randn(D, device=cuda, generator=g)
+    f = dict(device=cuda, dtype=torch.float32)
+    hpo, hpp, _ = lg.packed
+    hubs, rows = center_hubs(deg, hpo.cpu().numpy(), hpp.cpu().numpy())
+    runs = []
+    for device_sched in (False, True):
+        got = [torch.full((E, D), float("nan"), **f), torch.full((T, H), float("nan"), **f),
+               torch.full((E, H), float("nan"), **f), torch.full((E, H), float("nan"), **f),
+               torch.full((E, 2), float("nan"), **f), torch.full((E, 7, D), float("nan"), **f)]
+        lg.pack_order, lg.center_packs = (p_order, p_ptr) if device_sched else (hpo, hpp)
+        lg.pack_info = info if device_sched else _pack_info(lg, hpo)
+        lg.center_rows = 17 if device_sched else rows
+        lg.center_hubs, lg.center_mixed = (0, True) if device_sched else (hubs, False)
+        order, packs, inf_t, launches = ops._center_split(lg)
+        common = (ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type), ops.EDGE_PER_DST, ptr(radial),
+                  ptr(y), ptr(W), ptr(bias), ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(order),
+                  ptr(packs), ptr(inf_t))
+        ops._center_launch(launches, common, (E, T, H, C, *[ptr(t) for t in got[:5]], None, ptr(got[5]),
+                                              stream_ptr()))
+        for t in got:
+            assert not torch.isnan(t).any()
+        runs.append(got)
+    for a, r in zip(*runs):
+        assert torch.equal(a, r)
+
+
+def _lib_mod():
+    from x2gnn import _lib
+
+    return _lib.load()

@@ -33,15 +33,16 @@ def grad_scale(z, names):
 
 def record_calls(monkeypatch):
     """Every C-ABI entry the host layer calls from here on: [(name, args)] (ops.call wrapped)."""
-    from x2gnn import ops
+    from x2gnn import _lib, ops
 
-    seen, inner = [], ops.call
+    seen, inner = [], _lib.call
 
     def rec(name, *args):
         seen.append((name, args))
         return inner(name, *args)
 
     monkeypatch.setattr(ops, "call", rec)
+    monkeypatch.setattr(_lib, "call", rec)  # (modules that import it at call time: data._meta_on_device)
     return seen
 
 
@@ -92,14 +93,13 @@ def test_model_energies_and_gradients_vs_reference(cuda, monkeypatch, fixture, p
     wide = model_cfg(z)["in_channels"] == 128
     if path == "shipped" and wide:
         layers = model_cfg(z)["conv_layers"]
+        # the fused-projection forward with pack_ptr and atom_info handed over, plus its source-tiled form for
+        # the atoms of more than 17 rows (model_aid: degree 35); no S projection, no S-reading forward
         fwd = [(n, a) for n, a in seen if n.startswith("x2g_sbf_attention_fwd_center")]
-        assert len(fwd) == layers
-        # the fused-projection form with pack_ptr and atom_info handed over (or, for atoms whose LDS image
-        # does not fit it, the S-reading center forward)
-        assert all(a[15] and a[16] for n, a in fwd if n == "x2g_sbf_attention_fwd_center_sf")
-        if max_degree(z) <= 33:
-            assert all(n == "x2g_sbf_attention_fwd_center_sf" for n, _ in fwd)
-            assert "x2g_sbf_project" not in names
+        assert names.count("x2g_sbf_attention_fwd_center_sf") == layers
+        assert names.count("x2g_sbf_attention_fwd_center_sf_tiled") == (layers if max_degree(z) > 17 else 0)
+        assert all(a[15] and a[16] for _, a in fwd)
+        assert "x2g_sbf_project" not in names and "x2g_sbf_attention_fwd_center" not in names
         assert names.count("x2g_sbf_attention_bwd_center") == layers
         assert "x2g_sbf_attention_bwd_dst_g" not in names
     else:
@@ -457,11 +457,12 @@ def test_config3_molwise_add_batch256_vs_oracle(cuda):
         assert err <= 2e-3 * float(g_ref.abs().max()) + 1e-6 * scale, (n, err)
 
 
-def test_config5_aid_batch64_inference(cuda):
+def test_config5_aid_batch64_inference(cuda, monkeypatch):
     """Config 5 shape: 64 AID_kcal molecules (~83 atoms, T ~3.4M triplets) at full width,
     inference: finite energies, per-molecule energies invariant to batch composition, and eight
     molecules spread over the batch's triplet-count range (the smallest to the largest) against the
-    oracle, each within 1e-4 relative — the whole-batch (tiled) result itself, not a re-run."""
+    oracle, each within 1e-4 relative — the whole-batch result itself, not a re-run.  The attention runs
+    fused (the atoms of degree > 17, up to 61, in source tiles): no S = lin_sbf(sbf) is projected."""
     import os
 
     import x2gnn
@@ -477,9 +478,12 @@ def test_config5_aid_batch64_inference(cuda):
     m = x2gnn.xgnn_poly(device="cuda", **cfg)
     load_seeded(m, 79)
     m = m.to(cuda).eval()
+    seen = record_calls(monkeypatch)
     with torch.no_grad():
         res = m(b.to(cuda)).cpu().numpy()
         assert np.isfinite(res).all() and res.shape == (64,)
+        names = [n for n, _ in seen]
+        assert names.count("x2g_sbf_attention_fwd_center_sf_tiled") == 4 and "x2g_sbf_project" not in names
         order = np.argsort(b._meta["triplets"])
         pick = order[np.linspace(0, 63, 8).round().astype(int)]
         sub = [mols[i] for i in pick]
@@ -783,10 +787,13 @@ def test_foreign_pyg_style_batch_vs_reference(cuda, monkeypatch, fixture):
     seen = record_calls(monkeypatch)
     res = m(fb)
     assert check_vs_fixture(m, z, res, fb.y) >= 5
-    if model_cfg(z)["in_channels"] == 128:
+    if model_cfg(z)["in_channels"] == 128:  # the device-made schedule (x2g_center_schedule) drives the center kernels
         names = [n for n, _ in seen]
-        assert sum(n.startswith("x2g_sbf_attention_fwd_center") for n in names) == model_cfg(z)["conv_layers"]
-        assert names.count("x2g_sbf_attention_bwd_center") == model_cfg(z)["conv_layers"]
+        layers = model_cfg(z)["conv_layers"]
+        assert names.count("x2g_center_schedule") == 1
+        assert names.count("x2g_sbf_attention_fwd_center_sf") == layers
+        assert names.count("x2g_sbf_attention_fwd_center_sf_tiled") == (layers if max_degree(z) > 17 else 0)
+        assert names.count("x2g_sbf_attention_bwd_center") == layers and "x2g_sbf_project" not in names
 
 
 def test_foreign_batch_meta_on_device_and_forward_time(cuda):

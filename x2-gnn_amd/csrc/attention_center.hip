@@ -97,11 +97,14 @@ __device__ __forceinline__ UnitRows unit_rows_carve(int* p, int max_rows) {
 // With info (int32 [.., 4] per atom in the order's positions: atom, first out-edge, degree, edge-table
 // row; the host's, data.center_packs) a member's row range is one load instead of three dependent ones
 // (order -> rowptr -> src_row).
+// A unit of more than max_rows rows (a device-made schedule lists the atoms beyond the LDS image among the
+// packs: x2g_sbf_attention_fwd_center_sf_tiled takes them) writes no table entry and reports 0 rows, so
+// the workgroup leaves.
 __device__ __forceinline__ void unit_rows_build(const UnitRows& u, const int32_t* __restrict__ order,
                                                 const int32_t* __restrict__ packs, int64_t unit,
                                                 const int32_t* __restrict__ rowptr,
                                                 const int32_t* __restrict__ src_row,
-                                                const int4* __restrict__ info) {
+                                                const int4* __restrict__ info, int max_rows) {
   if (threadIdx.x >= 64) return;
   const int lane = threadIdx.x;
   int64_t m0 = unit, m1 = unit + 1;
@@ -134,6 +137,14 @@ __device__ __forceinline__ void unit_rows_build(const UnitRows& u, const int32_t
     if (lane >= o) inc += v;
   }
   const int base = inc - n;
+  const int total = __shfl(inc, 63);
+  if (total > max_rows) {  // (wave-uniform)
+    if (lane == 63) {
+      u.NRS[0] = 0;
+      u.NRS[1] = 0;
+    }
+    return;
+  }
   if (lane < M) {
     u.MA[lane] = b;
     u.MI[lane] = base | n << 16;
@@ -292,6 +303,7 @@ struct FwdSfArgs {
   const int4* info;      // per order position: atom, first out-edge, degree, edge-table row (NULL: derived)
   int64_t atom0, n_atoms;  // units atom0 .. atom0 + n_atoms - 1
   int max_rows;            // rows of the largest unit (the LDS image is sized for it)
+  int skip_rows;           // source-tiled form: units whose (first) atom has at most this many rows are left out
   int H;
   float sqrt_c;
   float *out, *alpha, *smax, *sden, *sp;  // sp: S [T, 128] out (NULL: not stored)
@@ -306,7 +318,8 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_fwd_center_sf_kernel(const
   extern __shared__ cf4 lds[];
   const UnitRows u = unit_rows_carve(reinterpret_cast<int*>(lds), a.max_rows);
   // (the host orders the units by decreasing work: the longest start first, the short ones fill the tail)
-  unit_rows_build(u, a.order, a.packs, a.atom0 + blockIdx.x, a.atom_rowptr, EDGE ? a.src_row : nullptr, a.info);
+  unit_rows_build(u, a.order, a.packs, a.atom0 + blockIdx.x, a.atom_rowptr, EDGE ? a.src_row : nullptr, a.info,
+                  a.max_rows);
   __syncthreads();
   const int n_rows = uniform(u.NRS[0]);
   if (n_rows <= 0) return;  // (workgroup-uniform)
@@ -504,6 +517,224 @@ int fwd_sf_launch(const FwdSfArgs& a, bool edge, hipStream_t st) {
     return last_launch_status();
   };
   return edge ? go(attn_fwd_center_sf_kernel<LPH, W, B, true>) : go(attn_fwd_center_sf_kernel<LPH, W, B, false>);
+}
+
+// ------------------------------------------------------------------------------ forward, fused, source tiles
+// Center atoms whose block does not fit the fused forward's LDS image (4.7 KB per source row: degree > 17 at
+// two workgroups per CU; config 5's AID atoms have median degree 24 and reach 61): the same forward with the
+// atom's SOURCES staged kTileRows at a time.  One workgroup per atom; its 16 half-wave owners take the
+// destination rows g = owner + 16 r (r < RMAX), whose online-softmax state (acc, max, den) lives in registers
+// across the tiles; per tile the sources' k + e, v + e, radial rows and P rows are formed in LDS exactly as the
+// untiled kernel forms them, and every owner runs its destinations' batches over the tile's sources, in the
+// untiled kernel's order of sources; batches of 4 sources per memory round trip (the state of RMAX
+// destinations takes the registers the untiled kernel's batches of 8 use), so the online softmax rescales
+// at other points: equal to fp32 rounding.
+constexpr int kTileRows = 16;
+
+template <int LPH, int WAVES, int B, bool EDGE, int RMAX>
+__global__ void __launch_bounds__(64 * WAVES, 4) attn_fwd_center_sf_tiled_kernel(const FwdSfArgs a) {
+  static_assert(kTileRows % B == 0, "batches never cross a tile");
+  extern __shared__ cf4 lds[];  // [TS][32] (k + e), [TS][32] (v + e), [TS][7][32] P, [TS][42] R
+  constexpr int TS = kTileRows, NT = 64 * WAVES, NO = 2 * WAVES;
+  cf4* KE = lds;
+  cf4* VE = KE + TS * 32;
+  cf4* P = VE + TS * 32;
+  float* RS = reinterpret_cast<float*>(P + TS * kSfL * 32);
+  // the unit: one atom (the host routes the units of more than max_rows rows here, each a single atom)
+  const int64_t unit = a.atom0 + blockIdx.x;
+  int64_t pos = unit;
+  if (a.packs) {
+    pos = a.packs[unit];
+    if (a.packs[unit + 1] <= pos) return;  // an empty unit slot (x2g_center_schedule's layout)
+  }
+  int r0, n, er = 0;
+  if (a.info) {
+    const int4 v = a.info[pos];
+    r0 = uniform(v.y);
+    n = uniform(v.z);
+    if (EDGE) er = uniform(v.w);
+  } else {
+    const int b = a.order ? a.order[pos] : static_cast<int>(pos);
+    r0 = uniform(a.atom_rowptr[b]);
+    n = uniform(a.atom_rowptr[b + 1]) - r0;
+    if (EDGE && n > 0) er = uniform(a.src_row[r0]);
+  }
+  // (workgroup-uniform; skip_rows: a device-made schedule's list mixes the packs of small atoms, which the
+  // untiled form takes, with the single atoms beyond its LDS image)
+  if (n <= 0 || n <= a.skip_rows) return;
+  const int tid = threadIdx.x;
+  const int l32 = tid & 31, half = (tid >> 5) & 1, wave = tid >> 6;
+  const int owner = 2 * wave + half;
+  const int head = l32 / LPH;
+  const bool leader = (l32 % LPH) == 0;
+  const int c0 = 4 * l32;
+  const int nt = n - 1;
+  // (the destinations' ids and triplet blocks are re-read per tile, L2 hits: registers go to the state)
+  cf4 acc[RMAX];
+  float m[RMAX], den[RMAX];
+#pragma unroll
+  for (int r = 0; r < RMAX; ++r) {
+    acc[r] = cf4{0.f, 0.f, 0.f, 0.f};
+    m[r] = -INFINITY;
+    den[r] = 0.f;
+  }
+  const cf4 bias4 = ld4(a.bias + c0);
+  constexpr int NG = NT / 256;  // P thread groups of 7 x 32 (as the untiled kernel)
+  const int pg = tid / 256, prest = tid % 256;
+  const bool pthr = prest < kSfL * 32;
+  const int pl = pthr ? prest >> 5 : 0, pc4 = prest & 31;
+  for (int t0 = 0; t0 < n; t0 += TS) {
+    const int ts = n - t0 < TS ? n - t0 : TS;
+    __syncthreads();  // the previous tile's rows are no longer read
+    const cf4 e4 = EDGE ? ld4(a.edge + static_cast<int64_t>(er) * kCD + 4 * (tid & 31)) : cf4{0.f, 0.f, 0.f, 0.f};
+    for (int idx = tid; idx < ts * 32; idx += NT) {
+      const int64_t row = static_cast<int64_t>(r0 + t0 + (idx >> 5)) * kCD + 4 * (idx & 31);
+      KE[idx] = ld4(a.k + row) + e4;
+      VE[idx] = ld4(a.v + row) + e4;
+    }
+    for (int idx = tid; idx < ts * kSfK; idx += NT) RS[idx] = a.radial[static_cast<int64_t>(r0 + t0) * kSfK + idx];
+    float wv[4][kSfR];
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+      for (int r = 0; r < kSfR; ++r) wv[cc][r] = a.w[(4 * pc4 + cc) * kSfK + kSfR * pl + r];
+    __syncthreads();
+    if (pthr) {
+      for (int j = pg; j < ts; j += NG) {
+        const float* rr = RS + j * kSfK + kSfR * pl;
+        float rv[kSfR];
+#pragma unroll
+        for (int r = 0; r < kSfR; ++r) rv[r] = rr[r];
+        cf4 p;
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+          float s = wv[cc][0] * rv[0];
+#pragma unroll
+          for (int r = 1; r < kSfR; ++r) s = fmaf(wv[cc][r], rv[r], s);
+          p[cc] = s;
+        }
+        P[(j * kSfL + pl) * 32 + pc4] = p;
+        // P rows out for the backward (each source row is in exactly one tile)
+        if (a.pp) st4(a.pp + (static_cast<int64_t>(r0 + t0 + j) * kSfL + pl) * kCD + 4 * pc4, p);
+      }
+    }
+    __syncthreads();
+    const int t1 = t0 + ts;
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) {
+      const int i = owner + NO * r;  // this destination's row in the block
+      if (i >= n) continue;          // (per owner)
+      const int dd = a.edge_rev[r0 + i], tb = a.rev_trip[r0 + i];
+      const cf4 qv = ld4(a.q + static_cast<int64_t>(dd) * kCD + c0);
+      auto batch = [&](int j0, auto bb) {
+        constexpr int BB = decltype(bb)::value;
+        float yv[BB];
+        int tt[BB];
+#pragma unroll
+        for (int uu = 0; uu < BB; ++uu) {
+          const int j = j0 + uu;
+          int jj = j - (j > i ? 1 : 0);
+          jj = jj < nt ? jj : nt - 1;  // clamped: every load unconditional
+          tt[uu] = tb + jj;
+          yv[uu] = a.y[static_cast<int64_t>(tt[uu]) * 8 + (l32 & 7)];
+        }
+        cf4 sv[BB];
+        float lg[BB];
+        float mb = -INFINITY;
+#pragma unroll
+        for (int uu = 0; uu < BB; ++uu) {
+          const int j = j0 + uu;
+          const bool ok = j < n && j != i;
+          const int jr = (j < t1 ? j : t1 - 1) - t0;  // the source's row in the tile
+          float yl[kSfL];
+          yl[0] = dpp_mov<0x150>(yv[uu]);
+          yl[1] = dpp_mov<0x151>(yv[uu]);
+          yl[2] = dpp_mov<0x152>(yv[uu]);
+          yl[3] = dpp_mov<0x153>(yv[uu]);
+          yl[4] = dpp_mov<0x154>(yv[uu]);
+          yl[5] = dpp_mov<0x155>(yv[uu]);
+          yl[6] = dpp_mov<0x156>(yv[uu]);
+          cf4 s4 = bias4;
+#pragma unroll
+          for (int l = 0; l < kSfL; ++l) s4 += yl[l] * P[(jr * kSfL + l) * 32 + l32];
+          sv[uu] = s4;
+          if (a.sp && ok) st4(a.sp + static_cast<int64_t>(tt[uu]) * kCD + c0, s4);
+          const cf4 kr = KE[jr * 32 + l32];
+          float dot = qv[0] * kr[0];
+          dot = fmaf(qv[1], kr[1], dot);
+          dot = fmaf(qv[2], kr[2], dot);
+          dot = fmaf(qv[3], kr[3], dot);
+          const float logit = head_sum<LPH>(dot) / a.sqrt_c;
+          lg[uu] = ok ? logit : -INFINITY;
+          mb = fmaxf(mb, lg[uu]);
+          if (a.alpha && ok && leader) a.alpha[static_cast<int64_t>(tt[uu]) * a.H + head] = logit;
+        }
+        const float m_new = fmaxf(m[r], mb);
+        const float corr = m_new == -INFINITY ? 1.f : expf(m[r] - m_new);
+        den[r] *= corr;
+        acc[r] *= corr;
+#pragma unroll
+        for (int uu = 0; uu < BB; ++uu) {
+          const int j = j0 + uu;
+          const float p = lg[uu] == -INFINITY ? 0.f : expf(lg[uu] - m_new);
+          const cf4 vr = VE[((j < t1 ? j : t1 - 1) - t0) * 32 + l32];
+          den[r] += p;
+          acc[r] += p * (vr * sv[uu]);
+        }
+        m[r] = m_new;
+      };
+      if (nt > 0) {  // (n = 1: an empty softmax, out = skip)
+        int j0 = t0;
+        for (; j0 < t1 && n - j0 > B / 2; j0 += B) batch(j0, std::integral_constant<int, B>{});
+        if (j0 < t1) batch(j0, std::integral_constant<int, B / 2>{});
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RMAX; ++r) {
+    if (owner + NO * r >= n) continue;
+    const int dd = a.edge_rev[r0 + owner + NO * r];
+    const int64_t drow = static_cast<int64_t>(dd) * kCD + c0;
+    const float inv = 1.0f / (den[r] + kCEps);
+    const cf4 o = acc[r] * inv + ld4(a.skip + drow);
+    st4(a.out + drow, o);
+    if (a.row_stats) {
+      const float mu = half_sum(o[0] + o[1] + o[2] + o[3], half) / static_cast<float>(kCD);
+      const cf4 dv = o - mu;
+      const float q2 = half_sum(dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2] + dv[3] * dv[3], half);
+      if (l32 == 0) a.row_stats[dd] = make_float2(mu, q2);
+    }
+    if (leader) {
+      a.smax[static_cast<int64_t>(dd) * a.H + head] = m[r];
+      a.sden[static_cast<int64_t>(dd) * a.H + head] = den[r];
+    }
+  }
+}
+
+constexpr size_t fwd_sf_tiled_lds() { return static_cast<size_t>(kTileRows) * ((2 + kSfL) * kCD + kSfK) * 4; }
+
+template <int LPH>
+int fwd_sf_tiled_launch(const FwdSfArgs& a, bool edge, int max_degree, hipStream_t st) {
+  // batches of 4 sources: with 8 the RMAX destinations' state spills (4-6 VGPRs at RMAX 2, 15-17 at 4)
+  constexpr int W = 8, B = 4;
+  const size_t lds = fwd_sf_tiled_lds();
+  const unsigned grid = static_cast<unsigned>(a.n_atoms);
+  auto go = [&](auto kern) -> int {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    if (e != hipSuccess) return static_cast<int>(e);
+    kern<<<grid, 64 * W, lds, st>>>(a);
+    return last_launch_status();
+  };
+  constexpr int NO = 2 * W;
+  if (max_degree <= 2 * NO)
+    return edge ? go(attn_fwd_center_sf_tiled_kernel<LPH, W, B, true, 2>)
+                : go(attn_fwd_center_sf_tiled_kernel<LPH, W, B, false, 2>);
+  if (max_degree <= 4 * NO)
+    return edge ? go(attn_fwd_center_sf_tiled_kernel<LPH, W, B, true, 4>)
+                : go(attn_fwd_center_sf_tiled_kernel<LPH, W, B, false, 4>);
+  return edge ? go(attn_fwd_center_sf_tiled_kernel<LPH, W, B, true, 8>)
+              : go(attn_fwd_center_sf_tiled_kernel<LPH, W, B, false, 8>);
 }
 
 template <int LPH>
@@ -994,6 +1225,56 @@ X2G_API int x2g_sbf_attention_fwd_center_sf(const float* q, const float* k, cons
     case 2: return fwd_sf_launch<2>(a, edge_on, st);
     case 4: return fwd_sf_launch<4>(a, edge_on, st);
     case 8: return fwd_sf_launch<8>(a, edge_on, st);
+    default: return X2G_EUNSUPPORTED;
+  }
+}
+
+X2G_API size_t x2g_sbf_attention_fwd_center_sf_tiled_lds(void) { return fwd_sf_tiled_lds(); }
+
+X2G_API int x2g_sbf_attention_fwd_center_sf_tiled(const float* q, const float* k, const float* v, const float* skip,
+                                                  const float* edge, const int32_t* src_row, int edge_mode,
+                                                  const float* radial, const float* sph_y, const float* w_sbf,
+                                                  const float* b_sbf, const int32_t* atom_rowptr,
+                                                  const int32_t* edge_rev, const int32_t* rev_trip,
+                                                  const int32_t* atom_order, const int32_t* pack_ptr,
+                                                  const int32_t* atom_info, int64_t unit0, int64_t n_units,
+                                                  int32_t max_degree, int32_t skip_rows, int64_t num_edges,
+                                                  int64_t num_triplets,
+                                                  int32_t heads, int32_t channels, float* out, float* alpha_raw,
+                                                  float* seg_max, float* seg_den, float* row_stats,
+                                                  float* sbfproj_out, float* sbf_p_out, void* stream) {
+  if (n_units < 0 || unit0 < 0 || num_edges < 0 || num_triplets < 0 || heads <= 0 || channels <= 0)
+    return X2G_EINVAL;
+  if (edge_mode != X2G_EDGE_NONE && edge_mode != X2G_EDGE_PER_DST) return X2G_EUNSUPPORTED;
+  if (heads * channels != kCD || channels % 4 || max_degree < 0 || max_degree > X2G_CENTER_MAX_DEGREE)
+    return X2G_EUNSUPPORTED;
+  if (n_units == 0 || num_edges == 0) return X2G_OK;
+  if (!q || !k || !v || !skip || !radial || !sph_y || !w_sbf || !b_sbf || !atom_rowptr || !edge_rev || !rev_trip ||
+      !out || !seg_max || !seg_den || (pack_ptr && !atom_order))
+    return X2G_EINVAL;
+  if (edge_mode == X2G_EDGE_PER_DST && (!edge || !src_row)) return X2G_EINVAL;
+  const auto al = [](const void* p, int m) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % m == 0; };
+  if (!al(q, 16) || !al(k, 16) || !al(v, 16) || !al(skip, 16) || !al(edge, 16) || !al(out, 16) || !al(b_sbf, 16) ||
+      !al(sbfproj_out, 16) || !al(sbf_p_out, 16) || !al(row_stats, 8) || !al(atom_info, 16))
+    return X2G_EUNSUPPORTED;
+  FwdSfArgs a{};
+  a.info = reinterpret_cast<const int4*>(atom_info);
+  a.pp = sbf_p_out;
+  a.q = q; a.k = k; a.v = v; a.skip = skip; a.edge = edge; a.src_row = src_row; a.radial = radial; a.y = sph_y;
+  a.w = w_sbf; a.bias = b_sbf; a.atom_rowptr = atom_rowptr; a.edge_rev = edge_rev; a.rev_trip = rev_trip;
+  a.order = atom_order; a.packs = pack_ptr; a.atom0 = unit0; a.n_atoms = n_units;
+  a.max_rows = max_degree > 0 ? max_degree : 1; a.H = heads; a.skip_rows = skip_rows;
+  a.sqrt_c = static_cast<float>(sqrt(static_cast<double>(channels)));
+  a.out = out; a.alpha = alpha_raw; a.smax = seg_max; a.sden = seg_den; a.sp = sbfproj_out;
+  a.row_stats = reinterpret_cast<float2*>(row_stats);
+  const bool edge_on = edge_mode == X2G_EDGE_PER_DST;
+  const int md = max_degree > 0 ? max_degree : 1;
+  hipStream_t st = as_stream(stream);
+  switch (channels / 4) {
+    case 1: return fwd_sf_tiled_launch<1>(a, edge_on, md, st);
+    case 2: return fwd_sf_tiled_launch<2>(a, edge_on, md, st);
+    case 4: return fwd_sf_tiled_launch<4>(a, edge_on, md, st);
+    case 8: return fwd_sf_tiled_launch<8>(a, edge_on, md, st);
     default: return X2G_EUNSUPPORTED;
   }
 }

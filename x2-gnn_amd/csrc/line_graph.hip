@@ -625,7 +625,7 @@ X2G_API int x2g_batch_meta(const int64_t* edge_index, const int64_t* x, const in
   return last_launch_status();
 }
 
-X2G_API int x2g_abi_version(void) { return 15; }
+X2G_API int x2g_abi_version(void) { return 16; }
 
 X2G_API const char* x2g_status_string(int status) {
   switch (status) {
@@ -822,5 +822,150 @@ X2G_API int x2g_line_graph_sym_build(const int32_t* edge_src, const int32_t* edg
   emit_transpose_sym_kernel<<<blocks_for(E * kEmitGroup, 256), 256, 0, st>>>(
       edge_src, edge_dst, atom_rowptr, trip_rowptr, src_rowptr, E, T, trip_src, trip_dst, atom_j, atom_i, atom_k,
       src_perm, src_dst, edge_rev, rev_trip);
+  return last_launch_status();
+}
+
+namespace x2g {
+
+// ----------------------------------------------------------------------------- center-atom schedule
+// The center-atom attention kernels' workgroup schedule made on the device (a batch made elsewhere — the
+// reference trainer's PyG DataLoader batch, trainer.py:25-27,37-40 — carries none; x2gnn's collate makes the
+// same kind of schedule on the host, data.center_packs):
+//   * the fused forward's UNITS: per molecule, its atoms by decreasing degree packed best-fit into units of
+//     <= 16 rows and <= 16 members (an atom of degree >= 16 alone, atoms without edges 16 to a unit), one wave
+//     per molecule: the units' remaining rows sit one per lane and each atom's best fit is a wave minimum.
+//     Unit slots are the molecule's atom slots [mol_ptr[m], mol_ptr[m + 1]): slot s holds unit s - mol_ptr[m]
+//     of the molecule, or nothing (pack_ptr[s] == pack_ptr[s + 1]), so the layout needs no global scan and a
+//     launch over all N slots covers every unit (empty slots leave at once).  A molecule of more than 64 atoms
+//     gets one atom per unit.
+//   * atom_info per position of pack_order: (atom, first out-edge, degree, src_row of its first out-edge).
+//   * center_order: every atom by decreasing degree (the backward's one-atom workgroups, longest first): a
+//     degree histogram (integer atomics), then each atom's position from the histogram's suffix sum and a
+//     per-degree cursor.  The order among atoms of one degree follows the atomics: no output of the center
+//     kernels depends on it (each atom's block is computed whole by one workgroup in a fixed order).
+constexpr int kSchedCap = 16;       // rows per unit (data.CENTER_PACK_ROWS)
+constexpr int kSchedMembers = 16;   // atoms per unit (data.CENTER_PACK_MEMBERS)
+constexpr int kSchedDeg = 128;      // degree histogram bins (X2G_CENTER_MAX_DEGREE; larger degrees share the last)
+
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+__global__ void __launch_bounds__(64) center_pack_mol_kernel(const int32_t* __restrict__ rowptr,
+                                                             const int32_t* __restrict__ mol_ptr,
+                                                             const int32_t* __restrict__ src_row, int64_t B,
+                                                             int32_t* __restrict__ pack_order,
+                                                             int32_t* __restrict__ pack_ptr, int4* __restrict__ info,
+                                                             int32_t* __restrict__ hist) {
+  __shared__ int sd[64], sa[64], unit_of[64], idx_in[64];
+  const int m = blockIdx.x, lane = threadIdx.x;
+  const int a0 = mol_ptr[m], a1 = mol_ptr[m + 1], na = a1 - a0;
+  auto deg = [&](int a) { return rowptr[a + 1] - rowptr[a]; };
+  auto put = [&](int pos, int a, int d) {
+    pack_order[pos] = a;
+    info[pos] = make_int4(a, rowptr[a], d, (src_row && d > 0) ? src_row[rowptr[a]] : 0);
+  };
+  for (int a = a0 + lane; a < a1; a += 64) atomicAdd(&hist[min(deg(a), kSchedDeg)], 1);
+  if (m == B - 1 && lane == 0) pack_ptr[a1] = a1;  // the slots' end
+  if (na > 64) {  // one atom per unit, in index order
+    for (int a = a0 + lane; a < a1; a += 64) {
+      pack_ptr[a] = a;
+      put(a, a, deg(a));
+    }
+    return;
+  }
+  const int d = lane < na ? deg(a0 + lane) : -1;
+  int rank = 0;  // by decreasing degree, ties by index
+  for (int k = 0; k < na; ++k) {
+    const int dk = __shfl(d, k, 64);
+    rank += (dk > d || (dk == d && k < lane)) ? 1 : 0;
+  }
+  if (lane < na) {
+    sd[rank] = d;
+    sa[rank] = lane;
+  }
+  __syncthreads();
+  // unit u's state in lane u: rows left, members, whether it holds atoms without edges
+  int space = 0, mem = 0, zero = 0, nu = 0;
+  for (int r = 0; r < na; ++r) {
+    const int dr = sd[r];
+    int key = 0x7fffffff;
+    if (dr > 0 && dr < kSchedCap) {  // best fit: the fullest unit that takes it (lowest lane on ties)
+      if (lane < nu && !zero && space >= dr && mem < kSchedMembers) key = (space << 6) | lane;
+    } else if (dr == 0) {  // atoms without edges: with each other
+      if (lane < nu && zero && mem < kSchedMembers) key = lane;
+    }
+    key = wave_min_i(key);
+    int u;
+    if (key == 0x7fffffff) {
+      u = nu++;
+      if (lane == u) {
+        space = dr >= kSchedCap ? 0 : kSchedCap - dr;
+        zero = dr == 0;
+      }
+    } else {
+      u = key & 63;
+      if (lane == u) space -= dr;
+    }
+    const int before = __shfl(mem, u, 64);
+    if (lane == u) ++mem;
+    if (lane == 0) {
+      unit_of[r] = u;
+      idx_in[r] = before;
+    }
+  }
+  // the units' first positions: exclusive scan of their member counts
+  int inc = lane < nu ? mem : 0;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
+  }
+  const int start = inc - (lane < nu ? mem : 0);
+  __syncthreads();
+  if (lane < na) {
+    pack_ptr[a0 + lane] = a0 + (lane < nu ? start : na);
+    const int r = lane;  // the r-th atom by degree
+    const int u = unit_of[r];
+    const int pos = a0 + __shfl(start, u, 64) + idx_in[r];
+    put(pos, a0 + sa[r], sd[r]);
+  }
+}
+
+__global__ void center_order_kernel(const int32_t* __restrict__ rowptr, int64_t N, const int32_t* __restrict__ hist,
+                                    int32_t* __restrict__ cursor, int32_t* __restrict__ order) {
+  const int64_t a = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (a >= N) return;
+  const int d = min(rowptr[a + 1] - rowptr[a], kSchedDeg);
+  int start = 0;
+  for (int e = kSchedDeg; e > d; --e) start += hist[e];
+  order[start + atomicAdd(&cursor[d], 1)] = static_cast<int32_t>(a);
+}
+
+}  // namespace x2g
+
+X2G_API size_t x2g_center_schedule_workspace(void) { return 2 * (x2g::kSchedDeg + 1) * sizeof(int32_t); }
+
+X2G_API int x2g_center_schedule(const int32_t* atom_rowptr, const int32_t* mol_ptr, const int32_t* src_row,
+                                int64_t num_atoms, int64_t num_graphs, int32_t* center_order, int32_t* pack_order,
+                                int32_t* pack_ptr, int32_t* atom_info, void* workspace, size_t ws_bytes,
+                                void* stream) {
+  using namespace x2g;
+  if (num_atoms < 0 || num_graphs < 0 || num_atoms > 0x7fffffff) return X2G_EINVAL;
+  if (ws_bytes < x2g_center_schedule_workspace() || !workspace) return X2G_EWORKSPACE;
+  if (num_atoms == 0 || num_graphs == 0) return X2G_OK;
+  if (!atom_rowptr || !mol_ptr || !center_order || !pack_order || !pack_ptr || !atom_info) return X2G_EINVAL;
+  if (reinterpret_cast<uintptr_t>(atom_info) % 16 || num_graphs > 0x7fffffff) return X2G_EUNSUPPORTED;
+  hipStream_t st = as_stream(stream);
+  int32_t* hist = static_cast<int32_t*>(workspace);
+  int32_t* cursor = hist + (kSchedDeg + 1);
+  const hipError_t e = hipMemsetAsync(hist, 0, x2g_center_schedule_workspace(), st);
+  if (e != hipSuccess) return static_cast<int>(e);
+  center_pack_mol_kernel<<<static_cast<unsigned>(num_graphs), 64, 0, st>>>(
+      atom_rowptr, mol_ptr, src_row, num_graphs, pack_order, pack_ptr, reinterpret_cast<int4*>(atom_info), hist);
+  if (int rc = last_launch_status()) return rc;
+  center_order_kernel<<<blocks_for(num_atoms, 256), 256, 0, st>>>(atom_rowptr, num_atoms, hist, cursor, center_order);
   return last_launch_status();
 }

@@ -78,6 +78,11 @@ SIGNATURES = {
                                      _I64, _I64, _I32, _I32, _P, _P, _P, _P, _P, _P],
     "x2g_sbf_attention_fwd_center_sf": [_P] * 6 + [ctypes.c_int] + [_P] * 10 + [_I64, _I64, _I32, _I64, _I64, _I32,
                                                                                 _I32] + [_P] * 8,
+    "x2g_sbf_attention_fwd_center_sf_tiled": [_P] * 6 + [ctypes.c_int] + [_P] * 10 + [_I64, _I64, _I32, _I32, _I64,
+                                                                                      _I64, _I32, _I32] + [_P] * 8,
+    "x2g_sbf_attention_fwd_center_sf_tiled_lds": [],
+    "x2g_center_schedule_workspace": [],
+    "x2g_center_schedule": [_P, _P, _P, _I64, _I64, _P, _P, _P, _P, _P, _SZ, _P],
     "x2g_sbf_attention_bwd_center_lds": [_I32, _I32],
     "x2g_sbf_attention_bwd_center": [_P] * 5 + [ctypes.c_int] + [_P] * 12 + [_I64, _I32, _I64, _I64, _I32, _I32] +
                                     [_P] * 7,
@@ -160,7 +165,8 @@ RESTYPES = {"x2g_status_string": ctypes.c_char_p, "x2g_vertex_to_edge_workspace"
             "x2g_tiled_wgrad_flat_rows_workspace": _SZ,
             "x2g_conv_proj_bwd_gate_splits": ctypes.c_int32,
             "x2g_conv_proj_bwd_gate_workspace": _SZ, "x2g_graph_layernorm_bwd_workspace": _SZ,
-            "x2g_sbf_attention_bwd_center_lds": _SZ}
+            "x2g_sbf_attention_bwd_center_lds": _SZ, "x2g_sbf_attention_fwd_center_sf_tiled_lds": _SZ,
+            "x2g_center_schedule_workspace": _SZ}
 
 _lib = None
 

@@ -129,6 +129,16 @@ def _meta_on_device(data):
     _lib.load()
     call("x2g_batch_meta", ptr(ei), ptr(x), ptr(batch), E, n, B, ptr(src), ptr(dst), ptr(src_t), ptr(dst_t),
          ptr(atom_t), ptr(line_ptr), ptr(mol_ptr), ptr(rowptr), ptr(info), stream_ptr())
+    # the center-atom kernels' schedule (degree order, the fused forward's packs and atom_info), made on the device
+    # as collate makes it on the host for x2gnn's own batches (data.center_packs)
+    off = 4 * ((3 * n + 1 + 3) // 4)  # atom_info 16-byte aligned after order / pack order / pack_ptr
+    sched = torch.empty(off + 4 * n, dtype=torch.int32, device=dev)
+    c_order, p_order, p_ptr = torch.split(sched[:3 * n + 1], [n, n, n + 1])
+    a_info = sched[off:off + 4 * n]
+    ws_b = int(_lib.load().x2g_center_schedule_workspace())
+    ws = torch.empty(ws_b, dtype=torch.uint8, device=dev)
+    call("x2g_center_schedule", ptr(rowptr), ptr(mol_ptr), ptr(src_t), n, B, ptr(c_order), ptr(p_order), ptr(p_ptr),
+         ptr(a_info), ptr(ws), ws_b, stream_ptr())
     host = info.cpu().numpy()  # the one device->host copy: sizes per molecule and the flags
     mp_, lp, tr, fl = host[:B + 1], host[B + 1:2 * B + 2], host[2 * B + 2:3 * B + 2], host[3 * B + 2:]
     if fl[2]:
@@ -136,7 +146,9 @@ def _meta_on_device(data):
                          "(the order the reference's radius graph emits, atom_graph.py:42-45)")
     index = {"_x2g_edge_src": src, "_x2g_edge_dst": dst, "_x2g_src_type": src_t, "_x2g_dst_type": dst_t,
              "_x2g_atom_type": atom_t, "_x2g_line_ptr": line_ptr, "_x2g_mol_ptr": mol_ptr,
-             "_x2g_symmetric": bool(fl[0] == 0), "_x2g_max_degree": int(fl[1])}
+             "_x2g_symmetric": bool(fl[0] == 0), "_x2g_max_degree": int(fl[1]),
+             "_x2g_center_order": c_order, "_x2g_pack_order": p_order, "_x2g_center_packs": p_ptr,
+             "_x2g_pack_info": a_info, "_x2g_center_rows": CENTER_SF_MAX_ROWS, "_x2g_center_mixed": True}
     if fl[3] == 0 and B > 0:  # every edge inside its molecule: the per-molecule line-graph builder
         index["_x2g_mol_trips"] = info[2 * B + 2:3 * B + 2]  # (a view of the device block: no copy)
         index["_x2g_max_mol_atoms"] = int(np.diff(mp_).max())
@@ -212,6 +224,10 @@ def _add_device_indices(b, nodes, edges):
     order, packs, rows = center_packs(deg)
     b._store["_x2g_pack_order"] = torch.from_numpy(order)
     b._store["_x2g_center_packs"] = torch.from_numpy(packs)
+    # the leading units of more rows than the fused forward's LDS image holds (single atoms: the source-tiled
+    # kernel), and the largest row count of the rest
+    hubs, rows = center_hubs(deg, order, packs)
+    b._store["_x2g_center_hubs"] = hubs
     b._store["_x2g_center_rows"] = rows
     # per pack-order position: (atom, first out-edge, degree, element): the fused forward's row tables in one
     # load per atom (x2g_sbf_attention_fwd_center_sf atom_info)
@@ -262,6 +278,23 @@ def center_packs(deg, cap=CENTER_PACK_ROWS, max_members=CENTER_PACK_MEMBERS):
     order = np.fromiter((a for u in units for a in u), dtype=np.int32, count=len(deg))
     packs = np.concatenate([[0], np.cumsum([len(u) for u in units])]).astype(np.int32)
     return order, packs, int(max(rows, default=0))
+
+
+CENTER_SF_MAX_ROWS = 17  # ops.CENTER_SF_MAX_ROWS
+
+
+def center_hubs(deg, order, packs, max_rows=CENTER_SF_MAX_ROWS):
+    """(hubs, rows): the units of center_packs' (order, packs) are by decreasing largest degree, so those of
+    more than ``max_rows`` rows (single atoms) are the first ``hubs``; ``rows`` is the largest row count of
+    the others."""
+    deg = np.asarray(deg, dtype=np.int64)
+    if len(packs) < 2:
+        return 0, 0
+    urows = np.add.reduceat(deg[order], packs[:-1]) if len(order) else np.zeros(len(packs) - 1, np.int64)
+    big = urows > max_rows
+    hubs = int(np.argmin(big)) if not big.all() else int(len(big))
+    assert not big[hubs:].any(), "units over the row bound must lead"
+    return hubs, int(urows[hubs:].max(initial=0))
 
 
 def _is_symmetric(ei, n):

@@ -109,8 +109,11 @@ class LineGraph:
         self.atom_type = None
         # the center kernels' workgroups (collate's; None: the identity): int32 [N] the atoms by decreasing
         # degree (one per workgroup), and the fused forward's packs (data.center_packs): int32 [N] the atoms
-        # unit by unit, int32 [P + 1] the units' bounds in it, the largest unit's row count
+        # unit by unit, int32 [P + 1] the units' bounds in it, the largest row count of the units after the
+        # first center_hubs (single atoms of more rows than the fused forward's LDS image holds: the tiled form)
         self.center_order = self.pack_order = self.center_packs = self.center_rows = self.pack_info = None
+        self.center_hubs = 0
+        self.center_mixed = False  # the schedule is x2g_center_schedule's (hub units among the packs)
         if molecules is not None:
             mol_ptr, line_ptr, trips, max_atoms = molecules
             call("x2g_vertex_to_edge_sym_mol", ptr(edge_src), ptr(edge_dst), self.E, self.N, self.T, ptr(mol_ptr),
@@ -154,6 +157,8 @@ class LineGraph:
         lg.symmetric = False
         lg.edge_rev = lg.rev_trip = lg.max_degree = lg.atom_type = None
         lg.center_order = lg.pack_order = lg.center_packs = lg.center_rows = lg.pack_info = None
+        lg.center_hubs = 0
+        lg.center_mixed = False
         ws_bytes = int(_lib.load().x2g_vertex_to_edge_workspace(lg.E, 0))
         lg._ws = torch.empty(ws_bytes, dtype=torch.uint8, device=lg.trip_src.device)
         return lg
@@ -289,8 +294,9 @@ def spherical_basis(pos, lg: LineGraph, rbf_env, want_cos=False, num_spherical: 
     out = torch.empty(lg.T, S, dtype=torch.float32, device=pos.device)
     cos_t = torch.empty(lg.T, dtype=torch.float32, device=pos.device) if want_cos else None
     # the factors are kept for the factorised backward and for the fused-projection center forward (which
-    # also runs without grad, in inference, when its LDS image fits the batch's largest degree)
-    sf_fits = getattr(lg, "max_degree", None) is not None and 4776 * max(lg.max_degree, 1) <= 160 * 1024
+    # also runs without grad, in inference: its source-tiled form takes every degree up to the center kernels'
+    # bound)
+    sf_fits = getattr(lg, "max_degree", None) is not None and lg.max_degree <= CENTER_MAX_DEGREE
     fold = _FOLD_SBF and (num_spherical, num_radial) == FOLD_BASIS and (torch.is_grad_enabled() or sf_fits)
     ylm = torch.empty(lg.T, 8, dtype=torch.float32, device=pos.device) if fold else None
     call("x2g_spherical_basis", ptr(pos), ptr(lg.atom_i), ptr(lg.atom_j), ptr(lg.atom_k), None, ptr(lg.trip_src),
@@ -367,6 +373,46 @@ def _center_units(lg, packed):
     return lg.center_order, None, lg.N, max(int(lg.max_degree), 1), None
 
 
+# Units of more rows than this go to the source-tiled fused forward (x2g_sbf_attention_fwd_center_sf_tiled):
+# the fused forward's LDS image of 17 rows (81.7 KB) is the largest that keeps two workgroups per CU
+# (data.CENTER_SF_MAX_ROWS; config 2's largest degree is 17, config 5's AID atoms reach 61).
+CENTER_SF_MAX_ROWS = 17
+
+
+def _center_split(lg):
+    """(order, pack_ptr, info, launches): the fused forward's units and the launches that cover them, each
+    (entry, unit0, n_units, rows, skip_rows): with collate's packs the first ``center_hubs`` units (single
+    atoms of more than CENTER_SF_MAX_ROWS rows, by decreasing degree) take the source-tiled form and the rest
+    (at most ``center_rows`` rows each) the untiled one; with a device-made schedule (x2g_center_schedule:
+    hubs among the packs) both forms run over all units, each leaving out the other's (skip_rows / max_rows);
+    without either (unpacked) every atom is a unit by decreasing degree, all of them tiled when any exceeds
+    the bound."""
+    order, packs, units, rows, info = _center_units(lg, _PACK_FWD)
+    sf, tiled = "x2g_sbf_attention_fwd_center_sf", "x2g_sbf_attention_fwd_center_sf_tiled"
+    if packs is not None and getattr(lg, "center_mixed", False):
+        launches = [(sf, 0, units, CENTER_SF_MAX_ROWS, 0)]
+        if lg.max_degree > CENTER_SF_MAX_ROWS:
+            launches.insert(0, (tiled, 0, units, lg.max_degree, CENTER_SF_MAX_ROWS))
+        return order, packs, info, launches
+    if packs is not None:
+        hubs = int(getattr(lg, "center_hubs", 0) or 0)
+        launches = [(tiled, 0, hubs, lg.max_degree, 0)] if hubs else []
+        if units > hubs:
+            launches.append((sf, hubs, units - hubs, rows, 0))
+        return order, packs, info, launches
+    if rows > CENTER_SF_MAX_ROWS:
+        return order, None, None, [(tiled, 0, units, lg.max_degree, 0)]
+    return order, None, None, [(sf, 0, units, rows, 0)]
+
+
+def _center_launch(launches, common, outs):
+    for entry, u0, n, rows, skip in launches:
+        if entry.endswith("_tiled"):
+            call(entry, *common, u0, n, rows, skip, *outs)
+        else:
+            call(entry, *common, u0, n, rows, *outs)
+
+
 # Workgroup packs (data.center_packs) in the fused forward: 16 owners per workgroup keep 90 % instead of
 # 57 % of them busy, and its owners never wait for one another (no barrier after the P products).  The
 # backward stays one atom per workgroup on 4 waves: with packs (8 waves) its phase barriers waited for
@@ -382,12 +428,12 @@ def _unit_rows_lds(rows):  # csrc/attention_center.hip unit_rows_lds
 
 
 def _center_sf_ok(lg, factors, D):
-    """Whether the fused-projection center forward applies: the sbf factors are this call's, and the
-    unit's LDS image (k + e, v + e, 7 P rows and the radial row per source row: 4.66 KB x rows) fits."""
+    """Whether the fused-projection center forward applies: the sbf factors are this call's (the units of more
+    rows than its LDS image holds take its source-tiled form)."""
     if not (_CENTER_SF and factors is not None and factors[1] is not None and D == 128 and lg.max_degree is not None):
         return False
-    rows = _center_units(lg, _PACK_FWD)[3]
-    return _unit_rows_lds(rows) + 4776 * rows <= 160 * 1024
+    _, _, _, launches = _center_split(lg)
+    return all(e.endswith("_tiled") or _unit_rows_lds(r) + 4776 * r <= 160 * 1024 for e, _, _, r, _ in launches)
 
 
 def _center_bwd_ok(lg, heads, s_rows=False):
@@ -449,12 +495,14 @@ class _SBFAttention(torch.autograd.Function):
                     sbf_p = torch.empty(E, 7, D, dtype=torch.float32, device=dev)
                 else:
                     sproj = torch.empty(T, D, dtype=torch.float32, device=dev)
-            order, packs, units, rows, info = _center_units(lg, _PACK_FWD)
-            call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(src_row),
-                 edge_mode, ptr(factors[0]), ptr(factors[1]), ptr(w_sbf), ptr(b_sbf), ptr(lg.atom_rowptr),
-                 ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(order), ptr(packs), ptr(info), 0, units, rows, E, T, heads,
-                 channels, ptr(out), ptr(alpha), ptr(smax), ptr(sden), ptr(rstats), ptr(sproj), ptr(sbf_p),
-                 stream_ptr())
+            # (the atoms beyond the untiled form's LDS image take the source-tiled form: _center_split)
+            order, packs, info, launches = _center_split(lg)
+            common = (ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(src_row), edge_mode, ptr(factors[0]),
+                      ptr(factors[1]), ptr(w_sbf), ptr(b_sbf), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
+                      ptr(lg.rev_trip), ptr(order), ptr(packs), ptr(info))
+            outs = (E, T, heads, channels, ptr(out), ptr(alpha), ptr(smax), ptr(sden), ptr(rstats), ptr(sproj),
+                    ptr(sbf_p), stream_ptr())
+            _center_launch(launches, common, outs)
         else:
             # S = lin_sbf(sbf) once per layer [T, D], right before this layer's attention (so it is still
             # in the MALL when the attention kernels read its rows: sbf pointer = S, weight pointer NULL)

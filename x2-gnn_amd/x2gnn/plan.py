@@ -80,6 +80,8 @@ class GraphPlan:
             p.lg.center_packs = st.get("_x2g_center_packs")
             p.lg.center_rows = st.get("_x2g_center_rows")
             p.lg.pack_info = st.get("_x2g_pack_info")
+            p.lg.center_hubs = st.get("_x2g_center_hubs", 0)
+            p.lg.center_mixed = st.get("_x2g_center_mixed", False)
         else:
             p.lg = ops.vertex_to_edge(ei, p.num_atoms, p.num_triplets, meta.get("symmetric", False))
             p.line_ptr = _ptr_from_counts(data.edge_num, p.num_graphs, dev)
