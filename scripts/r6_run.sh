@@ -35,6 +35,8 @@ for s in "$@"; do
             -- python "$ROOT/bench.py" --steps 50 --warmup 3 --no-cpu-baseline ;;
     prof_c5) step prof_c5 420 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5_$TAG -o run --output-format csv \
             -- python "$ROOT/bench.py" --workload aid_infer --steps 10 --warmup 2 --no-cpu-baseline ;;
+    ab) step ab 900 python -u scripts/step_ab.py ${AB_ROUNDS:-3} $AB_VARIANTS ;;
+    ab_c5) step ab_c5 900 python -u scripts/step_ab.py ${AB_ROUNDS:-3} $AB_VARIANTS ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

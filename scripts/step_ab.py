@@ -24,8 +24,10 @@ for r in range(rounds):
         # AB_ROOT: run that tree's bench.py (and so its x2gnn package), e.g. ab_base/ from
         # scripts/build_base_tree.sh for a host-side change
         broot = os.path.join(root, env["AB_ROOT"]) if "AB_ROOT" in env else root
+        # AB_ARGS: extra bench.py arguments for every variant (e.g. "--workload aid_infer --steps 30")
+        extra = os.environ.get("AB_ARGS", "").split()
         out = subprocess.run([sys.executable, os.path.join(broot, "bench.py"), "--step-only", "--steps", "200",
-                              "--warmup", "10"], env=e, capture_output=True, text=True, timeout=300)
+                              "--warmup", "10", *extra], env=e, capture_output=True, text=True, timeout=300)
         line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
         if out.returncode != 0 or not line:
             print(name, "FAILED", out.returncode, out.stderr[-2000:], flush=True)

@@ -531,7 +531,7 @@ int fwd_sf_launch(const FwdSfArgs& a, bool edge, hipStream_t st) {
 // at other points: equal to fp32 rounding.
 constexpr int kTileRows = 16;
 
-template <int LPH, int WAVES, int B, bool EDGE, int RMAX>
+template <int LPH, int WAVES, int B, bool EDGE, int RMAX, bool STORE>
 __global__ void __launch_bounds__(64 * WAVES, 4) attn_fwd_center_sf_tiled_kernel(const FwdSfArgs a) {
   static_assert(kTileRows % B == 0, "batches never cross a tile");
   extern __shared__ cf4 lds[];  // [TS][32] (k + e), [TS][32] (v + e), [TS][7][32] P, [TS][42] R
@@ -626,67 +626,81 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_fwd_center_sf_tiled_kernel
       if (i >= n) continue;          // (per owner)
       const int dd = a.edge_rev[r0 + i], tb = a.rev_trip[r0 + i];
       const cf4 qv = ld4(a.q + static_cast<int64_t>(dd) * kCD + c0);
-      auto batch = [&](int j0, auto bb) {
-        constexpr int BB = decltype(bb)::value;
-        float yv[BB];
-        int tt[BB];
-#pragma unroll
-        for (int uu = 0; uu < BB; ++uu) {
-          const int j = j0 + uu;
-          int jj = j - (j > i ? 1 : 0);
-          jj = jj < nt ? jj : nt - 1;  // clamped: every load unconditional
-          tt[uu] = tb + jj;
-          yv[uu] = a.y[static_cast<int64_t>(tt[uu]) * 8 + (l32 & 7)];
-        }
-        cf4 sv[BB];
-        float lg[BB];
-        float mb = -INFINITY;
-#pragma unroll
-        for (int uu = 0; uu < BB; ++uu) {
-          const int j = j0 + uu;
-          const bool ok = j < n && j != i;
-          const int jr = (j < t1 ? j : t1 - 1) - t0;  // the source's row in the tile
-          float yl[kSfL];
-          yl[0] = dpp_mov<0x150>(yv[uu]);
-          yl[1] = dpp_mov<0x151>(yv[uu]);
-          yl[2] = dpp_mov<0x152>(yv[uu]);
-          yl[3] = dpp_mov<0x153>(yv[uu]);
-          yl[4] = dpp_mov<0x154>(yv[uu]);
-          yl[5] = dpp_mov<0x155>(yv[uu]);
-          yl[6] = dpp_mov<0x156>(yv[uu]);
-          cf4 s4 = bias4;
-#pragma unroll
-          for (int l = 0; l < kSfL; ++l) s4 += yl[l] * P[(jr * kSfL + l) * 32 + l32];
-          sv[uu] = s4;
-          if (a.sp && ok) st4(a.sp + static_cast<int64_t>(tt[uu]) * kCD + c0, s4);
-          const cf4 kr = KE[jr * 32 + l32];
-          float dot = qv[0] * kr[0];
-          dot = fmaf(qv[1], kr[1], dot);
-          dot = fmaf(qv[2], kr[2], dot);
-          dot = fmaf(qv[3], kr[3], dot);
-          const float logit = head_sum<LPH>(dot) / a.sqrt_c;
-          lg[uu] = ok ? logit : -INFINITY;
-          mb = fmaxf(mb, lg[uu]);
-          if (a.alpha && ok && leader) a.alpha[static_cast<int64_t>(tt[uu]) * a.H + head] = logit;
-        }
-        const float m_new = fmaxf(m[r], mb);
-        const float corr = m_new == -INFINITY ? 1.f : expf(m[r] - m_new);
-        den[r] *= corr;
-        acc[r] *= corr;
-#pragma unroll
-        for (int uu = 0; uu < BB; ++uu) {
-          const int j = j0 + uu;
-          const float p = lg[uu] == -INFINITY ? 0.f : expf(lg[uu] - m_new);
-          const cf4 vr = VE[((j < t1 ? j : t1 - 1) - t0) * 32 + l32];
-          den[r] += p;
-          acc[r] += p * (vr * sv[uu]);
-        }
-        m[r] = m_new;
-      };
       if (nt > 0) {  // (n = 1: an empty softmax, out = skip)
-        int j0 = t0;
-        for (; j0 < t1 && n - j0 > B / 2; j0 += B) batch(j0, std::integral_constant<int, B>{});
-        if (j0 < t1) batch(j0, std::integral_constant<int, B / 2>{});
+        // batches of B sources, software-pipelined: batch j0 + B's Y values are loaded before batch j0's
+        // arithmetic (clamped indices: every load unconditional), so a destination waits out one load
+        // latency per tile instead of one per batch; the last batch of the atom masked
+        float yv[B];
+        int tt[B];
+        auto load = [&](int j0, float (&y_)[B], int (&t_)[B]) {
+#pragma unroll
+          for (int uu = 0; uu < B; ++uu) {
+            const int j = j0 + uu;
+            int jj = j - (j > i ? 1 : 0);
+            jj = jj < nt ? jj : nt - 1;
+            t_[uu] = tb + jj;
+            y_[uu] = a.y[static_cast<int64_t>(t_[uu]) * 8 + (l32 & 7)];
+          }
+        };
+        load(t0, yv, tt);
+        for (int j0 = t0; j0 < t1; j0 += B) {
+          float yn[B];
+          int tn[B];
+          load(j0 + B, yn, tn);
+          cf4 sv[B];
+          float lg[B];
+          float mb = -INFINITY;
+#pragma unroll
+          for (int uu = 0; uu < B; ++uu) {
+            const int j = j0 + uu;
+            const bool ok = j < n && j != i;
+            const int jr = (j < t1 ? j : t1 - 1) - t0;  // the source's row in the tile
+            float yl[kSfL];
+            yl[0] = dpp_mov<0x150>(yv[uu]);
+            yl[1] = dpp_mov<0x151>(yv[uu]);
+            yl[2] = dpp_mov<0x152>(yv[uu]);
+            yl[3] = dpp_mov<0x153>(yv[uu]);
+            yl[4] = dpp_mov<0x154>(yv[uu]);
+            yl[5] = dpp_mov<0x155>(yv[uu]);
+            yl[6] = dpp_mov<0x156>(yv[uu]);
+            cf4 s4 = bias4;
+#pragma unroll
+            for (int l = 0; l < kSfL; ++l) s4 += yl[l] * P[(jr * kSfL + l) * 32 + l32];
+            sv[uu] = s4;
+            if constexpr (STORE) {
+              if (a.sp && ok) st4(a.sp + static_cast<int64_t>(tt[uu]) * kCD + c0, s4);
+            }
+            const cf4 kr = KE[jr * 32 + l32];
+            float dot = qv[0] * kr[0];
+            dot = fmaf(qv[1], kr[1], dot);
+            dot = fmaf(qv[2], kr[2], dot);
+            dot = fmaf(qv[3], kr[3], dot);
+            const float logit = head_sum<LPH>(dot) / a.sqrt_c;
+            lg[uu] = ok ? logit : -INFINITY;
+            mb = fmaxf(mb, lg[uu]);
+            if constexpr (STORE) {
+              if (a.alpha && ok && leader) a.alpha[static_cast<int64_t>(tt[uu]) * a.H + head] = logit;
+            }
+          }
+          const float m_new = fmaxf(m[r], mb);
+          const float corr = m_new == -INFINITY ? 1.f : expf(m[r] - m_new);
+          den[r] *= corr;
+          acc[r] *= corr;
+#pragma unroll
+          for (int uu = 0; uu < B; ++uu) {
+            const int j = j0 + uu;
+            const float p = lg[uu] == -INFINITY ? 0.f : expf(lg[uu] - m_new);
+            const cf4 vr = VE[((j < t1 ? j : t1 - 1) - t0) * 32 + l32];
+            den[r] += p;
+            acc[r] += p * (vr * sv[uu]);
+          }
+          m[r] = m_new;
+#pragma unroll
+          for (int uu = 0; uu < B; ++uu) {
+            yv[uu] = yn[uu];
+            tt[uu] = tn[uu];
+          }
+        }
       }
     }
   }
@@ -727,14 +741,20 @@ int fwd_sf_tiled_launch(const FwdSfArgs& a, bool edge, int max_degree, hipStream
     return last_launch_status();
   };
   constexpr int NO = 2 * W;
-  if (max_degree <= 2 * NO)
-    return edge ? go(attn_fwd_center_sf_tiled_kernel<LPH, W, B, true, 2>)
-                : go(attn_fwd_center_sf_tiled_kernel<LPH, W, B, false, 2>);
-  if (max_degree <= 4 * NO)
-    return edge ? go(attn_fwd_center_sf_tiled_kernel<LPH, W, B, true, 4>)
-                : go(attn_fwd_center_sf_tiled_kernel<LPH, W, B, false, 4>);
-  return edge ? go(attn_fwd_center_sf_tiled_kernel<LPH, W, B, true, 8>)
-              : go(attn_fwd_center_sf_tiled_kernel<LPH, W, B, false, 8>);
+  // STORE: logits / S rows / P rows for a backward or the attention weights (inference stores none: no store
+  // in the pipelined batch loop, whose load waits then stay counted)
+  const bool store = a.alpha || a.sp || a.pp;
+  auto pick = [&](auto rmax) -> int {
+    constexpr int R = decltype(rmax)::value;
+    if (store)
+      return edge ? go(attn_fwd_center_sf_tiled_kernel<LPH, W, B, true, R, true>)
+                  : go(attn_fwd_center_sf_tiled_kernel<LPH, W, B, false, R, true>);
+    return edge ? go(attn_fwd_center_sf_tiled_kernel<LPH, W, B, true, R, false>)
+                : go(attn_fwd_center_sf_tiled_kernel<LPH, W, B, false, R, false>);
+  };
+  if (max_degree <= 2 * NO) return pick(std::integral_constant<int, 2>{});
+  if (max_degree <= 4 * NO) return pick(std::integral_constant<int, 4>{});
+  return pick(std::integral_constant<int, 8>{});
 }
 
 template <int LPH>
@@ -958,11 +978,70 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const Bw
         dv += at * (go * st);
       }
     };
-    if (nt > 0) {  // (workgroup-uniform)
-      constexpr int B1 = FACT ? kFactBatch : B;
+    if constexpr (FACT) {
+      // software-pipelined: batch i0 + 4's Y and logit loads are issued before batch i0's arithmetic, so
+      // only the first batch of a source waits out the load latency (every batch full, the last masked;
+      // every load and store unconditional — clamped indices, the (g, a) store of a masked triplet to an
+      // out-of-range offset — so the compiler's vmcnt waits stay counted)
+      constexpr int BB = kFactBatch;
+      if (nt > 0) {  // (workgroup-uniform)
+        float yv[BB], al[BB];
+        int tt[BB];
+        auto load = [&](int i0, float (&y_)[BB], float (&a_)[BB], int (&t_)[BB]) {
+#pragma unroll
+          for (int u = 0; u < BB; ++u) {
+            const int i = i0 + u < n ? i0 + u : n - 1;
+            t_[u] = trip(i, j);
+            y_[u] = ldf(y_r, (t_[u] * 8 + (l32 & 7)) * 4);
+            a_[u] = ldf(al_r, (t_[u] * H + head) * 4);
+          }
+        };
+        load(0, yv, al, tt);
+        for (int i0 = 0; i0 < n; i0 += BB) {
+          float yn[BB], an[BB];
+          int tn[BB];
+          load(i0 + BB, yn, an, tn);
+#pragma unroll
+          for (int u = 0; u < BB; ++u) {
+            const int i = i0 + u < n ? i0 + u : n - 1;
+            const bool ok = i0 + u < n && i != j;
+            float yl[kSfL];
+            yl[0] = dpp_mov<0x150>(yv[u]);
+            yl[1] = dpp_mov<0x151>(yv[u]);
+            yl[2] = dpp_mov<0x152>(yv[u]);
+            yl[3] = dpp_mov<0x153>(yv[u]);
+            yl[4] = dpp_mov<0x154>(yv[u]);
+            yl[5] = dpp_mov<0x155>(yv[u]);
+            yl[6] = dpp_mov<0x156>(yv[u]);
+            cf4 st = bias4;  // S_t = b + sum_l Y_l(t) P_j[l], the forward's arithmetic in its order
+#pragma unroll
+            for (int l = 0; l < kSfL; ++l) st += yl[l] * pj[l];
+            const float at = ok ? expf(al[u] - MX[i * H + head]) * IV[i * H + head] : 0.f;
+            const cf4 go = GO[i * 32 + l32];
+            const cf4 gu = go * ue;
+            float gp = gu[0] * st[0];
+            gp = fmaf(gu[1], st[1], gp);
+            gp = fmaf(gu[2], st[2], gp);
+            gp = fmaf(gu[3], st[3], gp);
+            const float g = head_sum<LPH>(gp);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned,
+                                                                     make_float2(g, at)),
+                                                  ag_r, (ok && leader) ? (tt[u] * H + head) * 8 : static_cast<int>(0x80000000u),
+                                                  0, 0);
+            dv += at * (go * st);
+          }
+#pragma unroll
+          for (int u = 0; u < BB; ++u) {
+            yv[u] = yn[u];
+            al[u] = an[u];
+            tt[u] = tn[u];
+          }
+        }
+      }
+    } else if (nt > 0) {  // (workgroup-uniform)
       int i0 = 0;
-      for (; n - i0 > B1 / 2; i0 += B1) batch(i0, std::integral_constant<int, B1>{});
-      if (i0 < n) batch(i0, std::integral_constant<int, B1 / 2>{});
+      for (; n - i0 > B / 2; i0 += B) batch(i0, std::integral_constant<int, B>{});
+      if (i0 < n) batch(i0, std::integral_constant<int, B / 2>{});
     }
     st4(a.dv + srow, dv);
     DE[j * 32 + l32] = dv;  // (the edge term's gradient: dk added in pass 2)
