@@ -25,7 +25,8 @@ for r in range(rounds):
         # scripts/build_base_tree.sh for a host-side change
         broot = os.path.join(root, env["AB_ROOT"]) if "AB_ROOT" in env else root
         # AB_ARGS: extra bench.py arguments for every variant (e.g. "--workload aid_infer --steps 30")
-        extra = os.environ.get("AB_ARGS", "").split()
+        # (a variant's own BENCH_ARGS entry adds arguments for that variant alone)
+        extra = os.environ.get("AB_ARGS", "").split() + env.get("BENCH_ARGS", "").split()
         out = subprocess.run([sys.executable, os.path.join(broot, "bench.py"), "--step-only", "--steps", "200",
                               "--warmup", "10", *extra], env=e, capture_output=True, text=True, timeout=300)
         line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]

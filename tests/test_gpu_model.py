@@ -903,3 +903,39 @@ def test_two_models_on_two_streams_equal_serial(cuda):
     torch.cuda.synchronize()
     assert da is not db and da.flat_launches and db.flat_launches
     assert torch.equal(ka.flat, serial[0]) and torch.equal(kb.flat, serial[1])
+
+
+@pytest.mark.parametrize("shape", ["S160", "aid"])
+def test_device_schedule_equals_host_schedule(cuda, monkeypatch, shape):
+    """data.HOST_SCHEDULE False: collate leaves the center kernels' schedule out and the step makes it on the
+    device (ops.center_schedule, x2g_center_schedule: per-molecule packs, hub units among them) — energies and
+    every parameter gradient equal the host-scheduled batch's bit for bit (no output of the center kernels
+    depends on the packing or the order)."""
+    import os
+
+    import x2gnn
+    from conftest import GOLDEN
+    from x2gnn import data as xdata
+    from x2gnn.synth import molecules_from_geometry_file, synthetic_molecules
+
+    mols = (synthetic_molecules(32, "S160", seed=5) if shape == "S160" else
+            molecules_from_geometry_file(os.path.join(GOLDEN, "aid_geom.npz"), indices=[0, 3, 7], seed=0))
+    cfg = dict(conv_layers=4, sbf_dim=7, rbf_dim=6, in_channels=128, heads=16, embedding_size=128)
+    out = []
+    for host in (True, False):
+        monkeypatch.setattr(xdata, "HOST_SCHEDULE", host)
+        b = xdata.collate(mols)
+        assert ("_x2g_device_schedule" in b._store) == (not host)
+        torch.manual_seed(0)
+        m = x2gnn.xgnn_poly(device="cuda", **cfg).to(cuda)
+        seen = record_calls(monkeypatch)
+        e = m(b.to(cuda))
+        torch.nn.functional.smooth_l1_loss(e, b.y.to(cuda)).backward()
+        torch.cuda.synchronize()
+        names = [n for n, _ in seen]
+        assert names.count("x2g_center_schedule") == (0 if host else 1)
+        assert "x2g_sbf_project" not in names
+        out.append((e.detach().cpu(), [p.grad.detach().cpu().clone() for p in m.parameters() if p.grad is not None]))
+    assert torch.equal(out[0][0], out[1][0])
+    for a, r in zip(out[0][1], out[1][1]):
+        assert torch.equal(a, r)

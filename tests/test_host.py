@@ -148,3 +148,36 @@ def test_center_packs_and_atom_info():
     o2, p2, r2 = center_packs(np.array([0, 3, 0, 20, 5, 16, 1]))
     u2 = [o2[p2[u]:p2[u + 1]].tolist() for u in range(len(p2) - 1)]
     assert u2[-1] == [0, 2] and [3] in u2 and [5] in u2 and r2 == 20
+
+
+@pytest.mark.parametrize("host_schedule", [True, False])
+def test_fast_collate_equals_pyg_from_data_list(monkeypatch, host_schedule):
+    """collate (one numpy concatenation per key) == Batch.from_data_list over per-molecule Data objects (PyG
+    2.1's collate restated, data.py), every key, dtype and the host metadata; with data.HOST_SCHEDULE False
+    the center schedule is left to the device (and collate is cheaper)."""
+    import time
+
+    from x2gnn import data
+    from x2gnn.synth import synthetic_molecules
+
+    monkeypatch.setattr(data, "HOST_SCHEDULE", host_schedule)
+    mols = synthetic_molecules(24, "S5A", seed=3)
+    a = data.collate(mols)
+    b = data.Batch.from_data_list([data.molecule_to_data(m) for m in mols])
+    b._store["y"] = b._store["y"].to(torch.float32)
+    assert list(a._store) == list(b._store)
+    for k, va in a._store.items():
+        vb = b._store[k]
+        if torch.is_tensor(va):
+            assert va.dtype == vb.dtype and torch.equal(va, vb), k
+        else:
+            assert va == vb, k
+    for k in ("nodes", "edges", "triplets"):
+        assert np.array_equal(a._meta[k], b._meta[k])
+    assert ("_x2g_center_packs" in a._store) == host_schedule
+    mols = synthetic_molecules(128, "S160", seed=1000)
+    data.collate(mols)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        data.collate(mols)
+    print(f"collate of 128 S160 molecules (host schedule {host_schedule}): {(time.perf_counter() - t0) / 5 * 1e3:.2f} ms")

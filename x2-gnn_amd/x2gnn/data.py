@@ -68,6 +68,16 @@ class Data:
             out._store[k] = v.to(device, non_blocking=non_blocking) if torch.is_tensor(v) else v
         return out
 
+    def pin_memory(self):
+        """A copy with every tensor in page-locked host memory (torch DataLoader(pin_memory=True) calls this), so
+        ``to(device, non_blocking=True)`` overlaps the copy with device work."""
+        out = type(self).__new__(type(self))
+        object.__setattr__(out, "_store", _Store())
+        object.__setattr__(out, "_meta", self._meta)
+        for k, v in self._store.items():
+            out._store[k] = v.pin_memory() if torch.is_tensor(v) else v
+        return out
+
     def host_meta(self):
         """Per-molecule (atoms, edges, triplets) counts as int64 numpy arrays (host)."""
         if self._meta is None:
@@ -129,17 +139,13 @@ def _meta_on_device(data):
     _lib.load()
     call("x2g_batch_meta", ptr(ei), ptr(x), ptr(batch), E, n, B, ptr(src), ptr(dst), ptr(src_t), ptr(dst_t),
          ptr(atom_t), ptr(line_ptr), ptr(mol_ptr), ptr(rowptr), ptr(info), stream_ptr())
-    # the center-atom kernels' schedule (degree order, the fused forward's packs and atom_info), made on the device
-    # as collate makes it on the host for x2gnn's own batches (data.center_packs)
-    off = 4 * ((3 * n + 1 + 3) // 4)  # atom_info 16-byte aligned after order / pack order / pack_ptr
-    sched = torch.empty(off + 4 * n, dtype=torch.int32, device=dev)
-    c_order, p_order, p_ptr = torch.split(sched[:3 * n + 1], [n, n, n + 1])
-    a_info = sched[off:off + 4 * n]
-    ws_b = int(_lib.load().x2g_center_schedule_workspace())
-    ws = torch.empty(ws_b, dtype=torch.uint8, device=dev)
-    call("x2g_center_schedule", ptr(rowptr), ptr(mol_ptr), ptr(src_t), n, B, ptr(c_order), ptr(p_order), ptr(p_ptr),
-         ptr(a_info), ptr(ws), ws_b, stream_ptr())
     host = info.cpu().numpy()  # the one device->host copy: sizes per molecule and the flags
+    # the center-atom kernels' schedule (degree order, the fused forward's packs and atom_info), made on the device
+    # as collate makes it on the host for x2gnn's own batches (data.center_packs); enqueued after the read-back,
+    # which then waits for nothing it does not need
+    from .ops import center_schedule
+
+    c_order, p_order, p_ptr, a_info = center_schedule(rowptr, mol_ptr, src_t, n, B)
     mp_, lp, tr, fl = host[:B + 1], host[B + 1:2 * B + 2], host[2 * B + 2:3 * B + 2], host[3 * B + 2:]
     if fl[2]:
         raise ValueError("edge_index must list each directed edge once, sorted by (source, destination) "
@@ -218,6 +224,9 @@ def _add_device_indices(b, nodes, edges):
         b._store["_x2g_max_mol_atoms"] = int(nodes.max()) if len(nodes) else 0
     deg = np.bincount(ei_np[0], minlength=int(nodes.sum()))
     b._store["_x2g_max_degree"] = int(deg.max()) if deg.size else 0
+    if not HOST_SCHEDULE:  # the plan makes it on the device (ops.center_schedule) from the built line graph
+        b._store["_x2g_device_schedule"] = True
+        return
     # the center-atom kernels' workgroups: one atom each by decreasing degree (the longest blocks first), and
     # the fused forward's units of atoms packed by degree (the longest units first)
     b._store["_x2g_center_order"] = torch.from_numpy(np.argsort(-deg, kind="stable").astype(np.int32))
@@ -236,6 +245,11 @@ def _add_device_indices(b, nodes, edges):
     info = np.stack([order, first[order], deg[order], z[order]], axis=1).astype(np.int32)
     b._store["_x2g_pack_info"] = torch.from_numpy(np.ascontiguousarray(info).reshape(-1))
 
+
+# The center kernels' schedule (degree order, the fused forward's packs, atom_info) of a collated batch: made
+# here on the host (center_packs: best fit over the whole batch) or, False, on the device when the step builds
+# the batch's line graph (ops.center_schedule: best fit per molecule), which takes it off the collate.
+HOST_SCHEDULE = True
 
 CENTER_PACK_ROWS = 16  # the center kernels' half-wave owners per workgroup (csrc/attention_center.hip)
 CENTER_PACK_MEMBERS = 16
@@ -328,7 +342,28 @@ def molecule_to_data(mol: dict) -> Data:
 
 
 def collate(mols) -> Batch:
-    """Molecule dicts -> collated ``Batch`` on the host."""
-    b = Batch.from_data_list([molecule_to_data(m) for m in mols])
-    b._store["y"] = b._store["y"].to(torch.float32)
+    """Molecule dicts -> collated ``Batch`` on the host: Batch.from_data_list([molecule_to_data(m) ...]) (PyG's
+    collate restated, with y as float32) computed straight from the dicts' arrays — one numpy concatenation
+    per key instead of a Data object and five tensors per molecule (tests/test_host.py checks the two equal)."""
+    B = len(mols)
+    nodes = np.fromiter((len(m["x"]) for m in mols), dtype=np.int64, count=B)
+    edges = np.fromiter((int(m["edge_num"]) for m in mols), dtype=np.int64, count=B)
+    trips = np.fromiter((int(m["triplet_num"]) for m in mols), dtype=np.int64, count=B)
+    offs = np.concatenate([[0], np.cumsum(nodes)[:-1]])
+    b = Batch()
+    object.__setattr__(b, "_meta", {"nodes": nodes, "edges": edges, "triplets": trips})
+    st = b._store
+    st["x"] = torch.from_numpy(np.concatenate([np.asarray(m["x"], dtype=np.int64).reshape(-1) for m in mols]))
+    st["atom_pos"] = torch.from_numpy(np.concatenate([np.asarray(m["atom_pos"], dtype=np.float32).reshape(-1, 3)
+                                                      for m in mols]))
+    st["edge_index"] = torch.from_numpy(np.concatenate(
+        [np.asarray(m["edge_index"], dtype=np.int64).reshape(2, -1) + o for m, o in zip(mols, offs)], axis=1))
+    if "edge_attr" in mols[0]:
+        st["edge_attr"] = torch.from_numpy(np.concatenate([np.asarray(m["edge_attr"], dtype=np.float32)
+                                                           for m in mols]))
+    st["edge_num"] = torch.from_numpy(edges.copy())
+    st["y"] = torch.from_numpy(np.array([float(m.get("y", 0.0)) for m in mols], dtype=np.float32))
+    st["batch"] = torch.repeat_interleave(torch.arange(B), torch.from_numpy(nodes))
+    st["ptr"] = torch.from_numpy(np.concatenate([[0], np.cumsum(nodes)]))
+    _add_device_indices(b, nodes, edges)
     return b

@@ -405,6 +405,24 @@ def _center_split(lg):
     return order, None, None, [(sf, 0, units, rows, 0)]
 
 
+def center_schedule(atom_rowptr, mol_ptr, src_row, num_atoms: int, num_graphs: int):
+    """The center kernels' schedule made on the device (x2g_center_schedule): (center_order [N], pack_order [N],
+    pack_ptr [N + 1], atom_info [N * 4]) — the same kind data.center_packs makes on the host, per molecule; its
+    hub units sit among the packs (LineGraph.center_mixed)."""
+    n = int(num_atoms)
+    dev = atom_rowptr.device
+    off = 4 * ((3 * n + 1 + 3) // 4)  # atom_info 16-byte aligned after the order / pack order / pack_ptr
+    buf = torch.empty(off + 4 * n, dtype=torch.int32, device=dev)
+    c_order, p_order, p_ptr = torch.split(buf[:3 * n + 1], [n, n, n + 1])
+    info = buf[off:off + 4 * n]
+    lib = _lib.load()
+    ws_b = int(lib.x2g_center_schedule_workspace())
+    ws = torch.empty(ws_b, dtype=torch.uint8, device=dev)
+    call("x2g_center_schedule", ptr(atom_rowptr), ptr(mol_ptr), ptr(src_row), n, int(num_graphs), ptr(c_order),
+         ptr(p_order), ptr(p_ptr), ptr(info), ptr(ws), ws_b, stream_ptr())
+    return c_order, p_order, p_ptr, info
+
+
 def _center_launch(launches, common, outs):
     for entry, u0, n, rows, skip in launches:
         if entry.endswith("_tiled"):

@@ -82,6 +82,10 @@ class GraphPlan:
             p.lg.pack_info = st.get("_x2g_pack_info")
             p.lg.center_hubs = st.get("_x2g_center_hubs", 0)
             p.lg.center_mixed = st.get("_x2g_center_mixed", False)
+            if st.get("_x2g_device_schedule", False) and p.lg.edge_rev is not None:  # (data.HOST_SCHEDULE False)
+                sched = ops.center_schedule(p.lg.atom_rowptr, p.mol_ptr, src_type, p.num_atoms, p.num_graphs)
+                p.lg.center_order, p.lg.pack_order, p.lg.center_packs, p.lg.pack_info = sched
+                p.lg.center_rows, p.lg.center_mixed = ops.CENTER_SF_MAX_ROWS, True
         else:
             p.lg = ops.vertex_to_edge(ei, p.num_atoms, p.num_triplets, meta.get("symmetric", False))
             p.line_ptr = _ptr_from_counts(data.edge_num, p.num_graphs, dev)
