@@ -127,6 +127,7 @@ def parse():
     ap.add_argument("--shape", default="S160", choices=["S160", "S5A"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-loader", action="store_true", help="skip the fresh-batch DataLoader side field")
+    ap.add_argument("--no-lazy-sbf", action="store_true", help="write the [T, 42] sbf rows (ops.LAZY_SBF False)")
     ap.add_argument("--device-schedule", action="store_true",
                     help="collate without the center schedule: the step makes it on the device (data.HOST_SCHEDULE)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
@@ -727,6 +728,8 @@ def cpu_baseline(mols, budget_s, global_pool=None, train=True, sample=None):
 # ------------------------------------------------------------------------------------------ main
 def main():
     args = parse()
+    if args.no_lazy_sbf:
+        ops.LAZY_SBF = False
     if args.device_schedule:
         import x2gnn.data as xdata
 

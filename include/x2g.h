@@ -298,22 +298,22 @@ int x2g_sbf_attention_fwd_center(const float* q, const float* k, const float* v,
 
 /* The center-atom kernels' schedule made on the device, for a batch that does not carry collate's
  * (data.center_packs; the reference trainer's PyG batch, trainer.py:25-27,37-40): from the atoms' out-edge
- * row pointer atom_rowptr [N + 1], the molecules' atom row pointer mol_ptr [B + 1] (atoms of molecule m:
- * mol_ptr[m] .. mol_ptr[m + 1] - 1, covering 0 .. N - 1) and src_row [E] (or NULL), writes
+ * row pointer atom_rowptr [N + 1] and src_row [E] (or NULL), writes
  *   center_order [N]: every atom by decreasing degree (the center backward's workgroups);
- *   pack_order [N], pack_ptr [N + 1], atom_info [N, 4] (16-byte aligned): the fused forward's units, per
- *   molecule its atoms by decreasing degree packed best-fit into units of <= 16 rows and <= 16 atoms (an atom
- *   of degree >= 16 alone; one atom per unit in a molecule of more than 64 atoms), unit slots = the
- *   molecule's atom slots, unused slots empty (pack_ptr[s] == pack_ptr[s + 1]): launch the fused forwards over
- *   all N units (x2g_sbf_attention_fwd_center_sf with max_rows 17 leaves out the units of more rows,
- *   x2g_sbf_attention_fwd_center_sf_tiled with skip_rows 17 takes exactly those).
- * workspace: x2g_center_schedule_workspace() bytes.  Two launches and a memset on the stream, no host read.
- * The order among atoms of equal degree follows integer atomics; no output of the center kernels depends on
- * it. */
-size_t x2g_center_schedule_workspace(void);
-int x2g_center_schedule(const int32_t* atom_rowptr, const int32_t* mol_ptr, const int32_t* src_row,
-                        int64_t num_atoms, int64_t num_graphs, int32_t* center_order, int32_t* pack_order,
-                        int32_t* pack_ptr, int32_t* atom_info, void* workspace, size_t ws_bytes, void* stream);
+ *   pack_order [N], pack_ptr [N + 1], atom_info [N, 4] (16-byte aligned): the fused forward's units — per
+ *   window of 64 consecutive atoms its atoms by decreasing degree packed best-fit into units of <= 16 rows and
+ *   <= 16 atoms (an atom of degree >= 16 alone) — in one list by decreasing largest degree, units 0 .. U - 1,
+ *   the slots U .. N - 1 empty (pack_ptr[s] == pack_ptr[s + 1] == N): launch the fused forwards over all N
+ *   units (x2g_sbf_attention_fwd_center_sf with max_rows 17 leaves out the units of more rows,
+ *   x2g_sbf_attention_fwd_center_sf_tiled with skip_rows 17 takes exactly those; the empty slots leave at once).
+ * workspace: x2g_center_schedule_workspace(N) bytes, 8-byte aligned.  Three launches and a memset on the
+ * stream, no host read.  The order among atoms (units) of equal degree follows integer atomics; no output of
+ * the center kernels depends on it.  (ABI 17; ABI 16 took mol_ptr / num_graphs and left the units in
+ * per-molecule slots.) */
+size_t x2g_center_schedule_workspace(int64_t num_atoms);
+int x2g_center_schedule(const int32_t* atom_rowptr, const int32_t* src_row, int64_t num_atoms,
+                        int32_t* center_order, int32_t* pack_order, int32_t* pack_ptr, int32_t* atom_info,
+                        void* workspace, size_t ws_bytes, void* stream);
 
 /* Workgroup UNITS of the fused-projection center forward below: with pack_ptr (int32 [units + 1], or NULL)
  * unit u is the PACK of center atoms atom_order[pack_ptr[u]] .. atom_order[pack_ptr[u + 1] - 1] (at most

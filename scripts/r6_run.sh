@@ -22,12 +22,15 @@ PT="python -u -m pytest -q -rf --timeout 300 --timeout-method thread -m gpu"
 for s in "$@"; do
   case $s in
     kc) step kc 400 $PT tests/test_gpu_kernels.py -k "center" ;;
+    opt) step opt 300 $PT tests/test_gpu_kernels.py -k "flat_adam" ;;
+    kch) step kch 400 $PT tests/test_gpu_kernels.py -k "chain or tiled or wgrad or schedule" ;;
     model) step model 600 $PT tests/test_gpu_model.py ;;
     dist) step dist 600 $PT tests/test_dist_gpu.py tests/test_rccl_gpu.py ;;
     gpu) step gputests 1000 $PT tests ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     c2) step bench_c2 300 python bench.py --no-cpu-baseline ;;
     c2full) step bench_c2full 420 python bench.py ;;
+    c2dev) step bench_c2dev 300 python bench.py --no-cpu-baseline --device-schedule ;;
     s5a) step bench_s5a 300 python bench.py --shape S5A --no-cpu-baseline ;;
     c3) step bench_c3 300 python bench.py --workload qm9_allprop --target 0 --no-cpu-baseline ;;
     c5) step bench_c5 300 python bench.py --workload aid_infer --steps 50 --warmup 5 --no-cpu-baseline ;;

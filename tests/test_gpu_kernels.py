@@ -2367,7 +2367,8 @@ def test_center_fused_source_tiles_equal_projected(cuda, graph):
 def test_device_center_schedule(cuda, graph):
     """x2g_center_schedule (the center kernels' schedule made on the device, for batches without collate's):
     center_order is a permutation by non-increasing degree; every atom sits in exactly one unit, a unit of
-    several atoms holds <= 16 rows and <= 16 atoms, units stay inside their molecule's slots; atom_info
+    several atoms holds <= 16 rows and <= 16 atoms from one 64-atom window, the units come by non-increasing
+    largest degree and the empty slots after them; atom_info
     matches the line graph; and the fused forward over it (both forms over all unit slots, each leaving out
     the other's units) equals the forward over collate's host schedule bit for bit."""
     from x2gnn import ops
@@ -2377,29 +2378,33 @@ def test_device_center_schedule(cuda, graph):
 
     if graph == "s160":
         b = collate(synthetic_molecules(128, "S160", seed=21))
-    else:  # degrees up to ~50; a molecule of > 64 atoms takes the one-atom-per-unit layout
+    else:  # degrees up to ~50, molecules of more than 64 atoms (windows inside and across molecules)
         b = collate(molecules_from_geometry_file(os.path.join(GOLDEN, "aid_geom.npz"), indices=[0, 5, 9, 30], seed=0))
-    ei, n, B = b.edge_index.numpy(), b.num_nodes, b.num_graphs
+    ei, n = b.edge_index.numpy(), b.num_nodes
     lg = _sym_lg(ei, n, cuda)
     deg = np.bincount(ei[0], minlength=n)
-    mol_ptr = torch.from_numpy(np.concatenate([[0], np.cumsum(b._meta["nodes"])]).astype(np.int32)).to(cuda)
     i32 = dict(dtype=torch.int32, device=cuda)
     c_order, p_order, p_ptr = torch.full((n,), -1, **i32), torch.full((n,), -1, **i32), torch.full((n + 1,), -1, **i32)
     info = torch.full((4 * n,), -1, **i32)
-    ws_b = int(_lib_mod().x2g_center_schedule_workspace())
+    ws_b = int(_lib_mod().x2g_center_schedule_workspace(n))
     ws = torch.empty(ws_b, dtype=torch.uint8, device=cuda)
-    call("x2g_center_schedule", ptr(lg.atom_rowptr), ptr(mol_ptr), ptr(lg.src_type), n, B, ptr(c_order), ptr(p_order),
-         ptr(p_ptr), ptr(info), ptr(ws), ws_b, stream_ptr())
+    call("x2g_center_schedule", ptr(lg.atom_rowptr), ptr(lg.src_type), n, ptr(c_order), ptr(p_order), ptr(p_ptr),
+         ptr(info), ptr(ws), ws_b, stream_ptr())
     co, po, pp = c_order.cpu().numpy(), p_order.cpu().numpy(), p_ptr.cpu().numpy()
     assert np.array_equal(np.sort(co), np.arange(n)) and (np.diff(deg[co]) <= 0).all()
     assert np.array_equal(np.sort(po), np.arange(n)) and pp[0] == 0 and pp[n] == n and (np.diff(pp) >= 0).all()
-    mp = mol_ptr.cpu().numpy()
-    for m in range(B):
-        for s in range(mp[m], mp[m + 1]):
-            mem = po[pp[s]:pp[s + 1]]
-            assert ((mem >= mp[m]) & (mem < mp[m + 1])).all()
-            if len(mem) > 1:
-                assert deg[mem].sum() <= 16 and len(mem) <= 16
+    keys, n_units = [], 0
+    for u in range(n):
+        mem = po[pp[u]:pp[u + 1]]
+        if len(mem) == 0:
+            continue
+        assert u == n_units, "empty unit slots only after the units"
+        n_units += 1
+        assert (mem // 64 == mem[0] // 64).all()
+        if len(mem) > 1:
+            assert deg[mem].sum() <= 16 and len(mem) <= 16
+        keys.append(min(deg[mem].max(), 128))
+    assert (np.diff(keys) <= 0).all() and (pp[n_units:] == n).all()
     inf = info.cpu().numpy().reshape(n, 4)
     rp = lg.atom_rowptr.cpu().numpy()
     st = lg.src_type.cpu().numpy()

@@ -908,7 +908,7 @@ def test_two_models_on_two_streams_equal_serial(cuda):
 @pytest.mark.parametrize("shape", ["S160", "aid"])
 def test_device_schedule_equals_host_schedule(cuda, monkeypatch, shape):
     """data.HOST_SCHEDULE False: collate leaves the center kernels' schedule out and the step makes it on the
-    device (ops.center_schedule, x2g_center_schedule: per-molecule packs, hub units among them) — energies and
+    device (ops.center_schedule, x2g_center_schedule: packs per 64-atom window, hub units among them) — energies and
     every parameter gradient equal the host-scheduled batch's bit for bit (no output of the center kernels
     depends on the packing or the order)."""
     import os
@@ -936,6 +936,35 @@ def test_device_schedule_equals_host_schedule(cuda, monkeypatch, shape):
         assert names.count("x2g_center_schedule") == (0 if host else 1)
         assert "x2g_sbf_project" not in names
         out.append((e.detach().cpu(), [p.grad.detach().cpu().clone() for p in m.parameters() if p.grad is not None]))
+    assert torch.equal(out[0][0], out[1][0])
+    for a, r in zip(out[0][1], out[1][1]):
+        assert torch.equal(a, r)
+
+
+@pytest.mark.parametrize("fixture", ["model_full.npz", "model_small.npz", "model_aid.npz"])
+@pytest.mark.parametrize("path", ["shipped", "dst_major"])
+def test_lazy_sbf_equals_materialized(cuda, monkeypatch, fixture, path):
+    """ops.LAZY_SBF: the model's forward leaves the [T, 42] sbf rows unwritten (the fused center forward reads
+    only their factors) and materialize_sbf fills them for any consumer that reads them (the S projection of
+    the destination-major path, D = 32): energies and every gradient equal the always-written run bit for
+    bit, and on the fused path no sbf row is written at all."""
+    from x2gnn import ops
+
+    z = golden(fixture)
+    out = []
+    for lazy in (True, False):
+        monkeypatch.setattr(ops, "LAZY_SBF", lazy)
+        m = product_model(z, cuda)
+        b = batch_from_fixture(z, shipped=path == "shipped").to(cuda)
+        seen = record_calls(monkeypatch)
+        res = m(b)
+        torch.nn.functional.smooth_l1_loss(res, b.y).backward()
+        torch.cuda.synchronize()
+        sph = [a for n, a in seen if n == "x2g_spherical_basis"]
+        fused = path == "shipped" and model_cfg(z)["in_channels"] == 128
+        if lazy and fused:  # one launch, factors only (sbf output NULL)
+            assert len(sph) == 1 and sph[0][10] is None
+        out.append((res.detach().cpu(), [p.grad.detach().cpu().clone() for p in m.parameters() if p.grad is not None]))
     assert torch.equal(out[0][0], out[1][0])
     for a, r in zip(out[0][1], out[1][1]):
         assert torch.equal(a, r)

@@ -22,7 +22,7 @@ def test_library_built_and_loads():
 
     assert os.path.exists(_lib.LIB_PATH), "run `make -C x2-gnn_amd` (or __graft_entry__.build())"
     lib = _lib.load()
-    assert lib.x2g_abi_version() == 16
+    assert lib.x2g_abi_version() == 17
 
 
 def test_every_declared_symbol_is_exported_and_bound():

@@ -625,7 +625,7 @@ X2G_API int x2g_batch_meta(const int64_t* edge_index, const int64_t* x, const in
   return last_launch_status();
 }
 
-X2G_API int x2g_abi_version(void) { return 16; }
+X2G_API int x2g_abi_version(void) { return 17; }
 
 X2G_API const char* x2g_status_string(int status) {
   switch (status) {
@@ -831,55 +831,88 @@ namespace x2g {
 // The center-atom attention kernels' workgroup schedule made on the device (a batch made elsewhere — the
 // reference trainer's PyG DataLoader batch, trainer.py:25-27,37-40 — carries none; x2gnn's collate makes the
 // same kind of schedule on the host, data.center_packs):
-//   * the fused forward's UNITS: per molecule, its atoms by decreasing degree packed best-fit into units of
-//     <= 16 rows and <= 16 members (an atom of degree >= 16 alone, atoms without edges 16 to a unit), one wave
-//     per molecule: the units' remaining rows sit one per lane and each atom's best fit is a wave minimum.
-//     Unit slots are the molecule's atom slots [mol_ptr[m], mol_ptr[m + 1]): slot s holds unit s - mol_ptr[m]
-//     of the molecule, or nothing (pack_ptr[s] == pack_ptr[s + 1]), so the layout needs no global scan and a
-//     launch over all N slots covers every unit (empty slots leave at once).  A molecule of more than 64 atoms
-//     gets one atom per unit.
+//   * the fused forward's UNITS: per window of 64 consecutive atoms, its atoms by decreasing degree packed
+//     best-fit into units of <= 16 rows and <= 16 members (an atom of degree >= 16 alone, atoms without edges
+//     16 to a unit), one wave per window: the units' remaining rows sit one per lane and each atom's best
+//     fit is a 4-step ballot minimum over the lanes (no cross-lane shuffles in the serial loop).  A unit may
+//     span molecules (nothing in the center kernels is per molecule).
+//   * the units then in ONE list by decreasing largest degree (collate's order: the longest workgroups start
+//     first, so no heavy unit is dispatched at the launch's tail) and compact (units 0 .. U - 1, slots U .. N
+//     empty): a histogram of the units' keys and member counts, its suffix sums, and each unit's place from
+//     one 64-bit atomic per unit on its key's (units, members) cursor — the unit index and the first member
+//     position come from the same atomic, so pack_ptr stays monotonic.
 //   * atom_info per position of pack_order: (atom, first out-edge, degree, src_row of its first out-edge).
-//   * center_order: every atom by decreasing degree (the backward's one-atom workgroups, longest first): a
-//     degree histogram (integer atomics), then each atom's position from the histogram's suffix sum and a
-//     per-degree cursor.  The order among atoms of one degree follows the atomics: no output of the center
-//     kernels depends on it (each atom's block is computed whole by one workgroup in a fixed order).
+//   * center_order: every atom by decreasing degree (the backward's one-atom workgroups, longest first): the
+//     degree histogram's suffix sums and a per-degree cursor.
+// The order among atoms (units) of one degree (key) follows the atomics: no output of the center kernels
+// depends on it (each atom's block is computed whole by one workgroup in a fixed order).
+// Round 6's first forms, units in per-molecule (then per-window) slot order with empty slots between them,
+// ran the fused forwards 45 % (config 2) and 50 % (config 5) slower than collate's ordered list
+// (profiles/r6j_sched_kernels.txt): heavy units dispatched late and empty workgroups interleaved.
 constexpr int kSchedCap = 16;       // rows per unit (data.CENTER_PACK_ROWS)
 constexpr int kSchedMembers = 16;   // atoms per unit (data.CENTER_PACK_MEMBERS)
-constexpr int kSchedDeg = 128;      // degree histogram bins (X2G_CENTER_MAX_DEGREE; larger degrees share the last)
+constexpr int kSchedDeg = 128;      // degree / key bins (X2G_CENTER_MAX_DEGREE; larger degrees share the last)
+constexpr int kSchedWin = 64;       // atoms per window (one wave)
+constexpr int kSchedBins = kSchedDeg + 1;
 
-__device__ __forceinline__ int wave_min_i(int v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
-  return v;
+// workspace (int32 words): atom degree histogram and cursors, unit (units << 32 | members) histogram and
+// cursors (64-bit), the three suffix sums, then per atom slot the window-local pack order, the unit word of
+// the window's unit slots and per window-local position (unit, index in it)
+struct SchedWs {
+  int32_t* hist;
+  int32_t* acur;
+  unsigned long long* ubin;
+  unsigned long long* ucur;
+  int32_t* apre;
+  int32_t* upre;
+  int32_t* mpre;
+  int32_t* t_order;
+  int32_t* t_unit;
+  int32_t* t_posu;
+};
+constexpr int kSchedUbinWord = (2 * kSchedBins + 1) & ~1;           // 8-byte aligned
+constexpr int kSchedApreWord = kSchedUbinWord + 4 * kSchedBins;      // (the memset clears the words before)
+constexpr int kSchedTempWord = kSchedApreWord + 3 * kSchedBins;
+
+inline SchedWs sched_ws(void* base, int64_t N) {
+  int32_t* w = static_cast<int32_t*>(base);
+  SchedWs r;
+  r.hist = w;
+  r.acur = w + kSchedBins;
+  r.ubin = reinterpret_cast<unsigned long long*>(w + kSchedUbinWord);
+  r.ucur = r.ubin + kSchedBins;
+  r.apre = w + kSchedApreWord;
+  r.upre = r.apre + kSchedBins;
+  r.mpre = r.upre + kSchedBins;
+  r.t_order = w + kSchedTempWord;
+  r.t_unit = r.t_order + N;
+  r.t_posu = r.t_unit + N;
+  return r;
 }
 
-__global__ void __launch_bounds__(64) center_pack_mol_kernel(const int32_t* __restrict__ rowptr,
-                                                             const int32_t* __restrict__ mol_ptr,
-                                                             const int32_t* __restrict__ src_row, int64_t B,
-                                                             int32_t* __restrict__ pack_order,
-                                                             int32_t* __restrict__ pack_ptr, int4* __restrict__ info,
-                                                             int32_t* __restrict__ hist) {
-  __shared__ int sd[64], sa[64], unit_of[64], idx_in[64];
-  const int m = blockIdx.x, lane = threadIdx.x;
-  const int a0 = mol_ptr[m], a1 = mol_ptr[m + 1], na = a1 - a0;
-  auto deg = [&](int a) { return rowptr[a + 1] - rowptr[a]; };
-  auto put = [&](int pos, int a, int d) {
-    pack_order[pos] = a;
-    info[pos] = make_int4(a, rowptr[a], d, (src_row && d > 0) ? src_row[rowptr[a]] : 0);
-  };
-  for (int a = a0 + lane; a < a1; a += 64) atomicAdd(&hist[min(deg(a), kSchedDeg)], 1);
-  if (m == B - 1 && lane == 0) pack_ptr[a1] = a1;  // the slots' end
-  if (na > 64) {  // one atom per unit, in index order
-    for (int a = a0 + lane; a < a1; a += 64) {
-      pack_ptr[a] = a;
-      put(a, a, deg(a));
-    }
-    return;
+// minimum over the wave's lanes of a 4-bit value v among the lanes with ok set: the mask of the lanes
+// holding it (0 when no lane is ok), by ballots from the top bit down
+__device__ __forceinline__ unsigned long long ballot_min4(bool ok, int v) {
+  unsigned long long cand = __ballot(ok);
+#pragma unroll
+  for (int bit = 3; bit >= 0; --bit) {
+    const unsigned long long zero = cand & __ballot(((v >> bit) & 1) == 0);
+    if (zero) cand = zero;
   }
-  const int d = lane < na ? deg(a0 + lane) : -1;
+  return cand;
+}
+
+__global__ void __launch_bounds__(64) center_pack_window_kernel(const int32_t* __restrict__ rowptr, int64_t N,
+                                                                SchedWs ws) {
+  __shared__ int sd[kSchedWin], sa[kSchedWin];
+  const int lane = threadIdx.x;
+  const int a0 = kSchedWin * static_cast<int>(blockIdx.x);
+  const int na = static_cast<int>(N - a0 < kSchedWin ? N - a0 : kSchedWin);
+  const int d = lane < na ? rowptr[a0 + lane + 1] - rowptr[a0 + lane] : -1;
+  if (lane < na) atomicAdd(&ws.hist[min(d, kSchedDeg)], 1);
   int rank = 0;  // by decreasing degree, ties by index
   for (int k = 0; k < na; ++k) {
-    const int dk = __shfl(d, k, 64);
+    const int dk = __builtin_amdgcn_readlane(d, k);
     rank += (dk > d || (dk == d && k < lane)) ? 1 : 0;
   }
   if (lane < na) {
@@ -887,36 +920,39 @@ __global__ void __launch_bounds__(64) center_pack_mol_kernel(const int32_t* __re
     sa[rank] = lane;
   }
   __syncthreads();
-  // unit u's state in lane u: rows left, members, whether it holds atoms without edges
-  int space = 0, mem = 0, zero = 0, nu = 0;
+  const int sdv = lane < na ? sd[lane] : 0;  // lane r: the r-th degree (read below with readlane: no LDS
+                                             // round trip in the serial loop)
+  // unit u's state in lane u: rows left, members, whether it holds atoms without edges, its key (the degree
+  // of its first, largest atom); atom r's unit and index in it end in lane r
+  int space = 0, mem = 0, zero = 0, key = 0, nu = 0, my_u = 0, my_idx = 0;
   for (int r = 0; r < na; ++r) {
-    const int dr = sd[r];
-    int key = 0x7fffffff;
-    if (dr > 0 && dr < kSchedCap) {  // best fit: the fullest unit that takes it (lowest lane on ties)
-      if (lane < nu && !zero && space >= dr && mem < kSchedMembers) key = (space << 6) | lane;
-    } else if (dr == 0) {  // atoms without edges: with each other
-      if (lane < nu && zero && mem < kSchedMembers) key = lane;
-    }
-    key = wave_min_i(key);
+    const int dr = __builtin_amdgcn_readlane(sdv, r);
+    const bool open = lane < nu && mem < kSchedMembers;
+    unsigned long long m = 0;
+    if (dr > 0 && dr < kSchedCap)  // best fit: the fullest unit that takes it (lowest lane on ties)
+      m = ballot_min4(open && !zero && space >= dr, space);
+    else if (dr == 0)  // atoms without edges: with each other
+      m = __ballot(open && zero);
     int u;
-    if (key == 0x7fffffff) {
+    if (m == 0) {
       u = nu++;
       if (lane == u) {
         space = dr >= kSchedCap ? 0 : kSchedCap - dr;
         zero = dr == 0;
+        key = min(dr, kSchedDeg);
       }
     } else {
-      u = key & 63;
+      u = static_cast<int>(__builtin_ctzll(m));
       if (lane == u) space -= dr;
     }
-    const int before = __shfl(mem, u, 64);
+    const int before = __builtin_amdgcn_readlane(mem, u);
     if (lane == u) ++mem;
-    if (lane == 0) {
-      unit_of[r] = u;
-      idx_in[r] = before;
+    if (lane == r) {
+      my_u = u;
+      my_idx = before;
     }
   }
-  // the units' first positions: exclusive scan of their member counts
+  // the units' window-local first positions: exclusive scan of their member counts
   int inc = lane < nu ? mem : 0;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -924,48 +960,111 @@ __global__ void __launch_bounds__(64) center_pack_mol_kernel(const int32_t* __re
     if (lane >= o) inc += v;
   }
   const int start = inc - (lane < nu ? mem : 0);
-  __syncthreads();
+  const int ustart = __shfl(start, my_u, 64);
   if (lane < na) {
-    pack_ptr[a0 + lane] = a0 + (lane < nu ? start : na);
-    const int r = lane;  // the r-th atom by degree
-    const int u = unit_of[r];
-    const int pos = a0 + __shfl(start, u, 64) + idx_in[r];
-    put(pos, a0 + sa[r], sd[r]);
+    ws.t_order[a0 + ustart + my_idx] = a0 + sa[lane];
+    ws.t_posu[a0 + ustart + my_idx] = (my_u << 8) | my_idx;
+  }
+  if (lane < na) {
+    if (lane < nu) {
+      ws.t_unit[a0 + lane] = (key << 16) | (start << 8) | mem;
+      atomicAdd(&ws.ubin[key], (1ull << 32) | static_cast<unsigned long long>(mem));
+    } else {
+      ws.t_unit[a0 + lane] = -1;
+    }
   }
 }
 
-__global__ void center_order_kernel(const int32_t* __restrict__ rowptr, int64_t N, const int32_t* __restrict__ hist,
-                                    int32_t* __restrict__ cursor, int32_t* __restrict__ order) {
-  const int64_t a = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (a >= N) return;
-  const int d = min(rowptr[a + 1] - rowptr[a], kSchedDeg);
-  int start = 0;
-  for (int e = kSchedDeg; e > d; --e) start += hist[e];
-  order[start + atomicAdd(&cursor[d], 1)] = static_cast<int32_t>(a);
+// suffix sums over the bins (largest key first) and the empty slots' pack_ptr
+__global__ void __launch_bounds__(256) center_sched_scan_kernel(int64_t N, SchedWs ws, int32_t* __restrict__ pack_ptr) {
+  __shared__ int h[kSchedBins], uu[kSchedBins], mm[kSchedBins];
+  __shared__ int total_units;
+  const int t = threadIdx.x;
+  if (t < kSchedBins) {
+    h[t] = ws.hist[t];
+    const unsigned long long b = ws.ubin[t];
+    uu[t] = static_cast<int>(b >> 32);
+    mm[t] = static_cast<int>(b & 0xffffffffull);
+  }
+  __syncthreads();
+  if (t < kSchedBins) {
+    int sa = 0, su = 0, sm = 0;
+    for (int e = kSchedDeg; e > t; --e) {
+      sa += h[e];
+      su += uu[e];
+      sm += mm[e];
+    }
+    ws.apre[t] = sa;
+    ws.upre[t] = su;
+    ws.mpre[t] = sm;
+    if (t == 0) total_units = su + uu[0];
+  }
+  __syncthreads();
+  for (int64_t s = total_units + t; s <= N; s += 256) pack_ptr[s] = static_cast<int32_t>(N);
+}
+
+// one wave per window: its units' places (one atomic per unit), then its atoms' positions (lane p: the
+// window's p-th atom in pack order) — every dependent chain a few loads long
+__global__ void __launch_bounds__(64) center_sched_place_kernel(const int32_t* __restrict__ rowptr,
+                                                                const int32_t* __restrict__ src_row, int64_t N,
+                                                                SchedWs ws, int32_t* __restrict__ center_order,
+                                                                int32_t* __restrict__ pack_order,
+                                                                int32_t* __restrict__ pack_ptr,
+                                                                int4* __restrict__ info) {
+  __shared__ int mb[kSchedWin];
+  const int lane = threadIdx.x;
+  const int64_t a0 = static_cast<int64_t>(kSchedWin) * blockIdx.x;
+  const int na = static_cast<int>(N - a0 < kSchedWin ? N - a0 : kSchedWin);
+  const int64_t s = a0 + lane;
+  int d = 0;
+  if (lane < na) {
+    d = min(rowptr[s + 1] - rowptr[s], kSchedDeg);
+    center_order[ws.apre[d] + atomicAdd(&ws.acur[d], 1)] = static_cast<int32_t>(s);
+    const int tu = ws.t_unit[s];
+    if (tu >= 0) {  // lane u < nu: unit u of the window
+      const int key = tu >> 16, mem = tu & 0xff;
+      const unsigned long long cur = atomicAdd(&ws.ucur[key], (1ull << 32) | static_cast<unsigned long long>(mem));
+      const int mbase = ws.mpre[key] + static_cast<int>(cur & 0xffffffffull);
+      pack_ptr[ws.upre[key] + static_cast<int>(cur >> 32)] = mbase;
+      mb[lane] = mbase;
+    }
+  }
+  __syncthreads();
+  if (lane < na) {
+    const int a = ws.t_order[s], pu = ws.t_posu[s];
+    const int pos = mb[pu >> 8] + (pu & 0xff);
+    const int r = rowptr[a], da = rowptr[a + 1] - r;
+    pack_order[pos] = a;
+    info[pos] = make_int4(a, r, da, (src_row && da > 0) ? src_row[r] : 0);
+  }
 }
 
 }  // namespace x2g
 
-X2G_API size_t x2g_center_schedule_workspace(void) { return 2 * (x2g::kSchedDeg + 1) * sizeof(int32_t); }
+X2G_API size_t x2g_center_schedule_workspace(int64_t num_atoms) {
+  return num_atoms < 0 ? 0 : (x2g::kSchedTempWord + 3 * static_cast<size_t>(num_atoms)) * sizeof(int32_t);
+}
 
-X2G_API int x2g_center_schedule(const int32_t* atom_rowptr, const int32_t* mol_ptr, const int32_t* src_row,
-                                int64_t num_atoms, int64_t num_graphs, int32_t* center_order, int32_t* pack_order,
-                                int32_t* pack_ptr, int32_t* atom_info, void* workspace, size_t ws_bytes,
-                                void* stream) {
+X2G_API int x2g_center_schedule(const int32_t* atom_rowptr, const int32_t* src_row, int64_t num_atoms,
+                                int32_t* center_order, int32_t* pack_order, int32_t* pack_ptr, int32_t* atom_info,
+                                void* workspace, size_t ws_bytes, void* stream) {
   using namespace x2g;
-  if (num_atoms < 0 || num_graphs < 0 || num_atoms > 0x7fffffff) return X2G_EINVAL;
-  if (ws_bytes < x2g_center_schedule_workspace() || !workspace) return X2G_EWORKSPACE;
-  if (num_atoms == 0 || num_graphs == 0) return X2G_OK;
-  if (!atom_rowptr || !mol_ptr || !center_order || !pack_order || !pack_ptr || !atom_info) return X2G_EINVAL;
-  if (reinterpret_cast<uintptr_t>(atom_info) % 16 || num_graphs > 0x7fffffff) return X2G_EUNSUPPORTED;
+  if (num_atoms < 0 || num_atoms > 0x7fffffff - kSchedWin) return X2G_EINVAL;
+  if (ws_bytes < x2g_center_schedule_workspace(num_atoms) || !workspace) return X2G_EWORKSPACE;
+  if (num_atoms == 0) return X2G_OK;
+  if (!atom_rowptr || !center_order || !pack_order || !pack_ptr || !atom_info) return X2G_EINVAL;
+  if (reinterpret_cast<uintptr_t>(atom_info) % 16 || reinterpret_cast<uintptr_t>(workspace) % 8)
+    return X2G_EUNSUPPORTED;
   hipStream_t st = as_stream(stream);
-  int32_t* hist = static_cast<int32_t*>(workspace);
-  int32_t* cursor = hist + (kSchedDeg + 1);
-  const hipError_t e = hipMemsetAsync(hist, 0, x2g_center_schedule_workspace(), st);
+  const SchedWs ws = sched_ws(workspace, num_atoms);
+  const hipError_t e = hipMemsetAsync(workspace, 0, kSchedApreWord * sizeof(int32_t), st);
   if (e != hipSuccess) return static_cast<int>(e);
-  center_pack_mol_kernel<<<static_cast<unsigned>(num_graphs), 64, 0, st>>>(
-      atom_rowptr, mol_ptr, src_row, num_graphs, pack_order, pack_ptr, reinterpret_cast<int4*>(atom_info), hist);
+  center_pack_window_kernel<<<static_cast<unsigned>((num_atoms + kSchedWin - 1) / kSchedWin), kSchedWin, 0, st>>>(
+      atom_rowptr, num_atoms, ws);
   if (int rc = last_launch_status()) return rc;
-  center_order_kernel<<<blocks_for(num_atoms, 256), 256, 0, st>>>(atom_rowptr, num_atoms, hist, cursor, center_order);
+  center_sched_scan_kernel<<<1, 256, 0, st>>>(num_atoms, ws, pack_ptr);
+  if (int rc = last_launch_status()) return rc;
+  center_sched_place_kernel<<<static_cast<unsigned>((num_atoms + kSchedWin - 1) / kSchedWin), kSchedWin, 0, st>>>(
+      atom_rowptr, src_row, num_atoms, ws, center_order, pack_order, pack_ptr, reinterpret_cast<int4*>(atom_info));
   return last_launch_status();
 }

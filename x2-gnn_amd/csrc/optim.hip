@@ -1,10 +1,13 @@
 // The reference trainer's parameter update (trainer.py:39-48, train_ema.py:45-48) over ONE flat
 // fp32 parameter buffer: clip_grad_norm_(max_norm) -> Adam(amsgrad=False) -> EMA
 // (AveragedModel with avg_fn = d*avg + (1-d)*p).  torch's capturable Adam issues a few kernels
-// per parameter tensor (~300 launches for X2-GNN's 155 tensors); here it is three launches:
-//   1. per-block partial sums of g^2 over contiguous chunks (fixed order),
-//   2. one block: total norm, clip coefficient, step count + bias corrections -> scalars,
-//   3. elementwise Adam + EMA (a copy of the parameters at step 1, as AveragedModel does).
+// per parameter tensor (~300 launches for X2-GNN's 155 tensors); here it is two launches:
+//   1. per-block partial sums of g^2 over contiguous chunks (fixed order); block 0 also advances
+//      the step count and the learning-rate schedule (no block of this launch reads them),
+//   2. elementwise Adam + EMA (a copy of the parameters at step 1, as AveragedModel does); every
+//      block sums the kNormBlocks partials itself in the same fixed order (1 KB of L2 reads a
+//      block), so all blocks see one bit-identical norm without a finaliser launch or a fence,
+//      and block 0 publishes norm, clip coefficient and bias corrections to the scalar block.
 // Every value the update depends on that changes between steps (step count, norm, clip scale)
 // lives in device memory, so a captured HIP graph replays correctly; the hyper-parameters
 // (lr, betas, eps, max_norm, ema decay) are read from the same device scalar block so a
@@ -15,13 +18,14 @@
 
 namespace x2g {
 
-constexpr int kNormBlocks = 1024;
+constexpr int kNormBlocks = 256;
 constexpr int kNormThreads = 256;
 
 // scalars layout (float[16]); see x2g.h X2G_OPT_*
 __global__ void __launch_bounds__(kNormThreads) grad_sq_partial(const float4* __restrict__ g4,
                                                                 const float* __restrict__ g, int64_t n,
-                                                                float* __restrict__ partial) {
+                                                                float* __restrict__ partial,
+                                                                float* __restrict__ sc) {
   __shared__ float red[kNormThreads];
   const int64_t n4 = n >> 2;
   const int64_t per = (n4 + gridDim.x - 1) / gridDim.x;
@@ -43,13 +47,29 @@ __global__ void __launch_bounds__(kNormThreads) grad_sq_partial(const float4* __
     __syncthreads();
   }
   if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const float step = sc[X2G_OPT_STEP] + 1.0f;
+    sc[X2G_OPT_STEP] = step;
+    if (sc[X2G_OPT_WARMUP] > 0.f) {  // LinearWarmupExponentialDecay.lr_lambda(t), t = steps taken before this one
+      const double w = sc[X2G_OPT_WARMUP], t = static_cast<double>(step) - 1.0;
+      const double warm = fmin(1.0 / w + 1.0 / w * t, 1.0);
+      double ex = t / static_cast<double>(sc[X2G_OPT_DECAY_STEPS]);
+      if (sc[X2G_OPT_STAIRCASE] != 0.f) ex = floor(ex);
+      sc[X2G_OPT_LR] = static_cast<float>(static_cast<double>(sc[X2G_OPT_BASE_LR]) * warm *
+                                          pow(static_cast<double>(sc[X2G_OPT_DECAY_RATE]), ex));
+    }
+  }
 }
 
-__global__ void __launch_bounds__(kNormThreads) opt_finalize(const float* __restrict__ partial, int nparts,
-                                                             float* __restrict__ sc) {
+__global__ void __launch_bounds__(kNormThreads) adam_ema(float* __restrict__ p, float* __restrict__ g,
+                                                         float* __restrict__ m, float* __restrict__ v,
+                                                         float* __restrict__ ema, int64_t n,
+                                                         const float* __restrict__ partial, float* __restrict__ sc,
+                                                         int zero_grads) {
   __shared__ float red[kNormThreads];
+  __shared__ float upd[3];
   float s = 0.f;
-  for (int i = threadIdx.x; i < nparts; i += kNormThreads) s += partial[i];
+  for (int i = threadIdx.x; i < kNormBlocks; i += kNormThreads) s += partial[i];
   red[threadIdx.x] = s;
   __syncthreads();
   for (int off = kNormThreads / 2; off > 0; off >>= 1) {
@@ -61,33 +81,25 @@ __global__ void __launch_bounds__(kNormThreads) opt_finalize(const float* __rest
     const float max_norm = sc[X2G_OPT_MAX_NORM];
     // torch.nn.utils.clip_grad_norm_: coef = max_norm / (norm + 1e-6), clamped to <= 1
     const float coef = max_norm > 0.f ? fminf(max_norm / (norm + 1e-6f), 1.0f) : 1.0f;
-    const float step = sc[X2G_OPT_STEP] + 1.0f;
-    sc[X2G_OPT_STEP] = step;
-    if (sc[X2G_OPT_WARMUP] > 0.f) {  // LinearWarmupExponentialDecay.lr_lambda(t), t = steps taken before this one
-      const double w = sc[X2G_OPT_WARMUP], t = static_cast<double>(step) - 1.0;
-      const double warm = fmin(1.0 / w + 1.0 / w * t, 1.0);
-      double ex = t / static_cast<double>(sc[X2G_OPT_DECAY_STEPS]);
-      if (sc[X2G_OPT_STAIRCASE] != 0.f) ex = floor(ex);
-      sc[X2G_OPT_LR] = static_cast<float>(static_cast<double>(sc[X2G_OPT_BASE_LR]) * warm *
-                                          pow(static_cast<double>(sc[X2G_OPT_DECAY_RATE]), ex));
-    }
-    sc[X2G_OPT_NORM] = norm;
-    sc[X2G_OPT_CLIP] = coef;
-    // bias corrections as torch.optim.Adam computes them (in double, rounded to float)
+    // bias corrections as torch.optim.Adam computes them (in double, rounded to float); the step
+    // count and lr were advanced by grad_sq_partial
+    const double step = sc[X2G_OPT_STEP];
     const double b1 = sc[X2G_OPT_BETA1], b2 = sc[X2G_OPT_BETA2];
-    const double bc1 = 1.0 - pow(b1, static_cast<double>(step));
-    const double bc2 = 1.0 - pow(b2, static_cast<double>(step));
-    sc[X2G_OPT_STEP_SIZE] = static_cast<float>(sc[X2G_OPT_LR] / bc1);
-    sc[X2G_OPT_BC2_SQRT] = static_cast<float>(sqrt(bc2));
+    const float step_size = static_cast<float>(sc[X2G_OPT_LR] / (1.0 - pow(b1, step)));
+    const float bc2s = static_cast<float>(sqrt(1.0 - pow(b2, step)));
+    upd[0] = coef;
+    upd[1] = step_size;
+    upd[2] = bc2s;
+    if (blockIdx.x == 0) {  // published for the caller; no block of this launch reads them back
+      sc[X2G_OPT_NORM] = norm;
+      sc[X2G_OPT_CLIP] = coef;
+      sc[X2G_OPT_STEP_SIZE] = step_size;
+      sc[X2G_OPT_BC2_SQRT] = bc2s;
+    }
   }
-}
-
-__global__ void __launch_bounds__(256) adam_ema(float* __restrict__ p, float* __restrict__ g,
-                                                float* __restrict__ m, float* __restrict__ v,
-                                                float* __restrict__ ema, int64_t n, const float* __restrict__ sc,
-                                                int zero_grads) {
-  const float clip = sc[X2G_OPT_CLIP], b1 = sc[X2G_OPT_BETA1], b2 = sc[X2G_OPT_BETA2];
-  const float eps = sc[X2G_OPT_EPS], step_size = sc[X2G_OPT_STEP_SIZE], bc2s = sc[X2G_OPT_BC2_SQRT];
+  __syncthreads();
+  const float clip = upd[0], step_size = upd[1], bc2s = upd[2];
+  const float b1 = sc[X2G_OPT_BETA1], b2 = sc[X2G_OPT_BETA2], eps = sc[X2G_OPT_EPS];
   const float d = sc[X2G_OPT_EMA_DECAY];
   // AveragedModel.update_parameters copies the parameters on its first call (n_averaged == 0) and
   // applies avg_fn from the second on; the step count is already on the device (graph-safe)
@@ -125,11 +137,11 @@ static int clip_adam_ema(float* params, float* grads, float* exp_avg, float* exp
   if (reinterpret_cast<uintptr_t>(grads) % 16) return X2G_EINVAL;
   hipStream_t st = as_stream(stream);
   float* partial = static_cast<float*>(workspace);
-  grad_sq_partial<<<kNormBlocks, kNormThreads, 0, st>>>(reinterpret_cast<const float4*>(grads), grads, n, partial);
-  opt_finalize<<<1, kNormThreads, 0, st>>>(partial, kNormBlocks, scalars);
-  const int64_t want = (n + 255) / 256;
-  adam_ema<<<static_cast<unsigned>(want < 4096 ? want : 4096), 256, 0, st>>>(params, grads, exp_avg, exp_avg_sq, ema,
-                                                                              n, scalars, zero_grads);
+  grad_sq_partial<<<kNormBlocks, kNormThreads, 0, st>>>(reinterpret_cast<const float4*>(grads), grads, n, partial,
+                                                         scalars);
+  const int64_t want = (n + kNormThreads - 1) / kNormThreads;
+  adam_ema<<<static_cast<unsigned>(want < 2048 ? want : 2048), kNormThreads, 0, st>>>(
+      params, grads, exp_avg, exp_avg_sq, ema, n, partial, scalars, zero_grads);
   return last_launch_status();
 }
 

@@ -145,7 +145,7 @@ def _meta_on_device(data):
     # which then waits for nothing it does not need
     from .ops import center_schedule
 
-    c_order, p_order, p_ptr, a_info = center_schedule(rowptr, mol_ptr, src_t, n, B)
+    c_order, p_order, p_ptr, a_info = center_schedule(rowptr, src_t, n)
     mp_, lp, tr, fl = host[:B + 1], host[B + 1:2 * B + 2], host[2 * B + 2:3 * B + 2], host[3 * B + 2:]
     if fl[2]:
         raise ValueError("edge_index must list each directed edge once, sorted by (source, destination) "
@@ -248,7 +248,7 @@ def _add_device_indices(b, nodes, edges):
 
 # The center kernels' schedule (degree order, the fused forward's packs, atom_info) of a collated batch: made
 # here on the host (center_packs: best fit over the whole batch) or, False, on the device when the step builds
-# the batch's line graph (ops.center_schedule: best fit per molecule), which takes it off the collate.
+# the batch's line graph (ops.center_schedule: best fit per window of 64 atoms), which takes it off the collate.
 HOST_SCHEDULE = True
 
 CENTER_PACK_ROWS = 16  # the center kernels' half-wave owners per workgroup (csrc/attention_center.hip)

@@ -116,11 +116,12 @@ class F_B_2D(nn.Module):
         return ops.spherical_basis_from_angles(Angles, edge_index_1, self.radial(d), self.num_spherical,
                                                self.num_radial)
 
-    def from_positions(self, d, pos, line_graph, radial=None):
+    def from_positions(self, d, pos, line_graph, radial=None, lazy=False):
         """Fast path: angles computed in-kernel from the triplets' atom positions (xgnn.py:61-65);
-        ``radial`` = precomputed ``self.radial(d)`` (x2g_edge_basis writes it)."""
+        ``radial`` = precomputed ``self.radial(d)`` (x2g_edge_basis writes it); ``lazy``: the [T, S] rows
+        are filled only if a consumer reads them (ops.materialize_sbf)."""
         return ops.spherical_basis(pos, line_graph, self.radial(d) if radial is None else radial,
-                                   num_spherical=self.num_spherical, num_radial=self.num_radial)
+                                   num_spherical=self.num_spherical, num_radial=self.num_radial, lazy=lazy)
 
 
 class _ScaleGradByCount(torch.autograd.Function):

@@ -279,7 +279,8 @@ def edge_basis(pos, lg: LineGraph, freq, cutoff: float = 5.0, num_spherical: int
     return _EdgeBasis.apply(freq, pos, lg, cutoff, int(num_spherical), int(num_radial))
 
 
-def spherical_basis(pos, lg: LineGraph, rbf_env, want_cos=False, num_spherical: int = 7, num_radial: int = 6):
+def spherical_basis(pos, lg: LineGraph, rbf_env, want_cos=False, num_spherical: int = 7, num_radial: int = 6,
+                    lazy=False):
     """[T, S] sbf = rbf_env[src] * Y_l0(theta) (S = num_spherical * num_radial, l-major), theta from
     the triplet's atom positions.
 
@@ -299,10 +300,34 @@ def spherical_basis(pos, lg: LineGraph, rbf_env, want_cos=False, num_spherical: 
     sf_fits = getattr(lg, "max_degree", None) is not None and lg.max_degree <= CENTER_MAX_DEGREE
     fold = _FOLD_SBF and (num_spherical, num_radial) == FOLD_BASIS and (torch.is_grad_enabled() or sf_fits)
     ylm = torch.empty(lg.T, 8, dtype=torch.float32, device=pos.device) if fold else None
+    # lazy (the model's own forward): only the factors are written; the [T, S] rows are filled by
+    # materialize_sbf when a consumer reads them (the fused center forward never does: 586 MB per step at
+    # config 5, 33 MB at config 2)
+    lazy = lazy and fold and not want_cos
     call("x2g_spherical_basis", ptr(pos), ptr(lg.atom_i), ptr(lg.atom_j), ptr(lg.atom_k), None, ptr(lg.trip_src),
-         ptr(rbf_env), lg.T, num_spherical, num_radial, ptr(out), ptr(cos_t), ptr(ylm), stream_ptr())
+         ptr(rbf_env), lg.T, num_spherical, num_radial, None if lazy else ptr(out), ptr(cos_t), ptr(ylm),
+         stream_ptr())
     lg.sbf_factors = (out, rbf_env, ylm) if ylm is not None else None
+    lg.sbf_pending = (out, pos, rbf_env, num_spherical, num_radial) if lazy else None
     return (out, cos_t) if want_cos else out
+
+
+# The model's own forward asks spherical_basis for the factors only (lazy sbf rows): False = always write
+# the [T, S] rows (a constant: bench.py --no-lazy-sbf and the parity tests flip it).
+LAZY_SBF = True
+
+
+def materialize_sbf(lg, sbf):
+    """Fill the [T, S] sbf rows a lazy spherical_basis left unwritten, if ``sbf`` is them (every consumer that
+    reads sbf values, rather than its factors, calls this first)."""
+    pend = getattr(lg, "sbf_pending", None)
+    if pend is None or pend[0] is not sbf:
+        return sbf
+    out, pos, rbf_env, ns, nr = pend
+    call("x2g_spherical_basis", ptr(pos), ptr(lg.atom_i), ptr(lg.atom_j), ptr(lg.atom_k), None, ptr(lg.trip_src),
+         ptr(rbf_env), lg.T, ns, nr, ptr(out), None, None, stream_ptr())
+    lg.sbf_pending = None
+    return sbf
 
 
 def spherical_basis_from_angles(theta, trip_src, rbf_env, num_spherical: int = 7, num_radial: int = 6):
@@ -405,10 +430,11 @@ def _center_split(lg):
     return order, None, None, [(sf, 0, units, rows, 0)]
 
 
-def center_schedule(atom_rowptr, mol_ptr, src_row, num_atoms: int, num_graphs: int):
+def center_schedule(atom_rowptr, src_row, num_atoms: int):
     """The center kernels' schedule made on the device (x2g_center_schedule): (center_order [N], pack_order [N],
-    pack_ptr [N + 1], atom_info [N * 4]) — the same kind data.center_packs makes on the host, per molecule; its
-    hub units sit among the packs (LineGraph.center_mixed)."""
+    pack_ptr [N + 1], atom_info [N * 4]) — the same kind data.center_packs makes on the host (best fit per
+    window of 64 atoms, the units by decreasing largest degree); its hub units lead the packs, which the
+    launches find on the device (LineGraph.center_mixed)."""
     n = int(num_atoms)
     dev = atom_rowptr.device
     off = 4 * ((3 * n + 1 + 3) // 4)  # atom_info 16-byte aligned after the order / pack order / pack_ptr
@@ -416,10 +442,10 @@ def center_schedule(atom_rowptr, mol_ptr, src_row, num_atoms: int, num_graphs: i
     c_order, p_order, p_ptr = torch.split(buf[:3 * n + 1], [n, n, n + 1])
     info = buf[off:off + 4 * n]
     lib = _lib.load()
-    ws_b = int(lib.x2g_center_schedule_workspace())
+    ws_b = int(lib.x2g_center_schedule_workspace(n))
     ws = torch.empty(ws_b, dtype=torch.uint8, device=dev)
-    call("x2g_center_schedule", ptr(atom_rowptr), ptr(mol_ptr), ptr(src_row), n, int(num_graphs), ptr(c_order),
-         ptr(p_order), ptr(p_ptr), ptr(info), ptr(ws), ws_b, stream_ptr())
+    call("x2g_center_schedule", ptr(atom_rowptr), ptr(src_row), n, ptr(c_order), ptr(p_order), ptr(p_ptr),
+         ptr(info), ptr(ws), ws_b, stream_ptr())
     return c_order, p_order, p_ptr, info
 
 
@@ -526,6 +552,7 @@ class _SBFAttention(torch.autograd.Function):
             # in the MALL when the attention kernels read its rows: sbf pointer = S, weight pointer NULL)
             # instead of re-projecting per triplet
             sproj = torch.empty(T, D, dtype=torch.float32, device=dev)
+            materialize_sbf(lg, sbf)
             call("x2g_sbf_project", ptr(sbf), T, sbf.shape[1], ptr(w_sbf), ptr(b_sbf), D, ptr(sproj), stream_ptr())
             if center:
                 call("x2g_sbf_attention_fwd_center", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge), ptr(src_row),
@@ -588,6 +615,7 @@ class _SBFAttention(torch.autograd.Function):
             # rows of the edge table are shared by many destinations: sum d_edge per table row
             d_edge = keyed_row_sum(d_edge, ctx.edge_row, ctx.edge_shape[0])
         gw, gb = grad_sink(ctx.w_param), grad_sink(ctx.b_param)
+        materialize_sbf(lg, sbf)
         if gw is not None and gb is not None:
             dw, db = linear_wgrad(dproj, sbf, dw_out=gw, db_out=gb)  # summed into the bucket: None
         else:
@@ -1078,6 +1106,7 @@ def _attention_fwd_tiled(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode, 
     smax, sden = torch.empty(E, H, **f32), torch.empty(E, H, **f32)
     rstats = torch.empty(E, 2, **f32) if _LN_FUSE and D == 128 else None
     tiles = _infer_tiles(lg, tmax)
+    materialize_sbf(lg, sbf)
     S = torch.empty(max(t[3] - (t[2] & ~1) for t in tiles), D, **f32)
     st = stream_ptr()
     fb, ib = 4, 4  # bytes per float32 / int32 element

@@ -2,7 +2,7 @@
 
 ``FlatAdam`` re-homes every parameter as a view of ONE flat fp32 buffer (the gradient side is
 ``dist.GradBucket``'s flat buffer), so clip_grad_norm_ + Adam + the EMA of AveragedModel are
-three launches of ``x2g_clip_adam_ema`` over contiguous memory instead of torch's per-tensor
+two launches of ``x2g_clip_adam_ema`` over contiguous memory instead of torch's per-tensor
 foreach/capturable kernels.  Step count, norm and bias corrections live on the device, so the
 update can sit inside a captured HIP graph.
 """

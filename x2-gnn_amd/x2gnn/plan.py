@@ -83,7 +83,7 @@ class GraphPlan:
             p.lg.center_hubs = st.get("_x2g_center_hubs", 0)
             p.lg.center_mixed = st.get("_x2g_center_mixed", False)
             if st.get("_x2g_device_schedule", False) and p.lg.edge_rev is not None:  # (data.HOST_SCHEDULE False)
-                sched = ops.center_schedule(p.lg.atom_rowptr, p.mol_ptr, src_type, p.num_atoms, p.num_graphs)
+                sched = ops.center_schedule(p.lg.atom_rowptr, src_type, p.num_atoms)
                 p.lg.center_order, p.lg.pack_order, p.lg.center_packs, p.lg.pack_info = sched
                 p.lg.center_rows, p.lg.center_mixed = ops.CENTER_SF_MAX_ROWS, True
         else:

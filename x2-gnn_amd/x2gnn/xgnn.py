@@ -46,8 +46,10 @@ class _XGNNBase(nn.Module):
                 and isinstance(getattr(rbf, "frequencies", None), torch.Tensor) and rbf.frequencies.numel() <= 16
                 and abs(rbf.inv_cutoff * self.cutoff - 1.0) < 1e-12)
 
-    def line_graph_data(self, data):
-        """Featurisation (reference xgnn.py:39-72) -> (line-graph Data, GraphPlan)."""
+    def line_graph_data(self, data, lazy_sbf=False):
+        """Featurisation (reference xgnn.py:39-72) -> (line-graph Data, GraphPlan).  ``lazy_sbf`` (the
+        model's own forward): edge_sbf's [T, S] rows are written only if a consumer reads them rather than
+        their factors (ops.materialize_sbf; the fused center forward reads only the factors)."""
         if "batch" not in data._store:  # single molecule: the reference adds a zero batch vector
             data.batch = torch.zeros(data.x.shape[0], dtype=torch.int64, device=data.x.device)
         plan = GraphPlan.from_atom_batch(data)
@@ -70,7 +72,7 @@ class _XGNNBase(nn.Module):
         # under molecule sharding the embedding's per-batch rules count the global batch's atoms
         # (dist.collate_shard); otherwise this batch's
         table, edge_proj = self._edge_tables(data.x, data._store.get("_x2g_count_z"))
-        sbf = self.sbf_layer.from_positions(dist, pos, lg, bessel)
+        sbf = self.sbf_layer.from_positions(dist, pos, lg, bessel, lazy=lazy_sbf)
         if not fused_feat:
             neo_x = self.emb_trans.fused(neo_x, act=ops.ACT_SILU)
         line = Data(x=neo_x, edge_attr=table, edge_attr_row=plan.dst_type, edge_sbf=sbf, node_rbf=node_rbf)
@@ -98,7 +100,7 @@ class _XGNNBase(nn.Module):
         return emb.element_table(atomic_num, count_z), None
 
     def forward(self, data):
-        line, plan = self.line_graph_data(data)
+        line, plan = self.line_graph_data(data, lazy_sbf=ops.LAZY_SBF)
         return self.fin_model(line, edge_index_0=plan.lg.edge_src, atom_batch=data.batch)
 
 
