@@ -397,7 +397,6 @@ int x2g_sbf_attention_bwd_center(const float* q, const float* k, const float* v,
                                  int64_t num_atoms, int32_t max_degree, int64_t num_edges, int64_t num_triplets,
                                  int32_t heads, int32_t channels, float* dq, float* dk, float* dv, float* radial_grad,
                                  float* d_edge_atom, float* g_work, void* stream);
-
 /* Backward, destination-major: dq[E,HC]; d_edge ([E,HC] per destination for EDGE_PER_DST,
  * [T,HC] for EDGE_PER_TRIPLET); dlogit[T,H] (grad of alpha_raw); d_sbfproj[T,HC] (grad of S_t,
  * so dW_sbf = d_sbfproj^T sbf and db_sbf = column sums). */
@@ -1000,10 +999,9 @@ typedef struct {
 
 /* Backward of x2g_table_chain_fwd (stages in the forward's order): every stage's weight / bias
  * gradient and dx = dL/dx ([rows, D], may be NULL), with a workspace (x2g_table_chain_bwd_workspace
- * bytes, 16-byte aligned): a tree with
- * several leaves (X2-GNN's four lin_edge) runs its leaf stages side by side, one workgroup each,
- * then the inner stages (two launches; the one-workgroup chain otherwise).  The forward already runs
- * one workgroup per root-to-leaf path. */
+ * bytes, 16-byte aligned; it receives every stage's dz): two launches — the dz / dx chain through the
+ * tree in one workgroup (children before parents), then every stage's dW / db side by side, one
+ * workgroup each.  The forward runs one workgroup per root-to-leaf path. */
 size_t x2g_table_chain_bwd_workspace(int32_t n_stages);
 int x2g_table_chain_bwd_ex(const x2g_table_bwd_stage* stages, int32_t n_stages, int64_t rows, int32_t dim, float* dx,
                            void* workspace, size_t workspace_bytes, void* stream);

@@ -23,6 +23,7 @@ for s in "$@"; do
   case $s in
     kc) step kc 400 $PT tests/test_gpu_kernels.py -k "center" ;;
     opt) step opt 300 $PT tests/test_gpu_kernels.py -k "flat_adam" ;;
+    ktab) step ktab 300 $PT tests/test_gpu_kernels.py -k "table" ;;
     kch) step kch 400 $PT tests/test_gpu_kernels.py -k "chain or tiled or wgrad or schedule" ;;
     model) step model 600 $PT tests/test_gpu_model.py ;;
     dist) step dist 600 $PT tests/test_dist_gpu.py tests/test_rccl_gpu.py ;;

@@ -5,10 +5,10 @@
 // (sbftransformer_conv.py:144) run on the element table: <= 16 rows, D = 128.  As separate GEMM
 // launches each of those layers is pure latency (one workgroup loads a 64 KB weight, does 0.3
 // MFLOP, writes 5 KB): 7 launches forward and 7 backward at 7-12 us each.  Here the whole tree of
-// stages runs in ONE workgroup per direction: the rows stay in LDS from stage to stage, the next
-// stage's weight is prefetched into registers while the current one computes, and the backward
-// accumulates every stage's output gradient in LDS (children before parents), so the weight and
-// data gradients of all stages come out of one launch.  Deterministic: one workgroup, fixed order.
+// stages runs in ONE workgroup per path: the rows stay in LDS from stage to stage, the next stage's
+// weight is prefetched into registers while the current one computes, and the backward accumulates
+// every stage's output gradient in LDS (children before parents) in one workgroup, then forms all
+// weight gradients side by side in a second launch.  Deterministic: fixed orders throughout.
 #include "common.hpp"
 
 namespace x2g {
@@ -134,69 +134,52 @@ __global__ void __launch_bounds__(kTThreads) table_chain_fwd_kernel(const TableF
   }
 }
 
-// Backward with several leaves: launch 1 (leaf pass) runs each leaf stage in its own workgroup and
-// leaves its input-gradient share dy_leaf W_leaf in the workspace (part[leaf]); launch 2 runs the
-// other stages in one workgroup, adding the shares into their parents' gradients in leaf order.
+// Backward: the tree's stage arguments (launch 1 reads every stage's w / z / dy, launch 2 one stage each).
 struct TableBwdArgs {
   x2g_table_bwd_stage st[kTMax];
   float* dx;
   int n;
   int R;
-  uint32_t mask;          // launch 2: the stages it runs (the rest are leaves done by launch 1)
-  int leaf[kTMax];        // launch 1: workgroup b runs stage leaf[b]
-  float* part;            // [n][16][128] the leaves' input-gradient shares (or NULL: one launch)
+  float* part;  // [n][16][128] every stage's dz (launch 1 -> launch 2)
 };
 
-// Stage s's weight (read transposed: column block 16w, rows 16q + 4g + e), forward input and
-// pre-activation are loaded during stage s + 1; the old gradient-bucket values it adds to fly
-// during its own products.
-struct BwdPre {
+// ---- backward in two launches without a serial weight-gradient chain (round 6).  Round 5's form ran, per
+// stage, the dz / dx chain AND the stage's dW / db in one workgroup (32 strided stores per lane, the old
+// bucket values loaded behind them; the leaves side by side in a first launch), so every stage of the
+// serial chain also waited on its weight-gradient traffic: 38 us per step for 7 stages of 16 rows
+// (profiles/r5_step_work.json).  Now launch 1 (one
+// workgroup) runs only the chain — per stage dz = dL/dy_s SiLU'(z_s) into LDS and out to the workspace,
+// and dL/d in_s = dz W_s added into the parent's gradient — and launch 2 (one workgroup per stage, side by
+// side) forms every dW / db from the workspace's dz and the stage input: dW^T = in^T dz as v_mfma_f32_16x16x4
+// with the input as the A operand, so each lane ends with 4 consecutive columns of a dW row (16-byte loads of
+// the old bucket values and 16-byte stores).
+struct DzPre {
   f4 w[8];     // W[16q + 4g + e][16w + i]
-  f4 in;       // row tid >> 5, columns 4 (tid & 31) ..
   float z[4];  // pre-activation at (rows 4g + e, column 16w + i)
 };
 
-__device__ __forceinline__ void bwd_prefetch(const TableBwdArgs& a, int s, BwdPre& p) {
+__device__ __forceinline__ void dz_prefetch(const TableBwdArgs& a, int s, DzPre& p) {
   if (s < 0) return;
   const x2g_table_bwd_stage& S = a.st[s];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, g = lane >> 4, c = 16 * w + i;
-  const int R = a.R;
 #pragma unroll
   for (int q = 0; q < 8; ++q)
 #pragma unroll
     for (int e = 0; e < 4; ++e) p.w[q][e] = S.w[(16 * q + 4 * g + e) * kTD + c];
-  {
-    const int r = tid >> 5;
-    p.in = r < R ? *reinterpret_cast<const f4*>(S.in + r * kTD + 4 * (tid & 31)) : f4{0.f, 0.f, 0.f, 0.f};
-  }
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int r = 4 * g + e;
-    p.z[e] = (S.act && r < R) ? S.z[r * kTD + c] : 0.0f;
+    p.z[e] = (S.act && r < a.R) ? S.z[r * kTD + c] : 0.0f;
   }
 }
 
-// old values of stage s's dW / db when it accumulates into a gradient bucket (zero otherwise), in
-// the MFMA D layout of the dW product: old[t][e] = dw[16w + 4g + e][16t + i]
-__device__ __forceinline__ void load_old(const TableBwdArgs& a, int s, f4 (&old)[8]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
-  const bool on = s >= 0 && a.st[s >= 0 ? s : 0].accum;
-  const float* dw = a.st[s >= 0 ? s : 0].dw;
-#pragma unroll
-  for (int t = 0; t < 8; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) old[t][e] = on ? dw[(16 * w + 4 * g + e) * kTD + 16 * t + i] : 0.0f;
-}
-
-template <bool LEAF>
-__device__ __forceinline__ void bwd_stage(const TableBwdArgs& a, int s, int pf, BwdPre& cur, BwdPre& nxt,
-                                          float (*G)[kTRows * kTS], float* dZ, float* In, f4 (&old)[8]) {
+__device__ __forceinline__ void dz_stage(const TableBwdArgs& a, int s, int pf, DzPre& cur, DzPre& nxt,
+                                         float (*G)[kTRows * kTS], float* dZ) {
   const x2g_table_bwd_stage& S = a.st[s];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 15, g = lane >> 4, c = 16 * w + i;
-  __syncthreads();  // G[s + 1] is complete (every child has added its share); dZ, In are free
-  *reinterpret_cast<f4*>(In + (tid >> 5) * kTS + 4 * (tid & 31)) = cur.in;
+  __syncthreads();  // G[s + 1] is complete (every child has added its share); dZ is free
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int r = 4 * g + e;
@@ -204,30 +187,13 @@ __device__ __forceinline__ void bwd_stage(const TableBwdArgs& a, int s, int pf, 
     dZ[r * kTS + c] = S.act ? gv * silu_grad_(cur.z[e]) : gv;
   }
   __syncthreads();
-  bwd_prefetch(a, pf, nxt);
-  // dW[n][k] = sum_r dz[r][n] in[r][k]: wave w owns rows n = 16w + ..., all 8 column blocks; the
-  // old bucket values (old, loaded at the end of the previous stage) are added at the store
-  float ad[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) ad[e] = dZ[(4 * g + e) * kTS + c];  // A: (n = c, r = 4g + e)
-  f4 dwv[8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    dwv[t] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) dwv[t] = mfma4(ad[e], In[(4 * g + e) * kTS + 16 * t + i], dwv[t]);
+  dz_prefetch(a, pf, nxt);
+  {  // dz rows to the workspace (rows >= R are zero: their gradients and pre-activations are)
+    const int r = tid >> 5, c4 = 4 * (tid & 31);
+    *reinterpret_cast<f4*>(a.part + (static_cast<int64_t>(s) * kTRows + r) * kTD + c4) =
+        *reinterpret_cast<const f4*>(dZ + r * kTS + c4);
   }
-#pragma unroll
-  for (int t = 0; t < 8; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) S.dw[(16 * w + 4 * g + e) * kTD + 16 * t + i] = old[t][e] + dwv[t][e];
-  load_old(a, pf, old);  // the next stage's, in flight through its barriers and dz
-  if (S.db && tid < kTD) {
-    float acc = 0.0f;
-    for (int r = 0; r < a.R; ++r) acc += dZ[r * kTS + tid];
-    S.db[tid] = S.accum ? S.db[tid] + acc : acc;
-  }
-  // dL/d in[r][k] += sum_n dz[r][n] W[n][k]: wave w owns columns k = 16w + ...
+  // dL/d in[r][k] = sum_n dz[r][n] W[n][k]: wave w owns columns k = 16w + ...
   f4 acc = {0.f, 0.f, 0.f, 0.f};
   const float* dzr = dZ + i * kTS + 4 * g;
 #pragma unroll
@@ -236,40 +202,16 @@ __device__ __forceinline__ void bwd_stage(const TableBwdArgs& a, int s, int pf, 
 #pragma unroll
     for (int e = 0; e < 4; ++e) acc = mfma4(av[e], cur.w[q][e], acc);
   }
-  if (LEAF) {  // the share goes to the parent's gradient through the workspace
-    float* pp = a.part + static_cast<int64_t>(s) * kTRows * kTD;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) pp[(4 * g + e) * kTD + c] = acc[e];
-    return;
-  }
   float* gp = G[S.parent + 1];
 #pragma unroll
   for (int e = 0; e < 4; ++e) gp[(4 * g + e) * kTS + c] += acc[e];
 }
 
-template <bool LEAF>
-__global__ void __launch_bounds__(kTThreads) table_chain_bwd_kernel(const TableBwdArgs a) {
+__global__ void __launch_bounds__(kTThreads) table_bwd_dz_kernel(const TableBwdArgs a) {
   __shared__ __attribute__((aligned(16))) float G[kTMax + 1][kTRows * kTS];  // dL/d(x), dL/d(y_s)
   __shared__ __attribute__((aligned(16))) float dZ[kTRows * kTS];
-  __shared__ __attribute__((aligned(16))) float In[kTRows * kTS];
   const int tid = threadIdx.x;
   const int R = a.R;
-  BwdPre p0, p1;
-  f4 old[8];
-  if (LEAF) {  // launch 1: this workgroup's leaf stage alone
-    const int s = a.leaf[blockIdx.x];
-    bwd_prefetch(a, s, p0);
-    load_old(a, s, old);
-    const float* dy = a.st[s].dy;
-    if (dy)
-      rows_to_lds(G[s + 1], dy, R);
-    else
-      *reinterpret_cast<f4*>(G[s + 1] + (tid >> 5) * kTS + 4 * (tid & 31)) = f4{0.f, 0.f, 0.f, 0.f};
-    bwd_stage<true>(a, s, -1, p0, p1, G, dZ, In, old);
-    return;
-  }
-  const uint32_t mask = a.mask;
-  int s = prev_in(mask, a.n);
   for (int t = -1; t < a.n; ++t) {
     const float* dy = t >= 0 ? a.st[t].dy : nullptr;
     if (dy)
@@ -277,30 +219,54 @@ __global__ void __launch_bounds__(kTThreads) table_chain_bwd_kernel(const TableB
     else
       *reinterpret_cast<f4*>(G[t + 1] + (tid >> 5) * kTS + 4 * (tid & 31)) = f4{0.f, 0.f, 0.f, 0.f};
   }
-  if (a.part) {  // the leaves' shares, added in stage order (each thread its own elements: no race)
-    const int r = tid >> 5, c4 = 4 * (tid & 31);
-    for (int t = 0; t < a.n; ++t) {
-      if ((mask >> t) & 1u) continue;
-      float* gp = G[a.st[t].parent + 1] + r * kTS + c4;
-      const f4 v = r < R ? *reinterpret_cast<const f4*>(a.part + (static_cast<int64_t>(t) * kTRows + r) * kTD + c4)
-                         : f4{0.f, 0.f, 0.f, 0.f};
-      *reinterpret_cast<f4*>(gp) = *reinterpret_cast<const f4*>(gp) + v;
-    }
-  }
-  bwd_prefetch(a, s, p0);
-  load_old(a, s, old);
+  DzPre p0, p1;
+  int s = a.n - 1;  // children before parents: a stage's parent is an earlier stage
+  dz_prefetch(a, s, p0);
   while (s >= 0) {  // two register sets alternate (unrolled by two, no copies)
-    const int s1 = prev_in(mask, s);
-    bwd_stage<false>(a, s, s1, p0, p1, G, dZ, In, old);
-    if (s1 < 0) break;
-    const int s2 = prev_in(mask, s1);
-    bwd_stage<false>(a, s1, s2, p1, p0, G, dZ, In, old);
-    s = s2;
+    dz_stage(a, s, s - 1, p0, p1, G, dZ);
+    if (s - 1 < 0) break;
+    dz_stage(a, s - 1, s - 2, p1, p0, G, dZ);
+    s -= 2;
   }
   if (a.dx) {
     __syncthreads();
     const int r = tid >> 5, c4 = 4 * (tid & 31);
     if (r < R) *reinterpret_cast<f4*>(a.dx + r * kTD + c4) = *reinterpret_cast<const f4*>(G[0] + r * kTS + c4);
+  }
+}
+
+// workgroup s: dW_s (+)= dz_s^T in_s, db_s (+)= column sums of dz_s (rows ascending)
+__global__ void __launch_bounds__(kTThreads) table_bwd_wgrad_kernel(const TableBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) float Dz[kTRows * kTS];
+  __shared__ __attribute__((aligned(16))) float In[kTRows * kTS];
+  const int s = blockIdx.x;
+  const x2g_table_bwd_stage& S = a.st[s];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  rows_to_lds(Dz, a.part + static_cast<int64_t>(s) * kTRows * kTD, kTRows);
+  rows_to_lds(In, S.in, a.R);
+  float* dwrow = S.dw + (16 * w + i) * kTD + 4 * g;  // dW row 16w + i, columns 16t + 4g .. + 3
+  f4 old[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+    old[t] = S.accum ? *reinterpret_cast<const f4*>(dwrow + 16 * t) : f4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  // D = dW^T block t: D[16t + m][16w + n] = sum_r in[r][16t + m] dz[r][16w + n]; lane (i, g) ends with
+  // D[16t + 4g + e][16w + i] = dW[16w + i][16t + 4g + e]
+  float bv[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) bv[kk] = Dz[(4 * kk + g) * kTS + 16 * w + i];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    f4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) d = mfma4(In[(4 * kk + g) * kTS + 16 * t + i], bv[kk], d);
+    *reinterpret_cast<f4*>(dwrow + 16 * t) = old[t] + d;
+  }
+  if (S.db && tid < kTD) {
+    float acc = 0.0f;
+    for (int r = 0; r < a.R; ++r) acc += Dz[r * kTS + tid];
+    S.db[tid] = S.accum ? S.db[tid] + acc : acc;
   }
 }
 
@@ -348,26 +314,6 @@ X2G_API int x2g_table_chain_fwd(const float* x, int64_t rows, int32_t dim, const
   return last_launch_status();
 }
 
-// the one-workgroup chain (a tree with one leaf)
-static int table_chain_bwd_1wg(const x2g_table_bwd_stage* stages, int32_t n_stages, int64_t rows, float* dx,
-                               hipStream_t st) {
-  TableBwdArgs a{};
-  for (int s = 0; s < n_stages; ++s) {
-    const x2g_table_bwd_stage& S = stages[s];
-    if (!S.w || !S.in || !S.dw || S.parent < -1 || S.parent >= s || (S.act != 0 && S.act != 1) || (S.act && !S.z))
-      return X2G_EINVAL;
-    if (!al16(S.w) || !al16(S.in) || !al16(S.dy)) return X2G_EUNSUPPORTED;
-    a.st[s] = S;
-  }
-  // rows == 0 still launches: the weight gradients are zero, not left unwritten
-  a.dx = dx;
-  a.n = n_stages;
-  a.R = static_cast<int>(rows);
-  a.mask = n_stages >= 32 ? ~0u : (1u << n_stages) - 1u;
-  table_chain_bwd_kernel<false><<<1, kTThreads, 0, st>>>(a);
-  return last_launch_status();
-}
-
 X2G_API size_t x2g_table_chain_bwd_workspace(int32_t n_stages) {
   return n_stages > 0 ? static_cast<size_t>(n_stages) * kTRows * kTD * sizeof(float) : 0;
 }
@@ -376,35 +322,25 @@ X2G_API int x2g_table_chain_bwd_ex(const x2g_table_bwd_stage* stages, int32_t n_
                                    float* dx, void* workspace, size_t workspace_bytes, void* stream) {
   if (!stages || n_stages < 1 || n_stages > kTMax || rows < 0 || dim <= 0) return X2G_EINVAL;
   if (dim != kTD || rows > kTRows) return X2G_EUNSUPPORTED;
-  uint32_t has_child = 0;
-  for (int s = 0; s < n_stages; ++s)
-    if (stages[s].parent >= 0 && stages[s].parent < s) has_child |= 1u << stages[s].parent;
-  int nleaf = 0;
-  for (int s = 0; s < n_stages; ++s) nleaf += ((has_child >> s) & 1u) ? 0 : 1;
-  if (nleaf < 2) return table_chain_bwd_1wg(stages, n_stages, rows, dx, as_stream(stream));
   if (!workspace || workspace_bytes < x2g_table_chain_bwd_workspace(n_stages)) return X2G_EWORKSPACE;
-  if (!al16(workspace)) return X2G_EUNSUPPORTED;
+  if (!al16(workspace) || !al16(dx)) return X2G_EUNSUPPORTED;
   TableBwdArgs a{};
   for (int s = 0; s < n_stages; ++s) {
     const x2g_table_bwd_stage& S = stages[s];
     if (!S.w || !S.in || !S.dw || S.parent < -1 || S.parent >= s || (S.act != 0 && S.act != 1) || (S.act && !S.z))
       return X2G_EINVAL;
-    if (!al16(S.w) || !al16(S.in) || !al16(S.dy)) return X2G_EUNSUPPORTED;
+    if (!al16(S.w) || !al16(S.in) || !al16(S.dy) || !al16(S.dw)) return X2G_EUNSUPPORTED;
     a.st[s] = S;
   }
+  // rows == 0 still launches: the weight gradients are zero, not left unwritten
   a.dx = dx;
   a.n = n_stages;
   a.R = static_cast<int>(rows);
-  a.part = static_cast<float*>(workspace);
-  int nl = 0;
-  for (int s = 0; s < n_stages; ++s)
-    if (!((has_child >> s) & 1u)) a.leaf[nl++] = s;
+  a.part = static_cast<float*>(workspace);  // dz of every stage [n][16][128]
   hipStream_t st = as_stream(stream);
-  // launch 1: the leaves side by side (their dW / db, and their input-gradient shares)
-  table_chain_bwd_kernel<true><<<static_cast<unsigned>(nl), kTThreads, 0, st>>>(a);
+  // launch 1: the dz / dx chain in one workgroup; launch 2: every stage's dW / db side by side
+  table_bwd_dz_kernel<<<1, kTThreads, 0, st>>>(a);
   if (int rc = last_launch_status()) return rc;
-  // launch 2: the inner stages in one workgroup, the shares added into their parents' gradients
-  a.mask = has_child;
-  table_chain_bwd_kernel<false><<<1, kTThreads, 0, st>>>(a);
+  table_bwd_wgrad_kernel<<<static_cast<unsigned>(n_stages), kTThreads, 0, st>>>(a);
   return last_launch_status();
 }
