@@ -43,13 +43,13 @@ MFMA_F32_PEAK_TFS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32) peak, MI35
 # scripts/pmc_traffic.py outputs (rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench), per workload
 # the committed PMC summaries (scripts/pmc_traffic.py over rocprofv3 FETCH_SIZE / WRITE_SIZE passes of
 # this bench at the same workload and shape): bytes of each probe's own launch
-TRAFFIC_JSON = {("qm9_u0", "S160"): os.path.join(ROOT, "profiles", "r5_pmc_traffic.json"),
-                ("qm9_u0", "S5A"): os.path.join(ROOT, "profiles", "r5_pmc_traffic_s5a.json"),
-                ("qm9_allprop", "S160"): os.path.join(ROOT, "profiles", "r5_pmc_traffic_c3.json"),
-                ("aid_infer", "S160"): os.path.join(ROOT, "profiles", "r5_pmc_traffic_c5.json")}
+TRAFFIC_JSON = {("qm9_u0", "S160"): os.path.join(ROOT, "profiles", "r6_pmc_traffic.json"),
+                ("qm9_u0", "S5A"): os.path.join(ROOT, "profiles", "r6_pmc_traffic_s5a.json"),
+                ("qm9_allprop", "S160"): os.path.join(ROOT, "profiles", "r6_pmc_traffic_c3.json"),
+                ("aid_infer", "S160"): os.path.join(ROOT, "profiles", "r6_pmc_traffic_c5.json")}
 # the config-2 step's per-kernel work table (scripts/step_work.py: PMC HBM bytes, matrix FLOPs, trace time
 # per step) behind `step_roofline`
-STEP_WORK_JSON = os.path.join(ROOT, "profiles", "r5_step_work.json")
+STEP_WORK_JSON = os.path.join(ROOT, "profiles", "r6_step_work.json")
 
 
 def product_digest():

@@ -534,12 +534,16 @@ constexpr int kTileRows = 16;
 template <int LPH, int WAVES, int B, bool EDGE, int RMAX, bool STORE>
 __global__ void __launch_bounds__(64 * WAVES, 4) attn_fwd_center_sf_tiled_kernel(const FwdSfArgs a) {
   static_assert(kTileRows % B == 0, "batches never cross a tile");
-  extern __shared__ cf4 lds[];  // [TS][32] (k + e), [TS][32] (v + e), [TS][7][32] P, [TS][42] R
+  // [TS][32] (k + e), [TS][32] (v + e), [TS][7][32] P, [TS][42] R, then per destination row its id and
+  // triplet block [X2G_CENTER_MAX_DEGREE] x 2
+  extern __shared__ cf4 lds[];
   constexpr int TS = kTileRows, NT = 64 * WAVES, NO = 2 * WAVES;
   cf4* KE = lds;
   cf4* VE = KE + TS * 32;
   cf4* P = VE + TS * 32;
   float* RS = reinterpret_cast<float*>(P + TS * kSfL * 32);
+  int* DDs = reinterpret_cast<int*>(RS + TS * kSfK);
+  int* TBs = DDs + X2G_CENTER_MAX_DEGREE;
   // the unit: one atom (the host routes the units of more than max_rows rows here, each a single atom)
   const int64_t unit = a.atom0 + blockIdx.x;
   int64_t pos = unit;
@@ -569,7 +573,6 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_fwd_center_sf_tiled_kernel
   const bool leader = (l32 % LPH) == 0;
   const int c0 = 4 * l32;
   const int nt = n - 1;
-  // (the destinations' ids and triplet blocks are re-read per tile, L2 hits: registers go to the state)
   cf4 acc[RMAX];
   float m[RMAX], den[RMAX];
 #pragma unroll
@@ -583,6 +586,12 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_fwd_center_sf_tiled_kernel
   const int pg = tid / 256, prest = tid % 256;
   const bool pthr = prest < kSfL * 32;
   const int pl = pthr ? prest >> 5 : 0, pc4 = prest & 31;
+  // the destinations' ids and triplet blocks, once (each (destination, tile) pair then starts its q / Y
+  // loads from LDS instead of behind two dependent global round trips; read after the first tile's barrier)
+  for (int idx = tid; idx < n; idx += NT) {
+    DDs[idx] = a.edge_rev[r0 + idx];
+    TBs[idx] = a.rev_trip[r0 + idx];
+  }
   for (int t0 = 0; t0 < n; t0 += TS) {
     const int ts = n - t0 < TS ? n - t0 : TS;
     __syncthreads();  // the previous tile's rows are no longer read
@@ -624,7 +633,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_fwd_center_sf_tiled_kernel
     for (int r = 0; r < RMAX; ++r) {
       const int i = owner + NO * r;  // this destination's row in the block
       if (i >= n) continue;          // (per owner)
-      const int dd = a.edge_rev[r0 + i], tb = a.rev_trip[r0 + i];
+      const int dd = DDs[i], tb = TBs[i];
       const cf4 qv = ld4(a.q + static_cast<int64_t>(dd) * kCD + c0);
       if (nt > 0) {  // (n = 1: an empty softmax, out = skip)
         // batches of B sources, software-pipelined: batch j0 + B's Y values are loaded before batch j0's
@@ -707,7 +716,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_fwd_center_sf_tiled_kernel
 #pragma unroll
   for (int r = 0; r < RMAX; ++r) {
     if (owner + NO * r >= n) continue;
-    const int dd = a.edge_rev[r0 + owner + NO * r];
+    const int dd = DDs[owner + NO * r];
     const int64_t drow = static_cast<int64_t>(dd) * kCD + c0;
     const float inv = 1.0f / (den[r] + kCEps);
     const cf4 o = acc[r] * inv + ld4(a.skip + drow);
@@ -725,7 +734,9 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_fwd_center_sf_tiled_kernel
   }
 }
 
-constexpr size_t fwd_sf_tiled_lds() { return static_cast<size_t>(kTileRows) * ((2 + kSfL) * kCD + kSfK) * 4; }
+constexpr size_t fwd_sf_tiled_lds() {
+  return static_cast<size_t>(kTileRows) * ((2 + kSfL) * kCD + kSfK) * 4 + 2 * X2G_CENTER_MAX_DEGREE * 4;
+}
 
 template <int LPH>
 int fwd_sf_tiled_launch(const FwdSfArgs& a, bool edge, int max_degree, hipStream_t st) {

@@ -3,11 +3,12 @@
 // (AveragedModel with avg_fn = d*avg + (1-d)*p).  torch's capturable Adam issues a few kernels
 // per parameter tensor (~300 launches for X2-GNN's 155 tensors); here it is two launches:
 //   1. per-block partial sums of g^2 over contiguous chunks (fixed order); block 0 also advances
-//      the step count and the learning-rate schedule (no block of this launch reads them),
+//      the step count, the learning-rate schedule and Adam's bias corrections (no block of this
+//      launch reads them),
 //   2. elementwise Adam + EMA (a copy of the parameters at step 1, as AveragedModel does); every
 //      block sums the kNormBlocks partials itself in the same fixed order (1 KB of L2 reads a
-//      block), so all blocks see one bit-identical norm without a finaliser launch or a fence,
-//      and block 0 publishes norm, clip coefficient and bias corrections to the scalar block.
+//      block: one per thread, shuffle sums), so all blocks see one bit-identical norm without a
+//      finaliser launch or a fence, and block 0 publishes the norm and clip coefficient.
 // Every value the update depends on that changes between steps (step count, norm, clip scale)
 // lives in device memory, so a captured HIP graph replays correctly; the hyper-parameters
 // (lr, betas, eps, max_norm, ema decay) are read from the same device scalar block so a
@@ -58,6 +59,10 @@ __global__ void __launch_bounds__(kNormThreads) grad_sq_partial(const float4* __
       sc[X2G_OPT_LR] = static_cast<float>(static_cast<double>(sc[X2G_OPT_BASE_LR]) * warm *
                                           pow(static_cast<double>(sc[X2G_OPT_DECAY_RATE]), ex));
     }
+    // bias corrections as torch.optim.Adam computes them (in double, rounded to float)
+    const double b1 = sc[X2G_OPT_BETA1], b2 = sc[X2G_OPT_BETA2];
+    sc[X2G_OPT_STEP_SIZE] = static_cast<float>(sc[X2G_OPT_LR] / (1.0 - pow(b1, static_cast<double>(step))));
+    sc[X2G_OPT_BC2_SQRT] = static_cast<float>(sqrt(1.0 - pow(b2, static_cast<double>(step))));
   }
 }
 
@@ -66,39 +71,30 @@ __global__ void __launch_bounds__(kNormThreads) adam_ema(float* __restrict__ p, 
                                                          float* __restrict__ ema, int64_t n,
                                                          const float* __restrict__ partial, float* __restrict__ sc,
                                                          int zero_grads) {
-  __shared__ float red[kNormThreads];
-  __shared__ float upd[3];
-  float s = 0.f;
-  for (int i = threadIdx.x; i < kNormBlocks; i += kNormThreads) s += partial[i];
-  red[threadIdx.x] = s;
+  static_assert(kNormBlocks == kNormThreads, "one partial per thread");
+  __shared__ float red[kNormThreads / 64];
+  __shared__ float clip_s;
+  // the squared norm: one partial per thread, xor-shuffle sums per wave, the 4 wave sums in order — the
+  // same order in every block, so every block holds the same bits
+  float s = partial[threadIdx.x];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  for (int off = kNormThreads / 2; off > 0; off >>= 1) {
-    if (static_cast<int>(threadIdx.x) < off) red[threadIdx.x] += red[threadIdx.x + off];
-    __syncthreads();
-  }
   if (threadIdx.x == 0) {
-    const float norm = sqrtf(red[0]);
+    const float norm = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
     const float max_norm = sc[X2G_OPT_MAX_NORM];
     // torch.nn.utils.clip_grad_norm_: coef = max_norm / (norm + 1e-6), clamped to <= 1
     const float coef = max_norm > 0.f ? fminf(max_norm / (norm + 1e-6f), 1.0f) : 1.0f;
-    // bias corrections as torch.optim.Adam computes them (in double, rounded to float); the step
-    // count and lr were advanced by grad_sq_partial
-    const double step = sc[X2G_OPT_STEP];
-    const double b1 = sc[X2G_OPT_BETA1], b2 = sc[X2G_OPT_BETA2];
-    const float step_size = static_cast<float>(sc[X2G_OPT_LR] / (1.0 - pow(b1, step)));
-    const float bc2s = static_cast<float>(sqrt(1.0 - pow(b2, step)));
-    upd[0] = coef;
-    upd[1] = step_size;
-    upd[2] = bc2s;
+    clip_s = coef;
     if (blockIdx.x == 0) {  // published for the caller; no block of this launch reads them back
       sc[X2G_OPT_NORM] = norm;
       sc[X2G_OPT_CLIP] = coef;
-      sc[X2G_OPT_STEP_SIZE] = step_size;
-      sc[X2G_OPT_BC2_SQRT] = bc2s;
     }
   }
   __syncthreads();
-  const float clip = upd[0], step_size = upd[1], bc2s = upd[2];
+  // step size and bias correction were formed by grad_sq_partial's block 0 (one double pow per step)
+  const float clip = clip_s, step_size = sc[X2G_OPT_STEP_SIZE], bc2s = sc[X2G_OPT_BC2_SQRT];
   const float b1 = sc[X2G_OPT_BETA1], b2 = sc[X2G_OPT_BETA2], eps = sc[X2G_OPT_EPS];
   const float d = sc[X2G_OPT_EMA_DECAY];
   // AveragedModel.update_parameters copies the parameters on its first call (n_averaged == 0) and
