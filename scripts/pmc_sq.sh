@@ -18,7 +18,7 @@ pass() {  # pass <name> <counters...>
   local name=$1; shift
   echo "=== pmc $name: $*"
   timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-include-regex "$KRE" -d "gpurun_out/pmc_${name}_$TAG" -o run \
-    --output-format csv -- python "$ROOT/bench.py" --step-only --eager --steps 3 --warmup 1 \
+    --output-format csv -- python "$ROOT/bench.py" --step-only --eager --steps 3 --warmup 1 ${BARGS:-} \
     > "gpurun_out/pmc_${name}_$TAG.log" 2>&1
   local rc=$?
   echo "=== pmc $name rc=$rc"
