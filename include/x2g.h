@@ -310,6 +310,14 @@ int x2g_sbf_attention_fwd_center(const float* q, const float* k, const float* v,
  * stream, no host read.  The order among atoms (units) of equal degree follows integer atomics; no output of
  * the center kernels depends on it.  (ABI 17; ABI 16 took mol_ptr / num_graphs and left the units in
  * per-molecule slots.) */
+/* HOST function (no device work, no stream): collate's center-kernel units (x2gnn.data.center_packs) for
+ * the atom degrees deg [n]: the atoms by decreasing degree (ties by index) packed best-fit into units of
+ * <= cap rows and <= max_members atoms (the fullest open unit that takes an atom, the most recently opened of
+ * equally full ones; an atom of degree >= cap alone), atoms without edges max_members to a unit in index
+ * order after all others; the units in the order they were opened.  Writes order [n], packs [units + 1]
+ * (caller-sized n + 1), the unit count and the largest unit's row count. */
+int x2g_center_packs_host(const int64_t* deg, int64_t n, int32_t cap, int32_t max_members, int32_t* order,
+                          int32_t* packs, int64_t* n_units, int32_t* max_rows);
 size_t x2g_center_schedule_workspace(int64_t num_atoms);
 int x2g_center_schedule(const int32_t* atom_rowptr, const int32_t* src_row, int64_t num_atoms,
                         int32_t* center_order, int32_t* pack_order, int32_t* pack_ptr, int32_t* atom_info,

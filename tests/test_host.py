@@ -150,6 +150,69 @@ def test_center_packs_and_atom_info():
     assert u2[-1] == [0, 2] and [3] in u2 and [5] in u2 and r2 == 20
 
 
+def _center_packs_loop(deg, cap=16, max_members=16):
+    """The best-fit-decreasing packing as a plain Python loop (round 5's data.center_packs, kept here as the
+    checker of the native x2g_center_packs_host)."""
+    deg = np.asarray(deg, dtype=np.int64)
+    units, rows, free = [], [], [[] for _ in range(cap)]  # free[r]: open units with r rows left
+    for a in np.argsort(-deg, kind="stable").tolist():
+        d = int(deg[a])
+        if d == 0:
+            break
+        if d < cap:
+            for r in range(d, cap):  # the fullest open unit that takes it (the most recent on ties)
+                if free[r]:
+                    u = free[r].pop()
+                    units[u].append(a)
+                    rows[u] += d
+                    if len(units[u]) < max_members:
+                        free[r - d].append(u)
+                    break
+            else:
+                free[cap - d].append(len(units))
+                units.append([a])
+                rows.append(d)
+            continue
+        units.append([a])
+        rows.append(d)
+    zero = np.flatnonzero(deg == 0).tolist()
+    units += [zero[i:i + max_members] for i in range(0, len(zero), max_members)]
+    rows += [0] * ((len(zero) + max_members - 1) // max_members)
+    order = np.fromiter((a for u in units for a in u), dtype=np.int32, count=len(deg))
+    packs = np.concatenate([[0], np.cumsum([len(u) for u in units])]).astype(np.int32)
+    return order, packs, int(max(rows, default=0))
+
+
+@pytest.mark.parametrize("case", ["s160", "s5a", "random", "ones", "zeros", "hubs", "empty", "members"])
+def test_native_center_packs_equal_python_loop(case):
+    """data.center_packs (native x2g_center_packs_host) == the Python best-fit loop, unit for unit: collated
+    config-2 and S5A batches, random degrees with zeros and hubs, all-ones (the 16-member bound), no atoms."""
+    from x2gnn.data import center_packs, collate
+    from x2gnn.synth import synthetic_molecules
+
+    rng = np.random.default_rng(7)
+    if case in ("s160", "s5a"):
+        b = collate(synthetic_molecules(64, "S160" if case == "s160" else "S5A", seed=3))
+        deg = np.bincount(b.edge_index[0].numpy(), minlength=b.num_nodes)
+    elif case == "random":
+        deg = rng.integers(0, 40, size=3000)
+    elif case == "ones":
+        deg = np.ones(1000, dtype=np.int64)
+    elif case == "zeros":
+        deg = np.zeros(50, dtype=np.int64)
+    elif case == "hubs":
+        deg = np.concatenate([rng.integers(14, 70, size=200), rng.integers(0, 5, size=300)])
+    elif case == "members":
+        deg = rng.integers(1, 3, size=777)
+    else:
+        deg = np.zeros(0, dtype=np.int64)
+    for cap, mm in ((16, 16), (8, 5)):
+        o1, p1, r1 = center_packs(deg, cap, mm)
+        o2, p2, r2 = _center_packs_loop(deg, cap, mm)
+        assert np.array_equal(o1, o2) and np.array_equal(p1, p2) and r1 == r2, (case, cap, mm)
+        assert o1.dtype == np.int32 and p1.dtype == np.int32
+
+
 @pytest.mark.parametrize("host_schedule", [True, False])
 def test_fast_collate_equals_pyg_from_data_list(monkeypatch, host_schedule):
     """collate (one numpy concatenation per key) == Batch.from_data_list over per-molecule Data objects (PyG

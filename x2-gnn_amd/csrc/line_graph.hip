@@ -10,6 +10,10 @@
 // With edges sorted by (src, dst) -- np.argwhere order, atom_graph.py:42-45 -- the edges out
 // of atom b are the contiguous range atom_rowptr[b]..atom_rowptr[b+1] in ascending k, and the
 // id of edge (b->k) is its position in that range.
+#include <algorithm>
+#include <numeric>
+#include <vector>
+
 #include "common.hpp"
 
 namespace x2g {
@@ -1040,6 +1044,62 @@ __global__ void __launch_bounds__(64) center_sched_place_kernel(const int32_t* _
 }
 
 }  // namespace x2g
+
+// collate's center-kernel units on the HOST (data.center_packs; no device work): the atoms by decreasing
+// degree (ties by index) packed best-fit into units of <= cap rows and <= max_members atoms — for each
+// atom the fullest open unit that takes it (the most recently opened of equally full ones), a new unit
+// when none does, an atom of degree >= cap alone; atoms without edges max_members to a unit, in index
+// order, after all others.  Units in the order they were opened (so by decreasing largest degree).
+// The Python loop this replaces took 2/3 of a 128-molecule collate.
+X2G_API int x2g_center_packs_host(const int64_t* deg, int64_t n, int32_t cap, int32_t max_members, int32_t* order,
+                                  int32_t* packs, int64_t* n_units, int32_t* max_rows) {
+  if (n < 0 || cap < 1 || max_members < 1 || !n_units || !max_rows || n > 0x7fffffff) return X2G_EINVAL;
+  if (n > 0 && (!deg || !order || !packs)) return X2G_EINVAL;
+  std::vector<int32_t> idx(static_cast<size_t>(n));
+  std::iota(idx.begin(), idx.end(), 0);
+  std::stable_sort(idx.begin(), idx.end(), [&](int32_t x, int32_t y) { return deg[x] > deg[y]; });
+  std::vector<std::vector<int32_t>> units, free_(static_cast<size_t>(cap));
+  std::vector<int64_t> rows;
+  for (const int32_t a : idx) {
+    const int64_t d = deg[a];
+    if (d <= 0) break;  // (sorted: the rest have no edges either)
+    if (d < cap) {
+      bool placed = false;
+      for (int64_t r = d; r < cap && !placed; ++r) {
+        auto& fr = free_[static_cast<size_t>(r)];
+        if (fr.empty()) continue;
+        const int32_t u = fr.back();
+        fr.pop_back();
+        units[u].push_back(a);
+        rows[u] += d;
+        if (static_cast<int32_t>(units[u].size()) < max_members) free_[static_cast<size_t>(r - d)].push_back(u);
+        placed = true;
+      }
+      if (placed) continue;
+      free_[static_cast<size_t>(cap - d)].push_back(static_cast<int32_t>(units.size()));
+    }
+    units.push_back({a});
+    rows.push_back(d);
+  }
+  std::vector<int32_t> zero;
+  for (int64_t a = 0; a < n; ++a)
+    if (deg[a] <= 0) zero.push_back(static_cast<int32_t>(a));
+  for (size_t i = 0; i < zero.size(); i += static_cast<size_t>(max_members)) {
+    const size_t e = std::min(zero.size(), i + static_cast<size_t>(max_members));
+    units.emplace_back(zero.begin() + i, zero.begin() + e);
+    rows.push_back(0);
+  }
+  int64_t pos = 0, mr = 0;
+  if (packs) packs[0] = 0;
+  for (size_t u = 0; u < units.size(); ++u) {
+    for (const int32_t a : units[u]) order[pos++] = a;
+    packs[u + 1] = static_cast<int32_t>(pos);
+    mr = std::max(mr, rows[u]);
+  }
+  *n_units = static_cast<int64_t>(units.size());
+  *max_rows = static_cast<int32_t>(mr);
+  return X2G_OK;
+}
 
 X2G_API size_t x2g_center_schedule_workspace(int64_t num_atoms) {
   return num_atoms < 0 ? 0 : (x2g::kSchedTempWord + 3 * static_cast<size_t>(num_atoms)) * sizeof(int32_t);

@@ -82,6 +82,7 @@ SIGNATURES = {
                                                                                       _I64, _I32, _I32] + [_P] * 8,
     "x2g_sbf_attention_fwd_center_sf_tiled_lds": [],
     "x2g_center_schedule_workspace": [_I64],
+    "x2g_center_packs_host": [_P, _I64, _I32, _I32, _P, _P, _P, _P],
     "x2g_center_schedule": [_P, _P, _I64, _P, _P, _P, _P, _P, _SZ, _P],
     "x2g_sbf_attention_bwd_center_lds": [_I32, _I32],
     "x2g_sbf_attention_bwd_center": [_P] * 5 + [ctypes.c_int] + [_P] * 12 + [_I64, _I32, _I64, _I64, _I32, _I32] +

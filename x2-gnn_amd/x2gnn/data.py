@@ -264,34 +264,20 @@ def center_packs(deg, cap=CENTER_PACK_ROWS, max_members=CENTER_PACK_MEMBERS):
     the atoms unit by unit, packs int32 [P + 1]: unit p = order[packs[p] .. packs[p + 1]), max_rows: the
     largest unit's row count), the units in decreasing order of their largest degree (the longest
     workgroups start first)."""
-    deg = np.asarray(deg, dtype=np.int64)
-    units, rows, free = [], [], [[] for _ in range(cap)]  # free[r]: open units with r rows left
-    for a in np.argsort(-deg, kind="stable").tolist():
-        d = int(deg[a])
-        if d == 0:
-            break  # (sorted: the rest have no edges either)
-        if d < cap:
-            for r in range(d, cap):  # best fit: the fullest open unit that takes it
-                if free[r]:
-                    u = free[r].pop()
-                    units[u].append(a)
-                    rows[u] += d
-                    if len(units[u]) < max_members:
-                        free[r - d].append(u)
-                    break
-            else:
-                free[cap - d].append(len(units))
-                units.append([a])
-                rows.append(d)
-            continue
-        units.append([a])
-        rows.append(d)
-    zero = np.flatnonzero(deg == 0).tolist()
-    units += [zero[i:i + max_members] for i in range(0, len(zero), max_members)]
-    rows += [0] * ((len(zero) + max_members - 1) // max_members)
-    order = np.fromiter((a for u in units for a in u), dtype=np.int32, count=len(deg))
-    packs = np.concatenate([[0], np.cumsum([len(u) for u in units])]).astype(np.int32)
-    return order, packs, int(max(rows, default=0))
+    import ctypes
+
+    from . import _lib
+
+    deg = np.ascontiguousarray(deg, dtype=np.int64)
+    n = int(deg.shape[0])
+    order = np.empty(n, dtype=np.int32)
+    packs = np.empty(n + 1, dtype=np.int32)
+    units, rows = ctypes.c_int64(0), ctypes.c_int32(0)
+    # the best fit is a sequential loop over the atoms: native (csrc/line_graph.hip), a Python loop took two
+    # thirds of a 128-molecule collate (tests/test_host.py checks it against that loop)
+    _lib.call("x2g_center_packs_host", deg.ctypes.data, n, int(cap), int(max_members), order.ctypes.data,
+              packs.ctypes.data, ctypes.addressof(units), ctypes.addressof(rows))
+    return order, packs[:units.value + 1].copy(), int(rows.value)
 
 
 CENTER_SF_MAX_ROWS = 17  # ops.CENTER_SF_MAX_ROWS
