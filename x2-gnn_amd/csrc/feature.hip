@@ -186,6 +186,10 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
       if (tid < kFRows) envs[tid] = xt.env;
     }
     __syncthreads();
+    // the first two W1 groups before the next tile's span: loads retire in order, so issued after the
+    // span's (HBM) loads they would wait for them at the first MFMA (one HBM round trip per tile)
+    f4 wa0 = w1_frag(a.w1, K, c1a, 0, g), wb0 = w1_frag(a.w1, K, c1b, 0, g);
+    f4 wa1 = w1_frag(a.w1, K, c1a, 1, g), wb1 = w1_frag(a.w1, K, c1b, 1, g);
     if (tile + gridDim.x < ntiles) xtile_load(a, tile + gridDim.x, xt);  // in flight during the products
     // x * env in T layout: per 16-row tile and plane, float4 u of the 2048-float block holds
     // feature u >> 2, rows 4 (u & 3) .. +3.  (Issuing these 48 KB one piece per iteration of the first
@@ -200,14 +204,11 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
       for (int e = 0; e < 4; ++e) v[e] = A[(rr + e) * kFAS + 128 * p + f] * envs[rr + e];
       *reinterpret_cast<f4*>(a.xs_t + p * a.tf + t16 * 2048 + 4 * tid) = v;
     };
-    for (int it = 0; it < 6; ++it) xs_store(it);
     // z1 = env (x W1^T) + b1: wave w -> columns c1a, c1b, both 16-row blocks
     f4 acc[2][2] = {{zero4(), zero4()}, {zero4(), zero4()}};
     // W1 operands two groups ahead (set 0: even groups, set 1: odd; a set is reloaded right after
     // its MFMAs issue), the A rows of the next group read before this group's MFMAs
     const int KQn = KQ;
-    f4 wa0 = w1_frag(a.w1, K, c1a, 0, g), wb0 = w1_frag(a.w1, K, c1b, 0, g);
-    f4 wa1 = w1_frag(a.w1, K, c1a, 1, g), wb1 = w1_frag(a.w1, K, c1b, 1, g);
     f4 a0 = *reinterpret_cast<const f4*>(A + i * kFAS + 4 * g);
     f4 a1 = *reinterpret_cast<const f4*>(A + (16 + i) * kFAS + 4 * g);
     auto group = [&](int q, f4& ba, f4& bb) {
@@ -227,8 +228,7 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
       a0 = n0;
       a1 = n1;
     };
-    int q = 0;
-    for (; q < KQn; q += 2) {
+    for (int q = 0; q < KQn; q += 2) {
       group(q, wa0, wb0);
       if (q + 1 < KQn) group(q + 1, wa1, wb1);
     }
@@ -306,6 +306,9 @@ __global__ void __launch_bounds__(kFThreads, 1) feat_fwd_kernel(const FeatFwdArg
       if (ry < nr) *reinterpret_cast<f4*>(a.y2 + (r0 + ry) * kFN2 + 16 * w + 4 * qm) = yt;
       if (a.want_t) *reinterpret_cast<f4*>(a.z2_t + tpos(a.tf, t16, c2, g)) = z;
     }
+    // x * env to T layout last (A and envs hold this tile until the next one's barrier): issued before the
+    // products, these stores retired in order ahead of every W1 load behind them (a write round trip per tile)
+    for (int it = 0; it < 6; ++it) xs_store(it);
   }
 }
 
