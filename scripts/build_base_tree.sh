@@ -16,5 +16,7 @@ cp -r "$WT/x2-gnn_amd/x2gnn" "$ROOT/ab_base/x2-gnn_amd/"
 cp "$WT/x2-gnn_amd/lib/libx2g.so" "$ROOT/ab_base/x2-gnn_amd/lib/"
 cp -r "$WT/oracle" "$ROOT/ab_base/"
 cp "$WT"/profiles/*.json "$ROOT/ab_base/profiles/"
+mkdir -p "$ROOT/ab_base/tests/golden"
+cp "$WT"/tests/golden/aid_geom.npz "$ROOT/ab_base/tests/golden/"  # config 5's geometries (bench --workload aid_infer)
 git -C "$ROOT" worktree remove --force "$WT"
 echo "ab_base = $(git -C "$ROOT" rev-parse --short "$REV")"

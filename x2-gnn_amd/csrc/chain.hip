@@ -338,7 +338,7 @@ __device__ __forceinline__ void half_gemm(const f4* __restrict__ img, const f4 (
 
 // epilogue of blocks [RB0, RB1): z = acc + bias (stored), y = act(z) (+ residual) -> out image and
 // the T-layout copy; acc[rb] := y
-template <int RB0, int RB1, int N>
+template <int RB0, int RB1, int N, bool TC = true>
 __device__ __forceinline__ void half_epi(f4 (&acc)[N], const f4 (&held)[N], f4 bias, float silu_m, float res_m,
                                          rsrc_t zr, rsrc_t tr, f4* __restrict__ out, int r0, int nrows, int w,
                                          int rl, int g) {
@@ -357,11 +357,13 @@ __device__ __forceinline__ void half_epi(f4 (&acc)[N], const f4 (&held)[N], f4 b
     }
     out[ipos(r, 4 * w + g)] = y;
     acc[rb] = y;
-    f4 t = quad_transpose(y, j);
+    if constexpr (TC) {  // (inference: no weight gradient, no T-layout copy — not even dropped stores)
+      f4 t = quad_transpose(y, j);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) t[e] = 16 * rb + 4 * m + e < nrows ? t[e] : 0.0f;
-    bstore4(tr, t, rb < ntile ? 4 * static_cast<int>((static_cast<int64_t>(r0 >> 4) + rb) * (16 * kCD) + f * 16 + 4 * m)
-                              : kOOB);
+      for (int e = 0; e < 4; ++e) t[e] = 16 * rb + 4 * m + e < nrows ? t[e] : 0.0f;
+      bstore4(tr, t, rb < ntile ? 4 * static_cast<int>((static_cast<int64_t>(r0 >> 4) + rb) * (16 * kCD) + f * 16 + 4 * m)
+                                : kOOB);
+    }
   }
 }
 
@@ -435,7 +437,7 @@ __device__ __forceinline__ void pipe_sched() {
 
 // one stage of the v4 forward: in -> out (distinct arrays after inlining); RB row blocks per chunk (6,
 // or 3 for the small-row batched chains), computed in thirds of RB / 3 blocks
-template <int RB>
+template <int RB, bool TC = true>
 __device__ __forceinline__ void fwd4_stage(const ChainFwdArgs& a, int s, const f4* __restrict__ in,
                                            f4* __restrict__ out, const f4* __restrict__ rimg, f4 (&A)[8],
                                            f4 (&held)[RB], int r0, int nrows,
@@ -465,14 +467,14 @@ __device__ __forceinline__ void fwd4_stage(const ChainFwdArgs& a, int s, const f
   pipe_sched<BPT>();
   __builtin_amdgcn_sched_barrier(0);
   third_gemm<1, BPT>(in, A, acc, bo, rl, g);
-  half_epi<0, BPT>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
+  half_epi<0, BPT, RB, TC>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
   interleave_epi_sched<BPT>();
   __builtin_amdgcn_sched_barrier(0);
   third_gemm<2, BPT>(in, A, acc, bo, rl, g);
-  half_epi<BPT, 2 * BPT>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
+  half_epi<BPT, 2 * BPT, RB, TC>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
   interleave_epi_sched<BPT>();
   __builtin_amdgcn_sched_barrier(0);
-  half_epi<2 * BPT, 3 * BPT>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
+  half_epi<2 * BPT, 3 * BPT, RB, TC>(acc, held, bias, silu_m, res_m, zr, tr, out, r0, nrows, w, rl, g);
   pin(An);
   __syncthreads();
   if (S.y) store_img<RB>(S.y, out, r0, nrows);
@@ -651,7 +653,7 @@ __device__ __forceinline__ void stage_rows_ln(f4* __restrict__ img, const float*
   }
 }
 
-template <bool LN, int RB = kV2RB>
+template <bool LN, int RB = kV2RB, bool TC = true>
 __device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a, const ChainLn& ln) {
   static_assert(RB == 6 || RB == 3, "thirds of 2 or 1 row blocks");
   __shared__ f4 img0[RB * 16 * 32];
@@ -692,8 +694,8 @@ __device__ __forceinline__ void chain_fwd_v4_run(const ChainFwdArgs& a, const Ch
       store_t_slice(a.in_t, xs, r0, nrows, w, rl, g);
     }
     for (int s = 0; s < n; s += 2) {
-      fwd4_stage<RB>(a, s, img0, img1, imgr, A, held, r0, nrows, w, rl, g);
-      if (s + 1 < n) fwd4_stage<RB>(a, s + 1, img1, img0, imgr, A, held, r0, nrows, w, rl, g);
+      fwd4_stage<RB, TC>(a, s, img0, img1, imgr, A, held, r0, nrows, w, rl, g);
+      if (s + 1 < n) fwd4_stage<RB, TC>(a, s + 1, img1, img0, imgr, A, held, r0, nrows, w, rl, g);
     }
   }
 }
@@ -707,6 +709,10 @@ struct ChainFwdLnArgs {
 };
 __global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4_ln(const ChainFwdLnArgs b) {
   chain_fwd_v4_run<true>(b.a, b.ln);
+}
+// the same without the backward's T-layout copies (inference: in_t NULL)
+__global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4_ln_infer(const ChainFwdLnArgs b) {
+  chain_fwd_v4_run<true, kV2RB, false>(b.a, b.ln);
 }
 
 // several independent chains over the same row count in one launch (job = blockIdx.y): the
@@ -1668,7 +1674,10 @@ X2G_API int x2g_chain_fwd_ln(const float* x, const float* row_stats, const int32
   const ChainFwdLnArgs b{a, {reinterpret_cast<const float2*>(row_stats), seg_rowptr, x_norm, seg_mean, seg_rstd,
                              num_segments, eps}};
   const int64_t nblk = (rows + 15) / 16;
-  chain_fwd_v4_ln<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, as_stream(stream)>>>(b);
+  if (b.a.in_t)
+    chain_fwd_v4_ln<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, as_stream(stream)>>>(b);
+  else
+    chain_fwd_v4_ln_infer<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, as_stream(stream)>>>(b);
   return last_launch_status();
 }
 

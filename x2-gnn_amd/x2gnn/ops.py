@@ -524,7 +524,7 @@ class _SBFAttention(torch.autograd.Function):
         # the logits [T, H] are read by a backward or for the attention weights; the center forwards skip
         # the store otherwise (inference: 223 MB per layer at config 5)
         alpha = (torch.empty(T, heads, dtype=torch.float32, device=dev)
-                 if keep_alpha or any(ctx.needs_input_grad) or not center else None)
+                 if keep_alpha or _keeps(ctx) or not center else None)
         smax = torch.empty(E, heads, dtype=torch.float32, device=dev)
         sden = torch.empty(E, heads, dtype=torch.float32, device=dev)
         # per-row (mean, M2) of the output for a graph LayerNorm fused into the next row chain
@@ -534,7 +534,7 @@ class _SBFAttention(torch.autograd.Function):
             # lin_sbf fused into the center forward: S_t rebuilt per center atom from the sbf factors; for a
             # backward, the sources' P rows (the center backward rebuilds S_t from them) or the S rows
             sproj = None
-            if any(ctx.needs_input_grad):
+            if _keeps(ctx):
                 if _CENTER_P and _center_bwd_ok(lg, heads):
                     sbf_p = torch.empty(E, 7, D, dtype=torch.float32, device=dev)
                 else:
@@ -574,7 +574,7 @@ class _SBFAttention(torch.autograd.Function):
         ctx.lg, ctx.edge_mode, ctx.edge_row, ctx.heads, ctx.channels = lg, edge_mode, edge_row, heads, channels
         ctx.edge_shape = None if edge is None else edge.shape
         # (one call: a second mark_non_differentiable replaces the first's set)
-        ctx.mark_non_differentiable(alpha, smax, sden, *((rstats,) if rstats is not None else ()))
+        ctx.mark_non_differentiable(*(t for t in (alpha, smax, sden, rstats) if t is not None))
         # the logits / max / denominator outputs never receive gradients: do not let autograd
         # materialise zero-filled [T, H] / [E, H] tensors for them (three fill launches per layer)
         ctx.set_materialize_grads(False)
@@ -790,7 +790,7 @@ class _ReadoutMLPs(torch.autograd.Function):
         st = stream_ptr()
         ctx.chain = _readout_chain_ok(R, D, G, W1, B1, W2, B2)
         if ctx.chain:  # both hidden layers of every readout: one x2g_chain_fwd_batch launch
-            grad = any(ctx.needs_input_grad)  # inference: no transposed weights, no T-layout inputs
+            grad = _keeps(ctx)  # inference: no transposed weights, no T-layout inputs
             tf = int(_lib.load().x2g_chain_t_floats(R, D))
             WT = torch.empty(G, 2, D, D, **f32) if grad else None
             in_t = torch.empty(G, 2, tf, **f32) if grad else None
@@ -984,7 +984,7 @@ def readout_mlps(feats, mlps, pool=None):
         params += [mods[0].weight, mods[0].bias, mods[2].weight, mods[2].bias, mods[4].weight, mods[4].bias]
     if pool is not None:
         pool = (_i32(pool[0]), int(pool[1]))
-    return _ReadoutMLPs.apply(len(feats), pool, *feats, *params)
+    return _apply(_ReadoutMLPs, len(feats), pool, *feats, *params)
 
 
 def keyed_row_sum(src, key, num_keys: int):
@@ -1156,7 +1156,7 @@ def sbf_attention(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg: LineGraph, heads: 
         out, alpha, smax, sden, rstats = _attention_fwd_tiled(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode,
                                                               edge_row, heads, channels, INFER_TILE, return_attention)
     else:
-        out, alpha, smax, sden, rstats = _SBFAttention.apply(q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode,
+        out, alpha, smax, sden, rstats = _apply(_SBFAttention, q, k, v, skip, edge, sbf, w_sbf, b_sbf, lg, edge_mode,
                                                          edge_row, heads, channels, return_attention)
     if rstats is not None:  # for a graph LayerNorm fused into the consumer (ops.row_chain(ln=...))
         out._x2g_rowstats = rstats
@@ -1304,6 +1304,29 @@ def _defer_job(ws, offset, splits, n_w, n_b, dw, db, ld=0, cols=0, dw_ptr=None, 
                           (db_ptr if db_ptr is not None else db.data_ptr()) if has_b else None, n_w,
                           n_b if has_b else 0, splits, ld, cols))
     d.keep.append(ws)
+
+
+_APPLY_GRAD = [True]  # the caller's grad mode at the innermost Function.apply in flight (_apply)
+
+
+def _apply(fn, *args):
+    """``fn.apply(*args)`` with the caller's grad mode recorded for the forward: autograd runs forward() with
+    grad mode off and fills ``ctx.needs_input_grad`` from ``requires_grad`` alone, so under ``torch.no_grad()``
+    every parameter still "needs" a gradient and a forward that asked only ``needs_input_grad`` kept its
+    backward's operands for nothing (config 5's inference wrote ~0.7 GB of logits and P rows and the chains'
+    T-layout inputs per layer)."""
+    prev = _APPLY_GRAD[0]
+    _APPLY_GRAD[0] = torch.is_grad_enabled()
+    try:
+        return fn.apply(*args)
+    finally:
+        _APPLY_GRAD[0] = prev
+
+
+def _keeps(ctx):
+    """Whether this forward keeps the operands of a backward: an input needs a gradient AND the caller's
+    grad mode was on (see _apply)."""
+    return _APPLY_GRAD[0] and any(ctx.needs_input_grad)
 
 
 def grad_sink(param):
@@ -1597,7 +1620,7 @@ class _ChainFn(torch.autograd.Function):
         R, D = x2.shape
         r2 = _f32(res) if res is not None else None
         f32 = dict(dtype=torch.float32, device=x2.device)
-        grad = any(ctx.needs_input_grad)  # (autograd runs forward() itself with grad mode off)
+        grad = _keeps(ctx)  # (autograd runs forward() itself with grad mode off: _apply)
         zs = [torch.empty(R, D, **f32) if (flags[i] & CHAIN_SILU) and grad else None for i in range(n)]
         y = torch.empty(R, D, **f32)
         W = [_f32(w) for w in ws]
@@ -1706,7 +1729,7 @@ def row_chain(x, res, linears, flags, ln=None):
     if ln is not None:
         stats, rowptr, G, eps = ln
         ln = (_f32(stats), _i32(rowptr), int(G), float(eps))
-    return _ChainFn.apply(x, res, tuple(flags), ln, *params)
+    return _apply(_ChainFn, x, res, tuple(flags), ln, *params)
 
 
 # ------------------------------------------------------------------------------ small-table chains
@@ -1843,7 +1866,7 @@ class _FeaturizeFn(torch.autograd.Function):
         f32 = dict(dtype=torch.float32, device=dev)
         y = torch.empty(R, 128, **f32)
         # the backward's T-layout operands (8 planes, ~4 KB per row) only when a gradient is wanted
-        grad = any(ctx.needs_input_grad)
+        grad = _keeps(ctx)
         xs_t, z1_t, y1_t, z2_t = ((torch.empty(max(n * tf, 1), **f32) for n in (3, 2, 2, 1)) if grad
                                   else (None, None, None, None))
         e = _f32(env.reshape(-1)) if env is not None else None
@@ -1902,7 +1925,7 @@ class _FeaturizeFn(torch.autograd.Function):
 
 def featurize(x, env, lin1, lin2):
     """SiLU(lin2(SiLU(lin1(x * env[:, None])))) through the fused featurisation kernels."""
-    return _FeaturizeFn.apply(x, env, lin1.weight, lin1.bias, lin2.weight, lin2.bias)
+    return _apply(_FeaturizeFn, x, env, lin1.weight, lin1.bias, lin2.weight, lin2.bias)
 
 
 class TiledJob(ctypes.Structure):
@@ -1998,7 +2021,7 @@ class _ConvProjFusedFn(torch.autograd.Function):
         B = [_f32(t) if t is not None else None for t in (bq, bk, bv, bs)]
         f32 = dict(dtype=torch.float32, device=x2.device)
         outs = [torch.empty(E, D, **f32) for _ in range(4)]
-        grad = any(ctx.needs_input_grad)
+        grad = _keeps(ctx)
         lib = _lib.load()
         tf = int(lib.x2g_chain_t_floats(E, D))
         WT = torch.empty(4, D, D, **f32) if grad else None
@@ -2298,8 +2321,8 @@ def conv_projections(x, rbf, wr, wq, bq, wk, bk, wv, bv, ws, bs):
     if not x.is_cuda:
         raise RuntimeError("x2gnn device ops need GPU tensors (no CPU fallback by design)")
     if conv_proj_fused_supported(x, rbf, (wq, wk, wv, ws), (bq, bk, bv, bs)):
-        return _ConvProjFusedFn.apply(x, rbf, wr, wq, bq, wk, bk, wv, bv, ws, bs)
-    return _ConvProjFn.apply(x, rbf, wr, wq, bq, wk, bk, wv, bv, ws, bs)
+        return _apply(_ConvProjFusedFn, x, rbf, wr, wq, bq, wk, bk, wv, bv, ws, bs)
+    return _apply(_ConvProjFn, x, rbf, wr, wq, bq, wk, bk, wv, bv, ws, bs)
 
 
 def dense(x, weight, bias=None, act=ACT_NONE, res=None):
