@@ -389,7 +389,9 @@ int x2g_sbf_attention_fwd_center_sf_tiled(const float* q, const float* k, const 
  * edge term (sum over the atom's sources of dk + dv): the element-table gradient is its keyed sum by
  * atom element.  atom_order (or NULL): workgroup w takes atom atom_order[w] (x2gnn: by decreasing degree).
  * S_t comes from sbfproj [T, 128] rows, or (sbfproj NULL) from the fused forward's sbf_p [E, 7, 128] and
- * b_sbf [128] as S_t = b + sum_l Y_l(t) P_s[l] (exactly one of the two forms).
+ * b_sbf [128] as S_t = b + sum_l Y_l(t) P_s[l] (exactly one of the two forms).  With sbf_p, alpha_raw is not
+ * read (may be NULL): each logit is recomputed as q_i . (k_j + e) / sqrt(channels) in the forward's own
+ * arithmetic, bit for bit, from rows the workgroup stages anyway.
  * sph_y [T, 8] as x2g_spherical_basis writes it.  LDS per workgroup:
  * x2g_sbf_attention_bwd_center_lds(max_degree, heads) bytes (<= 160 KiB, else X2G_EUNSUPPORTED).
  * heads * channels = 128, channels a multiple of 4, 16-byte aligned rows.  T-row arrays are addressed with

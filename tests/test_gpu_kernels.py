@@ -2236,7 +2236,8 @@ def test_center_backward_from_p_rows_equals_s_rows(cuda):
     """The fused forward's P rows (sbf_p_out [E, 7, 128]: 3.5 KB per source instead of 512 B per triplet)
     feed the center backward, which rebuilds S_t = b + sum_l Y_l(t) P_s[l] in the forward's own arithmetic:
     every backward output equals the one from the S rows the same forward stores, bit for bit, with and
-    without the edge term; and the P rows equal W R_s per source (fp32)."""
+    without the edge term — the P-row form given no logits (it recomputes them as the forward formed them);
+    and the P rows equal W R_s per source (fp32)."""
     from x2gnn import ops
     from x2gnn._lib import call, ptr, stream_ptr
     from x2gnn.data import collate
@@ -2258,19 +2259,19 @@ def test_center_backward_from_p_rows_equals_s_rows(cuda):
     bias = 0.1 * torch.randn(D, device=cuda, generator=g)
     f = dict(device=cuda, dtype=torch.float32)
     po, pp, pr = lg.packed
-    fw = [torch.empty(E, D, **f), torch.empty(T, H, **f), torch.empty(E, H, **f), torch.empty(E, H, **f),
-          torch.empty(E, 2, **f)]
-    S, P = torch.full((T, D), float("nan"), **f), torch.full((E, 7, D), float("nan"), **f)
-    call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(table), ptr(lg.src_type),
-         ops.EDGE_PER_DST, ptr(radial), ptr(y), ptr(W), ptr(bias), ptr(lg.atom_rowptr), ptr(lg.edge_rev),
-         ptr(lg.rev_trip), ptr(po), ptr(pp), ptr(_pack_info(lg, po)), 0, int(pp.shape[0]) - 1, pr, E, T, H, C,
-         *[ptr(t) for t in fw], ptr(S),
-         ptr(P), stream_ptr())
-    ref_p = torch.einsum("clk,elk->elc", W.view(D, 7, 6), radial.view(E, 7, 6))
-    torch.testing.assert_close(P, ref_p, rtol=1e-5, atol=1e-5)
-    alpha, smax, sden = fw[1], fw[2], fw[3]
     for mode in (ops.EDGE_PER_DST, ops.EDGE_NONE):
         edge = table if mode == ops.EDGE_PER_DST else None
+        # the forward of this mode (the P-row backward recomputes this forward's logits)
+        fw = [torch.empty(E, D, **f), torch.empty(T, H, **f), torch.empty(E, H, **f), torch.empty(E, H, **f),
+              torch.empty(E, 2, **f)]
+        S, P = torch.full((T, D), float("nan"), **f), torch.full((E, 7, D), float("nan"), **f)
+        call("x2g_sbf_attention_fwd_center_sf", ptr(q), ptr(k), ptr(v), ptr(skip), ptr(edge),
+             ptr(lg.src_type) if edge is not None else None, mode, ptr(radial), ptr(y), ptr(W), ptr(bias),
+             ptr(lg.atom_rowptr), ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(po), ptr(pp), ptr(_pack_info(lg, po)), 0,
+             int(pp.shape[0]) - 1, pr, E, T, H, C, *[ptr(t) for t in fw], ptr(S), ptr(P), stream_ptr())
+        ref_p = torch.einsum("clk,elk->elc", W.view(D, 7, 6), radial.view(E, 7, 6))
+        torch.testing.assert_close(P, ref_p, rtol=1e-5, atol=1e-5)
+        alpha, smax, sden = fw[1], fw[2], fw[3]
         outs = []
         for from_p in (False, True):
             dq, dk, dv = (torch.full((E, D), float("nan"), **f) for _ in range(3))
@@ -2279,8 +2280,8 @@ def test_center_backward_from_p_rows_equals_s_rows(cuda):
             call("x2g_sbf_attention_bwd_center", ptr(q), ptr(k), ptr(v), ptr(edge),
                  ptr(lg.src_type) if edge is not None else None, mode, None if from_p else ptr(S),
                  ptr(P) if from_p else None, ptr(bias) if from_p else None, ptr(y), ptr(lg.atom_rowptr),
-                 ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order), ptr(alpha), ptr(smax), ptr(sden), ptr(dout),
-                 lg.N, lg.max_degree, E, T, H, C, ptr(dq), ptr(dk), ptr(dv), ptr(G), ptr(de),
+                 ptr(lg.edge_rev), ptr(lg.rev_trip), ptr(lg.center_order), None if from_p else ptr(alpha), ptr(smax),
+                 ptr(sden), ptr(dout), lg.N, lg.max_degree, E, T, H, C, ptr(dq), ptr(dk), ptr(dv), ptr(G), ptr(de),
                  ptr(torch.empty(2, T, H, **f)), stream_ptr())
             outs.append([t for t in (dq, dk, dv, G, de) if t is not None])
         for a, r in zip(*outs):

@@ -41,6 +41,18 @@ __device__ __forceinline__ float head_sum(float v) {
   return group_sum<LPH>(v);
 }
 
+// a head's logit q . kr / sqrt C over its LPH lanes, in one fixed arithmetic (explicitly rounded product and
+// fmas: no contraction choice left to the compiler), so that every forward and the backward that recomputes
+// it (x2g_sbf_attention_bwd_center from P rows) produce the same bits
+template <int LPH>
+__device__ __forceinline__ float qk_logit(cf4 qv, cf4 kr, float sqrt_c) {
+  float dot = __fmul_rn(qv[0], kr[0]);
+  dot = __fmaf_rn(qv[1], kr[1], dot);
+  dot = __fmaf_rn(qv[2], kr[2], dot);
+  dot = __fmaf_rn(qv[3], kr[3], dot);
+  return __fdiv_rn(head_sum<LPH>(dot), sqrt_c);
+}
+
 // sum over each aligned 32-lane half, in every lane of that half
 __device__ __forceinline__ float half_sum(float v, int half) {
   v = half32_sum_hi(v);
@@ -239,11 +251,7 @@ __global__ void __launch_bounds__(64 * WAVES) attn_fwd_center_kernel(const FwdCe
         const int j = j0 + u;
         const bool ok = j < n && j != i;
         const cf4 kr = ke[(j < n ? j : n - 1) * 32 + l32];
-        float dot = qv[0] * kr[0];
-        dot = fmaf(qv[1], kr[1], dot);
-        dot = fmaf(qv[2], kr[2], dot);
-        dot = fmaf(qv[3], kr[3], dot);
-        const float logit = head_sum<LPH>(dot) / a.sqrt_c;
+        const float logit = qk_logit<LPH>(qv, kr, a.sqrt_c);
         lg[u] = ok ? logit : -INFINITY;
         mb = fmaxf(mb, lg[u]);
         if (a.alpha && ok && leader) a.alpha[(static_cast<int64_t>(tb) + (j - (j > i ? 1 : 0))) * a.H + head] = logit;
@@ -445,11 +453,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_fwd_center_sf_kernel(const
         sv[uu] = s4;
         if (a.sp && ok) st4(a.sp + static_cast<int64_t>(tt[uu]) * kCD + c0, s4);
         const cf4 kr = KE[jr * 32 + l32];
-        float dot = qv[0] * kr[0];
-        dot = fmaf(qv[1], kr[1], dot);
-        dot = fmaf(qv[2], kr[2], dot);
-        dot = fmaf(qv[3], kr[3], dot);
-        const float logit = head_sum<LPH>(dot) / a.sqrt_c;
+        const float logit = qk_logit<LPH>(qv, kr, a.sqrt_c);
         lg[uu] = ok ? logit : -INFINITY;
         mb = fmaxf(mb, lg[uu]);
         if (a.alpha && ok && leader) a.alpha[static_cast<int64_t>(tt[uu]) * a.H + head] = logit;
@@ -680,11 +684,7 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_fwd_center_sf_tiled_kernel
               if (a.sp && ok) st4(a.sp + static_cast<int64_t>(tt[uu]) * kCD + c0, s4);
             }
             const cf4 kr = KE[jr * 32 + l32];
-            float dot = qv[0] * kr[0];
-            dot = fmaf(qv[1], kr[1], dot);
-            dot = fmaf(qv[2], kr[2], dot);
-            dot = fmaf(qv[3], kr[3], dot);
-            const float logit = head_sum<LPH>(dot) / a.sqrt_c;
+            const float logit = qk_logit<LPH>(qv, kr, a.sqrt_c);
             lg[uu] = ok ? logit : -INFINITY;
             mb = fmaxf(mb, lg[uu]);
             if constexpr (STORE) {
@@ -812,6 +812,7 @@ struct BwdCenterArgs {
   int64_t n_atoms, T;
   int H;
   float inv_sqrt_c;
+  float sqrt_c;  // FACT: the logits are recomputed as the forward formed them (q . (k + e) / sqrt C)
   float *dq, *dk, *dv, *gfold, *d_edge, *gw;  // gw: [T, H] (g, a) pairs of scratch
 };
 
@@ -994,24 +995,27 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const Bw
       // only the first batch of a source waits out the load latency (every batch full, the last masked;
       // every load and store unconditional — clamped indices, the (g, a) store of a masked triplet to an
       // out-of-range offset — so the compiler's vmcnt waits stay counted)
+      // The logits are not read back: a_t's logit is q_i . (k_j + e) / sqrt C over the head's lanes, from the
+      // QI / KE rows already in LDS, in the forward's own arithmetic (the same products, fma order and head
+      // sum: the same bits), so the forward stores no [T, H] logits for this backward (x2gnn passes none).
       constexpr int BB = kFactBatch;
       if (nt > 0) {  // (workgroup-uniform)
-        float yv[BB], al[BB];
+        const cf4 kj = KE[j * 32 + l32];
+        float yv[BB];
         int tt[BB];
-        auto load = [&](int i0, float (&y_)[BB], float (&a_)[BB], int (&t_)[BB]) {
+        auto load = [&](int i0, float (&y_)[BB], int (&t_)[BB]) {
 #pragma unroll
           for (int u = 0; u < BB; ++u) {
             const int i = i0 + u < n ? i0 + u : n - 1;
             t_[u] = trip(i, j);
             y_[u] = ldf(y_r, (t_[u] * 8 + (l32 & 7)) * 4);
-            a_[u] = ldf(al_r, (t_[u] * H + head) * 4);
           }
         };
-        load(0, yv, al, tt);
+        load(0, yv, tt);
         for (int i0 = 0; i0 < n; i0 += BB) {
-          float yn[BB], an[BB];
+          float yn[BB];
           int tn[BB];
-          load(i0 + BB, yn, an, tn);
+          load(i0 + BB, yn, tn);
 #pragma unroll
           for (int u = 0; u < BB; ++u) {
             const int i = i0 + u < n ? i0 + u : n - 1;
@@ -1027,7 +1031,8 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const Bw
             cf4 st = bias4;  // S_t = b + sum_l Y_l(t) P_j[l], the forward's arithmetic in its order
 #pragma unroll
             for (int l = 0; l < kSfL; ++l) st += yl[l] * pj[l];
-            const float at = ok ? expf(al[u] - MX[i * H + head]) * IV[i * H + head] : 0.f;
+            const float logit = qk_logit<LPH>(QI[i * 32 + l32], kj, a.sqrt_c);
+            const float at = ok ? expf(logit - MX[i * H + head]) * IV[i * H + head] : 0.f;
             const cf4 go = GO[i * 32 + l32];
             const cf4 gu = go * ue;
             float gp = gu[0] * st[0];
@@ -1044,7 +1049,6 @@ __global__ void __launch_bounds__(64 * WAVES, 4) attn_bwd_center_kernel(const Bw
 #pragma unroll
           for (int u = 0; u < BB; ++u) {
             yv[u] = yn[u];
-            al[u] = an[u];
             tt[u] = tn[u];
           }
         }
@@ -1201,8 +1205,8 @@ X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const f
   if (num_atoms == 0) return X2G_OK;
   if (!sbfproj == !sbf_p || (sbf_p && !b_sbf)) return X2G_EINVAL;  // S rows, or the P rows and the bias
   if (num_edges > 0 && (!q || !k || !v || !sph_y || !atom_rowptr || !edge_rev || !rev_trip ||
-                        !alpha_raw || !seg_max || !seg_den || !dout || !dq || !dk || !dv || !radial_grad ||
-                        (num_triplets > 0 && !g_work)))
+                        (!alpha_raw && !sbf_p) || !seg_max || !seg_den || !dout || !dq || !dk || !dv ||
+                        !radial_grad || (num_triplets > 0 && !g_work)))
     return X2G_EINVAL;
   if (!atom_rowptr) return X2G_EINVAL;
   if (edge_mode == X2G_EDGE_PER_DST && (!edge || !src_row)) return X2G_EINVAL;
@@ -1216,6 +1220,7 @@ X2G_API int x2g_sbf_attention_bwd_center(const float* q, const float* k, const f
   a.smax = seg_max; a.sden = seg_den; a.dout = dout; a.y = sph_y; a.atom_rowptr = atom_rowptr; a.edge_rev = edge_rev;
   a.rev_trip = rev_trip; a.order = atom_order; a.n_atoms = num_atoms; a.T = num_triplets; a.H = heads;
   a.inv_sqrt_c = static_cast<float>(1.0 / sqrt(static_cast<double>(channels)));
+  a.sqrt_c = static_cast<float>(sqrt(static_cast<double>(channels)));
   a.dq = dq; a.dk = dk; a.dv = dv; a.gfold = radial_grad; a.d_edge = d_edge_atom; a.gw = g_work;
   const int md = max_degree > 0 ? max_degree : 1;
   const bool edge_on = edge_mode == X2G_EDGE_PER_DST;

@@ -521,10 +521,13 @@ class _SBFAttention(torch.autograd.Function):
         dev = q.device
         out = torch.empty(E, D, dtype=torch.float32, device=dev)
         center, src_row = _center_rows(lg, edge_mode, edge_row, D, channels)
-        # the logits [T, H] are read by a backward or for the attention weights; the center forwards skip
-        # the store otherwise (inference: 223 MB per layer at config 5)
+        # the P-row center backward (the shipped training path) recomputes the logits from rows it stages
+        p_bwd = center and _CENTER_P and _center_sf_ok(lg, factors, D) and _center_bwd_ok(lg, heads)
+        # the logits [T, H] are read by the other backwards or for the attention weights; the center forwards
+        # skip the store otherwise (inference: 223 MB per layer at config 5; training: 12 MB written and read
+        # back per layer at config 2)
         alpha = (torch.empty(T, heads, dtype=torch.float32, device=dev)
-                 if keep_alpha or _keeps(ctx) or not center else None)
+                 if keep_alpha or not center or (_keeps(ctx) and not p_bwd) else None)
         smax = torch.empty(E, heads, dtype=torch.float32, device=dev)
         sden = torch.empty(E, heads, dtype=torch.float32, device=dev)
         # per-row (mean, M2) of the output for a graph LayerNorm fused into the next row chain
@@ -535,7 +538,7 @@ class _SBFAttention(torch.autograd.Function):
             # backward, the sources' P rows (the center backward rebuilds S_t from them) or the S rows
             sproj = None
             if _keeps(ctx):
-                if _CENTER_P and _center_bwd_ok(lg, heads):
+                if p_bwd:
                     sbf_p = torch.empty(E, 7, D, dtype=torch.float32, device=dev)
                 else:
                     sproj = torch.empty(T, D, dtype=torch.float32, device=dev)
