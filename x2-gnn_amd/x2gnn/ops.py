@@ -1226,7 +1226,10 @@ def _timed(name):
         return
     st = torch.cuda.current_stream()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda._sleep(200_000)  # ~0.1 ms of device time: the host enqueues the launch meanwhile
+    # ~0.1 ms of device time ahead of the start event while the host enqueues the launch.  (The eager
+    # launch still runs 3-8 % slower than the same launch in graph-replayed steps, box-dependent; a longer
+    # sleep or 0.2 ms of matrix work in its place did not change that: DESIGN.md section 5.)
+    torch.cuda._sleep(200_000)
     a.record(st)
     yield
     b.record(st)
@@ -1264,9 +1267,11 @@ def _flush_tiled(d):
         ws_bytes = int(lib.x2g_tiled_wgrad_flat_rows_workspace(rows, n, 128))
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=torch.device("cuda", torch.cuda.current_device()))
         out = (SlabJob * n)()
-        with _timed("tiled_wgrad_flat"):
-            call("x2g_tiled_wgrad_flat_rows", (TiledJob * n)(*[j for _, j in part]), rows, n, 128,
-                 ACCUM_WGRAD | DEFER_SLAB_SUM, out, ptr(ws), ws_bytes, stream_ptr())
+        jobs = (TiledJob * n)(*[j for _, j in part])
+        st = stream_ptr()
+        with _timed("tiled_wgrad_flat"):  # (nothing but the launch between the timing events)
+            call("x2g_tiled_wgrad_flat_rows", jobs, rows, n, 128, ACCUM_WGRAD | DEFER_SLAB_SUM, out, ptr(ws),
+                 ws_bytes, st)
         d.jobs.extend(out)
         d.keep.append(ws)
     d.tiled = {}
