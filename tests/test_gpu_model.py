@@ -484,6 +484,13 @@ def test_config5_aid_batch64_inference(cuda, monkeypatch):
         assert np.isfinite(res).all() and res.shape == (64,)
         names = [n for n, _ in seen]
         assert names.count("x2g_sbf_attention_fwd_center_sf_tiled") == 4 and "x2g_sbf_project" not in names
+        # no backward state under no_grad (ops._apply / _keeps): no logits, S rows or P rows from the center
+        # forwards (args: ..., out, alpha, smax, sden, row_stats, sbfproj_out, sbf_p_out, stream), no
+        # T-layout inputs from the trunk chains (x2g_chain_fwd_ln: ..., in_t, stream)
+        fwd = [a for n, a in seen if n.startswith("x2g_sbf_attention_fwd_center_sf")]
+        assert fwd and all(a[-7] is None and a[-3] is None and a[-2] is None for a in fwd)
+        chains = [a for n, a in seen if n == "x2g_chain_fwd_ln"]
+        assert chains and all(a[-2] is None for a in chains)
         order = np.argsort(b._meta["triplets"])
         pick = order[np.linspace(0, 63, 8).round().astype(int)]
         sub = [mols[i] for i in pick]

@@ -348,7 +348,7 @@ __device__ __forceinline__ void half_epi(f4 (&acc)[N], const f4 (&held)[N], f4 b
   for (int rb = RB0; rb < RB1; ++rb) {
     const int r = 16 * rb + rl;
     const f4 z = acc[rb] + bias;
-    bstore4(zr, z, r < nrows ? 4 * ((r0 + r) * kCD + 16 * w + 4 * g) : kOOB);
+    if constexpr (TC) bstore4(zr, z, r < nrows ? 4 * ((r0 + r) * kCD + 16 * w + 4 * g) : kOOB);
     f4 y;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -710,7 +710,8 @@ struct ChainFwdLnArgs {
 __global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4_ln(const ChainFwdLnArgs b) {
   chain_fwd_v4_run<true>(b.a, b.ln);
 }
-// the same without the backward's T-layout copies (inference: in_t NULL)
+// the same without the backward's T-layout copies and pre-activation stores (inference: in_t and every
+// stage's z NULL)
 __global__ void __launch_bounds__(kCThreads, 1) chain_fwd_v4_ln_infer(const ChainFwdLnArgs b) {
   chain_fwd_v4_run<true, kV2RB, false>(b.a, b.ln);
 }
@@ -1674,10 +1675,13 @@ X2G_API int x2g_chain_fwd_ln(const float* x, const float* row_stats, const int32
   const ChainFwdLnArgs b{a, {reinterpret_cast<const float2*>(row_stats), seg_rowptr, x_norm, seg_mean, seg_rstd,
                              num_segments, eps}};
   const int64_t nblk = (rows + 15) / 16;
-  if (b.a.in_t)
-    chain_fwd_v4_ln<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, as_stream(stream)>>>(b);
-  else
+  // inference (no T-layout inputs and no pre-activations asked for): the instance without those stores
+  bool infer = b.a.in_t == nullptr;
+  for (int s = 0; s < b.a.n; ++s) infer = infer && b.a.st[s].z == nullptr;
+  if (infer)
     chain_fwd_v4_ln_infer<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, as_stream(stream)>>>(b);
+  else
+    chain_fwd_v4_ln<<<static_cast<unsigned>(nblk < 256 ? nblk : 256), kCThreads, 0, as_stream(stream)>>>(b);
   return last_launch_status();
 }
 
