@@ -192,7 +192,7 @@ class Batch(Data):
                 out._store[k] = torch.cat(vals, dim=0)
             else:
                 out._store[k] = torch.as_tensor(np.array([np.asarray(v) for v in vals]).reshape(-1))
-        out._store["batch"] = torch.repeat_interleave(torch.arange(len(data_list)), torch.as_tensor(nodes))
+        out._store["batch"] = torch.from_numpy(np.repeat(np.arange(len(data_list), dtype=np.int64), nodes))
         out._store["ptr"] = torch.as_tensor(np.concatenate([[0], np.cumsum(nodes)]))
         _add_device_indices(out, nodes, edges)
         return out
@@ -349,7 +349,8 @@ def collate(mols) -> Batch:
                                                            for m in mols]))
     st["edge_num"] = torch.from_numpy(edges.copy())
     st["y"] = torch.from_numpy(np.array([float(m.get("y", 0.0)) for m in mols], dtype=np.float32))
-    st["batch"] = torch.repeat_interleave(torch.arange(B), torch.from_numpy(nodes))
+    # np.repeat: torch.repeat_interleave took 0.2-7 ms of a 128-molecule collate, after the edge_attr copy
+    st["batch"] = torch.from_numpy(np.repeat(np.arange(B, dtype=np.int64), nodes))
     st["ptr"] = torch.from_numpy(np.concatenate([[0], np.cumsum(nodes)]))
     _add_device_indices(b, nodes, edges)
     return b
