@@ -1327,7 +1327,8 @@ X2G_API int x2g_sbf_radial_wgrad(const float* radial_grad, const float* radial, 
   const int64_t rps = radial_rows_per_split(E);
   float* part_w = static_cast<float*>(workspace);
   float* part_b = part_w + static_cast<int64_t>(splits) * D * kS;
-  sbf_radial_wgrad_kernel<<<splits, 2 * D * kRadialGroups, 0, st>>>(radial_grad, radial, E, D, rps, part_w, part_b);
+  sbf_radial_wgrad_kernel<kRadialVpt>
+      <<<splits, 8 * D / kRadialVpt * kRadialGroups, 0, st>>>(radial_grad, radial, E, D, rps, part_w, part_b);
   if (int rc = last_launch_status()) return rc;
   if (flags & X2G_DEFER_SLAB_SUM) return X2G_OK;
   return sum_slabs_launch(part_w, static_cast<int64_t>(D) * kS, part_b, D, splits, dw, db, accum, st);
